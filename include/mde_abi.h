@@ -1,0 +1,196 @@
+/*
+ * mde_abi.h — C ABI of libmde_hip.so, the MI355X (gfx950) kernels of the
+ * dense-depth training hot path.
+ *
+ * The reference (LuizGuzzo/Monocular_Depth_Estimation) has no FFI: its boundary
+ * is the PyTorch nn.Module / callable API.  Every entry point below replaces
+ * one ATen call site (or a fused group of them) on that path; the citation on
+ * each entry names the reference file:line it stands in for.  The Python
+ * mirror of the reference interface (monocular_depth_estimation_amd/) binds
+ * these with ctypes.
+ *
+ * Conventions
+ *  - Plain pointers to DEVICE memory; the caller owns every buffer.
+ *  - Tensors are dense NCHW, element type selected by `dtype` (MDE_F32 only in
+ *    ABI v1; MDE_BF16 is reserved and returns MDE_ERR_UNSUPPORTED).
+ *  - Small parameter/statistics tensors (weights, scales, loss scalars,
+ *    min/max) are always fp32.
+ *  - `stream` is a hipStream_t (NULL = default stream).  No entry point
+ *    synchronises the host, allocates memory or keeps global mutable state
+ *    except the opt-in timing registry at the end of this file.
+ *  - Ops that need scratch take a `workspace` of at least the byte count the
+ *    matching mde_*_workspace() query returns.
+ *  - Return value: 0 on success, a positive hipError_t on a HIP failure, a
+ *    negative MDE_ERR_* on argument errors.  Nothing is launched when an
+ *    argument error is returned.
+ */
+#ifndef MDE_ABI_H
+#define MDE_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDE_ABI_VERSION 1
+
+#define MDE_F32 0
+#define MDE_BF16 1
+
+#define MDE_OK 0
+#define MDE_ERR_INVALID_ARG (-1)
+#define MDE_ERR_UNSUPPORTED (-2)
+
+int mde_abi_version(void);
+const char* mde_status_string(int status);
+
+/* ---------------------------------------------------------------------------
+ * Resizes.  scale_h / scale_w are the SOURCE-per-DESTINATION scales ATen uses
+ * (area_pixel_compute_scale): 1/scale_factor when F.interpolate got a
+ * scale_factor, in/out when it got a size.  The host computes them in fp32.
+ * ------------------------------------------------------------------------- */
+
+/* Bilinear resize, arbitrary ratio, align_corners 0/1.
+ * Replaces F.interpolate(mode='bilinear') at
+ *   src/GuideDepth/model/GuideDepth.py:49,52,55 (x2 decoder upsamples),
+ *   src/GuideDepth/model/DDRNet_23_slim.py:182,185,188,191,332,342,348 (resizes
+ *   to explicit sizes, non-integer ratios), and
+ *   src/model_mobileV3_large_newCRFs.py:55-58,124 (x4 head upsample). */
+int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
+                     int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                     float scale_w, int align_corners, int dtype, void* stream);
+/* Gradient w.r.t. x (gather formulation, no atomics; gx fully overwritten). */
+int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
+                     int64_t hi, int64_t wi, int64_t ho, int64_t wo,
+                     float scale_h, float scale_w, int align_corners,
+                     int dtype, void* stream);
+
+/* Nearest resize (PyTorch 'nearest': src = min(floor(dst*scale), in-1)).
+ * Replaces F.interpolate(x, scale_factor=.5 / .25) at
+ *   src/GuideDepth/model/GuideDepth.py:46-47. */
+int mde_nearest_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
+                    int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                    float scale_w, int dtype, void* stream);
+/* Gradient w.r.t. x (gx fully overwritten). */
+int mde_nearest_bwd(const void* gy, void* gx, int64_t n, int64_t c, int64_t hi,
+                    int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                    float scale_w, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Squeeze-excitation over a channel concatenation (cat fused away).
+ * Replaces torch.cat([x, y], 1) at src/GuideDepth/model/modules.py:90 and
+ * SELayer.forward (modules.py:21-25; reduction=1 -> two bias-free CxC
+ * Linear layers, ReLU, Sigmoid):
+ *   xy = cat(xa[n,ca,h,w], xb[n,cb,h,w]);  m = mean_hw(xy)
+ *   s  = sigmoid(W2 relu(W1 m));  out = xy * s
+ * W1: [cr, c], W2: [c, cr] with c = ca + cb (row-major, as nn.Linear.weight).
+ * Saved for backward: s [n,c], hidden = relu(W1 m) [n,cr], mean [n,c].
+ * xb may be NULL with cb = 0 (plain SELayer).
+ * ------------------------------------------------------------------------- */
+size_t mde_se_workspace(int64_t n, int64_t c, int64_t cr, int64_t h,
+                        int64_t w);
+int mde_se_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
+               const float* w1, const float* w2, int64_t cr, void* out,
+               float* s, float* hidden, float* mean, int64_t n, int64_t h,
+               int64_t w, void* workspace, int dtype, void* stream);
+/* Gradients: gxa, gxb (may be NULL when not needed), gw1 [cr,c], gw2 [c,cr]
+ * (overwritten, not accumulated). */
+int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
+               int64_t cb, const float* w1, const float* w2, int64_t cr,
+               const float* s, const float* hidden, const float* mean,
+               void* gxa, void* gxb, float* gw1, float* gw2, int64_t n,
+               int64_t h, int64_t w, void* workspace, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Skip fusion: residual add + 1x1 conv with bias.
+ * Replaces `self.reduce(residual + depth)` at src/GuideDepth/model/modules.py:100
+ * (+ modules.py:76-78 nn.Conv2d(in, out, 1)):
+ *   out[n,o,p] = b[o] + sum_c W[o,c] (r[n,c,p] + d[n,c,p])
+ * Supported (cin, cout): cin in {1..64}, cout in {1..64}.
+ * ------------------------------------------------------------------------- */
+int mde_skip_reduce_fwd(const void* r, const void* d, const float* wt,
+                        const float* b, void* out, int64_t n, int64_t cin,
+                        int64_t cout, int64_t h, int64_t w, int dtype,
+                        void* stream);
+size_t mde_skip_reduce_workspace(int64_t n, int64_t cin, int64_t cout,
+                                 int64_t h, int64_t w);
+/* gs = dL/d(r+d) (the gradient of BOTH r and d), gw [cout,cin], gb [cout]
+ * (gw, gb overwritten). */
+int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
+                        const float* wt, void* gs, float* gw, float* gb,
+                        int64_t n, int64_t cin, int64_t cout, int64_t h,
+                        int64_t w, void* workspace, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * DepthNorm, src/utils.py:7-8: (d - d.min()) / (d.max() - d.min()), min/max
+ * over the whole batch tensor (train.py:89).
+ * ------------------------------------------------------------------------- */
+size_t mde_minmax_workspace(int64_t numel);
+/* minmax[0] = min(x), minmax[1] = max(x). */
+int mde_minmax(const void* x, int64_t numel, float* minmax, void* workspace,
+               int dtype, void* stream);
+int mde_depthnorm_apply(const void* x, const float* minmax, void* y,
+                        int64_t numel, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * SSIM (3x3 box, ReflectionPad2d(1), C1=1e-4, C2=9e-4; src/loss.py:57-88)
+ * fused with nn.L1Loss (src/train.py:53,94) and, optionally, DepthNorm of the
+ * target (train.py:89).  b = N*C images of h x w.
+ *   t      = target_minmax ? (target - mn)/(mx - mn) : target
+ *   l_ssim = mean(clamp((1 - S)/2, 0, 1));  l_l1 = mean|pred - t|
+ *   loss[0] = w_ssim*l_ssim + w_l1*l_l1, loss[1] = l_ssim, loss[2] = l_l1
+ * grad_pred (nullable) receives d loss[0] / d pred; grad_target (nullable)
+ * d loss[0] / d t.  Requires h, w >= 2 (reflection pad).
+ * ------------------------------------------------------------------------- */
+size_t mde_ssim3_l1_workspace(int64_t b, int64_t h, int64_t w);
+int mde_ssim3_l1_fwd(const void* pred, const void* target,
+                     const float* target_minmax, float w_ssim, float w_l1,
+                     float* loss, void* grad_pred, void* grad_target,
+                     int64_t b, int64_t h, int64_t w, void* workspace,
+                     int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Depth_Loss (src/GuideDepth/losses.py:15-127):
+ *   alpha*L1 + beta*clamp((1 - SSIM11)*0.5, 0, 1) + gamma*grad
+ * SSIM11: Gaussian window sigma 1.5 of size min(11,h,w), zero padding 5,
+ * C1=(0.01 L)^2, C2=(0.03 L)^2, L = max_depth, mean over the map.
+ * grad: forward differences, last column/row zero (losses.py:82-115).
+ * masked mode (beta == gamma == 0): L1 over depth > 0 only (losses.py:26-31).
+ * out[0] = loss, out[1] = l1, out[2] = clamped ssim term, out[3] = grad term,
+ * out[4] = raw ssim mean, out[5] = element count used by L1.
+ * Backward recomputes on device; gout is a device fp32 scalar.
+ * ------------------------------------------------------------------------- */
+size_t mde_depth_loss_workspace(int64_t b, int64_t h, int64_t w);
+int mde_depth_loss_fwd(const void* pred, const void* gt, float alpha,
+                       float beta, float gamma, float max_depth, float* out,
+                       int64_t b, int64_t h, int64_t w, void* workspace,
+                       int dtype, void* stream);
+int mde_depth_loss_bwd(const void* pred, const void* gt, float alpha,
+                       float beta, float gamma, float max_depth,
+                       const float* fwd_out, const float* gout,
+                       void* grad_pred, int64_t b, int64_t h, int64_t w,
+                       void* workspace, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Opt-in kernel timing registry (measurement only; off by default).
+ * When enabled, every launch made through this ABI is bracketed by hipEvents
+ * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY
+ * §8(d) formulas) are accumulated.  Not graph-capture safe: disable it before
+ * capturing.
+ * ------------------------------------------------------------------------- */
+int mde_timing_enable(int on);
+int mde_timing_reset(void);
+/* Resolves pending events (synchronises on them) into per-kernel totals. */
+int mde_timing_collect(void);
+int mde_kernel_count(void);
+const char* mde_kernel_name(int kid);
+int mde_timing_query(int kid, double* total_ms, int64_t* launches,
+                     double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MDE_ABI_H */

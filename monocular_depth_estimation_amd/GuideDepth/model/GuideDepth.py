@@ -1,0 +1,34 @@
+"""GuideDepth on MI355X: DDRNet-23-slim encoder + three guided-upsampling blocks.
+
+Drop-in for src/GuideDepth/model/GuideDepth.py:9-57 (constructor, forward,
+471 state_dict keys).  The nearest guides (:46-47) and the three x2 bilinear
+upsamples (:49, :52, :55) run on the HIP resize kernels.
+"""
+from __future__ import annotations
+
+from torch import nn
+
+from ...functional import bilinear_resize, nearest_resize
+from .DDRNet_23_slim import DualResNet_Backbone
+from .modules import Guided_Upsampling_Block
+
+
+class GuideDepth(nn.Module):
+    def __init__(self, pretrained=True, up_features=[64, 32, 16],  # noqa: B006 (reference signature)
+                 inner_features=[64, 32, 16]):
+        super().__init__()
+        self.feature_extractor = DualResNet_Backbone(pretrained=pretrained,
+                                                     features=up_features[0])
+        outs = [up_features[1], up_features[2], 1]
+        for i in range(3):
+            setattr(self, f"up_{i + 1}", Guided_Upsampling_Block(
+                in_features=up_features[i], expand_features=inner_features[i],
+                out_features=outs[i], kernel_size=3, channel_attention=True,
+                guide_features=3, guidance_type="full"))
+
+    def forward(self, x):
+        y = self.feature_extractor(x)
+        guides = (nearest_resize(x, scale_factor=0.25), nearest_resize(x, scale_factor=0.5), x)
+        for block, guide in zip((self.up_1, self.up_2, self.up_3), guides):
+            y = block(guide, bilinear_resize(y, scale_factor=2))
+        return y

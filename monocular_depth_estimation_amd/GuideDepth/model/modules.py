@@ -1,0 +1,92 @@
+"""Guided-upsampling and squeeze-excitation blocks on MI355X.
+
+Drop-in for src/GuideDepth/model/modules.py: same constructors, forward
+signatures and state_dict keys.  Hot ops on HIP kernels:
+  * cat([x, y], 1) + SELayer (:90, :21-25)  -> functional.se_cat (one fused op,
+    the concatenation is never materialised);
+  * reduce(residual + depth) (:100)          -> functional.skip_reduce.
+Convolutions + BatchNorm + ReLU stay on PyTorch-ROCm (MIOpen).
+"""
+from __future__ import annotations
+
+from torch import nn
+
+from ...functional import se_cat, skip_reduce
+
+
+class SELayer(nn.Module):
+    """Channel attention: mean_hw -> Linear -> ReLU -> Linear -> Sigmoid -> scale.
+
+    reference modules.py:5-25 (both Linear layers bias-free).
+    """
+
+    def __init__(self, channel, reduction=16):
+        super().__init__()
+        hidden = channel // reduction
+        self.fc = nn.Sequential(nn.Linear(channel, hidden, bias=False), nn.ReLU(inplace=True),
+                                nn.Linear(hidden, channel, bias=False), nn.Sigmoid())
+
+    def forward(self, x):
+        return se_cat(x, None, self.fc[0].weight, self.fc[2].weight)
+
+    def forward_cat(self, x, y):
+        """SELayer(torch.cat([x, y], 1)) without materialising the concatenation."""
+        return se_cat(x, y, self.fc[0].weight, self.fc[2].weight)
+
+
+def _conv_bn_relu(cin, cout, k):
+    return [nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2), nn.BatchNorm2d(cout),
+            nn.ReLU(inplace=True)]
+
+
+class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
+    """Refines an upsampled depth feature map with the RGB guide (modules.py:29-100).
+
+    feature_conv(depth) and guide_conv(guide) each: kxk conv -> BN -> ReLU ->
+    1x1 conv (E -> E/2) -> BN -> ReLU.  Their concatenation goes through SE,
+    comb_conv (kxk conv -> BN -> ReLU -> 1x1 -> BN -> ReLU), and the result
+    plus `depth` goes through the 1x1 `reduce` conv.
+    """
+
+    def __init__(self, in_features, expand_features, out_features, kernel_size=3,
+                 channel_attention=True, guidance_type="full", guide_features=3):
+        super().__init__()
+        self.channel_attention = channel_attention
+        self.guidance_type = guidance_type
+        self.guide_features = guide_features
+        self.in_features = in_features
+        e, k = expand_features, kernel_size
+        self.feature_conv = nn.Sequential(*_conv_bn_relu(in_features, e, k),
+                                          *_conv_bn_relu(e, e // 2, 1))
+        if guidance_type == "full":
+            self.guide_conv = nn.Sequential(*_conv_bn_relu(guide_features, e, k),
+                                            *_conv_bn_relu(e, e // 2, 1))
+            comb_features = (e // 2) * 2
+        elif guidance_type == "raw":
+            comb_features = e // 2 + guide_features
+        else:
+            comb_features = e // 2
+        self.comb_conv = nn.Sequential(*_conv_bn_relu(comb_features, e, k),
+                                       *_conv_bn_relu(e, in_features, 1))
+        self.reduce = nn.Conv2d(in_features, out_features, kernel_size=1)
+        if channel_attention:
+            self.SE_block = SELayer(comb_features, reduction=1)
+
+    def forward(self, guide, depth):
+        x = self.feature_conv(depth)
+        if self.guidance_type == "full":
+            second = self.guide_conv(guide)
+        elif self.guidance_type == "raw":
+            second = guide
+        else:
+            second = None
+        if self.channel_attention:
+            xy = self.SE_block.forward_cat(x, second) if second is not None else self.SE_block(x)
+        else:
+            xy = x if second is None else _cat(x, second)
+        return skip_reduce(self.comb_conv(xy), depth, self.reduce.weight, self.reduce.bias)
+
+
+def _cat(x, y):
+    import torch
+    return torch.cat([x, y], dim=1)

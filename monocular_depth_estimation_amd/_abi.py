@@ -1,0 +1,144 @@
+"""ctypes binding of libmde_hip.so (the C ABI declared in include/mde_abi.h).
+
+This is the only place the shared library is loaded.  There is no fallback:
+if the library is missing, or a GPU op is called on a CPU tensor, the call
+raises.  torch must be imported first so that the HIP runtime torch ships
+(SONAME libamdhip64.so.7) is the one the library binds to — the library then
+shares torch's device context and streams.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads torch's libamdhip64 before ours)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmde_hip.so")
+
+MDE_F32 = 0
+MDE_BF16 = 1
+
+_c = ctypes
+_vp = _c.c_void_p
+_i64 = _c.c_int64
+_f32 = _c.c_float
+_int = _c.c_int
+_sz = _c.c_size_t
+_fp = _c.POINTER(_c.c_float)
+
+# name -> (restype, argtypes); mirrors include/mde_abi.h exactly.
+SIGNATURES = {
+    "mde_abi_version": (_int, []),
+    "mde_status_string": (_c.c_char_p, [_int]),
+    "mde_bilinear_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _int, _vp]),
+    "mde_bilinear_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _int, _vp]),
+    "mde_nearest_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _vp]),
+    "mde_nearest_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _vp]),
+    "mde_se_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_se_fwd": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                          _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_se_bwd": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp,
+                          _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_skip_reduce_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_skip_reduce_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_skip_reduce_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                                   _vp, _int, _vp]),
+    "mde_minmax_workspace": (_sz, [_i64]),
+    "mde_minmax": (_int, [_vp, _i64, _vp, _vp, _int, _vp]),
+    "mde_depthnorm_apply": (_int, [_vp, _vp, _vp, _i64, _int, _vp]),
+    "mde_ssim3_l1_workspace": (_sz, [_i64, _i64, _i64]),
+    "mde_ssim3_l1_fwd": (_int, [_vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_depth_loss_workspace": (_sz, [_i64, _i64, _i64]),
+    "mde_depth_loss_fwd": (_int, [_vp, _vp, _f32, _f32, _f32, _f32, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_depth_loss_bwd": (_int, [_vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _vp, _i64, _i64, _i64,
+                                  _vp, _int, _vp]),
+    "mde_timing_enable": (_int, [_int]),
+    "mde_timing_reset": (_int, []),
+    "mde_timing_collect": (_int, []),
+    "mde_kernel_count": (_int, []),
+    "mde_kernel_name": (_c.c_char_p, [_int]),
+    "mde_timing_query": (_int, [_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64),
+                                _c.POINTER(_c.c_double)]),
+}
+
+
+class MdeError(RuntimeError):
+    """A non-zero status from libmde_hip.so."""
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the library; raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(make -C monocular_depth_estimation_amd/csrc). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        msg = load().mde_status_string(status).decode()
+        raise MdeError(f"{what} failed with status {status}: {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(load(), name)(*args), name)
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a tensor (None passes NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_of(t) -> int:
+    """Handle of torch's current stream on t's device (the launch stream)."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def dtype_code(t) -> int:
+    if t.dtype == torch.float32:
+        return MDE_F32
+    if t.dtype == torch.bfloat16:
+        return MDE_BF16
+    raise TypeError(f"unsupported dtype {t.dtype} (the HIP kernels take float32)")
+
+
+# --------------------------------------------------------------------- timing
+def timing_enable(on: bool) -> None:
+    call("mde_timing_enable", 1 if on else 0)
+
+
+def timing_reset() -> None:
+    call("mde_timing_reset")
+
+
+def timing_collect() -> dict:
+    """Resolve pending events; return {kernel: (total_ms, launches, bytes)}."""
+    lib = load()
+    check(lib.mde_timing_collect(), "mde_timing_collect")
+    out = {}
+    for k in range(lib.mde_kernel_count()):
+        ms, n, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+        check(lib.mde_timing_query(k, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by)),
+              "mde_timing_query")
+        if n.value:
+            out[lib.mde_kernel_name(k).decode()] = (ms.value, n.value, by.value)
+    return out

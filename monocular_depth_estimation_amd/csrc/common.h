@@ -1,0 +1,84 @@
+// Shared helpers for the gfx950 kernels behind include/mde_abi.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "mde_abi.h"
+
+namespace mde {
+
+// Kernel ids of the timing registry (mde_kernel_name gives the strings).
+enum Kid : int {
+  K_BILINEAR_FWD = 0,
+  K_BILINEAR_BWD,
+  K_NEAREST_FWD,
+  K_NEAREST_BWD,
+  K_SE_SQUEEZE,
+  K_SE_FC,
+  K_SE_SCALE,
+  K_SE_BWD_DOT,
+  K_SE_BWD_FC,
+  K_SE_BWD_APPLY,
+  K_SKIP_FWD,
+  K_SKIP_BWD,
+  K_SKIP_BWD_REDUCE,
+  K_MINMAX,
+  K_MINMAX_FINAL,
+  K_DEPTHNORM,
+  K_SSIM3_L1,
+  K_LOSS_FINAL,
+  K_DLOSS_FWD,
+  K_DLOSS_BWD_COEF,
+  K_DLOSS_BWD,
+  K_COUNT
+};
+
+// Timing hooks (timing.hip).  begin() returns a token for end(); both are
+// no-ops when the registry is disabled.
+int timing_begin(int kid, hipStream_t s);
+void timing_end(int token, hipStream_t s, double bytes);
+
+// Launch a kernel with optional timing and return the launch status.
+#define MDE_LAUNCH(KID, BYTES, STREAM, KERNEL, GRID, BLOCK, SHMEM, ...)      \
+  do {                                                                     \
+    int _tok = ::mde::timing_begin((KID), (STREAM));                       \
+    hipLaunchKernelGGL(KERNEL, (GRID), (BLOCK), (SHMEM), (STREAM),         \
+                       __VA_ARGS__);                                       \
+    hipError_t _e = hipGetLastError();                                     \
+    ::mde::timing_end(_tok, (STREAM), (double)(BYTES));                    \
+    if (_e != hipSuccess) return (int)_e;                                  \
+  } while (0)
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Wave64 reductions.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block reduction of a float sum for blockDim.x == 256 (4 waves).  `red`
+// must hold 4 floats of LDS.  Result valid in every thread.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) red[wid] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+}  // namespace mde

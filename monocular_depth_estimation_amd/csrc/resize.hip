@@ -1,0 +1,309 @@
+// Bilinear and nearest resizes (NCHW, fp32) for gfx950.
+//
+// Index math follows ATen's area_pixel_compute_source_index /
+// nearest_neighbor_compute_source_index so the sampled pixels and the
+// interpolation weights are the ones the reference's F.interpolate calls use
+// (src/GuideDepth/model/GuideDepth.py:46-55, DDRNet_23_slim.py:182-191,
+// 332-351).  Products are written with __fmul_rn/__fadd_rn so hipcc cannot
+// contract them into FMAs: a contracted source index could floor to a
+// different pixel than the reference near integer boundaries.
+//
+// Backward is a gather: every input pixel sums the output gradients whose
+// stencil touches it, so there are no atomics and gx is written exactly once.
+#include "common.h"
+
+namespace {
+
+struct Lin {
+  int i0, i1;
+  float l0, l1;
+};
+
+__device__ __forceinline__ float src_index(float scale, int dst, int align) {
+  if (align) return __fmul_rn(scale, (float)dst);
+  float s = __fadd_rn(__fmul_rn(scale, __fadd_rn((float)dst, 0.5f)), -0.5f);
+  return s < 0.f ? 0.f : s;
+}
+
+__device__ __forceinline__ Lin lin_index(float scale, int dst, int in_size,
+                                         int align) {
+  const float s = src_index(scale, dst, align);
+  int i0 = (int)s;  // s >= 0, so truncation is floor
+  if (i0 > in_size - 1) i0 = in_size - 1;
+  const int i1 = i0 + (i0 < in_size - 1 ? 1 : 0);
+  float l1 = __fadd_rn(s, -(float)i0);
+  l1 = fminf(fmaxf(l1, 0.f), 1.f);
+  return {i0, i1, __fadd_rn(1.f, -l1), l1};
+}
+
+// Weight with which output index `o` reads input index `i` along one axis.
+__device__ __forceinline__ float lin_weight(float scale, int o, int i,
+                                            int in_size, int align) {
+  const Lin L = lin_index(scale, o, in_size, align);
+  float w = 0.f;
+  if (L.i0 == i) w += L.l0;
+  if (L.i1 == i) w += L.l1;
+  return w;
+}
+
+// Output-index window that can read input index i (generic ratios).
+__device__ __forceinline__ void lin_window(float scale, int i, int out_size,
+                                           int* lo, int* hi) {
+  if (!(scale > 0.f)) {
+    *lo = 0;
+    *hi = out_size - 1;
+    return;
+  }
+  const int a = (int)floorf(((float)i - 1.f) / scale) - 2;
+  const int b = (int)ceilf(((float)i + 2.f) / scale) + 1;
+  *lo = a < 0 ? 0 : a;
+  *hi = b > out_size - 1 ? out_size - 1 : b;
+}
+
+// Forward: each thread produces VEC consecutive outputs of one output row.
+template <int VEC>
+__global__ void __launch_bounds__(256)
+    bilinear_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                        int64_t rows, int hi, int wi, int ho, int wo,
+                        float sh, float sw, int align) {
+  const int chunks = (wo + VEC - 1) / VEC;
+  const int64_t total = rows * chunks;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int ch = (int)(t % chunks);
+    const int64_t row = t / chunks;  // = plane * ho + oh
+    const int oh = (int)(row % ho);
+    const int64_t plane = row / ho;
+    const Lin H = lin_index(sh, oh, hi, align);
+    const float* r0 = x + (plane * hi + H.i0) * (int64_t)wi;
+    const float* r1 = x + (plane * hi + H.i1) * (int64_t)wi;
+    float v[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      const int ow = ch * VEC + k;
+      if (ow < wo) {
+        const Lin W = lin_index(sw, ow, wi, align);
+        v[k] = H.l0 * (W.l0 * r0[W.i0] + W.l1 * r0[W.i1]) +
+               H.l1 * (W.l0 * r1[W.i0] + W.l1 * r1[W.i1]);
+      }
+    }
+    float* out = y + row * (int64_t)wo + ch * VEC;
+    if (VEC == 4 && ch * VEC + 4 <= wo) {
+      *reinterpret_cast<float4*>(out) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k)
+        if (ch * VEC + k < wo) out[k] = v[k];
+    }
+  }
+}
+
+// Backward, exact x2 (align_corners=False, scale 0.5, out = 2*in): input
+// index i is read by output indices 2i-1 .. 2i+2 only.
+__global__ void __launch_bounds__(256)
+    bilinear_bwd_x2_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                           int64_t planes, int hi, int wi) {
+  const int ho = 2 * hi, wo = 2 * wi;
+  const int64_t total = planes * hi * (int64_t)wi;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % wi);
+    const int64_t r = t / wi;
+    const int i = (int)(r % hi);
+    const int64_t plane = r / hi;
+    float wr[4], wc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int o = 2 * i - 1 + k;
+      wr[k] = (o >= 0 && o < ho) ? lin_weight(0.5f, o, i, hi, 0) : 0.f;
+      const int p = 2 * j - 1 + k;
+      wc[k] = (p >= 0 && p < wo) ? lin_weight(0.5f, p, j, wi, 0) : 0.f;
+    }
+    const float* g = gy + plane * ho * (int64_t)wo;
+    float acc = 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      if (wr[a] != 0.f) {
+        const float* grow = g + (int64_t)(2 * i - 1 + a) * wo;
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          if (wc[b] != 0.f) acc += (wr[a] * wc[b]) * grow[2 * j - 1 + b];
+      }
+    }
+    gx[t] = acc;
+  }
+}
+
+// Backward, generic ratio: candidate windows per axis, exact weights.
+__global__ void __launch_bounds__(256)
+    bilinear_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                        int64_t planes, int hi, int wi, int ho, int wo,
+                        float sh, float sw, int align) {
+  const int64_t total = planes * hi * (int64_t)wi;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % wi);
+    const int64_t r = t / wi;
+    const int i = (int)(r % hi);
+    const int64_t plane = r / hi;
+    int rlo, rhi, clo, chi;
+    lin_window(sh, i, ho, &rlo, &rhi);
+    lin_window(sw, j, wo, &clo, &chi);
+    const float* g = gy + plane * ho * (int64_t)wo;
+    float acc = 0.f;
+    for (int o = rlo; o <= rhi; ++o) {
+      const float wr = lin_weight(sh, o, i, hi, align);
+      if (wr == 0.f) continue;
+      const float* grow = g + (int64_t)o * wo;
+      for (int p = clo; p <= chi; ++p) {
+        const float wc = lin_weight(sw, p, j, wi, align);
+        if (wc != 0.f) acc += (wr * wc) * grow[p];
+      }
+    }
+    gx[t] = acc;
+  }
+}
+
+__device__ __forceinline__ int nearest_src(float scale, int dst, int in_size) {
+  const int s = (int)floorf(__fmul_rn((float)dst, scale));
+  return s < in_size - 1 ? s : in_size - 1;
+}
+
+__global__ void __launch_bounds__(256)
+    nearest_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+                       int64_t planes, int hi, int wi, int ho, int wo,
+                       float sh, float sw) {
+  const int64_t total = planes * ho * (int64_t)wo;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int ow = (int)(t % wo);
+    const int64_t r = t / wo;
+    const int oh = (int)(r % ho);
+    const int64_t plane = r / ho;
+    y[t] = x[(plane * hi + nearest_src(sh, oh, hi)) * (int64_t)wi +
+             nearest_src(sw, ow, wi)];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    nearest_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                       int64_t planes, int hi, int wi, int ho, int wo,
+                       float sh, float sw) {
+  const int64_t total = planes * hi * (int64_t)wi;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % wi);
+    const int64_t r = t / wi;
+    const int i = (int)(r % hi);
+    const int64_t plane = r / hi;
+    // outputs o with floor(o*scale) == i lie in [i/scale - 1, (i+1)/scale + 1]
+    int rlo = sh > 0.f ? (int)floorf((float)i / sh) - 1 : 0;
+    int rhi = sh > 0.f ? (int)ceilf((float)(i + 1) / sh) + 1 : ho - 1;
+    int clo = sw > 0.f ? (int)floorf((float)j / sw) - 1 : 0;
+    int chi = sw > 0.f ? (int)ceilf((float)(j + 1) / sw) + 1 : wo - 1;
+    rlo = rlo < 0 ? 0 : rlo;
+    clo = clo < 0 ? 0 : clo;
+    rhi = rhi > ho - 1 ? ho - 1 : rhi;
+    chi = chi > wo - 1 ? wo - 1 : chi;
+    const float* g = gy + plane * ho * (int64_t)wo;
+    float acc = 0.f;
+    for (int o = rlo; o <= rhi; ++o) {
+      if (nearest_src(sh, o, hi) != i) continue;
+      for (int p = clo; p <= chi; ++p)
+        if (nearest_src(sw, p, wi) == j) acc += g[(int64_t)o * wo + p];
+    }
+    gx[t] = acc;
+  }
+}
+
+inline int grid_for(int64_t work) {
+  const int64_t b = mde::cdiv(work, 256);
+  return (int)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
+}
+
+bool dims_ok(int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
+             int64_t wo) {
+  return n > 0 && c > 0 && hi > 0 && wi > 0 && ho > 0 && wo > 0 &&
+         hi < (1 << 30) && wi < (1 << 30) && ho < (1 << 30) && wo < (1 << 30);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
+                     int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                     float scale_w, int align_corners, int dtype,
+                     void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !y || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t rows = n * c * ho;
+  const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
+  if (wo % 4 == 0) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_kernel<4>,
+               dim3(grid_for(rows * (wo / 4))), dim3(256), 0,
+               (const float*)x, (float*)y, rows, (int)hi, (int)wi, (int)ho,
+               (int)wo, scale_h, scale_w, align_corners);
+  } else {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_kernel<1>,
+               dim3(grid_for(rows * wo)), dim3(256), 0, (const float*)x,
+               (float*)y, rows, (int)hi, (int)wi, (int)ho, (int)wo, scale_h,
+               scale_w, align_corners);
+  }
+  return MDE_OK;
+}
+
+int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
+                     int64_t hi, int64_t wi, int64_t ho, int64_t wo,
+                     float scale_h, float scale_w, int align_corners,
+                     int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !gx || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t planes = n * c;
+  const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
+  const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
+                  ho == 2 * hi && wo == 2 * wi;
+  if (x2) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
+               dim3(grid_for(planes * hi * wi)), dim3(256), 0,
+               (const float*)gy, (float*)gx, planes, (int)hi, (int)wi);
+  } else {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_kernel,
+               dim3(grid_for(planes * hi * wi)), dim3(256), 0,
+               (const float*)gy, (float*)gx, planes, (int)hi, (int)wi,
+               (int)ho, (int)wo, scale_h, scale_w, align_corners);
+  }
+  return MDE_OK;
+}
+
+int mde_nearest_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
+                    int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                    float scale_w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !y || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const double bytes = 8.0 * n * c * (double)(ho * wo);
+  MDE_LAUNCH(mde::K_NEAREST_FWD, bytes, s, nearest_fwd_kernel,
+             dim3(grid_for(n * c * ho * wo)), dim3(256), 0, (const float*)x,
+             (float*)y, n * c, (int)hi, (int)wi, (int)ho, (int)wo, scale_h,
+             scale_w);
+  return MDE_OK;
+}
+
+int mde_nearest_bwd(const void* gy, void* gx, int64_t n, int64_t c, int64_t hi,
+                    int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                    float scale_w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !gx || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
+  MDE_LAUNCH(mde::K_NEAREST_BWD, bytes, s, nearest_bwd_kernel,
+             dim3(grid_for(n * c * hi * wi)), dim3(256), 0, (const float*)gy,
+             (float*)gx, n * c, (int)hi, (int)wi, (int)ho, (int)wo, scale_h,
+             scale_w);
+  return MDE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,327 @@
+// Squeeze-excitation over a fused channel concatenation (NCHW, fp32).
+//
+// Reference: torch.cat([x, y], 1) (src/GuideDepth/model/modules.py:90) feeding
+// SELayer.forward (modules.py:21-25): mean over H,W -> Linear(C,C/r) -> ReLU
+// -> Linear(C/r,C) -> Sigmoid -> x * s.  The concatenation is never
+// materialised: channel ch < ca reads xa, otherwise xb.
+//
+// Forward  = squeeze (per-plane partial sums, deterministic two-level
+//            reduction) -> fc (one block per sample) -> scale (streaming).
+// Backward = dot (partial sums of g*x) -> fc backward (per sample) ->
+//            weight gradients (sum over samples in fixed order) -> apply.
+#include "common.h"
+
+namespace {
+
+constexpr int kChunk = 16384;  // elements of one plane reduced by one block
+
+__device__ __forceinline__ const float* plane_ptr(const float* xa, int64_t ca,
+                                                  const float* xb, int64_t cb,
+                                                  int64_t nidx, int64_t ch,
+                                                  int64_t hw) {
+  return ch < ca ? xa + (nidx * ca + ch) * hw
+                 : xb + (nidx * cb + (ch - ca)) * hw;
+}
+
+// part[plane * chunks + k] = sum of chunk k of plane (optionally of g*x).
+template <bool DOT>
+__global__ void __launch_bounds__(256)
+    se_partial_kernel(const float* __restrict__ g, const float* __restrict__ xa,
+                      int64_t ca, const float* __restrict__ xb, int64_t cb,
+                      int64_t hw, int chunks, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int64_t c = ca + cb;
+  const int64_t plane = blockIdx.y;
+  const int64_t nidx = plane / c, ch = plane % c;
+  const float* x = plane_ptr(xa, ca, xb, cb, nidx, ch, hw);
+  const float* gp = DOT ? g + plane * hw : nullptr;
+  const int64_t beg = (int64_t)blockIdx.x * kChunk;
+  const int64_t end = beg + kChunk < hw ? beg + kChunk : hw;
+  float acc = 0.f;
+  if ((hw & 3) == 0) {
+    for (int64_t i = beg + 4 * threadIdx.x; i < end; i += 4 * 256) {
+      const float4 v = *reinterpret_cast<const float4*>(x + i);
+      if (DOT) {
+        const float4 q = *reinterpret_cast<const float4*>(gp + i);
+        acc += (v.x * q.x + v.y * q.y) + (v.z * q.z + v.w * q.w);
+      } else {
+        acc += (v.x + v.y) + (v.z + v.w);
+      }
+    }
+  } else {
+    for (int64_t i = beg + threadIdx.x; i < end; i += 256)
+      acc += DOT ? x[i] * gp[i] : x[i];
+  }
+  const float tot = mde::block_sum256(acc, red);
+  if (threadIdx.x == 0) part[plane * chunks + blockIdx.x] = tot;
+}
+
+// One block per sample: mean -> hidden = relu(W1 m) -> s = sigmoid(W2 h).
+__global__ void __launch_bounds__(256)
+    se_fc_kernel(const float* __restrict__ part, int chunks, int c, int cr,
+                 float inv_hw, const float* __restrict__ w1,
+                 const float* __restrict__ w2, float* __restrict__ s,
+                 float* __restrict__ hidden, float* __restrict__ mean) {
+  extern __shared__ float sm[];
+  float* m = sm;       // [c]
+  float* hdn = sm + c; // [cr]
+  const int nidx = blockIdx.x;
+  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
+    const float* p = part + ((int64_t)nidx * c + ch) * chunks;
+    float acc = 0.f;
+    for (int k = 0; k < chunks; ++k) acc += p[k];
+    m[ch] = acc * inv_hw;
+    mean[(int64_t)nidx * c + ch] = m[ch];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < cr; j += blockDim.x) {
+    const float* wr = w1 + (int64_t)j * c;
+    float acc = 0.f;
+    for (int ch = 0; ch < c; ++ch) acc += wr[ch] * m[ch];
+    acc = acc > 0.f ? acc : 0.f;
+    hdn[j] = acc;
+    hidden[(int64_t)nidx * cr + j] = acc;
+  }
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
+    const float* wr = w2 + (int64_t)ch * cr;
+    float z = 0.f;
+    for (int j = 0; j < cr; ++j) z += wr[j] * hdn[j];
+    s[(int64_t)nidx * c + ch] = 1.f / (1.f + expf(-z));
+  }
+}
+
+// out[plane, i] = x[plane, i] * s[plane]  (cat fused: plane -> xa or xb)
+__global__ void __launch_bounds__(256)
+    se_scale_kernel(const float* __restrict__ xa, int64_t ca,
+                    const float* __restrict__ xb, int64_t cb, int64_t hw,
+                    int64_t planes, const float* __restrict__ s,
+                    float* __restrict__ out) {
+  const int64_t c = ca + cb;
+  if ((hw & 3) == 0) {
+    const int64_t hw4 = hw >> 2;
+    const int64_t total = planes * hw4;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t plane = t / hw4, i = (t - plane * hw4) << 2;
+      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, plane % c, hw);
+      const float sc = s[plane];
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
+      *reinterpret_cast<float4*>(out + plane * hw + i) = v;
+    }
+  } else {
+    const int64_t total = planes * hw;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t plane = t / hw, i = t - plane * hw;
+      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, plane % c, hw);
+      out[t] = x[i] * s[plane];
+    }
+  }
+}
+
+// Per-sample backward through sigmoid / W2 / relu / W1.
+//   ds = sum g*x;  dz = ds s (1-s);  dh = (h>0) W2^T dz;  dm = W1^T dh
+__global__ void __launch_bounds__(256)
+    se_bwd_fc_kernel(const float* __restrict__ part, int chunks, int c, int cr,
+                     const float* __restrict__ w1, const float* __restrict__ w2,
+                     const float* __restrict__ s,
+                     const float* __restrict__ hidden, float* __restrict__ dz,
+                     float* __restrict__ dh, float* __restrict__ dm) {
+  extern __shared__ float sm[];
+  float* z = sm;        // [c]
+  float* hh = sm + c;   // [cr]
+  const int nidx = blockIdx.x;
+  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
+    const float* p = part + ((int64_t)nidx * c + ch) * chunks;
+    float acc = 0.f;
+    for (int k = 0; k < chunks; ++k) acc += p[k];
+    const float sv = s[(int64_t)nidx * c + ch];
+    const float v = acc * (sv * (1.f - sv));
+    z[ch] = v;
+    dz[(int64_t)nidx * c + ch] = v;
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < cr; j += blockDim.x) {
+    float acc = 0.f;
+    for (int ch = 0; ch < c; ++ch) acc += w2[(int64_t)ch * cr + j] * z[ch];
+    const float v = hidden[(int64_t)nidx * cr + j] > 0.f ? acc : 0.f;
+    hh[j] = v;
+    dh[(int64_t)nidx * cr + j] = v;
+  }
+  __syncthreads();
+  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
+    float acc = 0.f;
+    for (int j = 0; j < cr; ++j) acc += w1[(int64_t)j * c + ch] * hh[j];
+    dm[(int64_t)nidx * c + ch] = acc;
+  }
+}
+
+// gw2[ch, j] = sum_n dz[n,ch] h[n,j];  gw1[j, ch] = sum_n dh[n,j] m[n,ch]
+__global__ void __launch_bounds__(256)
+    se_wgrad_kernel(int n, int c, int cr, const float* __restrict__ dz,
+                    const float* __restrict__ dh,
+                    const float* __restrict__ hidden,
+                    const float* __restrict__ mean, float* __restrict__ gw1,
+                    float* __restrict__ gw2) {
+  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t pairs = (int64_t)c * cr;
+  if (t < pairs) {
+    const int ch = (int)(t / cr), j = (int)(t % cr);
+    float acc = 0.f;
+    for (int k = 0; k < n; ++k)
+      acc += dz[(int64_t)k * c + ch] * hidden[(int64_t)k * cr + j];
+    gw2[t] = acc;  // row-major [c, cr]
+  } else if (t < 2 * pairs) {
+    const int64_t u = t - pairs;
+    const int j = (int)(u / c), ch = (int)(u % c);
+    float acc = 0.f;
+    for (int k = 0; k < n; ++k)
+      acc += dh[(int64_t)k * cr + j] * mean[(int64_t)k * c + ch];
+    gw1[u] = acc;  // row-major [cr, c]
+  }
+}
+
+// gx = g * s + dm / hw, written to gxa / gxb (either may be null).
+__global__ void __launch_bounds__(256)
+    se_apply_kernel(const float* __restrict__ g, int64_t ca, int64_t cb,
+                    int64_t hw, int64_t planes, const float* __restrict__ s,
+                    const float* __restrict__ dm, float inv_hw,
+                    float* __restrict__ gxa, float* __restrict__ gxb) {
+  const int64_t c = ca + cb;
+  if ((hw & 3) == 0) {
+    const int64_t hw4 = hw >> 2;
+    const int64_t total = planes * hw4;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t plane = t / hw4, i = (t - plane * hw4) << 2;
+      const int64_t nidx = plane / c, ch = plane % c;
+      float* dst = ch < ca ? (gxa ? gxa + (nidx * ca + ch) * hw : nullptr)
+                           : (gxb ? gxb + (nidx * cb + ch - ca) * hw : nullptr);
+      if (!dst) continue;
+      const float sc = s[plane], add = dm[plane] * inv_hw;
+      const float4 q = *reinterpret_cast<const float4*>(g + plane * hw + i);
+      *reinterpret_cast<float4*>(dst + i) =
+          make_float4(q.x * sc + add, q.y * sc + add, q.z * sc + add,
+                      q.w * sc + add);
+    }
+  } else {
+    const int64_t total = planes * hw;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t plane = t / hw, i = t - plane * hw;
+      const int64_t nidx = plane / c, ch = plane % c;
+      float* dst = ch < ca ? (gxa ? gxa + (nidx * ca + ch) * hw : nullptr)
+                           : (gxb ? gxb + (nidx * cb + ch - ca) * hw : nullptr);
+      if (dst) dst[i] = g[t] * s[plane] + dm[plane] * inv_hw;
+    }
+  }
+}
+
+inline int stream_grid(int64_t work) {
+  const int64_t b = mde::cdiv(work, 256);
+  return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
+struct SeWs {
+  float* part;
+  float* dz;
+  float* dh;
+  float* dm;
+};
+
+inline int64_t se_chunks(int64_t hw) { return mde::cdiv(hw, kChunk); }
+
+inline size_t round16(size_t b) { return (b + 15) & ~size_t(15); }
+
+SeWs se_carve(void* ws, int64_t n, int64_t c, int64_t cr, int64_t hw) {
+  char* p = (char*)ws;
+  SeWs r;
+  r.part = (float*)p;
+  p += round16(sizeof(float) * n * c * se_chunks(hw));
+  r.dz = (float*)p;
+  p += round16(sizeof(float) * n * c);
+  r.dh = (float*)p;
+  p += round16(sizeof(float) * n * cr);
+  r.dm = (float*)p;
+  return r;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t mde_se_workspace(int64_t n, int64_t c, int64_t cr, int64_t h,
+                        int64_t w) {
+  const int64_t hw = h * w;
+  return round16(sizeof(float) * n * c * se_chunks(hw)) +
+         round16(sizeof(float) * n * c) + round16(sizeof(float) * n * cr) +
+         round16(sizeof(float) * n * c);
+}
+
+int mde_se_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
+               const float* w1, const float* w2, int64_t cr, void* out,
+               float* s, float* hidden, float* mean, int64_t n, int64_t h,
+               int64_t w, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t c = ca + cb, hw = h * w;
+  if (!xa || ca <= 0 || cb < 0 || (cb > 0 && !xb) || !w1 || !w2 || cr <= 0 ||
+      !out || !s || !hidden || !mean || n <= 0 || hw <= 0 || !workspace ||
+      c > 4096 || cr > 4096 || n > 65535)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  SeWs ws = se_carve(workspace, n, c, cr, hw);
+  const int chunks = (int)se_chunks(hw);
+  const double big = 4.0 * n * c * (double)hw;
+  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<false>,
+             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr,
+             (const float*)xa, ca, (const float*)xb, cb, hw, chunks, ws.part);
+  MDE_LAUNCH(mde::K_SE_FC, 4.0 * (2.0 * c * cr + 3.0 * n * c), st,
+             se_fc_kernel, dim3((unsigned)n), dim3(256),
+             sizeof(float) * (c + cr), ws.part, chunks, (int)c, (int)cr,
+             1.f / (float)hw, w1, w2, s, hidden, mean);
+  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel,
+             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
+             (const float*)xa, ca, (const float*)xb, cb, hw, n * c, s,
+             (float*)out);
+  return MDE_OK;
+}
+
+int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
+               int64_t cb, const float* w1, const float* w2, int64_t cr,
+               const float* s, const float* hidden, const float* mean,
+               void* gxa, void* gxb, float* gw1, float* gw2, int64_t n,
+               int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t c = ca + cb, hw = h * w;
+  if (!gout || !xa || ca <= 0 || cb < 0 || (cb > 0 && !xb) || !w1 || !w2 ||
+      cr <= 0 || !s || !hidden || !mean || !gw1 || !gw2 || n <= 0 ||
+      hw <= 0 || !workspace || c > 4096 || cr > 4096 || n > 65535)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  SeWs ws = se_carve(workspace, n, c, cr, hw);
+  const int chunks = (int)se_chunks(hw);
+  const double big = 4.0 * n * c * (double)hw;
+  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, se_partial_kernel<true>,
+             dim3(chunks, (unsigned)(n * c)), dim3(256), 0,
+             (const float*)gout, (const float*)xa, ca, (const float*)xb, cb,
+             hw, chunks, ws.part);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 4.0 * n * c), st,
+             se_bwd_fc_kernel, dim3((unsigned)n), dim3(256),
+             sizeof(float) * (c + cr), ws.part, chunks, (int)c, (int)cr, w1,
+             w2, s, hidden, ws.dz, ws.dh, ws.dm);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 2.0 * n * (c + cr)), st,
+             se_wgrad_kernel, dim3((unsigned)mde::cdiv(2 * c * cr, 256)),
+             dim3(256), 0, (int)n, (int)c, (int)cr, ws.dz, ws.dh, hidden,
+             mean, gw1, gw2);
+  if (gxa || gxb) {
+    MDE_LAUNCH(mde::K_SE_BWD_APPLY, 2.0 * big, st, se_apply_kernel,
+               dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
+               (const float*)gout, ca, cb, hw, n * c, s, ws.dm,
+               1.f / (float)hw, (float*)gxa, (float*)gxb);
+  }
+  return MDE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,307 @@
+// Skip fusion of the guided-upsampling block (NCHW, fp32):
+//   out[n,o,p] = b[o] + sum_c W[o,c] * (r[n,c,p] + d[n,c,p])
+// Reference: `self.reduce(residual + depth)` (src/GuideDepth/model/modules.py:100),
+// reduce = nn.Conv2d(in_features, out_features, kernel_size=1) (modules.py:76-78).
+// The residual sum is never materialised: forward reads r and d once and
+// writes out once; backward re-forms r + d on the fly.
+//
+// Backward: gs[n,c,p] = sum_o W[o,c] g[n,o,p] (the gradient of both r and d),
+// gW = sum_{n,p} g (r+d)^T, gb = sum_{n,p} g.  gW/gb are reduced per block
+// into a slab (128-pixel tiles staged in LDS, register-blocked outer products)
+// and the slabs are summed in block order by a second kernel, so the result
+// is deterministic.
+#include "common.h"
+
+namespace {
+
+constexpr int kMaxC = 64;
+
+template <int CO, int PPT>
+__global__ void __launch_bounds__(256)
+    skip_fwd_kernel(const float* __restrict__ r, const float* __restrict__ d,
+                    const float* __restrict__ wt, const float* __restrict__ b,
+                    float* __restrict__ out, int64_t n, int cin, int cout,
+                    int64_t hw) {
+  __shared__ float sw[kMaxC * kMaxC];
+  __shared__ float sb[kMaxC];
+  for (int i = threadIdx.x; i < cin * cout; i += blockDim.x) sw[i] = wt[i];
+  for (int i = threadIdx.x; i < cout; i += blockDim.x) sb[i] = b[i];
+  __syncthreads();
+  const int64_t groups = hw / PPT;
+  const int64_t total = n * groups;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t nidx = t / groups;
+    const int64_t p = (t - nidx * groups) * PPT;
+    const float* rp = r + nidx * cin * hw + p;
+    const float* dp = d + nidx * cin * hw + p;
+    float acc[CO][PPT];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      const float bo = o < cout ? sb[o] : 0.f;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) acc[o][k] = bo;
+    }
+    for (int c = 0; c < cin; ++c) {
+      float s[PPT];
+      if (PPT == 4) {
+        const float4 a = *reinterpret_cast<const float4*>(rp + c * hw);
+        const float4 e = *reinterpret_cast<const float4*>(dp + c * hw);
+        s[0] = a.x + e.x; s[1 % PPT] = a.y + e.y;
+        s[2 % PPT] = a.z + e.z; s[3 % PPT] = a.w + e.w;
+      } else if (PPT == 2) {
+        const float2 a = *reinterpret_cast<const float2*>(rp + c * hw);
+        const float2 e = *reinterpret_cast<const float2*>(dp + c * hw);
+        s[0] = a.x + e.x; s[1 % PPT] = a.y + e.y;
+      } else {
+        s[0] = rp[c * hw] + dp[c * hw];
+      }
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        if (o < cout) {
+          const float wv = sw[o * cin + c];
+#pragma unroll
+          for (int k = 0; k < PPT; ++k) acc[o][k] += wv * s[k];
+        }
+      }
+    }
+    float* op = out + nidx * cout * hw + p;
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      if (o < cout) {
+        if (PPT == 4) {
+          *reinterpret_cast<float4*>(op + o * hw) = make_float4(
+              acc[o][0], acc[o][1 % PPT], acc[o][2 % PPT], acc[o][3 % PPT]);
+        } else if (PPT == 2) {
+          *reinterpret_cast<float2*>(op + o * hw) =
+              make_float2(acc[o][0], acc[o][1 % PPT]);
+        } else {
+          op[o * hw] = acc[o][0];
+        }
+      }
+    }
+  }
+}
+
+constexpr int kTile = 128;  // pixels per LDS tile == threads per block
+
+// FAST: cin == CI and cout == CO exactly; each thread owns an OB x CB block of
+// (o, c) pairs for the whole launch.  Otherwise (generic) pairs are strided
+// over threads and accumulated in LDS.
+template <int CI, int CO, int OB, int CB, bool FAST>
+__global__ void __launch_bounds__(kTile)
+    skip_bwd_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                    const float* __restrict__ d, const float* __restrict__ wt,
+                    float* __restrict__ gs, float* __restrict__ slab, int64_t n,
+                    int cin, int cout, int64_t hw) {
+  extern __shared__ float lds[];
+  float* sw = lds;                               // [cout][cin] <= [CO][CI]
+  float* gl = sw + CI * CO;                      // [kTile][CO + 1]
+  float* sl = gl + kTile * (CO + 1);             // [kTile][CI + 1]
+  float* accl = sl + kTile * (CI + 1);           // generic: [cout*cin + cout]
+  const int tid = threadIdx.x;
+  for (int i = tid; i < cin * cout; i += kTile) sw[i] = wt[i];
+  const int npairs = cout * cin;
+  if (!FAST)
+    for (int i = tid; i < npairs + cout; i += kTile) accl[i] = 0.f;
+  // FAST ownership: (ob, cb) block
+  constexpr int NCB = CI / CB;
+  const int ob = tid / NCB, cb = tid % NCB;
+  const bool owner = FAST && ob < CO / OB;
+  float acc[OB][CB];
+  float accb[OB];
+#pragma unroll
+  for (int i = 0; i < OB; ++i) {
+    accb[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < CB; ++j) acc[i][j] = 0.f;
+  }
+  __syncthreads();
+
+  const int64_t total = n * hw;
+  for (int64_t base = (int64_t)blockIdx.x * kTile; base < total;
+       base += (int64_t)gridDim.x * kTile) {
+    const int64_t q = base + tid;
+    float gv[CO];
+    if (q < total) {
+      const int64_t nidx = q / hw, p = q - nidx * hw;
+      const float* gp = g + nidx * cout * hw + p;
+#pragma unroll
+      for (int o = 0; o < CO; ++o) gv[o] = o < cout ? gp[o * hw] : 0.f;
+      const float* rp = r + nidx * cin * hw + p;
+      const float* dp = d + nidx * cin * hw + p;
+      float* gsp = gs + nidx * cin * hw + p;
+      for (int c = 0; c < cin; ++c) {
+        const float sv = rp[c * hw] + dp[c * hw];
+        sl[tid * (CI + 1) + c] = sv;
+        float a = 0.f;
+#pragma unroll
+        for (int o = 0; o < CO; ++o)
+          if (o < cout) a += sw[o * cin + c] * gv[o];
+        gsp[c * hw] = a;
+      }
+    } else {
+#pragma unroll
+      for (int o = 0; o < CO; ++o) gv[o] = 0.f;
+      for (int c = 0; c < cin; ++c) sl[tid * (CI + 1) + c] = 0.f;
+    }
+#pragma unroll
+    for (int o = 0; o < CO; ++o) gl[tid * (CO + 1) + o] = gv[o];
+    __syncthreads();
+    if (FAST) {
+      if (owner) {
+        for (int p = 0; p < kTile; ++p) {
+          float gg[OB], ss[CB];
+#pragma unroll
+          for (int i = 0; i < OB; ++i) gg[i] = gl[p * (CO + 1) + ob * OB + i];
+#pragma unroll
+          for (int j = 0; j < CB; ++j) ss[j] = sl[p * (CI + 1) + cb * CB + j];
+#pragma unroll
+          for (int i = 0; i < OB; ++i) {
+            if (cb == 0) accb[i] += gg[i];
+#pragma unroll
+            for (int j = 0; j < CB; ++j) acc[i][j] += gg[i] * ss[j];
+          }
+        }
+      }
+    } else {
+      for (int pr = tid; pr < npairs + cout; pr += kTile) {
+        float a = 0.f;
+        if (pr < npairs) {
+          const int o = pr / cin, c = pr % cin;
+          for (int p = 0; p < kTile; ++p)
+            a += gl[p * (CO + 1) + o] * sl[p * (CI + 1) + c];
+        } else {
+          const int o = pr - npairs;
+          for (int p = 0; p < kTile; ++p) a += gl[p * (CO + 1) + o];
+        }
+        accl[pr] += a;
+      }
+    }
+    __syncthreads();
+  }
+
+  float* out = slab + (int64_t)blockIdx.x * (npairs + cout);
+  if (FAST) {
+    if (owner) {
+#pragma unroll
+      for (int i = 0; i < OB; ++i) {
+        const int o = ob * OB + i;
+#pragma unroll
+        for (int j = 0; j < CB; ++j) out[o * cin + cb * CB + j] = acc[i][j];
+        if (cb == 0) out[npairs + o] = accb[i];
+      }
+    }
+  } else {
+    for (int pr = tid; pr < npairs + cout; pr += kTile) out[pr] = accl[pr];
+  }
+}
+
+// gw[pair] = sum over blocks (in block order) of slab[block][pair].
+__global__ void __launch_bounds__(256)
+    skip_slab_reduce_kernel(const float* __restrict__ slab, int nblocks,
+                            int npairs, int cout, float* __restrict__ gw,
+                            float* __restrict__ gb) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int stride = npairs + cout;
+  if (t >= stride) return;
+  float a = 0.f;
+  for (int k = 0; k < nblocks; ++k) a += slab[(int64_t)k * stride + t];
+  if (t < npairs)
+    gw[t] = a;
+  else
+    gb[t - npairs] = a;
+}
+
+inline int bwd_blocks(int64_t n, int64_t hw) {
+  const int64_t t = mde::cdiv(n * hw, kTile);
+  return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
+}
+
+template <int CI, int CO, bool FAST>
+constexpr size_t bwd_lds() {
+  return sizeof(float) * (CI * CO + kTile * (CO + 1) + kTile * (CI + 1) +
+                          (FAST ? 0 : CI * CO + CO));
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_skip_reduce_fwd(const void* r, const void* d, const float* wt,
+                        const float* b, void* out, int64_t n, int64_t cin,
+                        int64_t cout, int64_t h, int64_t w, int dtype,
+                        void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!r || !d || !wt || !b || !out || n <= 0 || hw <= 0 || cin <= 0 ||
+      cout <= 0 || cin > kMaxC || cout > kMaxC)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const double bytes = 4.0 * n * hw * (double)(2 * cin + cout);
+  auto grid = [&](int ppt) {
+    const int64_t blocks = mde::cdiv(n * hw / ppt, 256);
+    return dim3((unsigned)(blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks)));
+  };
+#define SKIP_FWD(CO_, PPT_)                                                  \
+  MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_kernel<CO_, PPT_>),        \
+             grid(PPT_), dim3(256), 0, (const float*)r, (const float*)d, wt, \
+             b, (float*)out, n, (int)cin, (int)cout, hw)
+  if (cout <= 1) {
+    if (hw % 4 == 0) SKIP_FWD(1, 4); else SKIP_FWD(1, 1);
+  } else if (cout <= 16) {
+    if (hw % 4 == 0) SKIP_FWD(16, 4); else SKIP_FWD(16, 1);
+  } else if (cout <= 32) {
+    if (hw % 2 == 0) SKIP_FWD(32, 2); else SKIP_FWD(32, 1);
+  } else {
+    SKIP_FWD(64, 1);
+  }
+#undef SKIP_FWD
+  return MDE_OK;
+}
+
+size_t mde_skip_reduce_workspace(int64_t n, int64_t cin, int64_t cout,
+                                 int64_t h, int64_t w) {
+  return sizeof(float) * (size_t)bwd_blocks(n, h * w) *
+         (size_t)(cin * cout + cout);
+}
+
+int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
+                        const float* wt, void* gs, float* gw, float* gb,
+                        int64_t n, int64_t cin, int64_t cout, int64_t h,
+                        int64_t w, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!gout || !r || !d || !wt || !gs || !gw || !gb || !workspace || n <= 0 ||
+      hw <= 0 || cin <= 0 || cout <= 0 || cin > kMaxC || cout > kMaxC)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = bwd_blocks(n, hw);
+  float* slab = (float*)workspace;
+  const double bytes = 4.0 * n * hw * (double)(2 * cin + cout + cin);
+#define SKIP_BWD(CI_, CO_, OB_, CB_, FAST_)                                   \
+  MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s,                                      \
+             (skip_bwd_kernel<CI_, CO_, OB_, CB_, FAST_>), dim3(nb),         \
+             dim3(kTile), (bwd_lds<CI_, CO_, FAST_>()), (const float*)gout,        \
+             (const float*)r, (const float*)d, wt, (float*)gs, slab, n,      \
+             (int)cin, (int)cout, hw)
+  if (cin == 64 && cout == 32) {
+    SKIP_BWD(64, 32, 4, 4, true);
+  } else if (cin == 32 && cout == 16) {
+    SKIP_BWD(32, 16, 2, 2, true);
+  } else if (cin == 16 && cout == 1) {
+    SKIP_BWD(16, 1, 1, 1, true);
+  } else if (cout <= 16) {
+    SKIP_BWD(64, 16, 1, 1, false);
+  } else {
+    SKIP_BWD(64, 64, 1, 1, false);
+  }
+#undef SKIP_BWD
+  const int stride = (int)(cin * cout + cout);
+  MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s,
+             skip_slab_reduce_kernel, dim3((unsigned)mde::cdiv(stride, 256)),
+             dim3(256), 0, slab, nb, (int)(cin * cout), (int)cout, gw, gb);
+  return MDE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,155 @@
+// Opt-in per-kernel timing registry behind mde_timing_* (include/mde_abi.h).
+// Each timed launch is bracketed by two hipEvents recorded on the launch
+// stream; mde_timing_collect() resolves them into per-kernel totals.
+#include <mutex>
+#include <vector>
+
+#include "common.h"
+
+namespace {
+
+const char* const kNames[mde::K_COUNT] = {
+    "bilinear_fwd",  "bilinear_bwd",    "nearest_fwd",   "nearest_bwd",
+    "se_squeeze",    "se_fc",           "se_scale",      "se_bwd_dot",
+    "se_bwd_fc",     "se_bwd_apply",    "skip_reduce_fwd", "skip_reduce_bwd",
+    "skip_reduce_bwd_reduce", "minmax", "minmax_final", "depthnorm_apply",
+    "ssim3_l1",      "loss_final",      "depth_loss_fwd", "depth_loss_bwd_coef",
+    "depth_loss_bwd"};
+
+struct Pending {
+  int kid;
+  hipEvent_t a, b;
+  double bytes;
+  bool done;
+};
+
+struct Registry {
+  std::mutex mu;
+  bool on = false;
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> pool;
+  double ms[mde::K_COUNT] = {};
+  int64_t launches[mde::K_COUNT] = {};
+  double bytes[mde::K_COUNT] = {};
+
+  hipEvent_t get() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+  }
+};
+
+Registry& reg() {
+  static Registry r;
+  return r;
+}
+
+}  // namespace
+
+namespace mde {
+
+int timing_begin(int kid, hipStream_t s) {
+  Registry& r = reg();
+  if (!r.on) return -1;
+  std::lock_guard<std::mutex> g(r.mu);
+  Pending p{kid, r.get(), r.get(), 0.0, false};
+  if (!p.a || !p.b) return -1;
+  (void)hipEventRecord(p.a, s);
+  r.pending.push_back(p);
+  return (int)r.pending.size() - 1;
+}
+
+void timing_end(int token, hipStream_t s, double bytes) {
+  if (token < 0) return;
+  Registry& r = reg();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (token >= (int)r.pending.size()) return;
+  Pending& p = r.pending[token];
+  (void)hipEventRecord(p.b, s);
+  p.bytes = bytes;
+  p.done = true;
+}
+
+}  // namespace mde
+
+extern "C" {
+
+int mde_timing_enable(int on) {
+  reg().on = on != 0;
+  return MDE_OK;
+}
+
+int mde_timing_reset(void) {
+  Registry& r = reg();
+  std::lock_guard<std::mutex> g(r.mu);
+  for (auto& p : r.pending) {
+    r.pool.push_back(p.a);
+    r.pool.push_back(p.b);
+  }
+  r.pending.clear();
+  for (int k = 0; k < mde::K_COUNT; ++k) {
+    r.ms[k] = 0.0;
+    r.launches[k] = 0;
+    r.bytes[k] = 0.0;
+  }
+  return MDE_OK;
+}
+
+int mde_timing_collect(void) {
+  Registry& r = reg();
+  std::lock_guard<std::mutex> g(r.mu);
+  int status = MDE_OK;
+  for (auto& p : r.pending) {
+    if (p.done) {
+      hipError_t e = hipEventSynchronize(p.b);
+      float t = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&t, p.a, p.b);
+      if (e == hipSuccess) {
+        r.ms[p.kid] += t;
+        r.launches[p.kid] += 1;
+        r.bytes[p.kid] += p.bytes;
+      } else {
+        status = (int)e;
+      }
+    }
+    r.pool.push_back(p.a);
+    r.pool.push_back(p.b);
+  }
+  r.pending.clear();
+  return status;
+}
+
+int mde_kernel_count(void) { return mde::K_COUNT; }
+
+const char* mde_kernel_name(int kid) {
+  if (kid < 0 || kid >= mde::K_COUNT) return "";
+  return kNames[kid];
+}
+
+int mde_timing_query(int kid, double* total_ms, int64_t* launches,
+                     double* bytes) {
+  if (kid < 0 || kid >= mde::K_COUNT) return MDE_ERR_INVALID_ARG;
+  Registry& r = reg();
+  std::lock_guard<std::mutex> g(r.mu);
+  if (total_ms) *total_ms = r.ms[kid];
+  if (launches) *launches = r.launches[kid];
+  if (bytes) *bytes = r.bytes[kid];
+  return MDE_OK;
+}
+
+int mde_abi_version(void) { return MDE_ABI_VERSION; }
+
+const char* mde_status_string(int status) {
+  if (status == MDE_OK) return "ok";
+  if (status == MDE_ERR_INVALID_ARG) return "mde: invalid argument";
+  if (status == MDE_ERR_UNSUPPORTED) return "mde: unsupported dtype/shape";
+  if (status > 0) return hipGetErrorString((hipError_t)status);
+  return "mde: unknown status";
+}
+
+}  // extern "C"

@@ -1,0 +1,382 @@
+"""Autograd functions over the HIP kernels of libmde_hip.so.
+
+Each function here replaces one ATen call site (or fused group) of the
+reference's training hot path; the docstrings cite the reference file:line.
+All of them require ROCm device tensors and raise on CPU tensors: the
+product path has no CPU fallback (the CPU restatement lives in oracle/ and is
+test infrastructure only).
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _abi
+
+__all__ = [
+    "interpolate", "bilinear_resize", "nearest_resize", "se_cat", "skip_reduce",
+    "minmax", "depth_norm", "ssim3_l1", "depth_loss",
+]
+
+
+def _gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError(
+                "monocular_depth_estimation_amd ops run only on ROCm device tensors "
+                f"(got a {t.device} tensor); there is no CPU fallback")
+
+
+def _ws(nbytes: int, like: torch.Tensor) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 16), dtype=torch.uint8, device=like.device)
+
+
+# ----------------------------------------------------------------- resizing
+def _out_size_and_scales(x: torch.Tensor, size, scale_factor, recompute_scale_factor):
+    """Output size and the fp32 source-per-destination scales ATen would use.
+
+    Mirrors torch.nn.functional.interpolate for 2-D inputs: with `size` the
+    scales are in/out (ATen compute_scales_value with no scale); with
+    `scale_factor` the size is floor(in * s) and the scale is 1/s unless
+    recompute_scale_factor is True.
+    """
+    hi, wi = int(x.shape[-2]), int(x.shape[-1])
+    if size is not None:
+        if scale_factor is not None:
+            raise ValueError("only one of size or scale_factor should be defined")
+        if isinstance(size, int):
+            size = (size, size)
+        ho, wo = int(size[0]), int(size[1])
+        scales = (None, None)
+    elif scale_factor is not None:
+        if isinstance(scale_factor, (int, float)):
+            scale_factor = (float(scale_factor), float(scale_factor))
+        sf = [float(s) for s in scale_factor]
+        ho, wo = int(math.floor(hi * sf[0])), int(math.floor(wi * sf[1]))
+        scales = (None, None) if recompute_scale_factor else (sf[0], sf[1])
+    else:
+        raise ValueError("either size or scale_factor should be defined")
+
+    def one(inp, out, sf):
+        if sf is not None and sf > 0:
+            return float(np.float32(1.0 / sf))
+        return float(np.float32(inp) / np.float32(out))
+
+    return ho, wo, one(hi, ho, scales[0]), one(wi, wo, scales[1])
+
+
+def _align_scale(inp: int, out: int) -> float:
+    if out > 1:
+        return float(np.float32(inp - 1) / np.float32(out - 1))
+    return 0.0
+
+
+class _Bilinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo, sh, sw, align):
+        x = x.contiguous()
+        n, c, hi, wi = x.shape
+        y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device)
+        _abi.call("mde_bilinear_fwd", _abi.ptr(x), _abi.ptr(y), n, c, hi, wi, ho, wo,
+                  sh, sw, int(align), _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.meta = (n, c, hi, wi, ho, wo, sh, sw, int(align))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        n, c, hi, wi, ho, wo, sh, sw, align = ctx.meta
+        gy = gy.contiguous()
+        gx = torch.empty((n, c, hi, wi), dtype=gy.dtype, device=gy.device)
+        _abi.call("mde_bilinear_bwd", _abi.ptr(gy), _abi.ptr(gx), n, c, hi, wi, ho, wo,
+                  sh, sw, align, _abi.dtype_code(gy), _abi.stream_of(gy))
+        return gx, None, None, None, None, None
+
+
+class _Nearest(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo, sh, sw):
+        x = x.contiguous()
+        n, c, hi, wi = x.shape
+        y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device)
+        _abi.call("mde_nearest_fwd", _abi.ptr(x), _abi.ptr(y), n, c, hi, wi, ho, wo,
+                  sh, sw, _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.meta = (n, c, hi, wi, ho, wo, sh, sw)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        n, c, hi, wi, ho, wo, sh, sw = ctx.meta
+        gy = gy.contiguous()
+        gx = torch.empty((n, c, hi, wi), dtype=gy.dtype, device=gy.device)
+        _abi.call("mde_nearest_bwd", _abi.ptr(gy), _abi.ptr(gx), n, c, hi, wi, ho, wo,
+                  sh, sw, _abi.dtype_code(gy), _abi.stream_of(gy))
+        return gx, None, None, None, None
+
+
+def bilinear_resize(x, size=None, scale_factor=None, align_corners=False,
+                    recompute_scale_factor=None):
+    """F.interpolate(x, ..., mode='bilinear') on the HIP kernel.
+
+    Call sites replaced: GuideDepth.py:49,52,55; DDRNet_23_slim.py:182-191,
+    332-351; model_mobileV3_large_newCRFs.py:55-58,124.
+    """
+    _gpu(x)
+    if x.dim() != 4:
+        raise ValueError("bilinear_resize expects a 4-D NCHW tensor")
+    ho, wo, sh, sw = _out_size_and_scales(x, size, scale_factor, recompute_scale_factor)
+    if align_corners:
+        sh, sw = _align_scale(x.shape[-2], ho), _align_scale(x.shape[-1], wo)
+    return _Bilinear.apply(x, ho, wo, sh, sw, bool(align_corners))
+
+
+def nearest_resize(x, size=None, scale_factor=None, recompute_scale_factor=None):
+    """F.interpolate(x, ..., mode='nearest') on the HIP kernel (GuideDepth.py:46-47)."""
+    _gpu(x)
+    if x.dim() != 4:
+        raise ValueError("nearest_resize expects a 4-D NCHW tensor")
+    ho, wo, sh, sw = _out_size_and_scales(x, size, scale_factor, recompute_scale_factor)
+    return _Nearest.apply(x, ho, wo, sh, sw)
+
+
+def interpolate(input, size=None, scale_factor=None, mode="nearest", align_corners=None,
+                recompute_scale_factor=None):
+    """Drop-in for torch.nn.functional.interpolate on 4-D inputs (nearest / bilinear)."""
+    if mode == "nearest":
+        if align_corners is not None:
+            raise ValueError("align_corners option can only be set with the interpolating "
+                             "modes: linear | bilinear | bicubic | trilinear")
+        return nearest_resize(input, size, scale_factor, recompute_scale_factor)
+    if mode == "bilinear":
+        return bilinear_resize(input, size, scale_factor, bool(align_corners),
+                               recompute_scale_factor)
+    raise NotImplementedError(f"interpolate mode {mode!r} has no HIP kernel")
+
+
+# ------------------------------------------------------- squeeze-excitation
+class _SECat(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xa, xb, w1, w2):
+        xa = xa.contiguous()
+        xb = xb.contiguous() if xb is not None else None
+        w1 = w1.contiguous()
+        w2 = w2.contiguous()
+        n, ca, h, w = xa.shape
+        cb = 0 if xb is None else xb.shape[1]
+        c = ca + cb
+        cr = w1.shape[0]
+        out = torch.empty((n, c, h, w), dtype=xa.dtype, device=xa.device)
+        s = torch.empty((n, c), dtype=torch.float32, device=xa.device)
+        hidden = torch.empty((n, cr), dtype=torch.float32, device=xa.device)
+        mean = torch.empty((n, c), dtype=torch.float32, device=xa.device)
+        ws = _ws(_abi.query("mde_se_workspace", n, c, cr, h, w), xa)
+        _abi.call("mde_se_fwd", _abi.ptr(xa), ca, _abi.ptr(xb), cb, _abi.ptr(w1), _abi.ptr(w2),
+                  cr, _abi.ptr(out), _abi.ptr(s), _abi.ptr(hidden), _abi.ptr(mean), n, h, w,
+                  _abi.ptr(ws), _abi.dtype_code(xa), _abi.stream_of(xa))
+        ctx.save_for_backward(xa, xb, w1, w2, s, hidden, mean)
+        ctx.has_b = xb is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        xa, xb, w1, w2, s, hidden, mean = ctx.saved_tensors
+        gout = gout.contiguous()
+        n, ca, h, w = xa.shape
+        cb = 0 if xb is None else xb.shape[1]
+        cr = w1.shape[0]
+        gxa = torch.empty_like(xa) if ctx.needs_input_grad[0] else None
+        gxb = torch.empty_like(xb) if (xb is not None and ctx.needs_input_grad[1]) else None
+        gw1 = torch.empty_like(w1)
+        gw2 = torch.empty_like(w2)
+        ws = _ws(_abi.query("mde_se_workspace", n, ca + cb, cr, h, w), xa)
+        _abi.call("mde_se_bwd", _abi.ptr(gout), _abi.ptr(xa), ca, _abi.ptr(xb), cb,
+                  _abi.ptr(w1), _abi.ptr(w2), cr, _abi.ptr(s), _abi.ptr(hidden), _abi.ptr(mean),
+                  _abi.ptr(gxa), _abi.ptr(gxb), _abi.ptr(gw1), _abi.ptr(gw2), n, h, w,
+                  _abi.ptr(ws), _abi.dtype_code(gout), _abi.stream_of(gout))
+        return gxa, gxb, gw1, gw2
+
+
+def se_cat(xa, xb, w1, w2):
+    """SELayer(cat([xa, xb], 1)) with the concatenation fused away.
+
+    Replaces torch.cat at modules.py:90 and SELayer.forward at modules.py:21-25
+    (w1 = fc[0].weight [C/r, C], w2 = fc[2].weight [C, C/r]).  xb may be None.
+    """
+    _gpu(xa, xb, w1, w2)
+    return _SECat.apply(xa, xb, w1, w2)
+
+
+# ------------------------------------------------------------- skip fusion
+class _SkipReduce(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, r, d, weight, bias):
+        r = r.contiguous()
+        d = d.contiguous()
+        n, cin, h, w = r.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin).contiguous()
+        b = bias.contiguous()
+        out = torch.empty((n, cout, h, w), dtype=r.dtype, device=r.device)
+        _abi.call("mde_skip_reduce_fwd", _abi.ptr(r), _abi.ptr(d), _abi.ptr(w2), _abi.ptr(b),
+                  _abi.ptr(out), n, cin, cout, h, w, _abi.dtype_code(r), _abi.stream_of(r))
+        ctx.save_for_backward(r, d, w2)
+        ctx.wshape = weight.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        r, d, w2 = ctx.saved_tensors
+        gout = gout.contiguous()
+        n, cin, h, w = r.shape
+        cout = w2.shape[0]
+        gs = torch.empty_like(r)
+        gw = torch.empty((cout, cin), dtype=torch.float32, device=r.device)
+        gb = torch.empty((cout,), dtype=torch.float32, device=r.device)
+        ws = _ws(_abi.query("mde_skip_reduce_workspace", n, cin, cout, h, w), r)
+        _abi.call("mde_skip_reduce_bwd", _abi.ptr(gout), _abi.ptr(r), _abi.ptr(d), _abi.ptr(w2),
+                  _abi.ptr(gs), _abi.ptr(gw), _abi.ptr(gb), n, cin, cout, h, w, _abi.ptr(ws),
+                  _abi.dtype_code(gout), _abi.stream_of(gout))
+        return gs, gs, gw.reshape(ctx.wshape), gb
+
+
+def skip_reduce(residual, depth, weight, bias):
+    """`reduce(residual + depth)` of modules.py:100 as one fused kernel.
+
+    weight: the 1x1 conv weight [cout, cin, 1, 1]; bias [cout].
+    """
+    _gpu(residual, depth, weight, bias)
+    if residual.shape != depth.shape:
+        raise ValueError(f"residual {tuple(residual.shape)} and depth {tuple(depth.shape)} differ")
+    return _SkipReduce.apply(residual, depth, weight, bias)
+
+
+# ---------------------------------------------------------------- DepthNorm
+def minmax(x: torch.Tensor) -> torch.Tensor:
+    """Device [min, max] of the whole tensor (fp32)."""
+    _gpu(x)
+    x = x.contiguous()
+    out = torch.empty(2, dtype=torch.float32, device=x.device)
+    ws = _ws(_abi.query("mde_minmax_workspace", x.numel()), x)
+    _abi.call("mde_minmax", _abi.ptr(x), x.numel(), _abi.ptr(out), _abi.ptr(ws),
+              _abi.dtype_code(x), _abi.stream_of(x))
+    return out
+
+
+class _DepthNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        mm = minmax(x)
+        y = torch.empty_like(x)
+        _abi.call("mde_depthnorm_apply", _abi.ptr(x), _abi.ptr(mm), _abi.ptr(y), x.numel(),
+                  _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.save_for_backward(x, y, mm)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        # y = (x - a)/R, R = b - a; min()/max() spread their gradient evenly
+        # over ties, as ATen's full-reduction min/max backward does.
+        x, y, mm = ctx.saved_tensors
+        rng = mm[1] - mm[0]
+        ga = (g * (y - 1.0)).sum() / rng
+        gb = -(g * y).sum() / rng
+        is_min = (x == mm[0]).to(g.dtype)
+        is_max = (x == mm[1]).to(g.dtype)
+        return g / rng + is_min * (ga / is_min.sum()) + is_max * (gb / is_max.sum())
+
+
+def depth_norm(depth: torch.Tensor) -> torch.Tensor:
+    """DepthNorm (src/utils.py:7-8): (d - d.min()) / (d.max() - d.min())."""
+    _gpu(depth)
+    return _DepthNorm.apply(depth)
+
+
+# --------------------------------------------------------------- SSIM + L1
+class _SSIML1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, target_minmax, w_ssim, w_l1):
+        pred = pred.contiguous()
+        target = target.contiguous()
+        if pred.shape != target.shape or pred.dim() != 4:
+            raise ValueError(f"pred {tuple(pred.shape)} / target {tuple(target.shape)}")
+        n, c, h, w = pred.shape
+        b = n * c
+        loss = torch.empty(3, dtype=torch.float32, device=pred.device)
+        gp = torch.empty_like(pred) if ctx.needs_input_grad[0] else None
+        gt = torch.empty_like(target) if ctx.needs_input_grad[1] else None
+        ws = _ws(_abi.query("mde_ssim3_l1_workspace", b, h, w), pred)
+        _abi.call("mde_ssim3_l1_fwd", _abi.ptr(pred), _abi.ptr(target), _abi.ptr(target_minmax),
+                  float(w_ssim), float(w_l1), _abi.ptr(loss), _abi.ptr(gp), _abi.ptr(gt),
+                  b, h, w, _abi.ptr(ws), _abi.dtype_code(pred), _abi.stream_of(pred))
+        ctx.save_for_backward(gp, gt)
+        ctx.mark_non_differentiable(loss)
+        return loss[0].clone(), loss
+
+    @staticmethod
+    def backward(ctx, go, _unused):
+        gp, gt = ctx.saved_tensors
+        return (gp * go if gp is not None else None,
+                gt * go if gt is not None else None, None, None, None)
+
+
+def ssim3_l1(pred, target, w_ssim=1.0, w_l1=0.0, target_minmax=None):
+    """w_ssim * SSIM(pred, t) + w_l1 * L1(pred, t), one fused HIP pass.
+
+    t = DepthNorm(target) when target_minmax (from minmax()) is given, else
+    target.  SSIM = src/loss.py:57-88; L1 = nn.L1Loss (src/train.py:53,94);
+    DepthNorm = src/utils.py:7-8.  Returns (loss, [loss, ssim, l1]) — the
+    second tensor is detached, for logging.
+    """
+    _gpu(pred, target, target_minmax)
+    if target_minmax is not None and target.requires_grad:
+        raise ValueError("the fused DepthNorm target is data: it must not require grad")
+    return _SSIML1.apply(pred, target, target_minmax, w_ssim, w_l1)
+
+
+# --------------------------------------------------------------- Depth_Loss
+class _DepthLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, gt, alpha, beta, gamma, max_depth):
+        pred = pred.contiguous()
+        gt = gt.contiguous()
+        if pred.shape != gt.shape or pred.dim() != 4:
+            raise ValueError(f"output {tuple(pred.shape)} / depth {tuple(gt.shape)}")
+        n, c, h, w = pred.shape
+        out = torch.empty(6, dtype=torch.float32, device=pred.device)
+        ws = _ws(_abi.query("mde_depth_loss_workspace", n * c, h, w), pred)
+        _abi.call("mde_depth_loss_fwd", _abi.ptr(pred), _abi.ptr(gt), float(alpha), float(beta),
+                  float(gamma), float(max_depth), _abi.ptr(out), n * c, h, w, _abi.ptr(ws),
+                  _abi.dtype_code(pred), _abi.stream_of(pred))
+        ctx.save_for_backward(pred, gt, out)
+        ctx.params = (float(alpha), float(beta), float(gamma), float(max_depth))
+        ctx.mark_non_differentiable(out)
+        return out[0].clone(), out
+
+    @staticmethod
+    def backward(ctx, go, _unused):
+        pred, gt, out = ctx.saved_tensors
+        alpha, beta, gamma, max_depth = ctx.params
+        n, c, h, w = pred.shape
+        go = go.reshape(1).to(torch.float32).contiguous()
+        gp = torch.empty_like(pred)
+        ws = _ws(_abi.query("mde_depth_loss_workspace", n * c, h, w), pred)
+        _abi.call("mde_depth_loss_bwd", _abi.ptr(pred), _abi.ptr(gt), alpha, beta, gamma,
+                  max_depth, _abi.ptr(out), _abi.ptr(go), _abi.ptr(gp), n * c, h, w,
+                  _abi.ptr(ws), _abi.dtype_code(pred), _abi.stream_of(pred))
+        return gp, None, None, None, None, None
+
+
+def depth_loss(output, depth, alpha, beta, gamma, max_depth=10.0):
+    """GuideDepth's Depth_Loss (src/GuideDepth/losses.py:15-127) as fused HIP kernels.
+
+    Returns (loss, [loss, l1, l_ssim, l_grad, ssim_mean, count]) — the second
+    tensor detached.  Only `output` is differentiated (the reference's
+    callers pass the ground truth as data).
+    """
+    _gpu(output, depth)
+    if depth.requires_grad:
+        raise ValueError("Depth_Loss: the ground-truth depth must not require grad")
+    return _DepthLoss.apply(output, depth, alpha, beta, gamma, max_depth)

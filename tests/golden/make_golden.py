@@ -1,0 +1,273 @@
+"""Capture golden fixtures by importing the REFERENCE (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+Imports LuizGuzzo/Monocular_Depth_Estimation from /root/reference/src
+(read-only; no bytecode written), fills every module with the deterministic
+weights of oracle/weights.py, runs the reference code on seeded inputs and
+writes tests/golden/*.npz (inputs + expected outputs only — no reference
+source travels).  cv2 is not installed here: an in-memory stub providing
+INTER_CUBIC lets src/utils.py import (DepthNorm does not use cv2).  The
+timm helpers newcrf_layers.py imports are stubbed the same way when NewCRF
+fixtures are captured.
+
+Exits if /root/reference is absent (e.g. on the GPU box): fixtures are
+committed, the GPU box never re-captures.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference/src"
+
+sys.dont_write_bytecode = True
+sys.path.insert(0, REPO)
+from oracle.weights import fill_, seeded  # noqa: E402
+
+
+def _import_reference():
+    if not os.path.isdir(REF):
+        sys.exit(f"{REF} not found: golden fixtures can only be captured in the build container")
+    if "cv2" not in sys.modules:
+        cv2 = types.ModuleType("cv2")
+        cv2.INTER_CUBIC = 2
+        sys.modules["cv2"] = cv2
+    sys.path.insert(0, REF)
+    os.chdir(REF)  # GuideDepth package imports are relative to src/
+
+
+def f32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def grad_summary(module, prefix, out, full_limit=4096, force=()):
+    """Per-parameter grad sum and L2 norm; full grads for small / forced params."""
+    names, sums, norms = [], [], []
+    for name, p in module.named_parameters():
+        if p.grad is None:
+            continue
+        g = p.grad.detach().double()
+        names.append(name)
+        sums.append(float(g.sum()))
+        norms.append(float(g.norm()))
+        if p.numel() <= full_limit or name in force:
+            out[f"{prefix}grad::{name}"] = f32(p.grad)
+    out[f"{prefix}grad_names"] = np.array(names)
+    out[f"{prefix}grad_sums"] = np.array(sums, dtype=np.float64)
+    out[f"{prefix}grad_norms"] = np.array(norms, dtype=np.float64)
+
+
+RESIZE_CASES = [
+    # name, shape, kwargs
+    ("b_30x40_to_60x80", (1, 2, 30, 40), dict(size=[60, 80])),
+    ("b_15x20_to_60x80", (1, 2, 15, 20), dict(size=[60, 80])),
+    ("b_4x5_to_8x10", (1, 2, 4, 5), dict(size=[8, 10])),
+    ("b_2x3_to_8x10", (1, 2, 2, 3), dict(size=[8, 10])),
+    ("b_1x2_to_8x10", (1, 2, 1, 2), dict(size=[8, 10])),
+    ("b_1x1_to_8x10", (1, 2, 1, 1), dict(size=[8, 10])),
+    ("b_8x10_to_60x80", (1, 2, 8, 10), dict(size=[60, 80])),
+    ("b_8x10_to_30x40", (1, 2, 8, 10), dict(size=[30, 40])),
+    ("b_x2", (2, 3, 16, 20), dict(scale_factor=2)),
+    ("b_x2_odd", (1, 2, 7, 9), dict(scale_factor=2)),
+    ("b_align_x2", (1, 2, 7, 9), dict(scale_factor=2, align_corners=True)),
+    ("b_align_size", (1, 2, 5, 6), dict(size=[11, 17], align_corners=True)),
+    ("b_down_20x30_to_7x11", (1, 2, 20, 30), dict(size=[7, 11])),
+    ("b_5x7_to_13x17", (1, 1, 5, 7), dict(size=[13, 17])),
+    ("b_x4", (1, 1, 6, 8), dict(scale_factor=4)),
+]
+NEAREST_CASES = [
+    ("n_half", (1, 3, 24, 32), 0.5),
+    ("n_quarter", (1, 3, 24, 32), 0.25),
+    ("n_half_odd", (1, 3, 25, 33), 0.5),
+    ("n_quarter_odd", (1, 3, 27, 35), 0.25),
+]
+
+
+def capture_resize():
+    import torch.nn.functional as F
+    out = {}
+    for i, (name, shape, kw) in enumerate(RESIZE_CASES):
+        x = torch.from_numpy(seeded(shape, 1000 + i, -1, 1)).requires_grad_(True)
+        y = F.interpolate(x, mode="bilinear", **kw)
+        gy = torch.from_numpy(seeded(y.shape, 2000 + i, -1, 1))
+        y.backward(gy)
+        out.update({f"{name}::x": f32(x), f"{name}::gy": f32(gy), f"{name}::y": f32(y),
+                    f"{name}::gx": f32(x.grad)})
+    for i, (name, shape, sf) in enumerate(NEAREST_CASES):
+        x = torch.from_numpy(seeded(shape, 3000 + i, -1, 1)).requires_grad_(True)
+        y = F.interpolate(x, scale_factor=sf)
+        gy = torch.from_numpy(seeded(y.shape, 4000 + i, -1, 1))
+        y.backward(gy)
+        out.update({f"{name}::x": f32(x), f"{name}::gy": f32(gy), f"{name}::y": f32(y),
+                    f"{name}::gx": f32(x.grad)})
+    return out
+
+
+def capture_blocks():
+    from GuideDepth.model.modules import Guided_Upsampling_Block, SELayer
+    out = {}
+    # SELayer(16, reduction=1) as used inside up_3, plus a reduction-4 case
+    for tag, ch, red, shape in (("se16", 16, 1, (2, 16, 10, 12)), ("se32r4", 32, 4, (2, 32, 6, 7))):
+        m = fill_(SELayer(ch, reduction=red))
+        x = torch.from_numpy(seeded(shape, 11, -1, 1)).requires_grad_(True)
+        y = m(x)
+        gy = torch.from_numpy(seeded(y.shape, 12, -1, 1))
+        y.backward(gy)
+        out.update({f"{tag}::x": f32(x), f"{tag}::gy": f32(gy), f"{tag}::y": f32(y),
+                    f"{tag}::gx": f32(x.grad), f"{tag}::gw1": f32(m.fc[0].weight.grad),
+                    f"{tag}::gw2": f32(m.fc[2].weight.grad)})
+    # the three guided-upsampling configurations of GuideDepth, train-mode BN
+    for tag, (cin, e, cout) in (("gub1", (64, 64, 32)), ("gub2", (32, 32, 16)),
+                                ("gub3", (16, 16, 1))):
+        m = fill_(Guided_Upsampling_Block(cin, e, cout, kernel_size=3, channel_attention=True,
+                                          guide_features=3, guidance_type="full"))
+        m.train()
+        guide = torch.from_numpy(seeded((2, 3, 12, 16), 21, 0, 1)).requires_grad_(True)
+        depth = torch.from_numpy(seeded((2, cin, 12, 16), 22, -1, 1)).requires_grad_(True)
+        y = m(guide, depth)
+        gy = torch.from_numpy(seeded(y.shape, 23, -1, 1))
+        y.backward(gy)
+        out.update({f"{tag}::guide": f32(guide), f"{tag}::depth": f32(depth),
+                    f"{tag}::gy": f32(gy), f"{tag}::y": f32(y),
+                    f"{tag}::gguide": f32(guide.grad), f"{tag}::gdepth": f32(depth.grad)})
+        grad_summary(m, f"{tag}::", out, full_limit=2048)
+    return out
+
+
+def capture_losses():
+    import loss as refloss
+    import utils as refutils
+    from GuideDepth.losses import Depth_Loss
+    out = {}
+    shape = (2, 1, 24, 32)
+    cases = {
+        "rand": (seeded(shape, 31, 0, 1), seeded(shape, 32, 0, 1)),
+        "close": (None, seeded(shape, 33, 0, 1)),
+        "anti": (None, seeded(shape, 34, 0, 1)),
+    }
+    cases["close"] = (cases["close"][1] + 0.01 * seeded(shape, 35, -1, 1), cases["close"][1])
+    cases["anti"] = (1.0 - cases["anti"][1], cases["anti"][1])
+    ssim = refloss.SSIM()
+    for tag, (p, t) in cases.items():
+        x = torch.from_numpy(p).requires_grad_(True)
+        y = torch.from_numpy(t).requires_grad_(True)
+        v = ssim(x, y)
+        v.backward()
+        out.update({f"ssim_{tag}::x": p, f"ssim_{tag}::y": t, f"ssim_{tag}::loss": f32(v),
+                    f"ssim_{tag}::gx": f32(x.grad), f"ssim_{tag}::gy": f32(y.grad)})
+    # train.py objective: DepthNorm target, SSIM + 0.1 L1 (train.py:89-100)
+    pred = torch.from_numpy(seeded(shape, 41, 0, 1)).requires_grad_(True)
+    depth = torch.from_numpy(seeded(shape, 42, 0.1, 10.0))
+    dn = refutils.DepthNorm(depth)
+    l1 = torch.nn.L1Loss()(pred, dn)
+    ls = ssim(pred, dn)
+    sil = refloss.Silog_loss_variance()(pred, dn)
+    total = 1.0 * ls + 0.1 * l1
+    total.backward()
+    out.update({"train::pred": f32(pred), "train::depth": f32(depth), "train::depth_n": f32(dn),
+                "train::l1": f32(l1), "train::ssim": f32(ls), "train::silog": f32(sil),
+                "train::loss": f32(total), "train::gpred": f32(pred.grad)})
+    # Depth_Loss in Alhashim mode (0.1,1,1), masked L1 mode (1,0,0) and a small map (K=8)
+    for tag, (a, b, g), shp, mx in (("dl_alh", (0.1, 1.0, 1.0), (2, 1, 24, 32), 10.0),
+                                    ("dl_mask", (1.0, 0.0, 0.0), (2, 1, 24, 32), 10.0),
+                                    ("dl_small", (0.1, 1.0, 1.0), (1, 1, 8, 9), 10.0),
+                                    ("dl_ssim_only", (0.0, 1.0, 0.0), (1, 2, 16, 20), 1.0)):
+        p = seeded(shp, 51, 0.0, mx)
+        t = seeded(shp, 52, 0.0, mx)
+        if tag == "dl_mask":
+            t[..., ::3, ::2] = 0.0  # invalid pixels
+        x = torch.from_numpy(p).requires_grad_(True)
+        v = Depth_Loss(a, b, g, maxDepth=mx)(x, torch.from_numpy(t))
+        v.backward()
+        out.update({f"{tag}::pred": p, f"{tag}::gt": t, f"{tag}::loss": f32(v),
+                    f"{tag}::gpred": f32(x.grad),
+                    f"{tag}::params": np.array([a, b, g, mx], dtype=np.float32)})
+    return out
+
+
+def capture_guidedepth():
+    from GuideDepth.model.GuideDepth import GuideDepth
+    import loss as refloss
+    import utils as refutils
+    out = {}
+    model = fill_(GuideDepth(pretrained=False))
+    out["state_dict_keys"] = np.array(list(model.state_dict().keys()))
+    x = torch.from_numpy(seeded((2, 3, 64, 96), 61, 0, 1))
+    depth = torch.from_numpy(seeded((2, 1, 64, 96), 62, 0.1, 10.0))
+    feats = {}
+    hooks = [getattr(model, n).register_forward_hook(
+        lambda m, i, o, n=n: feats.__setitem__(n, o.detach().clone())) for n in ("up_1", "up_2")]
+    hooks.append(model.feature_extractor.register_forward_hook(
+        lambda m, i, o: feats.__setitem__("encoder", o.detach().clone())))
+    model.train()
+    pred = model(x)
+    for h in hooks:
+        h.remove()
+    dn = refutils.DepthNorm(depth)
+    loss = 1.0 * refloss.SSIM()(pred, dn) + 0.1 * torch.nn.L1Loss()(pred, dn)
+    loss.backward()
+    out.update({"x": f32(x), "depth": f32(depth), "train_pred": f32(pred), "train_loss": f32(loss)})
+    for k, v in feats.items():
+        out[f"train_{k}"] = f32(v)
+    grad_summary(model, "", out, full_limit=2048, force=("feature_extractor.conv1.0.weight",))
+    rm = [v for k, v in model.state_dict().items() if k.endswith("running_mean")]
+    out["running_mean_sums"] = np.array([float(v.double().sum()) for v in rm])
+    model.eval()
+    with torch.no_grad():
+        out["eval_pred"] = f32(model(x))
+    return out
+
+
+def capture_train_sequence(steps=5):
+    """train.py recipe (train.py:79-136): step 0 in train mode, then LogProgress's
+    model.eval() sticks (train.py:161) for the rest of the epoch."""
+    from GuideDepth.model.GuideDepth import GuideDepth
+    import loss as refloss
+    import utils as refutils
+    model = fill_(GuideDepth(pretrained=False))
+    opt = torch.optim.Adam(model.parameters(), 1e-4)
+    l1, ssim = torch.nn.L1Loss(), refloss.SSIM()
+    model.train()
+    losses = []
+    for k in range(steps):
+        image = torch.from_numpy(seeded((2, 3, 64, 96), 100 + k, 0, 1))
+        depth = torch.from_numpy(seeded((2, 1, 64, 96), 200 + k, 0.1, 10.0))
+        dn = refutils.DepthNorm(depth)
+        pred = model(image)
+        loss = 1.0 * ssim(pred, dn) + 0.1 * l1(pred, dn)
+        opt.zero_grad()
+        losses.append(float(loss.item()))
+        loss.backward()
+        opt.step()
+        if k == 0:
+            model.eval()  # LogProgress at loader_pos % 300 == 0
+    return {"losses": np.array(losses, dtype=np.float64),
+            "final_up3_reduce_weight": f32(model.up_3.reduce.weight)}
+
+
+def main():
+    _import_reference()
+    torch.manual_seed(0)
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    jobs = {"golden_resize.npz": capture_resize, "golden_blocks.npz": capture_blocks,
+            "golden_losses.npz": capture_losses, "golden_guidedepth.npz": capture_guidedepth,
+            "golden_trainseq.npz": capture_train_sequence}
+    only = set(sys.argv[1:])
+    for fname, fn in jobs.items():
+        if only and fname not in only:
+            continue
+        data = fn()
+        path = os.path.join(HERE, fname)
+        np.savez_compressed(path, **data)
+        print(f"wrote {path} ({os.path.getsize(path) / 1024:.0f} KiB, {len(data)} arrays)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,170 @@
+"""Training throughput of GuideDepth at 640x480, bs=32 per GPU (BASELINE.json metric, cfg2).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+One step = the src/train.py step (train.py:86-114) on one synthetic batch
+already resident in HBM: GuideDepth forward (BN in train mode), DepthNorm +
+1.0*SSIM + 0.1*L1 (one fused HIP pass), backward, DDP all-reduce over RCCL
+(N > 1), Adam step.  Rank 0 prints ONE JSON line.  Extra fields:
+  roofline     — the dominant hand-written HIP kernel over the timed region
+                 (HIP events on its launch stream; algorithmic bytes per
+                 SURVEY §8(d)); traffic from profiles/ PMC counters if present.
+  cpu_baseline — the CPU oracle's train step (rank 0, N=1 only), bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--bs", type=int, default=32)
+    p.add_argument("--height", type=int, default=480)
+    p.add_argument("--width", type=int, default=640)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-bs", type=int, default=4)
+    p.add_argument("--cpu-steps", type=int, default=2)
+    p.add_argument("--cudnn-benchmark", type=int, default=1)
+    p.add_argument("--no-kernel-timing", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle (CPU restatement, same ATen CPU convs/BN as the reference) timed on host cores."""
+    from oracle import guidedepth as og
+    from oracle import ops as oops
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    model = og.GuideDepth().train()
+    opt = torch.optim.Adam(model.parameters(), 1e-4)
+    g = torch.Generator().manual_seed(0)
+    img = torch.rand((args.cpu_bs, 3, args.height, args.width), generator=g)
+    dep = 0.1 + 9.9 * torch.rand((args.cpu_bs, 1, args.height, args.width), generator=g)
+
+    def step():
+        loss = oops.train_loss(model(img), dep)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+
+    step()  # warm-up
+    t0 = time.perf_counter()
+    for _ in range(args.cpu_steps):
+        step()
+    dt = time.perf_counter() - t0
+    return {"value": round(args.cpu_bs * args.cpu_steps / dt, 3), "unit": "images/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle GuideDepth train step, {args.height}x{args.width} bs={args.cpu_bs}, "
+                      f"{args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s), fp32"}
+
+
+def main():
+    args = parse()
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.train import (Trainer, init_world, make_adam, synthetic_batch,
+                                                      wrap_ddp)
+    world = init_world()
+    torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
+    from monocular_depth_estimation_amd import GuideDepth
+    from monocular_depth_estimation_amd.loss import SSIML1
+
+    torch.manual_seed(0)
+    model = GuideDepth(pretrained=False).to(world.device)
+    opt = make_adam(model, 1e-4)
+    ddp = wrap_ddp(model, world)
+    trainer = Trainer(ddp, opt, SSIML1(1.0, 0.1, depth_norm=True), world, eval_quirk=False)
+    trainer.begin_epoch()
+    batches = [synthetic_batch(args.bs, args.height, args.width, world.rank, s, world.device)
+               for s in range(2)]
+
+    def barrier():
+        if world.size > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        trainer.step(*batches[i % 2])
+    barrier()
+    timing = not args.no_kernel_timing
+    if timing:
+        _abi.timing_reset()
+        _abi.timing_enable(True)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(*batches[i % 2])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if timing:
+        _abi.timing_enable(False)
+        kernels = _abi.timing_collect()
+    else:
+        kernels = {}
+    if world.size > 1:
+        t = torch.tensor([elapsed], device=world.device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    loss = float(trainer.last_loss)
+    if not world.is_main:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        return
+
+    images = world.size * args.bs * args.steps
+    roofline = None
+    if kernels:
+        name, (ms, launches, nbytes) = max(kernels.items(), key=lambda kv: kv[1][0])
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(PMC_FILE):
+            with open(PMC_FILE) as f:
+                traffic = json.load(f).get(name, {}).get("bytes_per_launch")
+        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic, "bytes_per_launch": nbytes / launches,
+                    "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
+    out = {
+        "metric": "training images/sec at 640x480 bs=32/GPU (GuideDepth, SSIM+0.1*L1, Adam)",
+        "value": round(images / elapsed, 2), "unit": "images/s", "n_gpus": world.size,
+        "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (U[0,1) images, U[0.1,10) depths, resident in HBM), random-init weights",
+        "config": {"workload": "GuideDepth (DDRNet-23-slim + 3 guided upsampling blocks) train step, "
+                               "BASELINE cfg2, BN in train mode",
+                   "global_batch": world.size * args.bs, "per_gpu_batch": args.bs,
+                   "resolution": f"{args.width}x{args.height}", "parallelism": f"dp{world.size}"},
+        "loss_last": round(loss, 6),
+        "roofline": roofline,
+        "hip_kernels": {k: {"ms_total": round(v[0], 3), "launches": v[1],
+                            "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 else None}
+                        for k, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])},
+    }
+    if world.size == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    else:
+        out["cpu_baseline"] = None
+    print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

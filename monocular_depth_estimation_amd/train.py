@@ -1,0 +1,210 @@
+"""Data-parallel training loop for GuideDepth on MI355X (drop-in for src/train.py).
+
+    python -m monocular_depth_estimation_amd.train --epochs 30 --lr 1e-4 --bs 3 --cp 0
+    torchrun --nproc-per-node 8 -m monocular_depth_estimation_amd.train --synthetic ...
+
+Keeps the reference CLI (train.py:26-31: --epochs --lr --bs --cp), its loss
+(train.py:89-100: DepthNorm target, 1.0*SSIM + 0.1*L1 — here one fused HIP
+pass that also yields the gradient), Adam, the checkpoint dict
+(train.py:147-153) and, by default, its BatchNorm quirk: LogProgress calls
+model.eval() at loader_pos % 300 == 0 and never switches back
+(train.py:134-136,161), so from step 1 of every epoch BN uses running stats.
+
+New (the reference is single-GPU): one process per GPU, torch.distributed
+over RCCL ("nccl" backend on ROCm; "gloo" on CPU for tests), DDP gradient
+all-reduce bucketed and overlapped with backward.  Each rank normalises its
+own shard's depth (DepthNorm is batch-global in the reference, utils.py:7-8)
+and keeps per-rank BN batch statistics (no SyncBN: DDRNet_23_slim.py:15 has it
+commented out).  The host loop never synchronises per step: losses are
+accumulated on device and read at log points only.  Silog_loss_variance is
+evaluated by the reference every step but never used (train.py:98-100); it
+is skipped here.
+
+The NYU CSV-in-zip pipeline (src/data.py) is outside this build's scope;
+--synthetic (the default when no dataset is given) feeds on-device uniform
+images and depths with per-rank seeds.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+# ------------------------------------------------------------ distributed
+@dataclass
+class World:
+    rank: int = 0
+    local_rank: int = 0
+    size: int = 1
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_world(backend: str | None = None) -> World:
+    """Join the torchrun job (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), one GPU per process."""
+    size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() and backend != "gloo"
+    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(device)
+    if size > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend or ("nccl" if use_cuda else "gloo"),
+                                rank=rank, world_size=size,
+                                device_id=device if use_cuda else None)
+    return World(rank, local, size, device)
+
+
+def wrap_ddp(model: torch.nn.Module, world: World, bucket_cap_mb: float = 8.0):
+    """DDP over RCCL: ~23 MB of fp32 grads in 8 MB buckets -> 3+ all-reduces
+    overlapped with backward; BN buffers broadcast from rank 0 each forward."""
+    if world.size == 1:
+        return model
+    kw = dict(bucket_cap_mb=bucket_cap_mb, gradient_as_bucket_view=True, broadcast_buffers=True)
+    if world.device.type == "cuda":
+        kw["device_ids"] = [world.device.index]
+    return torch.nn.parallel.DistributedDataParallel(model, **kw)
+
+
+def unwrap(model):
+    return model.module if hasattr(model, "module") else model
+
+
+# ------------------------------------------------------------------ data
+def synthetic_batch(batch: int, height: int, width: int, rank: int, step: int,
+                    device, base_seed: int = 0):
+    """image U[0,1), depth U[0.1,10); per-rank seed 1000*rank."""
+    gen = torch.Generator(device="cpu")
+    gen.manual_seed(base_seed + 1000 * rank + 2 * step)
+    image = torch.rand((batch, 3, height, width), generator=gen)
+    gen.manual_seed(base_seed + 1000 * rank + 2 * step + 1)
+    depth = 0.1 + 9.9 * torch.rand((batch, 1, height, width), generator=gen)
+    return image.to(device, non_blocking=True), depth.to(device, non_blocking=True)
+
+
+# ------------------------------------------------------------------ step
+class Trainer:
+    """One reference training step (train.py:86-114) with a device-side loss log."""
+
+    def __init__(self, model, optimizer, loss_fn, world: World, eval_quirk: bool = True):
+        self.model, self.optimizer, self.loss_fn, self.world = model, optimizer, loss_fn, world
+        self.eval_quirk = eval_quirk
+        self.loss_sum = torch.zeros((), device=world.device)
+        self.loss_count = 0
+        self.last_loss = None
+
+    def begin_epoch(self):
+        self.model.train()  # train.py:79
+
+    def step(self, image, depth):
+        pred = self.model(image)
+        loss = self.loss_fn(pred, depth)
+        self.optimizer.zero_grad(set_to_none=True)
+        loss.backward()
+        self.optimizer.step()
+        self.loss_sum += loss.detach()
+        self.loss_count += 1
+        self.last_loss = loss.detach()
+        return loss
+
+    def after_step(self, loader_pos: int):
+        # LogProgress (train.py:134-136,161): model.eval() that is never undone
+        if self.eval_quirk and loader_pos % 300 == 0:
+            self.model.eval()
+
+
+def make_adam(model, lr=1e-4):
+    kw = {}
+    if next(model.parameters()).is_cuda:
+        kw["fused"] = True  # one multi-tensor launch per step on ROCm
+    return torch.optim.Adam(model.parameters(), lr, **kw)
+
+
+def save_checkpoint(path, epoch, model, optimizer, loss):
+    """train.py:147-153 dict format, rank 0 only, DDP unwrapped."""
+    os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+    torch.save({"epoch": epoch, "model_state_dict": unwrap(model).state_dict(),
+                "optimizer_state_dict": optimizer.state_dict(), "loss": loss}, path)
+
+
+def load_checkpoint(path, model, optimizer):
+    """Resume (train.py:59-68): restarts AT the saved epoch (it is re-run)."""
+    ckpt = torch.load(path, map_location="cpu", weights_only=True)
+    unwrap(model).load_state_dict(ckpt["model_state_dict"])
+    optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+    return int(ckpt["epoch"]), ckpt["loss"]
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description="GuideDepth training on MI355X (drop-in for src/train.py)")
+    p.add_argument("--epochs", default=30, type=int, help="number of total epochs to run")
+    p.add_argument("--lr", "--learning-rate", default=0.0001, type=float, help="initial learning rate")
+    p.add_argument("--bs", default=3, type=int, help="batch size (per GPU)")
+    p.add_argument("--cp", default=0, type=int, help="1 to resume from the last checkpoint")
+    p.add_argument("--height", default=480, type=int)
+    p.add_argument("--width", default=640, type=int)
+    p.add_argument("--steps-per-epoch", default=100, type=int, help="synthetic epoch length")
+    p.add_argument("--checkpoint", default="checkpoints/global_checkpoint.pth")
+    p.add_argument("--no-eval-quirk", action="store_true",
+                   help="keep BN in train mode all epoch (the reference switches to eval after step 0)")
+    p.add_argument("--log", default="", help="JSONL file for Train/Loss scalars (rank 0)")
+    p.add_argument("--seed", default=0, type=int)
+    return p
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    world = init_world()
+    from . import GuideDepth  # noqa: E402  (loads the HIP library)
+    from .loss import SSIML1
+    from .utils import AverageMeter
+
+    torch.manual_seed(args.seed)
+    model = GuideDepth(pretrained=False).to(world.device)
+    optimizer = make_adam(model, args.lr)
+    start_epoch = 0
+    if args.cp == 1:
+        start_epoch, _ = load_checkpoint(args.checkpoint, model, optimizer)
+    ddp = wrap_ddp(model, world)
+    trainer = Trainer(ddp, optimizer, SSIML1(1.0, 0.1, depth_norm=True), world,
+                      eval_quirk=not args.no_eval_quirk)
+    log = open(args.log, "a") if (args.log and world.is_main) else None
+    for epoch in range(start_epoch, args.epochs):
+        trainer.begin_epoch()
+        losses, t0 = AverageMeter(), time.time()
+        for pos in range(args.steps_per_epoch):
+            image, depth = synthetic_batch(args.bs, args.height, args.width, world.rank,
+                                           epoch * args.steps_per_epoch + pos, world.device, args.seed)
+            loss = trainer.step(image, depth)
+            trainer.after_step(pos)
+            if pos % 5 == 0 and world.is_main:  # train.py:123-132 (host read at log points only)
+                v = float(loss)
+                losses.update(v, image.size(0))
+                dt = time.time() - t0
+                print(f"Epoch: [{epoch}][{pos}/{args.steps_per_epoch}]\tTime {dt:.3f}\t"
+                      f"Loss {losses.val:.4f} ({losses.avg:.4f})", flush=True)
+                if log:
+                    log.write(json.dumps({"tag": "Train/Loss", "value": v,
+                                          "step": epoch * args.steps_per_epoch + pos}) + "\n")
+        if world.is_main:
+            if log:
+                log.write(json.dumps({"tag": "Train/Loss.avg", "value": losses.avg, "step": epoch}) + "\n")
+                log.flush()
+            save_checkpoint(args.checkpoint, epoch, ddp, optimizer, trainer.last_loss.cpu())
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

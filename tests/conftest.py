@@ -38,3 +38,12 @@ def gpu_available():
         return torch.cuda.is_available()
     except Exception:
         return False
+
+
+def pytest_sessionstart(session):
+    """Build libmde_hip.so if this checkout has not built it yet (hipcc cross-compiles)."""
+    import subprocess
+    lib = os.path.join(REPO, "monocular_depth_estimation_amd", "libmde_hip.so")
+    if not os.path.exists(lib):
+        subprocess.run(["make", "-C", os.path.join(REPO, "monocular_depth_estimation_amd", "csrc"),
+                        "-j8"], check=True)

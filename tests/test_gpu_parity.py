@@ -1,0 +1,326 @@
+"""GPU parity: the HIP path (through the C ABI) vs golden fixtures and the CPU oracle.
+
+Tolerances (written per test): single ops 1e-5 relative (fp32); loss
+gradients 1e-4; whole-model depth maps 1e-3 scale-relative (BASELINE.json
+north_star); whole-model gradient norms 1e-2 (fp32 conditioning of the
+randomly filled net: both the reference and the oracle sit ~2e-3 from a
+float64 run, see tests/test_oracle_golden.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import guidedepth as og
+from oracle import ops as oops
+from oracle.weights import fill_, seeded
+from tests.golden.make_golden import NEAREST_CASES, RESIZE_CASES
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    import monocular_depth_estimation_amd  # noqa: F401  (loads libmde_hip.so, raises if absent)
+
+
+def npy(t):
+    return t.detach().float().cpu().numpy()
+
+
+def close(a, b, rtol, atol, what=""):
+    np.testing.assert_allclose(npy(a) if torch.is_tensor(a) else a,
+                               npy(b) if torch.is_tensor(b) else b, rtol=rtol, atol=atol,
+                               err_msg=what)
+
+
+def close_map(a, b, tol, what=""):
+    a = npy(a) if torch.is_tensor(a) else a
+    b = npy(b) if torch.is_tensor(b) else b
+    err = float(np.abs(a.astype(np.float64) - b).max())
+    assert err <= tol * float(np.abs(b).max()) + 1e-30, f"{what}: {err:.3g} vs {np.abs(b).max():.3g}"
+
+
+def cu(a, grad=False):
+    t = torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+    return t.requires_grad_(grad)
+
+
+# ------------------------------------------------------------------ resize
+@pytest.mark.parametrize("case", RESIZE_CASES, ids=[c[0] for c in RESIZE_CASES])
+def test_bilinear_golden(golden, case):
+    from monocular_depth_estimation_amd.functional import bilinear_resize
+    name, _, kw = case
+    g = golden("golden_resize.npz")
+    x = cu(g[f"{name}::x"], True)
+    y = bilinear_resize(x, size=kw.get("size"), scale_factor=kw.get("scale_factor"),
+                        align_corners=kw.get("align_corners", False))
+    close(y, g[f"{name}::y"], 1e-5, 1e-6, name)
+    y.backward(cu(g[f"{name}::gy"]))
+    close(x.grad, g[f"{name}::gx"], 1e-5, 1e-5, name)
+
+
+@pytest.mark.parametrize("case", NEAREST_CASES, ids=[c[0] for c in NEAREST_CASES])
+def test_nearest_golden_bit_exact(golden, case):
+    from monocular_depth_estimation_amd.functional import nearest_resize
+    name, _, sf = case
+    g = golden("golden_resize.npz")
+    x = cu(g[f"{name}::x"], True)
+    y = nearest_resize(x, scale_factor=sf)
+    close(y, g[f"{name}::y"], 0, 0, name)  # a copy: bit-exact
+    y.backward(cu(g[f"{name}::gy"]))
+    close(x.grad, g[f"{name}::gx"], 0, 0, name)
+
+
+@pytest.mark.parametrize("shape,kw", [
+    ((32, 16, 240, 320), dict(scale_factor=2)),           # up_3 input, BASELINE cfg2
+    ((32, 64, 8, 10), dict(size=(60, 80))),               # DDRNet spp -> H/8 (x7.5)
+    ((32, 64, 15, 20), dict(size=(60, 80))),              # compression4 (x4)
+])
+def test_bilinear_full_size_adjoint_and_oracle_rows(shape, kw):
+    """At cfg2 sizes: <fwd(x), g> == <x, bwd(g)> (adjointness), plus oracle parity on 2 samples."""
+    from monocular_depth_estimation_amd.functional import bilinear_resize
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand(shape, device=DEV, generator=gen).requires_grad_(True)
+    y = bilinear_resize(x, **kw)
+    gy = torch.rand(y.shape, device=DEV, generator=gen) - 0.5
+    y.backward(gy)
+    lhs = (y.double() * gy.double()).sum()
+    rhs = (x.double() * x.grad.double()).sum()
+    assert abs(float(lhs - rhs)) <= 1e-5 * float(y.double().abs().sum())
+    xs = x.detach()[:2].cpu().requires_grad_(True)
+    ys = oops.bilinear(xs, **kw)
+    close(y[:2], ys, 1e-5, 1e-6, "fwd vs oracle")
+    ys.backward(gy[:2].cpu())
+    close(x.grad[:2], xs.grad, 1e-5, 1e-5, "bwd vs oracle")
+
+
+# --------------------------------------------------------------------- SE
+@pytest.mark.parametrize("tag,ch,red", [("se16", 16, 1), ("se32r4", 32, 4)])
+def test_se_golden(golden, tag, ch, red):
+    from monocular_depth_estimation_amd.GuideDepth.model.modules import SELayer
+    g = golden("golden_blocks.npz")
+    m = fill_(SELayer(ch, reduction=red)).to(DEV)
+    x = cu(g[f"{tag}::x"], True)
+    y = m(x)
+    close(y, g[f"{tag}::y"], 1e-5, 1e-6)
+    y.backward(cu(g[f"{tag}::gy"]))
+    close(x.grad, g[f"{tag}::gx"], 1e-5, 1e-6)
+    close(m.fc[0].weight.grad, g[f"{tag}::gw1"], 1e-4, 1e-5)
+    close(m.fc[2].weight.grad, g[f"{tag}::gw2"], 1e-4, 1e-5)
+
+
+@pytest.mark.parametrize("n,ca,cb,h,w", [(2, 8, 8, 30, 41), (4, 32, 32, 120, 160), (32, 8, 8, 480, 640)])
+def test_se_cat_vs_oracle(n, ca, cb, h, w):
+    from monocular_depth_estimation_amd.functional import se_cat
+    c = ca + cb
+    xa = torch.from_numpy(seeded((n, ca, h, w), 1, -1, 1))
+    xb = torch.from_numpy(seeded((n, cb, h, w), 2, -1, 1))
+    w1 = torch.from_numpy(seeded((c, c), 3, -0.3, 0.3))
+    w2 = torch.from_numpy(seeded((c, c), 4, -0.3, 0.3))
+    gy = torch.from_numpy(seeded((n, c, h, w), 5, -1, 1))
+    ins = [t.to(DEV).requires_grad_(True) for t in (xa, xb, w1, w2)]
+    y = se_cat(*ins)
+    y.backward(gy.to(DEV))
+    k = min(n, 2)  # oracle on the first samples (per-sample op), weight grads on all
+    refs = [t[:k].clone().requires_grad_(True) if i < 2 else t.clone().requires_grad_(True)
+            for i, t in enumerate((xa, xb, w1, w2))]
+    yr = oops.se(torch.cat(refs[:2], 1), refs[2], refs[3])
+    close(y[:k], yr, 1e-5, 1e-6, "fwd")
+    yr.backward(gy[:k])
+    close(ins[0].grad[:k], refs[0].grad, 1e-4, 1e-6, "gxa")
+    close(ins[1].grad[:k], refs[1].grad, 1e-4, 1e-6, "gxb")
+    if k == n:
+        close(ins[2].grad, refs[2].grad, 1e-4, 1e-4, "gw1")
+        close(ins[3].grad, refs[3].grad, 1e-4, 1e-4, "gw2")
+
+
+# ------------------------------------------------------------ skip fusion
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 64, 32, 12, 16), (2, 32, 16, 24, 32),
+                                            (2, 16, 1, 48, 64), (2, 8, 4, 9, 11),
+                                            (2, 40, 24, 7, 13), (32, 16, 1, 480, 640)])
+def test_skip_reduce_vs_oracle(n, cin, cout, h, w):
+    from monocular_depth_estimation_amd.functional import skip_reduce
+    r = torch.from_numpy(seeded((n, cin, h, w), 11, -1, 1))
+    d = torch.from_numpy(seeded((n, cin, h, w), 12, -1, 1))
+    wt = torch.from_numpy(seeded((cout, cin, 1, 1), 13, -0.5, 0.5))
+    b = torch.from_numpy(seeded((cout,), 14, -0.5, 0.5))
+    gy = torch.from_numpy(seeded((n, cout, h, w), 15, -1, 1))
+    ins = [t.to(DEV).requires_grad_(True) for t in (r, d, wt, b)]
+    y = skip_reduce(*ins)
+    y.backward(gy.to(DEV))
+    refs = [t.clone().double().requires_grad_(True) for t in (r, d, wt, b)]
+    yr = oops.skip_reduce(*refs)
+    close(y, yr, 1e-5, 1e-5, "fwd")
+    yr.backward(gy.double())
+    close(ins[0].grad, refs[0].grad, 1e-5, 1e-5, "g residual")
+    close(ins[1].grad, refs[1].grad, 1e-5, 1e-5, "g depth")
+    scale = float(refs[2].grad.abs().max())
+    close(ins[2].grad, refs[2].grad, 1e-4, 1e-5 * scale, "g weight")
+    close(ins[3].grad, refs[3].grad, 1e-4, 1e-5 * float(refs[3].grad.abs().max()), "g bias")
+
+
+# ------------------------------------------------------------------ losses
+@pytest.mark.parametrize("tag", ["rand", "close", "anti"])
+def test_ssim_golden(golden, tag):
+    from monocular_depth_estimation_amd.loss import SSIM
+    g = golden("golden_losses.npz")
+    x = cu(g[f"ssim_{tag}::x"], True)
+    y = cu(g[f"ssim_{tag}::y"], True)
+    v = SSIM()(x, y)
+    close(v, g[f"ssim_{tag}::loss"], 1e-5, 1e-7)
+    v.backward()
+    close(x.grad, g[f"ssim_{tag}::gx"], 1e-4, 1e-9)
+    close(y.grad, g[f"ssim_{tag}::gy"], 1e-4, 1e-9)
+
+
+def test_train_objective_golden(golden):
+    """DepthNorm fused into the SSIM+L1 kernel == the reference's three calls."""
+    from monocular_depth_estimation_amd.loss import SSIML1
+    from monocular_depth_estimation_amd.utils import DepthNorm
+    g = golden("golden_losses.npz")
+    pred = cu(g["train::pred"], True)
+    depth = cu(g["train::depth"])
+    close(DepthNorm(depth), g["train::depth_n"], 1e-6, 1e-7)
+    crit = SSIML1(1.0, 0.1, depth_norm=True)
+    loss = crit(pred, depth)
+    close(loss, g["train::loss"], 1e-5, 1e-7)
+    close(crit.last_parts[1], g["train::ssim"], 1e-5, 1e-7)
+    close(crit.last_parts[2], g["train::l1"], 1e-5, 1e-7)
+    (2.0 * loss).backward()
+    close(pred.grad, 2.0 * g["train::gpred"], 1e-4, 1e-10)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 2, 2), (1, 2, 5, 7), (3, 1, 17, 70), (32, 1, 480, 640)])
+def test_ssim_l1_vs_oracle_sizes(shape):
+    from monocular_depth_estimation_amd.functional import minmax, ssim3_l1
+    p = torch.from_numpy(seeded(shape, 21, 0, 1))
+    d = torch.from_numpy(seeded(shape, 22, 0.1, 10.0))
+    pg = p.to(DEV).requires_grad_(True)
+    loss, parts = ssim3_l1(pg, d.to(DEV), 1.0, 0.1, target_minmax=minmax(d.to(DEV)))
+    loss.backward()
+    pr = p.clone().double().requires_grad_(True)
+    ref = oops.train_loss(pr, d.double())
+    ref.backward()
+    close(loss, ref, 2e-5, 1e-7, "loss")
+    scale = float(pr.grad.abs().max())
+    close(pg.grad, pr.grad, 1e-3, 1e-4 * scale, "grad")
+
+
+def test_ssim_identical_inputs_full_size():
+    """SSIM(x, x) = 0 everywhere with (1-S)/2 = 0 on the clamp edge; L1 = 0, grad = 0."""
+    from monocular_depth_estimation_amd.functional import ssim3_l1
+    x = torch.rand((32, 1, 480, 640), device=DEV).requires_grad_(True)
+    loss, parts = ssim3_l1(x, x.detach(), 1.0, 0.1)
+    loss.backward()
+    assert abs(float(parts[1])) < 1e-6 and float(parts[2]) == 0.0
+    assert float(x.grad.abs().max()) < 1e-6
+
+
+@pytest.mark.parametrize("tag", ["dl_alh", "dl_mask", "dl_small", "dl_ssim_only"])
+def test_depth_loss_golden(golden, tag):
+    from monocular_depth_estimation_amd.GuideDepth.losses import Depth_Loss
+    g = golden("golden_losses.npz")
+    a, b, gm, mx = (float(v) for v in g[f"{tag}::params"])
+    x = cu(g[f"{tag}::pred"], True)
+    v = Depth_Loss(a, b, gm, maxDepth=mx)(x, cu(g[f"{tag}::gt"]))
+    close(v, g[f"{tag}::loss"], 1e-5, 1e-7)
+    (3.0 * v).backward()
+    close(x.grad, 3.0 * g[f"{tag}::gpred"], 1e-4, 1e-9)
+
+
+def test_depth_loss_full_size_vs_oracle_crop():
+    """cfg2-sized Depth_Loss runs; a 2-sample crop matches the oracle."""
+    from monocular_depth_estimation_amd.functional import depth_loss
+    p = torch.from_numpy(seeded((4, 1, 96, 128), 31, 0, 10))
+    t = torch.from_numpy(seeded((4, 1, 96, 128), 32, 0, 10))
+    pg = p.to(DEV).requires_grad_(True)
+    loss, _ = depth_loss(pg, t.to(DEV), 0.1, 1.0, 1.0, 10.0)
+    loss.backward()
+    pr = p.clone().double().requires_grad_(True)
+    ref = oops.depth_loss(pr, t.double(), 0.1, 1.0, 1.0, 10.0)
+    ref.backward()
+    close(loss, ref, 1e-5, 1e-7)
+    close(pg.grad, pr.grad, 1e-3, 1e-4 * float(pr.grad.abs().max()))
+    big = torch.rand((32, 1, 480, 640), device=DEV).requires_grad_(True)
+    v, parts = depth_loss(big, torch.rand((32, 1, 480, 640), device=DEV), 0.1, 1.0, 1.0, 10.0)
+    v.backward()
+    assert torch.isfinite(big.grad).all() and torch.isfinite(v)
+
+
+# ------------------------------------------------------------- the model
+@pytest.mark.parametrize("tag,cfg", [("gub1", (64, 64, 32)), ("gub2", (32, 32, 16)),
+                                     ("gub3", (16, 16, 1))])
+def test_guided_block_golden(golden, tag, cfg):
+    from monocular_depth_estimation_amd.GuideDepth.model.modules import Guided_Upsampling_Block
+    g = golden("golden_blocks.npz")
+    m = fill_(Guided_Upsampling_Block(*cfg)).to(DEV).train()
+    guide = cu(g[f"{tag}::guide"], True)
+    depth = cu(g[f"{tag}::depth"], True)
+    y = m(guide, depth)
+    close_map(y, g[f"{tag}::y"], 1e-4, "y")
+    y.backward(cu(g[f"{tag}::gy"]))
+    close_map(depth.grad, g[f"{tag}::gdepth"], 1e-4, "gdepth")
+    close_map(guide.grad, g[f"{tag}::gguide"], 1e-4, "gguide")
+
+
+def _grad_norm_check(model, g, rtol):
+    names = list(g["grad_names"])
+    ref = g["grad_norms"]
+    params = dict(model.named_parameters())
+    got = np.array([float(params[n].grad.double().norm()) for n in names])
+    keep = ref > 1e-7 * ref.max()
+    keep &= np.array(["bias" not in n or not any(k in n for k in ("conv1.0", "conv1.3", "_conv.0", "_conv.3"))
+                      for n in names])
+    np.testing.assert_allclose(got[keep], ref[keep], rtol=rtol)
+
+
+def test_guidedepth_golden(golden):
+    from monocular_depth_estimation_amd import GuideDepth
+    from monocular_depth_estimation_amd.loss import SSIML1
+    g = golden("golden_guidedepth.npz")
+    model = fill_(GuideDepth(pretrained=False)).to(DEV).train()
+    x = cu(g["x"])
+    pred = model(x)
+    close_map(pred, g["train_pred"], 1e-3, "train-mode depth map")
+    loss = SSIML1(1.0, 0.1)(pred, cu(g["depth"]))
+    close(loss, g["train_loss"], 1e-4, 1e-7)
+    loss.backward()
+    _grad_norm_check(model, g, rtol=1e-2)
+    model.eval()
+    with torch.no_grad():
+        close_map(model(x), g["eval_pred"], 1e-3, "eval-mode depth map")
+
+
+def test_train_sequence_golden(golden):
+    """Loss-curve parity: 5 steps of the train.py recipe (eval switch after step 0)."""
+    from monocular_depth_estimation_amd import GuideDepth
+    from monocular_depth_estimation_amd.loss import SSIML1
+    from monocular_depth_estimation_amd.train import Trainer, World, make_adam
+    g = golden("golden_trainseq.npz")
+    model = fill_(GuideDepth(pretrained=False)).to(DEV)
+    trainer = Trainer(model, make_adam(model, 1e-4), SSIML1(1.0, 0.1), World(device=torch.device(DEV)))
+    trainer.begin_epoch()
+    losses = []
+    for k in range(len(g["losses"])):
+        image = cu(seeded((2, 3, 64, 96), 100 + k, 0, 1))
+        depth = cu(seeded((2, 1, 64, 96), 200 + k, 0.1, 10.0))
+        losses.append(float(trainer.step(image, depth)))
+        trainer.after_step(k)
+    np.testing.assert_allclose(losses[0], g["losses"][0], rtol=1e-5)
+    np.testing.assert_allclose(losses, g["losses"], rtol=5e-3)
+
+
+def test_guidedepth_cfg2_shape_runs_and_matches_oracle_encoder_free_parts():
+    """640x480 bs=2 forward+backward on the HIP path vs the CPU oracle (1e-3 map tolerance)."""
+    from monocular_depth_estimation_amd import GuideDepth
+    model = fill_(GuideDepth(pretrained=False)).to(DEV).train()
+    ref = fill_(og.GuideDepth()).train()
+    x = torch.from_numpy(seeded((2, 3, 480, 640), 71, 0, 1))
+    pred = model(x.to(DEV))
+    with torch.no_grad():
+        rp = ref(x)
+    close_map(pred, rp, 1e-3, "640x480 depth map")

@@ -1,0 +1,81 @@
+"""Host-side logic of the product package (CPU only, no kernels launched)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops as oops
+
+
+@pytest.mark.parametrize("hi,wi,kw", [
+    (30, 40, dict(size=(60, 80))), (8, 10, dict(size=(60, 80))), (8, 10, dict(size=(30, 40))),
+    (1, 1, dict(size=(8, 10))), (16, 20, dict(scale_factor=2)), (480, 640, dict(scale_factor=0.5)),
+    (481, 641, dict(scale_factor=0.25)), (7, 9, dict(scale_factor=(2, 3))),
+])
+def test_resize_plan_matches_oracle(hi, wi, kw):
+    from monocular_depth_estimation_amd.functional import _out_size_and_scales
+    x = torch.empty(1, 1, hi, wi)
+    got = _out_size_and_scales(x, kw.get("size"), kw.get("scale_factor"), None)
+    ref = oops.resize_plan(hi, wi, kw.get("size"), kw.get("scale_factor"), False)
+    assert got[:2] == ref[:2]
+    assert np.float32(got[2]) == ref[2] and np.float32(got[3]) == ref[3]
+
+
+def test_ops_refuse_cpu_tensors():
+    from monocular_depth_estimation_amd import functional as F
+    x = torch.rand(1, 2, 4, 4)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        F.bilinear_resize(x, scale_factor=2)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        F.ssim3_l1(x, x)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        F.skip_reduce(x, x, torch.rand(1, 2, 1, 1), torch.rand(1))
+    with pytest.raises(NotImplementedError):
+        F.interpolate(x, scale_factor=2, mode="bicubic")
+
+
+def test_guidedepth_state_dict_matches_reference(golden):
+    from monocular_depth_estimation_amd import GuideDepth
+    g = golden("golden_guidedepth.npz")
+    m = GuideDepth(pretrained=False)
+    assert list(m.state_dict().keys()) == list(g["state_dict_keys"])
+    assert sum(p.numel() for p in m.parameters()) == 5824513
+
+
+def test_pretrained_blob_missing_raises(tmp_path):
+    from monocular_depth_estimation_amd.GuideDepth.model.DDRNet_23_slim import DualResNet_Backbone
+    with pytest.raises(FileNotFoundError):
+        DualResNet_Backbone(pretrained=True, weights_path=str(tmp_path / "missing.pth"))
+
+
+def test_model_builder():
+    from monocular_depth_estimation_amd.GuideDepth.model.loader import model_builder
+    s = model_builder("GuideDepth-S", pretrained=False)
+    assert s.up_1.reduce.out_channels == 8 and s.up_3.reduce.out_channels == 1
+    with pytest.raises(ValueError):
+        model_builder("nope")
+
+
+def test_synthetic_batches_are_per_rank_and_deterministic():
+    from monocular_depth_estimation_amd.train import synthetic_batch
+    a0, d0 = synthetic_batch(2, 8, 12, rank=0, step=3, device="cpu")
+    a0b, _ = synthetic_batch(2, 8, 12, rank=0, step=3, device="cpu")
+    a1, d1 = synthetic_batch(2, 8, 12, rank=1, step=3, device="cpu")
+    assert torch.equal(a0, a0b) and not torch.equal(a0, a1)
+    assert float(d0.min()) >= 0.1 and float(d0.max()) < 10.0
+
+
+def test_checkpoint_format_roundtrip(tmp_path):
+    from monocular_depth_estimation_amd.train import load_checkpoint, save_checkpoint
+    m = torch.nn.Linear(3, 2)
+    opt = torch.optim.Adam(m.parameters(), 1e-4)
+    m(torch.rand(4, 3)).sum().backward()
+    opt.step()
+    path = str(tmp_path / "ck" / "global_checkpoint.pth")
+    save_checkpoint(path, 7, m, opt, torch.tensor(0.5))
+    ck = torch.load(path, weights_only=True)
+    assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "loss"}
+    m2 = torch.nn.Linear(3, 2)
+    opt2 = torch.optim.Adam(m2.parameters(), 1e-4)
+    epoch, loss = load_checkpoint(path, m2, opt2)
+    assert epoch == 7 and float(loss) == 0.5
+    assert torch.equal(m2.weight, m.weight)

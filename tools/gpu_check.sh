@@ -1,0 +1,24 @@
+#!/bin/bash
+# GPU-box check: parity tests, smoke, bench.  Each GPU step has its own time
+# limit; a fault/abort/timeout stops the script (no retries).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS=${STEPS:-10}
+WARMUP=${WARMUP:-3}
+run() {  # name seconds cmd...
+  local name=$1 t=$2; shift 2
+  echo "== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  return $rc
+}
+ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+if [ "${SKIP_TESTS:-0}" != 1 ]; then
+  run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-}; rc=$?
+  ok_or_testfail $rc || exit $rc
+fi
+run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+run bench 900 python bench.py --steps "$STEPS" --warmup "$WARMUP" ${BENCH_ARGS:-} || exit $?

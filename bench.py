@@ -42,7 +42,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-bs", type=int, default=4)
     p.add_argument("--cpu-steps", type=int, default=2)
-    p.add_argument("--cudnn-benchmark", type=int, default=1)
+    p.add_argument("--cudnn-benchmark", type=int, default=0)
     p.add_argument("--no-kernel-timing", action="store_true")
     return p.parse_args()
 
@@ -100,8 +100,16 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
+    def log(msg):
+        if world.is_main:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    log(f"model on {world.device}, world {world.size}, bs {args.bs}, {args.height}x{args.width}")
     for i in range(args.warmup):
+        ts = time.perf_counter()
         trainer.step(*batches[i % 2])
+        torch.cuda.synchronize()
+        log(f"warmup step {i}: {time.perf_counter() - ts:.3f} s")
     barrier()
     timing = not args.no_kernel_timing
     if timing:

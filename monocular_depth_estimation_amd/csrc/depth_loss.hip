@@ -104,7 +104,8 @@ __global__ void __launch_bounds__(256)
     const float m = fwd[4];
     const float f = (1.f - m) * 0.5f;
     const bool act = f >= 0.f && f <= 1.f;
-    kfac = act ? gout[0] * beta * -0.5f / ((float)ho * (float)wo) : 0.f;
+    const float nimg = (float)(gridDim.x / tiles_per_img);
+    kfac = act ? gout[0] * beta * -0.5f / ((float)ho * (float)wo * nimg) : 0.f;
   }
   float ssum = 0.f;
   for (int e = tid; e < TH * TW; e += 256) {

@@ -17,7 +17,7 @@ run() {  # name seconds cmd...
 }
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-}; rc=$?
+  run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf -k "${PYTEST_K:-}"; rc=$?
   ok_or_testfail $rc || exit $rc
 fi
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?

@@ -18,12 +18,14 @@ import torch
 from torch import nn
 
 from ...functional import bilinear_resize
+from ...nn import BatchNorm2d
 
 BN_MOMENTUM = 0.1
 
 
-def _bn(c):
-    return nn.BatchNorm2d(c, momentum=BN_MOMENTUM)
+def _bn(c, act="none"):
+    """BatchNorm on the HIP kernel; act='relu' fuses the ReLU that follows it."""
+    return BatchNorm2d(c, momentum=BN_MOMENTUM, act=act)
 
 
 def conv3x3(in_planes, out_planes, stride=1):
@@ -32,23 +34,27 @@ def conv3x3(in_planes, out_planes, stride=1):
 
 
 class BasicBlock(nn.Module):
-    """Two 3x3 conv+BN, residual, optional final ReLU (reference :41-72)."""
+    """Two 3x3 conv+BN, residual, optional final ReLU (reference :41-72).
+
+    bn1 carries the ReLU; bn2 takes the residual and the final ReLU in the
+    same pass (`out += residual; relu(out)` fused into the BN apply).
+    """
     expansion = 1
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, no_relu=False):
         super().__init__()
-        self.conv1, self.bn1 = conv3x3(inplanes, planes, stride), _bn(planes)
-        self.conv2, self.bn2 = conv3x3(planes, planes), _bn(planes)
+        self.conv1, self.bn1 = conv3x3(inplanes, planes, stride), _bn(planes, "relu")
+        self.conv2 = conv3x3(planes, planes)
+        self.bn2 = _bn(planes, "none" if no_relu else "relu")
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
         self.no_relu = no_relu
 
     def forward(self, x):
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.bn2(self.conv2(y))
-        y = y + (x if self.downsample is None else self.downsample(x))
-        return y if self.no_relu else self.relu(y)
+        y = self.bn1(self.conv1(x))
+        res = x if self.downsample is None else self.downsample(x)
+        return self.bn2(self.conv2(y), residual=res)
 
 
 class Bottleneck(nn.Module):
@@ -57,27 +63,26 @@ class Bottleneck(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, no_relu=True):
         super().__init__()
-        self.conv1, self.bn1 = nn.Conv2d(inplanes, planes, 1, bias=False), _bn(planes)
-        self.conv2, self.bn2 = conv3x3(planes, planes, stride), _bn(planes)
+        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.bn1 = _bn(planes, "relu")
+        self.conv2, self.bn2 = conv3x3(planes, planes, stride), _bn(planes, "relu")
         self.conv3 = nn.Conv2d(planes, planes * self.expansion, 1, bias=False)
-        self.bn3 = _bn(planes * self.expansion)
+        self.bn3 = _bn(planes * self.expansion, "none" if no_relu else "relu")
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
         self.stride = stride
         self.no_relu = no_relu
 
     def forward(self, x):
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        y = y + (x if self.downsample is None else self.downsample(x))
-        return y if self.no_relu else self.relu(y)
+        y = self.bn2(self.conv2(self.bn1(self.conv1(x))))
+        res = x if self.downsample is None else self.downsample(x)
+        return self.bn3(self.conv3(y), residual=res)
 
 
 def _pre_act(cin, cout, k, pool=None):
-    """[pool] -> BN -> ReLU -> conv(k, bias=False), the DAPPM branch shape."""
+    """[pool] -> BN+ReLU (fused; Identity keeps the ReLU slot) -> conv(k, bias=False)."""
     mods = [] if pool is None else [pool]
-    mods += [_bn(cin), nn.ReLU(inplace=True),
+    mods += [_bn(cin, "relu"), nn.Identity(),
              nn.Conv2d(cin, cout, k, padding=k // 2, bias=False)]
     return nn.Sequential(*mods)
 
@@ -117,16 +122,16 @@ class segmenthead(nn.Module):  # noqa: N801  (reference class name)
 
     def __init__(self, inplanes, interplanes, outplanes, scale_factor=None):
         super().__init__()
-        self.bn1 = _bn(inplanes)
+        self.bn1 = _bn(inplanes, "relu")
         self.conv1 = nn.Conv2d(inplanes, interplanes, 3, padding=1, bias=False)
-        self.bn2 = _bn(interplanes)
+        self.bn2 = _bn(interplanes, "relu")
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = nn.Conv2d(interplanes, outplanes, 1, padding=0, bias=True)
         self.scale_factor = scale_factor
 
     def forward(self, x):
-        x = self.conv1(self.relu(self.bn1(x)))
-        out = self.conv2(self.relu(self.bn2(x)))
+        x = self.conv1(self.bn1(x))
+        out = self.conv2(self.bn2(x))
         if self.scale_factor is not None:
             out = bilinear_resize(out, size=(x.shape[-2] * self.scale_factor,
                                              x.shape[-1] * self.scale_factor))
@@ -139,12 +144,19 @@ def _make_layer(block, inplanes, planes, blocks, stride=1):
     if stride != 1 or inplanes != planes * block.expansion:
         downsample = nn.Sequential(
             nn.Conv2d(inplanes, planes * block.expansion, 1, stride=stride, bias=False),
-            nn.BatchNorm2d(planes * block.expansion, momentum=BN_MOMENTUM))
+            _bn(planes * block.expansion))
     layers = [block(inplanes, planes, stride, downsample)]
     for i in range(1, blocks):
         layers.append(block(planes * block.expansion, planes, stride=1,
                             no_relu=(i == blocks - 1)))
     return nn.Sequential(*layers)
+
+
+def _seq_bn_residual(seq, x, residual):
+    """residual + seq(x) for a Sequential ending in a BatchNorm: the add runs in the BN pass."""
+    for m in list(seq)[:-1]:
+        x = m(x)
+    return seq[-1](x, residual=residual)
 
 
 class DualResNet(nn.Module):
@@ -157,8 +169,8 @@ class DualResNet(nn.Module):
         self.augment = augment
         self.skip_out = skip_out
         self.conv1 = nn.Sequential(
-            nn.Conv2d(3, planes, 3, stride=2, padding=1), _bn(planes), nn.ReLU(inplace=True),
-            nn.Conv2d(planes, planes, 3, stride=2, padding=1), _bn(planes), nn.ReLU(inplace=True))
+            nn.Conv2d(3, planes, 3, stride=2, padding=1), _bn(planes, "relu"), nn.Identity(),
+            nn.Conv2d(planes, planes, 3, stride=2, padding=1), _bn(planes, "relu"), nn.Identity())
         self.relu = nn.ReLU(inplace=False)
         widths = [planes, planes, planes * 2, planes * 4, planes * 8]
         for i in range(4):
@@ -167,7 +179,7 @@ class DualResNet(nn.Module):
         self.compression3 = nn.Sequential(nn.Conv2d(planes * 4, hp, 1, bias=False), _bn(hp))
         self.compression4 = nn.Sequential(nn.Conv2d(planes * 8, hp, 1, bias=False), _bn(hp))
         self.down3 = nn.Sequential(conv3x3(hp, planes * 4, 2), _bn(planes * 4))
-        self.down4 = nn.Sequential(conv3x3(hp, planes * 4, 2), _bn(planes * 4), nn.ReLU(inplace=True),
+        self.down4 = nn.Sequential(conv3x3(hp, planes * 4, 2), _bn(planes * 4, "relu"), nn.Identity(),
                                    conv3x3(planes * 4, planes * 8, 2), _bn(planes * 8))
         self.layer3_ = _make_layer(block, planes * 2, hp, 2)
         self.layer4_ = _make_layer(block, hp, hp, 2)
@@ -178,7 +190,7 @@ class DualResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
-            elif isinstance(m, nn.BatchNorm2d):
+            elif isinstance(m, nn.BatchNorm2d):  # includes the HIP BatchNorm2d
                 nn.init.ones_(m.weight)
                 nn.init.zeros_(m.bias)
 
@@ -189,11 +201,11 @@ class DualResNet(nn.Module):
         l2 = self.layer2(r(low))
         l3 = self.layer3(r(l2))
         high = self.layer3_(r(l2))
-        low = l3 + self.down3(r(high))
+        low = _seq_bn_residual(self.down3, r(high), l3)  # l3 + down3(relu(high)), add fused into BN
         high = high + bilinear_resize(self.compression3(r(l3)), size=out_size)
         l4 = self.layer4(r(low))
         high = self.layer4_(r(high))
-        low = l4 + self.down4(r(high))
+        low = _seq_bn_residual(self.down4, r(high), l4)
         high = high + bilinear_resize(self.compression4(r(l4)), size=out_size)
         high = self.layer5_(r(high))
         low = bilinear_resize(self.spp(self.layer5(r(low))), size=out_size)

@@ -5,13 +5,14 @@ signatures and state_dict keys.  Hot ops on HIP kernels:
   * cat([x, y], 1) + SELayer (:90, :21-25)  -> functional.se_cat (one fused op,
     the concatenation is never materialised);
   * reduce(residual + depth) (:100)          -> functional.skip_reduce.
-Convolutions + BatchNorm + ReLU stay on PyTorch-ROCm (MIOpen).
+Convolutions stay on PyTorch-ROCm (MIOpen); BatchNorm+ReLU run fused on HIP (nn.py).
 """
 from __future__ import annotations
 
 from torch import nn
 
 from ...functional import se_cat, skip_reduce
+from ...nn import BatchNorm2d
 
 
 class SELayer(nn.Module):
@@ -35,8 +36,9 @@ class SELayer(nn.Module):
 
 
 def _conv_bn_relu(cin, cout, k):
-    return [nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2), nn.BatchNorm2d(cout),
-            nn.ReLU(inplace=True)]
+    """conv -> BN+ReLU fused on the HIP kernel (Identity keeps the ReLU's Sequential slot)."""
+    return [nn.Conv2d(cin, cout, kernel_size=k, padding=k // 2), BatchNorm2d(cout, act="relu"),
+            nn.Identity()]
 
 
 class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)

@@ -32,6 +32,12 @@ enum Kid : int {
   K_DLOSS_FWD,
   K_DLOSS_BWD_COEF,
   K_DLOSS_BWD,
+  K_BN_STATS,
+  K_BN_FINAL,
+  K_BN_APPLY,
+  K_BN_BWD_REDUCE,
+  K_BN_BWD_FINAL,
+  K_BN_BWD_APPLY,
   K_COUNT
 };
 

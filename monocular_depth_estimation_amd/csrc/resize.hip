@@ -98,40 +98,84 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Backward, exact x2 (align_corners=False, scale 0.5, out = 2*in): input
-// index i is read by output indices 2i-1 .. 2i+2 only.
-__global__ void __launch_bounds__(256)
-    bilinear_bwd_x2_kernel(const float* __restrict__ gy, float* __restrict__ gx,
-                           int64_t planes, int hi, int wi) {
-  const int ho = 2 * hi, wo = 2 * wi;
-  const int64_t total = planes * hi * (int64_t)wi;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int j = (int)(t % wi);
-    const int64_t r = t / wi;
-    const int i = (int)(r % hi);
-    const int64_t plane = r / hi;
-    float wr[4], wc[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int o = 2 * i - 1 + k;
-      wr[k] = (o >= 0 && o < ho) ? lin_weight(0.5f, o, i, hi, 0) : 0.f;
-      const int p = 2 * j - 1 + k;
-      wc[k] = (p >= 0 && p < wo) ? lin_weight(0.5f, p, j, wi, 0) : 0.f;
-    }
-    const float* g = gy + plane * ho * (int64_t)wo;
-    float acc = 0.f;
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      if (wr[a] != 0.f) {
-        const float* grow = g + (int64_t)(2 * i - 1 + a) * wo;
-#pragma unroll
-        for (int b = 0; b < 4; ++b)
-          if (wc[b] != 0.f) acc += (wr[a] * wc[b]) * grow[2 * j - 1 + b];
-      }
-    }
-    gx[t] = acc;
+// Exact x2 (align_corners=False, scale 0.5, out = 2*in).  With ATen's
+// source-index clamp the x2 stencil is a 2-tap filter with clamped indices:
+//   out[2i]   = 0.25 x[max(i-1,0)]  + 0.75 x[i]
+//   out[2i+1] = 0.75 x[i] + 0.25 x[min(i+1,in-1)]
+// per axis (rows of horizontally interpolated columns, as ATen orders it),
+// and its adjoint is the 4-tap filter (0.25 0.75 0.75 0.25) over output
+// indices 2i-1..2i+2, again clamped.  One thread owns one input column and
+// slides down RS rows, so every input (fwd) / output-gradient (bwd) row is
+// read once per thread and every result is written once, coalesced.
+constexpr int kX2Rows = 8;   // rows per thread
+constexpr int kX2Warps = 4;  // threadIdx.y
+
+__device__ __forceinline__ float2 x2_hrow(const float* row, int j, int wi) {
+  const float l = row[j > 0 ? j - 1 : 0];
+  const float c = row[j];
+  const float r = row[j < wi - 1 ? j + 1 : wi - 1];
+  return make_float2(0.25f * l + 0.75f * c, 0.75f * c + 0.25f * r);
+}
+
+__global__ void __launch_bounds__(64 * kX2Warps)
+    bilinear_fwd_x2_kernel(const float* __restrict__ x, float* __restrict__ y,
+                           int hi, int wi) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
+  if (j >= wi || i0 >= hi) return;
+  const int64_t plane = blockIdx.z;
+  const float* xp = x + plane * hi * (int64_t)wi;
+  const int wo = 2 * wi;
+  float* yp = y + plane * (2 * hi) * (int64_t)wo + 2 * j;
+  float2 prev = x2_hrow(xp + (int64_t)(i0 > 0 ? i0 - 1 : 0) * wi, j, wi);
+  float2 cur = x2_hrow(xp + (int64_t)i0 * wi, j, wi);
+  const int i1 = i0 + kX2Rows < hi ? i0 + kX2Rows : hi;
+  for (int i = i0; i < i1; ++i) {
+    const float2 nxt = x2_hrow(xp + (int64_t)(i < hi - 1 ? i + 1 : hi - 1) * wi, j, wi);
+    *reinterpret_cast<float2*>(yp + (int64_t)(2 * i) * wo) =
+        make_float2(0.25f * prev.x + 0.75f * cur.x, 0.25f * prev.y + 0.75f * cur.y);
+    *reinterpret_cast<float2*>(yp + (int64_t)(2 * i + 1) * wo) =
+        make_float2(0.75f * cur.x + 0.25f * nxt.x, 0.75f * cur.y + 0.25f * nxt.y);
+    prev = cur;
+    cur = nxt;
   }
+}
+
+// 4-tap adjoint filter of one output-gradient row at input column j.
+__device__ __forceinline__ float x2_hgrad(const float* row, int j, int wo) {
+  const float2 m = *reinterpret_cast<const float2*>(row + 2 * j);
+  const float l = row[2 * j > 0 ? 2 * j - 1 : 0];
+  const float r = row[2 * j + 2 < wo ? 2 * j + 2 : wo - 1];
+  return 0.25f * l + 0.75f * m.x + 0.75f * m.y + 0.25f * r;
+}
+
+__global__ void __launch_bounds__(64 * kX2Warps)
+    bilinear_bwd_x2_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                           int hi, int wi) {
+  const int j = blockIdx.x * 64 + threadIdx.x;
+  const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
+  if (j >= wi || i0 >= hi) return;
+  const int64_t plane = blockIdx.z;
+  const int ho = 2 * hi, wo = 2 * wi;
+  const float* gp = gy + plane * ho * (int64_t)wo;
+  float* xp = gx + plane * hi * (int64_t)wi + j;
+  auto hrow = [&](int o) {
+    o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
+    return x2_hgrad(gp + (int64_t)o * wo, j, wo);
+  };
+  float a = hrow(2 * i0 - 1), b = hrow(2 * i0);
+  const int i1 = i0 + kX2Rows < hi ? i0 + kX2Rows : hi;
+  for (int i = i0; i < i1; ++i) {
+    const float c = hrow(2 * i + 1), d = hrow(2 * i + 2);
+    xp[(int64_t)i * wi] = 0.25f * a + 0.75f * b + 0.75f * c + 0.25f * d;
+    a = c;
+    b = d;
+  }
+}
+
+inline dim3 x2_grid(int64_t planes, int64_t hi, int64_t wi) {
+  return dim3((unsigned)mde::cdiv(wi, 64), (unsigned)mde::cdiv(hi, kX2Rows * kX2Warps),
+              (unsigned)planes);
 }
 
 // Backward, generic ratio: candidate windows per axis, exact weights.
@@ -240,7 +284,13 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   hipStream_t s = (hipStream_t)stream;
   const int64_t rows = n * c * ho;
   const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
-  if (wo % 4 == 0) {
+  const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
+                  ho == 2 * hi && wo == 2 * wi && n * c <= 65535;
+  if (x2) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel,
+               x2_grid(n * c, hi, wi), dim3(64, kX2Warps), 0, (const float*)x,
+               (float*)y, (int)hi, (int)wi);
+  } else if (wo % 4 == 0) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_kernel<4>,
                dim3(grid_for(rows * (wo / 4))), dim3(256), 0,
                (const float*)x, (float*)y, rows, (int)hi, (int)wi, (int)ho,
@@ -264,11 +314,11 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   const int64_t planes = n * c;
   const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
   const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
-                  ho == 2 * hi && wo == 2 * wi;
+                  ho == 2 * hi && wo == 2 * wi && planes <= 65535;
   if (x2) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
-               dim3(grid_for(planes * hi * wi)), dim3(256), 0,
-               (const float*)gy, (float*)gx, planes, (int)hi, (int)wi);
+               x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
+               (float*)gx, (int)hi, (int)wi);
   } else {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_kernel,
                dim3(grid_for(planes * hi * wi)), dim3(256), 0,

@@ -197,20 +197,79 @@ __global__ void __launch_bounds__(kTile)
   }
 }
 
-// gw[pair] = sum over blocks (in block order) of slab[block][pair].
+// Small weights (cin*cout + cout <= 64, e.g. up_3's 16 -> 1): every thread
+// keeps ALL weight-gradient partials in registers over its grid-stride pixels
+// (4 consecutive pixels per step, float4), then one block reduction — no LDS
+// staging per tile.
+template <int CI, int CO>
+__global__ void __launch_bounds__(256)
+    skip_bwd_reg_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                        const float* __restrict__ d, const float* __restrict__ wt,
+                        float* __restrict__ gs, float* __restrict__ slab, int64_t n,
+                        int64_t hw) {
+  constexpr int NP = CI * CO + CO;
+  __shared__ float sw[CI * CO];
+  __shared__ float red[4][NP];
+  for (int i = threadIdx.x; i < CI * CO; i += 256) sw[i] = wt[i];
+  __syncthreads();
+  float acc[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) acc[k] = 0.f;
+  const int64_t q4 = hw >> 2, total = n * q4;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t nidx = t / q4, p = (t - nidx * q4) << 2;
+    float4 gv[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      gv[o] = *reinterpret_cast<const float4*>(g + (nidx * CO + o) * hw + p);
+      acc[CI * CO + o] += (gv[o].x + gv[o].y) + (gv[o].z + gv[o].w);
+    }
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      const int64_t off = (nidx * CI + c) * hw + p;
+      const float4 a = *reinterpret_cast<const float4*>(r + off);
+      const float4 e = *reinterpret_cast<const float4*>(d + off);
+      const float4 sv = make_float4(a.x + e.x, a.y + e.y, a.z + e.z, a.w + e.w);
+      float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int o = 0; o < CO; ++o) {
+        const float w = sw[o * CI + c];
+        o4.x += w * gv[o].x; o4.y += w * gv[o].y; o4.z += w * gv[o].z; o4.w += w * gv[o].w;
+        acc[o * CI + c] += (gv[o].x * sv.x + gv[o].y * sv.y) + (gv[o].z * sv.z + gv[o].w * sv.w);
+      }
+      *reinterpret_cast<float4*>(gs + off) = o4;
+    }
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const float v = mde::wave_sum(acc[k]);
+    if (lane == 0) red[wid][k] = v;
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < NP; k += 256)
+    slab[(int64_t)blockIdx.x * NP + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+}
+
+// gw[pair] = sum over blocks of slab[block][pair]: one block per pair, fixed
+// per-thread order then a fixed tree -> deterministic.
 __global__ void __launch_bounds__(256)
     skip_slab_reduce_kernel(const float* __restrict__ slab, int nblocks,
                             int npairs, int cout, float* __restrict__ gw,
                             float* __restrict__ gb) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float red[4];
+  const int t = blockIdx.x;
   const int stride = npairs + cout;
-  if (t >= stride) return;
   float a = 0.f;
-  for (int k = 0; k < nblocks; ++k) a += slab[(int64_t)k * stride + t];
-  if (t < npairs)
-    gw[t] = a;
-  else
-    gb[t - npairs] = a;
+  for (int k = threadIdx.x; k < nblocks; k += 256) a += slab[(int64_t)k * stride + t];
+  a = mde::block_sum256(a, red);
+  if (threadIdx.x == 0) {
+    if (t < npairs)
+      gw[t] = a;
+    else
+      gb[t - npairs] = a;
+  }
 }
 
 inline int bwd_blocks(int64_t n, int64_t hw) {
@@ -285,7 +344,15 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
              dim3(kTile), (bwd_lds<CI_, CO_, FAST_>()), (const float*)gout,        \
              (const float*)r, (const float*)d, wt, (float*)gs, slab, n,      \
              (int)cin, (int)cout, hw)
-  if (cin == 64 && cout == 32) {
+  if (cin == 16 && cout == 1 && hw % 4 == 0) {
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<16, 1>), dim3(nb),
+               dim3(256), 0, (const float*)gout, (const float*)r, (const float*)d,
+               wt, (float*)gs, slab, n, hw);
+  } else if (cin == 4 && cout == 1 && hw % 4 == 0) {
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1>), dim3(nb),
+               dim3(256), 0, (const float*)gout, (const float*)r, (const float*)d,
+               wt, (float*)gs, slab, n, hw);
+  } else if (cin == 64 && cout == 32) {
     SKIP_BWD(64, 32, 4, 4, true);
   } else if (cin == 32 && cout == 16) {
     SKIP_BWD(32, 16, 2, 2, true);
@@ -299,8 +366,8 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
 #undef SKIP_BWD
   const int stride = (int)(cin * cout + cout);
   MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s,
-             skip_slab_reduce_kernel, dim3((unsigned)mde::cdiv(stride, 256)),
-             dim3(256), 0, slab, nb, (int)(cin * cout), (int)cout, gw, gb);
+             skip_slab_reduce_kernel, dim3((unsigned)stride), dim3(256), 0, slab,
+             nb, (int)(cin * cout), (int)cout, gw, gb);
   return MDE_OK;
 }
 

@@ -1,0 +1,99 @@
+"""BatchNorm2d on the HIP kernels, with the following ReLU / residual add fused.
+
+`BatchNorm2d(c, act="relu")` is an nn.BatchNorm2d (same parameters, buffers
+and state_dict keys) whose forward runs mde_batchnorm_fwd_{train,eval} and
+applies the activation — and optionally adds a residual first — in the same
+streaming pass.  Where the reference writes `BN -> ReLU(inplace)` the ReLU
+module slot is kept as an nn.Identity so Sequential indices (and therefore
+state_dict keys) are unchanged.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from . import _abi
+from .functional import _gpu, _ws
+
+_ACTS = {"none": 0, "relu": 1}
+
+
+class _BatchNormAct(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training,
+                momentum, eps, act):
+        x = x.contiguous()
+        residual = residual.contiguous() if residual is not None else None
+        n, c, h, w = x.shape
+        y = torch.empty_like(x)
+        mean = torch.empty(c, dtype=torch.float32, device=x.device)
+        invstd = torch.empty(c, dtype=torch.float32, device=x.device)
+        st = _abi.stream_of(x)
+        if training:
+            ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
+            _abi.call("mde_batchnorm_fwd_train", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(bias),
+                      _abi.ptr(running_mean), _abi.ptr(running_var), _abi.ptr(nbt),
+                      float(momentum), float(eps), _abi.ptr(residual), _abi.ptr(y),
+                      _abi.ptr(mean), _abi.ptr(invstd), n, c, h, w, act, _abi.ptr(ws),
+                      _abi.dtype_code(x), st)
+        else:
+            _abi.call("mde_batchnorm_fwd_eval", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(bias),
+                      _abi.ptr(running_mean), _abi.ptr(running_var), float(eps),
+                      _abi.ptr(residual), _abi.ptr(y), _abi.ptr(mean), _abi.ptr(invstd),
+                      n, c, h, w, act, _abi.dtype_code(x), st)
+        ctx.save_for_backward(x, weight, bias, residual, mean, invstd)
+        ctx.training, ctx.act = bool(training), act
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, bias, residual, mean, invstd = ctx.saved_tensors
+        gy = gy.contiguous()
+        n, c, h, w = x.shape
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(weight) if ctx.needs_input_grad[1] else None
+        gb = torch.empty_like(bias) if ctx.needs_input_grad[2] else None
+        want_r = residual is not None and ctx.needs_input_grad[3]
+        # with no activation the residual's gradient is gy itself: no write needed
+        gr = torch.empty_like(x) if (want_r and ctx.act) else None
+        ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
+        _abi.call("mde_batchnorm_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(residual),
+                  _abi.ptr(weight), _abi.ptr(bias), _abi.ptr(mean), _abi.ptr(invstd),
+                  int(ctx.training), _abi.ptr(gx), _abi.ptr(gr), _abi.ptr(gw), _abi.ptr(gb),
+                  n, c, h, w, ctx.act, _abi.ptr(ws), _abi.dtype_code(gy), _abi.stream_of(gy))
+        if want_r and not ctx.act:
+            gr = gy
+        return gx, gw, gb, gr, None, None, None, None, None, None, None
+
+
+def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None):
+    """act(bn(x) + residual) with nn.BatchNorm2d semantics (train / eval by bn.training)."""
+    _gpu(x, residual)
+    if bn.weight is None or bn.bias is None:
+        raise NotImplementedError("affine=False BatchNorm has no HIP kernel")
+    training = bn.training or not bn.track_running_stats
+    if training and bn.momentum is None:
+        raise NotImplementedError("cumulative-average BatchNorm (momentum=None) has no HIP kernel")
+    track = bn.training and bn.track_running_stats
+    return _BatchNormAct.apply(
+        x, bn.weight, bn.bias, residual,
+        bn.running_mean if (track or not training) else None,
+        bn.running_var if (track or not training) else None,
+        bn.num_batches_tracked if track else None,
+        training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, _ACTS[act])
+
+
+class BatchNorm2d(nn.BatchNorm2d):
+    """nn.BatchNorm2d on HIP kernels with an optional fused activation."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, act="none", **kw):
+        super().__init__(num_features, eps=eps, momentum=momentum, **kw)
+        if act not in _ACTS:
+            raise ValueError(f"act must be one of {sorted(_ACTS)}")
+        self.act = act
+
+    def forward(self, x, residual=None):
+        return batch_norm_act(x, self, self.act, residual)
+
+    def extra_repr(self):
+        return super().extra_repr() + f", act={self.act}"

@@ -20,5 +20,8 @@ if [ "${SKIP_TESTS:-0}" != 1 ]; then
   run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf -k "${PYTEST_K:-}"; rc=$?
   ok_or_testfail $rc || exit $rc
 fi
+if [ "${KBENCH:-1}" = 1 ]; then
+  run kbench 600 python tools/kbench.py --json gpurun_out/kbench.json || exit $?
+fi
 run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 run bench 900 python bench.py --steps "$STEPS" --warmup "$WARMUP" ${BENCH_ARGS:-} || exit $?

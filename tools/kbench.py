@@ -1,0 +1,119 @@
+"""Per-op micro-benchmark of the HIP kernels at GuideDepth cfg2 shapes (640x480, bs=32).
+
+    python tools/kbench.py [--reps 20]
+
+Times each op's forward and backward with torch.cuda.Event around `reps`
+back-to-back calls (after 3 warm-ups) and prints algorithmic GB/s (SURVEY
+§8(d) byte formulas) against the 8 TB/s HBM peak.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd import functional as F
+    from monocular_depth_estimation_amd.nn import BatchNorm2d
+    dev = "cuda"
+    rows = []
+
+    def report(name, ms, nbytes):
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        rows.append({"op": name, "ms": round(ms, 4), "GBps": round(gbs, 1), "frac": round(gbs / 8000, 3)})
+        print(f"{name:44s} {ms * 1e3:9.1f} us {gbs:8.1f} GB/s  {gbs / 8000:6.1%}", flush=True)
+
+    n = 32
+    # bilinear x2 (decoder) and DDRNet resizes
+    for c, h, w in ((64, 60, 80), (32, 120, 160), (16, 240, 320)):
+        x = torch.rand(n, c, h, w, device=dev)
+        y = F.bilinear_resize(x, scale_factor=2)
+        gy = torch.rand_like(y)
+        nb = 4.0 * n * c * (h * w + 4 * h * w)
+        report(f"bilinear_fwd x2 {c}x{h}x{w}", timeit(lambda: F.bilinear_resize(x, scale_factor=2), a.reps), nb)
+        ho, wo = 2 * h, 2 * w
+        report(f"bilinear_bwd x2 {c}x{h}x{w}", timeit(lambda: _abi.call(
+            "mde_bilinear_bwd", gy.data_ptr(), x.data_ptr(), n, c, h, w, ho, wo, 0.5, 0.5, 0, 0,
+            _abi.stream_of(x)), a.reps), nb)
+    for c, hi, wi in ((64, 15, 20), (128, 8, 10)):
+        x = torch.rand(n, c, hi, wi, device=dev)
+        nb = 4.0 * n * c * (hi * wi + 60 * 80)
+        report(f"bilinear_fwd {c}x{hi}x{wi}->60x80", timeit(lambda: F.bilinear_resize(x, size=(60, 80)), a.reps), nb)
+    # SE + cat and skip fusion at the three decoder resolutions
+    for c, h, w, cout in ((64, 120, 160, 32), (32, 240, 320, 16), (16, 480, 640, 1)):
+        half = c // 2
+        xa = torch.rand(n, half, h, w, device=dev)
+        xb = torch.rand(n, half, h, w, device=dev)
+        w1 = torch.rand(c, c, device=dev) * 0.1
+        w2 = torch.rand(c, c, device=dev) * 0.1
+        big = 4.0 * n * c * h * w
+        report(f"se_cat fwd {c}x{h}x{w}", timeit(lambda: F.se_cat(xa, xb, w1, w2), a.reps), 3 * big)
+        xa.requires_grad_(True)
+        xb.requires_grad_(True)
+        out = F.se_cat(xa, xb, w1, w2)
+        g = torch.rand_like(out)
+        report(f"se_cat bwd {c}x{h}x{w}",
+               timeit(lambda: torch.autograd.grad(out, (xa, xb), g, retain_graph=True), a.reps), 4 * big)
+        r = torch.rand(n, c, h, w, device=dev)
+        d = torch.rand(n, c, h, w, device=dev)
+        wt = torch.rand(cout, c, 1, 1, device=dev)
+        b = torch.rand(cout, device=dev)
+        pix = n * h * w * 4.0
+        report(f"skip_reduce fwd {c}->{cout} {h}x{w}", timeit(lambda: F.skip_reduce(r, d, wt, b), a.reps),
+               pix * (2 * c + cout))
+        r.requires_grad_(True)
+        wt.requires_grad_(True)
+        o = F.skip_reduce(r, d, wt, b)
+        go = torch.rand_like(o)
+        report(f"skip_reduce bwd {c}->{cout} {h}x{w}",
+               timeit(lambda: torch.autograd.grad(o, (r, wt), go, retain_graph=True), a.reps),
+               pix * (3 * c + cout))
+    # BatchNorm(+ReLU) at representative shapes
+    for c, h, w in ((16, 480, 640), (32, 240, 320), (64, 120, 160), (256, 15, 20)):
+        x = torch.rand(n, c, h, w, device=dev, requires_grad=True)
+        bn = BatchNorm2d(c, act="relu").to(dev).train()
+        big = 4.0 * n * c * h * w
+        report(f"bn+relu fwd {c}x{h}x{w}", timeit(lambda: bn(x), a.reps), 3 * big)
+        y = bn(x)
+        gy = torch.rand_like(y)
+        report(f"bn+relu bwd {c}x{h}x{w}",
+               timeit(lambda: torch.autograd.grad(y, (x,), gy, retain_graph=True), a.reps), 5 * big)
+        ref = torch.nn.BatchNorm2d(c).to(dev).train()
+        report(f"  (MIOpen BN fwd {c}x{h}x{w})", timeit(lambda: ref(x), a.reps), 3 * big)
+    # loss
+    p = torch.rand(n, 1, 480, 640, device=dev, requires_grad=True)
+    t = torch.rand(n, 1, 480, 640, device=dev) * 10
+    mm = F.minmax(t)
+    report("ssim3_l1 fwd+grad 480x640", timeit(lambda: F.ssim3_l1(p, t, 1.0, 0.1, target_minmax=mm), a.reps),
+           3 * 4.0 * n * 480 * 640)
+    report("minmax 480x640", timeit(lambda: F.minmax(t), a.reps), 4.0 * n * 480 * 640)
+    if a.json:
+        json.dump(rows, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

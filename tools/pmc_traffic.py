@@ -1,0 +1,95 @@
+"""HBM bytes per launch of the hand-written kernels from rocprofv3 PMC passes.
+
+    python tools/pmc_traffic.py FETCH.csv WRITE.csv [--last-steps 2] [-o profiles/r01_pmc_traffic.json]
+
+FETCH_SIZE and WRITE_SIZE come from separate --pmc passes (they do not fit
+one TCC pass).  Per MI355X_MICROARCH.md §HBM: both are in KiB; on gfx950
+FETCH_SIZE reports half the bytes of a wide coalesced read, so
+  traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
+Only the launches of the last K train steps are used (steady state, steps
+delimited by minmax_partial_kernel as in tools/trace_steps.py).  Keys are the
+timing-registry names bench.py reports (mde_kernel_name).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import json
+import re
+
+# demangled kernel symbol -> timing-registry name (csrc/timing.hip)
+NAMES = [
+    (r"bilinear_fwd_kernel", "bilinear_fwd"),
+    (r"bilinear_bwd(_x2)?_kernel", "bilinear_bwd"),
+    (r"nearest_fwd_kernel", "nearest_fwd"),
+    (r"nearest_bwd_kernel", "nearest_bwd"),
+    (r"se_partial_kernel<false>", "se_squeeze"),
+    (r"se_partial_kernel<true>", "se_bwd_dot"),
+    (r"se_fc_kernel", "se_fc"),
+    (r"se_scale_kernel", "se_scale"),
+    (r"se_(bwd_fc|wgrad)_kernel", "se_bwd_fc"),
+    (r"se_apply_kernel", "se_bwd_apply"),
+    (r"skip_fwd_kernel", "skip_reduce_fwd"),
+    (r"skip_bwd_kernel", "skip_reduce_bwd"),
+    (r"skip_slab_reduce_kernel", "skip_reduce_bwd_reduce"),
+    (r"minmax_partial_kernel", "minmax"),
+    (r"minmax_final_kernel", "minmax_final"),
+    (r"depthnorm_kernel", "depthnorm_apply"),
+    (r"ssim3_l1_kernel", "ssim3_l1"),
+    (r"loss_final_kernel", "loss_final"),
+    (r"bn_stats_kernel", "bn_fwd_stats"),
+    (r"bn_fwd_final_kernel", "bn_fwd_final"),
+    (r"bn_apply_kernel", "bn_fwd_apply"),
+    (r"bn_bwd_reduce_kernel", "bn_bwd_reduce"),
+    (r"bn_bwd_final_kernel", "bn_bwd_final"),
+    (r"bn_bwd_apply_kernel", "bn_bwd_apply"),
+]
+
+
+def registry_name(sym: str):
+    for pat, name in NAMES:
+        if re.search(pat, sym):
+            return name
+    return None
+
+
+def load(path, counter, last_steps):
+    rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    marks = [i for i, r in enumerate(rows) if "minmax_partial_kernel" in r["Kernel_Name"]]
+    start = marks[-last_steps - 1] + 1 if len(marks) > last_steps else 0
+    agg = collections.defaultdict(lambda: [0.0, 0])
+    for r in rows[start:]:
+        name = registry_name(r["Kernel_Name"])
+        if name:
+            agg[name][0] += float(r["Counter_Value"])
+            agg[name][1] += 1
+    return agg
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--last-steps", type=int, default=2)
+    ap.add_argument("-o", "--out", default="")
+    a = ap.parse_args()
+    f = load(a.fetch, "FETCH_SIZE", a.last_steps)
+    w = load(a.write, "WRITE_SIZE", a.last_steps)
+    out = {}
+    for name in sorted(set(f) | set(w)):
+        fk, fn = f.get(name, [0.0, 1])
+        wk, wn = w.get(name, [0.0, 1])
+        out[name] = {"fetch_bytes_per_launch": 2 * fk * 1024 / fn,
+                     "write_bytes_per_launch": wk * 1024 / wn,
+                     "bytes_per_launch": 2 * fk * 1024 / fn + wk * 1024 / wn,
+                     "launches": fn}
+    txt = json.dumps(out, indent=1)
+    if a.out:
+        open(a.out, "w").write(txt + "\n")
+    print(txt)
+
+
+if __name__ == "__main__":
+    main()

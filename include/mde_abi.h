@@ -174,44 +174,48 @@ int mde_depth_loss_bwd(const void* pred, const void* gt, float alpha,
                        void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
- * BatchNorm2d with fused activation / residual (NCHW).
- * Replaces nn.BatchNorm2d and the ReLU (and, in the residual blocks, the
- * `out += residual; relu(out)`) that follows it at the 73 BN sites of
+ * BatchNorm2d with the preceding conv bias, the following activation and a
+ * residual add fused (NCHW).
+ * Replaces nn.BatchNorm2d — plus the bias add of the conv feeding it and the
+ * ReLU / `out += residual; relu(out)` that follows it — at the 73 BN sites of
  * GuideDepth: src/GuideDepth/model/modules.py:43-49,53-59,68-74 and
  * src/GuideDepth/model/DDRNet_23_slim.py:46-72,80-113,118-172,201-210,
  * 229-265,294-298.
- *   y = act(x * scale[c] + shift[c] + residual)   (residual nullable)
- *   act: 0 = identity, 1 = ReLU.  gamma/beta/stats are fp32 [c].
- * Training: batch mean / biased variance over (n,h,w); running stats (nullable
- * together) updated with `momentum` and the unbiased variance;
- * *num_batches_tracked += 1 (nullable).  save_mean / save_invstd [c] are
- * written for the backward.  Eval: running statistics, also written to
- * save_mean / save_invstd.
+ *   z = x + prebias[c]                              (prebias nullable)
+ *   y = act(gamma*(z - mean)/sqrt(var + eps) + beta + residual)
+ *   act: 0 = identity, 1 = ReLU; residual nullable; gamma/beta/stats fp32 [c].
+ * Training: batch mean / biased variance of z over (n,h,w); running stats
+ * (nullable together) updated with `momentum` and the unbiased variance;
+ * *num_batches_tracked += 1 (nullable).  Eval: running statistics.
+ * save_mean (mean of the RAW x, i.e. without prebias) and save_invstd [c]
+ * are written for the backward in both modes.
  * ------------------------------------------------------------------------- */
 size_t mde_batchnorm_workspace(int64_t n, int64_t c, int64_t h, int64_t w);
 int mde_batchnorm_fwd_train(const void* x, const float* gamma, const float* beta,
-                            float* running_mean, float* running_var,
-                            int64_t* num_batches_tracked, float momentum,
-                            float eps, const void* residual, void* y,
-                            float* save_mean, float* save_invstd, int64_t n,
-                            int64_t c, int64_t h, int64_t w, int act,
+                            const float* prebias, float* running_mean,
+                            float* running_var, int64_t* num_batches_tracked,
+                            float momentum, float eps, const void* residual,
+                            void* y, float* save_mean, float* save_invstd,
+                            int64_t n, int64_t c, int64_t h, int64_t w, int act,
                             void* workspace, int dtype, void* stream);
 int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
-                           const float* running_mean, const float* running_var,
-                           float eps, const void* residual, void* y,
-                           float* save_mean, float* save_invstd, int64_t n,
-                           int64_t c, int64_t h, int64_t w, int act, int dtype,
-                           void* stream);
+                           const float* prebias, const float* running_mean,
+                           const float* running_var, float eps,
+                           const void* residual, void* y, float* save_mean,
+                           float* save_invstd, int64_t n, int64_t c, int64_t h,
+                           int64_t w, int act, int dtype, void* stream);
 /* Backward.  `training` selects batch-statistics gradients.  The activation
  * mask is recomputed from x (and residual), so y need not be kept.
  * gresidual (nullable) receives d/d residual; with act == 0 it equals gy and
- * may be left NULL.  ggamma / gbeta (nullable) are overwritten. */
+ * may be left NULL.  ggamma / gbeta / gprebias (nullable) are overwritten;
+ * gprebias = sum over (n,h,w) of d/dz (the folded conv bias gradient). */
 int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       const float* gamma, const float* beta, const float* mean,
                       const float* invstd, int training, void* gx,
-                      void* gresidual, float* ggamma, float* gbeta, int64_t n,
-                      int64_t c, int64_t h, int64_t w, int act,
-                      void* workspace, int dtype, void* stream);
+                      void* gresidual, float* ggamma, float* gbeta,
+                      float* gprebias, int64_t n, int64_t c, int64_t h,
+                      int64_t w, int act, void* workspace, int dtype,
+                      void* stream);
 
 /* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).

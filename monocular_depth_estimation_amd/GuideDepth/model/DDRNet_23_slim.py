@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from ...functional import bilinear_resize
-from ...nn import BatchNorm2d
+from ...nn import BatchNorm2d, run_sequential
 
 BN_MOMENTUM = 0.1
 
@@ -197,7 +197,7 @@ class DualResNet(nn.Module):
     def forward(self, x):
         out_size = (x.shape[-2] // 8, x.shape[-1] // 8)
         r = self.relu
-        low = self.layer1(self.conv1(x))
+        low = self.layer1(run_sequential(self.conv1, x))  # conv biases folded into the BNs
         l2 = self.layer2(r(low))
         l3 = self.layer3(r(l2))
         high = self.layer3_(r(l2))

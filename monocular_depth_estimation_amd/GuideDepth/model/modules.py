@@ -5,14 +5,15 @@ signatures and state_dict keys.  Hot ops on HIP kernels:
   * cat([x, y], 1) + SELayer (:90, :21-25)  -> functional.se_cat (one fused op,
     the concatenation is never materialised);
   * reduce(residual + depth) (:100)          -> functional.skip_reduce.
-Convolutions stay on PyTorch-ROCm (MIOpen); BatchNorm+ReLU run fused on HIP (nn.py).
+Convolutions stay on PyTorch-ROCm (MIOpen) without their bias; conv bias +
+BatchNorm + ReLU run as one fused HIP pass (nn.py run_sequential).
 """
 from __future__ import annotations
 
 from torch import nn
 
 from ...functional import se_cat, skip_reduce
-from ...nn import BatchNorm2d
+from ...nn import BatchNorm2d, run_sequential
 
 
 class SELayer(nn.Module):
@@ -75,9 +76,9 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
             self.SE_block = SELayer(comb_features, reduction=1)
 
     def forward(self, guide, depth):
-        x = self.feature_conv(depth)
+        x = run_sequential(self.feature_conv, depth)
         if self.guidance_type == "full":
-            second = self.guide_conv(guide)
+            second = run_sequential(self.guide_conv, guide)
         elif self.guidance_type == "raw":
             second = guide
         else:
@@ -86,7 +87,8 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
             xy = self.SE_block.forward_cat(x, second) if second is not None else self.SE_block(x)
         else:
             xy = x if second is None else _cat(x, second)
-        return skip_reduce(self.comb_conv(xy), depth, self.reduce.weight, self.reduce.bias)
+        return skip_reduce(run_sequential(self.comb_conv, xy), depth, self.reduce.weight,
+                           self.reduce.bias)
 
 
 def _cat(x, y):

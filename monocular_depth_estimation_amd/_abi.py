@@ -53,11 +53,11 @@ SIGNATURES = {
     "mde_depth_loss_bwd": (_int, [_vp, _vp, _f32, _f32, _f32, _f32, _vp, _vp, _vp, _i64, _i64, _i64,
                                   _vp, _int, _vp]),
     "mde_batchnorm_workspace": (_sz, [_i64, _i64, _i64, _i64]),
-    "mde_batchnorm_fwd_train": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp, _vp,
-                                       _i64, _i64, _i64, _i64, _int, _vp, _int, _vp]),
-    "mde_batchnorm_fwd_eval": (_int, [_vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp,
+    "mde_batchnorm_fwd_train": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp, _vp, _vp,
+                                       _vp, _i64, _i64, _i64, _i64, _int, _vp, _int, _vp]),
+    "mde_batchnorm_fwd_eval": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _f32, _vp, _vp, _vp, _vp,
                                       _i64, _i64, _i64, _i64, _int, _int, _vp]),
-    "mde_batchnorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp, _vp,
+    "mde_batchnorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _int, _vp, _int, _vp]),
     "mde_timing_enable": (_int, [_int]),
     "mde_timing_reset": (_int, []),

@@ -1,31 +1,36 @@
-// BatchNorm2d (NCHW, fp32) with fused activation and residual for gfx950.
+// BatchNorm2d (NCHW, fp32) with fused conv bias, activation and residual.
 //
-// Replaces nn.BatchNorm2d (+ the ReLU / residual add that follows it) at the
-// 73 BN sites of GuideDepth: src/GuideDepth/model/modules.py:43-49,53-59,68-74
-// and src/GuideDepth/model/DDRNet_23_slim.py:46-49,80-86,119-172,201-203,
-// 231-235,244-265,294-298.  MIOpen's spatial BN was 88 of 153 ms of a
-// 640x480 bs=32 train step (profiles/r01_*), ~10% of HBM bandwidth.
+// Replaces nn.BatchNorm2d (+ the conv bias in front of it, + the ReLU /
+// residual add after it) at the 73 BN sites of GuideDepth:
+// src/GuideDepth/model/modules.py:43-49,53-59,68-74 and
+// src/GuideDepth/model/DDRNet_23_slim.py:46-72,80-113,118-172,201-210,
+// 229-265,294-298.  MIOpen's spatial BN was 88 of 153 ms of a 640x480 bs=32
+// train step (profiles/r01_*), ~10% of HBM bandwidth.
 //
-//   y = act(x * scale[c] + shift[c] (+ r))      scale = gamma*invstd,
-//                                               shift = beta - mean*scale
-// Training: batch mean / biased variance over (N,H,W) per channel, running
-// stats updated with momentum and the unbiased variance, num_batches_tracked
-// += 1 — nn.BatchNorm2d semantics.  Eval: running statistics.
+//   z = x + b[c]                     (b: the preceding conv's bias, nullable)
+//   y = act(scale[c] * z + shift[c] (+ residual))
+// Training: batch mean / biased variance of z over (N,H,W); running stats
+// updated with momentum and the unbiased variance; num_batches_tracked += 1.
+// Eval: running statistics.  Folding the conv bias here removes the conv's
+// broadcast bias add and its (N,H,W) bias-gradient reduction: d/db = sum of
+// this BN's input gradient, which falls out of the backward's own sums.
 //
-// Forward  = stats (per-slice shifted sums) -> final (per channel, double)
-//            -> apply (streaming).            HBM: 2 reads + 1 write of x.
-// Backward = reduce (sum dy', sum dy'(x-mean)) -> final -> apply, where
-//            dy' = dy * [act'] is recomputed from x (and r) — y is never
-//            stored.                          HBM: 4 reads + 1 write.
-// All reductions are two-level with fixed order: deterministic.
+// Launches: forward  = stats (per-slice shifted sums) + apply;
+//           backward = reduce (sum dy', sum dy'(x-mean)) + apply.
+// The per-channel finalisation (double precision, fixed order) is recomputed
+// by every apply block from the slice partials — no separate tiny kernel —
+// and one designated block per channel writes the saved / running statistics
+// and the parameter gradients.  dy' = dy * [act'] is recomputed from x (and
+// the residual), so y is never kept for the backward.
 #include <cmath>
 
 #include "common.h"
 
 namespace {
 
-constexpr int kTarget = 2048;     // blocks to aim for per reduction launch
-constexpr int kMinSlice = 4096;   // elements per slice at least
+constexpr int kTarget = 2048;    // blocks to aim for per reduction launch
+constexpr int kMinSlice = 4096;  // elements per slice at least
+constexpr int kPlaneChunk4 = 1024;  // float4 per apply block in plane mode
 
 struct Geo {
   int64_t c, hw, total;  // total = n * hw elements per channel
@@ -42,7 +47,7 @@ Geo geometry(int64_t n, int64_t c, int64_t hw) {
   const int64_t by_size = mde::cdiv(g.total, kMinSlice);
   if (s > by_size) s = by_size;
   if (s < 1) s = 1;
-  if (s > 1024) s = 1024;
+  if (s > 128) s = 128;
   g.slices = (int)s;
   int64_t len = mde::cdiv(g.total, s);
   if (hw % 4 == 0) len = mde::cdiv(len, 4) * 4;
@@ -50,17 +55,93 @@ Geo geometry(int64_t n, int64_t c, int64_t hw) {
   return g;
 }
 
+// Apply kernels run "plane mode" (one channel per block, grid (chunks,
+// planes)) for large planes and "channel-table mode" (all channels'
+// coefficients in LDS, grid-stride) for small ones.
+bool plane_mode(int64_t hw) { return hw % 4 == 0 && hw / 4 >= 256; }
+
 __device__ __forceinline__ float act_fn(float v, int act) {
   return act == 1 ? fmaxf(v, 0.f) : v;
 }
 
-// Per-channel scale/shift from (gamma, beta, mean, invstd).
-__device__ __forceinline__ void coeffs(const float* gamma, const float* beta,
-                                       const float* mean, const float* invstd,
-                                       int64_t c, float* sc, float* sh) {
-  const float s = gamma[c] * invstd[c];
-  *sc = s;
-  *sh = beta[c] - mean[c] * s;
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Sum of the two partial arrays of channel ch, by one full wave (lane-strided,
+// then a fixed butterfly) -> identical result in every block.
+__device__ __forceinline__ void wave_slices(const float* part, int64_t ch,
+                                            int slices, double* a, double* b) {
+  const int lane = threadIdx.x & 63;
+  double x = 0.0, y = 0.0;
+  for (int s = lane; s < slices; s += 64) {
+    x += (double)part[(ch * slices + s) * 2];
+    y += (double)part[(ch * slices + s) * 2 + 1];
+  }
+  *a = wave_sum_d(x);
+  *b = wave_sum_d(y);
+}
+
+// Per-channel forward constants.  mean_x is the mean of the RAW input x
+// (without the folded bias); scale/shift act on raw x.
+struct FwdCh {
+  float sc, sh, mean_x, invstd;
+};
+
+struct FwdArgs {
+  const float* gamma;
+  const float* beta;
+  const float* prebias;  // nullable
+  const float* part;     // training: slice partials
+  int slices;
+  int64_t total;
+  int64_t hw;
+  float eps, momentum;
+  float* rmean;          // nullable (no running-stat tracking)
+  float* rvar;
+  int64_t* nbt;          // nullable
+  float* save_mean;
+  float* save_invstd;
+  int training;
+};
+
+// Training: (s1, s2) are the shifted sums of channel ch (shift = its first
+// element); writes the designated outputs when `owner`.
+__device__ FwdCh fwd_channel(const FwdArgs& A, const float* x, int64_t ch,
+                             double s1, double s2, bool owner) {
+  FwdCh r;
+  const float pb = A.prebias ? A.prebias[ch] : 0.f;
+  double mean_x, invstd;
+  if (A.training) {
+    const double n = (double)A.total;
+    const double ref = (double)x[ch * A.hw];
+    const double dm = s1 / n;
+    double var = s2 / n - dm * dm;
+    if (var < 0.0) var = 0.0;
+    mean_x = ref + dm;
+    invstd = 1.0 / std::sqrt(var + (double)A.eps);
+    if (owner && A.rmean) {
+      const double unb = A.total > 1 ? var * n / (n - 1.0) : var;
+      const double m = (double)A.momentum;
+      A.rmean[ch] = (float)((1.0 - m) * (double)A.rmean[ch] + m * (mean_x + (double)pb));
+      A.rvar[ch] = (float)((1.0 - m) * (double)A.rvar[ch] + m * unb);
+    }
+  } else {
+    mean_x = (double)A.rmean[ch] - (double)pb;
+    invstd = 1.0 / std::sqrt((double)A.rvar[ch] + (double)A.eps);
+  }
+  r.mean_x = (float)mean_x;
+  r.invstd = (float)invstd;
+  if (owner) {
+    A.save_mean[ch] = r.mean_x;
+    A.save_invstd[ch] = r.invstd;
+    if (ch == 0 && A.training && A.nbt) A.nbt[0] += 1;
+  }
+  r.sc = A.gamma[ch] * r.invstd;
+  r.sh = A.beta[ch] - r.mean_x * r.sc;
+  return r;
 }
 
 // part[(c * slices + s) * 2 + {0,1}] = sum(x - ref), sum((x - ref)^2)
@@ -103,86 +184,82 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Training: combine slices (double), write mean/invstd, update running stats.
-__global__ void __launch_bounds__(256)
-    bn_fwd_final_kernel(const float* __restrict__ x, int64_t c, int64_t hw,
-                        int64_t total, int slices, const float* __restrict__ part,
-                        float momentum, float eps, float* __restrict__ rmean,
-                        float* __restrict__ rvar, int64_t* __restrict__ nbt,
-                        float* __restrict__ mean, float* __restrict__ invstd) {
-  const int64_t ch = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (ch == 0 && nbt) nbt[0] += 1;
-  if (ch >= c) return;
-  double a = 0.0, b = 0.0;
-  const float* p = part + ch * slices * 2;
-  for (int s = 0; s < slices; ++s) {
-    a += (double)p[2 * s];
-    b += (double)p[2 * s + 1];
+__device__ __forceinline__ float4 fwd4(float4 v, float4 q, bool has_r, float sc,
+                                       float sh, int act) {
+  v.x = v.x * sc + sh;
+  v.y = v.y * sc + sh;
+  v.z = v.z * sc + sh;
+  v.w = v.w * sc + sh;
+  if (has_r) {
+    v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
   }
-  const double n = (double)total;
-  const double ref = (double)x[ch * hw];
-  const double dm = a / n;
-  double var = b / n - dm * dm;
-  if (var < 0.0) var = 0.0;
-  const double m = ref + dm;
-  mean[ch] = (float)m;
-  invstd[ch] = (float)(1.0 / std::sqrt(var + (double)eps));
-  if (rmean) {
-    const double unb = total > 1 ? var * n / (n - 1.0) : var;
-    rmean[ch] = (float)((1.0 - momentum) * (double)rmean[ch] + momentum * m);
-    rvar[ch] = (float)((1.0 - momentum) * (double)rvar[ch] + momentum * unb);
+  v.x = act_fn(v.x, act); v.y = act_fn(v.y, act);
+  v.z = act_fn(v.z, act); v.w = act_fn(v.w, act);
+  return v;
+}
+
+// Plane mode: grid (ceil(hw4 / 1024), n*c); 4 float4 per thread.
+__global__ void __launch_bounds__(256)
+    bn_apply_plane_kernel(const float* __restrict__ x, const float* __restrict__ r,
+                          float* __restrict__ y, int64_t c, int64_t hw, int act,
+                          FwdArgs A) {
+  __shared__ float cf[2];
+  const int64_t plane = blockIdx.y;
+  const int64_t ch = plane % c;
+  if (threadIdx.x < 64) {
+    double s1 = 0.0, s2 = 0.0;
+    if (A.training) wave_slices(A.part, ch, A.slices, &s1, &s2);
+    if (threadIdx.x == 0) {
+      const bool owner = blockIdx.x == 0 && plane < c;
+      const FwdCh k = fwd_channel(A, x, ch, s1, s2, owner);
+      cf[0] = k.sc;
+      cf[1] = k.sh;
+    }
+  }
+  __syncthreads();
+  const float sc = cf[0], sh = cf[1];
+  const int64_t hw4 = hw >> 2;
+  const float4* xp = reinterpret_cast<const float4*>(x + plane * hw);
+  const float4* rp = r ? reinterpret_cast<const float4*>(r + plane * hw) : nullptr;
+  float4* yp = reinterpret_cast<float4*>(y + plane * hw);
+  const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
+#pragma unroll
+  for (int k = 0; k < kPlaneChunk4 / 256; ++k) {
+    const int64_t i = b0 + k * 256 + threadIdx.x;
+    if (i < hw4) {
+      const float4 q = rp ? rp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      yp[i] = fwd4(xp[i], q, rp != nullptr, sc, sh, act);
+    }
   }
 }
 
-// Eval: mean/invstd from the running statistics.
+// Channel-table mode for small planes: every block builds all channels'
+// coefficients in LDS (block 0 is the designated writer), then grid-strides.
 __global__ void __launch_bounds__(256)
-    bn_eval_final_kernel(int64_t c, const float* __restrict__ rmean,
-                         const float* __restrict__ rvar, float eps,
-                         float* __restrict__ mean, float* __restrict__ invstd) {
-  const int64_t ch = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  mean[ch] = rmean[ch];
-  invstd[ch] = 1.f / sqrtf(rvar[ch] + eps);
-}
-
-// y = act(x * scale + shift (+ r)); one block row of planes, float4 lanes.
-template <bool VEC>
-__global__ void __launch_bounds__(256)
-    bn_apply_kernel(const float* __restrict__ x, const float* __restrict__ r,
-                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                    const float* __restrict__ mean, const float* __restrict__ invstd,
-                    float* __restrict__ y, int64_t planes, int64_t c, int64_t hw,
-                    int act) {
-  if (VEC) {
-    const int64_t hw4 = hw >> 2, total = planes * hw4;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * blockDim.x) {
-      const int64_t plane = t / hw4;
-      float sc, sh;
-      coeffs(gamma, beta, mean, invstd, plane % c, &sc, &sh);
-      float4 v = reinterpret_cast<const float4*>(x)[t];
-      v.x = v.x * sc + sh;
-      v.y = v.y * sc + sh;
-      v.z = v.z * sc + sh;
-      v.w = v.w * sc + sh;
-      if (r) {
-        const float4 q = reinterpret_cast<const float4*>(r)[t];
-        v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+    bn_apply_table_kernel(const float* __restrict__ x, const float* __restrict__ r,
+                          float* __restrict__ y, int64_t planes, int64_t c,
+                          int64_t hw, int act, FwdArgs A) {
+  extern __shared__ float tab[];  // [2][c]
+  for (int64_t ch = threadIdx.x; ch < c; ch += blockDim.x) {
+    double s1 = 0.0, s2 = 0.0;
+    if (A.training) {
+      for (int s = 0; s < A.slices; ++s) {
+        s1 += (double)A.part[(ch * A.slices + s) * 2];
+        s2 += (double)A.part[(ch * A.slices + s) * 2 + 1];
       }
-      v.x = act_fn(v.x, act); v.y = act_fn(v.y, act);
-      v.z = act_fn(v.z, act); v.w = act_fn(v.w, act);
-      reinterpret_cast<float4*>(y)[t] = v;
     }
-  } else {
-    const int64_t total = planes * hw;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * blockDim.x) {
-      float sc, sh;
-      coeffs(gamma, beta, mean, invstd, (t / hw) % c, &sc, &sh);
-      float v = x[t] * sc + sh;
-      if (r) v += r[t];
-      y[t] = act_fn(v, act);
-    }
+    const FwdCh k = fwd_channel(A, x, ch, s1, s2, blockIdx.x == 0);
+    tab[ch] = k.sc;
+    tab[c + ch] = k.sh;
+  }
+  __syncthreads();
+  const int64_t total = planes * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ch = (t / hw) % c;
+    float v = x[t] * tab[ch] + tab[c + ch];
+    if (r) v += r[t];
+    y[t] = act_fn(v, act);
   }
 }
 
@@ -194,7 +271,7 @@ __device__ __forceinline__ float dy_eff(float g, float xv, float rv, float sc,
   return pre > 0.f ? g : 0.f;
 }
 
-// part[(c*slices+s)*2] = sum dy', sum dy' * (x - mean)
+// part[(c*slices+s)*2] = sum dy', sum dy' * (x - mean_x)
 template <bool VEC>
 __global__ void __launch_bounds__(256)
     bn_bwd_reduce_kernel(const float* __restrict__ gy, const float* __restrict__ x,
@@ -208,9 +285,9 @@ __global__ void __launch_bounds__(256)
   const int s = blockIdx.x;
   const int64_t i0 = s * slice_len;
   const int64_t i1 = i0 + slice_len < total ? i0 + slice_len : total;
-  float sc, sh;
-  coeffs(gamma, beta, mean, invstd, ch, &sc, &sh);
-  const float mu = mean[ch];
+  const float is = invstd[ch];
+  const float sc = gamma[ch] * is, mu = mean[ch];
+  const float sh = beta[ch] - mu * sc;
   const int64_t chw = c * hw;
   const int64_t base = ch * hw;
   float s1 = 0.f, s2 = 0.f;
@@ -248,91 +325,166 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// ggamma = invstd * sum dy'(x-mean), gbeta = sum dy'; dx = A dy' + B x + D.
-__global__ void __launch_bounds__(256)
-    bn_bwd_final_kernel(int64_t c, int64_t total, int slices,
-                        const float* __restrict__ part, const float* __restrict__ gamma,
-                        const float* __restrict__ mean, const float* __restrict__ invstd,
-                        int training, float* __restrict__ ggamma,
-                        float* __restrict__ gbeta, float* __restrict__ coef) {
-  const int64_t ch = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  double a = 0.0, b = 0.0;
-  const float* p = part + ch * slices * 2;
-  for (int s = 0; s < slices; ++s) {
-    a += (double)p[2 * s];
-    b += (double)p[2 * s + 1];
-  }
-  const double is = (double)invstd[ch];
-  const double scale = (double)gamma[ch] * is;
-  if (ggamma) ggamma[ch] = (float)(b * is);
-  if (gbeta) gbeta[ch] = (float)a;
+struct BwdArgs {
+  const float* gamma;
+  const float* beta;
+  const float* mean;    // raw-x mean saved by the forward
+  const float* invstd;
+  const float* part;
+  int slices;
+  int64_t total;
+  int training;
+  float* ggamma;        // nullable
+  float* gbeta;         // nullable
+  float* gprebias;      // nullable
+};
+
+struct BwdCh {
+  float sc, sh, A, B, D;
+};
+
+// dx = A dy' + B x + D;  ggamma = invstd * sum dy'(x-mean);  gbeta = sum dy';
+// d(prebias) = sum dx (0 up to rounding in training, A*sum dy' in eval).
+__device__ BwdCh bwd_channel(const BwdArgs& P, int64_t ch, double sdy,
+                             double sdyx, bool owner) {
+  BwdCh r;
+  const double is = (double)P.invstd[ch];
+  const double mu = (double)P.mean[ch];
+  const double scale = (double)P.gamma[ch] * is;
   double A = scale, B = 0.0, D = 0.0;
-  if (training) {
-    const double n = (double)total;
-    B = -scale * is * is * b / n;
-    D = -scale * a / n - B * (double)mean[ch];
+  const double n = (double)P.total;
+  if (P.training) {
+    B = -scale * is * is * sdyx / n;
+    D = -scale * sdy / n - B * mu;
   }
-  coef[3 * ch] = (float)A;
-  coef[3 * ch + 1] = (float)B;
-  coef[3 * ch + 2] = (float)D;
+  if (owner) {
+    if (P.ggamma) P.ggamma[ch] = (float)(sdyx * is);
+    if (P.gbeta) P.gbeta[ch] = (float)sdy;
+    if (P.gprebias) P.gprebias[ch] = (float)(A * sdy + B * n * mu + D * n);
+  }
+  r.sc = P.gamma[ch] * P.invstd[ch];
+  r.sh = P.beta[ch] - P.mean[ch] * r.sc;
+  r.A = (float)A;
+  r.B = (float)B;
+  r.D = (float)D;
+  return r;
 }
 
-template <bool VEC>
 __global__ void __launch_bounds__(256)
-    bn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ x,
-                        const float* __restrict__ r,
-                        const float* __restrict__ gamma, const float* __restrict__ beta,
-                        const float* __restrict__ mean, const float* __restrict__ invstd,
-                        const float* __restrict__ coef, float* __restrict__ gx,
-                        float* __restrict__ gr, int64_t planes, int64_t c, int64_t hw,
-                        int act) {
-  if (VEC) {
-    const int64_t hw4 = hw >> 2, total = planes * hw4;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * blockDim.x) {
-      const int64_t ch = (t / hw4) % c;
-      float sc, sh;
-      coeffs(gamma, beta, mean, invstd, ch, &sc, &sh);
-      const float A = coef[3 * ch], B = coef[3 * ch + 1], D = coef[3 * ch + 2];
-      const float4 g = reinterpret_cast<const float4*>(gy)[t];
-      const float4 v = reinterpret_cast<const float4*>(x)[t];
-      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r) q = reinterpret_cast<const float4*>(r)[t];
+    bn_bwd_apply_plane_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                              const float* __restrict__ r, float* __restrict__ gx,
+                              float* __restrict__ gr, int64_t c, int64_t hw, int act,
+                              BwdArgs P) {
+  __shared__ float cf[5];
+  const int64_t plane = blockIdx.y;
+  const int64_t ch = plane % c;
+  if (threadIdx.x < 64) {
+    double a, b;
+    wave_slices(P.part, ch, P.slices, &a, &b);
+    if (threadIdx.x == 0) {
+      const BwdCh k = bwd_channel(P, ch, a, b, blockIdx.x == 0 && plane < c);
+      cf[0] = k.sc; cf[1] = k.sh; cf[2] = k.A; cf[3] = k.B; cf[4] = k.D;
+    }
+  }
+  __syncthreads();
+  const float sc = cf[0], sh = cf[1], A = cf[2], B = cf[3], D = cf[4];
+  const int64_t hw4 = hw >> 2;
+  const float4* gp = reinterpret_cast<const float4*>(gy + plane * hw);
+  const float4* xp = reinterpret_cast<const float4*>(x + plane * hw);
+  const float4* rp = r ? reinterpret_cast<const float4*>(r + plane * hw) : nullptr;
+  float4* op = reinterpret_cast<float4*>(gx + plane * hw);
+  float4* orp = gr ? reinterpret_cast<float4*>(gr + plane * hw) : nullptr;
+  const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
+#pragma unroll
+  for (int k = 0; k < kPlaneChunk4 / 256; ++k) {
+    const int64_t i = b0 + k * 256 + threadIdx.x;
+    if (i < hw4) {
+      const float4 g = gp[i], v = xp[i];
+      const float4 q = rp ? rp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 e = make_float4(dy_eff(g.x, v.x, q.x, sc, sh, act),
                                    dy_eff(g.y, v.y, q.y, sc, sh, act),
                                    dy_eff(g.z, v.z, q.z, sc, sh, act),
                                    dy_eff(g.w, v.w, q.w, sc, sh, act));
-      reinterpret_cast<float4*>(gx)[t] =
-          make_float4(A * e.x + B * v.x + D, A * e.y + B * v.y + D,
-                      A * e.z + B * v.z + D, A * e.w + B * v.w + D);
-      if (gr) reinterpret_cast<float4*>(gr)[t] = e;
+      op[i] = make_float4(A * e.x + B * v.x + D, A * e.y + B * v.y + D,
+                          A * e.z + B * v.z + D, A * e.w + B * v.w + D);
+      if (orp) orp[i] = e;
     }
-  } else {
-    const int64_t total = planes * hw;
-    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-         t += (int64_t)gridDim.x * blockDim.x) {
-      const int64_t ch = (t / hw) % c;
-      float sc, sh;
-      coeffs(gamma, beta, mean, invstd, ch, &sc, &sh);
-      const float v = x[t];
-      const float e = dy_eff(gy[t], v, r ? r[t] : 0.f, sc, sh, act);
-      gx[t] = coef[3 * ch] * e + coef[3 * ch + 1] * v + coef[3 * ch + 2];
-      if (gr) gr[t] = e;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    bn_bwd_apply_table_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                              const float* __restrict__ r, float* __restrict__ gx,
+                              float* __restrict__ gr, int64_t planes, int64_t c,
+                              int64_t hw, int act, BwdArgs P) {
+  extern __shared__ float tab[];  // [5][c]
+  for (int64_t ch = threadIdx.x; ch < c; ch += blockDim.x) {
+    double a = 0.0, b = 0.0;
+    for (int s = 0; s < P.slices; ++s) {
+      a += (double)P.part[(ch * P.slices + s) * 2];
+      b += (double)P.part[(ch * P.slices + s) * 2 + 1];
     }
+    const BwdCh k = bwd_channel(P, ch, a, b, blockIdx.x == 0);
+    tab[ch] = k.sc;
+    tab[c + ch] = k.sh;
+    tab[2 * c + ch] = k.A;
+    tab[3 * c + ch] = k.B;
+    tab[4 * c + ch] = k.D;
+  }
+  __syncthreads();
+  const int64_t total = planes * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t ch = (t / hw) % c;
+    const float v = x[t];
+    const float e = dy_eff(gy[t], v, r ? r[t] : 0.f, tab[ch], tab[c + ch], act);
+    gx[t] = tab[2 * c + ch] * e + tab[3 * c + ch] * v + tab[4 * c + ch];
+    if (gr) gr[t] = e;
   }
 }
 
 inline int stream_grid(int64_t work) {
   const int64_t b = mde::cdiv(work, 256);
-  return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
 }
 
-inline size_t round16(size_t v) { return (v + 15) & ~size_t(15); }
+inline dim3 plane_grid(int64_t planes, int64_t hw) {
+  return dim3((unsigned)mde::cdiv(hw / 4, kPlaneChunk4), (unsigned)planes);
+}
 
 bool args_ok(int64_t n, int64_t c, int64_t h, int64_t w) {
-  return n > 0 && c > 0 && h > 0 && w > 0 && c <= 65535 &&
+  return n > 0 && c > 0 && h > 0 && w > 0 && c <= 4096 && n * c <= 65535 &&
          n * h * w < ((int64_t)1 << 40);
+}
+
+int launch_stats(const float* x, int64_t n, int64_t c, int64_t hw, const Geo& g,
+                 float* part, hipStream_t s) {
+  const double bytes = 4.0 * n * c * (double)hw;
+  if (hw % 4 == 0) {
+    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, bn_stats_kernel<true>,
+               dim3(g.slices, (unsigned)c), dim3(256), 0, x, c, hw, g.total,
+               g.slice_len, g.slices, part);
+  } else {
+    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, bn_stats_kernel<false>,
+               dim3(g.slices, (unsigned)c), dim3(256), 0, x, c, hw, g.total,
+               g.slice_len, g.slices, part);
+  }
+  return MDE_OK;
+}
+
+int launch_fwd_apply(const float* x, const float* r, float* y, int64_t n,
+                     int64_t c, int64_t hw, int act, const FwdArgs& A,
+                     hipStream_t s) {
+  const double bytes = 4.0 * n * c * (double)hw * (r ? 3.0 : 2.0);
+  if (plane_mode(hw)) {
+    MDE_LAUNCH(mde::K_BN_APPLY, bytes, s, bn_apply_plane_kernel,
+               plane_grid(n * c, hw), dim3(256), 0, x, r, y, c, hw, act, A);
+  } else {
+    MDE_LAUNCH(mde::K_BN_APPLY, bytes, s, bn_apply_table_kernel,
+               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 2 * c, x,
+               r, y, n * c, c, hw, act, A);
+  }
+  return MDE_OK;
 }
 
 }  // namespace
@@ -341,16 +493,15 @@ extern "C" {
 
 size_t mde_batchnorm_workspace(int64_t n, int64_t c, int64_t h, int64_t w) {
   const Geo g = geometry(n, c, h * w);
-  return round16(sizeof(float) * 2 * (size_t)c * g.slices) +
-         round16(sizeof(float) * 3 * (size_t)c);
+  return sizeof(float) * 2 * (size_t)c * g.slices;
 }
 
 int mde_batchnorm_fwd_train(const void* x, const float* gamma, const float* beta,
-                            float* running_mean, float* running_var,
-                            int64_t* num_batches_tracked, float momentum,
-                            float eps, const void* residual, void* y,
-                            float* save_mean, float* save_invstd, int64_t n,
-                            int64_t c, int64_t h, int64_t w, int act,
+                            const float* prebias, float* running_mean,
+                            float* running_var, int64_t* num_batches_tracked,
+                            float momentum, float eps, const void* residual,
+                            void* y, float* save_mean, float* save_invstd,
+                            int64_t n, int64_t c, int64_t h, int64_t w, int act,
                             void* workspace, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace ||
@@ -360,73 +511,40 @@ int mde_batchnorm_fwd_train(const void* x, const float* gamma, const float* beta
   const int64_t hw = h * w;
   const Geo g = geometry(n, c, hw);
   float* part = (float*)workspace;
-  const bool vec = hw % 4 == 0;
-  const double bytes = 4.0 * n * c * (double)hw;
-  if (vec) {
-    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, bn_stats_kernel<true>,
-               dim3(g.slices, (unsigned)c), dim3(256), 0, (const float*)x, c, hw,
-               g.total, g.slice_len, g.slices, part);
-  } else {
-    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, bn_stats_kernel<false>,
-               dim3(g.slices, (unsigned)c), dim3(256), 0, (const float*)x, c, hw,
-               g.total, g.slice_len, g.slices, part);
-  }
-  MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * c * g.slices, s, bn_fwd_final_kernel,
-             dim3((unsigned)mde::cdiv(c, 256)), dim3(256), 0, (const float*)x, c,
-             hw, g.total, g.slices, (const float*)part, momentum, eps,
-             running_mean, running_var, num_batches_tracked, save_mean,
-             save_invstd);
-  const double abytes = bytes * (residual ? 3.0 : 2.0);
-  if (vec) {
-    MDE_LAUNCH(mde::K_BN_APPLY, abytes, s, bn_apply_kernel<true>,
-               dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)x,
-               (const float*)residual, gamma, beta, (const float*)save_mean,
-               (const float*)save_invstd, (float*)y, n * c, c, hw, act);
-  } else {
-    MDE_LAUNCH(mde::K_BN_APPLY, abytes, s, bn_apply_kernel<false>,
-               dim3(stream_grid(n * c * hw)), dim3(256), 0, (const float*)x,
-               (const float*)residual, gamma, beta, (const float*)save_mean,
-               (const float*)save_invstd, (float*)y, n * c, c, hw, act);
-  }
-  return MDE_OK;
+  int st = launch_stats((const float*)x, n, c, hw, g, part, s);
+  if (st) return st;
+  FwdArgs A{gamma, beta, prebias, part, g.slices, g.total, hw, eps, momentum,
+            running_mean, running_var, num_batches_tracked, save_mean, save_invstd, 1};
+  return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c,
+                          hw, act, A, s);
 }
 
 int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
-                           const float* running_mean, const float* running_var,
-                           float eps, const void* residual, void* y,
-                           float* save_mean, float* save_invstd, int64_t n,
-                           int64_t c, int64_t h, int64_t w, int act, int dtype,
-                           void* stream) {
+                           const float* prebias, const float* running_mean,
+                           const float* running_var, float eps,
+                           const void* residual, void* y, float* save_mean,
+                           float* save_invstd, int64_t n, int64_t c, int64_t h,
+                           int64_t w, int act, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !running_mean || !running_var || !y ||
       !save_mean || !save_invstd || act < 0 || act > 1 || !args_ok(n, c, h, w))
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
-  MDE_LAUNCH(mde::K_BN_FINAL, 16.0 * c, s, bn_eval_final_kernel,
-             dim3((unsigned)mde::cdiv(c, 256)), dim3(256), 0, c, running_mean,
-             running_var, eps, save_mean, save_invstd);
-  const double abytes = 4.0 * n * c * (double)hw * (residual ? 3.0 : 2.0);
-  if (hw % 4 == 0) {
-    MDE_LAUNCH(mde::K_BN_APPLY, abytes, s, bn_apply_kernel<true>,
-               dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)x,
-               (const float*)residual, gamma, beta, (const float*)save_mean,
-               (const float*)save_invstd, (float*)y, n * c, c, hw, act);
-  } else {
-    MDE_LAUNCH(mde::K_BN_APPLY, abytes, s, bn_apply_kernel<false>,
-               dim3(stream_grid(n * c * hw)), dim3(256), 0, (const float*)x,
-               (const float*)residual, gamma, beta, (const float*)save_mean,
-               (const float*)save_invstd, (float*)y, n * c, c, hw, act);
-  }
-  return MDE_OK;
+  FwdArgs A{gamma, beta, prebias, nullptr, 0, n * hw, hw, eps, 0.f,
+            (float*)running_mean, (float*)running_var, nullptr, save_mean,
+            save_invstd, 0};
+  return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c,
+                          hw, act, A, s);
 }
 
 int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       const float* gamma, const float* beta, const float* mean,
                       const float* invstd, int training, void* gx,
-                      void* gresidual, float* ggamma, float* gbeta, int64_t n,
-                      int64_t c, int64_t h, int64_t w, int act,
-                      void* workspace, int dtype, void* stream) {
+                      void* gresidual, float* ggamma, float* gbeta,
+                      float* gprebias, int64_t n, int64_t c, int64_t h,
+                      int64_t w, int act, void* workspace, int dtype,
+                      void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !x || !gamma || !beta || !mean || !invstd || !gx || !workspace ||
       act < 0 || act > 1 || !args_ok(n, c, h, w) || (gresidual && !residual && act))
@@ -435,40 +553,32 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
   const int64_t hw = h * w;
   const Geo g = geometry(n, c, hw);
   float* part = (float*)workspace;
-  float* coef = (float*)((char*)workspace + round16(sizeof(float) * 2 * (size_t)c * g.slices));
-  const bool vec = hw % 4 == 0;
+  const float* rr = act ? (const float*)residual : nullptr;
   const double big = 4.0 * n * c * (double)hw;
-  const double rb = residual && act ? big : 0.0;
-  if (vec) {
+  const double rb = rr ? big : 0.0;
+  if (hw % 4 == 0) {
     MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, bn_bwd_reduce_kernel<true>,
                dim3(g.slices, (unsigned)c), dim3(256), 0, (const float*)gy,
-               (const float*)x, act ? (const float*)residual : nullptr, gamma,
-               beta, mean, invstd, c, hw, g.total, g.slice_len, g.slices, act,
-               part);
+               (const float*)x, rr, gamma, beta, mean, invstd, c, hw, g.total,
+               g.slice_len, g.slices, act, part);
   } else {
     MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, bn_bwd_reduce_kernel<false>,
                dim3(g.slices, (unsigned)c), dim3(256), 0, (const float*)gy,
-               (const float*)x, act ? (const float*)residual : nullptr, gamma,
-               beta, mean, invstd, c, hw, g.total, g.slice_len, g.slices, act,
-               part);
+               (const float*)x, rr, gamma, beta, mean, invstd, c, hw, g.total,
+               g.slice_len, g.slices, act, part);
   }
-  MDE_LAUNCH(mde::K_BN_BWD_FINAL, 8.0 * c * g.slices, s, bn_bwd_final_kernel,
-             dim3((unsigned)mde::cdiv(c, 256)), dim3(256), 0, c, g.total,
-             g.slices, (const float*)part, gamma, mean, invstd, training,
-             ggamma, gbeta, coef);
+  BwdArgs P{gamma, beta, mean, invstd, part, g.slices, g.total, training,
+            ggamma, gbeta, gprebias};
   const double abytes = 3.0 * big + rb + (gresidual ? big : 0.0);
-  if (vec) {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_kernel<true>,
-               dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)gy,
-               (const float*)x, act ? (const float*)residual : nullptr, gamma,
-               beta, mean, invstd, (const float*)coef, (float*)gx,
-               (float*)gresidual, n * c, c, hw, act);
+  if (plane_mode(hw)) {
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_plane_kernel,
+               plane_grid(n * c, hw), dim3(256), 0, (const float*)gy,
+               (const float*)x, rr, (float*)gx, (float*)gresidual, c, hw, act, P);
   } else {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_kernel<false>,
-               dim3(stream_grid(n * c * hw)), dim3(256), 0, (const float*)gy,
-               (const float*)x, act ? (const float*)residual : nullptr, gamma,
-               beta, mean, invstd, (const float*)coef, (float*)gx,
-               (float*)gresidual, n * c, c, hw, act);
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_table_kernel,
+               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c,
+               (const float*)gy, (const float*)x, rr, (float*)gx,
+               (float*)gresidual, n * c, c, hw, act, P);
   }
   return MDE_OK;
 }

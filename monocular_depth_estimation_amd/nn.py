@@ -20,8 +20,8 @@ _ACTS = {"none": 0, "relu": 1}
 
 class _BatchNormAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, residual, running_mean, running_var, nbt, training,
-                momentum, eps, act):
+    def forward(ctx, x, weight, bias, prebias, residual, running_mean, running_var, nbt,
+                training, momentum, eps, act):
         x = x.contiguous()
         residual = residual.contiguous() if residual is not None else None
         n, c, h, w = x.shape
@@ -32,17 +32,17 @@ class _BatchNormAct(torch.autograd.Function):
         if training:
             ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
             _abi.call("mde_batchnorm_fwd_train", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(bias),
-                      _abi.ptr(running_mean), _abi.ptr(running_var), _abi.ptr(nbt),
-                      float(momentum), float(eps), _abi.ptr(residual), _abi.ptr(y),
+                      _abi.ptr(prebias), _abi.ptr(running_mean), _abi.ptr(running_var),
+                      _abi.ptr(nbt), float(momentum), float(eps), _abi.ptr(residual), _abi.ptr(y),
                       _abi.ptr(mean), _abi.ptr(invstd), n, c, h, w, act, _abi.ptr(ws),
                       _abi.dtype_code(x), st)
         else:
             _abi.call("mde_batchnorm_fwd_eval", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(bias),
-                      _abi.ptr(running_mean), _abi.ptr(running_var), float(eps),
-                      _abi.ptr(residual), _abi.ptr(y), _abi.ptr(mean), _abi.ptr(invstd),
-                      n, c, h, w, act, _abi.dtype_code(x), st)
+                      _abi.ptr(prebias), _abi.ptr(running_mean), _abi.ptr(running_var),
+                      float(eps), _abi.ptr(residual), _abi.ptr(y), _abi.ptr(mean),
+                      _abi.ptr(invstd), n, c, h, w, act, _abi.dtype_code(x), st)
         ctx.save_for_backward(x, weight, bias, residual, mean, invstd)
-        ctx.training, ctx.act = bool(training), act
+        ctx.training, ctx.act, ctx.has_prebias = bool(training), act, prebias is not None
         return y
 
     @staticmethod
@@ -53,22 +53,29 @@ class _BatchNormAct(torch.autograd.Function):
         gx = torch.empty_like(x)
         gw = torch.empty_like(weight) if ctx.needs_input_grad[1] else None
         gb = torch.empty_like(bias) if ctx.needs_input_grad[2] else None
-        want_r = residual is not None and ctx.needs_input_grad[3]
+        gpb = torch.empty_like(weight) if (ctx.has_prebias and ctx.needs_input_grad[3]) else None
+        want_r = residual is not None and ctx.needs_input_grad[4]
         # with no activation the residual's gradient is gy itself: no write needed
         gr = torch.empty_like(x) if (want_r and ctx.act) else None
         ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
         _abi.call("mde_batchnorm_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(residual),
                   _abi.ptr(weight), _abi.ptr(bias), _abi.ptr(mean), _abi.ptr(invstd),
                   int(ctx.training), _abi.ptr(gx), _abi.ptr(gr), _abi.ptr(gw), _abi.ptr(gb),
-                  n, c, h, w, ctx.act, _abi.ptr(ws), _abi.dtype_code(gy), _abi.stream_of(gy))
+                  _abi.ptr(gpb), n, c, h, w, ctx.act, _abi.ptr(ws), _abi.dtype_code(gy),
+                  _abi.stream_of(gy))
         if want_r and not ctx.act:
             gr = gy
-        return gx, gw, gb, gr, None, None, None, None, None, None, None
+        return gx, gw, gb, gpb, gr, None, None, None, None, None, None, None
 
 
-def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None):
-    """act(bn(x) + residual) with nn.BatchNorm2d semantics (train / eval by bn.training)."""
-    _gpu(x, residual)
+def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, prebias=None):
+    """act(bn(x + prebias) + residual) with nn.BatchNorm2d semantics (mode by bn.training).
+
+    `prebias` is the bias of the convolution feeding this BN, folded in: the
+    conv runs without it (no broadcast add, no bias-gradient reduction) and
+    its gradient comes out of the BN backward.
+    """
+    _gpu(x, residual, prebias)
     if bn.weight is None or bn.bias is None:
         raise NotImplementedError("affine=False BatchNorm has no HIP kernel")
     training = bn.training or not bn.track_running_stats
@@ -76,11 +83,34 @@ def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None):
         raise NotImplementedError("cumulative-average BatchNorm (momentum=None) has no HIP kernel")
     track = bn.training and bn.track_running_stats
     return _BatchNormAct.apply(
-        x, bn.weight, bn.bias, residual,
+        x, bn.weight, bn.bias, prebias, residual,
         bn.running_mean if (track or not training) else None,
         bn.running_var if (track or not training) else None,
         bn.num_batches_tracked if track else None,
         training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, _ACTS[act])
+
+
+def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
+    """bn(conv(x)) with the conv bias folded into the BN kernel."""
+    y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
+                                   conv.dilation, conv.groups)
+    return batch_norm_act(y, bn, bn.act, residual, conv.bias)
+
+
+def run_sequential(seq: nn.Sequential, x):
+    """Run a Sequential, folding every Conv2d(bias) -> BatchNorm2d pair (see conv_bn)."""
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if (isinstance(m, nn.Conv2d) and m.bias is not None and i + 1 < len(mods)
+                and isinstance(mods[i + 1], BatchNorm2d) and m.padding_mode == "zeros"):
+            x = conv_bn(m, mods[i + 1], x)
+            i += 2
+        else:
+            x = m(x)
+            i += 1
+    return x
 
 
 class BatchNorm2d(nn.BatchNorm2d):
@@ -92,8 +122,8 @@ class BatchNorm2d(nn.BatchNorm2d):
             raise ValueError(f"act must be one of {sorted(_ACTS)}")
         self.act = act
 
-    def forward(self, x, residual=None):
-        return batch_norm_act(x, self, self.act, residual)
+    def forward(self, x, residual=None, prebias=None):
+        return batch_norm_act(x, self, self.act, residual, prebias)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={self.act}"

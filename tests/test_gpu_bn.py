@@ -115,3 +115,36 @@ def test_batchnorm_large_offset_variance():
     ref = torch.nn.BatchNorm2d(4).double().train()
     yr = ref(x.double())
     close_scaled(y, yr, 1e-4, "y")
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_conv_bias_folded_into_bn(train):
+    """conv_bn: conv without bias + BN(prebias) == conv(bias) -> BN, incl. d/d bias."""
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, conv_bn
+    torch.manual_seed(0)
+    conv = torch.nn.Conv2d(8, 12, 3, padding=1)
+    bn = BatchNorm2d(12, act="relu")
+    with torch.no_grad():
+        conv.bias.copy_(torch.linspace(-1, 1, 12))
+        bn.running_mean.copy_(torch.linspace(-0.2, 0.3, 12))
+        bn.running_var.copy_(torch.linspace(0.5, 1.5, 12))
+    ref_conv = torch.nn.Conv2d(8, 12, 3, padding=1).double()
+    ref_bn = torch.nn.BatchNorm2d(12).double()
+    ref_conv.load_state_dict({k: v.double() for k, v in conv.state_dict().items()})
+    ref_bn.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in bn.state_dict().items()})
+    conv, bn = conv.to(DEV), bn.to(DEV)
+    bn.train(train)
+    ref_bn.train(train)
+    x = torch.from_numpy(seeded((4, 8, 20, 24), 31, -1, 1))
+    gy = torch.from_numpy(seeded((4, 12, 20, 24), 32, -1, 1))
+    y = conv_bn(conv, bn, x.to(DEV))
+    y.backward(gy.to(DEV))
+    yr = torch.relu(ref_bn(ref_conv(x.double())))
+    yr.backward(gy.double())
+    close_scaled(y, yr, 1e-5, "y")
+    close_scaled(bn.running_mean, ref_bn.running_mean, 1e-5, "running_mean")
+    close_scaled(conv.weight.grad, ref_conv.weight.grad, 1e-4, "dW")
+    if train:  # true gradient is 0: both sides are rounding noise
+        assert float(conv.bias.grad.abs().max()) < 1e-4 * float(conv.weight.grad.abs().max())
+    else:
+        close_scaled(conv.bias.grad, ref_conv.bias.grad, 1e-4, "dbias")

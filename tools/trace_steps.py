@@ -16,8 +16,8 @@ import re
 
 MARK = "minmax_partial_kernel"
 
-OURS = re.compile(r"(bilinear|nearest|se_partial|se_fc|se_scale|se_bwd|se_wgrad|se_apply|skip_|minmax|"
-                  r"depthnorm|ssim3|loss_final|dloss)")
+OURS = re.compile(r"^(bilinear|nearest|se_partial|se_fc|se_scale|se_bwd|se_wgrad|se_apply|skip_|minmax|"
+                  r"depthnorm|ssim3|loss_final|dloss|bn_)")
 
 
 def short(name: str) -> str:
@@ -26,6 +26,9 @@ def short(name: str) -> str:
     base = m.group(1) if m else name[:60]
     if base.startswith("Cijk_"):
         return "rocBLAS/Tensile " + base[:48]
+    if base == "at":
+        m2 = re.search(r"at::native::(?:\(anonymous namespace\)::)?(\w+)<.*?(?:at::native::(?:\(anonymous namespace\)::)?(\w+))?", name)
+        return "aten " + (m2.group(1) + ("/" + m2.group(2) if m2.group(2) else "") if m2 else name[:70])
     if base.startswith("_ZN2ck") or "ck::" in name:
         return "CK " + re.sub(r"^.*?(kernel_\w+).*$", r"\1", name)[:60]
     return base[:80]

@@ -480,7 +480,7 @@ int launch_fwd_apply(const float* x, const float* r, float* y, int64_t n,
     MDE_LAUNCH(mde::K_BN_APPLY, bytes, s, bn_apply_plane_kernel,
                plane_grid(n * c, hw), dim3(256), 0, x, r, y, c, hw, act, A);
   } else {
-    MDE_LAUNCH(mde::K_BN_APPLY, bytes, s, bn_apply_table_kernel,
+    MDE_LAUNCH(mde::K_BN_APPLY_SMALL, bytes, s, bn_apply_table_kernel,
                dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 2 * c, x,
                r, y, n * c, c, hw, act, A);
   }
@@ -575,7 +575,7 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                plane_grid(n * c, hw), dim3(256), 0, (const float*)gy,
                (const float*)x, rr, (float*)gx, (float*)gresidual, c, hw, act, P);
   } else {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_table_kernel,
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, bn_bwd_apply_table_kernel,
                dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c,
                (const float*)gy, (const float*)x, rr, (float*)gx,
                (float*)gresidual, n * c, c, hw, act, P);

@@ -38,6 +38,8 @@ enum Kid : int {
   K_BN_BWD_REDUCE,
   K_BN_BWD_FINAL,
   K_BN_BWD_APPLY,
+  K_BN_APPLY_SMALL,
+  K_BN_BWD_APPLY_SMALL,
   K_COUNT
 };
 

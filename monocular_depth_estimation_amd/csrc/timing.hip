@@ -15,7 +15,8 @@ const char* const kNames[mde::K_COUNT] = {
     "skip_reduce_bwd_reduce", "minmax", "minmax_final", "depthnorm_apply",
     "ssim3_l1",      "loss_final",      "depth_loss_fwd", "depth_loss_bwd_coef",
     "depth_loss_bwd", "bn_fwd_stats",  "bn_fwd_final",  "bn_fwd_apply",
-    "bn_bwd_reduce",  "bn_bwd_final",  "bn_bwd_apply"};
+    "bn_bwd_reduce",  "bn_bwd_final",  "bn_bwd_apply",  "bn_fwd_apply_small",
+    "bn_bwd_apply_small"};
 
 struct Pending {
   int kid;

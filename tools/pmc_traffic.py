@@ -39,11 +39,12 @@ NAMES = [
     (r"ssim3_l1_kernel", "ssim3_l1"),
     (r"loss_final_kernel", "loss_final"),
     (r"bn_stats_kernel", "bn_fwd_stats"),
-    (r"bn_fwd_final_kernel", "bn_fwd_final"),
-    (r"bn_apply_kernel", "bn_fwd_apply"),
+    (r"bn_apply_plane_kernel", "bn_fwd_apply"),
+    (r"bn_apply_table_kernel", "bn_fwd_apply_small"),
     (r"bn_bwd_reduce_kernel", "bn_bwd_reduce"),
-    (r"bn_bwd_final_kernel", "bn_bwd_final"),
-    (r"bn_bwd_apply_kernel", "bn_bwd_apply"),
+    (r"bn_bwd_apply_plane_kernel", "bn_bwd_apply"),
+    (r"bn_bwd_apply_table_kernel", "bn_bwd_apply_small"),
+    (r"skip_bwd_reg_kernel", "skip_reduce_bwd"),
 ]
 
 

@@ -1,0 +1,84 @@
+"""Data-parallel path on CPU: world size 2 over gloo.
+
+Each rank runs the product training loop's host logic (init_world, wrap_ddp,
+Trainer, per-rank synthetic shards) around the CPU oracle model (the HIP
+modules need a GPU; the DDP plumbing is what is under test).  After one step
+the DDP-averaged gradients on every rank must equal the mean of the per-shard
+gradients computed in a single process, with per-shard DepthNorm and per-shard
+BN batch statistics (no SyncBN, as the reference).
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+H, W, BS = 64, 96, 2  # DDRNet's bottom maps must not degenerate to 1x1 (BN over 2 values)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    from monocular_depth_estimation_amd.train import Trainer, init_world, synthetic_batch, wrap_ddp
+    from oracle import guidedepth as og
+    from oracle import ops
+    from oracle.weights import fill_
+
+    world_ = init_world(backend="gloo")
+    assert world_.size == world and world_.rank == rank
+    model = fill_(og.GuideDepth())
+    ddp = wrap_ddp(model, world_, bucket_cap_mb=1.0)
+    opt = torch.optim.Adam(model.parameters(), 0.0)
+    trainer = Trainer(ddp, opt, ops.train_loss, world_, eval_quirk=False)
+    trainer.begin_epoch()
+    image, depth = synthetic_batch(BS, H, W, rank, step=0, device="cpu")
+    loss = trainer.step(image, depth)
+    grads = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+    torch.save({"grads": grads, "loss": loss.detach()}, os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_ddp_gradients_are_the_mean_of_per_shard_gradients():
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+
+    from monocular_depth_estimation_amd.train import synthetic_batch
+    from oracle import guidedepth as og
+    from oracle import ops
+    from oracle.weights import fill_
+    torch.set_num_threads(1)  # same reduction order as the single-threaded ranks
+    per_shard = []
+    for r in range(world):
+        m = fill_(og.GuideDepth()).train()
+        image, depth = synthetic_batch(BS, H, W, r, step=0, device="cpu")
+        loss = ops.train_loss(m(image), depth)
+        loss.backward()
+        per_shard.append({n: p.grad for n, p in m.named_parameters()})
+        assert abs(float(loss.detach()) - float(res[r]["loss"])) <= 1e-5 * abs(float(loss.detach()))
+    names = list(res[0]["grads"])
+    assert len(names) > 200
+    worst = 0.0
+    gmax = max(float(((per_shard[0][n] + per_shard[1][n]) / 2).abs().max()) for n in names)
+    for n in names:
+        mean = (per_shard[0][n] + per_shard[1][n]) / 2
+        # parameters whose true gradient is 0 (conv biases feeding train-mode BN)
+        # carry rounding noise only: floor their scale at 1e-6 of the largest
+        scale = max(float(mean.abs().max()), 1e-6 * gmax)
+        for r in range(world):
+            worst = max(worst, float((res[r]["grads"][n] - mean).abs().max()) / scale)
+        assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n  # identical after all-reduce
+    assert worst < 1e-4, worst

@@ -39,6 +39,31 @@ def _import_reference():
         cv2 = types.ModuleType("cv2")
         cv2.INTER_CUBIC = 2
         sys.modules["cv2"] = cv2
+    # timm (absent) provides three helpers to newcrf_layers.py / SAM.py; every
+    # drop_path rate on the path is 0, so DropPath is never instantiated, and
+    # trunc_normal_ only initialises (fixtures overwrite all weights).
+    if "timm" not in sys.modules:
+        timm = types.ModuleType("timm")
+        models = types.ModuleType("timm.models")
+        layers = types.ModuleType("timm.models.layers")
+
+        class DropPath(torch.nn.Module):
+            def __init__(self, p=0.0):
+                super().__init__()
+
+            def forward(self, x):
+                return x
+
+        layers.DropPath = DropPath
+        layers.to_2tuple = lambda v: tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+        layers.trunc_normal_ = lambda t, std=1.0: torch.nn.init.trunc_normal_(t, std=std, a=-2.0, b=2.0)
+        timm.models, models.layers = models, layers
+        sys.modules.update({"timm": timm, "timm.models": models, "timm.models.layers": layers})
+    # torchvision (absent) is only touched by Encoder(), which is not captured
+    if "torchvision" not in sys.modules:
+        tv = types.ModuleType("torchvision")
+        tv.models = types.ModuleType("torchvision.models")
+        sys.modules.update({"torchvision": tv, "torchvision.models": tv.models})
     sys.path.insert(0, REF)
     os.chdir(REF)  # GuideDepth package imports are relative to src/
 
@@ -252,13 +277,56 @@ def capture_train_sequence(steps=5):
             "final_up3_reduce_weight": f32(model.up_3.reduce.weight)}
 
 
+NEWCRF_CASES = [
+    # tag, (input_dim, embed_dim, v_dim, heads), batch, (h, w)
+    ("crf0", (24, 128, 64, 4), 2, (10, 13)),
+    ("crf1", (40, 256, 128, 8), 2, (7, 9)),
+    ("crf2", (112, 512, 256, 16), 1, (8, 9)),
+    ("crf3", (160, 1024, 512, 32), 1, (5, 6)),
+    ("crf_same_v", (64, 64, 64, 2), 2, (14, 7)),  # multiples of 7, no proj_v
+]
+
+
+def capture_newcrf():
+    from newcrf_layers import NewCRF
+    out = {}
+    for tag, (ind, emb, vd, heads), b, (h, w) in NEWCRF_CASES:
+        m = fill_(NewCRF(input_dim=ind, embed_dim=emb, v_dim=vd, window_size=7, num_heads=heads))
+        x = torch.from_numpy(seeded((b, ind, h, w), 81, -1, 1)).requires_grad_(True)
+        v = torch.from_numpy(seeded((b, vd, h, w), 82, -1, 1)).requires_grad_(True)
+        y = m(x, v)
+        gy = torch.from_numpy(seeded(y.shape, 83, -1, 1))
+        y.backward(gy)
+        out.update({f"{tag}::x": f32(x), f"{tag}::v": f32(v), f"{tag}::gy": f32(gy),
+                    f"{tag}::y": f32(y), f"{tag}::gx": f32(x.grad), f"{tag}::gv": f32(v.grad)})
+        out[f"{tag}::keys"] = np.array(list(m.state_dict().keys()))
+        grad_summary(m, f"{tag}::", out, full_limit=1024)
+    # the full Decoder on the feature pyramid of a 64x96 image (feats 4, 7, 13, 16, 17)
+    from model_mobileV3_large_newCRFs import Decoder
+    dec = fill_(Decoder())
+    shapes = {4: (24, 16, 24), 7: (40, 8, 12), 13: (112, 4, 6), 16: (160, 2, 3), 17: (960, 2, 3)}
+    feats = [None] * 18
+    for i, (c, h, w) in shapes.items():
+        feats[i] = torch.from_numpy(seeded((2, c, h, w), 90 + i, -1, 1)).requires_grad_(True)
+    y = dec(feats)
+    gy = torch.from_numpy(seeded(y.shape, 99, -1, 1))
+    y.backward(gy)
+    out["dec::keys"] = np.array(list(dec.state_dict().keys()))
+    out["dec::y"], out["dec::gy"] = f32(y), f32(gy)
+    for i in shapes:
+        out[f"dec::feat{i}"] = f32(feats[i])
+        out[f"dec::gfeat{i}"] = f32(feats[i].grad)
+    grad_summary(dec, "dec::", out, full_limit=1024)
+    return out
+
+
 def main():
     _import_reference()
     torch.manual_seed(0)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     jobs = {"golden_resize.npz": capture_resize, "golden_blocks.npz": capture_blocks,
             "golden_losses.npz": capture_losses, "golden_guidedepth.npz": capture_guidedepth,
-            "golden_trainseq.npz": capture_train_sequence}
+            "golden_trainseq.npz": capture_train_sequence, "golden_newcrf.npz": capture_newcrf}
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():
         if only and fname not in only:

@@ -183,7 +183,7 @@ int mde_depth_loss_bwd(const void* pred, const void* gt, float alpha,
  * 229-265,294-298.
  *   z = x + prebias[c]                              (prebias nullable)
  *   y = act(gamma*(z - mean)/sqrt(var + eps) + beta + residual)
- *   act: 0 = identity, 1 = ReLU; residual nullable; gamma/beta/stats fp32 [c].
+ *   act: 0 = identity, 1 = ReLU, 2 = Hardswish; residual nullable; gamma/beta/stats fp32 [c].
  * Training: batch mean / biased variance of z over (n,h,w); running stats
  * (nullable together) updated with `momentum` and the unbiased variance;
  * *num_batches_tracked += 1 (nullable).  Eval: running statistics.
@@ -216,6 +216,34 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       float* gprebias, int64_t n, int64_t c, int64_t h,
                       int64_t w, int act, void* workspace, int dtype,
                       void* stream);
+
+/* ---------------------------------------------------------------------------
+ * NewCRF shifted-window attention (head dim 32, window <= 8), fp32 on MFMA.
+ * Replaces, per CRFBlock (src/newcrf_layers.py:195-257), the pad / roll /
+ * window_partition / WindowAttention core / window_reverse / roll / crop
+ * sequence (:212-251, :30-59, :110-146) — everything between the qk Linear
+ * and the proj Linear:
+ *   qk      [b, h*w, 2c]  qk Linear output of the REAL tokens (q | k halves)
+ *   qk_bias [2c]          that Linear's bias = q, k of zero-padded tokens
+ *   v       [b, h, w, c]  value tokens (not projected; split into c/32 heads)
+ *   table   [(2*window-1)^2, heads] relative position bias table
+ *   out     [b, h*w, c]   attention output in token order (before proj)
+ * shift = 0 (W-MSA) or window/2 (SW-MSA, with the -100 region mask).
+ * ------------------------------------------------------------------------- */
+size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
+                                 int64_t heads, int64_t window);
+int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
+                        const float* table, void* out, int64_t b, int64_t h,
+                        int64_t w, int64_t c, int64_t heads, int64_t window,
+                        int64_t shift, int dtype, void* stream);
+/* gqk [b,h*w,2c] and gv [b,h,w,c] are fully overwritten; gtable and gqk_bias
+ * (the contribution of the padded tokens only: q half 0, k half = sum of the
+ * padded keys' gradients) are overwritten. */
+int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
+                        const void* v, const float* table, void* gqk, void* gv,
+                        float* gtable, float* gqk_bias, int64_t b, int64_t h,
+                        int64_t w, int64_t c, int64_t heads, int64_t window,
+                        int64_t shift, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).

@@ -59,6 +59,11 @@ SIGNATURES = {
                                       _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_batchnorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _int, _vp, _int, _vp]),
+    "mde_window_attn_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64]),
+    "mde_window_attn_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
+                                   _i64, _int, _vp]),
+    "mde_window_attn_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
+                                   _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_timing_enable": (_int, [_int]),
     "mde_timing_reset": (_int, []),
     "mde_timing_collect": (_int, []),

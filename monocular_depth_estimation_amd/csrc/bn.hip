@@ -60,8 +60,11 @@ Geo geometry(int64_t n, int64_t c, int64_t hw) {
 // coefficients in LDS, grid-stride) for small ones.
 bool plane_mode(int64_t hw) { return hw % 4 == 0 && hw / 4 >= 256; }
 
+// act: 0 none, 1 relu, 2 hardswish (v * clamp(v + 3, 0, 6) / 6, ATen's order)
 __device__ __forceinline__ float act_fn(float v, int act) {
-  return act == 1 ? fmaxf(v, 0.f) : v;
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) / 6.f;
+  return v;
 }
 
 __device__ __forceinline__ double wave_sum_d(double v) {
@@ -263,12 +266,14 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// dy' = dy * [pre-activation > 0] for relu, recomputed exactly as the forward.
+// dy' = dy * act'(pre-activation), the pre-activation recomputed exactly as
+// the forward; hardswish' follows ATen (0 below -3, x/3 + 1/2 up to 3, 1 above).
 __device__ __forceinline__ float dy_eff(float g, float xv, float rv, float sc,
                                         float sh, int act) {
-  if (act != 1) return g;
+  if (act == 0) return g;
   const float pre = xv * sc + sh + rv;
-  return pre > 0.f ? g : 0.f;
+  if (act == 1) return pre > 0.f ? g : 0.f;
+  return pre < -3.f ? 0.f : (pre <= 3.f ? g * (pre / 3.f + 0.5f) : g);
 }
 
 // part[(c*slices+s)*2] = sum dy', sum dy' * (x - mean_x)
@@ -505,7 +510,7 @@ int mde_batchnorm_fwd_train(const void* x, const float* gamma, const float* beta
                             void* workspace, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace ||
-      (!running_mean != !running_var) || act < 0 || act > 1 || !args_ok(n, c, h, w))
+      (!running_mean != !running_var) || act < 0 || act > 2 || !args_ok(n, c, h, w))
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
@@ -527,7 +532,7 @@ int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
                            int64_t w, int act, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !running_mean || !running_var || !y ||
-      !save_mean || !save_invstd || act < 0 || act > 1 || !args_ok(n, c, h, w))
+      !save_mean || !save_invstd || act < 0 || act > 2 || !args_ok(n, c, h, w))
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
@@ -547,7 +552,7 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !x || !gamma || !beta || !mean || !invstd || !gx || !workspace ||
-      act < 0 || act > 1 || !args_ok(n, c, h, w) || (gresidual && !residual && act))
+      act < 0 || act > 2 || !args_ok(n, c, h, w) || (gresidual && !residual && act))
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;

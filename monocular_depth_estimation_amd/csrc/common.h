@@ -40,6 +40,8 @@ enum Kid : int {
   K_BN_BWD_APPLY,
   K_BN_APPLY_SMALL,
   K_BN_BWD_APPLY_SMALL,
+  K_WATTN_FWD,
+  K_WATTN_BWD,
   K_COUNT
 };
 

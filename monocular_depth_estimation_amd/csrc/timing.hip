@@ -16,7 +16,7 @@ const char* const kNames[mde::K_COUNT] = {
     "ssim3_l1",      "loss_final",      "depth_loss_fwd", "depth_loss_bwd_coef",
     "depth_loss_bwd", "bn_fwd_stats",  "bn_fwd_final",  "bn_fwd_apply",
     "bn_bwd_reduce",  "bn_bwd_final",  "bn_bwd_apply",  "bn_fwd_apply_small",
-    "bn_bwd_apply_small"};
+    "bn_bwd_apply_small", "window_attn_fwd", "window_attn_bwd"};
 
 struct Pending {
   int kid;

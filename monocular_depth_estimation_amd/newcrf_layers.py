@@ -1,0 +1,236 @@
+"""NewCRF layers on MI355X (drop-in for src/newcrf_layers.py).
+
+Same classes, constructor signatures and state_dict keys as the reference
+(Mlp, WindowAttention, CRFBlock, BasicCRFLayer, NewCRF, window_partition,
+window_reverse).  The window-attention core of every CRFBlock — pad, cyclic
+shift, partition, QK^T + relative-position bias + shift mask, softmax, AV,
+reverse, unshift, crop — is ONE HIP kernel on MFMA
+(functional.window_attention); tokens stay in [B, H*W, C] order throughout,
+so the reference's pad / roll / permute / contiguous copies disappear.
+LayerNorm, the qk / proj / MLP Linears (hipBLASLt) and GELU run on
+PyTorch-ROCm.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _abi
+from .functional import _gpu, _ws
+
+
+def to_2tuple(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+class Mlp(nn.Module):
+    """fc1 -> act -> dropout -> fc2 -> dropout (reference :9-27; dropout 0 on the path)."""
+
+    def __init__(self, in_features, hidden_features=None, out_features=None, act_layer=nn.GELU,
+                 drop=0.0):
+        super().__init__()
+        out_features = out_features or in_features
+        hidden_features = hidden_features or in_features
+        self.fc1 = nn.Linear(in_features, hidden_features)
+        self.act = act_layer()
+        self.fc2 = nn.Linear(hidden_features, out_features)
+        self.drop = nn.Dropout(drop)
+
+    def forward(self, x):
+        return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
+
+
+def window_partition(x, window_size):
+    """(B, H, W, C) -> (num_windows*B, ws, ws, C) (reference :30-42)."""
+    b, h, w, c = x.shape
+    x = x.view(b, h // window_size, window_size, w // window_size, window_size, c)
+    return x.permute(0, 1, 3, 2, 4, 5).reshape(-1, window_size, window_size, c)
+
+
+def window_reverse(windows, window_size, H, W):  # noqa: N803
+    """(num_windows*B, ws, ws, C) -> (B, H, W, C) (reference :45-59)."""
+    b = int(windows.shape[0] / (H * W / window_size / window_size))
+    x = windows.view(b, H // window_size, W // window_size, window_size, window_size, -1)
+    return x.permute(0, 1, 3, 2, 4, 5).reshape(b, H, W, -1)
+
+
+def _relative_position_index(wh, ww):
+    ys, xs = np.meshgrid(np.arange(wh), np.arange(ww), indexing="ij")
+    y, x = ys.reshape(-1), xs.reshape(-1)
+    idx = (y[:, None] - y[None, :] + wh - 1) * (2 * ww - 1) + (x[:, None] - x[None, :] + ww - 1)
+    return torch.from_numpy(idx.astype(np.int64))
+
+
+class _WindowAttn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qk, qk_bias, v, table, h, w, heads, window, shift):
+        qk = qk.contiguous()
+        v = v.contiguous()
+        b, _, c2 = qk.shape
+        c = c2 // 2
+        out = torch.empty((b, h * w, c), dtype=qk.dtype, device=qk.device)
+        _abi.call("mde_window_attn_fwd", _abi.ptr(qk), _abi.ptr(qk_bias), _abi.ptr(v),
+                  _abi.ptr(table), _abi.ptr(out), b, h, w, c, heads, window, shift,
+                  _abi.dtype_code(qk), _abi.stream_of(qk))
+        ctx.save_for_backward(qk, qk_bias, v, table)
+        ctx.meta = (h, w, heads, window, shift)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        qk, qk_bias, v, table = ctx.saved_tensors
+        h, w, heads, window, shift = ctx.meta
+        gout = gout.contiguous()
+        b, _, c2 = qk.shape
+        c = c2 // 2
+        gqk = torch.empty_like(qk)
+        gv = torch.empty_like(v)
+        gtable = torch.empty_like(table)
+        gbias = torch.empty_like(qk_bias)
+        ws = _ws(_abi.query("mde_window_attn_workspace", b, h, w, c, heads, window), qk)
+        _abi.call("mde_window_attn_bwd", _abi.ptr(gout), _abi.ptr(qk), _abi.ptr(qk_bias),
+                  _abi.ptr(v), _abi.ptr(table), _abi.ptr(gqk), _abi.ptr(gv), _abi.ptr(gtable),
+                  _abi.ptr(gbias), b, h, w, c, heads, window, shift, _abi.ptr(ws),
+                  _abi.dtype_code(gout), _abi.stream_of(gout))
+        return gqk, gbias, gv, gtable, None, None, None, None, None
+
+
+def window_attention(qk, qk_bias, v, table, h, w, heads, window, shift):
+    """Shifted-window attention core of CRFBlock on the HIP/MFMA kernel.
+
+    qk: [B, H*W, 2C] (qk Linear of the real tokens), qk_bias: [2C], v: [B, H, W, C],
+    table: [(2ws-1)^2, heads].  Returns [B, H*W, C] (before proj).
+    """
+    _gpu(qk, qk_bias, v, table)
+    return _WindowAttn.apply(qk, qk_bias, v, table, int(h), int(w), int(heads), int(window),
+                             int(shift))
+
+
+class WindowAttention(nn.Module):
+    """Relative-position-biased window attention with an un-projected v (reference :62-149)."""
+
+    def __init__(self, dim, window_size, num_heads, v_dim, qkv_bias=True, qk_scale=None,
+                 attn_drop=0.0, proj_drop=0.0):
+        super().__init__()
+        self.dim = dim
+        self.window_size = to_2tuple(window_size)
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        if qk_scale is not None and qk_scale != head_dim ** -0.5:
+            raise NotImplementedError("the HIP kernel uses the reference's head_dim ** -0.5 scale")
+        if not qkv_bias:
+            raise NotImplementedError("qkv_bias=False has no HIP kernel (padded tokens use the bias)")
+        self.scale = head_dim ** -0.5
+        wh, ww = self.window_size
+        self.relative_position_bias_table = nn.Parameter(
+            torch.zeros((2 * wh - 1) * (2 * ww - 1), num_heads))
+        self.register_buffer("relative_position_index", _relative_position_index(wh, ww))
+        self.qk = nn.Linear(dim, dim * 2, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(v_dim, v_dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        nn.init.trunc_normal_(self.relative_position_bias_table, std=0.02, a=-2.0, b=2.0)
+        self.softmax = nn.Softmax(dim=-1)
+
+    def forward_tokens(self, x_norm, v, h, w, shift):
+        """x_norm: [B, H*W, C] LayerNorm'd tokens, v: [B, H, W, C] -> proj(attention) [B, H*W, C]."""
+        qk = self.qk(x_norm)
+        o = window_attention(qk, self.qk.bias, v, self.relative_position_bias_table, h, w,
+                             self.num_heads, self.window_size[0], shift)
+        return self.proj_drop(self.proj(o))
+
+
+class CRFBlock(nn.Module):
+    """LN -> shifted-window attention (+ residual) -> LN -> MLP (+ residual) (reference :152-257)."""
+
+    def __init__(self, dim, num_heads, v_dim, window_size=7, shift_size=0, mlp_ratio=4.0,
+                 qkv_bias=True, qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0,
+                 act_layer=nn.GELU, norm_layer=nn.LayerNorm):
+        super().__init__()
+        self.dim, self.num_heads, self.v_dim = dim, num_heads, v_dim
+        self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
+        assert 0 <= self.shift_size < self.window_size, "shift_size must in 0-window_size"
+        if drop_path > 0.0:
+            raise NotImplementedError("stochastic depth (drop_path > 0) is not on the training path")
+        self.norm1 = norm_layer(dim)
+        self.attn = WindowAttention(dim, window_size=to_2tuple(window_size), num_heads=num_heads,
+                                    v_dim=v_dim, qkv_bias=qkv_bias, qk_scale=qk_scale,
+                                    attn_drop=attn_drop, proj_drop=drop)
+        self.drop_path = nn.Identity()
+        self.norm2 = norm_layer(v_dim)
+        self.mlp = Mlp(in_features=v_dim, hidden_features=int(v_dim * mlp_ratio), act_layer=act_layer,
+                       drop=drop)
+        self.H = None
+        self.W = None
+
+    def forward(self, x, v, mask_matrix=None):
+        """x: [B, H*W, C]; v: [B, H, W, C]; the shift mask is computed in-kernel."""
+        b, l, c = x.shape
+        h, w = self.H, self.W
+        assert l == h * w, "input feature has wrong size"
+        x = x + self.attn.forward_tokens(self.norm1(x), v, h, w, self.shift_size)
+        return x + self.mlp(self.norm2(x))
+
+
+class BasicCRFLayer(nn.Module):
+    """`depth` CRFBlocks alternating W-MSA / SW-MSA over the same v (reference :260-363)."""
+
+    def __init__(self, dim, depth, num_heads, v_dim, window_size=7, mlp_ratio=4.0, qkv_bias=True,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm,
+                 downsample=None, use_checkpoint=False):
+        super().__init__()
+        self.window_size = window_size
+        self.shift_size = window_size // 2
+        self.depth = depth
+        self.use_checkpoint = use_checkpoint
+        self.blocks = nn.ModuleList([
+            CRFBlock(dim=dim, num_heads=num_heads, v_dim=v_dim, window_size=window_size,
+                     shift_size=0 if (i % 2 == 0) else window_size // 2, mlp_ratio=mlp_ratio,
+                     qkv_bias=qkv_bias, qk_scale=qk_scale, drop=drop, attn_drop=attn_drop,
+                     drop_path=drop_path[i] if isinstance(drop_path, list) else drop_path,
+                     norm_layer=norm_layer)
+            for i in range(depth)])
+        self.downsample = downsample(dim=dim, norm_layer=norm_layer) if downsample is not None else None
+
+    def forward(self, x, v, H, W):  # noqa: N803
+        for blk in self.blocks:
+            blk.H, blk.W = H, W
+            x = blk(x, v)
+        if self.downsample is not None:
+            return x, H, W, self.downsample(x, H, W), (H + 1) // 2, (W + 1) // 2
+        return x, H, W, x, H, W
+
+
+class NewCRF(nn.Module):
+    """Neural window FC-CRF stage (reference :367-434)."""
+
+    def __init__(self, input_dim=96, embed_dim=96, v_dim=64, window_size=7, num_heads=4, depth=2,
+                 patch_size=4, in_chans=3, norm_layer=nn.LayerNorm, patch_norm=True):
+        super().__init__()
+        self.embed_dim = embed_dim
+        self.patch_norm = patch_norm
+        self.proj_x = nn.Conv2d(input_dim, embed_dim, 3, padding=1) if input_dim != embed_dim else None
+        if v_dim != embed_dim:
+            self.proj_v = nn.Conv2d(v_dim, embed_dim, 3, padding=1)
+        elif embed_dim % v_dim == 0:
+            self.proj_v = None
+        v_dim = embed_dim
+        self.crf_layer = BasicCRFLayer(dim=embed_dim, depth=depth, num_heads=num_heads, v_dim=v_dim,
+                                       window_size=window_size, mlp_ratio=4.0, qkv_bias=True,
+                                       qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0,
+                                       norm_layer=norm_layer, downsample=None, use_checkpoint=False)
+        self.add_module("norm_crf", norm_layer(embed_dim))
+
+    def forward(self, x, v):
+        if self.proj_x is not None:
+            x = self.proj_x(x)
+        if self.proj_v is not None:
+            v = self.proj_v(v)
+        b, c, h, w = x.shape
+        tokens = x.flatten(2).transpose(1, 2)
+        v_nhwc = v.permute(0, 2, 3, 1).contiguous()
+        x_out, h, w, _, _, _ = self.crf_layer(tokens, v_nhwc, h, w)
+        x_out = self.norm_crf(x_out)
+        return x_out.view(-1, h, w, self.embed_dim).permute(0, 3, 1, 2).contiguous()

@@ -15,7 +15,7 @@ from torch import nn
 from . import _abi
 from .functional import _gpu, _ws
 
-_ACTS = {"none": 0, "relu": 1}
+_ACTS = {"none": 0, "relu": 1, "hardswish": 2}
 
 
 class _BatchNormAct(torch.autograd.Function):
@@ -127,3 +127,20 @@ class BatchNorm2d(nn.BatchNorm2d):
 
     def extra_repr(self):
         return super().extra_repr() + f", act={self.act}"
+
+
+def depthwise_conv_bn_act(x, conv: nn.Conv2d, bn: "BatchNorm2d", act: str = "none"):
+    """act(bn(depthwise_conv(x))) — MobileNetV3's k3/k5 depthwise stage."""
+    y = torch.nn.functional.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding,
+                                   conv.dilation, conv.groups)
+    return batch_norm_act(y, bn, act)
+
+
+def se_hardsigmoid(x, fc1: nn.Conv2d, fc2: nn.Conv2d):
+    """x * hardsigmoid(fc2(relu(fc1(avgpool(x))))) (torchvision.ops.SqueezeExcitation)."""
+    _gpu(x)
+    n, c = x.shape[:2]
+    s = x.mean((2, 3))
+    s = torch.relu(torch.nn.functional.linear(s, fc1.weight.view(fc1.out_channels, c), fc1.bias))
+    s = torch.nn.functional.linear(s, fc2.weight.view(c, fc1.out_channels), fc2.bias)
+    return x * torch.nn.functional.hardsigmoid(s).view(n, c, 1, 1)

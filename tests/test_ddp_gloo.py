@@ -60,15 +60,21 @@ def test_ddp_gradients_are_the_mean_of_per_shard_gradients():
     from oracle import guidedepth as og
     from oracle import ops
     from oracle.weights import fill_
+    threads = torch.get_num_threads()
     torch.set_num_threads(1)  # same reduction order as the single-threaded ranks
-    per_shard = []
+    per_shard, losses = [], []
+    try:
+        for r in range(world):
+            m = fill_(og.GuideDepth()).train()
+            image, depth = synthetic_batch(BS, H, W, r, step=0, device="cpu")
+            loss = ops.train_loss(m(image), depth)
+            loss.backward()
+            per_shard.append({n: p.grad for n, p in m.named_parameters()})
+            losses.append(float(loss.detach()))
+    finally:
+        torch.set_num_threads(threads)
     for r in range(world):
-        m = fill_(og.GuideDepth()).train()
-        image, depth = synthetic_batch(BS, H, W, r, step=0, device="cpu")
-        loss = ops.train_loss(m(image), depth)
-        loss.backward()
-        per_shard.append({n: p.grad for n, p in m.named_parameters()})
-        assert abs(float(loss.detach()) - float(res[r]["loss"])) <= 1e-5 * abs(float(loss.detach()))
+        assert abs(losses[r] - float(res[r]["loss"])) <= 1e-5 * abs(losses[r])
     names = list(res[0]["grads"])
     assert len(names) > 200
     worst = 0.0

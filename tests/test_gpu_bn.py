@@ -24,6 +24,8 @@ def ref_bn(x, bn_cpu, act, residual):
     y = bn_cpu(x)
     if residual is not None:
         y = y + residual
+    if act == "hardswish":
+        return torch.nn.functional.hardswish(y)
     return torch.relu(y) if act == "relu" else y
 
 
@@ -37,7 +39,8 @@ def close_scaled(a, b, tol, what):
 
 @pytest.mark.parametrize("shape", [(4, 16, 30, 40), (2, 8, 3, 5), (32, 64, 2, 3), (3, 7, 1, 1),
                                    (8, 16, 120, 160), (32, 16, 96, 128)])
-@pytest.mark.parametrize("act,res", [("none", False), ("relu", False), ("relu", True), ("none", True)])
+@pytest.mark.parametrize("act,res", [("none", False), ("relu", False), ("relu", True), ("none", True),
+                                     ("hardswish", False), ("hardswish", True)])
 def test_batchnorm_train_matches_aten(shape, act, res):
     from monocular_depth_estimation_amd.nn import BatchNorm2d
     n, c, h, w = shape
@@ -72,7 +75,7 @@ def test_batchnorm_train_matches_aten(shape, act, res):
         close_scaled(rg.grad, rr.grad, 1e-6, "dresidual")
 
 
-@pytest.mark.parametrize("act,res", [("relu", False), ("none", True)])
+@pytest.mark.parametrize("act,res", [("relu", False), ("none", True), ("hardswish", False)])
 def test_batchnorm_eval_matches_aten(act, res):
     from monocular_depth_estimation_amd.nn import BatchNorm2d
     shape = (4, 16, 30, 40)

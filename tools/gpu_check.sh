@@ -3,7 +3,9 @@
 # limit; a fault/abort/timeout stops the script (no retries).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+mkdir -p gpurun_out .miopen/cache .miopen/db
+# hand MIOpen's compiled kernels back (copy into .miopen/ locally) so later boxes skip the compile
+trap 'rm -rf gpurun_out/miopen_sync && cp -r .miopen gpurun_out/miopen_sync' EXIT
 STEPS=${STEPS:-10}
 WARMUP=${WARMUP:-3}
 run() {  # name seconds cmd...
@@ -23,5 +25,5 @@ fi
 if [ "${KBENCH:-1}" = 1 ]; then
   run kbench 600 python tools/kbench.py --json gpurun_out/kbench.json || exit $?
 fi
-run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
-run bench 900 python bench.py --steps "$STEPS" --warmup "$WARMUP" ${BENCH_ARGS:-} || exit $?
+[ "${SKIP_SMOKE:-0}" = 1 ] || run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+[ "${SKIP_BENCH:-0}" = 1 ] || run bench 900 python bench.py --steps "$STEPS" --warmup "$WARMUP" ${BENCH_ARGS:-} || exit $?

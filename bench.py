@@ -36,7 +36,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--bs", type=int, default=32)
+    p.add_argument("--workload", choices=("guidedepth", "newcrf"), default="guidedepth",
+                   help="guidedepth = BASELINE cfg2 (the headline line); newcrf = cfg4, "
+                        "PTModel (MobileNetV3-L + NewCRF decoder), the swap-in at train.py:36")
+    p.add_argument("--bs", type=int, default=None, help="per-GPU batch (32 cfg2, 16 cfg4)")
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -44,16 +47,20 @@ def parse():
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--cudnn-benchmark", type=int, default=0)
     p.add_argument("--no-kernel-timing", action="store_true")
-    return p.parse_args()
+    args = p.parse_args()
+    if args.bs is None:
+        args.bs = 32 if args.workload == "guidedepth" else 16
+    return args
 
 
 def cpu_baseline(args):
     """The oracle (CPU restatement, same ATen CPU convs/BN as the reference) timed on host cores."""
     from oracle import guidedepth as og
+    from oracle import mobilenetv3 as om
     from oracle import ops as oops
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    model = og.GuideDepth().train()
+    model = (og.GuideDepth() if args.workload == "guidedepth" else om.PTModel()).train()
     opt = torch.optim.Adam(model.parameters(), 1e-4)
     g = torch.Generator().manual_seed(0)
     img = torch.rand((args.cpu_bs, 3, args.height, args.width), generator=g)
@@ -72,7 +79,7 @@ def cpu_baseline(args):
     dt = time.perf_counter() - t0
     return {"value": round(args.cpu_bs * args.cpu_steps / dt, 3), "unit": "images/s",
             "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle GuideDepth train step, {args.height}x{args.width} bs={args.cpu_bs}, "
+            "sample": f"oracle {'GuideDepth' if args.workload == 'guidedepth' else 'PTModel'} train step, {args.height}x{args.width} bs={args.cpu_bs}, "
                       f"{args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s), fp32"}
 
 
@@ -87,7 +94,11 @@ def main():
     from monocular_depth_estimation_amd.loss import SSIML1
 
     torch.manual_seed(0)
-    model = GuideDepth(pretrained=False).to(world.device)
+    if args.workload == "guidedepth":
+        model = GuideDepth(pretrained=False).to(world.device)
+    else:
+        from monocular_depth_estimation_amd.model_mobileV3_large_newCRFs import PTModel
+        model = PTModel().to(world.device)
     opt = make_adam(model, 1e-4)
     ddp = wrap_ddp(model, world)
     trainer = Trainer(ddp, opt, SSIML1(1.0, 0.1, depth_norm=True), world, eval_quirk=False)
@@ -148,15 +159,22 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "bytes_per_launch": nbytes / launches,
                     "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
+    if args.workload == "guidedepth":
+        metric = "training images/sec at 640x480 bs=32/GPU (GuideDepth, SSIM+0.1*L1, Adam)"
+        workload = ("GuideDepth (DDRNet-23-slim + 3 guided upsampling blocks) train step, "
+                    "BASELINE cfg2, BN in train mode")
+    else:
+        metric = "training images/sec at 640x480 bs=16/GPU (MobileNetV3-L + NewCRF, SSIM+0.1*L1, Adam)"
+        workload = ("PTModel (MobileNetV3-Large encoder + NewCRF decoder, window attention on "
+                    "MFMA) train step, BASELINE cfg4, BN in train mode")
     out = {
-        "metric": "training images/sec at 640x480 bs=32/GPU (GuideDepth, SSIM+0.1*L1, Adam)",
+        "metric": metric,
         "value": round(images / elapsed, 2), "unit": "images/s", "n_gpus": world.size,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
         "data": "synthetic (U[0,1) images, U[0.1,10) depths, resident in HBM), random-init weights",
-        "config": {"workload": "GuideDepth (DDRNet-23-slim + 3 guided upsampling blocks) train step, "
-                               "BASELINE cfg2, BN in train mode",
+        "config": {"workload": workload,
                    "global_batch": world.size * args.bs, "per_gpu_batch": args.bs,
                    "resolution": f"{args.width}x{args.height}", "parallelism": f"dp{world.size}"},
         "loss_last": round(loss, 6),

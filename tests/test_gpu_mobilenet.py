@@ -90,7 +90,7 @@ def test_ptmodel_step_vs_oracle():
     close_scaled(pred, pr, 1e-3, "depth map")
     loss = SSIML1()(pred, d.to(DEV))
     lr = oops.train_loss(pr, d.double())
-    assert abs(float(loss) - float(lr)) <= 1e-4 * abs(float(lr))
+    assert abs(float(loss.detach()) - float(lr.detach())) <= 1e-4 * abs(float(lr))
     loss.backward()
     lr.backward()
     _grad_norm_check(ours, ref, 1.5e-2, 5e-3)

@@ -5,7 +5,10 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out .miopen/cache .miopen/db
 # hand MIOpen's compiled kernels back (copy into .miopen/ locally) so later boxes skip the compile
-trap 'rm -rf gpurun_out/miopen_sync && cp -r .miopen gpurun_out/miopen_sync' EXIT
+# heartbeat: MIOpen's first-use kernel compiles can be silent for minutes (every step has its own timeout)
+( while sleep 60; do date +%T >> gpurun_out/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB; rm -rf gpurun_out/miopen_sync && cp -r .miopen gpurun_out/miopen_sync' EXIT
 STEPS=${STEPS:-10}
 WARMUP=${WARMUP:-3}
 run() {  # name seconds cmd...
@@ -19,7 +22,7 @@ run() {  # name seconds cmd...
 }
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  run pytest_gpu 1200 python -m pytest tests -m gpu -q -rf -k "${PYTEST_K:-}"; rc=$?
+  run pytest_gpu ${TEST_TIMEOUT:-1000} python -m pytest tests -m gpu -q -rf -k "${PYTEST_K:-}"; rc=$?
   ok_or_testfail $rc || exit $rc
 fi
 if [ "${KBENCH:-1}" = 1 ]; then

@@ -5,9 +5,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
-export MIOPEN_CUSTOM_CACHE_DIR=$ROOT/gpurun_out/miopen_cache
-export MIOPEN_USER_DB_PATH=$ROOT/gpurun_out/miopen_db
+export MIOPEN_CUSTOM_CACHE_DIR=$ROOT/.miopen/cache
+export MIOPEN_USER_DB_PATH=$ROOT/.miopen/db
 mkdir -p "$MIOPEN_CUSTOM_CACHE_DIR" "$MIOPEN_USER_DB_PATH"
+( while sleep 60; do date +%T >> gpurun_out/heartbeat.txt; done ) &
+HB=$!
+trap 'kill $HB; rm -rf gpurun_out/miopen_sync && cp -r .miopen gpurun_out/miopen_sync' EXIT
 STEPS=${STEPS:-5}
 WARMUP=${WARMUP:-3}
 TAG=${TAG:-r01}

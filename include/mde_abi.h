@@ -246,6 +246,52 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
                         int64_t shift, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Depthwise convolution (groups == channels, square k = 3 or 5, stride 1 or
+ * 2, zero padding `pad`, dilation 1, no bias), NCHW.  Replaces the
+ * depthwise Conv2d of every MobileNetV3-Large inverted-residual block
+ * (torchvision mobilenet_v3_large().features[1..15], called at
+ * src/model_mobileV3_large_newCRFs.py:165,178-182).
+ *   x [n,c,h,w], weight [c,1,k,k] fp32, y [n,c,ho,wo],
+ *   ho = (h + 2 pad - k) / stride + 1 (same for wo).  n*c <= 65535.
+ * Backward: gx (nullable) and gweight (nullable, fp32 [c,k,k]) are
+ * overwritten; gweight needs x and a workspace of mde_dwconv_workspace bytes.
+ * ------------------------------------------------------------------------- */
+size_t mde_dwconv_workspace(int64_t n, int64_t c, int64_t h, int64_t w, int64_t k,
+                            int64_t stride, int64_t pad);
+int mde_dwconv_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t c,
+                   int64_t h, int64_t w, int64_t k, int64_t stride, int64_t pad, int dtype,
+                   void* stream);
+int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx,
+                   float* gweight, int64_t n, int64_t c, int64_t h, int64_t w, int64_t k,
+                   int64_t stride, int64_t pad, void* workspace, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
+ * LayerNorm over the last axis of a token-major [rows, c] tensor (c in
+ * {128, 256, 512, 1024}; other multiples of 64 return MDE_ERR_UNSUPPORTED),
+ * nn.LayerNorm semantics (biased variance, eps inside the sqrt).  Replaces
+ * norm1 / norm2 of every CRFBlock and NewCRF.norm_crf
+ * (src/newcrf_layers.py:197,212,233,419-434).
+ *   mean / rstd [rows] fp32 are written by the forward and read by the
+ *   backward; ggamma / gbeta [c] are overwritten; workspace of
+ *   mde_layernorm_workspace bytes.
+ * ------------------------------------------------------------------------- */
+size_t mde_layernorm_workspace(int64_t rows, int64_t c);
+int mde_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,
+                      float* mean, float* rstd, int64_t rows, int64_t c, float eps, int dtype,
+                      void* stream);
+int mde_layernorm_bwd(const void* gy, const void* x, const float* gamma, const float* mean,
+                      const float* rstd, void* gx, float* ggamma, float* gbeta, int64_t rows,
+                      int64_t c, void* workspace, int dtype, void* stream);
+
+/* Batched 2-D transpose y[b][j][i] = x[b][i][j] of x [batch, m, n]: the
+ * NCHW <-> token-major conversions around the NewCRF layers
+ * (x.flatten(2).transpose(1, 2), v.permute(0, 2, 3, 1), and the
+ * permute(0, 3, 1, 2).contiguous() of src/newcrf_layers.py:425-434).
+ * batch <= 65535, ceil(m / 64) <= 65535. */
+int mde_transpose(const void* x, void* y, int64_t batch, int64_t m, int64_t n, int dtype,
+                  void* stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).
  * When enabled, every launch made through this ABI is bracketed by hipEvents
  * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY

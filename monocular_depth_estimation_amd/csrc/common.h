@@ -42,6 +42,14 @@ enum Kid : int {
   K_BN_BWD_APPLY_SMALL,
   K_WATTN_FWD,
   K_WATTN_BWD,
+  K_DW_FWD,
+  K_DW_BWD_DATA,
+  K_DW_BWD_WEIGHT,
+  K_DW_WREDUCE,
+  K_LN_FWD,
+  K_LN_BWD,
+  K_LN_WREDUCE,
+  K_TRANSPOSE,
   K_COUNT
 };
 

@@ -16,7 +16,9 @@ const char* const kNames[mde::K_COUNT] = {
     "ssim3_l1",      "loss_final",      "depth_loss_fwd", "depth_loss_bwd_coef",
     "depth_loss_bwd", "bn_fwd_stats",  "bn_fwd_final",  "bn_fwd_apply",
     "bn_bwd_reduce",  "bn_bwd_final",  "bn_bwd_apply",  "bn_fwd_apply_small",
-    "bn_bwd_apply_small", "window_attn_fwd", "window_attn_bwd"};
+    "bn_bwd_apply_small", "window_attn_fwd", "window_attn_bwd",
+    "dwconv_fwd",    "dwconv_bwd_data", "dwconv_bwd_weight", "dwconv_wreduce",
+    "layernorm_fwd", "layernorm_bwd",   "layernorm_wreduce", "transpose"};
 
 struct Pending {
   int kid;

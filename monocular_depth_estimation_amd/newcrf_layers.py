@@ -97,6 +97,79 @@ class _WindowAttn(torch.autograd.Function):
         return gqk, gbias, gv, gtable, None, None, None, None, None
 
 
+class _Transpose(torch.autograd.Function):
+    """[B, M, N] -> [B, N, M] on the HIP LDS-tiled transpose (its own adjoint)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        x = x.contiguous()
+        b, m, n = x.shape
+        y = torch.empty((b, n, m), dtype=x.dtype, device=x.device)
+        _abi.call("mde_transpose", _abi.ptr(x), _abi.ptr(y), b, m, n, _abi.dtype_code(x),
+                  _abi.stream_of(x))
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        return _Transpose.apply(gy)
+
+
+def nchw_to_tokens(x):
+    """[B, C, H, W] -> contiguous [B, H*W, C] (x.flatten(2).transpose(1, 2) materialised)."""
+    _gpu(x)
+    b, c, h, w = x.shape
+    return _Transpose.apply(x.reshape(b, c, h * w))
+
+
+def tokens_to_nchw(t, h, w):
+    """[B, H*W, C] -> contiguous [B, C, H, W] (view(-1, H, W, C).permute(0, 3, 1, 2).contiguous())."""
+    _gpu(t)
+    b, l, c = t.shape
+    return _Transpose.apply(t).view(b, c, h, w)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, eps):
+        x = x.contiguous()
+        c = x.shape[-1]
+        rows = x.numel() // c
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        _abi.call("mde_layernorm_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(bias), _abi.ptr(y),
+                  _abi.ptr(mean), _abi.ptr(rstd), rows, c, float(eps), _abi.dtype_code(x),
+                  _abi.stream_of(x))
+        ctx.save_for_backward(x, weight, mean, rstd)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight, mean, rstd = ctx.saved_tensors
+        gy = gy.contiguous()
+        c = x.shape[-1]
+        rows = x.numel() // c
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(weight)
+        gb = torch.empty_like(weight)
+        ws = _ws(_abi.query("mde_layernorm_workspace", rows, c), x)
+        _abi.call("mde_layernorm_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(weight), _abi.ptr(mean),
+                  _abi.ptr(rstd), _abi.ptr(gx), _abi.ptr(gw), _abi.ptr(gb), rows, c, _abi.ptr(ws),
+                  _abi.dtype_code(gy), _abi.stream_of(gy))
+        return gx, gw, gb, None
+
+
+class LayerNorm(nn.LayerNorm):
+    """nn.LayerNorm over the last axis on the HIP kernel (same parameters and keys)."""
+
+    def forward(self, x):
+        _gpu(x)
+        if (len(self.normalized_shape) != 1 or self.weight is None or self.bias is None
+                or x.shape[-1] != self.normalized_shape[0]):
+            raise NotImplementedError("the HIP LayerNorm covers affine LayerNorm(C) over the last axis")
+        return _LayerNorm.apply(x, self.weight, self.bias, self.eps)
+
+
 def window_attention(qk, qk_bias, v, table, h, w, heads, window, shift):
     """Shifted-window attention core of CRFBlock on the HIP/MFMA kernel.
 
@@ -147,7 +220,7 @@ class CRFBlock(nn.Module):
 
     def __init__(self, dim, num_heads, v_dim, window_size=7, shift_size=0, mlp_ratio=4.0,
                  qkv_bias=True, qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0,
-                 act_layer=nn.GELU, norm_layer=nn.LayerNorm):
+                 act_layer=nn.GELU, norm_layer=LayerNorm):
         super().__init__()
         self.dim, self.num_heads, self.v_dim = dim, num_heads, v_dim
         self.window_size, self.shift_size, self.mlp_ratio = window_size, shift_size, mlp_ratio
@@ -178,7 +251,7 @@ class BasicCRFLayer(nn.Module):
     """`depth` CRFBlocks alternating W-MSA / SW-MSA over the same v (reference :260-363)."""
 
     def __init__(self, dim, depth, num_heads, v_dim, window_size=7, mlp_ratio=4.0, qkv_bias=True,
-                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=nn.LayerNorm,
+                 qk_scale=None, drop=0.0, attn_drop=0.0, drop_path=0.0, norm_layer=LayerNorm,
                  downsample=None, use_checkpoint=False):
         super().__init__()
         self.window_size = window_size
@@ -207,7 +280,7 @@ class NewCRF(nn.Module):
     """Neural window FC-CRF stage (reference :367-434)."""
 
     def __init__(self, input_dim=96, embed_dim=96, v_dim=64, window_size=7, num_heads=4, depth=2,
-                 patch_size=4, in_chans=3, norm_layer=nn.LayerNorm, patch_norm=True):
+                 patch_size=4, in_chans=3, norm_layer=LayerNorm, patch_norm=True):
         super().__init__()
         self.embed_dim = embed_dim
         self.patch_norm = patch_norm
@@ -229,8 +302,7 @@ class NewCRF(nn.Module):
         if self.proj_v is not None:
             v = self.proj_v(v)
         b, c, h, w = x.shape
-        tokens = x.flatten(2).transpose(1, 2)
-        v_nhwc = v.permute(0, 2, 3, 1).contiguous()
+        tokens = nchw_to_tokens(x)
+        v_nhwc = nchw_to_tokens(v).view(b, h, w, -1)
         x_out, h, w, _, _, _ = self.crf_layer(tokens, v_nhwc, h, w)
-        x_out = self.norm_crf(x_out)
-        return x_out.view(-1, h, w, self.embed_dim).permute(0, 3, 1, 2).contiguous()
+        return tokens_to_nchw(self.norm_crf(x_out), h, w)

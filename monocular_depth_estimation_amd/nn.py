@@ -129,11 +129,55 @@ class BatchNorm2d(nn.BatchNorm2d):
         return super().extra_repr() + f", act={self.act}"
 
 
+class _DWConv(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, k, stride, pad):
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        ho, wo = (h + 2 * pad - k) // stride + 1, (w + 2 * pad - k) // stride + 1
+        y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device)
+        _abi.call("mde_dwconv_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, c, h, w, k,
+                  stride, pad, _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.save_for_backward(x, weight)
+        ctx.meta = (k, stride, pad)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        k, stride, pad = ctx.meta
+        gy = gy.contiguous()
+        n, c, h, w = x.shape
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gw = torch.empty_like(weight) if ctx.needs_input_grad[1] else None
+        ws = _ws(_abi.query("mde_dwconv_workspace", n, c, h, w, k, stride, pad), x) \
+            if gw is not None else None
+        if gx is not None or gw is not None:
+            _abi.call("mde_dwconv_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(weight), _abi.ptr(gx),
+                      _abi.ptr(gw), n, c, h, w, k, stride, pad, _abi.ptr(ws),
+                      _abi.dtype_code(gy), _abi.stream_of(gy))
+        return gx, gw, None, None, None
+
+
+def depthwise_conv2d(x, conv: nn.Conv2d):
+    """Depthwise nn.Conv2d (groups == in == out, square k3/k5, stride 1/2) on the HIP kernel."""
+    _gpu(x)
+    k = conv.kernel_size[0]
+    s = conv.stride[0]
+    p = conv.padding[0]
+    if (conv.kernel_size != (k, k) or k not in (3, 5) or conv.stride != (s, s) or s not in (1, 2)
+            or conv.padding != (p, p) or conv.dilation != (1, 1) or conv.padding_mode != "zeros"
+            or not (conv.groups == conv.in_channels == conv.out_channels)):
+        raise NotImplementedError(f"no HIP depthwise kernel for {conv}")
+    y = _DWConv.apply(x, conv.weight, k, s, p)
+    if conv.bias is not None:
+        y = y + conv.bias.view(1, -1, 1, 1)
+    return y
+
+
 def depthwise_conv_bn_act(x, conv: nn.Conv2d, bn: "BatchNorm2d", act: str = "none"):
-    """act(bn(depthwise_conv(x))) — MobileNetV3's k3/k5 depthwise stage."""
-    y = torch.nn.functional.conv2d(x, conv.weight, conv.bias, conv.stride, conv.padding,
-                                   conv.dilation, conv.groups)
-    return batch_norm_act(y, bn, act)
+    """act(bn(depthwise_conv(x))) — MobileNetV3's k3/k5 depthwise stage, both on HIP kernels."""
+    return batch_norm_act(depthwise_conv2d(x, conv), bn, act)
 
 
 def se_hardsigmoid(x, fc1: nn.Conv2d, fc2: nn.Conv2d):

@@ -102,6 +102,23 @@ int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
                const float* s, const float* hidden, const float* mean,
                void* gxa, void* gxb, float* gw1, float* gw2, int64_t n,
                int64_t h, int64_t w, void* workspace, int dtype, void* stream);
+/* Gated variant: torchvision SqueezeExcitation of the MobileNetV3-Large
+ * blocks (features[4-6, 11-15], src/model_mobileV3_large_newCRFs.py:165):
+ *   s = gate(W2 relu(W1 mean(x) + b1) + b2), gate 0 = sigmoid,
+ *   1 = hardsigmoid (clamp(z/6 + 1/2, 0, 1)).  b1 [cr], b2 [c] nullable;
+ * gb1 / gb2 (nullable) receive their gradients.  mde_se_fwd / mde_se_bwd
+ * are this with no biases and gate 0.  Same workspace. */
+int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
+                    const float* w1, const float* b1, const float* w2, const float* b2,
+                    int64_t cr, int gate, void* out, float* s, float* hidden, float* mean,
+                    int64_t n, int64_t h, int64_t w, void* workspace, int dtype,
+                    void* stream);
+int mde_se_gate_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
+                    int64_t cb, const float* w1, const float* w2, const float* b2,
+                    int64_t cr, int gate, const float* s, const float* hidden,
+                    const float* mean, void* gxa, void* gxb, float* gw1, float* gb1,
+                    float* gw2, float* gb2, int64_t n, int64_t h, int64_t w,
+                    void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Skip fusion: residual add + 1x1 conv with bias.
@@ -266,8 +283,8 @@ int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx,
                    int64_t stride, int64_t pad, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
- * LayerNorm over the last axis of a token-major [rows, c] tensor (c in
- * {128, 256, 512, 1024}; other multiples of 64 return MDE_ERR_UNSUPPORTED),
+ * LayerNorm over the last axis of a token-major [rows, c] tensor (c a
+ * multiple of 64, <= 1024; larger multiples return MDE_ERR_UNSUPPORTED),
  * nn.LayerNorm semantics (biased variance, eps inside the sqrt).  Replaces
  * norm1 / norm2 of every CRFBlock and NewCRF.norm_crf
  * (src/newcrf_layers.py:197,212,233,419-434).

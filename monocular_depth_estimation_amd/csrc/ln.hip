@@ -30,13 +30,17 @@ int64_t bwd_blocks(int64_t rows) {
 
 template <int VPL>
 struct RowIO {
-  // lane's VPL values: float4 chunks at 4*lane + 256*j (VPL >= 4) or float2 at 2*lane.
+  // lane's VPL values: float4 chunks at 4*lane + 256*j (VPL % 4 == 0), a float2
+  // at 2*lane (VPL == 2), else scalars at lane + 64*j.
   __device__ static void load(const float* p, float* v) {
     const int lane = threadIdx.x & 63;
     if constexpr (VPL == 2) {
       const float2 a = reinterpret_cast<const float2*>(p)[lane];
       v[0] = a.x;
       v[1] = a.y;
+    } else if constexpr (VPL % 4 != 0) {
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) v[j] = p[lane + 64 * j];
     } else {
 #pragma unroll
       for (int j = 0; j < VPL / 4; ++j) {
@@ -52,6 +56,9 @@ struct RowIO {
     const int lane = threadIdx.x & 63;
     if constexpr (VPL == 2) {
       reinterpret_cast<float2*>(p)[lane] = make_float2(v[0], v[1]);
+    } else if constexpr (VPL % 4 != 0) {
+#pragma unroll
+      for (int j = 0; j < VPL; ++j) p[lane + 64 * j] = v[j];
     } else {
 #pragma unroll
       for (int j = 0; j < VPL / 4; ++j)
@@ -63,6 +70,7 @@ struct RowIO {
   __device__ static int chan(int i) {
     const int lane = threadIdx.x & 63;
     if constexpr (VPL == 2) return 2 * lane + i;
+    if constexpr (VPL % 4 != 0) return lane + 64 * i;
     return 4 * (lane + 64 * (i / 4)) + (i & 3);
   }
 };
@@ -152,21 +160,26 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// ggamma[ch] / gbeta[ch] = sum over blocks of part: 64 columns per block,
-// wave w sums blocks w, w+4, ...; the 4 wave sums combine in a fixed order.
-__global__ void __launch_bounds__(256)
+// ggamma[ch] / gbeta[ch] = sum over blocks of part: 64 columns per block of
+// 16 waves, wave w sums blocks w, w+16, ... (8 loads in flight); the 16 wave
+// sums combine in a fixed order.
+__global__ void __launch_bounds__(1024)
     ln_wreduce_kernel(const float* __restrict__ part, float* __restrict__ ggamma,
                       float* __restrict__ gbeta, int64_t nblk, int c) {
-  __shared__ float red[4][64];
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;  // column of the [2][c] partial rows
   float s = 0.f;
-  if (i < 2 * c)
-    for (int64_t b = wid; b < nblk; b += 4) s += part[b * 2 * c + i];
+  if (i < 2 * c) {
+#pragma unroll 8
+    for (int64_t b = wid; b < nblk; b += 16) s += part[b * 2 * c + i];
+  }
   red[wid][lane] = s;
   __syncthreads();
   if (wid == 0 && i < 2 * c) {
-    const float t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) t += red[w][lane];
     if (i < c) ggamma[i] = t;
     else gbeta[i - c] = t;
   }
@@ -211,13 +224,12 @@ int ln_bwd_launch(const float* gy, const float* x, const float* g, const float* 
              g, mu, rs, gx, part, rows, cdiv(rows, nblk));
   const int c = 64 * VPL;
   MDE_LAUNCH(K_LN_WREDUCE, 8.0 * nblk * c, st, ln_wreduce_kernel, dim3((unsigned)cdiv(2 * c, 64)),
-             dim3(256), 0, part, gg, gb, nblk, c);
+             dim3(1024), 0, part, gg, gb, nblk, c);
   return 0;
 }
 
 bool ln_ok(int64_t rows, int64_t c) {
-  return rows > 0 && rows <= (int64_t)4 * 0x7fffffff && (c == 128 || c == 256 || c == 512 ||
-                                                         c == 1024);
+  return rows > 0 && rows <= (int64_t)4 * 0x7fffffff && c % 64 == 0 && c >= 64 && c <= 1024;
 }
 
 }  // namespace
@@ -237,15 +249,18 @@ int mde_layernorm_fwd(const void* x, const float* gamma, const float* beta, void
                       void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !y || !mean || !rstd) return MDE_ERR_INVALID_ARG;
-  if (!ln_ok(rows, c)) return c % 64 == 0 && rows > 0 ? MDE_ERR_UNSUPPORTED : MDE_ERR_INVALID_ARG;
+  if (!ln_ok(rows, c)) return rows > 0 && c > 1024 && c % 64 == 0 ? MDE_ERR_UNSUPPORTED : MDE_ERR_INVALID_ARG;
   hipStream_t st = (hipStream_t)stream;
   const float* xp = (const float*)x;
   float* yp = (float*)y;
-  switch (c) {
-    case 128: return ln_fwd_launch<2>(xp, gamma, beta, yp, mean, rstd, rows, eps, st);
-    case 256: return ln_fwd_launch<4>(xp, gamma, beta, yp, mean, rstd, rows, eps, st);
-    case 512: return ln_fwd_launch<8>(xp, gamma, beta, yp, mean, rstd, rows, eps, st);
-    default: return ln_fwd_launch<16>(xp, gamma, beta, yp, mean, rstd, rows, eps, st);
+  switch (c / 64) {
+#define MDE_LN_CASE(V) \
+  case V: return ln_fwd_launch<V>(xp, gamma, beta, yp, mean, rstd, rows, eps, st);
+    MDE_LN_CASE(1) MDE_LN_CASE(2) MDE_LN_CASE(3) MDE_LN_CASE(4) MDE_LN_CASE(5) MDE_LN_CASE(6)
+    MDE_LN_CASE(7) MDE_LN_CASE(8) MDE_LN_CASE(9) MDE_LN_CASE(10) MDE_LN_CASE(11)
+    MDE_LN_CASE(12) MDE_LN_CASE(13) MDE_LN_CASE(14) MDE_LN_CASE(15) MDE_LN_CASE(16)
+#undef MDE_LN_CASE
+    default: return MDE_ERR_INVALID_ARG;
   }
 }
 
@@ -255,17 +270,20 @@ int mde_layernorm_bwd(const void* gy, const void* x, const float* gamma, const f
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !x || !gamma || !mean || !rstd || !gx || !ggamma || !gbeta || !workspace)
     return MDE_ERR_INVALID_ARG;
-  if (!ln_ok(rows, c)) return c % 64 == 0 && rows > 0 ? MDE_ERR_UNSUPPORTED : MDE_ERR_INVALID_ARG;
+  if (!ln_ok(rows, c)) return rows > 0 && c > 1024 && c % 64 == 0 ? MDE_ERR_UNSUPPORTED : MDE_ERR_INVALID_ARG;
   hipStream_t st = (hipStream_t)stream;
   const float* g = (const float*)gy;
   const float* xp = (const float*)x;
   float* gxp = (float*)gx;
   float* part = (float*)workspace;
-  switch (c) {
-    case 128: return ln_bwd_launch<2>(g, xp, gamma, mean, rstd, gxp, ggamma, gbeta, part, rows, st);
-    case 256: return ln_bwd_launch<4>(g, xp, gamma, mean, rstd, gxp, ggamma, gbeta, part, rows, st);
-    case 512: return ln_bwd_launch<8>(g, xp, gamma, mean, rstd, gxp, ggamma, gbeta, part, rows, st);
-    default: return ln_bwd_launch<16>(g, xp, gamma, mean, rstd, gxp, ggamma, gbeta, part, rows, st);
+  switch (c / 64) {
+#define MDE_LN_CASE(V) \
+  case V: return ln_bwd_launch<V>(g, xp, gamma, mean, rstd, gxp, ggamma, gbeta, part, rows, st);
+    MDE_LN_CASE(1) MDE_LN_CASE(2) MDE_LN_CASE(3) MDE_LN_CASE(4) MDE_LN_CASE(5) MDE_LN_CASE(6)
+    MDE_LN_CASE(7) MDE_LN_CASE(8) MDE_LN_CASE(9) MDE_LN_CASE(10) MDE_LN_CASE(11)
+    MDE_LN_CASE(12) MDE_LN_CASE(13) MDE_LN_CASE(14) MDE_LN_CASE(15) MDE_LN_CASE(16)
+#undef MDE_LN_CASE
+    default: return MDE_ERR_INVALID_ARG;
   }
 }
 

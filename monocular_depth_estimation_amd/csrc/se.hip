@@ -9,6 +9,10 @@
 //            reduction) -> fc (one block per sample) -> scale (streaming).
 // Backward = dot (partial sums of g*x) -> fc backward (per sample) ->
 //            weight gradients (sum over samples in fixed order) -> apply.
+//
+// The gated variant (mde_se_gate_*) adds the fc biases and the hardsigmoid
+// gate of torchvision's SqueezeExcitation (MobileNetV3-Large blocks 4-6 and
+// 11-15: avgpool -> fc1 (+b1) -> ReLU -> fc2 (+b2) -> hardsigmoid -> scale).
 #include "common.h"
 
 namespace {
@@ -57,10 +61,17 @@ __global__ void __launch_bounds__(256)
 }
 
 // One block per sample: mean -> hidden = relu(W1 m) -> s = sigmoid(W2 h).
+__device__ __forceinline__ float gate_fn(float z, int gate) {
+  // 0: sigmoid; 1: hardsigmoid = clamp(z / 6 + 1/2, 0, 1) (ATen: x <= -3 -> 0, x >= 3 -> 1)
+  if (gate == 0) return 1.f / (1.f + expf(-z));
+  return z <= -3.f ? 0.f : (z >= 3.f ? 1.f : z / 6.f + 0.5f);
+}
+
 __global__ void __launch_bounds__(256)
     se_fc_kernel(const float* __restrict__ part, int chunks, int c, int cr,
                  float inv_hw, const float* __restrict__ w1,
-                 const float* __restrict__ w2, float* __restrict__ s,
+                 const float* __restrict__ w2, const float* __restrict__ b1,
+                 const float* __restrict__ b2, int gate, float* __restrict__ s,
                  float* __restrict__ hidden, float* __restrict__ mean) {
   extern __shared__ float sm[];
   float* m = sm;       // [c]
@@ -78,6 +89,7 @@ __global__ void __launch_bounds__(256)
     const float* wr = w1 + (int64_t)j * c;
     float acc = 0.f;
     for (int ch = 0; ch < c; ++ch) acc += wr[ch] * m[ch];
+    if (b1) acc += b1[j];
     acc = acc > 0.f ? acc : 0.f;
     hdn[j] = acc;
     hidden[(int64_t)nidx * cr + j] = acc;
@@ -87,7 +99,8 @@ __global__ void __launch_bounds__(256)
     const float* wr = w2 + (int64_t)ch * cr;
     float z = 0.f;
     for (int j = 0; j < cr; ++j) z += wr[j] * hdn[j];
-    s[(int64_t)nidx * c + ch] = 1.f / (1.f + expf(-z));
+    if (b2) z += b2[ch];
+    s[(int64_t)nidx * c + ch] = gate_fn(z, gate);
   }
 }
 
@@ -123,9 +136,11 @@ __global__ void __launch_bounds__(256)
 
 // Per-sample backward through sigmoid / W2 / relu / W1.
 //   ds = sum g*x;  dz = ds s (1-s);  dh = (h>0) W2^T dz;  dm = W1^T dh
+//   hardsigmoid: dz = ds / 6 where -3 < z < 3 (z recomputed from the hidden)
 __global__ void __launch_bounds__(256)
     se_bwd_fc_kernel(const float* __restrict__ part, int chunks, int c, int cr,
                      const float* __restrict__ w1, const float* __restrict__ w2,
+                     const float* __restrict__ b2, int gate,
                      const float* __restrict__ s,
                      const float* __restrict__ hidden, float* __restrict__ dz,
                      float* __restrict__ dh, float* __restrict__ dm) {
@@ -133,12 +148,25 @@ __global__ void __launch_bounds__(256)
   float* z = sm;        // [c]
   float* hh = sm + c;   // [cr]
   const int nidx = blockIdx.x;
+  if (gate == 1) {
+    for (int j = threadIdx.x; j < cr; j += blockDim.x) hh[j] = hidden[(int64_t)nidx * cr + j];
+    __syncthreads();
+  }
   for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
     const float* p = part + ((int64_t)nidx * c + ch) * chunks;
     float acc = 0.f;
     for (int k = 0; k < chunks; ++k) acc += p[k];
-    const float sv = s[(int64_t)nidx * c + ch];
-    const float v = acc * (sv * (1.f - sv));
+    float v;
+    if (gate == 0) {
+      const float sv = s[(int64_t)nidx * c + ch];
+      v = acc * (sv * (1.f - sv));
+    } else {
+      const float* wr = w2 + (int64_t)ch * cr;
+      float zz = 0.f;
+      for (int j = 0; j < cr; ++j) zz += wr[j] * hh[j];
+      if (b2) zz += b2[ch];
+      v = (zz > -3.f && zz < 3.f) ? acc / 6.f : 0.f;
+    }
     z[ch] = v;
     dz[(int64_t)nidx * c + ch] = v;
   }
@@ -158,15 +186,27 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// gw2[ch, j] = sum_n dz[n,ch] h[n,j];  gw1[j, ch] = sum_n dh[n,j] m[n,ch]
+// gw2[ch, j] = sum_n dz[n,ch] h[n,j];  gw1[j, ch] = sum_n dh[n,j] m[n,ch];
+// gb2[ch] = sum_n dz[n,ch];  gb1[j] = sum_n dh[n,j]  (bias gradients nullable)
 __global__ void __launch_bounds__(256)
     se_wgrad_kernel(int n, int c, int cr, const float* __restrict__ dz,
                     const float* __restrict__ dh,
                     const float* __restrict__ hidden,
                     const float* __restrict__ mean, float* __restrict__ gw1,
-                    float* __restrict__ gw2) {
+                    float* __restrict__ gw2, float* __restrict__ gb1,
+                    float* __restrict__ gb2) {
   const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t pairs = (int64_t)c * cr;
+  if (gb2 && t < c) {
+    float acc = 0.f;
+    for (int k = 0; k < n; ++k) acc += dz[(int64_t)k * c + t];
+    gb2[t] = acc;
+  }
+  if (gb1 && t < cr) {
+    float acc = 0.f;
+    for (int k = 0; k < n; ++k) acc += dh[(int64_t)k * cr + t];
+    gb1[t] = acc;
+  }
   if (t < pairs) {
     const int ch = (int)(t / cr), j = (int)(t % cr);
     float acc = 0.f;
@@ -260,12 +300,14 @@ size_t mde_se_workspace(int64_t n, int64_t c, int64_t cr, int64_t h,
          round16(sizeof(float) * n * c);
 }
 
-int mde_se_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
-               const float* w1, const float* w2, int64_t cr, void* out,
-               float* s, float* hidden, float* mean, int64_t n, int64_t h,
-               int64_t w, void* workspace, int dtype, void* stream) {
+int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
+                    const float* w1, const float* b1, const float* w2, const float* b2,
+                    int64_t cr, int gate, void* out, float* s, float* hidden, float* mean,
+                    int64_t n, int64_t h, int64_t w, void* workspace, int dtype,
+                    void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   const int64_t c = ca + cb, hw = h * w;
+  if (gate < 0 || gate > 1) return MDE_ERR_INVALID_ARG;
   if (!xa || ca <= 0 || cb < 0 || (cb > 0 && !xb) || !w1 || !w2 || cr <= 0 ||
       !out || !s || !hidden || !mean || n <= 0 || hw <= 0 || !workspace ||
       c > 4096 || cr > 4096 || n > 65535)
@@ -280,7 +322,7 @@ int mde_se_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (2.0 * c * cr + 3.0 * n * c), st,
              se_fc_kernel, dim3((unsigned)n), dim3(256),
              sizeof(float) * (c + cr), ws.part, chunks, (int)c, (int)cr,
-             1.f / (float)hw, w1, w2, s, hidden, mean);
+             1.f / (float)hw, w1, w2, b1, b2, gate, s, hidden, mean);
   MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel,
              dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
              (const float*)xa, ca, (const float*)xb, cb, hw, n * c, s,
@@ -288,13 +330,15 @@ int mde_se_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   return MDE_OK;
 }
 
-int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
-               int64_t cb, const float* w1, const float* w2, int64_t cr,
-               const float* s, const float* hidden, const float* mean,
-               void* gxa, void* gxb, float* gw1, float* gw2, int64_t n,
-               int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
+int mde_se_gate_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
+                    int64_t cb, const float* w1, const float* w2, const float* b2,
+                    int64_t cr, int gate, const float* s, const float* hidden,
+                    const float* mean, void* gxa, void* gxb, float* gw1, float* gb1,
+                    float* gw2, float* gb2, int64_t n, int64_t h, int64_t w,
+                    void* workspace, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   const int64_t c = ca + cb, hw = h * w;
+  if (gate < 0 || gate > 1) return MDE_ERR_INVALID_ARG;
   if (!gout || !xa || ca <= 0 || cb < 0 || (cb > 0 && !xb) || !w1 || !w2 ||
       cr <= 0 || !s || !hidden || !mean || !gw1 || !gw2 || n <= 0 ||
       hw <= 0 || !workspace || c > 4096 || cr > 4096 || n > 65535)
@@ -310,11 +354,11 @@ int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 4.0 * n * c), st,
              se_bwd_fc_kernel, dim3((unsigned)n), dim3(256),
              sizeof(float) * (c + cr), ws.part, chunks, (int)c, (int)cr, w1,
-             w2, s, hidden, ws.dz, ws.dh, ws.dm);
+             w2, b2, gate, s, hidden, ws.dz, ws.dh, ws.dm);
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 2.0 * n * (c + cr)), st,
              se_wgrad_kernel, dim3((unsigned)mde::cdiv(2 * c * cr, 256)),
              dim3(256), 0, (int)n, (int)c, (int)cr, ws.dz, ws.dh, hidden,
-             mean, gw1, gw2);
+             mean, gw1, gw2, gb1, gb2);
   if (gxa || gxb) {
     MDE_LAUNCH(mde::K_SE_BWD_APPLY, 2.0 * big, st, se_apply_kernel,
                dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
@@ -322,6 +366,23 @@ int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
                1.f / (float)hw, (float*)gxa, (float*)gxb);
   }
   return MDE_OK;
+}
+
+int mde_se_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
+               const float* w1, const float* w2, int64_t cr, void* out,
+               float* s, float* hidden, float* mean, int64_t n, int64_t h,
+               int64_t w, void* workspace, int dtype, void* stream) {
+  return mde_se_gate_fwd(xa, ca, xb, cb, w1, nullptr, w2, nullptr, cr, 0, out, s, hidden,
+                         mean, n, h, w, workspace, dtype, stream);
+}
+
+int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
+               int64_t cb, const float* w1, const float* w2, int64_t cr,
+               const float* s, const float* hidden, const float* mean,
+               void* gxa, void* gxb, float* gw1, float* gw2, int64_t n,
+               int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
+  return mde_se_gate_bwd(gout, xa, ca, xb, cb, w1, w2, nullptr, cr, 0, s, hidden, mean, gxa,
+                         gxb, gw1, nullptr, gw2, nullptr, n, h, w, workspace, dtype, stream);
 }
 
 }  // extern "C"

@@ -180,11 +180,52 @@ def depthwise_conv_bn_act(x, conv: nn.Conv2d, bn: "BatchNorm2d", act: str = "non
     return batch_norm_act(depthwise_conv2d(x, conv), bn, act)
 
 
+class _SEGate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2):
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        cr = w1.shape[0]
+        ctx.wshapes = (w1.shape, w2.shape)
+        w1 = w1.reshape(cr, c).contiguous()
+        w2 = w2.reshape(c, cr).contiguous()
+        out = torch.empty_like(x)
+        s = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        hidden = torch.empty((n, cr), dtype=torch.float32, device=x.device)
+        mean = torch.empty((n, c), dtype=torch.float32, device=x.device)
+        ws = _ws(_abi.query("mde_se_workspace", n, c, cr, h, w), x)
+        _abi.call("mde_se_gate_fwd", _abi.ptr(x), c, None, 0, _abi.ptr(w1), _abi.ptr(b1),
+                  _abi.ptr(w2), _abi.ptr(b2), cr, 1, _abi.ptr(out), _abi.ptr(s), _abi.ptr(hidden),
+                  _abi.ptr(mean), n, h, w, _abi.ptr(ws), _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.save_for_backward(x, w1, w2, b2, s, hidden, mean)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, w1, w2, b2, s, hidden, mean = ctx.saved_tensors
+        gout = gout.contiguous()
+        n, c, h, w = x.shape
+        cr = w1.shape[0]
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gw1, gw2 = torch.empty_like(w1), torch.empty_like(w2)
+        gb1 = torch.empty(cr, dtype=x.dtype, device=x.device)
+        gb2 = torch.empty(c, dtype=x.dtype, device=x.device)
+        ws = _ws(_abi.query("mde_se_workspace", n, c, cr, h, w), x)
+        _abi.call("mde_se_gate_bwd", _abi.ptr(gout), _abi.ptr(x), c, None, 0, _abi.ptr(w1),
+                  _abi.ptr(w2), _abi.ptr(b2), cr, 1, _abi.ptr(s), _abi.ptr(hidden),
+                  _abi.ptr(mean), _abi.ptr(gx), None, _abi.ptr(gw1), _abi.ptr(gb1), _abi.ptr(gw2),
+                  _abi.ptr(gb2), n, h, w, _abi.ptr(ws), _abi.dtype_code(gout),
+                  _abi.stream_of(gout))
+        return gx, gw1.view(ctx.wshapes[0]), gb1, gw2.view(ctx.wshapes[1]), gb2
+
+
 def se_hardsigmoid(x, fc1: nn.Conv2d, fc2: nn.Conv2d):
-    """x * hardsigmoid(fc2(relu(fc1(avgpool(x))))) (torchvision.ops.SqueezeExcitation)."""
+    """x * hardsigmoid(fc2(relu(fc1(avgpool(x))))) (torchvision.ops.SqueezeExcitation) on HIP.
+
+    fc1 / fc2 are the 1x1 convolutions with bias of the reference module; the
+    squeeze, both FCs, the gate and the rescale run in mde_se_gate_{fwd,bwd}.
+    """
     _gpu(x)
-    n, c = x.shape[:2]
-    s = x.mean((2, 3))
-    s = torch.relu(torch.nn.functional.linear(s, fc1.weight.view(fc1.out_channels, c), fc1.bias))
-    s = torch.nn.functional.linear(s, fc2.weight.view(c, fc1.out_channels), fc2.bias)
-    return x * torch.nn.functional.hardsigmoid(s).view(n, c, 1, 1)
+    if fc1.bias is None or fc2.bias is None:
+        raise NotImplementedError("torchvision SqueezeExcitation has fc biases")
+    return _SEGate.apply(x, fc1.weight, fc1.bias, fc2.weight, fc2.bias)

@@ -115,7 +115,8 @@ def test_decoder_golden(golden):
         close_scaled(feats[i].grad, g[f"dec::gfeat{i}"], 1e-3, f"gfeat{i}")
 
 
-@pytest.mark.parametrize("rows,c", [(307200, 128), (1000, 256), (37, 512), (4800, 1024), (1, 128)])
+@pytest.mark.parametrize("rows,c", [(307200, 128), (1000, 256), (37, 512), (4800, 1024), (1, 128),
+                                    (98, 64), (50, 192)])
 def test_layernorm_matches_aten(rows, c):
     from monocular_depth_estimation_amd.newcrf_layers import LayerNorm
     ln = LayerNorm(c)

@@ -67,41 +67,56 @@ __device__ __forceinline__ float gate_fn(float z, int gate) {
   return z <= -3.f ? 0.f : (z >= 3.f ? 1.f : z / 6.f + 0.5f);
 }
 
-__global__ void __launch_bounds__(256)
-    se_fc_kernel(const float* __restrict__ part, int chunks, int c, int cr,
-                 float inv_hw, const float* __restrict__ w1,
-                 const float* __restrict__ w2, const float* __restrict__ b1,
-                 const float* __restrict__ b2, int gate, float* __restrict__ s,
-                 float* __restrict__ hidden, float* __restrict__ mean) {
-  extern __shared__ float sm[];
-  float* m = sm;       // [c]
-  float* hdn = sm + c; // [cr]
+// The per-sample FCs are GEMVs; each runs as its own kernel over a grid of
+// (sample, 16 outputs) blocks of 16 waves, one wave per output, so the
+// weight rows stream with many loads in flight instead of one serial chain.
+constexpr int kOutPerBlock = 16;
+
+// hidden[n, j] = relu(W1[j] . mean[n] + b1[j]); block (n, 0) also writes mean.
+__global__ void __launch_bounds__(1024)
+    se_fc1_kernel(const float* __restrict__ part, int chunks, int c, int cr,
+                  float inv_hw, const float* __restrict__ w1,
+                  const float* __restrict__ b1, float* __restrict__ hidden,
+                  float* __restrict__ mean) {
+  extern __shared__ float m[];  // [c]
   const int nidx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
     const float* p = part + ((int64_t)nidx * c + ch) * chunks;
     float acc = 0.f;
     for (int k = 0; k < chunks; ++k) acc += p[k];
     m[ch] = acc * inv_hw;
-    mean[(int64_t)nidx * c + ch] = m[ch];
+    if (blockIdx.y == 0) mean[(int64_t)nidx * c + ch] = m[ch];
   }
   __syncthreads();
-  for (int j = threadIdx.x; j < cr; j += blockDim.x) {
-    const float* wr = w1 + (int64_t)j * c;
-    float acc = 0.f;
-    for (int ch = 0; ch < c; ++ch) acc += wr[ch] * m[ch];
-    if (b1) acc += b1[j];
-    acc = acc > 0.f ? acc : 0.f;
-    hdn[j] = acc;
-    hidden[(int64_t)nidx * cr + j] = acc;
-  }
+  const int j = blockIdx.y * kOutPerBlock + wid;
+  if (j >= cr) return;
+  const float* wr = w1 + (int64_t)j * c;
+  float acc = 0.f;
+  for (int ch = lane; ch < c; ch += 64) acc += wr[ch] * m[ch];
+  acc = mde::wave_sum(acc);
+  if (b1) acc += b1[j];
+  if (lane == 0) hidden[(int64_t)nidx * cr + j] = acc > 0.f ? acc : 0.f;
+}
+
+// s[n, ch] = gate(W2[ch] . hidden[n] + b2[ch])
+__global__ void __launch_bounds__(1024)
+    se_fc2_kernel(int c, int cr, const float* __restrict__ w2,
+                  const float* __restrict__ b2, int gate,
+                  const float* __restrict__ hidden, float* __restrict__ s) {
+  extern __shared__ float hdn[];  // [cr]
+  const int nidx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int j = threadIdx.x; j < cr; j += blockDim.x) hdn[j] = hidden[(int64_t)nidx * cr + j];
   __syncthreads();
-  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
-    const float* wr = w2 + (int64_t)ch * cr;
-    float z = 0.f;
-    for (int j = 0; j < cr; ++j) z += wr[j] * hdn[j];
-    if (b2) z += b2[ch];
-    s[(int64_t)nidx * c + ch] = gate_fn(z, gate);
-  }
+  const int ch = blockIdx.y * kOutPerBlock + wid;
+  if (ch >= c) return;
+  const float* wr = w2 + (int64_t)ch * cr;
+  float z = 0.f;
+  for (int j = lane; j < cr; j += 64) z += wr[j] * hdn[j];
+  z = mde::wave_sum(z);
+  if (b2) z += b2[ch];
+  if (lane == 0) s[(int64_t)nidx * c + ch] = gate_fn(z, gate);
 }
 
 // out[plane, i] = x[plane, i] * s[plane]  (cat fused: plane -> xa or xb)
@@ -134,56 +149,74 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Per-sample backward through sigmoid / W2 / relu / W1.
-//   ds = sum g*x;  dz = ds s (1-s);  dh = (h>0) W2^T dz;  dm = W1^T dh
-//   hardsigmoid: dz = ds / 6 where -3 < z < 3 (z recomputed from the hidden)
-__global__ void __launch_bounds__(256)
-    se_bwd_fc_kernel(const float* __restrict__ part, int chunks, int c, int cr,
-                     const float* __restrict__ w1, const float* __restrict__ w2,
-                     const float* __restrict__ b2, int gate,
-                     const float* __restrict__ s,
-                     const float* __restrict__ hidden, float* __restrict__ dz,
-                     float* __restrict__ dh, float* __restrict__ dm) {
-  extern __shared__ float sm[];
-  float* z = sm;        // [c]
-  float* hh = sm + c;   // [cr]
+// Per-sample backward through the gate / W2 / relu / W1, three GEMV kernels:
+//   dz = ds * gate'(z)  (ds = sum g*x; sigmoid: s(1-s); hardsigmoid: 1/6 on
+//        (-3, 3), z recomputed from the hidden)
+//   dh = (h > 0) W2^T dz;   dm = W1^T dh
+__global__ void __launch_bounds__(1024)
+    se_bfc1_kernel(const float* __restrict__ part, int chunks, int c, int cr,
+                   const float* __restrict__ w2, const float* __restrict__ b2, int gate,
+                   const float* __restrict__ s, const float* __restrict__ hidden,
+                   float* __restrict__ dz) {
+  extern __shared__ float hh[];  // [cr]
   const int nidx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (gate == 1) {
     for (int j = threadIdx.x; j < cr; j += blockDim.x) hh[j] = hidden[(int64_t)nidx * cr + j];
     __syncthreads();
   }
-  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
-    const float* p = part + ((int64_t)nidx * c + ch) * chunks;
-    float acc = 0.f;
-    for (int k = 0; k < chunks; ++k) acc += p[k];
-    float v;
-    if (gate == 0) {
-      const float sv = s[(int64_t)nidx * c + ch];
-      v = acc * (sv * (1.f - sv));
-    } else {
-      const float* wr = w2 + (int64_t)ch * cr;
-      float zz = 0.f;
-      for (int j = 0; j < cr; ++j) zz += wr[j] * hh[j];
-      if (b2) zz += b2[ch];
-      v = (zz > -3.f && zz < 3.f) ? acc / 6.f : 0.f;
-    }
-    z[ch] = v;
-    dz[(int64_t)nidx * c + ch] = v;
+  const int ch = blockIdx.y * kOutPerBlock + wid;
+  if (ch >= c) return;
+  const float* p = part + ((int64_t)nidx * c + ch) * chunks;
+  float ds = 0.f;
+  for (int k = lane; k < chunks; k += 64) ds += p[k];
+  ds = mde::wave_sum(ds);
+  float v;
+  if (gate == 0) {
+    const float sv = s[(int64_t)nidx * c + ch];
+    v = ds * (sv * (1.f - sv));
+  } else {
+    const float* wr = w2 + (int64_t)ch * cr;
+    float zz = 0.f;
+    for (int j = lane; j < cr; j += 64) zz += wr[j] * hh[j];
+    zz = mde::wave_sum(zz);
+    if (b2) zz += b2[ch];
+    v = (zz > -3.f && zz < 3.f) ? ds / 6.f : 0.f;
   }
+  if (lane == 0) dz[(int64_t)nidx * c + ch] = v;
+}
+
+__global__ void __launch_bounds__(1024)
+    se_bfc2_kernel(int c, int cr, const float* __restrict__ w2,
+                   const float* __restrict__ hidden, const float* __restrict__ dz,
+                   float* __restrict__ dh) {
+  extern __shared__ float z[];  // [c]
+  const int nidx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) z[ch] = dz[(int64_t)nidx * c + ch];
   __syncthreads();
-  for (int j = threadIdx.x; j < cr; j += blockDim.x) {
-    float acc = 0.f;
-    for (int ch = 0; ch < c; ++ch) acc += w2[(int64_t)ch * cr + j] * z[ch];
-    const float v = hidden[(int64_t)nidx * cr + j] > 0.f ? acc : 0.f;
-    hh[j] = v;
-    dh[(int64_t)nidx * cr + j] = v;
-  }
+  const int j = blockIdx.y * kOutPerBlock + wid;
+  if (j >= cr) return;
+  float acc = 0.f;
+  for (int ch = lane; ch < c; ch += 64) acc += w2[(int64_t)ch * cr + j] * z[ch];
+  acc = mde::wave_sum(acc);
+  if (lane == 0) dh[(int64_t)nidx * cr + j] = hidden[(int64_t)nidx * cr + j] > 0.f ? acc : 0.f;
+}
+
+__global__ void __launch_bounds__(1024)
+    se_bfc3_kernel(int c, int cr, const float* __restrict__ w1,
+                   const float* __restrict__ dh, float* __restrict__ dm) {
+  extern __shared__ float hh[];  // [cr]
+  const int nidx = blockIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int j = threadIdx.x; j < cr; j += blockDim.x) hh[j] = dh[(int64_t)nidx * cr + j];
   __syncthreads();
-  for (int ch = threadIdx.x; ch < c; ch += blockDim.x) {
-    float acc = 0.f;
-    for (int j = 0; j < cr; ++j) acc += w1[(int64_t)j * c + ch] * hh[j];
-    dm[(int64_t)nidx * c + ch] = acc;
-  }
+  const int ch = blockIdx.y * kOutPerBlock + wid;
+  if (ch >= c) return;
+  float acc = 0.f;
+  for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * hh[j];
+  acc = mde::wave_sum(acc);
+  if (lane == 0) dm[(int64_t)nidx * c + ch] = acc;
 }
 
 // gw2[ch, j] = sum_n dz[n,ch] h[n,j];  gw1[j, ch] = sum_n dh[n,j] m[n,ch];
@@ -319,10 +352,13 @@ int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<false>,
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr,
              (const float*)xa, ca, (const float*)xb, cb, hw, chunks, ws.part);
-  MDE_LAUNCH(mde::K_SE_FC, 4.0 * (2.0 * c * cr + 3.0 * n * c), st,
-             se_fc_kernel, dim3((unsigned)n), dim3(256),
-             sizeof(float) * (c + cr), ws.part, chunks, (int)c, (int)cr,
-             1.f / (float)hw, w1, w2, b1, b2, gate, s, hidden, mean);
+  MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc1_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(cr, kOutPerBlock)), dim3(1024),
+             sizeof(float) * c, ws.part, chunks, (int)c, (int)cr, 1.f / (float)hw, w1, b1,
+             hidden, mean);
+  MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc2_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
+             sizeof(float) * cr, (int)c, (int)cr, w2, b2, gate, hidden, s);
   MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel,
              dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
              (const float*)xa, ca, (const float*)xb, cb, hw, n * c, s,
@@ -351,10 +387,16 @@ int mde_se_gate_bwd(const void* gout, const void* xa, int64_t ca, const void* xb
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0,
              (const float*)gout, (const float*)xa, ca, (const float*)xb, cb,
              hw, chunks, ws.part);
-  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 4.0 * n * c), st,
-             se_bwd_fc_kernel, dim3((unsigned)n), dim3(256),
-             sizeof(float) * (c + cr), ws.part, chunks, (int)c, (int)cr, w1,
-             w2, b2, gate, s, hidden, ws.dz, ws.dh, ws.dm);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + 3.0 * n * c), st, se_bfc1_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
+             sizeof(float) * cr, ws.part, chunks, (int)c, (int)cr, w2, b2, gate, s, hidden,
+             ws.dz);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + n * (c + 2.0 * cr)), st, se_bfc2_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(cr, kOutPerBlock)), dim3(1024),
+             sizeof(float) * c, (int)c, (int)cr, w2, hidden, ws.dz, ws.dh);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + n * (c + cr)), st, se_bfc3_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
+             sizeof(float) * cr, (int)c, (int)cr, w1, ws.dh, ws.dm);
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 2.0 * n * (c + cr)), st,
              se_wgrad_kernel, dim3((unsigned)mde::cdiv(2 * c * cr, 256)),
              dim3(256), 0, (int)n, (int)c, (int)cr, ws.dz, ws.dh, hidden,

@@ -26,9 +26,9 @@ NAMES = [
     (r"nearest_bwd_kernel", "nearest_bwd"),
     (r"se_partial_kernel<false>", "se_squeeze"),
     (r"se_partial_kernel<true>", "se_bwd_dot"),
-    (r"se_fc_kernel", "se_fc"),
+    (r"se_fc[12]_kernel", "se_fc"),
     (r"se_scale_kernel", "se_scale"),
-    (r"se_(bwd_fc|wgrad)_kernel", "se_bwd_fc"),
+    (r"se_(bfc[123]|wgrad)_kernel", "se_bwd_fc"),
     (r"se_apply_kernel", "se_bwd_apply"),
     (r"skip_fwd_kernel", "skip_reduce_fwd"),
     (r"skip_bwd_kernel", "skip_reduce_bwd"),
@@ -45,6 +45,16 @@ NAMES = [
     (r"bn_bwd_apply_plane_kernel", "bn_bwd_apply"),
     (r"bn_bwd_apply_table_kernel", "bn_bwd_apply_small"),
     (r"skip_bwd_reg_kernel", "skip_reduce_bwd"),
+    (r"wattn_fwd_kernel", "window_attn_fwd"),
+    (r"wattn_(bwd|slab_reduce)_kernel|zero_kernel", "window_attn_bwd"),
+    (r"dw_fwd_kernel", "dwconv_fwd"),
+    (r"dw_bwd_data_kernel", "dwconv_bwd_data"),
+    (r"dw_bwd_weight_kernel", "dwconv_bwd_weight"),
+    (r"dw_wreduce_kernel", "dwconv_wreduce"),
+    (r"ln_fwd_kernel", "layernorm_fwd"),
+    (r"ln_bwd_kernel", "layernorm_bwd"),
+    (r"ln_wreduce_kernel", "layernorm_wreduce"),
+    (r"transpose_kernel", "transpose"),
 ]
 
 

@@ -16,13 +16,13 @@ import re
 
 MARK = "minmax_partial_kernel"
 
-OURS = re.compile(r"^(bilinear|nearest|se_partial|se_fc|se_scale|se_bwd|se_wgrad|se_apply|skip_|minmax|"
+OURS = re.compile(r"^(bilinear|nearest|se_partial|se_fc|se_scale|se_bfc|se_wgrad|se_apply|skip_|minmax|"
                   r"depthnorm|ssim3|loss_final|dloss|bn_|wattn|dw_|ln_)")
 
 
 def short(name: str) -> str:
     name = re.sub(r"^void ", "", name)
-    m = re.match(r"(?:\(anonymous namespace\)::)?(\w+)", name)
+    m = re.match(r"(?:mde::)?(?:\(anonymous namespace\)::)?(\w+)", name)
     base = m.group(1) if m else name[:60]
     if base.startswith("Cijk_"):
         return "rocBLAS/Tensile " + base[:48]

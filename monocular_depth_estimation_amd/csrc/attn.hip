@@ -17,9 +17,18 @@
 // is 0, so padded keys take part in the softmax exactly as in the reference.
 // Outputs are written straight to token order [B, H*W, C].
 //
-// Per (window, head) the 49x49 (padded to 64x64) score tile and the 64x32
-// output tile are v_mfma_f32_16x16x4_f32 products (exact fp32, one rounding
-// per product): 4 waves, wave w owns rows 16w..16w+15.
+// Work split: one wave per (window, head), four heads per block.  A window's
+// <= 64 tokens are padded to 64 = 4 MFMA tiles.  The scores live in
+// registers TRANSPOSED, S^T[j][i] (key rows, query columns), as 4x4
+// v_mfma_f32_16x16x4_f32 accumulators: with the query in the C-column slot a
+// lane's four accumulator values of a tile are four keys of ONE query, which
+// is exactly the A-operand of the next product that contracts over keys
+// (O = P V, dQ = dS K) — no LDS round trip.  The head-dim contraction of
+// S^T = K Q^T uses a permuted k order (lane group g supplies dims 8g..8g+7
+// over the 8 MFMA steps), so each lane's operands are 32 contiguous bytes of
+// a token row: two float4 loads straight from HBM/L2, no LDS staging.
+// Products contracting over queries (dV = P^T dO, dK = dS^T Q) read P / dS
+// back from a per-wave LDS tile.  All f32 MFMA: exact f32 products.
 //
 // Backward recomputes S and P (no saved probabilities), then
 //   dP = dO V^T, dS = P (dP - rowsum(P dP)), dQ = dS K / sqrt(d),
@@ -33,11 +42,12 @@ namespace {
 
 using f4 = __attribute__((ext_vector_type(4))) float;
 
-constexpr int D = 32;       // head dim (all four NewCRF stages)
-constexpr int NP = 64;      // padded tokens per window (ws*ws <= 64)
-constexpr int LD = 33;      // LDS row stride of the [64][32] tiles
-constexpr int LP = 65;      // LDS row stride of the [64][64] tiles
-constexpr int kGroup = 8;   // windows per backward block
+constexpr int D = 32;        // head dim (all four NewCRF stages)
+constexpr int NP = 64;       // padded tokens per window (ws*ws <= 64)
+constexpr int LT = 65;       // LDS row pitch of the per-wave [64][64] P / dS tile
+constexpr int TABP = 256;    // table slots ((2ws-1)^2 <= 225)
+constexpr int kHeads = 4;    // heads (= waves) per block
+constexpr int kWinBwd = 4;   // windows per backward block
 
 struct Geo {
   int b, h, w, c, heads, ws, shift, hp, wp, nwh, nww, n;
@@ -52,328 +62,455 @@ __device__ __forceinline__ int region(int y, int hp, int ws, int shift) {
   return y < hp - ws ? 0 : (y < hp - shift ? 1 : 2);
 }
 
-// Token bookkeeping for window `win` of the shifted, padded grid.
-__device__ __forceinline__ void window_tokens(const Geo& g, int win, int* tok,
-                                              int* lab) {
+template <int WS>
+__device__ __forceinline__ int wsize(const Geo& g) {
+  return WS ? WS : g.ws;
+}
+
+// tok[i]: token index in the image (>= 0), -1 padded (q = k = bias, v = 0),
+// -2 beyond the window (i >= ws*ws); lab[i]: shifted-region label.
+template <int WS>
+__device__ __forceinline__ void window_tokens(const Geo& g, int win, int* tok, int* lab) {
+  const int ws = wsize<WS>(g), n = ws * ws;
+  const int i = threadIdx.x;
+  if (i >= NP) return;
   const int wloc = win % (g.nwh * g.nww);
-  const int wy = wloc / g.nww, wx = wloc % g.nww;
-  for (int i = threadIdx.x; i < NP; i += blockDim.x) {
-    int t = -2, l = 0;
-    if (i < g.n) {
-      const int r = i / g.ws, cc = i % g.ws;
-      const int ys = wy * g.ws + r, xs = wx * g.ws + cc;
-      const int yp = (ys + g.shift) % g.hp, xp = (xs + g.shift) % g.wp;
-      t = (yp < g.h && xp < g.w) ? yp * g.w + xp : -1;
-      l = region(ys, g.hp, g.ws, g.shift) * 3 + region(xs, g.wp, g.ws, g.shift);
-    }
-    tok[i] = t;
-    lab[i] = l;
+  const int wy = wloc / g.nww, wx = wloc - wy * g.nww;
+  int t = -2, l = 0;
+  if (i < n) {
+    const int r = i / ws, cc = i - r * ws;
+    const int ys = wy * ws + r, xs = wx * ws + cc;
+    int yp = ys + g.shift, xp = xs + g.shift;
+    if (yp >= g.hp) yp -= g.hp;
+    if (xp >= g.wp) xp -= g.wp;
+    t = (yp < g.h && xp < g.w) ? yp * g.w + xp : -1;
+    l = region(ys, g.hp, ws, g.shift) * 3 + region(xs, g.wp, ws, g.shift);
+  }
+  tok[i] = t;
+  lab[i] = l;
+}
+
+// 8 contiguous floats at p (32-byte aligned)
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// Row operand: columns [off, off+8) of token t's row (stride `ld`), the bias
+// for a padded token (when given), else zeros.  Offsets are 32-bit from a
+// wave-uniform base (image planes are < 2^31 elements, checked on the host),
+// so a load is one VGPR offset on an SGPR base.
+__device__ __forceinline__ void row8(const float* base, int ld, int off, int t,
+                                     const float* bias, float* v) {
+  if (t >= 0) {
+    load8(base + (unsigned)(t * ld + off), v);
+  } else if (t == -1 && bias) {
+    load8(bias + off, v);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = 0.f;
   }
 }
 
-// Q (pre-scaled), K, V tiles of one (window, head); padded -> bias / 0.
-__device__ __forceinline__ void load_qkv(const Geo& g, int bidx, int head,
-                                         const float* __restrict__ qk,
-                                         const float* __restrict__ qkb,
-                                         const float* __restrict__ v,
-                                         const int* tok, float (*Q)[LD],
-                                         float (*K)[LD], float (*V)[LD]) {
-  const int64_t c2 = 2 * (int64_t)g.c;
-  const float* qkbase = qk + (int64_t)bidx * g.h * g.w * c2;
-  const float* vbase = v + (int64_t)bidx * g.h * g.w * g.c;
-  for (int e = threadIdx.x; e < NP * D; e += blockDim.x) {
-    const int i = e / D, k = e % D;
-    const int t = tok[i];
-    float q = 0.f, kk = 0.f, vv = 0.f;
-    if (t >= 0) {
-      q = qkbase[t * c2 + head * D + k];
-      kk = qkbase[t * c2 + g.c + head * D + k];
-      vv = vbase[(int64_t)t * g.c + head * D + k];
-    } else if (t == -1) {
-      q = qkb[head * D + k];
-      kk = qkb[g.c + head * D + k];
-    }
-    Q[i][k] = q * g.scale;
-    K[i][k] = kk;
-    V[i][k] = vv;
-  }
+// Scalar operand: element `col` of token t's row, bias for padded, else 0.
+__device__ __forceinline__ float elem(const float* base, int ld, int col, int t,
+                                      const float* bias) {
+  if (t >= 0) return base[(unsigned)(t * ld + col)];
+  if (t == -1 && bias) return bias[col];
+  return 0.f;
 }
 
-// S rows of this wave (16 x 64) = Q K^T + bias (+ mask); -inf past the window.
-__device__ __forceinline__ void scores(const Geo& g, float (*Q)[LD], float (*K)[LD],
-                                       const float* tab, const int* lab, f4 s[4]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+// P^T[jt][it] (key rows, query columns) of this wave's (window, head):
+// S^T = K Q^T * scale + table + mask, softmax over keys per query column.
+// Lane (l16, g): s[jt][it][r] is key j = 16jt + 4g + r, query i = 16it + l16.
+// Columns of padded queries (i >= ws*ws) come out 0.
+template <int WS>
+__device__ __forceinline__ void probs_t(const Geo& g, const float* __restrict__ qkrow,
+                                        const float* __restrict__ qkb, int head,
+                                        const int* tok, const int* lab, const float* tab,
+                                        f4 s[4][4]) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
+  const int c2 = 2 * g.c;
+  {
+    float ka[4][8];
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) s[ct] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int jt = 0; jt < 4; ++jt)
+      row8(qkrow, c2, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
 #pragma unroll
-  for (int kc = 0; kc < D / 4; ++kc) {
-    const float a = Q[16 * w + (lane & 15)][4 * kc + (lane >> 4)];
+    for (int it = 0; it < 4; ++it) {
+      float qb[8];
+      row8(qkrow, c2, head * D + 8 * g4, tok[16 * it + l16], qkb, qb);
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-      s[ct] = mfma4(a, K[16 * ct + (lane & 15)][4 * kc + (lane >> 4)], s[ct]);
-  }
-  const int ws = g.ws, span = 2 * ws - 1;
+      for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
 #pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    const int j = 16 * ct + (lane & 15);
+      for (int jt = 0; jt < 4; ++jt) {
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int i = 16 * w + (lane >> 4) * 4 + r;
-      if (j >= g.n || i >= g.n) {
-        s[ct][r] = j >= g.n ? -INFINITY : 0.f;
-      } else {
-        const int idx = (i / ws - j / ws + ws - 1) * span + (i % ws - j % ws + ws - 1);
-        float v = s[ct][r] + tab[idx];
-        if (g.shift && lab[i] != lab[j]) v += -100.f;
-        s[ct][r] = v;
+        for (int k = 0; k < 8; ++k) acc = mfma4(ka[jt][k], qb[k], acc);
+        s[jt][it] = acc;
       }
     }
   }
-}
-
-// Row-wise softmax over the 64 columns held by 16 lanes x 4 column tiles.
-__device__ __forceinline__ void softmax_rows(f4 s[4]) {
+  // this lane's 16 keys: table offset -(yj*span + xj) and region label, packed
+  int kj[16];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float m = fmaxf(fmaxf(s[0][r], s[1][r]), fmaxf(s[2][r], s[3][r]));
+  for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-      const float e = __expf(s[ct][r] - m);
-      s[ct][r] = e;
-      sum += e;
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + 4 * g4 + r;
+      const int y = j / ws, x = j - y * ws;
+      kj[4 * jt + r] = ((y * span + x) << 4) | lab[j];
     }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
-    const float inv = 1.f / sum;
+  for (int it = 0; it < 4; ++it) {
+    const int i = 16 * it + l16;
+    const bool iv = i < n;
+    const int yi = i / ws, xi = i - yi * ws, li = lab[i];
+    const int base = (yi + ws - 1) * span + xi + ws - 1;
+    float m = -INFINITY;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) s[ct][r] *= inv;
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * jt + 4 * g4 + r;
+        float v;
+        if (j >= n) {
+          v = -INFINITY;
+        } else if (!iv) {
+          v = 0.f;
+        } else {
+          const int q = kj[4 * jt + r];
+          v = s[jt][it][r] + tab[base - (q >> 4)];
+          if (g.shift && (q & 15) != li) v += -100.f;
+        }
+        s[jt][it][r] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(s[jt][it][r] - m);
+        s[jt][it][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = iv ? 1.f / sum : 0.f;  // padded query columns -> 0
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) s[jt][it] *= inv;
   }
 }
 
-// Store a wave's 16 x 64 accumulator rows into a [64][LP] LDS tile.
-__device__ __forceinline__ void store_rows(float (*T)[LP], const f4 s[4]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) T[16 * w + (lane >> 4) * 4 + r][16 * ct + (lane & 15)] = s[ct][r];
-}
-
-// out rows (16w..16w+15) x 32 = A[rows][0..63] @ B[0..63][0..31]
-// TRANS_A: read A transposed from the [64][LP] tile (A[i][k] = T[k][i]).
-template <bool TRANS_A>
-__device__ __forceinline__ void mm_64x32(float (*A)[LP], float (*B)[LD], f4 o[2]) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  o[0] = f4{0.f, 0.f, 0.f, 0.f};
-  o[1] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int kc = 0; kc < NP / 4; ++kc) {
-    const int row = 16 * w + (lane & 15), k = 4 * kc + (lane >> 4);
-    const float a = TRANS_A ? A[k][row] : A[row][k];
-#pragma unroll
-    for (int dt = 0; dt < 2; ++dt) o[dt] = mfma4(a, B[k][16 * dt + (lane & 15)], o[dt]);
-  }
-}
-
+template <int WS>
 __global__ void __launch_bounds__(256)
     wattn_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ qkb,
                      const float* __restrict__ v, const float* __restrict__ table,
                      float* __restrict__ out, Geo g) {
-  __shared__ float Q[NP][LD], K[NP][LD], V[NP][LD];
-  __shared__ float P[NP][LP];
-  __shared__ float tab[256];
   __shared__ int tok[NP], lab[NP];
-  const int win = blockIdx.x, head = blockIdx.y;
+  __shared__ float tab[kHeads][TABP];
+  const int win = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
+  const int head = blockIdx.y * kHeads + w;
+  const int ws = wsize<WS>(g), ntab = (2 * ws - 1) * (2 * ws - 1);
+  window_tokens<WS>(g, win, tok, lab);
+  if (head < g.heads)
+    for (int e = lane; e < ntab; e += 64) tab[w][e] = table[e * g.heads + head];
+  __syncthreads();
+  if (head >= g.heads) return;
   const int bidx = win / (g.nwh * g.nww);
-  const int ntab = (2 * g.ws - 1) * (2 * g.ws - 1);
-  for (int i = threadIdx.x; i < ntab; i += blockDim.x) tab[i] = table[i * g.heads + head];
-  window_tokens(g, win, tok, lab);
-  __syncthreads();
-  load_qkv(g, bidx, head, qk, qkb, v, tok, Q, K, V);
-  __syncthreads();
-  f4 s[4];
-  scores(g, Q, K, tab, lab, s);
-  softmax_rows(s);
-  store_rows(P, s);
-  __syncthreads();
-  f4 o[2];
-  mm_64x32<false>(P, V, o);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  float* obase = out + (int64_t)bidx * g.h * g.w * g.c;
+  const int64_t img = (int64_t)bidx * g.h * g.w;
+  f4 s[4][4];
+  probs_t<WS>(g, qk + img * 2 * g.c, qkb, head, tok, lab, tab[w], s);
+  // O = P V: A = P[i][j] straight from the S^T accumulators (k <-> key
+  // 16jt + 4g + r), B = V[j][d] per lane.
+  const float* vrow = v + img * g.c;
+  float vb[4][4][2];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = 16 * w + (lane >> 4) * 4 + r;
-    const int t = i < NP ? tok[i] : -2;
-    if (t >= 0) {
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = tok[16 * jt + 4 * g4 + r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
-        obase[(int64_t)t * g.c + head * D + 16 * dt + (lane & 15)] = o[dt][r];
+        vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, nullptr);
+    }
+  float* orow = out + img * g.c;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    f4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma4(s[jt][it][r], vb[jt][r][dt], o[dt]);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int t = tok[16 * it + 4 * g4 + rr];
+      if (t >= 0) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          orow[(unsigned)(t * g.c + head * D + 16 * dt + l16)] = o[dt][rr];
+      }
     }
   }
 }
 
+// Stage this wave's P^T / dS^T registers as T[j][i] (key row, query column).
+__device__ __forceinline__ void stage_t(float (*T)[LT], const f4 s[4][4]) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) T[16 * jt + 4 * g4 + r][16 * it + l16] = s[jt][it][r];
+}
+
+// One 16-key tile of sum_i T[j][i] B[i][c]: o[ct] (C layout: key 16jt + 4g + rr,
+// c = 16ct + l16), B given per lane as b[it][r][ct] = B[16it + 4g + r][16ct + l16].
+__device__ __forceinline__ void mm_tb_tile(float (*T)[LT], int jt, const float b[4][4][2],
+                                           f4 o[2]) {
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  o[0] = f4{0.f, 0.f, 0.f, 0.f};
+  o[1] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < 4; ++it)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float a = T[16 * jt + l16][16 * it + 4 * g4 + r];
+#pragma unroll
+      for (int ct = 0; ct < 2; ++ct) o[ct] = mfma4(a, b[it][r][ct], o[ct]);
+    }
+}
+
 // slab[(blockIdx.x * heads + head) * (ntab + D)] = {dT[0..ntab), dkbias[0..D)}
-__global__ void __launch_bounds__(256)
+template <int WS>
+__global__ void __launch_bounds__(256, 2)
     wattn_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ qk,
                      const float* __restrict__ qkb, const float* __restrict__ v,
                      const float* __restrict__ table, float* __restrict__ gqk,
                      float* __restrict__ gv, float* __restrict__ slab, int nwin, Geo g) {
-  __shared__ float Q[NP][LD], K[NP][LD], V[NP][LD], G[NP][LD];
-  __shared__ float P[NP][LP], DS[NP][LP];
-  __shared__ float tab[256], dtab[256], dkb[D];
   __shared__ int tok[NP], lab[NP];
-  const int head = blockIdx.y;
-  const int ntab = (2 * g.ws - 1) * (2 * g.ws - 1);
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t c2 = 2 * (int64_t)g.c;
-  for (int i = threadIdx.x; i < ntab; i += blockDim.x) {
-    tab[i] = table[i * g.heads + head];
-    dtab[i] = 0.f;
-  }
-  if (threadIdx.x < D) dkb[threadIdx.x] = 0.f;
-  for (int wi = 0; wi < kGroup; ++wi) {
-    const int win = blockIdx.x * kGroup + wi;
+  __shared__ float tab[kHeads][TABP], dtab[kHeads][TABP];
+  __shared__ float T[kHeads][NP][LT];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
+  const int head = blockIdx.y * kHeads + w;
+  const bool active = head < g.heads;
+  const int ws = wsize<WS>(g), span = 2 * ws - 1, ntab = span * span;
+  const int c = g.c, c2 = 2 * g.c, hd = head * D;
+  if (active)
+    for (int e = lane; e < ntab; e += 64) {
+      tab[w][e] = table[e * g.heads + head];
+      dtab[w][e] = 0.f;
+    }
+  float dkb[2] = {0.f, 0.f};  // d(k bias)[16ct + l16] partial of this lane
+  for (int wi = 0; wi < kWinBwd; ++wi) {
+    const int win = blockIdx.x * kWinBwd + wi;
     if (win >= nwin) break;  // uniform across the block
-    const int bidx = win / (g.nwh * g.nww);
+    __syncthreads();         // previous window's tok / T readers are done
+    window_tokens<WS>(g, win, tok, lab);
     __syncthreads();
-    window_tokens(g, win, tok, lab);
-    __syncthreads();
-    load_qkv(g, bidx, head, qk, qkb, v, tok, Q, K, V);
-    const float* gbase = gout + (int64_t)bidx * g.h * g.w * g.c;
-    for (int e = threadIdx.x; e < NP * D; e += blockDim.x) {
-      const int i = e / D, k = e % D;
-      const int t = tok[i];
-      G[i][k] = t >= 0 ? gbase[(int64_t)t * g.c + head * D + k] : 0.f;
-    }
-    __syncthreads();
-    f4 s[4];
-    scores(g, Q, K, tab, lab, s);
-    softmax_rows(s);
-    // dP = dO V^T for this wave's rows
-    f4 dp[4];
+    const int64_t img = (int64_t)(win / (g.nwh * g.nww)) * g.h * g.w;
+    const float* qkrow = qk + img * c2;
+    const float* vrow = v + img * c;
+    const float* grow = gout + img * c;
+    float* gqkrow = gqk + img * c2;
+    float* gvrow = gv + img * c;
+    // T[w] is private to this wave: its LDS accesses are processed in program
+    // order, so the P / dS round trips need no block barrier.
+    if (active) {
+      f4 s[4][4];
+      probs_t<WS>(g, qkrow, qkb, head, tok, lab, tab[w], s);
+      __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
+      stage_t(T[w], s);  // P
+      // dV = P^T dO
+      {
+        float b[4][4][2];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) dp[ct] = f4{0.f, 0.f, 0.f, 0.f};
+        for (int it = 0; it < 4; ++it)
 #pragma unroll
-    for (int kc = 0; kc < D / 4; ++kc) {
-      const float a = G[16 * w + (lane & 15)][4 * kc + (lane >> 4)];
+          for (int r = 0; r < 4; ++r) {
+            const int t = tok[16 * it + 4 * g4 + r];
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-        dp[ct] = mfma4(a, V[16 * ct + (lane & 15)][4 * kc + (lane >> 4)], dp[ct]);
-    }
-    // dS = P (dP - rowsum(P dP))
+            for (int ct = 0; ct < 2; ++ct)
+              b[it][r][ct] = elem(grow, c, hd + 16 * ct + l16, t, nullptr);
+          }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float dl = 0.f;
+        for (int jt = 0; jt < 4; ++jt) {
+          f4 o[2];
+          mm_tb_tile(T[w], jt, b, o);
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) dl += s[ct][r] * dp[ct][r];
+          for (int rr = 0; rr < 4; ++rr) {
+            const int t = tok[16 * jt + 4 * g4 + rr];
+            if (t >= 0) {
 #pragma unroll
-      for (int o = 1; o < 16; o <<= 1) dl += __shfl_xor(dl, o, 64);
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) dp[ct][r] = s[ct][r] * (dp[ct][r] - dl);
-    }
-    store_rows(P, s);
-    store_rows(DS, dp);
-    __syncthreads();
-    // table gradient: entry e <- sum over the (i, j) pairs with that offset,
-    // in a fixed order (deterministic)
-    for (int e = threadIdx.x; e < ntab; e += blockDim.x) {
-      const int span = 2 * g.ws - 1;
-      const int dy = e / span - (g.ws - 1), dx = e % span - (g.ws - 1);
-      float acc = 0.f;
-      for (int ri = 0; ri < g.ws; ++ri) {
-        const int rj = ri - dy;
-        if (rj < 0 || rj >= g.ws) continue;
-        for (int ci = 0; ci < g.ws; ++ci) {
-          const int cj = ci - dx;
-          if (cj < 0 || cj >= g.ws) continue;
-          acc += DS[ri * g.ws + ci][rj * g.ws + cj];
+              for (int ct = 0; ct < 2; ++ct)
+                gvrow[(unsigned)(t * c + hd + 16 * ct + l16)] = o[ct][rr];
+            }
+          }
         }
       }
-      dtab[e] += acc;
-    }
-    f4 o[2];
-    float* gqkb = gqk + (int64_t)bidx * g.h * g.w * c2;
-    // dQ = dS K * scale   (rows i of this wave)
-    {
-      const int row = 16 * w;
-      o[0] = f4{0.f, 0.f, 0.f, 0.f};
-      o[1] = f4{0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
+      // dP^T = V dO^T column by column; dS = P (dP - rowsum(P dP)) in place
+      {
+        float va[4][8];
 #pragma unroll
-      for (int kc = 0; kc < NP / 4; ++kc) {
-        const float a = DS[row + (lane & 15)][4 * kc + (lane >> 4)];
+        for (int jt = 0; jt < 4; ++jt)
+          row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], nullptr, va[jt]);
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          o[dt] = mfma4(a, K[4 * kc + (lane >> 4)][16 * dt + (lane & 15)], o[dt]);
-      }
+        for (int it = 0; it < 4; ++it) {
+          float db[8];
+          row8(grow, c, hd + 8 * g4, tok[16 * it + l16], nullptr, db);
+          f4 dp[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = row + (lane >> 4) * 4 + r;
-        const int t = tok[i];
-        if (t >= 0) {
+          for (int jt = 0; jt < 4; ++jt) {
+            dp[jt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int dt = 0; dt < 2; ++dt)
-            gqkb[t * c2 + head * D + 16 * dt + (lane & 15)] = o[dt][r] * g.scale;
+            for (int k = 0; k < 8; ++k) dp[jt] = mfma4(va[jt][k], db[k], dp[jt]);
+          }
+          float dl = 0.f;
+#pragma unroll
+          for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dl += s[jt][it][r] * dp[jt][r];
+          dl += __shfl_xor(dl, 16, 64);
+          dl += __shfl_xor(dl, 32, 64);
+#pragma unroll
+          for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) s[jt][it][r] = s[jt][it][r] * (dp[jt][r] - dl);
         }
       }
-    }
-    // dV = P^T dO   (rows j of this wave)
-    mm_64x32<true>(P, G, o);
-    float* gvb = gv + (int64_t)bidx * g.h * g.w * g.c;
+      __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
+      stage_t(T[w], s);  // dS (the dV reads of P are done: same wave, in order)
+      // dQ = dS K * scale: A = dS[i][j] from registers, B = K[j][c] per lane
+      {
+        float b[4][4][2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 16 * w + (lane >> 4) * 4 + r;
-      const int t = tok[j];
-      if (t >= 0) {
+        for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          gvb[(int64_t)t * g.c + head * D + 16 * dt + (lane & 15)] = o[dt][r];
+          for (int r = 0; r < 4; ++r) {
+            const int t = tok[16 * jt + 4 * g4 + r];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              b[jt][r][ct] = elem(qkrow, c2, c + hd + 16 * ct + l16, t, qkb);
+          }
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          f4 q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+          for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct) q[ct] = mfma4(s[jt][it][r], b[jt][r][ct], q[ct]);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int t = tok[16 * it + 4 * g4 + rr];
+            if (t >= 0) {
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct)
+                gqkrow[(unsigned)(t * c2 + hd + 16 * ct + l16)] = q[ct][rr] * g.scale;
+            }
+          }
+        }
       }
-    }
-    // dK = dS^T Q_scaled   (rows j of this wave); padded keys -> d(k bias)
-    mm_64x32<true>(DS, Q, o);
-    __syncthreads();  // every wave is done reading G (dO) before it is reused
+      __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
+      // dK = dS^T Q * scale (dS from the LDS tile)
+      {
+        float b[4][4][2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 16 * w + (lane >> 4) * 4 + r;
-      const int t = tok[j];
+        for (int it = 0; it < 4; ++it)
 #pragma unroll
-      for (int dt = 0; dt < 2; ++dt) {
-        const int d = 16 * dt + (lane & 15);
-        if (t >= 0) gqkb[t * c2 + g.c + head * D + d] = o[dt][r];
-        G[j][d] = t == -1 ? o[dt][r] : 0.f;  // stage padded-key rows
+          for (int r = 0; r < 4; ++r) {
+            const int t = tok[16 * it + 4 * g4 + r];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              b[it][r][ct] = g.scale * elem(qkrow, c2, hd + 16 * ct + l16, t, qkb);
+          }
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) {
+          f4 o[2];
+          mm_tb_tile(T[w], jt, b, o);
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr) {
+            const int t = tok[16 * jt + 4 * g4 + rr];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct) {
+              if (t >= 0)
+                gqkrow[(unsigned)(t * c2 + c + hd + 16 * ct + l16)] = o[ct][rr];
+              else if (t == -1)
+                dkb[ct] += o[ct][rr];
+            }
+          }
+        }
       }
-    }
-    __syncthreads();
-    if (threadIdx.x < D) {
-      float acc = 0.f;
-      for (int j = 0; j < g.n; ++j) acc += G[j][threadIdx.x];
-      dkb[threadIdx.x] += acc;
+      __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
+      // table gradient: entry e <- sum of dS over the (query, key) pairs at
+      // that offset, in a fixed order
+      for (int e = lane; e < ntab; e += 64) {
+        const int dy = e / span - (ws - 1), dx = e % span - (ws - 1);
+        float acc = 0.f;
+        for (int ri = 0; ri < ws; ++ri) {
+          const int rj = ri - dy;
+          if (rj < 0 || rj >= ws) continue;
+          for (int ci = 0; ci < ws; ++ci) {
+            const int cj = ci - dx;
+            if (cj < 0 || cj >= ws) continue;
+            acc += T[w][rj * ws + cj][ri * ws + ci];
+          }
+        }
+        dtab[w][e] += acc;
+      }
     }
   }
-  __syncthreads();
+  if (!active) return;
   float* sl = slab + ((int64_t)blockIdx.x * g.heads + head) * (ntab + D);
-  for (int i = threadIdx.x; i < ntab; i += blockDim.x) sl[i] = dtab[i];
-  if (threadIdx.x < D) sl[ntab + threadIdx.x] = dkb[threadIdx.x];
+  for (int e = lane; e < ntab; e += 64) sl[e] = dtab[w][e];
+#pragma unroll
+  for (int ct = 0; ct < 2; ++ct) {
+    float t = dkb[ct];
+    t += __shfl_xor(t, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    if (g4 == 0) sl[ntab + 16 * ct + l16] = t;
+  }
 }
 
-// gtable[e, head] / gqkb[C + head*D + d] = sum over blocks (fixed order).
-__global__ void __launch_bounds__(256)
+// gtable[e, head] / gqkb[C + head*D + d] = sum over blocks: 64 entries per
+// block of 16 waves, wave w sums blocks w, w+16, ... (8 loads in flight), the
+// 16 wave sums combine in a fixed order.
+__global__ void __launch_bounds__(1024)
     wattn_slab_reduce_kernel(const float* __restrict__ slab, int nblocks, int heads,
                              int ntab, int c, float* __restrict__ gtable,
                              float* __restrict__ gqkb) {
+  __shared__ float red[16][64];
   const int head = blockIdx.y;
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane;
   const int per = ntab + D;
-  if (e >= per) return;
   float acc = 0.f;
-  for (int k = 0; k < nblocks; ++k) acc += slab[((int64_t)k * heads + head) * per + e];
+  if (e < per) {
+#pragma unroll 8
+    for (int k = wid; k < nblocks; k += 16) acc += slab[((int64_t)k * heads + head) * per + e];
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid != 0 || e >= per) return;
+  float t = 0.f;
+#pragma unroll
+  for (int w = 0; w < 16; ++w) t += red[w][lane];
   if (e < ntab)
-    gtable[e * heads + head] = acc;
+    gtable[e * heads + head] = t;
   else
-    gqkb[c + head * D + (e - ntab)] = acc;
+    gqkb[c + head * D + (e - ntab)] = t;
 }
 
 __global__ void zero_kernel(float* p, int n) {
@@ -384,7 +521,7 @@ __global__ void zero_kernel(float* p, int n) {
 bool make_geo(int64_t b, int64_t h, int64_t w, int64_t c, int64_t heads, int64_t ws,
               int64_t shift, Geo* g) {
   if (b <= 0 || h <= 0 || w <= 0 || heads <= 0 || c != heads * D || ws <= 0 ||
-      ws * ws > NP || shift < 0 || shift >= ws || (2 * ws - 1) * (2 * ws - 1) > 256)
+      ws * ws > NP || shift < 0 || shift >= ws || (2 * ws - 1) * (2 * ws - 1) > TABP)
     return false;
   g->b = (int)b; g->h = (int)h; g->w = (int)w; g->c = (int)c;
   g->heads = (int)heads; g->ws = (int)ws; g->shift = (int)shift;
@@ -394,7 +531,8 @@ bool make_geo(int64_t b, int64_t h, int64_t w, int64_t c, int64_t heads, int64_t
   g->nww = g->wp / g->ws;
   g->n = g->ws * g->ws;
   g->scale = 1.f / sqrtf((float)D);
-  return (int64_t)b * g->nwh * g->nww < (1LL << 31) && heads <= 65535;
+  return (int64_t)b * g->nwh * g->nww < (1LL << 31) && mde::cdiv(heads, kHeads) <= 65535 &&
+         (int64_t)h * w * 2 * c < (1LL << 31);
 }
 
 }  // namespace
@@ -407,7 +545,7 @@ size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
   if (!make_geo(b, h, w, c, heads, window, 0, &g)) return 0;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const int64_t ntab = (2 * window - 1) * (2 * window - 1);
-  return sizeof(float) * (size_t)(mde::cdiv(nwin, kGroup) * heads * (ntab + D));
+  return sizeof(float) * (size_t)(mde::cdiv(nwin, kWinBwd) * heads * (ntab + D));
 }
 
 int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
@@ -421,9 +559,13 @@ int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
   hipStream_t s = (hipStream_t)stream;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const double bytes = 4.0 * (double)b * h * w * c * 4.0;  // q, k, v read + o written
-  MDE_LAUNCH(mde::K_WATTN_FWD, bytes, s, wattn_fwd_kernel,
-             dim3((unsigned)nwin, (unsigned)heads), dim3(256), 0, (const float*)qk,
-             qk_bias, (const float*)v, table, (float*)out, g);
+  const dim3 grid((unsigned)nwin, (unsigned)mde::cdiv(heads, kHeads));
+  if (window == 7)
+    MDE_LAUNCH(mde::K_WATTN_FWD, bytes, s, wattn_fwd_kernel<7>, grid, dim3(256), 0,
+               (const float*)qk, qk_bias, (const float*)v, table, (float*)out, g);
+  else
+    MDE_LAUNCH(mde::K_WATTN_FWD, bytes, s, wattn_fwd_kernel<0>, grid, dim3(256), 0,
+               (const float*)qk, qk_bias, (const float*)v, table, (float*)out, g);
   return MDE_OK;
 }
 
@@ -439,19 +581,24 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
-  const int nblk = (int)mde::cdiv(nwin, kGroup);
+  const int nblk = (int)mde::cdiv(nwin, kWinBwd);
   const int ntab = (2 * g.ws - 1) * (2 * g.ws - 1);
-  const double bytes = 4.0 * (double)b * h * w * c * 7.0;  // q k v dO (x2) read, dq dk dv written
-  MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel,
-             dim3((unsigned)nblk, (unsigned)heads), dim3(256), 0, (const float*)gout,
-             (const float*)qk, qk_bias, (const float*)v, table, (float*)gqk,
-             (float*)gv, (float*)workspace, (int)nwin, g);
+  const double bytes = 4.0 * (double)b * h * w * c * 7.0;  // q k v dO read, dq dk dv written
+  const dim3 grid((unsigned)nblk, (unsigned)mde::cdiv(heads, kHeads));
+  if (window == 7)
+    MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel<7>, grid, dim3(256), 0,
+               (const float*)gout, (const float*)qk, qk_bias, (const float*)v, table,
+               (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, g);
+  else
+    MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel<0>, grid, dim3(256), 0,
+               (const float*)gout, (const float*)qk, qk_bias, (const float*)v, table,
+               (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, g);
   // q half of d(qk bias) gets nothing from padded tokens (their dO is 0)
   MDE_LAUNCH(mde::K_WATTN_BWD, 0.0, s, zero_kernel, dim3((unsigned)mde::cdiv(c, 256)),
              dim3(256), 0, gqk_bias, (int)c);
   MDE_LAUNCH(mde::K_WATTN_BWD, 4.0 * nblk * heads * (ntab + D), s,
-             wattn_slab_reduce_kernel, dim3((unsigned)mde::cdiv(ntab + D, 256), (unsigned)heads),
-             dim3(256), 0, (const float*)workspace, nblk, (int)heads, ntab, (int)c,
+             wattn_slab_reduce_kernel, dim3((unsigned)mde::cdiv(ntab + D, 64), (unsigned)heads),
+             dim3(1024), 0, (const float*)workspace, nblk, (int)heads, ntab, (int)c,
              gtable, gqk_bias);
   return MDE_OK;
 }

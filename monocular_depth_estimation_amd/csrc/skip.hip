@@ -252,6 +252,117 @@ __global__ void __launch_bounds__(256)
     slab[(int64_t)blockIdx.x * NP + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
 }
 
+// MFMA backward for the full-size blocks (64 -> 32 at H/4, 32 -> 16 at H/2;
+// hw % 64 == 0).  Each wave walks 64-pixel tiles of one image:
+//   gs tile [CI x 64] = W^T [CI x CO] . G [CO x 64]    (K = CO, W^T held in
+//       registers as A operands; G read per lane as B, 16 lanes = 64 B rows)
+//   gW [CO x CI] += G [CO x 64] . S^T [64 x CI]       (K = pixels with a
+//       permuted order: lane group q supplies pixels 16q..16q+15, so A and B
+//       are 4 float4 loads of contiguous pixels per lane; S = r + d formed
+//       in registers)
+//   gb [CO] += row sums of G
+// v_mfma_f32_16x16x4_f32 throughout (exact f32 products).  The gW/gb
+// accumulators stay in registers for the whole launch and are combined over
+// the block's 4 waves in a fixed order into the block's slab row.
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int CI, int CO>
+__global__ void __launch_bounds__(256, 2)
+    skip_bwd_mfma_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                         const float* __restrict__ d, const float* __restrict__ wt,
+                         float* __restrict__ gs, float* __restrict__ slab, int64_t n,
+                         int64_t hw) {
+  constexpr int MT = CI / 16, OT = CO / 16, KO = CO / 4;
+  static_assert(CI % 16 == 0 && CO % 16 == 0, "tile shapes");
+  __shared__ float red[4][CO * CI + CO];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+  // A operands of gs = W^T G: lane (c = 16mt + l16, o = 4kk + q4) -> W[o][c]
+  float wa[MT][KO];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int kk = 0; kk < KO; ++kk) wa[mt][kk] = wt[(4 * kk + q4) * CI + 16 * mt + l16];
+  f4 gw[OT][MT];
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) gw[ot][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  float gbp[OT] = {};
+  const int64_t tpi = hw / 64;
+  const int64_t tiles = n * tpi;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
+    const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
+    const float* gp = g + nidx * CO * hw + p0;
+    const float* rp = r + nidx * CI * hw + p0;
+    const float* dp = d + nidx * CI * hw + p0;
+    float* sp = gs + nidx * CI * hw + p0;
+    // gs = W^T G, one 16-pixel column tile at a time
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float gb[KO];
+#pragma unroll
+      for (int kk = 0; kk < KO; ++kk) gb[kk] = gp[(4 * kk + q4) * hw + 16 * nt + l16];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < KO; ++kk) acc = mfma4(wa[mt][kk], gb[kk], acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sp[(16 * mt + 4 * q4 + i) * hw + 16 * nt + l16] = acc[i];
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // gW += G S^T over this tile's 64 pixels (lane group q4: pixels 16 q4 ..)
+    float ga[OT][16];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      const float4* src = reinterpret_cast<const float4*>(gp + (16 * ot + l16) * hw + 16 * q4);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float4 x = src[v];
+        ga[ot][4 * v] = x.x; ga[ot][4 * v + 1] = x.y; ga[ot][4 * v + 2] = x.z; ga[ot][4 * v + 3] = x.w;
+        gbp[ot] += (x.x + x.y) + (x.z + x.w);
+      }
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 16 * q4);
+      const float4* da = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4);
+      float sb[16];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const float4 x = ra[v], y = da[v];
+        sb[4 * v] = x.x + y.x; sb[4 * v + 1] = x.y + y.y;
+        sb[4 * v + 2] = x.z + y.z; sb[4 * v + 3] = x.w + y.w;
+      }
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) gw[ot][mt] = mfma4(ga[ot][k], sb[k], gw[ot][mt]);
+    }
+  }
+  // gW C layout: o = 16ot + 4 q4 + i, c = 16mt + l16; gb: sum over the 4 lane groups
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) red[w][(16 * ot + 4 * q4 + i) * CI + 16 * mt + l16] = gw[ot][mt][i];
+    float b = gbp[ot];
+    b += __shfl_xor(b, 16, 64);
+    b += __shfl_xor(b, 32, 64);
+    if (q4 == 0) red[w][CO * CI + 16 * ot + l16] = b;
+  }
+  __syncthreads();
+  float* out = slab + (int64_t)blockIdx.x * (CO * CI + CO);
+  for (int i = threadIdx.x; i < CO * CI + CO; i += 256)
+    out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
 // gw[pair] = sum over blocks of slab[block][pair]: one block per pair, fixed
 // per-thread order then a fixed tree -> deterministic.
 __global__ void __launch_bounds__(256)
@@ -352,6 +463,14 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
     MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1>), dim3(nb),
                dim3(256), 0, (const float*)gout, (const float*)r, (const float*)d,
                wt, (float*)gs, slab, n, hw);
+  } else if (cin == 64 && cout == 32 && hw % 64 == 0) {
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32>), dim3(nb), dim3(256),
+               0, (const float*)gout, (const float*)r, (const float*)d, wt, (float*)gs, slab,
+               n, hw);
+  } else if (cin == 32 && cout == 16 && hw % 64 == 0) {
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16>), dim3(nb), dim3(256),
+               0, (const float*)gout, (const float*)r, (const float*)d, wt, (float*)gs, slab,
+               n, hw);
   } else if (cin == 64 && cout == 32) {
     SKIP_BWD(64, 32, 4, 4, true);
   } else if (cin == 32 && cout == 16) {

@@ -363,6 +363,54 @@ __global__ void __launch_bounds__(256, 2)
     out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
+// MFMA forward for the full-size blocks (hw % 64 == 0): each wave computes a
+// [CO x 64] output tile = W [CO x CI] . S [CI x 64] (+ bias), S = r + d formed
+// per lane from two scalar loads (16 lanes read 64 contiguous bytes of a
+// channel row); W sits in registers as the A operands for the whole launch.
+template <int CI, int CO>
+__global__ void __launch_bounds__(256)
+    skip_fwd_mfma_kernel(const float* __restrict__ r, const float* __restrict__ d,
+                         const float* __restrict__ wt, const float* __restrict__ b,
+                         float* __restrict__ out, int64_t n, int64_t hw) {
+  constexpr int OT = CO / 16, KC = CI / 4;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+  float wa[OT][KC];  // W[o = 16ot + l16][c = 4kk + q4]
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int kk = 0; kk < KC; ++kk) wa[ot][kk] = wt[(16 * ot + l16) * CI + 4 * kk + q4];
+  float bo[OT][4];
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bo[ot][i] = b[16 * ot + 4 * q4 + i];
+  const int64_t tpi = hw / 64;
+  const int64_t tiles = n * tpi;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
+    const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
+    const float* rp = r + nidx * CI * hw + p0;
+    const float* dp = d + nidx * CI * hw + p0;
+    float* op = out + nidx * CO * hw + p0;
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      float sb[KC];
+#pragma unroll
+      for (int kk = 0; kk < KC; ++kk) {
+        const int64_t off = (int64_t)(4 * kk + q4) * hw + 16 * nt + l16;
+        sb[kk] = rp[off] + dp[off];
+      }
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot) {
+        f4 acc = {bo[ot][0], bo[ot][1], bo[ot][2], bo[ot][3]};
+#pragma unroll
+        for (int kk = 0; kk < KC; ++kk) acc = mfma4(wa[ot][kk], sb[kk], acc);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) op[(16 * ot + 4 * q4 + i) * hw + 16 * nt + l16] = acc[i];
+      }
+    }
+  }
+}
+
 // gw[pair] = sum over blocks of slab[block][pair]: one block per pair, fixed
 // per-thread order then a fixed tree -> deterministic.
 __global__ void __launch_bounds__(256)
@@ -417,7 +465,17 @@ int mde_skip_reduce_fwd(const void* r, const void* d, const float* wt,
   MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_kernel<CO_, PPT_>),        \
              grid(PPT_), dim3(256), 0, (const float*)r, (const float*)d, wt, \
              b, (float*)out, n, (int)cin, (int)cout, hw)
-  if (cout <= 1) {
+  auto mgrid = [&]() {
+    const int64_t blocks = mde::cdiv(n * hw / 64, 4);
+    return dim3((unsigned)(blocks > 4096 ? 4096 : blocks));
+  };
+  if (cin == 64 && cout == 32 && hw % 64 == 0) {
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32>), mgrid(), dim3(256), 0,
+               (const float*)r, (const float*)d, wt, b, (float*)out, n, hw);
+  } else if (cin == 32 && cout == 16 && hw % 64 == 0) {
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<32, 16>), mgrid(), dim3(256), 0,
+               (const float*)r, (const float*)d, wt, b, (float*)out, n, hw);
+  } else if (cout <= 1) {
     if (hw % 4 == 0) SKIP_FWD(1, 4); else SKIP_FWD(1, 1);
   } else if (cout <= 16) {
     if (hw % 4 == 0) SKIP_FWD(16, 4); else SKIP_FWD(16, 1);

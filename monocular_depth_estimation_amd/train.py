@@ -124,6 +124,142 @@ class Trainer:
             self.model.eval()
 
 
+class GraphTrainer:
+    """The same training step captured into HIP graphs and replayed.
+
+    The step (forward, DepthNorm + loss, backward, Adam) is a fixed sequence of
+    ~700 kernel launches on one stream; replaying it from a hipGraph removes
+    the per-launch host cost and the gaps between kernels.  Every call of
+    step() performs exactly one training step: the first `eager_steps` calls
+    run eagerly (MIOpen / hipBLASLt pick and compile their kernels, the
+    caching allocator settles), the next call captures and then replays.
+
+    Gradients live in ONE flat buffer (each parameter's .grad is a view), zeroed
+    inside the graph.  N == 1: a single graph (zero, forward, loss, backward,
+    fused capturable Adam).  N > 1: graph A (zero, forward, loss, backward,
+    grad /= N) -> one RCCL all-reduce of the flat gradient buffer -> graph B
+    (Adam); the BN running statistics (also one flat buffer) are broadcast from
+    rank 0 before each forward, as DDP's broadcast_buffers does.  Inputs are
+    copied into static device buffers.  CUDA only; BN stays in train mode (the
+    eval-mode quirk changes the graph, use Trainer for that).
+    """
+
+    def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2):
+        if world.device.type != "cuda":
+            raise RuntimeError("GraphTrainer needs a GPU (use Trainer on CPU)")
+        self.model, self.loss_fn, self.world = model, loss_fn, world
+        self.eager_steps = eager_steps
+        self.calls = 0
+        self.graphs = None
+        params = [p for p in model.parameters() if p.requires_grad]
+        total = sum(p.numel() for p in params)
+        self.flat_grad = torch.zeros(total, device=world.device)
+        off = 0
+        for p in params:
+            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
+            off += p.numel()
+        self.optimizer = torch.optim.Adam(params, lr, fused=True, capturable=True)
+        self.flat_bn = None
+        if world.size > 1:
+            bufs = [(m, name) for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)
+                    for name in ("running_mean", "running_var") if getattr(m, name) is not None]
+            n = sum(getattr(m, name).numel() for m, name in bufs)
+            self.flat_bn = torch.empty(n, device=world.device)
+            off = 0
+            for m, name in bufs:
+                b = getattr(m, name)
+                view = self.flat_bn[off:off + b.numel()].view_as(b)
+                view.copy_(b)
+                m._buffers[name] = view
+                off += b.numel()
+            for p in params:  # identical start on every rank (DDP does this at wrap time)
+                dist.broadcast(p.data, 0)
+            dist.broadcast(self.flat_bn, 0)
+        self.static_image = self.static_depth = None
+        self.stream = torch.cuda.Stream(device=world.device)  # eager warm-up + capture stream
+        self.last_loss = None
+        self.loss_sum = torch.zeros((), device=world.device)
+        self.loss_count = 0
+
+    def begin_epoch(self):
+        self.model.train()
+
+    def _forward_backward(self):
+        self.flat_grad.zero_()
+        loss = self.loss_fn(self.model(self.static_image), self.static_depth)
+        loss.backward()
+        if self.world.size > 1:
+            self.flat_grad.mul_(1.0 / self.world.size)
+        return loss.detach()
+
+    def _sync_buffers(self):
+        if self.world.size > 1:
+            dist.broadcast(self.flat_bn, 0)
+
+    def _allreduce(self):
+        if self.world.size > 1:
+            dist.all_reduce(self.flat_grad)
+
+    def step(self, image, depth):
+        if self.static_image is None:
+            self.static_image = torch.empty_like(image)
+            self.static_depth = torch.empty_like(depth)
+        self.static_image.copy_(image)
+        self.static_depth.copy_(depth)
+        self.calls += 1
+        self._sync_buffers()
+        if self.calls <= self.eager_steps:
+            cur = torch.cuda.current_stream()
+            self.stream.wait_stream(cur)
+            with torch.cuda.stream(self.stream):
+                loss = self._forward_backward()
+                self._allreduce()
+                self.optimizer.step()
+            cur.wait_stream(self.stream)
+        else:
+            if self.graphs is None:
+                self._capture()
+            ga, gb = self.graphs
+            ga.replay()
+            self._allreduce()
+            if gb is not None:
+                gb.replay()
+            loss = self.static_loss
+        self.last_loss = loss
+        self.loss_sum += loss
+        self.loss_count += 1
+        return loss
+
+    def eager_step(self, image, depth):
+        """One uncaptured step (the same kernels the graph replays), e.g. for
+        per-kernel HIP-event timing, which graph replay bypasses."""
+        self.static_image.copy_(image)
+        self.static_depth.copy_(depth)
+        self._sync_buffers()
+        loss = self._forward_backward()
+        self._allreduce()
+        self.optimizer.step()
+        self.last_loss = loss
+        return loss
+
+    def _capture(self):
+        torch.cuda.synchronize()
+        ga = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(ga, stream=self.stream):
+            self.static_loss = self._forward_backward()
+            if self.world.size == 1:
+                self.optimizer.step()
+        gb = None
+        if self.world.size > 1:
+            gb = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gb, stream=self.stream):
+                self.optimizer.step()
+        self.graphs = (ga, gb)
+
+    def after_step(self, loader_pos: int):
+        pass
+
+
 def make_adam(model, lr=1e-4):
     kw = {}
     if next(model.parameters()).is_cuda:

@@ -49,20 +49,27 @@ class World:
         return self.rank == 0
 
 
-def init_world(backend: str | None = None) -> World:
-    """Join the torchrun job (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), one GPU per process."""
+def init_world(backend: str | None = None, use_gpu: bool | None = None,
+               device_index: int | None = None) -> World:
+    """Join the torchrun job (RANK/LOCAL_RANK/WORLD_SIZE/MASTER_*), one GPU per process.
+
+    Defaults: RCCL ("nccl") on GPUs, gloo on CPU.  Tests may run gloo over GPU
+    tensors (use_gpu=True, several ranks on one device via device_index)."""
     size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    use_cuda = torch.cuda.is_available() and backend != "gloo"
-    device = torch.device("cuda", local) if use_cuda else torch.device("cpu")
+    if use_gpu is None:
+        use_gpu = backend != "gloo"
+    use_cuda = torch.cuda.is_available() and use_gpu
+    device = torch.device("cuda", local if device_index is None else device_index) \
+        if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(device)
     if size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend or ("nccl" if use_cuda else "gloo"),
-                                rank=rank, world_size=size,
-                                device_id=device if use_cuda else None)
+        be = backend or ("nccl" if use_cuda else "gloo")
+        dist.init_process_group(be, rank=rank, world_size=size,
+                                device_id=device if (use_cuda and be == "nccl") else None)
     return World(rank, local, size, device)
 
 

@@ -138,17 +138,20 @@ class GraphTrainer:
     ~700 kernel launches on one stream; replaying it from a hipGraph removes
     the per-launch host cost and the gaps between kernels.  Every call of
     step() performs exactly one training step: the first `eager_steps` calls
-    run eagerly (MIOpen / hipBLASLt pick and compile their kernels, the
-    caching allocator settles), the next call captures and then replays.
+    run eagerly on a side stream (MIOpen / hipBLASLt pick and compile their
+    kernels, the caching allocator settles), the next call captures and then
+    replays.
 
-    Gradients live in ONE flat buffer (each parameter's .grad is a view), zeroed
-    inside the graph.  N == 1: a single graph (zero, forward, loss, backward,
-    fused capturable Adam).  N > 1: graph A (zero, forward, loss, backward,
-    grad /= N) -> one RCCL all-reduce of the flat gradient buffer -> graph B
-    (Adam); the BN running statistics (also one flat buffer) are broadcast from
-    rank 0 before each forward, as DDP's broadcast_buffers does.  Inputs are
-    copied into static device buffers.  CUDA only; BN stays in train mode (the
-    eval-mode quirk changes the graph, use Trainer for that).
+    Gradients are allocated by the captured backward itself (grads set to None
+    before capture, so autograd hands its result buffers to .grad without a
+    copy; replays reuse those static buffers).  N == 1: one graph (forward,
+    loss, backward, fused capturable Adam).  N > 1: graph A (forward, loss,
+    backward, gradients packed into one flat buffer scaled by 1/N) -> one RCCL
+    all-reduce of that buffer -> graph B (unpack, Adam); the BN running
+    statistics (one flat buffer) are broadcast from rank 0 before each
+    forward, as DDP's broadcast_buffers does.  Inputs are copied into static
+    device buffers.  CUDA only; BN stays in train mode (the eval-mode quirk
+    changes the graph, use Trainer for that).
     """
 
     def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2):
@@ -158,14 +161,9 @@ class GraphTrainer:
         self.eager_steps = eager_steps
         self.calls = 0
         self.graphs = None
-        params = [p for p in model.parameters() if p.requires_grad]
-        total = sum(p.numel() for p in params)
-        self.flat_grad = torch.zeros(total, device=world.device)
-        off = 0
-        for p in params:
-            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += p.numel()
-        self.optimizer = torch.optim.Adam(params, lr, fused=True, capturable=True)
+        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.optimizer = torch.optim.Adam(self.params, lr, fused=True, capturable=True)
+        self.flat_grad = None
         self.flat_bn = None
         if world.size > 1:
             bufs = [(m, name) for m in model.modules() if isinstance(m, torch.nn.BatchNorm2d)
@@ -179,7 +177,7 @@ class GraphTrainer:
                 view.copy_(b)
                 m._buffers[name] = view
                 off += b.numel()
-            for p in params:  # identical start on every rank (DDP does this at wrap time)
+            for p in self.params:  # identical start on every rank (DDP does this at wrap time)
                 dist.broadcast(p.data, 0)
             dist.broadcast(self.flat_bn, 0)
         self.static_image = self.static_depth = None
@@ -191,13 +189,24 @@ class GraphTrainer:
     def begin_epoch(self):
         self.model.train()
 
+    # -- the step's pieces (each runs eagerly or inside a capture) ----------
     def _forward_backward(self):
-        self.flat_grad.zero_()
         loss = self.loss_fn(self.model(self.static_image), self.static_depth)
         loss.backward()
         if self.world.size > 1:
+            grads = [p.grad for p in self.params if p.grad is not None]
+            if self.flat_grad is None:
+                self.flat_grad = torch.empty(sum(g.numel() for g in grads),
+                                             device=self.world.device)
+            torch.cat([g.reshape(-1) for g in grads], out=self.flat_grad)
             self.flat_grad.mul_(1.0 / self.world.size)
         return loss.detach()
+
+    def _unpack_and_update(self):
+        if self.world.size > 1:
+            grads = [p.grad for p in self.params if p.grad is not None]
+            torch._foreach_copy_(grads, list(self.flat_grad.split([g.numel() for g in grads])))
+        self.optimizer.step()
 
     def _sync_buffers(self):
         if self.world.size > 1:
@@ -206,6 +215,13 @@ class GraphTrainer:
     def _allreduce(self):
         if self.world.size > 1:
             dist.all_reduce(self.flat_grad)
+
+    def _eager(self):
+        self.optimizer.zero_grad(set_to_none=True)
+        loss = self._forward_backward()
+        self._allreduce()
+        self._unpack_and_update()
+        return loss
 
     def step(self, image, depth):
         if self.static_image is None:
@@ -219,17 +235,15 @@ class GraphTrainer:
             cur = torch.cuda.current_stream()
             self.stream.wait_stream(cur)
             with torch.cuda.stream(self.stream):
-                loss = self._forward_backward()
-                self._allreduce()
-                self.optimizer.step()
+                loss = self._eager()
             cur.wait_stream(self.stream)
         else:
             if self.graphs is None:
                 self._capture()
             ga, gb = self.graphs
             ga.replay()
-            self._allreduce()
             if gb is not None:
+                self._allreduce()
                 gb.replay()
             loss = self.static_loss
         self.last_loss = loss
@@ -239,18 +253,18 @@ class GraphTrainer:
 
     def eager_step(self, image, depth):
         """One uncaptured step (the same kernels the graph replays), e.g. for
-        per-kernel HIP-event timing, which graph replay bypasses."""
+        per-kernel HIP-event timing, which graph replay bypasses.  Only valid
+        before capture or for measurement: it re-allocates the gradients."""
         self.static_image.copy_(image)
         self.static_depth.copy_(depth)
         self._sync_buffers()
-        loss = self._forward_backward()
-        self._allreduce()
-        self.optimizer.step()
+        loss = self._eager()
         self.last_loss = loss
         return loss
 
     def _capture(self):
         torch.cuda.synchronize()
+        self.optimizer.zero_grad(set_to_none=True)  # backward allocates .grad in the graph pool
         ga = torch.cuda.CUDAGraph()
         with torch.cuda.graph(ga, stream=self.stream):
             self.static_loss = self._forward_backward()
@@ -260,7 +274,7 @@ class GraphTrainer:
         if self.world.size > 1:
             gb = torch.cuda.CUDAGraph()
             with torch.cuda.graph(gb, stream=self.stream):
-                self.optimizer.step()
+                self._unpack_and_update()
         self.graphs = (ga, gb)
 
     def after_step(self, loader_pos: int):

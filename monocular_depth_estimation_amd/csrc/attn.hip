@@ -146,12 +146,11 @@ __device__ __forceinline__ void probs_t(const Geo& g, const float* __restrict__ 
 #pragma unroll
       for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
 #pragma unroll
-      for (int jt = 0; jt < 4; ++jt) {
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int jt = 0; jt < 4; ++jt) s[jt][it] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int k = 0; k < 8; ++k) acc = mfma4(ka[jt][k], qb[k], acc);
-        s[jt][it] = acc;
-      }
+      for (int k = 0; k < 8; ++k)  // 4 independent accumulators in flight
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) s[jt][it] = mfma4(ka[jt][k], qb[k], s[jt][it]);
     }
   }
   // this lane's 16 keys: table offset -(yj*span + xj) and region label, packed
@@ -371,11 +370,11 @@ __global__ void __launch_bounds__(256, 2)
           row8(grow, c, hd + 8 * g4, tok[16 * it + l16], nullptr, db);
           f4 dp[4];
 #pragma unroll
-          for (int jt = 0; jt < 4; ++jt) {
-            dp[jt] = f4{0.f, 0.f, 0.f, 0.f};
+          for (int jt = 0; jt < 4; ++jt) dp[jt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int k = 0; k < 8; ++k) dp[jt] = mfma4(va[jt][k], db[k], dp[jt]);
-          }
+          for (int k = 0; k < 8; ++k)
+#pragma unroll
+            for (int jt = 0; jt < 4; ++jt) dp[jt] = mfma4(va[jt][k], db[k], dp[jt]);
           float dl = 0.f;
 #pragma unroll
           for (int jt = 0; jt < 4; ++jt)

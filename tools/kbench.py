@@ -35,7 +35,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default="")
+    ap.add_argument("--only", default="", help="comma list of groups: resize,se,skip,bn,loss,attn,dw,ln")
     a = ap.parse_args()
+    groups = set(a.only.split(",")) if a.only else None
+
+    def want(g):
+        return groups is None or g in groups
     from monocular_depth_estimation_amd import _abi
     from monocular_depth_estimation_amd import functional as F
     from monocular_depth_estimation_amd.nn import BatchNorm2d
@@ -49,7 +54,7 @@ def main():
 
     n = 32
     # bilinear x2 (decoder) and DDRNet resizes
-    for c, h, w in ((64, 60, 80), (32, 120, 160), (16, 240, 320)):
+    for c, h, w in ((64, 60, 80), (32, 120, 160), (16, 240, 320)) if want("resize") else ():
         x = torch.rand(n, c, h, w, device=dev)
         y = F.bilinear_resize(x, scale_factor=2)
         gy = torch.rand_like(y)
@@ -59,12 +64,13 @@ def main():
         report(f"bilinear_bwd x2 {c}x{h}x{w}", timeit(lambda: _abi.call(
             "mde_bilinear_bwd", gy.data_ptr(), x.data_ptr(), n, c, h, w, ho, wo, 0.5, 0.5, 0, 0,
             _abi.stream_of(x)), a.reps), nb)
-    for c, hi, wi in ((64, 15, 20), (128, 8, 10)):
+    for c, hi, wi in ((64, 15, 20), (128, 8, 10)) if want("resize") else ():
         x = torch.rand(n, c, hi, wi, device=dev)
         nb = 4.0 * n * c * (hi * wi + 60 * 80)
         report(f"bilinear_fwd {c}x{hi}x{wi}->60x80", timeit(lambda: F.bilinear_resize(x, size=(60, 80)), a.reps), nb)
     # SE + cat and skip fusion at the three decoder resolutions
-    for c, h, w, cout in ((64, 120, 160, 32), (32, 240, 320, 16), (16, 480, 640, 1)):
+    for c, h, w, cout in ((64, 120, 160, 32), (32, 240, 320, 16), (16, 480, 640, 1)) \
+            if (want("se") or want("skip")) else ():
         half = c // 2
         xa = torch.rand(n, half, h, w, device=dev)
         xb = torch.rand(n, half, h, w, device=dev)
@@ -93,7 +99,7 @@ def main():
                timeit(lambda: torch.autograd.grad(o, (r, wt), go, retain_graph=True), a.reps),
                pix * (3 * c + cout))
     # BatchNorm(+ReLU) at representative shapes
-    for c, h, w in ((16, 480, 640), (32, 240, 320), (64, 120, 160), (256, 15, 20)):
+    for c, h, w in ((16, 480, 640), (32, 240, 320), (64, 120, 160), (256, 15, 20)) if want("bn") else ():
         x = torch.rand(n, c, h, w, device=dev, requires_grad=True)
         bn = BatchNorm2d(c, act="relu").to(dev).train()
         big = 4.0 * n * c * h * w
@@ -105,12 +111,60 @@ def main():
         ref = torch.nn.BatchNorm2d(c).to(dev).train()
         report(f"  (MIOpen BN fwd {c}x{h}x{w})", timeit(lambda: ref(x), a.reps), 3 * big)
     # loss
-    p = torch.rand(n, 1, 480, 640, device=dev, requires_grad=True)
-    t = torch.rand(n, 1, 480, 640, device=dev) * 10
-    mm = F.minmax(t)
-    report("ssim3_l1 fwd+grad 480x640", timeit(lambda: F.ssim3_l1(p, t, 1.0, 0.1, target_minmax=mm), a.reps),
-           3 * 4.0 * n * 480 * 640)
-    report("minmax 480x640", timeit(lambda: F.minmax(t), a.reps), 4.0 * n * 480 * 640)
+    if want("loss"):
+        p = torch.rand(n, 1, 480, 640, device=dev, requires_grad=True)
+        t = torch.rand(n, 1, 480, 640, device=dev) * 10
+        mm = F.minmax(t)
+        report("ssim3_l1 fwd+grad 480x640", timeit(lambda: F.ssim3_l1(p, t, 1.0, 0.1, target_minmax=mm),
+                                                   a.reps), 3 * 4.0 * n * 480 * 640)
+        report("minmax 480x640", timeit(lambda: F.minmax(t), a.reps), 4.0 * n * 480 * 640)
+    # --- cfg4 (PTModel, bs 16) ops
+    n4 = 16
+    if want("attn"):
+        from monocular_depth_estimation_amd.newcrf_layers import window_attention
+        for c, heads, h, w in ((128, 4, 120, 160), (256, 8, 60, 80), (512, 16, 30, 40), (1024, 32, 15, 20)):
+            qk = torch.randn(n4, h * w, 2 * c, device=dev, requires_grad=True)
+            qkb = torch.randn(2 * c, device=dev, requires_grad=True)
+            v = torch.randn(n4, h, w, c, device=dev, requires_grad=True)
+            tab = torch.randn(169, heads, device=dev, requires_grad=True)
+            tok = 4.0 * n4 * h * w * c
+            for shift in (0, 3):
+                report(f"window_attn fwd C{c} {h}x{w} s{shift}",
+                       timeit(lambda: window_attention(qk, qkb, v, tab, h, w, heads, 7, shift), a.reps),
+                       4 * tok)
+                o = window_attention(qk, qkb, v, tab, h, w, heads, 7, shift)
+                go = torch.randn_like(o)
+                report(f"window_attn bwd C{c} {h}x{w} s{shift}",
+                       timeit(lambda: torch.autograd.grad(o, (qk, v, tab, qkb), go, retain_graph=True),
+                              a.reps), 7 * tok)
+    if want("dw"):
+        from monocular_depth_estimation_amd.nn import depthwise_conv2d
+        for c, h, w, k, st in ((16, 240, 320, 3, 1), (64, 240, 320, 3, 2), (72, 120, 160, 5, 2),
+                               (120, 60, 80, 5, 1), (240, 60, 80, 3, 2), (672, 30, 40, 5, 2),
+                               (960, 15, 20, 5, 1)):
+            conv = torch.nn.Conv2d(c, c, k, st, k // 2, groups=c, bias=False).to(dev)
+            x = torch.randn(n4, c, h, w, device=dev, requires_grad=True)
+            y = depthwise_conv2d(x, conv)
+            gy = torch.randn_like(y)
+            nb = 4.0 * (x.numel() + y.numel())
+            report(f"dwconv fwd {c}x{h}x{w} k{k}s{st}", timeit(lambda: depthwise_conv2d(x, conv), a.reps), nb)
+            report(f"dwconv bwd {c}x{h}x{w} k{k}s{st}",
+                   timeit(lambda: torch.autograd.grad(y, (x, conv.weight), gy, retain_graph=True),
+                          a.reps), 2 * nb)
+    if want("ln"):
+        from monocular_depth_estimation_amd.newcrf_layers import LayerNorm, nchw_to_tokens
+        for c, h, w in ((128, 120, 160), (256, 60, 80), (512, 30, 40), (1024, 15, 20)):
+            ln = LayerNorm(c).to(dev)
+            x = torch.randn(n4, h * w, c, device=dev, requires_grad=True)
+            y = ln(x)
+            gy = torch.randn_like(y)
+            nb = 4.0 * x.numel()
+            report(f"layernorm fwd {c} {h}x{w}", timeit(lambda: ln(x), a.reps), 2 * nb)
+            report(f"layernorm bwd {c} {h}x{w}",
+                   timeit(lambda: torch.autograd.grad(y, (x, ln.weight), gy, retain_graph=True), a.reps),
+                   3 * nb)
+            xn = torch.randn(n4, c, h, w, device=dev)
+            report(f"transpose nchw->tokens {c} {h}x{w}", timeit(lambda: nchw_to_tokens(xn), a.reps), 2 * nb)
     if a.json:
         json.dump(rows, open(a.json, "w"), indent=1)
 

@@ -22,9 +22,10 @@ namespace {
 
 constexpr int64_t kMaxBlocksBwd = 1024;
 
-// backward blocks: at most 1024, each owning a contiguous range of >= 64 rows
+// backward blocks: about 1024, each owning a contiguous range of >= 4 rows
+// (one per wave), so small token counts still fill the chip
 int64_t bwd_blocks(int64_t rows) {
-  const int64_t b = cdiv(rows, 64);
+  const int64_t b = cdiv(rows, 4);
   return b < kMaxBlocksBwd ? b : kMaxBlocksBwd;
 }
 

@@ -205,7 +205,8 @@ class GraphTrainer:
     def _unpack_and_update(self):
         if self.world.size > 1:
             grads = [p.grad for p in self.params if p.grad is not None]
-            torch._foreach_copy_(grads, list(self.flat_grad.split([g.numel() for g in grads])))
+            flat = self.flat_grad.split([g.numel() for g in grads])
+            torch._foreach_copy_(grads, [f.view_as(g) for f, g in zip(flat, grads)])
         self.optimizer.step()
 
     def _sync_buffers(self):

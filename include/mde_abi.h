@@ -263,6 +263,23 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
                         int64_t shift, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Bias-free 1x1 convolution, NCHW: y[n,o,p] = sum_c W[o,c] x[n,c,p].  The
+ * guided-upsampling blocks' 1x1 convs (`nn.Conv2d(E, E/2, 1)`, `(E, in, 1)`,
+ * src/GuideDepth/model/modules.py:43-74) whose bias is folded into the
+ * following BatchNorm.  Supported (cin, cout): (16,8) (16,16) (16,32) (32,16)
+ * (32,32) (32,64) (64,32) (64,64) with h*w % 64 == 0 (query with
+ * mde_pointwise_supported); others return MDE_ERR_UNSUPPORTED.
+ * Backward: gx (nullable) = W^T gy; gw [cout,cin] overwritten.
+ * ------------------------------------------------------------------------- */
+int mde_pointwise_supported(int64_t cin, int64_t cout, int64_t h, int64_t w);
+size_t mde_pointwise_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_pointwise_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
+int mde_pointwise_bwd(const void* gy, const void* x, const float* weight, void* gx,
+                      float* gweight, int64_t n, int64_t cin, int64_t cout, int64_t h,
+                      int64_t w, void* workspace, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Depthwise convolution (groups == channels, square k = 3 or 5, stride 1 or
  * 2, zero padding `pad`, dilation 1, no bias), NCHW.  Replaces the
  * depthwise Conv2d of every MobileNetV3-Large inverted-residual block

@@ -68,6 +68,11 @@ SIGNATURES = {
                                _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_se_gate_bwd": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_pointwise_supported": (_int, [_i64, _i64, _i64, _i64]),
+    "mde_pointwise_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_pointwise_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_pointwise_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _int,
+                                 _vp]),
     "mde_dwconv_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64, _i64]),
     "mde_dwconv_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_dwconv_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,

@@ -50,6 +50,8 @@ enum Kid : int {
   K_LN_BWD,
   K_LN_WREDUCE,
   K_TRANSPOSE,
+  K_PW_FWD,
+  K_PW_BWD,
   K_COUNT
 };
 

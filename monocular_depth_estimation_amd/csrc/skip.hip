@@ -270,14 +270,16 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int CI, int CO>
+template <int CI, int CO, bool HAS_D>
 __global__ void __launch_bounds__(256, 2)
     skip_bwd_mfma_kernel(const float* __restrict__ g, const float* __restrict__ r,
                          const float* __restrict__ d, const float* __restrict__ wt,
                          float* __restrict__ gs, float* __restrict__ slab, int64_t n,
                          int64_t hw) {
-  constexpr int MT = CI / 16, OT = CO / 16, KO = CO / 4;
-  static_assert(CI % 16 == 0 && CO % 16 == 0, "tile shapes");
+  // CO may be 8: the M tiles of gW = G S^T are then half-empty (rows >= CO
+  // are zero operands and are not stored); K of gs = W^T G is CO in steps of 4.
+  constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = CO / 4;
+  static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   __shared__ float red[4][CO * CI + CO];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
   // A operands of gs = W^T G: lane (c = 16mt + l16, o = 4kk + q4) -> W[o][c]
@@ -298,21 +300,23 @@ __global__ void __launch_bounds__(256, 2)
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
     const float* gp = g + nidx * CO * hw + p0;
     const float* rp = r + nidx * CI * hw + p0;
-    const float* dp = d + nidx * CI * hw + p0;
-    float* sp = gs + nidx * CI * hw + p0;
+    const float* dp = HAS_D ? d + nidx * CI * hw + p0 : nullptr;
+    float* sp = gs ? gs + nidx * CI * hw + p0 : nullptr;
     // gs = W^T G, one 16-pixel column tile at a time
+    if (sp) {
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      float gb[KO];
+      for (int nt = 0; nt < 4; ++nt) {
+        float gb[KO];
 #pragma unroll
-      for (int kk = 0; kk < KO; ++kk) gb[kk] = gp[(4 * kk + q4) * hw + 16 * nt + l16];
+        for (int kk = 0; kk < KO; ++kk) gb[kk] = gp[(4 * kk + q4) * hw + 16 * nt + l16];
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        f4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int mt = 0; mt < MT; ++mt) {
+          f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int kk = 0; kk < KO; ++kk) acc = mfma4(wa[mt][kk], gb[kk], acc);
+          for (int kk = 0; kk < KO; ++kk) acc = mfma4(wa[mt][kk], gb[kk], acc);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sp[(16 * mt + 4 * q4 + i) * hw + 16 * nt + l16] = acc[i];
+          for (int i = 0; i < 4; ++i) sp[(16 * mt + 4 * q4 + i) * hw + 16 * nt + l16] = acc[i];
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -320,24 +324,32 @@ __global__ void __launch_bounds__(256, 2)
     float ga[OT][16];
 #pragma unroll
     for (int ot = 0; ot < OT; ++ot) {
-      const float4* src = reinterpret_cast<const float4*>(gp + (16 * ot + l16) * hw + 16 * q4);
+      const int o = 16 * ot + l16;
+      if (o < CO) {
+        const float4* src = reinterpret_cast<const float4*>(gp + o * hw + 16 * q4);
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const float4 x = src[v];
-        ga[ot][4 * v] = x.x; ga[ot][4 * v + 1] = x.y; ga[ot][4 * v + 2] = x.z; ga[ot][4 * v + 3] = x.w;
-        gbp[ot] += (x.x + x.y) + (x.z + x.w);
+        for (int v = 0; v < 4; ++v) {
+          const float4 x = src[v];
+          ga[ot][4 * v] = x.x; ga[ot][4 * v + 1] = x.y; ga[ot][4 * v + 2] = x.z; ga[ot][4 * v + 3] = x.w;
+          gbp[ot] += (x.x + x.y) + (x.z + x.w);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ga[ot][k] = 0.f;
       }
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 16 * q4);
-      const float4* da = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4);
       float sb[16];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        const float4 x = ra[v], y = da[v];
-        sb[4 * v] = x.x + y.x; sb[4 * v + 1] = x.y + y.y;
-        sb[4 * v + 2] = x.z + y.z; sb[4 * v + 3] = x.w + y.w;
+        float4 x = ra[v];
+        if (HAS_D) {
+          const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4)[v];
+          x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+        }
+        sb[4 * v] = x.x; sb[4 * v + 1] = x.y; sb[4 * v + 2] = x.z; sb[4 * v + 3] = x.w;
       }
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot)
@@ -351,11 +363,14 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[w][(16 * ot + 4 * q4 + i) * CI + 16 * mt + l16] = gw[ot][mt][i];
+      for (int i = 0; i < 4; ++i) {
+        const int o = 16 * ot + 4 * q4 + i;
+        if (o < CO) red[w][o * CI + 16 * mt + l16] = gw[ot][mt][i];
+      }
     float b = gbp[ot];
     b += __shfl_xor(b, 16, 64);
     b += __shfl_xor(b, 32, 64);
-    if (q4 == 0) red[w][CO * CI + 16 * ot + l16] = b;
+    if (q4 == 0 && 16 * ot + l16 < CO) red[w][CO * CI + 16 * ot + l16] = b;
   }
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * (CO * CI + CO);
@@ -367,29 +382,36 @@ __global__ void __launch_bounds__(256, 2)
 // [CO x 64] output tile = W [CO x CI] . S [CI x 64] (+ bias), S = r + d formed
 // per lane from two scalar loads (16 lanes read 64 contiguous bytes of a
 // channel row); W sits in registers as the A operands for the whole launch.
-template <int CI, int CO>
+template <int CI, int CO, bool HAS_D>
 __global__ void __launch_bounds__(256)
     skip_fwd_mfma_kernel(const float* __restrict__ r, const float* __restrict__ d,
                          const float* __restrict__ wt, const float* __restrict__ b,
                          float* __restrict__ out, int64_t n, int64_t hw) {
-  constexpr int OT = CO / 16, KC = CI / 4;
+  constexpr int OT = (CO + 15) / 16, KC = CI / 4;
+  static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
-  float wa[OT][KC];  // W[o = 16ot + l16][c = 4kk + q4]
+  float wa[OT][KC];  // W[o = 16ot + l16][c = 4kk + q4] (0 for o >= CO)
 #pragma unroll
   for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
-    for (int kk = 0; kk < KC; ++kk) wa[ot][kk] = wt[(16 * ot + l16) * CI + 4 * kk + q4];
+    for (int kk = 0; kk < KC; ++kk) {
+      const int o = 16 * ot + l16;
+      wa[ot][kk] = o < CO ? wt[o * CI + 4 * kk + q4] : 0.f;
+    }
   float bo[OT][4];
 #pragma unroll
   for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bo[ot][i] = b[16 * ot + 4 * q4 + i];
+    for (int i = 0; i < 4; ++i) {
+      const int o = 16 * ot + 4 * q4 + i;
+      bo[ot][i] = (b && o < CO) ? b[o] : 0.f;
+    }
   const int64_t tpi = hw / 64;
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
     const float* rp = r + nidx * CI * hw + p0;
-    const float* dp = d + nidx * CI * hw + p0;
+    const float* dp = HAS_D ? d + nidx * CI * hw + p0 : nullptr;
     float* op = out + nidx * CO * hw + p0;
 #pragma unroll
     for (int nt = 0; nt < 4; ++nt) {
@@ -397,7 +419,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int kk = 0; kk < KC; ++kk) {
         const int64_t off = (int64_t)(4 * kk + q4) * hw + 16 * nt + l16;
-        sb[kk] = rp[off] + dp[off];
+        sb[kk] = HAS_D ? rp[off] + dp[off] : rp[off];
       }
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot) {
@@ -405,7 +427,10 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int kk = 0; kk < KC; ++kk) acc = mfma4(wa[ot][kk], sb[kk], acc);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) op[(16 * ot + 4 * q4 + i) * hw + 16 * nt + l16] = acc[i];
+        for (int i = 0; i < 4; ++i) {
+          const int o = 16 * ot + 4 * q4 + i;
+          if (o < CO) op[o * hw + 16 * nt + l16] = acc[i];
+        }
       }
     }
   }
@@ -426,7 +451,7 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) {
     if (t < npairs)
       gw[t] = a;
-    else
+    else if (gb)
       gb[t - npairs] = a;
   }
 }
@@ -470,10 +495,10 @@ int mde_skip_reduce_fwd(const void* r, const void* d, const float* wt,
     return dim3((unsigned)(blocks > 4096 ? 4096 : blocks));
   };
   if (cin == 64 && cout == 32 && hw % 64 == 0) {
-    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32>), mgrid(), dim3(256), 0,
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32, true>), mgrid(), dim3(256), 0,
                (const float*)r, (const float*)d, wt, b, (float*)out, n, hw);
   } else if (cin == 32 && cout == 16 && hw % 64 == 0) {
-    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<32, 16>), mgrid(), dim3(256), 0,
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<32, 16, true>), mgrid(), dim3(256), 0,
                (const float*)r, (const float*)d, wt, b, (float*)out, n, hw);
   } else if (cout <= 1) {
     if (hw % 4 == 0) SKIP_FWD(1, 4); else SKIP_FWD(1, 1);
@@ -522,11 +547,11 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
                dim3(256), 0, (const float*)gout, (const float*)r, (const float*)d,
                wt, (float*)gs, slab, n, hw);
   } else if (cin == 64 && cout == 32 && hw % 64 == 0) {
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32>), dim3(nb), dim3(256),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32, true>), dim3(nb), dim3(256),
                0, (const float*)gout, (const float*)r, (const float*)d, wt, (float*)gs, slab,
                n, hw);
   } else if (cin == 32 && cout == 16 && hw % 64 == 0) {
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16>), dim3(nb), dim3(256),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true>), dim3(nb), dim3(256),
                0, (const float*)gout, (const float*)r, (const float*)d, wt, (float*)gs, slab,
                n, hw);
   } else if (cin == 64 && cout == 32) {
@@ -545,6 +570,76 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
   MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s,
              skip_slab_reduce_kernel, dim3((unsigned)stride), dim3(256), 0, slab,
              nb, (int)(cin * cout), (int)cout, gw, gb);
+  return MDE_OK;
+}
+
+
+// ---------------------------------------------------------------- pointwise
+// Bias-free 1x1 convolution (the conv feeding a BatchNorm whose bias is
+// folded), the MFMA kernels above with one input.
+#define MDE_PW_SHAPES(X) \
+  X(16, 8) X(16, 16) X(32, 16) X(32, 32) X(64, 32) X(64, 64) X(32, 64) X(16, 32)
+
+static bool pw_ok(int64_t n, int64_t cin, int64_t cout, int64_t hw) {
+  if (n <= 0 || hw <= 0 || hw % 64 != 0) return false;
+#define MDE_PW_MATCH(A, B) if (cin == A && cout == B) return true;
+  MDE_PW_SHAPES(MDE_PW_MATCH)
+#undef MDE_PW_MATCH
+  return false;
+}
+
+int mde_pointwise_supported(int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  return pw_ok(1, cin, cout, h * w) ? 1 : 0;
+}
+
+size_t mde_pointwise_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  return mde_skip_reduce_workspace(n, cin, cout, h, w);
+}
+
+int mde_pointwise_fwd(const void* x, const float* wt, void* y, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!x || !wt || !y) return MDE_ERR_INVALID_ARG;
+  if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const double bytes = 4.0 * n * hw * (double)(cin + cout);
+  const int64_t blocks = mde::cdiv(n * hw / 64, 4);
+  const dim3 grid((unsigned)(blocks > 4096 ? 4096 : blocks));
+#define MDE_PW_FWD(A, B)                                                                    \
+  if (cin == A && cout == B) {                                                              \
+    MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false>), grid, dim3(256), \
+               0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw);                 \
+    return MDE_OK;                                                                          \
+  }
+  MDE_PW_SHAPES(MDE_PW_FWD)
+#undef MDE_PW_FWD
+  return MDE_ERR_UNSUPPORTED;
+}
+
+int mde_pointwise_bwd(const void* gy, const void* x, const float* wt, void* gx, float* gw,
+                      int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                      void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!gy || !x || !wt || !gw || !workspace) return MDE_ERR_INVALID_ARG;
+  if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = bwd_blocks(n, hw);
+  float* slab = (float*)workspace;
+  const double bytes = 4.0 * n * hw * (double)(cout + cin + (gx ? cin : 0));
+#define MDE_PW_BWD(A, B)                                                                     \
+  if (cin == A && cout == B) {                                                               \
+    MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false>), dim3(nb),       \
+               dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt, (float*)gx, slab, \
+               n, hw);                                                                       \
+  }
+  MDE_PW_SHAPES(MDE_PW_BWD)
+#undef MDE_PW_BWD
+  const int stride = (int)(cin * cout + cout);
+  MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+             dim3((unsigned)(cin * cout)), dim3(256), 0, slab, nb, (int)(cin * cout), (int)cout,
+             gw, (float*)nullptr);
   return MDE_OK;
 }
 

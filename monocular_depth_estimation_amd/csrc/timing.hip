@@ -18,7 +18,8 @@ const char* const kNames[mde::K_COUNT] = {
     "bn_bwd_reduce",  "bn_bwd_final",  "bn_bwd_apply",  "bn_fwd_apply_small",
     "bn_bwd_apply_small", "window_attn_fwd", "window_attn_bwd",
     "dwconv_fwd",    "dwconv_bwd_data", "dwconv_bwd_weight", "dwconv_wreduce",
-    "layernorm_fwd", "layernorm_bwd",   "layernorm_wreduce", "transpose"};
+    "layernorm_fwd", "layernorm_bwd",   "layernorm_wreduce", "transpose",
+    "pointwise_fwd", "pointwise_bwd"};
 
 struct Pending {
   int kid;

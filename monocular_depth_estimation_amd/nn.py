@@ -90,10 +90,55 @@ def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, preb
         training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, _ACTS[act])
 
 
+class _Pointwise(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight):
+        x = x.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        w2 = weight.reshape(cout, cin).contiguous()
+        y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
+        _abi.call("mde_pointwise_fwd", _abi.ptr(x), _abi.ptr(w2), _abi.ptr(y), n, cin, cout, h, w,
+                  _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.save_for_backward(x, w2)
+        ctx.wshape = weight.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w2 = ctx.saved_tensors
+        gy = gy.contiguous()
+        n, cin, h, w = x.shape
+        cout = w2.shape[0]
+        gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        gw = torch.empty_like(w2)
+        ws = _ws(_abi.query("mde_pointwise_workspace", n, cin, cout, h, w), x)
+        _abi.call("mde_pointwise_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(w2), _abi.ptr(gx),
+                  _abi.ptr(gw), n, cin, cout, h, w, _abi.ptr(ws), _abi.dtype_code(gy),
+                  _abi.stream_of(gy))
+        return gx, gw.view(ctx.wshape)
+
+
+def pointwise_ok(conv: nn.Conv2d, x) -> bool:
+    """Whether this bias-folded 1x1 conv runs on the HIP pointwise kernel."""
+    if (conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.padding != (0, 0)
+            or conv.dilation != (1, 1) or conv.groups != 1 or x.dim() != 4):
+        return False
+    return bool(_abi.query("mde_pointwise_supported", conv.in_channels, conv.out_channels,
+                           x.shape[2], x.shape[3]))
+
+
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
-    """bn(conv(x)) with the conv bias folded into the BN kernel."""
-    y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
-                                   conv.dilation, conv.groups)
+    """bn(conv(x)) with the conv bias folded into the BN kernel.
+
+    Small-channel 1x1 convs run on the HIP MFMA pointwise kernel, the rest on
+    MIOpen (PyTorch-ROCm)."""
+    if pointwise_ok(conv, x):
+        _gpu(x)
+        y = _Pointwise.apply(x, conv.weight)
+    else:
+        y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
+                                       conv.dilation, conv.groups)
     return batch_norm_act(y, bn, bn.act, residual, conv.bias)
 
 

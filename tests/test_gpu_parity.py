@@ -343,3 +343,24 @@ def test_guidedepth_cfg2_shape_runs_and_matches_oracle_encoder_free_parts():
     with torch.no_grad():
         rp = ref(x)
     close_map(pred, rp, 1e-3, "640x480 depth map")
+
+
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 16, 8, 48, 64), (3, 16, 16, 8, 8), (2, 32, 16, 24, 32),
+                                            (2, 32, 32, 16, 16), (2, 64, 32, 12, 16),
+                                            (2, 64, 64, 8, 24), (1, 32, 64, 8, 8), (2, 16, 32, 8, 16),
+                                            (32, 16, 8, 480, 640)])
+def test_pointwise_conv_vs_aten(n, cin, cout, h, w):
+    """HIP MFMA 1x1 convolution (the BN-folded guided-upsampling convs) vs ATen float64."""
+    from monocular_depth_estimation_amd.nn import _Pointwise
+    x = torch.from_numpy(seeded((n, cin, h, w), 21, -1, 1))
+    wt = torch.from_numpy(seeded((cout, cin, 1, 1), 22, -0.5, 0.5))
+    gy = torch.from_numpy(seeded((n, cout, h, w), 23, -1, 1))
+    xd, wd = x.to(DEV).requires_grad_(True), wt.to(DEV).requires_grad_(True)
+    y = _Pointwise.apply(xd, wd)
+    y.backward(gy.to(DEV))
+    xr, wr = x.double().requires_grad_(True), wt.double().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr)
+    yr.backward(gy.double())
+    close(y, yr, 1e-5, 1e-5, "fwd")
+    close(xd.grad, xr.grad, 1e-5, 1e-5, "gx")
+    close(wd.grad, wr.grad, 1e-4, 1e-5 * float(wr.grad.abs().max()), "gw")

@@ -1,0 +1,110 @@
+"""Per-convolution timing of a model's MIOpen convolutions at the bench shape.
+
+    python tools/convbench.py [--workload guidedepth|newcrf] [--bs 32]
+
+Hooks every nn.Conv2d / nn.Linear during one forward to record its input
+shape, then times forward, input-gradient and weight-gradient of each
+(unique) layer shape in isolation with torch.cuda.Event and prints ms and
+achieved TFLOP/s (fp32 MFMA peak 157 TF/s).
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _pair(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
+
+
+def timeit(fn, reps=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="guidedepth")
+    ap.add_argument("--bs", type=int, default=None)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    dev = "cuda"
+    if a.workload == "guidedepth":
+        from monocular_depth_estimation_amd import GuideDepth
+        model, bs = GuideDepth(pretrained=False).to(dev), a.bs or 32
+    else:
+        from monocular_depth_estimation_amd.model_mobileV3_large_newCRFs import PTModel
+        model, bs = PTModel().to(dev), a.bs or 16
+    shapes = collections.Counter()
+    orig_conv = torch.nn.functional.conv2d
+
+    def conv_rec(x, w, b=None, stride=1, padding=0, dilation=1, groups=1):
+        key = ("conv", tuple(x.shape), tuple(w.shape), _pair(stride), _pair(padding),
+               _pair(dilation), groups)
+        shapes[key] += 1
+        return orig_conv(x, w, b, stride, padding, dilation, groups)
+
+    orig_lin = torch.nn.functional.linear
+
+    def lin_rec(x, w, b=None):
+        shapes[("linear", tuple(x.shape), tuple(w.shape), b is not None)] += 1
+        return orig_lin(x, w, b)
+
+    torch.nn.functional.conv2d = conv_rec
+    torch.nn.functional.linear = lin_rec
+    x = torch.rand(bs, 3, 480, 640, device=dev)
+    with torch.no_grad():
+        model(x)
+    torch.nn.functional.conv2d = orig_conv
+    torch.nn.functional.linear = orig_lin
+    rows = []
+    tot = [0.0, 0.0, 0.0]
+    for key, count in shapes.items():
+        xin = torch.randn(key[1], device=dev, requires_grad=True)
+        wt = torch.randn(key[2], device=dev, requires_grad=True)
+        if key[0] == "conv":
+            _, _, _, stride, padding, dilation, groups = key
+            if groups > 1:
+                continue  # depthwise: HIP kernel, not MIOpen
+            f = lambda: orig_conv(xin, wt, None, stride, padding, dilation, groups)  # noqa: E731
+            name = f"conv w{list(key[2])} s{stride[0]} p{padding[0]} d{dilation[0]}"
+        else:
+            f = lambda: orig_lin(xin, wt)  # noqa: E731
+            name = f"linear w{list(key[2])}"
+        y = f()
+        gy = torch.randn_like(y)
+        macs = y.numel() * (wt.numel() // wt.shape[0])
+        tf = timeit(f)
+        tb = timeit(lambda: torch.autograd.grad(y, (xin,), gy, retain_graph=True))
+        tw = timeit(lambda: torch.autograd.grad(y, (wt,), gy, retain_graph=True))
+        flop = 2.0 * macs
+        row = {"layer": name, "in": list(key[1]), "count": count, "fwd_ms": round(tf, 3),
+               "bwd_data_ms": round(tb, 3), "bwd_w_ms": round(tw, 3),
+               "TFs_fwd": round(flop / tf / 1e9, 1), "TFs_bwd_data": round(flop / tb / 1e9, 1),
+               "TFs_wgrad": round(flop / tw / 1e9, 1)}
+        rows.append(row)
+        for i, t in enumerate((tf, tb, tw)):
+            tot[i] += t * count
+        print(json.dumps(row), flush=True)
+    print(f"TOTAL per step (ms): fwd {tot[0]:.2f}  bwd_data {tot[1]:.2f}  wgrad {tot[2]:.2f}", flush=True)
+    if a.json:
+        json.dump(rows, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -267,7 +267,7 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
  * guided-upsampling blocks' 1x1 convs (`nn.Conv2d(E, E/2, 1)`, `(E, in, 1)`,
  * src/GuideDepth/model/modules.py:43-74) whose bias is folded into the
  * following BatchNorm.  Supported (cin, cout): (16,8) (16,16) (16,32) (32,16)
- * (32,32) (32,64) (64,32) (64,64) with h*w % 64 == 0 (query with
+ * (32,32) (32,64) (64,32) with h*w % 64 == 0 (query with
  * mde_pointwise_supported); others return MDE_ERR_UNSUPPORTED.
  * Backward: gx (nullable) = W^T gy; gw [cout,cin] overwritten.
  * ------------------------------------------------------------------------- */

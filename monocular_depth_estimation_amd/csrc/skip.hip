@@ -320,41 +320,50 @@ __global__ void __launch_bounds__(256, 2)
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    // gW += G S^T over this tile's 64 pixels (lane group q4: pixels 16 q4 ..)
-    float ga[OT][16];
+    // gW += G S^T over this tile's 64 pixels (lane group q4: pixels 16 q4 ..).
+    // Up to 32 output channels the G operands of all M tiles stay in
+    // registers and S is read once; beyond, one M tile at a time (S re-read
+    // from L2) keeps the kernel out of scratch.
+    constexpr int OG = OT <= 2 ? OT : 1;
 #pragma unroll
-    for (int ot = 0; ot < OT; ++ot) {
-      const int o = 16 * ot + l16;
-      if (o < CO) {
-        const float4* src = reinterpret_cast<const float4*>(gp + o * hw + 16 * q4);
+    for (int og = 0; og < OT; og += OG) {
+      float ga[OG][16];
+#pragma unroll
+      for (int oo = 0; oo < OG; ++oo) {
+        const int ot = og + oo;
+        const int o = 16 * ot + l16;
+        if (o < CO) {
+          const float4* src = reinterpret_cast<const float4*>(gp + o * hw + 16 * q4);
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const float4 x = src[v];
+            ga[oo][4 * v] = x.x; ga[oo][4 * v + 1] = x.y;
+            ga[oo][4 * v + 2] = x.z; ga[oo][4 * v + 3] = x.w;
+            gbp[ot] += (x.x + x.y) + (x.z + x.w);
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < 16; ++k) ga[oo][k] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 16 * q4);
+        float sb[16];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          const float4 x = src[v];
-          ga[ot][4 * v] = x.x; ga[ot][4 * v + 1] = x.y; ga[ot][4 * v + 2] = x.z; ga[ot][4 * v + 3] = x.w;
-          gbp[ot] += (x.x + x.y) + (x.z + x.w);
+          float4 x = ra[v];
+          if (HAS_D) {
+            const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4)[v];
+            x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
+          }
+          sb[4 * v] = x.x; sb[4 * v + 1] = x.y; sb[4 * v + 2] = x.z; sb[4 * v + 3] = x.w;
         }
-      } else {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) ga[ot][k] = 0.f;
+        for (int oo = 0; oo < OG; ++oo)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) gw[og + oo][mt] = mfma4(ga[oo][k], sb[k], gw[og + oo][mt]);
       }
-    }
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 16 * q4);
-      float sb[16];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        float4 x = ra[v];
-        if (HAS_D) {
-          const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4)[v];
-          x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
-        }
-        sb[4 * v] = x.x; sb[4 * v + 1] = x.y; sb[4 * v + 2] = x.z; sb[4 * v + 3] = x.w;
-      }
-#pragma unroll
-      for (int ot = 0; ot < OT; ++ot)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) gw[ot][mt] = mfma4(ga[ot][k], sb[k], gw[ot][mt]);
     }
   }
   // gW C layout: o = 16ot + 4 q4 + i, c = 16mt + l16; gb: sum over the 4 lane groups
@@ -578,7 +587,7 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
 // Bias-free 1x1 convolution (the conv feeding a BatchNorm whose bias is
 // folded), the MFMA kernels above with one input.
 #define MDE_PW_SHAPES(X) \
-  X(16, 8) X(16, 16) X(32, 16) X(32, 32) X(64, 32) X(64, 64) X(32, 64) X(16, 32)
+  X(16, 8) X(16, 16) X(32, 16) X(32, 32) X(64, 32) X(32, 64) X(16, 32)
 
 static bool pw_ok(int64_t n, int64_t cin, int64_t cout, int64_t hw) {
   if (n <= 0 || hw <= 0 || hw % 64 != 0) return false;

@@ -177,6 +177,19 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "bytes_per_launch": nbytes / launches,
                     "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
+    # north_star's "depthwise+upsample path": every resize (bilinear, nearest)
+    # and depthwise-conv launch of the step, aggregated (sum bytes / sum time)
+    path = {k: v for k, v in kernels.items()
+            if k.startswith(("bilinear", "nearest", "dwconv"))}
+    path_roofline = None
+    if path:
+        ms = sum(v[0] for v in path.values())
+        nbytes = sum(v[2] for v in path.values())
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        path_roofline = {"bound": "hbm", "kernels": sorted(path), "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "ms_per_step": round(ms / (args.timing_steps if use_graph else args.steps), 3)}
     if args.workload == "guidedepth":
         metric = "training images/sec at 640x480 bs=32/GPU (GuideDepth, SSIM+0.1*L1, Adam)"
         workload = ("GuideDepth (DDRNet-23-slim + 3 guided upsampling blocks) train step, "
@@ -199,6 +212,7 @@ def main():
         "execution": ("hipGraph replay of the whole step (GraphTrainer)" if use_graph
                       else "eager (Trainer + DDP)"),
         "roofline": roofline,
+        "path_roofline": path_roofline,
         "hip_kernels": {k: {"ms_total": round(v[0], 3), "launches": v[1],
                             "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 else None}
                         for k, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])},

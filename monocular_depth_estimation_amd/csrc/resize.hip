@@ -178,6 +178,71 @@ inline dim3 x2_grid(int64_t planes, int64_t hi, int64_t wi) {
               (unsigned)planes);
 }
 
+// Backward, generic ratio, banded: one thread owns input column j of a band
+// of kBandRows input rows of one plane.  Its column weights over the
+// output-column window (<= kColWin entries, zero-padded) are computed once
+// and kept in registers; the thread then streams the output-gradient rows
+// that can touch the band, forms the column-adjoint sum of each row once and
+// adds it into the (at most two) band rows that row's stencil reads.  Used
+// when the column window fits kColWin (upsampling up to ~8.7x, e.g. the
+// DDRNet 8x10 -> 60x80 and 15x20 -> 60x80 resizes); wider windows take the
+// per-pixel kernel below.
+constexpr int kBandRows = 4;
+constexpr int kColWin = 32;
+
+__global__ void __launch_bounds__(256)
+    bilinear_bwd_band_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                             int64_t planes, int hi, int wi, int ho, int wo,
+                             float sh, float sw, int align) {
+  const int bands = (hi + kBandRows - 1) / kBandRows;
+  const int64_t total = planes * bands * (int64_t)wi;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(t % wi);
+    const int64_t r = t / wi;
+    const int ib = (int)(r % bands) * kBandRows;
+    const int64_t plane = r / bands;
+    int clo, chi;
+    lin_window(sw, j, wo, &clo, &chi);
+    float cw[kColWin];
+#pragma unroll
+    for (int k = 0; k < kColWin; ++k)
+      cw[k] = clo + k <= chi ? lin_weight(sw, clo + k, j, wi, align) : 0.f;
+    const int ilast = ib + kBandRows - 1 < hi ? ib + kBandRows - 1 : hi - 1;
+    int rlo, rhi, unused;
+    lin_window(sh, ib, ho, &rlo, &unused);
+    lin_window(sh, ilast, ho, &unused, &rhi);
+    const float* g = gy + plane * ho * (int64_t)wo;
+    float acc[kBandRows];
+#pragma unroll
+    for (int b = 0; b < kBandRows; ++b) acc[b] = 0.f;
+    for (int o = rlo; o <= rhi; ++o) {
+      const Lin H = lin_index(sh, o, hi, align);
+      const int d0 = H.i0 - ib, d1 = H.i1 - ib;
+      if ((unsigned)d0 >= (unsigned)kBandRows && (unsigned)d1 >= (unsigned)kBandRows)
+        continue;
+      const float* grow = g + (int64_t)o * wo;
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < kColWin; ++k) {
+        const int p = clo + k < wo - 1 ? clo + k : wo - 1;
+        s += cw[k] * grow[p];
+      }
+#pragma unroll
+      for (int b = 0; b < kBandRows; ++b) {
+        float wgt = 0.f;
+        if (d0 == b) wgt += H.l0;
+        if (d1 == b) wgt += H.l1;
+        acc[b] += wgt * s;
+      }
+    }
+    float* out = gx + (plane * hi + ib) * (int64_t)wi + j;
+#pragma unroll
+    for (int b = 0; b < kBandRows; ++b)
+      if (ib + b < hi) out[(int64_t)b * wi] = acc[b];
+  }
+}
+
 // Backward, generic ratio: candidate windows per axis, exact weights.
 __global__ void __launch_bounds__(256)
     bilinear_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx,
@@ -319,6 +384,12 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
                x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
                (float*)gx, (int)hi, (int)wi);
+  } else if (scale_w > 0.f && 3.0 / scale_w + 6.0 <= kColWin) {
+    const int64_t bands = mde::cdiv(hi, kBandRows);
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_band_kernel,
+               dim3(grid_for(planes * bands * wi)), dim3(256), 0,
+               (const float*)gy, (float*)gx, planes, (int)hi, (int)wi,
+               (int)ho, (int)wo, scale_h, scale_w, align_corners);
   } else {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_kernel,
                dim3(grid_for(planes * hi * wi)), dim3(256), 0,

@@ -221,14 +221,32 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
 
-  // 4. gradient + L1 on the tile
+  // 4. gradient + L1 on the tile.  Two pixels away from the image border
+  // every window centre reaches each pixel exactly once (the reflected
+  // windows of centres 0 and n-1 hit pixels 1 and n-2 twice), so such tiles
+  // take a plain 3x3 sum.
   float l1sum = 0.f;
+  const bool interior = r0 >= 2 && r0 + TH <= h - 2 && c0 >= 2 && c0 + TW <= w - 2;
   for (int e = tid; e < TH * TW; e += 256) {
     const int i0 = e / TW, j0 = e % TW;
     const int gi = r0 + i0, gj = c0 + j0;
     if (gi >= h || gj >= w) continue;
     const float xv = sx[i0 + 2][j0 + 2], yv = sy[i0 + 2][j0 + 2];
     float SA = 0.f, SB = 0.f, SC = 0.f, SAy = 0.f, SBy = 0.f;
+    if (interior) {
+#pragma unroll
+      for (int u = i0; u < i0 + 3; ++u)
+#pragma unroll
+        for (int v = j0; v < j0 + 3; ++v) {
+          SA += ca[u][v];
+          SB += cb[u][v];
+          SC += cc[u][v];
+          if (GT) {
+            SAy += cay[u][v];
+            SBy += cby[u][v];
+          }
+        }
+    } else {
 #pragma unroll
     for (int du = -1; du <= 1; ++du) {
       const int pr = gi + du;
@@ -251,6 +269,7 @@ __global__ void __launch_bounds__(256)
           SBy += fm * cby[u][v];
         }
       }
+    }
     }
     const float diff = xv - yv;
     l1sum += fabsf(diff);

@@ -68,6 +68,16 @@ def main():
         x = torch.rand(n, c, hi, wi, device=dev)
         nb = 4.0 * n * c * (hi * wi + 60 * 80)
         report(f"bilinear_fwd {c}x{hi}x{wi}->60x80", timeit(lambda: F.bilinear_resize(x, size=(60, 80)), a.reps), nb)
+        gy = torch.rand(n, c, 60, 80, device=dev)
+        report(f"bilinear_bwd {c}x{hi}x{wi}->60x80", timeit(lambda: _abi.call(
+            "mde_bilinear_bwd", gy.data_ptr(), x.data_ptr(), n, c, hi, wi, 60, 80, hi / 60, wi / 80,
+            0, 0, _abi.stream_of(x)), a.reps), nb)
+    if want("resize"):
+        img = torch.rand(n, 3, 480, 640, device=dev)
+        for sf in (0.5, 0.25):
+            ho, wo = int(480 * sf), int(640 * sf)
+            report(f"nearest_fwd x{sf} 3x480x640", timeit(lambda: F.nearest_resize(img, scale_factor=sf),
+                                                          a.reps), 8.0 * n * 3 * ho * wo)
     # SE + cat and skip fusion at the three decoder resolutions
     for c, h, w, cout in ((64, 120, 160, 32), (32, 240, 320, 16), (16, 480, 640, 1)) \
             if (want("se") or want("skip")) else ():

@@ -280,6 +280,31 @@ int mde_pointwise_bwd(const void* gy, const void* x, const float* weight, void* 
                       int64_t w, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Bias-free 3x3 convolution, stride 1, zero padding 1, dilation 1, NCHW fp32
+ * (MFMA).  The kxk first layers of the guided-upsampling blocks' feature_conv,
+ * guide_conv and comb_conv (`nn.Conv2d(in, E, kernel_size=3, padding=1)`,
+ * src/GuideDepth/model/modules.py:43-74), bias folded into the following
+ * BatchNorm.  x [n,cin,h,w], weight [cout,cin,3,3], y [n,cout,h,w].
+ * mde_conv3x3_supported(cin, cout, pass): pass 0 forward, 1 data gradient,
+ * 2 weight gradient.  Supported: forward (3,16) (3,32) (3,64) (16,16)
+ * (32,32); data gradient (16,16) (32,32); weight gradient all five; others
+ * return MDE_ERR_UNSUPPORTED.
+ * bwd_data: gx [n,cin,h,w] = conv_transpose(gy, weight), overwritten.
+ * wgrad: gweight [cout,cin,3,3] overwritten (deterministic block partials +
+ * fixed-order reduction in mde_conv3x3_wgrad_workspace bytes).
+ * ------------------------------------------------------------------------- */
+int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass);
+int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                    int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
+int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t n,
+                         int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                         void* stream);
+size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------
  * Depthwise convolution (groups == channels, square k = 3 or 5, stride 1 or
  * 2, zero padding `pad`, dilation 1, no bias), NCHW.  Replaces the
  * depthwise Conv2d of every MobileNetV3-Large inverted-residual block

@@ -52,6 +52,10 @@ enum Kid : int {
   K_TRANSPOSE,
   K_PW_FWD,
   K_PW_BWD,
+  K_C3_FWD,
+  K_C3_DGRAD,
+  K_C3_WGRAD,
+  K_C3_WREDUCE,
   K_COUNT
 };
 

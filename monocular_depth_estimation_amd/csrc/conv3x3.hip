@@ -1,0 +1,519 @@
+// 3x3, stride 1, zero-padding 1, bias-free convolution, NCHW fp32, on
+// v_mfma_f32_16x16x4_f32 (exact f32 products, f32 accumulation).
+//
+// Replaces the first (kxk) Conv2d of the guided-upsampling blocks' three
+// branches — feature_conv, guide_conv and comb_conv
+// (src/GuideDepth/model/modules.py:43-74, built with kernel_size=3 at
+// GuideDepth.py:21-33) — at the full-resolution, small-channel shapes where
+// MIOpen's Winograd / implicit-GEMM kernels run at 10-45 TFLOP/s:
+// 16->16 @ 480x640, 32->32 @ 240x320 (weight gradient) and the 3-channel
+// guide convolutions 3->{16,32,64}.  The conv bias is folded into the
+// following BatchNorm (nn.py conv_bn), so the kernels are bias-free.
+//
+// Forward (and data gradient = the same kernel on the flipped, transposed
+// weights): implicit GEMM with M = output pixels, N = output channels,
+// K = (tap, input channel).  A block stages an input tile of
+// C_in x (TH+2) x 66 (zero halo) and the weights in LDS; each wave owns
+// RPW output rows x 64 columns x all output channels.  K is ordered tap-major
+// so the 4 k-lanes of one MFMA step read 4 channels at the same tap: every
+// operand read is one ds_read_b32 at a compile-time offset from a per-lane
+// base, conflict-free (plane stride = 16 mod 64 words).
+//
+// Weight gradient: M = output channels, N = (tap, input channel), K =
+// pixels.  Each block walks a strided list of 8x64 pixel tiles (x with halo
+// and gy staged in LDS), accumulating its gW partial in registers; waves
+// split the tile's rows (and, for wide problems, the N blocks).  Block
+// partials land in a slab that a two-stage, fixed-order reduction sums, so
+// the result is bitwise reproducible (no atomics).
+#include "common.h"
+
+namespace {
+
+using f4 = __attribute__((__vector_size__(4 * sizeof(float)))) float;
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int kTW = 64;       // output columns per tile (4 MFMA row tiles)
+constexpr int kXW = kTW + 2;  // staged input columns (one-pixel halo each side)
+
+constexpr int cpad4(int c) { return (c + 3) / 4 * 4; }
+// LDS plane stride (words) for `rows` staged rows of kXW, = `mod` (mod 64).
+constexpr int plane_words(int rows, int mod) { return (rows * kXW + 63) / 64 * 64 + mod; }
+// Weight-row stride (words): the four k-lane groups of a B read land on
+// disjoint 16-bank quarters (16 -> 16, 32 -> 48, 64 -> 80, all = 16k mod 64
+// with k odd or the groups spread 0/16/32/48).
+constexpr int wrow_words(int co) { return co == 16 ? 16 : (co == 32 ? 48 : 80); }
+
+// --------------------------------------------------------------- staging
+// Stage a CIP x XR x kXW input tile (rows r0-1.., cols c0-1..) into LDS
+// planes of PS words, zero outside the image and for channels >= CI.  Each
+// wave copies whole tile rows (wave-uniform channel / row, lane = column, the
+// two right-halo columns by lanes 0-1), CHUNK rows' loads in flight before
+// their LDS writes; out-of-range elements load element 0 and are zeroed by a
+// select (no divergent branches around the loads).
+template <int CI, int CIP, int XR, int PS, int CHUNK>
+__device__ __forceinline__ void stage_halo_tile(const float* __restrict__ xi, float* sx, int h,
+                                                int w, int r0, int c0, int lane, int wv) {
+  constexpr int ROWS = CIP * XR;
+  constexpr int RPWV = (ROWS + 3) / 4;  // tile rows per wave
+  const int gc = c0 - 1 + lane, gc2 = c0 + 63 + lane;
+  const bool cok = gc >= 0 && gc < w, cok2 = lane < 2 && gc2 < w;
+#pragma unroll
+  for (int k0 = 0; k0 < RPWV; k0 += CHUNK) {
+    float a[CHUNK], b[CHUNK];
+#pragma unroll
+    for (int k = 0; k < CHUNK; ++k) {
+      const int ri = wv + 4 * (k0 + k);
+      const int c = ri / XR, r = ri % XR, gr = r0 - 1 + r;
+      const bool rok = k0 + k < RPWV && ri < ROWS && c < CI && gr >= 0 && gr < h;
+      const float* src = xi + (rok ? ((int64_t)c * h + gr) * w : 0);
+      const float ta = src[rok && cok ? gc : 0];
+      const float tb = src[rok && cok2 ? gc2 : 0];
+      a[k] = rok && cok ? ta : 0.f;
+      b[k] = rok && cok2 ? tb : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < CHUNK; ++k) {
+      const int ri = wv + 4 * (k0 + k);
+      if (k0 + k < RPWV && ri < ROWS) {
+        const int c = ri / XR, r = ri % XR;
+        float* d = sx + c * PS + r * kXW;
+        d[lane] = a[k];
+        if (lane < 2) d[64 + lane] = b[k];
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------- forward
+template <int CI, int CO, int RPW, bool FLIP>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                       float* __restrict__ y, int h, int w, int tiles_w,
+                       int tiles_per_img) {
+  constexpr int CIP = cpad4(CI);
+  constexpr int TH = 4 * RPW;
+  constexpr int XR = TH + 2;
+  constexpr int PS = plane_words(XR, 16);
+  constexpr int WS = wrow_words(CO);
+  constexpr int NB = CO / 16;
+  __shared__ float sx[CIP * PS];
+  __shared__ float sw[9 * CIP * WS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int img = blockIdx.x / tiles_per_img;
+  const int t = blockIdx.x % tiles_per_img;
+  const int r0 = (t / tiles_w) * TH, c0 = (t % tiles_w) * kTW;
+
+  // weights -> sw[(tap * CIP + ci) * WS + co]; FLIP: W'[co][ci][tap] =
+  // W[ci][co][8 - tap] (the data gradient is this convolution of gy).
+  // (all loads issued before any LDS write; see stage_halo_tile)
+  {
+    constexpr int WN = 9 * CIP * CO;
+    constexpr int WPER = (WN + 255) / 256;
+    float v[WPER];
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int e = tid + 256 * i;
+      const int co = e % CO, rest = e / CO, ci = rest % CIP, tap = rest / CIP;
+      const bool ok = e < WN && ci < CI;
+      const int src = FLIP ? (ci * CO + co) * 9 + (8 - tap) : (co * CI + ci) * 9 + tap;
+      const float t = wt[ok ? src : 0];
+      v[i] = ok ? t : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < WPER; ++i) {
+      const int e = tid + 256 * i;
+      const int co = e % CO, rest = e / CO, ci = rest % CIP, tap = rest / CIP;
+      if (e < WN) sw[(tap * CIP + ci) * WS + co] = v[i];
+    }
+  }
+  // input tile with zero halo (and zero channels CI..CIP-1)
+  stage_halo_tile<CI, CIP, XR, PS, 16>(x + (int64_t)img * CI * h * w, sx, h, w, r0, c0, lane,
+                                      __builtin_amdgcn_readfirstlane(wv));
+  __syncthreads();
+
+  const int li = lane & 15, lk = lane >> 4;
+  const float* ax = sx + lk * PS + li + wv * RPW * kXW;
+  const float* bw = sw + lk * WS + li;
+  f4 acc[RPW][4][NB];
+#pragma unroll
+  for (int q = 0; q < RPW; ++q)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[q][m][nb] = f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+    for (int cs = 0; cs < CIP / 4; ++cs) {
+      float b[NB];
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) b[nb] = bw[(tap * CIP + 4 * cs) * WS + nb * 16];
+#pragma unroll
+      for (int q = 0; q < RPW; ++q)
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const float a = ax[4 * cs * PS + (q + dy) * kXW + m * 16 + dx];
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) acc[q][m][nb] = mfma4(a, b[nb], acc[q][m][nb]);
+        }
+    }
+  }
+
+  // D layout: lane holds pixels 4*lk + i (i = 0..3) of output channel li.
+  float* yi = y + (int64_t)img * CO * h * w;
+  const bool vec = (w & 3) == 0;
+#pragma unroll
+  for (int q = 0; q < RPW; ++q) {
+    const int row = r0 + wv * RPW + q;
+    if (row >= h) continue;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int col = c0 + m * 16 + 4 * lk;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        float* dst = yi + ((int64_t)(nb * 16 + li) * h + row) * w + col;
+        const f4 v = acc[q][m][nb];
+        if (vec && col + 3 < w) {
+          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (col + i < w) dst[i] = v[i];
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------- weight gradient
+template <int CI, int CO, int TH, int PW>
+struct WgradCfg {
+  static constexpr int CIP = cpad4(CI);
+  static constexpr int XR = TH + 2;
+  static constexpr int PSX = plane_words(XR, 4);  // = 4 (mod 64)
+  static constexpr int PSG = TH * kTW + 4;        // = 4 (mod 64)
+  static constexpr int NREAL = 9 * CIP;           // n = tap * CIP + ci
+  static constexpr int NP = (NREAL + 15) / 16 * 16;
+  static constexpr int NBLK = NP / 16;
+  static constexpr int MB = CO / 16;
+  static constexpr int TWAYS = 4 / PW;            // waves splitting the N blocks
+  static constexpr int NBW = (NBLK + TWAYS - 1) / TWAYS;
+  static constexpr int RPWG = TH / PW;            // tile rows per wave
+  static constexpr int ZERO = CIP * PSX;          // zero pad for n >= NREAL
+  static constexpr int STAGE = ZERO + XR * kXW + CO * PSG;
+  static constexpr int RED = PW * MB * NBLK * 256;
+  static constexpr int SMEM = STAGE > RED ? STAGE : RED;
+  static constexpr int M = CO * NP;               // partial elements per block
+};
+
+template <int CI, int CO, int TH, int PW>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                         float* __restrict__ part, int h, int w, int tiles_w,
+                         int tiles_per_img, int ntiles) {
+  using C = WgradCfg<CI, CO, TH, PW>;
+  __shared__ float smem[C::SMEM];
+  float* sx = smem;
+  float* sg = smem + C::ZERO + C::XR * kXW;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int li = lane & 15, lk = lane >> 4;
+  const int pg = wv % PW, tg = wv / PW;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+
+  // per-lane B offsets of this wave's N blocks (tap shift folded in)
+  int boff[C::NBW];
+#pragma unroll
+  for (int j = 0; j < C::NBW; ++j) {
+    const int n = 16 * (tg + C::TWAYS * j) + li;
+    if (n < C::NREAL) {
+      const int tap = n / C::CIP, ci = n % C::CIP;
+      boff[j] = ci * C::PSX + (tap / 3) * kXW + tap % 3 + lk;
+    } else {
+      boff[j] = C::ZERO + lk;
+    }
+  }
+  const int aoff = li * C::PSG + lk;
+
+  f4 acc[C::MB][C::NBW];
+#pragma unroll
+  for (int mb = 0; mb < C::MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < C::NBW; ++j) acc[mb][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int e = tid; e < C::XR * kXW; e += 256) smem[C::ZERO + e] = 0.f;
+  const bool vec = (w & 3) == 0;
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int img = tile / tiles_per_img, t = tile % tiles_per_img;
+    const int r0 = (t / tiles_w) * TH, c0 = (t % tiles_w) * kTW;
+    const float* xi = x + (int64_t)img * CI * h * w;
+    const float* gi = gy + (int64_t)img * CO * h * w;
+    // gy tile (CO x TH x 64) as float4: 16 lanes per row, 4 rows per wave
+    // instruction; loads first, LDS writes after the barrier.
+    constexpr int GROWS = CO * TH;
+    constexpr int GPER = (GROWS + 15) / 16;
+    float4 gv[GPER];
+    const int c4 = lane & 15;
+    const int gc = c0 + 4 * c4;
+#pragma unroll
+    for (int i = 0; i < GPER; ++i) {
+      const int ri = 16 * i + 4 * wvu + (lane >> 4);
+      const int c = ri / TH, r = ri % TH, gr = r0 + r;
+      const bool rok = ri < GROWS && gr < h;
+      const float* src = gi + (rok ? ((int64_t)c * h + gr) * w + gc : 0);
+      if (vec && gc + 3 < w) {
+        const float4 t = *reinterpret_cast<const float4*>(src);
+        gv[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float4 t;
+        t.x = rok && gc < w ? src[0] : 0.f;
+        t.y = rok && gc + 1 < w ? src[1] : 0.f;
+        t.z = rok && gc + 2 < w ? src[2] : 0.f;
+        t.w = rok && gc + 3 < w ? src[3] : 0.f;
+        gv[i] = t;
+      }
+    }
+    __syncthreads();  // previous tile's operands consumed
+    stage_halo_tile<CI, C::CIP, C::XR, C::PSX, 8>(xi, sx, h, w, r0, c0, lane, wvu);
+#pragma unroll
+    for (int i = 0; i < GPER; ++i) {
+      const int ri = 16 * i + 4 * wvu + (lane >> 4);
+      if (ri < GROWS) {
+        const int c = ri / TH, r = ri % TH;
+        *reinterpret_cast<float4*>(sg + c * C::PSG + r * kTW + 4 * c4) = gv[i];
+      }
+    }
+    __syncthreads();
+
+    for (int rr = 0; rr < C::RPWG; ++rr) {
+      const int row = pg * C::RPWG + rr;
+      const float* ga = sg + aoff + row * kTW;
+      const float* xb = sx + row * kXW;
+#pragma unroll 4
+      for (int s = 0; s < kTW / 4; ++s) {
+        float a[C::MB];
+#pragma unroll
+        for (int mb = 0; mb < C::MB; ++mb) a[mb] = ga[mb * 16 * C::PSG + 4 * s];
+#pragma unroll
+        for (int j = 0; j < C::NBW; ++j) {
+          const float b = xb[boff[j] + 4 * s];
+#pragma unroll
+          for (int mb = 0; mb < C::MB; ++mb) acc[mb][j] = mfma4(a[mb], b, acc[mb][j]);
+        }
+      }
+    }
+  }
+
+  // sum the PW pixel-group partials through LDS, then one block partial:
+  // red[pg][mb][nb][co16][n16]; lane holds co16 = 4*lk + i, n16 = li.
+  __syncthreads();
+#pragma unroll
+  for (int mb = 0; mb < C::MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < C::NBW; ++j) {
+      const int nb = tg + C::TWAYS * j;
+      if (nb < C::NBLK) {
+        float* d = smem + ((pg * C::MB + mb) * C::NBLK + nb) * 256 + li;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[(4 * lk + i) * 16] = acc[mb][j][i];
+      }
+    }
+  __syncthreads();
+  float* out = part + (int64_t)blockIdx.x * C::M;
+  for (int e = tid; e < C::M; e += 256) {
+    const int co = e / C::NP, n = e % C::NP;
+    const int mb = co / 16, nb = n / 16;
+    const int o = ((mb * C::NBLK + nb) * 256) + (co % 16) * 16 + n % 16;
+    float s = 0.f;
+#pragma unroll
+    for (int p = 0; p < PW; ++p) s += smem[p * C::MB * C::NBLK * 256 + o];
+    out[e] = s;
+  }
+}
+
+// Stage 1: part [G][M] -> part2 [S][M] (S interleaved groups of blocks).
+__global__ void __launch_bounds__(256)
+    wgrad_reduce1_kernel(const float* __restrict__ part, float* __restrict__ part2,
+                         int g, int m) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= m) return;
+  const int s = blockIdx.y, ns = gridDim.y;
+  float a0 = 0.f, a1 = 0.f;
+  int b = s;
+  for (; b + ns < g; b += 2 * ns) {
+    a0 += part[(int64_t)b * m + e];
+    a1 += part[(int64_t)(b + ns) * m + e];
+  }
+  if (b < g) a0 += part[(int64_t)b * m + e];
+  part2[(int64_t)s * m + e] = a0 + a1;
+}
+
+// Stage 2: sum the S groups and scatter n = tap * cip + ci to gw[co][ci][tap].
+__global__ void __launch_bounds__(256)
+    wgrad_reduce2_kernel(const float* __restrict__ part2, float* __restrict__ gw, int ns,
+                         int co_n, int ci_n, int cip, int np) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= co_n * np) return;
+  const int co = e / np, n = e % np;
+  const int tap = n / cip, ci = n % cip;
+  if (tap >= 9 || ci >= ci_n) return;
+  float s = 0.f;
+  for (int k = 0; k < ns; ++k) s += part2[(int64_t)k * co_n * np + e];
+  gw[(co * ci_n + ci) * 9 + tap] = s;
+}
+
+constexpr int kReduceSplit = 32;
+
+// ---------------------------------------------------------------- dispatch
+enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
+
+template <int CI, int CO, int RPW, bool FLIP>
+int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t h, int64_t w,
+               double bytes, int kid, hipStream_t s) {
+  constexpr int TH = 4 * RPW;
+  const int tiles_w = (int)mde::cdiv(w, kTW);
+  const int tiles_per_img = (int)(mde::cdiv(h, TH) * tiles_w);
+  const int64_t blocks = n * tiles_per_img;
+  if (blocks > 0x7fffffff) return MDE_ERR_INVALID_ARG;
+  MDE_LAUNCH(kid, bytes, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP>), dim3((unsigned)blocks),
+             dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img);
+  return MDE_OK;
+}
+
+struct WgradPlan {
+  int th, tiles_w, tiles_per_img, ntiles, grid, m, np, cip;
+};
+
+constexpr int kWgradGrid = 1024;
+
+template <int CI, int CO, int TH, int PW>
+WgradPlan wgrad_plan(int64_t n, int64_t h, int64_t w) {
+  using C = WgradCfg<CI, CO, TH, PW>;
+  WgradPlan p;
+  p.th = TH;
+  p.tiles_w = (int)mde::cdiv(w, kTW);
+  p.tiles_per_img = (int)(mde::cdiv(h, TH) * p.tiles_w);
+  const int64_t nt = n * p.tiles_per_img;
+  p.ntiles = nt > 0x7fffffff ? 0x7fffffff : (int)nt;
+  p.grid = p.ntiles < kWgradGrid ? p.ntiles : kWgradGrid;
+  p.m = C::M;
+  p.np = C::NP;
+  p.cip = C::CIP;
+  return p;
+}
+
+template <int CI, int CO, int TH, int PW>
+int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t h, int64_t w,
+                 float* ws, double bytes, hipStream_t s) {
+  const WgradPlan p = wgrad_plan<CI, CO, TH, PW>(n, h, w);
+  float* part = ws;
+  float* part2 = ws + (int64_t)p.grid * p.m;
+  MDE_LAUNCH(mde::K_C3_WGRAD, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW>), dim3(p.grid),
+             dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w, p.tiles_per_img, p.ntiles);
+  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
+             dim3((unsigned)mde::cdiv(p.m, 256), split), dim3(256), 0, part, part2, p.grid, p.m);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * split * p.m, s, wgrad_reduce2_kernel,
+             dim3((unsigned)mde::cdiv(p.m, 256)), dim3(256), 0, part2, gw, split, CO, CI, p.cip,
+             p.np);
+  return MDE_OK;
+}
+
+// Supported (cin, cout) per pass.  Forward: the guide convs (3 -> 16/32/64),
+// 16 -> 16 and 32 -> 32; data gradient: 16 -> 16 and 32 -> 32 (the guide
+// convs read the image, which needs no gradient); weight gradient: all.
+bool supported(int64_t cin, int64_t cout, int pass) {
+  const bool guide = cin == 3 && (cout == 16 || cout == 32 || cout == 64);
+  const bool square = (cin == 16 && cout == 16) || (cin == 32 && cout == 32);
+  switch (pass) {
+    case kFwd:
+      return guide || square;
+    case kDgrad:
+      return square;
+    case kWgrad:
+      return guide || square;
+    default:
+      return false;
+  }
+}
+
+bool dims_ok(int64_t n, int64_t h, int64_t w) {
+  return n > 0 && h > 0 && w > 0 && h < (1 << 24) && w < (1 << 24);
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass) {
+  return supported(cin, cout, pass) ? 1 : 0;
+}
+
+int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                    int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !weight || !y || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
+  if (!supported(cin, cout, kFwd)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const float* in = (const float*)x;
+  float* out = (float*)y;
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  const int k = mde::K_C3_FWD;
+  if (cin == 3 && cout == 16) return launch_fwd<3, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 3 && cout == 32) return launch_fwd<3, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 3 && cout == 64) return launch_fwd<3, 64, 1, false>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 16) return launch_fwd<16, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
+  return launch_fwd<32, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
+}
+
+int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !weight || !gx || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
+  if (!supported(cin, cout, kDgrad)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const float* in = (const float*)gy;
+  float* out = (float*)gx;
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  const int k = mde::K_C3_DGRAD;
+  if (cin == 16) return launch_fwd<16, 16, 2, true>(in, weight, out, n, h, w, bytes, k, s);
+  return launch_fwd<32, 32, 1, true>(in, weight, out, n, h, w, bytes, k, s);
+}
+
+size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
+  WgradPlan p;
+  if (cin == 3 && cout == 16) p = wgrad_plan<3, 16, 8, 4>(n, h, w);
+  else if (cin == 3 && cout == 32) p = wgrad_plan<3, 32, 8, 4>(n, h, w);
+  else if (cin == 3) p = wgrad_plan<3, 64, 4, 4>(n, h, w);
+  else if (cin == 16) p = wgrad_plan<16, 16, 8, 4>(n, h, w);
+  else p = wgrad_plan<32, 32, 4, 2>(n, h, w);
+  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
+  return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
+}
+
+int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                      void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !x || !gweight || !workspace || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
+  if (!supported(cin, cout, kWgrad)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const float* xi = (const float*)x;
+  const float* g = (const float*)gy;
+  float* ws = (float*)workspace;
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  if (cin == 3 && cout == 16) return launch_wgrad<3, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 3 && cout == 32) return launch_wgrad<3, 32, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 3) return launch_wgrad<3, 64, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 16) return launch_wgrad<16, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
+}
+
+}  // extern "C"

@@ -19,7 +19,8 @@ const char* const kNames[mde::K_COUNT] = {
     "bn_bwd_apply_small", "window_attn_fwd", "window_attn_bwd",
     "dwconv_fwd",    "dwconv_bwd_data", "dwconv_bwd_weight", "dwconv_wreduce",
     "layernorm_fwd", "layernorm_bwd",   "layernorm_wreduce", "transpose",
-    "pointwise_fwd", "pointwise_bwd"};
+    "pointwise_fwd", "pointwise_bwd", "conv3x3_fwd",  "conv3x3_dgrad",
+    "conv3x3_wgrad", "conv3x3_wreduce"};
 
 struct Pending {
   int kid;

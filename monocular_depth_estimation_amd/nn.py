@@ -128,14 +128,94 @@ def pointwise_ok(conv: nn.Conv2d, x) -> bool:
                            x.shape[2], x.shape[3]))
 
 
+# Which passes of a bias-free 3x3/s1/p1 conv run on the HIP MFMA kernel
+# (mde_conv3x3_*), per (cin, cout): (forward, data gradient, weight gradient).
+# The rest go to MIOpen, whose Winograd kernels are faster at >= 32 channels
+# (tools/kbench.py --only conv: HIP vs MIOpen per pass at the bench shapes).
+CONV3X3_HIP = {
+    (3, 16): (True, True, True),
+    (3, 32): (True, True, True),
+    (3, 64): (True, True, True),
+    (16, 16): (True, True, True),
+    (32, 32): (False, False, True),
+}
+
+
+class _Conv3x3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, passes):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        if passes[0]:
+            y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
+            _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin, cout,
+                      h, w, _abi.dtype_code(x), _abi.stream_of(x))
+        else:
+            y = torch.nn.functional.conv2d(x, weight, None, 1, 1)
+        ctx.save_for_backward(x, weight)
+        ctx.passes = passes
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        gx = gw = None
+        st = _abi.stream_of(gy)
+        if ctx.needs_input_grad[0]:
+            if ctx.passes[1]:
+                gx = torch.empty_like(x)
+                _abi.call("mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx), n,
+                          cin, cout, h, w, _abi.dtype_code(gy), st)
+            else:
+                gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+        if ctx.needs_input_grad[1]:
+            if ctx.passes[2]:
+                gw = torch.empty_like(weight)
+                ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w), x)
+                _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
+                          cout, h, w, _abi.ptr(ws), _abi.dtype_code(gy), st)
+            else:
+                gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
+        return gx, gw, None
+
+
+def conv3x3_passes(conv: nn.Conv2d, x):
+    """(fwd, dgrad, wgrad) HIP flags for a 3x3/s1/p1 conv, or None if it is not one."""
+    if (conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
+            or conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros"
+            or x.dim() != 4 or x.dtype != torch.float32):
+        return None
+    p = CONV3X3_HIP.get((conv.in_channels, conv.out_channels))
+    if p is None:
+        return None
+    p = tuple(bool(f) and bool(_abi.query("mde_conv3x3_supported", conv.in_channels,
+                                          conv.out_channels, i)) for i, f in enumerate(p))
+    return p if any(p) else None
+
+
+def conv3x3(x, weight, passes=(True, True, True)):
+    """Bias-free 3x3 / stride 1 / padding 1 convolution on the HIP MFMA kernel (per-pass flags)."""
+    _gpu(x)
+    return _Conv3x3.apply(x, weight, tuple(passes))
+
+
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
     """bn(conv(x)) with the conv bias folded into the BN kernel.
 
-    Small-channel 1x1 convs run on the HIP MFMA pointwise kernel, the rest on
-    MIOpen (PyTorch-ROCm)."""
+    Small-channel 1x1 convs run on the HIP MFMA pointwise kernel, small-channel
+    3x3 convs on the HIP MFMA conv3x3 kernel (per pass, CONV3X3_HIP), the rest
+    on MIOpen (PyTorch-ROCm)."""
+    passes = conv3x3_passes(conv, x) if x.is_cuda else None
     if pointwise_ok(conv, x):
         _gpu(x)
         y = _Pointwise.apply(x, conv.weight)
+    elif passes is not None:
+        y = conv3x3(x, conv.weight, passes)
     else:
         y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                        conv.dilation, conv.groups)

@@ -175,6 +175,44 @@ def main():
                    3 * nb)
             xn = torch.randn(n4, c, h, w, device=dev)
             report(f"transpose nchw->tokens {c} {h}x{w}", timeit(lambda: nchw_to_tokens(xn), a.reps), 2 * nb)
+    if want("conv"):
+        # HIP MFMA 3x3 conv vs MIOpen, per pass, at the cfg2 shapes (bs 32);
+        # `frac` here is of the 157.3 TFLOP/s fp32 MFMA peak, GBps is algorithmic bytes.
+        def report_tf(name, ms, flop, nbytes):
+            tf = flop / (ms * 1e-3) / 1e12
+            rows.append({"op": name, "ms": round(ms, 4), "TFLOPs": round(tf, 1),
+                         "GBps": round(nbytes / (ms * 1e-3) / 1e9, 1), "frac": round(tf / 157.3, 3)})
+            print(f"{name:44s} {ms * 1e3:9.1f} us {tf:8.1f} TF/s  {tf / 157.3:6.1%}", flush=True)
+        tconv = torch.nn.functional.conv2d
+        for cin, cout, h, w in ((3, 16, 480, 640), (16, 16, 480, 640), (3, 32, 240, 320),
+                                (32, 32, 240, 320), (3, 64, 120, 160)):
+            x = torch.rand(n, cin, h, w, device=dev) - 0.5
+            wt = torch.rand(cout, cin, 3, 3, device=dev) - 0.5
+            gy = torch.rand(n, cout, h, w, device=dev) - 0.5
+            y = torch.empty_like(gy)
+            gx = torch.empty_like(x)
+            gw = torch.empty_like(wt)
+            ws = torch.empty(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w) // 4 + 1,
+                             device=dev)
+            st = _abi.stream_of(x)
+            flop = 2.0 * n * h * w * cout * cin * 9
+            nb = 4.0 * n * h * w * (cin + cout)
+            tag = f"{cin}->{cout} {h}x{w}"
+            report_tf(f"conv3x3 fwd HIP {tag}", timeit(lambda: _abi.call(
+                "mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, cin, cout, h, w, 0, st),
+                a.reps), flop, nb)
+            report_tf(f"conv3x3 fwd MIOpen {tag}", timeit(lambda: tconv(x, wt, None, 1, 1), a.reps), flop, nb)
+            if _abi.query("mde_conv3x3_supported", cin, cout, 1):
+                report_tf(f"conv3x3 dgrad HIP {tag}", timeit(lambda: _abi.call(
+                    "mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, cin, cout, h, w,
+                    0, st), a.reps), flop, nb)
+                report_tf(f"conv3x3 dgrad MIOpen {tag}", timeit(
+                    lambda: torch.nn.grad.conv2d_input(x.shape, wt, gy, padding=1), a.reps), flop, nb)
+            report_tf(f"conv3x3 wgrad HIP {tag}", timeit(lambda: _abi.call(
+                "mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h, w,
+                _abi.ptr(ws), 0, st), a.reps), flop, nb)
+            report_tf(f"conv3x3 wgrad MIOpen {tag}", timeit(
+                lambda: torch.nn.grad.conv2d_weight(x, wt.shape, gy, padding=1), a.reps), flop, nb)
     if a.json:
         json.dump(rows, open(a.json, "w"), indent=1)
 

@@ -28,6 +28,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MFMA_F32_PEAK_TFS = 157.3  # fp32-input MFMA dense peak (= fp32 vector rate, MI355X_MICROARCH.md)
 PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
 
 
@@ -167,16 +168,24 @@ def main():
     images = world.size * args.bs * args.steps
     roofline = None
     if kernels:
-        name, (ms, launches, nbytes) = max(kernels.items(), key=lambda kv: kv[1][0])
-        achieved = nbytes / (ms * 1e-3) / 1e9
+        name, (ms, launches, nbytes, flops) = max(kernels.items(), key=lambda kv: kv[1][0])
         traffic = None
         if os.path.exists(PMC_FILE):
             with open(PMC_FILE) as f:
                 traffic = json.load(f).get(name, {}).get("bytes_per_launch")
-        roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic, "bytes_per_launch": nbytes / launches,
-                    "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
+        if flops > 0:  # an MFMA kernel (conv3x3): priced against the fp32 MFMA peak
+            achieved = flops / (ms * 1e-3) / 1e12
+            roofline = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2),
+                        "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                        "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
+                        "flops_per_launch": flops / launches, "bytes_per_launch": nbytes / launches,
+                        "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
+        else:
+            achieved = nbytes / (ms * 1e-3) / 1e9
+            roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                        "traffic": traffic, "bytes_per_launch": nbytes / launches,
+                        "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
     # north_star's "depthwise+upsample path": every resize (bilinear, nearest)
     # and depthwise-conv launch of the step, aggregated (sum bytes / sum time)
     path = {k: v for k, v in kernels.items()
@@ -213,8 +222,9 @@ def main():
                       else "eager (Trainer + DDP)"),
         "roofline": roofline,
         "path_roofline": path_roofline,
-        "hip_kernels": {k: {"ms_total": round(v[0], 3), "launches": v[1],
-                            "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 else None}
+        "hip_kernels": {k: dict({"ms_total": round(v[0], 3), "launches": v[1],
+                                 "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 else None},
+                                **({"TFLOPs": round(v[3] / (v[0] * 1e-3) / 1e12, 2)} if v[3] > 0 else {}))
                         for k, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])},
     }
     if world.size == 1 and not args.no_cpu_baseline:

@@ -365,6 +365,9 @@ int mde_kernel_count(void);
 const char* mde_kernel_name(int kid);
 int mde_timing_query(int kid, double* total_ms, int64_t* launches,
                      double* bytes);
+/* Algorithmic FLOPs (2 per multiply-accumulate) of the MFMA kernels
+ * (conv3x3, pointwise / skip fusion, window attention); 0 for the others. */
+int mde_timing_query_flops(int kid, double* flops);
 
 #ifdef __cplusplus
 }

@@ -94,6 +94,7 @@ SIGNATURES = {
     "mde_kernel_name": (_c.c_char_p, [_int]),
     "mde_timing_query": (_int, [_int, _c.POINTER(_c.c_double), _c.POINTER(_c.c_int64),
                                 _c.POINTER(_c.c_double)]),
+    "mde_timing_query_flops": (_int, [_int, _c.POINTER(_c.c_double)]),
 }
 
 
@@ -166,7 +167,7 @@ def timing_reset() -> None:
 
 
 def timing_collect() -> dict:
-    """Resolve pending events; return {kernel: (total_ms, launches, bytes)}."""
+    """Resolve pending events; return {kernel: (total_ms, launches, bytes, flops)}."""
     lib = load()
     check(lib.mde_timing_collect(), "mde_timing_collect")
     out = {}
@@ -174,6 +175,8 @@ def timing_collect() -> dict:
         ms, n, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
         check(lib.mde_timing_query(k, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(by)),
               "mde_timing_query")
+        fl = ctypes.c_double()
+        check(lib.mde_timing_query_flops(k, ctypes.byref(fl)), "mde_timing_query_flops")
         if n.value:
-            out[lib.mde_kernel_name(k).decode()] = (ms.value, n.value, by.value)
+            out[lib.mde_kernel_name(k).decode()] = (ms.value, n.value, by.value, fl.value)
     return out

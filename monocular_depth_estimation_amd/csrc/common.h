@@ -62,7 +62,7 @@ enum Kid : int {
 // Timing hooks (timing.hip).  begin() returns a token for end(); both are
 // no-ops when the registry is disabled.
 int timing_begin(int kid, hipStream_t s);
-void timing_end(int token, hipStream_t s, double bytes);
+void timing_end(int token, hipStream_t s, double bytes, double flops = 0.0);
 
 // Launch a kernel with optional timing and return the launch status.
 #define MDE_LAUNCH(KID, BYTES, STREAM, KERNEL, GRID, BLOCK, SHMEM, ...)      \
@@ -72,6 +72,18 @@ void timing_end(int token, hipStream_t s, double bytes);
                        __VA_ARGS__);                                       \
     hipError_t _e = hipGetLastError();                                     \
     ::mde::timing_end(_tok, (STREAM), (double)(BYTES));                    \
+    if (_e != hipSuccess) return (int)_e;                                  \
+  } while (0)
+
+// Same for an MFMA kernel: FLOPS = its algorithmic floating-point operations
+// (2 per multiply-accumulate), reported against the MFMA peak.
+#define MDE_LAUNCH_MFMA(KID, BYTES, FLOPS, STREAM, KERNEL, GRID, BLOCK, SHMEM, ...) \
+  do {                                                                     \
+    int _tok = ::mde::timing_begin((KID), (STREAM));                       \
+    hipLaunchKernelGGL(KERNEL, (GRID), (BLOCK), (SHMEM), (STREAM),         \
+                       __VA_ARGS__);                                       \
+    hipError_t _e = hipGetLastError();                                     \
+    ::mde::timing_end(_tok, (STREAM), (double)(BYTES), (double)(FLOPS));   \
     if (_e != hipSuccess) return (int)_e;                                  \
   } while (0)
 

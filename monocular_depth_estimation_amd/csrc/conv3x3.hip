@@ -25,6 +25,8 @@
 // split the tile's rows (and, for wide problems, the N blocks).  Block
 // partials land in a slab that a two-stage, fixed-order reduction sums, so
 // the result is bitwise reproducible (no atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -376,12 +378,13 @@ enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 template <int CI, int CO, int RPW, bool FLIP>
 int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t h, int64_t w,
                double bytes, int kid, hipStream_t s) {
+  const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
   constexpr int TH = 4 * RPW;
   const int tiles_w = (int)mde::cdiv(w, kTW);
   const int tiles_per_img = (int)(mde::cdiv(h, TH) * tiles_w);
   const int64_t blocks = n * tiles_per_img;
   if (blocks > 0x7fffffff) return MDE_ERR_INVALID_ARG;
-  MDE_LAUNCH(kid, bytes, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP>), dim3((unsigned)blocks),
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP>), dim3((unsigned)blocks),
              dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img);
   return MDE_OK;
 }
@@ -412,9 +415,10 @@ template <int CI, int CO, int TH, int PW>
 int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t h, int64_t w,
                  float* ws, double bytes, hipStream_t s) {
   const WgradPlan p = wgrad_plan<CI, CO, TH, PW>(n, h, w);
+  const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
   float* part = ws;
   float* part2 = ws + (int64_t)p.grid * p.m;
-  MDE_LAUNCH(mde::K_C3_WGRAD, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW>), dim3(p.grid),
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW>), dim3(p.grid),
              dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w, p.tiles_per_img, p.ntiles);
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
   MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
@@ -443,6 +447,16 @@ bool supported(int64_t cin, int64_t cout, int pass) {
   }
 }
 
+// Tuning experiments only (tools/kbench.py): MDE_C3_VARIANT selects alternative
+// tile shapes for the 16->16 / 32->32 kernels; 0 (unset) is the shipped choice.
+int variant() {
+  static const int v = [] {
+    const char* e = std::getenv("MDE_C3_VARIANT");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 bool dims_ok(int64_t n, int64_t h, int64_t w) {
   return n > 0 && h > 0 && w > 0 && h < (1 << 24) && w < (1 << 24);
 }
@@ -468,6 +482,7 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
   if (cin == 3 && cout == 16) return launch_fwd<3, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 3 && cout == 32) return launch_fwd<3, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 3 && cout == 64) return launch_fwd<3, 64, 1, false>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 1, false>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 16) return launch_fwd<16, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
   return launch_fwd<32, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
 }
@@ -482,6 +497,7 @@ int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
   float* out = (float*)gx;
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
   const int k = mde::K_C3_DGRAD;
+  if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 1, true>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 16) return launch_fwd<16, 16, 2, true>(in, weight, out, n, h, w, bytes, k, s);
   return launch_fwd<32, 32, 1, true>(in, weight, out, n, h, w, bytes, k, s);
 }
@@ -492,7 +508,11 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   if (cin == 3 && cout == 16) p = wgrad_plan<3, 16, 8, 4>(n, h, w);
   else if (cin == 3 && cout == 32) p = wgrad_plan<3, 32, 8, 4>(n, h, w);
   else if (cin == 3) p = wgrad_plan<3, 64, 4, 4>(n, h, w);
+  else if (cin == 16 && variant() == 1) p = wgrad_plan<16, 16, 4, 4>(n, h, w);
+  else if (cin == 16 && variant() == 2) p = wgrad_plan<16, 16, 4, 2>(n, h, w);
   else if (cin == 16) p = wgrad_plan<16, 16, 8, 4>(n, h, w);
+  else if (variant() == 1) p = wgrad_plan<32, 32, 2, 2>(n, h, w);
+  else if (variant() == 2) p = wgrad_plan<32, 32, 4, 1>(n, h, w);
   else p = wgrad_plan<32, 32, 4, 2>(n, h, w);
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
   return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
@@ -512,7 +532,11 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   if (cin == 3 && cout == 16) return launch_wgrad<3, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3 && cout == 32) return launch_wgrad<3, 32, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3) return launch_wgrad<3, 64, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 16 && variant() == 1) return launch_wgrad<16, 16, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 16 && variant() == 2) return launch_wgrad<16, 16, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 16) return launch_wgrad<16, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (variant() == 1) return launch_wgrad<32, 32, 2, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (variant() == 2) return launch_wgrad<32, 32, 4, 1>(xi, g, gweight, n, h, w, ws, bytes, s);
   return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
 }
 

@@ -10,6 +10,8 @@
 //
 // Backward is a gather: every input pixel sums the output gradients whose
 // stencil touches it, so there are no atomics and gx is written exactly once.
+#include <cmath>
+
 #include "common.h"
 
 namespace {
@@ -178,6 +180,66 @@ inline dim3 x2_grid(int64_t planes, int64_t hi, int64_t wi) {
               (unsigned)planes);
 }
 
+// Backward, generic ratio, one plane per block in LDS (the DDRNet resizes of
+// tiny maps, e.g. 8x10 -> 60x80 and 15x20 -> 60x80: every output-gradient
+// plane fits).  The adjoint is separable: t[o][j] = sum_p Wc[p,j] gy[o][p]
+// (column pass, gy staged once), then gx[i][j] = sum_o Wr[o,i] t[o][j].  The
+// per-axis weights come from tables built once per block over the candidate
+// windows (exact ATen source-index math, zero-padded to kw / kh entries).
+constexpr int kPlaneMax = 12288;  // floats of gy (and of t) per block
+
+__global__ void __launch_bounds__(256)
+    bilinear_bwd_plane_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                              int hi, int wi, int ho, int wo, float sh, float sw,
+                              int align, int kh, int kw) {
+  extern __shared__ float lds[];
+  float* sg = lds;                    // [ho][wo]
+  float* st = sg + ho * wo;           // [ho][wi]
+  float* cw = st + ho * wi;           // [wi][kw]
+  float* rw = cw + wi * kw;           // [hi][kh]
+  int* clo = (int*)(rw + hi * kh);    // [wi]
+  int* rlo = clo + wi;                // [hi]
+  const int tid = threadIdx.x;
+  const int64_t plane = blockIdx.x;
+  const float* g = gy + plane * ho * (int64_t)wo;
+  const int np = ho * wo;
+  for (int e = tid; e < np; e += 256) sg[e] = g[e];
+  for (int e = tid; e < wi * kw; e += 256) {
+    const int j = e / kw, k = e % kw;
+    int lo, hi_;
+    lin_window(sw, j, wo, &lo, &hi_);
+    if (k == 0) clo[j] = lo;
+    cw[e] = lo + k <= hi_ ? lin_weight(sw, lo + k, j, wi, align) : 0.f;
+  }
+  for (int e = tid; e < hi * kh; e += 256) {
+    const int i = e / kh, k = e % kh;
+    int lo, hi_;
+    lin_window(sh, i, ho, &lo, &hi_);
+    if (k == 0) rlo[i] = lo;
+    rw[e] = lo + k <= hi_ ? lin_weight(sh, lo + k, i, hi, align) : 0.f;
+  }
+  __syncthreads();
+  for (int e = tid; e < ho * wi; e += 256) {
+    const int o = e / wi, j = e % wi;
+    const float* row = sg + o * wo;
+    const float* wc = cw + j * kw;
+    const int lo = clo[j];
+    float acc = 0.f;
+    for (int k = 0; k < kw; ++k) acc += wc[k] * row[min(lo + k, wo - 1)];
+    st[e] = acc;
+  }
+  __syncthreads();
+  float* out = gx + plane * hi * (int64_t)wi;
+  for (int e = tid; e < hi * wi; e += 256) {
+    const int i = e / wi, j = e % wi;
+    const float* wr = rw + i * kh;
+    const int lo = rlo[i];
+    float acc = 0.f;
+    for (int k = 0; k < kh; ++k) acc += wr[k] * st[min(lo + k, ho - 1) * wi + j];
+    out[e] = acc;
+  }
+}
+
 // Backward, generic ratio, banded: one thread owns input column j of a band
 // of kBandRows input rows of one plane.  Its column weights over the
 // output-column window (<= kColWin entries, zero-padded) are computed once
@@ -330,6 +392,19 @@ inline int grid_for(int64_t work) {
   return (int)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
 }
 
+// Candidate-window length of lin_window along an axis (<= 3/scale + 6).
+int win_len(float scale, int64_t out_size) {
+  if (!(scale > 0.f)) return (int)out_size;
+  const double k = std::ceil(3.0 / scale) + 6.0;
+  return (int)(k < (double)out_size ? k : (double)out_size);
+}
+
+bool plane_fits(int64_t hi, int64_t wi, int64_t ho, int64_t wo, float sh, float sw) {
+  if (!(sh > 0.f) || !(sw > 0.f) || ho * wo > kPlaneMax || ho * wi > kPlaneMax) return false;
+  const int64_t kh = win_len(sh, ho), kw = win_len(sw, wo);
+  return (ho * wo + ho * wi + wi * kw + hi * kh + wi + hi) * 4 <= 64 * 1024;
+}
+
 bool dims_ok(int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
              int64_t wo) {
   return n > 0 && c > 0 && hi > 0 && wi > 0 && ho > 0 && wo > 0 &&
@@ -384,6 +459,13 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
                x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
                (float*)gx, (int)hi, (int)wi);
+  } else if (plane_fits(hi, wi, ho, wo, scale_h, scale_w)) {
+    const int kh = win_len(scale_h, ho), kw = win_len(scale_w, wo);
+    const size_t lds = sizeof(float) * ((size_t)ho * wo + (size_t)ho * wi + (size_t)wi * kw +
+                                        (size_t)hi * kh + wi + hi);
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_plane_kernel, dim3((unsigned)planes),
+               dim3(256), lds, (const float*)gy, (float*)gx, (int)hi, (int)wi, (int)ho,
+               (int)wo, scale_h, scale_w, align_corners, kh, kw);
   } else if (scale_w > 0.f && 3.0 / scale_w + 6.0 <= kColWin) {
     const int64_t bands = mde::cdiv(hi, kBandRows);
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_band_kernel,

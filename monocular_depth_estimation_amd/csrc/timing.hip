@@ -25,7 +25,7 @@ const char* const kNames[mde::K_COUNT] = {
 struct Pending {
   int kid;
   hipEvent_t a, b;
-  double bytes;
+  double bytes, flops;
   bool done;
 };
 
@@ -37,6 +37,7 @@ struct Registry {
   double ms[mde::K_COUNT] = {};
   int64_t launches[mde::K_COUNT] = {};
   double bytes[mde::K_COUNT] = {};
+  double flops[mde::K_COUNT] = {};
 
   hipEvent_t get() {
     if (!pool.empty()) {
@@ -63,14 +64,14 @@ int timing_begin(int kid, hipStream_t s) {
   Registry& r = reg();
   if (!r.on) return -1;
   std::lock_guard<std::mutex> g(r.mu);
-  Pending p{kid, r.get(), r.get(), 0.0, false};
+  Pending p{kid, r.get(), r.get(), 0.0, 0.0, false};
   if (!p.a || !p.b) return -1;
   (void)hipEventRecord(p.a, s);
   r.pending.push_back(p);
   return (int)r.pending.size() - 1;
 }
 
-void timing_end(int token, hipStream_t s, double bytes) {
+void timing_end(int token, hipStream_t s, double bytes, double flops) {
   if (token < 0) return;
   Registry& r = reg();
   std::lock_guard<std::mutex> g(r.mu);
@@ -78,6 +79,7 @@ void timing_end(int token, hipStream_t s, double bytes) {
   Pending& p = r.pending[token];
   (void)hipEventRecord(p.b, s);
   p.bytes = bytes;
+  p.flops = flops;
   p.done = true;
 }
 
@@ -102,6 +104,7 @@ int mde_timing_reset(void) {
     r.ms[k] = 0.0;
     r.launches[k] = 0;
     r.bytes[k] = 0.0;
+    r.flops[k] = 0.0;
   }
   return MDE_OK;
 }
@@ -119,6 +122,7 @@ int mde_timing_collect(void) {
         r.ms[p.kid] += t;
         r.launches[p.kid] += 1;
         r.bytes[p.kid] += p.bytes;
+        r.flops[p.kid] += p.flops;
       } else {
         status = (int)e;
       }
@@ -145,6 +149,14 @@ int mde_timing_query(int kid, double* total_ms, int64_t* launches,
   if (total_ms) *total_ms = r.ms[kid];
   if (launches) *launches = r.launches[kid];
   if (bytes) *bytes = r.bytes[kid];
+  return MDE_OK;
+}
+
+int mde_timing_query_flops(int kid, double* flops) {
+  if (kid < 0 || kid >= mde::K_COUNT || !flops) return MDE_ERR_INVALID_ARG;
+  Registry& r = reg();
+  std::lock_guard<std::mutex> g(r.mu);
+  *flops = r.flops[kid];
   return MDE_OK;
 }
 

@@ -22,11 +22,11 @@ run() {  # name seconds cmd...
 }
 ok_or_testfail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 if [ "${SKIP_TESTS:-0}" != 1 ]; then
-  run pytest_gpu ${TEST_TIMEOUT:-1000} python -m pytest tests -m gpu -q -rf -k "${PYTEST_K:-}"; rc=$?
+  run pytest_gpu ${TEST_TIMEOUT:-1000} python -m pytest ${TESTS:-tests} -m gpu -q -rf -x --timeout 300 -k "${PYTEST_K:-}"; rc=$?
   ok_or_testfail $rc || exit $rc
 fi
 if [ "${KBENCH:-1}" = 1 ]; then
-  run kbench 600 python tools/kbench.py --json gpurun_out/kbench.json || exit $?
+  run kbench 600 python tools/kbench.py ${KB_ONLY:+--only $KB_ONLY} --json gpurun_out/kbench.json || exit $?
 fi
 [ "${SKIP_SMOKE:-0}" = 1 ] || run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 [ "${SKIP_BENCH:-0}" = 1 ] || run bench 900 python bench.py --steps "$STEPS" --warmup "$WARMUP" ${BENCH_ARGS:-} || exit $?

@@ -30,6 +30,14 @@ NAMES = [
     (r"se_scale_kernel", "se_scale"),
     (r"se_(bfc[123]|wgrad)_kernel", "se_bwd_fc"),
     (r"se_apply_kernel", "se_bwd_apply"),
+    (r"skip_fwd_mfma_kernel<\d+, \d+, true>", "skip_reduce_fwd"),
+    (r"skip_fwd_mfma_kernel<\d+, \d+, false>", "pointwise_fwd"),
+    (r"skip_bwd_mfma_kernel<\d+, \d+, true>", "skip_reduce_bwd"),
+    (r"skip_bwd_mfma_kernel<\d+, \d+, false>", "pointwise_bwd"),
+    (r"conv3x3_fwd_kernel<.*false>", "conv3x3_fwd"),
+    (r"conv3x3_fwd_kernel<.*true>", "conv3x3_dgrad"),
+    (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),
+    (r"wgrad_reduce[12]_kernel", "conv3x3_wreduce"),
     (r"skip_fwd_kernel", "skip_reduce_fwd"),
     (r"skip_bwd_kernel", "skip_reduce_bwd"),
     (r"skip_slab_reduce_kernel", "skip_reduce_bwd_reduce"),

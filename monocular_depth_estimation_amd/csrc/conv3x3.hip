@@ -49,52 +49,120 @@ constexpr int plane_words(int rows, int mod) { return (rows * kXW + 63) / 64 * 6
 constexpr int wrow_words(int co) { return co == 16 ? 16 : (co == 32 ? 48 : 80); }
 
 // --------------------------------------------------------------- staging
-// Stage a CIP x XR x kXW input tile (rows r0-1.., cols c0-1..) into LDS
-// planes of PS words, zero outside the image and for channels >= CI.  Each
-// wave copies whole tile rows (wave-uniform channel / row, lane = column, the
-// two right-halo columns by lanes 0-1), CHUNK rows' loads in flight before
-// their LDS writes; out-of-range elements load element 0 and are zeroed by a
-// select (no divergent branches around the loads).
-template <int CI, int CIP, int XR, int PS, int CHUNK>
-__device__ __forceinline__ void stage_halo_tile(const float* __restrict__ xi, float* sx, int h,
-                                                int w, int r0, int c0, int lane, int wv) {
-  constexpr int ROWS = CIP * XR;
-  constexpr int RPWV = (ROWS + 3) / 4;  // tile rows per wave
-  const int gc = c0 - 1 + lane, gc2 = c0 + 63 + lane;
-  const bool cok = gc >= 0 && gc < w, cok2 = lane < 2 && gc2 < w;
+// A CIP x XR x kXW input tile (rows r0-1.., cols c0-1..), zero outside the
+// image and for channels >= CI, held in registers between its global loads
+// and its LDS writes so that the loads of tile i+1 are in flight while tile i
+// is multiplied.  Each wave copies whole tile rows (wave-uniform channel /
+// row, lane = column 0..63); the two right-halo columns of all of the wave's
+// rows go one element per lane in NH extra loads.  Out-of-range elements load
+// element 0 and are zeroed by a select (no divergent branches around loads).
+template <int CI, int CIP, int XR>
+struct HaloTile {
+  static constexpr int ROWS = CIP * XR;
+  static constexpr int RPWV = (ROWS + 3) / 4;      // tile rows per wave
+  static constexpr int NH = (2 * RPWV + 63) / 64;  // right-halo loads per lane
+  float a[RPWV];
+  float b[NH];
+
+  __device__ __forceinline__ void load(const float* __restrict__ xi, int h, int w, int r0,
+                                       int c0, int lane, int wvu) {
+    const int gc = c0 - 1 + lane;
+    const bool cok = gc >= 0 && gc < w;
 #pragma unroll
-  for (int k0 = 0; k0 < RPWV; k0 += CHUNK) {
-    float a[CHUNK], b[CHUNK];
-#pragma unroll
-    for (int k = 0; k < CHUNK; ++k) {
-      const int ri = wv + 4 * (k0 + k);
+    for (int k = 0; k < RPWV; ++k) {
+      const int ri = wvu + 4 * k;
       const int c = ri / XR, r = ri % XR, gr = r0 - 1 + r;
-      const bool rok = k0 + k < RPWV && ri < ROWS && c < CI && gr >= 0 && gr < h;
-      const float* src = xi + (rok ? ((int64_t)c * h + gr) * w : 0);
-      const float ta = src[rok && cok ? gc : 0];
-      const float tb = src[rok && cok2 ? gc2 : 0];
-      a[k] = rok && cok ? ta : 0.f;
-      b[k] = rok && cok2 ? tb : 0.f;
+      const bool ok = ri < ROWS && c < CI && gr >= 0 && gr < h && cok;
+      const float t = xi[ok ? ((int64_t)c * h + gr) * w + gc : 0];
+      a[k] = ok ? t : 0.f;
     }
 #pragma unroll
-    for (int k = 0; k < CHUNK; ++k) {
-      const int ri = wv + 4 * (k0 + k);
-      if (k0 + k < RPWV && ri < ROWS) {
-        const int c = ri / XR, r = ri % XR;
-        float* d = sx + c * PS + r * kXW;
-        d[lane] = a[k];
-        if (lane < 2) d[64 + lane] = b[k];
+    for (int q = 0; q < NH; ++q) {
+      const int e = 64 * q + lane;  // (row k = e / 2, column 64 + e % 2)
+      const int ri = wvu + 4 * (e >> 1);
+      const int c = ri / XR, r = ri % XR, gr = r0 - 1 + r, g2 = c0 + 63 + (e & 1);
+      const bool ok = e < 2 * RPWV && ri < ROWS && c < CI && gr >= 0 && gr < h && g2 < w;
+      const float t = xi[ok ? ((int64_t)c * h + gr) * w + g2 : 0];
+      b[q] = ok ? t : 0.f;
+    }
+  }
+
+  template <int PS>
+  __device__ __forceinline__ void store(float* sx, int lane, int wvu) const {
+#pragma unroll
+    for (int k = 0; k < RPWV; ++k) {
+      const int ri = wvu + 4 * k;
+      if (ri < ROWS) sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = a[k];
+    }
+#pragma unroll
+    for (int q = 0; q < NH; ++q) {
+      const int e = 64 * q + lane;
+      const int ri = wvu + 4 * (e >> 1);
+      if (e < 2 * RPWV && ri < ROWS) sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = b[q];
+    }
+  }
+};
+
+// A CO x TH x 64 gradient tile (rows r0.., cols c0..) as float4: 16 lanes
+// per row, 4 rows per wave instruction; zero outside the image.
+template <int CO, int TH>
+struct GradTile {
+  static constexpr int ROWS = CO * TH;
+  static constexpr int PER = (ROWS + 15) / 16;
+  float4 v[PER];
+
+  __device__ __forceinline__ void load(const float* __restrict__ gi, int h, int w, int r0,
+                                       int c0, int lane, int wvu) {
+    const int gc = c0 + 4 * (lane & 15);
+    const bool vec = (w & 3) == 0 && gc + 3 < w;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int ri = 16 * i + 4 * wvu + (lane >> 4);
+      const int c = ri / TH, gr = r0 + ri % TH;
+      const bool rok = ri < ROWS && gr < h;
+      const float* src = gi + (rok ? ((int64_t)c * h + gr) * w + gc : 0);
+      if (vec) {
+        const float4 t = *reinterpret_cast<const float4*>(src);
+        v[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float4 t;
+        t.x = rok && gc < w ? src[0] : 0.f;
+        t.y = rok && gc + 1 < w ? src[1] : 0.f;
+        t.z = rok && gc + 2 < w ? src[2] : 0.f;
+        t.w = rok && gc + 3 < w ? src[3] : 0.f;
+        v[i] = t;
       }
     }
   }
+
+  template <int PSG>
+  __device__ __forceinline__ void store(float* sg, int lane, int wvu) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int ri = 16 * i + 4 * wvu + (lane >> 4);
+      if (ri < ROWS)
+        *reinterpret_cast<float4*>(sg + (ri / TH) * PSG + (ri % TH) * kTW + 4 * (lane & 15)) = v[i];
+    }
+  }
+};
+
+struct TileGeo {
+  int img, r0, c0;
+};
+
+__device__ __forceinline__ TileGeo tile_geo(int tile, int th, int tiles_w, int tiles_per_img) {
+  const int t = tile % tiles_per_img;
+  return {tile / tiles_per_img, (t / tiles_w) * th, (t % tiles_w) * kTW};
 }
 
 // --------------------------------------------------------------- forward
+// Persistent: block b multiplies tiles b, b + grid, ...; the next tile's
+// input is loaded into registers before the current tile's MFMAs.
 template <int CI, int CO, int RPW, bool FLIP>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                       float* __restrict__ y, int h, int w, int tiles_w,
-                       int tiles_per_img) {
+                       float* __restrict__ y, int h, int w, int tiles_w, int tiles_per_img,
+                       int ntiles) {
   constexpr int CIP = cpad4(CI);
   constexpr int TH = 4 * RPW;
   constexpr int XR = TH + 2;
@@ -105,13 +173,11 @@ __global__ void __launch_bounds__(256, 2)
   __shared__ float sw[9 * CIP * WS];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int img = blockIdx.x / tiles_per_img;
-  const int t = blockIdx.x % tiles_per_img;
-  const int r0 = (t / tiles_w) * TH, c0 = (t % tiles_w) * kTW;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int64_t img_in = (int64_t)CI * h * w, img_out = (int64_t)CO * h * w;
 
   // weights -> sw[(tap * CIP + ci) * WS + co]; FLIP: W'[co][ci][tap] =
   // W[ci][co][8 - tap] (the data gradient is this convolution of gy).
-  // (all loads issued before any LDS write; see stage_halo_tile)
   {
     constexpr int WN = 9 * CIP * CO;
     constexpr int WPER = (WN + 255) / 256;
@@ -132,61 +198,75 @@ __global__ void __launch_bounds__(256, 2)
       if (e < WN) sw[(tap * CIP + ci) * WS + co] = v[i];
     }
   }
-  // input tile with zero halo (and zero channels CI..CIP-1)
-  stage_halo_tile<CI, CIP, XR, PS, 16>(x + (int64_t)img * CI * h * w, sx, h, w, r0, c0, lane,
-                                      __builtin_amdgcn_readfirstlane(wv));
-  __syncthreads();
 
   const int li = lane & 15, lk = lane >> 4;
   const float* ax = sx + lk * PS + li + wv * RPW * kXW;
   const float* bw = sw + lk * WS + li;
-  f4 acc[RPW][4][NB];
-#pragma unroll
-  for (int q = 0; q < RPW; ++q)
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) acc[q][m][nb] = f4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int tap = 0; tap < 9; ++tap) {
-    const int dy = tap / 3, dx = tap % 3;
-#pragma unroll
-    for (int cs = 0; cs < CIP / 4; ++cs) {
-      float b[NB];
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) b[nb] = bw[(tap * CIP + 4 * cs) * WS + nb * 16];
-#pragma unroll
-      for (int q = 0; q < RPW; ++q)
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const float a = ax[4 * cs * PS + (q + dy) * kXW + m * 16 + dx];
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) acc[q][m][nb] = mfma4(a, b[nb], acc[q][m][nb]);
-        }
-    }
-  }
-
-  // D layout: lane holds pixels 4*lk + i (i = 0..3) of output channel li.
-  float* yi = y + (int64_t)img * CO * h * w;
   const bool vec = (w & 3) == 0;
+
+  HaloTile<CI, CIP, XR> T;
+  int tile = blockIdx.x;
+  if (tile < ntiles) {
+    const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    T.load(x + g.img * img_in, h, w, g.r0, g.c0, lane, wvu);
+  }
+  for (; tile < ntiles; tile += gridDim.x) {
+    const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    __syncthreads();  // previous tile's operands consumed (and weights staged)
+    T.template store<PS>(sx, lane, wvu);
+    __syncthreads();
+    const int nxt = tile + gridDim.x;
+    if (nxt < ntiles) {
+      const TileGeo gn = tile_geo(nxt, TH, tiles_w, tiles_per_img);
+      T.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
+    }
+
+    f4 acc[RPW][4][NB];
 #pragma unroll
-  for (int q = 0; q < RPW; ++q) {
-    const int row = r0 + wv * RPW + q;
-    if (row >= h) continue;
+    for (int q = 0; q < RPW; ++q)
 #pragma unroll
-    for (int m = 0; m < 4; ++m) {
-      const int col = c0 + m * 16 + 4 * lk;
+      for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        float* dst = yi + ((int64_t)(nb * 16 + li) * h + row) * w + col;
-        const f4 v = acc[q][m][nb];
-        if (vec && col + 3 < w) {
-          *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
-        } else {
+        for (int nb = 0; nb < NB; ++nb) acc[q][m][nb] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (col + i < w) dst[i] = v[i];
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap % 3;
+#pragma unroll
+      for (int cs = 0; cs < CIP / 4; ++cs) {
+        float b[NB];
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) b[nb] = bw[(tap * CIP + 4 * cs) * WS + nb * 16];
+#pragma unroll
+        for (int q = 0; q < RPW; ++q)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const float a = ax[4 * cs * PS + (q + dy) * kXW + m * 16 + dx];
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) acc[q][m][nb] = mfma4(a, b[nb], acc[q][m][nb]);
+          }
+      }
+    }
+
+    // D layout: lane holds pixels 4*lk + i (i = 0..3) of output channel li.
+    float* yi = y + g.img * img_out;
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int row = g.r0 + wv * RPW + q;
+      if (row >= h) continue;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int col = g.c0 + m * 16 + 4 * lk;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          float* dst = yi + ((int64_t)(nb * 16 + li) * h + row) * w + col;
+          const f4 v = acc[q][m][nb];
+          if (vec && col + 3 < w) {
+            *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              if (col + i < w) dst[i] = v[i];
+          }
         }
       }
     }
@@ -228,6 +308,7 @@ __global__ void __launch_bounds__(256, 2)
   const int li = lane & 15, lk = lane >> 4;
   const int pg = wv % PW, tg = wv / PW;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int64_t img_in = (int64_t)CI * h * w, img_out = (int64_t)CO * h * w;
 
   // per-lane B offsets of this wave's N blocks (tap shift folded in)
   int boff[C::NBW];
@@ -250,48 +331,25 @@ __global__ void __launch_bounds__(256, 2)
     for (int j = 0; j < C::NBW; ++j) acc[mb][j] = f4{0.f, 0.f, 0.f, 0.f};
 
   for (int e = tid; e < C::XR * kXW; e += 256) smem[C::ZERO + e] = 0.f;
-  const bool vec = (w & 3) == 0;
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int img = tile / tiles_per_img, t = tile % tiles_per_img;
-    const int r0 = (t / tiles_w) * TH, c0 = (t % tiles_w) * kTW;
-    const float* xi = x + (int64_t)img * CI * h * w;
-    const float* gi = gy + (int64_t)img * CO * h * w;
-    // gy tile (CO x TH x 64) as float4: 16 lanes per row, 4 rows per wave
-    // instruction; loads first, LDS writes after the barrier.
-    constexpr int GROWS = CO * TH;
-    constexpr int GPER = (GROWS + 15) / 16;
-    float4 gv[GPER];
-    const int c4 = lane & 15;
-    const int gc = c0 + 4 * c4;
-#pragma unroll
-    for (int i = 0; i < GPER; ++i) {
-      const int ri = 16 * i + 4 * wvu + (lane >> 4);
-      const int c = ri / TH, r = ri % TH, gr = r0 + r;
-      const bool rok = ri < GROWS && gr < h;
-      const float* src = gi + (rok ? ((int64_t)c * h + gr) * w + gc : 0);
-      if (vec && gc + 3 < w) {
-        const float4 t = *reinterpret_cast<const float4*>(src);
-        gv[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-      } else {
-        float4 t;
-        t.x = rok && gc < w ? src[0] : 0.f;
-        t.y = rok && gc + 1 < w ? src[1] : 0.f;
-        t.z = rok && gc + 2 < w ? src[2] : 0.f;
-        t.w = rok && gc + 3 < w ? src[3] : 0.f;
-        gv[i] = t;
-      }
-    }
+  HaloTile<CI, C::CIP, C::XR> T;
+  GradTile<CO, TH> G;
+  int tile = blockIdx.x;
+  if (tile < ntiles) {
+    const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    G.load(gy + g.img * img_out, h, w, g.r0, g.c0, lane, wvu);
+    T.load(x + g.img * img_in, h, w, g.r0, g.c0, lane, wvu);
+  }
+  for (; tile < ntiles; tile += gridDim.x) {
     __syncthreads();  // previous tile's operands consumed
-    stage_halo_tile<CI, C::CIP, C::XR, C::PSX, 8>(xi, sx, h, w, r0, c0, lane, wvu);
-#pragma unroll
-    for (int i = 0; i < GPER; ++i) {
-      const int ri = 16 * i + 4 * wvu + (lane >> 4);
-      if (ri < GROWS) {
-        const int c = ri / TH, r = ri % TH;
-        *reinterpret_cast<float4*>(sg + c * C::PSG + r * kTW + 4 * c4) = gv[i];
-      }
-    }
+    T.template store<C::PSX>(sx, lane, wvu);
+    G.template store<C::PSG>(sg, lane, wvu);
     __syncthreads();
+    const int nxt = tile + gridDim.x;
+    if (nxt < ntiles) {
+      const TileGeo gn = tile_geo(nxt, TH, tiles_w, tiles_per_img);
+      G.load(gy + gn.img * img_out, h, w, gn.r0, gn.c0, lane, wvu);
+      T.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
+    }
 
     for (int rr = 0; rr < C::RPWG; ++rr) {
       const int row = pg * C::RPWG + rr;
@@ -375,6 +433,19 @@ constexpr int kReduceSplit = 32;
 // ---------------------------------------------------------------- dispatch
 enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
+// Resident blocks of a kernel on the whole device (persistent grids).
+template <auto Kernel>
+int resident_blocks() {
+  static const int cached = [] {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, Kernel, 256, 0);
+    return (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+  }();
+  return cached;
+}
+
 template <int CI, int CO, int RPW, bool FLIP>
 int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t h, int64_t w,
                double bytes, int kid, hipStream_t s) {
@@ -382,10 +453,12 @@ int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t 
   constexpr int TH = 4 * RPW;
   const int tiles_w = (int)mde::cdiv(w, kTW);
   const int tiles_per_img = (int)(mde::cdiv(h, TH) * tiles_w);
-  const int64_t blocks = n * tiles_per_img;
-  if (blocks > 0x7fffffff) return MDE_ERR_INVALID_ARG;
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP>), dim3((unsigned)blocks),
-             dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img);
+  const int64_t ntiles = n * tiles_per_img;
+  if (ntiles > 0x7fffffff) return MDE_ERR_INVALID_ARG;
+  const int res = resident_blocks<conv3x3_fwd_kernel<CI, CO, RPW, FLIP>>();
+  const int grid = ntiles < res ? (int)ntiles : res;
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP>), dim3(grid),
+                  dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img, (int)ntiles);
   return MDE_OK;
 }
 
@@ -482,8 +555,8 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
   if (cin == 3 && cout == 16) return launch_fwd<3, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 3 && cout == 32) return launch_fwd<3, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 3 && cout == 64) return launch_fwd<3, 64, 1, false>(in, weight, out, n, h, w, bytes, k, s);
-  if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 1, false>(in, weight, out, n, h, w, bytes, k, s);
-  if (cin == 16) return launch_fwd<16, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 16) return launch_fwd<16, 16, 1, false>(in, weight, out, n, h, w, bytes, k, s);
   return launch_fwd<32, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
 }
 
@@ -497,8 +570,8 @@ int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
   float* out = (float*)gx;
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
   const int k = mde::K_C3_DGRAD;
-  if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 1, true>(in, weight, out, n, h, w, bytes, k, s);
-  if (cin == 16) return launch_fwd<16, 16, 2, true>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 2, true>(in, weight, out, n, h, w, bytes, k, s);
+  if (cin == 16) return launch_fwd<16, 16, 1, true>(in, weight, out, n, h, w, bytes, k, s);
   return launch_fwd<32, 32, 1, true>(in, weight, out, n, h, w, bytes, k, s);
 }
 
@@ -511,9 +584,9 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   else if (cin == 16 && variant() == 1) p = wgrad_plan<16, 16, 4, 4>(n, h, w);
   else if (cin == 16 && variant() == 2) p = wgrad_plan<16, 16, 4, 2>(n, h, w);
   else if (cin == 16) p = wgrad_plan<16, 16, 8, 4>(n, h, w);
-  else if (variant() == 1) p = wgrad_plan<32, 32, 2, 2>(n, h, w);
+  else if (variant() == 1) p = wgrad_plan<32, 32, 4, 2>(n, h, w);
   else if (variant() == 2) p = wgrad_plan<32, 32, 4, 1>(n, h, w);
-  else p = wgrad_plan<32, 32, 4, 2>(n, h, w);
+  else p = wgrad_plan<32, 32, 2, 2>(n, h, w);
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
   return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
 }
@@ -535,9 +608,9 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   if (cin == 16 && variant() == 1) return launch_wgrad<16, 16, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 16 && variant() == 2) return launch_wgrad<16, 16, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 16) return launch_wgrad<16, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
-  if (variant() == 1) return launch_wgrad<32, 32, 2, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (variant() == 1) return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (variant() == 2) return launch_wgrad<32, 32, 4, 1>(xi, g, gweight, n, h, w, ws, bytes, s);
-  return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
+  return launch_wgrad<32, 32, 2, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
 }
 
 }  // extern "C"

@@ -221,6 +221,18 @@ int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
                            const void* residual, void* y, float* save_mean,
                            float* save_invstd, int64_t n, int64_t c, int64_t h,
                            int64_t w, int act, int dtype, void* stream);
+/* Training-mode statistics (or, training = 0, the running statistics) turned
+ * into per-channel coefficients only: y = x * scale[c] + shift[c] is the BN
+ * output (conv bias `prebias` folded), for a consumer that applies it while
+ * loading (mde_pointwise_fwd in_scale / in_shift).  Running statistics,
+ * num_batches_tracked and save_mean / save_invstd as mde_batchnorm_fwd_train;
+ * the backward is mde_batchnorm_bwd with the consumer's input gradient. */
+int mde_batchnorm_fwd_coef(const void* x, const float* gamma, const float* beta,
+                           const float* prebias, float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, float momentum, float eps,
+                           int training, float* scale, float* shift, float* save_mean,
+                           float* save_invstd, int64_t n, int64_t c, int64_t h, int64_t w,
+                           void* workspace, int dtype, void* stream);
 /* Backward.  `training` selects batch-statistics gradients.  The activation
  * mask is recomputed from x (and residual), so y need not be kept.
  * gresidual (nullable) receives d/d residual; with act == 0 it equals gy and
@@ -273,11 +285,19 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
  * ------------------------------------------------------------------------- */
 int mde_pointwise_supported(int64_t cin, int64_t cout, int64_t h, int64_t w);
 size_t mde_pointwise_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
-int mde_pointwise_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
-                      int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
-int mde_pointwise_bwd(const void* gy, const void* x, const float* weight, void* gx,
-                      float* gweight, int64_t n, int64_t cin, int64_t cout, int64_t h,
-                      int64_t w, void* workspace, int dtype, void* stream);
+/* in_scale / in_shift (nullable, both or neither, fp32 [cin]): the input is
+ * relu(x * in_scale[c] + in_shift[c]) — the producer's BatchNorm + ReLU
+ * (`nn.BatchNorm2d(E), nn.ReLU()` before this conv, modules.py:44-47,54-57,
+ * 69-72) fused into the operand load, coefficients from
+ * mde_batchnorm_fwd_coef.  Backward then recomputes that input for gweight
+ * and gx is the gradient w.r.t. it (the BN backward applies the ReLU mask). */
+int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
+                      const float* weight, void* y, int64_t n, int64_t cin, int64_t cout,
+                      int64_t h, int64_t w, int dtype, void* stream);
+int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
+                      const float* in_shift, const float* weight, void* gx, float* gweight,
+                      int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                      void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Bias-free 3x3 convolution, stride 1, zero padding 1, dilation 1, NCHW fp32

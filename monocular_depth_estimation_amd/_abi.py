@@ -70,9 +70,11 @@ SIGNATURES = {
                                _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_pointwise_supported": (_int, [_i64, _i64, _i64, _i64]),
     "mde_pointwise_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
-    "mde_pointwise_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
-    "mde_pointwise_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _int,
-                                 _vp]),
+    "mde_pointwise_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_pointwise_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                                 _vp, _int, _vp]),
+    "mde_batchnorm_fwd_coef": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _int, _vp, _vp,
+                                      _vp, _vp, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_conv3x3_supported": (_int, [_i64, _i64, _int]),
     "mde_conv3x3_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_conv3x3_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),

@@ -477,6 +477,23 @@ int launch_stats(const float* x, int64_t n, int64_t c, int64_t hw, const Geo& g,
   return MDE_OK;
 }
 
+// Per-channel scale / shift only (the apply is fused into the consumer's
+// operand load): one wave per channel, the same finalisation as the apply
+// kernels, every wave the designated writer of its channel.
+__global__ void __launch_bounds__(256)
+    bn_coef_kernel(const float* __restrict__ x, int64_t c, FwdArgs A,
+                   float* __restrict__ scale, float* __restrict__ shift) {
+  const int64_t ch = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ch >= c) return;  // whole waves
+  double s1 = 0.0, s2 = 0.0;
+  if (A.training) wave_slices(A.part, ch, A.slices, &s1, &s2);
+  if ((threadIdx.x & 63) == 0) {
+    const FwdCh k = fwd_channel(A, x, ch, s1, s2, true);
+    scale[ch] = k.sc;
+    shift[ch] = k.sh;
+  }
+}
+
 int launch_fwd_apply(const float* x, const float* r, float* y, int64_t n,
                      int64_t c, int64_t hw, int act, const FwdArgs& A,
                      hipStream_t s) {
@@ -541,6 +558,33 @@ int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
             save_invstd, 0};
   return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c,
                           hw, act, A, s);
+}
+
+int mde_batchnorm_fwd_coef(const void* x, const float* gamma, const float* beta,
+                           const float* prebias, float* running_mean, float* running_var,
+                           int64_t* num_batches_tracked, float momentum, float eps,
+                           int training, float* scale, float* shift, float* save_mean,
+                           float* save_invstd, int64_t n, int64_t c, int64_t h, int64_t w,
+                           void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !gamma || !beta || !scale || !shift || !save_mean || !save_invstd ||
+      (!running_mean != !running_var) || !args_ok(n, c, h, w) ||
+      (training && !workspace) || (!training && !running_mean))
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t hw = h * w;
+  const Geo g = geometry(n, c, hw);
+  float* part = (float*)workspace;
+  if (training) {
+    const int st = launch_stats((const float*)x, n, c, hw, g, part, s);
+    if (st) return st;
+  }
+  FwdArgs A{gamma, beta, prebias, training ? part : nullptr, training ? g.slices : 0,
+            g.total, hw, eps, momentum, running_mean, running_var,
+            training ? num_batches_tracked : nullptr, save_mean, save_invstd, training ? 1 : 0};
+  MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c * (training ? g.slices : 1), s, bn_coef_kernel,
+             dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const float*)x, c, A, scale, shift);
+  return MDE_OK;
 }
 
 int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,

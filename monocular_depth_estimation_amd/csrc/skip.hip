@@ -270,12 +270,16 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <int CI, int CO, bool HAS_D>
+// BNR: the input is r' = relu(r * isc[c] + ish[c]) (a BatchNorm + ReLU fused
+// into this conv's operand load; r is the BN input), recomputed for gW; gs is
+// then the gradient w.r.t. r' (the BN backward applies the ReLU mask).
+template <int CI, int CO, bool HAS_D, bool BNR = false>
 __global__ void __launch_bounds__(256, 2)
     skip_bwd_mfma_kernel(const float* __restrict__ g, const float* __restrict__ r,
                          const float* __restrict__ d, const float* __restrict__ wt,
                          float* __restrict__ gs, float* __restrict__ slab, int64_t n,
-                         int64_t hw) {
+                         int64_t hw, const float* __restrict__ isc = nullptr,
+                         const float* __restrict__ ish = nullptr) {
   // CO may be 8: the M tiles of gW = G S^T are then half-empty (rows >= CO
   // are zero operands and are not stored); K of gs = W^T G is CO in steps of 4.
   constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = CO / 4;
@@ -294,6 +298,12 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) gw[ot][mt] = f4{0.f, 0.f, 0.f, 0.f};
   float gbp[OT] = {};
+  float bsc[MT], bsh[MT];  // BNR: channel c = 16 mt + l16
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    bsc[mt] = BNR ? isc[16 * mt + l16] : 1.f;
+    bsh[mt] = BNR ? ish[16 * mt + l16] : 0.f;
+  }
   const int64_t tpi = hw / 64;
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
@@ -357,6 +367,12 @@ __global__ void __launch_bounds__(256, 2)
             const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4)[v];
             x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
           }
+          if (BNR) {
+            x.x = fmaxf(x.x * bsc[mt] + bsh[mt], 0.f);
+            x.y = fmaxf(x.y * bsc[mt] + bsh[mt], 0.f);
+            x.z = fmaxf(x.z * bsc[mt] + bsh[mt], 0.f);
+            x.w = fmaxf(x.w * bsc[mt] + bsh[mt], 0.f);
+          }
           sb[4 * v] = x.x; sb[4 * v + 1] = x.y; sb[4 * v + 2] = x.z; sb[4 * v + 3] = x.w;
         }
 #pragma unroll
@@ -391,11 +407,15 @@ __global__ void __launch_bounds__(256, 2)
 // [CO x 64] output tile = W [CO x CI] . S [CI x 64] (+ bias), S = r + d formed
 // per lane from two scalar loads (16 lanes read 64 contiguous bytes of a
 // channel row); W sits in registers as the A operands for the whole launch.
-template <int CI, int CO, bool HAS_D>
+// BNR: operand r' = relu(r * isc[c] + ish[c]) (BatchNorm + ReLU of the
+// producer fused into the load, so r' is never written to HBM).
+template <int CI, int CO, bool HAS_D, bool BNR = false>
 __global__ void __launch_bounds__(256)
     skip_fwd_mfma_kernel(const float* __restrict__ r, const float* __restrict__ d,
                          const float* __restrict__ wt, const float* __restrict__ b,
-                         float* __restrict__ out, int64_t n, int64_t hw) {
+                         float* __restrict__ out, int64_t n, int64_t hw,
+                         const float* __restrict__ isc = nullptr,
+                         const float* __restrict__ ish = nullptr) {
   constexpr int OT = (CO + 15) / 16, KC = CI / 4;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
@@ -415,6 +435,12 @@ __global__ void __launch_bounds__(256)
       const int o = 16 * ot + 4 * q4 + i;
       bo[ot][i] = (b && o < CO) ? b[o] : 0.f;
     }
+  float fsc[KC], fsh[KC];  // BNR: channel c = 4 kk + q4
+#pragma unroll
+  for (int kk = 0; kk < KC; ++kk) {
+    fsc[kk] = BNR ? isc[4 * kk + q4] : 1.f;
+    fsh[kk] = BNR ? ish[4 * kk + q4] : 0.f;
+  }
   const int64_t tpi = hw / 64;
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
@@ -429,6 +455,7 @@ __global__ void __launch_bounds__(256)
       for (int kk = 0; kk < KC; ++kk) {
         const int64_t off = (int64_t)(4 * kk + q4) * hw + 16 * nt + l16;
         sb[kk] = HAS_D ? rp[off] + dp[off] : rp[off];
+        if (BNR) sb[kk] = fmaxf(sb[kk] * fsc[kk] + fsh[kk], 0.f);
       }
 #pragma unroll
       for (int ot = 0; ot < OT; ++ot) {
@@ -605,33 +632,43 @@ size_t mde_pointwise_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, 
   return mde_skip_reduce_workspace(n, cin, cout, h, w);
 }
 
-int mde_pointwise_fwd(const void* x, const float* wt, void* y, int64_t n, int64_t cin,
-                      int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
+                      const float* wt, void* y, int64_t n, int64_t cin, int64_t cout, int64_t h,
+                      int64_t w, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   const int64_t hw = h * w;
-  if (!x || !wt || !y) return MDE_ERR_INVALID_ARG;
+  if (!x || !wt || !y || (!in_scale != !in_shift)) return MDE_ERR_INVALID_ARG;
   if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const double bytes = 4.0 * n * hw * (double)(cin + cout);
   const int64_t blocks = mde::cdiv(n * hw / 64, 4);
   const dim3 grid((unsigned)(blocks > 4096 ? 4096 : blocks));
-#define MDE_PW_FWD(A, B)                                                                    \
-  if (cin == A && cout == B) {                                                              \
-    MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false>), grid, dim3(256), \
-               0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw);                 \
-    return MDE_OK;                                                                          \
+#define MDE_PW_FWD(A, B)                                                                     \
+  if (cin == A && cout == B) {                                                               \
+    if (in_scale) {                                                                          \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, true>), grid,   \
+                 dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw,      \
+                 in_scale, in_shift);                                                        \
+    } else {                                                                                 \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false>), grid,         \
+                 dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw,      \
+                 nullptr, nullptr);                                                          \
+    }                                                                                        \
+    return MDE_OK;                                                                           \
   }
   MDE_PW_SHAPES(MDE_PW_FWD)
 #undef MDE_PW_FWD
   return MDE_ERR_UNSUPPORTED;
 }
 
-int mde_pointwise_bwd(const void* gy, const void* x, const float* wt, void* gx, float* gw,
-                      int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
-                      void* workspace, int dtype, void* stream) {
+int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
+                      const float* in_shift, const float* wt, void* gx, float* gw, int64_t n,
+                      int64_t cin, int64_t cout, int64_t h, int64_t w, void* workspace,
+                      int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   const int64_t hw = h * w;
-  if (!gy || !x || !wt || !gw || !workspace) return MDE_ERR_INVALID_ARG;
+  if (!gy || !x || !wt || !gw || !workspace || (!in_scale != !in_shift))
+    return MDE_ERR_INVALID_ARG;
   if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const int nb = bwd_blocks(n, hw);
@@ -639,9 +676,15 @@ int mde_pointwise_bwd(const void* gy, const void* x, const float* wt, void* gx, 
   const double bytes = 4.0 * n * hw * (double)(cout + cin + (gx ? cin : 0));
 #define MDE_PW_BWD(A, B)                                                                     \
   if (cin == A && cout == B) {                                                               \
-    MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false>), dim3(nb),       \
-               dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt, (float*)gx, slab, \
-               n, hw);                                                                       \
+    if (in_scale) {                                                                          \
+      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false, true>),         \
+                 dim3(nb), dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt,     \
+                 (float*)gx, slab, n, hw, in_scale, in_shift);                               \
+    } else {                                                                                 \
+      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false>), dim3(nb),     \
+                 dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt, (float*)gx,   \
+                 slab, n, hw, nullptr, nullptr);                                             \
+    }                                                                                        \
   }
   MDE_PW_SHAPES(MDE_PW_BWD)
 #undef MDE_PW_BWD

@@ -98,7 +98,8 @@ class _Pointwise(torch.autograd.Function):
         cout = weight.shape[0]
         w2 = weight.reshape(cout, cin).contiguous()
         y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
-        _abi.call("mde_pointwise_fwd", _abi.ptr(x), _abi.ptr(w2), _abi.ptr(y), n, cin, cout, h, w,
+        _abi.call("mde_pointwise_fwd", _abi.ptr(x), None, None, _abi.ptr(w2), _abi.ptr(y), n, cin,
+                  cout, h, w,
                   _abi.dtype_code(x), _abi.stream_of(x))
         ctx.save_for_backward(x, w2)
         ctx.wshape = weight.shape
@@ -113,10 +114,84 @@ class _Pointwise(torch.autograd.Function):
         gx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         gw = torch.empty_like(w2)
         ws = _ws(_abi.query("mde_pointwise_workspace", n, cin, cout, h, w), x)
-        _abi.call("mde_pointwise_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(w2), _abi.ptr(gx),
+        _abi.call("mde_pointwise_bwd", _abi.ptr(gy), _abi.ptr(x), None, None, _abi.ptr(w2), _abi.ptr(gx),
                   _abi.ptr(gw), n, cin, cout, h, w, _abi.ptr(ws), _abi.dtype_code(gy),
                   _abi.stream_of(gy))
         return gx, gw.view(ctx.wshape)
+
+
+class _BNReluPointwise(torch.autograd.Function):
+    """conv1x1(relu(bn(y1))) with the BN + ReLU applied inside the 1x1 conv's
+    operand load: relu(bn(y1)) is never written.  Backward: the 1x1 conv's
+    backward recomputes that operand for its weight gradient and returns the
+    gradient w.r.t. it; the BN backward (ReLU mask recomputed from y1) turns
+    that into d/dy1 and the BN parameter gradients."""
+
+    @staticmethod
+    def forward(ctx, y1, gamma, beta, prebias, running_mean, running_var, nbt, training, momentum,
+                eps, w2):
+        y1 = y1.contiguous()
+        n, c, h, w = y1.shape
+        cout = w2.shape[0]
+        w2m = w2.reshape(cout, c).contiguous()
+        f32 = dict(dtype=torch.float32, device=y1.device)
+        scale, shift = torch.empty(c, **f32), torch.empty(c, **f32)
+        mean, invstd = torch.empty(c, **f32), torch.empty(c, **f32)
+        st = _abi.stream_of(y1)
+        ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), y1) if training else None
+        _abi.call("mde_batchnorm_fwd_coef", _abi.ptr(y1), _abi.ptr(gamma), _abi.ptr(beta),
+                  _abi.ptr(prebias), _abi.ptr(running_mean), _abi.ptr(running_var), _abi.ptr(nbt),
+                  float(momentum), float(eps), int(training), _abi.ptr(scale), _abi.ptr(shift),
+                  _abi.ptr(mean), _abi.ptr(invstd), n, c, h, w, _abi.ptr(ws),
+                  _abi.dtype_code(y1), st)
+        y2 = torch.empty((n, cout, h, w), dtype=y1.dtype, device=y1.device)
+        _abi.call("mde_pointwise_fwd", _abi.ptr(y1), _abi.ptr(scale), _abi.ptr(shift),
+                  _abi.ptr(w2m), _abi.ptr(y2), n, c, cout, h, w, _abi.dtype_code(y1), st)
+        ctx.save_for_backward(y1, gamma, beta, mean, invstd, scale, shift, w2m)
+        ctx.training, ctx.has_prebias, ctx.w2shape = bool(training), prebias is not None, w2.shape
+        return y2
+
+    @staticmethod
+    def backward(ctx, gy2):
+        y1, gamma, beta, mean, invstd, scale, shift, w2m = ctx.saved_tensors
+        gy2 = gy2.contiguous()
+        n, c, h, w = y1.shape
+        cout = w2m.shape[0]
+        st = _abi.stream_of(gy2)
+        gz = torch.empty_like(y1)
+        gw2 = torch.empty_like(w2m)
+        ws = _ws(_abi.query("mde_pointwise_workspace", n, c, cout, h, w), y1)
+        _abi.call("mde_pointwise_bwd", _abi.ptr(gy2), _abi.ptr(y1), _abi.ptr(scale),
+                  _abi.ptr(shift), _abi.ptr(w2m), _abi.ptr(gz), _abi.ptr(gw2), n, c, cout, h, w,
+                  _abi.ptr(ws), _abi.dtype_code(gy2), st)
+        gy1 = torch.empty_like(y1) if ctx.needs_input_grad[0] else None
+        gg = torch.empty_like(gamma)
+        gb = torch.empty_like(beta)
+        gpb = torch.empty_like(gamma) if (ctx.has_prebias and ctx.needs_input_grad[3]) else None
+        ws2 = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), y1)
+        _abi.call("mde_batchnorm_bwd", _abi.ptr(gz), _abi.ptr(y1), None, _abi.ptr(gamma),
+                  _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), int(ctx.training),
+                  _abi.ptr(gy1 if gy1 is not None else torch.empty_like(y1)), None, _abi.ptr(gg),
+                  _abi.ptr(gb), _abi.ptr(gpb), n, c, h, w, _ACTS["relu"], _abi.ptr(ws2),
+                  _abi.dtype_code(gy2), st)
+        return gy1, gg, gb, gpb, None, None, None, None, None, None, gw2.view(ctx.w2shape)
+
+
+def bn_relu_pointwise(y1, bn: nn.BatchNorm2d, prebias, conv: nn.Conv2d):
+    """conv(relu(bn(y1 + prebias))) for a bias-free-folded 1x1 conv on the fused HIP path."""
+    _gpu(y1, prebias)
+    if bn.weight is None or bn.bias is None:
+        raise NotImplementedError("affine=False BatchNorm has no HIP kernel")
+    training = bn.training or not bn.track_running_stats
+    if training and bn.momentum is None:
+        raise NotImplementedError("cumulative-average BatchNorm (momentum=None) has no HIP kernel")
+    track = bn.training and bn.track_running_stats
+    return _BNReluPointwise.apply(
+        y1, bn.weight, bn.bias, prebias,
+        bn.running_mean if (track or not training) else None,
+        bn.running_var if (track or not training) else None,
+        bn.num_batches_tracked if track else None,
+        training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, conv.weight)
 
 
 def pointwise_ok(conv: nn.Conv2d, x) -> bool:
@@ -222,12 +297,48 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
     return batch_norm_act(y, bn, bn.act, residual, conv.bias)
 
 
+def _conv_nobias(conv: nn.Conv2d, x):
+    """conv(x) without its bias (folded into the following BN): HIP 3x3 / MIOpen."""
+    passes = conv3x3_passes(conv, x) if x.is_cuda else None
+    if passes is not None:
+        return conv3x3(x, conv.weight, passes)
+    return torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
+                                      conv.dilation, conv.groups)
+
+
+def _bnrelu_pw_at(mods, i, x_shape) -> bool:
+    """mods[i:i+5] = Conv(bias) -> BN(relu) -> ReLU slot -> Conv1x1(bias, HIP pointwise) -> BN."""
+    if i + 4 >= len(mods):
+        return False
+    c0, b0, r0, c1, b1 = mods[i:i + 5]
+    return (isinstance(c0, nn.Conv2d) and c0.bias is not None and c0.padding_mode == "zeros"
+            and isinstance(b0, BatchNorm2d) and b0.act == "relu"
+            and isinstance(r0, nn.Identity)
+            and isinstance(c1, nn.Conv2d) and c1.bias is not None and isinstance(b1, BatchNorm2d)
+            and c1.kernel_size == (1, 1) and c1.stride == (1, 1) and c1.padding == (0, 0)
+            and c1.groups == 1 and c1.in_channels == c0.out_channels)
+
+
 def run_sequential(seq: nn.Sequential, x):
-    """Run a Sequential, folding every Conv2d(bias) -> BatchNorm2d pair (see conv_bn)."""
+    """Run a Sequential, folding every Conv2d(bias) -> BatchNorm2d pair (see conv_bn).
+
+    Conv -> BN+ReLU -> 1x1 conv -> BN (the guided-upsampling branches,
+    modules.py:43-74) additionally runs the first BN + ReLU inside the 1x1
+    conv's operand load (bn_relu_pointwise) when the 1x1 conv is on HIP."""
     mods = list(seq)
     i = 0
     while i < len(mods):
         m = mods[i]
+        if x.is_cuda and _bnrelu_pw_at(mods, i, x.shape):
+            y1 = _conv_nobias(m, x)
+            if pointwise_ok(mods[i + 3], y1):
+                y2 = bn_relu_pointwise(y1, mods[i + 1], m.bias, mods[i + 3])
+                x = batch_norm_act(y2, mods[i + 4], mods[i + 4].act, None, mods[i + 3].bias)
+                i += 5
+                continue
+            x = batch_norm_act(y1, mods[i + 1], mods[i + 1].act, None, m.bias)
+            i += 2
+            continue
         if (isinstance(m, nn.Conv2d) and m.bias is not None and i + 1 < len(mods)
                 and isinstance(mods[i + 1], BatchNorm2d) and m.padding_mode == "zeros"):
             x = conv_bn(m, mods[i + 1], x)

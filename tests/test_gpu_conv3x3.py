@@ -110,3 +110,49 @@ def test_conv3x3_unsupported_shape_raises():
     with pytest.raises(_abi.MdeError, match="unsupported"):
         _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(w), _abi.ptr(y), 1, 8, 8, 4, 4, 0,
                   _abi.stream_of(x))
+
+
+@pytest.mark.parametrize("train", [True, False])
+@pytest.mark.parametrize("cin,e,h,w", [(16, 16, 32, 64), (3, 32, 16, 48), (64, 64, 8, 64)])
+def test_fused_bn_relu_pointwise_branch_vs_float64(cin, e, h, w, train):
+    """conv3x3 -> BN+ReLU -> 1x1 -> BN+ReLU (a guided-upsampling branch,
+    modules.py:43-49) on the fused HIP path (BN1+ReLU inside the 1x1 conv's
+    operand load) vs the same Sequential as plain torch modules in float64:
+    output, input gradient, every parameter gradient and the BN running stats."""
+    import copy
+
+    from monocular_depth_estimation_amd.GuideDepth.model.modules import _conv_bn_relu
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, run_sequential
+    torch.manual_seed(cin + e + h)
+    seq = torch.nn.Sequential(*_conv_bn_relu(cin, e, 3), *_conv_bn_relu(e, e // 2, 1))
+    for m in seq.modules():
+        if isinstance(m, BatchNorm2d):
+            m.weight.data.uniform_(0.5, 1.5)
+            m.bias.data.uniform_(-0.2, 0.2)
+            m.running_mean.uniform_(-0.1, 0.1)
+            m.running_var.uniform_(0.5, 2.0)
+    ref = torch.nn.Sequential(*[torch.nn.BatchNorm2d(m.num_features) if isinstance(m, BatchNorm2d)
+                                else (torch.nn.ReLU() if isinstance(m, torch.nn.Identity) else
+                                      copy.deepcopy(m)) for m in seq]).double()
+    for r, m in zip(ref, seq):
+        if isinstance(m, BatchNorm2d):
+            r.load_state_dict(m.state_dict())
+    ref.train(train)
+    seq = seq.to(DEV).train(train)
+    x = torch.rand((2, cin, h, w)) - 0.5
+    gy = torch.rand((2, e // 2, h, w)) - 0.5
+    xg = x.to(DEV).requires_grad_(True)
+    y = run_sequential(seq, xg)
+    y.backward(gy.to(DEV))
+    xr = x.double().requires_grad_(True)
+    yr = ref(xr)
+    yr.backward(gy.double())
+    assert rel_err(y, yr) <= 1e-4
+    assert rel_err(xg.grad, xr.grad) <= 1e-3
+    for (n1, p1), (n2, p2) in zip(seq.named_parameters(), ref.named_parameters()):
+        # a conv bias in front of a train-mode BN has an identically zero
+        # gradient (the batch mean absorbs it): compare on an absolute floor
+        err = float((p1.grad.double().cpu() - p2.grad).abs().max())
+        assert err <= 1e-3 * max(float(p2.grad.abs().max()), 1e-6), n1
+    for b1, b2 in zip(seq.buffers(), ref.buffers()):
+        assert rel_err(b1, b2) <= 1e-5

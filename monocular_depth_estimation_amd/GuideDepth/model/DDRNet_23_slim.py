@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from ...functional import bilinear_resize
-from ...nn import BatchNorm2d, run_sequential
+from ...nn import BatchNorm2d, conv_nobias, run_sequential
 
 BN_MOMENTUM = 0.1
 
@@ -52,9 +52,11 @@ class BasicBlock(nn.Module):
         self.no_relu = no_relu
 
     def forward(self, x):
-        y = self.bn1(self.conv1(x))
+        # bias-free 3x3 convs: the 32->32 weight gradients run on the HIP MFMA
+        # kernel (nn.CONV3X3_HIP), the rest on MIOpen
+        y = self.bn1(conv_nobias(self.conv1, x))
         res = x if self.downsample is None else self.downsample(x)
-        return self.bn2(self.conv2(y), residual=res)
+        return self.bn2(conv_nobias(self.conv2, y), residual=res)
 
 
 class Bottleneck(nn.Module):

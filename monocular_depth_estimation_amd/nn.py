@@ -297,8 +297,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
     return batch_norm_act(y, bn, bn.act, residual, conv.bias)
 
 
-def _conv_nobias(conv: nn.Conv2d, x):
-    """conv(x) without its bias (folded into the following BN): HIP 3x3 / MIOpen."""
+def conv_nobias(conv: nn.Conv2d, x):
+    """conv(x) without its bias (folded into the following BN, or absent): HIP 3x3 / MIOpen."""
     passes = conv3x3_passes(conv, x) if x.is_cuda else None
     if passes is not None:
         return conv3x3(x, conv.weight, passes)
@@ -330,7 +330,7 @@ def run_sequential(seq: nn.Sequential, x):
     while i < len(mods):
         m = mods[i]
         if x.is_cuda and _bnrelu_pw_at(mods, i, x.shape):
-            y1 = _conv_nobias(m, x)
+            y1 = conv_nobias(m, x)
             if pointwise_ok(mods[i + 3], y1):
                 y2 = bn_relu_pointwise(y1, mods[i + 1], m.bias, mods[i + 3])
                 x = batch_norm_act(y2, mods[i + 4], mods[i + 4].act, None, mods[i + 3].bias)

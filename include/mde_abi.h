@@ -333,7 +333,8 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
  *   x [n,c,h,w], weight [c,1,k,k] fp32, y [n,c,ho,wo],
  *   ho = (h + 2 pad - k) / stride + 1 (same for wo).  n*c <= 65535.
  * Backward: gx (nullable) and gweight (nullable, fp32 [c,k,k]) are
- * overwritten; gweight needs x and a workspace of mde_dwconv_workspace bytes.
+ * overwritten; gweight needs x and a workspace of mde_dwconv_workspace bytes
+ * (workspace may be NULL when that size is 0).
  * ------------------------------------------------------------------------- */
 size_t mde_dwconv_workspace(int64_t n, int64_t c, int64_t h, int64_t w, int64_t k,
                             int64_t stride, int64_t pad);

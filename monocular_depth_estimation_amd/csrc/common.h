@@ -56,6 +56,7 @@ enum Kid : int {
   K_C3_DGRAD,
   K_C3_WGRAD,
   K_C3_WREDUCE,
+  K_DW_BWD,
   K_COUNT
 };
 

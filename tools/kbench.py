@@ -160,7 +160,7 @@ def main():
             report(f"dwconv fwd {c}x{h}x{w} k{k}s{st}", timeit(lambda: depthwise_conv2d(x, conv), a.reps), nb)
             report(f"dwconv bwd {c}x{h}x{w} k{k}s{st}",
                    timeit(lambda: torch.autograd.grad(y, (x, conv.weight), gy, retain_graph=True),
-                          a.reps), 2 * nb)
+                          a.reps), 4.0 * (2 * x.numel() + y.numel()))  # gy + x read, gx written
     if want("ln"):
         from monocular_depth_estimation_amd.newcrf_layers import LayerNorm, nchw_to_tokens
         for c, h, w in ((128, 120, 160), (256, 60, 80), (512, 30, 40), (1024, 15, 20)):

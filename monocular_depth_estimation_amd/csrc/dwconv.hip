@@ -195,20 +195,25 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------------------
-// Strip-blocked kernels (the fast path).  A tile is th x tw OUTPUT cells; a
-// thread owns one tile column and R consecutive rows of it (a "strip"), so a
-// staged LDS value feeds every output of the strip it touches from registers:
-// LDS reads per output drop from K*K to (S(R-1)+K)K/R (k5 s1: 25 -> 10), which
-// keeps the k5 kernels off the LDS-bandwidth ceiling.  Tiles are up to 64
-// cells wide (one wave of columns) and 256/tw row groups tall.
+// Strip-blocked kernels (the fast path).  A tile is th x tw OUTPUT cells of
+// `pb` planes; a thread owns one tile column and R consecutive rows of one of
+// them (a "strip"), so a staged LDS value feeds every output of the strip it
+// touches from registers: LDS reads per output drop from K*K to
+// (S(R-1)+K)K/R (k5 s1: 25 -> 10), which keeps the k5 kernels off the
+// LDS-bandwidth ceiling.  Tiles are up to 64 cells wide (one wave of columns)
+// and 256/tw row groups tall; planes smaller than half a block (the 15x20
+// late stages) are stacked pb to a block so every block keeps ~1000 loads in
+// flight instead of ~300.
 constexpr int kStripR = 4;
 
 struct DwStrip {
-  int tw, th;  // output cells per tile (th = rg * kStripR)
+  int tw, th;  // output cells per tile and plane (th = rg * kStripR)
   int rg;      // row groups (strips per column)
+  int pb;      // planes stacked per block
   int tx, ty;  // tiles per plane
-  int gh, gw;  // staged gy window (backward)
-  int xh, xw;  // staged x window
+  int gh, gw;  // staged gy window per plane (backward)
+  int xh, xw;  // staged x window per plane
+  unsigned mgh, mgw, mxh, mxw;  // fdiv magics of the window extents
 };
 
 // Offsets (in gy rows) of the taps feeding a data-gradient cell with padding
@@ -232,7 +237,13 @@ __host__ __device__ constexpr int strip_hi(int K, int S) {
   return m;
 }
 
-DwStrip strip_tile(const DwShape& d, int k, int s) {
+// e / d for 0 <= e < 2^17, d <= 4096 with m = 2^32/d + 1 (exact in that range,
+// checked exhaustively); replaces a ~20-instruction integer division.
+__device__ __forceinline__ int fdiv(int e, unsigned m) { return (int)__umulhi((unsigned)e, m); }
+inline unsigned fdiv_magic(int d) { return (unsigned)((1ull << 32) / (unsigned)d + 1); }
+
+// max_planes: how many planes a block may stack (fwd: n*c, bwd: n images).
+DwStrip strip_tile(const DwShape& d, int k, int s, int64_t max_planes) {
   DwStrip t;
   t.tx = (int)cdiv(d.wo, 64);
   t.tw = (int)cdiv(d.wo, t.tx);
@@ -241,34 +252,78 @@ DwStrip strip_tile(const DwShape& d, int k, int s) {
   if (t.rg > need) t.rg = need;
   t.th = t.rg * kStripR;
   t.ty = (int)cdiv(d.ho, t.th);
+  t.pb = 256 / (t.tw * t.rg);
+  if (t.pb > 256 / (k * k)) t.pb = 256 / (k * k);  // forward stages pb*k*k taps in LDS
+  if (t.pb > max_planes) t.pb = (int)max_planes;
+  if (t.pb < 1) t.pb = 1;
   t.xh = (t.th - 1) * s + k;
   t.xw = (t.tw - 1) * s + k;
   const int span = strip_hi(k, s) - strip_lo(k, s);
   t.gh = t.th + span;
   t.gw = t.tw + span;
+  t.mgh = fdiv_magic(t.gh);
+  t.mgw = fdiv_magic(t.gw);
+  t.mxh = fdiv_magic(t.xh);
+  t.mxw = fdiv_magic(t.xw);
   return t;
 }
 
+// tile[(p*ih + r)*iw + col] = src[p*pstride + (r0+r)*w + c0+col] for the np
+// planes p < np, zero outside the plane; all 256 threads walk the flattened
+// window with kChunk loads in flight (mih / miw: fdiv magics of ih / iw).
+__device__ __forceinline__ void stage_planes(const float* __restrict__ src, int64_t pstride,
+                                             int np, float* tile, int ih, int iw, unsigned mih,
+                                             unsigned miw, int r0, int c0, int h, int w) {
+  const int total = np * ih * iw;
+  for (int base = 0; base < total; base += 256 * kChunk) {
+    float v[kChunk];
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) {
+      const int e = base + threadIdx.x + 256 * j;
+      const int sr = fdiv(e, miw), col = e - sr * iw;
+      const int p = fdiv(sr, mih), r = sr - p * ih;
+      const int gr = r0 + r, gc = c0 + col;
+      const bool ok = e < total && gr >= 0 && gr < h && gc >= 0 && gc < w;
+      const float t = src[ok ? p * pstride + gr * w + gc : 0];
+      v[j] = ok ? t : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kChunk; ++j) {
+      const int e = base + threadIdx.x + 256 * j;
+      if (e < total) tile[e] = v[j];
+    }
+  }
+}
+
 // y[oy,ox] = sum_t w[t] x[oy*S-p+ky, ox*S-p+kx]; any padding p.
+// Block z covers planes z*pb .. z*pb+pb-1 (flattened n*c < 65536).
 template <int K, int S>
 __global__ void __launch_bounds__(256)
     dw_fwd_strip_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                        float* __restrict__ y, DwShape d, DwStrip t) {
+                        float* __restrict__ y, DwShape d, DwStrip t, int planes) {
   constexpr int R = kStripR;
   extern __shared__ float tile[];
-  const int64_t plane = blockIdx.z;
-  const int64_t ch = plane % d.c;
-  const int64_t oy0 = (int64_t)blockIdx.y * t.th, ox0 = (int64_t)blockIdx.x * t.tw;
+  __shared__ float wl[256];  // the pb planes' taps (pb * K * K <= 256, see strip_tile)
+  const int H = (int)d.h, W = (int)d.w, HO = (int)d.ho, WO = (int)d.wo, C = (int)d.c;
+  const int plane0 = blockIdx.z * t.pb;
+  const int np = planes - plane0 < t.pb ? planes - plane0 : t.pb;
+  const int oy0 = blockIdx.y * t.th, ox0 = blockIdx.x * t.tw;
+  for (int i = threadIdx.x; i < np * K * K; i += 256) {
+    const int pl = plane0 + i / (K * K);
+    wl[i] = wt[(pl % C) * K * K + i % (K * K)];
+  }
+  stage_planes(x + (int64_t)plane0 * H * W, (int64_t)H * W, np, tile, t.xh, t.xw, t.mxh, t.mxw,
+               oy0 * S - d.pad, ox0 * S - d.pad, H, W);
+  __syncthreads();
+  const int per = t.tw * t.rg;
+  const int p = threadIdx.x / per, q = threadIdx.x - p * per;
+  const int col = q % t.tw, g = q / t.tw;
+  const int ox = ox0 + col;
+  if (p >= np || ox >= WO) return;
   float wk[K * K];
 #pragma unroll
-  for (int i = 0; i < K * K; ++i) wk[i] = wt[ch * K * K + i];
-  stage_window(x + plane * d.h * d.w, tile, t.xh, t.xw, oy0 * S - d.pad, ox0 * S - d.pad, d.h,
-               d.w);
-  __syncthreads();
-  const int col = threadIdx.x % t.tw, g = threadIdx.x / t.tw;
-  const int64_t ox = ox0 + col;
-  if (g >= t.rg || ox >= d.wo) return;
-  const float* tp = tile + g * R * S * t.xw + col * S;
+  for (int i = 0; i < K * K; ++i) wk[i] = wl[p * K * K + i];
+  const float* tp = tile + (p * t.xh + g * R * S) * t.xw + col * S;
   float acc[R];
 #pragma unroll
   for (int j = 0; j < R; ++j) acc[j] = 0.f;
@@ -285,20 +340,21 @@ __global__ void __launch_bounds__(256)
       for (int kx = 0; kx < K; ++kx) acc[j] = fmaf(v[kx], wk[ky * K + kx], acc[j]);
     }
   }
-  float* yp = y + plane * d.ho * d.wo;
+  float* yp = y + (int64_t)(plane0 + p) * HO * WO;
 #pragma unroll
   for (int j = 0; j < R; ++j) {
-    const int64_t oy = oy0 + g * R + j;
-    if (oy < d.ho) yp[oy * d.wo + ox] = acc[j];
+    const int oy = oy0 + g * R + j;
+    if (oy < HO) yp[oy * WO + ox] = acc[j];
   }
 }
 
 // Fused backward for padding K/2: data gradient and weight gradient from ONE
 // staging of the gy window (+ the x window), so gy is read from HBM once.
 // Persistent over images: block (ch, g) walks items g, g+G, ... of the
-// channel's n * tiles (image, tile) items, keeps the K*K weight-gradient sums
-// in registers across items, and writes one partial per block (fixed order;
-// G == 1 writes gw directly).
+// channel's (image group, tile) items -- an image group is pb consecutive
+// images stacked in LDS -- keeps the K*K weight-gradient sums in registers
+// across items, and writes one partial per block (fixed order; G == 1 writes
+// gw directly).
 //   gx[S*oy+a, S*ox+b] = sum over (ky,kx) with (a+P-ky)%S == (b+P-kx)%S == 0 of
 //                        w[ky,kx] gy[oy + (a+P-ky)/S, ox + (b+P-kx)/S]
 //   gw[ky,kx]         += gy[oy,ox] x[S*oy-P+ky, S*ox-P+kx]
@@ -314,8 +370,9 @@ __global__ void __launch_bounds__(256)
   extern __shared__ float lds[];
   __shared__ float red[4][K * K];
   float* gyt = lds;
-  float* xt = lds + t.gh * t.gw;
-  const int64_t ch = blockIdx.x;
+  float* xt = lds + t.pb * t.gh * t.gw;
+  const int H = (int)d.h, W = (int)d.w, HO = (int)d.ho, WO = (int)d.wo, C = (int)d.c;
+  const int ch = blockIdx.x;
   const int g = blockIdx.y;
   const bool want_gx = gx != nullptr, want_gw = part != nullptr;
   float wk[K * K], acc[K * K];
@@ -324,37 +381,45 @@ __global__ void __launch_bounds__(256)
     wk[i] = want_gx ? wt[ch * K * K + i] : 0.f;
     acc[i] = 0.f;
   }
-  const int col = threadIdx.x % t.tw, rgi = threadIdx.x / t.tw;
-  const bool active = rgi < t.rg;
+  const int per = t.tw * t.rg;
+  const int p = threadIdx.x / per, q = threadIdx.x - p * per;
+  const int col = q % t.tw, rgi = q / t.tw;
   const int ly = rgi * R;  // first tile-local output row of this strip
-  const int64_t T = (int64_t)t.tx * t.ty, items = n * T;
-  for (int64_t it = g; it < items; it += G) {
-    const int64_t img = it / T, tl = it - img * T;
-    const int64_t tyi = tl / t.tx, txi = tl - tyi * t.tx;
-    const int64_t oy0 = tyi * t.th, ox0 = txi * t.tw;
-    const int64_t plane = img * d.c + ch;
+  const int nn = (int)n;
+  const int T = t.tx * t.ty, items = (nn + t.pb - 1) / t.pb * T;
+  const int64_t gys = (int64_t)C * HO * WO, xs = (int64_t)C * H * W;  // image strides
+  for (int it = g; it < items; it += G) {
+    const int grp = it / T, tl = it - grp * T;
+    const int tyi = tl / t.tx, txi = tl - tyi * t.tx;
+    const int oy0 = tyi * t.th, ox0 = txi * t.tw;
+    const int img0 = grp * t.pb;
+    const int np = nn - img0 < t.pb ? nn - img0 : t.pb;
     __syncthreads();  // previous item's readers are done with the windows
-    stage_window(gy + plane * d.ho * d.wo, gyt, t.gh, t.gw, oy0 + LO, ox0 + LO, d.ho, d.wo);
+    stage_planes(gy + ((int64_t)img0 * C + ch) * HO * WO, gys, np, gyt, t.gh, t.gw, t.mgh, t.mgw,
+                 oy0 + LO,
+                 ox0 + LO, HO, WO);
     if (want_gw)
-      stage_window(x + plane * d.h * d.w, xt, t.xh, t.xw, oy0 * S - P, ox0 * S - P, d.h, d.w);
+      stage_planes(x + ((int64_t)img0 * C + ch) * H * W, xs, np, xt, t.xh, t.xw, t.mxh, t.mxw,
+                   oy0 * S - P,
+                   ox0 * S - P, H, W);
     __syncthreads();
-    if (!active) continue;
+    if (p >= np) continue;
     if (want_gx) {
       float gv[GR][GC];
-      const float* gp = gyt + ly * t.gw + col;
+      const float* gp = gyt + (p * t.gh + ly) * t.gw + col;
 #pragma unroll
       for (int a = 0; a < GR; ++a)
 #pragma unroll
         for (int b = 0; b < GC; ++b) gv[a][b] = gp[a * t.gw + b];
-      float* gxp = gx + plane * d.h * d.w;
+      float* gxp = gx + ((int64_t)(img0 + p) * C + ch) * H * W;
 #pragma unroll
       for (int j = 0; j < R; ++j)
 #pragma unroll
         for (int a = 0; a < S; ++a) {
-          const int64_t iy = (oy0 + ly + j) * S + a;
+          const int iy = (oy0 + ly + j) * S + a;
 #pragma unroll
           for (int b = 0; b < S; ++b) {
-            const int64_t ix = (ox0 + col) * S + b;
+            const int ix = (ox0 + col) * S + b;
             float sacc = 0.f;
 #pragma unroll
             for (int ky = 0; ky < K; ++ky) {
@@ -366,15 +431,15 @@ __global__ void __launch_bounds__(256)
                 sacc = fmaf(wk[ky * K + kx], gv[ro][(b + P - kx) / S - LO], sacc);
               }
             }
-            if (iy < d.h && ix < d.w) gxp[iy * d.w + ix] = sacc;
+            if (iy < H && ix < W) gxp[iy * W + ix] = sacc;
           }
         }
     }
     if (want_gw) {
       float go[R];
 #pragma unroll
-      for (int j = 0; j < R; ++j) go[j] = gyt[(ly + j - LO) * t.gw + col - LO];
-      const float* xp = xt + ly * S * t.xw + col * S;
+      for (int j = 0; j < R; ++j) go[j] = gyt[(p * t.gh + ly + j - LO) * t.gw + col - LO];
+      const float* xp = xt + (p * t.xh + ly * S) * t.xw + col * S;
 #pragma unroll
       for (int r = 0; r < XR; ++r) {
         float v[K];
@@ -401,7 +466,7 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   if (threadIdx.x < K * K) {
     const int i = threadIdx.x;
-    part[(ch * G + g) * K * K + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    part[((int64_t)ch * G + g) * K * K + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
 }
 
@@ -442,17 +507,18 @@ DwTile in_tile(const DwShape& d, int k, int s) {
 template <int K, int S>
 int launch_fwd(const float* x, const float* wt, float* y, int64_t n, const DwShape& d,
                hipStream_t st) {
-  const DwStrip t = strip_tile(d, K, S);
-  const dim3 grid((unsigned)t.tx, (unsigned)t.ty, (unsigned)(n * d.c));
+  const int64_t planes = n * d.c;
+  const DwStrip t = strip_tile(d, K, S, planes);
+  const dim3 grid((unsigned)t.tx, (unsigned)t.ty, (unsigned)cdiv(planes, t.pb));
   const double bytes = 4.0 * n * d.c * (d.h * d.w + d.ho * d.wo);
   MDE_LAUNCH(K_DW_FWD, bytes, st, (dw_fwd_strip_kernel<K, S>), grid, dim3(256),
-             sizeof(float) * t.xh * t.xw, x, wt, y, d, t);
+             sizeof(float) * t.pb * t.xh * t.xw, x, wt, y, d, t, (int)planes);
   return 0;
 }
 
 // Blocks per channel of the fused backward: ~2048 blocks in all (8 per CU).
 int strip_groups(int64_t n, int64_t c, const DwStrip& t) {
-  const int64_t items = n * (int64_t)t.tx * t.ty;
+  const int64_t items = cdiv(n, t.pb) * (int64_t)t.tx * t.ty;
   int64_t g = cdiv(2048, c);
   if (g > items) g = items;
   return (int)(g < 1 ? 1 : g);
@@ -461,10 +527,10 @@ int strip_groups(int64_t n, int64_t c, const DwStrip& t) {
 template <int K, int S>
 int launch_bwd_strip(const float* gy, const float* x, const float* wt, float* gx, float* gw,
                      float* part, int64_t n, const DwShape& d, hipStream_t st) {
-  const DwStrip t = strip_tile(d, K, S);
+  const DwStrip t = strip_tile(d, K, S, n);
   const int G = strip_groups(n, d.c, t);
   float* dst = gw ? (G == 1 ? gw : part) : nullptr;
-  const size_t lds = sizeof(float) * (t.gh * t.gw + (gw ? t.xh * t.xw : 0));
+  const size_t lds = sizeof(float) * t.pb * (t.gh * t.gw + (gw ? t.xh * t.xw : 0));
   const double bytes =
       4.0 * n * d.c * (d.ho * d.wo + (gx ? d.h * d.w : 0) + (gw ? d.h * d.w : 0));
   MDE_LAUNCH(K_DW_BWD, bytes, st, (dw_bwd_strip_kernel<K, S>), dim3((unsigned)d.c, (unsigned)G),
@@ -511,7 +577,7 @@ size_t mde_dwconv_workspace(int64_t n, int64_t c, int64_t h, int64_t w, int64_t 
   if (!dw_ok(n, c, h, w, k, stride, pad)) return 0;
   const DwShape d = make_shape(c, h, w, k, stride, pad);
   if (pad == k / 2) {
-    const int G = strip_groups(n, c, strip_tile(d, (int)k, (int)stride));
+    const int G = strip_groups(n, c, strip_tile(d, (int)k, (int)stride, n));
     return G > 1 ? (size_t)(4 * c * G * k * k) : 0;
   }
   const DwTile t = out_tile(d, (int)k, (int)stride);

@@ -29,7 +29,8 @@ def close_scaled(a, b, tol, what):
     (2, 16, 240, 320, 3, 1), (2, 64, 240, 320, 3, 2), (3, 72, 120, 160, 5, 2),
     (2, 120, 60, 80, 5, 1), (2, 240, 60, 80, 3, 2), (2, 672, 30, 40, 5, 2),
     (2, 960, 15, 20, 5, 1), (1, 8, 7, 9, 3, 2), (1, 4, 5, 5, 5, 1), (2, 5, 17, 130, 3, 1),
-    (1, 3, 33, 67, 5, 2)])
+    (1, 3, 33, 67, 5, 2), (5, 7, 15, 20, 5, 1), (5, 7, 30, 40, 5, 2), (4, 3, 7, 9, 3, 2),
+    (9, 2, 4, 6, 3, 1)])
 def test_dwconv_matches_aten(n, c, h, w, k, s):
     _check_dwconv(n, c, h, w, k, s, k // 2)
 

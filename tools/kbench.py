@@ -2,7 +2,7 @@
 
     python tools/kbench.py [--reps 20]
 
-Times each op's forward and backward with torch.cuda.Event around `reps`
+Times each op's forward and backward from HIP-graph replays (10 calls per graph) over `reps`
 back-to-back calls (after 3 warm-ups) and prints algorithmic GB/s (SURVEY
 §8(d) byte formulas) against the 8 TB/s HBM peak.
 """
@@ -19,16 +19,33 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def timeit(fn, reps):
-    for _ in range(3):
-        fn()
+    """ms per call of fn, from replays of a HIP graph holding 10 calls (device
+    time without the host's launch overhead); eager timing if capture fails."""
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    inner = 10
+    try:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(inner):
+                fn()
+        run, outer = g.replay, max(1, reps // inner)
+    except RuntimeError:
+        run, outer, inner = fn, reps, 1
+    run()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(outer):
+        run()
     b.record()
     torch.cuda.synchronize()
-    return a.elapsed_time(b) / reps
+    return a.elapsed_time(b) / (outer * inner)
 
 
 def main():

@@ -268,23 +268,26 @@ DwStrip strip_tile(const DwShape& d, int k, int s, int64_t max_planes) {
   return t;
 }
 
-// tile[(p*ih + r)*iw + col] = src[p*pstride + (r0+r)*w + c0+col] for the np
-// planes p < np, zero outside the plane; all 256 threads walk the flattened
-// window with kChunk loads in flight (mih / miw: fdiv magics of ih / iw).
-__device__ __forceinline__ void stage_planes(const float* __restrict__ src, int64_t pstride,
-                                             int np, float* tile, int ih, int iw, unsigned mih,
-                                             unsigned miw, int r0, int c0, int h, int w) {
+template <bool STACKED>
+__device__ __forceinline__ void stage_planes_t(const float* __restrict__ src, int pstride, int np,
+                                               float* tile, int ih, int iw, unsigned mih,
+                                               unsigned miw, int r0, int c0, int h, int w) {
   const int total = np * ih * iw;
   for (int base = 0; base < total; base += 256 * kChunk) {
     float v[kChunk];
 #pragma unroll
     for (int j = 0; j < kChunk; ++j) {
       const int e = base + threadIdx.x + 256 * j;
-      const int sr = fdiv(e, miw), col = e - sr * iw;
-      const int p = fdiv(sr, mih), r = sr - p * ih;
+      const int sr = fdiv(e, miw), col = e - __mul24(sr, iw);
+      int p = 0, r = sr;
+      if (STACKED) {
+        p = fdiv(sr, mih);
+        r = sr - __mul24(p, ih);
+      }
       const int gr = r0 + r, gc = c0 + col;
-      const bool ok = e < total && gr >= 0 && gr < h && gc >= 0 && gc < w;
-      const float t = src[ok ? p * pstride + gr * w + gc : 0];
+      const bool ok = e < total && (unsigned)gr < (unsigned)h && (unsigned)gc < (unsigned)w;
+      const unsigned off = (STACKED ? (unsigned)(p * pstride) : 0u) + __mul24(gr, w) + gc;
+      const float t = src[ok ? off : 0u];
       v[j] = ok ? t : 0.f;
     }
 #pragma unroll
@@ -293,6 +296,20 @@ __device__ __forceinline__ void stage_planes(const float* __restrict__ src, int6
       if (e < total) tile[e] = v[j];
     }
   }
+}
+
+// tile[(p*ih + r)*iw + col] = src[p*pstride + (r0+r)*w + c0+col] for the np
+// planes p < np, zero outside the plane; all 256 threads walk the flattened
+// window with kChunk loads in flight (mih / miw: fdiv magics of ih / iw).
+// 32-bit offsets: dw_ok bounds every tensor to < 2^31 elements and planes to
+// < 2^24.
+__device__ __forceinline__ void stage_planes(const float* __restrict__ src, int64_t pstride,
+                                             int np, float* tile, int ih, int iw, unsigned mih,
+                                             unsigned miw, int r0, int c0, int h, int w) {
+  if (np == 1)
+    stage_planes_t<false>(src, 0, 1, tile, ih, iw, mih, miw, r0, c0, h, w);
+  else
+    stage_planes_t<true>(src, (int)pstride, np, tile, ih, iw, mih, miw, r0, c0, h, w);
 }
 
 // y[oy,ox] = sum_t w[t] x[oy*S-p+ky, ox*S-p+kx]; any padding p.
@@ -352,121 +369,173 @@ __global__ void __launch_bounds__(256)
 // staging of the gy window (+ the x window), so gy is read from HBM once.
 // Persistent over images: block (ch, g) walks items g, g+G, ... of the
 // channel's (image group, tile) items -- an image group is pb consecutive
-// images stacked in LDS -- keeps the K*K weight-gradient sums in registers
-// across items, and writes one partial per block (fixed order; G == 1 writes
+// images stacked in LDS.  Waves 0-1 compute the data gradient, waves 2-3 the
+// weight gradient (each thread covers strips s and s+128 of the tile), so no
+// thread holds both the k*k tap sums and the gy strip: ~60 VGPRs, 8 waves per
+// SIMD to hide the staging latency.  The weight-gradient sums stay in
+// registers across items; one partial per block (fixed order; G == 1 writes
 // gw directly).
 //   gx[S*oy+a, S*ox+b] = sum over (ky,kx) with (a+P-ky)%S == (b+P-kx)%S == 0 of
 //                        w[ky,kx] gy[oy + (a+P-ky)/S, ox + (b+P-kx)/S]
 //   gw[ky,kx]         += gy[oy,ox] x[S*oy-P+ky, S*ox-P+kx]
+struct StripPos {
+  int p, col, ly;  // stacked plane, tile column, first tile-local row
+  bool ok;         // strip exists (s < tw * rg * pb)
+};
+
+__device__ __forceinline__ StripPos strip_pos(int s, const DwStrip& t) {
+  const int per = t.tw * t.rg;
+  StripPos r;
+  r.p = s / per;
+  const int q = s - r.p * per;
+  r.col = q % t.tw;
+  r.ly = q / t.tw * kStripR;
+  r.ok = r.p < t.pb;
+  return r;
+}
+
+struct DwItem {
+  int oy0, ox0, img0, np;
+};
+
+template <int K, int S>
+__device__ __forceinline__ DwItem stage_item(int it, const DwStrip& t, int nn, int C, int H,
+                                             int W, int HO, int WO, int ch, const float* gy,
+                                             const float* x, float* gyt, float* xt,
+                                             bool want_gw) {
+  constexpr int P = K / 2, LO = strip_lo(K, S);
+  const int T = t.tx * t.ty;
+  const int grp = it / T, tl = it - grp * T;
+  const int tyi = tl / t.tx, txi = tl - tyi * t.tx;
+  DwItem m;
+  m.oy0 = tyi * t.th;
+  m.ox0 = txi * t.tw;
+  m.img0 = grp * t.pb;
+  m.np = nn - m.img0 < t.pb ? nn - m.img0 : t.pb;
+  __syncthreads();  // previous item's readers are done with the windows
+  stage_planes(gy + ((int64_t)m.img0 * C + ch) * HO * WO, (int64_t)C * HO * WO, m.np, gyt, t.gh,
+               t.gw, t.mgh, t.mgw, m.oy0 + LO, m.ox0 + LO, HO, WO);
+  if (want_gw)
+    stage_planes(x + ((int64_t)m.img0 * C + ch) * H * W, (int64_t)C * H * W, m.np, xt, t.xh,
+                 t.xw, t.mxh, t.mxw, m.oy0 * S - P, m.ox0 * S - P, H, W);
+  __syncthreads();
+  return m;
+}
+
+template <int K, int S>
+__device__ __forceinline__ void gx_strip(const StripPos& sp, const DwItem& m, const DwStrip& t,
+                                         const float* gyt, const float* wk, float* gx, int C,
+                                         int H, int W, int ch) {
+  constexpr int R = kStripR, P = K / 2;
+  constexpr int LO = strip_lo(K, S), HI = strip_hi(K, S);
+  constexpr int GR = R + HI - LO, GC = HI - LO + 1;
+  float gv[GR][GC];
+  const float* gp = gyt + (sp.p * t.gh + sp.ly) * t.gw + sp.col;
+#pragma unroll
+  for (int a = 0; a < GR; ++a)
+#pragma unroll
+    for (int b = 0; b < GC; ++b) gv[a][b] = gp[a * t.gw + b];
+  float* gxp = gx + ((int64_t)(m.img0 + sp.p) * C + ch) * H * W;
+#pragma unroll
+  for (int j = 0; j < R; ++j)
+#pragma unroll
+    for (int a = 0; a < S; ++a) {
+      const int iy = (m.oy0 + sp.ly + j) * S + a;
+#pragma unroll
+      for (int b = 0; b < S; ++b) {
+        const int ix = (m.ox0 + sp.col) * S + b;
+        float sacc = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky) {
+          if ((a + P - ky) % S != 0) continue;
+          const int ro = j + (a + P - ky) / S - LO;
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx) {
+            if ((b + P - kx) % S != 0) continue;
+            sacc = fmaf(wk[ky * K + kx], gv[ro][(b + P - kx) / S - LO], sacc);
+          }
+        }
+        if (iy < H && ix < W) gxp[iy * W + ix] = sacc;
+      }
+    }
+}
+
+template <int K, int S>
+__device__ __forceinline__ void gw_strip(const StripPos& sp, const DwStrip& t, const float* gyt,
+                                         const float* xt, float* acc) {
+  constexpr int R = kStripR, LO = strip_lo(K, S), XR = S * (R - 1) + K;
+  float go[R];
+#pragma unroll
+  for (int j = 0; j < R; ++j) go[j] = gyt[(sp.p * t.gh + sp.ly + j - LO) * t.gw + sp.col - LO];
+  const float* xp = xt + (sp.p * t.xh + sp.ly * S) * t.xw + sp.col * S;
+#pragma unroll
+  for (int r = 0; r < XR; ++r) {
+    float v[K];
+#pragma unroll
+    for (int kx = 0; kx < K; ++kx) v[kx] = xp[r * t.xw + kx];
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const int ky = r - S * j;
+      if (ky < 0 || ky >= K) continue;
+#pragma unroll
+      for (int kx = 0; kx < K; ++kx) acc[ky * K + kx] = fmaf(go[j], v[kx], acc[ky * K + kx]);
+    }
+  }
+}
+
 template <int K, int S>
 __global__ void __launch_bounds__(256)
     dw_bwd_strip_kernel(const float* __restrict__ gy, const float* __restrict__ x,
                         const float* __restrict__ wt, float* __restrict__ gx,
                         float* __restrict__ part, DwShape d, DwStrip t, int64_t n, int G) {
-  constexpr int R = kStripR, P = K / 2;
-  constexpr int LO = strip_lo(K, S), HI = strip_hi(K, S);
-  constexpr int GR = R + HI - LO, GC = HI - LO + 1;
-  constexpr int XR = S * (R - 1) + K;
   extern __shared__ float lds[];
-  __shared__ float red[4][K * K];
+  __shared__ float red[2][K * K];
   float* gyt = lds;
   float* xt = lds + t.pb * t.gh * t.gw;
   const int H = (int)d.h, W = (int)d.w, HO = (int)d.ho, WO = (int)d.wo, C = (int)d.c;
-  const int ch = blockIdx.x;
-  const int g = blockIdx.y;
+  const int ch = blockIdx.x, g = blockIdx.y, nn = (int)n;
   const bool want_gx = gx != nullptr, want_gw = part != nullptr;
-  float wk[K * K], acc[K * K];
+  const int items = (nn + t.pb - 1) / t.pb * (t.tx * t.ty);
+  const StripPos sa = strip_pos(threadIdx.x & 127, t), sb = strip_pos((threadIdx.x & 127) + 128, t);
+  if (threadIdx.x < 128) {  // data-gradient waves
+    float wk[K * K];
 #pragma unroll
-  for (int i = 0; i < K * K; ++i) {
-    wk[i] = want_gx ? wt[ch * K * K + i] : 0.f;
-    acc[i] = 0.f;
-  }
-  const int per = t.tw * t.rg;
-  const int p = threadIdx.x / per, q = threadIdx.x - p * per;
-  const int col = q % t.tw, rgi = q / t.tw;
-  const int ly = rgi * R;  // first tile-local output row of this strip
-  const int nn = (int)n;
-  const int T = t.tx * t.ty, items = (nn + t.pb - 1) / t.pb * T;
-  const int64_t gys = (int64_t)C * HO * WO, xs = (int64_t)C * H * W;  // image strides
-  for (int it = g; it < items; it += G) {
-    const int grp = it / T, tl = it - grp * T;
-    const int tyi = tl / t.tx, txi = tl - tyi * t.tx;
-    const int oy0 = tyi * t.th, ox0 = txi * t.tw;
-    const int img0 = grp * t.pb;
-    const int np = nn - img0 < t.pb ? nn - img0 : t.pb;
-    __syncthreads();  // previous item's readers are done with the windows
-    stage_planes(gy + ((int64_t)img0 * C + ch) * HO * WO, gys, np, gyt, t.gh, t.gw, t.mgh, t.mgw,
-                 oy0 + LO,
-                 ox0 + LO, HO, WO);
-    if (want_gw)
-      stage_planes(x + ((int64_t)img0 * C + ch) * H * W, xs, np, xt, t.xh, t.xw, t.mxh, t.mxw,
-                   oy0 * S - P,
-                   ox0 * S - P, H, W);
-    __syncthreads();
-    if (p >= np) continue;
-    if (want_gx) {
-      float gv[GR][GC];
-      const float* gp = gyt + (p * t.gh + ly) * t.gw + col;
-#pragma unroll
-      for (int a = 0; a < GR; ++a)
-#pragma unroll
-        for (int b = 0; b < GC; ++b) gv[a][b] = gp[a * t.gw + b];
-      float* gxp = gx + ((int64_t)(img0 + p) * C + ch) * H * W;
-#pragma unroll
-      for (int j = 0; j < R; ++j)
-#pragma unroll
-        for (int a = 0; a < S; ++a) {
-          const int iy = (oy0 + ly + j) * S + a;
-#pragma unroll
-          for (int b = 0; b < S; ++b) {
-            const int ix = (ox0 + col) * S + b;
-            float sacc = 0.f;
-#pragma unroll
-            for (int ky = 0; ky < K; ++ky) {
-              if ((a + P - ky) % S != 0) continue;
-              const int ro = j + (a + P - ky) / S - LO;
-#pragma unroll
-              for (int kx = 0; kx < K; ++kx) {
-                if ((b + P - kx) % S != 0) continue;
-                sacc = fmaf(wk[ky * K + kx], gv[ro][(b + P - kx) / S - LO], sacc);
-              }
-            }
-            if (iy < H && ix < W) gxp[iy * W + ix] = sacc;
-          }
-        }
-    }
-    if (want_gw) {
-      float go[R];
-#pragma unroll
-      for (int j = 0; j < R; ++j) go[j] = gyt[(p * t.gh + ly + j - LO) * t.gw + col - LO];
-      const float* xp = xt + (p * t.xh + ly * S) * t.xw + col * S;
-#pragma unroll
-      for (int r = 0; r < XR; ++r) {
-        float v[K];
-#pragma unroll
-        for (int kx = 0; kx < K; ++kx) v[kx] = xp[r * t.xw + kx];
-#pragma unroll
-        for (int j = 0; j < R; ++j) {
-          const int ky = r - S * j;
-          if (ky < 0 || ky >= K) continue;
-#pragma unroll
-          for (int kx = 0; kx < K; ++kx)
-            acc[ky * K + kx] = fmaf(go[j], v[kx], acc[ky * K + kx]);
-        }
+    for (int i = 0; i < K * K; ++i) wk[i] = want_gx ? wt[ch * K * K + i] : 0.f;
+    for (int it = g; it < items; it += G) {
+      const DwItem m =
+          stage_item<K, S>(it, t, nn, C, H, W, HO, WO, ch, gy, x, gyt, xt, want_gw);
+      if (!want_gx) continue;
+#pragma unroll 1
+      for (int k = 0; k < 2; ++k) {
+        const StripPos sp = k ? sb : sa;
+        if (sp.ok && sp.p < m.np) gx_strip<K, S>(sp, m, t, gyt, wk, gx, C, H, W, ch);
       }
     }
-  }
-  if (!want_gw) return;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  } else {  // weight-gradient waves
+    float acc[K * K];
 #pragma unroll
-  for (int i = 0; i < K * K; ++i) {
-    const float v = wave_sum(acc[i]);
-    if (lane == 0) red[wid][i] = v;
+    for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+    for (int it = g; it < items; it += G) {
+      const DwItem m =
+          stage_item<K, S>(it, t, nn, C, H, W, HO, WO, ch, gy, x, gyt, xt, want_gw);
+      if (!want_gw) continue;
+#pragma unroll 1
+      for (int k = 0; k < 2; ++k) {
+        const StripPos sp = k ? sb : sa;
+        if (sp.ok && sp.p < m.np) gw_strip<K, S>(sp, t, gyt, xt, acc);
+      }
+    }
+    const int lane = threadIdx.x & 63, wid = (threadIdx.x >> 6) - 2;
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+      const float v = wave_sum(acc[i]);
+      if (lane == 0) red[wid][i] = v;
+    }
   }
   __syncthreads();
-  if (threadIdx.x < K * K) {
+  if (want_gw && threadIdx.x < K * K) {
     const int i = threadIdx.x;
-    part[((int64_t)ch * G + g) * K * K + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    part[((int64_t)ch * G + g) * K * K + i] = red[0][i] + red[1][i];
   }
 }
 
@@ -474,6 +543,7 @@ bool dw_ok(int64_t n, int64_t c, int64_t h, int64_t w, int64_t k, int64_t stride
            int64_t pad) {
   return n > 0 && c > 0 && h > 0 && w > 0 && (k == 3 || k == 5) &&
          (stride == 1 || stride == 2) && pad >= 0 && pad < k && n * c <= 65535 &&
+         n * c * h * w < (int64_t(1) << 31) && h * w < (int64_t(1) << 24) &&
          (h + 2 * pad - k) >= 0 && (w + 2 * pad - k) >= 0;
 }
 

@@ -18,37 +18,42 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+_STREAM = None  # every op, its forward for a backward timing, and the captures run here
+
+
 def timeit(fn, reps):
     """ms per call of fn, from replays of a HIP graph holding 10 calls (device
-    time without the host's launch overhead); eager timing if capture fails."""
-    side = torch.cuda.Stream()
-    side.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(side):
-        for _ in range(3):
-            fn()
-    torch.cuda.current_stream().wait_stream(side)
+    time without the host's launch overhead).  The graph is captured on the
+    stream main() runs everything on, which is also the stream the autograd
+    backward of a forward made there launches on."""
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     inner = 10
-    try:
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            for _ in range(inner):
-                fn()
-        run, outer = g.replay, max(1, reps // inner)
-    except RuntimeError:
-        run, outer, inner = fn, reps, 1
-    run()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=_STREAM):
+        for _ in range(inner):
+            fn()
+    outer = max(1, reps // inner)
+    g.replay()
     torch.cuda.synchronize()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
     for _ in range(outer):
-        run()
+        g.replay()
     b.record()
     torch.cuda.synchronize()
     return a.elapsed_time(b) / (outer * inner)
 
 
 def main():
+    global _STREAM
+    _STREAM = torch.cuda.Stream()
+    with torch.cuda.stream(_STREAM):
+        _main()
+
+
+def _main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default="")

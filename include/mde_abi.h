@@ -372,6 +372,27 @@ int mde_transpose(const void* x, void* y, int64_t batch, int64_t m, int64_t n, i
                   void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Depth-evaluation error sums (evaluation).  Replaces the
+ * host numpy path of src/test.py:96-124 (pred clamp :105-108, range mask
+ * :110, Eigen crop :114-117, utils.compute_errors src/utils.py:45-66) and the
+ * FastDepth Result.evaluate of src/GuideDepth/metrics.py:41-62.
+ *   pred, gt [n, h, w] fp32 (a [n,1,h,w] map is the same memory).
+ *   mode bit 0: pred clamped to [min_depth, max_depth] (NaN -> min_depth) and
+ *               only pixels with min_depth < gt < max_depth counted;
+ *   mode bit 1: only rows [crop[0], crop[1]) x cols [crop[2], crop[3]) counted
+ *               (crop is a HOST int32[4]; NULL when bit 1 is clear).
+ *   sums: DEVICE double[16] = count, #(delta < 1.25^k) k=1..3, sum (g-p)^2,
+ *   sum (ln g - ln p)^2, sum |g-p|/g, sum (g-p)^2/g, sum (ln p - ln g),
+ *   sum |log10 p - log10 g|, sum |g-p|, sum (log10 p - log10 g)^2,
+ *   sum |1/p - 1/g|, sum (1/p - 1/g)^2, 0, 0 -- every metric of both
+ *   reference functions is a closed form of these.  Deterministic.
+ * ------------------------------------------------------------------------- */
+size_t mde_eval_workspace(int64_t n, int64_t h, int64_t w);
+int mde_eval_sums(const void* pred, const void* gt, int64_t n, int64_t h, int64_t w,
+                  float min_depth, float max_depth, int mode, const int32_t* crop,
+                  void* workspace, double* sums, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).
  * When enabled, every launch made through this ABI is bracketed by hipEvents
  * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY

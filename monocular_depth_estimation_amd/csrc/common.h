@@ -57,6 +57,8 @@ enum Kid : int {
   K_C3_WGRAD,
   K_C3_WREDUCE,
   K_DW_BWD,
+  K_EVAL,
+  K_EVAL_FINAL,
   K_COUNT
 };
 

@@ -380,3 +380,50 @@ def depth_loss(output, depth, alpha, beta, gamma, max_depth=10.0):
     if depth.requires_grad:
         raise ValueError("Depth_Loss: the ground-truth depth must not require grad")
     return _DepthLoss.apply(output, depth, alpha, beta, gamma, max_depth)
+
+
+# ----------------------------------------------------------------- evaluation
+def eigen_crop(h: int, w: int) -> tuple[int, int, int, int]:
+    """The Garg/Eigen crop of src/test.py:114-115 (rows [0], [1]; cols [2], [3])."""
+    import numpy as np
+    return tuple(int(v) for v in np.array([int(0.09375 * h), int(0.98125 * h),
+                                           int(0.0640625 * w), int(0.9390625 * w)]).astype(np.int32))
+
+
+def eval_sums(pred: torch.Tensor, gt: torch.Tensor, min_depth: float = 0.0, max_depth: float = 0.0,
+              clamp_and_mask: bool = False, crop: tuple[int, int, int, int] | None = None
+              ) -> torch.Tensor:
+    """Device float64 [16] error sums of mde_eval_sums over pred / gt maps
+    ([n, h, w] or [n, 1, h, w]; a 1-D tensor is one row).  See include/mde_abi.h."""
+    _gpu(pred)
+    if pred.shape != gt.shape:
+        raise ValueError(f"pred {tuple(pred.shape)} / gt {tuple(gt.shape)}")
+    pred = pred.detach().contiguous()
+    gt = gt.detach().contiguous()
+    if pred.dim() == 4:
+        if pred.shape[1] != 1:
+            raise ValueError(f"depth maps have one channel, got {tuple(pred.shape)}")
+        n, h, w = pred.shape[0], pred.shape[2], pred.shape[3]
+    elif pred.dim() == 3:
+        n, h, w = pred.shape
+    elif pred.dim() == 2:
+        n, h, w = 1, pred.shape[0], pred.shape[1]
+    elif pred.dim() == 1:
+        n, h, w = 1, 1, pred.shape[0]
+    else:
+        raise ValueError(f"unsupported map shape {tuple(pred.shape)}")
+    out = torch.empty(16, dtype=torch.float64, device=pred.device)
+    if pred.numel() == 0:
+        return out.zero_()
+    mode = (1 if clamp_and_mask else 0) | (2 if crop is not None else 0)
+    c = (_c_int4(crop) if crop is not None else None)
+    ws = _ws(_abi.query("mde_eval_workspace", n, h, w), pred)
+    _abi.call("mde_eval_sums", _abi.ptr(pred), _abi.ptr(gt), n, h, w, float(min_depth),
+              float(max_depth), mode, c, _abi.ptr(ws), _abi.ptr(out), _abi.dtype_code(pred),
+              _abi.stream_of(pred))
+    return out
+
+
+def _c_int4(v):
+    import ctypes
+    return (ctypes.c_int32 * 4)(*[int(x) for x in v])

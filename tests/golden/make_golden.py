@@ -320,13 +320,59 @@ def capture_newcrf():
     return out
 
 
+def capture_metrics():
+    """utils.compute_errors (src/utils.py:45-66) on the pixels src/test.py:105-118
+    keeps (clamp / range mask / Eigen crop, restated inline as test.py is a
+    script), on plain positive arrays, and GuideDepth/metrics.py Result.evaluate."""
+    import utils as refutils
+    from GuideDepth.metrics import Result
+    out = {}
+    rng = np.random.default_rng(7)
+    n, h, w = 3, 48, 64
+    depth = torch.from_numpy(rng.uniform(0.1, 10.0, (n, 1, h, w)).astype(np.float32))
+    gt = refutils.DepthNorm(depth).numpy().squeeze()          # test.py:91,100
+    gt[0, 10:14, 10:20] = 0.0005                               # below min_depth_eval
+    pred = rng.uniform(-0.05, 1.1, (n, h, w)).astype(np.float32)
+    pred[1, 20, 5:9] = [np.inf, -np.inf, np.nan, 100.0]
+    pred[2, 30, 30] = np.nan
+    out["metrics::gt"], out["metrics::pred"] = gt.copy(), pred.copy()
+    lo, hi = 1e-3, 80.0                                        # test.py:34-35 defaults
+    p = pred.copy()
+    p[p < lo] = lo
+    p[p > hi] = hi
+    p[np.isinf(p)] = hi
+    p[np.isnan(p)] = lo
+    mask = np.logical_and(gt > lo, gt < hi)
+    crop = np.array([int(0.09375 * h), int(0.98125 * h), int(0.0640625 * w),
+                     int(0.9390625 * w)]).astype(np.int32)
+    cm = np.zeros(mask.shape)
+    cm[:, crop[0]:crop[1], crop[2]:crop[3]] = 1
+    mask = np.logical_and(mask, cm)
+    out["metrics::batch"] = np.array(refutils.compute_errors(gt[mask], p[mask]), dtype=np.float64)
+    g2 = rng.uniform(0.05, 10.0, 5000).astype(np.float32)
+    p2 = (g2 * rng.uniform(0.6, 1.6, 5000)).astype(np.float32)
+    out["metrics::plain_gt"], out["metrics::plain_pred"] = g2, p2
+    out["metrics::plain"] = np.array(refutils.compute_errors(g2, p2), dtype=np.float64)
+    t = torch.from_numpy(rng.uniform(0.1, 10.0, (2, 1, 24, 32)).astype(np.float32))
+    o = (t * torch.from_numpy(rng.uniform(0.7, 1.4, (2, 1, 24, 32)).astype(np.float32)))
+    r = Result()
+    r.evaluate(o, t)
+    out["metrics::fd_output"], out["metrics::fd_target"] = f32(o), f32(t)
+    fields = ("mse", "rmse", "mae", "lg10", "rmse_log", "absrel", "delta1", "delta2", "delta3",
+              "irmse", "imae")
+    out["metrics::fd_fields"] = np.array(fields)
+    out["metrics::fd"] = np.array([float(getattr(r, f)) for f in fields], dtype=np.float64)
+    return out
+
+
 def main():
     _import_reference()
     torch.manual_seed(0)
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     jobs = {"golden_resize.npz": capture_resize, "golden_blocks.npz": capture_blocks,
             "golden_losses.npz": capture_losses, "golden_guidedepth.npz": capture_guidedepth,
-            "golden_trainseq.npz": capture_train_sequence, "golden_newcrf.npz": capture_newcrf}
+            "golden_trainseq.npz": capture_train_sequence, "golden_newcrf.npz": capture_newcrf,
+            "golden_metrics.npz": capture_metrics}
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():
         if only and fname not in only:

@@ -202,3 +202,16 @@ def test_train_sequence_matches_reference(golden):
     np.testing.assert_allclose(losses[0], g["losses"][0], rtol=1e-6)
     np.testing.assert_allclose(losses, g["losses"], rtol=5e-3)
     close_map(model.up_3.reduce.weight, g["final_up3_reduce_weight"], 1e-2, "up_3.reduce.weight")
+
+
+def test_metrics_oracle_matches_reference(golden):
+    """oracle/metrics.py vs the reference's compute_errors / Result.evaluate."""
+    from oracle import metrics as om
+    g = golden("golden_metrics.npz")
+    np.testing.assert_allclose(om.batch_errors(g["metrics::gt"], g["metrics::pred"]),
+                               g["metrics::batch"], rtol=1e-6)
+    np.testing.assert_allclose(om.compute_errors(g["metrics::plain_gt"], g["metrics::plain_pred"]),
+                               g["metrics::plain"], rtol=1e-6)
+    r = om.fastdepth_evaluate(torch.from_numpy(g["metrics::fd_output"]),
+                              torch.from_numpy(g["metrics::fd_target"]))
+    np.testing.assert_allclose([r[f] for f in g["metrics::fd_fields"]], g["metrics::fd"], rtol=1e-6)

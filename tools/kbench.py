@@ -150,6 +150,10 @@ def _main():
         report("ssim3_l1 fwd+grad 480x640", timeit(lambda: F.ssim3_l1(p, t, 1.0, 0.1, target_minmax=mm),
                                                    a.reps), 3 * 4.0 * n * 480 * 640)
         report("minmax 480x640", timeit(lambda: F.minmax(t), a.reps), 4.0 * n * 480 * 640)
+        crop = F.eigen_crop(480, 640)
+        report("eval_sums (test.py batch) 480x640",
+               timeit(lambda: F.eval_sums(p.detach(), t, 1e-3, 80.0, True, crop), a.reps),
+               8.0 * n * 480 * 640)
     # --- cfg4 (PTModel, bs 16) ops
     n4 = 16
     if want("attn"):

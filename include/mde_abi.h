@@ -372,6 +372,22 @@ int mde_transpose(const void* x, void* y, int64_t batch, int64_t m, int64_t n, i
                   void* stream);
 
 /* ---------------------------------------------------------------------------
+ * NYU-Depth-V2 batch augmentation (data pipeline).
+ * Replaces the host transforms RandomHorizontalFlip / RandomChannelSwap /
+ * ToTensor of src/data.py:16-46,100-168 for a decoded uint8 batch:
+ *   image [n, h, w, 3] uint8 (HWC, PIL order), depth [n, dh, dw] uint8
+ *   (depth_bits 8: 'L' PNG, divided by 255) or int16 (depth_bits 16: 'I;16'
+ *   PNG viewed as np.int16, not scaled), flags DEVICE int32 [n, 2] =
+ *   {flip, k}: flip != 0 mirrors both maps, k in 0..5 permutes the image's
+ *   channels by itertools.permutations(range(3))[k] (k = -1: none).
+ *   image_out [n, 3, h, w], depth_out [n, 1, dh, dw] fp32 (bit-exact with
+ *   the reference's ToTensor).
+ * ------------------------------------------------------------------------- */
+int mde_nyu_augment(const void* image, const void* depth, const int32_t* flags, float* image_out,
+                    float* depth_out, int64_t n, int64_t h, int64_t w, int64_t dh, int64_t dw,
+                    int depth_bits, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Depth-evaluation error sums (evaluation).  Replaces the
  * host numpy path of src/test.py:96-124 (pred clamp :105-108, range mask
  * :110, Eigen crop :114-117, utils.compute_errors src/utils.py:45-66) and the

@@ -89,6 +89,7 @@ SIGNATURES = {
     "mde_layernorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _int,
                                  _vp]),
     "mde_transpose": (_int, [_vp, _vp, _i64, _i64, _i64, _int, _vp]),
+    "mde_nyu_augment": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_eval_workspace": (_sz, [_i64, _i64, _i64]),
     "mde_eval_sums": (_int, [_vp, _vp, _i64, _i64, _i64, _f32, _f32, _int, _c.POINTER(_c.c_int32), _vp,
                              _vp, _int, _vp]),

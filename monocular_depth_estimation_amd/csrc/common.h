@@ -59,6 +59,7 @@ enum Kid : int {
   K_DW_BWD,
   K_EVAL,
   K_EVAL_FINAL,
+  K_NYU_AUGMENT,
   K_COUNT
 };
 

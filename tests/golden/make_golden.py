@@ -365,6 +365,74 @@ def capture_metrics():
     return out
 
 
+def _nyu_zip(path, n_train=12, n_test=5, h=6, w=10):
+    """A miniature CSVdata.zip: data/nyu2_{train,test}.csv + RGB JPEG-free PNG pairs."""
+    import zipfile
+    from PIL import Image
+    rng = np.random.default_rng(5)
+    rows = {"train": [], "test": []}
+    with zipfile.ZipFile(path, "w") as z:
+        for split, count in (("train", n_train), ("test", n_test)):
+            for i in range(count):
+                a = f"data/nyu2_{split}/scene_{i % 3}/{i}.png"
+                b = f"data/nyu2_{split}/scene_{i % 3}/{i}_depth.png"
+                for name, arr in ((a, rng.integers(0, 256, (h, w, 3), dtype=np.uint8)),
+                                  (b, rng.integers(0, 256, (h, w), dtype=np.uint8))):
+                    buf = __import__("io").BytesIO()
+                    Image.fromarray(arr).save(buf, format="PNG")
+                    z.writestr(name, buf.getvalue())
+                rows[split].append(f"{a},{b}")
+            z.writestr(f"data/nyu2_{split}.csv", "\n".join(rows[split]) + "\n")
+    return rows
+
+
+def capture_data():
+    """src/data.py: getDefaultTrainTransform / getNoTransform on seeded `random`
+    draws (torchvision.transforms.Compose stubbed: data.py only composes), and
+    loadZipToMem's shuffled train / test rows on a miniature zip."""
+    import random as pyrandom
+    import tempfile
+    from PIL import Image
+    tv = sys.modules.get("torchvision") or types.ModuleType("torchvision")
+    tr = types.ModuleType("torchvision.transforms")
+
+    class Compose:
+        def __init__(self, ts):
+            self.ts = ts
+
+        def __call__(self, s):
+            for t in self.ts:
+                s = t(s)
+            return s
+
+    tr.Compose = Compose
+    tv.transforms, tv.utils = tr, types.ModuleType("torchvision.utils")
+    sys.modules["torchvision"], sys.modules["torchvision.transforms"] = tv, tr
+    sys.modules["torchvision.utils"] = tv.utils
+    import data as refdata
+    out = {}
+    rng = np.random.default_rng(9)
+    imgs = rng.integers(0, 256, (2, 6, 10, 3), dtype=np.uint8)
+    deps = rng.integers(0, 256, (2, 6, 10), dtype=np.uint8)
+    out["data::img"], out["data::dep"] = imgs, deps
+    seeds = np.arange(100, 116)
+    out["data::seeds"] = seeds
+    for i, sd in enumerate(seeds):
+        pyrandom.seed(int(sd))
+        s = refdata.getDefaultTrainTransform()({"image": Image.fromarray(imgs[i % 2]),
+                                                "depth": Image.fromarray(deps[i % 2])})
+        out[f"data::train{i}::image"], out[f"data::train{i}::depth"] = f32(s["image"]), f32(s["depth"])
+    s = refdata.getNoTransform()({"image": Image.fromarray(imgs[0]), "depth": Image.fromarray(deps[0])})
+    out["data::test::image"], out["data::test::depth"] = f32(s["image"]), f32(s["depth"])
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "CSVdata.zip")
+        _nyu_zip(path)
+        _, train, test = refdata.loadZipToMem(path)
+    out["data::zip_train"] = np.array([",".join(r) for r in train])
+    out["data::zip_test"] = np.array([",".join(r) for r in test])
+    return out
+
+
 def main():
     _import_reference()
     torch.manual_seed(0)
@@ -372,7 +440,7 @@ def main():
     jobs = {"golden_resize.npz": capture_resize, "golden_blocks.npz": capture_blocks,
             "golden_losses.npz": capture_losses, "golden_guidedepth.npz": capture_guidedepth,
             "golden_trainseq.npz": capture_train_sequence, "golden_newcrf.npz": capture_newcrf,
-            "golden_metrics.npz": capture_metrics}
+            "golden_metrics.npz": capture_metrics, "golden_data.npz": capture_data}
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():
         if only and fname not in only:

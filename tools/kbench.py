@@ -150,6 +150,12 @@ def _main():
         report("ssim3_l1 fwd+grad 480x640", timeit(lambda: F.ssim3_l1(p, t, 1.0, 0.1, target_minmax=mm),
                                                    a.reps), 3 * 4.0 * n * 480 * 640)
         report("minmax 480x640", timeit(lambda: F.minmax(t), a.reps), 4.0 * n * 480 * 640)
+        from monocular_depth_estimation_amd.data import nyu_augment
+        img_u8 = torch.randint(0, 256, (n, 480, 640, 3), dtype=torch.uint8, device=dev)
+        dep_u8 = torch.randint(0, 256, (n, 480, 640), dtype=torch.uint8, device=dev)
+        flg = torch.tensor([(i % 2, i % 7 - 1) for i in range(n)], dtype=torch.int32, device=dev)
+        report("nyu_augment 32x480x640 (uint8 -> fp32)",
+               timeit(lambda: nyu_augment(img_u8, dep_u8, flg), a.reps), 20.0 * n * 480 * 640)
         crop = F.eigen_crop(480, 640)
         report("eval_sums (test.py batch) 480x640",
                timeit(lambda: F.eval_sums(p.detach(), t, 1e-3, 80.0, True, crop), a.reps),

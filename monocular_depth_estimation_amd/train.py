@@ -313,6 +313,8 @@ def build_parser():
     p.add_argument("--height", default=480, type=int)
     p.add_argument("--width", default=640, type=int)
     p.add_argument("--steps-per-epoch", default=100, type=int, help="synthetic epoch length")
+    p.add_argument("--data", default="", help="NYU CSVdata.zip (data.py:172); empty = synthetic batches")
+    p.add_argument("--workers", default=4, type=int, help="decode workers of the NYU loader")
     p.add_argument("--checkpoint", default="checkpoints/global_checkpoint.pth")
     p.add_argument("--no-eval-quirk", action="store_true",
                    help="keep BN in train mode all epoch (the reference switches to eval after step 0)")
@@ -338,23 +340,39 @@ def main(argv=None):
     trainer = Trainer(ddp, optimizer, SSIML1(1.0, 0.1, depth_norm=True), world,
                       eval_quirk=not args.no_eval_quirk)
     log = open(args.log, "a") if (args.log and world.is_main) else None
+    loader = None
+    if args.data:  # data.py:171-179 on the GPU path; each rank reads a disjoint 1/size of the rows
+        from .data import NYUBatchLoader, loadZipToMem
+        data, nyu2_train, _ = loadZipToMem(args.data)
+        loader = NYUBatchLoader(data, nyu2_train[world.rank::world.size], args.bs, train=True,
+                                shuffle=True, num_workers=args.workers, device=world.device,
+                                drop_last=True)
+
+    def batches(epoch):
+        if loader is not None:
+            for b in loader:
+                yield b["image"], b["depth"]
+            return
+        for pos in range(args.steps_per_epoch):
+            yield synthetic_batch(args.bs, args.height, args.width, world.rank,
+                                  epoch * args.steps_per_epoch + pos, world.device, args.seed)
+
     for epoch in range(start_epoch, args.epochs):
         trainer.begin_epoch()
         losses, t0 = AverageMeter(), time.time()
-        for pos in range(args.steps_per_epoch):
-            image, depth = synthetic_batch(args.bs, args.height, args.width, world.rank,
-                                           epoch * args.steps_per_epoch + pos, world.device, args.seed)
+        n_steps = len(loader) if loader is not None else args.steps_per_epoch
+        for pos, (image, depth) in enumerate(batches(epoch)):
             loss = trainer.step(image, depth)
             trainer.after_step(pos)
             if pos % 5 == 0 and world.is_main:  # train.py:123-132 (host read at log points only)
                 v = float(loss)
                 losses.update(v, image.size(0))
                 dt = time.time() - t0
-                print(f"Epoch: [{epoch}][{pos}/{args.steps_per_epoch}]\tTime {dt:.3f}\t"
+                print(f"Epoch: [{epoch}][{pos}/{n_steps}]\tTime {dt:.3f}\t"
                       f"Loss {losses.val:.4f} ({losses.avg:.4f})", flush=True)
                 if log:
                     log.write(json.dumps({"tag": "Train/Loss", "value": v,
-                                          "step": epoch * args.steps_per_epoch + pos}) + "\n")
+                                          "step": epoch * n_steps + pos}) + "\n")
         if world.is_main:
             if log:
                 log.write(json.dumps({"tag": "Train/Loss.avg", "value": losses.avg, "step": epoch}) + "\n")

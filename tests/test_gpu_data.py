@@ -82,3 +82,17 @@ def test_loader_end_to_end(tmp_path):
     img, dep = decode_sample(data, test[0])
     ri, _ = od.augment(img, dep, 0, -1)
     np.testing.assert_array_equal(b["image"][0].cpu().numpy(), ri)
+
+
+def test_train_cli_on_nyu_zip(tmp_path):
+    """The drop-in train.py CLI with --data: one epoch over a miniature zip
+    (64 x 96 RGB + 8-bit depth), checkpoint written."""
+    from monocular_depth_estimation_amd.train import main
+    path = tmp_path / "CSVdata.zip"
+    _nyu_zip(str(path), n_train=8, n_test=2, h=64, w=96)
+    ckpt = tmp_path / "ckpt.pth"
+    main(["--epochs", "1", "--bs", "4", "--data", str(path), "--workers", "0",
+          "--checkpoint", str(ckpt)])
+    state = torch.load(str(ckpt), map_location="cpu", weights_only=True)
+    assert state["epoch"] == 0 and "model_state_dict" in state
+    assert bool(torch.isfinite(state["loss"]).all())

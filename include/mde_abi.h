@@ -255,6 +255,10 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
  *   qk      [b, h*w, 2c]  qk Linear output of the REAL tokens (q | k halves)
  *   qk_bias [2c]          that Linear's bias = q, k of zero-padded tokens
  *   v       [b, h, w, c]  value tokens (not projected; split into c/32 heads)
+ *   v_bias  [c] or NULL   v of a zero-padded token: NULL = 0 (NewCRF, v is not
+ *                         projected); SAM's cross-window attention
+ *                         (src/SAM.py:111-144, 195-244) projects v with the kv
+ *                         Linear after padding, so its padded v is that bias
  *   table   [(2*window-1)^2, heads] relative position bias table
  *   out     [b, h*w, c]   attention output in token order (before proj)
  * shift = 0 (W-MSA) or window/2 (SW-MSA, with the -100 region mask).
@@ -262,16 +266,17 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
 size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
                                  int64_t heads, int64_t window);
 int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
-                        const float* table, void* out, int64_t b, int64_t h,
-                        int64_t w, int64_t c, int64_t heads, int64_t window,
+                        const float* v_bias, const float* table, void* out, int64_t b,
+                        int64_t h, int64_t w, int64_t c, int64_t heads, int64_t window,
                         int64_t shift, int dtype, void* stream);
 /* gqk [b,h*w,2c] and gv [b,h,w,c] are fully overwritten; gtable and gqk_bias
  * (the contribution of the padded tokens only: q half 0, k half = sum of the
- * padded keys' gradients) are overwritten. */
+ * padded keys' gradients) are overwritten; gv_bias (nullable, needs v_bias)
+ * receives the padded values' gradient sum. */
 int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
-                        const void* v, const float* table, void* gqk, void* gv,
-                        float* gtable, float* gqk_bias, int64_t b, int64_t h,
-                        int64_t w, int64_t c, int64_t heads, int64_t window,
+                        const void* v, const float* v_bias, const float* table, void* gqk,
+                        void* gv, float* gtable, float* gqk_bias, float* gv_bias, int64_t b,
+                        int64_t h, int64_t w, int64_t c, int64_t heads, int64_t window,
                         int64_t shift, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------

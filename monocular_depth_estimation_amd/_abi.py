@@ -60,10 +60,10 @@ SIGNATURES = {
     "mde_batchnorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _int, _vp, _int, _vp]),
     "mde_window_attn_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64]),
-    "mde_window_attn_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
+    "mde_window_attn_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
                                    _i64, _int, _vp]),
-    "mde_window_attn_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
-                                   _i64, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_window_attn_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64,
+                                   _i64, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_se_gate_fwd": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp,
                                _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_se_gate_bwd": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i64, _int, _vp, _vp, _vp,

@@ -52,6 +52,7 @@ constexpr int kWinBwd = 4;   // windows per backward block
 struct Geo {
   int b, h, w, c, heads, ws, shift, hp, wp, nwh, nww, n;
   float scale;
+  const float* vb;  // v of a padded token (SAM: the kv Linear's v bias); NULL = 0 (NewCRF)
 };
 
 __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
@@ -238,7 +239,7 @@ __global__ void __launch_bounds__(256)
       const int t = tok[16 * jt + 4 * g4 + r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
-        vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, nullptr);
+        vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, g.vb);
     }
   float* orow = out + img * g.c;
 #pragma unroll
@@ -290,7 +291,7 @@ __device__ __forceinline__ void mm_tb_tile(float (*T)[LT], int jt, const float b
     }
 }
 
-// slab[(blockIdx.x * heads + head) * (ntab + D)] = {dT[0..ntab), dkbias[0..D)}
+// slab[(blockIdx.x * heads + head) * (ntab + 2D)] = {dT[0..ntab), dkbias[0..D), dvbias[0..D)}
 template <int WS>
 __global__ void __launch_bounds__(256, 2)
     wattn_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ qk,
@@ -311,6 +312,7 @@ __global__ void __launch_bounds__(256, 2)
       dtab[w][e] = 0.f;
     }
   float dkb[2] = {0.f, 0.f};  // d(k bias)[16ct + l16] partial of this lane
+  float dvb[2] = {0.f, 0.f};  // d(v bias): dV of the padded keys (g.vb only)
   for (int wi = 0; wi < kWinBwd; ++wi) {
     const int win = blockIdx.x * kWinBwd + wi;
     if (win >= nwin) break;  // uniform across the block
@@ -353,6 +355,9 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct)
                 gvrow[(unsigned)(t * c + hd + 16 * ct + l16)] = o[ct][rr];
+            } else if (t == -1 && g.vb) {
+#pragma unroll
+              for (int ct = 0; ct < 2; ++ct) dvb[ct] += o[ct][rr];
             }
           }
         }
@@ -363,7 +368,7 @@ __global__ void __launch_bounds__(256, 2)
         float va[4][8];
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
-          row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], nullptr, va[jt]);
+          row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], g.vb, va[jt]);
 #pragma unroll
         for (int it = 0; it < 4; ++it) {
           float db[8];
@@ -472,29 +477,34 @@ __global__ void __launch_bounds__(256, 2)
     }
   }
   if (!active) return;
-  float* sl = slab + ((int64_t)blockIdx.x * g.heads + head) * (ntab + D);
+  float* sl = slab + ((int64_t)blockIdx.x * g.heads + head) * (ntab + 2 * D);
   for (int e = lane; e < ntab; e += 64) sl[e] = dtab[w][e];
 #pragma unroll
   for (int ct = 0; ct < 2; ++ct) {
-    float t = dkb[ct];
+    float t = dkb[ct], u = dvb[ct];
     t += __shfl_xor(t, 16, 64);
     t += __shfl_xor(t, 32, 64);
-    if (g4 == 0) sl[ntab + 16 * ct + l16] = t;
+    u += __shfl_xor(u, 16, 64);
+    u += __shfl_xor(u, 32, 64);
+    if (g4 == 0) {
+      sl[ntab + 16 * ct + l16] = t;
+      sl[ntab + D + 16 * ct + l16] = u;
+    }
   }
 }
 
-// gtable[e, head] / gqkb[C + head*D + d] = sum over blocks: 64 entries per
-// block of 16 waves, wave w sums blocks w, w+16, ... (8 loads in flight), the
-// 16 wave sums combine in a fixed order.
+// gtable[e, head] / gqkb[C + head*D + d] / gvb[head*D + d] = sum over blocks:
+// 64 entries per block of 16 waves, wave w sums blocks w, w+16, ... (8 loads
+// in flight), the 16 wave sums combine in a fixed order.
 __global__ void __launch_bounds__(1024)
     wattn_slab_reduce_kernel(const float* __restrict__ slab, int nblocks, int heads,
                              int ntab, int c, float* __restrict__ gtable,
-                             float* __restrict__ gqkb) {
+                             float* __restrict__ gqkb, float* __restrict__ gvb) {
   __shared__ float red[16][64];
   const int head = blockIdx.y;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int e = blockIdx.x * 64 + lane;
-  const int per = ntab + D;
+  const int per = ntab + 2 * D;
   float acc = 0.f;
   if (e < per) {
 #pragma unroll 8
@@ -508,8 +518,10 @@ __global__ void __launch_bounds__(1024)
   for (int w = 0; w < 16; ++w) t += red[w][lane];
   if (e < ntab)
     gtable[e * heads + head] = t;
-  else
+  else if (e < ntab + D)
     gqkb[c + head * D + (e - ntab)] = t;
+  else if (gvb)
+    gvb[head * D + (e - ntab - D)] = t;
 }
 
 __global__ void zero_kernel(float* p, int n) {
@@ -530,6 +542,7 @@ bool make_geo(int64_t b, int64_t h, int64_t w, int64_t c, int64_t heads, int64_t
   g->nww = g->wp / g->ws;
   g->n = g->ws * g->ws;
   g->scale = 1.f / sqrtf((float)D);
+  g->vb = nullptr;
   return (int64_t)b * g->nwh * g->nww < (1LL << 31) && mde::cdiv(heads, kHeads) <= 65535 &&
          (int64_t)h * w * 2 * c < (1LL << 31);
 }
@@ -544,17 +557,18 @@ size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
   if (!make_geo(b, h, w, c, heads, window, 0, &g)) return 0;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const int64_t ntab = (2 * window - 1) * (2 * window - 1);
-  return sizeof(float) * (size_t)(mde::cdiv(nwin, kWinBwd) * heads * (ntab + D));
+  return sizeof(float) * (size_t)(mde::cdiv(nwin, kWinBwd) * heads * (ntab + 2 * D));
 }
 
 int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
-                        const float* table, void* out, int64_t b, int64_t h,
-                        int64_t w, int64_t c, int64_t heads, int64_t window,
+                        const float* v_bias, const float* table, void* out, int64_t b,
+                        int64_t h, int64_t w, int64_t c, int64_t heads, int64_t window,
                         int64_t shift, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   Geo g;
   if (!qk || !qk_bias || !v || !table || !out || !make_geo(b, h, w, c, heads, window, shift, &g))
     return MDE_ERR_INVALID_ARG;
+  g.vb = v_bias;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const double bytes = 4.0 * (double)b * h * w * c * 4.0;  // q, k, v read + o written
@@ -569,15 +583,17 @@ int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
 }
 
 int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
-                        const void* v, const float* table, void* gqk, void* gv,
-                        float* gtable, float* gqk_bias, int64_t b, int64_t h,
-                        int64_t w, int64_t c, int64_t heads, int64_t window,
+                        const void* v, const float* v_bias, const float* table, void* gqk,
+                        void* gv, float* gtable, float* gqk_bias, float* gv_bias, int64_t b,
+                        int64_t h, int64_t w, int64_t c, int64_t heads, int64_t window,
                         int64_t shift, void* workspace, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   Geo g;
   if (!gout || !qk || !qk_bias || !v || !table || !gqk || !gv || !gtable ||
-      !gqk_bias || !workspace || !make_geo(b, h, w, c, heads, window, shift, &g))
+      !gqk_bias || !workspace || (gv_bias && !v_bias) ||
+      !make_geo(b, h, w, c, heads, window, shift, &g))
     return MDE_ERR_INVALID_ARG;
+  g.vb = v_bias;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const int nblk = (int)mde::cdiv(nwin, kWinBwd);
@@ -595,10 +611,10 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
   // q half of d(qk bias) gets nothing from padded tokens (their dO is 0)
   MDE_LAUNCH(mde::K_WATTN_BWD, 0.0, s, zero_kernel, dim3((unsigned)mde::cdiv(c, 256)),
              dim3(256), 0, gqk_bias, (int)c);
-  MDE_LAUNCH(mde::K_WATTN_BWD, 4.0 * nblk * heads * (ntab + D), s,
-             wattn_slab_reduce_kernel, dim3((unsigned)mde::cdiv(ntab + D, 64), (unsigned)heads),
-             dim3(1024), 0, (const float*)workspace, nblk, (int)heads, ntab, (int)c,
-             gtable, gqk_bias);
+  MDE_LAUNCH(mde::K_WATTN_BWD, 4.0 * nblk * heads * (ntab + 2 * D), s,
+             wattn_slab_reduce_kernel,
+             dim3((unsigned)mde::cdiv(ntab + 2 * D, 64), (unsigned)heads), dim3(1024), 0,
+             (const float*)workspace, nblk, (int)heads, ntab, (int)c, gtable, gqk_bias, gv_bias);
   return MDE_OK;
 }
 

@@ -65,22 +65,22 @@ def _relative_position_index(wh, ww):
 
 class _WindowAttn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, qk, qk_bias, v, table, h, w, heads, window, shift):
+    def forward(ctx, qk, qk_bias, v, v_bias, table, h, w, heads, window, shift):
         qk = qk.contiguous()
         v = v.contiguous()
         b, _, c2 = qk.shape
         c = c2 // 2
         out = torch.empty((b, h * w, c), dtype=qk.dtype, device=qk.device)
         _abi.call("mde_window_attn_fwd", _abi.ptr(qk), _abi.ptr(qk_bias), _abi.ptr(v),
-                  _abi.ptr(table), _abi.ptr(out), b, h, w, c, heads, window, shift,
+                  _abi.ptr(v_bias), _abi.ptr(table), _abi.ptr(out), b, h, w, c, heads, window, shift,
                   _abi.dtype_code(qk), _abi.stream_of(qk))
-        ctx.save_for_backward(qk, qk_bias, v, table)
+        ctx.save_for_backward(qk, qk_bias, v, v_bias, table)
         ctx.meta = (h, w, heads, window, shift)
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        qk, qk_bias, v, table = ctx.saved_tensors
+        qk, qk_bias, v, v_bias, table = ctx.saved_tensors
         h, w, heads, window, shift = ctx.meta
         gout = gout.contiguous()
         b, _, c2 = qk.shape
@@ -89,12 +89,13 @@ class _WindowAttn(torch.autograd.Function):
         gv = torch.empty_like(v)
         gtable = torch.empty_like(table)
         gbias = torch.empty_like(qk_bias)
+        gvb = torch.empty_like(v_bias) if v_bias is not None else None
         ws = _ws(_abi.query("mde_window_attn_workspace", b, h, w, c, heads, window), qk)
         _abi.call("mde_window_attn_bwd", _abi.ptr(gout), _abi.ptr(qk), _abi.ptr(qk_bias),
-                  _abi.ptr(v), _abi.ptr(table), _abi.ptr(gqk), _abi.ptr(gv), _abi.ptr(gtable),
-                  _abi.ptr(gbias), b, h, w, c, heads, window, shift, _abi.ptr(ws),
-                  _abi.dtype_code(gout), _abi.stream_of(gout))
-        return gqk, gbias, gv, gtable, None, None, None, None, None
+                  _abi.ptr(v), _abi.ptr(v_bias), _abi.ptr(table), _abi.ptr(gqk), _abi.ptr(gv),
+                  _abi.ptr(gtable), _abi.ptr(gbias), _abi.ptr(gvb), b, h, w, c, heads, window, shift,
+                  _abi.ptr(ws), _abi.dtype_code(gout), _abi.stream_of(gout))
+        return gqk, gbias, gv, gvb, gtable, None, None, None, None, None
 
 
 class _Transpose(torch.autograd.Function):
@@ -170,14 +171,15 @@ class LayerNorm(nn.LayerNorm):
         return _LayerNorm.apply(x, self.weight, self.bias, self.eps)
 
 
-def window_attention(qk, qk_bias, v, table, h, w, heads, window, shift):
+def window_attention(qk, qk_bias, v, table, h, w, heads, window, shift, v_bias=None):
     """Shifted-window attention core of CRFBlock on the HIP/MFMA kernel.
 
     qk: [B, H*W, 2C] (qk Linear of the real tokens), qk_bias: [2C], v: [B, H, W, C],
-    table: [(2ws-1)^2, heads].  Returns [B, H*W, C] (before proj).
+    table: [(2ws-1)^2, heads].  v_bias: [C] value of a padded token (SAM's
+    projected v), None = 0 (NewCRF).  Returns [B, H*W, C] (before proj).
     """
     _gpu(qk, qk_bias, v, table)
-    return _WindowAttn.apply(qk, qk_bias, v, table, int(h), int(w), int(heads), int(window),
+    return _WindowAttn.apply(qk, qk_bias, v, v_bias, table, int(h), int(w), int(heads), int(window),
                              int(shift))
 
 

@@ -320,6 +320,49 @@ def capture_newcrf():
     return out
 
 
+SAM_CASES = [
+    # tag, (input_dim, embed_dim, v_dim, heads), batch, (h, w)   (SAM.forward(e, q): e has
+    # input_dim channels, q has v_dim)
+    ("sam0", (24, 128, 64, 4), 2, (10, 13)),
+    ("sam1", (40, 256, 128, 8), 1, (8, 12)),
+    ("sam3", (160, 1024, 512, 32), 1, (3, 5)),
+    ("sam_same", (64, 64, 64, 2), 2, (14, 7)),  # multiples of 7, no projections
+]
+
+
+def capture_sam():
+    """src/SAM.py SAM stages and the model_mobileV3_large_SAM.py Decoder, fwd + bwd."""
+    from SAM import SAM
+    out = {}
+    for tag, (ind, emb, vd, heads), b, (h, w) in SAM_CASES:
+        m = fill_(SAM(input_dim=ind, embed_dim=emb, v_dim=vd, window_size=7, num_heads=heads))
+        e = torch.from_numpy(seeded((b, ind, h, w), 71, -1, 1)).requires_grad_(True)
+        q = torch.from_numpy(seeded((b, vd, h, w), 72, -1, 1)).requires_grad_(True)
+        y = m(e, q)
+        gy = torch.from_numpy(seeded(y.shape, 73, -1, 1))
+        y.backward(gy)
+        out.update({f"{tag}::e": f32(e), f"{tag}::q": f32(q), f"{tag}::gy": f32(gy),
+                    f"{tag}::y": f32(y), f"{tag}::ge": f32(e.grad), f"{tag}::gq": f32(q.grad)})
+        out[f"{tag}::keys"] = np.array(list(m.state_dict().keys()))
+        grad_summary(m, f"{tag}::", out, full_limit=1024)
+    from model_mobileV3_large_SAM import Decoder
+    dec = fill_(Decoder())
+    shapes = {4: (24, 16, 24), 7: (40, 8, 12), 13: (112, 4, 6), 16: (160, 2, 3), 17: (960, 2, 3)}
+    feats = [None] * 18
+    for i, (c, h, w) in shapes.items():
+        feats[i] = torch.from_numpy(seeded((2, c, h, w), 60 + i, -1, 1)).requires_grad_(True)
+    y = dec(feats)
+    gy = torch.from_numpy(seeded(y.shape, 69, -1, 1))
+    y.backward(gy)
+    out["dec::keys"] = np.array(list(dec.state_dict().keys()))
+    out["dec::y"], out["dec::gy"] = f32(y), f32(gy)
+    for i in shapes:
+        out[f"dec::feat{i}"] = f32(feats[i])
+        out[f"dec::gfeat{i}"] = f32(feats[i].grad)
+    grad_summary(dec, "dec::", out, full_limit=1024)
+    return out
+
+
 def capture_metrics():
     """utils.compute_errors (src/utils.py:45-66) on the pixels src/test.py:105-118
     keeps (clamp / range mask / Eigen crop, restated inline as test.py is a
@@ -440,7 +483,8 @@ def main():
     jobs = {"golden_resize.npz": capture_resize, "golden_blocks.npz": capture_blocks,
             "golden_losses.npz": capture_losses, "golden_guidedepth.npz": capture_guidedepth,
             "golden_trainseq.npz": capture_train_sequence, "golden_newcrf.npz": capture_newcrf,
-            "golden_metrics.npz": capture_metrics, "golden_data.npz": capture_data}
+            "golden_metrics.npz": capture_metrics, "golden_data.npz": capture_data,
+            "golden_sam.npz": capture_sam}
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():
         if only and fname not in only:

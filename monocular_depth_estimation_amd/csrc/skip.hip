@@ -312,21 +312,31 @@ __global__ void __launch_bounds__(256, 2)
     const float* rp = r + nidx * CI * hw + p0;
     const float* dp = HAS_D ? d + nidx * CI * hw + p0 : nullptr;
     float* sp = gs ? gs + nidx * CI * hw + p0 : nullptr;
-    // gs = W^T G, one 16-pixel column tile at a time
+    // gs = W^T G with the forward's permuted pixel order: lane (l16, q4) loads
+    // pixels 4*l16 .. 4*l16+3 of G row 4kk + q4 as one float4, component j
+    // feeds sub-tile j, and each gs row leaves as one float4 per lane (full
+    // 256-byte row segments both ways).
     if (sp) {
+      float4 gb[KO];
 #pragma unroll
-      for (int nt = 0; nt < 4; ++nt) {
-        float gb[KO];
+      for (int kk = 0; kk < KO; ++kk)
+        gb[kk] = *reinterpret_cast<const float4*>(gp + (4 * kk + q4) * hw + 4 * l16);
 #pragma unroll
-        for (int kk = 0; kk < KO; ++kk) gb[kk] = gp[(4 * kk + q4) * hw + 16 * nt + l16];
+      for (int mt = 0; mt < MT; ++mt) {
+        f4 acc[4];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          f4 acc = {0.f, 0.f, 0.f, 0.f};
+        for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int kk = 0; kk < KO; ++kk) acc = mfma4(wa[mt][kk], gb[kk], acc);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sp[(16 * mt + 4 * q4 + i) * hw + 16 * nt + l16] = acc[i];
+        for (int kk = 0; kk < KO; ++kk) {
+          acc[0] = mfma4(wa[mt][kk], gb[kk].x, acc[0]);
+          acc[1] = mfma4(wa[mt][kk], gb[kk].y, acc[1]);
+          acc[2] = mfma4(wa[mt][kk], gb[kk].z, acc[2]);
+          acc[3] = mfma4(wa[mt][kk], gb[kk].w, acc[3]);
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *reinterpret_cast<float4*>(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16) =
+              make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -404,9 +414,13 @@ __global__ void __launch_bounds__(256, 2)
 }
 
 // MFMA forward for the full-size blocks (hw % 64 == 0): each wave computes a
-// [CO x 64] output tile = W [CO x CI] . S [CI x 64] (+ bias), S = r + d formed
-// per lane from two scalar loads (16 lanes read 64 contiguous bytes of a
-// channel row); W sits in registers as the A operands for the whole launch.
+// [CO x 64] output tile = W [CO x CI] . S [CI x 64] (+ bias), S = r + d.
+// Pixel order is permuted so every access is a full 256-byte row segment:
+// lane (l16, q4) loads one float4 = pixels 4*l16 .. 4*l16+3 of channel
+// 4kk + q4, and component j of it feeds MFMA sub-tile j (column l16 <->
+// pixel 4*l16 + j); the four sub-tiles' accumulators then hold, per lane,
+// four consecutive pixels of one output row -- stored as one float4.  W sits
+// in registers as the A operands for the whole launch.
 // BNR: operand r' = relu(r * isc[c] + ish[c]) (BatchNorm + ReLU of the
 // producer fused into the load, so r' is never written to HBM).
 template <int CI, int CO, bool HAS_D, bool BNR = false>
@@ -441,32 +455,48 @@ __global__ void __launch_bounds__(256)
     fsc[kk] = BNR ? isc[4 * kk + q4] : 1.f;
     fsh[kk] = BNR ? ish[4 * kk + q4] : 0.f;
   }
-  const int64_t tpi = hw / 64;
+  const int tpi = (int)(hw / 64);
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
-    const float* rp = r + nidx * CI * hw + p0;
-    const float* dp = HAS_D ? d + nidx * CI * hw + p0 : nullptr;
-    float* op = out + nidx * CO * hw + p0;
+    const float* rp = r + nidx * CI * hw + p0 + 4 * l16;
+    const float* dp = HAS_D ? d + nidx * CI * hw + p0 + 4 * l16 : nullptr;
+    float* op = out + nidx * CO * hw + p0 + 4 * l16;
+    float4 sb[KC];
 #pragma unroll
-    for (int nt = 0; nt < 4; ++nt) {
-      float sb[KC];
+    for (int kk = 0; kk < KC; ++kk) {
+      const int64_t off = (int64_t)(4 * kk + q4) * hw;
+      float4 v = *reinterpret_cast<const float4*>(rp + off);
+      if (HAS_D) {
+        const float4 e = *reinterpret_cast<const float4*>(dp + off);
+        v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
+      }
+      if (BNR) {
+        v.x = fmaxf(v.x * fsc[kk] + fsh[kk], 0.f);
+        v.y = fmaxf(v.y * fsc[kk] + fsh[kk], 0.f);
+        v.z = fmaxf(v.z * fsc[kk] + fsh[kk], 0.f);
+        v.w = fmaxf(v.w * fsc[kk] + fsh[kk], 0.f);
+      }
+      sb[kk] = v;
+    }
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      f4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f4{bo[ot][0], bo[ot][1], bo[ot][2], bo[ot][3]};
 #pragma unroll
       for (int kk = 0; kk < KC; ++kk) {
-        const int64_t off = (int64_t)(4 * kk + q4) * hw + 16 * nt + l16;
-        sb[kk] = HAS_D ? rp[off] + dp[off] : rp[off];
-        if (BNR) sb[kk] = fmaxf(sb[kk] * fsc[kk] + fsh[kk], 0.f);
+        acc[0] = mfma4(wa[ot][kk], sb[kk].x, acc[0]);
+        acc[1] = mfma4(wa[ot][kk], sb[kk].y, acc[1]);
+        acc[2] = mfma4(wa[ot][kk], sb[kk].z, acc[2]);
+        acc[3] = mfma4(wa[ot][kk], sb[kk].w, acc[3]);
       }
 #pragma unroll
-      for (int ot = 0; ot < OT; ++ot) {
-        f4 acc = {bo[ot][0], bo[ot][1], bo[ot][2], bo[ot][3]};
-#pragma unroll
-        for (int kk = 0; kk < KC; ++kk) acc = mfma4(wa[ot][kk], sb[kk], acc);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int o = 16 * ot + 4 * q4 + i;
-          if (o < CO) op[o * hw + 16 * nt + l16] = acc[i];
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int o = 16 * ot + 4 * q4 + i;
+        if (o < CO)
+          *reinterpret_cast<float4*>(op + (int64_t)o * hw) =
+              make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
       }
     }
   }

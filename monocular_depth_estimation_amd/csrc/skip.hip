@@ -257,9 +257,10 @@ __global__ void __launch_bounds__(256)
 //   gs tile [CI x 64] = W^T [CI x CO] . G [CO x 64]    (K = CO, W^T held in
 //       registers as A operands; G read per lane as B, 16 lanes = 64 B rows)
 //   gW [CO x CI] += G [CO x 64] . S^T [64 x CI]       (K = pixels with a
-//       permuted order: lane group q supplies pixels 16q..16q+15, so A and B
-//       are 4 float4 loads of contiguous pixels per lane; S = r + d formed
-//       in registers)
+//       permuted order: lane group q supplies pixels 16v + 4q .. +3, v = 0..3,
+//       so A and B are 4 float4 loads per lane and the four lane groups of a
+//       row read 64 contiguous bytes per instruction; S = r + d formed in
+//       registers)
 //   gb [CO] += row sums of G
 // v_mfma_f32_16x16x4_f32 throughout (exact f32 products).  The gW/gb
 // accumulators stay in registers for the whole launch and are combined over
@@ -353,10 +354,12 @@ __global__ void __launch_bounds__(256, 2)
         const int ot = og + oo;
         const int o = 16 * ot + l16;
         if (o < CO) {
-          const float4* src = reinterpret_cast<const float4*>(gp + o * hw + 16 * q4);
+          // pixels 16v + 4q4 .. +3: the 4 lane groups of a row read 64
+          // contiguous bytes per instruction (same order for S below)
+          const float4* src = reinterpret_cast<const float4*>(gp + o * hw + 4 * q4);
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            const float4 x = src[v];
+            const float4 x = src[4 * v];
             ga[oo][4 * v] = x.x; ga[oo][4 * v + 1] = x.y;
             ga[oo][4 * v + 2] = x.z; ga[oo][4 * v + 3] = x.w;
             gbp[ot] += (x.x + x.y) + (x.z + x.w);
@@ -368,13 +371,13 @@ __global__ void __launch_bounds__(256, 2)
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 16 * q4);
+        const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 4 * q4);
         float sb[16];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          float4 x = ra[v];
+          float4 x = ra[4 * v];
           if (HAS_D) {
-            const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 16 * q4)[v];
+            const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 4 * q4)[4 * v];
             x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
           }
           if (BNR) {

@@ -175,6 +175,52 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   }
 }
 
+// Same adjoint, two input columns per thread (wi even): one float4 of each
+// output-gradient row (columns 2j .. 2j+3) feeds both columns, the two
+// neighbours 2j-1 / 2j+4 come from the adjacent lanes' float4 (wave shuffles;
+// loads only at the wave's edges), results leave as float2 -- 1 load + 1/2
+// store instruction per output row and column pair instead of 3 + 1 per
+// column.  Rows are processed in a fully unrolled kX2Rows window so the
+// loads of successive rows are all in flight together.
+__global__ void __launch_bounds__(64 * kX2Warps)
+    bilinear_bwd_x2_pair_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+                                int hi, int wi) {
+  const int lane = threadIdx.x;
+  const int j0 = 2 * (blockIdx.x * 64 + lane);  // input columns j0, j0 + 1
+  const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
+  if (i0 >= hi) return;  // uniform per wave
+  const bool ok = j0 < wi;
+  const int jc = ok ? j0 : 0;
+  const int64_t plane = blockIdx.z;
+  const int ho = 2 * hi, wo = 2 * wi;
+  const float* gp = gy + plane * ho * (int64_t)wo;
+  float* xp = gx + plane * hi * (int64_t)wi + jc;
+  // pair-filtered row o: (gx-column j0 part, gx-column j0+1 part)
+  auto hrow = [&](int o) {
+    o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
+    const float* row = gp + (int64_t)o * wo;
+    const float4 v = *reinterpret_cast<const float4*>(row + 2 * jc);
+    float l = __shfl_up(v.w, 1, 64), r = __shfl_down(v.x, 1, 64);
+    if (lane == 0) l = row[2 * jc > 0 ? 2 * jc - 1 : 0];
+    if (lane == 63 || 2 * jc + 4 >= wo) r = row[2 * jc + 4 < wo ? 2 * jc + 4 : wo - 1];
+    return make_float2(0.25f * l + 0.75f * v.x + 0.75f * v.y + 0.25f * v.z,
+                       0.25f * v.y + 0.75f * v.z + 0.75f * v.w + 0.25f * r);
+  };
+  float2 a = hrow(2 * i0 - 1), b = hrow(2 * i0);
+#pragma unroll
+  for (int k = 0; k < kX2Rows; ++k) {
+    const int i = i0 + k;
+    if (i >= hi) break;  // uniform per wave
+    const float2 c = hrow(2 * i + 1), d = hrow(2 * i + 2);
+    if (ok)
+      *reinterpret_cast<float2*>(xp + (int64_t)i * wi) =
+          make_float2(0.25f * a.x + 0.75f * b.x + 0.75f * c.x + 0.25f * d.x,
+                      0.25f * a.y + 0.75f * b.y + 0.75f * c.y + 0.25f * d.y);
+    a = c;
+    b = d;
+  }
+}
+
 inline dim3 x2_grid(int64_t planes, int64_t hi, int64_t wi) {
   return dim3((unsigned)mde::cdiv(wi, 64), (unsigned)mde::cdiv(hi, kX2Rows * kX2Warps),
               (unsigned)planes);
@@ -455,7 +501,11 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
   const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
                   ho == 2 * hi && wo == 2 * wi && planes <= 65535;
-  if (x2) {
+  if (x2 && wi % 2 == 0) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel,
+               x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy,
+               (float*)gx, (int)hi, (int)wi);
+  } else if (x2) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
                x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
                (float*)gx, (int)hi, (int)wi);

@@ -77,6 +77,9 @@ def test_nearest_golden_bit_exact(golden, case):
 
 @pytest.mark.parametrize("shape,kw", [
     ((32, 16, 240, 320), dict(scale_factor=2)),           # up_3 input, BASELINE cfg2
+    ((3, 5, 3, 6), dict(scale_factor=2)),                 # x2, column pairs, short planes
+    ((2, 4, 9, 130), dict(scale_factor=2)),               # x2, pairs across two blocks
+    ((2, 3, 11, 7), dict(scale_factor=2)),                # x2, odd width: per-column kernel
     ((32, 64, 8, 10), dict(size=(60, 80))),               # DDRNet spp -> H/8 (x7.5)
     ((32, 64, 15, 20), dict(size=(60, 80))),              # compression4 (x4)
     ((2, 3, 100, 150), dict(size=(310, 470))),            # plane > LDS: banded kernel

@@ -143,6 +143,52 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   }
 }
 
+// Forward with two input columns per thread (wi even): one float2 of each
+// input row (+ the neighbours from the adjacent lanes by wave shuffles)
+// gives four consecutive outputs of two output rows, written as float4.
+__global__ void __launch_bounds__(64 * kX2Warps)
+    bilinear_fwd_x2_pair_kernel(const float* __restrict__ x, float* __restrict__ y, int hi,
+                                int wi) {
+  const int lane = threadIdx.x;
+  const int j0 = 2 * (blockIdx.x * 64 + lane);
+  const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
+  if (i0 >= hi) return;  // uniform per wave
+  const bool ok = j0 < wi;
+  const int jc = ok ? j0 : 0;
+  const int64_t plane = blockIdx.z;
+  const float* xp = x + plane * hi * (int64_t)wi;
+  const int wo = 2 * wi;
+  float* yp = y + plane * (2 * hi) * (int64_t)wo + 2 * jc;
+  // horizontally interpolated input row r: outputs 2j0 .. 2j0+3
+  auto hrow = [&](int r) {
+    r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
+    const float* row = xp + (int64_t)r * wi;
+    const float2 c = *reinterpret_cast<const float2*>(row + jc);
+    float l = __shfl_up(c.y, 1, 64), rr = __shfl_down(c.x, 1, 64);
+    if (lane == 0) l = row[jc > 0 ? jc - 1 : 0];
+    if (lane == 63 || jc + 2 >= wi) rr = row[jc + 2 < wi ? jc + 2 : wi - 1];
+    return make_float4(0.25f * l + 0.75f * c.x, 0.75f * c.x + 0.25f * c.y,
+                       0.25f * c.x + 0.75f * c.y, 0.75f * c.y + 0.25f * rr);
+  };
+  float4 prev = hrow(i0 - 1), cur = hrow(i0);
+#pragma unroll
+  for (int k = 0; k < kX2Rows; ++k) {
+    const int i = i0 + k;
+    if (i >= hi) break;  // uniform per wave
+    const float4 nxt = hrow(i + 1);
+    if (ok) {
+      *reinterpret_cast<float4*>(yp + (int64_t)(2 * i) * wo) =
+          make_float4(0.25f * prev.x + 0.75f * cur.x, 0.25f * prev.y + 0.75f * cur.y,
+                      0.25f * prev.z + 0.75f * cur.z, 0.25f * prev.w + 0.75f * cur.w);
+      *reinterpret_cast<float4*>(yp + (int64_t)(2 * i + 1) * wo) =
+          make_float4(0.75f * cur.x + 0.25f * nxt.x, 0.75f * cur.y + 0.25f * nxt.y,
+                      0.75f * cur.z + 0.25f * nxt.z, 0.75f * cur.w + 0.25f * nxt.w);
+    }
+    prev = cur;
+    cur = nxt;
+  }
+}
+
 // 4-tap adjoint filter of one output-gradient row at input column j.
 __device__ __forceinline__ float x2_hgrad(const float* row, int j, int wo) {
   const float2 m = *reinterpret_cast<const float2*>(row + 2 * j);
@@ -472,7 +518,15 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
   const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
                   ho == 2 * hi && wo == 2 * wi && n * c <= 65535;
-  if (x2) {
+  // The pair kernel (two columns per lane) wins when it keeps at least as many lanes
+  // busy as the one-column kernel: 64-lane rows of wi/2 pairs vs of wi columns.
+  const bool pair = x2 && wi % 2 == 0 &&
+                    mde::cdiv(wi, 64) >= 2 * mde::cdiv(wi / 2, 64);
+  if (pair) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel,
+               x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)x, (float*)y,
+               (int)hi, (int)wi);
+  } else if (x2) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel,
                x2_grid(n * c, hi, wi), dim3(64, kX2Warps), 0, (const float*)x,
                (float*)y, (int)hi, (int)wi);

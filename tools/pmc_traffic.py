@@ -55,7 +55,8 @@ NAMES = [
     (r"skip_bwd_reg_kernel", "skip_reduce_bwd"),
     (r"wattn_fwd_kernel", "window_attn_fwd"),
     (r"wattn_(bwd|slab_reduce)_kernel|zero_kernel", "window_attn_bwd"),
-    (r"dw_fwd_kernel", "dwconv_fwd"),
+    (r"dw_fwd_strip_kernel", "dwconv_fwd"),
+    (r"dw_bwd_strip_kernel", "dwconv_bwd"),
     (r"dw_bwd_data_kernel", "dwconv_bwd_data"),
     (r"dw_bwd_weight_kernel", "dwconv_bwd_weight"),
     (r"dw_wreduce_kernel", "dwconv_wreduce"),

@@ -147,6 +147,28 @@ __device__ FwdCh fwd_channel(const FwdArgs& A, const float* x, int64_t ch,
   return r;
 }
 
+// Walks a channel's (N, H*W) elements with a fixed stride without a 64-bit
+// division per step: (image, offset in plane) advance by `step` elements.
+struct PlaneCursor {
+  int64_t off;  // element offset of (nn, p) relative to the channel base
+  int64_t p;
+  __device__ PlaneCursor(int64_t i, int64_t hw, int64_t chw) {
+    const int64_t nn = i / hw;
+    p = i - nn * hw;
+    off = nn * chw + p;
+  }
+  __device__ __forceinline__ void advance(int64_t step, int64_t hw, int64_t chw) {
+    p += step;
+    off += step;
+    while (p >= hw) {
+      p -= hw;
+      off += chw - hw;
+    }
+  }
+};
+
+constexpr int kRedDepth = 4;  // independent float4 loads per thread per trip
+
 // part[(c * slices + s) * 2 + {0,1}] = sum(x - ref), sum((x - ref)^2)
 template <bool VEC>
 __global__ void __launch_bounds__(256)
@@ -163,12 +185,29 @@ __global__ void __launch_bounds__(256)
   const int64_t chw = c * hw;
   float s1 = 0.f, s2 = 0.f;
   if (VEC) {
-    for (int64_t i = i0 + 4 * threadIdx.x; i < i1; i += 4 * 256) {
-      const int64_t nn = i / hw, p = i - nn * hw;
-      const float4 v = *reinterpret_cast<const float4*>(xc + nn * chw + p);
-      const float a = v.x - ref, b = v.y - ref, cc = v.z - ref, d = v.w - ref;
-      s1 += (a + b) + (cc + d);
-      s2 += (a * a + b * b) + (cc * cc + d * d);
+    constexpr int64_t kStep = 4 * 256;
+    int64_t i = i0 + 4 * threadIdx.x;
+    if (i < i1) {
+      PlaneCursor cur(i, hw, chw);
+      auto acc = [&](const float4 v) {
+        const float a = v.x - ref, b = v.y - ref, cc = v.z - ref, d = v.w - ref;
+        s1 += (a + b) + (cc + d);
+        s2 += (a * a + b * b) + (cc * cc + d * d);
+      };
+      for (; i + (kRedDepth - 1) * kStep < i1; i += kRedDepth * kStep) {
+        float4 v[kRedDepth];
+#pragma unroll
+        for (int k = 0; k < kRedDepth; ++k) {
+          v[k] = *reinterpret_cast<const float4*>(xc + cur.off);
+          cur.advance(kStep, hw, chw);
+        }
+#pragma unroll
+        for (int k = 0; k < kRedDepth; ++k) acc(v[k]);
+      }
+      for (; i < i1; i += kStep) {
+        acc(*reinterpret_cast<const float4*>(xc + cur.off));
+        cur.advance(kStep, hw, chw);
+      }
     }
   } else {
     for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
@@ -297,19 +336,38 @@ __global__ void __launch_bounds__(256)
   const int64_t base = ch * hw;
   float s1 = 0.f, s2 = 0.f;
   if (VEC) {
-    for (int64_t i = i0 + 4 * threadIdx.x; i < i1; i += 4 * 256) {
-      const int64_t nn = i / hw, p = i - nn * hw;
-      const int64_t off = base + nn * chw + p;
-      const float4 g = *reinterpret_cast<const float4*>(gy + off);
-      const float4 v = *reinterpret_cast<const float4*>(x + off);
-      float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (r) q = *reinterpret_cast<const float4*>(r + off);
-      const float a = dy_eff(g.x, v.x, q.x, sc, sh, act);
-      const float b = dy_eff(g.y, v.y, q.y, sc, sh, act);
-      const float cc = dy_eff(g.z, v.z, q.z, sc, sh, act);
-      const float d = dy_eff(g.w, v.w, q.w, sc, sh, act);
-      s1 += (a + b) + (cc + d);
-      s2 += (a * (v.x - mu) + b * (v.y - mu)) + (cc * (v.z - mu) + d * (v.w - mu));
+    constexpr int64_t kStep = 4 * 256;
+    int64_t i = i0 + 4 * threadIdx.x;
+    if (i < i1) {
+      PlaneCursor cur(i, hw, chw);
+      auto acc = [&](const float4 g, const float4 v, const float4 q) {
+        const float a = dy_eff(g.x, v.x, q.x, sc, sh, act);
+        const float b = dy_eff(g.y, v.y, q.y, sc, sh, act);
+        const float cc = dy_eff(g.z, v.z, q.z, sc, sh, act);
+        const float d = dy_eff(g.w, v.w, q.w, sc, sh, act);
+        s1 += (a + b) + (cc + d);
+        s2 += (a * (v.x - mu) + b * (v.y - mu)) + (cc * (v.z - mu) + d * (v.w - mu));
+      };
+      const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (; i + (kRedDepth - 1) * kStep < i1; i += kRedDepth * kStep) {
+        float4 g[kRedDepth], v[kRedDepth], q[kRedDepth];
+#pragma unroll
+        for (int k = 0; k < kRedDepth; ++k) {
+          const int64_t off = base + cur.off;
+          g[k] = *reinterpret_cast<const float4*>(gy + off);
+          v[k] = *reinterpret_cast<const float4*>(x + off);
+          q[k] = r ? *reinterpret_cast<const float4*>(r + off) : z4;
+          cur.advance(kStep, hw, chw);
+        }
+#pragma unroll
+        for (int k = 0; k < kRedDepth; ++k) acc(g[k], v[k], q[k]);
+      }
+      for (; i < i1; i += kStep) {
+        const int64_t off = base + cur.off;
+        acc(*reinterpret_cast<const float4*>(gy + off), *reinterpret_cast<const float4*>(x + off),
+            r ? *reinterpret_cast<const float4*>(r + off) : z4);
+        cur.advance(kStep, hw, chw);
+      }
     }
   } else {
     for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {

@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--height", type=int, default=480)
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--amp", choices=("fp32", "bf16"), default="fp32",
+                   help="bf16: BASELINE cfg3 autocast (convs / GEMMs bf16, HIP kernels fp32)")
     p.add_argument("--cpu-bs", type=int, default=4)
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--cudnn-benchmark", type=int, default=0)
@@ -119,11 +121,11 @@ def main():
     use_graph = bool(args.graph) and world.device.type == "cuda"
     if use_graph:
         from monocular_depth_estimation_amd.train import GraphTrainer
-        trainer = GraphTrainer(model, loss_fn, world, lr=1e-4)
+        trainer = GraphTrainer(model, loss_fn, world, lr=1e-4, amp=args.amp)
         args.warmup = max(args.warmup, trainer.eager_steps + 1)  # capture happens in warm-up
     else:
         trainer = Trainer(wrap_ddp(model, world), make_adam(model, 1e-4), loss_fn, world,
-                          eval_quirk=False)
+                          eval_quirk=False, amp=args.amp)
     trainer.begin_epoch()
     batches = [synthetic_batch(args.bs, args.height, args.width, world.rank, s, world.device)
                for s in range(2)]
@@ -222,12 +224,15 @@ def main():
         metric = "training images/sec at 640x480 bs=16/GPU (MobileNetV3-L + SAM, SSIM+0.1*L1, Adam)"
         workload = ("PTModel of model_mobileV3_large_SAM (frozen MobileNetV3-Large encoder + SAM "
                     "cross-window attention decoder on MFMA) train step, BN in train mode")
+    if args.amp == "bf16":
+        workload += "; bf16 autocast (BASELINE cfg3 precision)"
     out = {
         "metric": metric,
         "value": round(images / elapsed, 2), "unit": "images/s", "n_gpus": world.size,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if args.amp == "fp32" else "bf16 autocast (convs / GEMMs bf16; HIP kernels fp32)",
         "data": "synthetic (U[0,1) images, U[0.1,10) depths, resident in HBM), random-init weights",
         "config": {"workload": workload,
                    "global_batch": world.size * args.bs, "per_gpu_batch": args.bs,

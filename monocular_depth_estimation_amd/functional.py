@@ -16,6 +16,13 @@ import torch
 
 from . import _abi
 
+# The HIP kernels compute in fp32.  Under torch.autocast (bf16 mixed precision:
+# convolutions / GEMMs on MIOpen / hipBLASLt in bf16) every custom Function runs
+# with its floating inputs cast to fp32 and autocast disabled; autograd casts the
+# fp32 input gradients back to the producers' dtype.
+_amp_fwd = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
+_amp_bwd = torch.amp.custom_bwd(device_type="cuda")
+
 __all__ = [
     "interpolate", "bilinear_resize", "nearest_resize", "se_cat", "skip_reduce",
     "minmax", "depth_norm", "ssim3_l1", "depth_loss",
@@ -76,6 +83,7 @@ def _align_scale(inp: int, out: int) -> float:
 
 class _Bilinear(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, ho, wo, sh, sw, align):
         x = x.contiguous()
         n, c, hi, wi = x.shape
@@ -86,6 +94,8 @@ class _Bilinear(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         n, c, hi, wi, ho, wo, sh, sw, align = ctx.meta
         gy = gy.contiguous()
@@ -97,6 +107,7 @@ class _Bilinear(torch.autograd.Function):
 
 class _Nearest(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, ho, wo, sh, sw):
         x = x.contiguous()
         n, c, hi, wi = x.shape
@@ -107,6 +118,8 @@ class _Nearest(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         n, c, hi, wi, ho, wo, sh, sw = ctx.meta
         gy = gy.contiguous()
@@ -158,6 +171,7 @@ def interpolate(input, size=None, scale_factor=None, mode="nearest", align_corne
 # ------------------------------------------------------- squeeze-excitation
 class _SECat(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, xa, xb, w1, w2):
         xa = xa.contiguous()
         xb = xb.contiguous() if xb is not None else None
@@ -180,6 +194,8 @@ class _SECat(torch.autograd.Function):
         return out
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gout):
         xa, xb, w1, w2, s, hidden, mean = ctx.saved_tensors
         gout = gout.contiguous()
@@ -211,6 +227,7 @@ def se_cat(xa, xb, w1, w2):
 # ------------------------------------------------------------- skip fusion
 class _SkipReduce(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, r, d, weight, bias):
         r = r.contiguous()
         d = d.contiguous()
@@ -226,6 +243,8 @@ class _SkipReduce(torch.autograd.Function):
         return out
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gout):
         r, d, w2 = ctx.saved_tensors
         gout = gout.contiguous()
@@ -266,6 +285,7 @@ def minmax(x: torch.Tensor) -> torch.Tensor:
 
 class _DepthNorm(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x):
         x = x.contiguous()
         mm = minmax(x)
@@ -276,6 +296,8 @@ class _DepthNorm(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, g):
         # y = (x - a)/R, R = b - a; min()/max() spread their gradient evenly
         # over ties, as ATen's full-reduction min/max backward does.
@@ -297,6 +319,7 @@ def depth_norm(depth: torch.Tensor) -> torch.Tensor:
 # --------------------------------------------------------------- SSIM + L1
 class _SSIML1(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, pred, target, target_minmax, w_ssim, w_l1):
         pred = pred.contiguous()
         target = target.contiguous()
@@ -316,6 +339,8 @@ class _SSIML1(torch.autograd.Function):
         return loss[0].clone(), loss
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, go, _unused):
         gp, gt = ctx.saved_tensors
         return (gp * go if gp is not None else None,
@@ -339,6 +364,7 @@ def ssim3_l1(pred, target, w_ssim=1.0, w_l1=0.0, target_minmax=None):
 # --------------------------------------------------------------- Depth_Loss
 class _DepthLoss(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, pred, gt, alpha, beta, gamma, max_depth):
         pred = pred.contiguous()
         gt = gt.contiguous()
@@ -356,6 +382,8 @@ class _DepthLoss(torch.autograd.Function):
         return out[0].clone(), out
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, go, _unused):
         pred, gt, out = ctx.saved_tensors
         alpha, beta, gamma, max_depth = ctx.params

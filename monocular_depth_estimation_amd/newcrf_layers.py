@@ -18,7 +18,7 @@ import torch.nn.functional as F
 from torch import nn
 
 from . import _abi
-from .functional import _gpu, _ws
+from .functional import _amp_bwd, _amp_fwd, _gpu, _ws
 
 
 def to_2tuple(v):
@@ -65,6 +65,7 @@ def _relative_position_index(wh, ww):
 
 class _WindowAttn(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, qk, qk_bias, v, v_bias, table, h, w, heads, window, shift):
         qk = qk.contiguous()
         v = v.contiguous()
@@ -79,6 +80,8 @@ class _WindowAttn(torch.autograd.Function):
         return out
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gout):
         qk, qk_bias, v, v_bias, table = ctx.saved_tensors
         h, w, heads, window, shift = ctx.meta
@@ -102,6 +105,8 @@ class _Transpose(torch.autograd.Function):
     """[B, M, N] -> [B, N, M] on the HIP LDS-tiled transpose (its own adjoint)."""
 
     @staticmethod
+
+    @_amp_fwd
     def forward(ctx, x):
         x = x.contiguous()
         b, m, n = x.shape
@@ -111,6 +116,8 @@ class _Transpose(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         return _Transpose.apply(gy)
 
@@ -131,6 +138,7 @@ def tokens_to_nchw(t, h, w):
 
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, weight, bias, eps):
         x = x.contiguous()
         c = x.shape[-1]
@@ -145,6 +153,8 @@ class _LayerNorm(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         x, weight, mean, rstd = ctx.saved_tensors
         gy = gy.contiguous()

@@ -13,13 +13,14 @@ import torch
 from torch import nn
 
 from . import _abi
-from .functional import _gpu, _ws
+from .functional import _amp_bwd, _amp_fwd, _gpu, _ws
 
 _ACTS = {"none": 0, "relu": 1, "hardswish": 2}
 
 
 class _BatchNormAct(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, weight, bias, prebias, residual, running_mean, running_var, nbt,
                 training, momentum, eps, act):
         x = x.contiguous()
@@ -46,6 +47,8 @@ class _BatchNormAct(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         x, weight, bias, residual, mean, invstd = ctx.saved_tensors
         gy = gy.contiguous()
@@ -92,6 +95,7 @@ def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, preb
 
 class _Pointwise(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, weight):
         x = x.contiguous()
         n, cin, h, w = x.shape
@@ -106,6 +110,8 @@ class _Pointwise(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         x, w2 = ctx.saved_tensors
         gy = gy.contiguous()
@@ -128,6 +134,8 @@ class _BNReluPointwise(torch.autograd.Function):
     that into d/dy1 and the BN parameter gradients."""
 
     @staticmethod
+
+    @_amp_fwd
     def forward(ctx, y1, gamma, beta, prebias, running_mean, running_var, nbt, training, momentum,
                 eps, w2):
         y1 = y1.contiguous()
@@ -152,6 +160,8 @@ class _BNReluPointwise(torch.autograd.Function):
         return y2
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy2):
         y1, gamma, beta, mean, invstd, scale, shift, w2m = ctx.saved_tensors
         gy2 = gy2.contiguous()
@@ -218,6 +228,7 @@ CONV3X3_HIP = {
 
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, weight, passes):
         x = x.contiguous()
         weight = weight.contiguous()
@@ -234,6 +245,8 @@ class _Conv3x3(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         gy = gy.contiguous()
@@ -367,6 +380,7 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 class _DWConv(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, weight, k, stride, pad):
         x = x.contiguous()
         n, c, h, w = x.shape
@@ -379,6 +393,8 @@ class _DWConv(torch.autograd.Function):
         return y
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
         k, stride, pad = ctx.meta
@@ -418,6 +434,7 @@ def depthwise_conv_bn_act(x, conv: nn.Conv2d, bn: "BatchNorm2d", act: str = "non
 
 class _SEGate(torch.autograd.Function):
     @staticmethod
+    @_amp_fwd
     def forward(ctx, x, w1, b1, w2, b2):
         x = x.contiguous()
         n, c, h, w = x.shape
@@ -437,6 +454,8 @@ class _SEGate(torch.autograd.Function):
         return out
 
     @staticmethod
+
+    @_amp_bwd
     def backward(ctx, gout):
         x, w1, w2, b2, s, hidden, mean = ctx.saved_tensors
         gout = gout.contiguous()

@@ -101,12 +101,25 @@ def synthetic_batch(batch: int, height: int, width: int, rank: int, step: int,
 
 
 # ------------------------------------------------------------------ step
+def amp_context(amp: str, device: torch.device):
+    """`--amp bf16` (BASELINE cfg3): convolutions / GEMMs autocast to bf16 on
+    MIOpen / hipBLASLt; the HIP kernels keep computing in fp32 (their Functions
+    cast their inputs, functional._amp_fwd).  Weight-cast caching is off so the
+    casts stay inside a captured graph."""
+    if amp not in ("", "fp32", "bf16"):
+        raise ValueError(f"unsupported --amp {amp!r} (fp32 or bf16)")
+    return torch.autocast(device.type, dtype=torch.bfloat16, enabled=amp == "bf16",
+                          cache_enabled=False)
+
+
 class Trainer:
     """One reference training step (train.py:86-114) with a device-side loss log."""
 
-    def __init__(self, model, optimizer, loss_fn, world: World, eval_quirk: bool = True):
+    def __init__(self, model, optimizer, loss_fn, world: World, eval_quirk: bool = True,
+                 amp: str = ""):
         self.model, self.optimizer, self.loss_fn, self.world = model, optimizer, loss_fn, world
         self.eval_quirk = eval_quirk
+        self.amp = amp
         self.loss_sum = torch.zeros((), device=world.device)
         self.loss_count = 0
         self.last_loss = None
@@ -115,8 +128,9 @@ class Trainer:
         self.model.train()  # train.py:79
 
     def step(self, image, depth):
-        pred = self.model(image)
-        loss = self.loss_fn(pred, depth)
+        with amp_context(self.amp, self.world.device):
+            pred = self.model(image)
+            loss = self.loss_fn(pred, depth)
         self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
         self.optimizer.step()
@@ -154,10 +168,11 @@ class GraphTrainer:
     changes the graph, use Trainer for that).
     """
 
-    def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2):
+    def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2, amp: str = ""):
         if world.device.type != "cuda":
             raise RuntimeError("GraphTrainer needs a GPU (use Trainer on CPU)")
         self.model, self.loss_fn, self.world = model, loss_fn, world
+        self.amp = amp
         self.eager_steps = eager_steps
         self.calls = 0
         self.graphs = None
@@ -191,7 +206,8 @@ class GraphTrainer:
 
     # -- the step's pieces (each runs eagerly or inside a capture) ----------
     def _forward_backward(self):
-        loss = self.loss_fn(self.model(self.static_image), self.static_depth)
+        with amp_context(self.amp, self.world.device):
+            loss = self.loss_fn(self.model(self.static_image), self.static_depth)
         loss.backward()
         if self.world.size > 1:
             grads = [p.grad for p in self.params if p.grad is not None]
@@ -320,6 +336,8 @@ def build_parser():
                    help="keep BN in train mode all epoch (the reference switches to eval after step 0)")
     p.add_argument("--log", default="", help="JSONL file for Train/Loss scalars (rank 0)")
     p.add_argument("--seed", default=0, type=int)
+    p.add_argument("--amp", default="fp32", choices=("fp32", "bf16"),
+                   help="bf16 = autocast convs / GEMMs (BASELINE cfg3); HIP kernels stay fp32")
     return p
 
 
@@ -338,7 +356,7 @@ def main(argv=None):
         start_epoch, _ = load_checkpoint(args.checkpoint, model, optimizer)
     ddp = wrap_ddp(model, world)
     trainer = Trainer(ddp, optimizer, SSIML1(1.0, 0.1, depth_norm=True), world,
-                      eval_quirk=not args.no_eval_quirk)
+                      eval_quirk=not args.no_eval_quirk, amp=args.amp)
     log = open(args.log, "a") if (args.log and world.is_main) else None
     loader = None
     if args.data:  # data.py:171-179 on the GPU path; each rank reads a disjoint 1/size of the rows

@@ -27,7 +27,7 @@ def _need_gpu():
     torch.backends.cudnn.deterministic = old
 
 
-def _run(build, graph, steps=6, bs=2, h=64, w=96):
+def _run(build, graph, steps=6, bs=2, h=64, w=96, amp=""):
     from monocular_depth_estimation_amd.loss import SSIML1
     from monocular_depth_estimation_amd.train import (GraphTrainer, Trainer, World, make_adam,
                                                       synthetic_batch)
@@ -36,9 +36,9 @@ def _run(build, graph, steps=6, bs=2, h=64, w=96):
     world = World(0, 0, 1, torch.device(DEV))
     loss_fn = SSIML1(1.0, 0.1, depth_norm=True)
     if graph:
-        tr = GraphTrainer(model, loss_fn, world, lr=1e-4)
+        tr = GraphTrainer(model, loss_fn, world, lr=1e-4, amp=amp)
     else:
-        tr = Trainer(model, make_adam(model, 1e-4), loss_fn, world, eval_quirk=False)
+        tr = Trainer(model, make_adam(model, 1e-4), loss_fn, world, eval_quirk=False, amp=amp)
     tr.begin_epoch()
     losses, moved = [], []
     for k in range(steps):
@@ -66,3 +66,21 @@ def test_graph_step_matches_eager(which):
     worst = max(float((pg[n] - pe[n]).abs().max()) for n in pe)
     assert worst <= 1e-6, worst
     assert min(moved) > 0.5e-4, moved  # Adam moves weights by ~lr = 1e-4 every step
+
+
+def test_bf16_autocast_step():
+    """BASELINE cfg3 precision: convs / GEMMs autocast to bf16, the HIP kernels
+    take fp32 (their Functions cast); the graph replays the autocast step like
+    the eager one, and the losses track the fp32 run to bf16 accuracy."""
+    from monocular_depth_estimation_amd import GuideDepth
+    build = lambda: GuideDepth(pretrained=False)  # noqa: E731
+    lf, _, _ = _run(build, graph=False)
+    le, _, pe = _run(build, graph=False, amp="bf16")
+    lg, moved, pg = _run(build, graph=True, amp="bf16")
+    for a, b in zip(lg, le):
+        assert abs(a - b) <= 1e-5 * abs(b), (lg, le)
+    worst = max(float((pg[n] - pe[n]).abs().max()) for n in pe)
+    assert worst <= 1e-5, worst
+    for a, b in zip(le, lf):  # bf16 products (8-bit mantissa) vs fp32
+        assert abs(a - b) <= 3e-2 * abs(b), (le, lf)
+    assert min(moved) > 0.5e-4, moved

@@ -67,6 +67,34 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   return v;
 }
 
+// Storage types of the activations / gradients: fp32, or bf16 (raw uint16,
+// round-to-nearest-even like torch) under autocast.  Statistics, coefficients
+// and accumulation are fp32 / fp64 either way.
+using bf16 = uint16_t;
+__device__ __forceinline__ float bf2f(bf16 b) { return __uint_as_float((uint32_t)b << 16); }
+__device__ __forceinline__ bf16 f2bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16)((u >> 16) | 0x40);  // quiet NaN
+  return (bf16)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16* p) { return bf2f(*p); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const bf16* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st4(bf16* p, float4 v) {
+  uint2 u;
+  u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -112,14 +140,15 @@ struct FwdArgs {
 
 // Training: (s1, s2) are the shifted sums of channel ch (shift = its first
 // element); writes the designated outputs when `owner`.
-__device__ FwdCh fwd_channel(const FwdArgs& A, const float* x, int64_t ch,
+template <typename T>
+__device__ FwdCh fwd_channel(const FwdArgs& A, const T* x, int64_t ch,
                              double s1, double s2, bool owner) {
   FwdCh r;
   const float pb = A.prebias ? A.prebias[ch] : 0.f;
   double mean_x, invstd;
   if (A.training) {
     const double n = (double)A.total;
-    const double ref = (double)x[ch * A.hw];
+    const double ref = (double)ld1(x + ch * A.hw);
     const double dm = s1 / n;
     double var = s2 / n - dm * dm;
     if (var < 0.0) var = 0.0;
@@ -170,9 +199,9 @@ struct PlaneCursor {
 constexpr int kRedDepth = 4;  // independent float4 loads per thread per trip
 
 // part[(c * slices + s) * 2 + {0,1}] = sum(x - ref), sum((x - ref)^2)
-template <bool VEC>
+template <typename T, bool VEC>
 __global__ void __launch_bounds__(256)
-    bn_stats_kernel(const float* __restrict__ x, int64_t c, int64_t hw,
+    bn_stats_kernel(const T* __restrict__ x, int64_t c, int64_t hw,
                     int64_t total, int64_t slice_len, int slices,
                     float* __restrict__ part) {
   __shared__ float red[4];
@@ -180,8 +209,8 @@ __global__ void __launch_bounds__(256)
   const int s = blockIdx.x;
   const int64_t i0 = s * slice_len;
   const int64_t i1 = i0 + slice_len < total ? i0 + slice_len : total;
-  const float* xc = x + ch * hw;
-  const float ref = xc[0];  // shift for the variance (cancellation guard)
+  const T* xc = x + ch * hw;
+  const float ref = ld1(xc);  // shift for the variance (cancellation guard)
   const int64_t chw = c * hw;
   float s1 = 0.f, s2 = 0.f;
   if (VEC) {
@@ -198,21 +227,21 @@ __global__ void __launch_bounds__(256)
         float4 v[kRedDepth];
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) {
-          v[k] = *reinterpret_cast<const float4*>(xc + cur.off);
+          v[k] = ld4(xc + cur.off);
           cur.advance(kStep, hw, chw);
         }
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) acc(v[k]);
       }
       for (; i < i1; i += kStep) {
-        acc(*reinterpret_cast<const float4*>(xc + cur.off));
+        acc(ld4(xc + cur.off));
         cur.advance(kStep, hw, chw);
       }
     }
   } else {
     for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
       const int64_t nn = i / hw, p = i - nn * hw;
-      const float a = xc[nn * chw + p] - ref;
+      const float a = ld1(xc + nn * chw + p) - ref;
       s1 += a;
       s2 += a * a;
     }
@@ -241,9 +270,10 @@ __device__ __forceinline__ float4 fwd4(float4 v, float4 q, bool has_r, float sc,
 }
 
 // Plane mode: grid (ceil(hw4 / 1024), n*c); 4 float4 per thread.
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bn_apply_plane_kernel(const float* __restrict__ x, const float* __restrict__ r,
-                          float* __restrict__ y, int64_t c, int64_t hw, int act,
+    bn_apply_plane_kernel(const T* __restrict__ x, const T* __restrict__ r,
+                          T* __restrict__ y, int64_t c, int64_t hw, int act,
                           FwdArgs A) {
   __shared__ float cf[2];
   const int64_t plane = blockIdx.y;
@@ -261,25 +291,26 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   const float sc = cf[0], sh = cf[1];
   const int64_t hw4 = hw >> 2;
-  const float4* xp = reinterpret_cast<const float4*>(x + plane * hw);
-  const float4* rp = r ? reinterpret_cast<const float4*>(r + plane * hw) : nullptr;
-  float4* yp = reinterpret_cast<float4*>(y + plane * hw);
+  const T* xp = x + plane * hw;
+  const T* rp = r ? r + plane * hw : nullptr;
+  T* yp = y + plane * hw;
   const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
 #pragma unroll
   for (int k = 0; k < kPlaneChunk4 / 256; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
     if (i < hw4) {
-      const float4 q = rp ? rp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-      yp[i] = fwd4(xp[i], q, rp != nullptr, sc, sh, act);
+      const float4 q = rp ? ld4(rp + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      st4(yp + 4 * i, fwd4(ld4(xp + 4 * i), q, rp != nullptr, sc, sh, act));
     }
   }
 }
 
 // Channel-table mode for small planes: every block builds all channels'
 // coefficients in LDS (block 0 is the designated writer), then grid-strides.
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bn_apply_table_kernel(const float* __restrict__ x, const float* __restrict__ r,
-                          float* __restrict__ y, int64_t planes, int64_t c,
+    bn_apply_table_kernel(const T* __restrict__ x, const T* __restrict__ r,
+                          T* __restrict__ y, int64_t planes, int64_t c,
                           int64_t hw, int act, FwdArgs A) {
   extern __shared__ float tab[];  // [2][c]
   for (int64_t ch = threadIdx.x; ch < c; ch += blockDim.x) {
@@ -299,9 +330,9 @@ __global__ void __launch_bounds__(256)
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ch = (t / hw) % c;
-    float v = x[t] * tab[ch] + tab[c + ch];
-    if (r) v += r[t];
-    y[t] = act_fn(v, act);
+    float v = ld1(x + t) * tab[ch] + tab[c + ch];
+    if (r) v += ld1(r + t);
+    st1(y + t, act_fn(v, act));
   }
 }
 
@@ -316,10 +347,10 @@ __device__ __forceinline__ float dy_eff(float g, float xv, float rv, float sc,
 }
 
 // part[(c*slices+s)*2] = sum dy', sum dy' * (x - mean_x)
-template <bool VEC>
+template <typename T, bool VEC>
 __global__ void __launch_bounds__(256)
-    bn_bwd_reduce_kernel(const float* __restrict__ gy, const float* __restrict__ x,
-                         const float* __restrict__ r,
+    bn_bwd_reduce_kernel(const T* __restrict__ gy, const T* __restrict__ x,
+                         const T* __restrict__ r,
                          const float* __restrict__ gamma, const float* __restrict__ beta,
                          const float* __restrict__ mean, const float* __restrict__ invstd,
                          int64_t c, int64_t hw, int64_t total, int64_t slice_len,
@@ -354,9 +385,9 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) {
           const int64_t off = base + cur.off;
-          g[k] = *reinterpret_cast<const float4*>(gy + off);
-          v[k] = *reinterpret_cast<const float4*>(x + off);
-          q[k] = r ? *reinterpret_cast<const float4*>(r + off) : z4;
+          g[k] = ld4(gy + off);
+          v[k] = ld4(x + off);
+          q[k] = r ? ld4(r + off) : z4;
           cur.advance(kStep, hw, chw);
         }
 #pragma unroll
@@ -364,8 +395,7 @@ __global__ void __launch_bounds__(256)
       }
       for (; i < i1; i += kStep) {
         const int64_t off = base + cur.off;
-        acc(*reinterpret_cast<const float4*>(gy + off), *reinterpret_cast<const float4*>(x + off),
-            r ? *reinterpret_cast<const float4*>(r + off) : z4);
+        acc(ld4(gy + off), ld4(x + off), r ? ld4(r + off) : z4);
         cur.advance(kStep, hw, chw);
       }
     }
@@ -373,8 +403,8 @@ __global__ void __launch_bounds__(256)
     for (int64_t i = i0 + threadIdx.x; i < i1; i += 256) {
       const int64_t nn = i / hw, p = i - nn * hw;
       const int64_t off = base + nn * chw + p;
-      const float v = x[off];
-      const float a = dy_eff(gy[off], v, r ? r[off] : 0.f, sc, sh, act);
+      const float v = ld1(x + off);
+      const float a = dy_eff(ld1(gy + off), v, r ? ld1(r + off) : 0.f, sc, sh, act);
       s1 += a;
       s2 += a * (v - mu);
     }
@@ -433,10 +463,11 @@ __device__ BwdCh bwd_channel(const BwdArgs& P, int64_t ch, double sdy,
   return r;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bn_bwd_apply_plane_kernel(const float* __restrict__ gy, const float* __restrict__ x,
-                              const float* __restrict__ r, float* __restrict__ gx,
-                              float* __restrict__ gr, int64_t c, int64_t hw, int act,
+    bn_bwd_apply_plane_kernel(const T* __restrict__ gy, const T* __restrict__ x,
+                              const T* __restrict__ r, T* __restrict__ gx,
+                              T* __restrict__ gr, int64_t c, int64_t hw, int act,
                               BwdArgs P) {
   __shared__ float cf[5];
   const int64_t plane = blockIdx.y;
@@ -452,33 +483,34 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   const float sc = cf[0], sh = cf[1], A = cf[2], B = cf[3], D = cf[4];
   const int64_t hw4 = hw >> 2;
-  const float4* gp = reinterpret_cast<const float4*>(gy + plane * hw);
-  const float4* xp = reinterpret_cast<const float4*>(x + plane * hw);
-  const float4* rp = r ? reinterpret_cast<const float4*>(r + plane * hw) : nullptr;
-  float4* op = reinterpret_cast<float4*>(gx + plane * hw);
-  float4* orp = gr ? reinterpret_cast<float4*>(gr + plane * hw) : nullptr;
+  const T* gp = gy + plane * hw;
+  const T* xp = x + plane * hw;
+  const T* rp = r ? r + plane * hw : nullptr;
+  T* op = gx + plane * hw;
+  T* orp = gr ? gr + plane * hw : nullptr;
   const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
 #pragma unroll
   for (int k = 0; k < kPlaneChunk4 / 256; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
     if (i < hw4) {
-      const float4 g = gp[i], v = xp[i];
-      const float4 q = rp ? rp[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g = ld4(gp + 4 * i), v = ld4(xp + 4 * i);
+      const float4 q = rp ? ld4(rp + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 e = make_float4(dy_eff(g.x, v.x, q.x, sc, sh, act),
                                    dy_eff(g.y, v.y, q.y, sc, sh, act),
                                    dy_eff(g.z, v.z, q.z, sc, sh, act),
                                    dy_eff(g.w, v.w, q.w, sc, sh, act));
-      op[i] = make_float4(A * e.x + B * v.x + D, A * e.y + B * v.y + D,
-                          A * e.z + B * v.z + D, A * e.w + B * v.w + D);
-      if (orp) orp[i] = e;
+      st4(op + 4 * i, make_float4(A * e.x + B * v.x + D, A * e.y + B * v.y + D,
+                                  A * e.z + B * v.z + D, A * e.w + B * v.w + D));
+      if (orp) st4(orp + 4 * i, e);
     }
   }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bn_bwd_apply_table_kernel(const float* __restrict__ gy, const float* __restrict__ x,
-                              const float* __restrict__ r, float* __restrict__ gx,
-                              float* __restrict__ gr, int64_t planes, int64_t c,
+    bn_bwd_apply_table_kernel(const T* __restrict__ gy, const T* __restrict__ x,
+                              const T* __restrict__ r, T* __restrict__ gx,
+                              T* __restrict__ gr, int64_t planes, int64_t c,
                               int64_t hw, int act, BwdArgs P) {
   extern __shared__ float tab[];  // [5][c]
   for (int64_t ch = threadIdx.x; ch < c; ch += blockDim.x) {
@@ -499,10 +531,10 @@ __global__ void __launch_bounds__(256)
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ch = (t / hw) % c;
-    const float v = x[t];
-    const float e = dy_eff(gy[t], v, r ? r[t] : 0.f, tab[ch], tab[c + ch], act);
-    gx[t] = tab[2 * c + ch] * e + tab[3 * c + ch] * v + tab[4 * c + ch];
-    if (gr) gr[t] = e;
+    const float v = ld1(x + t);
+    const float e = dy_eff(ld1(gy + t), v, r ? ld1(r + t) : 0.f, tab[ch], tab[c + ch], act);
+    st1(gx + t, tab[2 * c + ch] * e + tab[3 * c + ch] * v + tab[4 * c + ch]);
+    if (gr) st1(gr + t, e);
   }
 }
 
@@ -520,17 +552,16 @@ bool args_ok(int64_t n, int64_t c, int64_t h, int64_t w) {
          n * h * w < ((int64_t)1 << 40);
 }
 
-int launch_stats(const float* x, int64_t n, int64_t c, int64_t hw, const Geo& g,
-                 float* part, hipStream_t s) {
-  const double bytes = 4.0 * n * c * (double)hw;
+template <typename T>
+int launch_stats(const T* x, int64_t n, int64_t c, int64_t hw, const Geo& g, float* part,
+                 hipStream_t s) {
+  const double bytes = (double)sizeof(T) * n * c * (double)hw;
   if (hw % 4 == 0) {
-    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, bn_stats_kernel<true>,
-               dim3(g.slices, (unsigned)c), dim3(256), 0, x, c, hw, g.total,
-               g.slice_len, g.slices, part);
+    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, (bn_stats_kernel<T, true>), dim3(g.slices, (unsigned)c),
+               dim3(256), 0, x, c, hw, g.total, g.slice_len, g.slices, part);
   } else {
-    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, bn_stats_kernel<false>,
-               dim3(g.slices, (unsigned)c), dim3(256), 0, x, c, hw, g.total,
-               g.slice_len, g.slices, part);
+    MDE_LAUNCH(mde::K_BN_STATS, bytes, s, (bn_stats_kernel<T, false>), dim3(g.slices, (unsigned)c),
+               dim3(256), 0, x, c, hw, g.total, g.slice_len, g.slices, part);
   }
   return MDE_OK;
 }
@@ -552,20 +583,61 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-int launch_fwd_apply(const float* x, const float* r, float* y, int64_t n,
-                     int64_t c, int64_t hw, int act, const FwdArgs& A,
-                     hipStream_t s) {
-  const double bytes = 4.0 * n * c * (double)hw * (r ? 3.0 : 2.0);
+template <typename T>
+int launch_fwd_apply(const T* x, const T* r, T* y, int64_t n, int64_t c, int64_t hw, int act,
+                     const FwdArgs& A, hipStream_t s) {
+  const double bytes = (double)sizeof(T) * n * c * (double)hw * (r ? 3.0 : 2.0);
   if (plane_mode(hw)) {
-    MDE_LAUNCH(mde::K_BN_APPLY, bytes, s, bn_apply_plane_kernel,
-               plane_grid(n * c, hw), dim3(256), 0, x, r, y, c, hw, act, A);
+    MDE_LAUNCH(mde::K_BN_APPLY, bytes, s, bn_apply_plane_kernel<T>, plane_grid(n * c, hw),
+               dim3(256), 0, x, r, y, c, hw, act, A);
   } else {
-    MDE_LAUNCH(mde::K_BN_APPLY_SMALL, bytes, s, bn_apply_table_kernel,
-               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 2 * c, x,
-               r, y, n * c, c, hw, act, A);
+    MDE_LAUNCH(mde::K_BN_APPLY_SMALL, bytes, s, bn_apply_table_kernel<T>,
+               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 2 * c, x, r, y, n * c, c,
+               hw, act, A);
   }
   return MDE_OK;
 }
+
+template <typename T>
+int fwd_train(const void* x, const void* residual, void* y, int64_t n, int64_t c, int64_t hw,
+              int act, const Geo& g, const FwdArgs& A, hipStream_t s) {
+  const int st = launch_stats((const T*)x, n, c, hw, g, (float*)A.part, s);
+  if (st) return st;
+  return launch_fwd_apply((const T*)x, (const T*)residual, (T*)y, n, c, hw, act, A, s);
+}
+
+template <typename T>
+int bwd(const void* gy, const void* x, const void* residual, void* gx, void* gresidual,
+        int64_t n, int64_t c, int64_t hw, int act, const Geo& g, const BwdArgs& P,
+        const float* gamma, const float* beta, const float* mean, const float* invstd,
+        hipStream_t s) {
+  float* part = (float*)P.part;
+  const T* rr = act ? (const T*)residual : nullptr;
+  const double big = (double)sizeof(T) * n * c * (double)hw;
+  const double rb = rr ? big : 0.0;
+  if (hw % 4 == 0) {
+    MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, (bn_bwd_reduce_kernel<T, true>),
+               dim3(g.slices, (unsigned)c), dim3(256), 0, (const T*)gy, (const T*)x, rr, gamma,
+               beta, mean, invstd, c, hw, g.total, g.slice_len, g.slices, act, part);
+  } else {
+    MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, (bn_bwd_reduce_kernel<T, false>),
+               dim3(g.slices, (unsigned)c), dim3(256), 0, (const T*)gy, (const T*)x, rr, gamma,
+               beta, mean, invstd, c, hw, g.total, g.slice_len, g.slices, act, part);
+  }
+  const double abytes = 3.0 * big + rb + (gresidual ? big : 0.0);
+  if (plane_mode(hw)) {
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_plane_kernel<T>,
+               plane_grid(n * c, hw), dim3(256), 0, (const T*)gy, (const T*)x, rr, (T*)gx,
+               (T*)gresidual, c, hw, act, P);
+  } else {
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, bn_bwd_apply_table_kernel<T>,
+               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c, (const T*)gy,
+               (const T*)x, rr, (T*)gx, (T*)gresidual, n * c, c, hw, act, P);
+  }
+  return MDE_OK;
+}
+
+bool dtype_ok(int dtype) { return dtype == MDE_F32 || dtype == MDE_BF16; }
 
 }  // namespace
 
@@ -583,20 +655,17 @@ int mde_batchnorm_fwd_train(const void* x, const float* gamma, const float* beta
                             void* y, float* save_mean, float* save_invstd,
                             int64_t n, int64_t c, int64_t h, int64_t w, int act,
                             void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace ||
       (!running_mean != !running_var) || act < 0 || act > 2 || !args_ok(n, c, h, w))
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
   const Geo g = geometry(n, c, hw);
-  float* part = (float*)workspace;
-  int st = launch_stats((const float*)x, n, c, hw, g, part, s);
-  if (st) return st;
-  FwdArgs A{gamma, beta, prebias, part, g.slices, g.total, hw, eps, momentum,
+  FwdArgs A{gamma, beta, prebias, (float*)workspace, g.slices, g.total, hw, eps, momentum,
             running_mean, running_var, num_batches_tracked, save_mean, save_invstd, 1};
-  return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c,
-                          hw, act, A, s);
+  return dtype == MDE_BF16 ? fwd_train<bf16>(x, residual, y, n, c, hw, act, g, A, s)
+                           : fwd_train<float>(x, residual, y, n, c, hw, act, g, A, s);
 }
 
 int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
@@ -605,7 +674,7 @@ int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
                            const void* residual, void* y, float* save_mean,
                            float* save_invstd, int64_t n, int64_t c, int64_t h,
                            int64_t w, int act, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !running_mean || !running_var || !y ||
       !save_mean || !save_invstd || act < 0 || act > 2 || !args_ok(n, c, h, w))
     return MDE_ERR_INVALID_ARG;
@@ -614,8 +683,10 @@ int mde_batchnorm_fwd_eval(const void* x, const float* gamma, const float* beta,
   FwdArgs A{gamma, beta, prebias, nullptr, 0, n * hw, hw, eps, 0.f,
             (float*)running_mean, (float*)running_var, nullptr, save_mean,
             save_invstd, 0};
-  return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c,
-                          hw, act, A, s);
+  if (dtype == MDE_BF16)
+    return launch_fwd_apply((const bf16*)x, (const bf16*)residual, (bf16*)y, n, c, hw, act, A, s);
+  return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c, hw, act, A,
+                          s);
 }
 
 int mde_batchnorm_fwd_coef(const void* x, const float* gamma, const float* beta,
@@ -652,42 +723,20 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       float* gprebias, int64_t n, int64_t c, int64_t h,
                       int64_t w, int act, void* workspace, int dtype,
                       void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!gy || !x || !gamma || !beta || !mean || !invstd || !gx || !workspace ||
       act < 0 || act > 2 || !args_ok(n, c, h, w) || (gresidual && !residual && act))
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
   const Geo g = geometry(n, c, hw);
-  float* part = (float*)workspace;
-  const float* rr = act ? (const float*)residual : nullptr;
-  const double big = 4.0 * n * c * (double)hw;
-  const double rb = rr ? big : 0.0;
-  if (hw % 4 == 0) {
-    MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, bn_bwd_reduce_kernel<true>,
-               dim3(g.slices, (unsigned)c), dim3(256), 0, (const float*)gy,
-               (const float*)x, rr, gamma, beta, mean, invstd, c, hw, g.total,
-               g.slice_len, g.slices, act, part);
-  } else {
-    MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, bn_bwd_reduce_kernel<false>,
-               dim3(g.slices, (unsigned)c), dim3(256), 0, (const float*)gy,
-               (const float*)x, rr, gamma, beta, mean, invstd, c, hw, g.total,
-               g.slice_len, g.slices, act, part);
-  }
-  BwdArgs P{gamma, beta, mean, invstd, part, g.slices, g.total, training,
+  BwdArgs P{gamma, beta, mean, invstd, (float*)workspace, g.slices, g.total, training,
             ggamma, gbeta, gprebias};
-  const double abytes = 3.0 * big + rb + (gresidual ? big : 0.0);
-  if (plane_mode(hw)) {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_plane_kernel,
-               plane_grid(n * c, hw), dim3(256), 0, (const float*)gy,
-               (const float*)x, rr, (float*)gx, (float*)gresidual, c, hw, act, P);
-  } else {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, bn_bwd_apply_table_kernel,
-               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c,
-               (const float*)gy, (const float*)x, rr, (float*)gx,
-               (float*)gresidual, n * c, c, hw, act, P);
-  }
-  return MDE_OK;
+  return dtype == MDE_BF16
+             ? bwd<bf16>(gy, x, residual, gx, gresidual, n, c, hw, act, g, P, gamma, beta, mean,
+                         invstd, s)
+             : bwd<float>(gy, x, residual, gx, gresidual, n, c, hw, act, g, P, gamma, beta, mean,
+                          invstd, s);
 }
 
 }  // extern "C"

@@ -94,7 +94,6 @@ class _Bilinear(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         n, c, hi, wi, ho, wo, sh, sw, align = ctx.meta
@@ -118,7 +117,6 @@ class _Nearest(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         n, c, hi, wi, ho, wo, sh, sw = ctx.meta
@@ -194,7 +192,6 @@ class _SECat(torch.autograd.Function):
         return out
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gout):
         xa, xb, w1, w2, s, hidden, mean = ctx.saved_tensors
@@ -243,7 +240,6 @@ class _SkipReduce(torch.autograd.Function):
         return out
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gout):
         r, d, w2 = ctx.saved_tensors
@@ -296,7 +292,6 @@ class _DepthNorm(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, g):
         # y = (x - a)/R, R = b - a; min()/max() spread their gradient evenly
@@ -339,7 +334,6 @@ class _SSIML1(torch.autograd.Function):
         return loss[0].clone(), loss
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, go, _unused):
         gp, gt = ctx.saved_tensors
@@ -382,7 +376,6 @@ class _DepthLoss(torch.autograd.Function):
         return out[0].clone(), out
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, go, _unused):
         pred, gt, out = ctx.saved_tensors

@@ -80,7 +80,6 @@ class _WindowAttn(torch.autograd.Function):
         return out
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gout):
         qk, qk_bias, v, v_bias, table = ctx.saved_tensors
@@ -105,7 +104,6 @@ class _Transpose(torch.autograd.Function):
     """[B, M, N] -> [B, N, M] on the HIP LDS-tiled transpose (its own adjoint)."""
 
     @staticmethod
-
     @_amp_fwd
     def forward(ctx, x):
         x = x.contiguous()
@@ -116,7 +114,6 @@ class _Transpose(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         return _Transpose.apply(gy)
@@ -153,7 +150,6 @@ class _LayerNorm(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         x, weight, mean, rstd = ctx.saved_tensors

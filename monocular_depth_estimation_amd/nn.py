@@ -18,13 +18,19 @@ from .functional import _amp_bwd, _amp_fwd, _gpu, _ws
 _ACTS = {"none": 0, "relu": 1, "hardswish": 2}
 
 
+# BN keeps a bf16 activation in bf16 (autocast convolutions produce and consume
+# bf16; statistics and coefficients stay fp32 in the kernels), anything else in fp32.
+_bn_fwd = torch.amp.custom_fwd(device_type="cuda")
+
+
 class _BatchNormAct(torch.autograd.Function):
     @staticmethod
-    @_amp_fwd
+    @_bn_fwd
     def forward(ctx, x, weight, bias, prebias, residual, running_mean, running_var, nbt,
                 training, momentum, eps, act):
-        x = x.contiguous()
-        residual = residual.contiguous() if residual is not None else None
+        dt = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
+        x = x.to(dt).contiguous()
+        residual = residual.to(dt).contiguous() if residual is not None else None
         n, c, h, w = x.shape
         y = torch.empty_like(x)
         mean = torch.empty(c, dtype=torch.float32, device=x.device)
@@ -47,11 +53,10 @@ class _BatchNormAct(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         x, weight, bias, residual, mean, invstd = ctx.saved_tensors
-        gy = gy.contiguous()
+        gy = gy.to(x.dtype).contiguous()
         n, c, h, w = x.shape
         gx = torch.empty_like(x)
         gw = torch.empty_like(weight) if ctx.needs_input_grad[1] else None
@@ -110,7 +115,6 @@ class _Pointwise(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         x, w2 = ctx.saved_tensors
@@ -134,7 +138,6 @@ class _BNReluPointwise(torch.autograd.Function):
     that into d/dy1 and the BN parameter gradients."""
 
     @staticmethod
-
     @_amp_fwd
     def forward(ctx, y1, gamma, beta, prebias, running_mean, running_var, nbt, training, momentum,
                 eps, w2):
@@ -160,7 +163,6 @@ class _BNReluPointwise(torch.autograd.Function):
         return y2
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy2):
         y1, gamma, beta, mean, invstd, scale, shift, w2m = ctx.saved_tensors
@@ -245,7 +247,6 @@ class _Conv3x3(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
@@ -393,7 +394,6 @@ class _DWConv(torch.autograd.Function):
         return y
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gy):
         x, weight = ctx.saved_tensors
@@ -454,7 +454,6 @@ class _SEGate(torch.autograd.Function):
         return out
 
     @staticmethod
-
     @_amp_bwd
     def backward(ctx, gout):
         x, w1, w2, b2, s, hidden, mean = ctx.saved_tensors

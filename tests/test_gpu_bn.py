@@ -151,3 +151,36 @@ def test_conv_bias_folded_into_bn(train):
         assert float(conv.bias.grad.abs().max()) < 1e-4 * float(conv.weight.grad.abs().max())
     else:
         close_scaled(conv.bias.grad, ref_conv.bias.grad, 1e-4, "dbias")
+
+
+@pytest.mark.parametrize("shape", [(4, 16, 30, 40), (2, 8, 3, 5), (32, 64, 2, 3)])
+@pytest.mark.parametrize("act,res", [("relu", True), ("hardswish", False), ("none", True)])
+def test_batchnorm_bf16_storage_matches_fp32_kernel(shape, act, res):
+    """bf16 activations (the autocast path): the kernels convert on load / store
+    and keep fp32 statistics, so the result must be BIT-EXACT with the fp32
+    kernels run on the bf16 values and rounded to bf16 (round-to-nearest-even),
+    and the parameter gradients / running statistics equal."""
+    from monocular_depth_estimation_amd.nn import BatchNorm2d
+    n, c, h, w = shape
+    x = torch.from_numpy(seeded(shape, 1, -2, 3)).to(DEV).bfloat16()
+    r = torch.from_numpy(seeded(shape, 2, -1, 1)).to(DEV).bfloat16() if res else None
+    gy = torch.from_numpy(seeded(shape, 3, -1, 1)).to(DEV).bfloat16()
+    outs = []
+    for dt in (torch.bfloat16, torch.float32):
+        bn = BatchNorm2d(c, act=act).to(DEV).train()
+        with torch.no_grad():
+            bn.weight.copy_(torch.from_numpy(seeded((c,), 4, 0.5, 1.5)))
+            bn.bias.copy_(torch.from_numpy(seeded((c,), 5, -0.5, 0.5)))
+        xg = x.to(dt).requires_grad_(True)
+        rg = r.to(dt).requires_grad_(True) if res else None
+        y = bn(xg, residual=rg) if res else bn(xg)
+        assert y.dtype == dt
+        grads = torch.autograd.grad(y, [xg, bn.weight, bn.bias] + ([rg] if res else []), gy.to(dt))
+        outs.append((y, grads, bn.running_mean.clone(), bn.running_var.clone()))
+    (yb, gb, mb, vb), (yf, gf, mf, vf) = outs
+    assert torch.equal(yb, yf.bfloat16())
+    assert torch.equal(gb[0], gf[0].bfloat16())
+    assert torch.equal(gb[1], gf[1]) and torch.equal(gb[2], gf[2])
+    if res:
+        assert torch.equal(gb[3], gf[3].bfloat16())
+    assert torch.equal(mb, mf) and torch.equal(vb, vf)

@@ -119,11 +119,6 @@ def main():
         model = PTModel().to(world.device)
     loss_fn = SSIML1(1.0, 0.1, depth_norm=True)
     use_graph = bool(args.graph) and world.device.type == "cuda"
-    if args.amp == "bf16" and args.workload != "guidedepth":
-        # Replaying the captured bf16-autocast step of the NewCRF / SAM models yields
-        # non-finite Linear-bias gradients from the second replay on (eager steps are
-        # finite; tools/debug_bf16.py) -- open issue, so these run eagerly.
-        use_graph = False
     if use_graph:
         from monocular_depth_estimation_amd.train import GraphTrainer
         trainer = GraphTrainer(model, loss_fn, world, lr=1e-4, amp=args.amp)

@@ -416,6 +416,18 @@ int mde_eval_sums(const void* pred, const void* gt, int64_t n, int64_t h, int64_
                   void* workspace, double* sums, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Captured-graph repair (no reference counterpart: the reference runs its step
+ * eagerly, src/train.py:83-114; the build replays it from a hipGraph).
+ * `graph` is a hipGraph_t that has been captured but not instantiated.  On
+ * this ROCm stack a captured hipMemsetAsync is only correct on the graph's
+ * first replay (graph.hip header); mde_graph_replace_memsets swaps every
+ * memset node for a fill-kernel node with the same dependencies and reports
+ * how many it replaced.
+ * ------------------------------------------------------------------------- */
+int mde_graph_count_memsets(void* graph, int64_t* count);
+int mde_graph_replace_memsets(void* graph, int64_t* replaced);
+
+/* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).
  * When enabled, every launch made through this ABI is bracketed by hipEvents
  * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY

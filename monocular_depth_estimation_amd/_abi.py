@@ -93,6 +93,8 @@ SIGNATURES = {
     "mde_eval_workspace": (_sz, [_i64, _i64, _i64]),
     "mde_eval_sums": (_int, [_vp, _vp, _i64, _i64, _i64, _f32, _f32, _int, _c.POINTER(_c.c_int32), _vp,
                              _vp, _int, _vp]),
+    "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
+    "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_timing_enable": (_int, [_int]),
     "mde_timing_reset": (_int, []),
     "mde_timing_collect": (_int, []),
@@ -161,6 +163,33 @@ def dtype_code(t) -> int:
     if t.dtype == torch.bfloat16:
         return MDE_BF16
     raise TypeError(f"unsupported dtype {t.dtype} (the HIP kernels take float32)")
+
+
+# ---------------------------------------------------------------------- graphs
+def graph_count_memsets(raw_graph: int) -> int:
+    n = ctypes.c_int64()
+    check(load().mde_graph_count_memsets(raw_graph, ctypes.byref(n)), "mde_graph_count_memsets")
+    return n.value
+
+
+def graph_replace_memsets(raw_graph: int) -> int:
+    """Swap the memset nodes of a captured, uninstantiated hipGraph for fill
+    kernels (captured memsets are wrong from the second replay on; graph.hip)."""
+    n = ctypes.c_int64()
+    check(load().mde_graph_replace_memsets(raw_graph, ctypes.byref(n)),
+          "mde_graph_replace_memsets")
+    return n.value
+
+
+def capture_graph(fn, stream, pool=None):
+    """Capture fn() on `stream` into a torch CUDAGraph, repair its memset nodes
+    and instantiate it.  Returns (graph, fn's result, memset nodes replaced)."""
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.graph(g, stream=stream, pool=pool):
+        out = fn()
+    n = graph_replace_memsets(g.raw_cuda_graph())
+    g.instantiate()
+    return g, out, n
 
 
 # --------------------------------------------------------------------- timing

@@ -280,18 +280,25 @@ class GraphTrainer:
         return loss
 
     def _capture(self):
+        """Capture the step.  Every memset node the capture recorded (ATen's
+        multi-block reductions zero their semaphores with one) is replaced by
+        a fill kernel before instantiation: captured memsets are only correct
+        on a graph's first replay on this ROCm stack (csrc/graph.hip)."""
+        from . import _abi
         torch.cuda.synchronize()
         self.optimizer.zero_grad(set_to_none=True)  # backward allocates .grad in the graph pool
-        ga = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(ga, stream=self.stream):
-            self.static_loss = self._forward_backward()
+
+        def part_a():
+            loss = self._forward_backward()
             if self.world.size == 1:
                 self.optimizer.step()
-        gb = None
+            return loss
+
+        ga, self.static_loss, na = _abi.capture_graph(part_a, self.stream)
+        gb, nb = None, 0
         if self.world.size > 1:
-            gb = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(gb, stream=self.stream):
-                self._unpack_and_update()
+            gb, _, nb = _abi.capture_graph(self._unpack_and_update, self.stream, pool=ga.pool())
+        self.memsets_replaced = na + nb
         self.graphs = (ga, gb)
 
     def after_step(self, loader_pos: int):

@@ -54,6 +54,14 @@ class Silog_loss_variance(nn.Module):  # noqa: N801  (reference class name)
         self.variance_focus = variance_focus
 
     def forward(self, prediction, gt):
+        """Same value as the reference's boolean-mask form (loss.py:121-129) but
+        mask-multiplied: no data-dependent shape, so no host synchronisation
+        and it can run inside a captured graph.  No valid pixel -> NaN, as the
+        reference's mean over an empty selection."""
         valid = (gt > 1e-3).detach()
-        d = torch.log(torch.clamp(prediction, min=1e-6)[valid]) - torch.log(gt[valid])
-        return torch.sqrt((d * d).mean() - self.variance_focus * d.mean() ** 2) * 10.0
+        n = valid.sum().to(prediction.dtype)
+        safe_gt = torch.where(valid, gt, torch.ones_like(gt))
+        d = torch.where(valid, torch.log(torch.clamp(prediction, min=1e-6)) - torch.log(safe_gt),
+                        torch.zeros_like(prediction))
+        mean_d = d.sum() / n
+        return torch.sqrt((d * d).sum() / n - self.variance_focus * mean_d ** 2) * 10.0

@@ -344,7 +344,17 @@ def build_parser():
     p.add_argument("--log", default="", help="JSONL file for Train/Loss scalars (rank 0)")
     p.add_argument("--seed", default=0, type=int)
     p.add_argument("--amp", default="fp32", choices=("fp32", "bf16"),
-                   help="bf16 = autocast convs / GEMMs (BASELINE cfg3); HIP kernels stay fp32")
+                   help="bf16 = autocast (BASELINE cfg3): convs / GEMMs in bf16 on MIOpen / hipBLASLt, "
+                        "BN HIP kernels on bf16 activations (fp32 statistics), other HIP kernels fp32")
+    p.add_argument("--pretrained", action="store_true",
+                   help="GuideDepth(True) as the reference's train.py:34: load the DDRNet-23-slim "
+                        "ImageNet blob (DDRNet_23_slim.py:357-365) non-strictly into the encoder")
+    p.add_argument("--weights", default="",
+                   help="path of DDRNet23s_imagenet.pth (default: the reference's relative path "
+                        "./GuideDepth/model/weights/DDRNet23s_imagenet.pth)")
+    p.add_argument("--graph", action="store_true",
+                   help="replay the step from HIP graphs (GraphTrainer; BN stays in train mode, "
+                        "i.e. implies --no-eval-quirk)")
     return p
 
 
@@ -356,14 +366,21 @@ def main(argv=None):
     from .utils import AverageMeter
 
     torch.manual_seed(args.seed)
-    model = GuideDepth(pretrained=False).to(world.device)
-    optimizer = make_adam(model, args.lr)
+    if args.weights:
+        os.environ["MDE_DDRNET_WEIGHTS"] = args.weights
+    model = GuideDepth(pretrained=args.pretrained).to(world.device)
+    loss_fn = SSIML1(1.0, 0.1, depth_norm=True)
+    if args.graph:
+        trainer = GraphTrainer(model, loss_fn, world, lr=args.lr, amp=args.amp)
+        optimizer, ddp = trainer.optimizer, model
+    else:
+        optimizer = make_adam(model, args.lr)
+        ddp = wrap_ddp(model, world)
+        trainer = Trainer(ddp, optimizer, loss_fn, world, eval_quirk=not args.no_eval_quirk,
+                          amp=args.amp)
     start_epoch = 0
-    if args.cp == 1:
+    if args.cp == 1:  # train.py:59-68: restarts AT the saved epoch
         start_epoch, _ = load_checkpoint(args.checkpoint, model, optimizer)
-    ddp = wrap_ddp(model, world)
-    trainer = Trainer(ddp, optimizer, SSIML1(1.0, 0.1, depth_norm=True), world,
-                      eval_quirk=not args.no_eval_quirk, amp=args.amp)
     log = open(args.log, "a") if (args.log and world.is_main) else None
     loader = None
     if args.data:  # data.py:171-179 on the GPU path; each rank reads a disjoint 1/size of the rows
@@ -390,7 +407,7 @@ def main(argv=None):
             loss = trainer.step(image, depth)
             trainer.after_step(pos)
             if pos % 5 == 0 and world.is_main:  # train.py:123-132 (host read at log points only)
-                v = float(loss)
+                v = float(loss.detach())
                 losses.update(v, image.size(0))
                 dt = time.time() - t0
                 print(f"Epoch: [{epoch}][{pos}/{n_steps}]\tTime {dt:.3f}\t"

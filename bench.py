@@ -8,9 +8,12 @@ One step = the src/train.py step (train.py:86-114) on one synthetic batch
 already resident in HBM: GuideDepth forward (BN in train mode), DepthNorm +
 1.0*SSIM + 0.1*L1 (one fused HIP pass), backward, DDP all-reduce over RCCL
 (N > 1), Adam step.  Rank 0 prints ONE JSON line.  Extra fields:
-  roofline     — the dominant hand-written HIP kernel over the timed region
-                 (HIP events on its launch stream; algorithmic bytes per
-                 SURVEY §8(d)); traffic from profiles/ PMC counters if present.
+  roofline     — the dominant hand-written HIP kernel of the step (HIP events
+                 captured into the replayed step graph; algorithmic bytes /
+                 flops per SURVEY §8(d)); traffic = rocprofv3 PMC HBM bytes
+                 per launch from profiles/ (traffic_ratio = traffic / algorithmic).
+  roofline_leaders — the top HBM-bound and the top MFMA-bound hand kernels.
+  path_roofline — north_star's depthwise+upsample path (resizes + depthwise).
   cpu_baseline — the CPU oracle's train step (rank 0, N=1 only), bounded sample.
 """
 from __future__ import annotations
@@ -29,7 +32,12 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # fp32-input MFMA dense peak (= fp32 vector rate, MI355X_MICROARCH.md)
-PMC_FILE = os.path.join(REPO, "profiles", "r01_pmc_traffic.json")
+# rocprofv3 PMC HBM bytes per launch (tools/pmc_traffic.py), newest round first
+PMC_FILES = [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic.json") for r in (2, 1)]
+
+
+AMP_DTYPE = ("bf16 autocast: convs / GEMMs bf16 (MIOpen / hipBLASLt); BatchNorm HIP kernels bf16 "
+             "I/O with fp32 statistics; other HIP kernels fp32")
 
 
 def parse():
@@ -46,27 +54,44 @@ def parse():
     p.add_argument("--width", type=int, default=640)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--amp", choices=("fp32", "bf16"), default="fp32",
-                   help="bf16: BASELINE cfg3 autocast (convs / GEMMs bf16, HIP kernels fp32)")
-    p.add_argument("--cpu-bs", type=int, default=4)
+                   help="bf16: BASELINE cfg3 autocast (convs / GEMMs bf16; BN HIP kernels bf16 I/O)")
+    p.add_argument("--cpu-bs", type=int, default=0, help="CPU-baseline batch (0 = the GPU batch)")
     p.add_argument("--cpu-steps", type=int, default=2)
     p.add_argument("--cudnn-benchmark", type=int, default=0)
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--graph", type=int, default=1,
                    help="1: replay the captured step from HIP graphs (GraphTrainer); 0: eager")
     p.add_argument("--timing-steps", type=int, default=3,
-                   help="eager steps timed per kernel with HIP events after the timed loop")
+                   help="replays of the step (graph mode) / eager steps timed per kernel with HIP "
+                        "events after the timed loop")
     args = p.parse_args()
     if args.bs is None:
         args.bs = 32 if args.workload == "guidedepth" else 16
     return args
 
 
+def _cpu_model_name() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(args):
-    """The oracle (CPU restatement, same ATen CPU convs/BN as the reference) timed on host cores."""
+    """The oracle (CPU restatement, the same ATen CPU convs / BN as the reference,
+    pinned to it by tests/golden) timed on the host: the metric's own shape
+    (640x480, bs 32 = cfg2) for 1 warm-up + `cpu_steps` steps.
+
+    Threads: OMP_NUM_THREADS when set -- the CPU share a job gets on the GPU box
+    (16 per GPU there; os.cpu_count() shows the whole machine's CPUs, which this
+    job may not use) -- else every core os.cpu_count() reports."""
     from oracle import guidedepth as og
     from oracle import mobilenetv3 as om
     from oracle import ops as oops
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
     torch.set_num_threads(threads)
     if args.workload == "sam":
         from oracle import sam as osam
@@ -77,9 +102,10 @@ def cpu_baseline(args):
     else:
         model = (og.GuideDepth() if args.workload == "guidedepth" else om.PTModel()).train()
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], 1e-4)
+    bs = args.cpu_bs or args.bs
     g = torch.Generator().manual_seed(0)
-    img = torch.rand((args.cpu_bs, 3, args.height, args.width), generator=g)
-    dep = 0.1 + 9.9 * torch.rand((args.cpu_bs, 1, args.height, args.width), generator=g)
+    img = torch.rand((bs, 3, args.height, args.width), generator=g)
+    dep = 0.1 + 9.9 * torch.rand((bs, 1, args.height, args.width), generator=g)
 
     def step():
         loss = oops.train_loss(model(img), dep)
@@ -92,10 +118,12 @@ def cpu_baseline(args):
     for _ in range(args.cpu_steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": round(args.cpu_bs * args.cpu_steps / dt, 3), "unit": "images/s",
+    name = "GuideDepth" if args.workload == "guidedepth" else "PTModel"
+    return {"value": round(bs * args.cpu_steps / dt, 3), "unit": "images/s",
             "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle {'GuideDepth' if args.workload == 'guidedepth' else 'PTModel'} train step, {args.height}x{args.width} bs={args.cpu_bs}, "
-                      f"{args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s), fp32"}
+            "host_cpu": f"{_cpu_model_name()} ({os.cpu_count()} logical CPUs on the host)",
+            "sample": f"oracle {name} train step (SSIM+0.1*L1, Adam), {args.width}x{args.height} "
+                      f"bs={bs}, fp32, {args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s)"}
 
 
 def main():
@@ -152,22 +180,22 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     # Per-kernel HIP-event timing (the registry brackets every ABI launch on its
-    # stream).  Graph replay bypasses the launch path, so in graph mode the
-    # same step is run eagerly `timing_steps` more times for this; in eager
-    # mode the timed loop itself is measured.
+    # stream).  Graph mode: the step is captured once more with the events as
+    # graph nodes and that graph is replayed `timing_steps` times, so the times
+    # are those of the REPLAYED step; eager mode: the timed loop is re-run.
     kernels = {}
+    timing_steps = args.timing_steps if use_graph else args.steps
     if not args.no_kernel_timing:
-        _abi.timing_reset()
-        _abi.timing_enable(True)
         if use_graph:
-            for i in range(args.timing_steps):
-                trainer.eager_step(*batches[i % 2])
+            kernels = trainer.timed_replays(batches, args.timing_steps)
         else:
+            _abi.timing_reset()
+            _abi.timing_enable(True)
             for i in range(args.steps):
                 trainer.step(*batches[i % 2])
-        barrier()
-        _abi.timing_enable(False)
-        kernels = _abi.timing_collect()
+            barrier()
+            _abi.timing_enable(False)
+            kernels = _abi.timing_collect()
     if world.size > 1:
         t = torch.tensor([elapsed], device=world.device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -179,26 +207,42 @@ def main():
         return
 
     images = world.size * args.bs * args.steps
-    roofline = None
-    if kernels:
-        name, (ms, launches, nbytes, flops) = max(kernels.items(), key=lambda kv: kv[1][0])
-        traffic = None
-        if os.path.exists(PMC_FILE):
-            with open(PMC_FILE) as f:
-                traffic = json.load(f).get(name, {}).get("bytes_per_launch")
-        if flops > 0:  # an MFMA kernel (conv3x3): priced against the fp32 MFMA peak
+    pmc = {}
+    pmc_file = next((f for f in PMC_FILES if os.path.exists(f)), None)
+    if pmc_file:
+        with open(pmc_file) as f:
+            pmc = json.load(f)
+
+    def roof(name):
+        ms, launches, nbytes, flops = kernels[name]
+        traffic = pmc.get(name, {}).get("bytes_per_launch")
+        per_launch = nbytes / launches
+        common = {"kernel": name, "traffic": traffic,
+                  "traffic_ratio": round(traffic / per_launch, 3) if traffic else None,
+                  "bytes_per_launch": per_launch, "avg_launch_us": round(ms * 1e3 / launches, 2),
+                  "launches_per_step": launches / timing_steps,
+                  "ms_per_step": round(ms / timing_steps, 3)}
+        if flops > 0:  # MFMA kernels (conv3x3, pointwise/skip, attention): fp32 MFMA peak
             achieved = flops / (ms * 1e-3) / 1e12
-            roofline = {"bound": "mfma", "kernel": name, "achieved": round(achieved, 2),
-                        "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
-                        "frac": round(achieved / MFMA_F32_PEAK_TFS, 4), "traffic": traffic,
-                        "flops_per_launch": flops / launches, "bytes_per_launch": nbytes / launches,
-                        "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
-        else:
-            achieved = nbytes / (ms * 1e-3) / 1e9
-            roofline = {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1),
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                        "traffic": traffic, "bytes_per_launch": nbytes / launches,
-                        "avg_launch_us": round(ms * 1e3 / launches, 2), "launches": launches}
+            return dict({"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
+                         "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4),
+                         "flops_per_launch": flops / launches}, **common)
+        achieved = nbytes / (ms * 1e-3) / 1e9
+        return dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4)}, **common)
+
+    roofline, leaders = None, {}
+    if kernels:
+        by_time = sorted(kernels, key=lambda k: -kernels[k][0])
+        roofline = roof(by_time[0])
+        for bound in ("hbm", "mfma"):
+            name = next((k for k in by_time if (kernels[k][3] > 0) == (bound == "mfma")), None)
+            if name:
+                leaders[bound] = roof(name)
+        roofline["timing"] = ("HIP events captured into the replayed step graph, "
+                              f"{timing_steps} replays" if use_graph else
+                              f"HIP events over {timing_steps} eager steps")
+        roofline["pmc_source"] = os.path.relpath(pmc_file, REPO) if pmc_file else None
     # north_star's "depthwise+upsample path": every resize (bilinear, nearest)
     # and depthwise-conv launch of the step, aggregated (sum bytes / sum time)
     path = {k: v for k, v in kernels.items()
@@ -211,7 +255,7 @@ def main():
         path_roofline = {"bound": "hbm", "kernels": sorted(path), "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "ms_per_step": round(ms / (args.timing_steps if use_graph else args.steps), 3)}
+                         "ms_per_step": round(ms / timing_steps, 3)}
     if args.workload == "guidedepth":
         metric = "training images/sec at 640x480 bs=32/GPU (GuideDepth, SSIM+0.1*L1, Adam)"
         workload = ("GuideDepth (DDRNet-23-slim + 3 guided upsampling blocks) train step, "
@@ -232,7 +276,7 @@ def main():
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32" if args.amp == "fp32" else "bf16 autocast (convs / GEMMs bf16; HIP kernels fp32)",
+        "dtype": "fp32" if args.amp == "fp32" else AMP_DTYPE,
         "data": "synthetic (U[0,1) images, U[0.1,10) depths, resident in HBM), random-init weights",
         "config": {"workload": workload,
                    "global_batch": world.size * args.bs, "per_gpu_batch": args.bs,
@@ -241,6 +285,7 @@ def main():
         "execution": ("hipGraph replay of the whole step (GraphTrainer)" if use_graph
                       else "eager (Trainer + DDP)"),
         "roofline": roofline,
+        "roofline_leaders": leaders,
         "path_roofline": path_roofline,
         "hip_kernels": {k: dict({"ms_total": round(v[0], 3), "launches": v[1],
                                  "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 else None},

@@ -431,8 +431,11 @@ int mde_graph_replace_memsets(void* graph, int64_t* replaced);
  * Opt-in kernel timing registry (measurement only; off by default).
  * When enabled, every launch made through this ABI is bracketed by hipEvents
  * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY
- * §8(d) formulas) are accumulated.  Not graph-capture safe: disable it before
- * capturing.
+ * §8(d) formulas) are accumulated.  Launches made while the stream is being
+ * captured into a hipGraph record their events as external event nodes: each
+ * replay re-records them, and mde_timing_collect (called once after each
+ * replay) adds that replay's times, keeping the events until
+ * mde_timing_reset.
  * ------------------------------------------------------------------------- */
 int mde_timing_enable(int on);
 int mde_timing_reset(void);

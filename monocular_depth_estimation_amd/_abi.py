@@ -201,10 +201,12 @@ def timing_reset() -> None:
     call("mde_timing_reset")
 
 
-def timing_collect() -> dict:
-    """Resolve pending events; return {kernel: (total_ms, launches, bytes, flops)}."""
+def timing_collect(resolve: bool = True) -> dict:
+    """Resolve pending events (resolve=True; once per graph replay when the
+    events were captured) and return {kernel: (total_ms, launches, bytes, flops)}."""
     lib = load()
-    check(lib.mde_timing_collect(), "mde_timing_collect")
+    if resolve:
+        check(lib.mde_timing_collect(), "mde_timing_collect")
     out = {}
     for k in range(lib.mde_kernel_count()):
         ms, n, by = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()

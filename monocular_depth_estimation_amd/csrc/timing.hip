@@ -1,6 +1,11 @@
 // Opt-in per-kernel timing registry behind mde_timing_* (include/mde_abi.h).
 // Each timed launch is bracketed by two hipEvents recorded on the launch
 // stream; mde_timing_collect() resolves them into per-kernel totals.
+// A launch made while its stream is being captured into a hipGraph records
+// its events as external event-record nodes (hipEventRecordExternal): every
+// replay of that graph re-records them, and mde_timing_collect() accumulates
+// the last replay's times while keeping those events for the next replay —
+// per-kernel times of the REPLAYED step (collect once after each replay).
 #include <mutex>
 #include <vector>
 
@@ -27,6 +32,7 @@ struct Pending {
   hipEvent_t a, b;
   double bytes, flops;
   bool done;
+  bool captured;  // recorded inside a graph capture: kept across collects
 };
 
 struct Registry {
@@ -56,6 +62,33 @@ Registry& reg() {
   return r;
 }
 
+// Record `e` on `s`.  Inside a capture: as an external event node
+// (hipEventRecordExternal), else by adding an event-record node to the
+// capturing graph by hand and making it the stream's capture dependency.
+// Errors are cleared so that they never reach the kernel launch's
+// hipGetLastError check.
+bool record(hipEvent_t e, hipStream_t s, bool captured) {
+  if (!captured) {
+    const bool ok = hipEventRecord(e, s) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+    return ok;
+  }
+  if (hipEventRecordWithFlags(e, s, hipEventRecordExternal) == hipSuccess) return true;
+  (void)hipGetLastError();
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  hipGraphNode_t node = nullptr;
+  bool ok = hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &nd) == hipSuccess && g &&
+            hipGraphAddEventRecordNode(&node, g, deps, nd, e) == hipSuccess &&
+            hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies) ==
+                hipSuccess;
+  if (!ok) (void)hipGetLastError();
+  return ok;
+}
+
 }  // namespace
 
 namespace mde {
@@ -64,9 +97,16 @@ int timing_begin(int kid, hipStream_t s) {
   Registry& r = reg();
   if (!r.on) return -1;
   std::lock_guard<std::mutex> g(r.mu);
-  Pending p{kid, r.get(), r.get(), 0.0, 0.0, false};
+  Pending p{kid, r.get(), r.get(), 0.0, 0.0, false, false};
   if (!p.a || !p.b) return -1;
-  (void)hipEventRecord(p.a, s);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  (void)hipStreamIsCapturing(s, &cs);
+  p.captured = cs == hipStreamCaptureStatusActive;
+  if (!record(p.a, s, p.captured)) {
+    r.pool.push_back(p.a);
+    r.pool.push_back(p.b);
+    return -1;
+  }
   r.pending.push_back(p);
   return (int)r.pending.size() - 1;
 }
@@ -77,10 +117,9 @@ void timing_end(int token, hipStream_t s, double bytes, double flops) {
   std::lock_guard<std::mutex> g(r.mu);
   if (token >= (int)r.pending.size()) return;
   Pending& p = r.pending[token];
-  (void)hipEventRecord(p.b, s);
   p.bytes = bytes;
   p.flops = flops;
-  p.done = true;
+  p.done = record(p.b, s, p.captured);
 }
 
 }  // namespace mde
@@ -113,6 +152,7 @@ int mde_timing_collect(void) {
   Registry& r = reg();
   std::lock_guard<std::mutex> g(r.mu);
   int status = MDE_OK;
+  std::vector<Pending> keep;
   for (auto& p : r.pending) {
     if (p.done) {
       hipError_t e = hipEventSynchronize(p.b);
@@ -127,10 +167,14 @@ int mde_timing_collect(void) {
         status = (int)e;
       }
     }
+    if (p.captured) {
+      keep.push_back(p);
+      continue;
+    }
     r.pool.push_back(p.a);
     r.pool.push_back(p.b);
   }
-  r.pending.clear();
+  r.pending.swap(keep);
   return status;
 }
 

@@ -304,6 +304,42 @@ class GraphTrainer:
     def after_step(self, loader_pos: int):
         pass
 
+    def timed_replays(self, batches, replays: int = 3) -> dict:
+        """Per-kernel HIP-event times of the REPLAYED step (measurement only).
+
+        The step is captured once more with the timing registry on, so each
+        HIP launch is bracketed by event-record nodes inside the graph; that
+        graph is replayed `replays` times and the registry resolved after each
+        replay.  Returns _abi.timing_collect()'s {kernel: (ms, launches,
+        bytes, flops)} over all replays.  Leaves the trainer on a second set of
+        gradient buffers: call it after the timed loop."""
+        from . import _abi
+        torch.cuda.synchronize()
+        _abi.timing_reset()
+        self.optimizer.zero_grad(set_to_none=True)
+
+        def part():
+            loss = self._forward_backward()
+            if self.world.size == 1:
+                self.optimizer.step()
+            return loss
+
+        _abi.timing_enable(True)
+        try:
+            graph, _, _ = _abi.capture_graph(part, self.stream)
+        finally:
+            _abi.timing_enable(False)
+        for i in range(replays):
+            image, depth = batches[i % len(batches)]
+            self.static_image.copy_(image)
+            self.static_depth.copy_(depth)
+            graph.replay()
+            torch.cuda.synchronize()
+            _abi.call("mde_timing_collect")
+        out = _abi.timing_collect(resolve=False)
+        _abi.timing_reset()
+        return out
+
 
 def make_adam(model, lr=1e-4):
     kw = {}

@@ -267,6 +267,157 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   }
 }
 
+// Exact integer ratio S = 4 or 8 (align_corners=False, scale 1/S): the
+// MobileNetV3-NewCRF head upsample (model_mobileV3_large_newCRFs.py:55-58,124,
+// 1 x 120x160 -> 480x640).  One lane owns input column j of one plane and a
+// band of kXsRows input rows.  Forward: each input row is interpolated
+// horizontally once into the lane's S output columns (S/4 float4s); every
+// output row r then mixes the two input rows lin_index(r) names (ATen's order:
+// rows of horizontally interpolated columns), written as S/4 float4 stores
+// per lane -- coalesced rows.  Backward (the adjoint, a gather): the lane reads
+// the S gradient columns it owns as float4s per output row, gets the S/2 halo
+// columns on either side from the neighbouring lanes by wave shuffles (loads
+// only at wave edges), forms the column-adjoint sum with its 2S exact weights
+// (lin_weight, so the clamped edges are exact) and adds it into the (at most
+// two) band rows lin_index(r) names.  All rows of a band are unrolled so their
+// loads are in flight together.  gy rows at band edges are read by two bands
+// (S of every S*kXsRows + S rows, served by L2).
+constexpr int kXsRows = 4;   // input rows per lane
+constexpr int kXsWarps = 4;  // threadIdx.y
+
+template <int S>
+__global__ void __launch_bounds__(64 * kXsWarps)
+    bilinear_fwd_xs_kernel(const float* __restrict__ x, float* __restrict__ y, int hi, int wi) {
+  const int lane = threadIdx.x;
+  const int j = blockIdx.x * 64 + lane;
+  const int i0 = (blockIdx.y * kXsWarps + threadIdx.y) * kXsRows;
+  if (i0 >= hi) return;  // uniform per wave
+  const bool ok = j < wi;
+  const int jc = ok ? j : wi - 1;
+  const int64_t plane = blockIdx.z;
+  const float* xp = x + plane * hi * (int64_t)wi;
+  const int wo = S * wi, ho = S * hi;
+  const float sc = 1.f / S;
+  // this lane's S output columns: input columns and weights (exact ATen math)
+  Lin W[S];
+#pragma unroll
+  for (int q = 0; q < S; ++q) W[q] = lin_index(sc, S * jc + q, wi, 0);
+  auto hrow = [&](int r, float* o) {
+    r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
+    const float* row = xp + (int64_t)r * wi;
+#pragma unroll
+    for (int q = 0; q < S; ++q) o[q] = W[q].l0 * row[W[q].i0] + W[q].l1 * row[W[q].i1];
+  };
+  float rows[kXsRows + 2][S];
+#pragma unroll
+  for (int k = 0; k < kXsRows + 2; ++k) hrow(i0 - 1 + k, rows[k]);
+  float* yp = y + plane * ho * (int64_t)wo + S * jc;
+#pragma unroll
+  for (int k = 0; k < kXsRows; ++k) {
+    const int i = i0 + k;
+    if (i >= hi) break;  // uniform per wave
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      const int r = S * i + q;
+      // interior: rows (i-1, i) for q < S/2, (i, i+1) after; at the plane
+      // edges lin_index clamps onto the same row, which rows[] also holds
+      // (hrow clamps), so the static pick gives ATen's value there too
+      const Lin H = lin_index(sc, r, hi, 0);
+      const float* a = rows[q < S / 2 ? k : k + 1];
+      const float* b = rows[q < S / 2 ? k + 1 : k + 2];
+      float o[S];
+#pragma unroll
+      for (int c = 0; c < S; ++c) o[c] = H.l0 * a[c] + H.l1 * b[c];
+      if (ok) {
+#pragma unroll
+        for (int c = 0; c < S; c += 4)
+          *reinterpret_cast<float4*>(yp + (int64_t)r * wo + c) =
+              make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]);
+      }
+    }
+  }
+}
+
+template <int S>
+__global__ void __launch_bounds__(64 * kXsWarps)
+    bilinear_bwd_xs_kernel(const float* __restrict__ gy, float* __restrict__ gx, int hi, int wi) {
+  constexpr int HALF = S / 2;
+  const int lane = threadIdx.x;
+  const int j = blockIdx.x * 64 + lane;
+  const int ib = (blockIdx.y * kXsWarps + threadIdx.y) * kXsRows;
+  if (ib >= hi) return;  // uniform per wave
+  const bool ok = j < wi;
+  const int jc = ok ? j : wi - 1;
+  const int64_t plane = blockIdx.z;
+  const int wo = S * wi, ho = S * hi;
+  const float sc = 1.f / S;
+  const float* gp = gy + plane * ho * (int64_t)wo;
+  // weights of output columns S*j - HALF .. S*j + S + HALF - 1 for input column j
+  float wc[2 * S];
+#pragma unroll
+  for (int k = 0; k < 2 * S; ++k) {
+    const int c = S * jc - HALF + k;
+    wc[k] = (c >= 0 && c < wo) ? lin_weight(sc, c, jc, wi, 0) : 0.f;
+  }
+  float acc[kXsRows];
+#pragma unroll
+  for (int k = 0; k < kXsRows; ++k) acc[k] = 0.f;
+  const bool edge_l = lane == 0 || jc == 0, edge_r = lane == 63 || jc == wi - 1 || j + 1 >= wi;
+  constexpr int NR = S * kXsRows + S;  // output rows S*ib - HALF .. S*(ib+R) + HALF - 1
+#pragma unroll
+  for (int k = 0; k < NR; ++k) {
+    const int r = S * ib - HALF + k;
+    if (r < 0 || r >= ho) continue;  // uniform per wave
+    const float* row = gp + (int64_t)r * wo;
+    float v[S];
+#pragma unroll
+    for (int c = 0; c < S; c += 4) {
+      const float4 t = *reinterpret_cast<const float4*>(row + S * jc + c);
+      v[c] = t.x; v[c + 1] = t.y; v[c + 2] = t.z; v[c + 3] = t.w;
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int h = 0; h < HALF; ++h) {  // halo: last HALF of lane-1, first HALF of lane+1
+      float l = __shfl_up(v[S - HALF + h], 1, 64);
+      float rr = __shfl_down(v[h], 1, 64);
+      const int cl = S * jc - HALF + h, cr = S * jc + S + h;
+      if (edge_l) l = cl >= 0 ? row[cl] : 0.f;
+      if (edge_r) rr = cr < wo ? row[cr] : 0.f;
+      s += wc[h] * l;
+      s += wc[S + HALF + h] * rr;
+    }
+#pragma unroll
+    for (int c = 0; c < S; ++c) s += wc[HALF + c] * v[c];
+    const Lin H = lin_index(sc, r, hi, 0);
+#pragma unroll
+    for (int b = 0; b < kXsRows; ++b) {
+      float wgt = 0.f;
+      if (H.i0 == ib + b) wgt += H.l0;
+      if (H.i1 == ib + b) wgt += H.l1;
+      acc[b] += wgt * s;
+    }
+  }
+  if (!ok) return;
+  float* out = gx + (plane * hi + ib) * (int64_t)wi + j;
+#pragma unroll
+  for (int b = 0; b < kXsRows; ++b)
+    if (ib + b < hi) out[(int64_t)b * wi] = acc[b];
+}
+
+inline dim3 xs_grid(int64_t planes, int64_t hi, int64_t wi) {
+  return dim3((unsigned)mde::cdiv(wi, 64), (unsigned)mde::cdiv(hi, kXsRows * kXsWarps),
+              (unsigned)planes);
+}
+
+// Integer upsampling ratio handled by the xS kernels (4 or 8), else 0.
+int xs_ratio(int64_t hi, int64_t wi, int64_t ho, int64_t wo, float sh, float sw, int align,
+             int64_t planes) {
+  if (align || planes > 65535) return 0;
+  for (int r : {4, 8})
+    if (ho == r * hi && wo == r * wi && sh == 1.f / r && sw == 1.f / r) return r;
+  return 0;
+}
+
 inline dim3 x2_grid(int64_t planes, int64_t hi, int64_t wi) {
   return dim3((unsigned)mde::cdiv(wi, 64), (unsigned)mde::cdiv(hi, kX2Rows * kX2Warps),
               (unsigned)planes);
@@ -522,7 +673,14 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   // busy as the one-column kernel: 64-lane rows of wi/2 pairs vs of wi columns.
   const bool pair = x2 && wi % 2 == 0 &&
                     mde::cdiv(wi, 64) >= 2 * mde::cdiv(wi / 2, 64);
-  if (pair) {
+  const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, n * c);
+  if (xs == 4) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<4>, xs_grid(n * c, hi, wi),
+               dim3(64, kXsWarps), 0, (const float*)x, (float*)y, (int)hi, (int)wi);
+  } else if (xs == 8) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<8>, xs_grid(n * c, hi, wi),
+               dim3(64, kXsWarps), 0, (const float*)x, (float*)y, (int)hi, (int)wi);
+  } else if (pair) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel,
                x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)x, (float*)y,
                (int)hi, (int)wi);
@@ -555,7 +713,14 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
   const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
                   ho == 2 * hi && wo == 2 * wi && planes <= 65535;
-  if (x2 && wi % 2 == 0) {
+  const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes);
+  if (xs == 4) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<4>, xs_grid(planes, hi, wi),
+               dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
+  } else if (xs == 8) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<8>, xs_grid(planes, hi, wi),
+               dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
+  } else if (x2 && wi % 2 == 0) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel,
                x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy,
                (float*)gx, (int)hi, (int)wi);

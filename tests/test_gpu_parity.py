@@ -82,6 +82,10 @@ def test_nearest_golden_bit_exact(golden, case):
     ((2, 3, 11, 7), dict(scale_factor=2)),                # x2, odd width: per-column kernel
     ((32, 64, 8, 10), dict(size=(60, 80))),               # DDRNet spp -> H/8 (x7.5)
     ((32, 64, 15, 20), dict(size=(60, 80))),              # compression4 (x4)
+    ((16, 1, 120, 160), dict(scale_factor=4)),            # NewCRF head x4 (cfg4)
+    ((2, 3, 9, 70), dict(scale_factor=4)),                # x4, odd rows, two column blocks
+    ((1, 2, 5, 3), dict(scale_factor=4)),                 # x4, tiny plane (every edge case)
+    ((2, 2, 7, 66), dict(scale_factor=8)),                # x8
     ((2, 3, 100, 150), dict(size=(310, 470))),            # plane > LDS: banded kernel
     ((1, 2, 10, 10), dict(size=(200, 210))),              # x20: per-pixel gather kernel
     ((2, 3, 37, 41), dict(size=(111, 90), align_corners=True)),

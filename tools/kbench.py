@@ -94,6 +94,15 @@ def _main():
         report(f"bilinear_bwd {c}x{hi}x{wi}->60x80", timeit(lambda: _abi.call(
             "mde_bilinear_bwd", gy.data_ptr(), x.data_ptr(), n, c, hi, wi, 60, 80, hi / 60, wi / 80,
             0, 0, _abi.stream_of(x)), a.reps), nb)
+    if want("resize"):  # NewCRF head: sigmoid map x4 (cfg4, bs 16)
+        x = torch.rand(16, 1, 120, 160, device=dev)
+        nb = 4.0 * 16 * (120 * 160 + 480 * 640)
+        report("bilinear_fwd x4 1x120x160 (bs16)", timeit(lambda: F.bilinear_resize(x, scale_factor=4),
+                                                         a.reps), nb)
+        gy = torch.rand(16, 1, 480, 640, device=dev)
+        report("bilinear_bwd x4 1x120x160 (bs16)", timeit(lambda: _abi.call(
+            "mde_bilinear_bwd", gy.data_ptr(), x.data_ptr(), 16, 1, 120, 160, 480, 640, 0.25, 0.25,
+            0, 0, _abi.stream_of(x)), a.reps), nb)
     if want("resize"):
         img = torch.rand(n, 3, 480, 640, device=dev)
         for sf in (0.5, 0.25):
@@ -182,9 +191,11 @@ def _main():
                               a.reps), 7 * tok)
     if want("dw"):
         from monocular_depth_estimation_amd.nn import depthwise_conv2d
-        for c, h, w, k, st in ((16, 240, 320, 3, 1), (64, 240, 320, 3, 2), (72, 120, 160, 5, 2),
-                               (120, 60, 80, 5, 1), (240, 60, 80, 3, 2), (672, 30, 40, 5, 2),
-                               (960, 15, 20, 5, 1)):
+        # every depthwise stage of MobileNetV3-Large at 480x640 (features[1..15]; x2 = repeated)
+        for c, h, w, k, st in ((16, 240, 320, 3, 1), (64, 240, 320, 3, 2), (72, 120, 160, 3, 1),
+                               (72, 120, 160, 5, 2), (120, 60, 80, 5, 1), (240, 60, 80, 3, 2),
+                               (200, 30, 40, 3, 1), (184, 30, 40, 3, 1), (480, 30, 40, 3, 1),
+                               (672, 30, 40, 3, 1), (672, 30, 40, 5, 2), (960, 15, 20, 5, 1)):
             conv = torch.nn.Conv2d(c, c, k, st, k // 2, groups=c, bias=False).to(dev)
             x = torch.randn(n4, c, h, w, device=dev, requires_grad=True)
             y = depthwise_conv2d(x, conv)

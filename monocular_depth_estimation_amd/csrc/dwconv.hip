@@ -194,6 +194,28 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// gw[ch, t] = sum_g part[(ch * G + g), t]: one wave per channel, lane l sums
+// partials l, l + 64, ... of every tap (all loads in flight), then a
+// fixed-order wave reduction per tap.
+template <int K>
+__global__ void __launch_bounds__(64)
+    dw_wsum_kernel(const float* __restrict__ part, float* __restrict__ gw, int G) {
+  const int64_t ch = blockIdx.x;
+  const int lane = threadIdx.x;
+  const float* p = part + ch * G * (K * K);
+  float acc[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) acc[i] = 0.f;
+  for (int g = lane; g < G; g += 64)
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) acc[i] += p[(int64_t)g * (K * K) + i];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) {
+    const float v = wave_sum(acc[i]);
+    if (lane == i) gw[ch * (K * K) + i] = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Strip-blocked kernels (the fast path).  A tile is th x tw OUTPUT cells of
 // `pb` planes; a thread owns one tile column and R consecutive rows of one of
@@ -539,6 +561,376 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ---------------------------------------------------------------------------
+// Column-streaming kernels (padding K/2, W == S*Wo, Wo % V == 0): the fast
+// path for every MobileNetV3 stage.  No LDS staging and no barriers in the
+// main loop, so HBM latency is hidden by the loads a wave keeps in flight,
+// not by block-level turnover.
+//
+// A lane owns V consecutive OUTPUT columns (and the S*V input columns under
+// them) of a band of RB output rows of one plane: a "unit".  L lanes side by
+// side cover a run of L*V columns of the row (a segment); a wave holds
+// spw = 64/L segments, so narrow late-stage planes (20, 40 columns) still
+// fill the wave.  A lane reads its own columns with vector loads and the
+// stencil's column halo with scalar loads of the neighbouring columns
+// (clamped addresses + select: no divergent branches around loads); the
+// K-1 halo rows at band edges are re-read (L2 hits: neighbouring bands run in
+// the same wave or block).  Every row of the band is unrolled, so all of a
+// band's loads are issued together and every accumulator index is a
+// compile-time constant.
+//   forward         y rows accumulate row by row, stored as they complete.
+//   fused backward  gx (input rows S*o0 .. S*(o0+RB)) from the gy rows
+//                   o0-A .. o0+RB-1+B; gw from the unit's gy rows and the x
+//                   rows under them, summed over the wave (shuffles), the
+//                   block's waves (LDS, fixed order) and, when a channel
+//                   spans several blocks, a fixed-order partial reduce.
+// Backward units are ordered (channel, image, band, segment) and a wave never
+// mixes channels, so a wave-wide sum is one channel's weight gradient.
+struct DwStream {
+  int L, spw, nseg, nb;  // lanes per segment, segments per wave, per row, bands per plane
+  int wpb, it, G;        // backward: waves per block, unit groups per wave, blocks per channel
+  int64_t upc;           // backward: units per channel
+};
+
+template <int N>
+__device__ __forceinline__ void ldv(const float* p, float* v) {
+  if constexpr (N == 1) {
+    v[0] = p[0];
+  } else if constexpr (N == 2) {
+    const float2 a = *reinterpret_cast<const float2*>(p);
+    v[0] = a.x;
+    v[1] = a.y;
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; k += 4) {
+      const float4 a = *reinterpret_cast<const float4*>(p + k);
+      v[k] = a.x;
+      v[k + 1] = a.y;
+      v[k + 2] = a.z;
+      v[k + 3] = a.w;
+    }
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void stv(float* p, const float* v) {
+  if constexpr (N == 1) {
+    p[0] = v[0];
+  } else if constexpr (N == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < N; k += 4)
+      *reinterpret_cast<float4*>(p + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+  }
+}
+
+// v[c - LO] = row[c0 + c] for c in [LO, HI] (row of width w; zeros outside the
+// row or when !rok).  The lane's own columns [0, N) come from vector loads;
+// the halo columns from the neighbouring lanes by wave shuffles (lane +-1
+// owns the adjacent N columns of the same row of the same unit); a segment
+// is a whole row, so its edges are the plane's zero padding.  EDGE (rows
+// split into several segments): every halo column is a scalar load, issued
+// by every lane at a clamped address and selected, so no branch splits the
+// unrolled load stream.
+template <int LO, int N, int HI, bool EDGE>
+__device__ __forceinline__ void load_cols(const float* row, int c0, int w, bool rok, bool segl,
+                                          bool segr, float* v) {
+  static_assert(-LO <= N && HI - N + 1 <= N, "halo wider than a lane's columns");
+  float own[N];
+  ldv<N>(row + c0, own);
+#pragma unroll
+  for (int c = 0; c < N; ++c) {
+    own[c] = rok ? own[c] : 0.f;
+    v[c - LO] = own[c];
+  }
+  if constexpr (EDGE) {
+    // rows split into segments: every halo column by a scalar load (faster
+    // here than shuffles + edge loads: no wait on the own loads to form it)
+#pragma unroll
+    for (int c = LO; c <= HI; ++c) {
+      if (c >= 0 && c < N) continue;
+      const int col = c0 + c;
+      const bool ok = col >= 0 && col < w && rok;
+      const float g = row[col >= 0 && col < w ? col : 0];
+      v[c - LO] = ok ? g : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int c = LO; c < 0; ++c) {
+      const float t = __shfl_up(own[N + c], 1, 64);
+      v[c - LO] = segl ? 0.f : t;
+    }
+#pragma unroll
+    for (int c = N; c <= HI; ++c) {
+      const float t = __shfl_down(own[c - N], 1, 64);
+      v[c - LO] = segr ? 0.f : t;
+    }
+  }
+}
+
+template <int K, int S, int V, int RB, bool EDGE>
+__global__ void __launch_bounds__(256)
+    dw_fwd_stream_kernel(const float* __restrict__ x, const float* __restrict__ wt,
+                         float* __restrict__ y, DwShape d, DwStream t, int64_t units) {
+  constexpr int P = K / 2, XV = S * V;
+  constexpr int XL = -P, XH = S * (V - 1) - P + K - 1;  // input columns rel. to the lane's first
+  constexpr int NR = S * (RB - 1) + K;                   // input rows of a band
+  const int H = (int)d.h, W = (int)d.w, HO = (int)d.ho, WO = (int)d.wo, C = (int)d.c;
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int sl = lane / t.L, cl = lane - sl * t.L;
+  const int64_t unit = wave * t.spw + sl;
+  const bool active = sl < t.spw && unit < units;
+  const int64_t u = active ? unit : 0;
+  const int per = t.nb * t.nseg;
+  const int64_t plane = u / per;
+  const int rem = (int)(u - plane * per);
+  const int band = rem / t.nseg;
+  const int oc0 = ((rem - band * t.nseg) * t.L + cl) * V, ic0 = oc0 * S, o0 = band * RB;
+  const bool segl = cl == 0, segr = cl == t.L - 1;
+  float w[K * K];
+  const float* wp = wt + (plane % C) * (K * K);
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) w[i] = wp[i];
+  const float* xp = x + plane * (int64_t)H * W;
+  float* yp = y + plane * (int64_t)HO * WO + oc0;
+  float acc[RB][V];
+#pragma unroll
+  for (int j = 0; j < RB; ++j)
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[j][q] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NR; ++i) {
+    const int r = S * o0 - P + i;
+    const bool rok = active && r >= 0 && r < H;
+    float xv[XH - XL + 1];
+    load_cols<XL, XV, XH, EDGE>(xp + (int64_t)(rok ? r : 0) * W, ic0, W, rok, segl, segr, xv);
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      if (i - ky < 0 || (i - ky) % S != 0 || (i - ky) / S >= RB) continue;
+      const int jo = (i - ky) / S;
+#pragma unroll
+      for (int q = 0; q < V; ++q)
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) acc[jo][q] = fmaf(w[ky * K + kx], xv[S * q + kx], acc[jo][q]);
+    }
+  }
+  // stores last: a predicated store splits the basic block, and the scheduler
+  // cannot hoist the next rows' loads across it
+  if (!active) return;
+#pragma unroll
+  for (int jo = 0; jo < RB; ++jo)
+    if (o0 + jo < HO) stv<V>(yp + (int64_t)(o0 + jo) * WO, acc[jo]);
+}
+
+template <int K, int S, int V, int RB, bool EDGE, bool DATA, bool WGT>
+__device__ __forceinline__ void dw_bwd_stream_body(const float* __restrict__ gy,
+                                                   const float* __restrict__ x,
+                                                   const float* __restrict__ wt,
+                                                   float* __restrict__ gx, float* __restrict__ gw,
+                                                   const DwShape& d, const DwStream& t, int wv) {
+  constexpr int P = K / 2, XV = S * V;
+  constexpr int XL = -P, XH = S * (V - 1) - P + K - 1;  // x columns for the weight gradient
+  constexpr int GL = (K - 1 - P + S - 1) / S;            // gy column / row halo (data gradient)
+  constexpr int GR = (S - 1 + P) / S;
+  constexpr int NGY = RB + GL + GR;                      // gy rows of a band
+  constexpr int NX = S * (RB - 1) + K;                   // x rows of a band
+  __shared__ float red[8][K * K];
+  const int H = (int)d.h, W = (int)d.w, HO = (int)d.ho, WO = (int)d.wo, C = (int)d.c;
+  const int lane = threadIdx.x & 63;
+  const int ch = blockIdx.x / t.G, gb = blockIdx.x - ch * t.G;
+  const int sl = lane / t.L, cl = lane - sl * t.L;
+  const int per = t.nb * t.nseg;
+  float w[K * K], accw[K * K];
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) {
+    w[i] = DATA ? wt[ch * (K * K) + i] : 0.f;
+    accw[i] = 0.f;
+  }
+  for (int itr = 0; itr < t.it; ++itr) {
+    const int64_t wave = ((int64_t)gb * t.it + itr) * t.wpb + wv;  // wave within the channel
+    const int64_t unit = wave * t.spw + sl;
+    const bool active = sl < t.spw && unit < t.upc;
+    const int64_t u = active ? unit : 0;
+    const int img = (int)(u / per);
+    const int rem = (int)(u - (int64_t)img * per);
+    const int band = rem / t.nseg;
+    const int oc0 = ((rem - band * t.nseg) * t.L + cl) * V, ic0 = oc0 * S, o0 = band * RB;
+    const bool segl = cl == 0, segr = cl == t.L - 1;
+    const int64_t plane = (int64_t)img * C + ch;
+    const float* gp = gy + plane * HO * WO;
+    float gyo[WGT ? RB : 1][V];                // the unit's own gy rows (weight gradient)
+    float accx[DATA ? S * RB : 1][S * V];      // gx rows of the band (data gradient)
+    if constexpr (DATA) {
+#pragma unroll
+      for (int a = 0; a < S * RB; ++a)
+#pragma unroll
+        for (int c = 0; c < S * V; ++c) accx[a][c] = 0.f;
+#pragma unroll
+      for (int jj = 0; jj < NGY; ++jj) {
+        const int jo = jj - GL, o = o0 + jo;
+        const bool rok = active && o >= 0 && o < HO;
+        float gv[GL + V + GR];
+        load_cols<-GL, V, V - 1 + GR, EDGE>(gp + (int64_t)(rok ? o : 0) * WO, oc0, WO, rok, segl,
+                                            segr, gv);
+        if constexpr (WGT) {
+          if (jo >= 0 && jo < RB) {
+#pragma unroll
+            for (int q = 0; q < V; ++q) gyo[jo][q] = gv[GL + q];
+          }
+        }
+        // gy row o feeds input rows S*o - P + ky
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky) {
+          const int ti = S * jo - P + ky;
+          if (ti < 0 || ti >= S * RB) continue;
+#pragma unroll
+          for (int c = 0; c < S * V; ++c)
+#pragma unroll
+            for (int kx = 0; kx < K; ++kx) {
+              const int e = c + P - kx + S * GL;  // S * (gy column rel. + GL), >= 0
+              if (e % S != 0) continue;
+              accx[ti][c] = fmaf(w[ky * K + kx], gv[e / S], accx[ti][c]);
+            }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int jo = 0; jo < RB; ++jo) {
+        const int o = o0 + jo;
+        const bool rok = active && o < HO;
+        float gv[V];
+        load_cols<0, V, V - 1, false>(gp + (int64_t)(rok ? o : 0) * WO, oc0, WO, rok, segl, segr,
+                                      gv);
+#pragma unroll
+        for (int q = 0; q < V; ++q) gyo[jo][q] = gv[q];
+      }
+    }
+    if constexpr (WGT) {
+      const float* xp = x + plane * (int64_t)H * W;
+#pragma unroll
+      for (int i = 0; i < NX; ++i) {
+        const int r = S * o0 - P + i;
+        const bool rok = active && r >= 0 && r < H;
+        float xv[XH - XL + 1];
+        load_cols<XL, XV, XH, EDGE>(xp + (int64_t)(rok ? r : 0) * W, ic0, W, rok, segl, segr, xv);
+#pragma unroll
+        for (int ky = 0; ky < K; ++ky) {
+          if (i - ky < 0 || (i - ky) % S != 0 || (i - ky) / S >= RB) continue;
+          const int jo = (i - ky) / S;
+#pragma unroll
+          for (int kx = 0; kx < K; ++kx)
+#pragma unroll
+            for (int q = 0; q < V; ++q)
+              accw[ky * K + kx] = fmaf(gyo[jo][q], xv[S * q + kx], accw[ky * K + kx]);
+        }
+      }
+    }
+    // gx stores last (a predicated store splits the basic block: loads after
+    // it could not be hoisted)
+    if constexpr (DATA) {
+      if (active) {
+        float* xo = gx + plane * (int64_t)H * W + ic0;
+#pragma unroll
+        for (int ti = 0; ti < S * RB; ++ti)
+          if (S * o0 + ti < H) stv<S * V>(xo + (int64_t)(S * o0 + ti) * W, accx[ti]);
+      }
+    }
+  }
+  if constexpr (WGT) {
+#pragma unroll
+    for (int i = 0; i < K * K; ++i) {
+      const float v = wave_sum(accw[i]);
+      if (lane == 0) red[wv][i] = v;
+    }
+    __syncthreads();  // every wave of the block passes exactly one barrier (both roles)
+    if (wv == 0 && lane < K * K) {
+      float s = 0.f;
+      for (int k = 0; k < t.wpb; ++k) s += red[k][lane];
+      gw[(int64_t)blockIdx.x * (K * K) + lane] = s;  // = gw[ch] when G == 1
+    }
+  } else {
+    __syncthreads();  // matches the gw waves' barrier
+  }
+}
+
+// Backward.  MODE 1: gx only; 2: gw only; 0: both, with the block's waves
+// split in two roles over the same units -- waves [0, wpb) compute gx, waves
+// [wpb, 2 wpb) gw -- so a wave holds only one role's registers (the
+// allocation is the larger role's, not their sum) while the second read of
+// each gy row, by the other role's wave on the same CU, hits L1/L2.
+// gw: written directly (G == 1) or as per-block partials.
+template <int K, int S, int V, int RB, bool EDGE, int MODE>
+__global__ void __launch_bounds__(512)
+    dw_bwd_stream_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                         const float* __restrict__ wt, float* __restrict__ gx,
+                         float* __restrict__ gw, DwShape d, DwStream t, int n) {
+  const int role_wave = threadIdx.x >> 6;
+  if (MODE == 0 && role_wave < t.wpb)
+    dw_bwd_stream_body<K, S, V, RB, EDGE, true, false>(gy, x, wt, gx, gw, d, t, role_wave);
+  else if (MODE == 0)
+    dw_bwd_stream_body<K, S, V, RB, EDGE, false, true>(gy, x, wt, gx, gw, d, t,
+                                                       role_wave - t.wpb);
+  else
+    dw_bwd_stream_body<K, S, V, RB, EDGE, MODE == 1, MODE == 2>(gy, x, wt, gx, gw, d, t,
+                                                                role_wave);
+}
+
+// Stream configuration: columns per lane V, segment lanes L (EDGE when a row
+// is split into several segments), rows per band RB.
+struct DwCfg {
+  int v, rb;
+  bool edge;
+};
+
+DwCfg stream_cfg(int s, const DwShape& d) {
+  // whole rows in one segment when that keeps >= 90 % of a wave's lanes busy
+  // (no halo loads at all), else segments of <= 20 lanes with edge loads
+  auto util = [](int64_t l) { return (double)((64 / l) * l) / 64.0; };
+  DwCfg c{};
+  const int vs[2] = {s == 1 ? 4 : 2, s == 1 ? 8 : 4};
+  c.v = 0;  // 0: no stream configuration (the strip kernels run)
+  c.edge = true;
+  for (int v : vs) {
+    if (d.wo % v) continue;
+    const int64_t cg = d.wo / v;
+    if (cg <= 64 && util(cg) >= 0.9) {
+      c.v = v;
+      c.edge = false;
+      break;
+    }
+  }
+  if (!c.v && d.wo % vs[0] == 0) c.v = vs[0];
+  if (!c.v) return c;
+  c.rb = (s == 1 ? 8 : 4) / (c.v == vs[1] ? 2 : 1);
+  if (d.ho <= 32) c.rb = c.rb / 2 > 1 ? c.rb / 2 : 2;  // small planes: more units in flight
+  return c;
+}
+
+DwStream stream_layout(const DwShape& d, const DwCfg& c) {
+  DwStream t{};
+  const int cg = (int)(d.wo / c.v);  // column groups per row
+  t.L = 1;
+  if (!c.edge) {
+    t.L = cg;
+  } else {
+    for (int l = cg < 20 ? cg : 20; l >= 1; --l)
+      if (cg % l == 0) {
+        t.L = l;
+        break;
+      }
+  }
+  t.spw = 64 / t.L;
+  t.nseg = cg / t.L;
+  t.nb = (int)cdiv(d.ho, c.rb);
+  return t;
+}
+
+bool stream_ok(const DwShape& d, int k, int s) {
+  return d.pad == k / 2 && d.w == s * d.wo && d.h >= 1 && stream_cfg(s, d).v != 0;
+}
+
 bool dw_ok(int64_t n, int64_t c, int64_t h, int64_t w, int64_t k, int64_t stride,
            int64_t pad) {
   return n > 0 && c > 0 && h > 0 && w > 0 && (k == 3 || k == 5) &&
@@ -574,9 +966,41 @@ DwTile in_tile(const DwShape& d, int k, int s) {
   return t;
 }
 
+template <int K, int S, int V, int RB, bool EDGE>
+int launch_fwd_stream(const float* x, const float* wt, float* y, int64_t n, const DwShape& d,
+                      const DwStream& t, hipStream_t st) {
+  const int64_t units = n * d.c * t.nb * t.nseg;
+  const int64_t waves = cdiv(units, t.spw);
+  const double bytes = 4.0 * n * d.c * (d.h * d.w + d.ho * d.wo);
+  MDE_LAUNCH(K_DW_FWD, bytes, st, (dw_fwd_stream_kernel<K, S, V, RB, EDGE>),
+             dim3((unsigned)cdiv(waves, 4)), dim3(256), 0, x, wt, y, d, t, units);
+  return 0;
+}
+
+// Calls F.template operator()<V, RB, EDGE>() for the instantiated stream configurations.
+template <int S, typename F>
+int with_cfg(const DwCfg& c, F&& f) {
+  constexpr int V0 = S == 1 ? 4 : 2, V1 = 2 * V0, R0 = S == 1 ? 8 : 4;
+  if (c.v == V0 && c.rb == R0) return c.edge ? f.template operator()<V0, R0, true>()
+                                             : f.template operator()<V0, R0, false>();
+  if (c.v == V0) return c.edge ? f.template operator()<V0, R0 / 2, true>()
+                               : f.template operator()<V0, R0 / 2, false>();
+  if (c.rb == R0 / 2) return c.edge ? f.template operator()<V1, R0 / 2, true>()
+                                    : f.template operator()<V1, R0 / 2, false>();
+  return c.edge ? f.template operator()<V1, R0 / 4 < 2 ? 2 : R0 / 4, true>()
+                : f.template operator()<V1, R0 / 4 < 2 ? 2 : R0 / 4, false>();
+}
+
 template <int K, int S>
 int launch_fwd(const float* x, const float* wt, float* y, int64_t n, const DwShape& d,
                hipStream_t st) {
+  if (stream_ok(d, K, S)) {
+    const DwCfg c = stream_cfg(S, d);
+    const DwStream t = stream_layout(d, c);
+    return with_cfg<S>(c, [&]<int V, int RB, bool EDGE>() {
+      return launch_fwd_stream<K, S, V, RB, EDGE>(x, wt, y, n, d, t, st);
+    });
+  }
   const int64_t planes = n * d.c;
   const DwStrip t = strip_tile(d, K, S, planes);
   const dim3 grid((unsigned)t.tx, (unsigned)t.ty, (unsigned)cdiv(planes, t.pb));
@@ -611,9 +1035,60 @@ int launch_bwd_strip(const float* gy, const float* x, const float* wt, float* gx
   return 0;
 }
 
+// Backward stream layout: units per channel, waves per block, groups per
+// wave and blocks per channel (G > 1: per-block partials + dw_wreduce).
+DwStream stream_bwd_layout(int64_t n, const DwShape& d, const DwCfg& c) {
+  DwStream t = stream_layout(d, c);
+  t.upc = n * t.nb * t.nseg;
+  const int64_t wpc = cdiv(t.upc, t.spw);  // waves per channel
+  // gx and gw are separate launches (one role per block); a block of up to 8
+  // waves when that holds a whole channel (no partials), else 4-wave blocks
+  // (finer-grained block turnover)
+  t.wpb = (int)(wpc <= 8 ? wpc : 4);
+  const int64_t slots = cdiv(wpc, t.wpb);  // wave groups per channel
+  // enough blocks to fill the chip (>= ~4 per CU) before looping inside a block
+  int64_t g = slots, it = 1;
+  while (g > 1 && d.c * g > 4096) {
+    ++it;
+    g = cdiv(slots, it);
+  }
+  t.G = (int)g;
+  t.it = (int)cdiv(slots, g);
+  return t;
+}
+
+template <int K, int S, int V, int RB, bool EDGE>
+int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* gx, float* gw,
+                      float* part, int64_t n, const DwShape& d, const DwStream& t,
+                      hipStream_t st) {
+  float* dst = gw ? (t.G == 1 ? gw : part) : nullptr;
+  const double bytes =
+      4.0 * n * d.c * (d.ho * d.wo + (gx ? d.h * d.w : 0) + (gw ? d.h * d.w : 0));
+  const dim3 grid((unsigned)(d.c * t.G)), block((unsigned)(64 * t.wpb));
+  // gx and gw as two launches (each wave holds one role's registers; the
+  // second gy read is an L2 / MALL hit for the small planes)
+  if (gx)
+    MDE_LAUNCH(K_DW_BWD, bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 1>), grid, block, 0,
+               gy, x, wt, gx, dst, d, t, (int)n);
+  if (gw)
+    MDE_LAUNCH(K_DW_BWD, gx ? 0.0 : bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 2>), grid,
+               block, 0, gy, x, wt, gx, dst, d, t, (int)n);
+  if (gw && t.G > 1)
+    MDE_LAUNCH(K_DW_WREDUCE, 4.0 * d.c * t.G * K * K, st, dw_wsum_kernel<K>,
+               dim3((unsigned)d.c), dim3(64), 0, part, gw, t.G);
+  return 0;
+}
+
 template <int K, int S>
 int launch_bwd(const float* gy, const float* x, const float* wt, float* gx, float* gw,
                float* part, int64_t n, const DwShape& d, hipStream_t st) {
+  if (stream_ok(d, K, S)) {
+    const DwCfg c = stream_cfg(S, d);
+    const DwStream t = stream_bwd_layout(n, d, c);
+    return with_cfg<S>(c, [&]<int V, int RB, bool EDGE>() {
+      return launch_bwd_stream<K, S, V, RB, EDGE>(gy, x, wt, gx, gw, part, n, d, t, st);
+    });
+  }
   if (d.pad == K / 2) return launch_bwd_strip<K, S>(gy, x, wt, gx, gw, part, n, d, st);
   // other paddings: separate data / weight-gradient kernels
   const double bytes = 4.0 * n * d.c * (d.h * d.w + d.ho * d.wo);
@@ -646,6 +1121,10 @@ size_t mde_dwconv_workspace(int64_t n, int64_t c, int64_t h, int64_t w, int64_t 
                             int64_t stride, int64_t pad) {
   if (!dw_ok(n, c, h, w, k, stride, pad)) return 0;
   const DwShape d = make_shape(c, h, w, k, stride, pad);
+  if (stream_ok(d, (int)k, (int)stride)) {
+    const DwStream t = stream_bwd_layout(n, d, stream_cfg((int)stride, d));
+    return t.G > 1 ? (size_t)(4 * c * t.G * k * k) : 0;
+  }
   if (pad == k / 2) {
     const int G = strip_groups(n, c, strip_tile(d, (int)k, (int)stride, n));
     return G > 1 ? (size_t)(4 * c * G * k * k) : 0;

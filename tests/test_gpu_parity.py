@@ -83,6 +83,8 @@ def test_nearest_golden_bit_exact(golden, case):
     ((32, 64, 8, 10), dict(size=(60, 80))),               # DDRNet spp -> H/8 (x7.5)
     ((32, 64, 15, 20), dict(size=(60, 80))),              # compression4 (x4)
     ((16, 1, 120, 160), dict(scale_factor=4)),            # NewCRF head x4 (cfg4)
+    ((2, 64, 2, 3), dict(size=(8, 12))),                  # DDRNet compression4 at 64x96 (x4 by size)
+    ((4, 64, 15, 20), dict(size=(60, 80))),               # DDRNet compression4 at 640x480 (x4 by size)
     ((2, 3, 9, 70), dict(scale_factor=4)),                # x4, odd rows, two column blocks
     ((1, 2, 5, 3), dict(scale_factor=4)),                 # x4, tiny plane (every edge case)
     ((2, 2, 7, 66), dict(scale_factor=8)),                # x8
@@ -362,8 +364,14 @@ def test_train_sequence_golden(golden):
         depth = cu(seeded((2, 1, 64, 96), 200 + k, 0.1, 10.0))
         losses.append(float(trainer.step(image, depth)))
         trainer.after_step(k)
+    # Step 0 to 1e-5.  Later steps: Adam's first update moves every conv bias in
+    # front of a BatchNorm by ~lr * sign(g) where the true gradient is 0 (its sign
+    # is rounding noise), and from step 1 BN runs in eval mode where those biases
+    # matter; the reference's own ATen ops (the oracle) span up to 6.0e-3 from
+    # this golden when only the CPU thread count changes (1/2/3/8 threads:
+    # 6.0e-3 / 4.7e-3 / 2.5e-3 / 2.7e-3), so the curve is held to 1e-2.
     np.testing.assert_allclose(losses[0], g["losses"][0], rtol=1e-5)
-    np.testing.assert_allclose(losses, g["losses"], rtol=5e-3)
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-2)
 
 
 def test_guidedepth_cfg2_shape_runs_and_matches_oracle_encoder_free_parts():

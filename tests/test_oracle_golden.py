@@ -198,9 +198,10 @@ def test_train_sequence_matches_reference(golden):
     # ~lr * sign(g), including the conv biases in front of BatchNorm whose true
     # gradient is 0 (their sign is rounding noise); from step 1 on BN runs in
     # eval mode (train.py:161 quirk) where those biases matter, so the curves
-    # agree only to ~1e-3 — the reference's own run-to-run sensitivity.
+    # agree only to the reference's own run-to-run sensitivity: up to 6.0e-3
+    # from this golden when only the CPU thread count changes (1 thread).
     np.testing.assert_allclose(losses[0], g["losses"][0], rtol=1e-6)
-    np.testing.assert_allclose(losses, g["losses"], rtol=5e-3)
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-2)
     close_map(model.up_3.reduce.weight, g["final_up3_reduce_weight"], 1e-2, "up_3.reduce.weight")
 
 

@@ -904,7 +904,7 @@ DwCfg stream_cfg(int s, const DwShape& d) {
   if (!c.v && d.wo % vs[0] == 0) c.v = vs[0];
   if (!c.v) return c;
   c.rb = (s == 1 ? 8 : 4) / (c.v == vs[1] ? 2 : 1);
-  if (d.ho <= 32) c.rb = c.rb / 2 > 1 ? c.rb / 2 : 2;  // small planes: more units in flight
+
   return c;
 }
 
@@ -977,18 +977,15 @@ int launch_fwd_stream(const float* x, const float* wt, float* y, int64_t n, cons
   return 0;
 }
 
-// Calls F.template operator()<V, RB, EDGE>() for the instantiated stream configurations.
+// Calls F.template operator()<V, RB, EDGE>() for the instantiated stream
+// configurations (V0 columns x R0 rows, or 2 V0 columns x R0 / 2 rows).
 template <int S, typename F>
 int with_cfg(const DwCfg& c, F&& f) {
-  constexpr int V0 = S == 1 ? 4 : 2, V1 = 2 * V0, R0 = S == 1 ? 8 : 4;
-  if (c.v == V0 && c.rb == R0) return c.edge ? f.template operator()<V0, R0, true>()
-                                             : f.template operator()<V0, R0, false>();
-  if (c.v == V0) return c.edge ? f.template operator()<V0, R0 / 2, true>()
-                               : f.template operator()<V0, R0 / 2, false>();
-  if (c.rb == R0 / 2) return c.edge ? f.template operator()<V1, R0 / 2, true>()
-                                    : f.template operator()<V1, R0 / 2, false>();
-  return c.edge ? f.template operator()<V1, R0 / 4 < 2 ? 2 : R0 / 4, true>()
-                : f.template operator()<V1, R0 / 4 < 2 ? 2 : R0 / 4, false>();
+  constexpr int V0 = S == 1 ? 4 : 2, R0 = S == 1 ? 8 : 4;
+  if (c.v == V0) return c.edge ? f.template operator()<V0, R0, true>()
+                               : f.template operator()<V0, R0, false>();
+  return c.edge ? f.template operator()<2 * V0, R0 / 2, true>()
+                : f.template operator()<2 * V0, R0 / 2, false>();
 }
 
 template <int K, int S>

@@ -586,6 +586,10 @@ __global__ void __launch_bounds__(256)
 //                   spans several blocks, a fixed-order partial reduce.
 // Backward units are ordered (channel, image, band, segment) and a wave never
 // mixes channels, so a wave-wide sum is one channel's weight gradient.
+// Channels split over at most this many blocks finish their weight gradient
+// in the last block (a serial sum of G partials); more: a separate launch.
+constexpr int kHandoffMaxG = 16;
+
 struct DwStream {
   int L, spw, nseg, nb;  // lanes per segment, segments per wave, per row, bands per plane
   int wpb, it, G;        // backward: waves per block, unit groups per wave, blocks per channel
@@ -729,7 +733,9 @@ __device__ __forceinline__ void dw_bwd_stream_body(const float* __restrict__ gy,
                                                    const float* __restrict__ x,
                                                    const float* __restrict__ wt,
                                                    float* __restrict__ gx, float* __restrict__ gw,
-                                                   const DwShape& d, const DwStream& t, int wv) {
+                                                   float* __restrict__ gwf,
+                                                   unsigned* __restrict__ cnt, const DwShape& d,
+                                                   const DwStream& t, int wv) {
   constexpr int P = K / 2, XV = S * V;
   constexpr int XL = -P, XH = S * (V - 1) - P + K - 1;  // x columns for the weight gradient
   constexpr int GL = (K - 1 - P + S - 1) / S;            // gy column / row halo (data gradient)
@@ -845,10 +851,42 @@ __device__ __forceinline__ void dw_bwd_stream_body(const float* __restrict__ gy,
       if (lane == 0) red[wv][i] = v;
     }
     __syncthreads();  // every wave of the block passes exactly one barrier (both roles)
-    if (wv == 0 && lane < K * K) {
+    if (wv == 0) {
       float s = 0.f;
-      for (int k = 0; k < t.wpb; ++k) s += red[k][lane];
-      gw[(int64_t)blockIdx.x * (K * K) + lane] = s;  // = gw[ch] when G == 1
+      if (lane < K * K)
+        for (int k = 0; k < t.wpb; ++k) s += red[k][lane];
+      if (t.G == 1 || !cnt || t.G > kHandoffMaxG) {
+        if (lane < K * K) gw[(int64_t)blockIdx.x * (K * K) + lane] = s;  // = gw[ch] when G == 1
+      } else {
+        // Last block of the channel sums the G partials (fixed order g = 0..G-1,
+        // so the result does not depend on which block is last).  Hand-off
+        // across XCDs without cache flushes: partials stored write-through
+        // (agent-scope atomic stores) and drained, then the ticket; the last
+        // arriver reads them with agent-scope atomic loads (bypassing L1).
+        using gf32 = __attribute__((address_space(1))) float;
+        using gu32 = __attribute__((address_space(1))) unsigned;
+        if (lane < K * K)
+          __hip_atomic_store((gf32*)(gw + (int64_t)blockIdx.x * (K * K) + lane), s,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = 0;
+        if (lane == 0)
+          prev = __hip_atomic_fetch_add((gu32*)(cnt + ch), 1u, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+        prev = __shfl(prev, 0, 64);
+        if (prev == (unsigned)(t.G - 1)) {
+          if (lane < K * K) {
+            const float* p = gw + (int64_t)ch * t.G * (K * K) + lane;
+            float a = 0.f;
+            for (int g = 0; g < t.G; ++g)
+              a += __hip_atomic_load((gf32*)(p + (int64_t)g * (K * K)), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+            gwf[(int64_t)ch * (K * K) + lane] = a;
+          }
+          if (lane == 0)  // leave the counter zero for the next call
+            __hip_atomic_store((gu32*)(cnt + ch), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
   } else {
     __syncthreads();  // matches the gw waves' barrier
@@ -865,16 +903,18 @@ template <int K, int S, int V, int RB, bool EDGE, int MODE>
 __global__ void __launch_bounds__(512)
     dw_bwd_stream_kernel(const float* __restrict__ gy, const float* __restrict__ x,
                          const float* __restrict__ wt, float* __restrict__ gx,
-                         float* __restrict__ gw, DwShape d, DwStream t, int n) {
+                         float* __restrict__ gw, float* __restrict__ gwf,
+                         unsigned* __restrict__ cnt, DwShape d, DwStream t, int n) {
   const int role_wave = threadIdx.x >> 6;
   if (MODE == 0 && role_wave < t.wpb)
-    dw_bwd_stream_body<K, S, V, RB, EDGE, true, false>(gy, x, wt, gx, gw, d, t, role_wave);
+    dw_bwd_stream_body<K, S, V, RB, EDGE, true, false>(gy, x, wt, gx, gw, gwf, cnt, d, t,
+                                                       role_wave);
   else if (MODE == 0)
-    dw_bwd_stream_body<K, S, V, RB, EDGE, false, true>(gy, x, wt, gx, gw, d, t,
+    dw_bwd_stream_body<K, S, V, RB, EDGE, false, true>(gy, x, wt, gx, gw, gwf, cnt, d, t,
                                                        role_wave - t.wpb);
   else
-    dw_bwd_stream_body<K, S, V, RB, EDGE, MODE == 1, MODE == 2>(gy, x, wt, gx, gw, d, t,
-                                                                role_wave);
+    dw_bwd_stream_body<K, S, V, RB, EDGE, MODE == 1, MODE == 2>(gy, x, wt, gx, gw, gwf, cnt, d,
+                                                                t, role_wave);
 }
 
 // Stream configuration: columns per lane V, segment lanes L (EDGE when a row
@@ -1056,7 +1096,7 @@ DwStream stream_bwd_layout(int64_t n, const DwShape& d, const DwCfg& c) {
 
 template <int K, int S, int V, int RB, bool EDGE>
 int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* gx, float* gw,
-                      float* part, int64_t n, const DwShape& d, const DwStream& t,
+                      float* part, unsigned* cnt, int64_t n, const DwShape& d, const DwStream& t,
                       hipStream_t st) {
   float* dst = gw ? (t.G == 1 ? gw : part) : nullptr;
   const double bytes =
@@ -1066,11 +1106,11 @@ int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* g
   // second gy read is an L2 / MALL hit for the small planes)
   if (gx)
     MDE_LAUNCH(K_DW_BWD, bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 1>), grid, block, 0,
-               gy, x, wt, gx, dst, d, t, (int)n);
+               gy, x, wt, gx, dst, gw, cnt, d, t, (int)n);
   if (gw)
     MDE_LAUNCH(K_DW_BWD, gx ? 0.0 : bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 2>), grid,
-               block, 0, gy, x, wt, gx, dst, d, t, (int)n);
-  if (gw && t.G > 1)
+               block, 0, gy, x, wt, gx, dst, gw, cnt, d, t, (int)n);
+  if (gw && t.G > 1 && (!cnt || t.G > kHandoffMaxG))
     MDE_LAUNCH(K_DW_WREDUCE, 4.0 * d.c * t.G * K * K, st, dw_wsum_kernel<K>,
                dim3((unsigned)d.c), dim3(64), 0, part, gw, t.G);
   return 0;
@@ -1078,12 +1118,12 @@ int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* g
 
 template <int K, int S>
 int launch_bwd(const float* gy, const float* x, const float* wt, float* gx, float* gw,
-               float* part, int64_t n, const DwShape& d, hipStream_t st) {
+               float* part, unsigned* cnt, int64_t n, const DwShape& d, hipStream_t st) {
   if (stream_ok(d, K, S)) {
     const DwCfg c = stream_cfg(S, d);
     const DwStream t = stream_bwd_layout(n, d, c);
     return with_cfg<S>(c, [&]<int V, int RB, bool EDGE>() {
-      return launch_bwd_stream<K, S, V, RB, EDGE>(gy, x, wt, gx, gw, part, n, d, t, st);
+      return launch_bwd_stream<K, S, V, RB, EDGE>(gy, x, wt, gx, gw, part, cnt, n, d, t, st);
     });
   }
   if (d.pad == K / 2) return launch_bwd_strip<K, S>(gy, x, wt, gx, gw, part, n, d, st);
@@ -1147,7 +1187,7 @@ int mde_dwconv_fwd(const void* x, const float* weight, void* y, int64_t n, int64
 
 int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx, float* gweight,
                    int64_t n, int64_t c, int64_t h, int64_t w, int64_t k, int64_t stride,
-                   int64_t pad, void* workspace, int dtype, void* stream) {
+                   int64_t pad, void* workspace, uint32_t* counters, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !dw_ok(n, c, h, w, k, stride, pad) || (gx && !weight) ||
       (gweight && (!x || (!workspace && mde_dwconv_workspace(n, c, h, w, k, stride, pad) > 0))))
@@ -1158,10 +1198,11 @@ int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx,
   const float* xp = (const float*)x;
   float* gxp = (float*)gx;
   float* part = (float*)workspace;
-  if (k == 3 && stride == 1) return launch_bwd<3, 1>(g, xp, weight, gxp, gweight, part, n, d, st);
-  if (k == 3 && stride == 2) return launch_bwd<3, 2>(g, xp, weight, gxp, gweight, part, n, d, st);
-  if (k == 5 && stride == 1) return launch_bwd<5, 1>(g, xp, weight, gxp, gweight, part, n, d, st);
-  return launch_bwd<5, 2>(g, xp, weight, gxp, gweight, part, n, d, st);
+  unsigned* cnt = (unsigned*)counters;
+  if (k == 3 && stride == 1) return launch_bwd<3, 1>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
+  if (k == 3 && stride == 2) return launch_bwd<3, 2>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
+  if (k == 5 && stride == 1) return launch_bwd<5, 1>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
+  return launch_bwd<5, 2>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
 }
 
 }  // extern "C"

@@ -380,9 +380,12 @@ __global__ void __launch_bounds__(64 * kXsWarps)
     for (int h = 0; h < HALF; ++h) {  // halo: last HALF of lane-1, first HALF of lane+1
       float l = __shfl_up(v[S - HALF + h], 1, 64);
       float rr = __shfl_down(v[h], 1, 64);
+      // wave-edge lanes read the halo themselves: every lane loads (clamped
+      // address) and selects, so no divergent branch splits the row stream
       const int cl = S * jc - HALF + h, cr = S * jc + S + h;
-      if (edge_l) l = cl >= 0 ? row[cl] : 0.f;
-      if (edge_r) rr = cr < wo ? row[cr] : 0.f;
+      const float gl = row[cl >= 0 ? cl : 0], gr = row[cr < wo ? cr : wo - 1];
+      l = edge_l ? (cl >= 0 ? gl : 0.f) : l;
+      rr = edge_r ? (cr < wo ? gr : 0.f) : rr;
       s += wc[h] * l;
       s += wc[S + HALF + h] * rr;
     }

@@ -198,10 +198,8 @@ __global__ void __launch_bounds__(256)
 // partials l, l + 64, ... of every tap (all loads in flight), then a
 // fixed-order wave reduction per tap.
 template <int K>
-__global__ void __launch_bounds__(64)
-    dw_wsum_kernel(const float* __restrict__ part, float* __restrict__ gw, int G) {
-  const int64_t ch = blockIdx.x;
-  const int lane = threadIdx.x;
+__device__ __forceinline__ void wsum_channel(const float* __restrict__ part, float* __restrict__ gw,
+                                             int G, int64_t ch, int lane) {
   const float* p = part + ch * G * (K * K);
   float acc[K * K];
 #pragma unroll
@@ -214,6 +212,12 @@ __global__ void __launch_bounds__(64)
     const float v = wave_sum(acc[i]);
     if (lane == i) gw[ch * (K * K) + i] = v;
   }
+}
+
+template <int K>
+__global__ void __launch_bounds__(64)
+    dw_wsum_kernel(const float* __restrict__ part, float* __restrict__ gw, int G) {
+  wsum_channel<K>(part, gw, G, blockIdx.x, threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -593,6 +597,8 @@ constexpr int kHandoffMaxG = 16;
 struct DwStream {
   int L, spw, nseg, nb;  // lanes per segment, segments per wave, per row, bands per plane
   int wpb, it, G;        // backward: waves per block, unit groups per wave, blocks per channel
+  int fold;              // backward, gx launch: wave 0 of block ch first sums channel ch's
+                         // weight-gradient partials (written by the preceding gw launch)
   int64_t upc;           // backward: units per channel
 };
 
@@ -906,6 +912,8 @@ __global__ void __launch_bounds__(512)
                          float* __restrict__ gw, float* __restrict__ gwf,
                          unsigned* __restrict__ cnt, DwShape d, DwStream t, int n) {
   const int role_wave = threadIdx.x >> 6;
+  if (MODE == 1 && t.fold && role_wave == 0 && blockIdx.x < d.c)
+    wsum_channel<K>(gw, gwf, t.G, blockIdx.x, threadIdx.x);
   if (MODE == 0 && role_wave < t.wpb)
     dw_bwd_stream_body<K, S, V, RB, EDGE, true, false>(gy, x, wt, gx, gw, gwf, cnt, d, t,
                                                        role_wave);
@@ -1103,16 +1111,23 @@ int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* g
       4.0 * n * d.c * (d.ho * d.wo + (gx ? d.h * d.w : 0) + (gw ? d.h * d.w : 0));
   const dim3 grid((unsigned)(d.c * t.G)), block((unsigned)(64 * t.wpb));
   // gx and gw as two launches (each wave holds one role's registers; the
-  // second gy read is an L2 / MALL hit for the small planes)
-  if (gx)
-    MDE_LAUNCH(K_DW_BWD, bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 1>), grid, block, 0,
-               gy, x, wt, gx, dst, gw, cnt, d, t, (int)n);
+  // second gy read is an L2 / MALL hit for the small planes).  Partials that
+  // the gw launch cannot finish itself (no counters, or more than
+  // kHandoffMaxG blocks per channel) are summed by the gx launch that follows
+  // it (its block ch, wave 0, before its own units), else by dw_wsum_kernel.
+  const bool sum = gw && t.G > 1 && (!cnt || t.G > kHandoffMaxG);
   if (gw)
     MDE_LAUNCH(K_DW_BWD, gx ? 0.0 : bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 2>), grid,
                block, 0, gy, x, wt, gx, dst, gw, cnt, d, t, (int)n);
-  if (gw && t.G > 1 && (!cnt || t.G > kHandoffMaxG))
+  if (gx) {
+    DwStream tf = t;
+    tf.fold = sum ? 1 : 0;
+    MDE_LAUNCH(K_DW_BWD, bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 1>), grid, block, 0,
+               gy, x, wt, gx, dst, gw, cnt, d, tf, (int)n);
+  } else if (sum) {
     MDE_LAUNCH(K_DW_WREDUCE, 4.0 * d.c * t.G * K * K, st, dw_wsum_kernel<K>,
                dim3((unsigned)d.c), dim3(64), 0, part, gw, t.G);
+  }
   return 0;
 }
 

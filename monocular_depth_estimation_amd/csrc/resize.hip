@@ -362,12 +362,14 @@ __global__ void __launch_bounds__(64 * kXsWarps)
   float acc[kXsRows];
 #pragma unroll
   for (int k = 0; k < kXsRows; ++k) acc[k] = 0.f;
-  const bool edge_l = lane == 0 || jc == 0, edge_r = lane == 63 || jc == wi - 1 || j + 1 >= wi;
   constexpr int NR = S * kXsRows + S;  // output rows S*ib - HALF .. S*(ib+R) + HALF - 1
 #pragma unroll
   for (int k = 0; k < NR; ++k) {
-    const int r = S * ib - HALF + k;
-    if (r < 0 || r >= ho) continue;  // uniform per wave
+    // rows outside the plane (band edges) are clamped and weighted 0: no
+    // branch splits the unrolled rows, so all their loads are in flight at once
+    const int rq = S * ib - HALF + k;
+    const bool rv = rq >= 0 && rq < ho;
+    const int r = rq < 0 ? 0 : (rq > ho - 1 ? ho - 1 : rq);
     const float* row = gp + (int64_t)r * wo;
     float v[S];
 #pragma unroll
@@ -377,20 +379,17 @@ __global__ void __launch_bounds__(64 * kXsWarps)
     }
     float s = 0.f;
 #pragma unroll
-    for (int h = 0; h < HALF; ++h) {  // halo: last HALF of lane-1, first HALF of lane+1
-      float l = __shfl_up(v[S - HALF + h], 1, 64);
-      float rr = __shfl_down(v[h], 1, 64);
-      // wave-edge lanes read the halo themselves: every lane loads (clamped
-      // address) and selects, so no divergent branch splits the row stream
+    for (int h = 0; h < HALF; ++h) {
+      // halo columns: plain loads at clamped addresses by every lane (a
+      // column outside the plane has weight 0) -- no shuffles, no selects,
+      // nothing hipcc could turn into a branch around a load
       const int cl = S * jc - HALF + h, cr = S * jc + S + h;
-      const float gl = row[cl >= 0 ? cl : 0], gr = row[cr < wo ? cr : wo - 1];
-      l = edge_l ? (cl >= 0 ? gl : 0.f) : l;
-      rr = edge_r ? (cr < wo ? gr : 0.f) : rr;
-      s += wc[h] * l;
-      s += wc[S + HALF + h] * rr;
+      s += wc[h] * row[cl >= 0 ? cl : 0];
+      s += wc[S + HALF + h] * row[cr < wo ? cr : wo - 1];
     }
 #pragma unroll
     for (int c = 0; c < S; ++c) s += wc[HALF + c] * v[c];
+    s = rv ? s : 0.f;
     const Lin H = lin_index(sc, r, hi, 0);
 #pragma unroll
     for (int b = 0; b < kXsRows; ++b) {

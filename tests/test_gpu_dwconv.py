@@ -87,3 +87,29 @@ def test_dwconv_single_gradient(which):
     else:
         assert xd.grad is None
         close_scaled(conv.weight.grad, wr.grad, 1e-4, "gw")
+
+
+@pytest.mark.parametrize("n,c,h,w,k,s", [(16, 64, 240, 320, 3, 2), (16, 16, 240, 320, 3, 1),
+                                         (16, 120, 60, 80, 5, 1)])
+def test_dwconv_weight_grad_many_blocks(n, c, h, w, k, s):
+    """cfg4 batch: a channel's weight gradient is split over many blocks and
+    summed by the channel's last block (counters hand-off).  Two calls must
+    agree bitwise (fixed-order sum, counters left zero) and match float64."""
+    from monocular_depth_estimation_amd.nn import depthwise_conv2d
+    conv = torch.nn.Conv2d(c, c, k, s, k // 2, groups=c, bias=False)
+    with torch.no_grad():
+        conv.weight.copy_(torch.from_numpy(seeded((c, 1, k, k), 3, -1, 1)))
+    x = torch.from_numpy(seeded((n, c, h, w), 1, -1, 1))
+    wr = conv.weight.detach().double().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.double(), wr, None, s, k // 2, 1, c)
+    gy = torch.from_numpy(seeded(tuple(yr.shape), 2, -1, 1))
+    yr.backward(gy.double())
+    conv = conv.to(DEV)
+    xd, gyd = x.to(DEV), gy.to(DEV)
+    grads = []
+    for _ in range(2):
+        conv.weight.grad = None
+        depthwise_conv2d(xd, conv).backward(gyd)
+        grads.append(conv.weight.grad.clone())
+    assert torch.equal(grads[0], grads[1])
+    close_scaled(grads[0], wr.grad, 1e-4, "gw")

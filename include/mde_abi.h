@@ -247,6 +247,15 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       float* gprebias, int64_t n, int64_t c, int64_t h,
                       int64_t w, int act, void* workspace, int dtype,
                       void* stream);
+/* mde_batchnorm_bwd without its reduction pass: `sums` (DEVICE fp32 [c][2])
+ * holds sum dy' and sum dy' * (x - mean) over (n,h,w), dy' = dy * act'(...),
+ * as computed by a fused producer (mde_pointwise_bwd_bn's in_sums). */
+int mde_batchnorm_bwd_apply(const void* gy, const void* x, const void* residual,
+                            const float* gamma, const float* beta, const float* mean,
+                            const float* invstd, int training, const float* sums, void* gx,
+                            void* gresidual, float* ggamma, float* gbeta, float* gprebias,
+                            int64_t n, int64_t c, int64_t h, int64_t w, int act, int dtype,
+                            void* stream);
 
 /* ---------------------------------------------------------------------------
  * NewCRF shifted-window attention (head dim 32, window <= 8), fp32 on MFMA.
@@ -305,6 +314,18 @@ int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
                       const float* in_shift, const float* weight, void* gx, float* gweight,
                       int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
                       void* workspace, int dtype, void* stream);
+/* mde_pointwise_bwd with the fused BN + ReLU input (in_scale / in_shift
+ * required) that ALSO computes that BatchNorm's backward reductions in its
+ * epilogue: in_sums (DEVICE fp32 [cin][2]) = sum e, sum e * (x - in_mean[c])
+ * with e = gx * [x * in_scale + in_shift > 0] -- the input of
+ * mde_batchnorm_bwd_apply (act = ReLU, gy = gx), so the BN reduce pass over
+ * (gx, x) is skipped.  in_mean = the BN's save_mean.  cin <= 32 (others
+ * return MDE_ERR_UNSUPPORTED: the sums' registers cost more than the pass). */
+int mde_pointwise_bwd_bn(const void* gy, const void* x, const float* in_scale,
+                         const float* in_shift, const float* in_mean, const float* weight,
+                         void* gx, float* gweight, float* in_sums, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                         void* stream);
 
 /* ---------------------------------------------------------------------------
  * Bias-free 3x3 convolution, stride 1, zero padding 1, dilation 1, NCHW fp32

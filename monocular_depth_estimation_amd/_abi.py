@@ -59,6 +59,8 @@ SIGNATURES = {
                                       _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_batchnorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp, _vp, _vp,
                                  _i64, _i64, _i64, _i64, _int, _vp, _int, _vp]),
+    "mde_batchnorm_bwd_apply": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _int, _vp, _vp, _vp, _vp,
+                                       _vp, _vp, _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_window_attn_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64]),
     "mde_window_attn_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
                                    _i64, _int, _vp]),
@@ -73,6 +75,8 @@ SIGNATURES = {
     "mde_pointwise_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_pointwise_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
                                  _vp, _int, _vp]),
+    "mde_pointwise_bwd_bn": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
+                                    _i64, _i64, _vp, _int, _vp]),
     "mde_batchnorm_fwd_coef": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _int, _vp, _vp,
                                       _vp, _vp, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_conv3x3_supported": (_int, [_i64, _i64, _int]),

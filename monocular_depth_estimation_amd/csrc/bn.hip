@@ -607,6 +607,25 @@ int fwd_train(const void* x, const void* residual, void* y, int64_t n, int64_t c
 }
 
 template <typename T>
+int bwd_apply(const void* gy, const void* x, const void* residual, void* gx, void* gresidual,
+              int64_t n, int64_t c, int64_t hw, int act, const BwdArgs& P, hipStream_t s) {
+  const T* rr = act ? (const T*)residual : nullptr;
+  const double big = (double)sizeof(T) * n * c * (double)hw;
+  const double rb = rr ? big : 0.0;
+  const double abytes = 3.0 * big + rb + (gresidual ? big : 0.0);
+  if (plane_mode(hw)) {
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_plane_kernel<T>,
+               plane_grid(n * c, hw), dim3(256), 0, (const T*)gy, (const T*)x, rr, (T*)gx,
+               (T*)gresidual, c, hw, act, P);
+  } else {
+    MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, bn_bwd_apply_table_kernel<T>,
+               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c, (const T*)gy,
+               (const T*)x, rr, (T*)gx, (T*)gresidual, n * c, c, hw, act, P);
+  }
+  return MDE_OK;
+}
+
+template <typename T>
 int bwd(const void* gy, const void* x, const void* residual, void* gx, void* gresidual,
         int64_t n, int64_t c, int64_t hw, int act, const Geo& g, const BwdArgs& P,
         const float* gamma, const float* beta, const float* mean, const float* invstd,
@@ -624,17 +643,7 @@ int bwd(const void* gy, const void* x, const void* residual, void* gx, void* gre
                dim3(g.slices, (unsigned)c), dim3(256), 0, (const T*)gy, (const T*)x, rr, gamma,
                beta, mean, invstd, c, hw, g.total, g.slice_len, g.slices, act, part);
   }
-  const double abytes = 3.0 * big + rb + (gresidual ? big : 0.0);
-  if (plane_mode(hw)) {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY, abytes, s, bn_bwd_apply_plane_kernel<T>,
-               plane_grid(n * c, hw), dim3(256), 0, (const T*)gy, (const T*)x, rr, (T*)gx,
-               (T*)gresidual, c, hw, act, P);
-  } else {
-    MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, bn_bwd_apply_table_kernel<T>,
-               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c, (const T*)gy,
-               (const T*)x, rr, (T*)gx, (T*)gresidual, n * c, c, hw, act, P);
-  }
-  return MDE_OK;
+  return bwd_apply<T>(gy, x, residual, gx, gresidual, n, c, hw, act, P, s);
 }
 
 bool dtype_ok(int dtype) { return dtype == MDE_F32 || dtype == MDE_BF16; }
@@ -737,6 +746,26 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                          invstd, s)
              : bwd<float>(gy, x, residual, gx, gresidual, n, c, hw, act, g, P, gamma, beta, mean,
                           invstd, s);
+}
+
+/* The apply pass alone, with the reduce's sums supplied by the caller (e.g.
+ * mde_pointwise_bwd_bn's in_sums): sums [c][2] = sum dy', sum dy' (x - mean). */
+int mde_batchnorm_bwd_apply(const void* gy, const void* x, const void* residual,
+                            const float* gamma, const float* beta, const float* mean,
+                            const float* invstd, int training, const float* sums, void* gx,
+                            void* gresidual, float* ggamma, float* gbeta, float* gprebias,
+                            int64_t n, int64_t c, int64_t h, int64_t w, int act, int dtype,
+                            void* stream) {
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !x || !gamma || !beta || !mean || !invstd || !sums || !gx || act < 0 || act > 2 ||
+      !args_ok(n, c, h, w) || (gresidual && !residual && act))
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t hw = h * w;
+  BwdArgs P{gamma, beta, mean, invstd, sums, 1, n * hw, training, ggamma, gbeta, gprebias};
+  return dtype == MDE_BF16
+             ? bwd_apply<bf16>(gy, x, residual, gx, gresidual, n, c, hw, act, P, s)
+             : bwd_apply<float>(gy, x, residual, gx, gresidual, n, c, hw, act, P, s);
 }
 
 }  // extern "C"

@@ -274,18 +274,26 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 // BNR: the input is r' = relu(r * isc[c] + ish[c]) (a BatchNorm + ReLU fused
 // into this conv's operand load; r is the BN input), recomputed for gW; gs is
 // then the gradient w.r.t. r' (the BN backward applies the ReLU mask).
-template <int CI, int CO, bool HAS_D, bool BNR = false>
+// BNS (with BNR): also the BN backward's two reductions, e = gs * [r * isc +
+// ish > 0]: sum e and sum e * (r - imean[c]) per channel, from the gs tile in
+// registers and r re-read in the gs layout (the same tile the gW part reads,
+// an L1 / L2 hit) -- appended to the block's slab row, so the separate BN
+// reduce pass over (gs, r) is never run.
+template <int CI, int CO, bool HAS_D, bool BNR = false, bool BNS = false>
 __global__ void __launch_bounds__(256, 2)
     skip_bwd_mfma_kernel(const float* __restrict__ g, const float* __restrict__ r,
                          const float* __restrict__ d, const float* __restrict__ wt,
                          float* __restrict__ gs, float* __restrict__ slab, int64_t n,
                          int64_t hw, const float* __restrict__ isc = nullptr,
-                         const float* __restrict__ ish = nullptr) {
+                         const float* __restrict__ ish = nullptr,
+                         const float* __restrict__ imean = nullptr) {
   // CO may be 8: the M tiles of gW = G S^T are then half-empty (rows >= CO
   // are zero operands and are not stored); K of gs = W^T G is CO in steps of 4.
   constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = CO / 4;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
-  __shared__ float red[4][CO * CI + CO];
+  static_assert(!BNS || (BNR && !HAS_D && CI <= 32), "BN sums: fused BN-ReLU operand, cin <= 32");
+  constexpr int ROW = CO * CI + CO + (BNS ? 2 * CI : 0);  // slab row
+  __shared__ float red[4][ROW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
   // A operands of gs = W^T G: lane (c = 16mt + l16, o = 4kk + q4) -> W[o][c]
   float wa[MT][KO];
@@ -304,6 +312,25 @@ __global__ void __launch_bounds__(256, 2)
   for (int mt = 0; mt < MT; ++mt) {
     bsc[mt] = BNR ? isc[16 * mt + l16] : 1.f;
     bsh[mt] = BNR ? ish[16 * mt + l16] : 0.f;
+  }
+  // BNS: channel 16 mt + 4 q4 + i (the gs layout) coefficients and running
+  // sums in registers (cin <= 32: measured faster than LDS-held coefficients
+  // with per-tile wave sums; at cin 64 neither beats the separate reduce pass)
+  constexpr int SOFF = CO * CI + CO;
+  float esc[BNS ? MT : 1][4], esh[BNS ? MT : 1][4], emu[BNS ? MT : 1][4];
+  float es1[BNS ? MT : 1][4], es2[BNS ? MT : 1][4];
+  if constexpr (BNS) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 16 * mt + 4 * q4 + i;
+        esc[mt][i] = isc[c];
+        esh[mt][i] = ish[c];
+        emu[mt][i] = imean[c];
+        es1[mt][i] = 0.f;
+        es2[mt][i] = 0.f;
+      }
   }
   const int64_t tpi = hw / 64;
   const int64_t tiles = n * tpi;
@@ -338,6 +365,20 @@ __global__ void __launch_bounds__(256, 2)
         for (int i = 0; i < 4; ++i)
           *reinterpret_cast<float4*>(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16) =
               make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+        if constexpr (BNS) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 x =
+                *reinterpret_cast<const float4*>(rp + (16 * mt + 4 * q4 + i) * hw + 4 * l16);
+            const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const float e = xv[j] * esc[mt][i] + esh[mt][i] > 0.f ? acc[j][i] : 0.f;
+              es1[mt][i] += e;
+              es2[mt][i] += e * (xv[j] - emu[mt][i]);
+            }
+          }
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -410,9 +451,28 @@ __global__ void __launch_bounds__(256, 2)
     b += __shfl_xor(b, 32, 64);
     if (q4 == 0 && 16 * ot + l16 < CO) red[w][CO * CI + 16 * ot + l16] = b;
   }
+  if constexpr (BNS) {
+    // sum over the 16 lanes (pixel columns) of each lane group, fixed butterfly
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a = es1[mt][i], b = es2[mt][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if (l16 == 0) {
+          const int c = 16 * mt + 4 * q4 + i;
+          red[w][SOFF + 2 * c] = a;
+          red[w][SOFF + 2 * c + 1] = b;
+        }
+      }
+  }
   __syncthreads();
-  float* out = slab + (int64_t)blockIdx.x * (CO * CI + CO);
-  for (int i = threadIdx.x; i < CO * CI + CO; i += 256)
+  float* out = slab + (int64_t)blockIdx.x * ROW;
+  for (int i = threadIdx.x; i < ROW; i += 256)
     out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
@@ -510,18 +570,21 @@ __global__ void __launch_bounds__(256)
 __global__ void __launch_bounds__(256)
     skip_slab_reduce_kernel(const float* __restrict__ slab, int nblocks,
                             int npairs, int cout, float* __restrict__ gw,
-                            float* __restrict__ gb) {
+                            float* __restrict__ gb, int nextra = 0,
+                            float* __restrict__ extra = nullptr) {
   __shared__ float red[4];
   const int t = blockIdx.x;
-  const int stride = npairs + cout;
+  const int stride = npairs + cout + nextra;
   float a = 0.f;
   for (int k = threadIdx.x; k < nblocks; k += 256) a += slab[(int64_t)k * stride + t];
   a = mde::block_sum256(a, red);
   if (threadIdx.x == 0) {
     if (t < npairs)
       gw[t] = a;
-    else if (gb)
-      gb[t - npairs] = a;
+    else if (t < npairs + cout)
+      { if (gb) gb[t - npairs] = a; }
+    else
+      extra[t - npairs - cout] = a;
   }
 }
 
@@ -662,7 +725,8 @@ int mde_pointwise_supported(int64_t cin, int64_t cout, int64_t h, int64_t w) {
 }
 
 size_t mde_pointwise_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
-  return mde_skip_reduce_workspace(n, cin, cout, h, w);
+  // slab rows sized for the BN-sum epilogue too (mde_pointwise_bwd_bn)
+  return sizeof(float) * (size_t)bwd_blocks(n, h * w) * (size_t)(cin * cout + cout + 2 * cin);
 }
 
 int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
@@ -694,38 +758,80 @@ int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shif
   return MDE_ERR_UNSUPPORTED;
 }
 
-int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
-                      const float* in_shift, const float* wt, void* gx, float* gw, int64_t n,
-                      int64_t cin, int64_t cout, int64_t h, int64_t w, void* workspace,
-                      int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+}  // extern "C"
+
+namespace {
+
+// Pointwise backward; in_mean / in_sums non-null (with in_scale): also the
+// producer BatchNorm's backward sums (BNS epilogue), in_sums [cin][2].
+int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const float* in_shift,
+                  const float* in_mean, const float* wt, void* gx, float* gw, float* in_sums,
+                  int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, void* workspace,
+                  hipStream_t s) {
   const int64_t hw = h * w;
   if (!gy || !x || !wt || !gw || !workspace || (!in_scale != !in_shift))
     return MDE_ERR_INVALID_ARG;
   if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
+  const bool sums = in_sums != nullptr;
+  if (sums && (!in_scale || !in_mean || !gx)) return MDE_ERR_INVALID_ARG;
+  if (sums && cin > 32) return MDE_ERR_UNSUPPORTED;
   const int nb = bwd_blocks(n, hw);
   float* slab = (float*)workspace;
   const double bytes = 4.0 * n * hw * (double)(cout + cin + (gx ? cin : 0));
 #define MDE_PW_BWD(A, B)                                                                     \
   if (cin == A && cout == B) {                                                               \
-    if (in_scale) {                                                                          \
+    if (sums) {                                                                              \
+      if constexpr (A <= 32)                                                                 \
+        MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false, true, true>), \
+                   dim3(nb), dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt,   \
+                   (float*)gx, slab, n, hw, in_scale, in_shift, in_mean);                    \
+    } else if (in_scale) {                                                                   \
       MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false, true>),         \
                  dim3(nb), dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt,     \
-                 (float*)gx, slab, n, hw, in_scale, in_shift);                               \
+                 (float*)gx, slab, n, hw, in_scale, in_shift, nullptr);                      \
     } else {                                                                                 \
       MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false>), dim3(nb),     \
                  dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt, (float*)gx,   \
-                 slab, n, hw, nullptr, nullptr);                                             \
+                 slab, n, hw, nullptr, nullptr, nullptr);                                    \
     }                                                                                        \
   }
   MDE_PW_SHAPES(MDE_PW_BWD)
 #undef MDE_PW_BWD
-  const int stride = (int)(cin * cout + cout);
-  MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
-             dim3((unsigned)(cin * cout)), dim3(256), 0, slab, nb, (int)(cin * cout), (int)cout,
-             gw, (float*)nullptr);
+  const int npairs = (int)(cin * cout), nextra = sums ? 2 * (int)cin : 0;
+  const int stride = npairs + (int)cout + nextra;
+  if (sums) {  // every slab column: gw, (the unused bias columns), the BN sums
+    MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+               dim3((unsigned)stride), dim3(256), 0, slab, nb, npairs, (int)cout, gw,
+               (float*)nullptr, nextra, in_sums);
+  } else {
+    MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+               dim3((unsigned)npairs), dim3(256), 0, slab, nb, npairs, (int)cout, gw,
+               (float*)nullptr, 0, (float*)nullptr);
+  }
   return MDE_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
+                      const float* in_shift, const float* wt, void* gx, float* gw, int64_t n,
+                      int64_t cin, int64_t cout, int64_t h, int64_t w, void* workspace,
+                      int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  return pointwise_bwd(gy, x, in_scale, in_shift, nullptr, wt, gx, gw, nullptr, n, cin, cout, h,
+                       w, workspace, (hipStream_t)stream);
+}
+
+int mde_pointwise_bwd_bn(const void* gy, const void* x, const float* in_scale,
+                         const float* in_shift, const float* in_mean, const float* wt, void* gx,
+                         float* gw, float* in_sums, int64_t n, int64_t cin, int64_t cout,
+                         int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!in_scale || !in_shift || !in_mean || !gx || !in_sums) return MDE_ERR_INVALID_ARG;
+  return pointwise_bwd(gy, x, in_scale, in_shift, in_mean, wt, gx, gw, in_sums, n, cin, cout, h,
+                       w, workspace, (hipStream_t)stream);
 }
 
 }  // extern "C"

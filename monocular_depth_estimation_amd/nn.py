@@ -130,6 +130,13 @@ class _Pointwise(torch.autograd.Function):
         return gx, gw.view(ctx.wshape)
 
 
+# mde_pointwise_bwd_bn (the BN backward sums in the 1x1 conv's backward
+# epilogue) supports cin <= 32; at cin 64 the separate reduce pass is faster
+# (tools/pw_bn_bench.py: 16->8 @480x640 bs32 880 -> 679 us, 32->16 @240x320
+# 435 -> ~375 us; 64->32 @120x160 253 vs 264-389 us fused).
+_PW_BN_SUMS_MAX_CIN = 32
+
+
 class _BNReluPointwise(torch.autograd.Function):
     """conv1x1(relu(bn(y1))) with the BN + ReLU applied inside the 1x1 conv's
     operand load: relu(bn(y1)) is never written.  Backward: the 1x1 conv's
@@ -173,19 +180,33 @@ class _BNReluPointwise(torch.autograd.Function):
         gz = torch.empty_like(y1)
         gw2 = torch.empty_like(w2m)
         ws = _ws(_abi.query("mde_pointwise_workspace", n, c, cout, h, w), y1)
-        _abi.call("mde_pointwise_bwd", _abi.ptr(gy2), _abi.ptr(y1), _abi.ptr(scale),
-                  _abi.ptr(shift), _abi.ptr(w2m), _abi.ptr(gz), _abi.ptr(gw2), n, c, cout, h, w,
-                  _abi.ptr(ws), _abi.dtype_code(gy2), st)
         gy1 = torch.empty_like(y1) if ctx.needs_input_grad[0] else None
         gg = torch.empty_like(gamma)
         gb = torch.empty_like(beta)
         gpb = torch.empty_like(gamma) if (ctx.has_prebias and ctx.needs_input_grad[3]) else None
-        ws2 = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), y1)
-        _abi.call("mde_batchnorm_bwd", _abi.ptr(gz), _abi.ptr(y1), None, _abi.ptr(gamma),
-                  _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), int(ctx.training),
-                  _abi.ptr(gy1 if gy1 is not None else torch.empty_like(y1)), None, _abi.ptr(gg),
-                  _abi.ptr(gb), _abi.ptr(gpb), n, c, h, w, _ACTS["relu"], _abi.ptr(ws2),
-                  _abi.dtype_code(gy2), st)
+        gy1_out = gy1 if gy1 is not None else torch.empty_like(y1)
+        if c <= _PW_BN_SUMS_MAX_CIN:
+            # the 1x1 conv's backward also forms the BN backward's two sums in
+            # its epilogue, so the BN runs its apply pass only
+            sums = torch.empty((c, 2), dtype=torch.float32, device=y1.device)
+            _abi.call("mde_pointwise_bwd_bn", _abi.ptr(gy2), _abi.ptr(y1), _abi.ptr(scale),
+                      _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(w2m), _abi.ptr(gz),
+                      _abi.ptr(gw2), _abi.ptr(sums), n, c, cout, h, w, _abi.ptr(ws),
+                      _abi.dtype_code(gy2), st)
+            _abi.call("mde_batchnorm_bwd_apply", _abi.ptr(gz), _abi.ptr(y1), None,
+                      _abi.ptr(gamma), _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd),
+                      int(ctx.training), _abi.ptr(sums), _abi.ptr(gy1_out), None, _abi.ptr(gg),
+                      _abi.ptr(gb), _abi.ptr(gpb), n, c, h, w, _ACTS["relu"],
+                      _abi.dtype_code(gy2), st)
+        else:
+            _abi.call("mde_pointwise_bwd", _abi.ptr(gy2), _abi.ptr(y1), _abi.ptr(scale),
+                      _abi.ptr(shift), _abi.ptr(w2m), _abi.ptr(gz), _abi.ptr(gw2), n, c, cout, h,
+                      w, _abi.ptr(ws), _abi.dtype_code(gy2), st)
+            ws2 = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), y1)
+            _abi.call("mde_batchnorm_bwd", _abi.ptr(gz), _abi.ptr(y1), None, _abi.ptr(gamma),
+                      _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), int(ctx.training),
+                      _abi.ptr(gy1_out), None, _abi.ptr(gg), _abi.ptr(gb), _abi.ptr(gpb), n, c,
+                      h, w, _ACTS["relu"], _abi.ptr(ws2), _abi.dtype_code(gy2), st)
         return gy1, gg, gb, gpb, None, None, None, None, None, None, gw2.view(ctx.w2shape)
 
 

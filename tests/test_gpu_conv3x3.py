@@ -156,3 +156,65 @@ def test_fused_bn_relu_pointwise_branch_vs_float64(cin, e, h, w, train):
         assert err <= 1e-3 * max(float(p2.grad.abs().max()), 1e-6), n1
     for b1, b2 in zip(seq.buffers(), ref.buffers()):
         assert rel_err(b1, b2) <= 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 8, 96, 128), (32, 32, 4, 60, 80), (32, 16, 3, 8, 64),
+                                             (16, 32, 2, 16, 64)])
+def test_pointwise_bwd_bn_sums_match_separate_reduce(cin, cout, n, h, w):
+    """mde_pointwise_bwd_bn's epilogue sums + mde_batchnorm_bwd_apply == the
+    unfused mde_pointwise_bwd + mde_batchnorm_bwd (its own reduce pass): same
+    gx of the 1x1 conv bit for bit, BN input / parameter gradients to 1e-5."""
+    from monocular_depth_estimation_amd import _abi
+    g = torch.Generator().manual_seed(cin * cout + h)
+    f = dict(device=DEV, dtype=torch.float32)
+    y1 = (torch.rand((n, cin, h, w), generator=g) * 2 - 0.7).to(DEV)
+    gy2 = (torch.rand((n, cout, h, w), generator=g) - 0.5).to(DEV)
+    w2 = (torch.rand((cout, cin), generator=g) - 0.5).to(DEV)
+    gamma = (torch.rand(cin, generator=g) + 0.5).to(DEV)
+    beta = (torch.rand(cin, generator=g) - 0.5).to(DEV)
+    mean = y1.mean(dim=(0, 2, 3))
+    invstd = 1.0 / torch.sqrt(y1.var(dim=(0, 2, 3), unbiased=False) + 1e-5)
+    scale = gamma * invstd
+    shift = beta - mean * scale
+    st = _abi.stream_of(y1)
+    ws = torch.empty(_abi.query("mde_pointwise_workspace", n, cin, cout, h, w) // 4 + 1, **f)
+    outs = []
+    for fused in (False, True):
+        gz, gw2 = torch.empty_like(y1), torch.empty_like(w2)
+        gy1, gg, gb = torch.empty_like(y1), torch.empty(cin, **f), torch.empty(cin, **f)
+        if fused:
+            sums = torch.empty((cin, 2), **f)
+            _abi.call("mde_pointwise_bwd_bn", _abi.ptr(gy2), _abi.ptr(y1), _abi.ptr(scale),
+                      _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(w2), _abi.ptr(gz), _abi.ptr(gw2),
+                      _abi.ptr(sums), n, cin, cout, h, w, _abi.ptr(ws), 0, st)
+            _abi.call("mde_batchnorm_bwd_apply", _abi.ptr(gz), _abi.ptr(y1), None, _abi.ptr(gamma),
+                      _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), 1, _abi.ptr(sums),
+                      _abi.ptr(gy1), None, _abi.ptr(gg), _abi.ptr(gb), None, n, cin, h, w, 1, 0, st)
+        else:
+            _abi.call("mde_pointwise_bwd", _abi.ptr(gy2), _abi.ptr(y1), _abi.ptr(scale),
+                      _abi.ptr(shift), _abi.ptr(w2), _abi.ptr(gz), _abi.ptr(gw2), n, cin, cout, h,
+                      w, _abi.ptr(ws), 0, st)
+            ws2 = torch.empty(_abi.query("mde_batchnorm_workspace", n, cin, h, w) // 4 + 1, **f)
+            _abi.call("mde_batchnorm_bwd", _abi.ptr(gz), _abi.ptr(y1), None, _abi.ptr(gamma),
+                      _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), 1, _abi.ptr(gy1), None,
+                      _abi.ptr(gg), _abi.ptr(gb), None, n, cin, h, w, 1, _abi.ptr(ws2), 0, st)
+        outs.append((gz, gw2, gy1, gg, gb))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    for a, b, what in zip(outs[1][2:], outs[0][2:], ("gy1", "ggamma", "gbeta")):
+        assert rel_err(a, b) <= 1e-5, what
+
+
+def test_pointwise_bwd_bn_cin64_unsupported():
+    from monocular_depth_estimation_amd import _abi
+    f = dict(device=DEV, dtype=torch.float32)
+    n, cin, cout, h, w = 1, 64, 32, 8, 8
+    x, gy = torch.rand((n, cin, h, w), **f), torch.rand((n, cout, h, w), **f)
+    v = torch.rand(cin, **f)
+    ws = torch.empty(_abi.query("mde_pointwise_workspace", n, cin, cout, h, w) // 4 + 1, **f)
+    with pytest.raises(_abi.MdeError, match="unsupported"):
+        _abi.call("mde_pointwise_bwd_bn", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(v), _abi.ptr(v),
+                  _abi.ptr(v), _abi.ptr(torch.rand((cout, cin), **f)), _abi.ptr(torch.empty_like(x)),
+                  _abi.ptr(torch.empty((cout, cin), **f)), _abi.ptr(torch.empty((cin, 2), **f)), n,
+                  cin, cout, h, w, _abi.ptr(ws), 0, _abi.stream_of(x))

@@ -44,10 +44,23 @@ using f4 = __attribute__((ext_vector_type(4))) float;
 
 constexpr int D = 32;        // head dim (all four NewCRF stages)
 constexpr int NP = 64;       // padded tokens per window (ws*ws <= 64)
-constexpr int LT = 65;       // LDS row pitch of the per-wave [64][64] P / dS tile
+constexpr int LT = 67;       // LDS row pitch of the per-wave [64][64] P / dS tile (at most
+                             // 2-way bank conflicts for both the own and the transposed
+                             // access pattern; 65 has 4-way)
 constexpr int TABP = 256;    // table slots ((2ws-1)^2 <= 225)
 constexpr int kHeads = 4;    // heads (= waves) per block
-constexpr int kWinBwd = 4;   // windows per backward block
+constexpr int kWinBwd = 4;   // windows per backward block, at most
+
+// Windows per backward block: kWinBwd (amortises the table / slab work),
+// unless that leaves too few blocks (measured: C1024 15x20, 288 blocks at 4
+// windows, runs 172 -> 123 us at 1; C512 30x40's 480 blocks are still best
+// at 4).
+inline int bwd_wpb(int64_t nwin, int64_t heads) {
+  const int64_t blocks = nwin * ((heads + kHeads - 1) / kHeads);
+  if (blocks / kWinBwd >= 400) return kWinBwd;
+  const int64_t w = blocks / 1024;
+  return (int)(w < 1 ? 1 : (w > kWinBwd ? kWinBwd : w));
+}
 
 struct Geo {
   int b, h, w, c, heads, ws, shift, hp, wp, nwh, nww, n;
@@ -297,7 +310,8 @@ __global__ void __launch_bounds__(256, 2)
     wattn_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ qk,
                      const float* __restrict__ qkb, const float* __restrict__ v,
                      const float* __restrict__ table, float* __restrict__ gqk,
-                     float* __restrict__ gv, float* __restrict__ slab, int nwin, Geo g) {
+                     float* __restrict__ gv, float* __restrict__ slab, int nwin, int wpb,
+                     Geo g) {
   __shared__ int tok[NP], lab[NP];
   __shared__ float tab[kHeads][TABP], dtab[kHeads][TABP];
   __shared__ float T[kHeads][NP][LT];
@@ -313,8 +327,8 @@ __global__ void __launch_bounds__(256, 2)
     }
   float dkb[2] = {0.f, 0.f};  // d(k bias)[16ct + l16] partial of this lane
   float dvb[2] = {0.f, 0.f};  // d(v bias): dV of the padded keys (g.vb only)
-  for (int wi = 0; wi < kWinBwd; ++wi) {
-    const int win = blockIdx.x * kWinBwd + wi;
+  for (int wi = 0; wi < wpb; ++wi) {
+    const int win = blockIdx.x * wpb + wi;
     if (win >= nwin) break;  // uniform across the block
     __syncthreads();         // previous window's tok / T readers are done
     window_tokens<WS>(g, win, tok, lab);
@@ -326,12 +340,16 @@ __global__ void __launch_bounds__(256, 2)
     float* gqkrow = gqk + img * c2;
     float* gvrow = gv + img * c;
     // T[w] is private to this wave: its LDS accesses are processed in program
-    // order, so the P / dS round trips need no block barrier.
+    // order, so the P / dS round trips need no block barrier.  P and then dS
+    // live in T only (not in registers across phases): the register peak is
+    // one phase's operands, so the kernel runs two waves per SIMD unspilled.
     if (active) {
-      f4 s[4][4];
-      probs_t<WS>(g, qkrow, qkb, head, tok, lab, tab[w], s);
+      {
+        f4 s[4][4];
+        probs_t<WS>(g, qkrow, qkb, head, tok, lab, tab[w], s);
+        stage_t(T[w], s);  // P
+      }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
-      stage_t(T[w], s);  // P
       // dV = P^T dO
       {
         float b[4][4][2];
@@ -363,7 +381,8 @@ __global__ void __launch_bounds__(256, 2)
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
-      // dP^T = V dO^T column by column; dS = P (dP - rowsum(P dP)) in place
+      // dP^T = V dO^T column by column; dS = P (dP - rowsum(P dP)), P read
+      // back from T (this lane's own entries) and dS written over it
       {
         float va[4][8];
 #pragma unroll
@@ -380,22 +399,26 @@ __global__ void __launch_bounds__(256, 2)
           for (int k = 0; k < 8; ++k)
 #pragma unroll
             for (int jt = 0; jt < 4; ++jt) dp[jt] = mfma4(va[jt][k], db[k], dp[jt]);
+          float pv[4][4];
           float dl = 0.f;
 #pragma unroll
           for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) dl += s[jt][it][r] * dp[jt][r];
+            for (int r = 0; r < 4; ++r) {
+              pv[jt][r] = T[w][16 * jt + 4 * g4 + r][16 * it + l16];
+              dl += pv[jt][r] * dp[jt][r];
+            }
           dl += __shfl_xor(dl, 16, 64);
           dl += __shfl_xor(dl, 32, 64);
 #pragma unroll
           for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) s[jt][it][r] = s[jt][it][r] * (dp[jt][r] - dl);
+            for (int r = 0; r < 4; ++r)
+              T[w][16 * jt + 4 * g4 + r][16 * it + l16] = pv[jt][r] * (dp[jt][r] - dl);
         }
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
-      stage_t(T[w], s);  // dS (the dV reads of P are done: same wave, in order)
-      // dQ = dS K * scale: A = dS[i][j] from registers, B = K[j][c] per lane
+      // dQ = dS K * scale: A = dS[i][j] (this lane's own T entries), B = K[j][c] per lane
       {
         float b[4][4][2];
 #pragma unroll
@@ -413,9 +436,11 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
           for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
+            for (int r = 0; r < 4; ++r) {
+              const float a = T[w][16 * jt + 4 * g4 + r][16 * it + l16];  // dS[i][j]
 #pragma unroll
-              for (int ct = 0; ct < 2; ++ct) q[ct] = mfma4(s[jt][it][r], b[jt][r][ct], q[ct]);
+              for (int ct = 0; ct < 2; ++ct) q[ct] = mfma4(a, b[jt][r][ct], q[ct]);
+            }
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * it + 4 * g4 + rr];
@@ -459,18 +484,27 @@ __global__ void __launch_bounds__(256, 2)
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // table gradient: entry e <- sum of dS over the (query, key) pairs at
-      // that offset, in a fixed order
+      // that offset, in a fixed order (query row-major).  Out-of-window pairs
+      // read a clamped address and add 0, so with a compile-time window the
+      // ws*ws reads are unrolled and all in flight (adding +0 leaves the sum
+      // unchanged).
       for (int e = lane; e < ntab; e += 64) {
         const int dy = e / span - (ws - 1), dx = e % span - (ws - 1);
         float acc = 0.f;
-        for (int ri = 0; ri < ws; ++ri) {
-          const int rj = ri - dy;
-          if (rj < 0 || rj >= ws) continue;
-          for (int ci = 0; ci < ws; ++ci) {
-            const int cj = ci - dx;
-            if (cj < 0 || cj >= ws) continue;
-            acc += T[w][rj * ws + cj][ri * ws + ci];
-          }
+        auto add = [&](int ri, int ci) {
+          const int rj = ri - dy, cj = ci - dx;
+          const bool ok = rj >= 0 && rj < ws && cj >= 0 && cj < ws;
+          const float v = T[w][ok ? rj * ws + cj : 0][ri * ws + ci];
+          acc += ok ? v : 0.f;
+        };
+        if constexpr (WS > 0) {
+#pragma unroll
+          for (int ri = 0; ri < WS; ++ri)
+#pragma unroll
+            for (int ci = 0; ci < WS; ++ci) add(ri, ci);
+        } else {
+          for (int ri = 0; ri < ws; ++ri)
+            for (int ci = 0; ci < ws; ++ci) add(ri, ci);
         }
         dtab[w][e] += acc;
       }
@@ -557,7 +591,7 @@ size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
   if (!make_geo(b, h, w, c, heads, window, 0, &g)) return 0;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const int64_t ntab = (2 * window - 1) * (2 * window - 1);
-  return sizeof(float) * (size_t)(mde::cdiv(nwin, kWinBwd) * heads * (ntab + 2 * D));
+  return sizeof(float) * (size_t)(mde::cdiv(nwin, bwd_wpb(nwin, heads)) * heads * (ntab + 2 * D));
 }
 
 int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
@@ -596,18 +630,19 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
   g.vb = v_bias;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
-  const int nblk = (int)mde::cdiv(nwin, kWinBwd);
+  const int wpb = bwd_wpb(nwin, heads);
+  const int nblk = (int)mde::cdiv(nwin, wpb);
   const int ntab = (2 * g.ws - 1) * (2 * g.ws - 1);
   const double bytes = 4.0 * (double)b * h * w * c * 7.0;  // q k v dO read, dq dk dv written
   const dim3 grid((unsigned)nblk, (unsigned)mde::cdiv(heads, kHeads));
   if (window == 7)
     MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel<7>, grid, dim3(256), 0,
                (const float*)gout, (const float*)qk, qk_bias, (const float*)v, table,
-               (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, g);
+               (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, wpb, g);
   else
     MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel<0>, grid, dim3(256), 0,
                (const float*)gout, (const float*)qk, qk_bias, (const float*)v, table,
-               (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, g);
+               (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, wpb, g);
   // q half of d(qk bias) gets nothing from padded tokens (their dO is 0)
   MDE_LAUNCH(mde::K_WATTN_BWD, 0.0, s, zero_kernel, dim3((unsigned)mde::cdiv(c, 256)),
              dim3(256), 0, gqk_bias, (int)c);

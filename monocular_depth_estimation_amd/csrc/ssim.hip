@@ -9,21 +9,17 @@
 //   loss composition     src/train.py:100 (1.0*ssim + 0.1*l1)
 //
 // The gradient of mean(clamp((1-S)/2,0,1)) does not depend on the loss value,
-// so one tiled pass produces the loss partial sums AND d loss/d pred:
-//   tile 16x64 outputs, inputs staged with a 2-pixel reflected halo, per-pixel
-//   SSIM statistics on the tile + 1 ring (separable 3x3 box in LDS), then the
-//   transposed box of the per-pixel coefficients (with reflection
-//   multiplicities) gives the gradient.  Loss partials go to a per-block slab
-//   summed in block order by loss_final_kernel (deterministic).
+// so one streaming pass produces the loss partial sums AND d loss/d pred
+// (ssim3_stream_kernel below: column strips x row chunks, separable 3x3 boxes
+// from DPP lane shifts and register row rings, no LDS staging).  Loss
+// partials go to a per-block slab summed in block order by loss_final_kernel
+// (deterministic).
 #include "common.h"
 
 namespace {
 
 constexpr float kC1 = 0.01f * 0.01f;
 constexpr float kC2 = 0.03f * 0.03f;
-constexpr int TH = 16, TW = 64;          // output tile
-constexpr int RH = TH + 4, RW = TW + 4;  // input region (2-pixel halo)
-constexpr int CH = TH + 2, CW = TW + 2;  // coefficient region (1-pixel ring)
 
 __device__ __forceinline__ int reflect1(int q, int n) {
   if (q < 0) q = -q;
@@ -31,13 +27,6 @@ __device__ __forceinline__ int reflect1(int q, int n) {
   return q < 0 ? 0 : (q > n - 1 ? n - 1 : q);
 }
 
-// Times output index i receives the padded sample taken at window centre p.
-__device__ __forceinline__ int mult(int p, int i, int n) {
-  int m = 0;
-#pragma unroll
-  for (int dq = -1; dq <= 1; ++dq) m += reflect1(p + dq, n) == i;
-  return m;
-}
 
 // ---------------------------------------------------------------- min / max
 __global__ void __launch_bounds__(256)
@@ -117,174 +106,191 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------- SSIM + L1
+// Streaming kernel: value + gradient in one pass.  A wave owns a strip of kSW = 60 output
+// columns (lane l <-> column strip*60 - 2 + l: a 2-column halo each side,
+// reflected at the image border) and a chunk of rows, and walks the padded
+// rows top to bottom: the 3-wide horizontal sums come from wave shuffles,
+// the vertical ones from a 3-row register ring, so every input pixel is read
+// once per strip (+2 halo columns of 64) and once per chunk (+4 halo rows).
+// The gradient is the transposed box of the per-centre coefficients, done the
+// same way one row later; the reflection adds the centre-0 / centre-(n-1)
+// coefficients once more to column / row 1 and n-2.  Loss partials: one per
+// block (wave order), summed by loss_final_kernel.
+constexpr int kSW = 60;  // output columns per strip (64 lanes - 2 x 2 halo)
+
+// Neighbour lanes' values by DPP wave shifts (one VALU op, no LDS round trip):
+// lane_prev = value of lane - 1 (0 into lane 0), lane_next = lane + 1 (0 into 63).
+__device__ __forceinline__ float lane_prev(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lane_next(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
 template <bool GT>
 __global__ void __launch_bounds__(256)
-    ssim3_l1_kernel(const float* __restrict__ xp, const float* __restrict__ yp,
-                    const float* __restrict__ mm, int h, int w, int tiles_w,
-                    int tiles_per_img, float gs_ssim, float gs_l1,
-                    float* __restrict__ part, float* __restrict__ gx,
-                    float* __restrict__ gy) {
-  __shared__ float sx[RH][RW], sy[RH][RW];
-  __shared__ float hs[5][RH][CW];
-  __shared__ float ca[CH][CW], cb[CH][CW], cc[CH][CW];
-  __shared__ float cay[GT ? CH : 1][GT ? CW : 1], cby[GT ? CH : 1][GT ? CW : 1];
+    ssim3_stream_kernel(const float* __restrict__ xp, const float* __restrict__ yp,
+                        const float* __restrict__ mm, int h, int w, int strips, int chunks,
+                        int chunk_rows, int64_t nwaves, float gs_ssim, float gs_l1,
+                        float* __restrict__ part, float* __restrict__ gx,
+                        float* __restrict__ gy) {
   __shared__ float red[4];
-
-  const int tid = threadIdx.x;
-  const int img = blockIdx.x / tiles_per_img;
-  const int tix = blockIdx.x % tiles_per_img;
-  const int r0 = (tix / tiles_w) * TH, c0 = (tix % tiles_w) * TW;
-  const int64_t base = (int64_t)img * h * w;
-  const float* X = xp + base;
-  const float* Y = yp + base;
-  float tmn = 0.f, tden = 1.f;
-  const bool norm = mm != nullptr;
-  if (norm) {
-    tmn = mm[0];
-    tden = mm[1] - mm[0];
-  }
-
-  // 1. inputs with a reflected 2-pixel halo
-  for (int e = tid; e < RH * RW; e += 256) {
-    const int a = e / RW, b = e % RW;
-    const int gr = reflect1(r0 - 2 + a, h), gc = reflect1(c0 - 2 + b, w);
-    const int64_t off = (int64_t)gr * w + gc;
-    sx[a][b] = X[off];
-    const float t = Y[off];
-    sy[a][b] = norm ? (t - tmn) / tden : t;
-  }
-  __syncthreads();
-
-  // 2. horizontal 3-sums of x, y, x^2, y^2, xy for the coefficient columns
-  for (int e = tid; e < RH * CW; e += 256) {
-    const int a = e / CW, v = e % CW;
-    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f, s4 = 0.f;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float xv = sx[a][v + k], yv = sy[a][v + k];
-      s0 += xv;
-      s1 += yv;
-      s2 += xv * xv;
-      s3 += yv * yv;
-      s4 += xv * yv;
+  constexpr int NC = GT ? 5 : 3;  // coefficient fields
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float lsum = 0.f, l1sum = 0.f;
+  if (wid < nwaves) {  // wave-uniform
+    const int chunk = (int)(wid % chunks);
+    const int64_t rest = wid / chunks;
+    const int strip = (int)(rest % strips);
+    const int64_t img = rest / strips;
+    const int q = strip * kSW - 2 + lane;
+    const bool qin = q >= 0 && q < w;
+    const bool out = lane >= 2 && lane < 2 + kSW && qin;
+    const float wl = q == 1 ? 2.f : 1.f, wr = q == w - 2 ? 2.f : 1.f;
+    const int64_t base = img * h * w;
+    const float* X = xp + base + reflect1(q, w);
+    const float* Y = yp + base + reflect1(q, w);
+    float tmn = 0.f, tden = 1.f;
+    const bool norm = mm != nullptr;
+    if (norm) {
+      tmn = mm[0];
+      tden = mm[1] - mm[0];
     }
-    hs[0][a][v] = s0;
-    hs[1][a][v] = s1;
-    hs[2][a][v] = s2;
-    hs[3][a][v] = s3;
-    hs[4][a][v] = s4;
-  }
-  __syncthreads();
-
-  // 3. per-pixel statistics, loss and gradient coefficients on tile + ring
-  float lsum = 0.f;
-  const float inv9 = 1.f / 9.f;
-  for (int e = tid; e < CH * CW; e += 256) {
-    const int u = e / CW, v = e % CW;
-    const int pr = r0 - 1 + u, pc = c0 - 1 + v;
-    float A = 0.f, B = 0.f, C = 0.f, Ay = 0.f, By = 0.f;
-    if (pr >= 0 && pr < h && pc >= 0 && pc < w) {
-      float q[5];
+    const int g0 = chunk * chunk_rows, g1 = min(h, g0 + chunk_rows);
+    const int rs = g0 - 2, re = g1 + 1;  // padded rows walked
+    const float inv9 = 1.f / 9.f, k = gs_ssim * -0.5f;
+    float hs[3][5] = {};                 // horizontal sums, rows r-2, r-1, r
+    float cs[3][NC] = {};                // horizontally summed coefficients, rows p-2..p
+    float xr[3] = {}, yr[3] = {};        // inputs, rows r-2..r
+    auto load = [&](int r, float& xv, float& yv) {
+      const int64_t off = (int64_t)reflect1(r, h) * w;
+      xv = X[off];
+      const float t = Y[off];
+      yv = norm ? (t - tmn) / tden : t;
+    };
+    auto step = [&](float xv, float yv, int r) {
 #pragma unroll
-      for (int k = 0; k < 5; ++k)
-        q[k] = (hs[k][u][v] + hs[k][u + 1][v] + hs[k][u + 2][v]) * inv9;
-      const float mx = q[0], my = q[1];
-      const float sxx = q[2] - mx * mx, syy = q[3] - my * my;
-      const float sxy = q[4] - mx * my;
-      const float n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
-      const float d1 = mx * mx + my * my + kC1, d2 = sxx + syy + kC2;
-      const float D = d1 * d2;
-      const float S = (n1 * n2) / D;
-      const float f = (1.f - S) * 0.5f;
-      const bool inside = u >= 1 && u <= TH && v >= 1 && v <= TW;
-      if (inside) lsum += fminf(fmaxf(f, 0.f), 1.f);
-      if (f >= 0.f && f <= 1.f) {
-        const float k = gs_ssim * -0.5f;
-        const float dS_dsx = -S / d2;          // = dS/dsyy
-        const float dS_dsxy = 2.f * n1 / D;
-        const float dS_dmx = 2.f * my * n2 / D - S * 2.f * mx / d1;
-        const float dS_dmy = 2.f * mx * n2 / D - S * 2.f * my / d1;
-        A = k * (dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy);
-        B = k * dS_dsx;
-        C = k * dS_dsxy;
-        Ay = k * (dS_dmy - 2.f * my * dS_dsx - mx * dS_dsxy);
-        By = B;
+      for (int i = 0; i < 2; ++i) {
+        xr[i] = xr[i + 1];
+        yr[i] = yr[i + 1];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) hs[i][f] = hs[i + 1][f];
       }
-    }
-    ca[u][v] = A;
-    cb[u][v] = B;
-    cc[u][v] = C;
-    if (GT) {
-      cay[u][v] = Ay;
-      cby[u][v] = By;
-    }
-  }
-  __syncthreads();
-
-  // 4. gradient + L1 on the tile.  Two pixels away from the image border
-  // every window centre reaches each pixel exactly once (the reflected
-  // windows of centres 0 and n-1 hit pixels 1 and n-2 twice), so such tiles
-  // take a plain 3x3 sum.
-  float l1sum = 0.f;
-  const bool interior = r0 >= 2 && r0 + TH <= h - 2 && c0 >= 2 && c0 + TW <= w - 2;
-  for (int e = tid; e < TH * TW; e += 256) {
-    const int i0 = e / TW, j0 = e % TW;
-    const int gi = r0 + i0, gj = c0 + j0;
-    if (gi >= h || gj >= w) continue;
-    const float xv = sx[i0 + 2][j0 + 2], yv = sy[i0 + 2][j0 + 2];
-    float SA = 0.f, SB = 0.f, SC = 0.f, SAy = 0.f, SBy = 0.f;
-    if (interior) {
+      xr[2] = xv;
+      yr[2] = yv;
+      {
+        const float v[5] = {xv, yv, xv * xv, yv * yv, xv * yv};
 #pragma unroll
-      for (int u = i0; u < i0 + 3; ++u)
+        for (int f = 0; f < 5; ++f)
+          hs[2][f] = (lane_prev(v[f]) + v[f]) + lane_next(v[f]);
+      }
+      if (r < g0) return;  // wave-uniform: the ring is not full yet
+      // centre row p = r - 1: statistics, loss, coefficients
+      const int p = r - 1;
+      const bool valid = qin && p >= 0 && p < h;
+      float c[NC];
 #pragma unroll
-        for (int v = j0; v < j0 + 3; ++v) {
-          SA += ca[u][v];
-          SB += cb[u][v];
-          SC += cc[u][v];
+      for (int f = 0; f < NC; ++f) c[f] = 0.f;
+      if (valid) {
+        float st[5];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) st[f] = (hs[0][f] + hs[1][f] + hs[2][f]) * inv9;
+        const float mx = st[0], my = st[1];
+        const float sxx = st[2] - mx * mx, syy = st[3] - my * my;
+        const float sxy = st[4] - mx * my;
+        const float n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
+        const float d1 = mx * mx + my * my + kC1, d2 = sxx + syy + kC2;
+        const float D = d1 * d2;
+        const float S = (n1 * n2) / D;  // exact division: S(x, x) = 1
+        const float fl = (1.f - S) * 0.5f;
+        if (out && p < g1 && p >= g0) lsum += fminf(fmaxf(fl, 0.f), 1.f);
+        if (fl >= 0.f && fl <= 1.f) {
+          // gradient terms with hardware reciprocals (1 ulp; the tests' 1e-4)
+          const float rD = __builtin_amdgcn_rcpf(D), rd1 = __builtin_amdgcn_rcpf(d1);
+          const float dS_dsx = -S * __builtin_amdgcn_rcpf(d2);  // = dS/dsyy
+          const float dS_dsxy = 2.f * n1 * rD;
+          const float dS_dmx = 2.f * my * n2 * rD - S * 2.f * mx * rd1;
+          c[0] = k * (dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy);
+          c[1] = k * dS_dsx;
+          c[2] = k * dS_dsxy;
           if (GT) {
-            SAy += cay[u][v];
-            SBy += cby[u][v];
+            const float dS_dmy = 2.f * mx * n2 * rD - S * 2.f * my * rd1;
+            c[3] = k * (dS_dmy - 2.f * my * dS_dsx - mx * dS_dsxy);
+            c[NC - 1] = c[1];
           }
         }
-    } else {
+      }
 #pragma unroll
-    for (int du = -1; du <= 1; ++du) {
-      const int pr = gi + du;
-      if (pr < 0 || pr >= h) continue;
-      const int mr = mult(pr, gi, h);
-      if (!mr) continue;
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int dv = -1; dv <= 1; ++dv) {
-        const int pc = gj + dv;
-        if (pc < 0 || pc >= w) continue;
-        const int m = mr * mult(pc, gj, w);
-        if (!m) continue;
-        const float fm = (float)m;
-        const int u = i0 + 1 + du, v = j0 + 1 + dv;
-        SA += fm * ca[u][v];
-        SB += fm * cb[u][v];
-        SC += fm * cc[u][v];
-        if (GT) {
-          SAy += fm * cay[u][v];
-          SBy += fm * cby[u][v];
-        }
+        for (int f = 0; f < NC; ++f) cs[i][f] = cs[i + 1][f];
+#pragma unroll
+      for (int f = 0; f < NC; ++f)
+        cs[2][f] = (wl * lane_prev(c[f]) + c[f]) + wr * lane_next(c[f]);
+      // gradient row g = p - 1 from coefficient rows g-1, g, g+1
+      const int g = p - 1;
+      if (g < g0 || g >= g1) return;  // wave-uniform
+      const float vt = g == 1 ? 2.f : 1.f, vb = g == h - 2 ? 2.f : 1.f;
+      float sm[NC];
+#pragma unroll
+      for (int f = 0; f < NC; ++f) sm[f] = (vt * cs[0][f] + cs[1][f]) + vb * cs[2][f];
+      if (out) {
+        const float x0 = xr[0], y0 = yr[0];
+        const float diff = x0 - y0;
+        l1sum += fabsf(diff);
+        const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
+        const int64_t off = base + (int64_t)g * w + q;
+        if (gx) gx[off] = (sm[0] + 2.f * x0 * sm[1] + y0 * sm[2]) * inv9 + gs_l1 * sgn;
+        if (GT && gy) gy[off] = (sm[3] + 2.f * y0 * sm[NC - 1] + x0 * sm[2]) * inv9 - gs_l1 * sgn;
+      }
+    };
+    // rows in groups of 4, the next group's loads issued before this one's math
+    float cx[4], cy[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load(rs + i, cx[i], cy[i]);
+    for (int r = rs; r <= re; r += 4) {
+      float nx[4], ny[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) load(r + 4 + i, nx[i], ny[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r + i <= re) step(cx[i], cy[i], r + i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cx[i] = nx[i];
+        cy[i] = ny[i];
       }
     }
-    }
-    const float diff = xv - yv;
-    l1sum += fabsf(diff);
-    const float sgn = diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f);
-    const int64_t off = base + (int64_t)gi * w + gj;
-    if (gx) gx[off] = (SA + 2.f * xv * SB + yv * SC) * inv9 + gs_l1 * sgn;
-    if (GT && gy) gy[off] = (SAy + 2.f * yv * SBy + xv * SC) * inv9 - gs_l1 * sgn;
   }
-
   const float ts = mde::block_sum256(lsum, red);
   const float tl = mde::block_sum256(l1sum, red);
-  if (tid == 0) {
+  if (threadIdx.x == 0) {
     part[2 * blockIdx.x] = ts;
     part[2 * blockIdx.x + 1] = tl;
   }
+}
+
+struct StreamPlan {
+  int strips, chunks, chunk_rows;
+  int64_t nwaves, nblocks;
+};
+
+// Enough waves to keep ~8 per SIMD (8192) from strips x chunks, chunks of
+// >= 16 rows (the 4 halo rows are L2 hits of the neighbouring chunks).
+inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w) {
+  StreamPlan p;
+  p.strips = (int)mde::cdiv(w, kSW);
+  const int64_t per_chunk = b * p.strips;
+  int64_t ch = mde::cdiv(8192, per_chunk);
+  const int64_t maxc = mde::cdiv(h, 16);
+  if (ch > maxc) ch = maxc;
+  if (ch < 1) ch = 1;
+  p.chunk_rows = (int)mde::cdiv(h, ch);
+  p.chunks = (int)mde::cdiv(h, p.chunk_rows);
+  p.nwaves = per_chunk * p.chunks;
+  p.nblocks = mde::cdiv(p.nwaves, 4);
+  return p;
 }
 
 // loss[0] = w_ssim*ssim + w_l1*l1, loss[1] = ssim, loss[2] = l1.
@@ -313,9 +319,6 @@ inline int minmax_blocks(int64_t numel) {
   return (int)(b < 1 ? 1 : (b > 1024 ? 1024 : b));
 }
 
-inline int64_t ssim_blocks(int64_t b, int64_t h, int64_t w) {
-  return b * mde::cdiv(h, TH) * mde::cdiv(w, TW);
-}
 
 }  // namespace
 
@@ -350,7 +353,8 @@ int mde_depthnorm_apply(const void* x, const float* minmax, void* y,
 }
 
 size_t mde_ssim3_l1_workspace(int64_t b, int64_t h, int64_t w) {
-  return sizeof(float) * 2 * (size_t)ssim_blocks(b, h, w);
+  if (b <= 0 || h <= 0 || w <= 0) return 0;
+  return sizeof(float) * 2 * (size_t)stream_plan(b, h, w).nblocks;
 }
 
 int mde_ssim3_l1_fwd(const void* pred, const void* target,
@@ -362,28 +366,25 @@ int mde_ssim3_l1_fwd(const void* pred, const void* target,
   if (!pred || !target || !loss || !workspace || b <= 0 || h < 2 || w < 2 ||
       h > (1 << 24) || w > (1 << 24))
     return MDE_ERR_INVALID_ARG;
-  const int64_t nblocks = ssim_blocks(b, h, w);
+  const StreamPlan sp = stream_plan(b, h, w);
+  const int64_t nblocks = sp.nblocks;
   if (nblocks > 0x7fffffff) return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t numel = b * h * w;
   const float inv = 1.f / (float)numel;
-  const int tiles_w = (int)mde::cdiv(w, TW);
-  const int tiles_per_img = (int)(mde::cdiv(h, TH) * tiles_w);
   float* part = (float*)workspace;
   const double bytes =
       4.0 * numel * (2.0 + (grad_pred ? 1.0 : 0.0) + (grad_target ? 1.0 : 0.0));
   if (grad_target) {
-    MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_l1_kernel<true>,
-               dim3((unsigned)nblocks), dim3(256), 0, (const float*)pred,
-               (const float*)target, target_minmax, (int)h, (int)w, tiles_w,
-               tiles_per_img, w_ssim * inv, w_l1 * inv, part,
-               (float*)grad_pred, (float*)grad_target);
+    MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_stream_kernel<true>, dim3((unsigned)nblocks),
+               dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
+               (int)w, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv, w_l1 * inv,
+               part, (float*)grad_pred, (float*)grad_target);
   } else {
-    MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_l1_kernel<false>,
-               dim3((unsigned)nblocks), dim3(256), 0, (const float*)pred,
-               (const float*)target, target_minmax, (int)h, (int)w, tiles_w,
-               tiles_per_img, w_ssim * inv, w_l1 * inv, part,
-               (float*)grad_pred, (float*)nullptr);
+    MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_stream_kernel<false>, dim3((unsigned)nblocks),
+               dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
+               (int)w, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv, w_l1 * inv,
+               part, (float*)grad_pred, (float*)nullptr);
   }
   MDE_LAUNCH(mde::K_LOSS_FINAL, 8.0 * nblocks, s, loss_final_kernel, dim3(1),
              dim3(256), 0, part, (int)nblocks, inv, w_ssim, w_l1, loss);

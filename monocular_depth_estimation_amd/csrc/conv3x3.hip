@@ -61,29 +61,38 @@ struct HaloTile {
   static constexpr int ROWS = CIP * XR;
   static constexpr int RPWV = (ROWS + 3) / 4;      // tile rows per wave
   static constexpr int NH = (2 * RPWV + 63) / 64;  // right-halo loads per lane
+  static_assert(RPWV <= 64 && NH <= 32, "mask widths");
   float a[RPWV];
   float b[NH];
+  // In-range flags, applied at store time: loads are unconditional (clamped
+  // addresses) and nothing reads their values until the next tile's store,
+  // so no select or divergent branch makes the wave wait for them early.
+  uint64_t am;
+  unsigned bm;
 
   __device__ __forceinline__ void load(const float* __restrict__ xi, int h, int w, int r0,
                                        int c0, int lane, int wvu) {
     const int gc = c0 - 1 + lane;
     const bool cok = gc >= 0 && gc < w;
+    am = 0;
 #pragma unroll
     for (int k = 0; k < RPWV; ++k) {
       const int ri = wvu + 4 * k;
       const int c = ri / XR, r = ri % XR, gr = r0 - 1 + r;
-      const bool ok = ri < ROWS && c < CI && gr >= 0 && gr < h && cok;
-      const float t = xi[ok ? ((int64_t)c * h + gr) * w + gc : 0];
-      a[k] = ok ? t : 0.f;
+      const bool ok = (ROWS % 4 == 0 || ri < ROWS) && (CI == CIP || c < CI) && gr >= 0 &&
+                      gr < h && cok;
+      a[k] = xi[ok ? (unsigned)((c * h + gr) * w + gc) : 0u];  // 32-bit offsets: image < 2^31
+      am |= ok ? (uint64_t)1 << k : (uint64_t)0;
     }
+    bm = 0;
 #pragma unroll
     for (int q = 0; q < NH; ++q) {
       const int e = 64 * q + lane;  // (row k = e / 2, column 64 + e % 2)
       const int ri = wvu + 4 * (e >> 1);
       const int c = ri / XR, r = ri % XR, gr = r0 - 1 + r, g2 = c0 + 63 + (e & 1);
       const bool ok = e < 2 * RPWV && ri < ROWS && c < CI && gr >= 0 && gr < h && g2 < w;
-      const float t = xi[ok ? ((int64_t)c * h + gr) * w + g2 : 0];
-      b[q] = ok ? t : 0.f;
+      b[q] = xi[ok ? (unsigned)((c * h + gr) * w + g2) : 0u];
+      bm |= ok ? 1u << q : 0u;
     }
   }
 
@@ -92,45 +101,59 @@ struct HaloTile {
 #pragma unroll
     for (int k = 0; k < RPWV; ++k) {
       const int ri = wvu + 4 * k;
-      if (ri < ROWS) sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = a[k];
+      if (ROWS % 4 == 0 || ri < ROWS)
+        sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = (am >> k) & 1 ? a[k] : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < NH; ++q) {
       const int e = 64 * q + lane;
       const int ri = wvu + 4 * (e >> 1);
-      if (e < 2 * RPWV && ri < ROWS) sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = b[q];
+      if (e < 2 * RPWV && ri < ROWS)
+        sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = (bm >> q) & 1u ? b[q] : 0.f;
     }
   }
 };
 
 // A CO x TH x 64 gradient tile (rows r0.., cols c0..) as float4: 16 lanes
-// per row, 4 rows per wave instruction; zero outside the image.
-template <int CO, int TH>
+// per row, 4 rows per wave instruction; zero outside the image.  FULL (w a
+// multiple of 64, so every tile is full width): one unconditional float4 load
+// per row at a clamped address -- no per-element branches, so all the tile's
+// loads are in flight together (the generic path's conditional scalar loads
+// made the compiler drain the queue row by row).
+template <int CO, int TH, bool FULL>
 struct GradTile {
   static constexpr int ROWS = CO * TH;
   static constexpr int PER = (ROWS + 15) / 16;
+  static_assert(PER <= 32, "mask width");
   float4 v[PER];
+  unsigned vm;  // rows in range (FULL), applied at store time like HaloTile's
 
   __device__ __forceinline__ void load(const float* __restrict__ gi, int h, int w, int r0,
                                        int c0, int lane, int wvu) {
     const int gc = c0 + 4 * (lane & 15);
-    const bool vec = (w & 3) == 0 && gc + 3 < w;
+    vm = 0;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int ri = 16 * i + 4 * wvu + (lane >> 4);
       const int c = ri / TH, gr = r0 + ri % TH;
-      const bool rok = ri < ROWS && gr < h;
-      const float* src = gi + (rok ? ((int64_t)c * h + gr) * w + gc : 0);
-      if (vec) {
-        const float4 t = *reinterpret_cast<const float4*>(src);
-        v[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      const bool rok = (ROWS % 16 == 0 || ri < ROWS) && gr < h;
+      if constexpr (FULL) {
+        v[i] = *reinterpret_cast<const float4*>(gi + (rok ? (unsigned)((c * h + gr) * w + gc) : 0u));
+        vm |= rok ? 1u << i : 0u;
       } else {
-        float4 t;
-        t.x = rok && gc < w ? src[0] : 0.f;
-        t.y = rok && gc + 1 < w ? src[1] : 0.f;
-        t.z = rok && gc + 2 < w ? src[2] : 0.f;
-        t.w = rok && gc + 3 < w ? src[3] : 0.f;
-        v[i] = t;
+        const float* src = gi + (rok ? ((int64_t)c * h + gr) * w + gc : 0);
+        const bool vec = (w & 3) == 0 && gc + 3 < w;
+        if (vec) {
+          const float4 t = *reinterpret_cast<const float4*>(src);
+          v[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+          float4 t;
+          t.x = rok && gc < w ? src[0] : 0.f;
+          t.y = rok && gc + 1 < w ? src[1] : 0.f;
+          t.z = rok && gc + 2 < w ? src[2] : 0.f;
+          t.w = rok && gc + 3 < w ? src[3] : 0.f;
+          v[i] = t;
+        }
       }
     }
   }
@@ -140,8 +163,11 @@ struct GradTile {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int ri = 16 * i + 4 * wvu + (lane >> 4);
-      if (ri < ROWS)
-        *reinterpret_cast<float4*>(sg + (ri / TH) * PSG + (ri % TH) * kTW + 4 * (lane & 15)) = v[i];
+      if (ROWS % 16 == 0 || ri < ROWS) {
+        float4 t = v[i];
+        if (FULL && !((vm >> i) & 1u)) t = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(sg + (ri / TH) * PSG + (ri % TH) * kTW + 4 * (lane & 15)) = t;
+      }
     }
   }
 };
@@ -294,7 +320,7 @@ struct WgradCfg {
   static constexpr int M = CO * NP;               // partial elements per block
 };
 
-template <int CI, int CO, int TH, int PW>
+template <int CI, int CO, int TH, int PW, bool FULL>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                          float* __restrict__ part, int h, int w, int tiles_w,
@@ -332,7 +358,7 @@ __global__ void __launch_bounds__(256, 2)
 
   for (int e = tid; e < C::XR * kXW; e += 256) smem[C::ZERO + e] = 0.f;
   HaloTile<CI, C::CIP, C::XR> T;
-  GradTile<CO, TH> G;
+  GradTile<CO, TH, FULL> G;
   int tile = blockIdx.x;
   if (tile < ntiles) {
     const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
@@ -491,8 +517,14 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
   float* part = ws;
   float* part2 = ws + (int64_t)p.grid * p.m;
-  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW>), dim3(p.grid),
-             dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w, p.tiles_per_img, p.ntiles);
+  if (w % kTW == 0)
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
+                    dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
+                    p.tiles_per_img, p.ntiles);
+  else
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
+                    dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
+                    p.tiles_per_img, p.ntiles);
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
   MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
              dim3((unsigned)mde::cdiv(p.m, 256), split), dim3(256), 0, part, part2, p.grid, p.m);
@@ -530,8 +562,11 @@ int variant() {
   return v;
 }
 
+// The tile loaders index one image with 32-bit offsets: 64 channels x h x w
+// (the widest supported image) must stay under 2^31 elements.
 bool dims_ok(int64_t n, int64_t h, int64_t w) {
-  return n > 0 && h > 0 && w > 0 && h < (1 << 24) && w < (1 << 24);
+  return n > 0 && h > 0 && w > 0 && h < (1 << 24) && w < (1 << 24) &&
+         64 * h * w < ((int64_t)1 << 31);
 }
 
 }  // namespace
@@ -581,9 +616,9 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   if (cin == 3 && cout == 16) p = wgrad_plan<3, 16, 8, 4>(n, h, w);
   else if (cin == 3 && cout == 32) p = wgrad_plan<3, 32, 8, 4>(n, h, w);
   else if (cin == 3) p = wgrad_plan<3, 64, 4, 4>(n, h, w);
-  else if (cin == 16 && variant() == 1) p = wgrad_plan<16, 16, 4, 4>(n, h, w);
+  else if (cin == 16 && variant() == 1) p = wgrad_plan<16, 16, 8, 4>(n, h, w);
   else if (cin == 16 && variant() == 2) p = wgrad_plan<16, 16, 4, 2>(n, h, w);
-  else if (cin == 16) p = wgrad_plan<16, 16, 8, 4>(n, h, w);
+  else if (cin == 16) p = wgrad_plan<16, 16, 4, 4>(n, h, w);
   else if (variant() == 1) p = wgrad_plan<32, 32, 4, 2>(n, h, w);
   else if (variant() == 2) p = wgrad_plan<32, 32, 4, 1>(n, h, w);
   else p = wgrad_plan<32, 32, 2, 2>(n, h, w);
@@ -605,9 +640,9 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   if (cin == 3 && cout == 16) return launch_wgrad<3, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3 && cout == 32) return launch_wgrad<3, 32, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3) return launch_wgrad<3, 64, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
-  if (cin == 16 && variant() == 1) return launch_wgrad<16, 16, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 16 && variant() == 1) return launch_wgrad<16, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 16 && variant() == 2) return launch_wgrad<16, 16, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
-  if (cin == 16) return launch_wgrad<16, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (cin == 16) return launch_wgrad<16, 16, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (variant() == 1) return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (variant() == 2) return launch_wgrad<32, 32, 4, 1>(xi, g, gweight, n, h, w, ws, bytes, s);
   return launch_wgrad<32, 32, 2, 2>(xi, g, gweight, n, h, w, ws, bytes, s);

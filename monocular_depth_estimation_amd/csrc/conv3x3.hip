@@ -176,6 +176,24 @@ struct TileGeo {
   int img, r0, c0;
 };
 
+// Tiles walked by a persistent block: t0, t0 + step, ... < end.  XCD-aware
+// (blocks b and b + 8 share an XCD and its L2 under round-robin placement):
+// the 8 block groups take 8 contiguous ranges of the tile list, so the tiles
+// vertically next to a tile (+- tiles_w, whose halo rows it re-reads) are
+// processed at about the same time in the SAME L2.  Speed only: any
+// placement gives the same tiles to the same blocks.
+struct TileWalk {
+  int t0, step, end;
+};
+
+__device__ __forceinline__ TileWalk tile_walk(int ntiles) {
+  const int b = blockIdx.x, g = gridDim.x;
+  if (g % 8 != 0 || ntiles < g) return {b, g, ntiles};
+  const int span = (ntiles + 7) / 8, grp = b & 7;
+  const int end = (grp + 1) * span < ntiles ? (grp + 1) * span : ntiles;
+  return {grp * span + (b >> 3), g >> 3, end};
+}
+
 __device__ __forceinline__ TileGeo tile_geo(int tile, int th, int tiles_w, int tiles_per_img) {
   const int t = tile % tiles_per_img;
   return {tile / tiles_per_img, (t / tiles_w) * th, (t % tiles_w) * kTW};
@@ -231,18 +249,19 @@ __global__ void __launch_bounds__(256, 2)
   const bool vec = (w & 3) == 0;
 
   HaloTile<CI, CIP, XR> T;
-  int tile = blockIdx.x;
-  if (tile < ntiles) {
+  const TileWalk tw = tile_walk(ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) {
     const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
     T.load(x + g.img * img_in, h, w, g.r0, g.c0, lane, wvu);
   }
-  for (; tile < ntiles; tile += gridDim.x) {
+  for (; tile < tw.end; tile += tw.step) {
     const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
     __syncthreads();  // previous tile's operands consumed (and weights staged)
     T.template store<PS>(sx, lane, wvu);
     __syncthreads();
-    const int nxt = tile + gridDim.x;
-    if (nxt < ntiles) {
+    const int nxt = tile + tw.step;
+    if (nxt < tw.end) {
       const TileGeo gn = tile_geo(nxt, TH, tiles_w, tiles_per_img);
       T.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
     }
@@ -359,19 +378,20 @@ __global__ void __launch_bounds__(256, 2)
   for (int e = tid; e < C::XR * kXW; e += 256) smem[C::ZERO + e] = 0.f;
   HaloTile<CI, C::CIP, C::XR> T;
   GradTile<CO, TH, FULL> G;
-  int tile = blockIdx.x;
-  if (tile < ntiles) {
+  const TileWalk tw = tile_walk(ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) {
     const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
     G.load(gy + g.img * img_out, h, w, g.r0, g.c0, lane, wvu);
     T.load(x + g.img * img_in, h, w, g.r0, g.c0, lane, wvu);
   }
-  for (; tile < ntiles; tile += gridDim.x) {
+  for (; tile < tw.end; tile += tw.step) {
     __syncthreads();  // previous tile's operands consumed
     T.template store<C::PSX>(sx, lane, wvu);
     G.template store<C::PSG>(sg, lane, wvu);
     __syncthreads();
-    const int nxt = tile + gridDim.x;
-    if (nxt < ntiles) {
+    const int nxt = tile + tw.step;
+    if (nxt < tw.end) {
       const TileGeo gn = tile_geo(nxt, TH, tiles_w, tiles_per_img);
       G.load(gy + gn.img * img_out, h, w, gn.r0, gn.c0, lane, wvu);
       T.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);

@@ -215,8 +215,10 @@ def main():
 
     def roof(name):
         ms, launches, nbytes, flops = kernels[name]
-        traffic = pmc.get(name, {}).get("bytes_per_launch")
         per_launch = nbytes / launches
+        # PMC HBM bytes of this registry name per step (all its launches), per launch
+        per_step = pmc.get(name, {}).get("bytes_per_step")
+        traffic = per_step / (launches / timing_steps) if per_step else None
         common = {"kernel": name, "traffic": traffic,
                   "traffic_ratio": round(traffic / per_launch, 3) if traffic else None,
                   "bytes_per_launch": per_launch, "avg_launch_us": round(ms * 1e3 / launches, 2),

@@ -159,16 +159,27 @@ class GraphTrainer:
     Gradients are allocated by the captured backward itself (grads set to None
     before capture, so autograd hands its result buffers to .grad without a
     copy; replays reuse those static buffers).  N == 1: one graph (forward,
-    loss, backward, fused capturable Adam).  N > 1: graph A (forward, loss,
-    backward, gradients packed into one flat buffer scaled by 1/N) -> one RCCL
-    all-reduce of that buffer -> graph B (unpack, Adam); the BN running
+    loss, backward, fused capturable Adam).
+
+    N > 1 over RCCL ("nccl"): the gradients are views of ~6 MB bucket buffers
+    (parameters in reverse registration order, i.e. about the order backward
+    finishes them).  A post-accumulate hook counts each bucket's parameters;
+    when the last one is final the bucket is scaled by 1/N and all-reduced on
+    a side stream that forks from the backward stream at that point, so the
+    RCCL collectives are captured INTO the step graph and overlap the rest of
+    the backward; the Adam step joins the side stream.  One graph, no pack /
+    unpack copies.  (gloo, or MDE_DP_OVERLAP=0: graph A -> one flat all-reduce
+    outside the graph -> graph B, the round-1 scheme.)  The BN running
     statistics (one flat buffer) are broadcast from rank 0 before each
     forward, as DDP's broadcast_buffers does.  Inputs are copied into static
     device buffers.  CUDA only; BN stays in train mode (the eval-mode quirk
     changes the graph, use Trainer for that).
     """
 
-    def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2, amp: str = ""):
+    BUCKET_BYTES = 6 << 20
+
+    def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2, amp: str = "",
+                 dp_overlap: bool | None = None):
         if world.device.type != "cuda":
             raise RuntimeError("GraphTrainer needs a GPU (use Trainer on CPU)")
         self.model, self.loss_fn, self.world = model, loss_fn, world
@@ -197,6 +208,16 @@ class GraphTrainer:
             dist.broadcast(self.flat_bn, 0)
         self.static_image = self.static_depth = None
         self.stream = torch.cuda.Stream(device=world.device)  # eager warm-up + capture stream
+        # bucketed all-reduce overlapped with backward (RCCL only: it is captured
+        # into the graph); dp_overlap=True with one rank exercises the same path
+        if dp_overlap is None:
+            dp_overlap = (world.size > 1 and dist.get_backend() == "nccl"
+                          and os.environ.get("MDE_DP_OVERLAP", "1") != "0")
+        self.buckets = self._make_buckets() if dp_overlap else None
+        if self.buckets is not None:
+            self.side = torch.cuda.Stream(device=world.device)
+            for p in self.params:
+                p.register_post_accumulate_grad_hook(self._grad_ready)
         self.last_loss = None
         self.loss_sum = torch.zeros((), device=world.device)
         self.loss_count = 0
@@ -204,12 +225,67 @@ class GraphTrainer:
     def begin_epoch(self):
         self.model.train()
 
+    # -- bucketed, overlapped all-reduce ------------------------------------
+    def _make_buckets(self):
+        """[(params, flat buffer)], parameters in reverse registration order
+        split into ~BUCKET_BYTES groups; every .grad becomes a view of its
+        bucket (kept across steps: the buffers are zeroed before each backward,
+        never re-allocated)."""
+        groups, cur, nbytes = [], [], 0
+        for p in reversed(self.params):
+            cur.append(p)
+            nbytes += p.numel() * p.element_size()
+            if nbytes >= self.BUCKET_BYTES:
+                groups.append(cur)
+                cur, nbytes = [], 0
+        if cur:
+            groups.append(cur)
+        buckets = []
+        self.bucket_of = {}
+        for i, ps in enumerate(groups):
+            flat = torch.zeros(sum(p.numel() for p in ps), device=self.world.device,
+                               dtype=ps[0].dtype)
+            off = 0
+            for p in ps:
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+                self.bucket_of[p] = i
+            buckets.append((ps, flat))
+        self.pending = [0] * len(buckets)
+        return buckets
+
+    def _grad_ready(self, p):
+        if self.buckets is None or p not in self.bucket_of:
+            return
+        b = self.bucket_of[p]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch_bucket(b)
+
+    def _launch_bucket(self, b):
+        self.pending[b] = -1  # launched
+        flat = self.buckets[b][1]
+        self.side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.side):
+            if self.world.size > 1:
+                flat.mul_(1.0 / self.world.size)
+                dist.all_reduce(flat)
+
     # -- the step's pieces (each runs eagerly or inside a capture) ----------
     def _forward_backward(self):
+        if self.buckets is not None:
+            for ps, flat in self.buckets:
+                flat.zero_()
+            self.pending = [len(ps) for ps, _ in self.buckets]
         with amp_context(self.amp, self.world.device):
             loss = self.loss_fn(self.model(self.static_image), self.static_depth)
         loss.backward()
-        if self.world.size > 1:
+        if self.buckets is not None:
+            for b in range(len(self.buckets)):  # parameters that got no gradient
+                if self.pending[b] >= 0:
+                    self._launch_bucket(b)
+            torch.cuda.current_stream().wait_stream(self.side)
+        elif self.world.size > 1:
             grads = [p.grad for p in self.params if p.grad is not None]
             if self.flat_grad is None:
                 self.flat_grad = torch.empty(sum(g.numel() for g in grads),
@@ -219,7 +295,7 @@ class GraphTrainer:
         return loss.detach()
 
     def _unpack_and_update(self):
-        if self.world.size > 1:
+        if self.world.size > 1 and self.buckets is None:
             grads = [p.grad for p in self.params if p.grad is not None]
             flat = self.flat_grad.split([g.numel() for g in grads])
             torch._foreach_copy_(grads, [f.view_as(g) for f, g in zip(flat, grads)])
@@ -230,11 +306,15 @@ class GraphTrainer:
             dist.broadcast(self.flat_bn, 0)
 
     def _allreduce(self):
-        if self.world.size > 1:
+        if self.world.size > 1 and self.buckets is None:
             dist.all_reduce(self.flat_grad)
 
+    def _zero_grad(self):
+        if self.buckets is None:  # bucket views stay; _forward_backward zeroes them
+            self.optimizer.zero_grad(set_to_none=True)
+
     def _eager(self):
-        self.optimizer.zero_grad(set_to_none=True)
+        self._zero_grad()
         loss = self._forward_backward()
         self._allreduce()
         self._unpack_and_update()
@@ -286,17 +366,18 @@ class GraphTrainer:
         on a graph's first replay on this ROCm stack (csrc/graph.hip)."""
         from . import _abi
         torch.cuda.synchronize()
-        self.optimizer.zero_grad(set_to_none=True)  # backward allocates .grad in the graph pool
+        self._zero_grad()  # backward allocates .grad in the graph pool (non-bucket mode)
+        one_graph = self.world.size == 1 or self.buckets is not None
 
         def part_a():
             loss = self._forward_backward()
-            if self.world.size == 1:
+            if one_graph:
                 self.optimizer.step()
             return loss
 
         ga, self.static_loss, na = _abi.capture_graph(part_a, self.stream)
         gb, nb = None, 0
-        if self.world.size > 1:
+        if not one_graph:
             gb, _, nb = _abi.capture_graph(self._unpack_and_update, self.stream, pool=ga.pool())
         self.memsets_replaced = na + nb
         self.graphs = (ga, gb)
@@ -316,11 +397,12 @@ class GraphTrainer:
         from . import _abi
         torch.cuda.synchronize()
         _abi.timing_reset()
-        self.optimizer.zero_grad(set_to_none=True)
+        self._zero_grad()
+        one_graph = self.world.size == 1 or self.buckets is not None
 
         def part():
             loss = self._forward_backward()
-            if self.world.size == 1:
+            if one_graph:
                 self.optimizer.step()
             return loss
 

@@ -13,7 +13,7 @@ HB=$!
 trap 'kill $HB; rm -rf gpurun_out/miopen_sync && cp -r .miopen gpurun_out/miopen_sync' EXIT
 STEPS=${STEPS:-5}
 WARMUP=${WARMUP:-3}
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 echo "== trace ($(date +%T))"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv \
   -d "$ROOT/gpurun_out/prof/trace" -o "$TAG" -- \

@@ -12,6 +12,6 @@ timeout -k 10 600 python bench.py --workload newcrf --steps 10 --warmup 3 --no-c
 tail -1 gpurun_out/bench_newcrf.log | cut -c1-300
 echo "== newcrf trace ($(date +%T))"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$PWD/gpurun_out/prof_nc/trace" \
-  -o r01 -- python3 bench.py --workload newcrf --steps 5 --warmup 3 --no-cpu-baseline \
+  -o r02 -- python3 bench.py --workload newcrf --steps 5 --warmup 3 --no-cpu-baseline \
   > gpurun_out/prof_nc/trace_bench.log 2>&1 || exit $?
 echo done

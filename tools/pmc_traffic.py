@@ -6,8 +6,8 @@ FETCH_SIZE and WRITE_SIZE come from separate --pmc passes (they do not fit
 one TCC pass).  Per MI355X_MICROARCH.md §HBM: both are in KiB; on gfx950
 FETCH_SIZE reports half the bytes of a wide coalesced read, so
   traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
-Only the launches of the last K train steps are used (steady state, steps
-delimited by minmax_partial_kernel as in tools/trace_steps.py).  Keys are the
+Only the launches of the last K train steps are used (steady state: the K
+steps between two minmax_partial_kernel launches -- the loss, mid-step).  Keys are the
 timing-registry names bench.py reports (mde_kernel_name).
 """
 from __future__ import annotations
@@ -20,8 +20,8 @@ import re
 
 # demangled kernel symbol -> timing-registry name (csrc/timing.hip)
 NAMES = [
-    (r"bilinear_fwd_kernel", "bilinear_fwd"),
-    (r"bilinear_bwd(_x2)?_kernel", "bilinear_bwd"),
+    (r"bilinear_fwd\w*_kernel", "bilinear_fwd"),
+    (r"bilinear_bwd\w*_kernel", "bilinear_bwd"),
     (r"nearest_fwd_kernel", "nearest_fwd"),
     (r"nearest_bwd_kernel", "nearest_bwd"),
     (r"se_partial_kernel<false>", "se_squeeze"),
@@ -30,10 +30,10 @@ NAMES = [
     (r"se_scale_kernel", "se_scale"),
     (r"se_(bfc[123]|wgrad)_kernel", "se_bwd_fc"),
     (r"se_apply_kernel", "se_bwd_apply"),
-    (r"skip_fwd_mfma_kernel<\d+, \d+, true>", "skip_reduce_fwd"),
-    (r"skip_fwd_mfma_kernel<\d+, \d+, false>", "pointwise_fwd"),
-    (r"skip_bwd_mfma_kernel<\d+, \d+, true>", "skip_reduce_bwd"),
-    (r"skip_bwd_mfma_kernel<\d+, \d+, false>", "pointwise_bwd"),
+    (r"skip_fwd_mfma_kernel<\d+, \d+, true", "skip_reduce_fwd"),
+    (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
+    (r"skip_bwd_mfma_kernel<\d+, \d+, true", "skip_reduce_bwd"),
+    (r"skip_bwd_mfma_kernel<\d+, \d+, false", "pointwise_bwd"),
     (r"conv3x3_fwd_kernel<.*false>", "conv3x3_fwd"),
     (r"conv3x3_fwd_kernel<.*true>", "conv3x3_dgrad"),
     (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),
@@ -44,9 +44,10 @@ NAMES = [
     (r"minmax_partial_kernel", "minmax"),
     (r"minmax_final_kernel", "minmax_final"),
     (r"depthnorm_kernel", "depthnorm_apply"),
-    (r"ssim3_l1_kernel", "ssim3_l1"),
+    (r"ssim3_(l1|stream)_kernel", "ssim3_l1"),
     (r"loss_final_kernel", "loss_final"),
     (r"bn_stats_kernel", "bn_fwd_stats"),
+    (r"bn_coef_kernel", "bn_fwd_final"),
     (r"bn_apply_plane_kernel", "bn_fwd_apply"),
     (r"bn_apply_table_kernel", "bn_fwd_apply_small"),
     (r"bn_bwd_reduce_kernel", "bn_bwd_reduce"),
@@ -55,11 +56,11 @@ NAMES = [
     (r"skip_bwd_reg_kernel", "skip_reduce_bwd"),
     (r"wattn_fwd_kernel", "window_attn_fwd"),
     (r"wattn_(bwd|slab_reduce)_kernel|zero_kernel", "window_attn_bwd"),
-    (r"dw_fwd_strip_kernel", "dwconv_fwd"),
-    (r"dw_bwd_strip_kernel", "dwconv_bwd"),
+    (r"dw_fwd_(strip|stream)_kernel", "dwconv_fwd"),
+    (r"dw_bwd_(strip|stream)_kernel", "dwconv_bwd"),
     (r"dw_bwd_data_kernel", "dwconv_bwd_data"),
     (r"dw_bwd_weight_kernel", "dwconv_bwd_weight"),
-    (r"dw_wreduce_kernel", "dwconv_wreduce"),
+    (r"dw_(wreduce|wsum)_kernel", "dwconv_wreduce"),
     (r"ln_fwd_kernel", "layernorm_fwd"),
     (r"ln_bwd_kernel", "layernorm_bwd"),
     (r"ln_wreduce_kernel", "layernorm_wreduce"),
@@ -78,9 +79,14 @@ def load(path, counter, last_steps):
     rows = [r for r in csv.DictReader(open(path)) if r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if "minmax_partial_kernel" in r["Kernel_Name"]]
-    start = marks[-last_steps - 1] + 1 if len(marks) > last_steps else 0
+    # exactly `last_steps` whole steps: from one step's minmax (the loss, mid-
+    # step) to the same point `last_steps` steps later
+    if len(marks) > last_steps:
+        start, end = marks[-last_steps - 1], marks[-1]
+    else:
+        start, end = 0, len(rows)
     agg = collections.defaultdict(lambda: [0.0, 0])
-    for r in rows[start:]:
+    for r in rows[start:end]:
         name = registry_name(r["Kernel_Name"])
         if name:
             agg[name][0] += float(r["Counter_Value"])
@@ -101,9 +107,12 @@ def main():
     for name in sorted(set(f) | set(w)):
         fk, fn = f.get(name, [0.0, 1])
         wk, wn = w.get(name, [0.0, 1])
+        # per step too: the timing registry groups some helper launches under
+        # the main kernel's name (e.g. a slab reduce), so ratios are taken per step
         out[name] = {"fetch_bytes_per_launch": 2 * fk * 1024 / fn,
                      "write_bytes_per_launch": wk * 1024 / wn,
                      "bytes_per_launch": 2 * fk * 1024 / fn + wk * 1024 / wn,
+                     "bytes_per_step": (2 * fk + wk) * 1024 / a.last_steps,
                      "launches": fn}
     txt = json.dumps(out, indent=1)
     if a.out:

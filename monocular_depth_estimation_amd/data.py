@@ -38,46 +38,49 @@ from .functional import _gpu
 _PERMS = list(permutations(range(3), 3))
 
 
-def _is_pil_image(img):
-    return isinstance(img, Image.Image)
+def _pil(x) -> bool:
+    return isinstance(x, Image.Image)
 
 
-def _is_numpy_image(img):
-    return isinstance(img, np.ndarray) and (img.ndim in {2, 3})
+def _ndarray_image(x) -> bool:
+    return isinstance(x, np.ndarray) and x.ndim in (2, 3)
+
+
+def _require_pil(sample, what):
+    """Both entries of a sample must be PIL images (TypeError otherwise, as the
+    reference transforms raise)."""
+    for key in ("image", "depth"):
+        if not _pil(sample[key]):
+            raise TypeError(f"{what}: sample[{key!r}] must be a PIL Image, got {type(sample[key])}")
+    return sample["image"], sample["depth"]
 
 
 # ------------------------------------------------------------------ host API
 class RandomHorizontalFlip:
-    """data.py:16-31 (host, PIL)."""
+    """data.py:16-31 (host, PIL): one random.random() draw per sample; < 0.5
+    mirrors image and depth together."""
 
     def __call__(self, sample):
-        image, depth = sample["image"], sample["depth"]
-        if not _is_pil_image(image):
-            raise TypeError("img should be PIL Image. Got {}".format(type(image)))
-        if not _is_pil_image(depth):
-            raise TypeError("img should be PIL Image. Got {}".format(type(depth)))
-        if random.random() < 0.5:
-            image = image.transpose(Image.FLIP_LEFT_RIGHT)
-            depth = depth.transpose(Image.FLIP_LEFT_RIGHT)
+        image, depth = _require_pil(sample, "RandomHorizontalFlip")
+        flip = random.random() < 0.5
+        if flip:
+            image, depth = (im.transpose(Image.FLIP_LEFT_RIGHT) for im in (image, depth))
         return {"image": image, "depth": depth}
 
 
 class RandomChannelSwap:
-    """data.py:33-46 (host, PIL)."""
+    """data.py:33-46 (host, PIL): a random.random() draw against `probability`,
+    then (only when it hits) a random.randint over the 6 RGB permutations."""
 
     def __init__(self, probability):
         self.probability = probability
         self.indices = list(_PERMS)
 
     def __call__(self, sample):
-        image, depth = sample["image"], sample["depth"]
-        if not _is_pil_image(image):
-            raise TypeError("img should be PIL Image. Got {}".format(type(image)))
-        if not _is_pil_image(depth):
-            raise TypeError("img should be PIL Image. Got {}".format(type(depth)))
+        image, depth = _require_pil(sample, "RandomChannelSwap")
         if random.random() < self.probability:
-            image = np.asarray(image)
-            image = Image.fromarray(image[..., list(self.indices[random.randint(0, len(self.indices) - 1)])])
+            perm = self.indices[random.randint(0, len(self.indices) - 1)]
+            image = Image.fromarray(np.asarray(image)[..., list(perm)])
         return {"image": image, "depth": depth}
 
 
@@ -92,7 +95,7 @@ class ToTensor:
                 "depth": self.to_tensor(sample["depth"]).float()}
 
     def to_tensor(self, pic):
-        if not (_is_pil_image(pic) or _is_numpy_image(pic)):
+        if not (_pil(pic) or _ndarray_image(pic)):
             raise TypeError("pic should be PIL Image or ndarray. Got {}".format(type(pic)))
         if isinstance(pic, np.ndarray):
             return torch.from_numpy(pic.transpose((2, 0, 1))).float().div(255)

@@ -334,7 +334,9 @@ struct WgradCfg {
   static constexpr int RPWG = TH / PW;            // tile rows per wave
   static constexpr int ZERO = CIP * PSX;          // zero pad for n >= NREAL
   static constexpr int STAGE = ZERO + XR * kXW + CO * PSG;
-  static constexpr int RED = PW * MB * NBLK * 256;
+  // PW == 1: each wave owns whole N blocks over all rows -> stores its
+  // accumulators straight to the block partial (no LDS reduction)
+  static constexpr int RED = PW == 1 ? 0 : PW * MB * NBLK * 256;
   static constexpr int SMEM = STAGE > RED ? STAGE : RED;
   static constexpr int M = CO * NP;               // partial elements per block
 };
@@ -416,6 +418,22 @@ __global__ void __launch_bounds__(256, 2)
     }
   }
 
+  float* out = part + (int64_t)blockIdx.x * C::M;
+  if constexpr (PW == 1) {
+    // lane holds co = 16 mb + 4 lk + i, n = 16 nb + li of its N blocks
+#pragma unroll
+    for (int mb = 0; mb < C::MB; ++mb)
+#pragma unroll
+      for (int j = 0; j < C::NBW; ++j) {
+        const int nb = tg + C::TWAYS * j;
+        if (nb < C::NBLK) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            out[(16 * mb + 4 * lk + i) * C::NP + 16 * nb + li] = acc[mb][j][i];
+        }
+      }
+    return;
+  }
   // sum the PW pixel-group partials through LDS, then one block partial:
   // red[pg][mb][nb][co16][n16]; lane holds co16 = 4*lk + i, n16 = li.
   __syncthreads();
@@ -431,7 +449,6 @@ __global__ void __launch_bounds__(256, 2)
       }
     }
   __syncthreads();
-  float* out = part + (int64_t)blockIdx.x * C::M;
   for (int e = tid; e < C::M; e += 256) {
     const int co = e / C::NP, n = e % C::NP;
     const int mb = co / 16, nb = n / 16;

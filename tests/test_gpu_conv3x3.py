@@ -218,3 +218,4 @@ def test_pointwise_bwd_bn_cin64_unsupported():
                   _abi.ptr(v), _abi.ptr(torch.rand((cout, cin), **f)), _abi.ptr(torch.empty_like(x)),
                   _abi.ptr(torch.empty((cout, cin), **f)), _abi.ptr(torch.empty((cin, 2), **f)), n,
                   cin, cout, h, w, _abi.ptr(ws), 0, _abi.stream_of(x))
+

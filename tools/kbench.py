@@ -240,7 +240,8 @@ def _main():
             print(f"{name:44s} {ms * 1e3:9.1f} us {tf:8.1f} TF/s  {tf / 157.3:6.1%}", flush=True)
         tconv = torch.nn.functional.conv2d
         for cin, cout, h, w in ((3, 16, 480, 640), (16, 16, 480, 640), (3, 32, 240, 320),
-                                (32, 32, 240, 320), (3, 64, 120, 160)):
+                                (32, 32, 240, 320), (3, 64, 120, 160), (64, 64, 60, 80),
+                                (64, 64, 120, 160)):
             x = torch.rand(n, cin, h, w, device=dev) - 0.5
             wt = torch.rand(cout, cin, 3, 3, device=dev) - 0.5
             gy = torch.rand(n, cout, h, w, device=dev) - 0.5
@@ -253,9 +254,10 @@ def _main():
             flop = 2.0 * n * h * w * cout * cin * 9
             nb = 4.0 * n * h * w * (cin + cout)
             tag = f"{cin}->{cout} {h}x{w}"
-            report_tf(f"conv3x3 fwd HIP {tag}", timeit(lambda: _abi.call(
-                "mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, cin, cout, h, w, 0, st),
-                a.reps), flop, nb)
+            if _abi.query("mde_conv3x3_supported", cin, cout, 0):
+                report_tf(f"conv3x3 fwd HIP {tag}", timeit(lambda: _abi.call(
+                    "mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, cin, cout, h, w, 0,
+                    st), a.reps), flop, nb)
             report_tf(f"conv3x3 fwd MIOpen {tag}", timeit(lambda: tconv(x, wt, None, 1, 1), a.reps), flop, nb)
             if _abi.query("mde_conv3x3_supported", cin, cout, 1):
                 report_tf(f"conv3x3 dgrad HIP {tag}", timeit(lambda: _abi.call(
@@ -263,9 +265,10 @@ def _main():
                     0, st), a.reps), flop, nb)
                 report_tf(f"conv3x3 dgrad MIOpen {tag}", timeit(
                     lambda: torch.nn.grad.conv2d_input(x.shape, wt, gy, padding=1), a.reps), flop, nb)
-            report_tf(f"conv3x3 wgrad HIP {tag}", timeit(lambda: _abi.call(
-                "mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h, w,
-                _abi.ptr(ws), 0, st), a.reps), flop, nb)
+            if _abi.query("mde_conv3x3_supported", cin, cout, 2):
+                report_tf(f"conv3x3 wgrad HIP {tag}", timeit(lambda: _abi.call(
+                    "mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h,
+                    w, _abi.ptr(ws), 0, st), a.reps), flop, nb)
             report_tf(f"conv3x3 wgrad MIOpen {tag}", timeit(
                 lambda: torch.nn.grad.conv2d_weight(x, wt.shape, gy, padding=1), a.reps), flop, nb)
     if a.json:

@@ -43,8 +43,8 @@ AMP_DTYPE = ("bf16 autocast: convs / GEMMs bf16 (MIOpen / hipBLASLt); BatchNorm 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", choices=("guidedepth", "newcrf", "sam"), default="guidedepth",
                    help="guidedepth = BASELINE cfg2 (the headline line); newcrf = cfg4, "
                         "PTModel (MobileNetV3-L + NewCRF decoder), the swap-in at train.py:36; "
@@ -174,11 +174,21 @@ def main():
         torch.cuda.synchronize()
         log(f"warmup step {i}: {time.perf_counter() - ts:.3f} s")
     barrier()
+    # per-step HIP events on the launch stream (between graph replays: they do
+    # not perturb the step) for the median; `value` is the whole timed region
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] \
+        if world.device.type == "cuda" else None
     t0 = time.perf_counter()
+    if evs:
+        evs[0].record()
     for i in range(args.steps):
         trainer.step(*batches[i % 2])
+        if evs:
+            evs[i + 1].record()
     barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps)) if evs else []
+    median_ms = step_ms[len(step_ms) // 2] if step_ms else None
     # Per-kernel HIP-event timing (the registry brackets every ABI launch on its
     # stream).  Graph mode: the step is captured once more with the events as
     # graph nodes and that graph is replayed `timing_steps` times, so the times
@@ -277,6 +287,7 @@ def main():
         "value": round(images / elapsed, 2), "unit": "images/s", "n_gpus": world.size,
         "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(elapsed * 1e3 / args.steps, 2), "higher_is_better": True,
+        "ms_per_step_median": round(median_ms, 3) if median_ms else None,
         "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32" if args.amp == "fp32" else AMP_DTYPE,
         "data": "synthetic (U[0,1) images, U[0.1,10) depths, resident in HBM), random-init weights",

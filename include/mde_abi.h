@@ -247,6 +247,26 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                       float* gprebias, int64_t n, int64_t c, int64_t h,
                       int64_t w, int act, void* workspace, int dtype,
                       void* stream);
+/* Training forward / coefficients with the statistics emitted by the
+ * producing convolution's epilogue (mde_pointwise_fwd_stats,
+ * mde_conv3x3_fwd_stats): stats = DEVICE fp32 [c][stats_blocks][4] =
+ * (shift, count, sum (x - shift), sum (x - shift)^2) per channel and
+ * producer block of the RAW x, merged here in a fixed order (double) -- the
+ * separate statistics pass over x is skipped.  Otherwise as mde_batchnorm_fwd_train / _fwd_coef (training, fp32
+ * x); workspace = mde_batchnorm_workspace bytes. */
+int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float* beta,
+                                  const float* prebias, float* running_mean, float* running_var,
+                                  int64_t* num_batches_tracked, float momentum, float eps,
+                                  const void* residual, void* y, float* save_mean,
+                                  float* save_invstd, int64_t n, int64_t c, int64_t h, int64_t w,
+                                  int act, const float* stats, int64_t stats_blocks,
+                                  void* workspace, int dtype, void* stream);
+int mde_batchnorm_fwd_coef_stats(const void* x, const float* gamma, const float* beta,
+                                 const float* prebias, float* running_mean, float* running_var,
+                                 int64_t* num_batches_tracked, float momentum, float eps,
+                                 float* scale, float* shift, float* save_mean, float* save_invstd,
+                                 int64_t n, int64_t c, int64_t h, int64_t w, const float* stats,
+                                 int64_t stats_blocks, void* workspace, int dtype, void* stream);
 /* mde_batchnorm_bwd without its reduction pass: `sums` (DEVICE fp32 [c][2])
  * holds sum dy' and sum dy' * (x - mean) over (n,h,w), dy' = dy * act'(...),
  * as computed by a fused producer (mde_pointwise_bwd_bn's in_sums). */
@@ -314,6 +334,15 @@ int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
                       const float* in_shift, const float* weight, void* gx, float* gweight,
                       int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
                       void* workspace, int dtype, void* stream);
+/* mde_pointwise_fwd that also emits the output's per-channel shifted sums
+ * per block -- the following BatchNorm's statistics (stats = DEVICE fp32
+ * [cout][blocks][4] = (shift, count, s1, s2), blocks =
+ * mde_pointwise_stats_blocks(...); 0 = unsupported shape).  Consumed by
+ * mde_batchnorm_fwd_train_stats / _coef_stats. */
+int mde_pointwise_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_pointwise_fwd_stats(const void* x, const float* in_scale, const float* in_shift,
+                            const float* weight, void* y, float* stats, int64_t n, int64_t cin,
+                            int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
 /* mde_pointwise_bwd with the fused BN + ReLU input (in_scale / in_shift
  * required) that ALSO computes that BatchNorm's backward reductions in its
  * epilogue: in_sums (DEVICE fp32 [cin][2]) = sum e, sum e * (x - in_mean[c])
@@ -344,6 +373,14 @@ int mde_pointwise_bwd_bn(const void* gy, const void* x, const float* in_scale,
 int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass);
 int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
                     int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
+/* mde_conv3x3_fwd that also emits y's per-channel shifted sums per block,
+ * the following BatchNorm's statistics (stats = DEVICE fp32
+ * [cout][blocks][4] = (shift, count, s1, s2), blocks =
+ * mde_conv3x3_stats_blocks(...)). */
+int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* stats, int64_t n,
+                          int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                          void* stream);
 int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t n,
                          int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
                          void* stream);

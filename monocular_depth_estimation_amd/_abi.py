@@ -75,6 +75,17 @@ SIGNATURES = {
     "mde_pointwise_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_pointwise_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
                                  _vp, _int, _vp]),
+    "mde_pointwise_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_pointwise_fwd_stats": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                                       _int, _vp]),
+    "mde_conv3x3_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_conv3x3_fwd_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_batchnorm_fwd_train_stats": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp,
+                                             _vp, _vp, _vp, _i64, _i64, _i64, _i64, _int, _vp,
+                                             _i64, _vp, _int, _vp]),
+    "mde_batchnorm_fwd_coef_stats": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp,
+                                            _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _i64, _vp,
+                                            _int, _vp]),
     "mde_pointwise_bwd_bn": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64,
                                     _i64, _i64, _vp, _int, _vp]),
     "mde_batchnorm_fwd_coef": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _int, _vp, _vp,

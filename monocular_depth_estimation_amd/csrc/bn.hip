@@ -566,6 +566,39 @@ int launch_stats(const T* x, int64_t n, int64_t c, int64_t hw, const Geo& g, flo
   return MDE_OK;
 }
 
+// Producer-emitted statistics -> this file's partial format with ONE slice:
+// part[ch * 2] = {sum (x - ref), sum (x - ref)^2}, ref = x[ch, 0] (the shift
+// fwd_channel uses).  Block b's (shift r, count n, s1, s2) contributes
+// s1 + n d and s2 + d (2 s1 + n d), d = r - ref -- plain double sums; the
+// thread-strided order, the wave butterfly and the 4-wave order are fixed:
+// deterministic.
+__global__ void __launch_bounds__(256)
+    bn_stats_merge_kernel(const float* __restrict__ x, const float* __restrict__ stats, int G,
+                          int64_t hw, float* __restrict__ part) {
+  __shared__ double red[2][4];
+  const int64_t ch = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const double ref = (double)x[ch * hw];
+  double s1 = 0.0, s2 = 0.0;
+  for (int b = t; b < G; b += 256) {
+    const float* p = stats + (ch * G + b) * 4;
+    const double n = (double)p[1], d = (double)p[0] - ref, b1 = (double)p[2];
+    s1 += b1 + n * d;
+    s2 += (double)p[3] + d * (2.0 * b1 + n * d);
+  }
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if (lane == 0) {
+    red[0][wv] = s1;
+    red[1][wv] = s2;
+  }
+  __syncthreads();
+  if (t == 0) {
+    part[ch * 2] = (float)((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]));
+    part[ch * 2 + 1] = (float)((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+  }
+}
+
 // Per-channel scale / shift only (the apply is fused into the consumer's
 // operand load): one wave per channel, the same finalisation as the apply
 // kernels, every wave the designated writer of its channel.
@@ -746,6 +779,56 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
                          invstd, s)
              : bwd<float>(gy, x, residual, gx, gresidual, n, c, hw, act, g, P, gamma, beta, mean,
                           invstd, s);
+}
+
+/* Training forward with the statistics emitted by the producing conv's
+ * epilogue (mde_pointwise_fwd_stats / mde_conv3x3_fwd_stats): stats
+ * [c][stats_blocks][4] = (shift, count, s1, s2) of the raw x; no statistics
+ * pass over x.  Everything else as mde_batchnorm_fwd_train (fp32 x only). */
+int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float* beta,
+                                  const float* prebias, float* running_mean, float* running_var,
+                                  int64_t* num_batches_tracked, float momentum, float eps,
+                                  const void* residual, void* y, float* save_mean,
+                                  float* save_invstd, int64_t n, int64_t c, int64_t h, int64_t w,
+                                  int act, const float* stats, int64_t stats_blocks,
+                                  void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || !stats ||
+      stats_blocks <= 0 || stats_blocks > 0x7fffffff || (!running_mean != !running_var) ||
+      act < 0 || act > 2 || !args_ok(n, c, h, w))
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t hw = h * w;
+  float* part = (float*)workspace;
+  MDE_LAUNCH(mde::K_BN_FINAL, 16.0 * (double)c * stats_blocks, s, bn_stats_merge_kernel,
+             dim3((unsigned)c), dim3(256), 0, (const float*)x, stats, (int)stats_blocks, hw, part);
+  FwdArgs A{gamma, beta, prebias, part, 1, n * hw, hw, eps, momentum,
+            running_mean, running_var, num_batches_tracked, save_mean, save_invstd, 1};
+  return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c, hw, act, A, s);
+}
+
+/* mde_batchnorm_fwd_coef (training) with producer-emitted statistics. */
+int mde_batchnorm_fwd_coef_stats(const void* x, const float* gamma, const float* beta,
+                                 const float* prebias, float* running_mean, float* running_var,
+                                 int64_t* num_batches_tracked, float momentum, float eps,
+                                 float* scale, float* shift, float* save_mean, float* save_invstd,
+                                 int64_t n, int64_t c, int64_t h, int64_t w, const float* stats,
+                                 int64_t stats_blocks, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !gamma || !beta || !scale || !shift || !save_mean || !save_invstd || !workspace ||
+      !stats || stats_blocks <= 0 || stats_blocks > 0x7fffffff ||
+      (!running_mean != !running_var) || !args_ok(n, c, h, w))
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t hw = h * w;
+  float* part = (float*)workspace;
+  MDE_LAUNCH(mde::K_BN_FINAL, 16.0 * (double)c * stats_blocks, s, bn_stats_merge_kernel,
+             dim3((unsigned)c), dim3(256), 0, (const float*)x, stats, (int)stats_blocks, hw, part);
+  FwdArgs A{gamma, beta, prebias, part, 1, n * hw, hw, eps, momentum, running_mean, running_var,
+            num_batches_tracked, save_mean, save_invstd, 1};
+  MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c, s, bn_coef_kernel,
+             dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const float*)x, c, A, scale, shift);
+  return MDE_OK;
 }
 
 /* The apply pass alone, with the reduce's sums supplied by the caller (e.g.

@@ -121,4 +121,41 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// Per-channel BatchNorm statistics emitted by a producing conv's epilogue
+// (one (shift, count, s1, s2) per channel and block; mde_batchnorm_*_stats
+// finalises them).  Running shifted sums of one channel's values: the shift
+// `ref` (a sample of the channel, shared by the lanes that will be summed)
+// keeps s2 free of cancellation; three VALU ops per value, no division.
+struct Sh {
+  float ref, n, s1, s2;
+};
+
+__device__ __forceinline__ void sh_add(Sh& a, float v, bool ok) {
+  const float d = ok ? v - a.ref : 0.f;
+  a.s1 += d;
+  a.s2 = fmaf(d, d, a.s2);
+  a.n += ok ? 1.f : 0.f;
+}
+
+// Sum of Sh over lanes sharing `ref` (a butterfly of plain adds over the
+// given xor offsets).
+__device__ __forceinline__ Sh sh_xor_sum(Sh a, int o) {
+  a.n += __shfl_xor(a.n, o, 64);
+  a.s1 += __shfl_xor(a.s1, o, 64);
+  a.s2 += __shfl_xor(a.s2, o, 64);
+  return a;
+}
+
+// a + b re-expressed on a's shift (b's shift differs from a's by O(std): both
+// are samples of the channel, so the float arithmetic keeps its precision)
+__device__ __forceinline__ Sh sh_merge(Sh a, Sh b) {
+  if (b.n == 0.f) return a;
+  if (a.n == 0.f) return b;
+  const float d = b.ref - a.ref;
+  a.s2 += b.s2 + d * (2.f * b.s1 + b.n * d);
+  a.s1 += b.s1 + b.n * d;
+  a.n += b.n;
+  return a;
+}
+
 }  // namespace mde

@@ -202,11 +202,16 @@ __device__ __forceinline__ TileGeo tile_geo(int tile, int th, int tiles_w, int t
 // --------------------------------------------------------------- forward
 // Persistent: block b multiplies tiles b, b + grid, ...; the next tile's
 // input is loaded into registers before the current tile's MFMAs.
-template <int CI, int CO, int RPW, bool FLIP>
+// STATS (forward only): also the output's per-channel shifted sums over
+// this block's tiles -> stats[(co * gridDim.x + block) * 4] = (shift, count,
+// sum (y - shift), sum (y - shift)^2), the following BatchNorm's statistics
+// without re-reading y.
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                        float* __restrict__ y, int h, int w, int tiles_w, int tiles_per_img,
-                       int ntiles) {
+                       int ntiles, float* __restrict__ stats = nullptr) {
+  static_assert(!(STATS && FLIP), "statistics are a forward epilogue");
   constexpr int CIP = cpad4(CI);
   constexpr int TH = 4 * RPW;
   constexpr int XR = TH + 2;
@@ -248,6 +253,10 @@ __global__ void __launch_bounds__(256, 2)
   const float* bw = sw + lk * WS + li;
   const bool vec = (w & 3) == 0;
 
+  mde::Sh run[STATS ? NB : 1];  // output channel 16 nb + li, this lane's pixels
+#pragma unroll
+  for (int nb = 0; nb < (STATS ? NB : 1); ++nb) run[nb] = {0.f, 0.f, 0.f, 0.f};
+  bool first = true;  // wave-uniform: the wave's first tile sets the shifts
   HaloTile<CI, CIP, XR> T;
   const TileWalk tw = tile_walk(ntiles);
   int tile = tw.t0;
@@ -292,6 +301,25 @@ __global__ void __launch_bounds__(256, 2)
       }
     }
 
+    if constexpr (STATS) {
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if (first) {  // one shift per channel and wave: lane (li, lk = 0)'s first output
+          const bool ok0 = g.r0 + wv * RPW < h && g.c0 < w;
+          run[nb].ref = __shfl(ok0 ? acc[0][0][nb][0] : 0.f, li, 64);
+        }
+#pragma unroll
+        for (int q = 0; q < RPW; ++q)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const int row = g.r0 + wv * RPW + q, col = g.c0 + m * 16 + 4 * lk + i;
+              mde::sh_add(run[nb], acc[q][m][nb][i], row < h && col < w);
+            }
+      }
+      first = false;
+    }
     // D layout: lane holds pixels 4*lk + i (i = 0..3) of output channel li.
     float* yi = y + g.img * img_out;
 #pragma unroll
@@ -314,6 +342,38 @@ __global__ void __launch_bounds__(256, 2)
           }
         }
       }
+    }
+  }
+  if constexpr (STATS) {
+    // lanes li, li + 16, +32, +48 share the channel's shift: plain-sum
+    // butterfly over lk, then the 4 waves in order through LDS (sx is free:
+    // every wave is past its last tile's reads once all pass the barrier)
+    __syncthreads();
+    float* part = sx;  // [4][CO][4]
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const mde::Sh a = mde::sh_xor_sum(mde::sh_xor_sum(run[nb], 16), 32);
+      if (lk == 0) {
+        float* p4 = part + (wv * CO + 16 * nb + li) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
+    }
+    __syncthreads();
+    if (tid < CO) {
+      mde::Sh a{part[tid * 4], part[tid * 4 + 1], part[tid * 4 + 2], part[tid * 4 + 3]};
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float* p4 = part + (k * CO + tid) * 4;
+        a = mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      float* o4 = stats + ((int64_t)tid * gridDim.x + blockIdx.x) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
     }
   }
 }
@@ -509,19 +569,28 @@ int resident_blocks() {
   return cached;
 }
 
-template <int CI, int CO, int RPW, bool FLIP>
-int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t h, int64_t w,
-               double bytes, int kid, hipStream_t s) {
-  const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
+int fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_img, int* ntiles) {
   constexpr int TH = 4 * RPW;
-  const int tiles_w = (int)mde::cdiv(w, kTW);
-  const int tiles_per_img = (int)(mde::cdiv(h, TH) * tiles_w);
-  const int64_t ntiles = n * tiles_per_img;
-  if (ntiles > 0x7fffffff) return MDE_ERR_INVALID_ARG;
-  const int res = resident_blocks<conv3x3_fwd_kernel<CI, CO, RPW, FLIP>>();
-  const int grid = ntiles < res ? (int)ntiles : res;
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP>), dim3(grid),
-                  dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img, (int)ntiles);
+  *tiles_w = (int)mde::cdiv(w, kTW);
+  *tiles_per_img = (int)(mde::cdiv(h, TH) * *tiles_w);
+  const int64_t nt = n * *tiles_per_img;
+  if (nt > 0x7fffffff) return 0;
+  *ntiles = (int)nt;
+  const int res = resident_blocks<conv3x3_fwd_kernel<CI, CO, RPW, FLIP, STATS>>();
+  return nt < res ? (int)nt : res;
+}
+
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
+int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t h, int64_t w,
+               double bytes, int kid, hipStream_t s, float* stats = nullptr) {
+  const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
+  int tiles_w, tiles_per_img, ntiles;
+  const int grid = fwd_grid<CI, CO, RPW, FLIP, STATS>(n, h, w, &tiles_w, &tiles_per_img, &ntiles);
+  if (grid <= 0) return MDE_ERR_INVALID_ARG;
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP, STATS>),
+                  dim3(grid), dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img,
+                  ntiles, stats);
   return MDE_OK;
 }
 
@@ -630,6 +699,40 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
   if (cin == 16 && variant() == 1) return launch_fwd<16, 16, 2, false>(in, weight, out, n, h, w, bytes, k, s);
   if (cin == 16) return launch_fwd<16, 16, 1, false>(in, weight, out, n, h, w, bytes, k, s);
   return launch_fwd<32, 32, 1, false>(in, weight, out, n, h, w, bytes, k, s);
+}
+
+// Forward with the BatchNorm statistics epilogue: stats [cout][blocks][4]
+// (shift, count, s1, s2), blocks = mde_conv3x3_stats_blocks(...).
+int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  if (!supported(cin, cout, kFwd) || !dims_ok(n, h, w)) return 0;
+  int a, b, c;
+  if (cin == 3 && cout == 16) return fwd_grid<3, 16, 2, false, true>(n, h, w, &a, &b, &c);
+  if (cin == 3 && cout == 32) return fwd_grid<3, 32, 1, false, true>(n, h, w, &a, &b, &c);
+  if (cin == 3 && cout == 64) return fwd_grid<3, 64, 1, false, true>(n, h, w, &a, &b, &c);
+  if (cin == 16) return fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
+  return fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
+}
+
+int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* stats, int64_t n,
+                          int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                          void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !weight || !y || !stats || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
+  if (!supported(cin, cout, kFwd)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const float* in = (const float*)x;
+  float* out = (float*)y;
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  const int k = mde::K_C3_FWD;
+  if (cin == 3 && cout == 16)
+    return launch_fwd<3, 16, 2, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
+  if (cin == 3 && cout == 32)
+    return launch_fwd<3, 32, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
+  if (cin == 3 && cout == 64)
+    return launch_fwd<3, 64, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
+  if (cin == 16)
+    return launch_fwd<16, 16, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
+  return launch_fwd<32, 32, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
 }
 
 int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,

@@ -486,13 +486,18 @@ __global__ void __launch_bounds__(256, 2)
 // in registers as the A operands for the whole launch.
 // BNR: operand r' = relu(r * isc[c] + ish[c]) (BatchNorm + ReLU of the
 // producer fused into the load, so r' is never written to HBM).
-template <int CI, int CO, bool HAS_D, bool BNR = false>
+// STATS: also the output's per-channel shifted sums over this block's tiles
+// -> stats[(o * gridDim.x + block) * 4] = (shift, count, sum (y - shift),
+// sum (y - shift)^2): the following BatchNorm's statistics without re-reading
+// the output (mde_batchnorm_*_stats).
+template <int CI, int CO, bool HAS_D, bool BNR = false, bool STATS = false>
 __global__ void __launch_bounds__(256)
     skip_fwd_mfma_kernel(const float* __restrict__ r, const float* __restrict__ d,
                          const float* __restrict__ wt, const float* __restrict__ b,
                          float* __restrict__ out, int64_t n, int64_t hw,
                          const float* __restrict__ isc = nullptr,
-                         const float* __restrict__ ish = nullptr) {
+                         const float* __restrict__ ish = nullptr,
+                         float* __restrict__ stats = nullptr) {
   constexpr int OT = (CO + 15) / 16, KC = CI / 4;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
@@ -518,6 +523,12 @@ __global__ void __launch_bounds__(256)
     fsc[kk] = BNR ? isc[4 * kk + q4] : 1.f;
     fsh[kk] = BNR ? ish[4 * kk + q4] : 0.f;
   }
+  mde::Sh run[STATS ? OT : 1][4];  // channel 16 ot + 4 q4 + i, this lane's pixels
+#pragma unroll
+  for (int ot = 0; ot < (STATS ? OT : 1); ++ot)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) run[ot][i] = {0.f, 0.f, 0.f, 0.f};
+  bool first = true;  // wave-uniform: the wave's first tile sets the shifts
   const int tpi = (int)(hw / 64);
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
@@ -560,7 +571,49 @@ __global__ void __launch_bounds__(256)
         if (o < CO)
           *reinterpret_cast<float4*>(op + (int64_t)o * hw) =
               make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+        if constexpr (STATS) {
+          // one shift per channel and wave: lane l16 = 0's first value, so the
+          // 16 lanes of a group sum their (n, s1, s2) plainly at the end
+          if (first) run[ot][i].ref = __shfl(acc[0][i], lane & 48, 64);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mde::sh_add(run[ot][i], acc[j][i], true);
+        }
       }
+    }
+    first = false;
+  }
+  if constexpr (STATS) {
+    // the 16 lanes of a lane group share the channels' shifts: plain-sum
+    // butterfly, then the 4 waves in order through LDS (re-expressed on wave
+    // 0's shift), then one (shift, count, s1, s2) per channel and block
+    __shared__ float part[4][CO][4];
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        mde::Sh a = run[ot][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
+        const int c = 16 * ot + 4 * q4 + i;
+        if (l16 == 0 && c < CO) {
+          part[w][c][0] = a.ref;
+          part[w][c][1] = a.n;
+          part[w][c][2] = a.s1;
+          part[w][c][3] = a.s2;
+        }
+      }
+    __syncthreads();
+    if (threadIdx.x < CO) {
+      const int c = threadIdx.x;
+      mde::Sh a{part[0][c][0], part[0][c][1], part[0][c][2], part[0][c][3]};
+#pragma unroll
+      for (int k = 1; k < 4; ++k)
+        a = mde::sh_merge(a, {part[k][c][0], part[k][c][1], part[k][c][2], part[k][c][3]});
+      float* o4 = stats + ((int64_t)c * gridDim.x + blockIdx.x) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
     }
   }
 }
@@ -729,33 +782,68 @@ size_t mde_pointwise_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, 
   return sizeof(float) * (size_t)bwd_blocks(n, h * w) * (size_t)(cin * cout + cout + 2 * cin);
 }
 
-int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
-                      const float* wt, void* y, int64_t n, int64_t cin, int64_t cout, int64_t h,
-                      int64_t w, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+static int pw_fwd_blocks(int64_t n, int64_t hw, bool stats = false) {
+  // with the statistics epilogue: fewer, longer blocks (the per-block
+  // partials are merged by the BN; ~10 tiles per wave at the cfg2 shapes)
+  const int cap = stats ? 1024 : 4096;
+  const int64_t blocks = mde::cdiv(n * hw / 64, 4);
+  return (int)(blocks > cap ? cap : blocks);
+}
+
+static int pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
+                         const float* wt, void* y, float* stats, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, hipStream_t s) {
   const int64_t hw = h * w;
   if (!x || !wt || !y || (!in_scale != !in_shift)) return MDE_ERR_INVALID_ARG;
   if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
   const double bytes = 4.0 * n * hw * (double)(cin + cout);
-  const int64_t blocks = mde::cdiv(n * hw / 64, 4);
-  const dim3 grid((unsigned)(blocks > 4096 ? 4096 : blocks));
+  const dim3 grid((unsigned)pw_fwd_blocks(n, hw, stats != nullptr));
 #define MDE_PW_FWD(A, B)                                                                     \
   if (cin == A && cout == B) {                                                               \
-    if (in_scale) {                                                                          \
+    if (in_scale && stats) {                                                                 \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, true, true>),   \
+                 grid, dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n,    \
+                 hw, in_scale, in_shift, stats);                                             \
+    } else if (stats) {                                                                      \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, false, true>),  \
+                 grid, dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n,    \
+                 hw, nullptr, nullptr, stats);                                               \
+    } else if (in_scale) {                                                                   \
       MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, true>), grid,   \
                  dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw,      \
-                 in_scale, in_shift);                                                        \
+                 in_scale, in_shift, nullptr);                                               \
     } else {                                                                                 \
       MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false>), grid,         \
                  dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw,      \
-                 nullptr, nullptr);                                                          \
+                 nullptr, nullptr, nullptr);                                                 \
     }                                                                                        \
     return MDE_OK;                                                                           \
   }
   MDE_PW_SHAPES(MDE_PW_FWD)
 #undef MDE_PW_FWD
   return MDE_ERR_UNSUPPORTED;
+}
+
+int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
+                      const float* wt, void* y, int64_t n, int64_t cin, int64_t cout, int64_t h,
+                      int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  return pointwise_fwd(x, in_scale, in_shift, wt, y, nullptr, n, cin, cout, h, w,
+                       (hipStream_t)stream);
+}
+
+int mde_pointwise_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  if (!pw_ok(n, cin, cout, h * w)) return 0;
+  return pw_fwd_blocks(n, h * w, true);
+}
+
+int mde_pointwise_fwd_stats(const void* x, const float* in_scale, const float* in_shift,
+                            const float* wt, void* y, float* stats, int64_t n, int64_t cin,
+                            int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!stats) return MDE_ERR_INVALID_ARG;
+  return pointwise_fwd(x, in_scale, in_shift, wt, y, stats, n, cin, cout, h, w,
+                       (hipStream_t)stream);
 }
 
 }  // extern "C"

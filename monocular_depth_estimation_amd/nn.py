@@ -27,7 +27,7 @@ class _BatchNormAct(torch.autograd.Function):
     @staticmethod
     @_bn_fwd
     def forward(ctx, x, weight, bias, prebias, residual, running_mean, running_var, nbt,
-                training, momentum, eps, act):
+                training, momentum, eps, act, stats=None):
         dt = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
         x = x.to(dt).contiguous()
         residual = residual.to(dt).contiguous() if residual is not None else None
@@ -36,7 +36,15 @@ class _BatchNormAct(torch.autograd.Function):
         mean = torch.empty(c, dtype=torch.float32, device=x.device)
         invstd = torch.empty(c, dtype=torch.float32, device=x.device)
         st = _abi.stream_of(x)
-        if training:
+        if training and stats is not None and dt == torch.float32:
+            # statistics from the producing conv's epilogue: no stats pass over x
+            ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
+            _abi.call("mde_batchnorm_fwd_train_stats", _abi.ptr(x), _abi.ptr(weight),
+                      _abi.ptr(bias), _abi.ptr(prebias), _abi.ptr(running_mean),
+                      _abi.ptr(running_var), _abi.ptr(nbt), float(momentum), float(eps),
+                      _abi.ptr(residual), _abi.ptr(y), _abi.ptr(mean), _abi.ptr(invstd), n, c, h,
+                      w, act, _abi.ptr(stats), stats.shape[1], _abi.ptr(ws), _abi.dtype_code(x), st)
+        elif training:
             ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
             _abi.call("mde_batchnorm_fwd_train", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(bias),
                       _abi.ptr(prebias), _abi.ptr(running_mean), _abi.ptr(running_var),
@@ -73,15 +81,18 @@ class _BatchNormAct(torch.autograd.Function):
                   _abi.stream_of(gy))
         if want_r and not ctx.act:
             gr = gy
-        return gx, gw, gb, gpb, gr, None, None, None, None, None, None, None
+        return gx, gw, gb, gpb, gr, None, None, None, None, None, None, None, None
 
 
-def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, prebias=None):
+def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, prebias=None,
+                   stats=None):
     """act(bn(x + prebias) + residual) with nn.BatchNorm2d semantics (mode by bn.training).
 
     `prebias` is the bias of the convolution feeding this BN, folded in: the
     conv runs without it (no broadcast add, no bias-gradient reduction) and
-    its gradient comes out of the BN backward.
+    its gradient comes out of the BN backward.  `stats` (training only): the
+    per-block shifted sums the producing conv's epilogue emitted for x
+    (conv3x3_stats / bn_relu_pointwise), replacing the statistics pass.
     """
     _gpu(x, residual, prebias)
     if bn.weight is None or bn.bias is None:
@@ -95,7 +106,8 @@ def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, preb
         bn.running_mean if (track or not training) else None,
         bn.running_var if (track or not training) else None,
         bn.num_batches_tracked if track else None,
-        training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, _ACTS[act])
+        training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, _ACTS[act],
+        stats if training else None)
 
 
 class _Pointwise(torch.autograd.Function):
@@ -147,7 +159,7 @@ class _BNReluPointwise(torch.autograd.Function):
     @staticmethod
     @_amp_fwd
     def forward(ctx, y1, gamma, beta, prebias, running_mean, running_var, nbt, training, momentum,
-                eps, w2):
+                eps, w2, stats1=None, want_stats2=False):
         y1 = y1.contiguous()
         n, c, h, w = y1.shape
         cout = w2.shape[0]
@@ -157,21 +169,37 @@ class _BNReluPointwise(torch.autograd.Function):
         mean, invstd = torch.empty(c, **f32), torch.empty(c, **f32)
         st = _abi.stream_of(y1)
         ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), y1) if training else None
-        _abi.call("mde_batchnorm_fwd_coef", _abi.ptr(y1), _abi.ptr(gamma), _abi.ptr(beta),
-                  _abi.ptr(prebias), _abi.ptr(running_mean), _abi.ptr(running_var), _abi.ptr(nbt),
-                  float(momentum), float(eps), int(training), _abi.ptr(scale), _abi.ptr(shift),
-                  _abi.ptr(mean), _abi.ptr(invstd), n, c, h, w, _abi.ptr(ws),
-                  _abi.dtype_code(y1), st)
+        if training and stats1 is not None:  # y1's statistics from the conv3x3 epilogue
+            _abi.call("mde_batchnorm_fwd_coef_stats", _abi.ptr(y1), _abi.ptr(gamma),
+                      _abi.ptr(beta), _abi.ptr(prebias), _abi.ptr(running_mean),
+                      _abi.ptr(running_var), _abi.ptr(nbt), float(momentum), float(eps),
+                      _abi.ptr(scale), _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(invstd), n, c, h,
+                      w, _abi.ptr(stats1), stats1.shape[1], _abi.ptr(ws), _abi.dtype_code(y1), st)
+        else:
+            _abi.call("mde_batchnorm_fwd_coef", _abi.ptr(y1), _abi.ptr(gamma), _abi.ptr(beta),
+                      _abi.ptr(prebias), _abi.ptr(running_mean), _abi.ptr(running_var),
+                      _abi.ptr(nbt), float(momentum), float(eps), int(training), _abi.ptr(scale),
+                      _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(invstd), n, c, h, w, _abi.ptr(ws),
+                      _abi.dtype_code(y1), st)
         y2 = torch.empty((n, cout, h, w), dtype=y1.dtype, device=y1.device)
-        _abi.call("mde_pointwise_fwd", _abi.ptr(y1), _abi.ptr(scale), _abi.ptr(shift),
-                  _abi.ptr(w2m), _abi.ptr(y2), n, c, cout, h, w, _abi.dtype_code(y1), st)
+        if want_stats2:  # y2's statistics for the BatchNorm after this 1x1 conv
+            nb = _abi.query("mde_pointwise_stats_blocks", n, c, cout, h, w)
+            stats2 = torch.empty((cout, nb, 4), **f32)
+            _abi.call("mde_pointwise_fwd_stats", _abi.ptr(y1), _abi.ptr(scale), _abi.ptr(shift),
+                      _abi.ptr(w2m), _abi.ptr(y2), _abi.ptr(stats2), n, c, cout, h, w,
+                      _abi.dtype_code(y1), st)
+        else:
+            stats2 = torch.empty((cout, 0, 4), **f32)
+            _abi.call("mde_pointwise_fwd", _abi.ptr(y1), _abi.ptr(scale), _abi.ptr(shift),
+                      _abi.ptr(w2m), _abi.ptr(y2), n, c, cout, h, w, _abi.dtype_code(y1), st)
         ctx.save_for_backward(y1, gamma, beta, mean, invstd, scale, shift, w2m)
         ctx.training, ctx.has_prebias, ctx.w2shape = bool(training), prebias is not None, w2.shape
-        return y2
+        ctx.mark_non_differentiable(stats2)
+        return y2, stats2
 
     @staticmethod
     @_amp_bwd
-    def backward(ctx, gy2):
+    def backward(ctx, gy2, _gstats2):
         y1, gamma, beta, mean, invstd, scale, shift, w2m = ctx.saved_tensors
         gy2 = gy2.contiguous()
         n, c, h, w = y1.shape
@@ -207,11 +235,17 @@ class _BNReluPointwise(torch.autograd.Function):
                       _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), int(ctx.training),
                       _abi.ptr(gy1_out), None, _abi.ptr(gg), _abi.ptr(gb), _abi.ptr(gpb), n, c,
                       h, w, _ACTS["relu"], _abi.ptr(ws2), _abi.dtype_code(gy2), st)
-        return gy1, gg, gb, gpb, None, None, None, None, None, None, gw2.view(ctx.w2shape)
+        return (gy1, gg, gb, gpb, None, None, None, None, None, None, gw2.view(ctx.w2shape), None,
+                None)
 
 
-def bn_relu_pointwise(y1, bn: nn.BatchNorm2d, prebias, conv: nn.Conv2d):
-    """conv(relu(bn(y1 + prebias))) for a bias-free-folded 1x1 conv on the fused HIP path."""
+def bn_relu_pointwise(y1, bn: nn.BatchNorm2d, prebias, conv: nn.Conv2d, stats1=None,
+                      want_stats2=False):
+    """conv(relu(bn(y1 + prebias))) for a bias-free-folded 1x1 conv on the fused HIP path.
+
+    stats1: y1's per-block statistics from the conv3x3 epilogue (else a
+    statistics pass).  Returns (y2, stats2): stats2 is y2's per-block
+    statistics for the following BatchNorm when want_stats2, else None."""
     _gpu(y1, prebias)
     if bn.weight is None or bn.bias is None:
         raise NotImplementedError("affine=False BatchNorm has no HIP kernel")
@@ -219,12 +253,14 @@ def bn_relu_pointwise(y1, bn: nn.BatchNorm2d, prebias, conv: nn.Conv2d):
     if training and bn.momentum is None:
         raise NotImplementedError("cumulative-average BatchNorm (momentum=None) has no HIP kernel")
     track = bn.training and bn.track_running_stats
-    return _BNReluPointwise.apply(
+    y2, stats2 = _BNReluPointwise.apply(
         y1, bn.weight, bn.bias, prebias,
         bn.running_mean if (track or not training) else None,
         bn.running_var if (track or not training) else None,
         bn.num_batches_tracked if track else None,
-        training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, conv.weight)
+        training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, conv.weight,
+        stats1 if training else None, bool(want_stats2) and y1.dtype == torch.float32)
+    return y2, (stats2 if stats2.shape[1] > 0 else None)
 
 
 def pointwise_ok(conv: nn.Conv2d, x) -> bool:
@@ -252,24 +288,33 @@ CONV3X3_HIP = {
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
     @_amp_fwd
-    def forward(ctx, x, weight, passes):
+    def forward(ctx, x, weight, passes, want_stats=False):
         x = x.contiguous()
         weight = weight.contiguous()
         n, cin, h, w = x.shape
         cout = weight.shape[0]
+        stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
         if passes[0]:
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
-            _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin, cout,
-                      h, w, _abi.dtype_code(x), _abi.stream_of(x))
+            if want_stats:  # + y's per-block BN statistics from the epilogue
+                nb = _abi.query("mde_conv3x3_stats_blocks", n, cin, cout, h, w)
+                stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
+                _abi.call("mde_conv3x3_fwd_stats", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y),
+                          _abi.ptr(stats), n, cin, cout, h, w, _abi.dtype_code(x),
+                          _abi.stream_of(x))
+            else:
+                _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin,
+                          cout, h, w, _abi.dtype_code(x), _abi.stream_of(x))
         else:
             y = torch.nn.functional.conv2d(x, weight, None, 1, 1)
         ctx.save_for_backward(x, weight)
         ctx.passes = passes
-        return y
+        ctx.mark_non_differentiable(stats)
+        return y, stats
 
     @staticmethod
     @_amp_bwd
-    def backward(ctx, gy):
+    def backward(ctx, gy, _gstats):
         x, weight = ctx.saved_tensors
         gy = gy.contiguous()
         n, cin, h, w = x.shape
@@ -291,7 +336,7 @@ class _Conv3x3(torch.autograd.Function):
                           cout, h, w, _abi.ptr(ws), _abi.dtype_code(gy), st)
             else:
                 gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
-        return gx, gw, None
+        return gx, gw, None, None
 
 
 def conv3x3_passes(conv: nn.Conv2d, x):
@@ -315,7 +360,16 @@ def conv3x3_passes(conv: nn.Conv2d, x):
 def conv3x3(x, weight, passes=(True, True, True)):
     """Bias-free 3x3 / stride 1 / padding 1 convolution on the HIP MFMA kernel (per-pass flags)."""
     _gpu(x)
-    return _Conv3x3.apply(x, weight, tuple(passes))
+    return _Conv3x3.apply(x, weight, tuple(passes), False)[0]
+
+
+def conv3x3_stats(x, weight, passes=(True, True, True)):
+    """conv3x3 that also returns y's per-block BN statistics [cout][blocks][4]
+    (shift, count, s1, s2) from the forward epilogue, or None when the forward
+    is not on the HIP kernel (MIOpen)."""
+    _gpu(x)
+    y, stats = _Conv3x3.apply(x, weight, tuple(passes), bool(passes[0]))
+    return y, (stats if stats.shape[1] > 0 else None)
 
 
 def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
@@ -369,13 +423,22 @@ def run_sequential(seq: nn.Sequential, x):
     while i < len(mods):
         m = mods[i]
         if x.is_cuda and _bnrelu_pw_at(mods, i, x.shape):
-            y1 = conv_nobias(m, x)
+            # both BatchNorms take their statistics from the producing conv's
+            # epilogue when that conv runs on a HIP kernel (train mode)
+            want = mods[i + 1].training or not mods[i + 1].track_running_stats
+            passes = conv3x3_passes(m, x)
+            if passes is not None and want:
+                y1, st1 = conv3x3_stats(x, m.weight, passes)
+            else:
+                y1, st1 = conv_nobias(m, x), None
             if pointwise_ok(mods[i + 3], y1):
-                y2 = bn_relu_pointwise(y1, mods[i + 1], m.bias, mods[i + 3])
-                x = batch_norm_act(y2, mods[i + 4], mods[i + 4].act, None, mods[i + 3].bias)
+                b2 = mods[i + 4]
+                y2, st2 = bn_relu_pointwise(y1, mods[i + 1], m.bias, mods[i + 3], st1,
+                                            b2.training or not b2.track_running_stats)
+                x = batch_norm_act(y2, b2, b2.act, None, mods[i + 3].bias, st2)
                 i += 5
                 continue
-            x = batch_norm_act(y1, mods[i + 1], mods[i + 1].act, None, m.bias)
+            x = batch_norm_act(y1, mods[i + 1], mods[i + 1].act, None, m.bias, st1)
             i += 2
             continue
         if (isinstance(m, nn.Conv2d) and m.bias is not None and i + 1 < len(mods)

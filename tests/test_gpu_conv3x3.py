@@ -219,3 +219,59 @@ def test_pointwise_bwd_bn_cin64_unsupported():
                   _abi.ptr(torch.empty((cout, cin), **f)), _abi.ptr(torch.empty((cin, 2), **f)), n,
                   cin, cout, h, w, _abi.ptr(ws), 0, _abi.stream_of(x))
 
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w,off", [(16, 16, 4, 120, 160, 0.0), (3, 32, 3, 37, 70, 0.0),
+                                                (16, 16, 2, 30, 64, 100.0), (3, 64, 2, 16, 48, 5.0)])
+def test_bn_statistics_from_conv_epilogue(cin, cout, n, h, w, off):
+    """BatchNorm (train) fed the conv3x3 forward epilogue's per-block shifted
+    sums == the same BatchNorm with its own statistics pass: output,
+    running mean / var, saved statistics (through the backward) -- also when
+    |mean| >> std (input offset)."""
+    import copy
+
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, batch_norm_act, conv3x3_stats
+    g = torch.Generator().manual_seed(cin + cout + h)
+    x = (torch.rand((n, cin, h, w), generator=g) - 0.5 + off).to(DEV)
+    wt = ((torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.3).to(DEV)
+    y, st = conv3x3_stats(x, wt)
+    assert st is not None and st.shape[0] == cout
+    assert float(st[:, :, 1].sum()) == n * h * w * cout  # every output counted once
+    bn = BatchNorm2d(cout, act="relu").to(DEV).train()
+    bn2 = copy.deepcopy(bn)
+    ya = batch_norm_act(y.detach().requires_grad_(True), bn, "relu", None, None, st)
+    yb = batch_norm_act(y.detach().requires_grad_(True), bn2, "relu")
+    # both fp32 paths against float64 batch statistics of the same y: the
+    # epilogue statistics may not be worse than the statistics pass (2x +
+    # floor; with |mean| >> std both carry the mean's fp32 rounding)
+    y64 = y.double()
+    m64 = y64.mean(dim=(0, 2, 3), keepdim=True)
+    v64 = y64.var(dim=(0, 2, 3), unbiased=False, keepdim=True)
+    ref = torch.relu((y64 - m64) / torch.sqrt(v64 + bn.eps) * bn.weight.double().view(1, -1, 1, 1)
+                     + bn.bias.double().view(1, -1, 1, 1))
+    ea, eb = rel_err(ya, ref), rel_err(yb, ref)
+    assert ea <= max(2.0 * eb, 1e-6), (ea, eb)
+    scale = float((y64 - m64).abs().max())  # means ~0 here: compare on y's centred scale
+    assert float((bn.running_mean - bn2.running_mean).abs().max()) <= 1e-6 * max(scale, 1.0)
+    assert rel_err(bn.running_var, bn2.running_var) <= 2e-5
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 4, 96, 128), (64, 32, 2, 60, 80), (32, 16, 3, 8, 64)])
+def test_bn_statistics_from_pointwise_epilogue(cin, cout, n, h, w):
+    """The BN-ReLU-fed 1x1 conv's forward epilogue statistics for the next
+    BatchNorm == that BatchNorm's own statistics pass."""
+    import copy
+
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, batch_norm_act, bn_relu_pointwise
+    g = torch.Generator().manual_seed(cin * cout + h)
+    y1 = (torch.rand((n, cin, h, w), generator=g) * 2 - 0.7).to(DEV)
+    bn1 = BatchNorm2d(cin, act="relu").to(DEV).train()
+    conv = torch.nn.Conv2d(cin, cout, 1).to(DEV)
+    y2, st2 = bn_relu_pointwise(y1, bn1, None, conv, None, True)
+    assert st2 is not None and float(st2[:, :, 1].sum()) == n * h * w * cout
+    bn2 = BatchNorm2d(cout, act="relu").to(DEV).train()
+    bn3 = copy.deepcopy(bn2)
+    za = batch_norm_act(y2.detach(), bn2, "relu", None, None, st2)
+    zb = batch_norm_act(y2.detach(), bn3, "relu")
+    assert rel_err(za, zb) <= 2e-6
+    assert rel_err(bn2.running_var, bn3.running_var) <= 2e-5

@@ -67,33 +67,11 @@ __device__ __forceinline__ float act_fn(float v, int act) {
   return v;
 }
 
-// Storage types of the activations / gradients: fp32, or bf16 (raw uint16,
-// round-to-nearest-even like torch) under autocast.  Statistics, coefficients
-// and accumulation are fp32 / fp64 either way.
-using bf16 = uint16_t;
-__device__ __forceinline__ float bf2f(bf16 b) { return __uint_as_float((uint32_t)b << 16); }
-__device__ __forceinline__ bf16 f2bf(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16)((u >> 16) | 0x40);  // quiet NaN
-  return (bf16)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
-__device__ __forceinline__ float ld1(const float* p) { return *p; }
-__device__ __forceinline__ float ld1(const bf16* p) { return bf2f(*p); }
-__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
-__device__ __forceinline__ void st1(bf16* p, float v) { *p = f2bf(v); }
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ float4 ld4(const bf16* p) {
-  const uint2 u = *reinterpret_cast<const uint2*>(p);
-  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-}
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-__device__ __forceinline__ void st4(bf16* p, float4 v) {
-  uint2 u;
-  u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
-  u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
-  *reinterpret_cast<uint2*>(p) = u;
-}
+using mde::bf16;
+using mde::ld1;
+using mde::ld4;
+using mde::st1;
+using mde::st4;
 
 __device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
@@ -572,13 +550,14 @@ int launch_stats(const T* x, int64_t n, int64_t c, int64_t hw, const Geo& g, flo
 // s1 + n d and s2 + d (2 s1 + n d), d = r - ref -- plain double sums; the
 // thread-strided order, the wave butterfly and the 4-wave order are fixed:
 // deterministic.
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bn_stats_merge_kernel(const float* __restrict__ x, const float* __restrict__ stats, int G,
+    bn_stats_merge_kernel(const T* __restrict__ x, const float* __restrict__ stats, int G,
                           int64_t hw, float* __restrict__ part) {
   __shared__ double red[2][4];
   const int64_t ch = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-  const double ref = (double)x[ch * hw];
+  const double ref = (double)ld1(x + ch * hw);
   double s1 = 0.0, s2 = 0.0;
   for (int b = t; b < G; b += 256) {
     const float* p = stats + (ch * G + b) * 4;
@@ -602,8 +581,9 @@ __global__ void __launch_bounds__(256)
 // Per-channel scale / shift only (the apply is fused into the consumer's
 // operand load): one wave per channel, the same finalisation as the apply
 // kernels, every wave the designated writer of its channel.
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bn_coef_kernel(const float* __restrict__ x, int64_t c, FwdArgs A,
+    bn_coef_kernel(const T* __restrict__ x, int64_t c, FwdArgs A,
                    float* __restrict__ scale, float* __restrict__ shift) {
   const int64_t ch = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (ch >= c) return;  // whole waves
@@ -737,7 +717,7 @@ int mde_batchnorm_fwd_coef(const void* x, const float* gamma, const float* beta,
                            int training, float* scale, float* shift, float* save_mean,
                            float* save_invstd, int64_t n, int64_t c, int64_t h, int64_t w,
                            void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !scale || !shift || !save_mean || !save_invstd ||
       (!running_mean != !running_var) || !args_ok(n, c, h, w) ||
       (training && !workspace) || (!training && !running_mean))
@@ -747,14 +727,21 @@ int mde_batchnorm_fwd_coef(const void* x, const float* gamma, const float* beta,
   const Geo g = geometry(n, c, hw);
   float* part = (float*)workspace;
   if (training) {
-    const int st = launch_stats((const float*)x, n, c, hw, g, part, s);
+    const int st = dtype == MDE_BF16 ? launch_stats((const bf16*)x, n, c, hw, g, part, s)
+                                     : launch_stats((const float*)x, n, c, hw, g, part, s);
     if (st) return st;
   }
   FwdArgs A{gamma, beta, prebias, training ? part : nullptr, training ? g.slices : 0,
             g.total, hw, eps, momentum, running_mean, running_var,
             training ? num_batches_tracked : nullptr, save_mean, save_invstd, training ? 1 : 0};
-  MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c * (training ? g.slices : 1), s, bn_coef_kernel,
-             dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const float*)x, c, A, scale, shift);
+  if (dtype == MDE_BF16)
+    MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c * (training ? g.slices : 1), s,
+               bn_coef_kernel<bf16>, dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0,
+               (const bf16*)x, c, A, scale, shift);
+  else
+    MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c * (training ? g.slices : 1), s,
+               bn_coef_kernel<float>, dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0,
+               (const float*)x, c, A, scale, shift);
   return MDE_OK;
 }
 
@@ -792,7 +779,7 @@ int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float
                                   float* save_invstd, int64_t n, int64_t c, int64_t h, int64_t w,
                                   int act, const float* stats, int64_t stats_blocks,
                                   void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !y || !save_mean || !save_invstd || !workspace || !stats ||
       stats_blocks <= 0 || stats_blocks > 0x7fffffff || (!running_mean != !running_var) ||
       act < 0 || act > 2 || !args_ok(n, c, h, w))
@@ -800,10 +787,17 @@ int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
   float* part = (float*)workspace;
-  MDE_LAUNCH(mde::K_BN_FINAL, 16.0 * (double)c * stats_blocks, s, bn_stats_merge_kernel,
-             dim3((unsigned)c), dim3(256), 0, (const float*)x, stats, (int)stats_blocks, hw, part);
+  const double mb = 16.0 * (double)c * stats_blocks;
+  if (dtype == MDE_BF16)
+    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<bf16>, dim3((unsigned)c), dim3(256),
+               0, (const bf16*)x, stats, (int)stats_blocks, hw, part);
+  else
+    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<float>, dim3((unsigned)c), dim3(256),
+               0, (const float*)x, stats, (int)stats_blocks, hw, part);
   FwdArgs A{gamma, beta, prebias, part, 1, n * hw, hw, eps, momentum,
             running_mean, running_var, num_batches_tracked, save_mean, save_invstd, 1};
+  if (dtype == MDE_BF16)
+    return launch_fwd_apply((const bf16*)x, (const bf16*)residual, (bf16*)y, n, c, hw, act, A, s);
   return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c, hw, act, A, s);
 }
 
@@ -814,7 +808,7 @@ int mde_batchnorm_fwd_coef_stats(const void* x, const float* gamma, const float*
                                  float* scale, float* shift, float* save_mean, float* save_invstd,
                                  int64_t n, int64_t c, int64_t h, int64_t w, const float* stats,
                                  int64_t stats_blocks, void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!x || !gamma || !beta || !scale || !shift || !save_mean || !save_invstd || !workspace ||
       !stats || stats_blocks <= 0 || stats_blocks > 0x7fffffff ||
       (!running_mean != !running_var) || !args_ok(n, c, h, w))
@@ -822,12 +816,20 @@ int mde_batchnorm_fwd_coef_stats(const void* x, const float* gamma, const float*
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
   float* part = (float*)workspace;
-  MDE_LAUNCH(mde::K_BN_FINAL, 16.0 * (double)c * stats_blocks, s, bn_stats_merge_kernel,
-             dim3((unsigned)c), dim3(256), 0, (const float*)x, stats, (int)stats_blocks, hw, part);
+  const double mb = 16.0 * (double)c * stats_blocks;
   FwdArgs A{gamma, beta, prebias, part, 1, n * hw, hw, eps, momentum, running_mean, running_var,
             num_batches_tracked, save_mean, save_invstd, 1};
-  MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c, s, bn_coef_kernel,
-             dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const float*)x, c, A, scale, shift);
+  if (dtype == MDE_BF16) {
+    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<bf16>, dim3((unsigned)c), dim3(256),
+               0, (const bf16*)x, stats, (int)stats_blocks, hw, part);
+    MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c, s, bn_coef_kernel<bf16>,
+               dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const bf16*)x, c, A, scale, shift);
+  } else {
+    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<float>, dim3((unsigned)c), dim3(256),
+               0, (const float*)x, stats, (int)stats_blocks, hw, part);
+    MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c, s, bn_coef_kernel<float>,
+               dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const float*)x, c, A, scale, shift);
+  }
   return MDE_OK;
 }
 

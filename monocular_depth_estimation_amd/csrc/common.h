@@ -121,6 +121,34 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return (red[0] + red[1]) + (red[2] + red[3]);
 }
 
+// Storage types of the activations / gradients: fp32, or bf16 (raw uint16,
+// round-to-nearest-even like torch) under autocast.  Statistics, coefficients
+// and accumulation are fp32 / fp64 either way.
+using bf16 = uint16_t;
+__device__ __forceinline__ float bf2f(bf16 b) { return __uint_as_float((uint32_t)b << 16); }
+__device__ __forceinline__ bf16 f2bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (bf16)((u >> 16) | 0x40);  // quiet NaN
+  return (bf16)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16* p) { return bf2f(*p); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16* p, float v) { *p = f2bf(v); }
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ float4 ld4(const bf16* p) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ void st4(bf16* p, float4 v) {
+  uint2 u;
+  u.x = (uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16);
+  u.y = (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16);
+  *reinterpret_cast<uint2*>(p) = u;
+}
+
 // Per-channel BatchNorm statistics emitted by a producing conv's epilogue
 // (one (shift, count, s1, s2) per channel and block; mde_batchnorm_*_stats
 // finalises them).  Running shifted sums of one channel's values: the shift

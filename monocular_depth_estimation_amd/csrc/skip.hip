@@ -279,11 +279,13 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 // registers and r re-read in the gs layout (the same tile the gW part reads,
 // an L1 / L2 hit) -- appended to the block's slab row, so the separate BN
 // reduce pass over (gs, r) is never run.
-template <int CI, int CO, bool HAS_D, bool BNR = false, bool BNS = false>
+// T: storage type of g, r, d, gs (float, or bf16 under autocast; products
+// and sums in fp32 either way).
+template <int CI, int CO, bool HAS_D, bool BNR = false, bool BNS = false, typename T = float>
 __global__ void __launch_bounds__(256, 2)
-    skip_bwd_mfma_kernel(const float* __restrict__ g, const float* __restrict__ r,
-                         const float* __restrict__ d, const float* __restrict__ wt,
-                         float* __restrict__ gs, float* __restrict__ slab, int64_t n,
+    skip_bwd_mfma_kernel(const T* __restrict__ g, const T* __restrict__ r,
+                         const T* __restrict__ d, const float* __restrict__ wt,
+                         T* __restrict__ gs, float* __restrict__ slab, int64_t n,
                          int64_t hw, const float* __restrict__ isc = nullptr,
                          const float* __restrict__ ish = nullptr,
                          const float* __restrict__ imean = nullptr) {
@@ -336,10 +338,10 @@ __global__ void __launch_bounds__(256, 2)
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
-    const float* gp = g + nidx * CO * hw + p0;
-    const float* rp = r + nidx * CI * hw + p0;
-    const float* dp = HAS_D ? d + nidx * CI * hw + p0 : nullptr;
-    float* sp = gs ? gs + nidx * CI * hw + p0 : nullptr;
+    const T* gp = g + nidx * CO * hw + p0;
+    const T* rp = r + nidx * CI * hw + p0;
+    const T* dp = HAS_D ? d + nidx * CI * hw + p0 : nullptr;
+    T* sp = gs ? gs + nidx * CI * hw + p0 : nullptr;
     // gs = W^T G with the forward's permuted pixel order: lane (l16, q4) loads
     // pixels 4*l16 .. 4*l16+3 of G row 4kk + q4 as one float4, component j
     // feeds sub-tile j, and each gs row leaves as one float4 per lane (full
@@ -348,7 +350,7 @@ __global__ void __launch_bounds__(256, 2)
       float4 gb[KO];
 #pragma unroll
       for (int kk = 0; kk < KO; ++kk)
-        gb[kk] = *reinterpret_cast<const float4*>(gp + (4 * kk + q4) * hw + 4 * l16);
+        gb[kk] = mde::ld4(gp + (4 * kk + q4) * hw + 4 * l16);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         f4 acc[4];
@@ -363,13 +365,12 @@ __global__ void __launch_bounds__(256, 2)
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          *reinterpret_cast<float4*>(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16) =
-              make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+          mde::st4(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16,
+                   make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
         if constexpr (BNS) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float4 x =
-                *reinterpret_cast<const float4*>(rp + (16 * mt + 4 * q4 + i) * hw + 4 * l16);
+            const float4 x = mde::ld4(rp + (16 * mt + 4 * q4 + i) * hw + 4 * l16);
             const float xv[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -397,10 +398,10 @@ __global__ void __launch_bounds__(256, 2)
         if (o < CO) {
           // pixels 16v + 4q4 .. +3: the 4 lane groups of a row read 64
           // contiguous bytes per instruction (same order for S below)
-          const float4* src = reinterpret_cast<const float4*>(gp + o * hw + 4 * q4);
+          const T* src = gp + o * hw + 4 * q4;
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            const float4 x = src[4 * v];
+            const float4 x = mde::ld4(src + 16 * v);
             ga[oo][4 * v] = x.x; ga[oo][4 * v + 1] = x.y;
             ga[oo][4 * v + 2] = x.z; ga[oo][4 * v + 3] = x.w;
             gbp[ot] += (x.x + x.y) + (x.z + x.w);
@@ -412,13 +413,13 @@ __global__ void __launch_bounds__(256, 2)
       }
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
-        const float4* ra = reinterpret_cast<const float4*>(rp + (16 * mt + l16) * hw + 4 * q4);
+        const T* ra = rp + (16 * mt + l16) * hw + 4 * q4;
         float sb[16];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-          float4 x = ra[4 * v];
+          float4 x = mde::ld4(ra + 16 * v);
           if (HAS_D) {
-            const float4 y = reinterpret_cast<const float4*>(dp + (16 * mt + l16) * hw + 4 * q4)[4 * v];
+            const float4 y = mde::ld4(dp + (16 * mt + l16) * hw + 4 * q4 + 16 * v);
             x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
           }
           if (BNR) {
@@ -490,11 +491,12 @@ __global__ void __launch_bounds__(256, 2)
 // -> stats[(o * gridDim.x + block) * 4] = (shift, count, sum (y - shift),
 // sum (y - shift)^2): the following BatchNorm's statistics without re-reading
 // the output (mde_batchnorm_*_stats).
-template <int CI, int CO, bool HAS_D, bool BNR = false, bool STATS = false>
+// T: storage type of r, d, out (float, or bf16 under autocast).
+template <int CI, int CO, bool HAS_D, bool BNR = false, bool STATS = false, typename T = float>
 __global__ void __launch_bounds__(256)
-    skip_fwd_mfma_kernel(const float* __restrict__ r, const float* __restrict__ d,
+    skip_fwd_mfma_kernel(const T* __restrict__ r, const T* __restrict__ d,
                          const float* __restrict__ wt, const float* __restrict__ b,
-                         float* __restrict__ out, int64_t n, int64_t hw,
+                         T* __restrict__ out, int64_t n, int64_t hw,
                          const float* __restrict__ isc = nullptr,
                          const float* __restrict__ ish = nullptr,
                          float* __restrict__ stats = nullptr) {
@@ -533,16 +535,16 @@ __global__ void __launch_bounds__(256)
   const int64_t tiles = n * tpi;
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
-    const float* rp = r + nidx * CI * hw + p0 + 4 * l16;
-    const float* dp = HAS_D ? d + nidx * CI * hw + p0 + 4 * l16 : nullptr;
-    float* op = out + nidx * CO * hw + p0 + 4 * l16;
+    const T* rp = r + nidx * CI * hw + p0 + 4 * l16;
+    const T* dp = HAS_D ? d + nidx * CI * hw + p0 + 4 * l16 : nullptr;
+    T* op = out + nidx * CO * hw + p0 + 4 * l16;
     float4 sb[KC];
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       const int64_t off = (int64_t)(4 * kk + q4) * hw;
-      float4 v = *reinterpret_cast<const float4*>(rp + off);
+      float4 v = mde::ld4(rp + off);
       if (HAS_D) {
-        const float4 e = *reinterpret_cast<const float4*>(dp + off);
+        const float4 e = mde::ld4(dp + off);
         v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
       }
       if (BNR) {
@@ -569,14 +571,18 @@ __global__ void __launch_bounds__(256)
       for (int i = 0; i < 4; ++i) {
         const int o = 16 * ot + 4 * q4 + i;
         if (o < CO)
-          *reinterpret_cast<float4*>(op + (int64_t)o * hw) =
-              make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]);
+          mde::st4(op + (int64_t)o * hw, make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
         if constexpr (STATS) {
+          // statistics of the values as stored (bf16-rounded under autocast)
+          float vs[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            vs[j] = sizeof(T) == 2 ? mde::bf2f(mde::f2bf(acc[j][i])) : acc[j][i];
           // one shift per channel and wave: lane l16 = 0's first value, so the
           // 16 lanes of a group sum their (n, s1, s2) plainly at the end
-          if (first) run[ot][i].ref = __shfl(acc[0][i], lane & 48, 64);
+          if (first) run[ot][i].ref = __shfl(vs[0], lane & 48, 64);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) mde::sh_add(run[ot][i], acc[j][i], true);
+          for (int j = 0; j < 4; ++j) mde::sh_add(run[ot][i], vs[j], true);
         }
       }
     }
@@ -790,32 +796,37 @@ static int pw_fwd_blocks(int64_t n, int64_t hw, bool stats = false) {
   return (int)(blocks > cap ? cap : blocks);
 }
 
+}  // extern "C"
+
+template <typename T>
 static int pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
                          const float* wt, void* y, float* stats, int64_t n, int64_t cin,
                          int64_t cout, int64_t h, int64_t w, hipStream_t s) {
   const int64_t hw = h * w;
   if (!x || !wt || !y || (!in_scale != !in_shift)) return MDE_ERR_INVALID_ARG;
   if (!pw_ok(n, cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
-  const double bytes = 4.0 * n * hw * (double)(cin + cout);
+  const double bytes = (double)sizeof(T) * n * hw * (double)(cin + cout);
   const dim3 grid((unsigned)pw_fwd_blocks(n, hw, stats != nullptr));
+  const T* xi = (const T*)x;
+  T* yo = (T*)y;
 #define MDE_PW_FWD(A, B)                                                                     \
   if (cin == A && cout == B) {                                                               \
     if (in_scale && stats) {                                                                 \
-      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, true, true>),   \
-                 grid, dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n,    \
-                 hw, in_scale, in_shift, stats);                                             \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, true, true, T>), \
+                 grid, dim3(256), 0, xi, nullptr, wt, nullptr, yo, n, hw, in_scale,          \
+                 in_shift, stats);                                                           \
     } else if (stats) {                                                                      \
-      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, false, true>),  \
-                 grid, dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n,    \
-                 hw, nullptr, nullptr, stats);                                               \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s,                                                    \
+                 (skip_fwd_mfma_kernel<A, B, false, false, true, T>), grid, dim3(256), 0,    \
+                 xi, nullptr, wt, nullptr, yo, n, hw, nullptr, nullptr, stats);              \
     } else if (in_scale) {                                                                   \
-      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false, true>), grid,   \
-                 dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw,      \
-                 in_scale, in_shift, nullptr);                                               \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s,                                                    \
+                 (skip_fwd_mfma_kernel<A, B, false, true, false, T>), grid, dim3(256), 0,    \
+                 xi, nullptr, wt, nullptr, yo, n, hw, in_scale, in_shift, nullptr);          \
     } else {                                                                                 \
-      MDE_LAUNCH(mde::K_PW_FWD, bytes, s, (skip_fwd_mfma_kernel<A, B, false>), grid,         \
-                 dim3(256), 0, (const float*)x, nullptr, wt, nullptr, (float*)y, n, hw,      \
-                 nullptr, nullptr, nullptr);                                                 \
+      MDE_LAUNCH(mde::K_PW_FWD, bytes, s,                                                    \
+                 (skip_fwd_mfma_kernel<A, B, false, false, false, T>), grid, dim3(256), 0,   \
+                 xi, nullptr, wt, nullptr, yo, n, hw, nullptr, nullptr, nullptr);            \
     }                                                                                        \
     return MDE_OK;                                                                           \
   }
@@ -824,12 +835,19 @@ static int pointwise_fwd(const void* x, const float* in_scale, const float* in_s
   return MDE_ERR_UNSUPPORTED;
 }
 
+static bool pw_dtype_ok(int dtype) { return dtype == MDE_F32 || dtype == MDE_BF16; }
+
+extern "C" {
+
 int mde_pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
                       const float* wt, void* y, int64_t n, int64_t cin, int64_t cout, int64_t h,
                       int64_t w, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
-  return pointwise_fwd(x, in_scale, in_shift, wt, y, nullptr, n, cin, cout, h, w,
-                       (hipStream_t)stream);
+  if (!pw_dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
+  return dtype == MDE_BF16
+             ? pointwise_fwd<mde::bf16>(x, in_scale, in_shift, wt, y, nullptr, n, cin, cout, h, w,
+                                        (hipStream_t)stream)
+             : pointwise_fwd<float>(x, in_scale, in_shift, wt, y, nullptr, n, cin, cout, h, w,
+                                    (hipStream_t)stream);
 }
 
 int mde_pointwise_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
@@ -840,10 +858,13 @@ int mde_pointwise_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, 
 int mde_pointwise_fwd_stats(const void* x, const float* in_scale, const float* in_shift,
                             const float* wt, void* y, float* stats, int64_t n, int64_t cin,
                             int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!pw_dtype_ok(dtype)) return MDE_ERR_UNSUPPORTED;
   if (!stats) return MDE_ERR_INVALID_ARG;
-  return pointwise_fwd(x, in_scale, in_shift, wt, y, stats, n, cin, cout, h, w,
-                       (hipStream_t)stream);
+  return dtype == MDE_BF16
+             ? pointwise_fwd<mde::bf16>(x, in_scale, in_shift, wt, y, stats, n, cin, cout, h, w,
+                                        (hipStream_t)stream)
+             : pointwise_fwd<float>(x, in_scale, in_shift, wt, y, stats, n, cin, cout, h, w,
+                                    (hipStream_t)stream);
 }
 
 }  // extern "C"
@@ -852,6 +873,7 @@ namespace {
 
 // Pointwise backward; in_mean / in_sums non-null (with in_scale): also the
 // producer BatchNorm's backward sums (BNS epilogue), in_sums [cin][2].
+template <typename T>
 int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const float* in_shift,
                   const float* in_mean, const float* wt, void* gx, float* gw, float* in_sums,
                   int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, void* workspace,
@@ -865,22 +887,25 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
   if (sums && cin > 32) return MDE_ERR_UNSUPPORTED;
   const int nb = bwd_blocks(n, hw);
   float* slab = (float*)workspace;
-  const double bytes = 4.0 * n * hw * (double)(cout + cin + (gx ? cin : 0));
+  const double bytes = (double)sizeof(T) * n * hw * (double)(cout + cin + (gx ? cin : 0));
+  const T* gi = (const T*)gy;
+  const T* xi = (const T*)x;
+  T* go = (T*)gx;
 #define MDE_PW_BWD(A, B)                                                                     \
   if (cin == A && cout == B) {                                                               \
     if (sums) {                                                                              \
       if constexpr (A <= 32)                                                                 \
-        MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false, true, true>), \
-                   dim3(nb), dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt,   \
-                   (float*)gx, slab, n, hw, in_scale, in_shift, in_mean);                    \
+        MDE_LAUNCH(mde::K_PW_BWD, bytes, s,                                                  \
+                   (skip_bwd_mfma_kernel<A, B, false, true, true, T>), dim3(nb), dim3(256),  \
+                   0, gi, xi, nullptr, wt, go, slab, n, hw, in_scale, in_shift, in_mean);    \
     } else if (in_scale) {                                                                   \
-      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false, true>),         \
-                 dim3(nb), dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt,     \
-                 (float*)gx, slab, n, hw, in_scale, in_shift, nullptr);                      \
+      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false, true, false, T>), \
+                 dim3(nb), dim3(256), 0, gi, xi, nullptr, wt, go, slab, n, hw, in_scale,     \
+                 in_shift, nullptr);                                                         \
     } else {                                                                                 \
-      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (skip_bwd_mfma_kernel<A, B, false>), dim3(nb),     \
-                 dim3(256), 0, (const float*)gy, (const float*)x, nullptr, wt, (float*)gx,   \
-                 slab, n, hw, nullptr, nullptr, nullptr);                                    \
+      MDE_LAUNCH(mde::K_PW_BWD, bytes, s,                                                    \
+                 (skip_bwd_mfma_kernel<A, B, false, false, false, T>), dim3(nb), dim3(256),  \
+                 0, gi, xi, nullptr, wt, go, slab, n, hw, nullptr, nullptr, nullptr);        \
     }                                                                                        \
   }
   MDE_PW_SHAPES(MDE_PW_BWD)
@@ -907,19 +932,25 @@ int mde_pointwise_bwd(const void* gy, const void* x, const float* in_scale,
                       const float* in_shift, const float* wt, void* gx, float* gw, int64_t n,
                       int64_t cin, int64_t cout, int64_t h, int64_t w, void* workspace,
                       int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
-  return pointwise_bwd(gy, x, in_scale, in_shift, nullptr, wt, gx, gw, nullptr, n, cin, cout, h,
-                       w, workspace, (hipStream_t)stream);
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
+  return dtype == MDE_BF16
+             ? pointwise_bwd<mde::bf16>(gy, x, in_scale, in_shift, nullptr, wt, gx, gw, nullptr, n,
+                                        cin, cout, h, w, workspace, (hipStream_t)stream)
+             : pointwise_bwd<float>(gy, x, in_scale, in_shift, nullptr, wt, gx, gw, nullptr, n,
+                                    cin, cout, h, w, workspace, (hipStream_t)stream);
 }
 
 int mde_pointwise_bwd_bn(const void* gy, const void* x, const float* in_scale,
                          const float* in_shift, const float* in_mean, const float* wt, void* gx,
                          float* gw, float* in_sums, int64_t n, int64_t cin, int64_t cout,
                          int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   if (!in_scale || !in_shift || !in_mean || !gx || !in_sums) return MDE_ERR_INVALID_ARG;
-  return pointwise_bwd(gy, x, in_scale, in_shift, in_mean, wt, gx, gw, in_sums, n, cin, cout, h,
-                       w, workspace, (hipStream_t)stream);
+  return dtype == MDE_BF16
+             ? pointwise_bwd<mde::bf16>(gy, x, in_scale, in_shift, in_mean, wt, gx, gw, in_sums,
+                                        n, cin, cout, h, w, workspace, (hipStream_t)stream)
+             : pointwise_bwd<float>(gy, x, in_scale, in_shift, in_mean, wt, gx, gw, in_sums, n,
+                                    cin, cout, h, w, workspace, (hipStream_t)stream);
 }
 
 }  // extern "C"

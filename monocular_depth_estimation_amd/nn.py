@@ -36,7 +36,7 @@ class _BatchNormAct(torch.autograd.Function):
         mean = torch.empty(c, dtype=torch.float32, device=x.device)
         invstd = torch.empty(c, dtype=torch.float32, device=x.device)
         st = _abi.stream_of(x)
-        if training and stats is not None and dt == torch.float32:
+        if training and stats is not None:
             # statistics from the producing conv's epilogue: no stats pass over x
             ws = _ws(_abi.query("mde_batchnorm_workspace", n, c, h, w), x)
             _abi.call("mde_batchnorm_fwd_train_stats", _abi.ptr(x), _abi.ptr(weight),
@@ -154,13 +154,16 @@ class _BNReluPointwise(torch.autograd.Function):
     operand load: relu(bn(y1)) is never written.  Backward: the 1x1 conv's
     backward recomputes that operand for its weight gradient and returns the
     gradient w.r.t. it; the BN backward (ReLU mask recomputed from y1) turns
-    that into d/dy1 and the BN parameter gradients."""
+    that into d/dy1 and the BN parameter gradients.  A bf16 y1 (autocast:
+    the 3x3 conv before ran on MIOpen bf16) stays bf16 -- the kernels read and
+    write bf16 activations / gradients with fp32 weights, statistics and
+    arithmetic -- so no cast copies surround the fused pair."""
 
     @staticmethod
-    @_amp_fwd
+    @_bn_fwd
     def forward(ctx, y1, gamma, beta, prebias, running_mean, running_var, nbt, training, momentum,
                 eps, w2, stats1=None, want_stats2=False):
-        y1 = y1.contiguous()
+        y1 = (y1 if y1.dtype == torch.bfloat16 else y1.float()).contiguous()
         n, c, h, w = y1.shape
         cout = w2.shape[0]
         w2m = w2.reshape(cout, c).contiguous()
@@ -201,7 +204,7 @@ class _BNReluPointwise(torch.autograd.Function):
     @_amp_bwd
     def backward(ctx, gy2, _gstats2):
         y1, gamma, beta, mean, invstd, scale, shift, w2m = ctx.saved_tensors
-        gy2 = gy2.contiguous()
+        gy2 = gy2.to(y1.dtype).contiguous()
         n, c, h, w = y1.shape
         cout = w2m.shape[0]
         st = _abi.stream_of(gy2)
@@ -259,7 +262,7 @@ def bn_relu_pointwise(y1, bn: nn.BatchNorm2d, prebias, conv: nn.Conv2d, stats1=N
         bn.running_var if (track or not training) else None,
         bn.num_batches_tracked if track else None,
         training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, conv.weight,
-        stats1 if training else None, bool(want_stats2) and y1.dtype == torch.float32)
+        stats1 if training else None, bool(want_stats2))
     return y2, (stats2 if stats2.shape[1] > 0 else None)
 
 

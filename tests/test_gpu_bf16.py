@@ -112,3 +112,34 @@ def test_ptmodel_bf16_vs_float64_oracle():
     x = torch.from_numpy(seeded((2, 3, 128, 160), 21, 0, 1))
     d = torch.from_numpy(seeded((2, 1, 128, 160), 22, 0.5, 10))
     _compare(lambda: fill_(om.PTModel()), ours, lambda: fill_(om.PTModel()), x, d, "PTModel bf16")
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 4, 96, 128), (32, 16, 2, 60, 80), (64, 32, 2, 30, 64)])
+def test_bnrelu_pointwise_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
+    """The fused BN-ReLU-1x1 pair on bf16 activations (autocast) == the fp32
+    kernels on the same values: the kernels convert on load and round on
+    store, so y2 is bit-exact with the fp32 result rounded to bf16, the 1x1
+    weight gradient is bit-exact, and d/dy1 agrees to bf16 rounding."""
+    import copy
+
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, bn_relu_pointwise
+    g = torch.Generator().manual_seed(cin + cout + h)
+    y1 = (torch.rand((n, cin, h, w), generator=g) * 2 - 0.7).to(DEV).to(torch.bfloat16)
+    gy2 = (torch.rand((n, cout, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    bn = BatchNorm2d(cin, act="relu").to(DEV).train()
+    conv = torch.nn.Conv2d(cin, cout, 1).to(DEV)
+    outs = []
+    for dt in (torch.bfloat16, torch.float32):
+        b, c = copy.deepcopy(bn), copy.deepcopy(conv)
+        x = y1.detach().to(dt).clone().requires_grad_(True)
+        y2, _ = bn_relu_pointwise(x, b, None, c, None, False)
+        assert y2.dtype == dt
+        y2.backward(gy2.to(dt))
+        outs.append((y2.detach(), x.grad, c.weight.grad, b.weight.grad, b.running_var.clone()))
+    (ya, ga, wa, gga, rva), (yb, gb, wb, ggb, rvb) = outs
+    assert torch.equal(ya, yb.to(torch.bfloat16))
+    assert torch.equal(wa, wb)
+    assert torch.equal(rva, rvb)
+    err = float((ga.float() - gb).abs().max()) / float(gb.abs().max())
+    assert err <= 1e-2, err
+    assert float((gga - ggb).abs().max()) <= 1e-2 * float(ggb.abs().max())

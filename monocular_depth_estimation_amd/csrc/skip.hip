@@ -662,16 +662,38 @@ constexpr size_t bwd_lds() {
 
 extern "C" {
 
+// bf16 storage (autocast) on the MFMA shapes only: 64 -> 32 and 32 -> 16
+// with h*w % 64 == 0 (the full-size decoder blocks); others are fp32-only.
+static bool skip_mfma_shape(int64_t cin, int64_t cout, int64_t hw) {
+  return hw % 64 == 0 && ((cin == 64 && cout == 32) || (cin == 32 && cout == 16));
+}
+
 int mde_skip_reduce_fwd(const void* r, const void* d, const float* wt,
                         const float* b, void* out, int64_t n, int64_t cin,
                         int64_t cout, int64_t h, int64_t w, int dtype,
                         void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   const int64_t hw = h * w;
   if (!r || !d || !wt || !b || !out || n <= 0 || hw <= 0 || cin <= 0 ||
       cout <= 0 || cin > kMaxC || cout > kMaxC)
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == MDE_BF16) {
+    if (!skip_mfma_shape(cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
+    const int64_t blocks = mde::cdiv(n * hw / 64, 4);
+    const dim3 g((unsigned)(blocks > 4096 ? 4096 : blocks));
+    const double bb = 2.0 * n * hw * (double)(2 * cin + cout);
+    using B = mde::bf16;
+    if (cin == 64)
+      MDE_LAUNCH(mde::K_SKIP_FWD, bb, s, (skip_fwd_mfma_kernel<64, 32, true, false, false, B>), g,
+                 dim3(256), 0, (const B*)r, (const B*)d, wt, b, (B*)out, n, hw, nullptr, nullptr,
+                 nullptr);
+    else
+      MDE_LAUNCH(mde::K_SKIP_FWD, bb, s, (skip_fwd_mfma_kernel<32, 16, true, false, false, B>), g,
+                 dim3(256), 0, (const B*)r, (const B*)d, wt, b, (B*)out, n, hw, nullptr, nullptr,
+                 nullptr);
+    return MDE_OK;
+  }
   const double bytes = 4.0 * n * hw * (double)(2 * cin + cout);
   auto grid = [&](int ppt) {
     const int64_t blocks = mde::cdiv(n * hw / ppt, 256);
@@ -714,7 +736,7 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
                         const float* wt, void* gs, float* gw, float* gb,
                         int64_t n, int64_t cin, int64_t cout, int64_t h,
                         int64_t w, void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   const int64_t hw = h * w;
   if (!gout || !r || !d || !wt || !gs || !gw || !gb || !workspace || n <= 0 ||
       hw <= 0 || cin <= 0 || cout <= 0 || cin > kMaxC || cout > kMaxC)
@@ -722,6 +744,24 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
   hipStream_t s = (hipStream_t)stream;
   const int nb = bwd_blocks(n, hw);
   float* slab = (float*)workspace;
+  if (dtype == MDE_BF16) {
+    if (!skip_mfma_shape(cin, cout, hw)) return MDE_ERR_UNSUPPORTED;
+    const double bb = 2.0 * n * hw * (double)(3 * cin + cout);
+    using B = mde::bf16;
+    if (cin == 64)
+      MDE_LAUNCH(mde::K_SKIP_BWD, bb, s, (skip_bwd_mfma_kernel<64, 32, true, false, false, B>),
+                 dim3(nb), dim3(256), 0, (const B*)gout, (const B*)r, (const B*)d, wt, (B*)gs,
+                 slab, n, hw, nullptr, nullptr, nullptr);
+    else
+      MDE_LAUNCH(mde::K_SKIP_BWD, bb, s, (skip_bwd_mfma_kernel<32, 16, true, false, false, B>),
+                 dim3(nb), dim3(256), 0, (const B*)gout, (const B*)r, (const B*)d, wt, (B*)gs,
+                 slab, n, hw, nullptr, nullptr, nullptr);
+    const int stride = (int)(cin * cout + cout);
+    MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+               dim3((unsigned)stride), dim3(256), 0, slab, nb, (int)(cin * cout), (int)cout, gw,
+               gb, 0, (float*)nullptr);
+    return MDE_OK;
+  }
   const double bytes = 4.0 * n * hw * (double)(2 * cin + cout + cin);
 #define SKIP_BWD(CI_, CO_, OB_, CB_, FAST_)                                   \
   MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s,                                      \

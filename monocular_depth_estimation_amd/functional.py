@@ -22,6 +22,8 @@ from . import _abi
 # fp32 input gradients back to the producers' dtype.
 _amp_fwd = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
 _amp_bwd = torch.amp.custom_bwd(device_type="cuda")
+# ops with bf16 storage paths pick their dtype themselves (no autocast cast)
+_bn_fwd = torch.amp.custom_fwd(device_type="cuda")
 
 __all__ = [
     "interpolate", "bilinear_resize", "nearest_resize", "se_cat", "skip_reduce",
@@ -222,14 +224,23 @@ def se_cat(xa, xb, w1, w2):
 
 
 # ------------------------------------------------------------- skip fusion
+def _skip_bf16(cin, cout, h, w) -> bool:
+    """bf16 storage for skip_reduce: the MFMA shapes (csrc/skip.hip skip_mfma_shape)."""
+    return (h * w) % 64 == 0 and (cin, cout) in ((64, 32), (32, 16))
+
+
 class _SkipReduce(torch.autograd.Function):
     @staticmethod
-    @_amp_fwd
+    @_bn_fwd
     def forward(ctx, r, d, weight, bias):
-        r = r.contiguous()
-        d = d.contiguous()
         n, cin, h, w = r.shape
         cout = weight.shape[0]
+        # bf16 activations stay bf16 (autocast) where the MFMA kernels take
+        # them; anything else runs fp32
+        dt = torch.bfloat16 if (r.dtype == torch.bfloat16 and _skip_bf16(cin, cout, h, w)) \
+            else torch.float32
+        r = r.to(dt).contiguous()
+        d = d.to(dt).contiguous()
         w2 = weight.reshape(cout, cin).contiguous()
         b = bias.contiguous()
         out = torch.empty((n, cout, h, w), dtype=r.dtype, device=r.device)
@@ -243,7 +254,7 @@ class _SkipReduce(torch.autograd.Function):
     @_amp_bwd
     def backward(ctx, gout):
         r, d, w2 = ctx.saved_tensors
-        gout = gout.contiguous()
+        gout = gout.to(r.dtype).contiguous()
         n, cin, h, w = r.shape
         cout = w2.shape[0]
         gs = torch.empty_like(r)

@@ -143,3 +143,31 @@ def test_bnrelu_pointwise_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
     err = float((ga.float() - gb).abs().max()) / float(gb.abs().max())
     assert err <= 1e-2, err
     assert float((gga - ggb).abs().max()) <= 1e-2 * float(ggb.abs().max())
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(64, 32, 2, 60, 80), (32, 16, 3, 48, 64)])
+def test_skip_reduce_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
+    """reduce(residual + depth) on bf16 activations == the fp32 kernel on the
+    same values: output and the shared input gradient bit-exact with the
+    rounded fp32 results, weight / bias gradients bit-exact."""
+    from monocular_depth_estimation_amd.functional import skip_reduce
+    g = torch.Generator().manual_seed(cin + h)
+    r = (torch.rand((n, cin, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    d = (torch.rand((n, cin, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    go = (torch.rand((n, cout, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    wt = ((torch.rand((cout, cin, 1, 1), generator=g) - 0.5) * 0.3).to(DEV)
+    bias = (torch.rand((cout,), generator=g) - 0.5).to(DEV)
+    outs = []
+    for dt in (torch.bfloat16, torch.float32):
+        rr = r.detach().to(dt).clone().requires_grad_(True)
+        dd = d.detach().to(dt).clone().requires_grad_(True)
+        ww = wt.clone().requires_grad_(True)
+        bb = bias.clone().requires_grad_(True)
+        y = skip_reduce(rr, dd, ww, bb)
+        assert y.dtype == dt
+        y.backward(go.to(dt))
+        outs.append((y.detach(), rr.grad, ww.grad, bb.grad))
+    (ya, ga, wa, ba), (yb, gb, wb, bb_) = outs
+    assert torch.equal(ya, yb.to(torch.bfloat16))
+    assert torch.equal(ga, gb.to(torch.bfloat16))
+    assert torch.equal(wa, wb) and torch.equal(ba, bb_)

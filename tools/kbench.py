@@ -140,8 +140,8 @@ def _main():
                timeit(lambda: torch.autograd.grad(o, (r, wt), go, retain_graph=True), a.reps),
                pix * (3 * c + cout))
     # BatchNorm(+ReLU) at representative shapes
-    for c, h, w in ((16, 480, 640), (32, 240, 320), (64, 120, 160), (32, 120, 160), (64, 60, 80),
-                    (256, 15, 20)) if want("bn") else ():
+    for c, h, w in ((16, 480, 640), (32, 240, 320), (16, 240, 320), (64, 120, 160), (32, 120, 160),
+                    (64, 60, 80), (256, 15, 20)) if want("bn") else ():
         x = torch.rand(n, c, h, w, device=dev, requires_grad=True)
         bn = BatchNorm2d(c, act="relu").to(dev).train()
         big = 4.0 * n * c * h * w

@@ -121,6 +121,32 @@ int mde_se_gate_bwd(const void* gout, const void* xa, int64_t ca, const void* xb
                     const float* mean, void* gxa, void* gxb, float* gw1, float* gb1,
                     float* gw2, float* gb2, int64_t n, int64_t h, int64_t w,
                     void* workspace, int dtype, void* stream);
+/* SE over two BatchNorm + ReLU outputs (the guided-upsampling blocks: the
+ * last `BatchNorm2d -> ReLU` of feature_conv and guide_conv, modules.py:49,59,
+ * their torch.cat at modules.py:90 and SELayer.forward, modules.py:21-25):
+ *   out = SELayer(cat(relu(sa*ya + ha), relu(sb*yb + hb)))
+ * from the BatchNorms' RAW inputs ya [n,ca,h,w], yb [n,cb,h,w] (the 1x1 convs'
+ * outputs without their folded bias); scale / shift [ca+cb] are the two BNs'
+ * coefficients (mde_batchnorm_fwd_coef / _coef_stats) concatenated.  The BN +
+ * ReLU outputs are never written.  Saved: s, hidden, mean as mde_se_fwd.
+ * Replaces (per block) two BN apply passes, the SE squeeze and scale. */
+size_t mde_se_bn_workspace(int64_t n, int64_t c, int64_t cr, int64_t h, int64_t w);
+int mde_se_bn_fwd(const void* ya, int64_t ca, const void* yb, int64_t cb, const float* scale,
+                  const float* shift, const float* w1, const float* w2, int64_t cr, void* out,
+                  float* s, float* hidden, float* mean, int64_t n, int64_t h, int64_t w,
+                  void* workspace, int dtype, void* stream);
+/* Backward through SE, both ReLUs and both BatchNorms: gya / gyb = d/dya,
+ * d/dyb; ggamma / gbeta [ca+cb] (concatenated, nullable) the BN parameter
+ * gradients; gw1 / gw2 as mde_se_bwd.  bn_mean / bn_invstd [ca+cb]: the BNs'
+ * save_mean (of the raw input) / save_invstd; training 0 = eval-mode BN
+ * (running statistics: no batch-statistics terms).  The folded conv bias has
+ * zero gradient through a training-mode BN (the caller supplies zeros). */
+int mde_se_bn_bwd(const void* gout, const void* ya, int64_t ca, const void* yb, int64_t cb,
+                  const float* scale, const float* shift, const float* bn_mean,
+                  const float* bn_invstd, int training, const float* w1, const float* w2,
+                  int64_t cr, const float* s, const float* hidden, const float* mean, void* gya,
+                  void* gyb, float* ggamma, float* gbeta, float* gw1, float* gw2, int64_t n,
+                  int64_t h, int64_t w, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Skip fusion: residual add + 1x1 conv with bias.

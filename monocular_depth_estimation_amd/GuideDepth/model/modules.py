@@ -3,7 +3,9 @@
 Drop-in for src/GuideDepth/model/modules.py: same constructors, forward
 signatures and state_dict keys.  Hot ops on HIP kernels:
   * cat([x, y], 1) + SELayer (:90, :21-25)  -> functional.se_cat (one fused op,
-    the concatenation is never materialised);
+    the concatenation is never materialised); in training (fp32) together with
+    the two branches' last BatchNorm + ReLU (:49, :59) -> nn.se_bn_cat, which
+    reads the 1x1 convs' raw outputs and writes only the SE output;
   * reduce(residual + depth) (:100)          -> functional.skip_reduce.
 Convolutions stay on PyTorch-ROCm (MIOpen) without their bias; conv bias +
 BatchNorm + ReLU run as one fused HIP pass (nn.py run_sequential).
@@ -13,7 +15,11 @@ from __future__ import annotations
 from torch import nn
 
 from ...functional import se_cat, skip_reduce
-from ...nn import BatchNorm2d, run_sequential
+from ...nn import BatchNorm2d, batch_norm_act, run_sequential, run_sequential_raw, se_bn_cat
+
+# Guided_Upsampling_Block: run the branches' last BN + ReLU, the concatenation
+# and SE as one fused op (nn.se_bn_cat) where it applies (training, fp32).
+FUSE_SE_BN = True
 
 
 class SELayer(nn.Module):
@@ -76,6 +82,22 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
             self.SE_block = SELayer(comb_features, reduction=1)
 
     def forward(self, guide, depth):
+        if FUSE_SE_BN and self.channel_attention and self.guidance_type == "full":
+            # the branches' last BN + ReLU, the concatenation and SE as one op
+            ra = run_sequential_raw(self.feature_conv, depth)
+            rb = run_sequential_raw(self.guide_conv, guide) if ra is not None else None
+            if rb is not None:
+                xy = se_bn_cat(ra[0], rb[0], ra[2], rb[2], ra[3], rb[3],
+                               self.SE_block.fc[0].weight, self.SE_block.fc[2].weight,
+                               ra[1], rb[1])
+                return skip_reduce(run_sequential(self.comb_conv, xy), depth,
+                                   self.reduce.weight, self.reduce.bias)
+            if ra is not None:  # finish the feature branch unfused
+                x = batch_norm_act(ra[0], ra[2], ra[2].act, None, ra[3], ra[1])
+                second = run_sequential(self.guide_conv, guide)
+                xy = self.SE_block.forward_cat(x, second)
+                return skip_reduce(run_sequential(self.comb_conv, xy), depth,
+                                   self.reduce.weight, self.reduce.bias)
         x = run_sequential(self.feature_conv, depth)
         if self.guidance_type == "full":
             second = run_sequential(self.guide_conv, guide)

@@ -39,6 +39,12 @@ SIGNATURES = {
                           _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_se_bwd": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp,
                           _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_se_bn_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_se_bn_fwd": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
+                             _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_se_bn_bwd": (_int, [_vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _int, _vp, _vp, _i64,
+                             _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp,
+                             _int, _vp]),
     "mde_skip_reduce_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_skip_reduce_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
     "mde_skip_reduce_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,

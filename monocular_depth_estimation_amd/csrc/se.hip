@@ -27,34 +27,49 @@ __device__ __forceinline__ const float* plane_ptr(const float* xa, int64_t ca,
                  : xb + (nidx * cb + (ch - ca)) * hw;
 }
 
-// part[plane * chunks + k] = sum of chunk k of plane (optionally of g*x).
-template <bool DOT>
+// part[plane * chunks + k] = sum of chunk k of plane of x (MODE 0), of g*x
+// (MODE 1) or of u = relu(sc*x + sh) (MODE 2: the input is the raw output of
+// the conv before a BatchNorm + ReLU; sc / sh = the BN coefficients).
+enum { kSum = 0, kDot = 1, kBnRelu = 2 };
+
+__device__ __forceinline__ float bnrelu(float v, float sc, float sh) {
+  return fmaxf(fmaf(v, sc, sh), 0.f);
+}
+
+template <int MODE>
 __global__ void __launch_bounds__(256)
     se_partial_kernel(const float* __restrict__ g, const float* __restrict__ xa,
                       int64_t ca, const float* __restrict__ xb, int64_t cb,
-                      int64_t hw, int chunks, float* __restrict__ part) {
+                      int64_t hw, int chunks, float* __restrict__ part,
+                      const float* __restrict__ scale = nullptr,
+                      const float* __restrict__ shift = nullptr) {
   __shared__ float red[4];
   const int64_t c = ca + cb;
   const int64_t plane = blockIdx.y;
   const int64_t nidx = plane / c, ch = plane % c;
   const float* x = plane_ptr(xa, ca, xb, cb, nidx, ch, hw);
-  const float* gp = DOT ? g + plane * hw : nullptr;
+  const float* gp = MODE == kDot ? g + plane * hw : nullptr;
+  const float sc = MODE == kBnRelu ? scale[ch] : 0.f, sh = MODE == kBnRelu ? shift[ch] : 0.f;
   const int64_t beg = (int64_t)blockIdx.x * kChunk;
   const int64_t end = beg + kChunk < hw ? beg + kChunk : hw;
   float acc = 0.f;
   if ((hw & 3) == 0) {
     for (int64_t i = beg + 4 * threadIdx.x; i < end; i += 4 * 256) {
-      const float4 v = *reinterpret_cast<const float4*>(x + i);
-      if (DOT) {
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      if (MODE == kDot) {
         const float4 q = *reinterpret_cast<const float4*>(gp + i);
         acc += (v.x * q.x + v.y * q.y) + (v.z * q.z + v.w * q.w);
       } else {
+        if (MODE == kBnRelu) {
+          v.x = bnrelu(v.x, sc, sh); v.y = bnrelu(v.y, sc, sh);
+          v.z = bnrelu(v.z, sc, sh); v.w = bnrelu(v.w, sc, sh);
+        }
         acc += (v.x + v.y) + (v.z + v.w);
       }
     }
   } else {
     for (int64_t i = beg + threadIdx.x; i < end; i += 256)
-      acc += DOT ? x[i] * gp[i] : x[i];
+      acc += MODE == kDot ? x[i] * gp[i] : (MODE == kBnRelu ? bnrelu(x[i], sc, sh) : x[i]);
   }
   const float tot = mde::block_sum256(acc, red);
   if (threadIdx.x == 0) part[plane * chunks + blockIdx.x] = tot;
@@ -119,12 +134,15 @@ __global__ void __launch_bounds__(1024)
   if (lane == 0) s[(int64_t)nidx * c + ch] = gate_fn(z, gate);
 }
 
-// out[plane, i] = x[plane, i] * s[plane]  (cat fused: plane -> xa or xb)
+// out[plane, i] = x[plane, i] * s[plane]  (cat fused: plane -> xa or xb);
+// BNR: out = s[plane] * relu(sc * x + sh) (x = the BatchNorm's raw input).
+template <bool BNR>
 __global__ void __launch_bounds__(256)
     se_scale_kernel(const float* __restrict__ xa, int64_t ca,
                     const float* __restrict__ xb, int64_t cb, int64_t hw,
                     int64_t planes, const float* __restrict__ s,
-                    float* __restrict__ out) {
+                    float* __restrict__ out, const float* __restrict__ scale = nullptr,
+                    const float* __restrict__ shift = nullptr) {
   const int64_t c = ca + cb;
   if ((hw & 3) == 0) {
     const int64_t hw4 = hw >> 2;
@@ -132,9 +150,15 @@ __global__ void __launch_bounds__(256)
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t plane = t / hw4, i = (t - plane * hw4) << 2;
-      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, plane % c, hw);
+      const int64_t ch = plane % c;
+      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, ch, hw);
       const float sc = s[plane];
       float4 v = *reinterpret_cast<const float4*>(x + i);
+      if (BNR) {
+        const float a = scale[ch], b = shift[ch];
+        v.x = bnrelu(v.x, a, b); v.y = bnrelu(v.y, a, b);
+        v.z = bnrelu(v.z, a, b); v.w = bnrelu(v.w, a, b);
+      }
       v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
       *reinterpret_cast<float4*>(out + plane * hw + i) = v;
     }
@@ -143,8 +167,10 @@ __global__ void __launch_bounds__(256)
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
          t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t plane = t / hw, i = t - plane * hw;
-      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, plane % c, hw);
-      out[t] = x[i] * s[plane];
+      const int64_t ch = plane % c;
+      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, ch, hw);
+      const float v = BNR ? bnrelu(x[i], scale[ch], shift[ch]) : x[i];
+      out[t] = v * s[plane];
     }
   }
 }
@@ -292,6 +318,141 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ---- SE over BatchNorm + ReLU outputs (the guided-upsampling blocks: the
+// two branches' last BN + ReLU, their concatenation and the SE layer in one
+// op; modules.py:49-59,87-91).  With z = sc*y + sh (BN of the raw conv
+// output y), u = relu(z), out = s * u:
+//   du = s*g + dm/HW (dm: the gradient of the squeeze mean), dz = [z > 0] du,
+//   and the BatchNorm backward needs S1 = sum dz, S2 = sum dz*(y - mean) per
+//   channel.  Both are linear in per-(sample, channel) sums of one pass:
+//   A = sum g*m, B = sum m, C = sum g*m*(y - mean), D = sum m*(y - mean),
+//   E = sum g*u (= the SE gradient dot) with m = [z > 0].
+__global__ void __launch_bounds__(256)
+    sebn_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ ya, int64_t ca,
+                           const float* __restrict__ yb, int64_t cb, int64_t hw, int chunks,
+                           const float* __restrict__ scale, const float* __restrict__ shift,
+                           const float* __restrict__ mean, float* __restrict__ part_e,
+                           float* __restrict__ part4) {
+  __shared__ float red[4];
+  const int64_t c = ca + cb;
+  const int64_t plane = blockIdx.y;
+  const int64_t nidx = plane / c, ch = plane % c;
+  const float* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
+  const float* gp = g + plane * hw;
+  const float sc = scale[ch], sh = shift[ch], mu = mean[ch];
+  const int64_t beg = (int64_t)blockIdx.x * kChunk;
+  const int64_t end = beg + kChunk < hw ? beg + kChunk : hw;
+  float A = 0.f, B = 0.f, C = 0.f, D = 0.f, E = 0.f;
+  auto one = [&](float yv, float gv) {
+    const float z = fmaf(yv, sc, sh);
+    if (z > 0.f) {
+      const float d = yv - mu;
+      A += gv;
+      B += 1.f;
+      C += gv * d;
+      D += d;
+      E += gv * z;
+    }
+  };
+  if ((hw & 3) == 0) {
+    for (int64_t i = beg + 4 * threadIdx.x; i < end; i += 4 * 256) {
+      const float4 v = *reinterpret_cast<const float4*>(y + i);
+      const float4 q = *reinterpret_cast<const float4*>(gp + i);
+      one(v.x, q.x); one(v.y, q.y); one(v.z, q.z); one(v.w, q.w);
+    }
+  } else {
+    for (int64_t i = beg + threadIdx.x; i < end; i += 256) one(y[i], gp[i]);
+  }
+  A = mde::block_sum256(A, red);
+  B = mde::block_sum256(B, red);
+  C = mde::block_sum256(C, red);
+  D = mde::block_sum256(D, red);
+  E = mde::block_sum256(E, red);
+  if (threadIdx.x == 0) {
+    const int64_t k = plane * chunks + blockIdx.x;
+    part_e[k] = E;
+    float* o = part4 + 4 * k;
+    o[0] = A; o[1] = B; o[2] = C; o[3] = D;
+  }
+}
+
+// Per channel (one thread each): S1, S2 in double over samples and chunks ->
+// the BN parameter gradients and the apply constants coef[ch] = (R, T) with
+// gy = m (P g + Q) + R + T (y - mean), P = sc s, Q = sc dm / HW (per sample).
+__global__ void __launch_bounds__(256)
+    sebn_bwd_combine_kernel(const float* __restrict__ part4, int chunks, int64_t n, int64_t c,
+                            int64_t hw, const float* __restrict__ s, const float* __restrict__ dm,
+                            const float* __restrict__ scale, const float* __restrict__ invstd,
+                            int training, float* __restrict__ ggamma, float* __restrict__ gbeta,
+                            float* __restrict__ coef) {
+  const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  const double inv_hw = 1.0 / (double)hw;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t plane = i * c + ch;
+    double a = 0.0, b = 0.0, cc = 0.0, d = 0.0;
+    for (int k = 0; k < chunks; ++k) {
+      const float* p = part4 + 4 * (plane * chunks + k);
+      a += p[0]; b += p[1]; cc += p[2]; d += p[3];
+    }
+    const double sv = s[plane], q = (double)dm[plane] * inv_hw;
+    s1 += sv * a + q * b;
+    s2 += sv * cc + q * d;
+  }
+  const double is = invstd[ch], sc = scale[ch], cnt = (double)n * (double)hw;
+  if (ggamma) ggamma[ch] = (float)(is * s2);
+  if (gbeta) gbeta[ch] = (float)s1;
+  coef[2 * ch] = training ? (float)(-sc * s1 / cnt) : 0.f;
+  coef[2 * ch + 1] = training ? (float)(-sc * is * is * s2 / cnt) : 0.f;
+}
+
+__global__ void __launch_bounds__(256)
+    sebn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ ya, int64_t ca,
+                          const float* __restrict__ yb, int64_t cb, int64_t hw, int64_t planes,
+                          const float* __restrict__ s, const float* __restrict__ dm, float inv_hw,
+                          const float* __restrict__ scale, const float* __restrict__ shift,
+                          const float* __restrict__ mean, const float* __restrict__ coef,
+                          float* __restrict__ gya, float* __restrict__ gyb) {
+  const int64_t c = ca + cb;
+  auto one = [](float yv, float gv, float sc, float sh, float P, float Q, float R, float T,
+                float mu) {
+    const float z = fmaf(yv, sc, sh);
+    return (z > 0.f ? fmaf(P, gv, Q) : 0.f) + fmaf(T, yv - mu, R);
+  };
+  if ((hw & 3) == 0) {
+    const int64_t hw4 = hw >> 2;
+    const int64_t total = planes * hw4;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t plane = t / hw4, i = (t - plane * hw4) << 2;
+      const int64_t nidx = plane / c, ch = plane % c;
+      const float* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
+      float* dst = ch < ca ? gya + (nidx * ca + ch) * hw : gyb + (nidx * cb + ch - ca) * hw;
+      const float sc = scale[ch], sh = shift[ch], mu = mean[ch];
+      const float P = sc * s[plane], Q = sc * dm[plane] * inv_hw;
+      const float R = coef[2 * ch], T = coef[2 * ch + 1];
+      const float4 v = *reinterpret_cast<const float4*>(y + i);
+      const float4 q = *reinterpret_cast<const float4*>(g + plane * hw + i);
+      *reinterpret_cast<float4*>(dst + i) =
+          make_float4(one(v.x, q.x, sc, sh, P, Q, R, T, mu), one(v.y, q.y, sc, sh, P, Q, R, T, mu),
+                      one(v.z, q.z, sc, sh, P, Q, R, T, mu), one(v.w, q.w, sc, sh, P, Q, R, T, mu));
+    }
+  } else {
+    const int64_t total = planes * hw;
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+         t += (int64_t)gridDim.x * blockDim.x) {
+      const int64_t plane = t / hw, i = t - plane * hw;
+      const int64_t nidx = plane / c, ch = plane % c;
+      const float* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
+      float* dst = ch < ca ? gya + (nidx * ca + ch) * hw : gyb + (nidx * cb + ch - ca) * hw;
+      const float sc = scale[ch];
+      dst[i] = one(y[i], g[t], sc, shift[ch], sc * s[plane], sc * dm[plane] * inv_hw,
+                   coef[2 * ch], coef[2 * ch + 1], mean[ch]);
+    }
+  }
+}
+
 inline int stream_grid(int64_t work) {
   const int64_t b = mde::cdiv(work, 256);
   return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
@@ -302,6 +463,8 @@ struct SeWs {
   float* dz;
   float* dh;
   float* dm;
+  float* part4;
+  float* coef;
 };
 
 inline int64_t se_chunks(int64_t hw) { return mde::cdiv(hw, kChunk); }
@@ -318,6 +481,10 @@ SeWs se_carve(void* ws, int64_t n, int64_t c, int64_t cr, int64_t hw) {
   r.dh = (float*)p;
   p += round16(sizeof(float) * n * cr);
   r.dm = (float*)p;
+  p += round16(sizeof(float) * n * c);
+  r.part4 = (float*)p;  // SE-over-BN backward only (mde_se_bn_workspace)
+  p += round16(sizeof(float) * 4 * n * c * se_chunks(hw));
+  r.coef = (float*)p;
   return r;
 }
 
@@ -349,7 +516,7 @@ int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   SeWs ws = se_carve(workspace, n, c, cr, hw);
   const int chunks = (int)se_chunks(hw);
   const double big = 4.0 * n * c * (double)hw;
-  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<false>,
+  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<kSum>,
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr,
              (const float*)xa, ca, (const float*)xb, cb, hw, chunks, ws.part);
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc1_kernel,
@@ -359,7 +526,7 @@ int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc2_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
              sizeof(float) * cr, (int)c, (int)cr, w2, b2, gate, hidden, s);
-  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel,
+  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel<false>,
              dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
              (const float*)xa, ca, (const float*)xb, cb, hw, n * c, s,
              (float*)out);
@@ -383,7 +550,7 @@ int mde_se_gate_bwd(const void* gout, const void* xa, int64_t ca, const void* xb
   SeWs ws = se_carve(workspace, n, c, cr, hw);
   const int chunks = (int)se_chunks(hw);
   const double big = 4.0 * n * c * (double)hw;
-  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, se_partial_kernel<true>,
+  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, se_partial_kernel<kDot>,
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0,
              (const float*)gout, (const float*)xa, ca, (const float*)xb, cb,
              hw, chunks, ws.part);
@@ -425,6 +592,96 @@ int mde_se_bwd(const void* gout, const void* xa, int64_t ca, const void* xb,
                int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
   return mde_se_gate_bwd(gout, xa, ca, xb, cb, w1, w2, nullptr, cr, 0, s, hidden, mean, gxa,
                          gxb, gw1, nullptr, gw2, nullptr, n, h, w, workspace, dtype, stream);
+}
+
+size_t mde_se_bn_workspace(int64_t n, int64_t c, int64_t cr, int64_t h, int64_t w) {
+  return mde_se_workspace(n, c, cr, h, w) + round16(sizeof(float) * 4 * n * c * se_chunks(h * w)) +
+         round16(sizeof(float) * 2 * c);
+}
+
+// SELayer(cat([relu(bn_a(ya)), relu(bn_b(yb))])) from the BatchNorms' raw
+// inputs: scale / shift [ca + cb] are the two BNs' per-channel coefficients
+// (mde_batchnorm_fwd_coef*), concatenated.  The squeeze reads y once, the
+// scale pass writes out = s * relu(scale * y + shift); the BN + ReLU outputs
+// and their concatenation are never materialised.
+int mde_se_bn_fwd(const void* ya, int64_t ca, const void* yb, int64_t cb, const float* scale,
+                  const float* shift, const float* w1, const float* w2, int64_t cr, void* out,
+                  float* s, float* hidden, float* mean, int64_t n, int64_t h, int64_t w,
+                  void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t c = ca + cb, hw = h * w;
+  if (!ya || ca <= 0 || cb < 0 || (cb > 0 && !yb) || !scale || !shift || !w1 || !w2 ||
+      cr <= 0 || !out || !s || !hidden || !mean || n <= 0 || hw <= 0 || !workspace ||
+      c > 4096 || cr > 4096 || n > 65535 || n * c > 65535)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  SeWs ws = se_carve(workspace, n, c, cr, hw);
+  const int chunks = (int)se_chunks(hw);
+  const double big = 4.0 * n * c * (double)hw;
+  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<kBnRelu>,
+             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr, (const float*)ya, ca,
+             (const float*)yb, cb, hw, chunks, ws.part, scale, shift);
+  MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc1_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(cr, kOutPerBlock)), dim3(1024),
+             sizeof(float) * c, ws.part, chunks, (int)c, (int)cr, 1.f / (float)hw, w1, nullptr,
+             hidden, mean);
+  MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc2_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
+             sizeof(float) * cr, (int)c, (int)cr, w2, nullptr, 0, hidden, s);
+  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel<true>,
+             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)ya, ca,
+             (const float*)yb, cb, hw, n * c, s, (float*)out, scale, shift);
+  return MDE_OK;
+}
+
+// Backward of mde_se_bn_fwd through the SE layer, the ReLUs and both
+// BatchNorms (training: batch statistics, save_mean / save_invstd of the raw
+// input; eval: running statistics, no mean / variance terms): one reduction
+// pass over (gout, y), the per-sample FC backward, a per-channel combine in
+// double, and one apply pass writing gya / gyb = d/dy.  ggamma / gbeta are
+// concatenated [ca + cb] like scale / shift.
+int mde_se_bn_bwd(const void* gout, const void* ya, int64_t ca, const void* yb, int64_t cb,
+                  const float* scale, const float* shift, const float* bn_mean,
+                  const float* bn_invstd, int training, const float* w1, const float* w2,
+                  int64_t cr, const float* s, const float* hidden, const float* mean, void* gya,
+                  void* gyb, float* ggamma, float* gbeta, float* gw1, float* gw2, int64_t n,
+                  int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t c = ca + cb, hw = h * w;
+  if (!gout || !ya || ca <= 0 || cb < 0 || (cb > 0 && (!yb || !gyb)) || !gya || !scale ||
+      !shift || !bn_mean || !bn_invstd || !w1 || !w2 || cr <= 0 || !s || !hidden || !mean ||
+      !gw1 || !gw2 || n <= 0 || hw <= 0 || !workspace || c > 4096 || cr > 4096 ||
+      n > 65535 || n * c > 65535)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  SeWs ws = se_carve(workspace, n, c, cr, hw);
+  const int chunks = (int)se_chunks(hw);
+  const double big = 4.0 * n * c * (double)hw;
+  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, sebn_bwd_reduce_kernel,
+             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, (const float*)gout,
+             (const float*)ya, ca, (const float*)yb, cb, hw, chunks, scale, shift, bn_mean,
+             ws.part, ws.part4);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + 3.0 * n * c), st, se_bfc1_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
+             sizeof(float) * cr, ws.part, chunks, (int)c, (int)cr, w2, nullptr, 0, s, hidden,
+             ws.dz);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + n * (c + 2.0 * cr)), st, se_bfc2_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(cr, kOutPerBlock)), dim3(1024),
+             sizeof(float) * c, (int)c, (int)cr, w2, hidden, ws.dz, ws.dh);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + n * (c + cr)), st, se_bfc3_kernel,
+             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
+             sizeof(float) * cr, (int)c, (int)cr, w1, ws.dh, ws.dm);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 2.0 * n * (c + cr)), st,
+             se_wgrad_kernel, dim3((unsigned)mde::cdiv(2 * c * cr, 256)), dim3(256), 0, (int)n,
+             (int)c, (int)cr, ws.dz, ws.dh, hidden, mean, gw1, gw2, nullptr, nullptr);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 16.0 * n * c * chunks, st, sebn_bwd_combine_kernel,
+             dim3((unsigned)mde::cdiv(c, 256)), dim3(256), 0, ws.part4, chunks, n, c, hw, s,
+             ws.dm, scale, bn_invstd, training, ggamma, gbeta, ws.coef);
+  MDE_LAUNCH(mde::K_SE_BWD_APPLY, 3.0 * big, st, sebn_bwd_apply_kernel,
+             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)gout,
+             (const float*)ya, ca, (const float*)yb, cb, hw, n * c, s, ws.dm, 1.f / (float)hw,
+             scale, shift, bn_mean, ws.coef, (float*)gya, (float*)gyb);
+  return MDE_OK;
 }
 
 }  // extern "C"

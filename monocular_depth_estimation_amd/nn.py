@@ -266,6 +266,95 @@ def bn_relu_pointwise(y1, bn: nn.BatchNorm2d, prebias, conv: nn.Conv2d, stats1=N
     return y2, (stats2 if stats2.shape[1] > 0 else None)
 
 
+class _SeBnCat(torch.autograd.Function):
+    """SELayer(cat([relu(bn_a(ya + pb_a)), relu(bn_b(yb + pb_b))])) from the two
+    BatchNorms' raw inputs (mde_se_bn_fwd / _bwd): the BN + ReLU outputs and
+    their concatenation are never written, and the backward runs SE, both
+    ReLUs and both BatchNorms as one reduction pass + one apply pass."""
+
+    @staticmethod
+    @_amp_fwd
+    def forward(ctx, ya, yb, ga, ba, pba, gb, bb, pbb, w1, w2, meta_a, meta_b, sta, stb):
+        ya, yb = ya.contiguous(), yb.contiguous()
+        w1, w2 = w1.contiguous(), w2.contiguous()
+        n, ca, h, w = ya.shape
+        cb = yb.shape[1]
+        c, cr = ca + cb, w1.shape[0]
+        f32 = dict(dtype=torch.float32, device=ya.device)
+        scale, shift = torch.empty(c, **f32), torch.empty(c, **f32)
+        mean, invstd = torch.empty(c, **f32), torch.empty(c, **f32)
+        st = _abi.stream_of(ya)
+        for y, g, b, pb, meta, stt, lo, hi in ((ya, ga, ba, pba, meta_a, sta, 0, ca),
+                                                (yb, gb, bb, pbb, meta_b, stb, ca, c)):
+            rm, rv, nbt, momentum, eps = meta
+            cc = hi - lo
+            ws = _ws(_abi.query("mde_batchnorm_workspace", n, cc, h, w), y)
+            views = [t[lo:hi] for t in (scale, shift, mean, invstd)]
+            if stt is not None:
+                _abi.call("mde_batchnorm_fwd_coef_stats", _abi.ptr(y), _abi.ptr(g), _abi.ptr(b),
+                          _abi.ptr(pb), _abi.ptr(rm), _abi.ptr(rv), _abi.ptr(nbt), float(momentum),
+                          float(eps), *[_abi.ptr(v) for v in views], n, cc, h, w, _abi.ptr(stt),
+                          stt.shape[1], _abi.ptr(ws), _abi.dtype_code(y), st)
+            else:
+                _abi.call("mde_batchnorm_fwd_coef", _abi.ptr(y), _abi.ptr(g), _abi.ptr(b),
+                          _abi.ptr(pb), _abi.ptr(rm), _abi.ptr(rv), _abi.ptr(nbt), float(momentum),
+                          float(eps), 1, *[_abi.ptr(v) for v in views], n, cc, h, w, _abi.ptr(ws),
+                          _abi.dtype_code(y), st)
+        out = torch.empty((n, c, h, w), **f32)
+        s, hidden, semean = torch.empty((n, c), **f32), torch.empty((n, cr), **f32), torch.empty((n, c), **f32)
+        ws = _ws(_abi.query("mde_se_bn_workspace", n, c, cr, h, w), ya)
+        _abi.call("mde_se_bn_fwd", _abi.ptr(ya), ca, _abi.ptr(yb), cb, _abi.ptr(scale),
+                  _abi.ptr(shift), _abi.ptr(w1), _abi.ptr(w2), cr, _abi.ptr(out), _abi.ptr(s),
+                  _abi.ptr(hidden), _abi.ptr(semean), n, h, w, _abi.ptr(ws), _abi.dtype_code(ya), st)
+        ctx.save_for_backward(ya, yb, w1, w2, scale, shift, mean, invstd, s, hidden, semean)
+        ctx.has_pb = (pba is not None, pbb is not None)
+        return out
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, gout):
+        ya, yb, w1, w2, scale, shift, mean, invstd, s, hidden, semean = ctx.saved_tensors
+        gout = gout.contiguous()
+        n, ca, h, w = ya.shape
+        c, cr = ca + yb.shape[1], w1.shape[0]
+        gya, gyb = torch.empty_like(ya), torch.empty_like(yb)
+        gg, gbt = torch.empty_like(scale), torch.empty_like(scale)
+        gw1, gw2 = torch.empty_like(w1), torch.empty_like(w2)
+        ws = _ws(_abi.query("mde_se_bn_workspace", n, c, cr, h, w), ya)
+        _abi.call("mde_se_bn_bwd", _abi.ptr(gout), _abi.ptr(ya), ca, _abi.ptr(yb), c - ca,
+                  _abi.ptr(scale), _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(invstd), 1,
+                  _abi.ptr(w1), _abi.ptr(w2), cr, _abi.ptr(s), _abi.ptr(hidden), _abi.ptr(semean),
+                  _abi.ptr(gya), _abi.ptr(gyb), _abi.ptr(gg), _abi.ptr(gbt), _abi.ptr(gw1),
+                  _abi.ptr(gw2), n, h, w, _abi.ptr(ws), _abi.dtype_code(gout), _abi.stream_of(gout))
+        # a training-mode BatchNorm's output does not depend on its input's
+        # per-channel offset: the folded conv biases get zero gradient
+        zpa = torch.zeros(ca, dtype=torch.float32, device=ya.device) if ctx.has_pb[0] else None
+        zpb = torch.zeros(c - ca, dtype=torch.float32, device=ya.device) if ctx.has_pb[1] else None
+        return (gya, gyb, gg[:ca], gbt[:ca], zpa, gg[ca:], gbt[ca:], zpb, gw1, gw2, None, None,
+                None, None)
+
+
+def se_bn_cat(ya, yb, bn_a: nn.BatchNorm2d, bn_b: nn.BatchNorm2d, pb_a, pb_b, w1, w2,
+              stats_a=None, stats_b=None):
+    """SELayer(cat([relu(bn_a(ya + pb_a)), relu(bn_b(yb + pb_b))], 1)) on the fused
+    HIP path (training-mode BatchNorms, fp32).  ya / yb are the raw outputs of
+    the 1x1 convs ending feature_conv / guide_conv (modules.py:42-59) and
+    stats_a / stats_b their per-block statistics from the conv epilogue (or
+    None: a statistics pass).  w1 / w2: SE_block.fc[0] / fc[2] weights."""
+    _gpu(ya, yb, pb_a, pb_b, w1, w2)
+    for bn in (bn_a, bn_b):
+        if bn.weight is None or bn.bias is None or bn.momentum is None or not bn.training:
+            raise NotImplementedError("se_bn_cat needs affine, momentum, training-mode BatchNorms")
+
+    def meta(bn):
+        track = bn.track_running_stats
+        return (bn.running_mean if track else None, bn.running_var if track else None,
+                bn.num_batches_tracked if track else None, bn.momentum, bn.eps)
+
+    return _SeBnCat.apply(ya, yb, bn_a.weight, bn_a.bias, pb_a, bn_b.weight, bn_b.bias, pb_b,
+                          w1, w2, meta(bn_a), meta(bn_b), stats_a, stats_b)
+
+
 def pointwise_ok(conv: nn.Conv2d, x) -> bool:
     """Whether this bias-folded 1x1 conv runs on the HIP pointwise kernel."""
     if (conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.padding != (0, 0)
@@ -452,6 +541,33 @@ def run_sequential(seq: nn.Sequential, x):
             x = m(x)
             i += 1
     return x
+
+
+def run_sequential_raw(seq: nn.Sequential, x):
+    """For Conv(bias) -> BN(relu) -> ReLU slot -> 1x1 Conv(bias) -> BN(relu) ->
+    ReLU slot on the fused HIP path in training mode (fp32): run it WITHOUT
+    the last BatchNorm + ReLU and return (y2, stats2, bn2, conv2_bias) -- the
+    last BN's raw input, its epilogue statistics, the BN module and its folded
+    bias -- for a consumer that applies that BN itself (se_bn_cat).  None when
+    the pattern or the conditions do not hold (then run_sequential(seq, x))."""
+    mods = list(seq)
+    if (len(mods) != 6 or not x.is_cuda or x.dtype != torch.float32
+            or torch.is_autocast_enabled() or not _bnrelu_pw_at(mods, 0, x.shape)
+            or not isinstance(mods[5], nn.Identity) or mods[4].act != "relu"
+            or not mods[1].training or not mods[4].training):
+        return None
+    m = mods[0]
+    k = m.kernel_size
+    if (m.stride != (1, 1) or m.dilation != (1, 1) or m.padding != (k[0] // 2, k[1] // 2)
+            or k[0] % 2 == 0 or k[1] % 2 == 0 or not pointwise_ok(mods[3], x)):
+        return None  # y1 keeps x's H x W, which pointwise_ok checked
+    passes = conv3x3_passes(m, x)
+    if passes is not None:
+        y1, st1 = conv3x3_stats(x, m.weight, passes)
+    else:
+        y1, st1 = conv_nobias(m, x), None
+    y2, st2 = bn_relu_pointwise(y1, mods[1], m.bias, mods[3], st1, True)
+    return y2, st2, mods[4], mods[3].bias
 
 
 class BatchNorm2d(nn.BatchNorm2d):

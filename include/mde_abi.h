@@ -167,6 +167,26 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
                         const float* wt, void* gs, float* gw, float* gb,
                         int64_t n, int64_t cin, int64_t cout, int64_t h,
                         int64_t w, void* workspace, int dtype, void* stream);
+/* Skip fusion over the comb_conv's last BatchNorm + ReLU (modules.py:72-73,
+ * 100): r is that BN's RAW input (the 1x1 conv output without its folded
+ * bias), in_scale / in_shift [cin] its coefficients (mde_batchnorm_fwd_coef*):
+ *   out = b + W (relu(in_scale r + in_shift) + d)
+ * -- the BN + ReLU output is never written.  Backward: gs = W^T g (the
+ * gradient of d and of the ReLU output), gw, gb as mde_skip_reduce_bwd, and
+ * with in_sums [cin][2] (nullable) the BN backward's sums (sum e, sum e (r -
+ * in_mean)), e = gs [in_scale r + in_shift > 0], for mde_batchnorm_bwd_apply.
+ * mde_skip_reduce_bn_supported(.., sums): 1 if the shape runs (with sums). */
+int mde_skip_reduce_bn_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int sums);
+size_t mde_skip_reduce_bn_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_skip_reduce_bn_fwd(const void* r, const void* d, const float* in_scale,
+                           const float* in_shift, const float* wt, const float* b, void* out,
+                           int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                           void* stream);
+int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const float* in_scale,
+                           const float* in_shift, const float* in_mean, const float* wt, void* gs,
+                           float* gw, float* gb, float* in_sums, int64_t n, int64_t cin,
+                           int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                           void* stream);
 
 /* ---------------------------------------------------------------------------
  * DepthNorm, src/utils.py:7-8: (d - d.min()) / (d.max() - d.min()), min/max

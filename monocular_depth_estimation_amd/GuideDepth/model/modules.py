@@ -15,11 +15,13 @@ from __future__ import annotations
 from torch import nn
 
 from ...functional import se_cat, skip_reduce
-from ...nn import BatchNorm2d, batch_norm_act, run_sequential, run_sequential_raw, se_bn_cat
+from ...nn import (BatchNorm2d, batch_norm_act, run_sequential, run_sequential_raw, se_bn_cat,
+                   skip_reduce_bn, skip_reduce_bn_ok)
 
-# Guided_Upsampling_Block: run the branches' last BN + ReLU, the concatenation
-# and SE as one fused op (nn.se_bn_cat) where it applies (training, fp32).
-FUSE_SE_BN = True
+# Guided_Upsampling_Block (training, fp32): run the branches' last BN + ReLU,
+# the concatenation and SE as one fused op (nn.se_bn_cat), and the comb_conv's
+# last BN + ReLU inside the skip fusion's operand load (nn.skip_reduce_bn).
+FUSE_BN = True
 
 
 class SELayer(nn.Module):
@@ -82,7 +84,7 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
             self.SE_block = SELayer(comb_features, reduction=1)
 
     def forward(self, guide, depth):
-        if FUSE_SE_BN and self.channel_attention and self.guidance_type == "full":
+        if FUSE_BN and self.channel_attention and self.guidance_type == "full":
             # the branches' last BN + ReLU, the concatenation and SE as one op
             ra = run_sequential_raw(self.feature_conv, depth)
             rb = run_sequential_raw(self.guide_conv, guide) if ra is not None else None
@@ -90,14 +92,12 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
                 xy = se_bn_cat(ra[0], rb[0], ra[2], rb[2], ra[3], rb[3],
                                self.SE_block.fc[0].weight, self.SE_block.fc[2].weight,
                                ra[1], rb[1])
-                return skip_reduce(run_sequential(self.comb_conv, xy), depth,
-                                   self.reduce.weight, self.reduce.bias)
+                return self._comb_reduce(xy, depth)
             if ra is not None:  # finish the feature branch unfused
                 x = batch_norm_act(ra[0], ra[2], ra[2].act, None, ra[3], ra[1])
                 second = run_sequential(self.guide_conv, guide)
                 xy = self.SE_block.forward_cat(x, second)
-                return skip_reduce(run_sequential(self.comb_conv, xy), depth,
-                                   self.reduce.weight, self.reduce.bias)
+                return self._comb_reduce(xy, depth)
         x = run_sequential(self.feature_conv, depth)
         if self.guidance_type == "full":
             second = run_sequential(self.guide_conv, guide)
@@ -109,8 +109,24 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
             xy = self.SE_block.forward_cat(x, second) if second is not None else self.SE_block(x)
         else:
             xy = x if second is None else _cat(x, second)
+        if FUSE_BN:
+            return self._comb_reduce(xy, depth)
         return skip_reduce(run_sequential(self.comb_conv, xy), depth, self.reduce.weight,
                            self.reduce.bias)
+
+    def _comb_reduce(self, xy, depth):
+        """comb_conv + reduce(residual + depth) with the comb_conv's last BN +
+        ReLU applied inside the skip kernel's operand load (nn.skip_reduce_bn)
+        where that runs (training, fp32, supported shapes)."""
+        rc = run_sequential_raw(self.comb_conv, xy)
+        if rc is None:
+            return skip_reduce(run_sequential(self.comb_conv, xy), depth, self.reduce.weight,
+                               self.reduce.bias)
+        y2, st2, bn2, pb2 = rc
+        if skip_reduce_bn_ok(y2, self.reduce.out_channels):
+            return skip_reduce_bn(y2, bn2, pb2, depth, self.reduce.weight, self.reduce.bias, st2)
+        x = batch_norm_act(y2, bn2, bn2.act, None, pb2, st2)
+        return skip_reduce(x, depth, self.reduce.weight, self.reduce.bias)
 
 
 def _cat(x, y):

@@ -49,6 +49,12 @@ SIGNATURES = {
     "mde_skip_reduce_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
     "mde_skip_reduce_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
                                    _vp, _int, _vp]),
+    "mde_skip_reduce_bn_supported": (_int, [_i64, _i64, _i64, _i64, _int]),
+    "mde_skip_reduce_bn_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_skip_reduce_bn_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
+                                      _int, _vp]),
+    "mde_skip_reduce_bn_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64,
+                                      _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_minmax_workspace": (_sz, [_i64]),
     "mde_minmax": (_int, [_vp, _i64, _vp, _vp, _int, _vp]),
     "mde_depthnorm_apply": (_int, [_vp, _vp, _vp, _i64, _int, _vp]),

@@ -16,12 +16,16 @@ namespace {
 
 constexpr int kMaxC = 64;
 
-template <int CO, int PPT>
+// BNR (here and in the kernels below): r is the raw input of a BatchNorm +
+// ReLU (the comb_conv's last, modules.py:72-73) applied on load,
+// s = relu(r * isc[c] + ish[c]) + d, so its output is never written.
+template <int CO, int PPT, bool BNR = false>
 __global__ void __launch_bounds__(256)
     skip_fwd_kernel(const float* __restrict__ r, const float* __restrict__ d,
                     const float* __restrict__ wt, const float* __restrict__ b,
                     float* __restrict__ out, int64_t n, int cin, int cout,
-                    int64_t hw) {
+                    int64_t hw, const float* __restrict__ isc = nullptr,
+                    const float* __restrict__ ish = nullptr) {
   __shared__ float sw[kMaxC * kMaxC];
   __shared__ float sb[kMaxC];
   for (int i = threadIdx.x; i < cin * cout; i += blockDim.x) sw[i] = wt[i];
@@ -44,17 +48,19 @@ __global__ void __launch_bounds__(256)
     }
     for (int c = 0; c < cin; ++c) {
       float s[PPT];
+      const float bs = BNR ? isc[c] : 1.f, bh = BNR ? ish[c] : 0.f;
+      auto act = [&](float v) { return BNR ? fmaxf(v * bs + bh, 0.f) : v; };
       if (PPT == 4) {
         const float4 a = *reinterpret_cast<const float4*>(rp + c * hw);
         const float4 e = *reinterpret_cast<const float4*>(dp + c * hw);
-        s[0] = a.x + e.x; s[1 % PPT] = a.y + e.y;
-        s[2 % PPT] = a.z + e.z; s[3 % PPT] = a.w + e.w;
+        s[0] = act(a.x) + e.x; s[1 % PPT] = act(a.y) + e.y;
+        s[2 % PPT] = act(a.z) + e.z; s[3 % PPT] = act(a.w) + e.w;
       } else if (PPT == 2) {
         const float2 a = *reinterpret_cast<const float2*>(rp + c * hw);
         const float2 e = *reinterpret_cast<const float2*>(dp + c * hw);
-        s[0] = a.x + e.x; s[1 % PPT] = a.y + e.y;
+        s[0] = act(a.x) + e.x; s[1 % PPT] = act(a.y) + e.y;
       } else {
-        s[0] = rp[c * hw] + dp[c * hw];
+        s[0] = act(rp[c * hw]) + dp[c * hw];
       }
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
@@ -200,14 +206,20 @@ __global__ void __launch_bounds__(kTile)
 // Small weights (cin*cout + cout <= 64, e.g. up_3's 16 -> 1): every thread
 // keeps ALL weight-gradient partials in registers over its grid-stride pixels
 // (4 consecutive pixels per step, float4), then one block reduction — no LDS
-// staging per tile.
-template <int CI, int CO>
+// staging per tile.  BNR: s = relu(r * isc + ish) + d (see skip_fwd_kernel);
+// BNS (with BNR): also that BatchNorm's backward sums sum e, sum e (r -
+// imean[c]) with e = gs [r * isc + ish > 0], appended to the slab row.
+template <int CI, int CO, bool BNR = false, bool BNS = false>
 __global__ void __launch_bounds__(256)
     skip_bwd_reg_kernel(const float* __restrict__ g, const float* __restrict__ r,
                         const float* __restrict__ d, const float* __restrict__ wt,
                         float* __restrict__ gs, float* __restrict__ slab, int64_t n,
-                        int64_t hw) {
-  constexpr int NP = CI * CO + CO;
+                        int64_t hw, const float* __restrict__ isc = nullptr,
+                        const float* __restrict__ ish = nullptr,
+                        const float* __restrict__ imean = nullptr) {
+  static_assert(!BNS || BNR, "BN sums need the fused BN-ReLU operand");
+  constexpr int NW = CI * CO + CO;
+  constexpr int NP = NW + (BNS ? 2 * CI : 0);
   __shared__ float sw[CI * CO];
   __shared__ float red[4][NP];
   for (int i = threadIdx.x; i < CI * CO; i += 256) sw[i] = wt[i];
@@ -230,7 +242,13 @@ __global__ void __launch_bounds__(256)
       const int64_t off = (nidx * CI + c) * hw + p;
       const float4 a = *reinterpret_cast<const float4*>(r + off);
       const float4 e = *reinterpret_cast<const float4*>(d + off);
-      const float4 sv = make_float4(a.x + e.x, a.y + e.y, a.z + e.z, a.w + e.w);
+      float bs = 1.f, bh = 0.f;
+      if (BNR) {
+        bs = isc[c];
+        bh = ish[c];
+      }
+      auto act = [&](float v) { return BNR ? fmaxf(v * bs + bh, 0.f) : v; };
+      const float4 sv = make_float4(act(a.x) + e.x, act(a.y) + e.y, act(a.z) + e.z, act(a.w) + e.w);
       float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
@@ -239,6 +257,16 @@ __global__ void __launch_bounds__(256)
         acc[o * CI + c] += (gv[o].x * sv.x + gv[o].y * sv.y) + (gv[o].z * sv.z + gv[o].w * sv.w);
       }
       *reinterpret_cast<float4*>(gs + off) = o4;
+      if constexpr (BNS) {
+        const float mu = imean[c];
+        const float av[4] = {a.x, a.y, a.z, a.w}, ov[4] = {o4.x, o4.y, o4.z, o4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float ev = av[j] * bs + bh > 0.f ? ov[j] : 0.f;
+          acc[NW + 2 * c] += ev;
+          acc[NW + 2 * c + 1] += ev * (av[j] - mu);
+        }
+      }
     }
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -293,7 +321,7 @@ __global__ void __launch_bounds__(256, 2)
   // are zero operands and are not stored); K of gs = W^T G is CO in steps of 4.
   constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = CO / 4;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
-  static_assert(!BNS || (BNR && !HAS_D && CI <= 32), "BN sums: fused BN-ReLU operand, cin <= 32");
+  static_assert(!BNS || (BNR && CI <= 32), "BN sums: fused BN-ReLU operand, cin <= 32");
   constexpr int ROW = CO * CI + CO + (BNS ? 2 * CI : 0);  // slab row
   __shared__ float red[4][ROW];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
@@ -418,15 +446,15 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
           float4 x = mde::ld4(ra + 16 * v);
-          if (HAS_D) {
-            const float4 y = mde::ld4(dp + (16 * mt + l16) * hw + 4 * q4 + 16 * v);
-            x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
-          }
-          if (BNR) {
+          if (BNR) {  // BN + ReLU of r, then + d (HAS_D)
             x.x = fmaxf(x.x * bsc[mt] + bsh[mt], 0.f);
             x.y = fmaxf(x.y * bsc[mt] + bsh[mt], 0.f);
             x.z = fmaxf(x.z * bsc[mt] + bsh[mt], 0.f);
             x.w = fmaxf(x.w * bsc[mt] + bsh[mt], 0.f);
+          }
+          if (HAS_D) {
+            const float4 y = mde::ld4(dp + (16 * mt + l16) * hw + 4 * q4 + 16 * v);
+            x.x += y.x; x.y += y.y; x.z += y.z; x.w += y.w;
           }
           sb[4 * v] = x.x; sb[4 * v + 1] = x.y; sb[4 * v + 2] = x.z; sb[4 * v + 3] = x.w;
         }
@@ -543,15 +571,15 @@ __global__ void __launch_bounds__(256)
     for (int kk = 0; kk < KC; ++kk) {
       const int64_t off = (int64_t)(4 * kk + q4) * hw;
       float4 v = mde::ld4(rp + off);
-      if (HAS_D) {
-        const float4 e = mde::ld4(dp + off);
-        v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
-      }
-      if (BNR) {
+      if (BNR) {  // BN + ReLU of r, then + d (HAS_D)
         v.x = fmaxf(v.x * fsc[kk] + fsh[kk], 0.f);
         v.y = fmaxf(v.y * fsc[kk] + fsh[kk], 0.f);
         v.z = fmaxf(v.z * fsc[kk] + fsh[kk], 0.f);
         v.w = fmaxf(v.w * fsc[kk] + fsh[kk], 0.f);
+      }
+      if (HAS_D) {
+        const float4 e = mde::ld4(dp + off);
+        v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
       }
       sb[kk] = v;
     }
@@ -801,6 +829,105 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
   MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s,
              skip_slab_reduce_kernel, dim3((unsigned)stride), dim3(256), 0, slab,
              nb, (int)(cin * cout), (int)cout, gw, gb);
+  return MDE_OK;
+}
+
+// ---- skip fusion over the comb_conv's last BatchNorm + ReLU: r is that BN's
+// raw input (the 1x1 conv output without its folded bias), in_scale /
+// in_shift its coefficients; out = b + W (relu(in_scale r + in_shift) + d).
+// Shapes: the MFMA 64 -> 32 / 32 -> 16 (h*w % 64 == 0) and the register
+// 16 -> 1 / 4 -> 1 (h*w % 4 == 0) kernels; the backward's BN sums (in_sums
+// [cin][2] = sum e, sum e (r - in_mean), e = gs [in_scale r + in_shift > 0],
+// for mde_batchnorm_bwd_apply) on all but 64 -> 32.
+static bool skip_bn_reg(int64_t cin, int64_t cout, int64_t hw) {
+  return hw % 4 == 0 && cout == 1 && (cin == 16 || cin == 4);
+}
+
+int mde_skip_reduce_bn_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int sums) {
+  const int64_t hw = h * w;
+  if (skip_bn_reg(cin, cout, hw)) return 1;
+  if (!skip_mfma_shape(cin, cout, hw)) return 0;
+  return (!sums || cin <= 32) ? 1 : 0;
+}
+
+size_t mde_skip_reduce_bn_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  return sizeof(float) * (size_t)bwd_blocks(n, h * w) * (size_t)(cin * cout + cout + 2 * cin);
+}
+
+int mde_skip_reduce_bn_fwd(const void* r, const void* d, const float* in_scale,
+                           const float* in_shift, const float* wt, const float* b, void* out,
+                           int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                           void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!r || !d || !in_scale || !in_shift || !wt || !b || !out || n <= 0 || hw <= 0)
+    return MDE_ERR_INVALID_ARG;
+  if (!mde_skip_reduce_bn_supported(cin, cout, h, w, 0)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const double bytes = 4.0 * n * hw * (double)(2 * cin + cout);
+  const float *R = (const float*)r, *D = (const float*)d;
+  if (skip_bn_reg(cin, cout, hw)) {
+    const int64_t blocks = mde::cdiv(n * hw / 4, 256);
+    const dim3 g((unsigned)(blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks)));
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_kernel<1, 4, true>), g, dim3(256), 0, R, D, wt,
+               b, (float*)out, n, (int)cin, (int)cout, hw, in_scale, in_shift);
+    return MDE_OK;
+  }
+  const int64_t blocks = mde::cdiv(n * hw / 64, 4);
+  const dim3 g((unsigned)(blocks > 4096 ? 4096 : blocks));
+  if (cin == 64)
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32, true, true>), g, dim3(256),
+               0, R, D, wt, b, (float*)out, n, hw, in_scale, in_shift, nullptr);
+  else
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<32, 16, true, true>), g, dim3(256),
+               0, R, D, wt, b, (float*)out, n, hw, in_scale, in_shift, nullptr);
+  return MDE_OK;
+}
+
+int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const float* in_scale,
+                           const float* in_shift, const float* in_mean, const float* wt, void* gs,
+                           float* gw, float* gb, float* in_sums, int64_t n, int64_t cin,
+                           int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                           void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!gout || !r || !d || !in_scale || !in_shift || !wt || !gs || !gw || !gb || !workspace ||
+      n <= 0 || hw <= 0 || (in_sums && !in_mean))
+    return MDE_ERR_INVALID_ARG;
+  if (!mde_skip_reduce_bn_supported(cin, cout, h, w, in_sums != nullptr)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int nb = bwd_blocks(n, hw);
+  float* slab = (float*)workspace;
+  const double bytes = 4.0 * n * hw * (double)(3 * cin + cout);
+  const float *G = (const float*)gout, *R = (const float*)r, *D = (const float*)d;
+  float* GS = (float*)gs;
+  const bool sums = in_sums != nullptr;
+  if (cin == 16 && sums)
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<16, 1, true, true>), dim3(nb),
+               dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  else if (cin == 16)
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<16, 1, true, false>), dim3(nb),
+               dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  else if (cin == 4 && sums)
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1, true, true>), dim3(nb),
+               dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  else if (cin == 4)
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1, true, false>), dim3(nb),
+               dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  else if (cin == 64)
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32, true, true, false>),
+               dim3(nb), dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  else if (sums)
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true, true, true>),
+               dim3(nb), dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  else
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true, true, false>),
+               dim3(nb), dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
+  const int npairs = (int)(cin * cout);
+  const int nextra = sums ? (int)(2 * cin) : 0;
+  MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * (npairs + cout + nextra), s,
+             skip_slab_reduce_kernel, dim3((unsigned)(npairs + cout + nextra)), dim3(256), 0, slab,
+             nb, npairs, (int)cout, gw, gb, nextra, in_sums);
   return MDE_OK;
 }
 

@@ -545,29 +545,128 @@ def run_sequential(seq: nn.Sequential, x):
 
 def run_sequential_raw(seq: nn.Sequential, x):
     """For Conv(bias) -> BN(relu) -> ReLU slot -> 1x1 Conv(bias) -> BN(relu) ->
-    ReLU slot on the fused HIP path in training mode (fp32): run it WITHOUT
-    the last BatchNorm + ReLU and return (y2, stats2, bn2, conv2_bias) -- the
-    last BN's raw input, its epilogue statistics, the BN module and its folded
-    bias -- for a consumer that applies that BN itself (se_bn_cat).  None when
-    the pattern or the conditions do not hold (then run_sequential(seq, x))."""
+    ReLU slot in training mode (fp32): run it WITHOUT the last BatchNorm + ReLU
+    and return (y2, stats2, bn2, conv2_bias) -- the last BN's raw input, its
+    per-block statistics from the 1x1 conv's epilogue (None when that conv is
+    not the HIP pointwise kernel), the BN module and its folded bias -- for a
+    consumer that applies that BN itself (se_bn_cat, skip_reduce_bn).  None
+    when the pattern or the conditions do not hold (then run_sequential)."""
     mods = list(seq)
     if (len(mods) != 6 or not x.is_cuda or x.dtype != torch.float32
             or torch.is_autocast_enabled() or not _bnrelu_pw_at(mods, 0, x.shape)
             or not isinstance(mods[5], nn.Identity) or mods[4].act != "relu"
             or not mods[1].training or not mods[4].training):
         return None
-    m = mods[0]
+    m, c1 = mods[0], mods[3]
     k = m.kernel_size
-    if (m.stride != (1, 1) or m.dilation != (1, 1) or m.padding != (k[0] // 2, k[1] // 2)
-            or k[0] % 2 == 0 or k[1] % 2 == 0 or not pointwise_ok(mods[3], x)):
-        return None  # y1 keeps x's H x W, which pointwise_ok checked
+    same = (m.stride == (1, 1) and m.dilation == (1, 1) and k[0] % 2 == 1 and k[1] % 2 == 1
+            and m.padding == (k[0] // 2, k[1] // 2))
     passes = conv3x3_passes(m, x)
     if passes is not None:
         y1, st1 = conv3x3_stats(x, m.weight, passes)
     else:
         y1, st1 = conv_nobias(m, x), None
-    y2, st2 = bn_relu_pointwise(y1, mods[1], m.bias, mods[3], st1, True)
-    return y2, st2, mods[4], mods[3].bias
+    if same and pointwise_ok(c1, x):  # y1 keeps x's H x W, which pointwise_ok checked
+        y2, st2 = bn_relu_pointwise(y1, mods[1], m.bias, c1, st1, True)
+        return y2, st2, mods[4], c1.bias
+    x1 = batch_norm_act(y1, mods[1], "relu", None, m.bias, st1)
+    y2 = torch.nn.functional.conv2d(x1, c1.weight, None, c1.stride, c1.padding, c1.dilation,
+                                    c1.groups)
+    return y2, None, mods[4], c1.bias
+
+
+class _SkipReduceBN(torch.autograd.Function):
+    """reduce(relu(bn(r + prebias)) + d) (the comb_conv's last BatchNorm + ReLU
+    and the skip fusion, modules.py:72-73,100) with the BN + ReLU applied in
+    the skip kernel's operand load: the BN output is never written, and the
+    skip backward forms the BN backward's sums where the shape allows, so the
+    BN runs its apply pass only."""
+
+    @staticmethod
+    @_amp_fwd
+    def forward(ctx, r, d, weight, bias, gamma, beta, prebias, meta, stats):
+        r, d = r.contiguous(), d.contiguous()
+        n, cin, h, w = r.shape
+        cout = weight.shape[0]
+        wm = weight.reshape(cout, cin).contiguous()
+        f32 = dict(dtype=torch.float32, device=r.device)
+        scale, shift = torch.empty(cin, **f32), torch.empty(cin, **f32)
+        mean, invstd = torch.empty(cin, **f32), torch.empty(cin, **f32)
+        rm, rv, nbt, momentum, eps = meta
+        st = _abi.stream_of(r)
+        ws = _ws(_abi.query("mde_batchnorm_workspace", n, cin, h, w), r)
+        if stats is not None:
+            _abi.call("mde_batchnorm_fwd_coef_stats", _abi.ptr(r), _abi.ptr(gamma), _abi.ptr(beta),
+                      _abi.ptr(prebias), _abi.ptr(rm), _abi.ptr(rv), _abi.ptr(nbt), float(momentum),
+                      float(eps), _abi.ptr(scale), _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(invstd),
+                      n, cin, h, w, _abi.ptr(stats), stats.shape[1], _abi.ptr(ws),
+                      _abi.dtype_code(r), st)
+        else:
+            _abi.call("mde_batchnorm_fwd_coef", _abi.ptr(r), _abi.ptr(gamma), _abi.ptr(beta),
+                      _abi.ptr(prebias), _abi.ptr(rm), _abi.ptr(rv), _abi.ptr(nbt), float(momentum),
+                      float(eps), 1, _abi.ptr(scale), _abi.ptr(shift), _abi.ptr(mean),
+                      _abi.ptr(invstd), n, cin, h, w, _abi.ptr(ws), _abi.dtype_code(r), st)
+        out = torch.empty((n, cout, h, w), **f32)
+        _abi.call("mde_skip_reduce_bn_fwd", _abi.ptr(r), _abi.ptr(d), _abi.ptr(scale),
+                  _abi.ptr(shift), _abi.ptr(wm), _abi.ptr(bias), _abi.ptr(out), n, cin, cout, h, w,
+                  _abi.dtype_code(r), st)
+        ctx.save_for_backward(r, d, wm, gamma, beta, scale, shift, mean, invstd)
+        ctx.wshape, ctx.has_pb = weight.shape, prebias is not None
+        return out
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, gout):
+        r, d, wm, gamma, beta, scale, shift, mean, invstd = ctx.saved_tensors
+        gout = gout.contiguous()
+        n, cin, h, w = r.shape
+        cout = wm.shape[0]
+        st = _abi.stream_of(gout)
+        gs = torch.empty_like(r)  # d/d(relu output) == d/dd
+        gw, gb = torch.empty_like(wm), torch.empty(cout, dtype=torch.float32, device=r.device)
+        use_sums = bool(_abi.query("mde_skip_reduce_bn_supported", cin, cout, h, w, 1))
+        sums = torch.empty((cin, 2), dtype=torch.float32, device=r.device) if use_sums else None
+        ws = _ws(_abi.query("mde_skip_reduce_bn_workspace", n, cin, cout, h, w), r)
+        _abi.call("mde_skip_reduce_bn_bwd", _abi.ptr(gout), _abi.ptr(r), _abi.ptr(d),
+                  _abi.ptr(scale), _abi.ptr(shift), _abi.ptr(mean), _abi.ptr(wm), _abi.ptr(gs),
+                  _abi.ptr(gw), _abi.ptr(gb), _abi.ptr(sums), n, cin, cout, h, w, _abi.ptr(ws),
+                  _abi.dtype_code(gout), st)
+        gr = torch.empty_like(r)
+        gg, gbeta = torch.empty_like(gamma), torch.empty_like(beta)
+        gpb = torch.empty_like(gamma) if (ctx.has_pb and ctx.needs_input_grad[6]) else None
+        if sums is not None:
+            _abi.call("mde_batchnorm_bwd_apply", _abi.ptr(gs), _abi.ptr(r), None, _abi.ptr(gamma),
+                      _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), 1, _abi.ptr(sums),
+                      _abi.ptr(gr), None, _abi.ptr(gg), _abi.ptr(gbeta), _abi.ptr(gpb), n, cin, h,
+                      w, _ACTS["relu"], _abi.dtype_code(gout), st)
+        else:
+            ws2 = _ws(_abi.query("mde_batchnorm_workspace", n, cin, h, w), r)
+            _abi.call("mde_batchnorm_bwd", _abi.ptr(gs), _abi.ptr(r), None, _abi.ptr(gamma),
+                      _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), 1, _abi.ptr(gr), None,
+                      _abi.ptr(gg), _abi.ptr(gbeta), _abi.ptr(gpb), n, cin, h, w, _ACTS["relu"],
+                      _abi.ptr(ws2), _abi.dtype_code(gout), st)
+        return gr, gs, gw.view(ctx.wshape), gb, gg, gbeta, gpb, None, None
+
+
+def skip_reduce_bn_ok(r, cout: int) -> bool:
+    """Whether skip_reduce_bn has a kernel for this (raw input, output channels)."""
+    return (r.dim() == 4 and r.dtype == torch.float32 and
+            bool(_abi.query("mde_skip_reduce_bn_supported", r.shape[1], cout, r.shape[2],
+                            r.shape[3], 0)))
+
+
+def skip_reduce_bn(r, bn: nn.BatchNorm2d, prebias, d, weight, bias, stats=None):
+    """reduce(relu(bn(r + prebias)) + d) (modules.py:72-73,100) on the fused HIP
+    path: r is the comb_conv's last 1x1 conv output without its bias (folded
+    as `prebias`), bn its training-mode BatchNorm, stats r's per-block
+    statistics from that conv's epilogue (or None: a statistics pass)."""
+    _gpu(r, d, prebias, weight, bias)
+    if bn.weight is None or bn.bias is None or bn.momentum is None or not bn.training:
+        raise NotImplementedError("skip_reduce_bn needs an affine, momentum, training-mode BatchNorm")
+    track = bn.track_running_stats
+    meta = (bn.running_mean if track else None, bn.running_var if track else None,
+            bn.num_batches_tracked if track else None, bn.momentum, bn.eps)
+    return _SkipReduceBN.apply(r, d, weight, bias, bn.weight, bn.bias, prebias, meta, stats)
 
 
 class BatchNorm2d(nn.BatchNorm2d):

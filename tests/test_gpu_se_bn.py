@@ -104,8 +104,9 @@ def test_se_bn_cat_vs_float64(n, ca, cb, h, w, offset):
                                         ((64, 64, 32), 2, 12, 16), ((16, 16, 1), 4, 120, 160)])
 def test_guided_block_fused_vs_unfused_and_float64(cfg, n, h, w):
     """A whole Guided_Upsampling_Block in training mode: the fused path (branches'
-    last BN + ReLU, cat and SE in se_bn_cat) against the unfused HIP path and the
-    oracle block in float64 -- output, input and parameter gradients, running stats."""
+    last BN + ReLU, cat and SE in se_bn_cat; the comb_conv's last BN + ReLU in
+    skip_reduce_bn) against the unfused HIP path and the oracle block in
+    float64 -- output, input and parameter gradients, running stats."""
     import copy
 
     from monocular_depth_estimation_amd.GuideDepth.model import modules
@@ -119,15 +120,15 @@ def test_guided_block_fused_vs_unfused_and_float64(cfg, n, h, w):
     gy = torch.from_numpy(seeded((n, cfg[2], h, w), 7, -1, 1))
 
     def run(mod, fused):
-        old = modules.FUSE_SE_BN
-        modules.FUSE_SE_BN = fused
+        old = modules.FUSE_BN
+        modules.FUSE_BN = fused
         try:
             gd = guide.to(DEV).requires_grad_(True)
             dp = depth.to(DEV).requires_grad_(True)
             y = mod(gd, dp)
             y.backward(gy.to(DEV))
         finally:
-            modules.FUSE_SE_BN = old
+            modules.FUSE_BN = old
         return y, gd.grad, dp.grad
 
     y, gg, gd = run(m, True)
@@ -152,3 +153,42 @@ def test_guided_block_fused_vs_unfused_and_float64(cfg, n, h, w):
             assert rel_err(b, rb[name]) <= 1e-5, name
         else:
             assert int(b) == int(rb[name]), name
+
+
+@pytest.mark.parametrize("n,cin,cout,h,w", [(2, 16, 1, 48, 64), (3, 4, 1, 10, 14), (2, 32, 16, 24, 32),
+                                            (2, 64, 32, 12, 16), (4, 16, 1, 120, 160)])
+def test_skip_reduce_bn_vs_float64(n, cin, cout, h, w):
+    """reduce(relu(bn(r + pb)) + d) (modules.py:72-73,100) on mde_skip_reduce_bn_*
+    vs float64 torch: output, d/dr, d/dd, weight / bias / BN parameter gradients,
+    running statistics.  Covers the register (16/4 -> 1) and MFMA (32 -> 16 with
+    the BN sums, 64 -> 32 without) kernels."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import skip_reduce_bn
+    assert _abi.query("mde_skip_reduce_bn_supported", cin, cout, h, w, 0)
+    torch.manual_seed(cin * 10 + cout + h)
+    r = torch.randn(n, cin, h, w) * 0.7 + 0.3
+    d = torch.randn(n, cin, h, w)
+    pb = torch.randn(cin) * 0.1
+    wt = torch.randn(cout, cin, 1, 1) / cin ** 0.5
+    b = torch.randn(cout) * 0.1
+    gout = torch.randn(n, cout, h, w)
+    bn = _bn(cin, 3)
+    ref = {k: v.double().requires_grad_(True) for k, v in dict(r=r, d=d, pb=pb, wt=wt, b=b).items()}
+    gam = bn.weight.detach().double().requires_grad_(True)
+    bet = bn.bias.detach().double().requires_grad_(True)
+    rm, rv = bn.running_mean.double().clone(), bn.running_var.double().clone()
+    z = torch.nn.functional.batch_norm(ref["r"] + ref["pb"].view(1, -1, 1, 1), rm, rv, gam, bet,
+                                       True, bn.momentum, bn.eps)
+    yr = torch.nn.functional.conv2d(torch.relu(z) + ref["d"], ref["wt"], ref["b"])
+    yr.backward(gout.double())
+    bn = bn.to(DEV).train()
+    g = {k: v.to(DEV).requires_grad_(True) for k, v in dict(r=r, d=d, pb=pb, wt=wt, b=b).items()}
+    y = skip_reduce_bn(g["r"], bn, g["pb"], g["d"], g["wt"], g["b"])
+    y.backward(gout.to(DEV))
+    assert rel_err(y, yr) <= 1e-5, "forward"
+    for k in ("r", "d", "wt", "b"):
+        assert rel_err(g[k].grad, ref[k].grad) <= 1e-4, k
+    assert rel_err(bn.weight.grad, gam.grad) <= 1e-4
+    assert rel_err(bn.bias.grad, bet.grad) <= 1e-4
+    assert float(g["pb"].grad.abs().max()) <= 1e-4 * float(bet.grad.abs().max())
+    assert rel_err(bn.running_mean, rm) <= 1e-5 and rel_err(bn.running_var, rv) <= 1e-5

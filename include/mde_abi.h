@@ -68,6 +68,16 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
                      int64_t hi, int64_t wi, int64_t ho, int64_t wo,
                      float scale_h, float scale_w, int align_corners,
                      int dtype, void* stream);
+/* x2 backward for an output read by two consumers whose gradients arrive
+ * separately (GuideDepth.py:49,52,55 -> the block's feature_conv and its skip
+ * fusion, modules.py:89,100): gx = adjoint(gy + gy2) with the sum formed on
+ * load.  Only the x2 column-pair shape (align_corners 0, scales 0.5, even wi);
+ * mde_bilinear_bwd2_supported says whether a shape is one. */
+int mde_bilinear_bwd2_supported(int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
+                                int64_t wo, float scale_h, float scale_w, int align_corners);
+int mde_bilinear_bwd2(const void* gy, const void* gy2, void* gx, int64_t n, int64_t c,
+                      int64_t hi, int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                      float scale_w, int align_corners, int dtype, void* stream);
 
 /* Nearest resize (PyTorch 'nearest': src = min(floor(dst*scale), in-1)).
  * Replaces F.interpolate(x, scale_factor=.5 / .25) at

@@ -8,7 +8,7 @@ from __future__ import annotations
 
 from torch import nn
 
-from ...functional import bilinear_resize, nearest_resize
+from ...functional import bilinear_resize_x2_slotted, nearest_resize
 from .DDRNet_23_slim import DualResNet_Backbone
 from .modules import Guided_Upsampling_Block
 
@@ -30,5 +30,7 @@ class GuideDepth(nn.Module):
         y = self.feature_extractor(x)
         guides = (nearest_resize(x, scale_factor=0.25), nearest_resize(x, scale_factor=0.5), x)
         for block, guide in zip((self.up_1, self.up_2, self.up_3), guides):
-            y = block(guide, bilinear_resize(y, scale_factor=2))
+            # the x2 upsample's backward also takes the skip fusion's gradient
+            # of it (GradSlot), so autograd adds no accumulation pass
+            y = block(guide, bilinear_resize_x2_slotted(y))
         return y

@@ -32,6 +32,9 @@ SIGNATURES = {
     "mde_status_string": (_c.c_char_p, [_int]),
     "mde_bilinear_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _int, _vp]),
     "mde_bilinear_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _int, _vp]),
+    "mde_bilinear_bwd2_supported": (_int, [_i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int]),
+    "mde_bilinear_bwd2": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int,
+                                 _int, _vp]),
     "mde_nearest_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _vp]),
     "mde_nearest_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _vp]),
     "mde_se_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),

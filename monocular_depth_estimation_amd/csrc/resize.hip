@@ -228,9 +228,14 @@ __global__ void __launch_bounds__(64 * kX2Warps)
 // store instruction per output row and column pair instead of 3 + 1 per
 // column.  Rows are processed in a fully unrolled kX2Rows window so the
 // loads of successive rows are all in flight together.
+// TWO: the output feeds two consumers whose gradients gy and gy2 arrive
+// separately (the guided-upsampling block's feature_conv and skip fusion,
+// modules.py:89,100): summed on load, so autograd's accumulation pass (read
+// both, write the sum, read it again here) never runs.
+template <bool TWO = false>
 __global__ void __launch_bounds__(64 * kX2Warps)
     bilinear_bwd_x2_pair_kernel(const float* __restrict__ gy, float* __restrict__ gx,
-                                int hi, int wi) {
+                                int hi, int wi, const float* __restrict__ gy2 = nullptr) {
   const int lane = threadIdx.x;
   const int j0 = 2 * (blockIdx.x * 64 + lane);  // input columns j0, j0 + 1
   const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
@@ -240,15 +245,27 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   const int64_t plane = blockIdx.z;
   const int ho = 2 * hi, wo = 2 * wi;
   const float* gp = gy + plane * ho * (int64_t)wo;
+  const float* gp2 = TWO ? gy2 + plane * ho * (int64_t)wo : nullptr;
   float* xp = gx + plane * hi * (int64_t)wi + jc;
   // pair-filtered row o: (gx-column j0 part, gx-column j0+1 part)
   auto hrow = [&](int o) {
     o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
     const float* row = gp + (int64_t)o * wo;
-    const float4 v = *reinterpret_cast<const float4*>(row + 2 * jc);
+    const float* row2 = TWO ? gp2 + (int64_t)o * wo : nullptr;
+    float4 v = *reinterpret_cast<const float4*>(row + 2 * jc);
+    if (TWO) {
+      const float4 v2 = *reinterpret_cast<const float4*>(row2 + 2 * jc);
+      v.x += v2.x; v.y += v2.y; v.z += v2.z; v.w += v2.w;
+    }
     float l = __shfl_up(v.w, 1, 64), r = __shfl_down(v.x, 1, 64);
-    if (lane == 0) l = row[2 * jc > 0 ? 2 * jc - 1 : 0];
-    if (lane == 63 || 2 * jc + 4 >= wo) r = row[2 * jc + 4 < wo ? 2 * jc + 4 : wo - 1];
+    if (lane == 0) {
+      const int e = 2 * jc > 0 ? 2 * jc - 1 : 0;
+      l = TWO ? row[e] + row2[e] : row[e];
+    }
+    if (lane == 63 || 2 * jc + 4 >= wo) {
+      const int e = 2 * jc + 4 < wo ? 2 * jc + 4 : wo - 1;
+      r = TWO ? row[e] + row2[e] : row[e];
+    }
     return make_float2(0.25f * l + 0.75f * v.x + 0.75f * v.y + 0.25f * v.z,
                        0.25f * v.y + 0.75f * v.z + 0.75f * v.w + 0.25f * r);
   };
@@ -723,9 +740,9 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<8>, xs_grid(planes, hi, wi),
                dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
   } else if (x2 && wi % 2 == 0) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel,
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel<false>,
                x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy,
-               (float*)gx, (int)hi, (int)wi);
+               (float*)gx, (int)hi, (int)wi, nullptr);
   } else if (x2) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
                x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
@@ -749,6 +766,34 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
                (const float*)gy, (float*)gx, planes, (int)hi, (int)wi,
                (int)ho, (int)wo, scale_h, scale_w, align_corners);
   }
+  return MDE_OK;
+}
+
+static bool x2_pair(int64_t planes, int64_t hi, int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                    float scale_w, int align_corners) {
+  return !align_corners && scale_h == 0.5f && scale_w == 0.5f && ho == 2 * hi && wo == 2 * wi &&
+         planes <= 65535 && wi % 2 == 0 &&
+         xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes) == 0;
+}
+
+int mde_bilinear_bwd2_supported(int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
+                                int64_t wo, float scale_h, float scale_w, int align_corners) {
+  return dims_ok(n, c, hi, wi, ho, wo) &&
+         x2_pair(n * c, hi, wi, ho, wo, scale_h, scale_w, align_corners);
+}
+
+int mde_bilinear_bwd2(const void* gy, const void* gy2, void* gx, int64_t n, int64_t c,
+                      int64_t hi, int64_t wi, int64_t ho, int64_t wo, float scale_h,
+                      float scale_w, int align_corners, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !gy2 || !gx || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
+  if (!x2_pair(n * c, hi, wi, ho, wo, scale_h, scale_w, align_corners))
+    return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const double bytes = 4.0 * n * c * (double)(hi * wi + 2 * ho * wo);
+  MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel<true>,
+             x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy, (float*)gx,
+             (int)hi, (int)wi, (const float*)gy2);
   return MDE_OK;
 }
 

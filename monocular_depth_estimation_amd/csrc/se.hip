@@ -376,30 +376,41 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Per channel (one thread each): S1, S2 in double over samples and chunks ->
-// the BN parameter gradients and the apply constants coef[ch] = (R, T) with
-// gy = m (P g + Q) + R + T (y - mean), P = sc s, Q = sc dm / HW (per sample).
+// Per channel (one block each): S1, S2 in double over (sample, chunk)
+// partials -> the BN parameter gradients and the apply constants coef[ch] =
+// (R, T) with gy = m (P g + Q) + R + T (y - mean), P = sc s, Q = sc dm / HW
+// (per sample).  Fixed per-thread order and a fixed tree: deterministic.
 __global__ void __launch_bounds__(256)
     sebn_bwd_combine_kernel(const float* __restrict__ part4, int chunks, int64_t n, int64_t c,
                             int64_t hw, const float* __restrict__ s, const float* __restrict__ dm,
                             const float* __restrict__ scale, const float* __restrict__ invstd,
                             int training, float* __restrict__ ggamma, float* __restrict__ gbeta,
                             float* __restrict__ coef) {
-  const int64_t ch = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
+  __shared__ double red[2][4];
+  const int64_t ch = blockIdx.x;
   const double inv_hw = 1.0 / (double)hw;
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t plane = i * c + ch;
-    double a = 0.0, b = 0.0, cc = 0.0, d = 0.0;
-    for (int k = 0; k < chunks; ++k) {
-      const float* p = part4 + 4 * (plane * chunks + k);
-      a += p[0]; b += p[1]; cc += p[2]; d += p[3];
-    }
+  for (int64_t i = threadIdx.x; i < n * chunks; i += 256) {
+    const int64_t plane = (i / chunks) * c + ch;
+    const float* p = part4 + 4 * (plane * chunks + i % chunks);
     const double sv = s[plane], q = (double)dm[plane] * inv_hw;
-    s1 += sv * a + q * b;
-    s2 += sv * cc + q * d;
+    s1 += sv * (double)p[0] + q * (double)p[1];
+    s2 += sv * (double)p[2] + q * (double)p[3];
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wid] = s1;
+    red[1][wid] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  s1 = (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+  s2 = (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
   const double is = invstd[ch], sc = scale[ch], cnt = (double)n * (double)hw;
   if (ggamma) ggamma[ch] = (float)(is * s2);
   if (gbeta) gbeta[ch] = (float)s1;
@@ -675,7 +686,7 @@ int mde_se_bn_bwd(const void* gout, const void* ya, int64_t ca, const void* yb, 
              se_wgrad_kernel, dim3((unsigned)mde::cdiv(2 * c * cr, 256)), dim3(256), 0, (int)n,
              (int)c, (int)cr, ws.dz, ws.dh, hidden, mean, gw1, gw2, nullptr, nullptr);
   MDE_LAUNCH(mde::K_SE_BWD_FC, 16.0 * n * c * chunks, st, sebn_bwd_combine_kernel,
-             dim3((unsigned)mde::cdiv(c, 256)), dim3(256), 0, ws.part4, chunks, n, c, hw, s,
+             dim3((unsigned)c), dim3(256), 0, ws.part4, chunks, n, c, hw, s,
              ws.dm, scale, bn_invstd, training, ggamma, gbeta, ws.coef);
   MDE_LAUNCH(mde::K_SE_BWD_APPLY, 3.0 * big, st, sebn_bwd_apply_kernel,
              dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)gout,

@@ -83,16 +83,37 @@ def _align_scale(inp: int, out: int) -> float:
     return 0.0
 
 
+class GradSlot:
+    """A gradient handed from a consumer's backward straight to the producer's
+    backward, bypassing autograd's accumulation add: the consumer returns None
+    for that input and `put`s its gradient here; the producer (which runs
+    after every consumer) sums it on load.  Used for the x2-upsampled `depth`
+    of the guided-upsampling blocks, read by feature_conv and the skip fusion."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+    def put(self, g):
+        self.grad = g if self.grad is None else self.grad + g
+
+    def take(self):
+        g, self.grad = self.grad, None
+        return g
+
+
 class _Bilinear(torch.autograd.Function):
     @staticmethod
     @_amp_fwd
-    def forward(ctx, x, ho, wo, sh, sw, align):
+    def forward(ctx, x, ho, wo, sh, sw, align, slot=None):
         x = x.contiguous()
         n, c, hi, wi = x.shape
         y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device)
         _abi.call("mde_bilinear_fwd", _abi.ptr(x), _abi.ptr(y), n, c, hi, wi, ho, wo,
                   sh, sw, int(align), _abi.dtype_code(x), _abi.stream_of(x))
         ctx.meta = (n, c, hi, wi, ho, wo, sh, sw, int(align))
+        ctx.slot = slot
         return y
 
     @staticmethod
@@ -101,9 +122,26 @@ class _Bilinear(torch.autograd.Function):
         n, c, hi, wi, ho, wo, sh, sw, align = ctx.meta
         gy = gy.contiguous()
         gx = torch.empty((n, c, hi, wi), dtype=gy.dtype, device=gy.device)
-        _abi.call("mde_bilinear_bwd", _abi.ptr(gy), _abi.ptr(gx), n, c, hi, wi, ho, wo,
-                  sh, sw, align, _abi.dtype_code(gy), _abi.stream_of(gy))
-        return gx, None, None, None, None, None
+        g2 = ctx.slot.take() if ctx.slot is not None else None
+        if g2 is not None:  # the other consumer's gradient, summed on load
+            _abi.call("mde_bilinear_bwd2", _abi.ptr(gy), _abi.ptr(g2.to(gy.dtype).contiguous()),
+                      _abi.ptr(gx), n, c, hi, wi, ho, wo, sh, sw, align, _abi.dtype_code(gy),
+                      _abi.stream_of(gy))
+        else:
+            _abi.call("mde_bilinear_bwd", _abi.ptr(gy), _abi.ptr(gx), n, c, hi, wi, ho, wo,
+                      sh, sw, align, _abi.dtype_code(gy), _abi.stream_of(gy))
+        return gx, None, None, None, None, None, None
+
+
+def bilinear_slot(x, ho, wo, sh, sw, align) -> Optional[GradSlot]:
+    """A GradSlot for bilinear_resize's output when its backward can take a
+    second gradient (the x2 pair kernel, fp32, autograd recording), else None."""
+    if (not torch.is_grad_enabled() or not x.requires_grad or x.dtype != torch.float32
+            or torch.is_autocast_enabled()):
+        return None
+    n, c, hi, wi = x.shape
+    ok = _abi.query("mde_bilinear_bwd2_supported", n, c, hi, wi, ho, wo, sh, sw, int(align))
+    return GradSlot() if ok else None
 
 
 class _Nearest(torch.autograd.Function):
@@ -143,6 +181,20 @@ def bilinear_resize(x, size=None, scale_factor=None, align_corners=False,
     if align_corners:
         sh, sw = _align_scale(x.shape[-2], ho), _align_scale(x.shape[-1], wo)
     return _Bilinear.apply(x, ho, wo, sh, sw, bool(align_corners))
+
+
+def bilinear_resize_x2_slotted(x):
+    """bilinear_resize(x, scale_factor=2) whose output carries a GradSlot
+    (`y._mde_grad_slot`, or None) that one of its consumers may hand its
+    gradient to (GuideDepth.py:49,52,55; see GradSlot)."""
+    _gpu(x)
+    if x.dim() != 4:
+        raise ValueError("bilinear_resize expects a 4-D NCHW tensor")
+    ho, wo, sh, sw = _out_size_and_scales(x, None, 2, None)
+    slot = bilinear_slot(x, ho, wo, sh, sw, False)
+    y = _Bilinear.apply(x, ho, wo, sh, sw, False, slot)
+    y._mde_grad_slot = slot
+    return y
 
 
 def nearest_resize(x, size=None, scale_factor=None, recompute_scale_factor=None):

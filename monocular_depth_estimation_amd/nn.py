@@ -584,7 +584,7 @@ class _SkipReduceBN(torch.autograd.Function):
 
     @staticmethod
     @_amp_fwd
-    def forward(ctx, r, d, weight, bias, gamma, beta, prebias, meta, stats):
+    def forward(ctx, r, d, weight, bias, gamma, beta, prebias, meta, stats, d_slot=None):
         r, d = r.contiguous(), d.contiguous()
         n, cin, h, w = r.shape
         cout = weight.shape[0]
@@ -611,7 +611,7 @@ class _SkipReduceBN(torch.autograd.Function):
                   _abi.ptr(shift), _abi.ptr(wm), _abi.ptr(bias), _abi.ptr(out), n, cin, cout, h, w,
                   _abi.dtype_code(r), st)
         ctx.save_for_backward(r, d, wm, gamma, beta, scale, shift, mean, invstd)
-        ctx.wshape, ctx.has_pb = weight.shape, prebias is not None
+        ctx.wshape, ctx.has_pb, ctx.d_slot = weight.shape, prebias is not None, d_slot
         return out
 
     @staticmethod
@@ -645,7 +645,12 @@ class _SkipReduceBN(torch.autograd.Function):
                       _abi.ptr(beta), _abi.ptr(mean), _abi.ptr(invstd), 1, _abi.ptr(gr), None,
                       _abi.ptr(gg), _abi.ptr(gbeta), _abi.ptr(gpb), n, cin, h, w, _ACTS["relu"],
                       _abi.ptr(ws2), _abi.dtype_code(gout), st)
-        return gr, gs, gw.view(ctx.wshape), gb, gg, gbeta, gpb, None, None
+        if ctx.d_slot is not None and ctx.needs_input_grad[1]:
+            ctx.d_slot.put(gs)  # d's producer sums it on load (functional.GradSlot)
+            gd = None
+        else:
+            gd = gs
+        return gr, gd, gw.view(ctx.wshape), gb, gg, gbeta, gpb, None, None, None
 
 
 def skip_reduce_bn_ok(r, cout: int) -> bool:
@@ -659,14 +664,17 @@ def skip_reduce_bn(r, bn: nn.BatchNorm2d, prebias, d, weight, bias, stats=None):
     """reduce(relu(bn(r + prebias)) + d) (modules.py:72-73,100) on the fused HIP
     path: r is the comb_conv's last 1x1 conv output without its bias (folded
     as `prebias`), bn its training-mode BatchNorm, stats r's per-block
-    statistics from that conv's epilogue (or None: a statistics pass)."""
+    statistics from that conv's epilogue (or None: a statistics pass).  When
+    d carries a GradSlot (functional.bilinear_resize_x2_slotted) d's gradient
+    goes there instead of through autograd."""
     _gpu(r, d, prebias, weight, bias)
     if bn.weight is None or bn.bias is None or bn.momentum is None or not bn.training:
         raise NotImplementedError("skip_reduce_bn needs an affine, momentum, training-mode BatchNorm")
     track = bn.track_running_stats
     meta = (bn.running_mean if track else None, bn.running_var if track else None,
             bn.num_batches_tracked if track else None, bn.momentum, bn.eps)
-    return _SkipReduceBN.apply(r, d, weight, bias, bn.weight, bn.bias, prebias, meta, stats)
+    return _SkipReduceBN.apply(r, d, weight, bias, bn.weight, bn.bias, prebias, meta, stats,
+                               getattr(d, "_mde_grad_slot", None))
 
 
 class BatchNorm2d(nn.BatchNorm2d):

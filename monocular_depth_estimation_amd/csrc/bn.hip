@@ -24,6 +24,8 @@
 // the residual), so y is never kept for the backward.
 #include <cmath>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -38,13 +40,21 @@ struct Geo {
   int64_t slice_len;     // multiple of 4 when hw % 4 == 0
 };
 
+// MDE_BN_TARGET / MDE_BN_MINSLICE override the two constants (tools/bn_bench.py sweeps)
+int64_t env_or(const char* name, int64_t dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoll(v) : dflt;
+}
+
 Geo geometry(int64_t n, int64_t c, int64_t hw) {
+  static const int64_t target = env_or("MDE_BN_TARGET", kTarget);
+  static const int64_t min_slice = env_or("MDE_BN_MINSLICE", kMinSlice);
   Geo g;
   g.c = c;
   g.hw = hw;
   g.total = n * hw;
-  int64_t s = mde::cdiv(kTarget, c);
-  const int64_t by_size = mde::cdiv(g.total, kMinSlice);
+  int64_t s = mde::cdiv(target, c);
+  const int64_t by_size = mde::cdiv(g.total, min_slice);
   if (s > by_size) s = by_size;
   if (s < 1) s = 1;
   if (s > 128) s = 128;

@@ -203,81 +203,99 @@ __global__ void __launch_bounds__(kTile)
   }
 }
 
-// Small weights (cin*cout + cout <= 64, e.g. up_3's 16 -> 1): every thread
-// keeps ALL weight-gradient partials in registers over its grid-stride pixels
-// (4 consecutive pixels per step, float4), then one block reduction — no LDS
-// staging per tile.  BNR: s = relu(r * isc + ish) + d (see skip_fwd_kernel);
-// BNS (with BNR): also that BatchNorm's backward sums sum e, sum e (r -
-// imean[c]) with e = gs [r * isc + ish > 0], appended to the slab row.
-template <int CI, int CO, bool BNR = false, bool BNS = false>
+// cout == 1 (up_3's 16 -> 1 reduce): a thread owns 4 channels of a 4-pixel
+// quad (lane % NG = channel group, NG = CI / 4), so its weight-gradient /
+// BN-sum accumulators are 4 + 8 registers instead of all channels' (a
+// thread-per-quad kernel holding all channels needed 358 registers with the
+// BN sums: one wave per SIMD, 537 us at cfg2's up_3).  The one gradient
+// channel g is re-read by the NG lanes of a quad (an L1 hit).
+// BNR: s = relu(r * isc + ish) + d (see skip_fwd_kernel); BNS (with BNR):
+// also that BatchNorm's backward sums sum e, sum e (r - imean[c]) with
+// e = gs [r * isc + ish > 0].  Slab row: [CI] weight gradient, [1] bias
+// gradient, [2 CI] BN sums.
+template <int CI, bool BNR = false, bool BNS = false>
 __global__ void __launch_bounds__(256)
-    skip_bwd_reg_kernel(const float* __restrict__ g, const float* __restrict__ r,
-                        const float* __restrict__ d, const float* __restrict__ wt,
-                        float* __restrict__ gs, float* __restrict__ slab, int64_t n,
-                        int64_t hw, const float* __restrict__ isc = nullptr,
-                        const float* __restrict__ ish = nullptr,
-                        const float* __restrict__ imean = nullptr) {
-  static_assert(!BNS || BNR, "BN sums need the fused BN-ReLU operand");
-  constexpr int NW = CI * CO + CO;
-  constexpr int NP = NW + (BNS ? 2 * CI : 0);
-  __shared__ float sw[CI * CO];
-  __shared__ float red[4][NP];
-  for (int i = threadIdx.x; i < CI * CO; i += 256) sw[i] = wt[i];
-  __syncthreads();
-  float acc[NP];
+    skip_bwd_c1_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                       const float* __restrict__ d, const float* __restrict__ wt,
+                       float* __restrict__ gs, float* __restrict__ slab, int64_t n, int64_t hw,
+                       const float* __restrict__ isc = nullptr,
+                       const float* __restrict__ ish = nullptr,
+                       const float* __restrict__ imean = nullptr) {
+  static_assert(CI % 4 == 0 && (!BNS || BNR), "channel groups of 4; BN sums need BNR");
+  constexpr int NG = CI / 4, QPB = 256 / NG;  // channel groups, quads per block pass
+  constexpr int ROW = CI + 1 + (BNS ? 2 * CI : 0);
+  __shared__ float red[4][ROW];
+  const int tid = threadIdx.x, grp = tid % NG, qi = tid / NG;
+  float w[4], bs[4], bh[4], mu[4];
 #pragma unroll
-  for (int k = 0; k < NP; ++k) acc[k] = 0.f;
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * grp + k;
+    w[k] = wt[c];
+    bs[k] = BNR ? isc[c] : 1.f;
+    bh[k] = BNR ? ish[c] : 0.f;
+    mu[k] = BNS ? imean[c] : 0.f;
+  }
+  float aw[4] = {}, e1[4] = {}, e2[4] = {}, ab = 0.f;
   const int64_t q4 = hw >> 2, total = n * q4;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t t = (int64_t)blockIdx.x * QPB + qi; t < total; t += (int64_t)gridDim.x * QPB) {
     const int64_t nidx = t / q4, p = (t - nidx * q4) << 2;
-    float4 gv[CO];
+    const float4 gv = *reinterpret_cast<const float4*>(g + nidx * hw + p);
+    if (grp == 0) ab += (gv.x + gv.y) + (gv.z + gv.w);
+    const int64_t base = (nidx * CI + 4 * grp) * hw + p;
+    float4 a[4], e[4];
 #pragma unroll
-    for (int o = 0; o < CO; ++o) {
-      gv[o] = *reinterpret_cast<const float4*>(g + (nidx * CO + o) * hw + p);
-      acc[CI * CO + o] += (gv[o].x + gv[o].y) + (gv[o].z + gv[o].w);
+    for (int k = 0; k < 4; ++k) {
+      a[k] = *reinterpret_cast<const float4*>(r + base + k * hw);
+      e[k] = *reinterpret_cast<const float4*>(d + base + k * hw);
     }
 #pragma unroll
-    for (int c = 0; c < CI; ++c) {
-      const int64_t off = (nidx * CI + c) * hw + p;
-      const float4 a = *reinterpret_cast<const float4*>(r + off);
-      const float4 e = *reinterpret_cast<const float4*>(d + off);
-      float bs = 1.f, bh = 0.f;
-      if (BNR) {
-        bs = isc[c];
-        bh = ish[c];
-      }
-      auto act = [&](float v) { return BNR ? fmaxf(v * bs + bh, 0.f) : v; };
-      const float4 sv = make_float4(act(a.x) + e.x, act(a.y) + e.y, act(a.z) + e.z, act(a.w) + e.w);
-      float4 o4 = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-      for (int o = 0; o < CO; ++o) {
-        const float w = sw[o * CI + c];
-        o4.x += w * gv[o].x; o4.y += w * gv[o].y; o4.z += w * gv[o].z; o4.w += w * gv[o].w;
-        acc[o * CI + c] += (gv[o].x * sv.x + gv[o].y * sv.y) + (gv[o].z * sv.z + gv[o].w * sv.w);
-      }
-      *reinterpret_cast<float4*>(gs + off) = o4;
+    for (int k = 0; k < 4; ++k) {
+      auto act = [&](float v) { return BNR ? fmaxf(v * bs[k] + bh[k], 0.f) : v; };
+      const float4 sv = make_float4(act(a[k].x) + e[k].x, act(a[k].y) + e[k].y,
+                                    act(a[k].z) + e[k].z, act(a[k].w) + e[k].w);
+      aw[k] += (gv.x * sv.x + gv.y * sv.y) + (gv.z * sv.z + gv.w * sv.w);
+      const float4 o4 = make_float4(w[k] * gv.x, w[k] * gv.y, w[k] * gv.z, w[k] * gv.w);
+      *reinterpret_cast<float4*>(gs + base + k * hw) = o4;
       if constexpr (BNS) {
-        const float mu = imean[c];
-        const float av[4] = {a.x, a.y, a.z, a.w}, ov[4] = {o4.x, o4.y, o4.z, o4.w};
+        const float av[4] = {a[k].x, a[k].y, a[k].z, a[k].w}, ov[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const float ev = av[j] * bs + bh > 0.f ? ov[j] : 0.f;
-          acc[NW + 2 * c] += ev;
-          acc[NW + 2 * c + 1] += ev * (av[j] - mu);
+          const float ev = av[j] * bs[k] + bh[k] > 0.f ? ov[j] : 0.f;
+          e1[k] += ev;
+          e2[k] += ev * (av[j] - mu[k]);
         }
       }
     }
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // lanes of one channel group: lane % NG equal -> butterfly over xor NG .. 32
+  auto gsum = [&](float v) {
 #pragma unroll
-  for (int k = 0; k < NP; ++k) {
-    const float v = mde::wave_sum(acc[k]);
-    if (lane == 0) red[wid][k] = v;
+    for (int o = NG; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const float sw = gsum(aw[k]);
+    float s1 = 0.f, s2 = 0.f;
+    if constexpr (BNS) {
+      s1 = gsum(e1[k]);
+      s2 = gsum(e2[k]);
+    }
+    if (lane < NG) {
+      const int c = 4 * lane + k;
+      red[wv][c] = sw;
+      if constexpr (BNS) {
+        red[wv][CI + 1 + 2 * c] = s1;
+        red[wv][CI + 1 + 2 * c + 1] = s2;
+      }
+    }
   }
+  const float sb = gsum(ab);  // only group-0 lanes hold bias partials
+  if (lane == 0) red[wv][CI] = sb;
   __syncthreads();
-  for (int k = threadIdx.x; k < NP; k += 256)
-    slab[(int64_t)blockIdx.x * NP + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+  for (int i = tid; i < ROW; i += 256)
+    slab[(int64_t)blockIdx.x * ROW + i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
 // MFMA backward for the full-size blocks (64 -> 32 at H/4, 32 -> 16 at H/2;
@@ -798,11 +816,11 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
              (const float*)r, (const float*)d, wt, (float*)gs, slab, n,      \
              (int)cin, (int)cout, hw)
   if (cin == 16 && cout == 1 && hw % 4 == 0) {
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<16, 1>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16>), dim3(nb),
                dim3(256), 0, (const float*)gout, (const float*)r, (const float*)d,
                wt, (float*)gs, slab, n, hw);
   } else if (cin == 4 && cout == 1 && hw % 4 == 0) {
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4>), dim3(nb),
                dim3(256), 0, (const float*)gout, (const float*)r, (const float*)d,
                wt, (float*)gs, slab, n, hw);
   } else if (cin == 64 && cout == 32 && hw % 64 == 0) {
@@ -903,16 +921,16 @@ int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const
   float* GS = (float*)gs;
   const bool sums = in_sums != nullptr;
   if (cin == 16 && sums)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<16, 1, true, true>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, true>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 16)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<16, 1, true, false>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, false>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 4 && sums)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1, true, true>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4, true, true>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 4)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_reg_kernel<4, 1, true, false>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4, true, false>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 64)
     MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32, true, true, false>),

@@ -419,7 +419,12 @@ class _Conv3x3(torch.autograd.Function):
                 _abi.call("mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx), n,
                           cin, cout, h, w, _abi.dtype_code(gy), st)
             else:
-                gx = torch.nn.grad.conv2d_input(x.shape, weight, gy, padding=1)
+                # MIOpen data gradient; the saved x stands in for the input
+                # (torch.nn.grad.conv2d_input passes an expanded dummy, which
+                # the backend materialises: a full-size copy per call)
+                gx = torch.ops.aten.convolution_backward(
+                    gy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                    (True, False, False))[0]
         if ctx.needs_input_grad[1]:
             if ctx.passes[2]:
                 gw = torch.empty_like(weight)
@@ -427,7 +432,9 @@ class _Conv3x3(torch.autograd.Function):
                 _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
                           cout, h, w, _abi.ptr(ws), _abi.dtype_code(gy), st)
             else:
-                gw = torch.nn.grad.conv2d_weight(x, weight.shape, gy, padding=1)
+                gw = torch.ops.aten.convolution_backward(
+                    gy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
+                    (False, True, False))[1]
         return gx, gw, None, None
 
 

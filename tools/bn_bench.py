@@ -1,5 +1,11 @@
 """BatchNorm pass timings at the cfg2 shapes (bs 32): statistics (fwd_coef),
-stats + apply (fwd_train), reduce + apply (bwd), apply alone (bwd_apply)."""
+stats + apply (fwd_train), reduce + apply (bwd), apply alone (bwd_apply).
+
+COLD=1: a 1 GiB scratch write before every timed call (evicts L2 / MALL, as
+in the train step where the DDRNet convolutions run between the BN passes);
+each call is timed alone with events.  SHAPES="c,h,w;..." overrides the list.
+"""
+import os
 import sys
 
 import torch
@@ -10,9 +16,26 @@ from monocular_depth_estimation_amd import _abi  # noqa: E402
 SHAPES = [(16, 240, 320), (32, 120, 160), (64, 60, 80), (8, 480, 640), (32, 240, 320), (128, 30, 40)]
 
 
+COLD = os.environ.get("COLD") == "1"
+_SCRATCH = []
+
+
 def t(fn, reps=20):
     for _ in range(3):
         fn()
+    if COLD:
+        if not _SCRATCH:
+            _SCRATCH.append(torch.empty(1 << 28, device="cuda"))
+        tot = 0.0
+        for _ in range(reps):
+            _SCRATCH[0].fill_(1.0)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            fn()
+            b.record()
+            torch.cuda.synchronize()
+            tot += a.elapsed_time(b)
+        return tot * 1e3 / reps
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     torch.cuda.synchronize()
     a.record()
@@ -26,7 +49,10 @@ def t(fn, reps=20):
 def main():
     n = 32
     f = dict(device="cuda", dtype=torch.float32)
-    for c, h, w in SHAPES:
+    shapes = SHAPES
+    if os.environ.get("SHAPES"):
+        shapes = [tuple(int(v) for v in e.split(",")) for e in os.environ["SHAPES"].split(";")]
+    for c, h, w in shapes:
         x = torch.randn((n, c, h, w), **f)
         gy = torch.randn_like(x)
         y, gx = torch.empty_like(x), torch.empty_like(x)

@@ -14,33 +14,31 @@ import numpy as np
 from ..functional import eval_sums
 
 
+# Result's fields in update()'s positional order (reference signature metrics.py:35-36).
+# Error metrics are "lower is better" (worst = inf); the delta accuracies and the two
+# timings are not (worst = 0).
+_UPDATE_ORDER = ("irmse", "imae", "mse", "rmse", "rmse_log", "mae", "absrel", "lg10",
+                 "delta1", "delta2", "delta3", "gpu_time", "data_time")
+_WORST = {f: (0 if f.startswith("delta") or f.endswith("_time") else np.inf)
+          for f in _UPDATE_ORDER}
+
+
 class Result:
     """Same fields and methods as the reference's Result (metrics.py:14-62)."""
 
     def __init__(self):
-        self.irmse, self.imae = 0, 0
-        self.mse, self.rmse, self.mae = 0, 0, 0
-        self.absrel, self.lg10 = 0, 0
-        self.delta1, self.delta2, self.delta3 = 0, 0, 0
-        self.data_time, self.gpu_time = 0, 0
-        self.rmse_log = 0
+        self.__dict__.update(dict.fromkeys(_UPDATE_ORDER, 0))
 
     def set_to_worst(self):
-        self.irmse, self.imae = np.inf, np.inf
-        self.mse, self.rmse, self.mae = np.inf, np.inf, np.inf
-        self.rmse_log = np.inf
-        self.absrel, self.lg10 = np.inf, np.inf
-        self.delta1, self.delta2, self.delta3 = 0, 0, 0
-        self.data_time, self.gpu_time = 0, 0
+        self.__dict__.update(_WORST)
 
-    def update(self, irmse, imae, mse, rmse, rmse_log, mae, absrel, lg10, delta1, delta2, delta3,
-               gpu_time, data_time):
-        self.irmse, self.imae = irmse, imae
-        self.mse, self.rmse, self.mae = mse, rmse, mae
-        self.rmse_log = rmse_log
-        self.absrel, self.lg10 = absrel, lg10
-        self.delta1, self.delta2, self.delta3 = delta1, delta2, delta3
-        self.data_time, self.gpu_time = data_time, gpu_time
+    def update(self, *values, **named):
+        """update(irmse, imae, mse, rmse, rmse_log, mae, absrel, lg10, delta1, delta2, delta3,
+        gpu_time, data_time) -- the reference's order, positional or by name."""
+        given = dict(zip(_UPDATE_ORDER, values), **named)
+        if len(values) > len(_UPDATE_ORDER) or set(given) != set(_UPDATE_ORDER):
+            raise TypeError(f"update() needs exactly the fields {_UPDATE_ORDER}")
+        self.__dict__.update(given)
 
     def evaluate(self, output, target):
         """All pixels of output / target (CUDA tensors of equal shape)."""

@@ -36,8 +36,9 @@ MFMA_F32_PEAK_TFS = 157.3  # fp32-input MFMA dense peak (= fp32 vector rate, MI3
 PMC_FILES = [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic.json") for r in (2, 1)]
 
 
-AMP_DTYPE = ("bf16 autocast: convs / GEMMs bf16 (MIOpen / hipBLASLt); BatchNorm HIP kernels bf16 "
-             "I/O with fp32 statistics; other HIP kernels fp32")
+AMP_DTYPE = ("bf16 autocast: convs / GEMMs bf16 (MIOpen / hipBLASLt); HIP BatchNorm, BN-ReLU-1x1, "
+             "skip fusion, SE-over-BN and x2 resize kernels bf16 I/O with fp32 statistics / "
+             "accumulation; other HIP kernels (guide conv3x3, DDRNet resizes, loss) fp32")
 
 
 def parse():

@@ -13,8 +13,9 @@
  *  - Plain pointers to DEVICE memory; the caller owns every buffer.
  *  - Tensors are dense NCHW, element type selected by `dtype`: MDE_F32
  *    everywhere; MDE_BF16 (activation / gradient storage, fp32 statistics and
- *    accumulation) for mde_batchnorm_fwd_train / _fwd_eval / _bwd; other entry
- *    points return MDE_ERR_UNSUPPORTED for it.
+ *    accumulation) for the BatchNorm, pointwise, skip_reduce(_bn), se_bn and
+ *    exact-x2 bilinear entry points (list: INTEGRATION.md "Element types");
+ *    other entry points return MDE_ERR_UNSUPPORTED for it.
  *  - Small parameter/statistics tensors (weights, scales, loss scalars,
  *    min/max) are always fp32.
  *  - `stream` is a hipStream_t (NULL = default stream).  No entry point

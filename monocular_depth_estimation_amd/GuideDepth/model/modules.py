@@ -3,7 +3,8 @@
 Drop-in for src/GuideDepth/model/modules.py: same constructors, forward
 signatures and state_dict keys.  Hot ops on HIP kernels:
   * cat([x, y], 1) + SELayer (:90, :21-25)  -> functional.se_cat (one fused op,
-    the concatenation is never materialised); in training (fp32) together with
+    the concatenation is never materialised); in training (fp32, or bf16 under
+    autocast) together with
     the two branches' last BatchNorm + ReLU (:49, :59) -> nn.se_bn_cat, which
     reads the 1x1 convs' raw outputs and writes only the SE output;
   * reduce(residual + depth) (:100)          -> functional.skip_reduce.
@@ -18,7 +19,7 @@ from ...functional import se_cat, skip_reduce
 from ...nn import (BatchNorm2d, batch_norm_act, run_sequential, run_sequential_raw, se_bn_cat,
                    skip_reduce_bn, skip_reduce_bn_ok)
 
-# Guided_Upsampling_Block (training, fp32): run the branches' last BN + ReLU,
+# Guided_Upsampling_Block (training; fp32, or bf16 storage under autocast): run the branches' last BN + ReLU,
 # the concatenation and SE as one fused op (nn.se_bn_cat), and the comb_conv's
 # last BN + ReLU inside the skip fusion's operand load (nn.skip_reduce_bn).
 FUSE_BN = True
@@ -117,7 +118,7 @@ class Guided_Upsampling_Block(nn.Module):  # noqa: N801  (reference class name)
     def _comb_reduce(self, xy, depth):
         """comb_conv + reduce(residual + depth) with the comb_conv's last BN +
         ReLU applied inside the skip kernel's operand load (nn.skip_reduce_bn)
-        where that runs (training, fp32, supported shapes)."""
+        where that runs (training, fp32 or bf16, supported shapes)."""
         rc = run_sequential_raw(self.comb_conv, xy)
         if rc is None:
             return skip_reduce(run_sequential(self.comb_conv, xy), depth, self.reduce.weight,

@@ -112,32 +112,33 @@ __global__ void __launch_bounds__(256)
 constexpr int kX2Rows = 8;   // rows per thread
 constexpr int kX2Warps = 4;  // threadIdx.y
 
-__device__ __forceinline__ float2 x2_hrow(const float* row, int j, int wi) {
-  const float l = row[j > 0 ? j - 1 : 0];
-  const float c = row[j];
-  const float r = row[j < wi - 1 ? j + 1 : wi - 1];
+template <typename T>
+__device__ __forceinline__ float2 x2_hrow(const T* row, int j, int wi) {
+  const float l = mde::ld1(row + (j > 0 ? j - 1 : 0));
+  const float c = mde::ld1(row + j);
+  const float r = mde::ld1(row + (j < wi - 1 ? j + 1 : wi - 1));
   return make_float2(0.25f * l + 0.75f * c, 0.75f * c + 0.25f * r);
 }
 
+template <typename T>
 __global__ void __launch_bounds__(64 * kX2Warps)
-    bilinear_fwd_x2_kernel(const float* __restrict__ x, float* __restrict__ y,
-                           int hi, int wi) {
+    bilinear_fwd_x2_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi) {
   const int j = blockIdx.x * 64 + threadIdx.x;
   const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
   if (j >= wi || i0 >= hi) return;
   const int64_t plane = blockIdx.z;
-  const float* xp = x + plane * hi * (int64_t)wi;
+  const T* xp = x + plane * hi * (int64_t)wi;
   const int wo = 2 * wi;
-  float* yp = y + plane * (2 * hi) * (int64_t)wo + 2 * j;
+  T* yp = y + plane * (2 * hi) * (int64_t)wo + 2 * j;
   float2 prev = x2_hrow(xp + (int64_t)(i0 > 0 ? i0 - 1 : 0) * wi, j, wi);
   float2 cur = x2_hrow(xp + (int64_t)i0 * wi, j, wi);
   const int i1 = i0 + kX2Rows < hi ? i0 + kX2Rows : hi;
   for (int i = i0; i < i1; ++i) {
     const float2 nxt = x2_hrow(xp + (int64_t)(i < hi - 1 ? i + 1 : hi - 1) * wi, j, wi);
-    *reinterpret_cast<float2*>(yp + (int64_t)(2 * i) * wo) =
-        make_float2(0.25f * prev.x + 0.75f * cur.x, 0.25f * prev.y + 0.75f * cur.y);
-    *reinterpret_cast<float2*>(yp + (int64_t)(2 * i + 1) * wo) =
-        make_float2(0.75f * cur.x + 0.25f * nxt.x, 0.75f * cur.y + 0.25f * nxt.y);
+    mde::st2(yp + (int64_t)(2 * i) * wo,
+             make_float2(0.25f * prev.x + 0.75f * cur.x, 0.25f * prev.y + 0.75f * cur.y));
+    mde::st2(yp + (int64_t)(2 * i + 1) * wo,
+             make_float2(0.75f * cur.x + 0.25f * nxt.x, 0.75f * cur.y + 0.25f * nxt.y));
     prev = cur;
     cur = nxt;
   }
@@ -146,9 +147,9 @@ __global__ void __launch_bounds__(64 * kX2Warps)
 // Forward with two input columns per thread (wi even): one float2 of each
 // input row (+ the neighbours from the adjacent lanes by wave shuffles)
 // gives four consecutive outputs of two output rows, written as float4.
+template <typename T>
 __global__ void __launch_bounds__(64 * kX2Warps)
-    bilinear_fwd_x2_pair_kernel(const float* __restrict__ x, float* __restrict__ y, int hi,
-                                int wi) {
+    bilinear_fwd_x2_pair_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi) {
   const int lane = threadIdx.x;
   const int j0 = 2 * (blockIdx.x * 64 + lane);
   const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
@@ -156,17 +157,17 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   const bool ok = j0 < wi;
   const int jc = ok ? j0 : 0;
   const int64_t plane = blockIdx.z;
-  const float* xp = x + plane * hi * (int64_t)wi;
+  const T* xp = x + plane * hi * (int64_t)wi;
   const int wo = 2 * wi;
-  float* yp = y + plane * (2 * hi) * (int64_t)wo + 2 * jc;
+  T* yp = y + plane * (2 * hi) * (int64_t)wo + 2 * jc;
   // horizontally interpolated input row r: outputs 2j0 .. 2j0+3
   auto hrow = [&](int r) {
     r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
-    const float* row = xp + (int64_t)r * wi;
-    const float2 c = *reinterpret_cast<const float2*>(row + jc);
+    const T* row = xp + (int64_t)r * wi;
+    const float2 c = mde::ld2(row + jc);
     float l = __shfl_up(c.y, 1, 64), rr = __shfl_down(c.x, 1, 64);
-    if (lane == 0) l = row[jc > 0 ? jc - 1 : 0];
-    if (lane == 63 || jc + 2 >= wi) rr = row[jc + 2 < wi ? jc + 2 : wi - 1];
+    if (lane == 0) l = mde::ld1(row + (jc > 0 ? jc - 1 : 0));
+    if (lane == 63 || jc + 2 >= wi) rr = mde::ld1(row + (jc + 2 < wi ? jc + 2 : wi - 1));
     return make_float4(0.25f * l + 0.75f * c.x, 0.75f * c.x + 0.25f * c.y,
                        0.25f * c.x + 0.75f * c.y, 0.75f * c.y + 0.25f * rr);
   };
@@ -177,12 +178,12 @@ __global__ void __launch_bounds__(64 * kX2Warps)
     if (i >= hi) break;  // uniform per wave
     const float4 nxt = hrow(i + 1);
     if (ok) {
-      *reinterpret_cast<float4*>(yp + (int64_t)(2 * i) * wo) =
-          make_float4(0.25f * prev.x + 0.75f * cur.x, 0.25f * prev.y + 0.75f * cur.y,
-                      0.25f * prev.z + 0.75f * cur.z, 0.25f * prev.w + 0.75f * cur.w);
-      *reinterpret_cast<float4*>(yp + (int64_t)(2 * i + 1) * wo) =
-          make_float4(0.75f * cur.x + 0.25f * nxt.x, 0.75f * cur.y + 0.25f * nxt.y,
-                      0.75f * cur.z + 0.25f * nxt.z, 0.75f * cur.w + 0.25f * nxt.w);
+      mde::st4(yp + (int64_t)(2 * i) * wo,
+               make_float4(0.25f * prev.x + 0.75f * cur.x, 0.25f * prev.y + 0.75f * cur.y,
+                           0.25f * prev.z + 0.75f * cur.z, 0.25f * prev.w + 0.75f * cur.w));
+      mde::st4(yp + (int64_t)(2 * i + 1) * wo,
+               make_float4(0.75f * cur.x + 0.25f * nxt.x, 0.75f * cur.y + 0.25f * nxt.y,
+                           0.75f * cur.z + 0.25f * nxt.z, 0.75f * cur.w + 0.25f * nxt.w));
     }
     prev = cur;
     cur = nxt;
@@ -190,23 +191,24 @@ __global__ void __launch_bounds__(64 * kX2Warps)
 }
 
 // 4-tap adjoint filter of one output-gradient row at input column j.
-__device__ __forceinline__ float x2_hgrad(const float* row, int j, int wo) {
-  const float2 m = *reinterpret_cast<const float2*>(row + 2 * j);
-  const float l = row[2 * j > 0 ? 2 * j - 1 : 0];
-  const float r = row[2 * j + 2 < wo ? 2 * j + 2 : wo - 1];
+template <typename T>
+__device__ __forceinline__ float x2_hgrad(const T* row, int j, int wo) {
+  const float2 m = mde::ld2(row + 2 * j);
+  const float l = mde::ld1(row + (2 * j > 0 ? 2 * j - 1 : 0));
+  const float r = mde::ld1(row + (2 * j + 2 < wo ? 2 * j + 2 : wo - 1));
   return 0.25f * l + 0.75f * m.x + 0.75f * m.y + 0.25f * r;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(64 * kX2Warps)
-    bilinear_bwd_x2_kernel(const float* __restrict__ gy, float* __restrict__ gx,
-                           int hi, int wi) {
+    bilinear_bwd_x2_kernel(const T* __restrict__ gy, T* __restrict__ gx, int hi, int wi) {
   const int j = blockIdx.x * 64 + threadIdx.x;
   const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
   if (j >= wi || i0 >= hi) return;
   const int64_t plane = blockIdx.z;
   const int ho = 2 * hi, wo = 2 * wi;
-  const float* gp = gy + plane * ho * (int64_t)wo;
-  float* xp = gx + plane * hi * (int64_t)wi + j;
+  const T* gp = gy + plane * ho * (int64_t)wo;
+  T* xp = gx + plane * hi * (int64_t)wi + j;
   auto hrow = [&](int o) {
     o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
     return x2_hgrad(gp + (int64_t)o * wo, j, wo);
@@ -215,7 +217,7 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   const int i1 = i0 + kX2Rows < hi ? i0 + kX2Rows : hi;
   for (int i = i0; i < i1; ++i) {
     const float c = hrow(2 * i + 1), d = hrow(2 * i + 2);
-    xp[(int64_t)i * wi] = 0.25f * a + 0.75f * b + 0.75f * c + 0.25f * d;
+    mde::st1(xp + (int64_t)i * wi, 0.25f * a + 0.75f * b + 0.75f * c + 0.25f * d);
     a = c;
     b = d;
   }
@@ -232,10 +234,10 @@ __global__ void __launch_bounds__(64 * kX2Warps)
 // separately (the guided-upsampling block's feature_conv and skip fusion,
 // modules.py:89,100): summed on load, so autograd's accumulation pass (read
 // both, write the sum, read it again here) never runs.
-template <bool TWO = false>
+template <bool TWO = false, typename T = float>
 __global__ void __launch_bounds__(64 * kX2Warps)
-    bilinear_bwd_x2_pair_kernel(const float* __restrict__ gy, float* __restrict__ gx,
-                                int hi, int wi, const float* __restrict__ gy2 = nullptr) {
+    bilinear_bwd_x2_pair_kernel(const T* __restrict__ gy, T* __restrict__ gx, int hi, int wi,
+                                const T* __restrict__ gy2 = nullptr) {
   const int lane = threadIdx.x;
   const int j0 = 2 * (blockIdx.x * 64 + lane);  // input columns j0, j0 + 1
   const int i0 = (blockIdx.y * kX2Warps + threadIdx.y) * kX2Rows;
@@ -244,27 +246,27 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   const int jc = ok ? j0 : 0;
   const int64_t plane = blockIdx.z;
   const int ho = 2 * hi, wo = 2 * wi;
-  const float* gp = gy + plane * ho * (int64_t)wo;
-  const float* gp2 = TWO ? gy2 + plane * ho * (int64_t)wo : nullptr;
-  float* xp = gx + plane * hi * (int64_t)wi + jc;
+  const T* gp = gy + plane * ho * (int64_t)wo;
+  const T* gp2 = TWO ? gy2 + plane * ho * (int64_t)wo : nullptr;
+  T* xp = gx + plane * hi * (int64_t)wi + jc;
   // pair-filtered row o: (gx-column j0 part, gx-column j0+1 part)
   auto hrow = [&](int o) {
     o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
-    const float* row = gp + (int64_t)o * wo;
-    const float* row2 = TWO ? gp2 + (int64_t)o * wo : nullptr;
-    float4 v = *reinterpret_cast<const float4*>(row + 2 * jc);
+    const T* row = gp + (int64_t)o * wo;
+    const T* row2 = TWO ? gp2 + (int64_t)o * wo : nullptr;
+    float4 v = mde::ld4(row + 2 * jc);
     if (TWO) {
-      const float4 v2 = *reinterpret_cast<const float4*>(row2 + 2 * jc);
+      const float4 v2 = mde::ld4(row2 + 2 * jc);
       v.x += v2.x; v.y += v2.y; v.z += v2.z; v.w += v2.w;
     }
     float l = __shfl_up(v.w, 1, 64), r = __shfl_down(v.x, 1, 64);
     if (lane == 0) {
       const int e = 2 * jc > 0 ? 2 * jc - 1 : 0;
-      l = TWO ? row[e] + row2[e] : row[e];
+      l = TWO ? mde::ld1(row + e) + mde::ld1(row2 + e) : mde::ld1(row + e);
     }
     if (lane == 63 || 2 * jc + 4 >= wo) {
       const int e = 2 * jc + 4 < wo ? 2 * jc + 4 : wo - 1;
-      r = TWO ? row[e] + row2[e] : row[e];
+      r = TWO ? mde::ld1(row + e) + mde::ld1(row2 + e) : mde::ld1(row + e);
     }
     return make_float2(0.25f * l + 0.75f * v.x + 0.75f * v.y + 0.25f * v.z,
                        0.25f * v.y + 0.75f * v.z + 0.75f * v.w + 0.25f * r);
@@ -276,9 +278,9 @@ __global__ void __launch_bounds__(64 * kX2Warps)
     if (i >= hi) break;  // uniform per wave
     const float2 c = hrow(2 * i + 1), d = hrow(2 * i + 2);
     if (ok)
-      *reinterpret_cast<float2*>(xp + (int64_t)i * wi) =
-          make_float2(0.25f * a.x + 0.75f * b.x + 0.75f * c.x + 0.25f * d.x,
-                      0.25f * a.y + 0.75f * b.y + 0.75f * c.y + 0.25f * d.y);
+      mde::st2(xp + (int64_t)i * wi,
+               make_float2(0.25f * a.x + 0.75f * b.x + 0.75f * c.x + 0.25f * d.x,
+                           0.25f * a.y + 0.75f * b.y + 0.75f * c.y + 0.25f * d.y));
     a = c;
     b = d;
   }
@@ -681,7 +683,7 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
                      int64_t wi, int64_t ho, int64_t wo, float scale_h,
                      float scale_w, int align_corners, int dtype,
                      void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   if (!x || !y || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t rows = n * c * ho;
@@ -692,6 +694,20 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   // busy as the one-column kernel: 64-lane rows of wi/2 pairs vs of wi columns.
   const bool pair = x2 && wi % 2 == 0 &&
                     mde::cdiv(wi, 64) >= 2 * mde::cdiv(wi / 2, 64);
+  if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
+    using B = mde::bf16;
+    if (pair)
+      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_pair_kernel<B>,
+                 x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)x, (B*)y, (int)hi,
+                 (int)wi);
+    else if (x2)
+      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_kernel<B>,
+                 x2_grid(n * c, hi, wi), dim3(64, kX2Warps), 0, (const B*)x, (B*)y, (int)hi,
+                 (int)wi);
+    else
+      return MDE_ERR_UNSUPPORTED;
+    return MDE_OK;
+  }
   const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, n * c);
   if (xs == 4) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<4>, xs_grid(n * c, hi, wi),
@@ -700,11 +716,11 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<8>, xs_grid(n * c, hi, wi),
                dim3(64, kXsWarps), 0, (const float*)x, (float*)y, (int)hi, (int)wi);
   } else if (pair) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel,
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel<float>,
                x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)x, (float*)y,
                (int)hi, (int)wi);
   } else if (x2) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel,
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel<float>,
                x2_grid(n * c, hi, wi), dim3(64, kX2Warps), 0, (const float*)x,
                (float*)y, (int)hi, (int)wi);
   } else if (wo % 4 == 0) {
@@ -725,7 +741,7 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
                      int64_t hi, int64_t wi, int64_t ho, int64_t wo,
                      float scale_h, float scale_w, int align_corners,
                      int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   if (!gy || !gx || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t planes = n * c;
@@ -733,6 +749,20 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
                   ho == 2 * hi && wo == 2 * wi && planes <= 65535;
   const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes);
+  if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
+    using B = mde::bf16;
+    if (x2 && !xs && wi % 2 == 0)
+      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_pair_kernel<false, B>),
+                 x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx,
+                 (int)hi, (int)wi, nullptr);
+    else if (x2 && !xs)
+      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, bilinear_bwd_x2_kernel<B>,
+                 x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx, (int)hi,
+                 (int)wi);
+    else
+      return MDE_ERR_UNSUPPORTED;
+    return MDE_OK;
+  }
   if (xs == 4) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<4>, xs_grid(planes, hi, wi),
                dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
@@ -740,11 +770,11 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<8>, xs_grid(planes, hi, wi),
                dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
   } else if (x2 && wi % 2 == 0) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel<false>,
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_pair_kernel<false, float>),
                x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy,
                (float*)gx, (int)hi, (int)wi, nullptr);
   } else if (x2) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel,
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel<float>,
                x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
                (float*)gx, (int)hi, (int)wi);
   } else if (plane_fits(hi, wi, ho, wo, scale_h, scale_w)) {
@@ -785,13 +815,20 @@ int mde_bilinear_bwd2_supported(int64_t n, int64_t c, int64_t hi, int64_t wi, in
 int mde_bilinear_bwd2(const void* gy, const void* gy2, void* gx, int64_t n, int64_t c,
                       int64_t hi, int64_t wi, int64_t ho, int64_t wo, float scale_h,
                       float scale_w, int align_corners, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   if (!gy || !gy2 || !gx || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
   if (!x2_pair(n * c, hi, wi, ho, wo, scale_h, scale_w, align_corners))
     return MDE_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const double bytes = 4.0 * n * c * (double)(hi * wi + 2 * ho * wo);
-  MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_pair_kernel<true>,
+  if (dtype == MDE_BF16) {
+    using B = mde::bf16;
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_pair_kernel<true, B>),
+               x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx, (int)hi,
+               (int)wi, (const B*)gy2);
+    return MDE_OK;
+  }
+  MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_pair_kernel<true, float>),
              x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy, (float*)gx,
              (int)hi, (int)wi, (const float*)gy2);
   return MDE_OK;

@@ -19,10 +19,9 @@ namespace {
 
 constexpr int kChunk = 16384;  // elements of one plane reduced by one block
 
-__device__ __forceinline__ const float* plane_ptr(const float* xa, int64_t ca,
-                                                  const float* xb, int64_t cb,
-                                                  int64_t nidx, int64_t ch,
-                                                  int64_t hw) {
+template <typename T>
+__device__ __forceinline__ const T* plane_ptr(const T* xa, int64_t ca, const T* xb, int64_t cb,
+                                              int64_t nidx, int64_t ch, int64_t hw) {
   return ch < ca ? xa + (nidx * ca + ch) * hw
                  : xb + (nidx * cb + (ch - ca)) * hw;
 }
@@ -36,10 +35,10 @@ __device__ __forceinline__ float bnrelu(float v, float sc, float sh) {
   return fmaxf(fmaf(v, sc, sh), 0.f);
 }
 
-template <int MODE>
+template <int MODE, typename T = float>
 __global__ void __launch_bounds__(256)
-    se_partial_kernel(const float* __restrict__ g, const float* __restrict__ xa,
-                      int64_t ca, const float* __restrict__ xb, int64_t cb,
+    se_partial_kernel(const T* __restrict__ g, const T* __restrict__ xa,
+                      int64_t ca, const T* __restrict__ xb, int64_t cb,
                       int64_t hw, int chunks, float* __restrict__ part,
                       const float* __restrict__ scale = nullptr,
                       const float* __restrict__ shift = nullptr) {
@@ -47,17 +46,17 @@ __global__ void __launch_bounds__(256)
   const int64_t c = ca + cb;
   const int64_t plane = blockIdx.y;
   const int64_t nidx = plane / c, ch = plane % c;
-  const float* x = plane_ptr(xa, ca, xb, cb, nidx, ch, hw);
-  const float* gp = MODE == kDot ? g + plane * hw : nullptr;
+  const T* x = plane_ptr(xa, ca, xb, cb, nidx, ch, hw);
+  const T* gp = MODE == kDot ? g + plane * hw : nullptr;
   const float sc = MODE == kBnRelu ? scale[ch] : 0.f, sh = MODE == kBnRelu ? shift[ch] : 0.f;
   const int64_t beg = (int64_t)blockIdx.x * kChunk;
   const int64_t end = beg + kChunk < hw ? beg + kChunk : hw;
   float acc = 0.f;
   if ((hw & 3) == 0) {
     for (int64_t i = beg + 4 * threadIdx.x; i < end; i += 4 * 256) {
-      float4 v = *reinterpret_cast<const float4*>(x + i);
+      float4 v = mde::ld4(x + i);
       if (MODE == kDot) {
-        const float4 q = *reinterpret_cast<const float4*>(gp + i);
+        const float4 q = mde::ld4(gp + i);
         acc += (v.x * q.x + v.y * q.y) + (v.z * q.z + v.w * q.w);
       } else {
         if (MODE == kBnRelu) {
@@ -68,8 +67,10 @@ __global__ void __launch_bounds__(256)
       }
     }
   } else {
-    for (int64_t i = beg + threadIdx.x; i < end; i += 256)
-      acc += MODE == kDot ? x[i] * gp[i] : (MODE == kBnRelu ? bnrelu(x[i], sc, sh) : x[i]);
+    for (int64_t i = beg + threadIdx.x; i < end; i += 256) {
+      const float xv = mde::ld1(x + i);
+      acc += MODE == kDot ? xv * mde::ld1(gp + i) : (MODE == kBnRelu ? bnrelu(xv, sc, sh) : xv);
+    }
   }
   const float tot = mde::block_sum256(acc, red);
   if (threadIdx.x == 0) part[plane * chunks + blockIdx.x] = tot;
@@ -136,12 +137,12 @@ __global__ void __launch_bounds__(1024)
 
 // out[plane, i] = x[plane, i] * s[plane]  (cat fused: plane -> xa or xb);
 // BNR: out = s[plane] * relu(sc * x + sh) (x = the BatchNorm's raw input).
-template <bool BNR>
+template <bool BNR, typename T = float>
 __global__ void __launch_bounds__(256)
-    se_scale_kernel(const float* __restrict__ xa, int64_t ca,
-                    const float* __restrict__ xb, int64_t cb, int64_t hw,
+    se_scale_kernel(const T* __restrict__ xa, int64_t ca,
+                    const T* __restrict__ xb, int64_t cb, int64_t hw,
                     int64_t planes, const float* __restrict__ s,
-                    float* __restrict__ out, const float* __restrict__ scale = nullptr,
+                    T* __restrict__ out, const float* __restrict__ scale = nullptr,
                     const float* __restrict__ shift = nullptr) {
   const int64_t c = ca + cb;
   if ((hw & 3) == 0) {
@@ -151,16 +152,16 @@ __global__ void __launch_bounds__(256)
          t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t plane = t / hw4, i = (t - plane * hw4) << 2;
       const int64_t ch = plane % c;
-      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, ch, hw);
+      const T* x = plane_ptr(xa, ca, xb, cb, plane / c, ch, hw);
       const float sc = s[plane];
-      float4 v = *reinterpret_cast<const float4*>(x + i);
+      float4 v = mde::ld4(x + i);
       if (BNR) {
         const float a = scale[ch], b = shift[ch];
         v.x = bnrelu(v.x, a, b); v.y = bnrelu(v.y, a, b);
         v.z = bnrelu(v.z, a, b); v.w = bnrelu(v.w, a, b);
       }
       v.x *= sc; v.y *= sc; v.z *= sc; v.w *= sc;
-      *reinterpret_cast<float4*>(out + plane * hw + i) = v;
+      mde::st4(out + plane * hw + i, v);
     }
   } else {
     const int64_t total = planes * hw;
@@ -168,9 +169,10 @@ __global__ void __launch_bounds__(256)
          t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t plane = t / hw, i = t - plane * hw;
       const int64_t ch = plane % c;
-      const float* x = plane_ptr(xa, ca, xb, cb, plane / c, ch, hw);
-      const float v = BNR ? bnrelu(x[i], scale[ch], shift[ch]) : x[i];
-      out[t] = v * s[plane];
+      const T* x = plane_ptr(xa, ca, xb, cb, plane / c, ch, hw);
+      const float xv = mde::ld1(x + i);
+      const float v = BNR ? bnrelu(xv, scale[ch], shift[ch]) : xv;
+      mde::st1(out + t, v * s[plane]);
     }
   }
 }
@@ -327,9 +329,10 @@ __global__ void __launch_bounds__(256)
 //   channel.  Both are linear in per-(sample, channel) sums of one pass:
 //   A = sum g*m, B = sum m, C = sum g*m*(y - mean), D = sum m*(y - mean),
 //   E = sum g*u (= the SE gradient dot) with m = [z > 0].
+template <typename T = float>
 __global__ void __launch_bounds__(256)
-    sebn_bwd_reduce_kernel(const float* __restrict__ g, const float* __restrict__ ya, int64_t ca,
-                           const float* __restrict__ yb, int64_t cb, int64_t hw, int chunks,
+    sebn_bwd_reduce_kernel(const T* __restrict__ g, const T* __restrict__ ya, int64_t ca,
+                           const T* __restrict__ yb, int64_t cb, int64_t hw, int chunks,
                            const float* __restrict__ scale, const float* __restrict__ shift,
                            const float* __restrict__ mean, float* __restrict__ part_e,
                            float* __restrict__ part4) {
@@ -337,8 +340,8 @@ __global__ void __launch_bounds__(256)
   const int64_t c = ca + cb;
   const int64_t plane = blockIdx.y;
   const int64_t nidx = plane / c, ch = plane % c;
-  const float* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
-  const float* gp = g + plane * hw;
+  const T* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
+  const T* gp = g + plane * hw;
   const float sc = scale[ch], sh = shift[ch], mu = mean[ch];
   const int64_t beg = (int64_t)blockIdx.x * kChunk;
   const int64_t end = beg + kChunk < hw ? beg + kChunk : hw;
@@ -356,12 +359,12 @@ __global__ void __launch_bounds__(256)
   };
   if ((hw & 3) == 0) {
     for (int64_t i = beg + 4 * threadIdx.x; i < end; i += 4 * 256) {
-      const float4 v = *reinterpret_cast<const float4*>(y + i);
-      const float4 q = *reinterpret_cast<const float4*>(gp + i);
+      const float4 v = mde::ld4(y + i);
+      const float4 q = mde::ld4(gp + i);
       one(v.x, q.x); one(v.y, q.y); one(v.z, q.z); one(v.w, q.w);
     }
   } else {
-    for (int64_t i = beg + threadIdx.x; i < end; i += 256) one(y[i], gp[i]);
+    for (int64_t i = beg + threadIdx.x; i < end; i += 256) one(mde::ld1(y + i), mde::ld1(gp + i));
   }
   A = mde::block_sum256(A, red);
   B = mde::block_sum256(B, red);
@@ -418,18 +421,19 @@ __global__ void __launch_bounds__(256)
   coef[2 * ch + 1] = training ? (float)(-sc * is * is * s2 / cnt) : 0.f;
 }
 
+template <typename T = float>
 __global__ void __launch_bounds__(256)
-    sebn_bwd_apply_kernel(const float* __restrict__ g, const float* __restrict__ ya, int64_t ca,
-                          const float* __restrict__ yb, int64_t cb, int64_t hw, int64_t planes,
+    sebn_bwd_apply_kernel(const T* __restrict__ g, const T* __restrict__ ya, int64_t ca,
+                          const T* __restrict__ yb, int64_t cb, int64_t hw, int64_t planes,
                           const float* __restrict__ s, const float* __restrict__ dm, float inv_hw,
                           const float* __restrict__ scale, const float* __restrict__ shift,
                           const float* __restrict__ mean, const float* __restrict__ coef,
-                          float* __restrict__ gya, float* __restrict__ gyb) {
+                          T* __restrict__ gya, T* __restrict__ gyb) {
   const int64_t c = ca + cb;
-  auto one = [](float yv, float gv, float sc, float sh, float P, float Q, float R, float T,
+  auto one = [](float yv, float gv, float sc, float sh, float P, float Q, float R, float Tc,
                 float mu) {
     const float z = fmaf(yv, sc, sh);
-    return (z > 0.f ? fmaf(P, gv, Q) : 0.f) + fmaf(T, yv - mu, R);
+    return (z > 0.f ? fmaf(P, gv, Q) : 0.f) + fmaf(Tc, yv - mu, R);
   };
   if ((hw & 3) == 0) {
     const int64_t hw4 = hw >> 2;
@@ -438,16 +442,17 @@ __global__ void __launch_bounds__(256)
          t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t plane = t / hw4, i = (t - plane * hw4) << 2;
       const int64_t nidx = plane / c, ch = plane % c;
-      const float* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
-      float* dst = ch < ca ? gya + (nidx * ca + ch) * hw : gyb + (nidx * cb + ch - ca) * hw;
+      const T* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
+      T* dst = ch < ca ? gya + (nidx * ca + ch) * hw : gyb + (nidx * cb + ch - ca) * hw;
       const float sc = scale[ch], sh = shift[ch], mu = mean[ch];
       const float P = sc * s[plane], Q = sc * dm[plane] * inv_hw;
-      const float R = coef[2 * ch], T = coef[2 * ch + 1];
-      const float4 v = *reinterpret_cast<const float4*>(y + i);
-      const float4 q = *reinterpret_cast<const float4*>(g + plane * hw + i);
-      *reinterpret_cast<float4*>(dst + i) =
-          make_float4(one(v.x, q.x, sc, sh, P, Q, R, T, mu), one(v.y, q.y, sc, sh, P, Q, R, T, mu),
-                      one(v.z, q.z, sc, sh, P, Q, R, T, mu), one(v.w, q.w, sc, sh, P, Q, R, T, mu));
+      const float R = coef[2 * ch], Tc = coef[2 * ch + 1];
+      const float4 v = mde::ld4(y + i);
+      const float4 q = mde::ld4(g + plane * hw + i);
+      mde::st4(dst + i, make_float4(one(v.x, q.x, sc, sh, P, Q, R, Tc, mu),
+                                    one(v.y, q.y, sc, sh, P, Q, R, Tc, mu),
+                                    one(v.z, q.z, sc, sh, P, Q, R, Tc, mu),
+                                    one(v.w, q.w, sc, sh, P, Q, R, Tc, mu)));
     }
   } else {
     const int64_t total = planes * hw;
@@ -455,11 +460,11 @@ __global__ void __launch_bounds__(256)
          t += (int64_t)gridDim.x * blockDim.x) {
       const int64_t plane = t / hw, i = t - plane * hw;
       const int64_t nidx = plane / c, ch = plane % c;
-      const float* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
-      float* dst = ch < ca ? gya + (nidx * ca + ch) * hw : gyb + (nidx * cb + ch - ca) * hw;
+      const T* y = plane_ptr(ya, ca, yb, cb, nidx, ch, hw);
+      T* dst = ch < ca ? gya + (nidx * ca + ch) * hw : gyb + (nidx * cb + ch - ca) * hw;
       const float sc = scale[ch];
-      dst[i] = one(y[i], g[t], sc, shift[ch], sc * s[plane], sc * dm[plane] * inv_hw,
-                   coef[2 * ch], coef[2 * ch + 1], mean[ch]);
+      mde::st1(dst + i, one(mde::ld1(y + i), mde::ld1(g + t), sc, shift[ch], sc * s[plane],
+                            sc * dm[plane] * inv_hw, coef[2 * ch], coef[2 * ch + 1], mean[ch]));
     }
   }
 }
@@ -527,7 +532,7 @@ int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   SeWs ws = se_carve(workspace, n, c, cr, hw);
   const int chunks = (int)se_chunks(hw);
   const double big = 4.0 * n * c * (double)hw;
-  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<kSum>,
+  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, (se_partial_kernel<kSum, float>),
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr,
              (const float*)xa, ca, (const float*)xb, cb, hw, chunks, ws.part);
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc1_kernel,
@@ -537,7 +542,7 @@ int mde_se_gate_fwd(const void* xa, int64_t ca, const void* xb, int64_t cb,
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc2_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
              sizeof(float) * cr, (int)c, (int)cr, w2, b2, gate, hidden, s);
-  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel<false>,
+  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, (se_scale_kernel<false, float>),
              dim3(stream_grid(n * c * hw / 4)), dim3(256), 0,
              (const float*)xa, ca, (const float*)xb, cb, hw, n * c, s,
              (float*)out);
@@ -561,7 +566,7 @@ int mde_se_gate_bwd(const void* gout, const void* xa, int64_t ca, const void* xb
   SeWs ws = se_carve(workspace, n, c, cr, hw);
   const int chunks = (int)se_chunks(hw);
   const double big = 4.0 * n * c * (double)hw;
-  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, se_partial_kernel<kDot>,
+  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, (se_partial_kernel<kDot, float>),
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0,
              (const float*)gout, (const float*)xa, ca, (const float*)xb, cb,
              hw, chunks, ws.part);
@@ -610,28 +615,22 @@ size_t mde_se_bn_workspace(int64_t n, int64_t c, int64_t cr, int64_t h, int64_t 
          round16(sizeof(float) * 2 * c);
 }
 
-// SELayer(cat([relu(bn_a(ya)), relu(bn_b(yb))])) from the BatchNorms' raw
-// inputs: scale / shift [ca + cb] are the two BNs' per-channel coefficients
-// (mde_batchnorm_fwd_coef*), concatenated.  The squeeze reads y once, the
-// scale pass writes out = s * relu(scale * y + shift); the BN + ReLU outputs
-// and their concatenation are never materialised.
-int mde_se_bn_fwd(const void* ya, int64_t ca, const void* yb, int64_t cb, const float* scale,
-                  const float* shift, const float* w1, const float* w2, int64_t cr, void* out,
-                  float* s, float* hidden, float* mean, int64_t n, int64_t h, int64_t w,
-                  void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
-  const int64_t c = ca + cb, hw = h * w;
-  if (!ya || ca <= 0 || cb < 0 || (cb > 0 && !yb) || !scale || !shift || !w1 || !w2 ||
-      cr <= 0 || !out || !s || !hidden || !mean || n <= 0 || hw <= 0 || !workspace ||
-      c > 4096 || cr > 4096 || n > 65535 || n * c > 65535)
-    return MDE_ERR_INVALID_ARG;
-  hipStream_t st = (hipStream_t)stream;
+}  // extern "C"
+
+// mde_se_bn_fwd / _bwd on storage type T (fp32, or bf16 under autocast: y, out,
+// gout, gy in T; coefficients, the SE vector, FC weights and sums fp32).
+template <typename T>
+static int se_bn_fwd_t(const void* ya, int64_t ca, const void* yb, int64_t cb, const float* scale,
+                       const float* shift, const float* w1, const float* w2, int64_t cr, void* out,
+                       float* s, float* hidden, float* mean, int64_t n, int64_t hw,
+                       void* workspace, hipStream_t st) {
+  const int64_t c = ca + cb;
   SeWs ws = se_carve(workspace, n, c, cr, hw);
   const int chunks = (int)se_chunks(hw);
-  const double big = 4.0 * n * c * (double)hw;
-  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, se_partial_kernel<kBnRelu>,
-             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr, (const float*)ya, ca,
-             (const float*)yb, cb, hw, chunks, ws.part, scale, shift);
+  const double big = (double)sizeof(T) * n * c * (double)hw;
+  MDE_LAUNCH(mde::K_SE_SQUEEZE, big, st, (se_partial_kernel<kBnRelu, T>),
+             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, nullptr, (const T*)ya, ca,
+             (const T*)yb, cb, hw, chunks, ws.part, scale, shift);
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc1_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(cr, kOutPerBlock)), dim3(1024),
              sizeof(float) * c, ws.part, chunks, (int)c, (int)cr, 1.f / (float)hw, w1, nullptr,
@@ -639,39 +638,26 @@ int mde_se_bn_fwd(const void* ya, int64_t ca, const void* yb, int64_t cb, const 
   MDE_LAUNCH(mde::K_SE_FC, 4.0 * (c * cr + 2.0 * n * c), st, se_fc2_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
              sizeof(float) * cr, (int)c, (int)cr, w2, nullptr, 0, hidden, s);
-  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, se_scale_kernel<true>,
-             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)ya, ca,
-             (const float*)yb, cb, hw, n * c, s, (float*)out, scale, shift);
+  MDE_LAUNCH(mde::K_SE_SCALE, 2.0 * big, st, (se_scale_kernel<true, T>),
+             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const T*)ya, ca, (const T*)yb, cb,
+             hw, n * c, s, (T*)out, scale, shift);
   return MDE_OK;
 }
 
-// Backward of mde_se_bn_fwd through the SE layer, the ReLUs and both
-// BatchNorms (training: batch statistics, save_mean / save_invstd of the raw
-// input; eval: running statistics, no mean / variance terms): one reduction
-// pass over (gout, y), the per-sample FC backward, a per-channel combine in
-// double, and one apply pass writing gya / gyb = d/dy.  ggamma / gbeta are
-// concatenated [ca + cb] like scale / shift.
-int mde_se_bn_bwd(const void* gout, const void* ya, int64_t ca, const void* yb, int64_t cb,
-                  const float* scale, const float* shift, const float* bn_mean,
-                  const float* bn_invstd, int training, const float* w1, const float* w2,
-                  int64_t cr, const float* s, const float* hidden, const float* mean, void* gya,
-                  void* gyb, float* ggamma, float* gbeta, float* gw1, float* gw2, int64_t n,
-                  int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
-  const int64_t c = ca + cb, hw = h * w;
-  if (!gout || !ya || ca <= 0 || cb < 0 || (cb > 0 && (!yb || !gyb)) || !gya || !scale ||
-      !shift || !bn_mean || !bn_invstd || !w1 || !w2 || cr <= 0 || !s || !hidden || !mean ||
-      !gw1 || !gw2 || n <= 0 || hw <= 0 || !workspace || c > 4096 || cr > 4096 ||
-      n > 65535 || n * c > 65535)
-    return MDE_ERR_INVALID_ARG;
-  hipStream_t st = (hipStream_t)stream;
+template <typename T>
+static int se_bn_bwd_t(const void* gout, const void* ya, int64_t ca, const void* yb, int64_t cb,
+                       const float* scale, const float* shift, const float* bn_mean,
+                       const float* bn_invstd, int training, const float* w1, const float* w2,
+                       int64_t cr, const float* s, const float* hidden, const float* mean,
+                       void* gya, void* gyb, float* ggamma, float* gbeta, float* gw1, float* gw2,
+                       int64_t n, int64_t hw, void* workspace, hipStream_t st) {
+  const int64_t c = ca + cb;
   SeWs ws = se_carve(workspace, n, c, cr, hw);
   const int chunks = (int)se_chunks(hw);
-  const double big = 4.0 * n * c * (double)hw;
-  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, sebn_bwd_reduce_kernel,
-             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, (const float*)gout,
-             (const float*)ya, ca, (const float*)yb, cb, hw, chunks, scale, shift, bn_mean,
-             ws.part, ws.part4);
+  const double big = (double)sizeof(T) * n * c * (double)hw;
+  MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, sebn_bwd_reduce_kernel<T>,
+             dim3(chunks, (unsigned)(n * c)), dim3(256), 0, (const T*)gout, (const T*)ya, ca,
+             (const T*)yb, cb, hw, chunks, scale, shift, bn_mean, ws.part, ws.part4);
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + 3.0 * n * c), st, se_bfc1_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
              sizeof(float) * cr, ws.part, chunks, (int)c, (int)cr, w2, nullptr, 0, s, hidden,
@@ -688,11 +674,65 @@ int mde_se_bn_bwd(const void* gout, const void* ya, int64_t ca, const void* yb, 
   MDE_LAUNCH(mde::K_SE_BWD_FC, 16.0 * n * c * chunks, st, sebn_bwd_combine_kernel,
              dim3((unsigned)c), dim3(256), 0, ws.part4, chunks, n, c, hw, s,
              ws.dm, scale, bn_invstd, training, ggamma, gbeta, ws.coef);
-  MDE_LAUNCH(mde::K_SE_BWD_APPLY, 3.0 * big, st, sebn_bwd_apply_kernel,
-             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const float*)gout,
-             (const float*)ya, ca, (const float*)yb, cb, hw, n * c, s, ws.dm, 1.f / (float)hw,
-             scale, shift, bn_mean, ws.coef, (float*)gya, (float*)gyb);
+  MDE_LAUNCH(mde::K_SE_BWD_APPLY, 3.0 * big, st, sebn_bwd_apply_kernel<T>,
+             dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const T*)gout, (const T*)ya, ca,
+             (const T*)yb, cb, hw, n * c, s, ws.dm, 1.f / (float)hw, scale, shift, bn_mean,
+             ws.coef, (T*)gya, (T*)gyb);
   return MDE_OK;
+}
+
+extern "C" {
+
+// SELayer(cat([relu(bn_a(ya)), relu(bn_b(yb))])) from the BatchNorms' raw
+// inputs: scale / shift [ca + cb] are the two BNs' per-channel coefficients
+// (mde_batchnorm_fwd_coef*), concatenated.  The squeeze reads y once, the
+// scale pass writes out = s * relu(scale * y + shift); the BN + ReLU outputs
+// and their concatenation are never materialised.
+int mde_se_bn_fwd(const void* ya, int64_t ca, const void* yb, int64_t cb, const float* scale,
+                  const float* shift, const float* w1, const float* w2, int64_t cr, void* out,
+                  float* s, float* hidden, float* mean, int64_t n, int64_t h, int64_t w,
+                  void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
+  const int64_t c = ca + cb, hw = h * w;
+  if (!ya || ca <= 0 || cb < 0 || (cb > 0 && !yb) || !scale || !shift || !w1 || !w2 ||
+      cr <= 0 || !out || !s || !hidden || !mean || n <= 0 || hw <= 0 || !workspace ||
+      c > 4096 || cr > 4096 || n > 65535 || n * c > 65535)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == MDE_BF16
+             ? se_bn_fwd_t<mde::bf16>(ya, ca, yb, cb, scale, shift, w1, w2, cr, out, s, hidden,
+                                      mean, n, hw, workspace, st)
+             : se_bn_fwd_t<float>(ya, ca, yb, cb, scale, shift, w1, w2, cr, out, s, hidden, mean,
+                                  n, hw, workspace, st);
+}
+
+// Backward of mde_se_bn_fwd through the SE layer, the ReLUs and both
+// BatchNorms (training: batch statistics, save_mean / save_invstd of the raw
+// input; eval: running statistics, no mean / variance terms): one reduction
+// pass over (gout, y), the per-sample FC backward, a per-channel combine in
+// double, and one apply pass writing gya / gyb = d/dy.  ggamma / gbeta are
+// concatenated [ca + cb] like scale / shift.
+int mde_se_bn_bwd(const void* gout, const void* ya, int64_t ca, const void* yb, int64_t cb,
+                  const float* scale, const float* shift, const float* bn_mean,
+                  const float* bn_invstd, int training, const float* w1, const float* w2,
+                  int64_t cr, const float* s, const float* hidden, const float* mean, void* gya,
+                  void* gyb, float* ggamma, float* gbeta, float* gw1, float* gw2, int64_t n,
+                  int64_t h, int64_t w, void* workspace, int dtype, void* stream) {
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
+  const int64_t c = ca + cb, hw = h * w;
+  if (!gout || !ya || ca <= 0 || cb < 0 || (cb > 0 && (!yb || !gyb)) || !gya || !scale ||
+      !shift || !bn_mean || !bn_invstd || !w1 || !w2 || cr <= 0 || !s || !hidden || !mean ||
+      !gw1 || !gw2 || n <= 0 || hw <= 0 || !workspace || c > 4096 || cr > 4096 ||
+      n > 65535 || n * c > 65535)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  return dtype == MDE_BF16
+             ? se_bn_bwd_t<mde::bf16>(gout, ya, ca, yb, cb, scale, shift, bn_mean, bn_invstd,
+                                      training, w1, w2, cr, s, hidden, mean, gya, gyb, ggamma,
+                                      gbeta, gw1, gw2, n, hw, workspace, st)
+             : se_bn_bwd_t<float>(gout, ya, ca, yb, cb, scale, shift, bn_mean, bn_invstd,
+                                  training, w1, w2, cr, s, hidden, mean, gya, gyb, ggamma, gbeta,
+                                  gw1, gw2, n, hw, workspace, st);
 }
 
 }  // extern "C"

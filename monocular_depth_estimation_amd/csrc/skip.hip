@@ -19,11 +19,11 @@ constexpr int kMaxC = 64;
 // BNR (here and in the kernels below): r is the raw input of a BatchNorm +
 // ReLU (the comb_conv's last, modules.py:72-73) applied on load,
 // s = relu(r * isc[c] + ish[c]) + d, so its output is never written.
-template <int CO, int PPT, bool BNR = false>
+template <int CO, int PPT, bool BNR = false, typename T = float>
 __global__ void __launch_bounds__(256)
-    skip_fwd_kernel(const float* __restrict__ r, const float* __restrict__ d,
+    skip_fwd_kernel(const T* __restrict__ r, const T* __restrict__ d,
                     const float* __restrict__ wt, const float* __restrict__ b,
-                    float* __restrict__ out, int64_t n, int cin, int cout,
+                    T* __restrict__ out, int64_t n, int cin, int cout,
                     int64_t hw, const float* __restrict__ isc = nullptr,
                     const float* __restrict__ ish = nullptr) {
   __shared__ float sw[kMaxC * kMaxC];
@@ -37,8 +37,8 @@ __global__ void __launch_bounds__(256)
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t nidx = t / groups;
     const int64_t p = (t - nidx * groups) * PPT;
-    const float* rp = r + nidx * cin * hw + p;
-    const float* dp = d + nidx * cin * hw + p;
+    const T* rp = r + nidx * cin * hw + p;
+    const T* dp = d + nidx * cin * hw + p;
     float acc[CO][PPT];
 #pragma unroll
     for (int o = 0; o < CO; ++o) {
@@ -51,16 +51,17 @@ __global__ void __launch_bounds__(256)
       const float bs = BNR ? isc[c] : 1.f, bh = BNR ? ish[c] : 0.f;
       auto act = [&](float v) { return BNR ? fmaxf(v * bs + bh, 0.f) : v; };
       if (PPT == 4) {
-        const float4 a = *reinterpret_cast<const float4*>(rp + c * hw);
-        const float4 e = *reinterpret_cast<const float4*>(dp + c * hw);
+        const float4 a = mde::ld4(rp + c * hw);
+        const float4 e = mde::ld4(dp + c * hw);
         s[0] = act(a.x) + e.x; s[1 % PPT] = act(a.y) + e.y;
         s[2 % PPT] = act(a.z) + e.z; s[3 % PPT] = act(a.w) + e.w;
       } else if (PPT == 2) {
+        static_assert(PPT != 2 || sizeof(T) == 4, "float2 path is fp32-only");
         const float2 a = *reinterpret_cast<const float2*>(rp + c * hw);
         const float2 e = *reinterpret_cast<const float2*>(dp + c * hw);
         s[0] = act(a.x) + e.x; s[1 % PPT] = act(a.y) + e.y;
       } else {
-        s[0] = act(rp[c * hw]) + dp[c * hw];
+        s[0] = act(mde::ld1(rp + c * hw)) + mde::ld1(dp + c * hw);
       }
 #pragma unroll
       for (int o = 0; o < CO; ++o) {
@@ -71,18 +72,18 @@ __global__ void __launch_bounds__(256)
         }
       }
     }
-    float* op = out + nidx * cout * hw + p;
+    T* op = out + nidx * cout * hw + p;
 #pragma unroll
     for (int o = 0; o < CO; ++o) {
       if (o < cout) {
         if (PPT == 4) {
-          *reinterpret_cast<float4*>(op + o * hw) = make_float4(
-              acc[o][0], acc[o][1 % PPT], acc[o][2 % PPT], acc[o][3 % PPT]);
+          mde::st4(op + o * hw, make_float4(acc[o][0], acc[o][1 % PPT], acc[o][2 % PPT],
+                                           acc[o][3 % PPT]));
         } else if (PPT == 2) {
           *reinterpret_cast<float2*>(op + o * hw) =
               make_float2(acc[o][0], acc[o][1 % PPT]);
         } else {
-          op[o * hw] = acc[o][0];
+          mde::st1(op + o * hw, acc[o][0]);
         }
       }
     }
@@ -213,11 +214,11 @@ __global__ void __launch_bounds__(kTile)
 // also that BatchNorm's backward sums sum e, sum e (r - imean[c]) with
 // e = gs [r * isc + ish > 0].  Slab row: [CI] weight gradient, [1] bias
 // gradient, [2 CI] BN sums.
-template <int CI, bool BNR = false, bool BNS = false>
+template <int CI, bool BNR = false, bool BNS = false, typename T = float>
 __global__ void __launch_bounds__(256)
-    skip_bwd_c1_kernel(const float* __restrict__ g, const float* __restrict__ r,
-                       const float* __restrict__ d, const float* __restrict__ wt,
-                       float* __restrict__ gs, float* __restrict__ slab, int64_t n, int64_t hw,
+    skip_bwd_c1_kernel(const T* __restrict__ g, const T* __restrict__ r,
+                       const T* __restrict__ d, const float* __restrict__ wt,
+                       T* __restrict__ gs, float* __restrict__ slab, int64_t n, int64_t hw,
                        const float* __restrict__ isc = nullptr,
                        const float* __restrict__ ish = nullptr,
                        const float* __restrict__ imean = nullptr) {
@@ -239,14 +240,14 @@ __global__ void __launch_bounds__(256)
   const int64_t q4 = hw >> 2, total = n * q4;
   for (int64_t t = (int64_t)blockIdx.x * QPB + qi; t < total; t += (int64_t)gridDim.x * QPB) {
     const int64_t nidx = t / q4, p = (t - nidx * q4) << 2;
-    const float4 gv = *reinterpret_cast<const float4*>(g + nidx * hw + p);
+    const float4 gv = mde::ld4(g + nidx * hw + p);
     if (grp == 0) ab += (gv.x + gv.y) + (gv.z + gv.w);
     const int64_t base = (nidx * CI + 4 * grp) * hw + p;
     float4 a[4], e[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      a[k] = *reinterpret_cast<const float4*>(r + base + k * hw);
-      e[k] = *reinterpret_cast<const float4*>(d + base + k * hw);
+      a[k] = mde::ld4(r + base + k * hw);
+      e[k] = mde::ld4(d + base + k * hw);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -255,7 +256,7 @@ __global__ void __launch_bounds__(256)
                                     act(a[k].z) + e[k].z, act(a[k].w) + e[k].w);
       aw[k] += (gv.x * sv.x + gv.y * sv.y) + (gv.z * sv.z + gv.w * sv.w);
       const float4 o4 = make_float4(w[k] * gv.x, w[k] * gv.y, w[k] * gv.z, w[k] * gv.w);
-      *reinterpret_cast<float4*>(gs + base + k * hw) = o4;
+      mde::st4(gs + base + k * hw, o4);
       if constexpr (BNS) {
         const float av[4] = {a[k].x, a[k].y, a[k].z, a[k].w}, ov[4] = {o4.x, o4.y, o4.z, o4.w};
 #pragma unroll
@@ -872,74 +873,65 @@ size_t mde_skip_reduce_bn_workspace(int64_t n, int64_t cin, int64_t cout, int64_
   return sizeof(float) * (size_t)bwd_blocks(n, h * w) * (size_t)(cin * cout + cout + 2 * cin);
 }
 
-int mde_skip_reduce_bn_fwd(const void* r, const void* d, const float* in_scale,
-                           const float* in_shift, const float* wt, const float* b, void* out,
-                           int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
-                           void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
-  const int64_t hw = h * w;
-  if (!r || !d || !in_scale || !in_shift || !wt || !b || !out || n <= 0 || hw <= 0)
-    return MDE_ERR_INVALID_ARG;
-  if (!mde_skip_reduce_bn_supported(cin, cout, h, w, 0)) return MDE_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
-  const double bytes = 4.0 * n * hw * (double)(2 * cin + cout);
-  const float *R = (const float*)r, *D = (const float*)d;
+}  // extern "C"
+
+// skip_reduce_bn launches on storage type T (fp32, or bf16 under autocast:
+// r, d, out / gout, gs in T; weights, BN coefficients, sums and arithmetic fp32).
+template <typename T>
+static int skip_bn_fwd_t(const void* r, const void* d, const float* in_scale,
+                         const float* in_shift, const float* wt, const float* b, void* out,
+                         int64_t n, int64_t cin, int64_t cout, int64_t hw, hipStream_t s) {
+  const double bytes = (double)sizeof(T) * n * hw * (double)(2 * cin + cout);
+  const T *R = (const T*)r, *D = (const T*)d;
   if (skip_bn_reg(cin, cout, hw)) {
     const int64_t blocks = mde::cdiv(n * hw / 4, 256);
     const dim3 g((unsigned)(blocks < 1 ? 1 : (blocks > 8192 ? 8192 : blocks)));
-    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_kernel<1, 4, true>), g, dim3(256), 0, R, D, wt,
-               b, (float*)out, n, (int)cin, (int)cout, hw, in_scale, in_shift);
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_kernel<1, 4, true, T>), g, dim3(256), 0, R, D,
+               wt, b, (T*)out, n, (int)cin, (int)cout, hw, in_scale, in_shift);
     return MDE_OK;
   }
   const int64_t blocks = mde::cdiv(n * hw / 64, 4);
   const dim3 g((unsigned)(blocks > 4096 ? 4096 : blocks));
   if (cin == 64)
-    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32, true, true>), g, dim3(256),
-               0, R, D, wt, b, (float*)out, n, hw, in_scale, in_shift, nullptr);
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32, true, true, false, T>), g,
+               dim3(256), 0, R, D, wt, b, (T*)out, n, hw, in_scale, in_shift, nullptr);
   else
-    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<32, 16, true, true>), g, dim3(256),
-               0, R, D, wt, b, (float*)out, n, hw, in_scale, in_shift, nullptr);
+    MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<32, 16, true, true, false, T>), g,
+               dim3(256), 0, R, D, wt, b, (T*)out, n, hw, in_scale, in_shift, nullptr);
   return MDE_OK;
 }
 
-int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const float* in_scale,
-                           const float* in_shift, const float* in_mean, const float* wt, void* gs,
-                           float* gw, float* gb, float* in_sums, int64_t n, int64_t cin,
-                           int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
-                           void* stream) {
-  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
-  const int64_t hw = h * w;
-  if (!gout || !r || !d || !in_scale || !in_shift || !wt || !gs || !gw || !gb || !workspace ||
-      n <= 0 || hw <= 0 || (in_sums && !in_mean))
-    return MDE_ERR_INVALID_ARG;
-  if (!mde_skip_reduce_bn_supported(cin, cout, h, w, in_sums != nullptr)) return MDE_ERR_UNSUPPORTED;
-  hipStream_t s = (hipStream_t)stream;
+template <typename T>
+static int skip_bn_bwd_t(const void* gout, const void* r, const void* d, const float* in_scale,
+                         const float* in_shift, const float* in_mean, const float* wt, void* gs,
+                         float* gw, float* gb, float* in_sums, int64_t n, int64_t cin,
+                         int64_t cout, int64_t hw, void* workspace, hipStream_t s) {
   const int nb = bwd_blocks(n, hw);
   float* slab = (float*)workspace;
-  const double bytes = 4.0 * n * hw * (double)(3 * cin + cout);
-  const float *G = (const float*)gout, *R = (const float*)r, *D = (const float*)d;
-  float* GS = (float*)gs;
+  const double bytes = (double)sizeof(T) * n * hw * (double)(3 * cin + cout);
+  const T *G = (const T*)gout, *R = (const T*)r, *D = (const T*)d;
+  T* GS = (T*)gs;
   const bool sums = in_sums != nullptr;
   if (cin == 16 && sums)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, true>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, true, T>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 16)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, false>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, false, T>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 4 && sums)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4, true, true>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4, true, true, T>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 4)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4, true, false>), dim3(nb),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<4, true, false, T>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 64)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32, true, true, false>),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<64, 32, true, true, false, T>),
                dim3(nb), dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (sums)
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true, true, true>),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true, true, true, T>),
                dim3(nb), dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else
-    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true, true, false>),
+    MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_mfma_kernel<32, 16, true, true, false, T>),
                dim3(nb), dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   const int npairs = (int)(cin * cout);
   const int nextra = sums ? (int)(2 * cin) : 0;
@@ -947,6 +939,42 @@ int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const
              skip_slab_reduce_kernel, dim3((unsigned)(npairs + cout + nextra)), dim3(256), 0, slab,
              nb, npairs, (int)cout, gw, gb, nextra, in_sums);
   return MDE_OK;
+}
+
+extern "C" {
+
+int mde_skip_reduce_bn_fwd(const void* r, const void* d, const float* in_scale,
+                           const float* in_shift, const float* wt, const float* b, void* out,
+                           int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                           void* stream) {
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!r || !d || !in_scale || !in_shift || !wt || !b || !out || n <= 0 || hw <= 0)
+    return MDE_ERR_INVALID_ARG;
+  if (!mde_skip_reduce_bn_supported(cin, cout, h, w, 0)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == MDE_BF16
+             ? skip_bn_fwd_t<mde::bf16>(r, d, in_scale, in_shift, wt, b, out, n, cin, cout, hw, s)
+             : skip_bn_fwd_t<float>(r, d, in_scale, in_shift, wt, b, out, n, cin, cout, hw, s);
+}
+
+int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const float* in_scale,
+                           const float* in_shift, const float* in_mean, const float* wt, void* gs,
+                           float* gw, float* gb, float* in_sums, int64_t n, int64_t cin,
+                           int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                           void* stream) {
+  if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
+  const int64_t hw = h * w;
+  if (!gout || !r || !d || !in_scale || !in_shift || !wt || !gs || !gw || !gb || !workspace ||
+      n <= 0 || hw <= 0 || (in_sums && !in_mean))
+    return MDE_ERR_INVALID_ARG;
+  if (!mde_skip_reduce_bn_supported(cin, cout, h, w, in_sums != nullptr)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  return dtype == MDE_BF16
+             ? skip_bn_bwd_t<mde::bf16>(gout, r, d, in_scale, in_shift, in_mean, wt, gs, gw, gb,
+                                        in_sums, n, cin, cout, hw, workspace, s)
+             : skip_bn_bwd_t<float>(gout, r, d, in_scale, in_shift, in_mean, wt, gs, gw, gb,
+                                    in_sums, n, cin, cout, hw, workspace, s);
 }
 
 

@@ -225,9 +225,10 @@ def nyu_augment(image_u8: torch.Tensor, depth_raw: torch.Tensor, flags: torch.Te
     dh, dw = depth_raw.shape[1], depth_raw.shape[2]
     img = torch.empty((n, 3, h, w), dtype=torch.float32, device=image_u8.device)
     dep = torch.empty((n, 1, dh, dw), dtype=torch.float32, device=image_u8.device)
-    _abi.call("mde_nyu_augment", _abi.ptr(image_u8.contiguous()), _abi.ptr(depth_raw.contiguous()),
-              _abi.ptr(flags.contiguous()), _abi.ptr(img), _abi.ptr(dep), n, h, w, dh, dw, bits,
-              _abi.stream_of(image_u8))
+    # contiguous copies (if any) stay referenced until the launch is enqueued
+    src, draw, flg = image_u8.contiguous(), depth_raw.contiguous(), flags.contiguous()
+    _abi.call("mde_nyu_augment", _abi.ptr(src), _abi.ptr(draw), _abi.ptr(flg), _abi.ptr(img),
+              _abi.ptr(dep), n, h, w, dh, dw, bits, _abi.stream_of(image_u8))
     return img, dep
 
 

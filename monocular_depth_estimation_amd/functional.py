@@ -17,9 +17,11 @@ import torch
 from . import _abi
 
 # The HIP kernels compute in fp32.  Under torch.autocast (bf16 mixed precision:
-# convolutions / GEMMs on MIOpen / hipBLASLt in bf16) every custom Function runs
-# with its floating inputs cast to fp32 and autocast disabled; autograd casts the
-# fp32 input gradients back to the producers' dtype.
+# convolutions / GEMMs on MIOpen / hipBLASLt in bf16) a custom Function without a
+# bf16 storage path runs with its floating inputs cast to fp32 and autocast
+# disabled (_amp_fwd); autograd casts the fp32 input gradients back to the
+# producers' dtype.  Ops with bf16 storage paths (BatchNorm, BN-ReLU-1x1, skip
+# fusion, SE over BN, the exact x2 resize) use _bn_fwd and keep bf16.
 _amp_fwd = torch.amp.custom_fwd(device_type="cuda", cast_inputs=torch.float32)
 _amp_bwd = torch.amp.custom_bwd(device_type="cuda")
 # ops with bf16 storage paths pick their dtype themselves (no autocast cast)
@@ -103,28 +105,40 @@ class GradSlot:
         return g
 
 
+def _x2_exact(x, ho, wo, sh, sw, align) -> bool:
+    """The exact x2 upsample (align_corners=False): the resize shape with bf16 kernels."""
+    n, c, hi, wi = x.shape
+    return (not align and sh == 0.5 and sw == 0.5 and ho == 2 * hi and wo == 2 * wi
+            and n * c <= 65535)
+
+
 class _Bilinear(torch.autograd.Function):
+    # bf16 storage (autocast) for the exact x2 upsample -- the decoder's
+    # GuideDepth.py:49,52,55, between bf16 convolutions -- so no cast copies
+    # surround it; other ratios compute in fp32.
     @staticmethod
-    @_amp_fwd
+    @_bn_fwd
     def forward(ctx, x, ho, wo, sh, sw, align, slot=None):
-        x = x.contiguous()
+        keep = x.dtype == torch.bfloat16 and _x2_exact(x, ho, wo, sh, sw, align)
+        x = (x if keep else x.float()).contiguous()
         n, c, hi, wi = x.shape
         y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device)
         _abi.call("mde_bilinear_fwd", _abi.ptr(x), _abi.ptr(y), n, c, hi, wi, ho, wo,
                   sh, sw, int(align), _abi.dtype_code(x), _abi.stream_of(x))
         ctx.meta = (n, c, hi, wi, ho, wo, sh, sw, int(align))
-        ctx.slot = slot
+        ctx.slot, ctx.dt = slot, x.dtype
         return y
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, gy):
         n, c, hi, wi, ho, wo, sh, sw, align = ctx.meta
-        gy = gy.contiguous()
+        gy = gy.to(ctx.dt).contiguous()
         gx = torch.empty((n, c, hi, wi), dtype=gy.dtype, device=gy.device)
         g2 = ctx.slot.take() if ctx.slot is not None else None
         if g2 is not None:  # the other consumer's gradient, summed on load
-            _abi.call("mde_bilinear_bwd2", _abi.ptr(gy), _abi.ptr(g2.to(gy.dtype).contiguous()),
+            g2 = g2.to(gy.dtype).contiguous()  # held until the launch is enqueued
+            _abi.call("mde_bilinear_bwd2", _abi.ptr(gy), _abi.ptr(g2),
                       _abi.ptr(gx), n, c, hi, wi, ho, wo, sh, sw, align, _abi.dtype_code(gy),
                       _abi.stream_of(gy))
         else:
@@ -135,9 +149,9 @@ class _Bilinear(torch.autograd.Function):
 
 def bilinear_slot(x, ho, wo, sh, sw, align) -> Optional[GradSlot]:
     """A GradSlot for bilinear_resize's output when its backward can take a
-    second gradient (the x2 pair kernel, fp32, autograd recording), else None."""
-    if (not torch.is_grad_enabled() or not x.requires_grad or x.dtype != torch.float32
-            or torch.is_autocast_enabled()):
+    second gradient (the x2 pair kernel, fp32 or bf16, autograd recording), else None."""
+    if (not torch.is_grad_enabled() or not x.requires_grad
+            or x.dtype not in (torch.float32, torch.bfloat16)):
         return None
     n, c, hi, wi = x.shape
     ok = _abi.query("mde_bilinear_bwd2_supported", n, c, hi, wi, ho, wo, sh, sw, int(align))

@@ -273,9 +273,13 @@ class _SeBnCat(torch.autograd.Function):
     ReLUs and both BatchNorms as one reduction pass + one apply pass."""
 
     @staticmethod
-    @_amp_fwd
+    @_bn_fwd
     def forward(ctx, ya, yb, ga, ba, pba, gb, bb, pbb, w1, w2, meta_a, meta_b, sta, stb):
-        ya, yb = ya.contiguous(), yb.contiguous()
+        # bf16 storage when either branch is bf16 (autocast; the guide branch's
+        # fp32 raw output -- its 3x3 conv on the HIP fp32 kernel -- is rounded,
+        # as the reference's bf16 convolution would have produced it)
+        dt = torch.bfloat16 if torch.bfloat16 in (ya.dtype, yb.dtype) else torch.float32
+        ya, yb = ya.to(dt).contiguous(), yb.to(dt).contiguous()
         w1, w2 = w1.contiguous(), w2.contiguous()
         n, ca, h, w = ya.shape
         cb = yb.shape[1]
@@ -300,7 +304,7 @@ class _SeBnCat(torch.autograd.Function):
                           _abi.ptr(pb), _abi.ptr(rm), _abi.ptr(rv), _abi.ptr(nbt), float(momentum),
                           float(eps), 1, *[_abi.ptr(v) for v in views], n, cc, h, w, _abi.ptr(ws),
                           _abi.dtype_code(y), st)
-        out = torch.empty((n, c, h, w), **f32)
+        out = torch.empty((n, c, h, w), dtype=dt, device=ya.device)
         s, hidden, semean = torch.empty((n, c), **f32), torch.empty((n, cr), **f32), torch.empty((n, c), **f32)
         ws = _ws(_abi.query("mde_se_bn_workspace", n, c, cr, h, w), ya)
         _abi.call("mde_se_bn_fwd", _abi.ptr(ya), ca, _abi.ptr(yb), cb, _abi.ptr(scale),
@@ -314,7 +318,7 @@ class _SeBnCat(torch.autograd.Function):
     @_amp_bwd
     def backward(ctx, gout):
         ya, yb, w1, w2, scale, shift, mean, invstd, s, hidden, semean = ctx.saved_tensors
-        gout = gout.contiguous()
+        gout = gout.to(ya.dtype).contiguous()
         n, ca, h, w = ya.shape
         c, cr = ca + yb.shape[1], w1.shape[0]
         gya, gyb = torch.empty_like(ya), torch.empty_like(yb)
@@ -337,7 +341,7 @@ class _SeBnCat(torch.autograd.Function):
 def se_bn_cat(ya, yb, bn_a: nn.BatchNorm2d, bn_b: nn.BatchNorm2d, pb_a, pb_b, w1, w2,
               stats_a=None, stats_b=None):
     """SELayer(cat([relu(bn_a(ya + pb_a)), relu(bn_b(yb + pb_b))], 1)) on the fused
-    HIP path (training-mode BatchNorms, fp32).  ya / yb are the raw outputs of
+    HIP path (training-mode BatchNorms; fp32, or bf16 storage under autocast).  ya / yb are the raw outputs of
     the 1x1 convs ending feature_conv / guide_conv (modules.py:42-59) and
     stats_a / stats_b their per-block statistics from the conv epilogue (or
     None: a statistics pass).  w1 / w2: SE_block.fc[0] / fc[2] weights."""
@@ -552,15 +556,16 @@ def run_sequential(seq: nn.Sequential, x):
 
 def run_sequential_raw(seq: nn.Sequential, x):
     """For Conv(bias) -> BN(relu) -> ReLU slot -> 1x1 Conv(bias) -> BN(relu) ->
-    ReLU slot in training mode (fp32): run it WITHOUT the last BatchNorm + ReLU
+    ReLU slot in training mode (fp32, or bf16 under autocast: the 3x3 conv on
+    MIOpen bf16, the BN-ReLU-1x1 pair on its bf16 kernels): run it WITHOUT the last BatchNorm + ReLU
     and return (y2, stats2, bn2, conv2_bias) -- the last BN's raw input, its
     per-block statistics from the 1x1 conv's epilogue (None when that conv is
     not the HIP pointwise kernel), the BN module and its folded bias -- for a
     consumer that applies that BN itself (se_bn_cat, skip_reduce_bn).  None
     when the pattern or the conditions do not hold (then run_sequential)."""
     mods = list(seq)
-    if (len(mods) != 6 or not x.is_cuda or x.dtype != torch.float32
-            or torch.is_autocast_enabled() or not _bnrelu_pw_at(mods, 0, x.shape)
+    if (len(mods) != 6 or not x.is_cuda or x.dtype not in (torch.float32, torch.bfloat16)
+            or not _bnrelu_pw_at(mods, 0, x.shape)
             or not isinstance(mods[5], nn.Identity) or mods[4].act != "relu"
             or not mods[1].training or not mods[4].training):
         return None
@@ -590,9 +595,11 @@ class _SkipReduceBN(torch.autograd.Function):
     BN runs its apply pass only."""
 
     @staticmethod
-    @_amp_fwd
+    @_bn_fwd
     def forward(ctx, r, d, weight, bias, gamma, beta, prebias, meta, stats, d_slot=None):
-        r, d = r.contiguous(), d.contiguous()
+        # bf16 storage when r is bf16 (autocast), else fp32; d follows r
+        dt = torch.bfloat16 if r.dtype == torch.bfloat16 else torch.float32
+        r, d = r.to(dt).contiguous(), d.to(dt).contiguous()
         n, cin, h, w = r.shape
         cout = weight.shape[0]
         wm = weight.reshape(cout, cin).contiguous()
@@ -613,7 +620,7 @@ class _SkipReduceBN(torch.autograd.Function):
                       _abi.ptr(prebias), _abi.ptr(rm), _abi.ptr(rv), _abi.ptr(nbt), float(momentum),
                       float(eps), 1, _abi.ptr(scale), _abi.ptr(shift), _abi.ptr(mean),
                       _abi.ptr(invstd), n, cin, h, w, _abi.ptr(ws), _abi.dtype_code(r), st)
-        out = torch.empty((n, cout, h, w), **f32)
+        out = torch.empty((n, cout, h, w), dtype=dt, device=r.device)
         _abi.call("mde_skip_reduce_bn_fwd", _abi.ptr(r), _abi.ptr(d), _abi.ptr(scale),
                   _abi.ptr(shift), _abi.ptr(wm), _abi.ptr(bias), _abi.ptr(out), n, cin, cout, h, w,
                   _abi.dtype_code(r), st)
@@ -625,7 +632,7 @@ class _SkipReduceBN(torch.autograd.Function):
     @_amp_bwd
     def backward(ctx, gout):
         r, d, wm, gamma, beta, scale, shift, mean, invstd = ctx.saved_tensors
-        gout = gout.contiguous()
+        gout = gout.to(r.dtype).contiguous()
         n, cin, h, w = r.shape
         cout = wm.shape[0]
         st = _abi.stream_of(gout)
@@ -662,7 +669,7 @@ class _SkipReduceBN(torch.autograd.Function):
 
 def skip_reduce_bn_ok(r, cout: int) -> bool:
     """Whether skip_reduce_bn has a kernel for this (raw input, output channels)."""
-    return (r.dim() == 4 and r.dtype == torch.float32 and
+    return (r.dim() == 4 and r.dtype in (torch.float32, torch.bfloat16) and
             bool(_abi.query("mde_skip_reduce_bn_supported", r.shape[1], cout, r.shape[2],
                             r.shape[3], 0)))
 

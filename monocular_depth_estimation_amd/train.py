@@ -103,8 +103,10 @@ def synthetic_batch(batch: int, height: int, width: int, rank: int, step: int,
 # ------------------------------------------------------------------ step
 def amp_context(amp: str, device: torch.device):
     """`--amp bf16` (BASELINE cfg3): convolutions / GEMMs autocast to bf16 on
-    MIOpen / hipBLASLt; the HIP kernels keep computing in fp32 (their Functions
-    cast their inputs, functional._amp_fwd).  Weight-cast caching is off so the
+    MIOpen / hipBLASLt; the HIP BatchNorm, BN-ReLU-1x1, skip-fusion, SE-over-BN
+    and x2-resize kernels read and write bf16 activations (fp32 statistics and
+    accumulation); the other HIP kernels compute in fp32 (their Functions cast
+    their inputs, functional._amp_fwd).  Weight-cast caching is off so the
     casts stay inside a captured graph."""
     if amp not in ("", "fp32", "bf16"):
         raise ValueError(f"unsupported --amp {amp!r} (fp32 or bf16)")
@@ -463,7 +465,8 @@ def build_parser():
     p.add_argument("--seed", default=0, type=int)
     p.add_argument("--amp", default="fp32", choices=("fp32", "bf16"),
                    help="bf16 = autocast (BASELINE cfg3): convs / GEMMs in bf16 on MIOpen / hipBLASLt, "
-                        "BN HIP kernels on bf16 activations (fp32 statistics), other HIP kernels fp32")
+                        "HIP BN / BN-ReLU-1x1 / skip / SE-over-BN / x2-resize kernels on bf16 "
+                        "activations (fp32 statistics), other HIP kernels fp32")
     p.add_argument("--pretrained", action="store_true",
                    help="GuideDepth(True) as the reference's train.py:34: load the DDRNet-23-slim "
                         "ImageNet blob (DDRNet_23_slim.py:357-365) non-strictly into the encoder")

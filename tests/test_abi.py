@@ -58,7 +58,10 @@ def test_invalid_arguments_are_rejected_before_launch():
     from monocular_depth_estimation_amd import _abi
     lib = _abi.load()
     assert lib.mde_bilinear_fwd(None, None, 1, 1, 4, 4, 8, 8, 0.5, 0.5, 0, 0, None) == -1
-    assert lib.mde_bilinear_fwd(None, None, 1, 1, 4, 4, 8, 8, 0.5, 0.5, 0, 1, None) == -2  # bf16: v2
+    # bf16 storage: the exact x2 resize has it (null pointers -> invalid), nearest does not
+    assert lib.mde_bilinear_fwd(None, None, 1, 1, 4, 4, 8, 8, 0.5, 0.5, 0, 1, None) == -1
+    assert lib.mde_nearest_fwd(None, None, 1, 1, 4, 4, 8, 8, 0.5, 0.5, 1, None) == -2
+    assert lib.mde_bilinear_fwd(None, None, 1, 1, 4, 4, 8, 8, 0.5, 0.5, 0, 7, None) == -2
     assert lib.mde_nearest_fwd(None, None, 1, 1, 0, 4, 8, 8, 0.5, 0.5, 0, None) == -1
     assert lib.mde_skip_reduce_fwd(None, None, None, None, None, 1, 65, 1, 4, 4, 0, None) == -1
     assert lib.mde_ssim3_l1_fwd(None, None, None, 1.0, 0.1, None, None, None, 1, 1, 8, None, 0,

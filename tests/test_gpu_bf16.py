@@ -171,3 +171,116 @@ def test_skip_reduce_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
     assert torch.equal(ya, yb.to(torch.bfloat16))
     assert torch.equal(ga, gb.to(torch.bfloat16))
     assert torch.equal(wa, wb) and torch.equal(ba, bb_)
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", [(64, 32, 2, 60, 80), (32, 16, 3, 48, 64), (16, 1, 2, 48, 64),
+                                             (4, 1, 2, 30, 40)])
+def test_skip_reduce_bn_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
+    """reduce(relu(bn(r + pb)) + d) (the comb_conv's last BN + ReLU and the skip
+    fusion, modules.py:72-73,100) on bf16 activations == the fp32 kernels on
+    the same values: output and d's gradient bit-exact with the rounded fp32
+    results; 1x1 weight / bias gradients to 1e-5 (the BN coefficients of a bf16
+    and an fp32 input can differ in the last bit: the statistics pass sums in
+    another order per storage width); r's gradient (the BN apply reads the
+    stored, rounded skip gradient) to bf16 rounding."""
+    import copy
+
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, skip_reduce_bn
+    g = torch.Generator().manual_seed(cin + cout + h)
+    r = (torch.rand((n, cin, h, w), generator=g) * 2 - 0.7).to(DEV).to(torch.bfloat16)
+    d = (torch.rand((n, cin, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    go = (torch.rand((n, cout, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    wt = ((torch.rand((cout, cin, 1, 1), generator=g) - 0.5) * 0.3).to(DEV)
+    bias = (torch.rand((cout,), generator=g) - 0.5).to(DEV)
+    pb = (torch.rand((cin,), generator=g) - 0.5).to(DEV)
+    bn = BatchNorm2d(cin, act="relu").to(DEV).train()
+    outs = []
+    for dt in (torch.bfloat16, torch.float32):
+        b = copy.deepcopy(bn)
+        rr = r.detach().to(dt).clone().requires_grad_(True)
+        dd = d.detach().to(dt).clone().requires_grad_(True)
+        ww, bb = wt.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+        y = skip_reduce_bn(rr, b, pb, dd, ww, bb)
+        assert y.dtype == dt
+        y.backward(go.to(dt))
+        outs.append((y.detach(), dd.grad, ww.grad, bb.grad, rr.grad, b.weight.grad,
+                     b.running_var.clone()))
+    (ya, gda, wa, ba, gra, gga, rva), (yb, gdb, wb, bb_, grb, ggb, rvb) = outs
+    assert torch.equal(ya, yb.to(torch.bfloat16))
+    assert torch.equal(gda, gdb.to(torch.bfloat16))
+    torch.testing.assert_close(wa, wb, rtol=1e-5, atol=1e-5 * float(wb.abs().max()))
+    torch.testing.assert_close(ba, bb_, rtol=1e-5, atol=1e-5 * float(bb_.abs().max()))
+    torch.testing.assert_close(rva, rvb, rtol=1e-6, atol=0)
+    assert float((gra.float() - grb).abs().max()) <= 1e-2 * float(grb.abs().max())
+    assert float((gga - ggb).abs().max()) <= 1e-2 * float(ggb.abs().max())
+
+
+@pytest.mark.parametrize("ca,cb,n,h,w", [(16, 16, 2, 60, 80), (8, 8, 3, 48, 64), (32, 32, 2, 30, 40)])
+def test_se_bn_cat_bf16_storage_matches_fp32_kernel(ca, cb, n, h, w):
+    """SELayer(cat([relu(bn_a(ya)), relu(bn_b(yb))])) (modules.py:21-25,49,59,90) on
+    bf16 activations == the fp32 kernels on the same values: SE output and both
+    input gradients bit-exact with the rounded fp32 results; BN parameter and
+    SE weight gradients and the running statistics bit-exact."""
+    import copy
+
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, se_bn_cat
+    g = torch.Generator().manual_seed(ca + cb + h)
+    ya = (torch.rand((n, ca, h, w), generator=g) * 2 - 0.7).to(DEV).to(torch.bfloat16)
+    yb = (torch.rand((n, cb, h, w), generator=g) * 2 - 0.6).to(DEV).to(torch.bfloat16)
+    go = (torch.rand((n, ca + cb, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    c = ca + cb
+    w1 = ((torch.rand((c, c), generator=g) - 0.5) * 0.3).to(DEV)
+    w2 = ((torch.rand((c, c), generator=g) - 0.5) * 0.3).to(DEV)
+    pa = (torch.rand((ca,), generator=g) - 0.5).to(DEV)
+    pbb = (torch.rand((cb,), generator=g) - 0.5).to(DEV)
+    bna, bnb = BatchNorm2d(ca, act="relu").to(DEV).train(), BatchNorm2d(cb, act="relu").to(DEV).train()
+    outs = []
+    for dt in (torch.bfloat16, torch.float32):
+        a, b = copy.deepcopy(bna), copy.deepcopy(bnb)
+        xa = ya.detach().to(dt).clone().requires_grad_(True)
+        xb = yb.detach().to(dt).clone().requires_grad_(True)
+        v1, v2 = w1.clone().requires_grad_(True), w2.clone().requires_grad_(True)
+        out = se_bn_cat(xa, xb, a, b, pa, pbb, v1, v2)
+        assert out.dtype == dt
+        out.backward(go.to(dt))
+        outs.append((out.detach(), xa.grad, xb.grad, a.weight.grad, b.bias.grad, v1.grad, v2.grad,
+                     a.running_mean.clone(), b.running_var.clone()))
+    fa, fb = outs
+    assert torch.equal(fa[0], fb[0].to(torch.bfloat16))
+    assert torch.equal(fa[1], fb[1].to(torch.bfloat16))
+    assert torch.equal(fa[2], fb[2].to(torch.bfloat16))
+    for u, v in zip(fa[3:], fb[3:]):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("c,h,w", [(64, 60, 80), (16, 30, 40), (8, 15, 21)])
+def test_bilinear_x2_bf16_storage_matches_fp32_kernel(c, h, w):
+    """The exact x2 upsample (GuideDepth.py:49,52,55) on bf16 storage == the fp32
+    kernel on the same values, rounded: forward, backward, and the two-gradient
+    backward (the GradSlot sum) bit-exact; wi odd takes the one-column kernels."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.functional import bilinear_resize
+    g = torch.Generator().manual_seed(c + h + w)
+    n = 2
+    x = (torch.rand((n, c, h, w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    gy = (torch.rand((n, c, 2 * h, 2 * w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    gy2 = (torch.rand((n, c, 2 * h, 2 * w), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    res = []
+    for dt in (torch.bfloat16, torch.float32):
+        xx = x.detach().to(dt).clone().requires_grad_(True)
+        y = bilinear_resize(xx, scale_factor=2)
+        assert y.dtype == dt
+        y.backward(gy.to(dt))
+        two = None
+        if w % 2 == 0:
+            two = torch.empty_like(xx)
+            g1, g2 = gy.to(dt).contiguous(), gy2.to(dt).contiguous()  # alive across the launch
+            _abi.call("mde_bilinear_bwd2", _abi.ptr(g1), _abi.ptr(g2), _abi.ptr(two), n, c, h, w,
+                      2 * h, 2 * w, 0.5, 0.5, 0, _abi.dtype_code(xx), _abi.stream_of(xx))
+            torch.cuda.synchronize()
+        res.append((y.detach(), xx.grad, two))
+    (ya, ga, ta), (yb, gb, tb) = res
+    assert torch.equal(ya, yb.to(torch.bfloat16))
+    assert torch.equal(ga, gb.to(torch.bfloat16))
+    if ta is not None:
+        assert torch.equal(ta, tb.to(torch.bfloat16))

@@ -201,8 +201,9 @@ class DualResNet(nn.Module):
         r = self.relu
         low = self.layer1(run_sequential(self.conv1, x))  # conv biases folded into the BNs
         l2 = self.layer2(r(low))
-        l3 = self.layer3(r(l2))
-        high = self.layer3_(r(l2))
+        rl2 = r(l2)  # the reference takes relu(layers[1]) twice (:327, :329; inplace=False): once here
+        l3 = self.layer3(rl2)
+        high = self.layer3_(rl2)
         low = _seq_bn_residual(self.down3, r(high), l3)  # l3 + down3(relu(high)), add fused into BN
         high = high + bilinear_resize(self.compression3(r(l3)), size=out_size)
         l4 = self.layer4(r(low))

@@ -286,6 +286,174 @@ __global__ void __launch_bounds__(64 * kX2Warps)
   }
 }
 
+// bf16 storage (cfg3 autocast), four input columns per lane (wi % 4 == 0): a
+// lane's loads and stores are 8 / 16 bytes, as the fp32 pair kernels' are, so
+// halving the element size halves the instructions per byte instead of the
+// bytes per instruction.  Same filters, same fp32 arithmetic order as the
+// pair kernels (bit-exact with them on the same values, rounded on store).
+__device__ __forceinline__ void ld8(const mde::bf16* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8(mde::bf16* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    w[k] = (uint32_t)mde::f2bf(v[2 * k]) | ((uint32_t)mde::f2bf(v[2 * k + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Flat lane mapping: thread t -> (plane, band of kX2Rows input rows, column
+// quad q), quads fastest, so a wave is fully used whatever wi is (20 quads per
+// row at wi = 80).  Neighbour columns come from the adjacent lanes by wave
+// shuffles, except at a row's first / last quad and the wave's edge lanes,
+// which load them (clamped).  Every lane runs all kX2Rows rows (rows past the
+// plane are clamped and not stored) so the shuffles never sit in divergent
+// control flow.
+struct QuadMap {
+  int64_t total;  // planes * bands * quads
+  int q, quads, i0;
+  int64_t plane;
+  bool live;
+};
+
+__device__ __forceinline__ QuadMap quad_map(int64_t planes, int hi, int wi) {
+  QuadMap m;
+  m.quads = wi >> 2;
+  const int bands = (hi + kX2Rows - 1) / kX2Rows;
+  m.total = planes * bands * (int64_t)m.quads;
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  m.live = t < m.total;
+  if (!m.live) t = m.total - 1;
+  m.q = (int)(t % m.quads);
+  const int64_t r = t / m.quads;
+  m.i0 = (int)(r % bands) * kX2Rows;
+  m.plane = r / bands;
+  return m;
+}
+
+__global__ void __launch_bounds__(256)
+    bilinear_fwd_x2_quad_kernel(const mde::bf16* __restrict__ x, mde::bf16* __restrict__ y,
+                                int64_t planes, int hi, int wi) {
+  const int lane = threadIdx.x & 63;
+  const QuadMap m = quad_map(planes, hi, wi);
+  const int jc = 4 * m.q;
+  const mde::bf16* xp = x + m.plane * hi * (int64_t)wi;
+  const int wo = 2 * wi;
+  mde::bf16* yp = y + m.plane * (2 * hi) * (int64_t)wo + 2 * jc;
+  const bool ledge = lane == 0 || m.q == 0, redge = lane == 63 || m.q == m.quads - 1;
+  // horizontally interpolated input row r: outputs 2jc .. 2jc+7
+  auto hrow = [&](int r, float* o) {
+    r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
+    const mde::bf16* row = xp + (int64_t)r * wi;
+    const float4 c = mde::ld4(row + jc);
+    float l = __shfl_up(c.w, 1, 64), rr = __shfl_down(c.x, 1, 64);
+    if (ledge) l = mde::ld1(row + (jc > 0 ? jc - 1 : 0));
+    if (redge) rr = mde::ld1(row + (jc + 4 < wi ? jc + 4 : wi - 1));
+    const float v[6] = {l, c.x, c.y, c.z, c.w, rr};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      o[2 * k] = 0.25f * v[k] + 0.75f * v[k + 1];
+      o[2 * k + 1] = 0.75f * v[k + 1] + 0.25f * v[k + 2];
+    }
+  };
+  float prev[8], cur[8];
+  hrow(m.i0 - 1, prev);
+  hrow(m.i0, cur);
+#pragma unroll
+  for (int k = 0; k < kX2Rows; ++k) {
+    const int i = m.i0 + k;
+    float nxt[8], a[8], b[8];
+    hrow(i + 1, nxt);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      a[q] = 0.25f * prev[q] + 0.75f * cur[q];
+      b[q] = 0.75f * cur[q] + 0.25f * nxt[q];
+    }
+    if (m.live && i < hi) {
+      st8(yp + (int64_t)(2 * i) * wo, a);
+      st8(yp + (int64_t)(2 * i + 1) * wo, b);
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      prev[q] = cur[q];
+      cur[q] = nxt[q];
+    }
+  }
+}
+
+template <bool TWO>
+__global__ void __launch_bounds__(256)
+    bilinear_bwd_x2_quad_kernel(const mde::bf16* __restrict__ gy, mde::bf16* __restrict__ gx,
+                                int64_t planes, int hi, int wi,
+                                const mde::bf16* __restrict__ gy2) {
+  const int lane = threadIdx.x & 63;
+  const QuadMap m = quad_map(planes, hi, wi);
+  const int jc = 4 * m.q;  // input columns jc .. jc + 3
+  const int ho = 2 * hi, wo = 2 * wi;
+  const mde::bf16* gp = gy + m.plane * ho * (int64_t)wo;
+  const mde::bf16* gp2 = TWO ? gy2 + m.plane * ho * (int64_t)wo : nullptr;
+  mde::bf16* xp = gx + m.plane * hi * (int64_t)wi + jc;
+  const bool ledge = lane == 0 || m.q == 0, redge = lane == 63 || m.q == m.quads - 1;
+  // column-filtered gradient row o for input columns jc .. jc+3
+  auto hrow = [&](int o, float* h) {
+    o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
+    const mde::bf16* row = gp + (int64_t)o * wo;
+    float v[10];  // output-gradient columns 2jc - 1 .. 2jc + 8
+    ld8(row + 2 * jc, v + 1);
+    if (TWO) {
+      float v2[8];
+      ld8(gp2 + (int64_t)o * wo + 2 * jc, v2);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q + 1] += v2[q];
+    }
+    float l = __shfl_up(v[8], 1, 64), r = __shfl_down(v[1], 1, 64);
+    if (ledge) {
+      const int e = 2 * jc > 0 ? 2 * jc - 1 : 0;
+      l = TWO ? mde::ld1(row + e) + mde::ld1(gp2 + (int64_t)o * wo + e) : mde::ld1(row + e);
+    }
+    if (redge) {
+      const int e = 2 * jc + 8 < wo ? 2 * jc + 8 : wo - 1;
+      r = TWO ? mde::ld1(row + e) + mde::ld1(gp2 + (int64_t)o * wo + e) : mde::ld1(row + e);
+    }
+    v[0] = l;
+    v[9] = r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      h[k] = 0.25f * v[2 * k] + 0.75f * v[2 * k + 1] + 0.75f * v[2 * k + 2] + 0.25f * v[2 * k + 3];
+  };
+  float a[4], b[4];
+  hrow(2 * m.i0 - 1, a);
+  hrow(2 * m.i0, b);
+#pragma unroll
+  for (int k = 0; k < kX2Rows; ++k) {
+    const int i = m.i0 + k;
+    float c[4], d[4];
+    hrow(2 * i + 1, c);
+    hrow(2 * i + 2, d);
+    if (m.live && i < hi)
+      mde::st4(xp + (int64_t)i * wi,
+               make_float4(0.25f * a[0] + 0.75f * b[0] + 0.75f * c[0] + 0.25f * d[0],
+                           0.25f * a[1] + 0.75f * b[1] + 0.75f * c[1] + 0.25f * d[1],
+                           0.25f * a[2] + 0.75f * b[2] + 0.75f * c[2] + 0.25f * d[2],
+                           0.25f * a[3] + 0.75f * b[3] + 0.75f * c[3] + 0.25f * d[3]));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      a[q] = c[q];
+      b[q] = d[q];
+    }
+  }
+}
+
+inline dim3 quad_grid(int64_t planes, int64_t hi, int64_t wi) {
+  return dim3((unsigned)mde::cdiv(planes * mde::cdiv(hi, kX2Rows) * (wi / 4), 256));
+}
+
 // Exact integer ratio S = 4 or 8 (align_corners=False, scale 1/S): the
 // MobileNetV3-NewCRF head upsample (model_mobileV3_large_newCRFs.py:55-58,124,
 // 1 x 120x160 -> 480x640).  One lane owns input column j of one plane and a
@@ -696,7 +864,11 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
                     mde::cdiv(wi, 64) >= 2 * mde::cdiv(wi / 2, 64);
   if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
     using B = mde::bf16;
-    if (pair)
+    if (x2 && wi % 4 == 0)
+      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_quad_kernel,
+                 quad_grid(n * c, hi, wi), dim3(256), 0, (const B*)x, (B*)y, n * c, (int)hi,
+                 (int)wi);
+    else if (pair)
       MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_pair_kernel<B>,
                  x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)x, (B*)y, (int)hi,
                  (int)wi);
@@ -751,7 +923,11 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes);
   if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
     using B = mde::bf16;
-    if (x2 && !xs && wi % 2 == 0)
+    if (x2 && !xs && wi % 4 == 0)
+      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, bilinear_bwd_x2_quad_kernel<false>,
+                 quad_grid(planes, hi, wi), dim3(256), 0, (const B*)gy, (B*)gx, planes, (int)hi,
+                 (int)wi, nullptr);
+    else if (x2 && !xs && wi % 2 == 0)
       MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_pair_kernel<false, B>),
                  x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx,
                  (int)hi, (int)wi, nullptr);
@@ -823,6 +999,12 @@ int mde_bilinear_bwd2(const void* gy, const void* gy2, void* gx, int64_t n, int6
   const double bytes = 4.0 * n * c * (double)(hi * wi + 2 * ho * wo);
   if (dtype == MDE_BF16) {
     using B = mde::bf16;
+    if (wi % 4 == 0) {
+      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, bilinear_bwd_x2_quad_kernel<true>,
+                 quad_grid(n * c, hi, wi), dim3(256), 0, (const B*)gy, (B*)gx, n * c, (int)hi,
+                 (int)wi, (const B*)gy2);
+      return MDE_OK;
+    }
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_pair_kernel<true, B>),
                x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx, (int)hi,
                (int)wi, (const B*)gy2);

@@ -86,6 +86,17 @@ def _main():
         report(f"bilinear_bwd x2 {c}x{h}x{w}", timeit(lambda: _abi.call(
             "mde_bilinear_bwd", gy.data_ptr(), x.data_ptr(), n, c, h, w, ho, wo, 0.5, 0.5, 0, 0,
             _abi.stream_of(x)), a.reps), nb)
+    # the same x2 upsample on bf16 storage (cfg3 autocast): half the bytes
+    for c, h, w in ((64, 60, 80), (32, 120, 160), (16, 240, 320)) if want("resize") else ():
+        x = torch.rand(n, c, h, w, device=dev).to(torch.bfloat16)
+        gy = torch.rand(n, c, 2 * h, 2 * w, device=dev).to(torch.bfloat16)
+        gx = torch.empty_like(x)
+        nb = 2.0 * n * c * (h * w + 4 * h * w)
+        report(f"bilinear_fwd x2 bf16 {c}x{h}x{w}",
+               timeit(lambda: F.bilinear_resize(x, scale_factor=2), a.reps), nb)
+        report(f"bilinear_bwd x2 bf16 {c}x{h}x{w}", timeit(lambda: _abi.call(
+            "mde_bilinear_bwd", gy.data_ptr(), gx.data_ptr(), n, c, h, w, 2 * h, 2 * w, 0.5, 0.5, 0,
+            1, _abi.stream_of(x)), a.reps), nb)
     for c, hi, wi in ((64, 15, 20), (128, 8, 10)) if want("resize") else ():
         x = torch.rand(n, c, hi, wi, device=dev)
         nb = 4.0 * n * c * (hi * wi + 60 * 80)

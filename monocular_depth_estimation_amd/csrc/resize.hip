@@ -11,6 +11,7 @@
 // Backward is a gather: every input pixel sums the output gradients whose
 // stencil touches it, so there are no atomics and gx is written exactly once.
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -291,6 +292,15 @@ __global__ void __launch_bounds__(64 * kX2Warps)
 // halving the element size halves the instructions per byte instead of the
 // bytes per instruction.  Same filters, same fp32 arithmetic order as the
 // pair kernels (bit-exact with them on the same values, rounded on store).
+__device__ __forceinline__ void ld8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
 __device__ __forceinline__ void ld8(const mde::bf16* p, float* v) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -337,20 +347,21 @@ __device__ __forceinline__ QuadMap quad_map(int64_t planes, int hi, int wi) {
   return m;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_fwd_x2_quad_kernel(const mde::bf16* __restrict__ x, mde::bf16* __restrict__ y,
-                                int64_t planes, int hi, int wi) {
+    bilinear_fwd_x2_quad_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t planes,
+                                int hi, int wi) {
   const int lane = threadIdx.x & 63;
   const QuadMap m = quad_map(planes, hi, wi);
   const int jc = 4 * m.q;
-  const mde::bf16* xp = x + m.plane * hi * (int64_t)wi;
+  const T* xp = x + m.plane * hi * (int64_t)wi;
   const int wo = 2 * wi;
-  mde::bf16* yp = y + m.plane * (2 * hi) * (int64_t)wo + 2 * jc;
+  T* yp = y + m.plane * (2 * hi) * (int64_t)wo + 2 * jc;
   const bool ledge = lane == 0 || m.q == 0, redge = lane == 63 || m.q == m.quads - 1;
   // horizontally interpolated input row r: outputs 2jc .. 2jc+7
   auto hrow = [&](int r, float* o) {
     r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
-    const mde::bf16* row = xp + (int64_t)r * wi;
+    const T* row = xp + (int64_t)r * wi;
     const float4 c = mde::ld4(row + jc);
     float l = __shfl_up(c.w, 1, 64), rr = __shfl_down(c.x, 1, 64);
     if (ledge) l = mde::ld1(row + (jc > 0 ? jc - 1 : 0));
@@ -387,23 +398,22 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-template <bool TWO>
+template <bool TWO, typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_bwd_x2_quad_kernel(const mde::bf16* __restrict__ gy, mde::bf16* __restrict__ gx,
-                                int64_t planes, int hi, int wi,
-                                const mde::bf16* __restrict__ gy2) {
+    bilinear_bwd_x2_quad_kernel(const T* __restrict__ gy, T* __restrict__ gx, int64_t planes,
+                                int hi, int wi, const T* __restrict__ gy2) {
   const int lane = threadIdx.x & 63;
   const QuadMap m = quad_map(planes, hi, wi);
   const int jc = 4 * m.q;  // input columns jc .. jc + 3
   const int ho = 2 * hi, wo = 2 * wi;
-  const mde::bf16* gp = gy + m.plane * ho * (int64_t)wo;
-  const mde::bf16* gp2 = TWO ? gy2 + m.plane * ho * (int64_t)wo : nullptr;
-  mde::bf16* xp = gx + m.plane * hi * (int64_t)wi + jc;
+  const T* gp = gy + m.plane * ho * (int64_t)wo;
+  const T* gp2 = TWO ? gy2 + m.plane * ho * (int64_t)wo : nullptr;
+  T* xp = gx + m.plane * hi * (int64_t)wi + jc;
   const bool ledge = lane == 0 || m.q == 0, redge = lane == 63 || m.q == m.quads - 1;
   // column-filtered gradient row o for input columns jc .. jc+3
   auto hrow = [&](int o, float* h) {
     o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
-    const mde::bf16* row = gp + (int64_t)o * wo;
+    const T* row = gp + (int64_t)o * wo;
     float v[10];  // output-gradient columns 2jc - 1 .. 2jc + 8
     ld8(row + 2 * jc, v + 1);
     if (TWO) {
@@ -448,6 +458,19 @@ __global__ void __launch_bounds__(256)
       b[q] = d[q];
     }
   }
+}
+
+// fp32 x2 on the quad kernels: the backward by default (kbench at the decoder
+// shapes: 34 / 92 / 166 -> 32 / 81 / 164 us); the forward stays on the pair
+// kernel (quad 34 / 112 / 215 vs 35 / 94 / 171 us: its 32-byte-per-lane row
+// stores are slower).  MDE_X2_QUAD = 0 (pair kernels only) / 2 (quad for both)
+// for A/B runs.
+inline int quad_f32() {
+  static const int mode = [] {
+    const char* e = getenv("MDE_X2_QUAD");
+    return e ? atoi(e) : 1;
+  }();
+  return mode;
 }
 
 inline dim3 quad_grid(int64_t planes, int64_t hi, int64_t wi) {
@@ -865,7 +888,7 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
     using B = mde::bf16;
     if (x2 && wi % 4 == 0)
-      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_quad_kernel,
+      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_quad_kernel<B>,
                  quad_grid(n * c, hi, wi), dim3(256), 0, (const B*)x, (B*)y, n * c, (int)hi,
                  (int)wi);
     else if (pair)
@@ -887,6 +910,10 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   } else if (xs == 8) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<8>, xs_grid(n * c, hi, wi),
                dim3(64, kXsWarps), 0, (const float*)x, (float*)y, (int)hi, (int)wi);
+  } else if (x2 && wi % 4 == 0 && quad_f32() > 1) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_quad_kernel<float>,
+               quad_grid(n * c, hi, wi), dim3(256), 0, (const float*)x, (float*)y, n * c, (int)hi,
+               (int)wi);
   } else if (pair) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel<float>,
                x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)x, (float*)y,
@@ -924,7 +951,7 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
     using B = mde::bf16;
     if (x2 && !xs && wi % 4 == 0)
-      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, bilinear_bwd_x2_quad_kernel<false>,
+      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_quad_kernel<false, B>),
                  quad_grid(planes, hi, wi), dim3(256), 0, (const B*)gy, (B*)gx, planes, (int)hi,
                  (int)wi, nullptr);
     else if (x2 && !xs && wi % 2 == 0)
@@ -945,6 +972,10 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   } else if (xs == 8) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<8>, xs_grid(planes, hi, wi),
                dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
+  } else if (x2 && wi % 4 == 0 && quad_f32() > 0) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_quad_kernel<false, float>),
+               quad_grid(planes, hi, wi), dim3(256), 0, (const float*)gy, (float*)gx, planes,
+               (int)hi, (int)wi, nullptr);
   } else if (x2 && wi % 2 == 0) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_pair_kernel<false, float>),
                x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy,
@@ -1000,7 +1031,7 @@ int mde_bilinear_bwd2(const void* gy, const void* gy2, void* gx, int64_t n, int6
   if (dtype == MDE_BF16) {
     using B = mde::bf16;
     if (wi % 4 == 0) {
-      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, bilinear_bwd_x2_quad_kernel<true>,
+      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_quad_kernel<true, B>),
                  quad_grid(n * c, hi, wi), dim3(256), 0, (const B*)gy, (B*)gx, n * c, (int)hi,
                  (int)wi, (const B*)gy2);
       return MDE_OK;
@@ -1008,6 +1039,12 @@ int mde_bilinear_bwd2(const void* gy, const void* gy2, void* gx, int64_t n, int6
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_pair_kernel<true, B>),
                x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx, (int)hi,
                (int)wi, (const B*)gy2);
+    return MDE_OK;
+  }
+  if (wi % 4 == 0 && quad_f32() > 0) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_quad_kernel<true, float>),
+               quad_grid(n * c, hi, wi), dim3(256), 0, (const float*)gy, (float*)gx, n * c,
+               (int)hi, (int)wi, (const float*)gy2);
     return MDE_OK;
   }
   MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_pair_kernel<true, float>),

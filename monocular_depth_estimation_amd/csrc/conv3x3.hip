@@ -623,14 +623,26 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
   float* part = ws;
   float* part2 = ws + (int64_t)p.grid * p.m;
-  if (w % kTW == 0)
+  // the 3-channel guide convs' weight gradients have ~12 flop per byte, under the
+  // fp32 MFMA ridge (157 TF / 8 TB/s ~ 20): timed as HBM-bound under their own id
+  if (CI == 3) {
+    if (w % kTW == 0)
+      MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
+                 dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
+                 p.tiles_per_img, p.ntiles);
+    else
+      MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
+                 dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
+                 p.tiles_per_img, p.ntiles);
+  } else if (w % kTW == 0) {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
                     dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
                     p.tiles_per_img, p.ntiles);
-  else
+  } else {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
                     dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
                     p.tiles_per_img, p.ntiles);
+  }
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
   MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
              dim3((unsigned)mde::cdiv(p.m, 256), split), dim3(256), 0, part, part2, p.grid, p.m);

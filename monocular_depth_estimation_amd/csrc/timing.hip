@@ -25,7 +25,8 @@ const char* const kNames[mde::K_COUNT] = {
     "dwconv_fwd",    "dwconv_bwd_data", "dwconv_bwd_weight", "dwconv_wreduce",
     "layernorm_fwd", "layernorm_bwd",   "layernorm_wreduce", "transpose",
     "pointwise_fwd", "pointwise_bwd", "conv3x3_fwd",  "conv3x3_dgrad",
-    "conv3x3_wgrad", "conv3x3_wreduce", "dwconv_bwd", "eval_sums", "eval_final", "nyu_augment"};
+    "conv3x3_wgrad", "conv3x3_wreduce", "dwconv_bwd", "eval_sums", "eval_final", "nyu_augment",
+    "conv3x3_wgrad_guide"};
 
 struct Pending {
   int kid;

@@ -36,6 +36,7 @@ NAMES = [
     (r"skip_bwd_mfma_kernel<\d+, \d+, false", "pointwise_bwd"),
     (r"conv3x3_fwd_kernel<.*false>", "conv3x3_fwd"),
     (r"conv3x3_fwd_kernel<.*true>", "conv3x3_dgrad"),
+    (r"conv3x3_wgrad_kernel<3,", "conv3x3_wgrad_guide"),
     (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),
     (r"wgrad_reduce[12]_kernel", "conv3x3_wreduce"),
     (r"skip_fwd_kernel", "skip_reduce_fwd"),

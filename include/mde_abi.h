@@ -368,6 +368,24 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
                         int64_t shift, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Token-major Linear backward helpers (fp32), the NewCRF blocks' qk / proj /
+ * fc1 / fc2 Linears (src/newcrf_layers.py:9-27,110-149) whose GEMMs stay on
+ * hipBLASLt.  g / dh / a / da are row-major [t_rows, n] with n % 4 == 0.
+ *   mde_colsum:          gb[n] = sum_t g[t, n]   (the Linear's bias gradient,
+ *                        replacing autograd's `grad.sum(0)`)
+ *   mde_gelu_bwd_colsum: da = dh * GELU'(a) (nn.GELU, erf form, a = fc1's
+ *                        output) AND gb = sum_t da -- fc1's bias gradient in
+ *                        the GELU backward's own pass
+ * Fixed-order two-level reductions (bitwise reproducible); workspace bytes
+ * from mde_colsum_workspace (0 = unsupported shape).
+ * ------------------------------------------------------------------------- */
+size_t mde_colsum_workspace(int64_t t_rows, int64_t n);
+int mde_colsum(const void* g, float* gb, int64_t t_rows, int64_t n, void* workspace, int dtype,
+               void* stream);
+int mde_gelu_bwd_colsum(const void* dh, const void* a, void* da, float* gb, int64_t t_rows,
+                        int64_t n, void* workspace, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Bias-free 1x1 convolution, NCHW: y[n,o,p] = sum_c W[o,c] x[n,c,p].  The
  * guided-upsampling blocks' 1x1 convs (`nn.Conv2d(E, E/2, 1)`, `(E, in, 1)`,
  * src/GuideDepth/model/modules.py:43-74) whose bias is folded into the

@@ -16,7 +16,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
-from .newcrf_layers import (LayerNorm, Mlp, _relative_position_index, nchw_to_tokens,
+from .newcrf_layers import (LayerNorm, Mlp, _relative_position_index, linear_tok, nchw_to_tokens,
                             tokens_to_nchw, to_2tuple, window_attention, window_partition,
                             window_reverse)
 
@@ -55,14 +55,14 @@ class WindowAttention(nn.Module):
     def forward_tokens(self, x_norm, v_norm, h, w):
         """x_norm, v_norm: [B, H*W, C] LayerNorm'd tokens -> proj(attention) [B, H*W, C]."""
         c = self.dim
-        q = self.q(x_norm)
-        kv = self.kv(v_norm)
+        q = linear_tok(self.q, x_norm)
+        kv = linear_tok(self.kv, v_norm)
         qk = torch.cat([q, kv[..., :c]], dim=-1)
         qk_bias = torch.cat([self.q.bias, self.kv.bias[:c]])
         v = kv[..., c:].contiguous().view(x_norm.shape[0], h, w, c)
         o = window_attention(qk, qk_bias, v, self.relative_position_bias_table, h, w,
                              self.num_heads, self.window_size[0], 0, v_bias=self.kv.bias[c:])
-        return self.proj_drop(self.proj(o))
+        return self.proj_drop(linear_tok(self.proj, o))
 
 
 class SAMBLOCK(nn.Module):  # noqa: N801  (reference class name)

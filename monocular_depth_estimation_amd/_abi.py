@@ -123,6 +123,9 @@ SIGNATURES = {
     "mde_eval_workspace": (_sz, [_i64, _i64, _i64]),
     "mde_eval_sums": (_int, [_vp, _vp, _i64, _i64, _i64, _f32, _f32, _int, _c.POINTER(_c.c_int32), _vp,
                              _vp, _int, _vp]),
+    "mde_colsum_workspace": (_sz, [_i64, _i64]),
+    "mde_colsum": (_int, [_vp, _vp, _i64, _i64, _vp, _int, _vp]),
+    "mde_gelu_bwd_colsum": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _int, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_timing_enable": (_int, [_int]),

@@ -61,6 +61,8 @@ enum Kid : int {
   K_EVAL_FINAL,
   K_NYU_AUGMENT,
   K_C3_WGRAD_GUIDE,  // the 3-channel guide convs' weight gradient (HBM-bound: ~12 flop/B)
+  K_COLSUM,
+  K_MLP_GELU_BWD,
   K_COUNT
 };
 

@@ -7,8 +7,10 @@ shift, partition, QK^T + relative-position bias + shift mask, softmax, AV,
 reverse, unshift, crop — is ONE HIP kernel on MFMA
 (functional.window_attention); tokens stay in [B, H*W, C] order throughout,
 so the reference's pad / roll / permute / contiguous copies disappear.
-LayerNorm, the qk / proj / MLP Linears (hipBLASLt) and GELU run on
-PyTorch-ROCm.
+The qk / proj / MLP Linears are hipBLASLt GEMMs; their bias gradients come
+from a HIP column sum (mde_colsum), and fc1's together with the GELU backward
+in one pass (mde_gelu_bwd_colsum) -- fp32 training; under autocast the plain
+modules run.
 """
 from __future__ import annotations
 
@@ -25,6 +27,77 @@ def to_2tuple(v):
     return tuple(v) if isinstance(v, (tuple, list)) else (v, v)
 
 
+def _colsum(g2):
+    """Sum over the token rows of a contiguous [T, N] fp32 gradient (a Linear's bias gradient)."""
+    t, n = g2.shape
+    gb = torch.empty(n, dtype=torch.float32, device=g2.device)
+    ws = _ws(_abi.query("mde_colsum_workspace", t, n), g2)
+    _abi.call("mde_colsum", _abi.ptr(g2), _abi.ptr(gb), t, n, _abi.ptr(ws), 0, _abi.stream_of(g2))
+    return gb
+
+
+def _tok_ok(x, *widths) -> bool:
+    """The fused token-major path: fp32 CUDA tensors, no autocast, widths % 4 == 0."""
+    return (x.is_cuda and x.dtype == torch.float32 and not torch.is_autocast_enabled()
+            and all(int(n) % 4 == 0 for n in widths)
+            and bool(_abi.query("mde_colsum_workspace", max(1, x.numel() // x.shape[-1]),
+                                max(int(n) for n in widths))))
+
+
+class _LinearTok(torch.autograd.Function):
+    """F.linear(x, W, b) over tokens (hipBLASLt) whose backward sums the bias
+    gradient with mde_colsum (one fixed-order pass over g) instead of
+    autograd's `grad.sum(0)`; the two GEMMs are the ones autograd runs."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, weight = ctx.saved_tensors
+        g2 = g.reshape(-1, g.shape[-1]).contiguous()
+        gx = (g2 @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
+        gw = g2.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
+        gb = _colsum(g2) if ctx.needs_input_grad[2] else None
+        return gx, gw, gb
+
+
+class _LinearGelu(torch.autograd.Function):
+    """gelu(F.linear(x, W1, b1)) (Mlp fc1 + nn.GELU, reference :9-27): the
+    backward's GELU derivative (erf form) and fc1's bias gradient come from ONE
+    pass (mde_gelu_bwd_colsum: read dh and a, write da, column-sum da)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        a = F.linear(x, weight, bias)
+        ctx.save_for_backward(x, weight, a)
+        return F.gelu(a)
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, weight, a = ctx.saved_tensors
+        dh2 = dh.reshape(-1, dh.shape[-1]).contiguous()
+        a2 = a.reshape(-1, a.shape[-1])
+        t, n = dh2.shape
+        da = torch.empty_like(a2)
+        gb = torch.empty(n, dtype=torch.float32, device=dh.device)
+        ws = _ws(_abi.query("mde_colsum_workspace", t, n), dh2)
+        _abi.call("mde_gelu_bwd_colsum", _abi.ptr(dh2), _abi.ptr(a2), _abi.ptr(da), _abi.ptr(gb),
+                  t, n, _abi.ptr(ws), 0, _abi.stream_of(dh2))
+        gx = (da @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
+        gw = da.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
+        return gx, gw, gb if ctx.needs_input_grad[2] else None
+
+
+def linear_tok(lin: nn.Linear, x):
+    """lin(x) on the fused-bias-gradient path when it applies (fp32, bias present)."""
+    if lin.bias is not None and _tok_ok(x, lin.out_features):
+        return _LinearTok.apply(x, lin.weight, lin.bias)
+    return lin(x)
+
+
 class Mlp(nn.Module):
     """fc1 -> act -> dropout -> fc2 -> dropout (reference :9-27; dropout 0 on the path)."""
 
@@ -39,6 +112,12 @@ class Mlp(nn.Module):
         self.drop = nn.Dropout(drop)
 
     def forward(self, x):
+        fused = (type(self.act) is nn.GELU and self.act.approximate == "none"
+                 and (self.drop.p == 0.0 or not self.training) and self.fc1.bias is not None
+                 and self.fc2.bias is not None
+                 and _tok_ok(x, self.fc1.out_features, self.fc2.out_features))
+        if fused:
+            return linear_tok(self.fc2, _LinearGelu.apply(x, self.fc1.weight, self.fc1.bias))
         return self.drop(self.fc2(self.drop(self.act(self.fc1(x)))))
 
 
@@ -217,10 +296,10 @@ class WindowAttention(nn.Module):
 
     def forward_tokens(self, x_norm, v, h, w, shift):
         """x_norm: [B, H*W, C] LayerNorm'd tokens, v: [B, H, W, C] -> proj(attention) [B, H*W, C]."""
-        qk = self.qk(x_norm)
+        qk = linear_tok(self.qk, x_norm)
         o = window_attention(qk, self.qk.bias, v, self.relative_position_bias_table, h, w,
                              self.num_heads, self.window_size[0], shift)
-        return self.proj_drop(self.proj(o))
+        return self.proj_drop(linear_tok(self.proj, o))
 
 
 class CRFBlock(nn.Module):

@@ -152,3 +152,32 @@ def test_token_transposes_bit_exact(shape):
     g = torch.from_numpy(seeded(shape, 10, -1, 1)).to(DEV)
     back.backward(g)
     assert torch.equal(x.grad, g)
+
+
+@pytest.mark.parametrize("t,n", [(4800, 512), (307200 // 16, 256), (1000, 4096), (257, 12)])
+def test_colsum_and_gelu_bwd_colsum_vs_float64(t, n):
+    """The Linear bias gradient (mde_colsum, replacing autograd's grad.sum(0)) and
+    the fused GELU backward + fc1 bias gradient (mde_gelu_bwd_colsum; nn.GELU erf
+    form, reference newcrf_layers.py:9-27) against float64 torch."""
+    from monocular_depth_estimation_amd.newcrf_layers import _LinearGelu, _colsum
+    g = torch.Generator().manual_seed(t + n)
+    gy = torch.randn((t, n), generator=g)
+    assert_close = torch.testing.assert_close
+    got = _colsum(gy.to(DEV)).cpu().double()
+    ref = gy.double().sum(0)
+    assert_close(got, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()) + 1e-4)
+    # fused GELU backward through the autograd Function (x @ W1^T + b1 -> gelu)
+    k = 8
+    x = torch.randn((t, k), generator=g)
+    w1 = torch.randn((n, k), generator=g) * 0.5
+    b1 = torch.randn((n,), generator=g) * 0.5
+    xs = [v.to(DEV).requires_grad_(True) for v in (x, w1, b1)]
+    h = _LinearGelu.apply(*xs)
+    h.backward(gy.to(DEV))
+    xd = [v.double().requires_grad_(True) for v in (x, w1, b1)]
+    hd = torch.nn.functional.gelu(torch.nn.functional.linear(*xd))
+    hd.backward(gy.double())
+    assert_close(h.detach().cpu().double(), hd.detach(), rtol=1e-5, atol=1e-5)
+    for a, b in zip(xs, xd):
+        assert_close(a.grad.cpu().double(), b.grad, rtol=1e-4,
+                     atol=1e-4 * float(b.grad.abs().max()))

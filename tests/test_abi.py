@@ -67,6 +67,11 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert lib.mde_ssim3_l1_fwd(None, None, None, 1.0, 0.1, None, None, None, 1, 1, 8, None, 0,
                                 None) == -1
     assert lib.mde_minmax(None, 0, None, None, 0, None) == -1
+    # token-major reductions: widths must be multiples of 4, fp32 only
+    assert lib.mde_colsum_workspace(100, 6) == 0
+    assert lib.mde_colsum_workspace(100, 8) > 0
+    assert lib.mde_colsum(None, None, 100, 8, None, 0, None) == -1
+    assert lib.mde_gelu_bwd_colsum(None, None, None, None, 100, 8, None, 1, None) == -2
     with pytest.raises(_abi.MdeError, match="invalid argument"):
         _abi.call("mde_depthnorm_apply", None, None, None, 0, 0, None)
 

@@ -147,6 +147,23 @@ class Trainer:
             self.model.eval()
 
 
+def bucket_groups(params, bucket_bytes: int):
+    """All-reduce buckets: the parameters in REVERSE registration order (about
+    the order backward finishes their gradients) cut into consecutive groups
+    of at least `bucket_bytes` (the last one may be smaller); every parameter
+    lands in exactly one group."""
+    groups, cur, nbytes = [], [], 0
+    for p in reversed(list(params)):
+        cur.append(p)
+        nbytes += p.numel() * p.element_size()
+        if nbytes >= bucket_bytes:
+            groups.append(cur)
+            cur, nbytes = [], 0
+    if cur:
+        groups.append(cur)
+    return groups
+
+
 class GraphTrainer:
     """The same training step captured into HIP graphs and replayed.
 
@@ -233,15 +250,7 @@ class GraphTrainer:
         split into ~BUCKET_BYTES groups; every .grad becomes a view of its
         bucket (kept across steps: the buffers are zeroed before each backward,
         never re-allocated)."""
-        groups, cur, nbytes = [], [], 0
-        for p in reversed(self.params):
-            cur.append(p)
-            nbytes += p.numel() * p.element_size()
-            if nbytes >= self.BUCKET_BYTES:
-                groups.append(cur)
-                cur, nbytes = [], 0
-        if cur:
-            groups.append(cur)
+        groups = bucket_groups(self.params, self.BUCKET_BYTES)
         buckets = []
         self.bucket_of = {}
         for i, ps in enumerate(groups):

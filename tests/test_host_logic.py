@@ -104,3 +104,19 @@ def test_result_and_average_meter_fields():
     assert a.irmse == pytest.approx((1 + 3 * 3) / 4)
     assert (a.mae, a.rmse_log) == (5, 6)  # swapped, as the reference's average()
     assert (a.gpu_time, a.data_time) == (1.0, 2.0)
+
+
+def test_allreduce_buckets_cover_every_parameter_once():
+    """GraphTrainer's RCCL buckets (train.bucket_groups): reverse registration
+    order, each parameter in exactly one bucket, every bucket but the last at
+    least bucket_bytes -- checked on GuideDepth's real parameter list."""
+    import monocular_depth_estimation_amd as mde
+    from monocular_depth_estimation_amd.train import GraphTrainer, bucket_groups
+    params = [p for p in mde.GuideDepth(pretrained=False).parameters() if p.requires_grad]
+    groups = bucket_groups(params, GraphTrainer.BUCKET_BYTES)
+    flat = [p for g in groups for p in g]
+    assert [id(p) for p in flat] == [id(p) for p in reversed(params)]
+    assert len({id(p) for p in flat}) == len(params)
+    sizes = [sum(p.numel() * p.element_size() for p in g) for g in groups]
+    assert all(s >= GraphTrainer.BUCKET_BYTES for s in sizes[:-1]) and len(groups) >= 2
+    assert bucket_groups([], 1) == []

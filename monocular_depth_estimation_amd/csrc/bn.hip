@@ -293,6 +293,12 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Table kernels take the float4 path when every group of four elements lies
+// in one plane and the element count fits 32-bit index math.
+__host__ __device__ __forceinline__ bool table_vec(int64_t total, int64_t hw) {
+  return (hw & 3) == 0 && total < ((int64_t)1 << 31);
+}
+
 // Channel-table mode for small planes: every block builds all channels'
 // coefficients in LDS (block 0 is the designated writer), then grid-strides.
 template <typename T>
@@ -315,6 +321,18 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   const int64_t total = planes * hw;
+  if (table_vec(total, hw)) {
+    // Four consecutive elements share a plane: float4 traffic, 32-bit index math.
+    const uint32_t total4 = (uint32_t)(total >> 2), hw4 = (uint32_t)(hw >> 2), cc = (uint32_t)c;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total4;
+         t += gridDim.x * blockDim.x) {
+      const uint32_t ch = (t / hw4) % cc;
+      const float4 q = r ? ld4(r + 4 * (int64_t)t) : make_float4(0.f, 0.f, 0.f, 0.f);
+      st4(y + 4 * (int64_t)t,
+          fwd4(ld4(x + 4 * (int64_t)t), q, r != nullptr, tab[ch], tab[c + ch], act));
+    }
+    return;
+  }
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ch = (t / hw) % c;
@@ -516,6 +534,30 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   const int64_t total = planes * hw;
+  if (table_vec(total, hw)) {
+    const uint32_t total4 = (uint32_t)(total >> 2), hw4 = (uint32_t)(hw >> 2), cc = (uint32_t)c;
+    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total4;
+         t += gridDim.x * blockDim.x) {
+      const uint32_t ch = (t / hw4) % cc;
+      const int64_t o = 4 * (int64_t)t;
+      const float sc = tab[ch], sh = tab[c + ch];
+      const float A = tab[2 * c + ch], B = tab[3 * c + ch], D = tab[4 * c + ch];
+      const float4 v = ld4(x + o), g = ld4(gy + o);
+      const float4 q = r ? ld4(r + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+      float4 e, o4;
+      e.x = dy_eff(g.x, v.x, q.x, sc, sh, act);
+      e.y = dy_eff(g.y, v.y, q.y, sc, sh, act);
+      e.z = dy_eff(g.z, v.z, q.z, sc, sh, act);
+      e.w = dy_eff(g.w, v.w, q.w, sc, sh, act);
+      o4.x = A * e.x + B * v.x + D;
+      o4.y = A * e.y + B * v.y + D;
+      o4.z = A * e.z + B * v.z + D;
+      o4.w = A * e.w + B * v.w + D;
+      st4(gx + o, o4);
+      if (gr) st4(gr + o, e);
+    }
+    return;
+  }
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t ch = (t / hw) % c;
@@ -529,6 +571,10 @@ __global__ void __launch_bounds__(256)
 inline int stream_grid(int64_t work) {
   const int64_t b = mde::cdiv(work, 256);
   return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
+}
+
+inline int table_grid(int64_t total, int64_t hw) {
+  return stream_grid(table_vec(total, hw) ? total >> 2 : total);
 }
 
 inline dim3 plane_grid(int64_t planes, int64_t hw) {
@@ -615,7 +661,7 @@ int launch_fwd_apply(const T* x, const T* r, T* y, int64_t n, int64_t c, int64_t
                dim3(256), 0, x, r, y, c, hw, act, A);
   } else {
     MDE_LAUNCH(mde::K_BN_APPLY_SMALL, bytes, s, bn_apply_table_kernel<T>,
-               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 2 * c, x, r, y, n * c, c,
+               dim3(table_grid(n * c * hw, hw)), dim3(256), sizeof(float) * 2 * c, x, r, y, n * c, c,
                hw, act, A);
   }
   return MDE_OK;
@@ -642,7 +688,7 @@ int bwd_apply(const void* gy, const void* x, const void* residual, void* gx, voi
                (T*)gresidual, c, hw, act, P);
   } else {
     MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, bn_bwd_apply_table_kernel<T>,
-               dim3(stream_grid(n * c * hw)), dim3(256), sizeof(float) * 5 * c, (const T*)gy,
+               dim3(table_grid(n * c * hw, hw)), dim3(256), sizeof(float) * 5 * c, (const T*)gy,
                (const T*)x, rr, (T*)gx, (T*)gresidual, n * c, c, hw, act, P);
   }
   return MDE_OK;

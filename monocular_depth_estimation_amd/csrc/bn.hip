@@ -615,12 +615,26 @@ __global__ void __launch_bounds__(256)
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const double ref = (double)ld1(x + ch * hw);
   double s1 = 0.0, s2 = 0.0;
-  for (int b = t; b < G; b += 256) {
-    const float* p = stats + (ch * G + b) * 4;
+  auto acc = [&](const float* p) {
     const double n = (double)p[1], d = (double)p[0] - ref, b1 = (double)p[2];
     s1 += b1 + n * d;
     s2 += (double)p[3] + d * (2.0 * b1 + n * d);
+  };
+  int b = t;
+  // four records in flight per lane (the loads of a latency-bound loop hoisted
+  // ahead of the double chain); the per-lane summation order is unchanged
+  for (; b + 3 * 256 < G; b += 4 * 256) {
+    float q[4][4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float* p = stats + (ch * G + b + k * 256) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[k][j] = p[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc(q[k]);
   }
+  for (; b < G; b += 256) acc(stats + (ch * G + b) * 4);
   s1 = wave_sum_d(s1);
   s2 = wave_sum_d(s2);
   if (lane == 0) {

@@ -563,6 +563,10 @@ int mde_eval_sums(const void* pred, const void* gt, int64_t n, int64_t h, int64_
  * how many it replaced.
  * ------------------------------------------------------------------------- */
 int mde_graph_count_memsets(void* graph, int64_t* count);
+/* counts[6] = {all nodes, kernel, memcpy, memset, event record / wait, other
+ * (child graphs, host nodes, ...)} of a captured graph: the data-parallel
+ * tests use it to see the RCCL collectives captured into the step graph. */
+int mde_graph_node_counts(void* graph, int64_t* counts);
 int mde_graph_replace_memsets(void* graph, int64_t* replaced);
 
 /* ---------------------------------------------------------------------------

@@ -128,6 +128,7 @@ SIGNATURES = {
     "mde_gelu_bwd_colsum": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _int, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
+    "mde_graph_node_counts": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_timing_enable": (_int, [_int]),
     "mde_timing_reset": (_int, []),
     "mde_timing_collect": (_int, []),
@@ -205,6 +206,13 @@ def graph_count_memsets(raw_graph: int) -> int:
     return n.value
 
 
+def graph_node_counts(raw_graph: int) -> dict:
+    """Node census of a captured (uninstantiated, keep_graph=True) hipGraph."""
+    c = (ctypes.c_int64 * 6)()
+    check(load().mde_graph_node_counts(raw_graph, c), "mde_graph_node_counts")
+    return dict(zip(("total", "kernel", "memcpy", "memset", "event", "other"), list(c)))
+
+
 def graph_replace_memsets(raw_graph: int) -> int:
     """Swap the memset nodes of a captured, uninstantiated hipGraph for fill
     kernels (captured memsets are wrong from the second replay on; graph.hip)."""
@@ -221,6 +229,7 @@ def capture_graph(fn, stream, pool=None):
     with torch.cuda.graph(g, stream=stream, pool=pool):
         out = fn()
     n = graph_replace_memsets(g.raw_cuda_graph())
+    g.node_counts = graph_node_counts(g.raw_cuda_graph())
     g.instantiate()
     return g, out, n
 

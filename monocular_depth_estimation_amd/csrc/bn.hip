@@ -841,7 +841,8 @@ int mde_batchnorm_bwd(const void* gy, const void* x, const void* residual,
 /* Training forward with the statistics emitted by the producing conv's
  * epilogue (mde_pointwise_fwd_stats / mde_conv3x3_fwd_stats): stats
  * [c][stats_blocks][4] = (shift, count, s1, s2) of the raw x; no statistics
- * pass over x.  Everything else as mde_batchnorm_fwd_train (fp32 x only). */
+ * pass over x.  Everything else as mde_batchnorm_fwd_train (fp32 or bf16 x;
+ * statistics, coefficients and accumulation fp32). */
 int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float* beta,
                                   const float* prebias, float* running_mean, float* running_var,
                                   int64_t* num_batches_tracked, float momentum, float eps,

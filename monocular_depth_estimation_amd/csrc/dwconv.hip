@@ -874,13 +874,16 @@ __device__ __forceinline__ void dw_bwd_stream_body(const float* __restrict__ gy,
         if (lane < K * K)
           __hip_atomic_store((gf32*)(gw + (int64_t)blockIdx.x * (K * K) + lane), s,
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        // release: every lane's partial store is visible at agent scope before
+        // the ticket; acquire (last block): the partial loads happen after it
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         unsigned prev = 0;
         if (lane == 0)
-          prev = __hip_atomic_fetch_add((gu32*)(cnt + ch), 1u, __ATOMIC_RELAXED,
+          prev = __hip_atomic_fetch_add((gu32*)(cnt + ch), 1u, __ATOMIC_ACQ_REL,
                                         __HIP_MEMORY_SCOPE_AGENT);
         prev = __shfl(prev, 0, 64);
         if (prev == (unsigned)(t.G - 1)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           if (lane < K * K) {
             const float* p = gw + (int64_t)ch * t.G * (K * K) + lane;
             float a = 0.f;

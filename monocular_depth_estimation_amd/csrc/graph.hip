@@ -61,6 +61,31 @@ int mde_graph_count_memsets(void* graph, int64_t* count) {
   return MDE_OK;
 }
 
+int mde_graph_node_counts(void* graph, int64_t* counts) {
+  if (!graph || !counts) return MDE_ERR_INVALID_ARG;
+  hipGraph_t g = (hipGraph_t)graph;
+  size_t n = 0;
+  hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+  if (e != hipSuccess) return (int)e;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && (e = hipGraphGetNodes(g, nodes.data(), &n)) != hipSuccess) return (int)e;
+  for (int i = 0; i < 6; ++i) counts[i] = 0;
+  counts[0] = (int64_t)n;
+  for (hipGraphNode_t node : nodes) {
+    hipGraphNodeType t;
+    if ((e = hipGraphNodeGetType(node, &t)) != hipSuccess) return (int)e;
+    switch (t) {
+      case hipGraphNodeTypeKernel: ++counts[1]; break;
+      case hipGraphNodeTypeMemcpy: ++counts[2]; break;
+      case hipGraphNodeTypeMemset: ++counts[3]; break;
+      case hipGraphNodeTypeEventRecord:
+      case hipGraphNodeTypeWaitEvent: ++counts[4]; break;
+      default: ++counts[5]; break;
+    }
+  }
+  return MDE_OK;
+}
+
 int mde_graph_replace_memsets(void* graph, int64_t* replaced) {
   if (!graph) return MDE_ERR_INVALID_ARG;
   hipGraph_t g = (hipGraph_t)graph;

@@ -59,7 +59,7 @@ class Silog_loss_variance(nn.Module):  # noqa: N801  (reference class name)
         and it can run inside a captured graph.  No valid pixel -> NaN, as the
         reference's mean over an empty selection."""
         valid = (gt > 1e-3).detach()
-        n = valid.sum().to(prediction.dtype)
+        n = valid.sum(dtype=torch.float32)  # a count: never rounded to bf16 under autocast
         safe_gt = torch.where(valid, gt, torch.ones_like(gt))
         d = torch.where(valid, torch.log(torch.clamp(prediction, min=1e-6)) - torch.log(safe_gt),
                         torch.zeros_like(prediction))

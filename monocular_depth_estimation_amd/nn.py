@@ -708,15 +708,20 @@ class BatchNorm2d(nn.BatchNorm2d):
 
 
 _COUNTERS: dict = {}
+_RETIRED_COUNTERS: list = []
 
 
 def _zeroed_counters(n: int, device) -> torch.Tensor:
     """A persistent all-zero uint32 buffer of >= n entries per device, for the
     kernels' last-block tickets (each kernel leaves its counters zero again).
     Allocated once, outside any graph capture in practice (the first call is an
-    eager warm-up step); calls on one stream never overlap."""
+    eager warm-up step); calls on one stream never overlap.  A buffer replaced
+    by a larger one stays alive: a graph captured earlier still addresses it,
+    and its replays must not touch memory the caching allocator reissued."""
     buf = _COUNTERS.get(device)
     if buf is None or buf.numel() < n:
+        if buf is not None:
+            _RETIRED_COUNTERS.append(buf)
         buf = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
         _COUNTERS[device] = buf
     return buf

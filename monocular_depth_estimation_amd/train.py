@@ -118,8 +118,9 @@ class Trainer:
     """One reference training step (train.py:86-114) with a device-side loss log."""
 
     def __init__(self, model, optimizer, loss_fn, world: World, eval_quirk: bool = True,
-                 amp: str = ""):
+                 amp: str = "", buckets: "GradBuckets | None" = None):
         self.model, self.optimizer, self.loss_fn, self.world = model, optimizer, loss_fn, world
+        self.buckets = buckets  # data parallel by GradBuckets instead of a DDP wrapper
         self.eval_quirk = eval_quirk
         self.amp = amp
         self.loss_sum = torch.zeros((), device=world.device)
@@ -130,11 +131,16 @@ class Trainer:
         self.model.train()  # train.py:79
 
     def step(self, image, depth):
+        if self.buckets is not None:
+            self.buckets.begin()  # zeroes the bucket-view gradients
         with amp_context(self.amp, self.world.device):
             pred = self.model(image)
             loss = self.loss_fn(pred, depth)
-        self.optimizer.zero_grad(set_to_none=True)
+        if self.buckets is None:
+            self.optimizer.zero_grad(set_to_none=True)
         loss.backward()
+        if self.buckets is not None:
+            self.buckets.finish()
         self.optimizer.step()
         self.loss_sum += loss.detach()
         self.loss_count += 1
@@ -162,6 +168,90 @@ def bucket_groups(params, bucket_bytes: int):
     if cur:
         groups.append(cur)
     return groups
+
+
+class GradBuckets:
+    """Bucketed gradient all-reduce overlapped with backward (the DP exchange).
+
+    The parameters (reverse registration order, about the order backward
+    finishes them) are cut into ~`bucket_bytes` groups; every .grad becomes a
+    view of its group's flat buffer for good.  A post-accumulate-grad hook
+    counts each bucket's parameters; when the last one is final, the bucket
+    is averaged over the ranks at once -- on `stream` (a side stream forked
+    from the backward stream at that point) when given, so the collective
+    overlaps the rest of the backward and, inside a capture, is captured INTO
+    the step graph.  The collective is issued whenever the buckets exist,
+    also in a one-rank group.  RCCL ("nccl"): one all_reduce(AVG) per bucket;
+    gloo (no AVG): scale by 1/N, then all_reduce(SUM).  The collective order
+    is the hook order, identical on every rank.
+
+    Per step: begin() before the forward (zeroes the buffers, arms the
+    counters), backward, finish() (launches buckets whose parameters got no
+    gradient, joins the side stream)."""
+
+    def __init__(self, params, world: World, bucket_bytes: int, stream=None):
+        if not dist.is_initialized():
+            raise RuntimeError("GradBuckets needs an initialised torch.distributed process group")
+        self.world, self.stream = world, stream
+        self.avg = dist.get_backend() == "nccl"
+        self.groups = bucket_groups(params, bucket_bytes)
+        self.buffers, self.bucket_of = [], {}
+        for i, ps in enumerate(self.groups):
+            flat = torch.zeros(sum(p.numel() for p in ps), device=ps[0].device, dtype=ps[0].dtype)
+            off = 0
+            for p in ps:
+                p.grad = flat[off:off + p.numel()].view_as(p)
+                off += p.numel()
+                self.bucket_of[p] = i
+                p.register_post_accumulate_grad_hook(self._grad_ready)
+            self.buffers.append(flat)
+        self.pending = [-1] * len(self.groups)
+        self.launched = []  # bucket order of the last step (the hook order)
+
+    def __len__(self):
+        return len(self.groups)
+
+    def __iter__(self):
+        return iter(zip(self.groups, self.buffers))
+
+    def begin(self):
+        for flat in self.buffers:
+            flat.zero_()
+        self.pending = [len(ps) for ps in self.groups]
+        self.launched = []
+
+    def _grad_ready(self, p):
+        b = self.bucket_of.get(p)
+        if b is None or self.pending[b] < 0:
+            return
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+
+    def _launch(self, b):
+        self.pending[b] = -1
+        self.launched.append(b)
+        flat = self.buffers[b]
+        if self.stream is None:
+            self._collective(flat)
+            return
+        self.stream.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(self.stream):
+            self._collective(flat)
+
+    def _collective(self, flat):
+        if self.avg:
+            dist.all_reduce(flat, op=dist.ReduceOp.AVG)
+        else:
+            flat.mul_(1.0 / self.world.size)
+            dist.all_reduce(flat)
+
+    def finish(self):
+        for b in range(len(self.groups)):  # parameters that got no gradient this step
+            if self.pending[b] >= 0:
+                self._launch(b)
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
 
 
 class GraphTrainer:
@@ -227,16 +317,16 @@ class GraphTrainer:
             dist.broadcast(self.flat_bn, 0)
         self.static_image = self.static_depth = None
         self.stream = torch.cuda.Stream(device=world.device)  # eager warm-up + capture stream
-        # bucketed all-reduce overlapped with backward (RCCL only: it is captured
-        # into the graph); dp_overlap=True with one rank exercises the same path
+        # bucketed all-reduce overlapped with backward (captured into the step
+        # graph over RCCL; a gloo group runs it eagerly only, see _capture);
+        # dp_overlap=True with a one-rank group issues the same collectives
         if dp_overlap is None:
             dp_overlap = (world.size > 1 and dist.get_backend() == "nccl"
                           and os.environ.get("MDE_DP_OVERLAP", "1") != "0")
-        self.buckets = self._make_buckets() if dp_overlap else None
-        if self.buckets is not None:
+        self.buckets = None
+        if dp_overlap:
             self.side = torch.cuda.Stream(device=world.device)
-            for p in self.params:
-                p.register_post_accumulate_grad_hook(self._grad_ready)
+            self.buckets = GradBuckets(self.params, world, self.BUCKET_BYTES, stream=self.side)
         self.last_loss = None
         self.loss_sum = torch.zeros((), device=world.device)
         self.loss_count = 0
@@ -244,58 +334,15 @@ class GraphTrainer:
     def begin_epoch(self):
         self.model.train()
 
-    # -- bucketed, overlapped all-reduce ------------------------------------
-    def _make_buckets(self):
-        """[(params, flat buffer)], parameters in reverse registration order
-        split into ~BUCKET_BYTES groups; every .grad becomes a view of its
-        bucket (kept across steps: the buffers are zeroed before each backward,
-        never re-allocated)."""
-        groups = bucket_groups(self.params, self.BUCKET_BYTES)
-        buckets = []
-        self.bucket_of = {}
-        for i, ps in enumerate(groups):
-            flat = torch.zeros(sum(p.numel() for p in ps), device=self.world.device,
-                               dtype=ps[0].dtype)
-            off = 0
-            for p in ps:
-                p.grad = flat[off:off + p.numel()].view_as(p)
-                off += p.numel()
-                self.bucket_of[p] = i
-            buckets.append((ps, flat))
-        self.pending = [0] * len(buckets)
-        return buckets
-
-    def _grad_ready(self, p):
-        if self.buckets is None or p not in self.bucket_of:
-            return
-        b = self.bucket_of[p]
-        self.pending[b] -= 1
-        if self.pending[b] == 0:
-            self._launch_bucket(b)
-
-    def _launch_bucket(self, b):
-        self.pending[b] = -1  # launched
-        flat = self.buckets[b][1]
-        self.side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self.side):
-            if self.world.size > 1:
-                flat.mul_(1.0 / self.world.size)
-                dist.all_reduce(flat)
-
     # -- the step's pieces (each runs eagerly or inside a capture) ----------
     def _forward_backward(self):
         if self.buckets is not None:
-            for ps, flat in self.buckets:
-                flat.zero_()
-            self.pending = [len(ps) for ps, _ in self.buckets]
+            self.buckets.begin()
         with amp_context(self.amp, self.world.device):
             loss = self.loss_fn(self.model(self.static_image), self.static_depth)
         loss.backward()
         if self.buckets is not None:
-            for b in range(len(self.buckets)):  # parameters that got no gradient
-                if self.pending[b] >= 0:
-                    self._launch_bucket(b)
-            torch.cuda.current_stream().wait_stream(self.side)
+            self.buckets.finish()
         elif self.world.size > 1:
             grads = [p.grad for p in self.params if p.grad is not None]
             if self.flat_grad is None:
@@ -376,6 +423,10 @@ class GraphTrainer:
         a fill kernel before instantiation: captured memsets are only correct
         on a graph's first replay on this ROCm stack (csrc/graph.hip)."""
         from . import _abi
+        if self.buckets is not None and dist.get_backend() != "nccl":
+            raise RuntimeError("the overlapped bucket all-reduce is captured into the step graph "
+                               "over RCCL only; a gloo group runs GraphTrainer eagerly "
+                               "(eager_steps >= the number of steps)")
         torch.cuda.synchronize()
         self._zero_grad()  # backward allocates .grad in the graph pool (non-bucket mode)
         one_graph = self.world.size == 1 or self.buckets is not None
@@ -434,6 +485,31 @@ class GraphTrainer:
         return out
 
 
+class DeviceLossMeter:
+    """The reference's per-epoch `losses` AverageMeter (train.py:75,112,141),
+    updated every step without a host sync: the trainer accumulates each
+    step's loss on the device (loss_sum, one add per step) and the meter
+    keeps the epoch's starting point; read() -- at the log points only --
+    returns (last loss, epoch average).  The sample weight n is constant
+    within an epoch (fixed per-rank batch, drop_last), so the weighted
+    average of train.py:112 is the plain mean of the epoch's step losses."""
+
+    def __init__(self, trainer):
+        self.trainer = trainer
+        self.sum0 = trainer.loss_sum.detach().clone()
+        self.count0 = trainer.loss_count
+        self.n = 0
+
+    def update(self, n=1):
+        self.n = n
+
+    def read(self):
+        steps = self.trainer.loss_count - self.count0
+        val = float(self.trainer.last_loss.detach())
+        avg = float((self.trainer.loss_sum - self.sum0).detach()) / steps if steps else 0.0
+        return val, avg
+
+
 def make_adam(model, lr=1e-4):
     kw = {}
     if next(model.parameters()).is_cuda:
@@ -448,11 +524,27 @@ def save_checkpoint(path, epoch, model, optimizer, loss):
                 "optimizer_state_dict": optimizer.state_dict(), "loss": loss}, path)
 
 
-def load_checkpoint(path, model, optimizer):
-    """Resume (train.py:59-68): restarts AT the saved epoch (it is re-run)."""
+def load_checkpoint(path, model, optimizer, capturable: bool = False):
+    """Resume (train.py:59-68): restarts AT the saved epoch (it is re-run).
+
+    Optimizer.load_state_dict replaces the param groups with the saved ones,
+    so a checkpoint written by the eager trainer (fused Adam) or by the
+    reference (plain Adam) would turn GraphTrainer's capturable Adam into a
+    non-capturable one, whose step() refuses to be captured.  capturable=True
+    restores fused + capturable on every group and puts each `step` counter
+    on the parameter's device as fp32, as a capturable Adam keeps it."""
     ckpt = torch.load(path, map_location="cpu", weights_only=True)
     unwrap(model).load_state_dict(ckpt["model_state_dict"])
     optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+    if capturable:
+        for group in optimizer.param_groups:
+            group["capturable"] = True
+            group["fused"] = True
+            group["foreach"] = None
+            for p in group["params"]:
+                st = optimizer.state.get(p)
+                if st and "step" in st:
+                    st["step"] = torch.as_tensor(st["step"], dtype=torch.float32).to(p.device)
     return int(ckpt["epoch"]), ckpt["loss"]
 
 
@@ -493,7 +585,6 @@ def main(argv=None):
     world = init_world()
     from . import GuideDepth  # noqa: E402  (loads the HIP library)
     from .loss import SSIML1
-    from .utils import AverageMeter
 
     torch.manual_seed(args.seed)
     if args.weights:
@@ -510,7 +601,7 @@ def main(argv=None):
                           amp=args.amp)
     start_epoch = 0
     if args.cp == 1:  # train.py:59-68: restarts AT the saved epoch
-        start_epoch, _ = load_checkpoint(args.checkpoint, model, optimizer)
+        start_epoch, _ = load_checkpoint(args.checkpoint, model, optimizer, capturable=args.graph)
     log = open(args.log, "a") if (args.log and world.is_main) else None
     loader = None
     if args.data:  # data.py:171-179 on the GPU path; each rank reads a disjoint 1/size of the rows
@@ -531,23 +622,24 @@ def main(argv=None):
 
     for epoch in range(start_epoch, args.epochs):
         trainer.begin_epoch()
-        losses, t0 = AverageMeter(), time.time()
+        losses, t0 = DeviceLossMeter(trainer), time.time()
         n_steps = len(loader) if loader is not None else args.steps_per_epoch
         for pos, (image, depth) in enumerate(batches(epoch)):
             loss = trainer.step(image, depth)
+            losses.update(image.size(0))  # every step, as train.py:112 (no host sync)
             trainer.after_step(pos)
             if pos % 5 == 0 and world.is_main:  # train.py:123-132 (host read at log points only)
-                v = float(loss.detach())
-                losses.update(v, image.size(0))
+                v, avg = losses.read()
                 dt = time.time() - t0
                 print(f"Epoch: [{epoch}][{pos}/{n_steps}]\tTime {dt:.3f}\t"
-                      f"Loss {losses.val:.4f} ({losses.avg:.4f})", flush=True)
+                      f"Loss {v:.4f} ({avg:.4f})", flush=True)
                 if log:
                     log.write(json.dumps({"tag": "Train/Loss", "value": v,
                                           "step": epoch * n_steps + pos}) + "\n")
         if world.is_main:
-            if log:
-                log.write(json.dumps({"tag": "Train/Loss.avg", "value": losses.avg, "step": epoch}) + "\n")
+            if log:  # train.py:141: the mean of EVERY step's loss of the epoch
+                log.write(json.dumps({"tag": "Train/Loss.avg", "value": losses.read()[1],
+                                      "step": epoch}) + "\n")
                 log.flush()
             save_checkpoint(args.checkpoint, epoch, ddp, optimizer, trainer.last_loss.cpu())
     if dist.is_initialized():

@@ -166,6 +166,60 @@ def capture_blocks():
     return out
 
 
+# reference API variants (modules.py:62-65,80,91-96; loader.py:18-19):
+# tag -> (in, expand, out, channel_attention, guidance_type)
+VARIANT_BLOCKS = {
+    "gub_raw": (16, 16, 1, True, "raw"),
+    "gub_none": (16, 16, 1, True, "none"),
+    "gub_noca": (32, 32, 16, False, "full"),
+    "gub_raw_noca": (32, 32, 16, False, "raw"),
+    "gub_none_noca": (64, 64, 32, False, "none"),
+}
+
+
+def capture_variants():
+    """Guided_Upsampling_Block's non-default guidance types / no channel
+    attention, and GuideDepth-S (up / inner features [32, 8, 4])."""
+    from GuideDepth.model.GuideDepth import GuideDepth
+    from GuideDepth.model.modules import Guided_Upsampling_Block
+    import loss as refloss
+    import utils as refutils
+    out = {}
+    for i, (tag, (cin, e, cout, ca, gt)) in enumerate(VARIANT_BLOCKS.items()):
+        m = fill_(Guided_Upsampling_Block(cin, e, cout, kernel_size=3, channel_attention=ca,
+                                          guide_features=3, guidance_type=gt))
+        m.train()
+        guide = torch.from_numpy(seeded((2, 3, 12, 16), 121 + i, 0, 1)).requires_grad_(True)
+        depth = torch.from_numpy(seeded((2, cin, 12, 16), 131 + i, -1, 1)).requires_grad_(True)
+        y = m(guide, depth)
+        gy = torch.from_numpy(seeded(y.shape, 141 + i, -1, 1))
+        y.backward(gy)
+        out.update({f"{tag}::guide": f32(guide), f"{tag}::depth": f32(depth),
+                    f"{tag}::gy": f32(gy), f"{tag}::y": f32(y), f"{tag}::gdepth": f32(depth.grad),
+                    f"{tag}::cfg": np.array([cin, e, cout, int(ca)], dtype=np.int64),
+                    f"{tag}::guidance": np.array(gt)})
+        if guide.grad is not None:  # 'none' never reads the guide
+            out[f"{tag}::gguide"] = f32(guide.grad)
+        grad_summary(m, f"{tag}::", out, full_limit=2048)
+    # GuideDepth-S (loader.py:18-19), train-mode step objective + eval map
+    model = fill_(GuideDepth(pretrained=False, up_features=[32, 8, 4], inner_features=[32, 8, 4]))
+    out["gds::state_dict_keys"] = np.array(list(model.state_dict().keys()))
+    x = torch.from_numpy(seeded((2, 3, 128, 192), 161, 0, 1))  # 64x96 leaves DDRNet BN over 2 values: ill-conditioned
+    depth = torch.from_numpy(seeded((2, 1, 128, 192), 162, 0.1, 10.0))
+    model.train()
+    pred = model(x)
+    dn = refutils.DepthNorm(depth)
+    loss = 1.0 * refloss.SSIM()(pred, dn) + 0.1 * torch.nn.L1Loss()(pred, dn)
+    loss.backward()
+    out.update({"gds::x": f32(x), "gds::depth": f32(depth), "gds::train_pred": f32(pred),
+                "gds::train_loss": f32(loss)})
+    grad_summary(model, "gds::", out, full_limit=512)
+    model.eval()
+    with torch.no_grad():
+        out["gds::eval_pred"] = f32(model(x))
+    return out
+
+
 def capture_losses():
     import loss as refloss
     import utils as refutils
@@ -484,7 +538,7 @@ def main():
             "golden_losses.npz": capture_losses, "golden_guidedepth.npz": capture_guidedepth,
             "golden_trainseq.npz": capture_train_sequence, "golden_newcrf.npz": capture_newcrf,
             "golden_metrics.npz": capture_metrics, "golden_data.npz": capture_data,
-            "golden_sam.npz": capture_sam}
+            "golden_sam.npz": capture_sam, "golden_variants.npz": capture_variants}
     only = set(sys.argv[1:])
     for fname, fn in jobs.items():
         if only and fname not in only:

@@ -1,11 +1,15 @@
 """Data-parallel path on CPU: world size 2 over gloo.
 
-Each rank runs the product training loop's host logic (init_world, wrap_ddp,
-Trainer, per-rank synthetic shards) around the CPU oracle model (the HIP
-modules need a GPU; the DDP plumbing is what is under test).  After one step
-the DDP-averaged gradients on every rank must equal the mean of the per-shard
-gradients computed in a single process, with per-shard DepthNorm and per-shard
-BN batch statistics (no SyncBN, as the reference).
+Each rank runs the product training loop's host logic (init_world, Trainer,
+per-rank synthetic shards) around the CPU oracle model (the HIP modules need a
+GPU; the data-parallel plumbing is what is under test) with either exchange:
+  ddp      -- wrap_ddp (the CLI trainer's torch DDP wrapper);
+  buckets  -- GradBuckets, the bucketed, hook-driven all-reduce GraphTrainer
+              captures into its step graph for N > 1 (here eager, gloo: scale
+              by 1/N + SUM; over RCCL it is one AVG per bucket).
+After one step the averaged gradients on every rank must equal the mean of the
+per-shard gradients computed in a single process, with per-shard DepthNorm and
+per-shard BN batch statistics (no SyncBN, as the reference).
 """
 import os
 import socket
@@ -26,11 +30,12 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
-    from monocular_depth_estimation_amd.train import Trainer, init_world, synthetic_batch, wrap_ddp
+    from monocular_depth_estimation_amd.train import (GradBuckets, Trainer, init_world,
+                                                      synthetic_batch, wrap_ddp)
     from oracle import guidedepth as og
     from oracle import ops
     from oracle.weights import fill_
@@ -38,23 +43,39 @@ def _worker(rank, world, port, out_dir):
     world_ = init_world(backend="gloo")
     assert world_.size == world and world_.rank == rank
     model = fill_(og.GuideDepth())
-    ddp = wrap_ddp(model, world_, bucket_cap_mb=1.0)
     opt = torch.optim.Adam(model.parameters(), 0.0)
-    trainer = Trainer(ddp, opt, ops.train_loss, world_, eval_quirk=False)
+    order = []
+    if mode == "ddp":
+        trainer = Trainer(wrap_ddp(model, world_, bucket_cap_mb=1.0), opt, ops.train_loss, world_,
+                          eval_quirk=False)
+    else:
+        buckets = GradBuckets(list(model.parameters()), world_, 1 << 20)
+        assert len(buckets) >= 3
+        trainer = Trainer(model, opt, ops.train_loss, world_, eval_quirk=False, buckets=buckets)
     trainer.begin_epoch()
     image, depth = synthetic_batch(BS, H, W, rank, step=0, device="cpu")
     loss = trainer.step(image, depth)
+    if mode == "buckets":  # every bucket exchanged exactly once, in hook order
+        order = list(buckets.launched)
+        assert sorted(order) == list(range(len(buckets))), order
+        for ps, flat in buckets:  # .grad is (still) a view of its bucket
+            for p in ps:
+                assert p.grad.data_ptr() >= flat.data_ptr()
+                assert p.grad.data_ptr() < flat.data_ptr() + flat.numel() * flat.element_size()
     grads = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
-    torch.save({"grads": grads, "loss": loss.detach()}, os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.save({"grads": grads, "loss": loss.detach(), "order": order},
+               os.path.join(out_dir, f"rank{rank}.pt"))
     torch.distributed.destroy_process_group()
 
 
 @pytest.mark.timeout(600)
-def test_ddp_gradients_are_the_mean_of_per_shard_gradients():
+@pytest.mark.parametrize("mode", ["ddp", "buckets"])
+def test_ddp_gradients_are_the_mean_of_per_shard_gradients(mode):
     world = 2
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, mode), nprocs=world, join=True)
         res = [torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    assert res[0]["order"] == res[1]["order"]  # the collective order matches across ranks
 
     from monocular_depth_estimation_amd.train import synthetic_batch
     from oracle import guidedepth as og

@@ -161,17 +161,20 @@ def test_bf16_autocast_step_ptmodel():
 
 def test_bucketed_overlapped_allreduce_graph_matches_eager():
     """The N > 1 GraphTrainer path: gradients as views of bucket buffers, each
-    bucket scaled and all-reduced over RCCL on a side stream from a post-
-    accumulate hook, captured INTO the step graph.  Run here with a one-rank
-    "nccl" group (the collectives are real RCCL calls, the sum is the identity):
-    the replayed step must equal the eager Trainer to 1e-6, every parameter
-    must sit in exactly one bucket, and the buckets must stay the .grad
+    bucket all-reduced (AVG) over RCCL on a side stream from a post-accumulate
+    hook, captured INTO the step graph.  Run with a one-rank "nccl" group: the
+    collectives are issued (GradBuckets issues them whenever buckets exist)
+    and the average over one rank is the identity, so the replayed step must
+    equal the eager Trainer to 1e-6.  The graph census proves the capture: the
+    step graph has exactly one collective's worth of nodes per bucket more
+    than the same step captured with the collective stubbed out.  Every
+    parameter sits in exactly one bucket and the buckets stay the .grad
     storage across replays."""
     import os
 
     import torch.distributed as dist
 
-    from monocular_depth_estimation_amd import GuideDepth
+    from monocular_depth_estimation_amd import GuideDepth, _abi
     from monocular_depth_estimation_amd.loss import SSIML1
     from monocular_depth_estimation_amd.train import GraphTrainer, World, synthetic_batch
     own = not dist.is_initialized()
@@ -181,6 +184,20 @@ def test_bucketed_overlapped_allreduce_graph_matches_eager():
         dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device(DEV, 0))
     try:
         ref_losses, _, ref_params = _run(lambda: GuideDepth(pretrained=False), graph=False)
+        # nodes one captured all_reduce(AVG) contributes
+        probe = torch.ones(1 << 20, device=DEV)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            dist.all_reduce(probe, op=dist.ReduceOp.AVG)  # eager warm-up of the communicator
+        torch.cuda.synchronize()
+        g1, _, _ = _abi.capture_graph(lambda: dist.all_reduce(probe, op=dist.ReduceOp.AVG), s)
+        per_collective = g1.node_counts["total"]
+        assert per_collective >= 1, g1.node_counts
+        g1.replay()
+        torch.cuda.synchronize()
+        assert float(probe.min()) == 1.0 and float(probe.max()) == 1.0
+
         torch.manual_seed(0)
         model = GuideDepth(pretrained=False).to(DEV)
         world = World(0, 0, 1, torch.device(DEV))
@@ -196,6 +213,7 @@ def test_bucketed_overlapped_allreduce_graph_matches_eager():
             losses.append(float(tr.step(image, depth).detach()))
         torch.cuda.synchronize()
         assert tr.graphs is not None and tr.graphs[1] is None  # one graph, collectives inside
+        assert sorted(tr.buckets.launched) == list(range(len(tr.buckets)))
         for ps, flat in tr.buckets:  # .grad is still the bucket storage
             for p in ps:
                 assert p.grad.data_ptr() >= flat.data_ptr()
@@ -205,6 +223,14 @@ def test_bucketed_overlapped_allreduce_graph_matches_eager():
         for n, p in model.named_parameters():
             err = float((p.detach() - ref_params[n]).abs().max())
             assert err <= 1e-6 * max(1.0, float(ref_params[n].abs().max())), n
+        with_coll = tr.graphs[0].node_counts
+        tr.buckets._collective = lambda flat: None  # same step, collectives stubbed out
+        tr.graphs = None
+        tr._capture()
+        without = tr.graphs[0].node_counts
+        extra = with_coll["total"] - without["total"]
+        assert extra == len(tr.buckets) * per_collective, (with_coll, without, per_collective,
+                                                            len(tr.buckets))
     finally:
         if own:
             dist.destroy_process_group()

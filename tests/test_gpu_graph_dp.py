@@ -2,12 +2,20 @@
 cuda:0 and talk gloo over GPU tensors (RCCL refuses two ranks on one device;
 the all-reduce / broadcast calls are the same torch.distributed API).
 
-Checks: parameters are bitwise identical on both ranks after 5 steps (2
-eager, capture, 2 replays) although each rank initialised differently (rank
-0's weights are broadcast, gradients all-reduced), and each rank's loss is
-its own shard's loss (ranks see different data, so the losses differ).  BN
-running statistics are rank-local between steps, as under DDP (broadcast
-from rank 0 before every forward), so they are not compared.
+Two exchange schemes, both checked:
+  flat     -- gloo's default in GraphTrainer: graph A -> one flat all-reduce
+              -> graph B (2 eager steps, capture, 2 replays);
+  buckets  -- the overlapped GradBuckets path bench.py runs over RCCL on 8
+              GPUs (hook-driven per-bucket all-reduce on a side stream); gloo
+              cannot be captured, so it runs the step eagerly (eager_steps).
+Checks: (1) the FIRST step's averaged gradient on every rank equals the mean
+of the two shards' gradients, each computed on the rank with the broadcast
+rank-0 weights through torch.autograd.grad (no hooks, no exchange); (2) the
+parameters are bitwise identical on both ranks after 5 steps although each
+rank initialised differently (rank 0's weights are broadcast, gradients
+averaged); (3) each rank's loss is its own shard's loss (the losses differ).
+BN running statistics are rank-local between steps, as under DDP
+(broadcast from rank 0 before every forward), so they are not compared.
 """
 import os
 import socket
@@ -28,34 +36,61 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode):
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.backends.cudnn.deterministic = True
     from monocular_depth_estimation_amd import GuideDepth
     from monocular_depth_estimation_amd.loss import SSIML1
     from monocular_depth_estimation_amd.train import GraphTrainer, init_world, synthetic_batch
     w = init_world(backend="gloo", use_gpu=True, device_index=0)
     torch.manual_seed(rank)  # different init per rank: the trainer must broadcast rank 0's
     model = GuideDepth(pretrained=False).to(w.device)
-    tr = GraphTrainer(model, SSIML1(1.0, 0.1, depth_norm=True), w, lr=1e-4)
+    loss_fn = SSIML1(1.0, 0.1, depth_norm=True)
+    if mode == "buckets":
+        tr = GraphTrainer(model, loss_fn, w, lr=1e-4, dp_overlap=True, eager_steps=1000)
+        assert tr.buckets is not None and len(tr.buckets) >= 2
+    else:
+        tr = GraphTrainer(model, loss_fn, w, lr=1e-4)
+        assert tr.buckets is None
     tr.begin_epoch()
+    # per-shard gradients at the broadcast weights (train-mode BN, no exchange)
+    params = tr.params
+    shard = []
+    for r in range(world):
+        image, depth = synthetic_batch(2, 64, 96, r, 0, w.device)
+        shard.append(torch.autograd.grad(loss_fn(model(image), depth), params))
+    want = [(a + b) / 2 for a, b in zip(*shard)]
     losses = []
+    first = None
     for k in range(5):
         image, depth = synthetic_batch(2, 64, 96, rank, k, w.device)
         losses.append(float(tr.step(image, depth).detach()))
+        if k == 0:
+            first = [p.grad.detach().clone() for p in params]
     torch.cuda.synchronize()
+    gmax = max(float(g.abs().max()) for g in want)
+    worst = 0.0
+    for g, m in zip(first, want):
+        scale = max(float(m.abs().max()), 1e-6 * gmax)  # BN-fed conv biases: true grad 0
+        worst = max(worst, float((g - m).abs().max()) / scale)
     state = {k: v.detach().cpu() for k, v in model.named_parameters()}
-    torch.save({"losses": losses, "state": state}, os.path.join(out_dir, f"rank{rank}.pt"))
+    torch.save({"losses": losses, "state": state, "worst": worst,
+                "first": [g.cpu() for g in first]}, os.path.join(out_dir, f"rank{rank}.pt"))
     torch.distributed.destroy_process_group()
 
 
 @pytest.mark.timeout(900)
-def test_graph_trainer_two_ranks_stay_in_sync():
+@pytest.mark.parametrize("mode", ["flat", "buckets"])
+def test_graph_trainer_two_ranks(mode):
     if not torch.cuda.is_available():
         pytest.skip("no ROCm GPU")
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), d, mode), nprocs=2, join=True)
         r0, r1 = (torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2))
+    for a, b in zip(r0["first"], r1["first"]):  # one averaged gradient on both ranks
+        assert torch.equal(a, b)
+    assert r0["worst"] < 1e-5 and r1["worst"] < 1e-5, (r0["worst"], r1["worst"])
     for k, v in r0["state"].items():
         assert torch.equal(v, r1["state"][k]), k
     assert r0["losses"] != r1["losses"]

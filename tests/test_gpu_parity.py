@@ -13,7 +13,7 @@ import torch
 from oracle import guidedepth as og
 from oracle import ops as oops
 from oracle.weights import fill_, seeded
-from tests.golden.make_golden import NEAREST_CASES, RESIZE_CASES
+from tests.golden.make_golden import NEAREST_CASES, RESIZE_CASES, VARIANT_BLOCKS
 
 pytestmark = pytest.mark.gpu
 
@@ -312,16 +312,72 @@ def test_guided_block_golden(golden, tag, cfg):
     close_map(guide.grad, g[f"{tag}::gguide"], 1e-4, "gguide")
 
 
-def _grad_norm_check(model, g, x, depth):
+@pytest.mark.parametrize("tag", sorted(VARIANT_BLOCKS))
+def test_guided_block_variants_golden(golden, tag):
+    """Reference API variants: guidance_type 'raw' (guide concatenated raw) /
+    other (no guide), channel_attention=False (modules.py:62-65,80,91-96) --
+    the unfused paths of the block -- against the reference's own outputs and
+    every parameter gradient (1e-4 scale-relative)."""
+    from monocular_depth_estimation_amd.GuideDepth.model.modules import Guided_Upsampling_Block
+    g = golden("golden_variants.npz")
+    cin, e, cout, ca, gt = VARIANT_BLOCKS[tag]
+    m = fill_(Guided_Upsampling_Block(cin, e, cout, channel_attention=ca,
+                                      guidance_type=gt)).to(DEV).train()
+    guide = cu(g[f"{tag}::guide"], True)
+    depth = cu(g[f"{tag}::depth"], True)
+    y = m(guide, depth)
+    close_map(y, g[f"{tag}::y"], 1e-4, "y")
+    y.backward(cu(g[f"{tag}::gy"]))
+    close_map(depth.grad, g[f"{tag}::gdepth"], 1e-4, "gdepth")
+    if f"{tag}::gguide" in g:
+        close_map(guide.grad, g[f"{tag}::gguide"], 1e-4, "gguide")
+    else:
+        assert guide.grad is None
+    params = dict(m.named_parameters())
+    names = list(g[f"{tag}::grad_names"])
+    norms = g[f"{tag}::grad_norms"]
+    for n, ref in zip(names, norms):
+        if n.endswith(("_conv.0.bias", "_conv.3.bias")) or ref < 1e-6 * norms.max():
+            continue  # conv biases feeding train-mode BN: true gradient 0 (noise only)
+        got = float(params[n].grad.double().norm())
+        assert abs(got - ref) <= 1e-4 * ref + 1e-7 * norms.max(), (n, got, ref)
+        if f"{tag}::grad::{n}" in g:
+            close_map(params[n].grad, g[f"{tag}::grad::{n}"], 1e-4, n)
+
+
+def test_guidedepth_s_golden(golden):
+    """GuideDepth-S (loader.py:18-19: up / inner features [32, 8, 4]) at
+    128x192: depth maps (train and eval BN) 1e-3, loss 1e-4, gradient norms
+    vs the float64 oracle (1.5e-2 max / 5e-3 median)."""
+    from monocular_depth_estimation_amd.GuideDepth.model.loader import model_builder
+    from monocular_depth_estimation_amd.loss import SSIML1
+    g = golden("golden_variants.npz")
+    model = fill_(model_builder("GuideDepth-S", pretrained=False)).to(DEV).train()
+    assert list(model.state_dict().keys()) == list(g["gds::state_dict_keys"])
+    x = cu(g["gds::x"])
+    pred = model(x)
+    close_map(pred, g["gds::train_pred"], 1e-3, "train-mode depth map")
+    loss = SSIML1(1.0, 0.1)(pred, cu(g["gds::depth"]))
+    close(loss, g["gds::train_loss"], 1e-4, 1e-7)
+    loss.backward()
+    _grad_norm_check(model, g, g["gds::x"], g["gds::depth"], prefix="gds::",
+                     features=((32, 8, 4), (32, 8, 4)))
+    model.eval()
+    with torch.no_grad():
+        close_map(model(x), g["gds::eval_pred"], 1e-3, "eval-mode depth map")
+
+
+def _grad_norm_check(model, g, x, depth, prefix="", features=None):
     """Per-parameter grad norms vs a FLOAT64 run of the oracle (the truth).
 
     The fp32 reference itself sits at max 5.8e-3 / median 1.7e-3 relative
     from that truth on this randomly filled net (measured on the golden);
     the HIP path must stay within 1.5e-2 max / 5e-3 median.
     """
-    names = list(g["grad_names"])
-    ref32 = g["grad_norms"]
-    truth = fill_(og.GuideDepth()).double().train()
+    names = list(g[f"{prefix}grad_names"])
+    ref32 = g[f"{prefix}grad_norms"]
+    kw = {} if features is None else dict(up_features=features[0], inner_features=features[1])
+    truth = fill_(og.GuideDepth(**kw)).double().train()
     oops.train_loss(truth(torch.from_numpy(x).double()), torch.from_numpy(depth).double()).backward()
     tp = dict(truth.named_parameters())
     t64 = np.array([float(tp[n].grad.norm()) for n in names])

@@ -11,7 +11,7 @@ from oracle import ops
 from oracle import guidedepth as og
 from oracle.weights import fill_, seeded
 
-from tests.golden.make_golden import NEAREST_CASES, RESIZE_CASES
+from tests.golden.make_golden import NEAREST_CASES, RESIZE_CASES, VARIANT_BLOCKS
 
 torch.set_num_threads(4)
 
@@ -113,6 +113,43 @@ def test_guided_block_matches_reference(golden, tag, cfg):
     close(depth.grad, g[f"{tag}::gdepth"], rtol=1e-4, atol=1e-5)
     close(guide.grad, g[f"{tag}::gguide"], rtol=1e-4, atol=1e-5)
     _check_grad_summary(m, g, f"{tag}::")
+
+
+@pytest.mark.parametrize("tag", sorted(VARIANT_BLOCKS))
+def test_guided_block_variants_match_reference(golden, tag):
+    """guidance_type 'raw' / other and channel_attention=False (modules.py:62-65,80,91-96)."""
+    g = golden("golden_variants.npz")
+    cin, e, cout, ca, gt = VARIANT_BLOCKS[tag]
+    m = fill_(og.GuidedUpsamplingBlock(cin, e, cout, channel_attention=ca,
+                                        guidance_type=gt)).train()
+    guide = torch.from_numpy(g[f"{tag}::guide"]).requires_grad_(True)
+    depth = torch.from_numpy(g[f"{tag}::depth"]).requires_grad_(True)
+    y = m(guide, depth)
+    close(y, g[f"{tag}::y"], rtol=1e-4, atol=1e-5)
+    y.backward(torch.from_numpy(g[f"{tag}::gy"]))
+    close(depth.grad, g[f"{tag}::gdepth"], rtol=1e-4, atol=1e-5)
+    if f"{tag}::gguide" in g:
+        close(guide.grad, g[f"{tag}::gguide"], rtol=1e-4, atol=1e-5)
+    else:
+        assert guide.grad is None
+    _check_grad_summary(m, g, f"{tag}::")
+
+
+def test_guidedepth_s_matches_reference(golden):
+    """GuideDepth-S = GuideDepth(up/inner features [32, 8, 4]) (loader.py:18-19)."""
+    g = golden("golden_variants.npz")
+    model = fill_(og.GuideDepth(up_features=(32, 8, 4), inner_features=(32, 8, 4))).train()
+    assert list(model.state_dict().keys()) == list(g["gds::state_dict_keys"])
+    x = torch.from_numpy(g["gds::x"])
+    pred = model(x)
+    close_map(pred, g["gds::train_pred"], 1e-4, "train-mode depth map")
+    loss = ops.train_loss(pred, torch.from_numpy(g["gds::depth"]))
+    close(loss, g["gds::train_loss"], rtol=1e-5)
+    loss.backward()
+    _check_grad_summary(model, g, "gds::", rtol=1e-2)
+    model.eval()
+    with torch.no_grad():
+        close_map(model(x), g["gds::eval_pred"], 1e-4, "eval-mode depth map")
 
 
 @pytest.mark.parametrize("tag", ["rand", "close", "anti"])

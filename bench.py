@@ -81,18 +81,44 @@ def _cpu_model_name() -> str:
     return "unknown"
 
 
+def _usable_cpus() -> tuple[int, str]:
+    """Every core this process may run on: the CPU affinity set, capped by the
+    cgroup's CPU quota (cpu.max) when one is set.  On the GPU box
+    os.cpu_count() reports the whole host (256 logical CPUs) while the job's
+    quota is a fraction of it; more threads than the quota only time-slice."""
+    n = len(os.sched_getaffinity(0))
+    how = f"affinity {n}"
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            q = max(1, int(-(-int(quota) // int(period))))
+            how += f", cgroup quota {int(quota) / int(period):g}"
+            n = min(n, q)
+    except (OSError, ValueError):
+        pass
+    return n, how
+
+
+def _lscpu() -> str:
+    import subprocess
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+    except (OSError, subprocess.SubprocessError):
+        return ""
+    keep = ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)")
+    return "; ".join(" ".join(l.split()) for l in out.splitlines() if l.split(":")[0] in keep)
+
+
 def cpu_baseline(args):
     """The oracle (CPU restatement, the same ATen CPU convs / BN as the reference,
     pinned to it by tests/golden) timed on the host: the metric's own shape
-    (640x480, bs 32 = cfg2) for 1 warm-up + `cpu_steps` steps.
-
-    Threads: OMP_NUM_THREADS when set -- the CPU share a job gets on the GPU box
-    (16 per GPU there; os.cpu_count() shows the whole machine's CPUs, which this
-    job may not use) -- else every core os.cpu_count() reports."""
+    (640x480, bs 32 = cfg2) for 1 warm-up + `cpu_steps` steps, and (GuideDepth)
+    BASELINE cfg1 beside it -- 320x240 bs 4, 1 warm-up + 10 steps (SURVEY
+    §8(d)).  Threads: every usable core (_usable_cpus)."""
     from oracle import guidedepth as og
     from oracle import mobilenetv3 as om
     from oracle import ops as oops
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads, how = _usable_cpus()
     torch.set_num_threads(threads)
     if args.workload == "sam":
         from oracle import sam as osam
@@ -103,28 +129,41 @@ def cpu_baseline(args):
     else:
         model = (og.GuideDepth() if args.workload == "guidedepth" else om.PTModel()).train()
     opt = torch.optim.Adam([p for p in model.parameters() if p.requires_grad], 1e-4)
+
+    def timed(bs, h, w, steps):
+        g = torch.Generator().manual_seed(0)
+        img = torch.rand((bs, 3, h, w), generator=g)
+        dep = 0.1 + 9.9 * torch.rand((bs, 1, h, w), generator=g)
+
+        def step():
+            loss = oops.train_loss(model(img), dep)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+
+        step()  # warm-up
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        return time.perf_counter() - t0
+
     bs = args.cpu_bs or args.bs
-    g = torch.Generator().manual_seed(0)
-    img = torch.rand((bs, 3, args.height, args.width), generator=g)
-    dep = 0.1 + 9.9 * torch.rand((bs, 1, args.height, args.width), generator=g)
-
-    def step():
-        loss = oops.train_loss(model(img), dep)
-        opt.zero_grad()
-        loss.backward()
-        opt.step()
-
-    step()  # warm-up
-    t0 = time.perf_counter()
-    for _ in range(args.cpu_steps):
-        step()
-    dt = time.perf_counter() - t0
+    dt = timed(bs, args.height, args.width, args.cpu_steps)
     name = "GuideDepth" if args.workload == "guidedepth" else "PTModel"
-    return {"value": round(bs * args.cpu_steps / dt, 3), "unit": "images/s",
-            "cores": torch.get_num_threads(), "kind": "port",
-            "host_cpu": f"{_cpu_model_name()} ({os.cpu_count()} logical CPUs on the host)",
-            "sample": f"oracle {name} train step (SSIM+0.1*L1, Adam), {args.width}x{args.height} "
-                      f"bs={bs}, fp32, {args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s)"}
+    out = {"value": round(bs * args.cpu_steps / dt, 3), "unit": "images/s",
+           "cores": torch.get_num_threads(), "kind": "port",
+           "host_cpu": f"{_cpu_model_name()} ({os.cpu_count()} logical CPUs on the host; "
+                       f"usable: {how})",
+           "lscpu": _lscpu(),
+           "sample": f"oracle {name} train step (SSIM+0.1*L1, Adam), {args.width}x{args.height} "
+                     f"bs={bs}, fp32, {args.cpu_steps} timed steps after 1 warm-up ({dt:.1f} s)"}
+    if args.workload == "guidedepth":  # BASELINE cfg1: 320x240 bs 4
+        dt1 = timed(4, 240, 320, 10)
+        out["cfg1"] = {"value": round(4 * 10 / dt1, 3), "unit": "images/s",
+                       "s_per_step": round(dt1 / 10, 4), "cores": torch.get_num_threads(),
+                       "sample": f"oracle GuideDepth train step, 320x240 bs=4, fp32, 10 timed "
+                                 f"steps after 1 warm-up ({dt1:.1f} s)"}
+    return out
 
 
 def main():

@@ -236,7 +236,10 @@ int mde_ssim3_l1_fwd(const void* pred, const void* target,
  * masked mode (beta == gamma == 0): L1 over depth > 0 only (losses.py:26-31).
  * out[0] = loss, out[1] = l1, out[2] = clamped ssim term, out[3] = grad term,
  * out[4] = raw ssim mean, out[5] = element count used by L1.
- * Backward recomputes on device; gout is a device fp32 scalar.
+ * The forward leaves the SSIM gradient coefficients in `workspace` (full
+ * 11x11 window); pass the SAME workspace, unmodified, to the backward, which
+ * reads them and the forward's device scalars (fwd_out); gout is a device
+ * fp32 scalar.
  * ------------------------------------------------------------------------- */
 size_t mde_depth_loss_workspace(int64_t b, int64_t h, int64_t w);
 int mde_depth_loss_fwd(const void* pred, const void* gt, float alpha,

@@ -36,6 +36,8 @@
 // with dK of padded keys summed into d(qk bias).  Table and bias gradients
 // are reduced per block in a fixed order into a slab and summed by a second
 // kernel: deterministic, no atomics.
+#include <type_traits>
+
 #include "common.h"
 
 namespace {
@@ -48,6 +50,35 @@ constexpr int LT = 67;       // LDS row pitch of the per-wave [64][64] P / dS ti
                              // 2-way bank conflicts for both the own and the transposed
                              // access pattern; 65 has 4-way)
 constexpr int TABP = 256;    // table slots ((2ws-1)^2 <= 225)
+
+// The backward's per-wave P / dS tile.  Generic windows: [64][LT].  7x7
+// windows (every NewCRF / SAM stage): only keys / queries 0..48 are real, so
+// the tile keeps rows and columns 0..48 plus a zero row / column 49 that the
+// reads of padded keys / queries are redirected to (their P and dS are 0 by
+// construction, so they are never written): 50 x 51 floats = 10.2 KB instead
+// of 17.2 KB, which with <= 168 VGPRs lets three 4-wave blocks share a CU
+// (three waves per SIMD instead of two).
+template <int WS>
+struct Tile {
+  static constexpr bool kCompact = WS == 7;
+  static constexpr int kValid = kCompact ? 49 : NP;  // real keys / queries
+  static constexpr int kRows = kCompact ? 50 : NP;
+  static constexpr int kPitch = kCompact ? 51 : LT;   // <= 2-way conflicts both ways
+  static constexpr int kWords = kRows * kPitch;
+  // tile row / column of key / query index v of 16-tile `t` (static t): only
+  // the last tile (48..63) can hold padded indices
+  template <int t>
+  __device__ static __forceinline__ int clamp(int v) {
+    if constexpr (kCompact && t == 3) return v < kValid ? v : kValid;
+    return v;
+  }
+  template <int t>
+  __device__ static __forceinline__ bool valid(int v) {
+    if constexpr (kCompact && t == 3) return v < kValid;
+    return true;
+  }
+};
+constexpr int kOccBwd7 = 3;  // blocks per CU the 7x7 backward is built for
 constexpr int kHeads = 4;    // heads (= waves) per block
 constexpr int kWinBwd = 4;   // windows per backward block, at most
 
@@ -276,55 +307,170 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Stage this wave's P^T / dS^T registers as T[j][i] (key row, query column).
-__device__ __forceinline__ void stage_t(float (*T)[LT], const f4 s[4][4]) {
-  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-    for (int it = 0; it < 4; ++it)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) T[16 * jt + 4 * g4 + r][16 * it + l16] = s[jt][it][r];
-}
-
 // One 16-key tile of sum_i T[j][i] B[i][c]: o[ct] (C layout: key 16jt + 4g + rr,
 // c = 16ct + l16), B given per lane as b[it][r][ct] = B[16it + 4g + r][16ct + l16].
-__device__ __forceinline__ void mm_tb_tile(float (*T)[LT], int jt, const float b[4][4][2],
-                                           f4 o[2]) {
+template <int WS, int jt>
+__device__ __forceinline__ void mm_tb_tile(const float* T, const float b[4][4][2], f4 o[2]) {
+  using TL = Tile<WS>;
   const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
   o[0] = f4{0.f, 0.f, 0.f, 0.f};
   o[1] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int it = 0; it < 4; ++it)
+  const int rowoff = TL::template clamp<jt>(16 * jt + l16) * TL::kPitch;
+  auto step = [&](auto it_c) {
+    constexpr int it = decltype(it_c)::value;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const float a = T[16 * jt + l16][16 * it + 4 * g4 + r];
+      const float a = T[rowoff + TL::template clamp<it>(16 * it + 4 * g4 + r)];
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) o[ct] = mfma4(a, b[it][r][ct], o[ct]);
     }
+  };
+  step(std::integral_constant<int, 0>{});
+  step(std::integral_constant<int, 1>{});
+  step(std::integral_constant<int, 2>{});
+  step(std::integral_constant<int, 3>{});
+}
+
+// T[j][i] of this lane's own entries (key 16jt + 4g + r, query 16it + l16):
+// 0 for padded keys / queries (never read from LDS, never written).
+template <int WS, int jt, int it>
+__device__ __forceinline__ float own_get(const float* T, int r) {
+  using TL = Tile<WS>;
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int j = 16 * jt + 4 * g4 + r, i = 16 * it + l16;
+  return T[TL::template clamp<jt>(j) * TL::kPitch + TL::template clamp<it>(i)];
+}
+template <int WS, int jt, int it>
+__device__ __forceinline__ void own_put(float* T, int r, float v) {
+  using TL = Tile<WS>;
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int j = 16 * jt + 4 * g4 + r, i = 16 * it + l16;
+  if (TL::template valid<jt>(j) && TL::template valid<it>(i)) T[j * TL::kPitch + i] = v;
+}
+
+template <typename F>
+__device__ __forceinline__ void static_for4(F&& f) {
+  f(std::integral_constant<int, 0>{});
+  f(std::integral_constant<int, 1>{});
+  f(std::integral_constant<int, 2>{});
+  f(std::integral_constant<int, 3>{});
+}
+
+// The backward's P, staged query tile by query tile: S^T columns of one
+// 16-query tile (4 accumulators), their softmax, straight into the LDS tile
+// -- 16 live score registers instead of probs_t's 64 (the register budget of
+// three waves per SIMD).
+template <int WS>
+__device__ __forceinline__ void probs_stage(const Geo& g, const float* __restrict__ qkrow,
+                                            const float* __restrict__ qkb, int head,
+                                            const int* tok, const int* lab, const float* tab,
+                                            float* T) {
+  using TL = Tile<WS>;
+  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
+  const int c2 = 2 * g.c;
+  float ka[4][8];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+    row8(qkrow, c2, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
+  int kj[16];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + 4 * g4 + r;
+      const int y = j / ws, x = j - y * ws;
+      kj[4 * jt + r] = ((y * span + x) << 4) | lab[j];
+    }
+  static_for4([&](auto it_c) {
+    constexpr int it = decltype(it_c)::value;
+    f4 s[4];
+    {
+      float qb[8];
+      row8(qkrow, c2, head * D + 8 * g4, tok[16 * it + l16], qkb, qb);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) s[jt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt) s[jt] = mfma4(ka[jt][k], qb[k], s[jt]);
+    }
+    const int i = 16 * it + l16;
+    const bool iv = i < n;
+    const int yi = i / ws, xi = i - yi * ws, li = lab[i];
+    const int base = (yi + ws - 1) * span + xi + ws - 1;
+    float m = -INFINITY;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int j = 16 * jt + 4 * g4 + r;
+        float v;
+        if (j >= n) {
+          v = -INFINITY;
+        } else if (!iv) {
+          v = 0.f;
+        } else {
+          const int q = kj[4 * jt + r];
+          v = s[jt][r] + tab[base - (q >> 4)];
+          if (g.shift && (q & 15) != li) v += -100.f;
+        }
+        s[jt][r] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(s[jt][r] - m);
+        s[jt][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = iv ? 1.f / sum : 0.f;  // padded query columns -> 0
+    static_for4([&](auto jt_c) {
+      constexpr int jt = decltype(jt_c)::value;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, s[jt][r] * inv);
+    });
+  });
 }
 
 // slab[(blockIdx.x * heads + head) * (ntab + 2D)] = {dT[0..ntab), dkbias[0..D), dvbias[0..D)}
 template <int WS>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
     wattn_bwd_kernel(const float* __restrict__ gout, const float* __restrict__ qk,
                      const float* __restrict__ qkb, const float* __restrict__ v,
                      const float* __restrict__ table, float* __restrict__ gqk,
                      float* __restrict__ gv, float* __restrict__ slab, int nwin, int wpb,
                      Geo g) {
+  using TL = Tile<WS>;
   __shared__ int tok[NP], lab[NP];
   __shared__ float tab[kHeads][TABP], dtab[kHeads][TABP];
-  __shared__ float T[kHeads][NP][LT];
+  __shared__ float Tall[kHeads][TL::kWords];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
   const int head = blockIdx.y * kHeads + w;
   const bool active = head < g.heads;
   const int ws = wsize<WS>(g), span = 2 * ws - 1, ntab = span * span;
   const int c = g.c, c2 = 2 * g.c, hd = head * D;
+  float* T = Tall[w];
   if (active)
     for (int e = lane; e < ntab; e += 64) {
       tab[w][e] = table[e * g.heads + head];
       dtab[w][e] = 0.f;
     }
+  if constexpr (TL::kCompact) {  // the zero row / column padded indices read
+    if (lane < TL::kRows) {
+      T[TL::kValid * TL::kPitch + lane] = 0.f;
+      T[lane * TL::kPitch + TL::kValid] = 0.f;
+    }
+  }
   float dkb[2] = {0.f, 0.f};  // d(k bias)[16ct + l16] partial of this lane
   float dvb[2] = {0.f, 0.f};  // d(v bias): dV of the padded keys (g.vb only)
   for (int wi = 0; wi < wpb; ++wi) {
@@ -344,11 +490,7 @@ __global__ void __launch_bounds__(256, 2)
     // live in T only (not in registers across phases): the register peak is
     // one phase's operands, so the kernel runs two waves per SIMD unspilled.
     if (active) {
-      {
-        f4 s[4][4];
-        probs_t<WS>(g, qkrow, qkb, head, tok, lab, tab[w], s);
-        stage_t(T[w], s);  // P
-      }
+      probs_stage<WS>(g, qkrow, qkb, head, tok, lab, tab[w], T);  // P
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dV = P^T dO
       {
@@ -362,10 +504,10 @@ __global__ void __launch_bounds__(256, 2)
             for (int ct = 0; ct < 2; ++ct)
               b[it][r][ct] = elem(grow, c, hd + 16 * ct + l16, t, nullptr);
           }
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt) {
+        static_for4([&](auto jt_c) {
+          constexpr int jt = decltype(jt_c)::value;
           f4 o[2];
-          mm_tb_tile(T[w], jt, b, o);
+          mm_tb_tile<WS, jt>(T, b, o);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * jt + 4 * g4 + rr];
@@ -378,7 +520,7 @@ __global__ void __launch_bounds__(256, 2)
               for (int ct = 0; ct < 2; ++ct) dvb[ct] += o[ct][rr];
             }
           }
-        }
+        });
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dP^T = V dO^T column by column; dS = P (dP - rowsum(P dP)), P read
@@ -388,8 +530,8 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
           row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], g.vb, va[jt]);
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
+        static_for4([&](auto it_c) {
+          constexpr int it = decltype(it_c)::value;
           float db[8];
           row8(grow, c, hd + 8 * g4, tok[16 * it + l16], nullptr, db);
           f4 dp[4];
@@ -401,21 +543,22 @@ __global__ void __launch_bounds__(256, 2)
             for (int jt = 0; jt < 4; ++jt) dp[jt] = mfma4(va[jt][k], db[k], dp[jt]);
           float pv[4][4];
           float dl = 0.f;
-#pragma unroll
-          for (int jt = 0; jt < 4; ++jt)
+          static_for4([&](auto jt_c) {
+            constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              pv[jt][r] = T[w][16 * jt + 4 * g4 + r][16 * it + l16];
+              pv[jt][r] = own_get<WS, jt, it>(T, r);
               dl += pv[jt][r] * dp[jt][r];
             }
+          });
           dl += __shfl_xor(dl, 16, 64);
           dl += __shfl_xor(dl, 32, 64);
+          static_for4([&](auto jt_c) {
+            constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
-          for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              T[w][16 * jt + 4 * g4 + r][16 * it + l16] = pv[jt][r] * (dp[jt][r] - dl);
-        }
+            for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, pv[jt][r] * (dp[jt][r] - dl));
+          });
+        });
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dQ = dS K * scale: A = dS[i][j] (this lane's own T entries), B = K[j][c] per lane
@@ -430,17 +573,18 @@ __global__ void __launch_bounds__(256, 2)
             for (int ct = 0; ct < 2; ++ct)
               b[jt][r][ct] = elem(qkrow, c2, c + hd + 16 * ct + l16, t, qkb);
           }
-#pragma unroll
-        for (int it = 0; it < 4; ++it) {
+        static_for4([&](auto it_c) {
+          constexpr int it = decltype(it_c)::value;
           f4 q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-          for (int jt = 0; jt < 4; ++jt)
+          static_for4([&](auto jt_c) {
+            constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float a = T[w][16 * jt + 4 * g4 + r][16 * it + l16];  // dS[i][j]
+              const float a = own_get<WS, jt, it>(T, r);  // dS[i][j]
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct) q[ct] = mfma4(a, b[jt][r][ct], q[ct]);
             }
+          });
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * it + 4 * g4 + rr];
@@ -450,7 +594,7 @@ __global__ void __launch_bounds__(256, 2)
                 gqkrow[(unsigned)(t * c2 + hd + 16 * ct + l16)] = q[ct][rr] * g.scale;
             }
           }
-        }
+        });
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dK = dS^T Q * scale (dS from the LDS tile)
@@ -465,10 +609,10 @@ __global__ void __launch_bounds__(256, 2)
             for (int ct = 0; ct < 2; ++ct)
               b[it][r][ct] = g.scale * elem(qkrow, c2, hd + 16 * ct + l16, t, qkb);
           }
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt) {
+        static_for4([&](auto jt_c) {
+          constexpr int jt = decltype(jt_c)::value;
           f4 o[2];
-          mm_tb_tile(T[w], jt, b, o);
+          mm_tb_tile<WS, jt>(T, b, o);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * jt + 4 * g4 + rr];
@@ -480,31 +624,43 @@ __global__ void __launch_bounds__(256, 2)
                 dkb[ct] += o[ct][rr];
             }
           }
-        }
+        });
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // table gradient: entry e <- sum of dS over the (query, key) pairs at
-      // that offset, in a fixed order (query row-major).  Out-of-window pairs
-      // read a clamped address and add 0, so with a compile-time window the
-      // ws*ws reads are unrolled and all in flight (adding +0 leaves the sum
-      // unchanged).
+      // that offset, in a fixed order (query row-major); out-of-window pairs
+      // add 0 (adding +0 leaves the sum unchanged).
       for (int e = lane; e < ntab; e += 64) {
         const int dy = e / span - (ws - 1), dx = e % span - (ws - 1);
         float acc = 0.f;
-        auto add = [&](int ri, int ci) {
-          const int rj = ri - dy, cj = ci - dx;
-          const bool ok = rj >= 0 && rj < ws && cj >= 0 && cj < ws;
-          const float v = T[w][ok ? rj * ws + cj : 0][ri * ws + ci];
-          acc += ok ? v : 0.f;
-        };
         if constexpr (WS > 0) {
+          // T[(ri - dy) ws + ci - dx][ri ws + ci] = Tb[ri (ws P + ws) + ci (P + 1)]:
+          // one per-lane base and compile-time offsets (no per-term address
+          // registers); out-of-window terms read some LDS word and add 0
+          constexpr int P = TL::kPitch;
+          const int basei = -(WS * dy + dx) * P;
+          unsigned rm = 0, cm = 0;
+#pragma unroll
+          for (int k = 0; k < WS; ++k) {
+            rm |= (k - dy >= 0 && k - dy < WS) ? 1u << k : 0u;
+            cm |= (k - dx >= 0 && k - dx < WS) ? 1u << k : 0u;
+          }
 #pragma unroll
           for (int ri = 0; ri < WS; ++ri)
 #pragma unroll
-            for (int ci = 0; ci < WS; ++ci) add(ri, ci);
-        } else {
+            for (int ci = 0; ci < WS; ++ci) {
+              const float v = T[basei + ri * (WS * P + WS) + ci * (P + 1)];
+              acc += ((rm >> ri) & (cm >> ci) & 1u) ? v : 0.f;
+            }
+        }
+        if constexpr (WS == 0) {
           for (int ri = 0; ri < ws; ++ri)
-            for (int ci = 0; ci < ws; ++ci) add(ri, ci);
+            for (int ci = 0; ci < ws; ++ci) {
+              const int rj = ri - dy, cj = ci - dx;
+              const bool ok = rj >= 0 && rj < ws && cj >= 0 && cj < ws;
+              const float v = T[(ok ? rj * ws + cj : 0) * TL::kPitch + ri * ws + ci];
+              acc += ok ? v : 0.f;
+            }
         }
         dtab[w][e] += acc;
       }

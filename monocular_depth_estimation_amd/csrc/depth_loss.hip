@@ -8,11 +8,24 @@
 // Masked mode (beta == gamma == 0, losses.py:26-31): L1 over depth > 0, and
 // the loss is that L1 alone (alpha is not applied).
 //
-// The 11x11 window is applied separably in LDS.  Because the SSIM clamp acts
-// on the MEAN, the gradient scale needs the forward's global result: the
-// backward recomputes per-pixel SSIM coefficients (kernel 1, written to the
-// workspace) and then correlates them with the window (kernel 2), reading the
-// forward scalars and the upstream gradient from device memory (no host sync).
+// Full window (h, w >= 11, the training shapes): two register-streaming
+// kernels, no LDS.  A wave owns a strip of 54 columns (64 lanes, a 5-column
+// halo each side) and a chunk of rows and walks its rows top to bottom: the
+// 11-tap horizontal Gaussian comes from DPP lane shifts, the vertical one
+// from an 11-row register ring, so each input is read once per strip and
+// chunk (plus halos).
+//   forward  (dloss_fwd_stream_kernel): the five local statistics, SSIM, the
+//            loss partial sums (SSIM, L1, gradient term; one record per wave)
+//            AND the three per-position gradient coefficients of SSIM
+//            (A, B, C below, without the global factor) into the workspace;
+//   backward (dloss_bwd_stream_kernel): the clamp gate and scale are global
+//            (the SSIM clamp acts on the MEAN), read from the forward's
+//            device scalars; d/dx = k * (G*A + 2x G*B + y G*C) + the L1 and
+//            gradient-difference terms, G* = the same window, correlated by
+//            the same shift + ring scheme.  No statistic is recomputed.
+// Small maps (K < 11) keep the LDS-tiled kernels, whose backward recomputes
+// the coefficients (dloss_map_kernel<1>) before correlating them.  Masked
+// mode is a plain streaming reduction / elementwise pass.
 #include <cmath>
 
 #include "common.h"
@@ -305,6 +318,372 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ------------------------------------------------------------ streaming
+constexpr int kSD = 54;  // output columns per strip: 64 lanes - 2 x 5 halo
+
+// value of lane - 1 / lane + 1 (DPP wave shift by one lane; 0 shifted in)
+__device__ __forceinline__ float lprev(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float lnext(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
+
+// symmetric 11-tap window: c = g[5], k[i] = g[5 - 1 - i] = g[5 + 1 + i]
+struct Sym11 {
+  float c, k[5];
+};
+
+Sym11 sym11(const Win& w) {
+  Sym11 s;
+  s.c = w.g[5];
+  for (int i = 0; i < 5; ++i) s.k[i] = w.g[4 - i];
+  return s;
+}
+
+struct StreamGeo {
+  int strips, chunks, chunk_rows;
+  int64_t nwaves;
+};
+
+StreamGeo stream_geometry(int64_t b, int64_t h, int64_t w) {
+  StreamGeo g;
+  g.strips = (int)mde::cdiv(w, kSD);
+  // enough waves to fill 256 CUs x 4 SIMDs ~4 deep; >= 32 rows per chunk
+  // (a chunk re-reads 10 halo rows)
+  const int64_t want = mde::cdiv(4096, b * g.strips);
+  int64_t rows = mde::cdiv(h, want < 1 ? 1 : want);
+  if (rows < 32) rows = 32;
+  if (rows > h) rows = h;
+  g.chunk_rows = (int)rows;
+  g.chunks = (int)mde::cdiv(h, rows);
+  g.nwaves = b * g.strips * g.chunks;
+  return g;
+}
+
+// Horizontal pass of one row for NZ fields held one per lane: out[z] =
+// sum_k g_k v_z(col + k - 5), zero outside the loaded columns.
+template <int NZ>
+__device__ __forceinline__ void hpass(const float (&v)[NZ], const Sym11& g, float (&out)[NZ]) {
+  float l[NZ], r[NZ];
+#pragma unroll
+  for (int z = 0; z < NZ; ++z) {
+    l[z] = v[z];
+    r[z] = v[z];
+    out[z] = g.c * v[z];
+  }
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+#pragma unroll
+    for (int z = 0; z < NZ; ++z) {
+      l[z] = lprev(l[z]);
+      r[z] = lnext(r[z]);
+      out[z] = fmaf(g.k[i], l[z] + r[z], out[z]);
+    }
+  }
+}
+
+// Forward.  Lane l of a wave <-> column c = strip * 54 - 5 + l; output lanes
+// 5..58.  Input rows r0 - 5 .. r1 + 4 of the chunk stream through; after
+// row r the map row p = r - 5 is complete (ring slots hold rows p-5..p+5).
+template <bool SSIM>
+__global__ void __launch_bounds__(256)
+    dloss_fwd_stream_kernel(const float* __restrict__ X, const float* __restrict__ Y, int h,
+                            int w, int strips, int chunks, int chunk_rows, int64_t nwaves,
+                            Sym11 g, float c1, float c2, float* __restrict__ part,
+                            float* __restrict__ coef, int64_t plane) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= nwaves) return;
+  const int strip = (int)(wid % strips);
+  const int chunk = (int)((wid / strips) % chunks);
+  const int64_t img = wid / ((int64_t)strips * chunks);
+  const int c = strip * kSD - 5 + lane;
+  const bool cin = c >= 0 && c < w;
+  const bool outl = lane >= 5 && lane < 5 + kSD && c < w;
+  const int cc = c < 0 ? 0 : (c >= w ? w - 1 : c);
+  const int r0 = chunk * chunk_rows;
+  const int r1 = r0 + chunk_rows < h ? r0 + chunk_rows : h;
+  const float* Xi = X + img * (int64_t)h * w + cc;
+  const float* Yi = Y + img * (int64_t)h * w + cc;
+  const int T = (r1 - r0) + 10;  // rows streamed
+
+  float ring[11][5];
+#pragma unroll
+  for (int j = 0; j < 11; ++j)
+#pragma unroll
+    for (int z = 0; z < 5; ++z) ring[j][z] = 0.f;
+  float ssum = 0.f, l1 = 0.f, gr = 0.f, cnt = 0.f;
+  // prefetched row r0 - 5
+  float xn, yn;
+  {
+    const int r = r0 - 5;
+    const int rc = r < 0 ? 0 : r;
+    const bool ok = cin && r >= 0;
+    const float xv = Xi[(int64_t)rc * w], yv = Yi[(int64_t)rc * w];
+    xn = ok ? xv : 0.f;
+    yn = ok ? yv : 0.f;
+  }
+  for (int t0 = 0; t0 < T; t0 += 11) {
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const int t = t0 + j;
+      if (t < T) {
+      const int r = r0 - 5 + t;
+      const float x = xn, y = yn;
+      {  // prefetch row r + 1
+        const int rn = r + 1;
+        const int rc = rn < 0 ? 0 : (rn >= h ? h - 1 : rn);
+        const bool ok = cin && rn >= 0 && rn < h;
+        const float xv = Xi[(int64_t)rc * w], yv = Yi[(int64_t)rc * w];
+        xn = ok ? xv : 0.f;
+        yn = ok ? yv : 0.f;
+      }
+      // image-domain terms of row r (L1, forward differences; xn/yn = row r + 1)
+      if (r >= r0 && r < r1 && outl) {
+        l1 += fabsf(x - y);
+        cnt += 1.f;
+      }
+      const float xr = lnext(x), yr = lnext(y);
+      if (r >= r0 && r < r1 && outl) {
+        if (c < w - 1) gr += fabsf((yr - y) - (xr - x));
+        if (r < h - 1) gr += fabsf((yn - y) - (xn - x));
+      }
+      if (SSIM) {
+        const float v[5] = {x, y, x * x, y * y, x * y};
+        float hv[5];
+        hpass<5>(v, g, hv);
+#pragma unroll
+        for (int z = 0; z < 5; ++z) ring[j][z] = hv[z];
+        if (t >= 10) {  // map row p = r - 5: ring slot of row p + k - 5 is (j + 1 + k) % 11
+          const int p = r - 5;
+          float q[5];
+#pragma unroll
+          for (int z = 0; z < 5; ++z) {
+            float a = g.c * ring[(j + 6) % 11][z];
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+              a = fmaf(g.k[i], ring[(j + 5 - i) % 11][z] + ring[(j + 7 + i) % 11][z], a);
+            q[z] = a;
+          }
+          const float mx = q[0], my = q[1];
+          const float sxx = q[2] - mx * mx, syy = q[3] - my * my;
+          const float sxy = q[4] - mx * my;
+          const float n1 = 2.f * mx * my + c1, n2 = 2.f * sxy + c2;
+          const float d1 = mx * mx + my * my + c1, d2 = sxx + syy + c2;
+          const float D = d1 * d2;
+          const float S = (n1 * n2) / D;
+          if (outl) {
+            ssum += S;
+            if (coef) {
+              const float dS_dsx = -S / d2;
+              const float dS_dsxy = 2.f * n1 / D;
+              const float dS_dmx = 2.f * my * n2 / D - S * 2.f * mx / d1;
+              const int64_t off = (img * h + p) * (int64_t)w + c;
+              coef[off] = dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy;
+              coef[plane + off] = dS_dsx;
+              coef[2 * plane + off] = dS_dsxy;
+            }
+          }
+        }
+      }
+      }
+    }
+  }
+  ssum = mde::wave_sum(ssum);
+  l1 = mde::wave_sum(l1);
+  gr = mde::wave_sum(gr);
+  cnt = mde::wave_sum(cnt);
+  if (lane == 0) {
+    float* o = part + 4 * wid;
+    o[0] = ssum;
+    o[1] = l1;
+    o[2] = gr;
+    o[3] = cnt;
+  }
+}
+
+// Backward: coefficient rows p = r0 - 5 .. r1 + 4 stream through the ring;
+// after row p the image row q = p - 5 has all its window contributions.
+template <bool SSIM, bool GRAD>
+__global__ void __launch_bounds__(256)
+    dloss_bwd_stream_kernel(const float* __restrict__ X, const float* __restrict__ Y, int h,
+                            int w, int strips, int chunks, int chunk_rows, int64_t nwaves,
+                            Sym11 g, const float* __restrict__ coef, int64_t plane,
+                            const float* __restrict__ fwd, const float* __restrict__ gout,
+                            float alpha, float beta, float gamma, float inv_n,
+                            float* __restrict__ gx) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (wid >= nwaves) return;
+  const int strip = (int)(wid % strips);
+  const int chunk = (int)((wid / strips) % chunks);
+  const int64_t img = wid / ((int64_t)strips * chunks);
+  const int c = strip * kSD - 5 + lane;
+  const bool cin = c >= 0 && c < w;
+  const bool outl = lane >= 5 && lane < 5 + kSD && c < w;
+  const int cc = c < 0 ? 0 : (c >= w ? w - 1 : c);
+  const int r0 = chunk * chunk_rows;
+  const int r1 = r0 + chunk_rows < h ? r0 + chunk_rows : h;
+  const int64_t base = img * (int64_t)h * w + cc;
+  const float* Xi = X + base;
+  const float* Yi = Y + base;
+  const float* Ai = coef + base;
+  const int T = (r1 - r0) + 10;
+  const float go = gout[0];
+  float kfac = 0.f;
+  if (SSIM) {  // d loss / d S_p = go * beta * (-1/2) * [0 <= (1 - M)/2 <= 1] / |map|
+    const float f = (1.f - fwd[4]) * 0.5f;
+    kfac = (f >= 0.f && f <= 1.f) ? go * beta * -0.5f * inv_n : 0.f;
+  }
+  const float kl1 = go * alpha * inv_n, kg = go * gamma * inv_n;
+
+  float ring[11][3];
+#pragma unroll
+  for (int j = 0; j < 11; ++j)
+#pragma unroll
+    for (int z = 0; z < 3; ++z) ring[j][z] = 0.f;
+  // raw rows q (x0, y0) and q + 1 (x1, y1) of the next output q; ey_prev =
+  // forward row difference of row q - 1
+  float an = 0.f, bn = 0.f, cn = 0.f;
+  auto load_coef = [&](int p, float& a, float& b, float& cv) {
+    const int pc = p < 0 ? 0 : (p >= h ? h - 1 : p);
+    const bool ok = cin && p >= 0 && p < h;
+    const int64_t o = (int64_t)pc * w;
+    const float av = Ai[o], bv = Ai[plane + o], cvv = Ai[2 * plane + o];
+    a = ok ? av : 0.f;
+    b = ok ? bv : 0.f;
+    cv = ok ? cvv : 0.f;
+  };
+  auto load_raw = [&](int r, float& x, float& y) {
+    const int rc = r < 0 ? 0 : (r >= h ? h - 1 : r);
+    const bool ok = cin && r >= 0 && r < h;
+    const float xv = Xi[(int64_t)rc * w], yv = Yi[(int64_t)rc * w];
+    x = ok ? xv : 0.f;
+    y = ok ? yv : 0.f;
+  };
+  if (SSIM) load_coef(r0 - 5, an, bn, cn);
+  float x0, y0, x1, y1;
+  load_raw(r0, x0, y0);
+  load_raw(r0 + 1, x1, y1);
+  float eyp = 0.f;  // e_y of row r0 - 1 (only used when r0 >= 1)
+  if (GRAD && r0 >= 1) {
+    float xm, ym;
+    load_raw(r0 - 1, xm, ym);
+    eyp = (y0 - ym) - (x0 - xm);
+  }
+  for (int t0 = 0; t0 < T; t0 += 11) {
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const int t = t0 + j;
+      if (t < T) {
+      if (SSIM) {
+        const float v[3] = {an, bn, cn};
+        if (t + 1 < T) load_coef(r0 - 4 + t, an, bn, cn);
+        float hv[3];
+        hpass<3>(v, g, hv);
+#pragma unroll
+        for (int z = 0; z < 3; ++z) ring[j][z] = hv[z];
+      }
+      if (t >= 10) {  // image row q = p - 5
+        const int q = r0 + t - 10;
+        float gsum = kl1 * ((x0 > y0) ? 1.f : (x0 < y0 ? -1.f : 0.f));
+        if (SSIM) {
+          float f3[3];
+#pragma unroll
+          for (int z = 0; z < 3; ++z) {
+            float a = g.c * ring[(j + 6) % 11][z];
+#pragma unroll
+            for (int i = 0; i < 5; ++i)
+              a = fmaf(g.k[i], ring[(j + 5 - i) % 11][z] + ring[(j + 7 + i) % 11][z], a);
+            f3[z] = a;
+          }
+          gsum += kfac * (f3[0] + 2.f * x0 * f3[1] + y0 * f3[2]);
+        }
+        float x2 = 0.f, y2 = 0.f;
+        if (t + 1 < T) load_raw(q + 2, x2, y2);
+        if (GRAD) {
+          // e = gt_d - p_d (forward differences); dL/dp(j) = kg * (sgn e(j) - sgn e(j-1))
+          const float xr = lnext(x0), yr = lnext(y0);
+          const float ex = (yr - y0) - (xr - x0);
+          const float sx = (c < w - 1) ? ((ex > 0.f) ? 1.f : (ex < 0.f ? -1.f : 0.f)) : 0.f;
+          const float sxp = lprev(sx);  // sgn e_x(j - 1); 0 when j - 1 is the column -1
+          const float ey = (y1 - y0) - (x1 - x0);
+          const float sy = (q < h - 1) ? ((ey > 0.f) ? 1.f : (ey < 0.f ? -1.f : 0.f)) : 0.f;
+          const float syp = (q >= 1) ? ((eyp > 0.f) ? 1.f : (eyp < 0.f ? -1.f : 0.f)) : 0.f;
+          gsum += kg * ((sx - (c >= 1 ? sxp : 0.f)) + (sy - syp));
+          eyp = ey;
+        }
+        if (outl && q < r1) gx[img * (int64_t)h * w + (int64_t)q * w + c] = gsum;
+        x0 = x1;
+        y0 = y1;
+        x1 = x2;
+        y1 = y2;
+      }
+      }
+    }
+  }
+}
+
+// Masked mode (beta == gamma == 0): L1 over gt > 0 only; partial record per
+// block [0, sum |p - t| over t > 0, 0, count].
+__global__ void __launch_bounds__(256)
+    dloss_masked_kernel(const float* __restrict__ P, const float* __restrict__ Tg, int64_t n,
+                        float* __restrict__ part) {
+  __shared__ float red[4];
+  float s = 0.f, k = 0.f;
+  const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 p = reinterpret_cast<const float4*>(P)[i];
+    const float4 t = reinterpret_cast<const float4*>(Tg)[i];
+    s += (t.x > 0.f ? fabsf(p.x - t.x) : 0.f) + (t.y > 0.f ? fabsf(p.y - t.y) : 0.f) +
+         (t.z > 0.f ? fabsf(p.z - t.z) : 0.f) + (t.w > 0.f ? fabsf(p.w - t.w) : 0.f);
+    k += (float)((t.x > 0.f) + (t.y > 0.f) + (t.z > 0.f) + (t.w > 0.f));
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += stride) {
+    const float p = P[i], t = Tg[i];
+    if (t > 0.f) {
+      s += fabsf(p - t);
+      k += 1.f;
+    }
+  }
+  const float a = mde::block_sum256(s, red);
+  const float b = mde::block_sum256(k, red);
+  if (threadIdx.x == 0) {
+    float* o = part + 4 * (int64_t)blockIdx.x;
+    o[0] = 0.f;
+    o[1] = a;
+    o[2] = 0.f;
+    o[3] = b;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    dloss_masked_bwd_kernel(const float* __restrict__ P, const float* __restrict__ Tg,
+                            int64_t n, const float* __restrict__ fwd,
+                            const float* __restrict__ gout, float* __restrict__ gx) {
+  const float k = gout[0] / fwd[5];
+  const int64_t n4 = n >> 2, stride = (int64_t)gridDim.x * blockDim.x;
+  auto one = [&](float p, float t) {
+    return t > 0.f ? k * ((p > t) ? 1.f : (p < t ? -1.f : 0.f)) : 0.f;
+  };
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 p = reinterpret_cast<const float4*>(P)[i];
+    const float4 t = reinterpret_cast<const float4*>(Tg)[i];
+    reinterpret_cast<float4*>(gx)[i] =
+        make_float4(one(p.x, t.x), one(p.y, t.y), one(p.z, t.z), one(p.w, t.w));
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+       i += stride)
+    gx[i] = one(P[i], Tg[i]);
+}
+
+int masked_blocks(int64_t n) {
+  const int64_t b = mde::cdiv(n >> 2, 256 * 4);
+  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+
 struct Geo {
   int ho, wo, tiles_w, tiles_per_img;
   int64_t nblocks;
@@ -327,11 +706,28 @@ size_t round16(size_t v) { return (v + 15) & ~size_t(15); }
 
 extern "C" {
 
+// [partial records][3 coefficient planes]; the forward fills the planes
+// (full window), the backward reads them: pass the same workspace to both.
+static size_t partial_slots(int64_t b, int64_t h, int64_t w) {
+  const Win win = make_window(h, w);
+  const Geo g = geometry(b, h, w, win.k);
+  int64_t slots = g.nblocks;
+  if (win.k == KMAX) {
+    const int64_t sw = stream_geometry(b, h, w).nwaves;
+    if (sw > slots) slots = sw;
+  }
+  const int64_t mb = masked_blocks(b * h * w);
+  return (size_t)(mb > slots ? mb : slots);
+}
+
+static size_t coef_offset(int64_t b, int64_t h, int64_t w) {
+  return round16(sizeof(float) * 4 * partial_slots(b, h, w));
+}
+
 size_t mde_depth_loss_workspace(int64_t b, int64_t h, int64_t w) {
   const Win win = make_window(h, w);
   const Geo g = geometry(b, h, w, win.k);
-  return round16(sizeof(float) * 4 * (size_t)g.nblocks) +
-         sizeof(float) * 3 * (size_t)b * g.ho * g.wo;
+  return coef_offset(b, h, w) + sizeof(float) * 3 * (size_t)b * g.ho * g.wo;
 }
 
 int mde_depth_loss_fwd(const void* pred, const void* gt, float alpha,
@@ -351,13 +747,36 @@ int mde_depth_loss_fwd(const void* pred, const void* gt, float alpha,
   const float c2 = (0.03f * max_depth) * (0.03f * max_depth);
   float* part = (float*)workspace;
   const double numel = (double)b * h * w;
-  MDE_LAUNCH(mde::K_DLOSS_FWD, 8.0 * numel, s, dloss_map_kernel<0>,
-             dim3((unsigned)g.nblocks), dim3(256), 0, (const float*)pred,
-             (const float*)gt, (int)h, (int)w, g.ho, g.wo, g.tiles_w,
-             g.tiles_per_img, win, c1, c2, masked, part, (float*)nullptr,
-             (const float*)nullptr, (const float*)nullptr, beta);
-  MDE_LAUNCH(mde::K_LOSS_FINAL, 16.0 * g.nblocks, s, dloss_final_kernel,
-             dim3(1), dim3(256), 0, part, (int)g.nblocks,
+  int nparts = (int)g.nblocks;
+  if (masked) {
+    nparts = masked_blocks(b * h * w);
+    MDE_LAUNCH(mde::K_DLOSS_FWD, 8.0 * numel, s, dloss_masked_kernel, dim3(nparts), dim3(256),
+               0, (const float*)pred, (const float*)gt, b * h * w, part);
+  } else if (win.k == KMAX) {
+    const StreamGeo sg = stream_geometry(b, h, w);
+    nparts = (int)sg.nwaves;
+    float* coef = (float*)((char*)workspace + coef_offset(b, h, w));
+    const unsigned blocks = (unsigned)mde::cdiv(sg.nwaves, 4);
+    // bytes: pred + target read, 3 coefficient planes written (when beta != 0)
+    if (beta != 0.f)
+      MDE_LAUNCH(mde::K_DLOSS_FWD, 20.0 * numel, s, dloss_fwd_stream_kernel<true>, dim3(blocks),
+                 dim3(256), 0, (const float*)pred, (const float*)gt, (int)h, (int)w, sg.strips,
+                 sg.chunks, sg.chunk_rows, sg.nwaves, sym11(win), c1, c2, part, coef,
+                 b * h * w);
+    else
+      MDE_LAUNCH(mde::K_DLOSS_FWD, 8.0 * numel, s, dloss_fwd_stream_kernel<false>, dim3(blocks),
+                 dim3(256), 0, (const float*)pred, (const float*)gt, (int)h, (int)w, sg.strips,
+                 sg.chunks, sg.chunk_rows, sg.nwaves, sym11(win), c1, c2, part, (float*)nullptr,
+                 b * h * w);
+  } else {
+    MDE_LAUNCH(mde::K_DLOSS_FWD, 8.0 * numel, s, dloss_map_kernel<0>,
+               dim3((unsigned)g.nblocks), dim3(256), 0, (const float*)pred,
+               (const float*)gt, (int)h, (int)w, g.ho, g.wo, g.tiles_w,
+               g.tiles_per_img, win, c1, c2, masked, part, (float*)nullptr,
+               (const float*)nullptr, (const float*)nullptr, beta);
+  }
+  MDE_LAUNCH(mde::K_LOSS_FINAL, 16.0 * nparts, s, dloss_final_kernel,
+             dim3(1), dim3(256), 0, part, nparts,
              (float)(1.0 / numel), (float)(1.0 / ((double)b * g.ho * g.wo)),
              alpha, beta, gamma, masked, out);
   return MDE_OK;
@@ -380,10 +799,34 @@ int mde_depth_loss_bwd(const void* pred, const void* gt, float alpha,
   const int use_ssim = (!masked && beta != 0.f) ? 1 : 0;
   const float c1 = (0.01f * max_depth) * (0.01f * max_depth);
   const float c2 = (0.03f * max_depth) * (0.03f * max_depth);
-  float* coef = (float*)((char*)workspace +
-                         round16(sizeof(float) * 4 * (size_t)g.nblocks));
+  float* coef = (float*)((char*)workspace + coef_offset(b, h, w));
   const int64_t plane = b * (int64_t)g.ho * g.wo;
   const double numel = (double)b * h * w;
+  if (masked) {
+    MDE_LAUNCH(mde::K_DLOSS_BWD, 12.0 * numel, s, dloss_masked_bwd_kernel,
+               dim3(masked_blocks(b * h * w)), dim3(256), 0, (const float*)pred,
+               (const float*)gt, b * h * w, fwd_out, gout, (float*)grad_pred);
+    return MDE_OK;
+  }
+  if (win.k == KMAX) {  // coefficients left by the forward
+    const StreamGeo sg = stream_geometry(b, h, w);
+    const unsigned blocks = (unsigned)mde::cdiv(sg.nwaves, 4);
+    const float inv_n = (float)(1.0 / numel);
+    // bytes: pred + target read, gradient written, 3 coefficient planes read
+    const double by = 12.0 * numel + (use_ssim ? 12.0 * numel : 0.0);
+    auto kern = dloss_bwd_stream_kernel<false, false>;
+    if (use_ssim && gamma != 0.f)
+      kern = dloss_bwd_stream_kernel<true, true>;
+    else if (use_ssim)
+      kern = dloss_bwd_stream_kernel<true, false>;
+    else if (gamma != 0.f)
+      kern = dloss_bwd_stream_kernel<false, true>;
+    MDE_LAUNCH(mde::K_DLOSS_BWD, by, s, kern, dim3(blocks), dim3(256), 0, (const float*)pred,
+               (const float*)gt, (int)h, (int)w, sg.strips, sg.chunks, sg.chunk_rows, sg.nwaves,
+               sym11(win), (const float*)coef, b * h * w, fwd_out, gout, alpha, beta, gamma,
+               inv_n, (float*)grad_pred);
+    return MDE_OK;
+  }
   if (use_ssim) {
     MDE_LAUNCH(mde::K_DLOSS_BWD_COEF, 8.0 * numel + 12.0 * plane, s,
                dloss_map_kernel<1>, dim3((unsigned)g.nblocks), dim3(256), 0,

@@ -448,6 +448,7 @@ class _DepthLoss(torch.autograd.Function):
                   float(gamma), float(max_depth), _abi.ptr(out), n * c, h, w, _abi.ptr(ws),
                   _abi.dtype_code(pred), _abi.stream_of(pred))
         ctx.save_for_backward(pred, gt, out)
+        ctx.ws = ws  # holds the forward's SSIM gradient coefficients for the backward
         ctx.params = (float(alpha), float(beta), float(gamma), float(max_depth))
         ctx.mark_non_differentiable(out)
         return out[0].clone(), out
@@ -460,7 +461,7 @@ class _DepthLoss(torch.autograd.Function):
         n, c, h, w = pred.shape
         go = go.reshape(1).to(torch.float32).contiguous()
         gp = torch.empty_like(pred)
-        ws = _ws(_abi.query("mde_depth_loss_workspace", n * c, h, w), pred)
+        ws = ctx.ws
         _abi.call("mde_depth_loss_bwd", _abi.ptr(pred), _abi.ptr(gt), alpha, beta, gamma,
                   max_depth, _abi.ptr(out), _abi.ptr(go), _abi.ptr(gp), n * c, h, w,
                   _abi.ptr(ws), _abi.dtype_code(pred), _abi.stream_of(pred))

@@ -72,7 +72,7 @@ def test_resume_matches_oracle_continuation(tmp_path):
     for pos in range(6):
         image, depth = synthetic_batch(2, 64, 96, 0, pos, "cpu")
         loss = oops.train_loss(ref(image), depth)
-        every.append(float(loss))
+        every.append(float(loss.detach()))
         if pos in (0, 5):
             want.append(float(loss))
         opt.zero_grad()
@@ -93,33 +93,49 @@ def test_graph_resume_from_eager_checkpoint(tmp_path):
     """--graph --cp 1 from a checkpoint the eager trainer wrote (fused,
     non-capturable Adam state): GraphTrainer's Adam must stay capturable after
     load_state_dict (the capture happens on its third step) and the resumed
-    run continue exactly like the oracle from that checkpoint (train-mode BN
-    throughout: the graph path has no eval-mode quirk)."""
+    graph run must continue exactly like the resumed EAGER run without the
+    eval-mode quirk (the graph path keeps BN in train mode), under MIOpen's
+    deterministic solvers, to 1e-5.  Against the oracle: the first step (no
+    update yet) to 1e-4; later steps of this 64x96 train-mode net drift by up
+    to a few 1e-3 between devices (BN over 1x2 maps at the bottom of DDRNet,
+    amplified by Adam's normalised steps), so the epoch average is checked at
+    1e-2."""
     from monocular_depth_estimation_amd.train import main, synthetic_batch
-    ck = str(tmp_path / "global_checkpoint.pth")
-    main(ARGS + ["--epochs", "1", "--checkpoint", ck])
-    state = torch.load(ck, map_location="cpu", weights_only=True)
+    old = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        ck = str(tmp_path / "global_checkpoint.pth")
+        main(ARGS + ["--epochs", "1", "--checkpoint", ck])
+        state = torch.load(ck, map_location="cpu", weights_only=True)
+        ck2 = str(tmp_path / "copy.pth")
+        torch.save(state, ck2)  # the eager resume overwrites its checkpoint at epoch end
+        main(ARGS + ["--epochs", "1", "--cp", "1", "--no-eval-quirk", "--checkpoint", ck,
+                     "--log", str(tmp_path / "e.jsonl")])
+        main(ARGS + ["--epochs", "1", "--cp", "1", "--graph", "--checkpoint", ck2,
+                     "--log", str(tmp_path / "g.jsonl")])
+    finally:
+        torch.backends.cudnn.deterministic = old
+    eager = [r["value"] for r in _losses(tmp_path / "e.jsonl")]
+    graph = [r["value"] for r in _losses(tmp_path / "g.jsonl")]
+    assert graph == pytest.approx(eager, rel=1e-5), (graph, eager)
+    assert _avgs(tmp_path / "g.jsonl")[0]["value"] == pytest.approx(
+        _avgs(tmp_path / "e.jsonl")[0]["value"], rel=1e-5)
     ref = og.GuideDepth()
     ref.load_state_dict(state["model_state_dict"], strict=True)
     opt = torch.optim.Adam(ref.parameters(), 1e-4)
     opt.load_state_dict(state["optimizer_state_dict"])
-    main(ARGS + ["--epochs", "1", "--cp", "1", "--graph", "--checkpoint", ck,
-                 "--log", str(tmp_path / "g.jsonl")])
     ref.train()
-    want, every = [], []
+    every = []
     for pos in range(6):
         image, depth = synthetic_batch(2, 64, 96, 0, pos, "cpu")
         loss = oops.train_loss(ref(image), depth)
-        every.append(float(loss))
-        if pos in (0, 5):
-            want.append(float(loss))
+        every.append(float(loss.detach()))
         opt.zero_grad()
         loss.backward()
         opt.step()
-    got = [r["value"] for r in _losses(tmp_path / "g.jsonl")]
-    assert got == pytest.approx(want, rel=1e-3), (got, want)
+    assert graph[0] == pytest.approx(every[0], rel=1e-4), (graph, every)
     avg = _avgs(tmp_path / "g.jsonl")
-    assert avg[0]["value"] == pytest.approx(sum(every) / len(every), rel=1e-3), (avg, every)
+    assert avg[0]["value"] == pytest.approx(sum(every) / len(every), rel=1e-2), (avg, every)
 
 
 def test_pretrained_flag_loads_encoder_blob(tmp_path):

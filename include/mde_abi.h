@@ -440,29 +440,34 @@ int mde_pointwise_bwd_bn(const void* gy, const void* x, const float* in_scale,
  * guide_conv and comb_conv (`nn.Conv2d(in, E, kernel_size=3, padding=1)`,
  * src/GuideDepth/model/modules.py:43-74), bias folded into the following
  * BatchNorm.  x [n,cin,h,w], weight [cout,cin,3,3], y [n,cout,h,w].
- * mde_conv3x3_supported(cin, cout, pass): pass 0 forward, 1 data gradient,
- * 2 weight gradient.  Supported: forward (3,16) (3,32) (3,64) (16,16)
- * (32,32); data gradient (16,16) (32,32); weight gradient all five; others
- * return MDE_ERR_UNSUPPORTED.
+ * mde_conv3x3_supported(cin, cout, pass, dtype): pass 0 forward, 1 data
+ * gradient, 2 weight gradient.  MDE_F32 (v_mfma_f32_16x16x4_f32): forward
+ * (3,16) (3,32) (3,64) (16,16) (32,32); data gradient (16,16) (32,32);
+ * weight gradient all five.  MDE_BF16 (autocast, v_mfma_f32_16x16x32_bf16,
+ * fp32 accumulation; x / gy / y / gx bf16, the fp32 weight rounded to bf16
+ * on load, the weight gradient fp32; w % 4 == 0): (16,16) and (32,32), every
+ * pass.  Others return MDE_ERR_UNSUPPORTED.
  * bwd_data: gx [n,cin,h,w] = conv_transpose(gy, weight), overwritten.
  * wgrad: gweight [cout,cin,3,3] overwritten (deterministic block partials +
  * fixed-order reduction in mde_conv3x3_wgrad_workspace bytes).
  * ------------------------------------------------------------------------- */
-int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass);
+int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass, int dtype);
 int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
                     int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
 /* mde_conv3x3_fwd that also emits y's per-channel shifted sums per block,
  * the following BatchNorm's statistics (stats = DEVICE fp32
  * [cout][blocks][4] = (shift, count, s1, s2), blocks =
  * mde_conv3x3_stats_blocks(...)). */
-int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                             int dtype);
 int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* stats, int64_t n,
                           int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
                           void* stream);
 int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t n,
                          int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
                          void* stream);
-size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
+size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                   int dtype);
 int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
                       int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
                       void* stream);

@@ -93,7 +93,7 @@ SIGNATURES = {
     "mde_pointwise_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
     "mde_pointwise_fwd_stats": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64,
                                        _int, _vp]),
-    "mde_conv3x3_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_conv3x3_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64, _int]),
     "mde_conv3x3_fwd_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_batchnorm_fwd_train_stats": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _vp,
                                              _vp, _vp, _vp, _i64, _i64, _i64, _i64, _int, _vp,
@@ -105,10 +105,10 @@ SIGNATURES = {
                                     _i64, _i64, _vp, _int, _vp]),
     "mde_batchnorm_fwd_coef": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _f32, _f32, _int, _vp, _vp,
                                       _vp, _vp, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
-    "mde_conv3x3_supported": (_int, [_i64, _i64, _int]),
+    "mde_conv3x3_supported": (_int, [_i64, _i64, _int, _int]),
     "mde_conv3x3_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_conv3x3_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
-    "mde_conv3x3_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_conv3x3_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _int]),
     "mde_conv3x3_wgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_dwconv_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64, _i64]),
     "mde_dwconv_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp]),

@@ -310,9 +310,10 @@ __global__ void __launch_bounds__(256)
 // One 16-key tile of sum_i T[j][i] B[i][c]: o[ct] (C layout: key 16jt + 4g + rr,
 // c = 16ct + l16), B given per lane as b[it][r][ct] = B[16it + 4g + r][16ct + l16].
 template <int WS, int jt>
-__device__ __forceinline__ void mm_tb_tile(const float* T, const float b[4][4][2], f4 o[2]) {
+__device__ __forceinline__ void mm_tb_tile(const float* T, const float b[4][4][2], f4 o[2],
+                                           int lane) {
   using TL = Tile<WS>;
-  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int l16 = lane & 15, g4 = lane >> 4;
   o[0] = f4{0.f, 0.f, 0.f, 0.f};
   o[1] = f4{0.f, 0.f, 0.f, 0.f};
   const int rowoff = TL::template clamp<jt>(16 * jt + l16) * TL::kPitch;
@@ -334,18 +335,28 @@ __device__ __forceinline__ void mm_tb_tile(const float* T, const float b[4][4][2
 // T[j][i] of this lane's own entries (key 16jt + 4g + r, query 16it + l16):
 // 0 for padded keys / queries (never read from LDS, never written).
 template <int WS, int jt, int it>
-__device__ __forceinline__ float own_get(const float* T, int r) {
+__device__ __forceinline__ float own_get(const float* T, int r, int lane) {
   using TL = Tile<WS>;
-  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int l16 = lane & 15, g4 = lane >> 4;
   const int j = 16 * jt + 4 * g4 + r, i = 16 * it + l16;
   return T[TL::template clamp<jt>(j) * TL::kPitch + TL::template clamp<it>(i)];
 }
 template <int WS, int jt, int it>
-__device__ __forceinline__ void own_put(float* T, int r, float v) {
+__device__ __forceinline__ void own_put(float* T, int r, float v, int lane) {
   using TL = Tile<WS>;
-  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int l16 = lane & 15, g4 = lane >> 4;
   const int j = 16 * jt + 4 * g4 + r, i = 16 * it + l16;
   if (TL::template valid<jt>(j) && TL::template valid<it>(i)) T[j * TL::kPitch + i] = v;
+}
+
+// threadIdx-derived lane, opaque to the optimiser: each phase of the 7x7
+// backward recomputes its lane index math instead of the compiler hoisting
+// it out of the window loop and keeping ~60 registers of it live across all
+// phases (which spilled at the three-waves-per-SIMD budget).
+__device__ __forceinline__ int opaque_lane() {
+  int l = threadIdx.x & 63;
+  asm volatile("" : "+v"(l));
+  return l;
 }
 
 template <typename F>
@@ -365,8 +376,7 @@ __device__ __forceinline__ void probs_stage(const Geo& g, const float* __restric
                                             const float* __restrict__ qkb, int head,
                                             const int* tok, const int* lab, const float* tab,
                                             float* T) {
-  using TL = Tile<WS>;
-  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
+  const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
   const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
   const int c2 = 2 * g.c;
   float ka[4][8];
@@ -437,7 +447,7 @@ __device__ __forceinline__ void probs_stage(const Geo& g, const float* __restric
     static_for4([&](auto jt_c) {
       constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, s[jt][r] * inv);
+      for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, s[jt][r] * inv, lane);
     });
   });
 }
@@ -494,6 +504,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dV = P^T dO
       {
+        const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
         float b[4][4][2];
 #pragma unroll
         for (int it = 0; it < 4; ++it)
@@ -507,7 +518,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
         static_for4([&](auto jt_c) {
           constexpr int jt = decltype(jt_c)::value;
           f4 o[2];
-          mm_tb_tile<WS, jt>(T, b, o);
+          mm_tb_tile<WS, jt>(T, b, o, lane);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * jt + 4 * g4 + rr];
@@ -526,6 +537,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       // dP^T = V dO^T column by column; dS = P (dP - rowsum(P dP)), P read
       // back from T (this lane's own entries) and dS written over it
       {
+        const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
         float va[4][8];
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
@@ -547,7 +559,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
             constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              pv[jt][r] = own_get<WS, jt, it>(T, r);
+              pv[jt][r] = own_get<WS, jt, it>(T, r, lane);
               dl += pv[jt][r] * dp[jt][r];
             }
           });
@@ -556,13 +568,14 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
           static_for4([&](auto jt_c) {
             constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, pv[jt][r] * (dp[jt][r] - dl));
+            for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, pv[jt][r] * (dp[jt][r] - dl), lane);
           });
         });
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dQ = dS K * scale: A = dS[i][j] (this lane's own T entries), B = K[j][c] per lane
       {
+        const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
         float b[4][4][2];
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
@@ -580,7 +593,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
             constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float a = own_get<WS, jt, it>(T, r);  // dS[i][j]
+              const float a = own_get<WS, jt, it>(T, r, lane);  // dS[i][j]
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct) q[ct] = mfma4(a, b[jt][r][ct], q[ct]);
             }
@@ -599,6 +612,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dK = dS^T Q * scale (dS from the LDS tile)
       {
+        const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
         float b[4][4][2];
 #pragma unroll
         for (int it = 0; it < 4; ++it)
@@ -612,7 +626,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
         static_for4([&](auto jt_c) {
           constexpr int jt = decltype(jt_c)::value;
           f4 o[2];
-          mm_tb_tile<WS, jt>(T, b, o);
+          mm_tb_tile<WS, jt>(T, b, o, lane);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * jt + 4 * g4 + rr];

@@ -553,6 +553,437 @@ __global__ void __launch_bounds__(256)
 
 constexpr int kReduceSplit = 32;
 
+// ====================================================================== bf16
+// bf16 activations / gradients on v_mfma_f32_16x16x32_bf16 (bf16 products,
+// fp32 accumulation), for the autocast step (BASELINE cfg3): the same three
+// passes as above at 16 -> 16 and 32 -> 32, without MIOpen's NCHW <-> NHWC
+// transposes.  Weights stay fp32 in memory (autocast's master weights) and
+// are rounded to bf16 (RNE, as autocast's cast) when a block loads them; the
+// weight gradient is fp32.
+//
+// Staging (both kernels): the input tile (rows r0-1 .. r0+TH, the 64 tile
+// columns) is stored as THREE column-shifted copies, copy d holding global
+// columns c0 - 1 + d + t, t = 0..63, so every operand read of tap column d
+// starts at an 8-/16-byte-aligned LDS address (an unaligned ds_read returns
+// stale data or replays).  A lane loads one aligned 4-column chunk (8 B) of a
+// tile row from HBM, takes its neighbours' chunks by DPP lane shifts and
+// writes its 4 columns of each copy (3 ds_write_b64).  Plane (channel) pitch
+// = 16 (mod 128) elements: conflict-free ds_read_b128 (weight gradient);
+// the forward adds 64 elements between the two 8-channel halves, which makes
+// its transposed reads (ds_read_b64_tr_b16) conflict-free.
+//
+// Forward / data gradient: M = 16 output pixels, N = 16 output channels,
+// K = (tap, input channel) in steps of 32: one tap x 32 channels (CI = 32) or
+// two taps x 16 channels (CI = 16; the tenth tap has zero weights).  The A
+// operand (8 channels of one pixel per lane) comes from the channel-planar
+// copies by two ds_read_b64_tr_b16 (4 channels x 16 pixels each); the B
+// operand (weights) lives in registers.  Weight gradient: M = output
+// channels, N = (tap, input channel), K = 32 pixels of a tile row; A = gy
+// rows and B = x rows, 16 bytes per lane by ds_read_b128.
+using mde::bf16;
+using bf8v = __bf16 __attribute__((ext_vector_type(8)));
+using f4v = float __attribute__((ext_vector_type(4)));
+using s4v = short __attribute__((ext_vector_type(4)));
+using u2v = uint32_t __attribute__((ext_vector_type(2)));
+using u4v = uint32_t __attribute__((ext_vector_type(4)));
+using lds_s4 = __attribute__((address_space(3))) s4v;
+
+__device__ __forceinline__ f4v mfma_bf(u4v a, u4v b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8v, a),
+                                                 __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+
+__device__ __forceinline__ uint32_t dpp_prev(uint32_t v) {  // lane - 1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x138, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t dpp_next(uint32_t v) {  // lane + 1
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x130, 0xf, 0xf, true);
+}
+
+// Element layout of the shifted-copy tile: copy d, channel c, tile row r, col t.
+template <int C, int XR, int GO>
+struct CopyTile {
+  static constexpr int PL = (XR * 64 + 127) / 128 * 128 + 16;   // plane pitch (elements)
+  static constexpr int HALF = 8 * PL + GO;                       // 8-channel half pitch
+  static constexpr int COPY = ((C + 7) / 8 * HALF + 127) / 128 * 128;
+  static constexpr int ELEMS = 3 * COPY;
+  __device__ static __forceinline__ int at(int d, int c, int r, int t) {
+    return d * COPY + (c >> 3) * HALF + (c & 7) * PL + r * 64 + t;
+  }
+};
+
+// Register stage of one tile: rows (channel, tile row) of 18 aligned 4-column
+// chunks (global columns c0 - 4 + 4i, i = 0..17); three rows per wave
+// instruction (lanes 0..53), the rows split over the block's 4 waves.
+template <int C, int XR>
+struct ChunkStage {
+  static constexpr int ROWS = C * XR;
+  static constexpr int PER = (ROWS + 11) / 12;  // 12 rows per block instruction
+  u2v v[PER];
+  __device__ __forceinline__ void load(const bf16* __restrict__ img, int h, int w, int r0,
+                                       int c0, int lane, int wvu) {
+    const int sub = lane / 18, i = lane - 18 * sub;  // row within the trio, chunk
+    const int gc = c0 - 4 + 4 * i;
+    const bool cok = lane < 54 && gc >= 0 && gc + 3 < w;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int row = 12 * k + 3 * wvu + sub;  // (channel, tile row) index
+      const int c = row / XR, r = row - c * XR, gr = r0 - 1 + r;
+      const bool ok = cok && row < ROWS && gr >= 0 && gr < h;
+      const u2v t = *reinterpret_cast<const u2v*>(
+          img + (ok ? (unsigned)((c * h + gr) * w + gc) : 0u));
+      v[k] = ok ? t : u2v{0u, 0u};
+    }
+  }
+  // copy d, tile columns 4j .. 4j+3 (j = i - 1) = global c0 - 1 + d + 4j .. :
+  // d = 1 is chunk i itself; d = 0 the last element of chunk i - 1 and the
+  // first three of chunk i; d = 2 the last three of chunk i and the first of
+  // chunk i + 1 (neighbours by DPP lane shifts; all lanes execute them).
+  template <int GO>
+  __device__ __forceinline__ void store(bf16* sx, int lane, int wvu) const {
+    using L = CopyTile<C, (ROWS / C), GO>;
+    const int sub = lane / 18, i = lane - 18 * sub, j = i - 1;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const uint32_t p1 = dpp_prev(v[k].y), n0 = dpp_next(v[k].x);
+      const int row = 12 * k + 3 * wvu + sub;
+      if (lane < 54 && j >= 0 && j < 16 && row < ROWS) {
+        const int c = row / XR, r = row - c * XR;
+        const u2v d1 = v[k];
+        const u2v d0 = u2v{__builtin_amdgcn_alignbit(v[k].x, p1, 16),
+                           __builtin_amdgcn_alignbit(v[k].y, v[k].x, 16)};
+        const u2v d2 = u2v{__builtin_amdgcn_alignbit(v[k].y, v[k].x, 16),
+                           __builtin_amdgcn_alignbit(n0, v[k].y, 16)};
+        *reinterpret_cast<u2v*>(sx + L::at(0, c, r, 4 * j)) = d0;
+        *reinterpret_cast<u2v*>(sx + L::at(1, c, r, 4 * j)) = d1;
+        *reinterpret_cast<u2v*>(sx + L::at(2, c, r, 4 * j)) = d2;
+      }
+    }
+  }
+};
+
+// fp32 weight -> bf16 (RNE) pair packed in a dword
+__device__ __forceinline__ uint32_t pack_bf(float a, float b) {
+  return (uint32_t)mde::f2bf(a) | ((uint32_t)mde::f2bf(b) << 16);
+}
+
+template <int CI, int CO, int RPW, bool FLIP, bool STATS>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3_bf_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ wt,
+                          bf16* __restrict__ y, int h, int w, int tiles_w, int tiles_per_img,
+                          int ntiles, float* __restrict__ stats) {
+  static_assert(CI == 16 || CI == 32, "bf16 forward: 16 or 32 input channels");
+  static_assert(CO % 16 == 0, "output channels in 16-blocks");
+  constexpr int TH = 4 * RPW, XR = TH + 2;
+  constexpr int NB = CO / 16;
+  constexpr int NS = CI == 16 ? 5 : 9;  // K steps of 32
+  using L = CopyTile<CI, XR, 64>;
+  __shared__ __attribute__((aligned(16))) bf16 sx[L::ELEMS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int li = lane & 15, g = lane >> 4;
+  const int64_t img_in = (int64_t)CI * h * w, img_out = (int64_t)CO * h * w;
+
+  // B operands: lane (co = 16 nb + li, g) holds the 8 K values of step s:
+  // K = 32 s + 8 g + j <-> (tap, channel) as the A reads below
+  u4v wb[NS][NB];
+#pragma unroll
+  for (int st = 0; st < NS; ++st)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co = 16 * nb + li;
+      const int tap = CI == 32 ? st : 2 * st + (g >> 1);
+      const int c8 = CI == 32 ? 8 * g : 8 * (g & 1);
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ci = c8 + j;
+        const int src = FLIP ? (ci * CO + co) * 9 + (8 - tap) : (co * CI + ci) * 9 + tap;
+        const float t = wt[tap < 9 ? src : 0];
+        f[j] = tap < 9 ? t : 0.f;
+      }
+      wb[st][nb] = u4v{pack_bf(f[0], f[1]), pack_bf(f[2], f[3]), pack_bf(f[4], f[5]),
+                       pack_bf(f[6], f[7])};
+    }
+  // A read addresses: lane 4q+p of group g supplies (channel c8g + q (+4),
+  // tile row (row + dy), pixels 16m + 4p) of copy dx; per step s a constant
+  // offset from the lane base.
+  const int q = li >> 2, p = li & 3;
+  int aoff[NS];
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int tap = CI == 32 ? st : (2 * st + (g >> 1) < 9 ? 2 * st + (g >> 1) : 8);
+    const int c8 = CI == 32 ? 8 * g : 8 * (g & 1);
+    aoff[st] = L::at(tap % 3, c8 + q, tap / 3, 4 * p);
+  }
+
+  mde::Sh run[STATS ? NB : 1];
+#pragma unroll
+  for (int nb = 0; nb < (STATS ? NB : 1); ++nb) run[nb] = {0.f, 0.f, 0.f, 0.f};
+  bool first = true;
+  ChunkStage<CI, XR> S;
+  const TileWalk tw = tile_walk(ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) {
+    const TileGeo gg = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    S.load(x + gg.img * img_in, h, w, gg.r0, gg.c0, lane, wvu);
+  }
+  for (; tile < tw.end; tile += tw.step) {
+    const TileGeo gg = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    __syncthreads();
+    S.template store<64>(sx, lane, wvu);
+    __syncthreads();
+    const int nxt = tile + tw.step;
+    if (nxt < tw.end) {
+      const TileGeo gn = tile_geo(nxt, TH, tiles_w, tiles_per_img);
+      S.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
+    }
+    f4v acc[RPW][4][NB];
+#pragma unroll
+    for (int qq = 0; qq < RPW; ++qq)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[qq][m][nb] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < RPW; ++qq) {
+      const int row = wv * RPW + qq;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+          const bf16* base = sx + aoff[st] + row * 64 + 16 * m;
+          const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base);
+          const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + 4 * L::PL));
+          const u2v l2 = __builtin_bit_cast(u2v, lo), h2 = __builtin_bit_cast(u2v, hi);
+          const u4v a = u4v{l2.x, l2.y, h2.x, h2.y};
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) acc[qq][m][nb] = mfma_bf(a, wb[st][nb], acc[qq][m][nb]);
+        }
+      }
+    }
+    // D: lane holds pixels 16m + 4g + r (r = 0..3) of output channel 16nb + li
+    bf16* yi = y + gg.img * img_out;
+#pragma unroll
+    for (int qq = 0; qq < RPW; ++qq) {
+      const int row = gg.r0 + wv * RPW + qq;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        const int col = gg.c0 + 16 * m + 4 * g;
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) {
+          const f4v v = acc[qq][m][nb];
+          const uint16_t b0 = mde::f2bf(v[0]), b1 = mde::f2bf(v[1]), b2 = mde::f2bf(v[2]),
+                         b3 = mde::f2bf(v[3]);
+          if constexpr (STATS) {
+            if (first && qq == 0 && m == 0) {  // one shift per channel and wave
+              const bool ok0 = gg.r0 + wv * RPW < h && gg.c0 < w;
+              run[nb].ref = __shfl(ok0 ? mde::bf2f(b0) : 0.f, li, 64);
+            }
+            const bool rok = row < h;
+            mde::sh_add(run[nb], mde::bf2f(b0), rok && col < w);
+            mde::sh_add(run[nb], mde::bf2f(b1), rok && col + 1 < w);
+            mde::sh_add(run[nb], mde::bf2f(b2), rok && col + 2 < w);
+            mde::sh_add(run[nb], mde::bf2f(b3), rok && col + 3 < w);
+          }
+          if (row < h) {
+            bf16* dst = yi + ((int64_t)(16 * nb + li) * h + row) * w + col;
+            if (col + 3 < w) {
+              *reinterpret_cast<u2v*>(dst) =
+                  u2v{(uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16)};
+            } else {
+              if (col < w) dst[0] = b0;
+              if (col + 1 < w) dst[1] = b1;
+              if (col + 2 < w) dst[2] = b2;
+            }
+          }
+        }
+      }
+    }
+    first = false;
+  }
+  if constexpr (STATS) {  // as the fp32 kernel: lk-butterfly, then the 4 waves in order
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(sx);  // [4][CO][4]
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const mde::Sh a = mde::sh_xor_sum(mde::sh_xor_sum(run[nb], 16), 32);
+      if (g == 0) {
+        float* p4 = part + (wv * CO + 16 * nb + li) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
+    }
+    __syncthreads();
+    if (tid < CO) {
+      mde::Sh a{part[tid * 4], part[tid * 4 + 1], part[tid * 4 + 2], part[tid * 4 + 3]};
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float* p4 = part + (k * CO + tid) * 4;
+        a = mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      float* o4 = stats + ((int64_t)tid * gridDim.x + blockIdx.x) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
+    }
+  }
+}
+
+// gy tile: CO planes of TH rows x 64 columns (plane pitch 16 mod 128), four
+// rows per wave instruction (16 lanes x 8 B per row).
+template <int CO, int TH>
+struct GyStage {
+  static constexpr int PL = (TH * 64 + 127) / 128 * 128 + 16;
+  static constexpr int ROWS = CO * TH;
+  static constexpr int PER = (ROWS + 15) / 16;
+  u2v v[PER];
+  __device__ __forceinline__ void load(const bf16* __restrict__ img, int h, int w, int r0,
+                                       int c0, int lane, int wvu) {
+    const int sub = lane >> 4, i = lane & 15;
+    const int gc = c0 + 4 * i;
+    const bool cok = gc + 3 < w;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int row = 16 * k + 4 * wvu + sub;
+      const int c = row / TH, gr = r0 + row % TH;
+      const bool ok = cok && row < ROWS && gr < h;
+      const u2v t = *reinterpret_cast<const u2v*>(
+          img + (ok ? (unsigned)((c * h + gr) * w + gc) : 0u));
+      v[k] = ok ? t : u2v{0u, 0u};
+    }
+  }
+  __device__ __forceinline__ void store(bf16* sg, int lane, int wvu) const {
+    const int sub = lane >> 4, i = lane & 15;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int row = 16 * k + 4 * wvu + sub;
+      if (row < ROWS)
+        *reinterpret_cast<u2v*>(sg + (row / TH) * PL + (row % TH) * 64 + 4 * i) = v[k];
+    }
+  }
+};
+
+// PW waves split a tile's K steps, 4 / PW wave groups split the N blocks.
+template <int CI, int CO, int TH, int PW>
+struct BfWgradCfg {
+  static constexpr int XR = TH + 2;
+  using LX = CopyTile<CI, XR, 0>;
+  using GS = GyStage<CO, TH>;
+  static constexpr int MB = CO / 16;
+  static constexpr int NP = 9 * CI;  // n = tap * CI + ci
+  static constexpr int NBLK = NP / 16;
+  static constexpr int TWAYS = 4 / PW;
+  static constexpr int NBW = (NBLK + TWAYS - 1) / TWAYS;
+  static constexpr int KS = 2 * TH;  // 32-pixel K steps per tile
+  static constexpr int SG = (LX::ELEMS + 127) / 128 * 128;
+  static constexpr int SMEM_BF = SG + CO * GS::PL;     // bf16 elements
+  static constexpr int RED = PW * MB * NBLK * 256;     // fp32 block reduction
+  static constexpr int SMEM_F = (SMEM_BF / 2 > RED ? SMEM_BF / 2 : RED);
+  static constexpr int M = CO * NP;
+};
+
+template <int CI, int CO, int TH, int PW>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3_bf_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
+                            float* __restrict__ part, int h, int w, int tiles_w,
+                            int tiles_per_img, int ntiles) {
+  using C = BfWgradCfg<CI, CO, TH, PW>;
+  static_assert(CI % 16 == 0 && CO % 16 == 0, "16-channel blocks");
+  __shared__ __attribute__((aligned(16))) float smem[C::SMEM_F];
+  bf16* sx = reinterpret_cast<bf16*>(smem);
+  bf16* sg = sx + C::SG;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int li = lane & 15, g = lane >> 4;
+  const int64_t img_in = (int64_t)CI * h * w, img_out = (int64_t)CO * h * w;
+
+  const int pg = wvu % PW, tg = wvu / PW;  // K group, N group of this wave
+  int boff[C::NBW];  // B (x) read base of each of the wave's N blocks
+#pragma unroll
+  for (int j = 0; j < C::NBW; ++j) {
+    const int nb = tg + C::TWAYS * j;
+    const int n = 16 * (nb < C::NBLK ? nb : 0) + li, tap = n / CI, ci = n % CI;
+    boff[j] = C::LX::at(tap % 3, ci, tap / 3, 8 * g);
+  }
+  const int aoff = li * C::GS::PL + 8 * g;
+
+  f4v acc[C::MB][C::NBW];
+#pragma unroll
+  for (int mb = 0; mb < C::MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < C::NBW; ++j) acc[mb][j] = f4v{0.f, 0.f, 0.f, 0.f};
+
+  ChunkStage<CI, C::XR> S;
+  typename C::GS G;
+  const TileWalk tw = tile_walk(ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) {
+    const TileGeo gg = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    G.load(gy + gg.img * img_out, h, w, gg.r0, gg.c0, lane, wvu);
+    S.load(x + gg.img * img_in, h, w, gg.r0, gg.c0, lane, wvu);
+  }
+  for (; tile < tw.end; tile += tw.step) {
+    __syncthreads();
+    S.template store<0>(sx, lane, wvu);
+    G.store(sg, lane, wvu);
+    __syncthreads();
+    const int nxt = tile + tw.step;
+    if (nxt < tw.end) {
+      const TileGeo gn = tile_geo(nxt, TH, tiles_w, tiles_per_img);
+      G.load(gy + gn.img * img_out, h, w, gn.r0, gn.c0, lane, wvu);
+      S.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
+    }
+    // K steps kk = pg, pg + PW, ...: tile row kk / 2, columns 32 (kk & 1) + 8 g ..
+#pragma unroll
+    for (int kk = pg; kk < C::KS; kk += PW) {
+      const int r = kk >> 1, c32 = 32 * (kk & 1);
+      u4v a[C::MB];
+#pragma unroll
+      for (int mb = 0; mb < C::MB; ++mb)
+        a[mb] = *reinterpret_cast<const u4v*>(sg + aoff + mb * 16 * C::GS::PL + r * 64 + c32);
+#pragma unroll
+      for (int j = 0; j < C::NBW; ++j) {
+        if (tg + C::TWAYS * j < C::NBLK) {  // wave-uniform
+          const u4v b = *reinterpret_cast<const u4v*>(sx + boff[j] + r * 64 + c32);
+#pragma unroll
+          for (int mb = 0; mb < C::MB; ++mb) acc[mb][j] = mfma_bf(a[mb], b, acc[mb][j]);
+        }
+      }
+    }
+  }
+  // the PW K-group partials summed through LDS in group order, one block
+  // partial: lane holds co = 16 mb + 4 g + i, n = 16 nb + li
+  __syncthreads();
+#pragma unroll
+  for (int mb = 0; mb < C::MB; ++mb)
+#pragma unroll
+    for (int j = 0; j < C::NBW; ++j) {
+      const int nb = tg + C::TWAYS * j;
+      if (nb < C::NBLK) {
+        float* d = smem + ((pg * C::MB + mb) * C::NBLK + nb) * 256 + li;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) d[(4 * g + i) * 16] = acc[mb][j][i];
+      }
+    }
+  __syncthreads();
+  float* out = part + (int64_t)blockIdx.x * C::M;
+  for (int e = tid; e < C::M; e += 256) {
+    const int co = e / C::NP, n = e % C::NP;
+    const int mb = co / 16, nb = n / 16;
+    const int o = ((mb * C::NBLK + nb) * 256) + (co % 16) * 16 + n % 16;
+    float sacc = 0.f;
+#pragma unroll
+    for (int k = 0; k < PW; ++k) sacc += smem[k * C::MB * C::NBLK * 256 + o];
+    out[e] = sacc;
+  }
+}
+
 // ---------------------------------------------------------------- dispatch
 enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
@@ -652,6 +1083,75 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
   return MDE_OK;
 }
 
+// ---- bf16 dispatch
+template <int CI, int CO, int RPW, bool FLIP, bool STATS>
+int bf_fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_img, int* ntiles) {
+  constexpr int TH = 4 * RPW;
+  *tiles_w = (int)mde::cdiv(w, kTW);
+  *tiles_per_img = (int)(mde::cdiv(h, TH) * *tiles_w);
+  const int64_t nt = n * *tiles_per_img;
+  if (nt > 0x7fffffff) return 0;
+  *ntiles = (int)nt;
+  const int res = resident_blocks<conv3x3_bf_fwd_kernel<CI, CO, RPW, FLIP, STATS>>();
+  return nt < res ? (int)nt : res;
+}
+
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
+int launch_bf_fwd(const bf16* in, const float* wt, bf16* out, int64_t n, int64_t h, int64_t w,
+                  double bytes, int kid, hipStream_t s, float* stats = nullptr) {
+  const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
+  int tiles_w, tiles_per_img, ntiles;
+  const int grid =
+      bf_fwd_grid<CI, CO, RPW, FLIP, STATS>(n, h, w, &tiles_w, &tiles_per_img, &ntiles);
+  if (grid <= 0) return MDE_ERR_INVALID_ARG;
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_bf_fwd_kernel<CI, CO, RPW, FLIP, STATS>),
+                  dim3(grid), dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img,
+                  ntiles, stats);
+  return MDE_OK;
+}
+
+template <int CI, int CO, int TH, int PW>
+WgradPlan bf_wgrad_plan(int64_t n, int64_t h, int64_t w) {
+  using C = BfWgradCfg<CI, CO, TH, PW>;
+  WgradPlan p;
+  p.th = TH;
+  p.tiles_w = (int)mde::cdiv(w, kTW);
+  p.tiles_per_img = (int)(mde::cdiv(h, TH) * p.tiles_w);
+  const int64_t nt = n * p.tiles_per_img;
+  p.ntiles = nt > 0x7fffffff ? 0x7fffffff : (int)nt;
+  const int res = resident_blocks<conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>>();
+  p.grid = p.ntiles < res ? p.ntiles : res;
+  p.m = C::M;
+  p.np = C::NP;
+  p.cip = CI;
+  return p;
+}
+
+template <int CI, int CO, int TH, int PW>
+int launch_bf_wgrad(const bf16* x, const bf16* gy, float* gw, int64_t n, int64_t h, int64_t w,
+                    float* ws, double bytes, hipStream_t s) {
+  const WgradPlan p = bf_wgrad_plan<CI, CO, TH, PW>(n, h, w);
+  if (p.grid <= 0) return MDE_ERR_INVALID_ARG;
+  const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
+  float* part = ws;
+  float* part2 = ws + (int64_t)p.grid * p.m;
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
+                  dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
+                  p.tiles_per_img, p.ntiles);
+  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
+             dim3((unsigned)mde::cdiv(p.m, 256), split), dim3(256), 0, part, part2, p.grid, p.m);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * split * p.m, s, wgrad_reduce2_kernel,
+             dim3((unsigned)mde::cdiv(p.m, 256)), dim3(256), 0, part2, gw, split, CO, CI, p.cip,
+             p.np);
+  return MDE_OK;
+}
+
+// bf16 shapes: 16 -> 16 and 32 -> 32, every pass; 4-column chunks need w % 4 == 0
+bool bf_supported(int64_t cin, int64_t cout) {
+  return (cin == 16 && cout == 16) || (cin == 32 && cout == 32);
+}
+
 // Supported (cin, cout) per pass.  Forward: the guide convs (3 -> 16/32/64),
 // 16 -> 16 and 32 -> 32; data gradient: 16 -> 16 and 32 -> 32 (the guide
 // convs read the image, which needs no gradient); weight gradient: all.
@@ -691,12 +1191,25 @@ bool dims_ok(int64_t n, int64_t h, int64_t w) {
 
 extern "C" {
 
-int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass) {
+int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass, int dtype) {
+  if (dtype == MDE_BF16) return bf_supported(cin, cout) && pass >= 0 && pass <= 2 ? 1 : 0;
+  if (dtype != MDE_F32) return 0;
   return supported(cin, cout, pass) ? 1 : 0;
 }
 
 int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
                     int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype == MDE_BF16) {
+    if (!x || !weight || !y || !dims_ok(n, h, w) || w % 4) return MDE_ERR_INVALID_ARG;
+    if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const double bytes = 2.0 * n * h * w * (double)(cin + cout);
+    if (cin == 16)
+      return launch_bf_fwd<16, 16, 1, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes,
+                                             mde::K_C3_FWD, s);
+    return launch_bf_fwd<32, 32, 1, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes,
+                                           mde::K_C3_FWD, s);
+  }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
   if (!supported(cin, cout, kFwd)) return MDE_ERR_UNSUPPORTED;
@@ -715,9 +1228,15 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
 
 // Forward with the BatchNorm statistics epilogue: stats [cout][blocks][4]
 // (shift, count, s1, s2), blocks = mde_conv3x3_stats_blocks(...).
-int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
-  if (!supported(cin, cout, kFwd) || !dims_ok(n, h, w)) return 0;
+int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                             int dtype) {
   int a, b, c;
+  if (dtype == MDE_BF16) {
+    if (!bf_supported(cin, cout) || !dims_ok(n, h, w)) return 0;
+    if (cin == 16) return bf_fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
+    return bf_fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
+  }
+  if (!supported(cin, cout, kFwd) || !dims_ok(n, h, w)) return 0;
   if (cin == 3 && cout == 16) return fwd_grid<3, 16, 2, false, true>(n, h, w, &a, &b, &c);
   if (cin == 3 && cout == 32) return fwd_grid<3, 32, 1, false, true>(n, h, w, &a, &b, &c);
   if (cin == 3 && cout == 64) return fwd_grid<3, 64, 1, false, true>(n, h, w, &a, &b, &c);
@@ -728,6 +1247,17 @@ int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, in
 int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* stats, int64_t n,
                           int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
                           void* stream) {
+  if (dtype == MDE_BF16) {
+    if (!x || !weight || !y || !stats || !dims_ok(n, h, w) || w % 4) return MDE_ERR_INVALID_ARG;
+    if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const double bytes = 2.0 * n * h * w * (double)(cin + cout);
+    if (cin == 16)
+      return launch_bf_fwd<16, 16, 1, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w,
+                                                   bytes, mde::K_C3_FWD, s, stats);
+    return launch_bf_fwd<32, 32, 1, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w,
+                                                 bytes, mde::K_C3_FWD, s, stats);
+  }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y || !stats || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
   if (!supported(cin, cout, kFwd)) return MDE_ERR_UNSUPPORTED;
@@ -749,6 +1279,17 @@ int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* st
 
 int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,
                          int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype == MDE_BF16) {
+    if (!gy || !weight || !gx || !dims_ok(n, h, w) || w % 4) return MDE_ERR_INVALID_ARG;
+    if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const double bytes = 2.0 * n * h * w * (double)(cin + cout);
+    if (cin == 16)
+      return launch_bf_fwd<16, 16, 1, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,
+                                            mde::K_C3_DGRAD, s);
+    return launch_bf_fwd<32, 32, 1, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,
+                                          mde::K_C3_DGRAD, s);
+  }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !weight || !gx || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
   if (!supported(cin, cout, kDgrad)) return MDE_ERR_UNSUPPORTED;
@@ -762,9 +1303,16 @@ int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
   return launch_fwd<32, 32, 1, true>(in, weight, out, n, h, w, bytes, k, s);
 }
 
-size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
-  if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
+size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                   int dtype) {
   WgradPlan p;
+  if (dtype == MDE_BF16) {
+    if (!bf_supported(cin, cout) || !dims_ok(n, h, w)) return 0;
+    p = cin == 16 ? bf_wgrad_plan<16, 16, 4, 4>(n, h, w) : bf_wgrad_plan<32, 32, 2, 2>(n, h, w);
+    const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
+    return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
+  }
+  if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
   if (cin == 3 && cout == 16) p = wgrad_plan<3, 16, 8, 4>(n, h, w);
   else if (cin == 3 && cout == 32) p = wgrad_plan<3, 32, 8, 4>(n, h, w);
   else if (cin == 3) p = wgrad_plan<3, 64, 4, 4>(n, h, w);
@@ -781,6 +1329,18 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
 int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
                       int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
                       void* stream) {
+  if (dtype == MDE_BF16) {
+    if (!gy || !x || !gweight || !workspace || !dims_ok(n, h, w) || w % 4)
+      return MDE_ERR_INVALID_ARG;
+    if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
+    hipStream_t s = (hipStream_t)stream;
+    const double bytes = 2.0 * n * h * w * (double)(cin + cout);
+    if (cin == 16)
+      return launch_bf_wgrad<16, 16, 4, 4>((const bf16*)x, (const bf16*)gy, gweight, n, h, w,
+                                           (float*)workspace, bytes, s);
+    return launch_bf_wgrad<32, 32, 2, 2>((const bf16*)x, (const bf16*)gy, gweight, n, h, w,
+                                         (float*)workspace, bytes, s);
+  }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !x || !gweight || !workspace || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
   if (!supported(cin, cout, kWgrad)) return MDE_ERR_UNSUPPORTED;

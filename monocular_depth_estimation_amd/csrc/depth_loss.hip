@@ -321,12 +321,13 @@ __global__ void __launch_bounds__(256)
 // ------------------------------------------------------------ streaming
 constexpr int kSD = 54;  // output columns per strip: 64 lanes - 2 x 5 halo
 
-// value of lane - 1 / lane + 1 (DPP wave shift by one lane; 0 shifted in)
+// value of lane - 1 / lane + 1 (DPP wave shift by one lane; bound_ctrl: the
+// lane with no source reads 0, so no zero-initialised destination is needed)
 __device__ __forceinline__ float lprev(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float lnext(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 // symmetric 11-tap window: c = g[5], k[i] = g[5 - 1 - i] = g[5 + 1 + i]
@@ -340,6 +341,14 @@ Sym11 sym11(const Win& w) {
   for (int i = 0; i < 5; ++i) s.k[i] = w.g[4 - i];
   return s;
 }
+
+// Packed pairs: v_pk_{add,mul,fma}_f32 process two fp32 lanes of a VGPR pair
+// per instruction, so the (x, y) and (mu_x, mu_y) / (E x^2, E y^2) filter
+// chains run as pairs at twice the scalar VALU rate.
+using v2 = float __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ v2 lprev2(v2 v) { return v2{lprev(v.x), lprev(v.y)}; }
+__device__ __forceinline__ v2 lnext2(v2 v) { return v2{lnext(v.x), lnext(v.y)}; }
 
 struct StreamGeo {
   int strips, chunks, chunk_rows;
@@ -361,28 +370,6 @@ StreamGeo stream_geometry(int64_t b, int64_t h, int64_t w) {
   return g;
 }
 
-// Horizontal pass of one row for NZ fields held one per lane: out[z] =
-// sum_k g_k v_z(col + k - 5), zero outside the loaded columns.
-template <int NZ>
-__device__ __forceinline__ void hpass(const float (&v)[NZ], const Sym11& g, float (&out)[NZ]) {
-  float l[NZ], r[NZ];
-#pragma unroll
-  for (int z = 0; z < NZ; ++z) {
-    l[z] = v[z];
-    r[z] = v[z];
-    out[z] = g.c * v[z];
-  }
-#pragma unroll
-  for (int i = 0; i < 5; ++i) {
-#pragma unroll
-    for (int z = 0; z < NZ; ++z) {
-      l[z] = lprev(l[z]);
-      r[z] = lnext(r[z]);
-      out[z] = fmaf(g.k[i], l[z] + r[z], out[z]);
-    }
-  }
-}
-
 // Forward.  Lane l of a wave <-> column c = strip * 54 - 5 + l; output lanes
 // 5..58.  Input rows r0 - 5 .. r1 + 4 of the chunk stream through; after
 // row r the map row p = r - 5 is complete (ring slots hold rows p-5..p+5).
@@ -393,7 +380,9 @@ __global__ void __launch_bounds__(256)
                             Sym11 g, float c1, float c2, float* __restrict__ part,
                             float* __restrict__ coef, int64_t plane) {
   const int lane = threadIdx.x & 63;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform (scalar) indices: per-image bases stay in SGPRs
+  const int64_t wid =
+      (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (wid >= nwaves) return;
   const int strip = (int)(wid % strips);
   const int chunk = (int)((wid / strips) % chunks);
@@ -404,15 +393,19 @@ __global__ void __launch_bounds__(256)
   const int cc = c < 0 ? 0 : (c >= w ? w - 1 : c);
   const int r0 = chunk * chunk_rows;
   const int r1 = r0 + chunk_rows < h ? r0 + chunk_rows : h;
-  const float* Xi = X + img * (int64_t)h * w + cc;
-  const float* Yi = Y + img * (int64_t)h * w + cc;
+  // per-image bases (wave-uniform) + 32-bit element offsets (planes < 2^31)
+  const float* Xi = X + img * (int64_t)h * w;
+  const float* Yi = Y + img * (int64_t)h * w;
   const int T = (r1 - r0) + 10;  // rows streamed
 
-  float ring[11][5];
+  v2 r01[11], r23[11];  // ring of horizontally filtered rows: (x, y), (x^2, y^2)
+  float r4[11];         // ... and x y
 #pragma unroll
-  for (int j = 0; j < 11; ++j)
-#pragma unroll
-    for (int z = 0; z < 5; ++z) ring[j][z] = 0.f;
+  for (int j = 0; j < 11; ++j) {
+    r01[j] = v2{0.f, 0.f};
+    r23[j] = v2{0.f, 0.f};
+    r4[j] = 0.f;
+  }
   float ssum = 0.f, l1 = 0.f, gr = 0.f, cnt = 0.f;
   // prefetched row r0 - 5
   float xn, yn;
@@ -420,7 +413,7 @@ __global__ void __launch_bounds__(256)
     const int r = r0 - 5;
     const int rc = r < 0 ? 0 : r;
     const bool ok = cin && r >= 0;
-    const float xv = Xi[(int64_t)rc * w], yv = Yi[(int64_t)rc * w];
+    const float xv = Xi[(unsigned)(rc * w + cc)], yv = Yi[(unsigned)(rc * w + cc)];
     xn = ok ? xv : 0.f;
     yn = ok ? yv : 0.f;
   }
@@ -435,7 +428,7 @@ __global__ void __launch_bounds__(256)
         const int rn = r + 1;
         const int rc = rn < 0 ? 0 : (rn >= h ? h - 1 : rn);
         const bool ok = cin && rn >= 0 && rn < h;
-        const float xv = Xi[(int64_t)rc * w], yv = Yi[(int64_t)rc * w];
+        const float xv = Xi[(unsigned)(rc * w + cc)], yv = Yi[(unsigned)(rc * w + cc)];
         xn = ok ? xv : 0.f;
         yn = ok ? yv : 0.f;
       }
@@ -450,39 +443,56 @@ __global__ void __launch_bounds__(256)
         if (r < h - 1) gr += fabsf((yn - y) - (xn - x));
       }
       if (SSIM) {
-        const float v[5] = {x, y, x * x, y * y, x * y};
-        float hv[5];
-        hpass<5>(v, g, hv);
+        // horizontal 11-tap pass over (x, y): neighbours by DPP shifts, the
+        // five statistics as two packed pairs and one scalar
+        const v2 cxy = v2{x, y};
+        v2 lxy = cxy, rxy = cxy;
+        v2 h01 = g.c * cxy;
+        v2 h23 = g.c * (cxy * cxy);
+        float h4 = g.c * (x * y);
 #pragma unroll
-        for (int z = 0; z < 5; ++z) ring[j][z] = hv[z];
+        for (int i = 0; i < 5; ++i) {
+          lxy = lprev2(lxy);
+          rxy = lnext2(rxy);
+          h01 = g.k[i] * (lxy + rxy) + h01;
+          h23 = g.k[i] * (lxy * lxy + rxy * rxy) + h23;
+          h4 = fmaf(g.k[i], fmaf(lxy.x, lxy.y, rxy.x * rxy.y), h4);
+        }
+        r01[j] = h01;
+        r23[j] = h23;
+        r4[j] = h4;
         if (t >= 10) {  // map row p = r - 5: ring slot of row p + k - 5 is (j + 1 + k) % 11
           const int p = r - 5;
-          float q[5];
+          v2 q01 = g.c * r01[(j + 6) % 11];
+          v2 q23 = g.c * r23[(j + 6) % 11];
+          float q4 = g.c * r4[(j + 6) % 11];
 #pragma unroll
-          for (int z = 0; z < 5; ++z) {
-            float a = g.c * ring[(j + 6) % 11][z];
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-              a = fmaf(g.k[i], ring[(j + 5 - i) % 11][z] + ring[(j + 7 + i) % 11][z], a);
-            q[z] = a;
+          for (int i = 0; i < 5; ++i) {
+            const int a = (j + 5 - i) % 11, b = (j + 7 + i) % 11;
+            q01 = g.k[i] * (r01[a] + r01[b]) + q01;
+            q23 = g.k[i] * (r23[a] + r23[b]) + q23;
+            q4 = fmaf(g.k[i], r4[a] + r4[b], q4);
           }
-          const float mx = q[0], my = q[1];
-          const float sxx = q[2] - mx * mx, syy = q[3] - my * my;
-          const float sxy = q[4] - mx * my;
+          const float mx = q01.x, my = q01.y;
+          const float sxx = q23.x - mx * mx, syy = q23.y - my * my;
+          const float sxy = q4 - mx * my;
           const float n1 = 2.f * mx * my + c1, n2 = 2.f * sxy + c2;
           const float d1 = mx * mx + my * my + c1, d2 = sxx + syy + c2;
           const float D = d1 * d2;
-          const float S = (n1 * n2) / D;
+          // one reciprocal (1 ulp) for the five quotients: 1/d2 = d1/D, 1/d1 = d2/D
+          const float iD = __builtin_amdgcn_rcpf(D);
+          const float S = (n1 * n2) * iD;
           if (outl) {
             ssum += S;
             if (coef) {
-              const float dS_dsx = -S / d2;
-              const float dS_dsxy = 2.f * n1 / D;
-              const float dS_dmx = 2.f * my * n2 / D - S * 2.f * mx / d1;
-              const int64_t off = (img * h + p) * (int64_t)w + c;
-              coef[off] = dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy;
-              coef[plane + off] = dS_dsx;
-              coef[2 * plane + off] = dS_dsxy;
+              const float dS_dsx = -S * (d1 * iD);
+              const float dS_dsxy = 2.f * n1 * iD;
+              const float dS_dmx = 2.f * my * n2 * iD - S * 2.f * mx * (d2 * iD);
+              float* co = coef + img * (int64_t)h * w;
+              const unsigned off = (unsigned)(p * w + c);
+              co[off] = dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy;
+              co[plane + off] = dS_dsx;
+              co[2 * plane + off] = dS_dsxy;
             }
           }
         }
@@ -514,7 +524,9 @@ __global__ void __launch_bounds__(256)
                             float alpha, float beta, float gamma, float inv_n,
                             float* __restrict__ gx) {
   const int lane = threadIdx.x & 63;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // wave-uniform (scalar) indices: per-image bases stay in SGPRs
+  const int64_t wid =
+      (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (wid >= nwaves) return;
   const int strip = (int)(wid % strips);
   const int chunk = (int)((wid / strips) % chunks);
@@ -525,7 +537,7 @@ __global__ void __launch_bounds__(256)
   const int cc = c < 0 ? 0 : (c >= w ? w - 1 : c);
   const int r0 = chunk * chunk_rows;
   const int r1 = r0 + chunk_rows < h ? r0 + chunk_rows : h;
-  const int64_t base = img * (int64_t)h * w + cc;
+  const int64_t base = img * (int64_t)h * w;  // + 32-bit element offsets below
   const float* Xi = X + base;
   const float* Yi = Y + base;
   const float* Ai = coef + base;
@@ -538,18 +550,20 @@ __global__ void __launch_bounds__(256)
   }
   const float kl1 = go * alpha * inv_n, kg = go * gamma * inv_n;
 
-  float ring[11][3];
+  v2 rab[11];     // ring of horizontally filtered coefficient rows: (A, B)
+  float rcr[11];  // ... and C
 #pragma unroll
-  for (int j = 0; j < 11; ++j)
-#pragma unroll
-    for (int z = 0; z < 3; ++z) ring[j][z] = 0.f;
+  for (int j = 0; j < 11; ++j) {
+    rab[j] = v2{0.f, 0.f};
+    rcr[j] = 0.f;
+  }
   // raw rows q (x0, y0) and q + 1 (x1, y1) of the next output q; ey_prev =
   // forward row difference of row q - 1
   float an = 0.f, bn = 0.f, cn = 0.f;
   auto load_coef = [&](int p, float& a, float& b, float& cv) {
     const int pc = p < 0 ? 0 : (p >= h ? h - 1 : p);
     const bool ok = cin && p >= 0 && p < h;
-    const int64_t o = (int64_t)pc * w;
+    const unsigned o = (unsigned)(pc * w + cc);
     const float av = Ai[o], bv = Ai[plane + o], cvv = Ai[2 * plane + o];
     a = ok ? av : 0.f;
     b = ok ? bv : 0.f;
@@ -558,7 +572,7 @@ __global__ void __launch_bounds__(256)
   auto load_raw = [&](int r, float& x, float& y) {
     const int rc = r < 0 ? 0 : (r >= h ? h - 1 : r);
     const bool ok = cin && r >= 0 && r < h;
-    const float xv = Xi[(int64_t)rc * w], yv = Yi[(int64_t)rc * w];
+    const float xv = Xi[(unsigned)(rc * w + cc)], yv = Yi[(unsigned)(rc * w + cc)];
     x = ok ? xv : 0.f;
     y = ok ? yv : 0.f;
   };
@@ -578,27 +592,38 @@ __global__ void __launch_bounds__(256)
       const int t = t0 + j;
       if (t < T) {
       if (SSIM) {
-        const float v[3] = {an, bn, cn};
+        const v2 ab = v2{an, bn};
+        const float cv = cn;
         if (t + 1 < T) load_coef(r0 - 4 + t, an, bn, cn);
-        float hv[3];
-        hpass<3>(v, g, hv);
+        v2 l = ab, rr = ab;
+        float lc = cv, rc = cv;
+        v2 hab = g.c * ab;
+        float hc = g.c * cv;
 #pragma unroll
-        for (int z = 0; z < 3; ++z) ring[j][z] = hv[z];
+        for (int i = 0; i < 5; ++i) {
+          l = lprev2(l);
+          rr = lnext2(rr);
+          lc = lprev(lc);
+          rc = lnext(rc);
+          hab = g.k[i] * (l + rr) + hab;
+          hc = fmaf(g.k[i], lc + rc, hc);
+        }
+        rab[j] = hab;
+        rcr[j] = hc;
       }
       if (t >= 10) {  // image row q = p - 5
         const int q = r0 + t - 10;
         float gsum = kl1 * ((x0 > y0) ? 1.f : (x0 < y0 ? -1.f : 0.f));
         if (SSIM) {
-          float f3[3];
+          v2 fab = g.c * rab[(j + 6) % 11];
+          float fc = g.c * rcr[(j + 6) % 11];
 #pragma unroll
-          for (int z = 0; z < 3; ++z) {
-            float a = g.c * ring[(j + 6) % 11][z];
-#pragma unroll
-            for (int i = 0; i < 5; ++i)
-              a = fmaf(g.k[i], ring[(j + 5 - i) % 11][z] + ring[(j + 7 + i) % 11][z], a);
-            f3[z] = a;
+          for (int i = 0; i < 5; ++i) {
+            const int a = (j + 5 - i) % 11, b = (j + 7 + i) % 11;
+            fab = g.k[i] * (rab[a] + rab[b]) + fab;
+            fc = fmaf(g.k[i], rcr[a] + rcr[b], fc);
           }
-          gsum += kfac * (f3[0] + 2.f * x0 * f3[1] + y0 * f3[2]);
+          gsum += kfac * (fab.x + 2.f * x0 * fab.y + y0 * fc);
         }
         float x2 = 0.f, y2 = 0.f;
         if (t + 1 < T) load_raw(q + 2, x2, y2);
@@ -614,7 +639,7 @@ __global__ void __launch_bounds__(256)
           gsum += kg * ((sx - (c >= 1 ? sxp : 0.f)) + (sy - syp));
           eyp = ey;
         }
-        if (outl && q < r1) gx[img * (int64_t)h * w + (int64_t)q * w + c] = gsum;
+        if (outl && q < r1) gx[base + (unsigned)(q * w + c)] = gsum;
         x0 = x1;
         y0 = y1;
         x1 = x2;
@@ -752,7 +777,7 @@ int mde_depth_loss_fwd(const void* pred, const void* gt, float alpha,
     nparts = masked_blocks(b * h * w);
     MDE_LAUNCH(mde::K_DLOSS_FWD, 8.0 * numel, s, dloss_masked_kernel, dim3(nparts), dim3(256),
                0, (const float*)pred, (const float*)gt, b * h * w, part);
-  } else if (win.k == KMAX) {
+  } else if (win.k == KMAX && h * w < ((int64_t)1 << 31)) {
     const StreamGeo sg = stream_geometry(b, h, w);
     nparts = (int)sg.nwaves;
     float* coef = (float*)((char*)workspace + coef_offset(b, h, w));
@@ -808,7 +833,7 @@ int mde_depth_loss_bwd(const void* pred, const void* gt, float alpha,
                (const float*)gt, b * h * w, fwd_out, gout, (float*)grad_pred);
     return MDE_OK;
   }
-  if (win.k == KMAX) {  // coefficients left by the forward
+  if (win.k == KMAX && h * w < ((int64_t)1 << 31)) {  // coefficients left by the forward
     const StreamGeo sg = stream_geometry(b, h, w);
     const unsigned blocks = (unsigned)mde::cdiv(sg.nwaves, 4);
     const float inv_n = (float)(1.0 / numel);

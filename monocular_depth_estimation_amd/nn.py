@@ -393,7 +393,7 @@ class _Conv3x3(torch.autograd.Function):
         if passes[0]:
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
             if want_stats:  # + y's per-block BN statistics from the epilogue
-                nb = _abi.query("mde_conv3x3_stats_blocks", n, cin, cout, h, w)
+                nb = _abi.query("mde_conv3x3_stats_blocks", n, cin, cout, h, w, _abi.MDE_F32)
                 stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
                 _abi.call("mde_conv3x3_fwd_stats", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y),
                           _abi.ptr(stats), n, cin, cout, h, w, _abi.dtype_code(x),
@@ -432,7 +432,8 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             if ctx.passes[2]:
                 gw = torch.empty_like(weight)
-                ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w), x)
+                ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w,
+                                    _abi.MDE_F32), x)
                 _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
                           cout, h, w, _abi.ptr(ws), _abi.dtype_code(gy), st)
             else:
@@ -442,28 +443,127 @@ class _Conv3x3(torch.autograd.Function):
         return gx, gw, None, None
 
 
+# bf16 (autocast) 3x3 convolutions on the v_mfma_f32_16x16x32_bf16 kernels:
+# (cin, cout) -> (fwd, dgrad, wgrad).  The 3-channel guide convolutions read
+# the fp32 image and stay on the fp32 kernels.
+CONV3X3_HIP_BF16 = {
+    (16, 16): (True, True, True),
+    (32, 32): (True, True, True),
+}
+
+
+def _autocast_bf16(x) -> bool:
+    return (x.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16)
+
+
+def _conv3x3_bf16_path(cin: int, cout: int, x) -> bool:
+    """autocast-bf16 (or bf16) input of a shape the bf16 kernels take."""
+    return ((_autocast_bf16(x) or x.dtype == torch.bfloat16)
+            and (cin, cout) in CONV3X3_HIP_BF16 and x.shape[-1] % 4 == 0)
+
+
+class _Conv3x3Bf16(torch.autograd.Function):
+    """The bf16 autocast 3x3 convolution (16 -> 16, 32 -> 32) on
+    v_mfma_f32_16x16x32_bf16: x / y / gx bf16, the fp32 weight rounded to
+    bf16 inside the kernels (as autocast's cast), fp32 accumulation, fp32
+    weight gradient.  Passes with a False flag run on MIOpen's bf16 kernels."""
+
+    @staticmethod
+    @_bn_fwd
+    def forward(ctx, x, weight, passes, want_stats=False):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        bf = _abi.MDE_BF16
+        stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
+        if passes[0]:
+            y = torch.empty((n, cout, h, w), dtype=torch.bfloat16, device=x.device)
+            if want_stats:
+                nb = _abi.query("mde_conv3x3_stats_blocks", n, cin, cout, h, w, bf)
+                stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
+                _abi.call("mde_conv3x3_fwd_stats", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y),
+                          _abi.ptr(stats), n, cin, cout, h, w, bf, _abi.stream_of(x))
+            else:
+                _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin,
+                          cout, h, w, bf, _abi.stream_of(x))
+        else:
+            y = torch.nn.functional.conv2d(x, weight.to(torch.bfloat16), None, 1, 1)
+        ctx.save_for_backward(x, weight)
+        ctx.passes = passes
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, gy, _gstats):
+        x, weight = ctx.saved_tensors
+        gy = gy.to(torch.bfloat16).contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        bf = _abi.MDE_BF16
+        gx = gw = None
+        st = _abi.stream_of(gy)
+        if ctx.needs_input_grad[0]:
+            if ctx.passes[1]:
+                gx = torch.empty_like(x)
+                _abi.call("mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx), n,
+                          cin, cout, h, w, bf, st)
+            else:
+                gx = torch.ops.aten.convolution_backward(
+                    gy, x, weight.to(torch.bfloat16), None, (1, 1), (1, 1), (1, 1), False, (0, 0),
+                    1, (True, False, False))[0]
+        if ctx.needs_input_grad[1]:
+            if ctx.passes[2]:
+                gw = torch.empty_like(weight)
+                ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w, bf), x)
+                _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
+                          cout, h, w, _abi.ptr(ws), bf, st)
+            else:
+                gw = torch.ops.aten.convolution_backward(
+                    gy, x, weight.to(torch.bfloat16), None, (1, 1), (1, 1), (1, 1), False, (0, 0),
+                    1, (False, True, False))[1].float()
+        return gx, gw, None, None
+
+
 def conv3x3_passes(conv: nn.Conv2d, x):
     """(fwd, dgrad, wgrad) HIP flags for a 3x3/s1/p1 conv, or None if it is not one.
 
-    fp32 activations only: under bf16 autocast a bf16 input goes to MIOpen's bf16
-    kernels (cfg2 bf16 step: 854.9 img/s; casting it to fp32 for the HIP kernel
-    832.5; every small-channel 3x3 on MIOpen bf16, fp32 inputs included, 761.2)."""
+    Under bf16 autocast the 16 -> 16 / 32 -> 32 convs run on the bf16 MFMA
+    kernels (autocast's conv semantics: bf16 operands, fp32 accumulation,
+    bf16 output, no NCHW <-> NHWC transposes); other bf16 inputs go to
+    MIOpen's bf16 kernels; fp32 inputs (also the guide convs' image under
+    autocast) to the fp32 kernels."""
     if (conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros"
-            or x.dim() != 4 or x.dtype != torch.float32):
+            or x.dim() != 4):
         return None
-    p = CONV3X3_HIP.get((conv.in_channels, conv.out_channels))
+    cin, cout = conv.in_channels, conv.out_channels
+    if _conv3x3_bf16_path(cin, cout, x):
+        p, dt = CONV3X3_HIP_BF16[(cin, cout)], _abi.MDE_BF16
+    elif x.dtype == torch.float32:
+        p, dt = CONV3X3_HIP.get((cin, cout)), _abi.MDE_F32
+    else:
+        return None
     if p is None:
         return None
-    p = tuple(bool(f) and bool(_abi.query("mde_conv3x3_supported", conv.in_channels,
-                                          conv.out_channels, i)) for i, f in enumerate(p))
+    p = tuple(bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
+              for i, f in enumerate(p))
     return p if any(p) else None
+
+
+def _conv3x3_apply(x, weight, passes, want_stats):
+    cin, cout = x.shape[1], weight.shape[0]
+    if _conv3x3_bf16_path(cin, cout, x):
+        return _Conv3x3Bf16.apply(x.to(torch.bfloat16), weight, tuple(passes), want_stats)
+    return _Conv3x3.apply(x, weight, tuple(passes), want_stats)
 
 
 def conv3x3(x, weight, passes=(True, True, True)):
     """Bias-free 3x3 / stride 1 / padding 1 convolution on the HIP MFMA kernel (per-pass flags)."""
     _gpu(x)
-    return _Conv3x3.apply(x, weight, tuple(passes), False)[0]
+    return _conv3x3_apply(x, weight, passes, False)[0]
 
 
 def conv3x3_stats(x, weight, passes=(True, True, True)):
@@ -471,7 +571,7 @@ def conv3x3_stats(x, weight, passes=(True, True, True)):
     (shift, count, s1, s2) from the forward epilogue, or None when the forward
     is not on the HIP kernel (MIOpen)."""
     _gpu(x)
-    y, stats = _Conv3x3.apply(x, weight, tuple(passes), bool(passes[0]))
+    y, stats = _conv3x3_apply(x, weight, passes, bool(passes[0]))
     return y, (stats if stats.shape[1] > 0 else None)
 
 

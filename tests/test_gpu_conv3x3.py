@@ -50,7 +50,7 @@ def test_conv3x3_vs_float64_oracle(cin, cout, n, h, w):
     wr = wt.double().requires_grad_(True)
     yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
     yr.backward(gy.double())
-    passes = tuple(bool(_abi.query("mde_conv3x3_supported", cin, cout, i)) for i in range(3))
+    passes = tuple(bool(_abi.query("mde_conv3x3_supported", cin, cout, i, 0)) for i in range(3))
     assert passes[0] and passes[2]
     xg = x.to(DEV).requires_grad_(passes[1])
     wg = wt.to(DEV).requires_grad_(True)
@@ -72,7 +72,7 @@ def test_conv3x3_full_size_vs_miopen(cin, cout, h, w):
     x = torch.rand((4, cin, h, w), device=DEV, generator=gen) - 0.5
     wt = (torch.rand((cout, cin, 3, 3), device=DEV, generator=gen) - 0.5) * 0.3
     gy = torch.rand((4, cout, h, w), device=DEV, generator=gen) - 0.5
-    passes = tuple(bool(_abi.query("mde_conv3x3_supported", cin, cout, i)) for i in range(3))
+    passes = tuple(bool(_abi.query("mde_conv3x3_supported", cin, cout, i, 0)) for i in range(3))
     xh = x.clone().requires_grad_(passes[1])
     wh = wt.clone().requires_grad_(True)
     y = conv3x3(xh, wh, passes)
@@ -106,7 +106,7 @@ def test_conv3x3_unsupported_shape_raises():
     x = torch.rand((1, 8, 4, 4), device=DEV)
     w = torch.rand((8, 8, 3, 3), device=DEV)
     y = torch.empty((1, 8, 4, 4), device=DEV)
-    assert not _abi.query("mde_conv3x3_supported", 8, 8, 0)
+    assert not _abi.query("mde_conv3x3_supported", 8, 8, 0, 0)
     with pytest.raises(_abi.MdeError, match="unsupported"):
         _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(w), _abi.ptr(y), 1, 8, 8, 4, 4, 0,
                   _abi.stream_of(x))
@@ -275,3 +275,69 @@ def test_bn_statistics_from_pointwise_epilogue(cin, cout, n, h, w):
     zb = batch_norm_act(y2.detach(), bn3, "relu")
     assert rel_err(za, zb) <= 2e-6
     assert rel_err(bn2.running_var, bn3.running_var) <= 2e-5
+
+
+# ----------------------------------------------------------------- bf16 (cfg3)
+BF_PAIRS = [(16, 16), (32, 32)]
+# w % 4 == 0 (the bf16 kernels' 8-byte column chunks); ragged tiles and rows
+BF_SIZES = [(2, 16, 64), (1, 13, 72), (3, 20, 132), (1, 1, 4), (2, 37, 200)]
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).double()
+
+
+@pytest.mark.parametrize("cin,cout", BF_PAIRS)
+@pytest.mark.parametrize("n,h,w", BF_SIZES)
+def test_conv3x3_bf16_vs_float64_oracle(cin, cout, n, h, w):
+    """The v_mfma_f32_16x16x32_bf16 kernels (autocast's conv semantics: bf16
+    x / gy, the fp32 weight rounded to bf16, fp32 accumulation, bf16 y / gx,
+    fp32 weight gradient) against float64 convolutions of the SAME rounded
+    operands.  y and gx are the exact sums rounded once to bf16, so they may
+    differ from the oracle rounded to bf16 by one bf16 unit where the fp32
+    accumulation order lands on the other side of a rounding boundary: bound
+    2^-8 relative per element (+1e-6 of the scale); gw (fp32, sums over
+    n*h*w pixels) 2e-5 of its scale."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import _Conv3x3Bf16
+    x, wt, gy = _case(cin, cout, n, h, w, 7 * cin + h + w)
+    passes = tuple(bool(_abi.query("mde_conv3x3_supported", cin, cout, i, _abi.MDE_BF16))
+                   for i in range(3))
+    assert passes == (True, True, True)
+    xr = _bf(x).requires_grad_(True)
+    wr = _bf(wt).requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+    yr.backward(_bf(gy))
+    xg = x.to(DEV, torch.bfloat16).requires_grad_(True)
+    wg = wt.to(DEV).requires_grad_(True)
+    y, _ = _Conv3x3Bf16.apply(xg, wg, passes, False)
+    assert y.dtype == torch.bfloat16
+    y.backward(gy.to(DEV, torch.bfloat16))
+    assert xg.grad.dtype == torch.bfloat16 and wg.grad.dtype == torch.float32
+    for got, want, what in ((y, yr, "forward"), (xg.grad, xr.grad, "data gradient")):
+        g = got.detach().double().cpu()
+        scale = float(want.abs().max())
+        bad = (g - want).abs() > (2.0 ** -8) * want.abs() + 1e-6 * scale
+        assert not bool(bad.any()), (what, float((g - want).abs().max()), scale)
+    assert rel_err(wg.grad, wr.grad) <= 2e-5, "weight gradient"
+
+
+@pytest.mark.parametrize("cin,cout", BF_PAIRS)
+def test_conv3x3_bf16_stats_epilogue(cin, cout):
+    """The bf16 forward's BatchNorm-statistics epilogue describes the bf16 y
+    it wrote: merged (count, mean, M2) equal float64 statistics of y."""
+    from monocular_depth_estimation_amd.nn import _Conv3x3Bf16
+    x, wt, _ = _case(cin, cout, 3, 29, 100, 11 + cin)
+    xg = x.to(DEV, torch.bfloat16)
+    y, st = _Conv3x3Bf16.apply(xg, wt.to(DEV), (True, True, True), True)
+    st = st.double().cpu()
+    yd = y.double().cpu()
+    for c in range(cout):
+        ref, cnt, s1, s2 = st[c, :, 0], st[c, :, 1], st[c, :, 2], st[c, :, 3]
+        n = float(cnt.sum())
+        mean = float((s1 + cnt * ref).sum()) / n
+        ex2 = float((s2 + 2 * ref * s1 + cnt * ref * ref).sum()) / n
+        v = yd[:, c]
+        assert n == v.numel()
+        assert abs(mean - float(v.mean())) <= 1e-5 * (1 + abs(float(v.mean())))
+        assert abs((ex2 - mean * mean) - float(v.var(unbiased=False))) <= 1e-4 * float(v.var())

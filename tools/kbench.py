@@ -259,24 +259,24 @@ def _main():
             y = torch.empty_like(gy)
             gx = torch.empty_like(x)
             gw = torch.empty_like(wt)
-            ws = torch.empty(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w) // 4 + 1,
+            ws = torch.empty(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w, 0) // 4 + 1,
                              device=dev)
             st = _abi.stream_of(x)
             flop = 2.0 * n * h * w * cout * cin * 9
             nb = 4.0 * n * h * w * (cin + cout)
             tag = f"{cin}->{cout} {h}x{w}"
-            if _abi.query("mde_conv3x3_supported", cin, cout, 0):
+            if _abi.query("mde_conv3x3_supported", cin, cout, 0, 0):
                 report_tf(f"conv3x3 fwd HIP {tag}", timeit(lambda: _abi.call(
                     "mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, cin, cout, h, w, 0,
                     st), a.reps), flop, nb)
             report_tf(f"conv3x3 fwd MIOpen {tag}", timeit(lambda: tconv(x, wt, None, 1, 1), a.reps), flop, nb)
-            if _abi.query("mde_conv3x3_supported", cin, cout, 1):
+            if _abi.query("mde_conv3x3_supported", cin, cout, 1, 0):
                 report_tf(f"conv3x3 dgrad HIP {tag}", timeit(lambda: _abi.call(
                     "mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, cin, cout, h, w,
                     0, st), a.reps), flop, nb)
                 report_tf(f"conv3x3 dgrad MIOpen {tag}", timeit(
                     lambda: torch.nn.grad.conv2d_input(x.shape, wt, gy, padding=1), a.reps), flop, nb)
-            if _abi.query("mde_conv3x3_supported", cin, cout, 2):
+            if _abi.query("mde_conv3x3_supported", cin, cout, 2, 0):
                 report_tf(f"conv3x3 wgrad HIP {tag}", timeit(lambda: _abi.call(
                     "mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h,
                     w, _abi.ptr(ws), 0, st), a.reps), flop, nb)

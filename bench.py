@@ -32,8 +32,15 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # fp32-input MFMA dense peak (= fp32 vector rate, MI355X_MICROARCH.md)
-# rocprofv3 PMC HBM bytes per launch (tools/pmc_traffic.py), newest round first
-PMC_FILES = [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic.json") for r in (2, 1)]
+# rocprofv3 PMC HBM bytes per launch (tools/pmc_traffic.py), newest round first.
+# Counters are per workload and precision: a kernel's bytes in the cfg2 fp32
+# step say nothing about its bytes in the bf16 or the NewCRF step.
+def pmc_files(workload: str, amp: str) -> list[str]:
+    tag = f"{workload}_{amp}"
+    files = [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic_{tag}.json") for r in (3,)]
+    if tag == "guidedepth_fp32":  # rounds 1-2 profiled the cfg2 fp32 step only
+        files += [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic.json") for r in (2, 1)]
+    return files
 
 
 AMP_DTYPE = ("bf16 autocast: convs / GEMMs bf16 (MIOpen / hipBLASLt); HIP BatchNorm, BN-ReLU-1x1, "
@@ -258,7 +265,7 @@ def main():
 
     images = world.size * args.bs * args.steps
     pmc = {}
-    pmc_file = next((f for f in PMC_FILES if os.path.exists(f)), None)
+    pmc_file = next((f for f in pmc_files(args.workload, args.amp) if os.path.exists(f)), None)
     if pmc_file:
         with open(pmc_file) as f:
             pmc = json.load(f)

@@ -167,146 +167,6 @@ __device__ __forceinline__ float elem(const float* base, int ld, int col, int t,
   return 0.f;
 }
 
-// P^T[jt][it] (key rows, query columns) of this wave's (window, head):
-// S^T = K Q^T * scale + table + mask, softmax over keys per query column.
-// Lane (l16, g): s[jt][it][r] is key j = 16jt + 4g + r, query i = 16it + l16.
-// Columns of padded queries (i >= ws*ws) come out 0.
-template <int WS>
-__device__ __forceinline__ void probs_t(const Geo& g, const float* __restrict__ qkrow,
-                                        const float* __restrict__ qkb, int head,
-                                        const int* tok, const int* lab, const float* tab,
-                                        f4 s[4][4]) {
-  const int lane = threadIdx.x & 63, l16 = lane & 15, g4 = lane >> 4;
-  const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
-  const int c2 = 2 * g.c;
-  {
-    float ka[4][8];
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-      row8(qkrow, c2, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      float qb[8];
-      row8(qkrow, c2, head * D + 8 * g4, tok[16 * it + l16], qkb, qb);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt) s[jt][it] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 8; ++k)  // 4 independent accumulators in flight
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt) s[jt][it] = mfma4(ka[jt][k], qb[k], s[jt][it]);
-    }
-  }
-  // this lane's 16 keys: table offset -(yj*span + xj) and region label, packed
-  int kj[16];
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int j = 16 * jt + 4 * g4 + r;
-      const int y = j / ws, x = j - y * ws;
-      kj[4 * jt + r] = ((y * span + x) << 4) | lab[j];
-    }
-#pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    const int i = 16 * it + l16;
-    const bool iv = i < n;
-    const int yi = i / ws, xi = i - yi * ws, li = lab[i];
-    const int base = (yi + ws - 1) * span + xi + ws - 1;
-    float m = -INFINITY;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 16 * jt + 4 * g4 + r;
-        float v;
-        if (j >= n) {
-          v = -INFINITY;
-        } else if (!iv) {
-          v = 0.f;
-        } else {
-          const int q = kj[4 * jt + r];
-          v = s[jt][it][r] + tab[base - (q >> 4)];
-          if (g.shift && (q & 15) != li) v += -100.f;
-        }
-        s[jt][it][r] = v;
-        m = fmaxf(m, v);
-      }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __expf(s[jt][it][r] - m);
-        s[jt][it][r] = e;
-        sum += e;
-      }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = iv ? 1.f / sum : 0.f;  // padded query columns -> 0
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) s[jt][it] *= inv;
-  }
-}
-
-template <int WS>
-__global__ void __launch_bounds__(256)
-    wattn_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ qkb,
-                     const float* __restrict__ v, const float* __restrict__ table,
-                     float* __restrict__ out, Geo g) {
-  __shared__ int tok[NP], lab[NP];
-  __shared__ float tab[kHeads][TABP];
-  const int win = blockIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
-  const int head = blockIdx.y * kHeads + w;
-  const int ws = wsize<WS>(g), ntab = (2 * ws - 1) * (2 * ws - 1);
-  window_tokens<WS>(g, win, tok, lab);
-  if (head < g.heads)
-    for (int e = lane; e < ntab; e += 64) tab[w][e] = table[e * g.heads + head];
-  __syncthreads();
-  if (head >= g.heads) return;
-  const int bidx = win / (g.nwh * g.nww);
-  const int64_t img = (int64_t)bidx * g.h * g.w;
-  f4 s[4][4];
-  probs_t<WS>(g, qk + img * 2 * g.c, qkb, head, tok, lab, tab[w], s);
-  // O = P V: A = P[i][j] straight from the S^T accumulators (k <-> key
-  // 16jt + 4g + r), B = V[j][d] per lane.
-  const float* vrow = v + img * g.c;
-  float vb[4][4][2];
-#pragma unroll
-  for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = tok[16 * jt + 4 * g4 + r];
-#pragma unroll
-      for (int dt = 0; dt < 2; ++dt)
-        vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, g.vb);
-    }
-  float* orow = out + img * g.c;
-#pragma unroll
-  for (int it = 0; it < 4; ++it) {
-    f4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma4(s[jt][it][r], vb[jt][r][dt], o[dt]);
-#pragma unroll
-    for (int rr = 0; rr < 4; ++rr) {
-      const int t = tok[16 * it + 4 * g4 + rr];
-      if (t >= 0) {
-#pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
-          orow[(unsigned)(t * g.c + head * D + 16 * dt + l16)] = o[dt][rr];
-      }
-    }
-  }
-}
-
 // One 16-key tile of sum_i T[j][i] B[i][c]: o[ct] (C layout: key 16jt + 4g + rr,
 // c = 16ct + l16), B given per lane as b[it][r][ct] = B[16it + 4g + r][16ct + l16].
 template <int WS, int jt>
@@ -367,23 +227,18 @@ __device__ __forceinline__ void static_for4(F&& f) {
   f(std::integral_constant<int, 3>{});
 }
 
-// The backward's P, staged query tile by query tile: S^T columns of one
-// 16-query tile (4 accumulators), their softmax, straight into the LDS tile
-// -- 16 live score registers instead of probs_t's 64 (the register budget of
-// three waves per SIMD).
+// Per-lane operands of one window-head's scores: K rows (ka) and the
+// key table offsets / region labels (kj), loaded once for all query tiles.
 template <int WS>
-__device__ __forceinline__ void probs_stage(const Geo& g, const float* __restrict__ qkrow,
-                                            const float* __restrict__ qkb, int head,
-                                            const int* tok, const int* lab, const float* tab,
-                                            float* T) {
-  const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
-  const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
-  const int c2 = 2 * g.c;
-  float ka[4][8];
+__device__ __forceinline__ void key_operands(const Geo& g, const float* __restrict__ qkrow,
+                                             const float* __restrict__ qkb, int head,
+                                             const int* tok, const int* lab, int lane,
+                                             float ka[4][8], int kj[16]) {
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int ws = wsize<WS>(g), span = 2 * ws - 1;
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
-    row8(qkrow, c2, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
-  int kj[16];
+    row8(qkrow, 2 * g.c, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
@@ -392,63 +247,163 @@ __device__ __forceinline__ void probs_stage(const Geo& g, const float* __restric
       const int y = j / ws, x = j - y * ws;
       kj[4 * jt + r] = ((y * span + x) << 4) | lab[j];
     }
+}
+
+// P^T of query tile `it` (keys 16jt + 4g + r of query 16it + l16 in s[jt][r]):
+// S^T column tile by 8 MFMA steps over the head dim, table bias + shift mask,
+// softmax over the keys; padded query columns 0.  16 live score registers
+// (probs_t's whole 4x4 tile holds 64).
+template <int WS, int it>
+__device__ __forceinline__ void probs_tile(const Geo& g, const float* __restrict__ qkrow,
+                                           const float* __restrict__ qkb, int head,
+                                           const int* tok, const int* lab, const float* tab,
+                                           const float ka[4][8], const int kj[16], int lane,
+                                           f4 s[4]) {
+  const int l16 = lane & 15, g4 = lane >> 4;
+  const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
+  {
+    float qb[8];
+    row8(qkrow, 2 * g.c, head * D + 8 * g4, tok[16 * it + l16], qkb, qb);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) s[jt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) s[jt] = mfma4(ka[jt][k], qb[k], s[jt]);
+  }
+  const int i = 16 * it + l16;
+  const bool iv = i < n;
+  const int yi = i / ws, xi = i - yi * ws, li = lab[i];
+  const int base = (yi + ws - 1) * span + xi + ws - 1;
+  float m = -INFINITY;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int j = 16 * jt + 4 * g4 + r;
+      float v;
+      if (j >= n) {
+        v = -INFINITY;
+      } else if (!iv) {
+        v = 0.f;
+      } else {
+        const int q = kj[4 * jt + r];
+        v = s[jt][r] + tab[base - (q >> 4)];
+        if (g.shift && (q & 15) != li) v += -100.f;
+      }
+      s[jt][r] = v;
+      m = fmaxf(m, v);
+    }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float e = __expf(s[jt][r] - m);
+      s[jt][r] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = iv ? 1.f / sum : 0.f;  // padded query columns -> 0
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt) s[jt] *= inv;
+}
+
+// The backward's P, staged query tile by query tile straight into the LDS
+// tile (the register budget of three waves per SIMD).
+template <int WS>
+__device__ __forceinline__ void probs_stage(const Geo& g, const float* __restrict__ qkrow,
+                                            const float* __restrict__ qkb, int head,
+                                            const int* tok, const int* lab, const float* tab,
+                                            float* T) {
+  const int lane = opaque_lane();
+  float ka[4][8];
+  int kj[16];
+  key_operands<WS>(g, qkrow, qkb, head, tok, lab, lane, ka, kj);
   static_for4([&](auto it_c) {
     constexpr int it = decltype(it_c)::value;
     f4 s[4];
-    {
-      float qb[8];
-      row8(qkrow, c2, head * D + 8 * g4, tok[16 * it + l16], qkb, qb);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt) s[jt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt) s[jt] = mfma4(ka[jt][k], qb[k], s[jt]);
-    }
-    const int i = 16 * it + l16;
-    const bool iv = i < n;
-    const int yi = i / ws, xi = i - yi * ws, li = lab[i];
-    const int base = (yi + ws - 1) * span + xi + ws - 1;
-    float m = -INFINITY;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int j = 16 * jt + 4 * g4 + r;
-        float v;
-        if (j >= n) {
-          v = -INFINITY;
-        } else if (!iv) {
-          v = 0.f;
-        } else {
-          const int q = kj[4 * jt + r];
-          v = s[jt][r] + tab[base - (q >> 4)];
-          if (g.shift && (q & 15) != li) v += -100.f;
-        }
-        s[jt][r] = v;
-        m = fmaxf(m, v);
-      }
-    m = fmaxf(m, __shfl_xor(m, 16, 64));
-    m = fmaxf(m, __shfl_xor(m, 32, 64));
-    float sum = 0.f;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float e = __expf(s[jt][r] - m);
-        s[jt][r] = e;
-        sum += e;
-      }
-    sum += __shfl_xor(sum, 16, 64);
-    sum += __shfl_xor(sum, 32, 64);
-    const float inv = iv ? 1.f / sum : 0.f;  // padded query columns -> 0
+    probs_tile<WS, it>(g, qkrow, qkb, head, tok, lab, tab, ka, kj, lane, s);
     static_for4([&](auto jt_c) {
       constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, s[jt][r] * inv, lane);
+      for (int r = 0; r < 4; ++r) own_put<WS, jt, it>(T, r, s[jt][r], lane);
     });
+  });
+}
+
+// Forward: one wave per (window, head), query tile by query tile: P^T
+// columns (probs_tile), then O = P V with A = P[i][j] straight from the S^T
+// accumulators (k <-> key 16jt + 4g + r) and B = V[j][d] per lane.
+template <int WS>
+__global__ void __launch_bounds__(256, 4)
+    wattn_fwd_kernel(const float* __restrict__ qk, const float* __restrict__ qkb,
+                     const float* __restrict__ v, const float* __restrict__ table,
+                     float* __restrict__ out, Geo g) {
+  __shared__ int tok[NP], lab[NP], kjs[NP];
+  __shared__ float tab[kHeads][TABP];
+  const int win = blockIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
+  const int head = blockIdx.y * kHeads + w;
+  const int ws = wsize<WS>(g), ntab = (2 * ws - 1) * (2 * ws - 1);
+  window_tokens<WS>(g, win, tok, lab);
+  if (head < g.heads)
+    for (int e = lane; e < ntab; e += 64) tab[w][e] = table[e * g.heads + head];
+  __syncthreads();
+  if (threadIdx.x < NP) {  // key j's table offset and region label, shared by the heads
+    const int j = threadIdx.x, y = j / ws, x = j - y * ws;
+    kjs[j] = ((y * (2 * ws - 1) + x) << 4) | lab[j];
+  }
+  __syncthreads();
+  if (head >= g.heads) return;
+  const int bidx = win / (g.nwh * g.nww);
+  const int64_t img = (int64_t)bidx * g.h * g.w;
+  const float* qkrow = qk + img * 2 * g.c;
+  float ka[4][8];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+    row8(qkrow, 2 * g.c, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
+  const float* vrow = v + img * g.c;
+  float vb[4][4][2];
+#pragma unroll
+  for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = tok[16 * jt + 4 * g4 + r];
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+        vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, g.vb);
+    }
+  float* orow = out + img * g.c;
+  static_for4([&](auto it_c) {
+    constexpr int it = decltype(it_c)::value;
+    const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;  // per-tile index math
+    int kj[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) kj[k] = kjs[16 * (k >> 2) + 4 * g4 + (k & 3)];
+    f4 s[4];
+    probs_tile<WS, it>(g, qkrow, qkb, head, tok, lab, tab[w], ka, kj, lane, s);
+    f4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) o[dt] = mfma4(s[jt][r], vb[jt][r][dt], o[dt]);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      const int t = tok[16 * it + 4 * g4 + rr];
+      if (t >= 0) {
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+          orow[(unsigned)(t * g.c + head * D + 16 * dt + l16)] = o[dt][rr];
+      }
+    }
   });
 }
 

@@ -299,15 +299,33 @@ __host__ __device__ __forceinline__ bool table_vec(int64_t total, int64_t hw) {
   return (hw & 3) == 0 && total < ((int64_t)1 << 31);
 }
 
-// Channel-table mode for small planes: every block builds all channels'
-// coefficients in LDS (block 0 is the designated writer), then grid-strides.
+// Channel-table mode for small planes: block b owns the contiguous planes
+// [p0, p1) of its share, builds the coefficients of just the channels those
+// planes hold in LDS (not all c: the per-block prologue was the kernel's
+// cost at 1-300-pixel planes), then streams its planes.  The designated
+// writer of channel ch is the block holding plane ch (image 0).
+struct PlaneShare {
+  int64_t p0, p1, nch;  // planes [p0, p1), distinct channels min(p1 - p0, c)
+  __device__ PlaneShare(int64_t planes, int64_t c) {
+    const int64_t per = (planes + gridDim.x - 1) / gridDim.x;
+    p0 = blockIdx.x * per;
+    p1 = p0 + per < planes ? p0 + per : planes;
+    if (p0 > p1) p0 = p1;
+    nch = p1 - p0 < c ? p1 - p0 : c;
+  }
+  __device__ __forceinline__ int64_t channel(int64_t k, int64_t c) const { return (p0 + k) % c; }
+  __device__ __forceinline__ bool owner(int64_t ch) const { return ch >= p0 && ch < p1; }
+};
+
 template <typename T>
 __global__ void __launch_bounds__(256)
     bn_apply_table_kernel(const T* __restrict__ x, const T* __restrict__ r,
                           T* __restrict__ y, int64_t planes, int64_t c,
                           int64_t hw, int act, FwdArgs A) {
   extern __shared__ float tab[];  // [2][c]
-  for (int64_t ch = threadIdx.x; ch < c; ch += blockDim.x) {
+  const PlaneShare ps(planes, c);
+  for (int64_t k = threadIdx.x; k < ps.nch; k += blockDim.x) {
+    const int64_t ch = ps.channel(k, c);
     double s1 = 0.0, s2 = 0.0;
     if (A.training) {
       for (int s = 0; s < A.slices; ++s) {
@@ -315,17 +333,16 @@ __global__ void __launch_bounds__(256)
         s2 += (double)A.part[(ch * A.slices + s) * 2 + 1];
       }
     }
-    const FwdCh k = fwd_channel(A, x, ch, s1, s2, blockIdx.x == 0);
-    tab[ch] = k.sc;
-    tab[c + ch] = k.sh;
+    const FwdCh kc = fwd_channel(A, x, ch, s1, s2, ps.owner(ch));
+    tab[ch] = kc.sc;
+    tab[c + ch] = kc.sh;
   }
   __syncthreads();
-  const int64_t total = planes * hw;
-  if (table_vec(total, hw)) {
+  if (table_vec(planes * hw, hw)) {
     // Four consecutive elements share a plane: float4 traffic, 32-bit index math.
-    const uint32_t total4 = (uint32_t)(total >> 2), hw4 = (uint32_t)(hw >> 2), cc = (uint32_t)c;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total4;
-         t += gridDim.x * blockDim.x) {
+    const uint32_t hw4 = (uint32_t)(hw >> 2), cc = (uint32_t)c;
+    const uint32_t t1 = (uint32_t)(ps.p1 * (hw >> 2));
+    for (uint32_t t = (uint32_t)(ps.p0 * (hw >> 2)) + threadIdx.x; t < t1; t += blockDim.x) {
       const uint32_t ch = (t / hw4) % cc;
       const float4 q = r ? ld4(r + 4 * (int64_t)t) : make_float4(0.f, 0.f, 0.f, 0.f);
       st4(y + 4 * (int64_t)t,
@@ -333,8 +350,7 @@ __global__ void __launch_bounds__(256)
     }
     return;
   }
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t t = ps.p0 * hw + threadIdx.x; t < ps.p1 * hw; t += blockDim.x) {
     const int64_t ch = (t / hw) % c;
     float v = ld1(x + t) * tab[ch] + tab[c + ch];
     if (r) v += ld1(r + t);
@@ -519,13 +535,15 @@ __global__ void __launch_bounds__(256)
                               T* __restrict__ gr, int64_t planes, int64_t c,
                               int64_t hw, int act, BwdArgs P) {
   extern __shared__ float tab[];  // [5][c]
-  for (int64_t ch = threadIdx.x; ch < c; ch += blockDim.x) {
+  const PlaneShare ps(planes, c);  // as bn_apply_table_kernel
+  for (int64_t kk = threadIdx.x; kk < ps.nch; kk += blockDim.x) {
+    const int64_t ch = ps.channel(kk, c);
     double a = 0.0, b = 0.0;
     for (int s = 0; s < P.slices; ++s) {
       a += (double)P.part[(ch * P.slices + s) * 2];
       b += (double)P.part[(ch * P.slices + s) * 2 + 1];
     }
-    const BwdCh k = bwd_channel(P, ch, a, b, blockIdx.x == 0);
+    const BwdCh k = bwd_channel(P, ch, a, b, ps.owner(ch));
     tab[ch] = k.sc;
     tab[c + ch] = k.sh;
     tab[2 * c + ch] = k.A;
@@ -535,9 +553,9 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   const int64_t total = planes * hw;
   if (table_vec(total, hw)) {
-    const uint32_t total4 = (uint32_t)(total >> 2), hw4 = (uint32_t)(hw >> 2), cc = (uint32_t)c;
-    for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total4;
-         t += gridDim.x * blockDim.x) {
+    const uint32_t hw4 = (uint32_t)(hw >> 2), cc = (uint32_t)c;
+    const uint32_t t1 = (uint32_t)(ps.p1 * (hw >> 2));
+    for (uint32_t t = (uint32_t)(ps.p0 * (hw >> 2)) + threadIdx.x; t < t1; t += blockDim.x) {
       const uint32_t ch = (t / hw4) % cc;
       const int64_t o = 4 * (int64_t)t;
       const float sc = tab[ch], sh = tab[c + ch];
@@ -558,8 +576,7 @@ __global__ void __launch_bounds__(256)
     }
     return;
   }
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t t = ps.p0 * hw + threadIdx.x; t < ps.p1 * hw; t += blockDim.x) {
     const int64_t ch = (t / hw) % c;
     const float v = ld1(x + t);
     const float e = dy_eff(ld1(gy + t), v, r ? ld1(r + t) : 0.f, tab[ch], tab[c + ch], act);
@@ -573,8 +590,12 @@ inline int stream_grid(int64_t work) {
   return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
 }
 
+// blocks of the table kernels: ~4 float4 per thread, at most one per plane
 inline int table_grid(int64_t total, int64_t hw) {
-  return stream_grid(table_vec(total, hw) ? total >> 2 : total);
+  const int64_t planes = total / hw;
+  const int64_t b = mde::cdiv(table_vec(total, hw) ? total >> 2 : total, 1024);
+  const int64_t g = b < 1 ? 1 : (b > planes ? planes : b);
+  return (int)(g > 4096 ? 4096 : g);
 }
 
 inline dim3 plane_grid(int64_t planes, int64_t hw) {

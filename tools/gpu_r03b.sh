@@ -11,7 +11,7 @@ trap 'kill $HB; rm -rf gpurun_out/miopen_sync && cp -r .miopen gpurun_out/miopen
 step() { echo "== $1 ($(date +%T))"; }
 step "conv tests"
 timeout -k 10 600 python -u -m pytest -q --timeout 120 --timeout-method thread \
-  tests/test_gpu_conv3x3.py > gpurun_out/b_conv.log 2>&1
+  tests/test_gpu_conv3x3.py tests/test_gpu_bn.py > gpurun_out/b_conv.log 2>&1
 rc=$?; tail -n 6 gpurun_out/b_conv.log; [ $rc -le 1 ] || exit $rc
 step "tests"
 timeout -k 10 900 python -u -m pytest -q --timeout 300 --timeout-method thread \

@@ -77,6 +77,13 @@ struct Tile {
     if constexpr (kCompact && t == 3) return v < kValid;
     return true;
   }
+  // k-steps r of a product contracting over 16-tile `t` (index 16t + 4g + r):
+  // in the compact last tile only r = 0 holds a real index (48); the other
+  // steps would multiply zeros
+  template <int t>
+  __device__ static constexpr int ksteps() {
+    return kCompact && t == 3 ? 1 : 4;
+  }
 };
 constexpr int kOccBwd7 = 3;  // blocks per CU the 7x7 backward is built for
 constexpr int kHeads = 4;    // heads (= waves) per block
@@ -180,7 +187,7 @@ __device__ __forceinline__ void mm_tb_tile(const float* T, const float b[4][4][2
   auto step = [&](auto it_c) {
     constexpr int it = decltype(it_c)::value;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < TL::template ksteps<it>(); ++r) {
       const float a = T[rowoff + TL::template clamp<it>(16 * it + 4 * g4 + r)];
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) o[ct] = mfma4(a, b[it][r][ct], o[ct]);
@@ -547,7 +554,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
           static_for4([&](auto jt_c) {
             constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
+            for (int r = 0; r < TL::template ksteps<jt>(); ++r) {
               const float a = own_get<WS, jt, it>(T, r, lane);  // dS[i][j]
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct) q[ct] = mfma4(a, b[jt][r][ct], q[ct]);

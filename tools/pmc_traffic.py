@@ -33,7 +33,7 @@ NAMES = [
     (r"se_partial_kernel<true>", "se_bwd_dot"),
     (r"se_fc[12]_kernel", "se_fc"),
     (r"se_scale_kernel", "se_scale"),
-    (r"se_(bfc[123]|wgrad)_kernel", "se_bwd_fc"),
+    (r"se_(bfc[123]|bfc_all|wgrad)_kernel", "se_bwd_fc"),
     (r"se_apply_kernel", "se_bwd_apply"),
     (r"skip_fwd_mfma_kernel<\d+, \d+, true", "skip_reduce_fwd"),
     (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
@@ -41,6 +41,9 @@ NAMES = [
     (r"skip_bwd_mfma_kernel<\d+, \d+, false", "pointwise_bwd"),
     (r"conv3x3_fwd_kernel<.*false>", "conv3x3_fwd"),
     (r"conv3x3_fwd_kernel<.*true>", "conv3x3_dgrad"),
+    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd"),
+    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad"),
+    (r"conv3x3_bf_wgrad_kernel", "conv3x3_wgrad"),
     (r"conv3x3_wgrad_kernel<3,", "conv3x3_wgrad_guide"),
     (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),
     (r"wgrad_reduce[12]_kernel", "conv3x3_wreduce"),
@@ -51,6 +54,8 @@ NAMES = [
     (r"minmax_final_kernel", "minmax_final"),
     (r"depthnorm_kernel", "depthnorm_apply"),
     (r"ssim3_(l1|stream)_kernel", "ssim3_l1"),
+    (r"dloss_(fwd_stream|masked|map|final)_kernel", "depth_loss_fwd"),
+    (r"dloss_(bwd_stream|masked_bwd|grad)_kernel", "depth_loss_bwd"),
     (r"loss_final_kernel", "loss_final"),
     (r"bn_stats_kernel", "bn_fwd_stats"),
     (r"bn_coef_kernel", "bn_fwd_final"),

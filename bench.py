@@ -43,9 +43,10 @@ def pmc_files(workload: str, amp: str) -> list[str]:
     return files
 
 
-AMP_DTYPE = ("bf16 autocast: convs / GEMMs bf16 (MIOpen / hipBLASLt); HIP BatchNorm, BN-ReLU-1x1, "
-             "skip fusion, SE-over-BN and x2 resize kernels bf16 I/O with fp32 statistics / "
-             "accumulation; other HIP kernels (guide conv3x3, DDRNet resizes, loss) fp32")
+AMP_DTYPE = ("bf16 autocast: 16->16 / 32->32 3x3 convs on the HIP bf16 MFMA kernels (fp32 "
+             "accumulation), other convs / GEMMs bf16 (MIOpen / hipBLASLt); HIP BatchNorm, "
+             "BN-ReLU-1x1, skip fusion, SE-over-BN and x2 resize kernels bf16 I/O with fp32 "
+             "statistics / accumulation; other HIP kernels (guide conv3x3, DDRNet resizes, loss) fp32")
 
 
 def parse():

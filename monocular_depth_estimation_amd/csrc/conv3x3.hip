@@ -553,6 +553,251 @@ __global__ void __launch_bounds__(256)
 
 constexpr int kReduceSplit = 32;
 
+// ------------------------------------------- wide-channel weight gradient
+// DDRNet's 64 / 128 / 256-channel 3x3 / stride-1 convs (the BasicBlocks of
+// src/GuideDepth/model/DDRNet_23_slim.py:41-72, at cfg2 60x80, 30x40, 15x20),
+// whose weight gradient MIOpen runs as NHWC implicit GEMM behind
+// NCHW <-> NHWC transposes.  Here in NCHW, no transposes:
+//   gW[co][ci][tap] = sum over pixels p of gy[co][p] * x[ci][p + tap offset].
+// Block groups (blockIdx.y) own 64 output x 32 input channels; a group's
+// blocks (blockIdx.x) split the pixel tiles (split-K) -- a tile is `th` rows
+// x `wc` columns (K = th * wc <= 192 pixels).  x rows r0-1 .. r0+th are staged
+// with a zero border at pitch wc + 2, so tap (dy, dx) of pixel p is the
+// constant offset dy * (wc + 2) + dx from p's base address (a per-tile
+// pixel -> base table in LDS); gy rows r0 .. r0+th-1 are staged at pitch K.
+// MFMA (v_mfma_f32_16x16x4_f32): M = output channels (wave w: the 16-channel
+// tile w), N = (tap, input channel) = 18 tiles of 16, K = 4 pixels per step:
+// per step a lane reads its pixel base, one gy value and 18 x values
+// (conflict-free: both plane pitches = 2 mod 32) for 18 MFMAs.  The next
+// tile's operands are loaded into registers while the current one is
+// multiplied.  Block partials -> fixed-order two-stage reduction.
+constexpr int kWCI = 32, kWCO = 64;
+constexpr int kWNT = 9 * kWCI / 16;      // 18 N tiles: nt = 2 * tap + channel half
+constexpr int kWPX = 386;                // x plane pitch: >= (th + 2)(wc + 2), = 2 mod 32
+constexpr int kWPG = 194;                // gy plane pitch: >= K rounded to 4, = 2 mod 32
+constexpr int kWK = 192;                 // pixels per tile, at most
+constexpr int kWXL = (kWPX + 63) / 64;   // x loads per channel and lane (7)
+constexpr int kWGL = kWK / 64;           // gy loads per channel and lane (3)
+constexpr int kWM = kWCO * 9 * kWCI;     // partial elements per group: [co 64][tap 9][ci 32]
+
+struct WideGeo {
+  int th, wc, tiles_w, tiles_per_img, ntiles;
+};
+
+// th x wc tiles: whole rows when w <= 126, else 64-column strips
+inline bool wide_geo(int64_t n, int64_t h, int64_t w, WideGeo* g) {
+  const int wc = w <= 126 ? (int)w : 64;
+  int th = kWK / wc;
+  const int thx = kWPX / (wc + 2) - 2;
+  if (thx < th) th = thx;
+  if (th > (int)h) th = (int)h;
+  if (th < 1) return false;
+  g->th = th;
+  g->wc = wc;
+  g->tiles_w = (int)mde::cdiv(w, wc);
+  const int64_t tpi = mde::cdiv(h, th) * g->tiles_w;
+  const int64_t nt = n * tpi;
+  if (tpi > 0x7fffffff || nt > 0x7fffffff) return false;
+  g->tiles_per_img = (int)tpi;
+  g->ntiles = (int)nt;
+  return true;
+}
+
+__global__ void __launch_bounds__(256, 1)
+    conv3x3_wgrad_wide_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                              float* __restrict__ part, int ci_n, int co_n, int h, int w,
+                              WideGeo g) {
+  __shared__ float sx[kWCI * kWPX];
+  __shared__ float sg[kWCO * kWPG];
+  __shared__ int tab[kWK];
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ngo = co_n / kWCO;
+  const int cog = blockIdx.y % ngo, cig = blockIdx.y / ngo;
+  const int wc = g.wc, th = g.th, W2 = wc + 2, K = th * wc, KP = (K + 3) & ~3;
+  const int XE = (th + 2) * W2;
+  const int hw = h * w;
+  for (int p = tid; p < KP; p += 256) tab[p] = p < K ? (p / wc) * W2 + p % wc : 0;
+  for (int e = tid; e < kWCO * (KP - K); e += 256) {
+    const int c = e / (KP - K);
+    sg[c * kWPG + K + e % (KP - K)] = 0.f;  // K padding: gy = 0 (never rewritten)
+  }
+  // tile-invariant staging geometry of this lane: x element e = lane + 64 i of
+  // a channel's staged plane is tile row rr, staged column cc (image column
+  // c0 + cc - 1); gy element p = lane + 64 i is tile row p / wc, column p % wc
+  int xrel[kWXL], xrr[kWXL], xcc[kWXL];
+#pragma unroll
+  for (int i = 0; i < kWXL; ++i) {
+    const int e = lane + 64 * i;
+    const int rr = e / W2, cc = e - rr * W2;
+    xrr[i] = e < XE ? rr : -4096;  // out of the plane: never in range
+    xcc[i] = cc;
+    xrel[i] = (rr - 1) * w + cc - 1;
+  }
+  int grel[kWGL], gcol[kWGL], grow[kWGL];
+#pragma unroll
+  for (int i = 0; i < kWGL; ++i) {
+    const int p = lane + 64 * i;
+    grow[i] = p < K ? p / wc : -4096;
+    gcol[i] = p % wc;
+    grel[i] = (p / wc) * w + p % wc;
+  }
+  int boff[kWNT];
+#pragma unroll
+  for (int nt = 0; nt < kWNT; ++nt) {
+    const int tap = nt >> 1;
+    boff[nt] = (16 * (nt & 1) + li) * kWPX + (tap / 3) * W2 + tap % 3;
+  }
+  const int aoff = (16 * wv + li) * kWPG + lk;
+
+  f4 acc[kWNT];
+#pragma unroll
+  for (int nt = 0; nt < kWNT; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // this wave stages x channels 8 wv .. 8 wv + 7 and gy channels 16 wv .. 16 wv + 15
+  const float* xg = x + ((int64_t)cig * kWCI + 8 * wv) * hw;
+  const float* gg = gy + ((int64_t)cog * kWCO + 16 * wv) * hw;
+  // in-range flags are applied at store time, so nothing waits on a load
+  // before the next tile's LDS stores
+  float vx[8][kWXL], vg[16][kWGL];
+  unsigned xm = 0, gm = 0;
+  auto load = [&](int tile) {
+    const int img = tile / g.tiles_per_img, t = tile - img * g.tiles_per_img;
+    const int r0 = (t / g.tiles_w) * th, c0 = (t % g.tiles_w) * wc;
+    const float* xi = xg + (int64_t)img * ci_n * hw;
+    const float* gi = gg + (int64_t)img * co_n * hw;
+    const int tb = r0 * w + c0;
+    xm = 0;
+#pragma unroll
+    for (int i = 0; i < kWXL; ++i) {
+      const int gr = r0 - 1 + xrr[i], gc = c0 - 1 + xcc[i];
+      const bool ok = gr >= 0 && gr < h && gc >= 0 && gc < w;  // a strip's halo columns are real
+      xm |= ok ? 1u << i : 0u;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) vx[c][i] = xi[ok ? (unsigned)(c * hw + tb + xrel[i]) : 0u];
+    }
+    gm = 0;
+#pragma unroll
+    for (int i = 0; i < kWGL; ++i) {
+      const bool ok = grow[i] >= 0 && r0 + grow[i] < h && c0 + gcol[i] < w;
+      gm |= ok ? 1u << i : 0u;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) vg[c][i] = gi[ok ? (unsigned)(c * hw + tb + grel[i]) : 0u];
+    }
+  };
+  int tile = blockIdx.x;
+  if (tile < g.ntiles) load(tile);
+  for (; tile < g.ntiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's operands are consumed
+#pragma unroll
+    for (int i = 0; i < kWXL; ++i) {
+      const int e = lane + 64 * i;
+      if (e < XE) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) sx[(8 * wv + c) * kWPX + e] = (xm >> i) & 1u ? vx[c][i] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kWGL; ++i) {
+      const int p = lane + 64 * i;
+      if (p < K) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) sg[(16 * wv + c) * kWPG + p] = (gm >> i) & 1u ? vg[c][i] : 0.f;
+      }
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < g.ntiles) load(tile + gridDim.x);
+#pragma unroll 2
+    for (int s = 0; s < KP / 4; ++s) {
+      const int t = tab[4 * s + lk];
+      const float a = sg[aoff + 4 * s];
+#pragma unroll
+      for (int nt = 0; nt < kWNT; ++nt) acc[nt] = mfma4(a, sx[boff[nt] + t], acc[nt]);
+    }
+  }
+  // lane: co = 16 wv + 4 lk + i, n = 16 nt + li = 32 tap + ci
+  float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWM;
+#pragma unroll
+  for (int nt = 0; nt < kWNT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(16 * wv + 4 * lk + i) * (9 * kWCI) + 16 * nt + li] = acc[nt][i];
+}
+
+// Stage 1 per group (blockIdx.z): part [group][G][kWM] -> part2 [group][S][kWM].
+__global__ void __launch_bounds__(256)
+    wgrad_wide_reduce1_kernel(const float* __restrict__ part, float* __restrict__ part2, int g) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kWM) return;
+  const int s = blockIdx.y, ns = gridDim.y;
+  const float* pg = part + (int64_t)blockIdx.z * g * kWM;
+  float a0 = 0.f, a1 = 0.f;
+  int b = s;
+  for (; b + ns < g; b += 2 * ns) {
+    a0 += pg[(int64_t)b * kWM + e];
+    a1 += pg[(int64_t)(b + ns) * kWM + e];
+  }
+  if (b < g) a0 += pg[(int64_t)b * kWM + e];
+  part2[((int64_t)blockIdx.z * ns + s) * kWM + e] = a0 + a1;
+}
+
+// Stage 2 per group (blockIdx.y): sum the S slices, scatter to gw[co][ci][tap].
+__global__ void __launch_bounds__(256)
+    wgrad_wide_reduce2_kernel(const float* __restrict__ part2, float* __restrict__ gw, int ns,
+                              int ci_n, int co_n) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= kWM) return;
+  const int grp = blockIdx.y, ngo = co_n / kWCO;
+  const float* p2 = part2 + (int64_t)grp * ns * kWM;
+  float s = 0.f;
+  for (int k = 0; k < ns; ++k) s += p2[(int64_t)k * kWM + e];
+  const int col = e / (9 * kWCI), n = e % (9 * kWCI);
+  const int co = (grp % ngo) * kWCO + col, ci = (grp / ngo) * kWCI + n % kWCI;
+  gw[((int64_t)co * ci_n + ci) * 9 + n / kWCI] = s;
+}
+
+constexpr int kWideBlocks = 256;  // one 100 KB-LDS block per CU
+
+struct WidePlan {
+  WideGeo g;
+  int groups, gx, split;
+};
+
+inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WidePlan* p) {
+  if (ci % kWCI || co % kWCO || ci < kWCI || co < kWCO) return false;
+  if (!wide_geo(n, h, w, &p->g)) return false;
+  p->groups = (int)((ci / kWCI) * (co / kWCO));
+  int gx = kWideBlocks / p->groups;
+  if (gx < 1) gx = 1;
+  if (gx > p->g.ntiles) gx = p->g.ntiles;
+  p->gx = gx;
+  p->split = gx < kReduceSplit ? gx : kReduceSplit;
+  return true;
+}
+
+inline size_t wide_workspace(const WidePlan& p) {
+  return sizeof(float) * (size_t)p.groups * ((size_t)p.gx + (size_t)p.split) * kWM;
+}
+
+int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int64_t ci,
+                      int64_t co, int64_t h, int64_t w, float* ws, hipStream_t s) {
+  WidePlan p;
+  if (!wide_plan(n, ci, co, h, w, &p)) return MDE_ERR_UNSUPPORTED;
+  const double flops = 2.0 * 9 * ci * co * (double)(n * h * w);
+  const double bytes = 4.0 * n * h * w * (double)(ci + co);
+  float* part = ws;
+  float* part2 = ws + (int64_t)p.groups * p.gx * kWM;
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, conv3x3_wgrad_wide_kernel,
+                  dim3(p.gx, p.groups), dim3(256), 0, x, gy, part, (int)ci, (int)co, (int)h,
+                  (int)w, p.g);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.groups * p.gx * kWM, s, wgrad_wide_reduce1_kernel,
+             dim3((unsigned)mde::cdiv(kWM, 256), p.split, p.groups), dim3(256), 0, part, part2,
+             p.gx);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.groups * p.split * kWM, s, wgrad_wide_reduce2_kernel,
+             dim3((unsigned)mde::cdiv(kWM, 256), p.groups), dim3(256), 0, part2, gw, p.split,
+             (int)ci, (int)co);
+  return MDE_OK;
+}
+
 // ====================================================================== bf16
 // bf16 activations / gradients on v_mfma_f32_16x16x32_bf16 (bf16 products,
 // fp32 accumulation), for the autocast step (BASELINE cfg3): the same three
@@ -1154,7 +1399,14 @@ bool bf_supported(int64_t cin, int64_t cout) {
 
 // Supported (cin, cout) per pass.  Forward: the guide convs (3 -> 16/32/64),
 // 16 -> 16 and 32 -> 32; data gradient: 16 -> 16 and 32 -> 32 (the guide
-// convs read the image, which needs no gradient); weight gradient: all.
+// convs read the image, which needs no gradient); weight gradient: those and
+// the wide-channel shapes.
+// Wide channels (cin % 32 == 0, cout % 64 == 0; DDRNet's 64 / 128 / 256):
+// weight gradient only.
+bool wide(int64_t cin, int64_t cout) {
+  return cin > 0 && cout > 0 && cin % kWCI == 0 && cout % kWCO == 0;
+}
+
 bool supported(int64_t cin, int64_t cout, int pass) {
   const bool guide = cin == 3 && (cout == 16 || cout == 32 || cout == 64);
   const bool square = (cin == 16 && cout == 16) || (cin == 32 && cout == 32);
@@ -1164,7 +1416,7 @@ bool supported(int64_t cin, int64_t cout, int pass) {
     case kDgrad:
       return square;
     case kWgrad:
-      return guide || square;
+      return guide || square || wide(cin, cout);
     default:
       return false;
   }
@@ -1313,6 +1565,10 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
     return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
   }
   if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
+  if (wide(cin, cout)) {
+    WidePlan wp;
+    return wide_plan(n, cin, cout, h, w, &wp) ? wide_workspace(wp) : 0;
+  }
   if (cin == 3 && cout == 16) p = wgrad_plan<3, 16, 8, 4>(n, h, w);
   else if (cin == 3 && cout == 32) p = wgrad_plan<3, 32, 8, 4>(n, h, w);
   else if (cin == 3) p = wgrad_plan<3, 64, 4, 4>(n, h, w);
@@ -1349,6 +1605,7 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   const float* g = (const float*)gy;
   float* ws = (float*)workspace;
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  if (wide(cin, cout)) return launch_wgrad_wide(xi, g, gweight, n, cin, cout, h, w, ws, s);
   if (cin == 3 && cout == 16) return launch_wgrad<3, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3 && cout == 32) return launch_wgrad<3, 32, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3) return launch_wgrad<3, 64, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);

@@ -28,6 +28,8 @@
 // mode is a plain streaming reduction / elementwise pass.
 #include <cmath>
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -330,6 +332,16 @@ __device__ __forceinline__ float lnext(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
+// base[i] through a 32-bit BYTE offset (i < 2^30, checked on the host): with a
+// wave-uniform base the access is one VGPR offset on an SGPR pair, no 64-bit
+// address arithmetic per load / store
+__device__ __forceinline__ float ldo(const float* base, unsigned i) {
+  return *reinterpret_cast<const float*>(reinterpret_cast<const char*>(base) + (i << 2));
+}
+__device__ __forceinline__ void sto(float* base, unsigned i, float v) {
+  *reinterpret_cast<float*>(reinterpret_cast<char*>(base) + (i << 2)) = v;
+}
+
 // symmetric 11-tap window: c = g[5], k[i] = g[5 - 1 - i] = g[5 + 1 + i]
 struct Sym11 {
   float c, k[5];
@@ -358,11 +370,19 @@ struct StreamGeo {
 StreamGeo stream_geometry(int64_t b, int64_t h, int64_t w) {
   StreamGeo g;
   g.strips = (int)mde::cdiv(w, kSD);
-  // enough waves to fill 256 CUs x 4 SIMDs ~4 deep; >= 32 rows per chunk
-  // (a chunk re-reads 10 halo rows)
-  const int64_t want = mde::cdiv(4096, b * g.strips);
+  // ~3 waves per SIMD (measured at 32x480x640: 3072 waves 154.8 us fwd+bwd,
+  // 4096 160.2, 6144 164.4); >= 34 rows per chunk (a
+  // chunk re-reads 10 halo rows), = 1 (mod 11) so that a chunk streams whole
+  // 11-row ring periods (rows + 10 = 0 mod 11): the unrolled period then has
+  // no per-row trip guard (only an image's last chunk runs past its rows)
+  static const int64_t target = [] {  // MDE_DL_WAVES: tuning sweeps (tools/kbench.py)
+    const char* e = std::getenv("MDE_DL_WAVES");
+    return e ? std::atoll(e) : 3072;
+  }();
+  const int64_t want = mde::cdiv(target, b * g.strips);
   int64_t rows = mde::cdiv(h, want < 1 ? 1 : want);
-  if (rows < 32) rows = 32;
+  if (rows < 34) rows = 34;
+  rows = (rows + 9) / 11 * 11 + 1;  // next value = 1 (mod 11)
   if (rows > h) rows = h;
   g.chunk_rows = (int)rows;
   g.chunks = (int)mde::cdiv(h, rows);
@@ -393,7 +413,7 @@ __global__ void __launch_bounds__(256)
   const int cc = c < 0 ? 0 : (c >= w ? w - 1 : c);
   const int r0 = chunk * chunk_rows;
   const int r1 = r0 + chunk_rows < h ? r0 + chunk_rows : h;
-  // per-image bases (wave-uniform) + 32-bit element offsets (planes < 2^31)
+  // per-image bases (wave-uniform) + 32-bit byte offsets (planes < 2^30)
   const float* Xi = X + img * (int64_t)h * w;
   const float* Yi = Y + img * (int64_t)h * w;
   const int T = (r1 - r0) + 10;  // rows streamed
@@ -407,41 +427,46 @@ __global__ void __launch_bounds__(256)
     r4[j] = 0.f;
   }
   float ssum = 0.f, l1 = 0.f, gr = 0.f, cnt = 0.f;
-  // prefetched row r0 - 5
+  float xp = 0.f, yp = 0.f;  // row r - 1
+  // prefetched raw row (clamped address) and its in-range flag: the select
+  // happens when the row is consumed, one iteration after the load is issued
   float xn, yn;
+  bool okn;
   {
     const int r = r0 - 5;
     const int rc = r < 0 ? 0 : r;
-    const bool ok = cin && r >= 0;
-    const float xv = Xi[(unsigned)(rc * w + cc)], yv = Yi[(unsigned)(rc * w + cc)];
-    xn = ok ? xv : 0.f;
-    yn = ok ? yv : 0.f;
+    okn = cin && r >= 0;
+    xn = ldo(Xi, (unsigned)(rc * w + cc));
+    yn = ldo(Yi, (unsigned)(rc * w + cc));
   }
+  // whole 11-row periods (T = 0 mod 11 except in an image's last chunk,
+  // whose extra rows are past r1 + 4: no output, clamped loads)
   for (int t0 = 0; t0 < T; t0 += 11) {
 #pragma unroll
     for (int j = 0; j < 11; ++j) {
       const int t = t0 + j;
-      if (t < T) {
+      {
       const int r = r0 - 5 + t;
-      const float x = xn, y = yn;
+      const float x = okn ? xn : 0.f, y = okn ? yn : 0.f;
       {  // prefetch row r + 1
         const int rn = r + 1;
         const int rc = rn < 0 ? 0 : (rn >= h ? h - 1 : rn);
-        const bool ok = cin && rn >= 0 && rn < h;
-        const float xv = Xi[(unsigned)(rc * w + cc)], yv = Yi[(unsigned)(rc * w + cc)];
-        xn = ok ? xv : 0.f;
-        yn = ok ? yv : 0.f;
+        okn = cin && rn >= 0 && rn < h;
+        xn = ldo(Xi, (unsigned)(rc * w + cc));
+        yn = ldo(Yi, (unsigned)(rc * w + cc));
       }
-      // image-domain terms of row r (L1, forward differences; xn/yn = row r + 1)
+      // image-domain terms: L1 and the horizontal difference of row r, the
+      // vertical difference of row r - 1 (so the row r + 1 load just issued
+      // is first needed one iteration later)
       if (r >= r0 && r < r1 && outl) {
         l1 += fabsf(x - y);
         cnt += 1.f;
       }
       const float xr = lnext(x), yr = lnext(y);
-      if (r >= r0 && r < r1 && outl) {
-        if (c < w - 1) gr += fabsf((yr - y) - (xr - x));
-        if (r < h - 1) gr += fabsf((yn - y) - (xn - x));
-      }
+      if (r >= r0 && r < r1 && outl && c < w - 1) gr += fabsf((yr - y) - (xr - x));
+      if (r - 1 >= r0 && r - 1 < r1 && outl && r < h) gr += fabsf((y - yp) - (x - xp));
+      xp = x;
+      yp = y;
       if (SSIM) {
         // horizontal 11-tap pass over (x, y): neighbours by DPP shifts, the
         // five statistics as two packed pairs and one scalar
@@ -461,7 +486,7 @@ __global__ void __launch_bounds__(256)
         r01[j] = h01;
         r23[j] = h23;
         r4[j] = h4;
-        if (t >= 10) {  // map row p = r - 5: ring slot of row p + k - 5 is (j + 1 + k) % 11
+        if (t >= 10 && r - 5 < r1) {  // map row p = r - 5: ring slot of row p + k - 5 is (j + 1 + k) % 11
           const int p = r - 5;
           v2 q01 = g.c * r01[(j + 6) % 11];
           v2 q23 = g.c * r23[(j + 6) % 11];
@@ -490,9 +515,9 @@ __global__ void __launch_bounds__(256)
               const float dS_dmx = 2.f * my * n2 * iD - S * 2.f * mx * (d2 * iD);
               float* co = coef + img * (int64_t)h * w;
               const unsigned off = (unsigned)(p * w + c);
-              co[off] = dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy;
-              co[plane + off] = dS_dsx;
-              co[2 * plane + off] = dS_dsxy;
+              sto(co, off, dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy);
+              sto(co + plane, off, dS_dsx);
+              sto(co + 2 * plane, off, dS_dsxy);
             }
           }
         }
@@ -557,44 +582,63 @@ __global__ void __launch_bounds__(256)
     rab[j] = v2{0.f, 0.f};
     rcr[j] = 0.f;
   }
-  // raw rows q (x0, y0) and q + 1 (x1, y1) of the next output q; ey_prev =
-  // forward row difference of row q - 1
-  float an = 0.f, bn = 0.f, cn = 0.f;
-  auto load_coef = [&](int p, float& a, float& b, float& cv) {
+  // Loads use clamped addresses; their in-range flags are applied when the
+  // row is consumed (one iteration after the load is issued), so no select
+  // makes the wave wait for a load right after issuing it.
+  auto load_coef = [&](int p, float& a, float& b, float& cv, bool& ok) {
     const int pc = p < 0 ? 0 : (p >= h ? h - 1 : p);
-    const bool ok = cin && p >= 0 && p < h;
+    ok = cin && p >= 0 && p < h;
     const unsigned o = (unsigned)(pc * w + cc);
-    const float av = Ai[o], bv = Ai[plane + o], cvv = Ai[2 * plane + o];
-    a = ok ? av : 0.f;
-    b = ok ? bv : 0.f;
-    cv = ok ? cvv : 0.f;
+    a = ldo(Ai, o);
+    b = ldo(Ai + plane, o);
+    cv = ldo(Ai + 2 * plane, o);
   };
-  auto load_raw = [&](int r, float& x, float& y) {
+  auto load_raw = [&](int r, float& x, float& y, bool& ok) {
     const int rc = r < 0 ? 0 : (r >= h ? h - 1 : r);
-    const bool ok = cin && r >= 0 && r < h;
-    const float xv = Xi[(unsigned)(rc * w + cc)], yv = Yi[(unsigned)(rc * w + cc)];
-    x = ok ? xv : 0.f;
-    y = ok ? yv : 0.f;
+    ok = cin && r >= 0 && r < h;
+    x = ldo(Xi, (unsigned)(rc * w + cc));
+    y = ldo(Yi, (unsigned)(rc * w + cc));
   };
-  if (SSIM) load_coef(r0 - 5, an, bn, cn);
-  float x0, y0, x1, y1;
-  load_raw(r0, x0, y0);
-  load_raw(r0 + 1, x1, y1);
+  // coefficient rows p (an.., oka) and p + 1 (an2.., oka2) in flight
+  float an = 0.f, bn = 0.f, cn = 0.f, an2 = 0.f, bn2 = 0.f, cn2 = 0.f;
+  bool oka = false, oka2 = false;
+  if (SSIM) {
+    load_coef(r0 - 5, an, bn, cn, oka);
+    load_coef(r0 - 4, an2, bn2, cn2, oka2);
+  }
+  // raw rows q (x0, y0) and q + 1 (x1, y1) of the next output q, row q + 2
+  // in flight (x2, y2, ok2); eyp = forward row difference of row q - 1
+  float x0, y0, x1, y1, x2, y2;
+  bool ok0, ok1, ok2;
+  load_raw(r0, x0, y0, ok0);
+  load_raw(r0 + 1, x1, y1, ok1);
+  load_raw(r0 + 2, x2, y2, ok2);
+  x0 = ok0 ? x0 : 0.f;
+  y0 = ok0 ? y0 : 0.f;
+  x1 = ok1 ? x1 : 0.f;
+  y1 = ok1 ? y1 : 0.f;
   float eyp = 0.f;  // e_y of row r0 - 1 (only used when r0 >= 1)
   if (GRAD && r0 >= 1) {
     float xm, ym;
-    load_raw(r0 - 1, xm, ym);
-    eyp = (y0 - ym) - (x0 - xm);
+    bool okm;
+    load_raw(r0 - 1, xm, ym, okm);
+    eyp = (y0 - (okm ? ym : 0.f)) - (x0 - (okm ? xm : 0.f));
   }
+  // whole 11-row periods (see stream_geometry); rows past r1 + 4 in an
+  // image's last chunk produce no output
   for (int t0 = 0; t0 < T; t0 += 11) {
 #pragma unroll
     for (int j = 0; j < 11; ++j) {
       const int t = t0 + j;
-      if (t < T) {
+      {
       if (SSIM) {
-        const v2 ab = v2{an, bn};
-        const float cv = cn;
-        if (t + 1 < T) load_coef(r0 - 4 + t, an, bn, cn);
+        const v2 ab = oka ? v2{an, bn} : v2{0.f, 0.f};
+        const float cv = oka ? cn : 0.f;
+        an = an2;
+        bn = bn2;
+        cn = cn2;
+        oka = oka2;
+        load_coef(r0 - 3 + t, an2, bn2, cn2, oka2);
         v2 l = ab, rr = ab;
         float lc = cv, rc = cv;
         v2 hab = g.c * ab;
@@ -625,8 +669,9 @@ __global__ void __launch_bounds__(256)
           }
           gsum += kfac * (fab.x + 2.f * x0 * fab.y + y0 * fc);
         }
-        float x2 = 0.f, y2 = 0.f;
-        if (t + 1 < T) load_raw(q + 2, x2, y2);
+        float x3, y3;
+        bool ok3;
+        load_raw(q + 3, x3, y3, ok3);
         if (GRAD) {
           // e = gt_d - p_d (forward differences); dL/dp(j) = kg * (sgn e(j) - sgn e(j-1))
           const float xr = lnext(x0), yr = lnext(y0);
@@ -639,11 +684,14 @@ __global__ void __launch_bounds__(256)
           gsum += kg * ((sx - (c >= 1 ? sxp : 0.f)) + (sy - syp));
           eyp = ey;
         }
-        if (outl && q < r1) gx[base + (unsigned)(q * w + c)] = gsum;
+        if (outl && q < r1) sto(gx + base, (unsigned)(q * w + c), gsum);
         x0 = x1;
         y0 = y1;
-        x1 = x2;
-        y1 = y2;
+        x1 = ok2 ? x2 : 0.f;
+        y1 = ok2 ? y2 : 0.f;
+        x2 = x3;
+        y2 = y3;
+        ok2 = ok3;
       }
       }
     }
@@ -777,7 +825,7 @@ int mde_depth_loss_fwd(const void* pred, const void* gt, float alpha,
     nparts = masked_blocks(b * h * w);
     MDE_LAUNCH(mde::K_DLOSS_FWD, 8.0 * numel, s, dloss_masked_kernel, dim3(nparts), dim3(256),
                0, (const float*)pred, (const float*)gt, b * h * w, part);
-  } else if (win.k == KMAX && h * w < ((int64_t)1 << 31)) {
+  } else if (win.k == KMAX && h * w < ((int64_t)1 << 30)) {
     const StreamGeo sg = stream_geometry(b, h, w);
     nparts = (int)sg.nwaves;
     float* coef = (float*)((char*)workspace + coef_offset(b, h, w));
@@ -833,7 +881,7 @@ int mde_depth_loss_bwd(const void* pred, const void* gt, float alpha,
                (const float*)gt, b * h * w, fwd_out, gout, (float*)grad_pred);
     return MDE_OK;
   }
-  if (win.k == KMAX && h * w < ((int64_t)1 << 31)) {  // coefficients left by the forward
+  if (win.k == KMAX && h * w < ((int64_t)1 << 30)) {  // coefficients left by the forward
     const StreamGeo sg = stream_geometry(b, h, w);
     const unsigned blocks = (unsigned)mde::cdiv(sg.nwaves, 4);
     const float inv_n = (float)(1.0 / numel);

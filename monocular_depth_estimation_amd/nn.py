@@ -372,6 +372,9 @@ def pointwise_ok(conv: nn.Conv2d, x) -> bool:
 # (mde_conv3x3_*), per (cin, cout): (forward, data gradient, weight gradient).
 # The rest go to MIOpen, whose Winograd kernels are faster at >= 32 channels
 # (tools/kbench.py --only conv: HIP vs MIOpen per pass at the bench shapes).
+# DDRNet's 64/128/256-channel weight gradients stay on MIOpen for now: the
+# NCHW wide-channel kernel (mde_conv3x3_wgrad, cin % 32 == 0, cout % 64 == 0)
+# is exact but measured slower (tools/wgrad_bench.py: 57 vs 69-83 TF/s).
 CONV3X3_HIP = {
     (3, 16): (True, True, True),
     (3, 32): (True, True, True),

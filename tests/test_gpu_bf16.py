@@ -87,14 +87,15 @@ def _compare(build_truth, build_ours, build_cpu, x, d, what, skip=""):
 def test_guidedepth_bf16_golden_vs_float64_oracle(golden):
     """Golden 2x3x64x96 step: map, loss and the DECODER's gradient norms.
 
-    The encoder's gradient norms are ill-conditioned at this shape (DAPPM's
-    pooled branches reach train-mode BatchNorm with a handful of values per
-    channel): the fp32 HIP step with the input perturbed by half a bf16 ulp
-    moves their median error vs float64 from 0.001 to 0.06-0.58 while the
-    decoder's stays at 0.07-0.09 (profiles/r03_bf16_grad_conditioning.txt,
-    tools/grad_conditioning.py), so any bf16 rounding difference lands
-    anywhere in that range.  The whole-model gradient check is the 240x320
-    case below."""
+    The encoder's gradient norms are ill-conditioned at batch 2 (DAPPM's
+    pooled branches reach train-mode BatchNorm with two values per channel at
+    1x1): the fp32 HIP step with its input perturbed by about one bf16
+    rounding (+-2^-9 relative) moves the encoder's median gradient-norm
+    difference by 0.07-2.5 while the decoder's stays at 0.04-0.06
+    (profiles/r03_bf16_grad_conditioning.txt, tools/grad_conditioning.py),
+    so any bf16 rounding difference lands anywhere in that range.  The
+    whole-model gradient check is the batch-8 case below, where the same
+    perturbation moves the encoder by 0.01."""
     from monocular_depth_estimation_amd import GuideDepth
     g = golden("golden_guidedepth.npz")
     _compare(lambda: fill_(og.GuideDepth()), lambda: fill_(GuideDepth(pretrained=False)),
@@ -103,11 +104,14 @@ def test_guidedepth_bf16_golden_vs_float64_oracle(golden):
 
 
 def test_guidedepth_bf16_240x320_vs_float64_oracle():
+    """Whole model (encoder included) at batch 8, 240x320: well-conditioned
+    (input perturbation of one bf16 rounding moves gradient norms by a median
+    0.01, p90 0.05-0.07; profiles/r03_bf16_grad_conditioning.txt)."""
     from monocular_depth_estimation_amd import GuideDepth
-    x = torch.from_numpy(seeded((2, 3, 240, 320), 71, 0, 1))
-    d = torch.from_numpy(seeded((2, 1, 240, 320), 72, 0.1, 10.0))
+    x = torch.from_numpy(seeded((8, 3, 240, 320), 71, 0, 1))
+    d = torch.from_numpy(seeded((8, 1, 240, 320), 72, 0.1, 10.0))
     _compare(lambda: fill_(og.GuideDepth()), lambda: fill_(GuideDepth(pretrained=False)),
-             lambda: fill_(og.GuideDepth()), x, d, "GuideDepth bf16 240x320")
+             lambda: fill_(og.GuideDepth()), x, d, "GuideDepth bf16 8x240x320")
 
 
 def test_ptmodel_bf16_vs_float64_oracle():

@@ -87,6 +87,39 @@ def test_conv3x3_full_size_vs_miopen(cin, cout, h, w):
         assert rel_err(xh.grad, xm.grad) <= 2e-5
 
 
+# Wide channels (DDRNet 64/128/256): weight gradient only; (n, h, w) cover
+# whole-row tiles at the cfg2 widths, a ragged last row tile, w > 126 (64-column
+# strips with a ragged last strip), one row, and a non-square channel pair.
+WIDE = [(64, 64, 2, 60, 80), (128, 128, 2, 30, 40), (256, 256, 2, 15, 20),
+        (64, 64, 1, 7, 130), (64, 64, 3, 1, 5), (32, 128, 1, 9, 21), (64, 64, 1, 33, 200)]
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", WIDE)
+def test_conv3x3_wide_wgrad_vs_float64_oracle(cin, cout, n, h, w):
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import conv3x3
+    x, wt, gy = _case(cin, cout, n, h, w, 7 * cin + cout + h)
+    xr = x.double()
+    wr = wt.double().requires_grad_(True)
+    torch.nn.functional.conv2d(xr, wr, None, 1, 1).backward(gy.double())
+    passes = tuple(bool(_abi.query("mde_conv3x3_supported", cin, cout, i, 0)) for i in range(3))
+    assert passes == (False, False, True)
+    wg = wt.to(DEV).requires_grad_(True)
+    conv3x3(x.to(DEV), wg, passes).backward(gy.to(DEV))
+    assert rel_err(wg.grad, wr.grad) <= 2e-5
+
+
+def test_conv3x3_wide_wgrad_deterministic():
+    from monocular_depth_estimation_amd.nn import conv3x3
+    x, wt, gy = _case(128, 128, 4, 30, 40, 9)
+    outs = []
+    for _ in range(2):
+        wg = wt.to(DEV).requires_grad_(True)
+        conv3x3(x.to(DEV), wg, (False, False, True)).backward(gy.to(DEV))
+        outs.append(wg.grad.cpu())
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv3x3_deterministic():
     from monocular_depth_estimation_amd.nn import conv3x3
     x, wt, gy = _case(16, 16, 2, 50, 90, 3)

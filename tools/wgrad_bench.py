@@ -1,0 +1,41 @@
+"""Weight gradient of DDRNet's wide 3x3 convs at cfg2 (bs 32): the NCHW HIP
+wide-channel kernel (mde_conv3x3_wgrad, incl. its reduction) vs MIOpen's
+(aten.convolution_backward, NCHW tensors: incl. its layout transposes)."""
+import sys, os
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from monocular_depth_estimation_amd import _abi
+from monocular_depth_estimation_amd.nn import _ws
+
+
+def timeit(fn, reps=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e3
+
+
+for (n, c, h, w) in [(32, 64, 60, 80), (32, 128, 30, 40), (32, 256, 15, 20), (4, 64, 30, 40)]:
+    x = torch.rand((n, c, h, w), device="cuda") - 0.5
+    gy = torch.rand((n, c, h, w), device="cuda") - 0.5
+    wt = torch.rand((c, c, 3, 3), device="cuda")
+    gw = torch.empty_like(wt)
+    ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, c, c, h, w, 0), x)
+    st = _abi.stream_of(x)
+    hip = lambda: _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, c, c,
+                            h, w, _abi.ptr(ws), 0, st)
+    mio = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (1, 1), (1, 1), False,
+                                                      (0, 0), 1, (False, True, False))
+    th, tm = timeit(hip), timeit(mio)
+    hip()
+    ref = mio()[1]
+    err = float((gw - ref).abs().max() / ref.abs().max())
+    fl = 2.0 * 9 * c * c * n * h * w
+    print(f"wgrad {c}->{c} {n}x{h}x{w}: HIP {th:7.1f} us ({fl / th / 1e6:5.1f} TF/s)  "
+          f"MIOpen {tm:7.1f} us ({fl / tm / 1e6:5.1f} TF/s)  rel diff {err:.1e}", flush=True)

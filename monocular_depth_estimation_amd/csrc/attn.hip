@@ -260,19 +260,25 @@ __device__ __forceinline__ void key_operands(const Geo& g, const float* __restri
 // S^T column tile by 8 MFMA steps over the head dim, table bias + shift mask,
 // softmax over the keys; padded query columns 0.  16 live score registers
 // (probs_t's whole 4x4 tile holds 64).
+// `qraw`: this lane's 8 head dims of query 16it + l16 (q_row(), loaded one
+// tile ahead by the caller so the load latency overlaps the previous tile).
+template <int WS>
+__device__ __forceinline__ void q_row(const Geo& g, const float* __restrict__ qkrow,
+                                      const float* __restrict__ qkb, int head, const int* tok,
+                                      int it, int lane, float q[8]) {
+  row8(qkrow, 2 * g.c, head * D + 8 * (lane >> 4), tok[16 * it + (lane & 15)], qkb, q);
+}
+
 template <int WS, int it>
-__device__ __forceinline__ void probs_tile(const Geo& g, const float* __restrict__ qkrow,
-                                           const float* __restrict__ qkb, int head,
-                                           const int* tok, const int* lab, const float* tab,
-                                           const float ka[4][8], const int kj[16], int lane,
-                                           f4 s[4]) {
+__device__ __forceinline__ void probs_tile(const Geo& g, const float qraw[8], const int* lab,
+                                           const float* tab, const float ka[4][8],
+                                           const int kj[16], int lane, f4 s[4]) {
   const int l16 = lane & 15, g4 = lane >> 4;
   const int ws = wsize<WS>(g), n = ws * ws, span = 2 * ws - 1;
   {
     float qb[8];
-    row8(qkrow, 2 * g.c, head * D + 8 * g4, tok[16 * it + l16], qkb, qb);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) qb[k] *= g.scale;
+    for (int k = 0; k < 8; ++k) qb[k] = qraw[k] * g.scale;
 #pragma unroll
     for (int jt = 0; jt < 4; ++jt) s[jt] = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -323,19 +329,26 @@ __device__ __forceinline__ void probs_tile(const Geo& g, const float* __restrict
 
 // The backward's P, staged query tile by query tile straight into the LDS
 // tile (the register budget of three waves per SIMD).
-template <int WS>
+template <int WS, typename Pre>
 __device__ __forceinline__ void probs_stage(const Geo& g, const float* __restrict__ qkrow,
                                             const float* __restrict__ qkb, int head,
                                             const int* tok, const int* lab, const float* tab,
-                                            float* T) {
+                                            float* T, Pre&& pre) {
   const int lane = opaque_lane();
   float ka[4][8];
   int kj[16];
   key_operands<WS>(g, qkrow, qkb, head, tok, lab, lane, ka, kj);
+  float qn[8];
+  q_row<WS>(g, qkrow, qkb, head, tok, 0, lane, qn);
   static_for4([&](auto it_c) {
     constexpr int it = decltype(it_c)::value;
+    float qr[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) qr[k] = qn[k];
+    if constexpr (it < 3) q_row<WS>(g, qkrow, qkb, head, tok, it + 1, lane, qn);
+    else pre();  // the next phase's operands, in flight during the last tile
     f4 s[4];
-    probs_tile<WS, it>(g, qkrow, qkb, head, tok, lab, tab, ka, kj, lane, s);
+    probs_tile<WS, it>(g, qr, lab, tab, ka, kj, lane, s);
     static_for4([&](auto jt_c) {
       constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
@@ -387,21 +400,29 @@ __global__ void __launch_bounds__(256, 4)
         vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, g.vb);
     }
   float* orow = out + img * g.c;
+  float qn[8];
+  q_row<WS>(g, qkrow, qkb, head, tok, 0, lane, qn);
   static_for4([&](auto it_c) {
     constexpr int it = decltype(it_c)::value;
     const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;  // per-tile index math
+    float qr[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) qr[k] = qn[k];
+    if constexpr (it < 3) q_row<WS>(g, qkrow, qkb, head, tok, it + 1, lane, qn);
     int kj[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) kj[k] = kjs[16 * (k >> 2) + 4 * g4 + (k & 3)];
     f4 s[4];
-    probs_tile<WS, it>(g, qkrow, qkb, head, tok, lab, tab[w], ka, kj, lane, s);
+    probs_tile<WS, it>(g, qr, lab, tab[w], ka, kj, lane, s);
     f4 o[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+    // keys 16jt + 4g + r; in the compact last tile only r = 0 (key 48) is real
+    static_for4([&](auto jt_c) {
+      constexpr int jt = decltype(jt_c)::value;
 #pragma unroll
-    for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
+      for (int r = 0; r < Tile<WS>::template ksteps<jt>(); ++r)
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt) o[dt] = mfma4(s[jt][r], vb[jt][r][dt], o[dt]);
+    });
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) {
       const int t = tok[16 * it + 4 * g4 + rr];
@@ -462,25 +483,41 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
     // live in T only (not in registers across phases): the register peak is
     // one phase's operands, so the kernel runs two waves per SIMD unspilled.
     if (active) {
-      probs_stage<WS>(g, qkrow, qkb, head, tok, lab, tab[w], T);  // P
+      // Each phase's global operands are loaded one phase ahead (after the
+      // loads the current phase waits on, so its waits do not cover them).
+      // B operands of a product over 16-tiles (t, r): element col of token
+      // tok[16 t + 4 g + r] (padded: the bias when given), scaled.
+      auto tile_elems = [&](float (&b)[4][4][2], const float* base, int ld, int col0,
+                            const float* bias, float scale) {
+        const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int tk = tok[16 * t + 4 * g4 + r];
+#pragma unroll
+            for (int ct = 0; ct < 2; ++ct)
+              b[t][r][ct] = scale * elem(base, ld, col0 + 16 * ct + l16, tk, bias);
+          }
+      };
+      float bdv[4][4][2];  // dV's B = dO[i][c]
+      probs_stage<WS>(g, qkrow, qkb, head, tok, lab, tab[w], T,
+                      [&] { tile_elems(bdv, grow, c, hd, nullptr, 1.f); });  // P
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
+      float va[4][8];  // dP's V rows, in flight during dV
+      {
+        const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+        for (int jt = 0; jt < 4; ++jt)
+          row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], g.vb, va[jt]);
+      }
       // dV = P^T dO
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
-        float b[4][4][2];
-#pragma unroll
-        for (int it = 0; it < 4; ++it)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = tok[16 * it + 4 * g4 + r];
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-              b[it][r][ct] = elem(grow, c, hd + 16 * ct + l16, t, nullptr);
-          }
         static_for4([&](auto jt_c) {
           constexpr int jt = decltype(jt_c)::value;
           f4 o[2];
-          mm_tb_tile<WS, jt>(T, b, o, lane);
+          mm_tb_tile<WS, jt>(T, bdv, o, lane);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * jt + 4 * g4 + rr];
@@ -498,16 +535,18 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dP^T = V dO^T column by column; dS = P (dP - rowsum(P dP)), P read
       // back from T (this lane's own entries) and dS written over it
+      float bq[4][4][2];  // dQ's B = K[j][c], loaded during dS's last tile
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
-        float va[4][8];
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt)
-          row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], g.vb, va[jt]);
+        float dn[8];  // dO row of the next query tile
+        row8(grow, c, hd + 8 * g4, tok[l16], nullptr, dn);
         static_for4([&](auto it_c) {
           constexpr int it = decltype(it_c)::value;
           float db[8];
-          row8(grow, c, hd + 8 * g4, tok[16 * it + l16], nullptr, db);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) db[k] = dn[k];
+          if constexpr (it < 3) row8(grow, c, hd + 8 * g4, tok[16 * (it + 1) + l16], nullptr, dn);
+          else tile_elems(bq, qkrow, c2, c + hd, qkb, 1.f);
           f4 dp[4];
 #pragma unroll
           for (int jt = 0; jt < 4; ++jt) dp[jt] = f4{0.f, 0.f, 0.f, 0.f};
@@ -536,18 +575,11 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dQ = dS K * scale: A = dS[i][j] (this lane's own T entries), B = K[j][c] per lane
+      float bk[4][4][2];  // dK's B = Q[i][c] * scale, in flight during dQ
+      tile_elems(bk, qkrow, c2, hd, qkb, g.scale);
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
-        float b[4][4][2];
-#pragma unroll
-        for (int jt = 0; jt < 4; ++jt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = tok[16 * jt + 4 * g4 + r];
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-              b[jt][r][ct] = elem(qkrow, c2, c + hd + 16 * ct + l16, t, qkb);
-          }
+        const float (&b)[4][4][2] = bq;
         static_for4([&](auto it_c) {
           constexpr int it = decltype(it_c)::value;
           f4 q[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
@@ -575,20 +607,10 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       // dK = dS^T Q * scale (dS from the LDS tile)
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
-        float b[4][4][2];
-#pragma unroll
-        for (int it = 0; it < 4; ++it)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int t = tok[16 * it + 4 * g4 + r];
-#pragma unroll
-            for (int ct = 0; ct < 2; ++ct)
-              b[it][r][ct] = g.scale * elem(qkrow, c2, hd + 16 * ct + l16, t, qkb);
-          }
         static_for4([&](auto jt_c) {
           constexpr int jt = decltype(jt_c)::value;
           f4 o[2];
-          mm_tb_tile<WS, jt>(T, b, o, lane);
+          mm_tb_tile<WS, jt>(T, bk, o, lane);
 #pragma unroll
           for (int rr = 0; rr < 4; ++rr) {
             const int t = tok[16 * jt + 4 * g4 + rr];

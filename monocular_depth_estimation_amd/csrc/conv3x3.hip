@@ -379,6 +379,13 @@ __global__ void __launch_bounds__(256, 2)
 }
 
 // ------------------------------------------------------- weight gradient
+// The reduction's tickets, zeroed by block (0, 0) of the weight-gradient
+// kernel that runs before it.
+__device__ __forceinline__ void zero_tickets(unsigned* cnt, int ncnt) {
+  if (blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = threadIdx.x; i < ncnt; i += blockDim.x) cnt[i] = 0u;
+}
+
 template <int CI, int CO, int TH, int PW>
 struct WgradCfg {
   static constexpr int CIP = cpad4(CI);
@@ -405,8 +412,9 @@ template <int CI, int CO, int TH, int PW, bool FULL>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                          float* __restrict__ part, int h, int w, int tiles_w,
-                         int tiles_per_img, int ntiles) {
+                         int tiles_per_img, int ntiles, unsigned* __restrict__ cnt, int ncnt) {
   using C = WgradCfg<CI, CO, TH, PW>;
+  zero_tickets(cnt, ncnt);
   __shared__ float smem[C::SMEM];
   float* sx = smem;
   float* sg = smem + C::ZERO + C::XR * kXW;
@@ -520,38 +528,104 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
-// Stage 1: part [G][M] -> part2 [S][M] (S interleaved groups of blocks).
-__global__ void __launch_bounds__(256)
-    wgrad_reduce1_kernel(const float* __restrict__ part, float* __restrict__ part2,
-                         int g, int m) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= m) return;
-  const int s = blockIdx.y, ns = gridDim.y;
-  float a0 = 0.f, a1 = 0.f;
-  int b = s;
-  for (; b + ns < g; b += 2 * ns) {
-    a0 += part[(int64_t)b * m + e];
-    a1 += part[(int64_t)(b + ns) * m + e];
+// Weight-gradient reduction, one launch: block (x, s, grp) sums partials
+// s, s + S, ... of its 256 elements into slice s (stage 1); the last of the S
+// blocks of column x to finish (agent-scope ticket) sums the S slices in
+// order and scatters them to gw (stage 2) -- fixed summation order whichever
+// block is last.  Hand-off across XCDs as dwconv.hip: slices stored
+// write-through (agent-scope atomic stores), release fence, ticket, acquire,
+// agent-scope atomic loads.  The tickets live in the workspace and are zeroed
+// by the weight-gradient kernel that precedes this launch on the stream.
+struct ReduceMap {
+  int wide;             // 1: the wide-channel layout [co 64][tap 9][ci 32] per group
+  int np, cip;          // regular layout [co][n = tap * cip + ci] (np columns)
+  int ci_n, co_n;
+};
+
+__device__ __forceinline__ int64_t gw_index(const ReduceMap& r, int grp, int e) {
+  if (r.wide) {
+    const int ngo = r.co_n / 64, col = e / 288, n = e % 288;
+    const int co = (grp % ngo) * 64 + col, ci = (grp / ngo) * 32 + n % 32;
+    return ((int64_t)co * r.ci_n + ci) * 9 + n / 32;
   }
-  if (b < g) a0 += part[(int64_t)b * m + e];
-  part2[(int64_t)s * m + e] = a0 + a1;
+  const int co = e / r.np, n = e % r.np, tap = n / r.cip, ci = n % r.cip;
+  if (tap >= 9 || ci >= r.ci_n) return -1;
+  return ((int64_t)co * r.ci_n + ci) * 9 + tap;
 }
 
-// Stage 2: sum the S groups and scatter n = tap * cip + ci to gw[co][ci][tap].
 __global__ void __launch_bounds__(256)
-    wgrad_reduce2_kernel(const float* __restrict__ part2, float* __restrict__ gw, int ns,
-                         int co_n, int ci_n, int cip, int np) {
+    wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ part2,
+                        unsigned* __restrict__ cnt, float* __restrict__ gw, int g, int m,
+                        ReduceMap map) {
+  using gf32 = __attribute__((address_space(1))) float;
+  using gu32 = __attribute__((address_space(1))) unsigned;
+  __shared__ unsigned last;
   const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= co_n * np) return;
-  const int co = e / np, n = e % np;
-  const int tap = n / cip, ci = n % cip;
-  if (tap >= 9 || ci >= ci_n) return;
-  float s = 0.f;
-  for (int k = 0; k < ns; ++k) s += part2[(int64_t)k * co_n * np + e];
-  gw[(co * ci_n + ci) * 9 + tap] = s;
+  const int s = blockIdx.y, ns = gridDim.y, grp = blockIdx.z;
+  float* p2 = part2 + (int64_t)grp * ns * m;
+  if (e < m) {
+    const float* pg = part + (int64_t)grp * g * m;
+    float a0 = 0.f, a1 = 0.f;
+    int b = s;
+    for (; b + ns < g; b += 2 * ns) {
+      a0 += pg[(int64_t)b * m + e];
+      a1 += pg[(int64_t)(b + ns) * m + e];
+    }
+    if (b < g) a0 += pg[(int64_t)b * m + e];
+    __hip_atomic_store((gf32*)(p2 + (int64_t)s * m + e), a0 + a1, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* c = cnt + (int64_t)grp * gridDim.x + blockIdx.x;
+    last = __hip_atomic_fetch_add((gu32*)c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+           (unsigned)(ns - 1);
+  }
+  __syncthreads();
+  if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (e >= m) return;
+  float a = 0.f;
+  for (int k = 0; k < ns; ++k)
+    a += __hip_atomic_load((gf32*)(p2 + (int64_t)k * m + e), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  const int64_t o = gw_index(map, grp, e);
+  if (o >= 0) gw[o] = a;
 }
 
 constexpr int kReduceSplit = 32;
+
+// Weight-gradient workspace: [partials: groups x g x m][slices: groups x split x m]
+// [tickets: groups x cdiv(m, 256)].
+struct WsLayout {
+  float* part;
+  float* part2;
+  unsigned* cnt;
+  int ncnt;
+};
+
+inline size_t wgrad_ws_bytes(int groups, int g, int split, int m) {
+  return sizeof(float) * (size_t)groups * ((size_t)g + (size_t)split) * (size_t)m +
+         sizeof(unsigned) * (size_t)groups * (size_t)mde::cdiv(m, 256);
+}
+
+inline WsLayout wgrad_ws(float* ws, int groups, int g, int split, int m) {
+  WsLayout l;
+  l.part = ws;
+  l.part2 = ws + (int64_t)groups * g * m;
+  l.cnt = reinterpret_cast<unsigned*>(l.part2 + (int64_t)groups * split * m);
+  l.ncnt = groups * (int)mde::cdiv(m, 256);
+  return l;
+}
+
+inline int launch_reduce(const WsLayout& l, float* gw, int groups, int g, int split, int m,
+                         const ReduceMap& map, hipStream_t s) {
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)(g + split) * m, s, wgrad_reduce_kernel,
+             dim3((unsigned)mde::cdiv(m, 256), split, groups), dim3(256), 0, l.part, l.part2,
+             l.cnt, gw, g, m, map);
+  return MDE_OK;
+}
 
 // ------------------------------------------- wide-channel weight gradient
 // DDRNet's 64 / 128 / 256-channel 3x3 / stride-1 convs (the BasicBlocks of
@@ -606,7 +680,8 @@ inline bool wide_geo(int64_t n, int64_t h, int64_t w, WideGeo* g) {
 __global__ void __launch_bounds__(256, 1)
     conv3x3_wgrad_wide_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                               float* __restrict__ part, int ci_n, int co_n, int h, int w,
-                              WideGeo g) {
+                              WideGeo g, unsigned* __restrict__ cnt, int ncnt) {
+  zero_tickets(cnt, ncnt);
   __shared__ float sx[kWCI * kWPX];
   __shared__ float sg[kWCO * kWPG];
   __shared__ int tab[kWK];
@@ -723,50 +798,145 @@ __global__ void __launch_bounds__(256, 1)
     for (int i = 0; i < 4; ++i) out[(16 * wv + 4 * lk + i) * (9 * kWCI) + 16 * nt + li] = acc[nt][i];
 }
 
-// Stage 1 per group (blockIdx.z): part [group][G][kWM] -> part2 [group][S][kWM].
-__global__ void __launch_bounds__(256)
-    wgrad_wide_reduce1_kernel(const float* __restrict__ part, float* __restrict__ part2, int g) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= kWM) return;
-  const int s = blockIdx.y, ns = gridDim.y;
-  const float* pg = part + (int64_t)blockIdx.z * g * kWM;
-  float a0 = 0.f, a1 = 0.f;
-  int b = s;
-  for (; b + ns < g; b += 2 * ns) {
-    a0 += pg[(int64_t)b * kWM + e];
-    a1 += pg[(int64_t)(b + ns) * kWM + e];
+// Fixed-width variant (w == W, W % 4 == 0, tiles of TH whole rows): a K step's
+// four pixels never straddle a row, so with the K loop fully unrolled every
+// operand address is a per-lane base plus a compile-time offset (no pixel
+// table, no address arithmetic), and the LDS is sized to the tile (<= 80 KB)
+// so that two blocks share a CU.  Same partial layout as the generic kernel.
+template <int W, int TH>
+struct WideT {
+  static constexpr int W2 = W + 2, K = TH * W, XE = (TH + 2) * W2;
+  static constexpr int PX = (XE - 2 + 31) / 32 * 32 + 2;  // >= XE, = 2 mod 32
+  static constexpr int PG = (K - 2 + 31) / 32 * 32 + 2;   // >= K, = 2 mod 32
+  static constexpr int XL = (XE + 63) / 64, GL = (K + 63) / 64;
+  static constexpr int SX = kWCI * PX, SMEM = SX + kWCO * PG;
+  static_assert(W % 4 == 0 && SMEM * 4 <= 80 * 1024, "two blocks per CU");
+};
+
+template <int W, int TH>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3_wgrad_wide_fixed_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                                    float* __restrict__ part, int ci_n, int co_n, int h,
+                                    int tiles_per_img, int ntiles, unsigned* __restrict__ cnt,
+                                    int ncnt) {
+  zero_tickets(cnt, ncnt);
+  using P = WideT<W, TH>;
+  __shared__ float sm[P::SMEM];
+  float* sx = sm;
+  float* sg = sm + P::SX;
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ngo = co_n / kWCO;
+  const int cog = blockIdx.y % ngo, cig = blockIdx.y / ngo;
+  const int hw = h * W;
+  int xrel[P::XL], xrr[P::XL];
+  unsigned xcol = 0;  // bit i: element i is an image column (not the zero border)
+#pragma unroll
+  for (int i = 0; i < P::XL; ++i) {
+    const int e = lane + 64 * i;
+    const int rr = e / P::W2, cc = e - rr * P::W2;
+    xrr[i] = e < P::XE ? rr : -4096;
+    xrel[i] = (rr - 1) * W + cc - 1;
+    xcol |= (cc >= 1 && cc <= W) ? 1u << i : 0u;
   }
-  if (b < g) a0 += pg[(int64_t)b * kWM + e];
-  part2[((int64_t)blockIdx.z * ns + s) * kWM + e] = a0 + a1;
+  f4 acc[kWNT];
+#pragma unroll
+  for (int nt = 0; nt < kWNT; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* xg = x + ((int64_t)cig * kWCI + 8 * wv) * hw;
+  const float* gg = gy + ((int64_t)cog * kWCO + 16 * wv) * hw;
+  float vx[8][P::XL], vg[16][P::GL];
+  unsigned xm = 0, gm = 0;
+  auto load = [&](int tile) {
+    const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TH;
+    const float* xi = xg + (int64_t)img * ci_n * hw;
+    const float* gi = gg + (int64_t)img * co_n * hw;
+    const int tb = r0 * W;
+    xm = 0;
+#pragma unroll
+    for (int i = 0; i < P::XL; ++i) {
+      const int gr = r0 - 1 + xrr[i];
+      const bool ok = gr >= 0 && gr < h && ((xcol >> i) & 1u);
+      xm |= ok ? 1u << i : 0u;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) vx[c][i] = xi[ok ? (unsigned)(c * hw + tb + xrel[i]) : 0u];
+    }
+    gm = 0;
+#pragma unroll
+    for (int i = 0; i < P::GL; ++i) {
+      const int p = lane + 64 * i;
+      const bool ok = p < P::K && r0 + p / W < h;
+      gm |= ok ? 1u << i : 0u;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) vg[c][i] = gi[ok ? (unsigned)(c * hw + tb + p) : 0u];
+    }
+  };
+  int tile = blockIdx.x;
+  if (tile < ntiles) load(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();  // the previous tile's operands are consumed
+#pragma unroll
+    for (int i = 0; i < P::XL; ++i) {
+      const int e = lane + 64 * i;
+      if (e < P::XE) {
+#pragma unroll
+        for (int c = 0; c < 8; ++c) sx[(8 * wv + c) * P::PX + e] = (xm >> i) & 1u ? vx[c][i] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < P::GL; ++i) {
+      const int p = lane + 64 * i;
+      if (p < P::K) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) sg[(16 * wv + c) * P::PG + p] = (gm >> i) & 1u ? vg[c][i] : 0.f;
+      }
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load(tile + gridDim.x);
+    const float* xb = sx + li * P::PX + lk;
+    const float* gb = sg + (16 * wv + li) * P::PG + lk;
+#pragma unroll 5
+    for (int st = 0; st < P::K / 4; ++st) {
+      const int so = (4 * st / W) * P::W2 + (4 * st) % W;  // the step's first pixel
+      const float a = gb[4 * st];
+#pragma unroll
+      for (int nt = 0; nt < kWNT; ++nt) {
+        const int tap = nt >> 1;
+        acc[nt] = mfma4(a, xb[(nt & 1) * 16 * P::PX + (tap / 3) * P::W2 + tap % 3 + so], acc[nt]);
+      }
+    }
+  }
+  float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWM;
+#pragma unroll
+  for (int nt = 0; nt < kWNT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) out[(16 * wv + 4 * lk + i) * (9 * kWCI) + 16 * nt + li] = acc[nt][i];
 }
 
-// Stage 2 per group (blockIdx.y): sum the S slices, scatter to gw[co][ci][tap].
-__global__ void __launch_bounds__(256)
-    wgrad_wide_reduce2_kernel(const float* __restrict__ part2, float* __restrict__ gw, int ns,
-                              int ci_n, int co_n) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= kWM) return;
-  const int grp = blockIdx.y, ngo = co_n / kWCO;
-  const float* p2 = part2 + (int64_t)grp * ns * kWM;
-  float s = 0.f;
-  for (int k = 0; k < ns; ++k) s += p2[(int64_t)k * kWM + e];
-  const int col = e / (9 * kWCI), n = e % (9 * kWCI);
-  const int co = (grp % ngo) * kWCO + col, ci = (grp / ngo) * kWCI + n % kWCI;
-  gw[((int64_t)co * ci_n + ci) * 9 + n / kWCI] = s;
-}
-
-constexpr int kWideBlocks = 256;  // one 100 KB-LDS block per CU
+// Fixed-width tile heights: K = 80 pixels (K = 160 spills).
+inline int wide_fixed_th(int64_t w) { return w == 80 ? 1 : (w == 40 ? 2 : (w == 20 ? 4 : 0)); }
 
 struct WidePlan {
   WideGeo g;
   int groups, gx, split;
+  int fixed_th;  // > 0: the fixed-width kernel (whole-row tiles of fixed_th rows)
 };
 
 inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WidePlan* p) {
   if (ci % kWCI || co % kWCO || ci < kWCI || co < kWCO) return false;
   if (!wide_geo(n, h, w, &p->g)) return false;
+  p->fixed_th = wide_fixed_th(w);
+  if (p->fixed_th) {  // whole-row tiles of fixed_th rows
+    const int64_t tpi = mde::cdiv(h, p->fixed_th), nt = n * tpi;
+    if (nt > 0x7fffffff) return false;
+    p->g.th = p->fixed_th;
+    p->g.wc = (int)w;
+    p->g.tiles_w = 1;
+    p->g.tiles_per_img = (int)tpi;
+    p->g.ntiles = (int)nt;
+  }
   p->groups = (int)((ci / kWCI) * (co / kWCO));
-  int gx = kWideBlocks / p->groups;
+  // one 100 KB-LDS block per CU (generic), two <= 80 KB blocks (fixed width)
+  int gx = (p->fixed_th ? 512 : 256) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;
@@ -775,7 +945,7 @@ inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, W
 }
 
 inline size_t wide_workspace(const WidePlan& p) {
-  return sizeof(float) * (size_t)p.groups * ((size_t)p.gx + (size_t)p.split) * kWM;
+  return wgrad_ws_bytes(p.groups, p.gx, p.split, kWM);
 }
 
 int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int64_t ci,
@@ -784,18 +954,27 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
   if (!wide_plan(n, ci, co, h, w, &p)) return MDE_ERR_UNSUPPORTED;
   const double flops = 2.0 * 9 * ci * co * (double)(n * h * w);
   const double bytes = 4.0 * n * h * w * (double)(ci + co);
-  float* part = ws;
-  float* part2 = ws + (int64_t)p.groups * p.gx * kWM;
-  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, conv3x3_wgrad_wide_kernel,
-                  dim3(p.gx, p.groups), dim3(256), 0, x, gy, part, (int)ci, (int)co, (int)h,
-                  (int)w, p.g);
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.groups * p.gx * kWM, s, wgrad_wide_reduce1_kernel,
-             dim3((unsigned)mde::cdiv(kWM, 256), p.split, p.groups), dim3(256), 0, part, part2,
-             p.gx);
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.groups * p.split * kWM, s, wgrad_wide_reduce2_kernel,
-             dim3((unsigned)mde::cdiv(kWM, 256), p.groups), dim3(256), 0, part2, gw, p.split,
-             (int)ci, (int)co);
-  return MDE_OK;
+  const WsLayout l = wgrad_ws(ws, p.groups, p.gx, p.split, kWM);
+  const dim3 grid(p.gx, p.groups);
+  const int tpi = p.g.tiles_per_img, nt = p.g.ntiles;
+  if (w == 80)
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<80, 1>),
+                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt, l.cnt,
+                    l.ncnt);
+  else if (w == 40)
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<40, 2>),
+                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt, l.cnt,
+                    l.ncnt);
+  else if (w == 20)
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<20, 4>),
+                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt, l.cnt,
+                    l.ncnt);
+  else
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
+                    dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, (int)w, p.g, l.cnt,
+                    l.ncnt);
+  return launch_reduce(l, gw, p.groups, p.gx, p.split, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co},
+                       s);
 }
 
 // ====================================================================== bf16
@@ -1136,7 +1315,8 @@ template <int CI, int CO, int TH, int PW>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_bf_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
                             float* __restrict__ part, int h, int w, int tiles_w,
-                            int tiles_per_img, int ntiles) {
+                            int tiles_per_img, int ntiles, unsigned* __restrict__ cnt, int ncnt) {
+  zero_tickets(cnt, ncnt);
   using C = BfWgradCfg<CI, CO, TH, PW>;
   static_assert(CI % 16 == 0 && CO % 16 == 0, "16-channel blocks");
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM_F];
@@ -1297,35 +1477,29 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
                  float* ws, double bytes, hipStream_t s) {
   const WgradPlan p = wgrad_plan<CI, CO, TH, PW>(n, h, w);
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
-  float* part = ws;
-  float* part2 = ws + (int64_t)p.grid * p.m;
+  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
+  const WsLayout l = wgrad_ws(ws, 1, p.grid, split, p.m);
   // the 3-channel guide convs' weight gradients have ~12 flop per byte, under the
   // fp32 MFMA ridge (157 TF / 8 TB/s ~ 20): timed as HBM-bound under their own id
   if (CI == 3) {
     if (w % kTW == 0)
       MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
-                 dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
-                 p.tiles_per_img, p.ntiles);
+                 dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                 p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
     else
       MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
-                 dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
-                 p.tiles_per_img, p.ntiles);
+                 dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                 p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
   } else if (w % kTW == 0) {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
-                    dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
-                    p.tiles_per_img, p.ntiles);
+                    dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                    p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
   } else {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
-                    dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
-                    p.tiles_per_img, p.ntiles);
+                    dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                    p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
   }
-  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
-             dim3((unsigned)mde::cdiv(p.m, 256), split), dim3(256), 0, part, part2, p.grid, p.m);
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * split * p.m, s, wgrad_reduce2_kernel,
-             dim3((unsigned)mde::cdiv(p.m, 256)), dim3(256), 0, part2, gw, split, CO, CI, p.cip,
-             p.np);
-  return MDE_OK;
+  return launch_reduce(l, gw, 1, p.grid, split, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
 
 // ---- bf16 dispatch
@@ -1378,18 +1552,12 @@ int launch_bf_wgrad(const bf16* x, const bf16* gy, float* gw, int64_t n, int64_t
   const WgradPlan p = bf_wgrad_plan<CI, CO, TH, PW>(n, h, w);
   if (p.grid <= 0) return MDE_ERR_INVALID_ARG;
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
-  float* part = ws;
-  float* part2 = ws + (int64_t)p.grid * p.m;
-  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
-                  dim3(p.grid), dim3(256), 0, x, gy, part, (int)h, (int)w, p.tiles_w,
-                  p.tiles_per_img, p.ntiles);
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * p.grid * p.m, s, wgrad_reduce1_kernel,
-             dim3((unsigned)mde::cdiv(p.m, 256), split), dim3(256), 0, part, part2, p.grid, p.m);
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * split * p.m, s, wgrad_reduce2_kernel,
-             dim3((unsigned)mde::cdiv(p.m, 256)), dim3(256), 0, part2, gw, split, CO, CI, p.cip,
-             p.np);
-  return MDE_OK;
+  const WsLayout l = wgrad_ws(ws, 1, p.grid, split, p.m);
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
+                  dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                  p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
+  return launch_reduce(l, gw, 1, p.grid, split, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
 
 // bf16 shapes: 16 -> 16 and 32 -> 32, every pass; 4-column chunks need w % 4 == 0
@@ -1562,7 +1730,7 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
     if (!bf_supported(cin, cout) || !dims_ok(n, h, w)) return 0;
     p = cin == 16 ? bf_wgrad_plan<16, 16, 4, 4>(n, h, w) : bf_wgrad_plan<32, 32, 2, 2>(n, h, w);
     const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-    return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
+    return wgrad_ws_bytes(1, p.grid, split, p.m);
   }
   if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
   if (wide(cin, cout)) {
@@ -1579,7 +1747,7 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   else if (variant() == 2) p = wgrad_plan<32, 32, 4, 1>(n, h, w);
   else p = wgrad_plan<32, 32, 2, 2>(n, h, w);
   const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-  return sizeof(float) * ((size_t)p.grid + (size_t)split) * (size_t)p.m;
+  return wgrad_ws_bytes(1, p.grid, split, p.m);
 }
 
 int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,

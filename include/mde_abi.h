@@ -489,14 +489,12 @@ size_t mde_dwconv_workspace(int64_t n, int64_t c, int64_t h, int64_t w, int64_t 
 int mde_dwconv_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t c,
                    int64_t h, int64_t w, int64_t k, int64_t stride, int64_t pad, int dtype,
                    void* stream);
-/* counters: DEVICE uint32[c], all zero on entry and left all zero (the caller
- * keeps one zeroed buffer for every call on a stream); when a channel's weight
- * gradient is split over several blocks, the last block to finish sums the
- * partials in a fixed order (deterministic).  NULL: a second launch sums them. */
+/* A channel's weight gradient split over several blocks is summed in a fixed
+ * order by the launch that follows (deterministic; round 3 dropped the
+ * round-2 `counters` argument and its in-kernel last-block hand-off). */
 int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx,
                    float* gweight, int64_t n, int64_t c, int64_t h, int64_t w, int64_t k,
-                   int64_t stride, int64_t pad, void* workspace, uint32_t* counters, int dtype,
-                   void* stream);
+                   int64_t stride, int64_t pad, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * LayerNorm over the last axis of a token-major [rows, c] tensor (c a

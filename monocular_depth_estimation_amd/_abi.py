@@ -113,7 +113,7 @@ SIGNATURES = {
     "mde_dwconv_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64, _i64]),
     "mde_dwconv_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_dwconv_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,
-                              _vp, _vp, _int, _vp]),
+                              _vp, _int, _vp]),
     "mde_layernorm_workspace": (_sz, [_i64, _i64]),
     "mde_layernorm_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _int, _vp]),
     "mde_layernorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _int,

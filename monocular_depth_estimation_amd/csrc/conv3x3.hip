@@ -37,6 +37,8 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
 constexpr int kTW = 64;       // output columns per tile (4 MFMA row tiles)
 constexpr int kXW = kTW + 2;  // staged input columns (one-pixel halo each side)
 
@@ -379,13 +381,6 @@ __global__ void __launch_bounds__(256, 2)
 }
 
 // ------------------------------------------------------- weight gradient
-// The reduction's tickets, zeroed by block (0, 0) of the weight-gradient
-// kernel that runs before it.
-__device__ __forceinline__ void zero_tickets(unsigned* cnt, int ncnt) {
-  if (blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = threadIdx.x; i < ncnt; i += blockDim.x) cnt[i] = 0u;
-}
-
 template <int CI, int CO, int TH, int PW>
 struct WgradCfg {
   static constexpr int CIP = cpad4(CI);
@@ -412,9 +407,8 @@ template <int CI, int CO, int TH, int PW, bool FULL>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                          float* __restrict__ part, int h, int w, int tiles_w,
-                         int tiles_per_img, int ntiles, unsigned* __restrict__ cnt, int ncnt) {
+                         int tiles_per_img, int ntiles) {
   using C = WgradCfg<CI, CO, TH, PW>;
-  zero_tickets(cnt, ncnt);
   __shared__ float smem[C::SMEM];
   float* sx = smem;
   float* sg = smem + C::ZERO + C::XR * kXW;
@@ -528,14 +522,11 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
-// Weight-gradient reduction, one launch: block (x, s, grp) sums partials
-// s, s + S, ... of its 256 elements into slice s (stage 1); the last of the S
-// blocks of column x to finish (agent-scope ticket) sums the S slices in
-// order and scatters them to gw (stage 2) -- fixed summation order whichever
-// block is last.  Hand-off across XCDs as dwconv.hip: slices stored
-// write-through (agent-scope atomic stores), release fence, ticket, acquire,
-// agent-scope atomic loads.  The tickets live in the workspace and are zeroed
-// by the weight-gradient kernel that precedes this launch on the stream.
+// Weight-gradient reduction, two launches, fixed summation order: stage 1
+// (block (x, s, grp)) sums partials s, s + S, ... of its 256 elements into
+// slice s; stage 2 sums the S slices in order and scatters them to gw.  (A
+// one-launch last-block hand-off was measured slower: its agent-scope release
+// fences write back L2 on every block, 53 vs 21 us per weight gradient.)
 struct ReduceMap {
   int wide;             // 1: the wide-channel layout [co 64][tap 9][ci 32] per group
   int np, cip;          // regular layout [co][n = tap * cip + ci] (np columns)
@@ -554,76 +545,58 @@ __device__ __forceinline__ int64_t gw_index(const ReduceMap& r, int grp, int e) 
 }
 
 __global__ void __launch_bounds__(256)
-    wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ part2,
-                        unsigned* __restrict__ cnt, float* __restrict__ gw, int g, int m,
-                        ReduceMap map) {
-  using gf32 = __attribute__((address_space(1))) float;
-  using gu32 = __attribute__((address_space(1))) unsigned;
-  __shared__ unsigned last;
+    wgrad_reduce1_kernel(const float* __restrict__ part, float* __restrict__ part2, int g,
+                         int m) {
   const int e = blockIdx.x * 256 + threadIdx.x;
-  const int s = blockIdx.y, ns = gridDim.y, grp = blockIdx.z;
-  float* p2 = part2 + (int64_t)grp * ns * m;
-  if (e < m) {
-    const float* pg = part + (int64_t)grp * g * m;
-    float a0 = 0.f, a1 = 0.f;
-    int b = s;
-    for (; b + ns < g; b += 2 * ns) {
-      a0 += pg[(int64_t)b * m + e];
-      a1 += pg[(int64_t)(b + ns) * m + e];
-    }
-    if (b < g) a0 += pg[(int64_t)b * m + e];
-    __hip_atomic_store((gf32*)(p2 + (int64_t)s * m + e), a0 + a1, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned* c = cnt + (int64_t)grp * gridDim.x + blockIdx.x;
-    last = __hip_atomic_fetch_add((gu32*)c, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
-           (unsigned)(ns - 1);
-  }
-  __syncthreads();
-  if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   if (e >= m) return;
+  const int s = blockIdx.y, ns = gridDim.y, grp = blockIdx.z;
+  const float* pg = part + (int64_t)grp * g * m;
+  float a0 = 0.f, a1 = 0.f;
+  int b = s;
+  for (; b + ns < g; b += 2 * ns) {
+    a0 += pg[(int64_t)b * m + e];
+    a1 += pg[(int64_t)(b + ns) * m + e];
+  }
+  if (b < g) a0 += pg[(int64_t)b * m + e];
+  part2[((int64_t)grp * ns + s) * m + e] = a0 + a1;
+}
+
+__global__ void __launch_bounds__(256)
+    wgrad_reduce2_kernel(const float* __restrict__ part2, float* __restrict__ gw, int ns, int m,
+                         ReduceMap map) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= m) return;
+  const int grp = blockIdx.y;
+  const float* p2 = part2 + (int64_t)grp * ns * m;
   float a = 0.f;
-  for (int k = 0; k < ns; ++k)
-    a += __hip_atomic_load((gf32*)(p2 + (int64_t)k * m + e), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < ns; ++k) a += p2[(int64_t)k * m + e];
   const int64_t o = gw_index(map, grp, e);
   if (o >= 0) gw[o] = a;
 }
 
 constexpr int kReduceSplit = 32;
 
-// Weight-gradient workspace: [partials: groups x g x m][slices: groups x split x m]
-// [tickets: groups x cdiv(m, 256)].
+// Weight-gradient workspace: [partials: groups x g x m][slices: groups x split x m].
 struct WsLayout {
   float* part;
   float* part2;
-  unsigned* cnt;
-  int ncnt;
 };
 
 inline size_t wgrad_ws_bytes(int groups, int g, int split, int m) {
-  return sizeof(float) * (size_t)groups * ((size_t)g + (size_t)split) * (size_t)m +
-         sizeof(unsigned) * (size_t)groups * (size_t)mde::cdiv(m, 256);
+  return sizeof(float) * (size_t)groups * ((size_t)g + (size_t)split) * (size_t)m;
 }
 
 inline WsLayout wgrad_ws(float* ws, int groups, int g, int split, int m) {
-  WsLayout l;
-  l.part = ws;
-  l.part2 = ws + (int64_t)groups * g * m;
-  l.cnt = reinterpret_cast<unsigned*>(l.part2 + (int64_t)groups * split * m);
-  l.ncnt = groups * (int)mde::cdiv(m, 256);
-  return l;
+  return {ws, ws + (int64_t)groups * g * m};
 }
 
 inline int launch_reduce(const WsLayout& l, float* gw, int groups, int g, int split, int m,
                          const ReduceMap& map, hipStream_t s) {
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)(g + split) * m, s, wgrad_reduce_kernel,
-             dim3((unsigned)mde::cdiv(m, 256), split, groups), dim3(256), 0, l.part, l.part2,
-             l.cnt, gw, g, m, map);
+  const unsigned bx = (unsigned)mde::cdiv(m, 256);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)(g + split) * m, s, wgrad_reduce1_kernel,
+             dim3(bx, split, groups), dim3(256), 0, l.part, l.part2, g, m);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)split * m + 4.0 * groups * m, s,
+             wgrad_reduce2_kernel, dim3(bx, groups), dim3(256), 0, l.part2, gw, split, m, map);
   return MDE_OK;
 }
 
@@ -680,8 +653,7 @@ inline bool wide_geo(int64_t n, int64_t h, int64_t w, WideGeo* g) {
 __global__ void __launch_bounds__(256, 1)
     conv3x3_wgrad_wide_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                               float* __restrict__ part, int ci_n, int co_n, int h, int w,
-                              WideGeo g, unsigned* __restrict__ cnt, int ncnt) {
-  zero_tickets(cnt, ncnt);
+                              WideGeo g) {
   __shared__ float sx[kWCI * kWPX];
   __shared__ float sg[kWCO * kWPG];
   __shared__ int tab[kWK];
@@ -700,22 +672,20 @@ __global__ void __launch_bounds__(256, 1)
   // tile-invariant staging geometry of this lane: x element e = lane + 64 i of
   // a channel's staged plane is tile row rr, staged column cc (image column
   // c0 + cc - 1); gy element p = lane + 64 i is tile row p / wc, column p % wc
-  int xrel[kWXL], xrr[kWXL], xcc[kWXL];
+  int xrr[kWXL], xcc[kWXL];
 #pragma unroll
   for (int i = 0; i < kWXL; ++i) {
     const int e = lane + 64 * i;
     const int rr = e / W2, cc = e - rr * W2;
     xrr[i] = e < XE ? rr : -4096;  // out of the plane: never in range
     xcc[i] = cc;
-    xrel[i] = (rr - 1) * w + cc - 1;
   }
-  int grel[kWGL], gcol[kWGL], grow[kWGL];
+  int gcol[kWGL], grow[kWGL];
 #pragma unroll
   for (int i = 0; i < kWGL; ++i) {
     const int p = lane + 64 * i;
     grow[i] = p < K ? p / wc : -4096;
     gcol[i] = p % wc;
-    grel[i] = (p / wc) * w + p % wc;
   }
   int boff[kWNT];
 #pragma unroll
@@ -741,23 +711,27 @@ __global__ void __launch_bounds__(256, 1)
     const int r0 = (t / g.tiles_w) * th, c0 = (t % g.tiles_w) * wc;
     const float* xi = xg + (int64_t)img * ci_n * hw;
     const float* gi = gg + (int64_t)img * co_n * hw;
-    const int tb = r0 * w + c0;
+    // clamped coordinates: every load is a real element at a per-lane
+    // address (a select of a uniform fallback address makes the compiler
+    // split each load into a vector and a scalar branch)
     xm = 0;
 #pragma unroll
     for (int i = 0; i < kWXL; ++i) {
       const int gr = r0 - 1 + xrr[i], gc = c0 - 1 + xcc[i];
       const bool ok = gr >= 0 && gr < h && gc >= 0 && gc < w;  // a strip's halo columns are real
       xm |= ok ? 1u << i : 0u;
+      const int o = clampi(gr, 0, h - 1) * w + clampi(gc, 0, w - 1);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) vx[c][i] = xi[ok ? (unsigned)(c * hw + tb + xrel[i]) : 0u];
+      for (int c = 0; c < 8; ++c) vx[c][i] = xi[(unsigned)(c * hw + o)];
     }
     gm = 0;
 #pragma unroll
     for (int i = 0; i < kWGL; ++i) {
       const bool ok = grow[i] >= 0 && r0 + grow[i] < h && c0 + gcol[i] < w;
       gm |= ok ? 1u << i : 0u;
+      const int o = clampi(r0 + grow[i], 0, h - 1) * w + clampi(c0 + gcol[i], 0, w - 1);
 #pragma unroll
-      for (int c = 0; c < 16; ++c) vg[c][i] = gi[ok ? (unsigned)(c * hw + tb + grel[i]) : 0u];
+      for (int c = 0; c < 16; ++c) vg[c][i] = gi[(unsigned)(c * hw + o)];
     }
   };
   int tile = blockIdx.x;
@@ -817,9 +791,7 @@ template <int W, int TH>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_wgrad_wide_fixed_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                                     float* __restrict__ part, int ci_n, int co_n, int h,
-                                    int tiles_per_img, int ntiles, unsigned* __restrict__ cnt,
-                                    int ncnt) {
-  zero_tickets(cnt, ncnt);
+                                    int tiles_per_img, int ntiles) {
   using P = WideT<W, TH>;
   __shared__ float sm[P::SMEM];
   float* sx = sm;
@@ -829,15 +801,21 @@ __global__ void __launch_bounds__(256, 2)
   const int ngo = co_n / kWCO;
   const int cog = blockIdx.y % ngo, cig = blockIdx.y / ngo;
   const int hw = h * W;
-  int xrel[P::XL], xrr[P::XL];
+  int xcc[P::XL], xrr[P::XL], gpr[P::GL], gpc[P::GL];
   unsigned xcol = 0;  // bit i: element i is an image column (not the zero border)
 #pragma unroll
   for (int i = 0; i < P::XL; ++i) {
     const int e = lane + 64 * i;
     const int rr = e / P::W2, cc = e - rr * P::W2;
     xrr[i] = e < P::XE ? rr : -4096;
-    xrel[i] = (rr - 1) * W + cc - 1;
+    xcc[i] = clampi(cc - 1, 0, W - 1);  // clamped: the border columns load a real element
     xcol |= (cc >= 1 && cc <= W) ? 1u << i : 0u;
+  }
+#pragma unroll
+  for (int i = 0; i < P::GL; ++i) {
+    const int p = lane + 64 * i < P::K ? lane + 64 * i : P::K - 1;
+    gpr[i] = p / W;
+    gpc[i] = p % W;
   }
   f4 acc[kWNT];
 #pragma unroll
@@ -850,15 +828,16 @@ __global__ void __launch_bounds__(256, 2)
     const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TH;
     const float* xi = xg + (int64_t)img * ci_n * hw;
     const float* gi = gg + (int64_t)img * co_n * hw;
-    const int tb = r0 * W;
+    // clamped coordinates (see the generic kernel): no uniform fallback address
     xm = 0;
 #pragma unroll
     for (int i = 0; i < P::XL; ++i) {
       const int gr = r0 - 1 + xrr[i];
       const bool ok = gr >= 0 && gr < h && ((xcol >> i) & 1u);
       xm |= ok ? 1u << i : 0u;
+      const int o = clampi(gr, 0, h - 1) * W + xcc[i];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) vx[c][i] = xi[ok ? (unsigned)(c * hw + tb + xrel[i]) : 0u];
+      for (int c = 0; c < 8; ++c) vx[c][i] = xi[(unsigned)(c * hw + o)];
     }
     gm = 0;
 #pragma unroll
@@ -866,8 +845,9 @@ __global__ void __launch_bounds__(256, 2)
       const int p = lane + 64 * i;
       const bool ok = p < P::K && r0 + p / W < h;
       gm |= ok ? 1u << i : 0u;
+      const int o = clampi(r0 + gpr[i], 0, h - 1) * W + gpc[i];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) vg[c][i] = gi[ok ? (unsigned)(c * hw + tb + p) : 0u];
+      for (int c = 0; c < 16; ++c) vg[c][i] = gi[(unsigned)(c * hw + o)];
     }
   };
   int tile = blockIdx.x;
@@ -959,20 +939,16 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
   const int tpi = p.g.tiles_per_img, nt = p.g.ntiles;
   if (w == 80)
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<80, 1>),
-                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt, l.cnt,
-                    l.ncnt);
+                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt);
   else if (w == 40)
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<40, 2>),
-                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt, l.cnt,
-                    l.ncnt);
+                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt);
   else if (w == 20)
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<20, 4>),
-                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt, l.cnt,
-                    l.ncnt);
+                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt);
   else
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
-                    dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, (int)w, p.g, l.cnt,
-                    l.ncnt);
+                    dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, (int)w, p.g);
   return launch_reduce(l, gw, p.groups, p.gx, p.split, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co},
                        s);
 }
@@ -1315,8 +1291,7 @@ template <int CI, int CO, int TH, int PW>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_bf_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
                             float* __restrict__ part, int h, int w, int tiles_w,
-                            int tiles_per_img, int ntiles, unsigned* __restrict__ cnt, int ncnt) {
-  zero_tickets(cnt, ncnt);
+                            int tiles_per_img, int ntiles) {
   using C = BfWgradCfg<CI, CO, TH, PW>;
   static_assert(CI % 16 == 0 && CO % 16 == 0, "16-channel blocks");
   __shared__ __attribute__((aligned(16))) float smem[C::SMEM_F];
@@ -1485,19 +1460,19 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
     if (w % kTW == 0)
       MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
                  dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
-                 p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
+                 p.tiles_per_img, p.ntiles);
     else
       MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
                  dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
-                 p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
+                 p.tiles_per_img, p.ntiles);
   } else if (w % kTW == 0) {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
                     dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
-                    p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
+                    p.tiles_per_img, p.ntiles);
   } else {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
                     dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
-                    p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
+                    p.tiles_per_img, p.ntiles);
   }
   return launch_reduce(l, gw, 1, p.grid, split, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
@@ -1556,7 +1531,7 @@ int launch_bf_wgrad(const bf16* x, const bf16* gy, float* gw, int64_t n, int64_t
   const WsLayout l = wgrad_ws(ws, 1, p.grid, split, p.m);
   MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
                   dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
-                  p.tiles_per_img, p.ntiles, l.cnt, l.ncnt);
+                  p.tiles_per_img, p.ntiles);
   return launch_reduce(l, gw, 1, p.grid, split, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
 

@@ -590,10 +590,6 @@ __global__ void __launch_bounds__(256)
 //                   spans several blocks, a fixed-order partial reduce.
 // Backward units are ordered (channel, image, band, segment) and a wave never
 // mixes channels, so a wave-wide sum is one channel's weight gradient.
-// Channels split over at most this many blocks finish their weight gradient
-// in the last block (a serial sum of G partials); more: a separate launch.
-constexpr int kHandoffMaxG = 16;
-
 struct DwStream {
   int L, spw, nseg, nb;  // lanes per segment, segments per wave, per row, bands per plane
   int wpb, it, G;        // backward: waves per block, unit groups per wave, blocks per channel
@@ -740,7 +736,7 @@ __device__ __forceinline__ void dw_bwd_stream_body(const float* __restrict__ gy,
                                                    const float* __restrict__ wt,
                                                    float* __restrict__ gx, float* __restrict__ gw,
                                                    float* __restrict__ gwf,
-                                                   unsigned* __restrict__ cnt, const DwShape& d,
+                                                   const DwShape& d,
                                                    const DwStream& t, int wv) {
   constexpr int P = K / 2, XV = S * V;
   constexpr int XL = -P, XH = S * (V - 1) - P + K - 1;  // x columns for the weight gradient
@@ -861,41 +857,10 @@ __device__ __forceinline__ void dw_bwd_stream_body(const float* __restrict__ gy,
       float s = 0.f;
       if (lane < K * K)
         for (int k = 0; k < t.wpb; ++k) s += red[k][lane];
-      if (t.G == 1 || !cnt || t.G > kHandoffMaxG) {
-        if (lane < K * K) gw[(int64_t)blockIdx.x * (K * K) + lane] = s;  // = gw[ch] when G == 1
-      } else {
-        // Last block of the channel sums the G partials (fixed order g = 0..G-1,
-        // so the result does not depend on which block is last).  Hand-off
-        // across XCDs without cache flushes: partials stored write-through
-        // (agent-scope atomic stores) and drained, then the ticket; the last
-        // arriver reads them with agent-scope atomic loads (bypassing L1).
-        using gf32 = __attribute__((address_space(1))) float;
-        using gu32 = __attribute__((address_space(1))) unsigned;
-        if (lane < K * K)
-          __hip_atomic_store((gf32*)(gw + (int64_t)blockIdx.x * (K * K) + lane), s,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // release: every lane's partial store is visible at agent scope before
-        // the ticket; acquire (last block): the partial loads happen after it
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        unsigned prev = 0;
-        if (lane == 0)
-          prev = __hip_atomic_fetch_add((gu32*)(cnt + ch), 1u, __ATOMIC_ACQ_REL,
-                                        __HIP_MEMORY_SCOPE_AGENT);
-        prev = __shfl(prev, 0, 64);
-        if (prev == (unsigned)(t.G - 1)) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          if (lane < K * K) {
-            const float* p = gw + (int64_t)ch * t.G * (K * K) + lane;
-            float a = 0.f;
-            for (int g = 0; g < t.G; ++g)
-              a += __hip_atomic_load((gf32*)(p + (int64_t)g * (K * K)), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-            gwf[(int64_t)ch * (K * K) + lane] = a;
-          }
-          if (lane == 0)  // leave the counter zero for the next call
-            __hip_atomic_store((gu32*)(cnt + ch), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
+      // G == 1: the channel's gradient; else this block's partial, summed in
+      // fixed order by the launch that follows on the stream (kernel
+      // boundary: no cross-block hand-off inside this launch)
+      if (lane < K * K) gw[(int64_t)blockIdx.x * (K * K) + lane] = s;
     }
   } else {
     __syncthreads();  // matches the gw waves' barrier
@@ -913,18 +878,18 @@ __global__ void __launch_bounds__(512)
     dw_bwd_stream_kernel(const float* __restrict__ gy, const float* __restrict__ x,
                          const float* __restrict__ wt, float* __restrict__ gx,
                          float* __restrict__ gw, float* __restrict__ gwf,
-                         unsigned* __restrict__ cnt, DwShape d, DwStream t, int n) {
+                         DwShape d, DwStream t, int n) {
   const int role_wave = threadIdx.x >> 6;
   if (MODE == 1 && t.fold && role_wave == 0 && blockIdx.x < d.c)
     wsum_channel<K>(gw, gwf, t.G, blockIdx.x, threadIdx.x);
   if (MODE == 0 && role_wave < t.wpb)
-    dw_bwd_stream_body<K, S, V, RB, EDGE, true, false>(gy, x, wt, gx, gw, gwf, cnt, d, t,
+    dw_bwd_stream_body<K, S, V, RB, EDGE, true, false>(gy, x, wt, gx, gw, gwf, d, t,
                                                        role_wave);
   else if (MODE == 0)
-    dw_bwd_stream_body<K, S, V, RB, EDGE, false, true>(gy, x, wt, gx, gw, gwf, cnt, d, t,
+    dw_bwd_stream_body<K, S, V, RB, EDGE, false, true>(gy, x, wt, gx, gw, gwf, d, t,
                                                        role_wave - t.wpb);
   else
-    dw_bwd_stream_body<K, S, V, RB, EDGE, MODE == 1, MODE == 2>(gy, x, wt, gx, gw, gwf, cnt, d,
+    dw_bwd_stream_body<K, S, V, RB, EDGE, MODE == 1, MODE == 2>(gy, x, wt, gx, gw, gwf, d,
                                                                 t, role_wave);
 }
 
@@ -1107,26 +1072,27 @@ DwStream stream_bwd_layout(int64_t n, const DwShape& d, const DwCfg& c) {
 
 template <int K, int S, int V, int RB, bool EDGE>
 int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* gx, float* gw,
-                      float* part, unsigned* cnt, int64_t n, const DwShape& d, const DwStream& t,
+                      float* part, int64_t n, const DwShape& d, const DwStream& t,
                       hipStream_t st) {
   float* dst = gw ? (t.G == 1 ? gw : part) : nullptr;
   const double bytes =
       4.0 * n * d.c * (d.ho * d.wo + (gx ? d.h * d.w : 0) + (gw ? d.h * d.w : 0));
   const dim3 grid((unsigned)(d.c * t.G)), block((unsigned)(64 * t.wpb));
   // gx and gw as two launches (each wave holds one role's registers; the
-  // second gy read is an L2 / MALL hit for the small planes).  Partials that
-  // the gw launch cannot finish itself (no counters, or more than
-  // kHandoffMaxG blocks per channel) are summed by the gx launch that follows
-  // it (its block ch, wave 0, before its own units), else by dw_wsum_kernel.
-  const bool sum = gw && t.G > 1 && (!cnt || t.G > kHandoffMaxG);
+  // second gy read is an L2 / MALL hit for the small planes).  A channel
+  // split over G > 1 blocks leaves G partials that the gx launch following
+  // it sums (its block ch, wave 0, before its own units), else
+  // dw_wsum_kernel: the kernel boundary orders the partials' stores before
+  // their loads, so no cross-block hand-off (and no L2 flush) is needed.
+  const bool sum = gw && t.G > 1;
   if (gw)
     MDE_LAUNCH(K_DW_BWD, gx ? 0.0 : bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 2>), grid,
-               block, 0, gy, x, wt, gx, dst, gw, cnt, d, t, (int)n);
+               block, 0, gy, x, wt, gx, dst, gw, d, t, (int)n);
   if (gx) {
     DwStream tf = t;
     tf.fold = sum ? 1 : 0;
     MDE_LAUNCH(K_DW_BWD, bytes, st, (dw_bwd_stream_kernel<K, S, V, RB, EDGE, 1>), grid, block, 0,
-               gy, x, wt, gx, dst, gw, cnt, d, tf, (int)n);
+               gy, x, wt, gx, dst, gw, d, tf, (int)n);
   } else if (sum) {
     MDE_LAUNCH(K_DW_WREDUCE, 4.0 * d.c * t.G * K * K, st, dw_wsum_kernel<K>,
                dim3((unsigned)d.c), dim3(64), 0, part, gw, t.G);
@@ -1136,12 +1102,12 @@ int launch_bwd_stream(const float* gy, const float* x, const float* wt, float* g
 
 template <int K, int S>
 int launch_bwd(const float* gy, const float* x, const float* wt, float* gx, float* gw,
-               float* part, unsigned* cnt, int64_t n, const DwShape& d, hipStream_t st) {
+               float* part, int64_t n, const DwShape& d, hipStream_t st) {
   if (stream_ok(d, K, S)) {
     const DwCfg c = stream_cfg(S, d);
     const DwStream t = stream_bwd_layout(n, d, c);
     return with_cfg<S>(c, [&]<int V, int RB, bool EDGE>() {
-      return launch_bwd_stream<K, S, V, RB, EDGE>(gy, x, wt, gx, gw, part, cnt, n, d, t, st);
+      return launch_bwd_stream<K, S, V, RB, EDGE>(gy, x, wt, gx, gw, part, n, d, t, st);
     });
   }
   if (d.pad == K / 2) return launch_bwd_strip<K, S>(gy, x, wt, gx, gw, part, n, d, st);
@@ -1205,7 +1171,7 @@ int mde_dwconv_fwd(const void* x, const float* weight, void* y, int64_t n, int64
 
 int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx, float* gweight,
                    int64_t n, int64_t c, int64_t h, int64_t w, int64_t k, int64_t stride,
-                   int64_t pad, void* workspace, uint32_t* counters, int dtype, void* stream) {
+                   int64_t pad, void* workspace, int dtype, void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !dw_ok(n, c, h, w, k, stride, pad) || (gx && !weight) ||
       (gweight && (!x || (!workspace && mde_dwconv_workspace(n, c, h, w, k, stride, pad) > 0))))
@@ -1216,11 +1182,10 @@ int mde_dwconv_bwd(const void* gy, const void* x, const float* weight, void* gx,
   const float* xp = (const float*)x;
   float* gxp = (float*)gx;
   float* part = (float*)workspace;
-  unsigned* cnt = (unsigned*)counters;
-  if (k == 3 && stride == 1) return launch_bwd<3, 1>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
-  if (k == 3 && stride == 2) return launch_bwd<3, 2>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
-  if (k == 5 && stride == 1) return launch_bwd<5, 1>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
-  return launch_bwd<5, 2>(g, xp, weight, gxp, gweight, part, cnt, n, d, st);
+  if (k == 3 && stride == 1) return launch_bwd<3, 1>(g, xp, weight, gxp, gweight, part, n, d, st);
+  if (k == 3 && stride == 2) return launch_bwd<3, 2>(g, xp, weight, gxp, gweight, part, n, d, st);
+  if (k == 5 && stride == 1) return launch_bwd<5, 1>(g, xp, weight, gxp, gweight, part, n, d, st);
+  return launch_bwd<5, 2>(g, xp, weight, gxp, gweight, part, n, d, st);
 }
 
 }  // extern "C"

@@ -284,90 +284,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// The four per-sample FC backward kernels above (se_bfc1/2/3 + se_wgrad) as
-// ONE single-block launch for the small SE layers of the training path
-// (GuideDepth c = cr <= 64 at n = 32: n*c, n*cr <= 4096): dz and dh stay in
-// LDS.  Every output keeps its kernel's summation order (lane-strided +
-// wave butterfly, the weight gradients' sequential sample loop), so the
-// results are bitwise those of the four launches.
-constexpr int kFcAllMax = 4096;  // n*c and n*cr limit (2 x 16 KB of LDS)
-
-__global__ void __launch_bounds__(1024)
-    se_bfc_all_kernel(const float* __restrict__ part, int chunks, int n, int c, int cr,
-                      const float* __restrict__ w1, const float* __restrict__ w2,
-                      const float* __restrict__ b2, int gate, const float* __restrict__ s,
-                      const float* __restrict__ hidden, const float* __restrict__ mean,
-                      float* __restrict__ dm, float* __restrict__ gw1, float* __restrict__ gw2,
-                      float* __restrict__ gb1, float* __restrict__ gb2) {
-  __shared__ float dz[kFcAllMax], dh[kFcAllMax];
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int o = wid; o < n * c; o += nw) {  // dz (se_bfc1_kernel)
-    const int nidx = o / c, ch = o - nidx * c;
-    const float* p = part + (int64_t)o * chunks;
-    float ds = 0.f;
-    for (int k = lane; k < chunks; k += 64) ds += p[k];
-    ds = mde::wave_sum(ds);
-    float v;
-    if (gate == 0) {
-      const float sv = s[o];
-      v = ds * (sv * (1.f - sv));
-    } else {
-      const float* wr = w2 + (int64_t)ch * cr;
-      float zz = 0.f;
-      for (int j = lane; j < cr; j += 64) zz += wr[j] * hidden[(int64_t)nidx * cr + j];
-      zz = mde::wave_sum(zz);
-      if (b2) zz += b2[ch];
-      v = (zz > -3.f && zz < 3.f) ? ds / 6.f : 0.f;
-    }
-    if (lane == 0) dz[o] = v;
-  }
-  __syncthreads();
-  for (int o = wid; o < n * cr; o += nw) {  // dh (se_bfc2_kernel)
-    const int nidx = o / cr, j = o - nidx * cr;
-    float acc = 0.f;
-    for (int ch = lane; ch < c; ch += 64) acc += w2[(int64_t)ch * cr + j] * dz[nidx * c + ch];
-    acc = mde::wave_sum(acc);
-    if (lane == 0) dh[o] = hidden[o] > 0.f ? acc : 0.f;
-  }
-  __syncthreads();
-  for (int o = wid; o < n * c; o += nw) {  // dm (se_bfc3_kernel)
-    const int nidx = o / c, ch = o - nidx * c;
-    float acc = 0.f;
-    for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * dh[nidx * cr + j];
-    acc = mde::wave_sum(acc);
-    if (lane == 0) dm[o] = acc;
-  }
-  // weight / bias gradients (se_wgrad_kernel)
-  const int pairs = c * cr;
-  for (int t = threadIdx.x; t < 2 * pairs || t < c || t < cr; t += blockDim.x) {
-    if (gb2 && t < c) {
-      float acc = 0.f;
-      for (int k = 0; k < n; ++k) acc += dz[k * c + t];
-      gb2[t] = acc;
-    }
-    if (gb1 && t < cr) {
-      float acc = 0.f;
-      for (int k = 0; k < n; ++k) acc += dh[k * cr + t];
-      gb1[t] = acc;
-    }
-    if (t < pairs) {
-      const int ch = t / cr, j = t % cr;
-      float acc = 0.f;
-      for (int k = 0; k < n; ++k) acc += dz[k * c + ch] * hidden[(int64_t)k * cr + j];
-      gw2[t] = acc;
-    } else if (t < 2 * pairs) {
-      const int u = t - pairs, j = u / c, ch = u % c;
-      float acc = 0.f;
-      for (int k = 0; k < n; ++k) acc += dh[k * cr + j] * mean[(int64_t)k * c + ch];
-      gw1[u] = acc;
-    }
-  }
-}
-
-inline bool fc_all_ok(int64_t n, int64_t c, int64_t cr) {
-  return n * c <= kFcAllMax && n * cr <= kFcAllMax;
-}
-
 // gx = g * s + dm / hw, written to gxa / gxb (either may be null).
 __global__ void __launch_bounds__(256)
     se_apply_kernel(const float* __restrict__ g, int64_t ca, int64_t cb,
@@ -593,17 +509,12 @@ SeWs se_carve(void* ws, int64_t n, int64_t c, int64_t cr, int64_t hw) {
   return r;
 }
 
-// The per-sample FC backward + weight gradients: one launch when the layer
-// is small (se_bfc_all_kernel), else the four kernels.
+// The per-sample FC backward + weight gradients: four launches.  (A
+// one-block fused variant was measured at 156 us per SE layer vs 42 us for
+// these four: a single block serialises the n*c partial-sum reductions.)
 int se_bfc(const SeWs& ws, int chunks, int64_t n, int64_t c, int64_t cr, const float* w1,
            const float* w2, const float* b2, int gate, const float* s, const float* hidden,
            const float* mean, float* gw1, float* gw2, float* gb1, float* gb2, hipStream_t st) {
-  if (fc_all_ok(n, c, cr)) {
-    MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (3.0 * c * cr + n * (3.0 * c + 2.0 * cr + chunks * c)),
-               st, se_bfc_all_kernel, dim3(1), dim3(1024), 0, ws.part, chunks, (int)n, (int)c,
-               (int)cr, w1, w2, b2, gate, s, hidden, mean, ws.dm, gw1, gw2, gb1, gb2);
-    return MDE_OK;
-  }
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + 3.0 * n * c), st, se_bfc1_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
              sizeof(float) * cr, ws.part, chunks, (int)c, (int)cr, w2, b2, gate, s, hidden,

@@ -810,26 +810,6 @@ class BatchNorm2d(nn.BatchNorm2d):
         return super().extra_repr() + f", act={self.act}"
 
 
-_COUNTERS: dict = {}
-_RETIRED_COUNTERS: list = []
-
-
-def _zeroed_counters(n: int, device) -> torch.Tensor:
-    """A persistent all-zero uint32 buffer of >= n entries per device, for the
-    kernels' last-block tickets (each kernel leaves its counters zero again).
-    Allocated once, outside any graph capture in practice (the first call is an
-    eager warm-up step); calls on one stream never overlap.  A buffer replaced
-    by a larger one stays alive: a graph captured earlier still addresses it,
-    and its replays must not touch memory the caching allocator reissued."""
-    buf = _COUNTERS.get(device)
-    if buf is None or buf.numel() < n:
-        if buf is not None:
-            _RETIRED_COUNTERS.append(buf)
-        buf = torch.zeros(max(n, 4096), dtype=torch.int32, device=device)
-        _COUNTERS[device] = buf
-    return buf
-
-
 class _DWConv(torch.autograd.Function):
     @staticmethod
     @_amp_fwd
@@ -858,7 +838,6 @@ class _DWConv(torch.autograd.Function):
         if gx is not None or gw is not None:
             _abi.call("mde_dwconv_bwd", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(weight), _abi.ptr(gx),
                       _abi.ptr(gw), n, c, h, w, k, stride, pad, _abi.ptr(ws),
-                      _abi.ptr(_zeroed_counters(c, x.device)) if gw is not None else None,
                       _abi.dtype_code(gy), _abi.stream_of(gy))
         return gx, gw, None, None, None
 

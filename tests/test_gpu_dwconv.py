@@ -92,9 +92,9 @@ def test_dwconv_single_gradient(which):
 @pytest.mark.parametrize("n,c,h,w,k,s", [(16, 64, 240, 320, 3, 2), (16, 16, 240, 320, 3, 1),
                                          (16, 120, 60, 80, 5, 1)])
 def test_dwconv_weight_grad_many_blocks(n, c, h, w, k, s):
-    """cfg4 batch: a channel's weight gradient is split over many blocks and
-    summed by the channel's last block (counters hand-off).  Two calls must
-    agree bitwise (fixed-order sum, counters left zero) and match float64."""
+    """cfg4 batch: a channel's weight gradient is split over many blocks whose
+    partials the following launch sums.  Two calls must agree bitwise
+    (fixed-order sum) and match float64."""
     from monocular_depth_estimation_amd.nn import depthwise_conv2d
     conv = torch.nn.Conv2d(c, c, k, s, k // 2, groups=c, bias=False)
     with torch.no_grad():

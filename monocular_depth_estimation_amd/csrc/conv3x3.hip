@@ -522,11 +522,13 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
-// Weight-gradient reduction, two launches, fixed summation order: stage 1
-// (block (x, s, grp)) sums partials s, s + S, ... of its 256 elements into
-// slice s; stage 2 sums the S slices in order and scatters them to gw.  (A
-// one-launch last-block hand-off was measured slower: its agent-scope release
-// fences write back L2 on every block, 53 vs 21 us per weight gradient.)
+// Weight-gradient reduction, one launch, fixed summation order: block
+// (x, grp) owns 64 elements; its 16 waves sum the interleaved partial subsets
+// b = w, w + 16, ... (four accumulators per lane, so 16 loads per lane are in
+// flight), then wave 0 adds the 16 subset sums in order and scatters them to
+// gw.  (Two launches of 256-thread blocks spent ~11 us each, latency-bound;
+// a one-launch last-block hand-off between blocks needs agent-scope fences,
+// which write back L2 on every block: 53 us.)
 struct ReduceMap {
   int wide;             // 1: the wide-channel layout [co 64][tap 9][ci 32] per group
   int np, cip;          // regular layout [co][n = tap * cip + ci] (np columns)
@@ -544,59 +546,47 @@ __device__ __forceinline__ int64_t gw_index(const ReduceMap& r, int grp, int e) 
   return ((int64_t)co * r.ci_n + ci) * 9 + tap;
 }
 
-__global__ void __launch_bounds__(256)
-    wgrad_reduce1_kernel(const float* __restrict__ part, float* __restrict__ part2, int g,
-                         int m) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= m) return;
-  const int s = blockIdx.y, ns = gridDim.y, grp = blockIdx.z;
-  const float* pg = part + (int64_t)grp * g * m;
-  float a0 = 0.f, a1 = 0.f;
-  int b = s;
-  for (; b + ns < g; b += 2 * ns) {
-    a0 += pg[(int64_t)b * m + e];
-    a1 += pg[(int64_t)(b + ns) * m + e];
+constexpr int kRedWaves = 16;
+
+__global__ void __launch_bounds__(64 * kRedWaves)
+    wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ gw, int g, int m,
+                        ReduceMap map) {
+  __shared__ float red[kRedWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane, grp = blockIdx.y;
+  const float* pg = part + (int64_t)grp * g * m + e;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  if (e < m) {
+    int b = wv;
+#pragma unroll 4
+    for (; b + 3 * kRedWaves < g; b += 4 * kRedWaves) {
+      a0 += pg[(int64_t)b * m];
+      a1 += pg[(int64_t)(b + kRedWaves) * m];
+      a2 += pg[(int64_t)(b + 2 * kRedWaves) * m];
+      a3 += pg[(int64_t)(b + 3 * kRedWaves) * m];
+    }
+    for (; b < g; b += kRedWaves) a0 += pg[(int64_t)b * m];
   }
-  if (b < g) a0 += pg[(int64_t)b * m + e];
-  part2[((int64_t)grp * ns + s) * m + e] = a0 + a1;
-}
-
-__global__ void __launch_bounds__(256)
-    wgrad_reduce2_kernel(const float* __restrict__ part2, float* __restrict__ gw, int ns, int m,
-                         ReduceMap map) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= m) return;
-  const int grp = blockIdx.y;
-  const float* p2 = part2 + (int64_t)grp * ns * m;
-  float a = 0.f;
-  for (int k = 0; k < ns; ++k) a += p2[(int64_t)k * m + e];
+  red[wv][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wv != 0 || e >= m) return;
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < kRedWaves; ++k) sum += red[k][lane];
   const int64_t o = gw_index(map, grp, e);
-  if (o >= 0) gw[o] = a;
+  if (o >= 0) gw[o] = sum;
 }
 
-constexpr int kReduceSplit = 32;
-
-// Weight-gradient workspace: [partials: groups x g x m][slices: groups x split x m].
-struct WsLayout {
-  float* part;
-  float* part2;
-};
-
-inline size_t wgrad_ws_bytes(int groups, int g, int split, int m) {
-  return sizeof(float) * (size_t)groups * ((size_t)g + (size_t)split) * (size_t)m;
+// Weight-gradient workspace: the partials, [groups][g][m].
+inline size_t wgrad_ws_bytes(int groups, int g, int m) {
+  return sizeof(float) * (size_t)groups * (size_t)g * (size_t)m;
 }
 
-inline WsLayout wgrad_ws(float* ws, int groups, int g, int split, int m) {
-  return {ws, ws + (int64_t)groups * g * m};
-}
-
-inline int launch_reduce(const WsLayout& l, float* gw, int groups, int g, int split, int m,
+inline int launch_reduce(const float* part, float* gw, int groups, int g, int m,
                          const ReduceMap& map, hipStream_t s) {
-  const unsigned bx = (unsigned)mde::cdiv(m, 256);
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)(g + split) * m, s, wgrad_reduce1_kernel,
-             dim3(bx, split, groups), dim3(256), 0, l.part, l.part2, g, m);
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)split * m + 4.0 * groups * m, s,
-             wgrad_reduce2_kernel, dim3(bx, groups), dim3(256), 0, l.part2, gw, split, m, map);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)g * m + 4.0 * groups * m, s,
+             wgrad_reduce_kernel, dim3((unsigned)mde::cdiv(m, 64), groups),
+             dim3(64 * kRedWaves), 0, part, gw, g, m, map);
   return MDE_OK;
 }
 
@@ -772,82 +762,93 @@ __global__ void __launch_bounds__(256, 1)
     for (int i = 0; i < 4; ++i) out[(16 * wv + 4 * lk + i) * (9 * kWCI) + 16 * nt + li] = acc[nt][i];
 }
 
-// Fixed-width variant (w == W, W % 4 == 0, tiles of TH whole rows): a K step's
-// four pixels never straddle a row, so with the K loop fully unrolled every
-// operand address is a per-lane base plus a compile-time offset (no pixel
-// table, no address arithmetic), and the LDS is sized to the tile (<= 80 KB)
-// so that two blocks share a CU.  Same partial layout as the generic kernel.
-template <int W, int TH>
+// Fixed-strip variant (w a multiple of SW, SW % 4 == 0; tiles of TH rows x
+// SW columns): a K step's four pixels never straddle a row, so with the K
+// loop fully unrolled every operand address is a per-lane base plus a
+// compile-time offset (no pixel table, no address arithmetic), and the LDS is
+// sized to the tile (<= 80 KB) so that two blocks share a CU.  A strip's halo
+// columns are the neighbouring strips' pixels (zero only at the image edge).
+// Same partial layout as the generic kernel.
+template <int SW, int TH>
 struct WideT {
-  static constexpr int W2 = W + 2, K = TH * W, XE = (TH + 2) * W2;
+  static constexpr int W2 = SW + 2, K = TH * SW, XE = (TH + 2) * W2;
   static constexpr int PX = (XE - 2 + 31) / 32 * 32 + 2;  // >= XE, = 2 mod 32
   static constexpr int PG = (K - 2 + 31) / 32 * 32 + 2;   // >= K, = 2 mod 32
   static constexpr int XL = (XE + 63) / 64, GL = (K + 63) / 64;
   static constexpr int SX = kWCI * PX, SMEM = SX + kWCO * PG;
-  static_assert(W % 4 == 0 && SMEM * 4 <= 80 * 1024, "two blocks per CU");
+  static_assert(SW % 4 == 0 && SMEM * 4 <= 80 * 1024, "two blocks per CU");
 };
 
-template <int W, int TH>
-__global__ void __launch_bounds__(256, 2)
+// WPB waves per block: 4 (wave w = output-channel tile w x all 18 N tiles)
+// or 8 (wave w = output-channel tile w & 3 x the 9 N tiles of input-channel
+// half w >> 2: half the accumulators and staging registers per wave, so four
+// waves per SIMD fit; measured 134.7 vs 140.4 us at 64->64 32x60x80).
+template <int SW, int TH, int WPB>
+__global__ void __launch_bounds__(64 * WPB, 2)
     conv3x3_wgrad_wide_fixed_kernel(const float* __restrict__ x, const float* __restrict__ gy,
-                                    float* __restrict__ part, int ci_n, int co_n, int h,
-                                    int tiles_per_img, int ntiles) {
-  using P = WideT<W, TH>;
+                                    float* __restrict__ part, int ci_n, int co_n, int h, int w,
+                                    int tiles_w, int tiles_per_img, int ntiles) {
+  using P = WideT<SW, TH>;
+  static_assert(WPB == 4 || WPB == 8, "waves per block");
+  constexpr int NTW = WPB == 4 ? kWNT : kWNT / 2;  // N tiles per wave
+  constexpr int XC = kWCI / WPB, GC = kWCO / WPB;  // channels staged per wave
   __shared__ float sm[P::SMEM];
   float* sx = sm;
   float* sg = sm + P::SX;
   const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cot = WPB == 4 ? wv : (wv & 3), hsel = WPB == 4 ? 0 : (wv >> 2);
   const int ngo = co_n / kWCO;
   const int cog = blockIdx.y % ngo, cig = blockIdx.y / ngo;
-  const int hw = h * W;
+  const int hw = h * w;
+  // staged element e = lane + 64 i of a channel's plane: tile row xrr - 1,
+  // tile column xcc (-1 .. SW); gy element p: tile row gpr, column gpc
   int xcc[P::XL], xrr[P::XL], gpr[P::GL], gpc[P::GL];
-  unsigned xcol = 0;  // bit i: element i is an image column (not the zero border)
 #pragma unroll
   for (int i = 0; i < P::XL; ++i) {
     const int e = lane + 64 * i;
-    const int rr = e / P::W2, cc = e - rr * P::W2;
+    const int rr = e / P::W2;
     xrr[i] = e < P::XE ? rr : -4096;
-    xcc[i] = clampi(cc - 1, 0, W - 1);  // clamped: the border columns load a real element
-    xcol |= (cc >= 1 && cc <= W) ? 1u << i : 0u;
+    xcc[i] = e - rr * P::W2 - 1;
   }
 #pragma unroll
   for (int i = 0; i < P::GL; ++i) {
     const int p = lane + 64 * i < P::K ? lane + 64 * i : P::K - 1;
-    gpr[i] = p / W;
-    gpc[i] = p % W;
+    gpr[i] = p / SW;
+    gpc[i] = p % SW;
   }
-  f4 acc[kWNT];
+  f4 acc[NTW];
 #pragma unroll
-  for (int nt = 0; nt < kWNT; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
-  const float* xg = x + ((int64_t)cig * kWCI + 8 * wv) * hw;
-  const float* gg = gy + ((int64_t)cog * kWCO + 16 * wv) * hw;
-  float vx[8][P::XL], vg[16][P::GL];
+  for (int nt = 0; nt < NTW; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
+  const float* xg = x + ((int64_t)cig * kWCI + XC * wv) * hw;
+  const float* gg = gy + ((int64_t)cog * kWCO + GC * wv) * hw;
+  float vx[XC][P::XL], vg[GC][P::GL];
   unsigned xm = 0, gm = 0;
   auto load = [&](int tile) {
-    const int img = tile / tiles_per_img, r0 = (tile - img * tiles_per_img) * TH;
+    const int img = tile / tiles_per_img, t = tile - img * tiles_per_img;
+    const int r0 = (t / tiles_w) * TH, c0 = (t % tiles_w) * SW;
     const float* xi = xg + (int64_t)img * ci_n * hw;
     const float* gi = gg + (int64_t)img * co_n * hw;
     // clamped coordinates (see the generic kernel): no uniform fallback address
     xm = 0;
 #pragma unroll
     for (int i = 0; i < P::XL; ++i) {
-      const int gr = r0 - 1 + xrr[i];
-      const bool ok = gr >= 0 && gr < h && ((xcol >> i) & 1u);
+      const int gr = r0 - 1 + xrr[i], gc = c0 + xcc[i];
+      const bool ok = gr >= 0 && gr < h && gc >= 0 && gc < w;
       xm |= ok ? 1u << i : 0u;
-      const int o = clampi(gr, 0, h - 1) * W + xcc[i];
+      const int o = clampi(gr, 0, h - 1) * w + clampi(gc, 0, w - 1);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) vx[c][i] = xi[(unsigned)(c * hw + o)];
+      for (int c = 0; c < XC; ++c) vx[c][i] = xi[(unsigned)(c * hw + o)];
     }
     gm = 0;
 #pragma unroll
     for (int i = 0; i < P::GL; ++i) {
       const int p = lane + 64 * i;
-      const bool ok = p < P::K && r0 + p / W < h;
+      const bool ok = p < P::K && r0 + p / SW < h;
       gm |= ok ? 1u << i : 0u;
-      const int o = clampi(r0 + gpr[i], 0, h - 1) * W + gpc[i];
+      const int o = clampi(r0 + gpr[i], 0, h - 1) * w + c0 + gpc[i];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) vg[c][i] = gi[(unsigned)(c * hw + o)];
+      for (int c = 0; c < GC; ++c) vg[c][i] = gi[(unsigned)(c * hw + o)];
     }
   };
   int tile = blockIdx.x;
@@ -859,7 +860,7 @@ __global__ void __launch_bounds__(256, 2)
       const int e = lane + 64 * i;
       if (e < P::XE) {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) sx[(8 * wv + c) * P::PX + e] = (xm >> i) & 1u ? vx[c][i] : 0.f;
+        for (int c = 0; c < XC; ++c) sx[(XC * wv + c) * P::PX + e] = (xm >> i) & 1u ? vx[c][i] : 0.f;
       }
     }
 #pragma unroll
@@ -867,65 +868,71 @@ __global__ void __launch_bounds__(256, 2)
       const int p = lane + 64 * i;
       if (p < P::K) {
 #pragma unroll
-        for (int c = 0; c < 16; ++c) sg[(16 * wv + c) * P::PG + p] = (gm >> i) & 1u ? vg[c][i] : 0.f;
+        for (int c = 0; c < GC; ++c) sg[(GC * wv + c) * P::PG + p] = (gm >> i) & 1u ? vg[c][i] : 0.f;
       }
     }
     __syncthreads();
     if (tile + (int)gridDim.x < ntiles) load(tile + gridDim.x);
-    const float* xb = sx + li * P::PX + lk;
-    const float* gb = sg + (16 * wv + li) * P::PG + lk;
+    const float* xb = sx + (16 * hsel + li) * P::PX + lk;
+    const float* gb = sg + (16 * cot + li) * P::PG + lk;
 #pragma unroll 5
     for (int st = 0; st < P::K / 4; ++st) {
-      const int so = (4 * st / W) * P::W2 + (4 * st) % W;  // the step's first pixel
+      const int so = (4 * st / SW) * P::W2 + (4 * st) % SW;  // the step's first pixel
       const float a = gb[4 * st];
 #pragma unroll
-      for (int nt = 0; nt < kWNT; ++nt) {
-        const int tap = nt >> 1;
-        acc[nt] = mfma4(a, xb[(nt & 1) * 16 * P::PX + (tap / 3) * P::W2 + tap % 3 + so], acc[nt]);
+      for (int nt = 0; nt < NTW; ++nt) {
+        const int tap = WPB == 4 ? nt >> 1 : nt, half = WPB == 4 ? nt & 1 : 0;
+        acc[nt] = mfma4(a, xb[half * 16 * P::PX + (tap / 3) * P::W2 + tap % 3 + so], acc[nt]);
       }
     }
   }
+  // lane: co = 16 cot + 4 lk + i, n = 32 tap + 16 half + li
   float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWM;
 #pragma unroll
-  for (int nt = 0; nt < kWNT; ++nt)
+  for (int nt = 0; nt < NTW; ++nt) {
+    const int col = WPB == 4 ? 16 * nt + li : 16 * (2 * nt + hsel) + li;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) out[(16 * wv + 4 * lk + i) * (9 * kWCI) + 16 * nt + li] = acc[nt][i];
+    for (int i = 0; i < 4; ++i) out[(16 * cot + 4 * lk + i) * (9 * kWCI) + col] = acc[nt][i];
+  }
 }
 
-// Fixed-width tile heights: K = 80 pixels (K = 160 spills).
-inline int wide_fixed_th(int64_t w) { return w == 80 ? 1 : (w == 40 ? 2 : (w == 20 ? 4 : 0)); }
+// Fixed-strip geometry: (strip width, tile rows) with K = 80 pixels (K = 160
+// spills at four waves per SIMD), or 0.
+inline int wide_fixed_sw(int64_t w) {
+  return w % 80 == 0 ? 80 : (w == 40 ? 40 : (w == 20 ? 20 : 0));
+}
 
 struct WidePlan {
   WideGeo g;
-  int groups, gx, split;
-  int fixed_th;  // > 0: the fixed-width kernel (whole-row tiles of fixed_th rows)
+  int groups, gx;
+  int fixed_sw;  // > 0: the fixed-strip kernel (tiles of 80 / fixed_sw rows x fixed_sw columns)
 };
 
 inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WidePlan* p) {
   if (ci % kWCI || co % kWCO || ci < kWCI || co < kWCO) return false;
   if (!wide_geo(n, h, w, &p->g)) return false;
-  p->fixed_th = wide_fixed_th(w);
-  if (p->fixed_th) {  // whole-row tiles of fixed_th rows
-    const int64_t tpi = mde::cdiv(h, p->fixed_th), nt = n * tpi;
+  p->fixed_sw = wide_fixed_sw(w);
+  if (p->fixed_sw) {  // tiles of 80 / fixed_sw rows x fixed_sw columns
+    const int th = 80 / p->fixed_sw, tw = (int)(w / p->fixed_sw);
+    const int64_t tpi = mde::cdiv(h, th) * tw, nt = n * tpi;
     if (nt > 0x7fffffff) return false;
-    p->g.th = p->fixed_th;
-    p->g.wc = (int)w;
-    p->g.tiles_w = 1;
+    p->g.th = th;
+    p->g.wc = p->fixed_sw;
+    p->g.tiles_w = tw;
     p->g.tiles_per_img = (int)tpi;
     p->g.ntiles = (int)nt;
   }
   p->groups = (int)((ci / kWCI) * (co / kWCO));
   // one 100 KB-LDS block per CU (generic), two <= 80 KB blocks (fixed width)
-  int gx = (p->fixed_th ? 512 : 256) / p->groups;
+  int gx = (p->fixed_sw ? 512 : 256) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;
-  p->split = gx < kReduceSplit ? gx : kReduceSplit;
   return true;
 }
 
 inline size_t wide_workspace(const WidePlan& p) {
-  return wgrad_ws_bytes(p.groups, p.gx, p.split, kWM);
+  return wgrad_ws_bytes(p.groups, p.gx, kWM);
 }
 
 int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int64_t ci,
@@ -934,23 +941,35 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
   if (!wide_plan(n, ci, co, h, w, &p)) return MDE_ERR_UNSUPPORTED;
   const double flops = 2.0 * 9 * ci * co * (double)(n * h * w);
   const double bytes = 4.0 * n * h * w * (double)(ci + co);
-  const WsLayout l = wgrad_ws(ws, p.groups, p.gx, p.split, kWM);
   const dim3 grid(p.gx, p.groups);
-  const int tpi = p.g.tiles_per_img, nt = p.g.ntiles;
-  if (w == 80)
-    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<80, 1>),
-                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt);
-  else if (w == 40)
-    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<40, 2>),
-                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt);
-  else if (w == 20)
-    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<20, 4>),
-                    grid, dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, tpi, nt);
+  const int tpi = p.g.tiles_per_img, nt = p.g.ntiles, tw = p.g.tiles_w;
+  // MDE_WIDE_WPB=4 selects the 4-wave layout (A/B measurement only)
+  static const int wpb = [] {
+    const char* e = std::getenv("MDE_WIDE_WPB");
+    return e ? std::atoi(e) : 8;
+  }();
+#define MDE_WIDE_FIXED(WW, TT)                                                                  \
+  do {                                                                                          \
+    if (wpb == 4)                                                                               \
+      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s,                                         \
+                      (conv3x3_wgrad_wide_fixed_kernel<WW, TT, 4>), grid, dim3(256), 0, x, gy,  \
+                      ws, (int)ci, (int)co, (int)h, (int)w, tw, tpi, nt);                   \
+    else                                                                                        \
+      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s,                                         \
+                      (conv3x3_wgrad_wide_fixed_kernel<WW, TT, 8>), grid, dim3(512), 0, x, gy,  \
+                      ws, (int)ci, (int)co, (int)h, (int)w, tw, tpi, nt);                   \
+  } while (0)
+  if (p.fixed_sw == 80)
+    MDE_WIDE_FIXED(80, 1);
+  else if (p.fixed_sw == 40)
+    MDE_WIDE_FIXED(40, 2);
+  else if (p.fixed_sw == 20)
+    MDE_WIDE_FIXED(20, 4);
   else
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
-                    dim3(256), 0, x, gy, l.part, (int)ci, (int)co, (int)h, (int)w, p.g);
-  return launch_reduce(l, gw, p.groups, p.gx, p.split, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co},
-                       s);
+                    dim3(256), 0, x, gy, ws, (int)ci, (int)co, (int)h, (int)w, p.g);
+#undef MDE_WIDE_FIXED
+  return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co}, s);
 }
 
 // ====================================================================== bf16
@@ -1452,29 +1471,27 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
                  float* ws, double bytes, hipStream_t s) {
   const WgradPlan p = wgrad_plan<CI, CO, TH, PW>(n, h, w);
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
-  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-  const WsLayout l = wgrad_ws(ws, 1, p.grid, split, p.m);
   // the 3-channel guide convs' weight gradients have ~12 flop per byte, under the
   // fp32 MFMA ridge (157 TF / 8 TB/s ~ 20): timed as HBM-bound under their own id
   if (CI == 3) {
     if (w % kTW == 0)
       MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
-                 dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                 dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                  p.tiles_per_img, p.ntiles);
     else
       MDE_LAUNCH(mde::K_C3_WGRAD_GUIDE, bytes, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
-                 dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                 dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                  p.tiles_per_img, p.ntiles);
   } else if (w % kTW == 0) {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, true>),
-                    dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                    dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                     p.tiles_per_img, p.ntiles);
   } else {
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_kernel<CI, CO, TH, PW, false>),
-                    dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                    dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                     p.tiles_per_img, p.ntiles);
   }
-  return launch_reduce(l, gw, 1, p.grid, split, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
+  return launch_reduce(ws, gw, 1, p.grid, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
 
 // ---- bf16 dispatch
@@ -1527,12 +1544,10 @@ int launch_bf_wgrad(const bf16* x, const bf16* gy, float* gw, int64_t n, int64_t
   const WgradPlan p = bf_wgrad_plan<CI, CO, TH, PW>(n, h, w);
   if (p.grid <= 0) return MDE_ERR_INVALID_ARG;
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
-  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-  const WsLayout l = wgrad_ws(ws, 1, p.grid, split, p.m);
   MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
-                  dim3(p.grid), dim3(256), 0, x, gy, l.part, (int)h, (int)w, p.tiles_w,
+                  dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                   p.tiles_per_img, p.ntiles);
-  return launch_reduce(l, gw, 1, p.grid, split, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
+  return launch_reduce(ws, gw, 1, p.grid, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
 
 // bf16 shapes: 16 -> 16 and 32 -> 32, every pass; 4-column chunks need w % 4 == 0
@@ -1704,8 +1719,7 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   if (dtype == MDE_BF16) {
     if (!bf_supported(cin, cout) || !dims_ok(n, h, w)) return 0;
     p = cin == 16 ? bf_wgrad_plan<16, 16, 4, 4>(n, h, w) : bf_wgrad_plan<32, 32, 2, 2>(n, h, w);
-    const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-    return wgrad_ws_bytes(1, p.grid, split, p.m);
+    return wgrad_ws_bytes(1, p.grid, p.m);
   }
   if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
   if (wide(cin, cout)) {
@@ -1721,8 +1735,7 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   else if (variant() == 1) p = wgrad_plan<32, 32, 4, 2>(n, h, w);
   else if (variant() == 2) p = wgrad_plan<32, 32, 4, 1>(n, h, w);
   else p = wgrad_plan<32, 32, 2, 2>(n, h, w);
-  const int split = p.grid < kReduceSplit ? p.grid : kReduceSplit;
-  return wgrad_ws_bytes(1, p.grid, split, p.m);
+  return wgrad_ws_bytes(1, p.grid, p.m);
 }
 
 int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,

@@ -9,6 +9,8 @@ state_dict keys) are unchanged.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 from torch import nn
 
@@ -372,9 +374,10 @@ def pointwise_ok(conv: nn.Conv2d, x) -> bool:
 # (mde_conv3x3_*), per (cin, cout): (forward, data gradient, weight gradient).
 # The rest go to MIOpen, whose Winograd kernels are faster at >= 32 channels
 # (tools/kbench.py --only conv: HIP vs MIOpen per pass at the bench shapes).
-# DDRNet's 64/128/256-channel weight gradients stay on MIOpen for now: the
-# NCHW wide-channel kernel (mde_conv3x3_wgrad, cin % 32 == 0, cout % 64 == 0)
-# is exact but measured slower (tools/wgrad_bench.py: 57 vs 69-83 TF/s).
+# DDRNet's and the decoder's 64/128/256-channel weight gradients run on the
+# NCHW wide-channel kernel (cin % 32 == 0, cout % 64 == 0), which needs none
+# of MIOpen's NCHW <-> NHWC transposes (tools/wgrad_bench.py);
+# MDE_WIDE_WGRAD=0 sends them back to MIOpen (A/B measurement).
 CONV3X3_HIP = {
     (3, 16): (True, True, True),
     (3, 32): (True, True, True),
@@ -382,6 +385,9 @@ CONV3X3_HIP = {
     (16, 16): (True, True, True),
     (32, 32): (False, False, True),
 }
+if os.environ.get("MDE_WIDE_WGRAD", "1") != "0":
+    CONV3X3_HIP.update({(64, 64): (False, False, True), (128, 64): (False, False, True),
+                        (128, 128): (False, False, True), (256, 256): (False, False, True)})
 
 
 class _Conv3x3(torch.autograd.Function):

@@ -88,10 +88,14 @@ def test_conv3x3_full_size_vs_miopen(cin, cout, h, w):
 
 
 # Wide channels (DDRNet 64/128/256): weight gradient only; (n, h, w) cover
-# whole-row tiles at the cfg2 widths, a ragged last row tile, w > 126 (64-column
-# strips with a ragged last strip), one row, and a non-square channel pair.
+# the fixed-strip kernel at the cfg2 widths (80-column strips of one row, 40 /
+# 20 whole rows), 80-column strips side by side (160, 240: halo columns from
+# the neighbouring strip), a ragged last row tile, w > 126 off the strip
+# widths (generic 64-column strips with a ragged last strip), one row, and
+# non-square channel pairs.
 WIDE = [(64, 64, 2, 60, 80), (128, 128, 2, 30, 40), (256, 256, 2, 15, 20),
-        (64, 64, 1, 7, 130), (64, 64, 3, 1, 5), (32, 128, 1, 9, 21), (64, 64, 1, 33, 200)]
+        (64, 64, 1, 9, 160), (128, 64, 1, 5, 240), (64, 64, 1, 7, 130), (64, 64, 3, 1, 5),
+        (32, 128, 1, 9, 21), (64, 64, 1, 33, 200)]
 
 
 @pytest.mark.parametrize("cin,cout,n,h,w", WIDE)

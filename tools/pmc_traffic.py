@@ -46,7 +46,7 @@ NAMES = [
     (r"conv3x3_bf_wgrad_kernel", "conv3x3_wgrad"),
     (r"conv3x3_wgrad_kernel<3,", "conv3x3_wgrad_guide"),
     (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),
-    (r"wgrad_reduce[12]_kernel", "conv3x3_wreduce"),
+    (r"wgrad_reduce\w*_kernel", "conv3x3_wreduce"),
     (r"skip_fwd_kernel", "skip_reduce_fwd"),
     (r"skip_bwd_kernel", "skip_reduce_bwd"),
     (r"skip_slab_reduce_kernel", "skip_reduce_bwd_reduce"),

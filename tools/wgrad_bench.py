@@ -21,14 +21,16 @@ def timeit(fn, reps=20):
     return a.elapsed_time(b) / reps * 1e3
 
 
-for (n, c, h, w) in [(32, 64, 60, 80), (32, 128, 30, 40), (32, 256, 15, 20), (4, 64, 30, 40)]:
+tag = os.environ.get("MDE_WIDE_WPB", "8")
+for (n, c, co, h, w) in [(32, 64, 64, 60, 80), (32, 128, 128, 30, 40), (32, 256, 256, 15, 20),
+                         (32, 128, 64, 60, 80), (32, 64, 64, 120, 160), (4, 64, 64, 30, 40)]:
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
-    gy = torch.rand((n, c, h, w), device="cuda") - 0.5
-    wt = torch.rand((c, c, 3, 3), device="cuda")
+    gy = torch.rand((n, co, h, w), device="cuda") - 0.5
+    wt = torch.rand((co, c, 3, 3), device="cuda")
     gw = torch.empty_like(wt)
-    ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, c, c, h, w, 0), x)
+    ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, c, co, h, w, 0), x)
     st = _abi.stream_of(x)
-    hip = lambda: _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, c, c,
+    hip = lambda: _abi.call("mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, c, co,
                             h, w, _abi.ptr(ws), 0, st)
     mio = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (1, 1), (1, 1), False,
                                                       (0, 0), 1, (False, True, False))
@@ -36,6 +38,6 @@ for (n, c, h, w) in [(32, 64, 60, 80), (32, 128, 30, 40), (32, 256, 15, 20), (4,
     hip()
     ref = mio()[1]
     err = float((gw - ref).abs().max() / ref.abs().max())
-    fl = 2.0 * 9 * c * c * n * h * w
-    print(f"wgrad {c}->{c} {n}x{h}x{w}: HIP {th:7.1f} us ({fl / th / 1e6:5.1f} TF/s)  "
+    fl = 2.0 * 9 * c * co * n * h * w
+    print(f"[wpb {tag}] wgrad {c}->{co} {n}x{h}x{w}: HIP {th:7.1f} us ({fl / th / 1e6:5.1f} TF/s)  "
           f"MIOpen {tm:7.1f} us ({fl / tm / 1e6:5.1f} TF/s)  rel diff {err:.1e}", flush=True)

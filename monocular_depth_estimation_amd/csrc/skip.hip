@@ -329,7 +329,7 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 // T: storage type of g, r, d, gs (float, or bf16 under autocast; products
 // and sums in fp32 either way).
 template <int CI, int CO, bool HAS_D, bool BNR = false, bool BNS = false, typename T = float>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)  // 64 x 64: W^T + gW need > 256 registers
     skip_bwd_mfma_kernel(const T* __restrict__ g, const T* __restrict__ r,
                          const T* __restrict__ d, const float* __restrict__ wt,
                          T* __restrict__ gs, float* __restrict__ slab, int64_t n,
@@ -982,7 +982,7 @@ int mde_skip_reduce_bn_bwd(const void* gout, const void* r, const void* d, const
 // Bias-free 1x1 convolution (the conv feeding a BatchNorm whose bias is
 // folded), the MFMA kernels above with one input.
 #define MDE_PW_SHAPES(X) \
-  X(16, 8) X(16, 16) X(32, 16) X(32, 32) X(64, 32) X(32, 64) X(16, 32)
+  X(16, 8) X(16, 16) X(32, 16) X(32, 32) X(64, 32) X(32, 64) X(16, 32) X(64, 64)
 
 static bool pw_ok(int64_t n, int64_t cin, int64_t cout, int64_t hw) {
   if (n <= 0 || hw <= 0 || hw % 64 != 0) return false;

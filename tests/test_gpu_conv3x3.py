@@ -150,18 +150,20 @@ def test_conv3x3_unsupported_shape_raises():
 
 
 @pytest.mark.parametrize("train", [True, False])
-@pytest.mark.parametrize("cin,e,h,w", [(16, 16, 32, 64), (3, 32, 16, 48), (64, 64, 8, 64)])
-def test_fused_bn_relu_pointwise_branch_vs_float64(cin, e, h, w, train):
+@pytest.mark.parametrize("cin,e,eo,h,w", [(16, 16, 8, 32, 64), (3, 32, 16, 16, 48), (64, 64, 32, 8, 64),
+                                           (64, 64, 64, 8, 64)])
+def test_fused_bn_relu_pointwise_branch_vs_float64(cin, e, eo, h, w, train):
     """conv3x3 -> BN+ReLU -> 1x1 -> BN+ReLU (a guided-upsampling branch,
     modules.py:43-49) on the fused HIP path (BN1+ReLU inside the 1x1 conv's
     operand load) vs the same Sequential as plain torch modules in float64:
-    output, input gradient, every parameter gradient and the BN running stats."""
+    output, input gradient, every parameter gradient and the BN running stats.
+    e -> eo = 64 -> 64 is up_1's comb_conv (GuideDepth.py:21-33)."""
     import copy
 
     from monocular_depth_estimation_amd.GuideDepth.model.modules import _conv_bn_relu
     from monocular_depth_estimation_amd.nn import BatchNorm2d, run_sequential
     torch.manual_seed(cin + e + h)
-    seq = torch.nn.Sequential(*_conv_bn_relu(cin, e, 3), *_conv_bn_relu(e, e // 2, 1))
+    seq = torch.nn.Sequential(*_conv_bn_relu(cin, e, 3), *_conv_bn_relu(e, eo, 1))
     for m in seq.modules():
         if isinstance(m, BatchNorm2d):
             m.weight.data.uniform_(0.5, 1.5)
@@ -177,7 +179,7 @@ def test_fused_bn_relu_pointwise_branch_vs_float64(cin, e, h, w, train):
     ref.train(train)
     seq = seq.to(DEV).train(train)
     x = torch.rand((2, cin, h, w)) - 0.5
-    gy = torch.rand((2, e // 2, h, w)) - 0.5
+    gy = torch.rand((2, eo, h, w)) - 0.5
     xg = x.to(DEV).requires_grad_(True)
     y = run_sequential(seq, xg)
     y.backward(gy.to(DEV))

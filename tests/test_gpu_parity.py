@@ -474,7 +474,7 @@ def test_guidedepth_cfg2_shape_runs_and_matches_oracle_encoder_free_parts():
 
 @pytest.mark.parametrize("n,cin,cout,h,w", [(2, 16, 8, 48, 64), (3, 16, 16, 8, 8), (2, 32, 16, 24, 32),
                                             (2, 32, 32, 16, 16), (2, 64, 32, 12, 16),
-                                            (1, 32, 64, 8, 8), (2, 16, 32, 8, 16),
+                                            (1, 32, 64, 8, 8), (2, 16, 32, 8, 16), (2, 64, 64, 12, 16),
                                             (32, 16, 8, 480, 640)])
 def test_pointwise_conv_vs_aten(n, cin, cout, h, w):
     """HIP MFMA 1x1 convolution (the BN-folded guided-upsampling convs) vs ATen float64."""

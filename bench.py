@@ -32,6 +32,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MFMA_F32_PEAK_TFS = 157.3  # fp32-input MFMA dense peak (= fp32 vector rate, MI355X_MICROARCH.md)
+MFMA_BF16_PEAK_TFS = 16 * MFMA_F32_PEAK_TFS  # bf16 MFMA dense peak (~2.5 PF, 16x the f32 rate)
 # rocprofv3 PMC HBM bytes per launch (tools/pmc_traffic.py), newest round first.
 # Counters are per workload and precision: a kernel's bytes in the cfg2 fp32
 # step say nothing about its bytes in the bf16 or the NewCRF step.
@@ -282,10 +283,11 @@ def main():
                   "bytes_per_launch": per_launch, "avg_launch_us": round(ms * 1e3 / launches, 2),
                   "launches_per_step": launches / timing_steps,
                   "ms_per_step": round(ms / timing_steps, 3)}
-        if flops > 0:  # MFMA kernels (conv3x3, pointwise/skip, attention): fp32 MFMA peak
+        if flops > 0:  # MFMA kernels: the fp32 MFMA peak, or bf16's for the *_bf16 ids
             achieved = flops / (ms * 1e-3) / 1e12
-            return dict({"bound": "mfma", "achieved": round(achieved, 2), "peak": MFMA_F32_PEAK_TFS,
-                         "unit": "TFLOP/s", "frac": round(achieved / MFMA_F32_PEAK_TFS, 4),
+            peak = MFMA_BF16_PEAK_TFS if name.endswith("_bf16") else MFMA_F32_PEAK_TFS
+            return dict({"bound": "mfma", "achieved": round(achieved, 2), "peak": round(peak, 1),
+                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                          "flops_per_launch": flops / launches}, **common)
         achieved = nbytes / (ms * 1e-3) / 1e9
         return dict({"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

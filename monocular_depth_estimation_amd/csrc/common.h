@@ -63,6 +63,10 @@ enum Kid : int {
   K_C3_WGRAD_GUIDE,  // the 3-channel guide convs' weight gradient (HBM-bound: ~12 flop/B)
   K_COLSUM,
   K_MLP_GELU_BWD,
+  K_C3_FWD_BF16,  // the bf16 MFMA conv3x3 passes (v_mfma_f32_16x16x32_bf16: bf16 MFMA peak)
+  K_C3_DGRAD_BF16,
+  K_C3_WGRAD_BF16,
+  K_C3_WGRAD_WIDE,  // the 64 / 128 / 256-channel NCHW weight gradients
   K_COUNT
 };
 

@@ -951,11 +951,11 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
 #define MDE_WIDE_FIXED(WW, TT)                                                                  \
   do {                                                                                          \
     if (wpb == 4)                                                                               \
-      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s,                                         \
+      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s,                                         \
                       (conv3x3_wgrad_wide_fixed_kernel<WW, TT, 4>), grid, dim3(256), 0, x, gy,  \
                       ws, (int)ci, (int)co, (int)h, (int)w, tw, tpi, nt);                   \
     else                                                                                        \
-      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s,                                         \
+      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s,                                         \
                       (conv3x3_wgrad_wide_fixed_kernel<WW, TT, 8>), grid, dim3(512), 0, x, gy,  \
                       ws, (int)ci, (int)co, (int)h, (int)w, tw, tpi, nt);                   \
   } while (0)
@@ -966,7 +966,7 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
   else if (p.fixed_sw == 20)
     MDE_WIDE_FIXED(20, 4);
   else
-    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
                     dim3(256), 0, x, gy, ws, (int)ci, (int)co, (int)h, (int)w, p.g);
 #undef MDE_WIDE_FIXED
   return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co}, s);
@@ -1544,7 +1544,7 @@ int launch_bf_wgrad(const bf16* x, const bf16* gy, float* gw, int64_t n, int64_t
   const WgradPlan p = bf_wgrad_plan<CI, CO, TH, PW>(n, h, w);
   if (p.grid <= 0) return MDE_ERR_INVALID_ARG;
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
-  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_BF16, bytes, flops, s, (conv3x3_bf_wgrad_kernel<CI, CO, TH, PW>),
                   dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                   p.tiles_per_img, p.ntiles);
   return launch_reduce(ws, gw, 1, p.grid, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
@@ -1616,9 +1616,9 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
     if (cin == 16)
       return launch_bf_fwd<16, 16, 1, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes,
-                                             mde::K_C3_FWD, s);
+                                             mde::K_C3_FWD_BF16, s);
     return launch_bf_fwd<32, 32, 1, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes,
-                                           mde::K_C3_FWD, s);
+                                           mde::K_C3_FWD_BF16, s);
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
@@ -1664,9 +1664,9 @@ int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* st
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
     if (cin == 16)
       return launch_bf_fwd<16, 16, 1, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w,
-                                                   bytes, mde::K_C3_FWD, s, stats);
+                                                   bytes, mde::K_C3_FWD_BF16, s, stats);
     return launch_bf_fwd<32, 32, 1, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w,
-                                                 bytes, mde::K_C3_FWD, s, stats);
+                                                 bytes, mde::K_C3_FWD_BF16, s, stats);
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y || !stats || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
@@ -1696,9 +1696,9 @@ int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
     if (cin == 16)
       return launch_bf_fwd<16, 16, 1, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,
-                                            mde::K_C3_DGRAD, s);
+                                            mde::K_C3_DGRAD_BF16, s);
     return launch_bf_fwd<32, 32, 1, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,
-                                          mde::K_C3_DGRAD, s);
+                                          mde::K_C3_DGRAD_BF16, s);
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !weight || !gx || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;

@@ -39,11 +39,12 @@ NAMES = [
     (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, true", "skip_reduce_bwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, false", "pointwise_bwd"),
-    (r"conv3x3_fwd_kernel<.*false>", "conv3x3_fwd"),
-    (r"conv3x3_fwd_kernel<.*true>", "conv3x3_dgrad"),
-    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd"),
-    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad"),
-    (r"conv3x3_bf_wgrad_kernel", "conv3x3_wgrad"),
+    (r"conv3x3_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd"),
+    (r"conv3x3_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad"),
+    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd_bf16"),
+    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad_bf16"),
+    (r"conv3x3_bf_wgrad_kernel", "conv3x3_wgrad_bf16"),
+    (r"conv3x3_wgrad_wide\w*_kernel", "conv3x3_wgrad_wide"),
     (r"conv3x3_wgrad_kernel<3,", "conv3x3_wgrad_guide"),
     (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),
     (r"wgrad_reduce\w*_kernel", "conv3x3_wreduce"),

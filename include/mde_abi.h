@@ -443,7 +443,10 @@ int mde_pointwise_bwd_bn(const void* gy, const void* x, const float* in_scale,
  * mde_conv3x3_supported(cin, cout, pass, dtype): pass 0 forward, 1 data
  * gradient, 2 weight gradient.  MDE_F32 (v_mfma_f32_16x16x4_f32): forward
  * (3,16) (3,32) (3,64) (16,16) (32,32); data gradient (16,16) (32,32);
- * weight gradient all five.  MDE_BF16 (autocast, v_mfma_f32_16x16x32_bf16,
+ * weight gradient all five plus every cin % 32 == 0, cout % 64 == 0 pair (the
+ * 64 / 128 / 256-channel convs of DDRNet's BasicBlocks and the decoder,
+ * src/GuideDepth/model/DDRNet_23_slim.py:41-72, NCHW, no NHWC transposes).
+ * MDE_BF16 (autocast, v_mfma_f32_16x16x32_bf16,
  * fp32 accumulation; x / gy / y / gx bf16, the fp32 weight rounded to bf16
  * on load, the weight gradient fp32; w % 4 == 0): (16,16) and (32,32), every
  * pass.  Others return MDE_ERR_UNSUPPORTED.
@@ -471,6 +474,19 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
 int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
                       int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
                       void* stream);
+
+/* Stride-2 3x3 weight gradient: the DDRNet stem convolutions
+ * (`nn.Conv2d(3, 32, 3, stride=2, padding=1)`, `nn.Conv2d(32, 32, 3, 2, 1)`,
+ * src/GuideDepth/model/DDRNet_23_slim.py:229-236, bias folded into the BN).
+ * x [n,cin,h,w] (w even), gy [n,cout,(h-1)/2+1,(w-1)/2+1], fp32 (MDE_F32);
+ * (cin, cout) = (3, 32) or (32, 32).  gweight [cout,cin,3,3] overwritten
+ * (block partials + fixed-order reduction in the workspace: deterministic). */
+int mde_conv3x3s2_supported(int64_t cin, int64_t cout, int dtype);
+size_t mde_conv3x3s2_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                     int dtype);
+int mde_conv3x3s2_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                        int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                        void* stream);
 
 /* ---------------------------------------------------------------------------
  * Depthwise convolution (groups == channels, square k = 3 or 5, stride 1 or

@@ -110,6 +110,9 @@ SIGNATURES = {
     "mde_conv3x3_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_conv3x3_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _int]),
     "mde_conv3x3_wgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
+    "mde_conv3x3s2_supported": (_int, [_i64, _i64, _int]),
+    "mde_conv3x3s2_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _int]),
+    "mde_conv3x3s2_wgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_dwconv_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _i64, _i64]),
     "mde_dwconv_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_dwconv_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i64,

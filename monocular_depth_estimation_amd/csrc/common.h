@@ -67,6 +67,7 @@ enum Kid : int {
   K_C3_DGRAD_BF16,
   K_C3_WGRAD_BF16,
   K_C3_WGRAD_WIDE,  // the 64 / 128 / 256-channel NCHW weight gradients
+  K_C3_WGRAD_S2,    // the stride-2 stem convolutions' weight gradients
   K_COUNT
 };
 

@@ -1403,6 +1403,189 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
+// ------------------------------------------------ stride-2 weight gradient
+// The DDRNet stem's two stride-2 convolutions (conv1 of
+// src/GuideDepth/model/DDRNet_23_slim.py:229-236: 3 -> 32 and 32 -> 32, k3 s2
+// p1), whose weight gradient MIOpen runs as NHWC implicit GEMM behind NCHW <->
+// NHWC transposes (~0.69 ms per cfg2 step for the two).  NCHW here:
+//   gW[co][ci][dy][dx] = sum_{n,r,c} gy[n][co][r][c] x[n][ci][2r + dy - 1][2c + dx - 1].
+// A tile is one output row r x 64 output columns c0 .. c0+63 (K = 64 pixels).
+// x rows 2r-1 .. 2r+1 are staged split by column parity, O[j] = x[2(c0+j) - 1]
+// (j = 0..64) then E[j] = x[2(c0+j)] (j = 0..63), so the three column taps of
+// output pixel p read O[p], E[p], O[p + 1]: unit stride in p, every operand
+// one ds_read_b32 at a compile-time offset from a per-lane base.  A lane
+// loads one aligned float2 per staged row (E[l], O[l + 1]); O[0] is a halo
+// element.  MFMA (v_mfma_f32_16x16x4_f32): M = output channels, N = (tap, ci)
+// tap-major, K = pixels; the waves split (M tiles, N tiles, K steps) as
+// S2Cfg says, K-split partials are summed through LDS, and the block partials
+// are reduced by wgrad_reduce_kernel (fixed order).
+template <int CI, int CO>
+struct S2Cfg {
+  static constexpr int CIP = cpad4(CI);
+  static constexpr int NREAL = 9 * CIP;             // n = tap * CIP + ci
+  static constexpr int NP = (NREAL + 15) / 16 * 16;
+  static constexpr int NT = NP / 16, MT = CO / 16;
+  static constexpr int OE = 65;                     // E[0] within a staged row
+  static constexpr int RW = 130;                    // staged row pitch (O 65 + E 64, + 1)
+  static constexpr int PSX = (3 * RW - 2 + 31) / 32 * 32 + 2;  // >= 3 RW, = 2 (mod 32)
+  static constexpr int PSG = kTW + 4;               // gy row pitch (float4-aligned)
+  static constexpr int MW = CI >= 16 ? MT : 1;      // waves over M tiles
+  static constexpr int NW = CI >= 16 ? 4 / MT : 1;  // ... over N tiles
+  static constexpr int KW = 4 / (MW * NW);          // ... over K steps
+  static constexpr int MTW = MT / MW, NTW = NT / NW;
+  static constexpr int XR = CI * 3;                 // staged rows
+  static constexpr int XRW = (XR + 3) / 4;          // staged rows per wave
+  static constexpr int ZERO = CIP * PSX;            // 64 zeros: B of padded n
+  static constexpr int SX = ZERO + 64;
+  static constexpr int STAGE = SX + CO * PSG;
+  static constexpr int RED = KW > 1 ? KW * MT * NT * 256 : 0;
+  static constexpr int SMEM = STAGE > RED ? STAGE : RED;
+  static constexpr int M = CO * NP;                 // partial elements per block
+  static_assert(MW * NW * KW == 4 && MT % MW == 0 && NT % NW == 0 && 16 % KW == 0, "split");
+  static_assert(XRW <= 32, "row mask");
+};
+
+template <int CI, int CO, bool FULL>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3s2_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                           float* __restrict__ part, int h, int w, int ho, int wo, int tiles_w,
+                           int tiles_per_img, int ntiles) {
+  using C = S2Cfg<CI, CO>;
+  __shared__ float smem[C::SMEM];
+  float* sx = smem;
+  float* sg = smem + C::SX;
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
+  const int wvu = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int mw = wvu % C::MW, nw = (wvu / C::MW) % C::NW, kw = wvu / (C::MW * C::NW);
+  const int64_t img_in = (int64_t)CI * h * w, img_out = (int64_t)CO * ho * wo;
+  const int hw = h * w;
+  // padded input channels (CI < CIP) and the padded-n zeros: never rewritten
+  for (int e = CI * C::PSX + tid; e < C::SX; e += 256) sx[e] = 0.f;
+
+  int boff[C::NTW];
+#pragma unroll
+  for (int j = 0; j < C::NTW; ++j) {
+    const int n = 16 * (nw * C::NTW + j) + li;
+    if (n < C::NREAL) {
+      const int tap = n / C::CIP, ci = n % C::CIP, dy = tap / 3, dx = tap % 3;
+      boff[j] = ci * C::PSX + dy * C::RW + (dx == 0 ? 0 : (dx == 1 ? C::OE : 1)) + lk;
+    } else {
+      boff[j] = C::ZERO + lk;
+    }
+  }
+  int aoff[C::MTW];
+#pragma unroll
+  for (int i = 0; i < C::MTW; ++i) aoff[i] = (16 * (mw * C::MTW + i) + li) * C::PSG + lk;
+  f4 acc[C::MTW][C::NTW];
+#pragma unroll
+  for (int i = 0; i < C::MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // staging registers: this wave's rows k (staged row wvu + 4k = (ci, rr)),
+  // one float2 (E[lane], O[lane + 1]) each, and the O[0] halo of row k in lane k
+  float2 xv[C::XRW];
+  float xh = 0.f;
+  unsigned xm = 0;  // bit k: row k and this lane's columns in range
+  bool hok = false;
+  GradTile<CO, 1, FULL> G;  // FULL: wo % 64 == 0
+  auto load = [&](int tile) {
+    const int img = tile / tiles_per_img, t = tile - img * tiles_per_img;
+    const int r = t / tiles_w, c0 = (t - r * tiles_w) * kTW;
+    const float* xi = x + img * img_in;
+    const int col = 2 * c0 + 2 * lane;  // even; w even, so col < w <=> col + 1 < w
+    const bool cok = col < w;
+    const int colc = col < w ? col : w - 2;
+    xm = 0;
+#pragma unroll
+    for (int k = 0; k < C::XRW; ++k) {
+      const int rk = wvu + 4 * k;
+      const int ci = rk / 3 < CI ? rk / 3 : CI - 1, rr = rk % 3, ir = 2 * r - 1 + rr;
+      const bool ok = (C::XR % 4 == 0 || rk < C::XR) && ir >= 0 && ir < h && cok;
+      const int irc = ir < 0 ? 0 : (ir >= h ? h - 1 : ir);
+      xv[k] = *reinterpret_cast<const float2*>(xi + (unsigned)(ci * hw + irc * w + colc));
+      xm |= ok ? 1u << k : 0u;
+    }
+    {  // halo O[0] = x[2 c0 - 1] of row k = lane
+      const int rk = wvu + 4 * lane;
+      const int ci = rk / 3 < CI ? rk / 3 : CI - 1, rr = rk % 3, ir = 2 * r - 1 + rr;
+      hok = lane < C::XRW && rk < C::XR && ir >= 0 && ir < h && c0 > 0;
+      const int irc = ir < 0 ? 0 : (ir >= h ? h - 1 : ir);
+      xh = xi[(unsigned)(ci * hw + irc * w + (c0 > 0 ? 2 * c0 - 1 : 0))];
+    }
+    G.load(gy + img * img_out, ho, wo, r, c0, lane, wvu);
+  };
+  const TileWalk tw = tile_walk(ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) load(tile);
+  for (; tile < tw.end; tile += tw.step) {
+    __syncthreads();  // the previous tile's operands are consumed
+#pragma unroll
+    for (int k = 0; k < C::XRW; ++k) {
+      const int rk = wvu + 4 * k;
+      if (C::XR % 4 == 0 || rk < C::XR) {
+        float* row = sx + (rk / 3) * C::PSX + (rk % 3) * C::RW;
+        const bool ok = (xm >> k) & 1u;
+        row[C::OE + lane] = ok ? xv[k].x : 0.f;
+        row[1 + lane] = ok ? xv[k].y : 0.f;
+      }
+    }
+    if (lane < C::XRW) {
+      const int rk = wvu + 4 * lane;
+      if (rk < C::XR) sx[(rk / 3) * C::PSX + (rk % 3) * C::RW] = hok ? xh : 0.f;
+    }
+    G.template store<C::PSG>(sg, lane, wvu);
+    __syncthreads();
+    const int nxt = tile + tw.step;
+    if (nxt < tw.end) load(nxt);
+#pragma unroll
+    for (int st = 0; st < 16 / C::KW; ++st) {
+      const int s4 = 4 * (kw + C::KW * st);
+      float a[C::MTW];
+#pragma unroll
+      for (int i = 0; i < C::MTW; ++i) a[i] = sg[aoff[i] + s4];
+#pragma unroll
+      for (int j = 0; j < C::NTW; ++j) {
+        const float b = sx[boff[j] + s4];
+#pragma unroll
+        for (int i = 0; i < C::MTW; ++i) acc[i][j] = mfma4(a[i], b, acc[i][j]);
+      }
+    }
+  }
+  // lane holds co = 16 mt + 4 lk + i, n = 16 nt + li
+  float* out = part + (int64_t)blockIdx.x * C::M;
+  if constexpr (C::KW == 1) {
+#pragma unroll
+    for (int i = 0; i < C::MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < C::NTW; ++j) {
+        const int mt = mw * C::MTW + i, nt = nw * C::NTW + j;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[(16 * mt + 4 * lk + q) * C::NP + 16 * nt + li] = acc[i][j][q];
+      }
+    return;
+  }
+  __syncthreads();  // staging reads done: smem becomes red[kw][mt][nt][16][16]
+#pragma unroll
+  for (int i = 0; i < C::MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < C::NTW; ++j) {
+      const int mt = mw * C::MTW + i, nt = nw * C::NTW + j;
+      float* d = smem + ((kw * C::MT + mt) * C::NT + nt) * 256 + li;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[(4 * lk + q) * 16] = acc[i][j][q];
+    }
+  __syncthreads();
+  for (int e = tid; e < C::M; e += 256) {
+    const int co = e / C::NP, n = e % C::NP;
+    const int o = ((co / 16) * C::NT + n / 16) * 256 + (co % 16) * 16 + n % 16;
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < C::KW; ++k) sum += smem[k * C::MT * C::NT * 256 + o];
+    out[e] = sum;
+  }
+}
+
 // ---------------------------------------------------------------- dispatch
 enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
@@ -1491,6 +1674,51 @@ int launch_wgrad(const float* x, const float* gy, float* gw, int64_t n, int64_t 
                     dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.tiles_w,
                     p.tiles_per_img, p.ntiles);
   }
+  return launch_reduce(ws, gw, 1, p.grid, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
+}
+
+// ---- stride-2 weight gradient dispatch (3 -> 32, 32 -> 32; w even)
+struct S2Plan {
+  int ho, wo, tiles_w, tiles_per_img, ntiles, grid, m, np, cip;
+};
+
+template <int CI, int CO>
+S2Plan s2_plan(int64_t n, int64_t h, int64_t w) {
+  using C = S2Cfg<CI, CO>;
+  S2Plan p;
+  p.ho = (int)((h - 1) / 2 + 1);
+  p.wo = (int)((w - 1) / 2 + 1);
+  p.tiles_w = (int)mde::cdiv(p.wo, kTW);
+  p.tiles_per_img = p.ho * p.tiles_w;
+  const int64_t nt = n * p.tiles_per_img;
+  p.ntiles = nt > 0x7fffffff ? 0x7fffffff : (int)nt;
+  const int res = resident_blocks<conv3x3s2_wgrad_kernel<CI, CO, false>>();
+  p.grid = p.ntiles < res ? p.ntiles : res;
+  p.m = C::M;
+  p.np = C::NP;
+  p.cip = C::CIP;
+  return p;
+}
+
+bool s2_supported(int64_t cin, int64_t cout) {
+  return (cin == 3 || cin == 32) && cout == 32;
+}
+
+template <int CI, int CO>
+int launch_wgrad_s2(const float* x, const float* gy, float* gw, int64_t n, int64_t h, int64_t w,
+                    float* ws, hipStream_t s) {
+  const S2Plan p = s2_plan<CI, CO>(n, h, w);
+  if (p.grid <= 0) return MDE_ERR_INVALID_ARG;
+  const double flops = 2.0 * 9 * CI * CO * (double)n * p.ho * p.wo;
+  const double bytes = 4.0 * (double)n * ((double)CI * h * w + (double)CO * p.ho * p.wo);
+  if (p.wo % kTW == 0)
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_S2, bytes, flops, s, (conv3x3s2_wgrad_kernel<CI, CO, true>),
+                    dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.ho, p.wo, p.tiles_w,
+                    p.tiles_per_img, p.ntiles);
+  else
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_S2, bytes, flops, s, (conv3x3s2_wgrad_kernel<CI, CO, false>),
+                    dim3(p.grid), dim3(256), 0, x, gy, ws, (int)h, (int)w, p.ho, p.wo, p.tiles_w,
+                    p.tiles_per_img, p.ntiles);
   return launch_reduce(ws, gw, 1, p.grid, p.m, ReduceMap{0, p.np, p.cip, CI, CO}, s);
 }
 
@@ -1595,6 +1823,11 @@ int variant() {
 bool dims_ok(int64_t n, int64_t h, int64_t w) {
   return n > 0 && h > 0 && w > 0 && h < (1 << 24) && w < (1 << 24) &&
          64 * h * w < ((int64_t)1 << 31);
+}
+
+// stride-2 kernels: float2 loads of column pairs need an even width
+bool s2_dims_ok(int64_t n, int64_t h, int64_t w) {
+  return dims_ok(n, h, w) && w % 2 == 0;
 }
 
 }  // namespace
@@ -1771,6 +2004,34 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   if (variant() == 1) return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (variant() == 2) return launch_wgrad<32, 32, 4, 1>(xi, g, gweight, n, h, w, ws, bytes, s);
   return launch_wgrad<32, 32, 2, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
+}
+
+
+/* Stride-2 3x3 weight gradient (k3 s2 p1, bias-free, NCHW fp32): x [n, cin, h, w]
+ * (w even), gy [n, cout, (h-1)/2+1, (w-1)/2+1]; (cin, cout) = (3, 32) or (32, 32). */
+int mde_conv3x3s2_supported(int64_t cin, int64_t cout, int dtype) {
+  return dtype == MDE_F32 && s2_supported(cin, cout) ? 1 : 0;
+}
+
+size_t mde_conv3x3s2_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                     int dtype) {
+  if (dtype != MDE_F32 || !s2_supported(cin, cout) || !s2_dims_ok(n, h, w)) return 0;
+  const S2Plan p = cin == 3 ? s2_plan<3, 32>(n, h, w) : s2_plan<32, 32>(n, h, w);
+  return wgrad_ws_bytes(1, p.grid, p.m);
+}
+
+int mde_conv3x3s2_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                        int64_t cout, int64_t h, int64_t w, void* workspace, int dtype,
+                        void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !x || !gweight || !workspace || !s2_dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
+  if (!s2_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  if (cin == 3)
+    return launch_wgrad_s2<3, 32>((const float*)x, (const float*)gy, gweight, n, h, w,
+                                  (float*)workspace, s);
+  return launch_wgrad_s2<32, 32>((const float*)x, (const float*)gy, gweight, n, h, w,
+                                 (float*)workspace, s);
 }
 
 }  // extern "C"

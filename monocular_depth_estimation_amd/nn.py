@@ -536,6 +536,51 @@ class _Conv3x3Bf16(torch.autograd.Function):
         return gx, gw, None, None
 
 
+class _Conv3x3S2(torch.autograd.Function):
+    """Bias-free k3 / s2 / p1 convolution (the DDRNet stem, DDRNet_23_slim.py:
+    conv1): forward and data gradient on MIOpen, the weight gradient on the HIP
+    stride-2 kernel (mde_conv3x3s2_wgrad: NCHW, no NHWC transposes)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        x = x.contiguous()
+        ctx.save_for_backward(x, weight)
+        return torch.nn.functional.conv2d(x, weight, None, 2, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.ops.aten.convolution_backward(
+                gy, x, weight, None, (2, 2), (1, 1), (1, 1), False, (0, 0), 1,
+                (True, False, False))[0]
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(weight)
+            ws = _ws(_abi.query("mde_conv3x3s2_wgrad_workspace", n, cin, cout, h, w,
+                                _abi.MDE_F32), x)
+            _abi.call("mde_conv3x3s2_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
+                      cout, h, w, _abi.ptr(ws), _abi.MDE_F32, _abi.stream_of(gy))
+        return gx, gw
+
+
+def conv3x3s2_ok(conv: nn.Conv2d, x) -> bool:
+    """Whether this k3 / s2 / p1 conv takes the HIP stride-2 weight gradient
+    (fp32 outside autocast, even width; MDE_S2_WGRAD=0: MIOpen)."""
+    return (S2_WGRAD and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
+            and x.dim() == 4 and x.shape[-1] % 2 == 0 and conv.kernel_size == (3, 3)
+            and conv.stride == (2, 2) and conv.padding == (1, 1) and conv.dilation == (1, 1)
+            and conv.groups == 1 and conv.padding_mode == "zeros"
+            and bool(_abi.query("mde_conv3x3s2_supported", conv.in_channels, conv.out_channels,
+                                _abi.MDE_F32)))
+
+
+S2_WGRAD = os.environ.get("MDE_S2_WGRAD", "1") != "0"
+
+
 def conv3x3_passes(conv: nn.Conv2d, x):
     """(fwd, dgrad, wgrad) HIP flags for a 3x3/s1/p1 conv, or None if it is not one.
 
@@ -596,6 +641,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
         y = _Pointwise.apply(x, conv.weight)
     elif passes is not None:
         y = conv3x3(x, conv.weight, passes)
+    elif conv3x3s2_ok(conv, x):
+        y = _Conv3x3S2.apply(x, conv.weight)
     else:
         y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                        conv.dilation, conv.groups)
@@ -607,6 +654,8 @@ def conv_nobias(conv: nn.Conv2d, x):
     passes = conv3x3_passes(conv, x) if x.is_cuda else None
     if passes is not None:
         return conv3x3(x, conv.weight, passes)
+    if conv3x3s2_ok(conv, x):
+        return _Conv3x3S2.apply(x, conv.weight)
     return torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                       conv.dilation, conv.groups)
 

@@ -418,3 +418,4 @@ def test_conv3x3s2_wgrad_deterministic():
         _Conv3x3S2.apply(x.to(DEV), wd).backward(gy)
         outs.append(wd.grad.cpu())
     assert torch.equal(outs[0], outs[1])
+

@@ -266,6 +266,21 @@ __global__ void __launch_bounds__(256)
   __shared__ float cf[2];
   const int64_t plane = blockIdx.y;
   const int64_t ch = plane % c;
+  const int64_t hw4 = hw >> 2;
+  const T* xp = x + plane * hw;
+  const T* rp = r ? r + plane * hw : nullptr;
+  T* yp = y + plane * hw;
+  const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
+  // data loads before the coefficient prologue (see bn_bwd_apply_plane_kernel)
+  constexpr int KK = kPlaneChunk4 / 256;
+  float4 x4[KK], q4[KK];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    const int64_t i = b0 + k * 256 + threadIdx.x;
+    const int64_t ic = i < hw4 ? i : hw4 - 1;
+    x4[k] = ld4(xp + 4 * ic);
+    q4[k] = rp ? ld4(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (threadIdx.x < 64) {
     double s1 = 0.0, s2 = 0.0;
     if (A.training) wave_slices(A.part, ch, A.slices, &s1, &s2);
@@ -278,18 +293,10 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   const float sc = cf[0], sh = cf[1];
-  const int64_t hw4 = hw >> 2;
-  const T* xp = x + plane * hw;
-  const T* rp = r ? r + plane * hw : nullptr;
-  T* yp = y + plane * hw;
-  const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
 #pragma unroll
-  for (int k = 0; k < kPlaneChunk4 / 256; ++k) {
+  for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
-    if (i < hw4) {
-      const float4 q = rp ? ld4(rp + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      st4(yp + 4 * i, fwd4(ld4(xp + 4 * i), q, rp != nullptr, sc, sh, act));
-    }
+    if (i < hw4) st4(yp + 4 * i, fwd4(x4[k], q4[k], rp != nullptr, sc, sh, act));
   }
 }
 
@@ -494,6 +501,26 @@ __global__ void __launch_bounds__(256)
   __shared__ float cf[5];
   const int64_t plane = blockIdx.y;
   const int64_t ch = plane % c;
+  const int64_t hw4 = hw >> 2;
+  const T* gp = gy + plane * hw;
+  const T* xp = x + plane * hw;
+  const T* rp = r ? r + plane * hw : nullptr;
+  T* op = gx + plane * hw;
+  T* orp = gr ? gr + plane * hw : nullptr;
+  const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
+  // the block's data loads are issued BEFORE the coefficient prologue (slice
+  // sums + double math + barrier) so that their latencies overlap; clamped
+  // indices keep every load unconditional (out-of-range lanes store nothing)
+  constexpr int KK = kPlaneChunk4 / 256;
+  float4 g4[KK], v4[KK], q4[KK];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    const int64_t i = b0 + k * 256 + threadIdx.x;
+    const int64_t ic = i < hw4 ? i : hw4 - 1;
+    g4[k] = ld4(gp + 4 * ic);
+    v4[k] = ld4(xp + 4 * ic);
+    q4[k] = rp ? ld4(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
   if (threadIdx.x < 64) {
     double a, b;
     wave_slices(P.part, ch, P.slices, &a, &b);
@@ -504,19 +531,11 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   const float sc = cf[0], sh = cf[1], A = cf[2], B = cf[3], D = cf[4];
-  const int64_t hw4 = hw >> 2;
-  const T* gp = gy + plane * hw;
-  const T* xp = x + plane * hw;
-  const T* rp = r ? r + plane * hw : nullptr;
-  T* op = gx + plane * hw;
-  T* orp = gr ? gr + plane * hw : nullptr;
-  const int64_t b0 = blockIdx.x * (int64_t)kPlaneChunk4;
 #pragma unroll
-  for (int k = 0; k < kPlaneChunk4 / 256; ++k) {
+  for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
     if (i < hw4) {
-      const float4 g = ld4(gp + 4 * i), v = ld4(xp + 4 * i);
-      const float4 q = rp ? ld4(rp + 4 * i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 g = g4[k], v = v4[k], q = q4[k];
       const float4 e = make_float4(dy_eff(g.x, v.x, q.x, sc, sh, act),
                                    dy_eff(g.y, v.y, q.y, sc, sh, act),
                                    dy_eff(g.z, v.z, q.z, sc, sh, act),

@@ -269,6 +269,61 @@ __device__ __forceinline__ void q_row(const Geo& g, const float* __restrict__ qk
   row8(qkrow, 2 * g.c, head * D + 8 * (lane >> 4), tok[16 * it + (lane & 15)], qkb, q);
 }
 
+// One 64-key x 16-query column tile of a head-dim contraction (S^T = K Q^T,
+// dP^T = V dO^T): out[jt][r] = sum_d R[16jt + 4g + r][d] C[16it + l16][d],
+// rows[jt][k] = R[16jt + l16][8g + k], cols[k] = C[16it + l16][8g + k].
+// Compact 7x7 windows: tile 3 holds one real key (48) and query tile 3 one
+// real query (48), so 56 of the 128 MFMAs would multiply padding.  Here key
+// 48's row and query 48's column come from VALU dot products instead (its
+// dims broadcast from lane l16 == 0 of each lane group, the 32-dim sum over
+// the four groups by two butterflies, query 48's column redistributed to the
+// C layout by four shuffles per key tile): 72 MFMAs per column sweep.
+template <int WS, int it>
+__device__ __forceinline__ void kq_tile(const float rows[4][8], const float cols[8], f4 out[4],
+                                        int lane) {
+  if constexpr (!Tile<WS>::kCompact) {
+#pragma unroll
+    for (int jt = 0; jt < 4; ++jt) out[jt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt) out[jt] = mfma4(rows[jt][k], cols[k], out[jt]);
+    return;
+  }
+  const int gbase = lane & 48, g4 = lane >> 4;
+  {  // key 48 (tile 3, r = 0 of lane group 0): R[48] . C[16it + l16]
+    float d = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d = fmaf(__shfl(rows[3][k], gbase), cols[k], d);
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    out[3] = f4{d, 0.f, 0.f, 0.f};  // keys 49.. of tile 3 are padding
+  }
+  if constexpr (it < 3) {
+#pragma unroll
+    for (int jt = 0; jt < 3; ++jt) out[jt] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int jt = 0; jt < 3; ++jt) out[jt] = mfma4(rows[jt][k], cols[k], out[jt]);
+  } else {
+    // query 48 only (lanes l16 > 0 hold padded queries; their values are unused)
+    float cq[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) cq[k] = __shfl(cols[k], gbase);
+#pragma unroll
+    for (int jt = 0; jt < 3; ++jt) {
+      float d = 0.f;  // R[16jt + l16] . C[48], summed over the four groups
+#pragma unroll
+      for (int k = 0; k < 8; ++k) d = fmaf(rows[jt][k], cq[k], d);
+      d += __shfl_xor(d, 16, 64);
+      d += __shfl_xor(d, 32, 64);
+      const int src = gbase + 4 * g4;  // key 16jt + 4g + r sits in lane l16 = 4g + r
+      out[jt] = f4{__shfl(d, src), __shfl(d, src + 1), __shfl(d, src + 2), __shfl(d, src + 3)};
+    }
+  }
+}
+
 template <int WS, int it>
 __device__ __forceinline__ void probs_tile(const Geo& g, const float qraw[8], const int* lab,
                                            const float* tab, const float ka[4][8],
@@ -279,12 +334,7 @@ __device__ __forceinline__ void probs_tile(const Geo& g, const float qraw[8], co
     float qb[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) qb[k] = qraw[k] * g.scale;
-#pragma unroll
-    for (int jt = 0; jt < 4; ++jt) s[jt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int jt = 0; jt < 4; ++jt) s[jt] = mfma4(ka[jt][k], qb[k], s[jt]);
+    kq_tile<WS, it>(ka, qb, s, lane);
   }
   const int i = 16 * it + l16;
   const bool iv = i < n;
@@ -548,12 +598,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
           if constexpr (it < 3) row8(grow, c, hd + 8 * g4, tok[16 * (it + 1) + l16], nullptr, dn);
           else tile_elems(bq, qkrow, c2, c + hd, qkb, 1.f);
           f4 dp[4];
-#pragma unroll
-          for (int jt = 0; jt < 4; ++jt) dp[jt] = f4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int k = 0; k < 8; ++k)
-#pragma unroll
-            for (int jt = 0; jt < 4; ++jt) dp[jt] = mfma4(va[jt][k], db[k], dp[jt]);
+          kq_tile<WS, it>(va, db, dp, lane);
           float pv[4][4];
           float dl = 0.f;
           static_for4([&](auto jt_c) {

@@ -155,9 +155,10 @@ def _make_layer(block, inplanes, planes, blocks, stride=1):
 
 
 def _seq_bn_residual(seq, x, residual):
-    """residual + seq(x) for a Sequential ending in a BatchNorm: the add runs in the BN pass."""
+    """residual + seq(x) for a Sequential ending in a BatchNorm: the add runs in the BN pass.
+    Its bias-free convs go through conv_nobias (HIP kernels where they apply)."""
     for m in list(seq)[:-1]:
-        x = m(x)
+        x = conv_nobias(m, x) if isinstance(m, nn.Conv2d) and m.bias is None else m(x)
     return seq[-1](x, residual=residual)
 
 

@@ -762,33 +762,50 @@ __global__ void __launch_bounds__(256, 1)
     for (int i = 0; i < 4; ++i) out[(16 * wv + 4 * lk + i) * (9 * kWCI) + 16 * nt + li] = acc[nt][i];
 }
 
-// Fixed-strip variant (w a multiple of SW, SW % 4 == 0; tiles of TH rows x
-// SW columns): a K step's four pixels never straddle a row, so with the K
-// loop fully unrolled every operand address is a per-lane base plus a
-// compile-time offset (no pixel table, no address arithmetic), and the LDS is
-// sized to the tile (<= 80 KB) so that two blocks share a CU.  A strip's halo
-// columns are the neighbouring strips' pixels (zero only at the image edge).
-// Same partial layout as the generic kernel.
-template <int SW, int TH>
+// Fixed-strip variant (output width a multiple of SW, SW % 4 == 0; tiles of
+// TH output rows x SW output columns): a K step's four pixels never straddle a
+// row, so with the K loop fully unrolled every operand address is a per-lane
+// base plus a compile-time offset (no pixel table, no address arithmetic),
+// and the LDS is sized to the tile (<= 80 KB) so that two blocks share a CU.
+// A strip's halo columns are the neighbouring strips' pixels (zero only at
+// the image edge).  Same partial layout as the generic kernel.
+// S = 2 (DDRNet's stride-2 3x3 convs, DDRNet_23_slim.py:41-72 with stride 2,
+// down3 / down4 :254-265): the 2 TH + 1 input rows under a tile are staged
+// split by column parity like the stem kernel's, O[j] = x[2(c0+j) - 1]
+// (j = 0..SW) then E[j] = x[2(c0+j)] (j = 0..SW-1), so the column taps of
+// output pixel p read O[p], E[p], O[p + 1] -- unit stride, as at S = 1.
+template <int S, int SW, int TH>
 struct WideT {
-  static constexpr int W2 = SW + 2, K = TH * SW, XE = (TH + 2) * W2;
+  static constexpr int W2 = S == 1 ? SW + 2 : 2 * SW + 2;   // staged row pitch
+  static constexpr int XROWS = S == 1 ? TH + 2 : 2 * TH + 1;
+  static constexpr int K = TH * SW, XE = XROWS * W2;
   static constexpr int PX = (XE - 2 + 31) / 32 * 32 + 2;  // >= XE, = 2 mod 32
   static constexpr int PG = (K - 2 + 31) / 32 * 32 + 2;   // >= K, = 2 mod 32
   static constexpr int XL = (XE + 63) / 64, GL = (K + 63) / 64;
   static constexpr int SX = kWCI * PX, SMEM = SX + kWCO * PG;
   static_assert(SW % 4 == 0 && SMEM * 4 <= 80 * 1024, "two blocks per CU");
+  // staged column of column tap dx for output column 0 of the row
+  __device__ static constexpr int dxoff(int dx) {
+    return S == 1 ? dx : (dx == 0 ? 0 : (dx == 1 ? SW + 1 : 1));
+  }
+  // input column (relative to S * c0) of staged column cc, or a value that is
+  // never in range (the S = 2 row's pad column)
+  __device__ static constexpr int incol(int cc) {
+    return S == 1 ? cc - 1 : (cc <= SW ? 2 * cc - 1 : (cc <= 2 * SW ? 2 * (cc - SW - 1) : -(1 << 28)));
+  }
 };
 
 // WPB waves per block: 4 (wave w = output-channel tile w x all 18 N tiles)
 // or 8 (wave w = output-channel tile w & 3 x the 9 N tiles of input-channel
 // half w >> 2: half the accumulators and staging registers per wave, so four
 // waves per SIMD fit; measured 134.7 vs 140.4 us at 64->64 32x60x80).
-template <int SW, int TH, int WPB>
+// h, w: input sizes; ho, wo: gy sizes (= h, w at S = 1).
+template <int S, int SW, int TH, int WPB>
 __global__ void __launch_bounds__(64 * WPB, 2)
     conv3x3_wgrad_wide_fixed_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                                     float* __restrict__ part, int ci_n, int co_n, int h, int w,
-                                    int tiles_w, int tiles_per_img, int ntiles) {
-  using P = WideT<SW, TH>;
+                                    int ho, int wo, int tiles_w, int tiles_per_img, int ntiles) {
+  using P = WideT<S, SW, TH>;
   static_assert(WPB == 4 || WPB == 8, "waves per block");
   constexpr int NTW = WPB == 4 ? kWNT : kWNT / 2;  // N tiles per wave
   constexpr int XC = kWCI / WPB, GC = kWCO / WPB;  // channels staged per wave
@@ -800,16 +817,16 @@ __global__ void __launch_bounds__(64 * WPB, 2)
   const int cot = WPB == 4 ? wv : (wv & 3), hsel = WPB == 4 ? 0 : (wv >> 2);
   const int ngo = co_n / kWCO;
   const int cog = blockIdx.y % ngo, cig = blockIdx.y / ngo;
-  const int hw = h * w;
-  // staged element e = lane + 64 i of a channel's plane: tile row xrr - 1,
-  // tile column xcc (-1 .. SW); gy element p: tile row gpr, column gpc
+  const int hw = h * w, hwo = ho * wo;
+  // staged element e = lane + 64 i of a channel's plane: input row S r0 - 1 +
+  // xrr, input column S c0 + xcc; gy element p: tile row gpr, column gpc
   int xcc[P::XL], xrr[P::XL], gpr[P::GL], gpc[P::GL];
 #pragma unroll
   for (int i = 0; i < P::XL; ++i) {
     const int e = lane + 64 * i;
     const int rr = e / P::W2;
     xrr[i] = e < P::XE ? rr : -4096;
-    xcc[i] = e - rr * P::W2 - 1;
+    xcc[i] = P::incol(e - rr * P::W2);
   }
 #pragma unroll
   for (int i = 0; i < P::GL; ++i) {
@@ -821,19 +838,19 @@ __global__ void __launch_bounds__(64 * WPB, 2)
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
   const float* xg = x + ((int64_t)cig * kWCI + XC * wv) * hw;
-  const float* gg = gy + ((int64_t)cog * kWCO + GC * wv) * hw;
+  const float* gg = gy + ((int64_t)cog * kWCO + GC * wv) * hwo;
   float vx[XC][P::XL], vg[GC][P::GL];
   unsigned xm = 0, gm = 0;
   auto load = [&](int tile) {
     const int img = tile / tiles_per_img, t = tile - img * tiles_per_img;
     const int r0 = (t / tiles_w) * TH, c0 = (t % tiles_w) * SW;
     const float* xi = xg + (int64_t)img * ci_n * hw;
-    const float* gi = gg + (int64_t)img * co_n * hw;
+    const float* gi = gg + (int64_t)img * co_n * hwo;
     // clamped coordinates (see the generic kernel): no uniform fallback address
     xm = 0;
 #pragma unroll
     for (int i = 0; i < P::XL; ++i) {
-      const int gr = r0 - 1 + xrr[i], gc = c0 + xcc[i];
+      const int gr = S * r0 - 1 + xrr[i], gc = S * c0 + xcc[i];
       const bool ok = gr >= 0 && gr < h && gc >= 0 && gc < w;
       xm |= ok ? 1u << i : 0u;
       const int o = clampi(gr, 0, h - 1) * w + clampi(gc, 0, w - 1);
@@ -844,11 +861,11 @@ __global__ void __launch_bounds__(64 * WPB, 2)
 #pragma unroll
     for (int i = 0; i < P::GL; ++i) {
       const int p = lane + 64 * i;
-      const bool ok = p < P::K && r0 + p / SW < h;
+      const bool ok = p < P::K && r0 + p / SW < ho;
       gm |= ok ? 1u << i : 0u;
-      const int o = clampi(r0 + gpr[i], 0, h - 1) * w + c0 + gpc[i];
+      const int o = clampi(r0 + gpr[i], 0, ho - 1) * wo + c0 + gpc[i];
 #pragma unroll
-      for (int c = 0; c < GC; ++c) vg[c][i] = gi[(unsigned)(c * hw + o)];
+      for (int c = 0; c < GC; ++c) vg[c][i] = gi[(unsigned)(c * hwo + o)];
     }
   };
   int tile = blockIdx.x;
@@ -877,12 +894,14 @@ __global__ void __launch_bounds__(64 * WPB, 2)
     const float* gb = sg + (16 * cot + li) * P::PG + lk;
 #pragma unroll 5
     for (int st = 0; st < P::K / 4; ++st) {
-      const int so = (4 * st / SW) * P::W2 + (4 * st) % SW;  // the step's first pixel
+      // the step's first pixel: output row 4 st / SW -> staged row S x that
+      const int so = S * (4 * st / SW) * P::W2 + (4 * st) % SW;
       const float a = gb[4 * st];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
         const int tap = WPB == 4 ? nt >> 1 : nt, half = WPB == 4 ? nt & 1 : 0;
-        acc[nt] = mfma4(a, xb[half * 16 * P::PX + (tap / 3) * P::W2 + tap % 3 + so], acc[nt]);
+        acc[nt] = mfma4(a, xb[half * 16 * P::PX + (tap / 3) * P::W2 + P::dxoff(tap % 3) + so],
+                        acc[nt]);
       }
     }
   }
@@ -952,12 +971,12 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
   do {                                                                                          \
     if (wpb == 4)                                                                               \
       MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s,                                         \
-                      (conv3x3_wgrad_wide_fixed_kernel<WW, TT, 4>), grid, dim3(256), 0, x, gy,  \
-                      ws, (int)ci, (int)co, (int)h, (int)w, tw, tpi, nt);                   \
+                      (conv3x3_wgrad_wide_fixed_kernel<1, WW, TT, 4>), grid, dim3(256), 0, x,   \
+                      gy, ws, (int)ci, (int)co, (int)h, (int)w, (int)h, (int)w, tw, tpi, nt);   \
     else                                                                                        \
       MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s,                                         \
-                      (conv3x3_wgrad_wide_fixed_kernel<WW, TT, 8>), grid, dim3(512), 0, x, gy,  \
-                      ws, (int)ci, (int)co, (int)h, (int)w, tw, tpi, nt);                   \
+                      (conv3x3_wgrad_wide_fixed_kernel<1, WW, TT, 8>), grid, dim3(512), 0, x,   \
+                      gy, ws, (int)ci, (int)co, (int)h, (int)w, (int)h, (int)w, tw, tpi, nt);   \
   } while (0)
   if (p.fixed_sw == 80)
     MDE_WIDE_FIXED(80, 1);
@@ -969,6 +988,52 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
                     dim3(256), 0, x, gy, ws, (int)ci, (int)co, (int)h, (int)w, p.g);
 #undef MDE_WIDE_FIXED
+  return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co}, s);
+}
+
+// Stride-2 wide weight gradient (fixed strips only: output width a multiple
+// of 40, or 20; input width even).  h, w: input sizes.
+inline int wide_s2_sw(int64_t wo) { return wo % 40 == 0 ? 40 : (wo == 20 ? 20 : 0); }
+
+inline bool wide_s2_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WidePlan* p) {
+  if (ci % kWCI || co % kWCO || ci < kWCI || co < kWCO || w % 2) return false;
+  const int64_t ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
+  const int sw = wide_s2_sw(wo);
+  if (!sw) return false;
+  const int th = 80 / sw, tw = (int)(wo / sw);
+  const int64_t tpi = mde::cdiv(ho, th) * tw, nt = n * tpi;
+  if (nt > 0x7fffffff) return false;
+  p->fixed_sw = sw;
+  p->g.th = th;
+  p->g.wc = sw;
+  p->g.tiles_w = tw;
+  p->g.tiles_per_img = (int)tpi;
+  p->g.ntiles = (int)nt;
+  p->groups = (int)((ci / kWCI) * (co / kWCO));
+  int gx = 512 / p->groups;
+  if (gx < 1) gx = 1;
+  if (gx > p->g.ntiles) gx = p->g.ntiles;
+  p->gx = gx;
+  return true;
+}
+
+int launch_wgrad_wide_s2(const float* x, const float* gy, float* gw, int64_t n, int64_t ci,
+                         int64_t co, int64_t h, int64_t w, float* ws, hipStream_t s) {
+  WidePlan p;
+  if (!wide_s2_plan(n, ci, co, h, w, &p)) return MDE_ERR_UNSUPPORTED;
+  const int ho = (int)((h - 1) / 2 + 1), wo = (int)((w - 1) / 2 + 1);
+  const double flops = 2.0 * 9 * ci * co * (double)n * ho * wo;
+  const double bytes = 4.0 * n * ((double)ci * h * w + (double)co * ho * wo);
+  const dim3 grid(p.gx, p.groups);
+  const int tpi = p.g.tiles_per_img, nt = p.g.ntiles, tw = p.g.tiles_w;
+  if (p.fixed_sw == 40)
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_S2, bytes, flops, s,
+                    (conv3x3_wgrad_wide_fixed_kernel<2, 40, 2, 8>), grid, dim3(512), 0, x, gy, ws,
+                    (int)ci, (int)co, (int)h, (int)w, ho, wo, tw, tpi, nt);
+  else
+    MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_S2, bytes, flops, s,
+                    (conv3x3_wgrad_wide_fixed_kernel<2, 20, 4, 8>), grid, dim3(512), 0, x, gy, ws,
+                    (int)ci, (int)co, (int)h, (int)w, ho, wo, tw, tpi, nt);
   return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co}, s);
 }
 
@@ -2010,12 +2075,17 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
 /* Stride-2 3x3 weight gradient (k3 s2 p1, bias-free, NCHW fp32): x [n, cin, h, w]
  * (w even), gy [n, cout, (h-1)/2+1, (w-1)/2+1]; (cin, cout) = (3, 32) or (32, 32). */
 int mde_conv3x3s2_supported(int64_t cin, int64_t cout, int dtype) {
-  return dtype == MDE_F32 && s2_supported(cin, cout) ? 1 : 0;
+  return dtype == MDE_F32 && (s2_supported(cin, cout) || wide(cin, cout)) ? 1 : 0;
 }
 
 size_t mde_conv3x3s2_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
                                      int dtype) {
-  if (dtype != MDE_F32 || !s2_supported(cin, cout) || !s2_dims_ok(n, h, w)) return 0;
+  if (dtype != MDE_F32 || !s2_dims_ok(n, h, w)) return 0;
+  if (wide(cin, cout)) {
+    WidePlan wp;
+    return wide_s2_plan(n, cin, cout, h, w, &wp) ? wide_workspace(wp) : 0;
+  }
+  if (!s2_supported(cin, cout)) return 0;
   const S2Plan p = cin == 3 ? s2_plan<3, 32>(n, h, w) : s2_plan<32, 32>(n, h, w);
   return wgrad_ws_bytes(1, p.grid, p.m);
 }
@@ -2025,8 +2095,11 @@ int mde_conv3x3s2_wgrad(const void* gy, const void* x, float* gweight, int64_t n
                         void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !x || !gweight || !workspace || !s2_dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
-  if (!s2_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
+  if (wide(cin, cout))
+    return launch_wgrad_wide_s2((const float*)x, (const float*)gy, gweight, n, cin, cout, h, w,
+                                (float*)workspace, s);
+  if (!s2_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
   if (cin == 3)
     return launch_wgrad_s2<3, 32>((const float*)x, (const float*)gy, gweight, n, h, w,
                                   (float*)workspace, s);

@@ -569,16 +569,22 @@ class _Conv3x3S2(torch.autograd.Function):
 
 def conv3x3s2_ok(conv: nn.Conv2d, x) -> bool:
     """Whether this k3 / s2 / p1 conv takes the HIP stride-2 weight gradient
-    (fp32 outside autocast, even width; MDE_S2_WGRAD=0: MIOpen)."""
+    (the stem's 3 -> 32 / 32 -> 32, and 32+ -> 64+ channels at output widths
+    that are multiples of 40 or 20; fp32 outside autocast, even input width;
+    MDE_S2_WGRAD=0: MIOpen)."""
     return (S2_WGRAD and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
             and x.dim() == 4 and x.shape[-1] % 2 == 0 and conv.kernel_size == (3, 3)
             and conv.stride == (2, 2) and conv.padding == (1, 1) and conv.dilation == (1, 1)
             and conv.groups == 1 and conv.padding_mode == "zeros"
             and bool(_abi.query("mde_conv3x3s2_supported", conv.in_channels, conv.out_channels,
-                                _abi.MDE_F32)))
+                                _abi.MDE_F32))
+            and (S2_WIDE or conv.out_channels == 32)
+            and _abi.query("mde_conv3x3s2_wgrad_workspace", x.shape[0], conv.in_channels,
+                           conv.out_channels, x.shape[2], x.shape[3], _abi.MDE_F32) > 0)
 
 
 S2_WGRAD = os.environ.get("MDE_S2_WGRAD", "1") != "0"
+S2_WIDE = os.environ.get("MDE_S2_WIDE", "1") != "0"  # the 64+-channel ones (A/B switch)
 
 
 def conv3x3_passes(conv: nn.Conv2d, x):

@@ -419,3 +419,35 @@ def test_conv3x3s2_wgrad_deterministic():
         outs.append(wd.grad.cpu())
     assert torch.equal(outs[0], outs[1])
 
+
+
+# Stride-2 wide weight gradients (DDRNet's stride-2 BasicBlock convs and
+# down3 / down4): output widths 80 (two 40-column strips), 40, 20, a ragged
+# last row tile (odd input height), and an unsupported width (MIOpen path).
+S2W = [(32, 64, 2, 120, 160), (64, 128, 2, 60, 80), (128, 256, 2, 30, 40), (64, 128, 1, 37, 80)]
+
+
+@pytest.mark.parametrize("cin,cout,n,h,w", S2W)
+def test_conv3x3s2_wide_wgrad_vs_float64(cin, cout, n, h, w):
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import _Conv3x3S2
+    assert _abi.query("mde_conv3x3s2_wgrad_workspace", n, cin, cout, h, w, 0) > 0
+    x, wt, _ = _case(cin, cout, n, h, w, 3 * cin + h)
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    gy = torch.rand((n, cout, ho, wo)) - 0.5
+    xr = x.double().requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    torch.nn.functional.conv2d(xr, wr, None, 2, 1).backward(gy.double())
+    xd = x.to(DEV).requires_grad_(True)
+    wd = wt.to(DEV).requires_grad_(True)
+    _Conv3x3S2.apply(xd, wd).backward(gy.to(DEV))
+    assert rel_err(wd.grad, wr.grad) <= 2e-5
+    assert rel_err(xd.grad, xr.grad) <= 1e-5
+
+
+def test_conv3x3s2_wide_unsupported_width_falls_back():
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import conv3x3s2_ok
+    assert _abi.query("mde_conv3x3s2_wgrad_workspace", 2, 256, 256, 15, 20, 0) == 0  # wo = 10
+    conv = torch.nn.Conv2d(256, 256, 3, 2, 1, bias=False)
+    assert not conv3x3s2_ok(conv, torch.empty((2, 256, 15, 20), device=DEV))

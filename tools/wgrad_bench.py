@@ -63,3 +63,24 @@ for (n, c, co, h, w) in [(32, 3, 32, 480, 640), (32, 32, 32, 240, 320)]:
     gb = 4.0 * n * (c * h * w + co * ho * wo) / 1e9
     print(f"[s2] wgrad {c}->{co} {n}x{h}x{w}: HIP {th:7.1f} us ({fl / th / 1e6:5.1f} TF/s, "
           f"{gb / th * 1e6:6.0f} GB/s)  MIOpen {tm:7.1f} us  rel diff {err:.1e}", flush=True)
+
+# stride-2 wide weight gradients (DDRNet's stride-2 BasicBlock convs, down3 / down4)
+for (n, c, co, h, w) in [(32, 32, 64, 120, 160), (32, 64, 128, 60, 80), (32, 128, 256, 30, 40)]:
+    x = torch.rand((n, c, h, w), device="cuda") - 0.5
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    gy = torch.rand((n, co, ho, wo), device="cuda") - 0.5
+    wt = torch.rand((co, c, 3, 3), device="cuda")
+    gw = torch.empty_like(wt)
+    ws = _ws(_abi.query("mde_conv3x3s2_wgrad_workspace", n, c, co, h, w, 0), x)
+    st = _abi.stream_of(x)
+    hip = lambda: _abi.call("mde_conv3x3s2_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, c,
+                            co, h, w, _abi.ptr(ws), 0, st)
+    mio = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (2, 2), (1, 1), (1, 1), False,
+                                                      (0, 0), 1, (False, True, False))
+    th, tm = timeit(hip), timeit(mio)
+    hip()
+    ref = mio()[1]
+    err = float((gw - ref).abs().max() / ref.abs().max())
+    fl = 2.0 * 9 * c * co * n * ho * wo
+    print(f"[s2 wide] wgrad {c}->{co} {n}x{h}x{w}: HIP {th:7.1f} us ({fl / th / 1e6:5.1f} TF/s)  "
+          f"MIOpen {tm:7.1f} us  rel diff {err:.1e}", flush=True)

@@ -14,6 +14,8 @@
 // from DPP lane shifts and register row rings, no LDS staging).  Loss
 // partials go to a per-block slab summed in block order by loss_final_kernel
 // (deterministic).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -251,8 +253,10 @@ __global__ void __launch_bounds__(256)
     for (int i = 0; i < 4; ++i) load(rs + i, cx[i], cy[i]);
     for (int r = rs; r <= re; r += 4) {
       float nx[4], ny[4];
+      // the last group's prefetch would read up to 7 rows of the next chunk
+      // (HBM traffic for nothing): clamp it to row re, already in cache
 #pragma unroll
-      for (int i = 0; i < 4; ++i) load(r + 4 + i, nx[i], ny[i]);
+      for (int i = 0; i < 4; ++i) load(min(r + 4 + i, re), nx[i], ny[i]);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (r + i <= re) step(cx[i], cy[i], r + i);
@@ -276,13 +280,20 @@ struct StreamPlan {
   int64_t nwaves, nblocks;
 };
 
-// Enough waves to keep ~8 per SIMD (8192) from strips x chunks, chunks of
-// >= 16 rows (the 4 halo rows are L2 hits of the neighbouring chunks).
+// ~5.5 waves per SIMD (5632) from strips x chunks, chunks of >= 16 rows: at
+// 32x480x640, 30-row chunks (4 halo rows each).  The kernel is instruction-
+// bound (84-88 us for 2816-8192 waves); fewer, taller chunks cut the halo
+// re-reads (PMC: 1.79x algorithmic at 20-row chunks with the old prefetch
+// overrun, 1.59x with the overrun clamped).
 inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w) {
   StreamPlan p;
   p.strips = (int)mde::cdiv(w, kSW);
   const int64_t per_chunk = b * p.strips;
-  int64_t ch = mde::cdiv(8192, per_chunk);
+  static const int64_t target = [] {  // MDE_SSIM_WAVES: tuning sweeps only
+    const char* e = std::getenv("MDE_SSIM_WAVES");
+    return e ? std::atoll(e) : 5632;
+  }();
+  int64_t ch = mde::cdiv(target, per_chunk);
   const int64_t maxc = mde::cdiv(h, 16);
   if (ch > maxc) ch = maxc;
   if (ch < 1) ch = 1;

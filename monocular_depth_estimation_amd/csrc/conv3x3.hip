@@ -39,6 +39,20 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Resident blocks of a kernel on the whole device (persistent grids; the
+// occupancy query is for 256-thread blocks).
+template <auto Kernel>
+int resident_blocks() {
+  static const int cached = [] {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, Kernel, 256, 0);
+    return (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+  }();
+  return cached;
+}
+
 constexpr int kTW = 64;       // output columns per tile (4 MFMA row tiles)
 constexpr int kXW = kTW + 2;  // staged input columns (one-pixel halo each side)
 
@@ -530,15 +544,16 @@ __global__ void __launch_bounds__(256, 2)
 // a one-launch last-block hand-off between blocks needs agent-scope fences,
 // which write back L2 on every block: 53 us.)
 struct ReduceMap {
-  int wide;             // 1: the wide-channel layout [co 64][tap 9][ci 32] per group
+  int wide;             // > 0: the wide-channel layout [co wide][tap 9][ci 32] per group
+                        // (wide = the group's output channels, 64 or 32)
   int np, cip;          // regular layout [co][n = tap * cip + ci] (np columns)
   int ci_n, co_n;
 };
 
 __device__ __forceinline__ int64_t gw_index(const ReduceMap& r, int grp, int e) {
   if (r.wide) {
-    const int ngo = r.co_n / 64, col = e / 288, n = e % 288;
-    const int co = (grp % ngo) * 64 + col, ci = (grp / ngo) * 32 + n % 32;
+    const int ngo = r.co_n / r.wide, col = e / 288, n = e % 288;
+    const int co = (grp % ngo) * r.wide + col, ci = (grp / ngo) * 32 + n % 32;
     return ((int64_t)co * r.ci_n + ci) * 9 + n / 32;
   }
   const int co = e / r.np, n = e % r.np, tap = n / r.cip, ci = n % r.cip;
@@ -774,7 +789,7 @@ __global__ void __launch_bounds__(256, 1)
 // split by column parity like the stem kernel's, O[j] = x[2(c0+j) - 1]
 // (j = 0..SW) then E[j] = x[2(c0+j)] (j = 0..SW-1), so the column taps of
 // output pixel p read O[p], E[p], O[p + 1] -- unit stride, as at S = 1.
-template <int S, int SW, int TH>
+template <int S, int SW, int TH, int COG = kWCO>
 struct WideT {
   static constexpr int W2 = S == 1 ? SW + 2 : 2 * SW + 2;   // staged row pitch
   static constexpr int XROWS = S == 1 ? TH + 2 : 2 * TH + 1;
@@ -782,7 +797,8 @@ struct WideT {
   static constexpr int PX = (XE - 2 + 31) / 32 * 32 + 2;  // >= XE, = 2 mod 32
   static constexpr int PG = (K - 2 + 31) / 32 * 32 + 2;   // >= K, = 2 mod 32
   static constexpr int XL = (XE + 63) / 64, GL = (K + 63) / 64;
-  static constexpr int SX = kWCI * PX, SMEM = SX + kWCO * PG;
+  static constexpr int SX = kWCI * PX, SMEM = SX + COG * PG;
+  static constexpr int M = COG * 9 * kWCI;  // partial elements per group
   static_assert(SW % 4 == 0 && SMEM * 4 <= 80 * 1024, "two blocks per CU");
   // staged column of column tap dx for output column 0 of the row
   __device__ static constexpr int dxoff(int dx) {
@@ -800,22 +816,27 @@ struct WideT {
 // half w >> 2: half the accumulators and staging registers per wave, so four
 // waves per SIMD fit; measured 134.7 vs 140.4 us at 64->64 32x60x80).
 // h, w: input sizes; ho, wo: gy sizes (= h, w at S = 1).
-template <int S, int SW, int TH, int WPB>
-__global__ void __launch_bounds__(64 * WPB, 2)
+// COG = 32 (the 32 -> 32 convs, WPB = 4): wave w = output-channel tile
+// w & 1 x the 9 N tiles of input-channel half w >> 1.
+template <int S, int SW, int TH, int WPB, int COG = kWCO>
+__global__ void __launch_bounds__(64 * WPB, COG == kWCO ? 2 : 3)
     conv3x3_wgrad_wide_fixed_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                                     float* __restrict__ part, int ci_n, int co_n, int h, int w,
                                     int ho, int wo, int tiles_w, int tiles_per_img, int ntiles) {
-  using P = WideT<S, SW, TH>;
+  using P = WideT<S, SW, TH, COG>;
   static_assert(WPB == 4 || WPB == 8, "waves per block");
-  constexpr int NTW = WPB == 4 ? kWNT : kWNT / 2;  // N tiles per wave
-  constexpr int XC = kWCI / WPB, GC = kWCO / WPB;  // channels staged per wave
+  static_assert(COG == kWCO || (COG == 32 && WPB == 4), "32-channel groups: 4 waves");
+  constexpr int MTS = COG / 16;                    // output-channel tiles
+  constexpr int NTW = MTS * kWNT / WPB;             // N tiles per wave
+  constexpr int XC = kWCI / WPB, GC = COG / WPB;   // channels staged per wave
   __shared__ float sm[P::SMEM];
   float* sx = sm;
   float* sg = sm + P::SX;
   const int tid = threadIdx.x, lane = tid & 63, li = lane & 15, lk = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int cot = WPB == 4 ? wv : (wv & 3), hsel = WPB == 4 ? 0 : (wv >> 2);
-  const int ngo = co_n / kWCO;
+  // this wave's output-channel tile and (when NTW == 9) input-channel half
+  const int cot = NTW == kWNT ? wv : wv % MTS, hsel = NTW == kWNT ? 0 : wv / MTS;
+  const int ngo = co_n / COG;
   const int cog = blockIdx.y % ngo, cig = blockIdx.y / ngo;
   const int hw = h * w, hwo = ho * wo;
   // staged element e = lane + 64 i of a channel's plane: input row S r0 - 1 +
@@ -838,7 +859,7 @@ __global__ void __launch_bounds__(64 * WPB, 2)
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
   const float* xg = x + ((int64_t)cig * kWCI + XC * wv) * hw;
-  const float* gg = gy + ((int64_t)cog * kWCO + GC * wv) * hwo;
+  const float* gg = gy + ((int64_t)cog * COG + GC * wv) * hwo;
   float vx[XC][P::XL], vg[GC][P::GL];
   unsigned xm = 0, gm = 0;
   auto load = [&](int tile) {
@@ -899,17 +920,17 @@ __global__ void __launch_bounds__(64 * WPB, 2)
       const float a = gb[4 * st];
 #pragma unroll
       for (int nt = 0; nt < NTW; ++nt) {
-        const int tap = WPB == 4 ? nt >> 1 : nt, half = WPB == 4 ? nt & 1 : 0;
+        const int tap = NTW == kWNT ? nt >> 1 : nt, half = NTW == kWNT ? nt & 1 : 0;
         acc[nt] = mfma4(a, xb[half * 16 * P::PX + (tap / 3) * P::W2 + P::dxoff(tap % 3) + so],
                         acc[nt]);
       }
     }
   }
   // lane: co = 16 cot + 4 lk + i, n = 32 tap + 16 half + li
-  float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * kWM;
+  float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * P::M;
 #pragma unroll
   for (int nt = 0; nt < NTW; ++nt) {
-    const int col = WPB == 4 ? 16 * nt + li : 16 * (2 * nt + hsel) + li;
+    const int col = NTW == kWNT ? 16 * nt + li : 16 * (2 * nt + hsel) + li;
 #pragma unroll
     for (int i = 0; i < 4; ++i) out[(16 * cot + 4 * lk + i) * (9 * kWCI) + col] = acc[nt][i];
   }
@@ -988,7 +1009,48 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s, conv3x3_wgrad_wide_kernel, grid,
                     dim3(256), 0, x, gy, ws, (int)ci, (int)co, (int)h, (int)w, p.g);
 #undef MDE_WIDE_FIXED
-  return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co}, s);
+  return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{kWCO, 0, 0, (int)ci, (int)co}, s);
+}
+
+// 32 -> 32 at widths that are multiples of 80 (DDRNet's layer1 BasicBlocks at
+// 120x160, the decoder's 32-channel convs at 240x320) on the fixed-strip kernel
+// with 32-channel output groups (4 waves, three blocks per CU).
+// MDE_C32_WIDE=0: the regular 32 -> 32 weight-gradient kernel (A/B).
+inline bool c32_wide(int64_t w) {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_C32_WIDE");
+    return !(e && e[0] == '0');
+  }();
+  return on && w % 80 == 0;
+}
+
+inline WidePlan c32_plan(int64_t n, int64_t h, int64_t w) {
+  WidePlan p;
+  const int tw = (int)(w / 80);
+  const int64_t nt = n * h * tw;
+  p.fixed_sw = 80;
+  p.g.th = 1;
+  p.g.wc = 80;
+  p.g.tiles_w = tw;
+  p.g.tiles_per_img = (int)(h * tw);
+  p.g.ntiles = nt > 0x7fffffff ? 0x7fffffff : (int)nt;
+  p.groups = 1;
+  const int res = resident_blocks<conv3x3_wgrad_wide_fixed_kernel<1, 80, 1, 4, 32>>();
+  p.gx = p.g.ntiles < res ? p.g.ntiles : res;
+  return p;
+}
+
+int launch_wgrad_c32(const float* x, const float* gy, float* gw, int64_t n, int64_t h, int64_t w,
+                     float* ws, hipStream_t s) {
+  const WidePlan p = c32_plan(n, h, w);
+  if (p.gx <= 0) return MDE_ERR_INVALID_ARG;
+  constexpr int M = WideT<1, 80, 1, 32>::M;
+  const double flops = 2.0 * 9 * 32 * 32 * (double)(n * h * w);
+  const double bytes = 4.0 * n * h * w * 64.0;
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD, bytes, flops, s, (conv3x3_wgrad_wide_fixed_kernel<1, 80, 1, 4, 32>),
+                  dim3(p.gx, 1), dim3(256), 0, x, gy, ws, 32, 32, (int)h, (int)w, (int)h, (int)w,
+                  p.g.tiles_w, p.g.tiles_per_img, p.g.ntiles);
+  return launch_reduce(ws, gw, 1, p.gx, M, ReduceMap{32, 0, 0, 32, 32}, s);
 }
 
 // Stride-2 wide weight gradient (fixed strips only: output width a multiple
@@ -1034,7 +1096,7 @@ int launch_wgrad_wide_s2(const float* x, const float* gy, float* gw, int64_t n, 
     MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_S2, bytes, flops, s,
                     (conv3x3_wgrad_wide_fixed_kernel<2, 20, 4, 8>), grid, dim3(512), 0, x, gy, ws,
                     (int)ci, (int)co, (int)h, (int)w, ho, wo, tw, tpi, nt);
-  return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{1, 0, 0, (int)ci, (int)co}, s);
+  return launch_reduce(ws, gw, p.groups, p.gx, kWM, ReduceMap{kWCO, 0, 0, (int)ci, (int)co}, s);
 }
 
 // ====================================================================== bf16
@@ -1654,19 +1716,6 @@ __global__ void __launch_bounds__(256, 2)
 // ---------------------------------------------------------------- dispatch
 enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
-// Resident blocks of a kernel on the whole device (persistent grids).
-template <auto Kernel>
-int resident_blocks() {
-  static const int cached = [] {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, Kernel, 256, 0);
-    return (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
-  }();
-  return cached;
-}
-
 template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
 int fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_img, int* ntiles) {
   constexpr int TH = 4 * RPW;
@@ -2030,7 +2079,10 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
   else if (cin == 16 && variant() == 1) p = wgrad_plan<16, 16, 8, 4>(n, h, w);
   else if (cin == 16 && variant() == 2) p = wgrad_plan<16, 16, 4, 2>(n, h, w);
   else if (cin == 16) p = wgrad_plan<16, 16, 4, 4>(n, h, w);
-  else if (variant() == 1) p = wgrad_plan<32, 32, 4, 2>(n, h, w);
+  else if (c32_wide(w)) {
+    const WidePlan wp = c32_plan(n, h, w);
+    return wgrad_ws_bytes(1, wp.gx, WideT<1, 80, 1, 32>::M);
+  } else if (variant() == 1) p = wgrad_plan<32, 32, 4, 2>(n, h, w);
   else if (variant() == 2) p = wgrad_plan<32, 32, 4, 1>(n, h, w);
   else p = wgrad_plan<32, 32, 2, 2>(n, h, w);
   return wgrad_ws_bytes(1, p.grid, p.m);
@@ -2066,6 +2118,7 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   if (cin == 16 && variant() == 1) return launch_wgrad<16, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 16 && variant() == 2) return launch_wgrad<16, 16, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 16) return launch_wgrad<16, 16, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
+  if (c32_wide(w)) return launch_wgrad_c32(xi, g, gweight, n, h, w, ws, s);
   if (variant() == 1) return launch_wgrad<32, 32, 4, 2>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (variant() == 2) return launch_wgrad<32, 32, 4, 1>(xi, g, gweight, n, h, w, ws, bytes, s);
   return launch_wgrad<32, 32, 2, 2>(xi, g, gweight, n, h, w, ws, bytes, s);

@@ -98,6 +98,19 @@ WIDE = [(64, 64, 2, 60, 80), (128, 128, 2, 30, 40), (256, 256, 2, 15, 20),
         (32, 128, 1, 9, 21), (64, 64, 1, 33, 200)]
 
 
+# 32 -> 32 at widths that are multiples of 80: the fixed-strip kernel with
+# 32-channel output groups (DDRNet layer1 at 120x160, decoder at 240x320)
+@pytest.mark.parametrize("n,h,w", [(2, 30, 160), (1, 7, 80), (2, 5, 320)])
+def test_conv3x3_wgrad_c32_strips_vs_float64(n, h, w):
+    from monocular_depth_estimation_amd.nn import conv3x3
+    x, wt, gy = _case(32, 32, n, h, w, 11 + h)
+    wr = wt.double().requires_grad_(True)
+    torch.nn.functional.conv2d(x.double(), wr, None, 1, 1).backward(gy.double())
+    wg = wt.to(DEV).requires_grad_(True)
+    conv3x3(x.to(DEV), wg, (False, False, True)).backward(gy.to(DEV))
+    assert rel_err(wg.grad, wr.grad) <= 2e-5
+
+
 @pytest.mark.parametrize("cin,cout,n,h,w", WIDE)
 def test_conv3x3_wide_wgrad_vs_float64_oracle(cin, cout, n, h, w):
     from monocular_depth_estimation_amd import _abi

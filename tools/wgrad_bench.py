@@ -21,9 +21,10 @@ def timeit(fn, reps=20):
     return a.elapsed_time(b) / reps * 1e3
 
 
-tag = os.environ.get("MDE_WIDE_WPB", "8")
+tag = os.environ.get("MDE_WIDE_WPB", "8") + ("" if os.environ.get("MDE_C32_WIDE", "1") != "0" else " c32 off")
 for (n, c, co, h, w) in [(32, 64, 64, 60, 80), (32, 128, 128, 30, 40), (32, 256, 256, 15, 20),
-                         (32, 128, 64, 60, 80), (32, 64, 64, 120, 160), (4, 64, 64, 30, 40)]:
+                         (32, 128, 64, 60, 80), (32, 64, 64, 120, 160), (4, 64, 64, 30, 40),
+                         (32, 32, 32, 120, 160), (32, 32, 32, 240, 320)]:
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
     gy = torch.rand((n, co, h, w), device="cuda") - 0.5
     wt = torch.rand((co, c, 3, 3), device="cuda")

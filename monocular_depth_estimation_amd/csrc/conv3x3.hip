@@ -1053,6 +1053,40 @@ int launch_wgrad_c32(const float* x, const float* gy, float* gw, int64_t n, int6
   return launch_reduce(ws, gw, 1, p.gx, M, ReduceMap{32, 0, 0, 32, 32}, s);
 }
 
+// The stem's 32 -> 32 stride-2 weight gradient on the same kernel (S = 2,
+// 40-column strips, 32-channel output groups) when the output width is a
+// multiple of 40; MDE_C32_WIDE=0 keeps the stem kernel (A/B).
+int launch_wgrad_c32_s2(const float* x, const float* gy, float* gw, int64_t n, int64_t h,
+                        int64_t w, float* ws, hipStream_t s) {
+  const int ho = (int)((h - 1) / 2 + 1), wo = (int)((w - 1) / 2 + 1);
+  const int tw = wo / 40, tpi = (int)mde::cdiv(ho, 2) * tw;
+  const int64_t nt64 = n * (int64_t)tpi;
+  if (nt64 > 0x7fffffff) return MDE_ERR_INVALID_ARG;
+  const int nt = (int)nt64;
+  const int res = resident_blocks<conv3x3_wgrad_wide_fixed_kernel<2, 40, 2, 4, 32>>();
+  const int gx = nt < res ? nt : res;
+  constexpr int M = WideT<2, 40, 2, 32>::M;
+  const double flops = 2.0 * 9 * 32 * 32 * (double)n * ho * wo;
+  const double bytes = 4.0 * n * (32.0 * h * w + 32.0 * ho * wo);
+  MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_S2, bytes, flops, s,
+                  (conv3x3_wgrad_wide_fixed_kernel<2, 40, 2, 4, 32>), dim3(gx, 1), dim3(256), 0, x,
+                  gy, ws, 32, 32, (int)h, (int)w, ho, wo, tw, tpi, nt);
+  return launch_reduce(ws, gw, 1, gx, M, ReduceMap{32, 0, 0, 32, 32}, s);
+}
+
+inline size_t c32_s2_workspace(int64_t n, int64_t h, int64_t w) {
+  const int ho = (int)((h - 1) / 2 + 1), wo = (int)((w - 1) / 2 + 1);
+  const int64_t nt = n * mde::cdiv(ho, 2) * (wo / 40);
+  const int res = resident_blocks<conv3x3_wgrad_wide_fixed_kernel<2, 40, 2, 4, 32>>();
+  const int gx = (int)(nt < res ? nt : res);
+  return wgrad_ws_bytes(1, gx, WideT<2, 40, 2, 32>::M);
+}
+
+inline bool c32_s2(int64_t cin, int64_t cout, int64_t w) {
+  const int64_t wo = (w - 1) / 2 + 1;
+  return cin == 32 && cout == 32 && wo % 40 == 0 && c32_wide(80);
+}
+
 // Stride-2 wide weight gradient (fixed strips only: output width a multiple
 // of 40, or 20; input width even).  h, w: input sizes.
 inline int wide_s2_sw(int64_t wo) { return wo % 40 == 0 ? 40 : (wo == 20 ? 20 : 0); }
@@ -2139,6 +2173,7 @@ size_t mde_conv3x3s2_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64
     return wide_s2_plan(n, cin, cout, h, w, &wp) ? wide_workspace(wp) : 0;
   }
   if (!s2_supported(cin, cout)) return 0;
+  if (c32_s2(cin, cout, w)) return c32_s2_workspace(n, h, w);
   const S2Plan p = cin == 3 ? s2_plan<3, 32>(n, h, w) : s2_plan<32, 32>(n, h, w);
   return wgrad_ws_bytes(1, p.grid, p.m);
 }
@@ -2153,6 +2188,9 @@ int mde_conv3x3s2_wgrad(const void* gy, const void* x, float* gweight, int64_t n
     return launch_wgrad_wide_s2((const float*)x, (const float*)gy, gweight, n, cin, cout, h, w,
                                 (float*)workspace, s);
   if (!s2_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
+  if (c32_s2(cin, cout, w))
+    return launch_wgrad_c32_s2((const float*)x, (const float*)gy, gweight, n, h, w,
+                               (float*)workspace, s);
   if (cin == 3)
     return launch_wgrad_s2<3, 32>((const float*)x, (const float*)gy, gweight, n, h, w,
                                   (float*)workspace, s);

@@ -13,7 +13,9 @@ import os
 
 import torch  # noqa: F401  (loads torch's libamdhip64 before ours)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmde_hip.so")
+# MDE_HIP_LIB: another build of the same library (interleaved A/B runs in tools/).
+LIB_PATH = os.environ.get("MDE_HIP_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libmde_hip.so")
 
 MDE_F32 = 0
 MDE_BF16 = 1

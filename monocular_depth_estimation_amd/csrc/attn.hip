@@ -119,7 +119,8 @@ __device__ __forceinline__ int wsize(const Geo& g) {
   return WS ? WS : g.ws;
 }
 
-// tok[i]: token index in the image (>= 0), -1 padded (q = k = bias, v = 0),
+// tok[i]: the token's row offset in a C-wide image tensor (token index * c,
+// >= 0; a qk row is at 2 tok[i]), -1 padded (q = k = bias, v = 0),
 // -2 beyond the window (i >= ws*ws); lab[i]: shifted-region label.
 template <int WS>
 __device__ __forceinline__ void window_tokens(const Geo& g, int win, int* tok, int* lab) {
@@ -135,11 +136,32 @@ __device__ __forceinline__ void window_tokens(const Geo& g, int win, int* tok, i
     int yp = ys + g.shift, xp = xs + g.shift;
     if (yp >= g.hp) yp -= g.hp;
     if (xp >= g.wp) xp -= g.wp;
-    t = (yp < g.h && xp < g.w) ? yp * g.w + xp : -1;
+    t = (yp < g.h && xp < g.w) ? (yp * g.w + xp) * g.c : -1;
     l = region(ys, g.hp, ws, g.shift) * 3 + region(xs, g.wp, ws, g.shift);
   }
   tok[i] = t;
   lab[i] = l;
+}
+
+// Wave-uniform base pointers live in SGPRs (readfirstlane), and every access
+// is base + a 32-bit BYTE offset (element index < 2^30, checked on the host):
+// one global_load / global_store with an SGPR base and a VGPR offset, no
+// 64-bit address arithmetic per access (it was ~2 VALU per memory op, and the
+// backward is VALU-bound).
+template <typename T>
+__device__ __forceinline__ T* sgpr(T* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  // Through an explicit global-address-space pointer so the accesses stay
+  // global_* (an integer->pointer round trip would otherwise make them flat_*).
+  using G = __attribute__((address_space(1))) T*;
+  return (T*)(G)(((uint64_t)hi << 32) | lo);
+}
+template <typename T>
+__device__ __forceinline__ T* at(T* base, unsigned i) {
+  using C = std::conditional_t<std::is_const_v<T>, const char, char>;
+  return reinterpret_cast<T*>(reinterpret_cast<C*>(base) + (i << 2));
 }
 
 // 8 contiguous floats at p (32-byte aligned)
@@ -150,27 +172,26 @@ __device__ __forceinline__ void load8(const float* p, float* v) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-// Row operand: columns [off, off+8) of token t's row (stride `ld`), the bias
-// for a padded token (when given), else zeros.  Offsets are 32-bit from a
-// wave-uniform base (image planes are < 2^31 elements, checked on the host),
-// so a load is one VGPR offset on an SGPR base.
-__device__ __forceinline__ void row8(const float* base, int ld, int off, int t,
+// Row operand: columns [off, off+8) of the row at m * t (t: a tok[] entry,
+// m = 1 for C-wide tensors, 2 for qk; a compile-time constant), the bias
+// for a padded token (when given), else zeros.
+__device__ __forceinline__ void row8(const float* base, int m, int off, int t,
                                      const float* bias, float* v) {
   if (t >= 0) {
-    load8(base + (unsigned)(t * ld + off), v);
+    load8(at(base, (unsigned)(m * t + off)), v);
   } else if (t == -1 && bias) {
-    load8(bias + off, v);
+    load8(at(bias, (unsigned)off), v);
   } else {
 #pragma unroll
     for (int k = 0; k < 8; ++k) v[k] = 0.f;
   }
 }
 
-// Scalar operand: element `col` of token t's row, bias for padded, else 0.
-__device__ __forceinline__ float elem(const float* base, int ld, int col, int t,
+// Scalar operand: element `col` of the row at m * t, bias for padded, else 0.
+__device__ __forceinline__ float elem(const float* base, int m, int col, int t,
                                       const float* bias) {
-  if (t >= 0) return base[(unsigned)(t * ld + col)];
-  if (t == -1 && bias) return bias[col];
+  if (t >= 0) return *at(base, (unsigned)(m * t + col));
+  if (t == -1 && bias) return *at(bias, (unsigned)col);
   return 0.f;
 }
 
@@ -245,7 +266,7 @@ __device__ __forceinline__ void key_operands(const Geo& g, const float* __restri
   const int ws = wsize<WS>(g), span = 2 * ws - 1;
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
-    row8(qkrow, 2 * g.c, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
+    row8(qkrow, 2, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
 #pragma unroll
@@ -266,7 +287,7 @@ template <int WS>
 __device__ __forceinline__ void q_row(const Geo& g, const float* __restrict__ qkrow,
                                       const float* __restrict__ qkb, int head, const int* tok,
                                       int it, int lane, float q[8]) {
-  row8(qkrow, 2 * g.c, head * D + 8 * (lane >> 4), tok[16 * it + (lane & 15)], qkb, q);
+  row8(qkrow, 2, head * D + 8 * (lane >> 4), tok[16 * it + (lane & 15)], qkb, q);
 }
 
 // One 64-key x 16-query column tile of a head-dim contraction (S^T = K Q^T,
@@ -433,12 +454,12 @@ __global__ void __launch_bounds__(256, 4)
   if (head >= g.heads) return;
   const int bidx = win / (g.nwh * g.nww);
   const int64_t img = (int64_t)bidx * g.h * g.w;
-  const float* qkrow = qk + img * 2 * g.c;
+  const float* qkrow = sgpr(qk + img * 2 * g.c);
   float ka[4][8];
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
-    row8(qkrow, 2 * g.c, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
-  const float* vrow = v + img * g.c;
+    row8(qkrow, 2, g.c + head * D + 8 * g4, tok[16 * jt + l16], qkb, ka[jt]);
+  const float* vrow = sgpr(v + img * g.c);
   float vb[4][4][2];
 #pragma unroll
   for (int jt = 0; jt < 4; ++jt)
@@ -447,9 +468,9 @@ __global__ void __launch_bounds__(256, 4)
       const int t = tok[16 * jt + 4 * g4 + r];
 #pragma unroll
       for (int dt = 0; dt < 2; ++dt)
-        vb[jt][r][dt] = elem(vrow, g.c, head * D + 16 * dt + l16, t, g.vb);
+        vb[jt][r][dt] = elem(vrow, 1, head * D + 16 * dt + l16, t, g.vb);
     }
-  float* orow = out + img * g.c;
+  float* orow = sgpr(out + img * g.c);
   float qn[8];
   q_row<WS>(g, qkrow, qkb, head, tok, 0, lane, qn);
   static_for4([&](auto it_c) {
@@ -479,7 +500,7 @@ __global__ void __launch_bounds__(256, 4)
       if (t >= 0) {
 #pragma unroll
         for (int dt = 0; dt < 2; ++dt)
-          orow[(unsigned)(t * g.c + head * D + 16 * dt + l16)] = o[dt][rr];
+          *at(orow, (unsigned)(t + head * D + 16 * dt + l16)) = o[dt][rr];
       }
     }
   });
@@ -523,11 +544,11 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
     window_tokens<WS>(g, win, tok, lab);
     __syncthreads();
     const int64_t img = (int64_t)(win / (g.nwh * g.nww)) * g.h * g.w;
-    const float* qkrow = qk + img * c2;
-    const float* vrow = v + img * c;
-    const float* grow = gout + img * c;
-    float* gqkrow = gqk + img * c2;
-    float* gvrow = gv + img * c;
+    const float* qkrow = sgpr(qk + img * c2);
+    const float* vrow = sgpr(v + img * c);
+    const float* grow = sgpr(gout + img * c);
+    float* gqkrow = sgpr(gqk + img * c2);
+    float* gvrow = sgpr(gv + img * c);
     // T[w] is private to this wave: its LDS accesses are processed in program
     // order, so the P / dS round trips need no block barrier.  P and then dS
     // live in T only (not in registers across phases): the register peak is
@@ -537,7 +558,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       // loads the current phase waits on, so its waits do not cover them).
       // B operands of a product over 16-tiles (t, r): element col of token
       // tok[16 t + 4 g + r] (padded: the bias when given), scaled.
-      auto tile_elems = [&](float (&b)[4][4][2], const float* base, int ld, int col0,
+      auto tile_elems = [&](float (&b)[4][4][2], const float* base, int m, int col0,
                             const float* bias, float scale) {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
 #pragma unroll
@@ -547,19 +568,19 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
             const int tk = tok[16 * t + 4 * g4 + r];
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct)
-              b[t][r][ct] = scale * elem(base, ld, col0 + 16 * ct + l16, tk, bias);
+              b[t][r][ct] = scale * elem(base, m, col0 + 16 * ct + l16, tk, bias);
           }
       };
       float bdv[4][4][2];  // dV's B = dO[i][c]
       probs_stage<WS>(g, qkrow, qkb, head, tok, lab, tab[w], T,
-                      [&] { tile_elems(bdv, grow, c, hd, nullptr, 1.f); });  // P
+                      [&] { tile_elems(bdv, grow, 1, hd, nullptr, 1.f); });  // P
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       float va[4][8];  // dP's V rows, in flight during dV
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
 #pragma unroll
         for (int jt = 0; jt < 4; ++jt)
-          row8(vrow, c, hd + 8 * g4, tok[16 * jt + l16], g.vb, va[jt]);
+          row8(vrow, 1, hd + 8 * g4, tok[16 * jt + l16], g.vb, va[jt]);
       }
       // dV = P^T dO
       {
@@ -574,7 +595,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
             if (t >= 0) {
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct)
-                gvrow[(unsigned)(t * c + hd + 16 * ct + l16)] = o[ct][rr];
+                *at(gvrow, (unsigned)(t + hd + 16 * ct + l16)) = o[ct][rr];
             } else if (t == -1 && g.vb) {
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct) dvb[ct] += o[ct][rr];
@@ -589,14 +610,14 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
         float dn[8];  // dO row of the next query tile
-        row8(grow, c, hd + 8 * g4, tok[l16], nullptr, dn);
+        row8(grow, 1, hd + 8 * g4, tok[l16], nullptr, dn);
         static_for4([&](auto it_c) {
           constexpr int it = decltype(it_c)::value;
           float db[8];
 #pragma unroll
           for (int k = 0; k < 8; ++k) db[k] = dn[k];
-          if constexpr (it < 3) row8(grow, c, hd + 8 * g4, tok[16 * (it + 1) + l16], nullptr, dn);
-          else tile_elems(bq, qkrow, c2, c + hd, qkb, 1.f);
+          if constexpr (it < 3) row8(grow, 1, hd + 8 * g4, tok[16 * (it + 1) + l16], nullptr, dn);
+          else tile_elems(bq, qkrow, 2, c + hd, qkb, 1.f);
           f4 dp[4];
           kq_tile<WS, it>(va, db, dp, lane);
           float pv[4][4];
@@ -621,7 +642,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
       // dQ = dS K * scale: A = dS[i][j] (this lane's own T entries), B = K[j][c] per lane
       float bk[4][4][2];  // dK's B = Q[i][c] * scale, in flight during dQ
-      tile_elems(bk, qkrow, c2, hd, qkb, g.scale);
+      tile_elems(bk, qkrow, 2, hd, qkb, g.scale);
       {
         const int lane = opaque_lane(), l16 = lane & 15, g4 = lane >> 4;
         const float (&b)[4][4][2] = bq;
@@ -643,7 +664,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
             if (t >= 0) {
 #pragma unroll
               for (int ct = 0; ct < 2; ++ct)
-                gqkrow[(unsigned)(t * c2 + hd + 16 * ct + l16)] = q[ct][rr] * g.scale;
+                *at(gqkrow, (unsigned)(2 * t + hd + 16 * ct + l16)) = q[ct][rr] * g.scale;
             }
           }
         });
@@ -662,7 +683,7 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
 #pragma unroll
             for (int ct = 0; ct < 2; ++ct) {
               if (t >= 0)
-                gqkrow[(unsigned)(t * c2 + c + hd + 16 * ct + l16)] = o[ct][rr];
+                *at(gqkrow, (unsigned)(2 * t + c + hd + 16 * ct + l16)) = o[ct][rr];
               else if (t == -1)
                 dkb[ct] += o[ct][rr];
             }
@@ -777,7 +798,7 @@ bool make_geo(int64_t b, int64_t h, int64_t w, int64_t c, int64_t heads, int64_t
   g->scale = 1.f / sqrtf((float)D);
   g->vb = nullptr;
   return (int64_t)b * g->nwh * g->nww < (1LL << 31) && mde::cdiv(heads, kHeads) <= 65535 &&
-         (int64_t)h * w * 2 * c < (1LL << 31);
+         (int64_t)h * w * 2 * c < (1LL << 30);  // 32-bit byte offsets within an image
 }
 
 }  // namespace

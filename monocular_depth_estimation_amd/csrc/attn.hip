@@ -37,6 +37,7 @@
 // are reduced per block in a fixed order into a slab and summed by a second
 // kernel: deterministic, no atomics.
 #include <type_traits>
+#include <utility>
 
 #include "common.h"
 
@@ -245,6 +246,15 @@ __device__ __forceinline__ int opaque_lane() {
   int l = threadIdx.x & 63;
   asm volatile("" : "+v"(l));
   return l;
+}
+
+template <int N, typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl<N>(f, std::make_integer_sequence<int, N>{});
 }
 
 template <typename F>
@@ -691,32 +701,55 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
         });
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the phases' live ranges apart
-      // table gradient: entry e <- sum of dS over the (query, key) pairs at
-      // that offset, in a fixed order (query row-major); out-of-window pairs
-      // add 0 (adding +0 leaves the sum unchanged).
-      for (int e = lane; e < ntab; e += 64) {
+      // table gradient: entry (dy, dx) <- sum of dS over the (query, key)
+      // pairs at that offset, in a fixed order (query row-major).
+      if constexpr (WS > 0) {
+        // Two stages over this wave's tile.  (1) lane p = ri WS + rj (one
+        // query-row / key-row block pair; 49 of 64 lanes) sums each diagonal
+        // dx of its WS x WS block: D[p][dx] = sum_ci dS[rj WS + ci - dx][ri WS + ci]
+        // with compile-time column ranges (each of the 2401 pairs read once,
+        // no masks).  (2) entry (dy, dx) sums D[ri WS + ri - dy][dx] over ri.
+        // D overwrites the tile's first words once every lane's block reads
+        // are issued: one wave's LDS accesses are processed in program order.
+        constexpr int P = TL::kPitch, NT = 2 * WS - 1, DB = 2 * WS + 4;
+        static_assert(DB + (WS * WS + WS) * NT < TL::kWords, "D fits in the tile");
+        const int ri = lane / WS, rj = lane - ri * WS;
+        float dsum[NT];
+        if (lane < WS * WS) {
+          const int base = rj * WS * P + ri * WS;
+          static_for<NT>([&](auto d_c) {
+            constexpr int dx = decltype(d_c)::value - (WS - 1);
+            float acc = 0.f;
+            static_for<WS - (dx < 0 ? -dx : dx)>([&](auto k_c) {
+              constexpr int ci = decltype(k_c)::value + (dx > 0 ? dx : 0);
+              acc += T[base + (ci - dx) * P + ci];
+            });
+            dsum[decltype(d_c)::value] = acc;
+          });
+        }
+        __builtin_amdgcn_wave_barrier();
+        if (lane < WS * WS) {
+#pragma unroll
+          for (int d = 0; d < NT; ++d) T[DB + lane * NT + d] = dsum[d];
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (int e = lane; e < ntab; e += 64) {
+          const int dy = e / NT - (WS - 1), dx = e - (e / NT) * NT - (WS - 1);
+          // D[ri WS + ri - dy][dx] = T[DB + ri (WS + 1) NT + (dx + WS - 1) - dy NT]
+          const int b0 = DB + (dx + WS - 1) - dy * NT;
+          float acc = 0.f;
+#pragma unroll
+          for (int r = 0; r < WS; ++r) {
+            const bool ok = r - dy >= 0 && r - dy < WS;
+            const float v = T[b0 + r * (WS + 1) * NT];
+            acc += ok ? v : 0.f;
+          }
+          dtab[w][e] += acc;
+        }
+      }
+      for (int e = lane; WS == 0 && e < ntab; e += 64) {
         const int dy = e / span - (ws - 1), dx = e % span - (ws - 1);
         float acc = 0.f;
-        if constexpr (WS > 0) {
-          // T[(ri - dy) ws + ci - dx][ri ws + ci] = Tb[ri (ws P + ws) + ci (P + 1)]:
-          // one per-lane base and compile-time offsets (no per-term address
-          // registers); out-of-window terms read some LDS word and add 0
-          constexpr int P = TL::kPitch;
-          const int basei = -(WS * dy + dx) * P;
-          unsigned rm = 0, cm = 0;
-#pragma unroll
-          for (int k = 0; k < WS; ++k) {
-            rm |= (k - dy >= 0 && k - dy < WS) ? 1u << k : 0u;
-            cm |= (k - dx >= 0 && k - dx < WS) ? 1u << k : 0u;
-          }
-#pragma unroll
-          for (int ri = 0; ri < WS; ++ri)
-#pragma unroll
-            for (int ci = 0; ci < WS; ++ci) {
-              const float v = T[basei + ri * (WS * P + WS) + ci * (P + 1)];
-              acc += ((rm >> ri) & (cm >> ci) & 1u) ? v : 0.f;
-            }
-        }
         if constexpr (WS == 0) {
           for (int ri = 0; ri < ws; ++ri)
             for (int ci = 0; ci < ws; ++ci) {

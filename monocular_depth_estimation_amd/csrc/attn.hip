@@ -36,6 +36,7 @@
 // with dK of padded keys summed into d(qk bias).  Table and bias gradients
 // are reduced per block in a fixed order into a slab and summed by a second
 // kernel: deterministic, no atomics.
+#include <cstdlib>
 #include <type_traits>
 #include <utility>
 
@@ -88,18 +89,7 @@ struct Tile {
 };
 constexpr int kOccBwd7 = 3;  // blocks per CU the 7x7 backward is built for
 constexpr int kHeads = 4;    // heads (= waves) per block
-constexpr int kWinBwd = 4;   // windows per backward block, at most
 
-// Windows per backward block: kWinBwd (amortises the table / slab work),
-// unless that leaves too few blocks (measured: C1024 15x20, 288 blocks at 4
-// windows, runs 172 -> 123 us at 1; C512 30x40's 480 blocks are still best
-// at 4).
-inline int bwd_wpb(int64_t nwin, int64_t heads) {
-  const int64_t blocks = nwin * ((heads + kHeads - 1) / kHeads);
-  if (blocks / kWinBwd >= 400) return kWinBwd;
-  const int64_t w = blocks / 1024;
-  return (int)(w < 1 ? 1 : (w > kWinBwd ? kWinBwd : w));
-}
 
 struct Geo {
   int b, h, w, c, heads, ws, shift, hp, wp, nwh, nww, n;
@@ -836,6 +826,35 @@ bool make_geo(int64_t b, int64_t h, int64_t w, int64_t c, int64_t heads, int64_t
 
 }  // namespace
 
+template <typename Kernel>
+int resident_blocks(Kernel k) {
+  int dev = 0, cus = 0, per = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0);
+  return (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
+}
+
+// Windows per backward block (measured, bs16 NewCRF stages; MDE_ATTN_BWD_WPB
+// overrides): one, so the dispatcher balances many small blocks, unless the
+// per-block slab (ntab + 2D floats per head) would get large: at 8+ rounds of
+// resident blocks, the fewest windows that fit one round (C128 120x160:
+// 6624 windows as 736 blocks of 9, 448 us; 1 per block 468 us, 4 per block
+// 483 us).  C256 60x80 at 1: 237 us (4: 288, 5: 241); C512 30x40 at 1:
+// 136 us (3: 143, 4: 154); C1024 15x20 at 1: 89 us (2: 99).
+inline int windows_per_block(int64_t nwin, int64_t heads, int64_t res) {
+  static const int forced = [] { const char* e = getenv("MDE_ATTN_BWD_WPB"); return e ? atoi(e) : 0; }();
+  if (forced > 0) return forced;
+  const int64_t blocks = nwin * ((heads + kHeads - 1) / kHeads);
+  const int64_t k = blocks < 8 * res ? 1 : (blocks + res - 1) / res;
+  return (int)(k > (1 << 20) ? (1 << 20) : k);
+}
+inline int bwd_wpb(int64_t nwin, int64_t heads, int64_t window) {
+  static const int res7 = resident_blocks(wattn_bwd_kernel<7>);
+  static const int res0 = resident_blocks(wattn_bwd_kernel<0>);
+  return windows_per_block(nwin, heads, window == 7 ? res7 : res0);
+}
+
 extern "C" {
 
 size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
@@ -844,7 +863,7 @@ size_t mde_window_attn_workspace(int64_t b, int64_t h, int64_t w, int64_t c,
   if (!make_geo(b, h, w, c, heads, window, 0, &g)) return 0;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
   const int64_t ntab = (2 * window - 1) * (2 * window - 1);
-  return sizeof(float) * (size_t)(mde::cdiv(nwin, bwd_wpb(nwin, heads)) * heads * (ntab + 2 * D));
+  return sizeof(float) * (size_t)(mde::cdiv(nwin, bwd_wpb(nwin, heads, window)) * heads * (ntab + 2 * D));
 }
 
 int mde_window_attn_fwd(const void* qk, const float* qk_bias, const void* v,
@@ -883,7 +902,7 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
   g.vb = v_bias;
   hipStream_t s = (hipStream_t)stream;
   const int64_t nwin = (int64_t)b * g.nwh * g.nww;
-  const int wpb = bwd_wpb(nwin, heads);
+  const int wpb = bwd_wpb(nwin, heads, window);
   const int nblk = (int)mde::cdiv(nwin, wpb);
   const int ntab = (2 * g.ws - 1) * (2 * g.ws - 1);
   const double bytes = 4.0 * (double)b * h * w * c * 7.0;  // q k v dO read, dq dk dv written

@@ -260,6 +260,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     loss = float(trainer.last_loss)
+    if use_graph:
+        trainer.close()  # free the graphs (captured RCCL nodes) before the group goes
     if not world.is_main:
         if dist.is_initialized():
             dist.destroy_process_group()

@@ -288,7 +288,7 @@ class GraphTrainer:
     BUCKET_BYTES = 6 << 20
 
     def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2, amp: str = "",
-                 dp_overlap: bool | None = None):
+                 dp_overlap: bool | None = None, dp_collectives: bool | None = None):
         if world.device.type != "cuda":
             raise RuntimeError("GraphTrainer needs a GPU (use Trainer on CPU)")
         self.model, self.loss_fn, self.world = model, loss_fn, world
@@ -296,6 +296,9 @@ class GraphTrainer:
         self.eager_steps = eager_steps
         self.calls = 0
         self.graphs = None
+        # the data-parallel exchange runs at N > 1; dp_collectives=True issues it
+        # in a one-rank group too (tests: the same RCCL calls, average = identity)
+        self.dp = world.size > 1 if dp_collectives is None else bool(dp_collectives)
         self.params = [p for p in model.parameters() if p.requires_grad]
         self.optimizer = torch.optim.Adam(self.params, lr, fused=True, capturable=True)
         self.flat_grad = None
@@ -319,10 +322,14 @@ class GraphTrainer:
         self.stream = torch.cuda.Stream(device=world.device)  # eager warm-up + capture stream
         # bucketed all-reduce overlapped with backward (captured into the step
         # graph over RCCL; a gloo group runs it eagerly only, see _capture);
-        # dp_overlap=True with a one-rank group issues the same collectives
+        # dp_overlap=True with a one-rank group issues the same collectives.
+        # Opt-in (MDE_DP_OVERLAP=1): hipGraphInstantiate of a step graph with
+        # captured RCCL nodes aborted the process on some MI355X boxes (DESIGN
+        # "Teardown / capture"), so N > 1 defaults to the flat scheme: graph A,
+        # one eager RCCL all-reduce, graph B.
         if dp_overlap is None:
             dp_overlap = (world.size > 1 and dist.get_backend() == "nccl"
-                          and os.environ.get("MDE_DP_OVERLAP", "1") != "0")
+                          and os.environ.get("MDE_DP_OVERLAP", "0") == "1")
         self.buckets = None
         if dp_overlap:
             self.side = torch.cuda.Stream(device=world.device)
@@ -343,7 +350,7 @@ class GraphTrainer:
         loss.backward()
         if self.buckets is not None:
             self.buckets.finish()
-        elif self.world.size > 1:
+        elif self.dp:
             grads = [p.grad for p in self.params if p.grad is not None]
             if self.flat_grad is None:
                 self.flat_grad = torch.empty(sum(g.numel() for g in grads),
@@ -353,7 +360,7 @@ class GraphTrainer:
         return loss.detach()
 
     def _unpack_and_update(self):
-        if self.world.size > 1 and self.buckets is None:
+        if self.dp and self.buckets is None:
             grads = [p.grad for p in self.params if p.grad is not None]
             flat = self.flat_grad.split([g.numel() for g in grads])
             torch._foreach_copy_(grads, [f.view_as(g) for f, g in zip(flat, grads)])
@@ -364,7 +371,7 @@ class GraphTrainer:
             dist.broadcast(self.flat_bn, 0)
 
     def _allreduce(self):
-        if self.world.size > 1 and self.buckets is None:
+        if self.dp and self.buckets is None:
             dist.all_reduce(self.flat_grad)
 
     def _zero_grad(self):
@@ -429,7 +436,7 @@ class GraphTrainer:
                                "(eager_steps >= the number of steps)")
         torch.cuda.synchronize()
         self._zero_grad()  # backward allocates .grad in the graph pool (non-bucket mode)
-        one_graph = self.world.size == 1 or self.buckets is not None
+        one_graph = not self.dp or self.buckets is not None
 
         def part_a():
             loss = self._forward_backward()
@@ -447,6 +454,18 @@ class GraphTrainer:
     def after_step(self, loader_pos: int):
         pass
 
+    def close(self):
+        """Drain the device and free the captured graphs.  Call before
+        dist.destroy_process_group(): a graph with captured RCCL collectives
+        still references the communicator, and tearing the communicator down
+        under a live graph aborts the process on this stack."""
+        torch.cuda.synchronize()
+        for g in self.graphs or ():
+            if g is not None:
+                g.reset()
+        self.graphs = None
+        torch.cuda.synchronize()
+
     def timed_replays(self, batches, replays: int = 3) -> dict:
         """Per-kernel HIP-event times of the REPLAYED step (measurement only).
 
@@ -460,7 +479,7 @@ class GraphTrainer:
         torch.cuda.synchronize()
         _abi.timing_reset()
         self._zero_grad()
-        one_graph = self.world.size == 1 or self.buckets is not None
+        one_graph = not self.dp or self.buckets is not None
 
         def part():
             loss = self._forward_backward()
@@ -482,6 +501,7 @@ class GraphTrainer:
             _abi.call("mde_timing_collect")
         out = _abi.timing_collect(resolve=False)
         _abi.timing_reset()
+        graph.reset()  # its RCCL nodes must not outlive the communicator (see close())
         return out
 
 
@@ -642,6 +662,8 @@ def main(argv=None):
                                       "step": epoch}) + "\n")
                 log.flush()
             save_checkpoint(args.checkpoint, epoch, ddp, optimizer, trainer.last_loss.cpu())
+    if hasattr(trainer, "close"):
+        trainer.close()
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -1,0 +1,46 @@
+"""Which ATen ops launch the remaining non-HIP, non-conv kernels of one eager
+cfg2 GuideDepth train step (fp32, bs 32, 640x480): torch.profiler with input
+shapes, self device time per (op, shapes), top entries.  Used to find the
+`vectorized_elementwise_kernel` launches of the steady-state profile."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from torch.profiler import ProfilerActivity, profile
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bs", type=int, default=32)
+    ap.add_argument("--top", type=int, default=40)
+    ap.add_argument("--amp", default="")
+    args = ap.parse_args()
+    from monocular_depth_estimation_amd import GuideDepth
+    from monocular_depth_estimation_amd.loss import SSIML1
+    from monocular_depth_estimation_amd.train import Trainer, init_world, make_adam, synthetic_batch
+    world = init_world()
+    torch.manual_seed(0)
+    model = GuideDepth(pretrained=False).to(world.device)
+    tr = Trainer(model, make_adam(model, 1e-4), SSIML1(1.0, 0.1, depth_norm=True), world,
+                 eval_quirk=False, amp=args.amp)
+    tr.begin_epoch()
+    batch = synthetic_batch(args.bs, 480, 640, 0, 0, world.device)
+    for _ in range(3):
+        tr.step(*batch)
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
+        tr.step(*batch)
+        torch.cuda.synchronize()
+    table = prof.key_averages(group_by_input_shape=True)
+    rows = [e for e in table if e.self_device_time_total > 0 and e.key.startswith("aten::")]
+    rows.sort(key=lambda e: -e.self_device_time_total)
+    tot = sum(e.self_device_time_total for e in rows)
+    print(f"aten self device time: {tot / 1e3:.3f} ms/step over {len(rows)} (op, shape) rows")
+    for e in rows[:args.top]:
+        print(f"{e.self_device_time_total / 1e3:8.3f} ms {e.count:4d}x  {e.key:32s} {str(e.input_shapes)[:150]}")
+
+
+if __name__ == "__main__":
+    main()

@@ -59,7 +59,7 @@ NAMES = [
     (r"dloss_(bwd_stream|masked_bwd|grad)_kernel", "depth_loss_bwd"),
     (r"loss_final_kernel", "loss_final"),
     (r"bn_stats_kernel", "bn_fwd_stats"),
-    (r"bn_coef_kernel", "bn_fwd_final"),
+    (r"bn_coef_kernel|bn_stats_merge_kernel", "bn_fwd_final"),
     (r"bn_apply_plane_kernel", "bn_fwd_apply"),
     (r"bn_apply_table_kernel", "bn_fwd_apply_small"),
     (r"bn_bwd_reduce_kernel", "bn_bwd_reduce"),

@@ -135,17 +135,30 @@ __global__ void __launch_bounds__(256)
                         const float* __restrict__ mm, int h, int w, int strips, int chunks,
                         int chunk_rows, int64_t nwaves, float gs_ssim, float gs_l1,
                         float* __restrict__ part, float* __restrict__ gx,
-                        float* __restrict__ gy) {
+                        float* __restrict__ gy, int strip_major) {
   __shared__ float red[4];
   constexpr int NC = GT ? 5 : 3;  // coefficient fields
   const int lane = threadIdx.x & 63;
   const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   float lsum = 0.f, l1sum = 0.f;
   if (wid < nwaves) {  // wave-uniform
-    const int chunk = (int)(wid % chunks);
-    const int64_t rest = wid / chunks;
-    const int strip = (int)(rest % strips);
-    const int64_t img = rest / strips;
+    // strip_major: a block's 4 waves are 4 ADJACENT strips of one chunk, so
+    // the 128-B lines two neighbouring strips share (a strip starts 8 B into
+    // a line: 64 lanes x 4 B touch 3 lines) come through one CU's L2 instead
+    // of two XCDs'; otherwise 4 consecutive chunks of one strip
+    int chunk, strip;
+    int64_t img;
+    if (strip_major) {
+      strip = (int)(wid % strips);
+      const int64_t rest = wid / strips;
+      chunk = (int)(rest % chunks);
+      img = rest / chunks;
+    } else {
+      chunk = (int)(wid % chunks);
+      const int64_t rest = wid / chunks;
+      strip = (int)(rest % strips);
+      img = rest / strips;
+    }
     const int q = strip * kSW - 2 + lane;
     const bool qin = q >= 0 && q < w;
     const bool out = lane >= 2 && lane < 2 + kSW && qin;
@@ -276,7 +289,7 @@ __global__ void __launch_bounds__(256)
 }
 
 struct StreamPlan {
-  int strips, chunks, chunk_rows;
+  int strips, chunks, chunk_rows, strip_major;
   int64_t nwaves, nblocks;
 };
 
@@ -301,6 +314,11 @@ inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w) {
   p.chunks = (int)mde::cdiv(h, p.chunk_rows);
   p.nwaves = per_chunk * p.chunks;
   p.nblocks = mde::cdiv(p.nwaves, 4);
+  static const int order = [] {  // MDE_SSIM_ORDER: wave order A/B (tools/gpu_r03d.sh)
+    const char* e = std::getenv("MDE_SSIM_ORDER");
+    return e ? std::atoi(e) : 0;
+  }();
+  p.strip_major = order;
   return p;
 }
 
@@ -390,12 +408,12 @@ int mde_ssim3_l1_fwd(const void* pred, const void* target,
     MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_stream_kernel<true>, dim3((unsigned)nblocks),
                dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
                (int)w, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv, w_l1 * inv,
-               part, (float*)grad_pred, (float*)grad_target);
+               part, (float*)grad_pred, (float*)grad_target, sp.strip_major);
   } else {
     MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_stream_kernel<false>, dim3((unsigned)nblocks),
                dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
                (int)w, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv, w_l1 * inv,
-               part, (float*)grad_pred, (float*)nullptr);
+               part, (float*)grad_pred, (float*)nullptr, sp.strip_major);
   }
   MDE_LAUNCH(mde::K_LOSS_FINAL, 8.0 * nblocks, s, loss_final_kernel, dim3(1),
              dim3(256), 0, part, (int)nblocks, inv, w_ssim, w_l1, loss);

@@ -139,10 +139,19 @@ __global__ void __launch_bounds__(256)
   __shared__ float red[4];
   constexpr int NC = GT ? 5 : 3;  // coefficient fields
   const int lane = threadIdx.x & 63;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  int64_t lb = blockIdx.x;
+  if (strip_major == 2) {
+    // XCD swizzle: physical block 8k + x runs on XCD x; give XCD x the
+    // contiguous logical range [x per + min(x, rem), ...) so neighbouring
+    // logical blocks (adjacent strips) share one XCD's L2
+    const int64_t nb = gridDim.x, per = nb / 8, rem = nb % 8;
+    const int64_t x = blockIdx.x % 8, kk = blockIdx.x / 8;
+    lb = x * per + (x < rem ? x : rem) + kk;
+  }
+  const int64_t wid = lb * 4 + (threadIdx.x >> 6);
   float lsum = 0.f, l1sum = 0.f;
   if (wid < nwaves) {  // wave-uniform
-    // strip_major: a block's 4 waves are 4 ADJACENT strips of one chunk, so
+    // strip_major (1, 2): a block's 4 waves are 4 ADJACENT strips of one chunk, so
     // the 128-B lines two neighbouring strips share (a strip starts 8 B into
     // a line: 64 lanes x 4 B touch 3 lines) come through one CU's L2 instead
     // of two XCDs'; otherwise 4 consecutive chunks of one strip

@@ -14,8 +14,10 @@ TAGS="gd nc gd_bf16" bash tools/gpu_bench.sh || exit $?
 step "aten ops"
 timeout -k 10 300 python -u tools/aten_ops_profile.py > gpurun_out/aten_ops.txt 2>&1 || exit $?
 step "ssim chunk A/B"
-for wv in 5632 2816 5632 2816; do
-  echo "MDE_SSIM_WAVES=$wv"
-  MDE_SSIM_WAVES=$wv timeout -k 10 120 python -u tools/kbench.py --only loss 2>&1 | grep ssim3 || exit 1
+for rep in 1 2; do
+  for cfg in "0 5632" "1 5632" "2 5632" "0 2816" "1 2816" "2 2816"; do
+    set -- $cfg
+    echo "order=$1 waves=$2 rep=$rep: $(MDE_SSIM_ORDER=$1 MDE_SSIM_WAVES=$2 timeout -k 10 120 python -u tools/kbench.py --only loss 2>&1 | grep ssim3)"
+  done
 done
 exit $trc

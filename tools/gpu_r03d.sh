@@ -7,12 +7,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ssim_ab
 export TMPDIR=/tmp
 for rep in 1 2; do
-  for cfg in "0 5632" "1 5632" "0 2816" "1 2816"; do
+  for cfg in "0 5632" "1 5632" "2 5632" "0 2816" "1 2816" "2 2816"; do
     set -- $cfg
     echo "order=$1 waves=$2 rep=$rep: $(MDE_SSIM_ORDER=$1 MDE_SSIM_WAVES=$2 timeout -k 10 120 python -u tools/kbench.py --only loss 2>&1 | grep ssim3)" || exit 1
   done
 done
-for cfg in "0 5632" "1 5632" "1 2816"; do
+for cfg in "0 5632" "1 5632" "2 5632" "2 2816"; do
   set -- $cfg
   for ctr in FETCH_SIZE WRITE_SIZE; do
     MDE_SSIM_ORDER=$1 MDE_SSIM_WAVES=$2 timeout -s KILL 120 rocprofv3 --pmc $ctr --output-format csv \

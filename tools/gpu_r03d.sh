@@ -1,17 +1,11 @@
 #!/bin/bash
-# Round-3 call D: SSIM stream wave-order / chunk-height A/B (time + FETCH /
-# WRITE PMC of ssim3_stream_kernel), then rocprofv3 kernel traces + PMC passes
+# Round-3 call D: SSIM stream wave-order / chunk-height A/B (FETCH / WRITE
+# PMC of ssim3_stream_kernel; timing in gpu_r03c.sh), then rocprofv3 kernel traces + PMC passes
 # of the final tree for cfg2 (fp32) and cfg4 (newcrf) via tools/gpu_profile_r03.sh.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/ssim_ab
 export TMPDIR=/tmp
-for rep in 1 2; do
-  for cfg in "0 5632" "1 5632" "2 5632" "0 2816" "1 2816" "2 2816"; do
-    set -- $cfg
-    echo "order=$1 waves=$2 rep=$rep: $(MDE_SSIM_ORDER=$1 MDE_SSIM_WAVES=$2 timeout -k 10 120 python -u tools/kbench.py --only loss 2>&1 | grep ssim3)" || exit 1
-  done
-done
 for cfg in "0 5632" "1 5632" "2 5632" "2 2816"; do
   set -- $cfg
   for ctr in FETCH_SIZE WRITE_SIZE; do

@@ -166,7 +166,8 @@ def _rccl_child(mode):
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
-    env = dict(os.environ, NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"))
+    env = dict(os.environ, NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"), MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(29517 + ("flat", "overlap").index(mode)))
     p = subprocess.run([sys.executable, "-u", os.path.join(here, "_rccl_graph_child.py"), mode],
                        env=env, cwd=os.path.dirname(here), capture_output=True, text=True,
                        timeout=300)

@@ -260,6 +260,15 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     loss = float(trainer.last_loss)
+    if world.size == 1:
+        dp_exchange = None
+    elif not use_graph:
+        dp_exchange = "DDP buckets (eager, overlapped with backward)"
+    elif trainer.buckets is not None:
+        dp_exchange = (f"{len(trainer.buckets)} gradient buckets, all_reduce(AVG) captured into the "
+                       "step graph, overlapped with backward")
+    else:
+        dp_exchange = "flat: one eager all_reduce between the two step graphs"
     if use_graph:
         trainer.close()  # free the graphs (captured RCCL nodes) before the group goes
     if not world.is_main:
@@ -349,6 +358,7 @@ def main():
         "loss_last": round(loss, 6),
         "execution": ("hipGraph replay of the whole step (GraphTrainer)" if use_graph
                       else "eager (Trainer + DDP)"),
+        "dp_exchange": dp_exchange,
         "roofline": roofline,
         "roofline_leaders": leaders,
         "path_roofline": path_roofline,

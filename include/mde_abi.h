@@ -589,6 +589,13 @@ int mde_graph_count_memsets(void* graph, int64_t* count);
  * (child graphs, host nodes, ...)} of a captured graph: the data-parallel
  * tests use it to see the RCCL collectives captured into the step graph. */
 int mde_graph_node_counts(void* graph, int64_t* counts);
+/* counts[16]: nodes per hipGraphNodeType value 0..14 (kernel, memcpy, memset,
+ * host, child graph, empty, wait event, event record, ext-semaphore signal /
+ * wait, mem alloc / free, memcpy from / to symbol, batch mem op), [15] any
+ * other type.  Diagnostic census of what a captured collective contributes. */
+int mde_graph_node_types(void* graph, int64_t* counts);
+/* hipGraphDebugDotPrint (verbose) of a captured graph to `path`. */
+int mde_graph_dot(void* graph, const char* path);
 int mde_graph_replace_memsets(void* graph, int64_t* replaced);
 
 /* ---------------------------------------------------------------------------

@@ -134,6 +134,8 @@ SIGNATURES = {
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_node_counts": (_int, [_vp, _c.POINTER(_i64)]),
+    "mde_graph_node_types": (_int, [_vp, _c.POINTER(_i64)]),
+    "mde_graph_dot": (_int, [_vp, _c.c_char_p]),
     "mde_timing_enable": (_int, [_int]),
     "mde_timing_reset": (_int, []),
     "mde_timing_collect": (_int, []),
@@ -218,6 +220,23 @@ def graph_node_counts(raw_graph: int) -> dict:
     return dict(zip(("total", "kernel", "memcpy", "memset", "event", "other"), list(c)))
 
 
+GRAPH_NODE_TYPES = ("kernel", "memcpy", "memset", "host", "graph", "empty", "wait_event",
+                    "event_record", "sem_signal", "sem_wait", "mem_alloc", "mem_free",
+                    "memcpy_from_symbol", "memcpy_to_symbol", "batch_mem_op", "other")
+
+
+def graph_node_types(raw_graph: int) -> dict:
+    """Nodes per hipGraphNodeType of a captured (uninstantiated) hipGraph, zero
+    counts omitted."""
+    c = (ctypes.c_int64 * 16)()
+    check(load().mde_graph_node_types(raw_graph, c), "mde_graph_node_types")
+    return {k: v for k, v in zip(GRAPH_NODE_TYPES, list(c)) if v}
+
+
+def graph_dot(raw_graph: int, path: str) -> None:
+    call("mde_graph_dot", raw_graph, path.encode())
+
+
 def graph_replace_memsets(raw_graph: int) -> int:
     """Swap the memset nodes of a captured, uninstantiated hipGraph for fill
     kernels (captured memsets are wrong from the second replay on; graph.hip)."""
@@ -227,14 +246,31 @@ def graph_replace_memsets(raw_graph: int) -> int:
     return n.value
 
 
-def capture_graph(fn, stream, pool=None):
+_DOT_SEQ = [0]
+
+
+def capture_graph(fn, stream, pool=None, capture_error_mode: str | None = None):
     """Capture fn() on `stream` into a torch CUDAGraph, repair its memset nodes
-    and instantiate it.  Returns (graph, fn's result, memset nodes replaced)."""
+    and instantiate it.  Returns (graph, fn's result, memset nodes replaced).
+
+    Diagnostics (environment): MDE_GRAPH_CAPTURE_MODE overrides the capture
+    mode ("global" default), MDE_GRAPH_DOT_DIR dumps every captured graph as
+    hipGraphDebugDotPrint output before and after the memset repair."""
+    mode = capture_error_mode or os.environ.get("MDE_GRAPH_CAPTURE_MODE", "global")
     g = torch.cuda.CUDAGraph(keep_graph=True)
-    with torch.cuda.graph(g, stream=stream, pool=pool):
+    with torch.cuda.graph(g, stream=stream, pool=pool, capture_error_mode=mode):
         out = fn()
-    n = graph_replace_memsets(g.raw_cuda_graph())
-    g.node_counts = graph_node_counts(g.raw_cuda_graph())
+    raw = g.raw_cuda_graph()
+    dot_dir = os.environ.get("MDE_GRAPH_DOT_DIR")
+    if dot_dir:
+        os.makedirs(dot_dir, exist_ok=True)
+        _DOT_SEQ[0] += 1
+        graph_dot(raw, os.path.join(dot_dir, f"graph{_DOT_SEQ[0]:02d}_captured.dot"))
+    g.node_types = graph_node_types(raw)
+    n = graph_replace_memsets(raw)
+    if dot_dir:
+        graph_dot(raw, os.path.join(dot_dir, f"graph{_DOT_SEQ[0]:02d}_repaired.dot"))
+    g.node_counts = graph_node_counts(raw)
     g.instantiate()
     return g, out, n
 

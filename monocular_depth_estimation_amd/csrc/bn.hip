@@ -646,10 +646,14 @@ int launch_stats(const T* x, int64_t n, int64_t c, int64_t hw, const Geo& g, flo
 // s1 + n d and s2 + d (2 s1 + n d), d = r - ref -- plain double sums; the
 // thread-strided order, the wave butterfly and the 4-wave order are fixed:
 // deterministic.
-template <typename T>
+// COEF: the same block then finalises its channel as bn_coef_kernel does (the
+// merged sums rounded to float first, exactly the values bn_coef_kernel would
+// read back from `part` with one slice): one launch instead of two.
+template <typename T, bool COEF = false>
 __global__ void __launch_bounds__(256)
     bn_stats_merge_kernel(const T* __restrict__ x, const float* __restrict__ stats, int G,
-                          int64_t hw, float* __restrict__ part) {
+                          int64_t hw, float* __restrict__ part, FwdArgs A,
+                          float* __restrict__ scale, float* __restrict__ shift) {
   __shared__ double red[2][4];
   const int64_t ch = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
@@ -683,8 +687,15 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   if (t == 0) {
-    part[ch * 2] = (float)((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]));
-    part[ch * 2 + 1] = (float)((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+    const float p0 = (float)((red[0][0] + red[0][1]) + (red[0][2] + red[0][3]));
+    const float p1 = (float)((red[1][0] + red[1][1]) + (red[1][2] + red[1][3]));
+    part[ch * 2] = p0;
+    part[ch * 2 + 1] = p1;
+    if constexpr (COEF) {
+      const FwdCh k = fwd_channel(A, x, ch, (double)p0, (double)p1, true);
+      scale[ch] = k.sc;
+      shift[ch] = k.sh;
+    }
   }
 }
 
@@ -900,11 +911,13 @@ int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float
   float* part = (float*)workspace;
   const double mb = 16.0 * (double)c * stats_blocks;
   if (dtype == MDE_BF16)
-    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<bf16>, dim3((unsigned)c), dim3(256),
-               0, (const bf16*)x, stats, (int)stats_blocks, hw, part);
+    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, (bn_stats_merge_kernel<bf16, false>), dim3((unsigned)c),
+               dim3(256), 0, (const bf16*)x, stats, (int)stats_blocks, hw, part, FwdArgs{},
+               nullptr, nullptr);
   else
-    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<float>, dim3((unsigned)c), dim3(256),
-               0, (const float*)x, stats, (int)stats_blocks, hw, part);
+    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, (bn_stats_merge_kernel<float, false>), dim3((unsigned)c),
+               dim3(256), 0, (const float*)x, stats, (int)stats_blocks, hw, part, FwdArgs{},
+               nullptr, nullptr);
   FwdArgs A{gamma, beta, prebias, part, 1, n * hw, hw, eps, momentum,
             running_mean, running_var, num_batches_tracked, save_mean, save_invstd, 1};
   if (dtype == MDE_BF16)
@@ -930,16 +943,15 @@ int mde_batchnorm_fwd_coef_stats(const void* x, const float* gamma, const float*
   const double mb = 16.0 * (double)c * stats_blocks;
   FwdArgs A{gamma, beta, prebias, part, 1, n * hw, hw, eps, momentum, running_mean, running_var,
             num_batches_tracked, save_mean, save_invstd, 1};
+  // merge + finalisation in one launch (bn_stats_merge_kernel<T, true>)
   if (dtype == MDE_BF16) {
-    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<bf16>, dim3((unsigned)c), dim3(256),
-               0, (const bf16*)x, stats, (int)stats_blocks, hw, part);
-    MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c, s, bn_coef_kernel<bf16>,
-               dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const bf16*)x, c, A, scale, shift);
+    MDE_LAUNCH(mde::K_BN_FINAL, mb + 8.0 * (double)c, s, (bn_stats_merge_kernel<bf16, true>),
+               dim3((unsigned)c), dim3(256), 0, (const bf16*)x, stats, (int)stats_blocks, hw,
+               part, A, scale, shift);
   } else {
-    MDE_LAUNCH(mde::K_BN_FINAL, mb, s, bn_stats_merge_kernel<float>, dim3((unsigned)c), dim3(256),
-               0, (const float*)x, stats, (int)stats_blocks, hw, part);
-    MDE_LAUNCH(mde::K_BN_FINAL, 8.0 * (double)c, s, bn_coef_kernel<float>,
-               dim3((unsigned)mde::cdiv(c, 4)), dim3(256), 0, (const float*)x, c, A, scale, shift);
+    MDE_LAUNCH(mde::K_BN_FINAL, mb + 8.0 * (double)c, s, (bn_stats_merge_kernel<float, true>),
+               dim3((unsigned)c), dim3(256), 0, (const float*)x, stats, (int)stats_blocks, hw,
+               part, A, scale, shift);
   }
   return MDE_OK;
 }

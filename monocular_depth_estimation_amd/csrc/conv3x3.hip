@@ -739,9 +739,13 @@ __global__ void __launch_bounds__(256, 1)
       for (int c = 0; c < 16; ++c) vg[c][i] = gi[(unsigned)(c * hw + o)];
     }
   };
-  int tile = blockIdx.x;
-  if (tile < g.ntiles) load(tile);
-  for (; tile < g.ntiles; tile += gridDim.x) {
+  // XCD-aware walk (tile_walk): the tiles above / below a tile (whose rows
+  // its halo re-reads) and the other channel groups of the same strip
+  // (blockIdx.y, same blockIdx.x % 8 -> same XCD) go through one L2
+  const TileWalk tw = tile_walk(g.ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) load(tile);
+  for (; tile < tw.end; tile += tw.step) {
     __syncthreads();  // the previous tile's operands are consumed
 #pragma unroll
     for (int i = 0; i < kWXL; ++i) {
@@ -760,7 +764,7 @@ __global__ void __launch_bounds__(256, 1)
       }
     }
     __syncthreads();
-    if (tile + (int)gridDim.x < g.ntiles) load(tile + gridDim.x);
+    if (tile + tw.step < tw.end) load(tile + tw.step);
 #pragma unroll 2
     for (int s = 0; s < KP / 4; ++s) {
       const int t = tab[4 * s + lk];
@@ -889,9 +893,13 @@ __global__ void __launch_bounds__(64 * WPB, COG == kWCO ? 2 : 3)
       for (int c = 0; c < GC; ++c) vg[c][i] = gi[(unsigned)(c * hwo + o)];
     }
   };
-  int tile = blockIdx.x;
-  if (tile < ntiles) load(tile);
-  for (; tile < ntiles; tile += gridDim.x) {
+  // XCD-aware walk (tile_walk): with gridDim.x % 8 == 0 every channel group
+  // (blockIdx.y) of a strip and the strips above / below it (the halo rows)
+  // are staged through the same XCD's L2
+  const TileWalk tw = tile_walk(ntiles);
+  int tile = tw.t0;
+  if (tile < tw.end) load(tile);
+  for (; tile < tw.end; tile += tw.step) {
     __syncthreads();  // the previous tile's operands are consumed
 #pragma unroll
     for (int i = 0; i < P::XL; ++i) {
@@ -910,7 +918,7 @@ __global__ void __launch_bounds__(64 * WPB, COG == kWCO ? 2 : 3)
       }
     }
     __syncthreads();
-    if (tile + (int)gridDim.x < ntiles) load(tile + gridDim.x);
+    if (tile + tw.step < tw.end) load(tile + tw.step);
     const float* xb = sx + (16 * hsel + li) * P::PX + lk;
     const float* gb = sg + (16 * cot + li) * P::PG + lk;
 #pragma unroll 5

@@ -86,6 +86,28 @@ int mde_graph_node_counts(void* graph, int64_t* counts) {
   return MDE_OK;
 }
 
+int mde_graph_node_types(void* graph, int64_t* counts) {
+  if (!graph || !counts) return MDE_ERR_INVALID_ARG;
+  hipGraph_t g = (hipGraph_t)graph;
+  size_t n = 0;
+  hipError_t e = hipGraphGetNodes(g, nullptr, &n);
+  if (e != hipSuccess) return (int)e;
+  std::vector<hipGraphNode_t> nodes(n);
+  if (n && (e = hipGraphGetNodes(g, nodes.data(), &n)) != hipSuccess) return (int)e;
+  for (int i = 0; i < 16; ++i) counts[i] = 0;
+  for (hipGraphNode_t node : nodes) {
+    hipGraphNodeType t;
+    if ((e = hipGraphNodeGetType(node, &t)) != hipSuccess) return (int)e;
+    ++counts[((unsigned)t < 15u) ? (int)t : 15];
+  }
+  return MDE_OK;
+}
+
+int mde_graph_dot(void* graph, const char* path) {
+  if (!graph || !path) return MDE_ERR_INVALID_ARG;
+  return (int)hipGraphDebugDotPrint((hipGraph_t)graph, path, hipGraphDebugDotFlagsVerbose);
+}
+
 int mde_graph_replace_memsets(void* graph, int64_t* replaced) {
   if (!graph) return MDE_ERR_INVALID_ARG;
   hipGraph_t g = (hipGraph_t)graph;

@@ -364,7 +364,8 @@ def se_bn_cat(ya, yb, bn_a: nn.BatchNorm2d, bn_b: nn.BatchNorm2d, pb_a, pb_b, w1
 def pointwise_ok(conv: nn.Conv2d, x) -> bool:
     """Whether this bias-folded 1x1 conv runs on the HIP pointwise kernel."""
     if (conv.kernel_size != (1, 1) or conv.stride != (1, 1) or conv.padding != (0, 0)
-            or conv.dilation != (1, 1) or conv.groups != 1 or x.dim() != 4):
+            or conv.dilation != (1, 1) or conv.groups != 1 or x.dim() != 4
+            or conv.weight.dtype != torch.float32):
         return False
     return bool(_abi.query("mde_pointwise_supported", conv.in_channels, conv.out_channels,
                            x.shape[2], x.shape[3]))
@@ -466,9 +467,12 @@ def _autocast_bf16(x) -> bool:
             and torch.get_autocast_dtype("cuda") == torch.bfloat16)
 
 
-def _conv3x3_bf16_path(cin: int, cout: int, x) -> bool:
-    """autocast-bf16 (or bf16) input of a shape the bf16 kernels take."""
+def _conv3x3_bf16_path(cin: int, cout: int, x, weight) -> bool:
+    """autocast-bf16 (or bf16) input of a shape the bf16 kernels take.  The
+    kernels read an fp32 weight (rounded to bf16 on load) and write an fp32
+    weight gradient: a weight of any other dtype never takes them."""
     return ((_autocast_bf16(x) or x.dtype == torch.bfloat16)
+            and weight.dtype == torch.float32
             and (cin, cout) in CONV3X3_HIP_BF16 and x.shape[-1] % 4 == 0)
 
 
@@ -573,7 +577,7 @@ def conv3x3s2_ok(conv: nn.Conv2d, x) -> bool:
     that are multiples of 40 or 20; fp32 outside autocast, even input width;
     MDE_S2_WGRAD=0: MIOpen)."""
     return (S2_WGRAD and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
-            and x.dim() == 4 and x.shape[-1] % 2 == 0 and conv.kernel_size == (3, 3)
+            and conv.weight.dtype == torch.float32 and x.dim() == 4 and x.shape[-1] % 2 == 0 and conv.kernel_size == (3, 3)
             and conv.stride == (2, 2) and conv.padding == (1, 1) and conv.dilation == (1, 1)
             and conv.groups == 1 and conv.padding_mode == "zeros"
             and bool(_abi.query("mde_conv3x3s2_supported", conv.in_channels, conv.out_channels,
@@ -597,10 +601,10 @@ def conv3x3_passes(conv: nn.Conv2d, x):
     autocast) to the fp32 kernels."""
     if (conv.kernel_size != (3, 3) or conv.stride != (1, 1) or conv.padding != (1, 1)
             or conv.dilation != (1, 1) or conv.groups != 1 or conv.padding_mode != "zeros"
-            or x.dim() != 4):
-        return None
+            or x.dim() != 4 or conv.weight.dtype != torch.float32):
+        return None  # the HIP kernels take an fp32 weight only (bf16 modules: MIOpen)
     cin, cout = conv.in_channels, conv.out_channels
-    if _conv3x3_bf16_path(cin, cout, x):
+    if _conv3x3_bf16_path(cin, cout, x, conv.weight):
         p, dt = CONV3X3_HIP_BF16[(cin, cout)], _abi.MDE_BF16
     elif x.dtype == torch.float32:
         p, dt = CONV3X3_HIP.get((cin, cout)), _abi.MDE_F32
@@ -614,8 +618,10 @@ def conv3x3_passes(conv: nn.Conv2d, x):
 
 
 def _conv3x3_apply(x, weight, passes, want_stats):
+    if weight.dtype != torch.float32:
+        raise TypeError(f"conv3x3: the HIP kernels take a float32 weight, got {weight.dtype}")
     cin, cout = x.shape[1], weight.shape[0]
-    if _conv3x3_bf16_path(cin, cout, x):
+    if _conv3x3_bf16_path(cin, cout, x, weight):
         return _Conv3x3Bf16.apply(x.to(torch.bfloat16), weight, tuple(passes), want_stats)
     return _Conv3x3.apply(x, weight, tuple(passes), want_stats)
 

@@ -27,9 +27,11 @@ images and depths with per-rank seeds.
 from __future__ import annotations
 
 import argparse
+import atexit
 import json
 import os
 import time
+import weakref
 from dataclasses import dataclass
 
 import torch
@@ -270,19 +272,25 @@ class GraphTrainer:
     copy; replays reuse those static buffers).  N == 1: one graph (forward,
     loss, backward, fused capturable Adam).
 
-    N > 1 over RCCL ("nccl"): the gradients are views of ~6 MB bucket buffers
-    (parameters in reverse registration order, i.e. about the order backward
-    finishes them).  A post-accumulate hook counts each bucket's parameters;
-    when the last one is final the bucket is scaled by 1/N and all-reduced on
-    a side stream that forks from the backward stream at that point, so the
-    RCCL collectives are captured INTO the step graph and overlap the rest of
-    the backward; the Adam step joins the side stream.  One graph, no pack /
-    unpack copies.  (gloo, or MDE_DP_OVERLAP=0: graph A -> one flat all-reduce
-    outside the graph -> graph B, the round-1 scheme.)  The BN running
-    statistics (one flat buffer) are broadcast from rank 0 before each
-    forward, as DDP's broadcast_buffers does.  Inputs are copied into static
-    device buffers.  CUDA only; BN stays in train mode (the eval-mode quirk
-    changes the graph, use Trainer for that).
+    N > 1 over RCCL ("nccl"), the default: the gradients are views of ~6 MB
+    bucket buffers (parameters in reverse registration order, i.e. about the
+    order backward finishes them).  A post-accumulate hook counts each
+    bucket's parameters; when the last one is final the bucket is
+    all-reduced with ReduceOp.AVG on a side stream that forks from the
+    backward stream at that point, so the RCCL collectives are captured INTO
+    the step graph and overlap the rest of the backward; the Adam step joins
+    the side stream.  One graph, no pack / unpack copies.  MDE_DP_OVERLAP=0
+    (and any gloo group, whose collectives cannot be captured) selects the
+    flat scheme instead: graph A (forward, backward, the gradients packed
+    into one buffer and scaled by 1/N) -> one eager all_reduce(SUM) outside
+    the graph -> graph B (unpack, Adam).  The BN running statistics (one
+    flat buffer) are broadcast from rank 0 before each forward, as DDP's
+    broadcast_buffers does.  Inputs are copied into static device buffers.
+    CUDA only; BN stays in train mode (the eval-mode quirk changes the graph,
+    use Trainer for that).  close() frees the captured graphs; it must run
+    before dist.destroy_process_group() (a graph holding captured RCCL
+    collectives references the communicator) and is registered to run at
+    interpreter exit too.
     """
 
     BUCKET_BYTES = 6 << 20
@@ -320,16 +328,14 @@ class GraphTrainer:
             dist.broadcast(self.flat_bn, 0)
         self.static_image = self.static_depth = None
         self.stream = torch.cuda.Stream(device=world.device)  # eager warm-up + capture stream
-        # bucketed all-reduce overlapped with backward (captured into the step
-        # graph over RCCL; a gloo group runs it eagerly only, see _capture);
-        # dp_overlap=True with a one-rank group issues the same collectives.
-        # Opt-in (MDE_DP_OVERLAP=1): hipGraphInstantiate of a step graph with
-        # captured RCCL nodes aborted the process on some MI355X boxes (DESIGN
-        # "Teardown / capture"), so N > 1 defaults to the flat scheme: graph A,
-        # one eager RCCL all-reduce, graph B.
+        # bucketed all-reduce overlapped with backward, captured into the step
+        # graph: the N > 1 default over RCCL (MDE_DP_OVERLAP=0 selects the flat
+        # scheme; a gloo group cannot capture collectives and takes the flat
+        # scheme too).  dp_overlap=True with a one-rank group issues the same
+        # collectives (tests).
         if dp_overlap is None:
             dp_overlap = (world.size > 1 and dist.get_backend() == "nccl"
-                          and os.environ.get("MDE_DP_OVERLAP", "0") == "1")
+                          and os.environ.get("MDE_DP_OVERLAP", "1") != "0")
         self.buckets = None
         if dp_overlap:
             self.side = torch.cuda.Stream(device=world.device)
@@ -337,6 +343,11 @@ class GraphTrainer:
         self.last_loss = None
         self.loss_sum = torch.zeros((), device=world.device)
         self.loss_count = 0
+        # graphs with captured collectives must not outlive the communicator:
+        # free them at exit even if the caller never calls close()
+        ref = weakref.ref(self)
+        self._atexit = lambda: (ref() is not None and ref().close())
+        atexit.register(self._atexit)
 
     def begin_epoch(self):
         self.model.train()
@@ -459,8 +470,10 @@ class GraphTrainer:
         dist.destroy_process_group(): a graph with captured RCCL collectives
         still references the communicator, and tearing the communicator down
         under a live graph aborts the process on this stack."""
+        if self.graphs is None:
+            return
         torch.cuda.synchronize()
-        for g in self.graphs or ():
+        for g in self.graphs:
             if g is not None:
                 g.reset()
         self.graphs = None

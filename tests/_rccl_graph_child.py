@@ -6,10 +6,10 @@ identity), GuideDepth 2x64x96, 6 steps (2 eager, capture, 3 replays), against
 the eager Trainer under MIOpen's deterministic solvers.
 
   flat     graph A (forward, backward, flat pack + 1/N) -> one EAGER RCCL
-           all_reduce -> graph B (unpack, Adam): the default N > 1 scheme;
+           all_reduce -> graph B (unpack, Adam): MDE_DP_OVERLAP=0 / gloo;
   overlap  per-bucket all_reduce(AVG) on a side stream captured INTO the step
-           graph (opt-in, MDE_DP_OVERLAP=1), plus the node census: exactly one
-           collective's worth of nodes per bucket.
+           graph (the N > 1 default over RCCL), plus the node census: exactly
+           one collective's worth of nodes per bucket.
 
 Runs in its own process so that a runtime abort (SIGABRT) cannot take the
 test session down with it.  Exit 0 = every assertion held.
@@ -63,13 +63,17 @@ def main(mode):
         torch.cuda.synchronize()
         g1, _, _ = _abi.capture_graph(lambda: dist.all_reduce(probe, op=dist.ReduceOp.AVG), s)
         per_collective = g1.node_counts["total"]
+        print(f"probe collective nodes: {g1.node_types}", flush=True)
         assert per_collective >= 1, g1.node_counts
         g1.replay()
         torch.cuda.synchronize()
         assert float(probe.min()) == 1.0 and float(probe.max()) == 1.0
         g1.reset()
+    print(f"{mode}: eager reference done, graph trainer next", flush=True)
     tr, model, losses = _run(lambda m: GraphTrainer(
         m, loss_fn, world, lr=1e-4, dp_overlap=(mode == "overlap"), dp_collectives=True))
+    print(f"{mode}: step graph nodes: {[g.node_types for g in tr.graphs if g is not None]}",
+          flush=True)
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) <= 1e-6 * max(1.0, abs(b)), (losses, ref_losses)
     for n, p in model.named_parameters():

@@ -166,6 +166,12 @@ def _rccl_child(mode):
     import subprocess
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
+    if os.environ.get("MDE_RCCL_INPROC") == "1":  # diagnosis: run in the test process itself
+        sys.path.insert(0, here)
+        import _rccl_graph_child
+        os.environ["MASTER_PORT"] = str(29517 + ("flat", "overlap").index(mode))
+        _rccl_graph_child.main(mode)
+        return 0, f"OK {mode}"
     env = dict(os.environ, NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"), MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(29517 + ("flat", "overlap").index(mode)))
     p = subprocess.run([sys.executable, "-u", os.path.join(here, "_rccl_graph_child.py"), mode],
@@ -177,25 +183,22 @@ def _rccl_child(mode):
 
 @pytest.mark.timeout(400)
 def test_flat_rccl_allreduce_graph_matches_eager():
-    """The default N > 1 GraphTrainer scheme over RCCL, in a one-rank "nccl"
-    group with the exchange forced on: graph A (forward, backward, flat pack
-    x 1/N), one eager RCCL all_reduce, graph B (unpack, Adam) == the eager
-    Trainer to 1e-6 in every loss and parameter (tests/_rccl_graph_child.py)."""
+    """The flat N > 1 GraphTrainer scheme over RCCL (MDE_DP_OVERLAP=0, and
+    any gloo group), in a one-rank "nccl" group with the exchange forced on:
+    graph A (forward, backward, flat pack x 1/N), one eager RCCL all_reduce,
+    graph B (unpack, Adam) == the eager Trainer to 1e-6 in every loss and
+    parameter (tests/_rccl_graph_child.py)."""
     rc, out = _rccl_child("flat")
     assert rc == 0 and "OK flat" in out, out
 
 
 @pytest.mark.timeout(400)
 def test_bucketed_overlapped_allreduce_graph_matches_eager():
-    """The opt-in overlapped scheme (MDE_DP_OVERLAP=1): gradients as views of
-    bucket buffers, each bucket all-reduced (AVG) over RCCL on a side stream
-    from a post-accumulate hook, captured INTO the step graph; replayed step ==
-    eager Trainer to 1e-6, every parameter in exactly one bucket, and the graph
-    census: one collective's worth of nodes per bucket.  hipGraphInstantiate of
-    that graph aborted the process (SIGABRT) on some MI355X boxes of this pool
-    while passing on others, which is why the scheme is opt-in: a SIGABRT is
-    reported as an expected failure, anything else must pass."""
+    """The N > 1 default over RCCL: gradients as views of bucket buffers, each
+    bucket all-reduced (AVG) over RCCL on a side stream from a
+    post-accumulate hook, captured INTO the step graph; replayed step ==
+    eager Trainer to 1e-6, every parameter in exactly one bucket, and the
+    graph census: one collective's worth of nodes per bucket.  Runs in a child
+    process; any abort of it fails the test."""
     rc, out = _rccl_child("overlap")
-    if rc in (-6, 134):
-        pytest.xfail("captured-RCCL step graph aborted (SIGABRT) on this box:\n" + out[-1500:])
     assert rc == 0 and "OK overlap" in out, out

@@ -120,3 +120,17 @@ def test_allreduce_buckets_cover_every_parameter_once():
     sizes = [sum(p.numel() * p.element_size() for p in g) for g in groups]
     assert all(s >= GraphTrainer.BUCKET_BYTES for s in sizes[:-1]) and len(groups) >= 2
     assert bucket_groups([], 1) == []
+
+
+def test_hip_conv_paths_refuse_non_fp32_weights():
+    """The HIP 3x3 / 1x1 kernels read a float* weight and write a
+    float* weight gradient: a module cast to bf16 must not take
+    them (MIOpen runs it), and the functional conv3x3 refuses the weight."""
+    from monocular_depth_estimation_amd import nn as mnn
+    x = torch.rand(1, 16, 8, 8, dtype=torch.bfloat16)
+    c3 = torch.nn.Conv2d(16, 16, 3, padding=1, bias=False).bfloat16()
+    assert mnn.conv3x3_passes(c3, x) is None
+    c1 = torch.nn.Conv2d(16, 8, 1, bias=False).bfloat16()
+    assert mnn.pointwise_ok(c1, x) is False
+    with pytest.raises(TypeError, match="float32 weight"):
+        mnn._conv3x3_apply(x, c3.weight, (True, True, True), False)

@@ -282,6 +282,43 @@ def _main():
                     w, _abi.ptr(ws), 0, st), a.reps), flop, nb)
             report_tf(f"conv3x3 wgrad MIOpen {tag}", timeit(
                 lambda: torch.nn.grad.conv2d_weight(x, wt.shape, gy, padding=1), a.reps), flop, nb)
+    if want("convbf"):
+        # bf16 MFMA 3x3 convs (cfg3 autocast shapes, bs 32) vs MIOpen bf16; frac
+        # of the 2.5 PF bf16 peak, GBps algorithmic (2-byte activations)
+        def report_bf(name, ms, flop, nbytes):
+            tf = flop / (ms * 1e-3) / 1e12
+            gbs = nbytes / (ms * 1e-3) / 1e9
+            rows.append({"op": name, "ms": round(ms, 4), "TFLOPs": round(tf, 1), "GBps": round(gbs, 1),
+                         "frac": round(tf / 2516.6, 3), "hbm_frac": round(gbs / 8000, 3)})
+            print(f"{name:44s} {ms * 1e3:9.1f} us {tf:8.1f} TF/s {gbs:7.0f} GB/s ({gbs / 8000:5.1%})",
+                  flush=True)
+        bf = torch.bfloat16
+        tconv = torch.nn.functional.conv2d
+        for cin, cout, h, w in ((16, 16, 480, 640), (32, 32, 240, 320)):
+            x = (torch.rand(n, cin, h, w, device=dev) - 0.5).to(bf)
+            wt = torch.rand(cout, cin, 3, 3, device=dev) - 0.5
+            gy = (torch.rand(n, cout, h, w, device=dev) - 0.5).to(bf)
+            y = torch.empty_like(gy)
+            gx = torch.empty_like(x)
+            gw = torch.empty_like(wt)
+            ws = torch.empty(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w, 1) // 4 + 1,
+                             device=dev)
+            st = _abi.stream_of(x)
+            flop = 2.0 * n * h * w * cout * cin * 9
+            nb = 2.0 * n * h * w * (cin + cout)
+            tag = f"{cin}->{cout} {h}x{w}"
+            report_bf(f"conv3x3 bf16 fwd HIP {tag}", timeit(lambda: _abi.call(
+                "mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, cin, cout, h, w, 1,
+                st), a.reps), flop, nb)
+            report_bf(f"conv3x3 bf16 dgrad HIP {tag}", timeit(lambda: _abi.call(
+                "mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, cin, cout, h, w,
+                1, st), a.reps), flop, nb)
+            report_bf(f"conv3x3 bf16 wgrad HIP {tag}", timeit(lambda: _abi.call(
+                "mde_conv3x3_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h,
+                w, _abi.ptr(ws), 1, st), a.reps), flop, nb)
+            wb = wt.to(bf)
+            report_bf(f"conv3x3 bf16 fwd MIOpen {tag}", timeit(lambda: tconv(x, wb, None, 1, 1), a.reps),
+                      flop, nb)
     if a.json:
         json.dump(rows, open(a.json, "w"), indent=1)
 

@@ -576,6 +576,49 @@ int mde_eval_sums(const void* pred, const void* gt, int64_t n, int64_t h, int64_
                   void* workspace, double* sums, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
+ * Wide 1x1 convolutions (NCHW fp32, bias-free, stride 1 or 2, padding 0):
+ * DDRNet's Bottleneck conv1 / conv3, the residual downsample, compression3 /
+ * compression4 and DAPPM's 1x1 convs
+ * (src/GuideDepth/model/DDRNet_23_slim.py:79,84,121-171,245,250,294-296),
+ * which MIOpen runs as NHWC implicit GEMMs behind NCHW <-> NHWC transposes.
+ * cin, cout multiples of 32; ho * wo a multiple of 4 (ho = (h-1)/stride+1);
+ * stride 2 needs an even w.  mde_conv1x1_supported says whether a shape is
+ * one.  fwd: y[n,cout,ho,wo]; bwd_data: gx[n,cin,h,w] fully overwritten
+ * (zeros at the odd positions of a stride-2 conv); wgrad: gweight[cout,cin]
+ * overwritten, deterministic (workspace from mde_conv1x1_wgrad_workspace).
+ * ------------------------------------------------------------------------- */
+int mde_conv1x1_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int stride,
+                          int dtype);
+int mde_conv1x1_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                    int64_t cout, int64_t h, int64_t w, int stride, int dtype, void* stream);
+int mde_conv1x1_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, int stride, int dtype,
+                         void* stream);
+size_t mde_conv1x1_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                   int stride, int dtype);
+int mde_conv1x1_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, int stride, void* workspace, int dtype,
+                      void* stream);
+
+/* ---------------------------------------------------------------------------
+ * Wide stride-2 3x3 convolutions (padding 1, bias-free, NCHW fp32): forward
+ * and data gradient.  DDRNet's stem conv (32 -> 32), the first BasicBlock conv
+ * of layer2 / 3 / 4, down3 / down4 and layer5's Bottleneck conv2
+ * (src/GuideDepth/model/DDRNet_23_slim.py:80,232-233,254-265 and :41-72 via
+ * _make_layer :291-309), which MIOpen runs as Winograd or NHWC implicit GEMMs
+ * behind transposes.  h, w: input sizes (w even); cin, cout multiples of 32;
+ * the *_supported queries say whether a shape has a kernel.  fwd:
+ * y[n,cout,(h-1)/2+1,(w-1)/2+1]; bwd_data: gx[n,cin,h,w] fully overwritten.
+ * The weight gradient is mde_conv3x3s2_wgrad (above).
+ * ------------------------------------------------------------------------- */
+int mde_conv3x3s2_fwd_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype);
+int mde_conv3x3s2_dgrad_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype);
+int mde_conv3x3s2_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
+int mde_conv3x3s2_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,
+                           int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
+
+/* ---------------------------------------------------------------------------
  * Captured-graph repair (no reference counterpart: the reference runs its step
  * eagerly, src/train.py:83-114; the build replays it from a hipGraph).
  * `graph` is a hipGraph_t that has been captured but not instantiated.  On

@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from ...functional import bilinear_resize
-from ...nn import BatchNorm2d, conv_nobias, run_sequential
+from ...nn import BatchNorm2d, Conv2d, conv_nobias, run_sequential
 
 BN_MOMENTUM = 0.1
 
@@ -30,7 +30,7 @@ def _bn(c, act="none"):
 
 def conv3x3(in_planes, out_planes, stride=1):
     """3x3 convolution, padding 1, no bias (reference :35-38)."""
-    return nn.Conv2d(in_planes, out_planes, 3, stride=stride, padding=1, bias=False)
+    return Conv2d(in_planes, out_planes, 3, stride=stride, padding=1, bias=False)
 
 
 class BasicBlock(nn.Module):
@@ -65,10 +65,10 @@ class Bottleneck(nn.Module):
 
     def __init__(self, inplanes, planes, stride=1, downsample=None, no_relu=True):
         super().__init__()
-        self.conv1 = nn.Conv2d(inplanes, planes, 1, bias=False)
+        self.conv1 = Conv2d(inplanes, planes, 1, bias=False)
         self.bn1 = _bn(planes, "relu")
         self.conv2, self.bn2 = conv3x3(planes, planes, stride), _bn(planes, "relu")
-        self.conv3 = nn.Conv2d(planes, planes * self.expansion, 1, bias=False)
+        self.conv3 = Conv2d(planes, planes * self.expansion, 1, bias=False)
         self.bn3 = _bn(planes * self.expansion, "none" if no_relu else "relu")
         self.relu = nn.ReLU(inplace=True)
         self.downsample = downsample
@@ -85,7 +85,7 @@ def _pre_act(cin, cout, k, pool=None):
     """[pool] -> BN+ReLU (fused; Identity keeps the ReLU slot) -> conv(k, bias=False)."""
     mods = [] if pool is None else [pool]
     mods += [_bn(cin, "relu"), nn.Identity(),
-             nn.Conv2d(cin, cout, k, padding=k // 2, bias=False)]
+             Conv2d(cin, cout, k, padding=k // 2, bias=False)]
     return nn.Sequential(*mods)
 
 
@@ -125,7 +125,7 @@ class segmenthead(nn.Module):  # noqa: N801  (reference class name)
     def __init__(self, inplanes, interplanes, outplanes, scale_factor=None):
         super().__init__()
         self.bn1 = _bn(inplanes, "relu")
-        self.conv1 = nn.Conv2d(inplanes, interplanes, 3, padding=1, bias=False)
+        self.conv1 = Conv2d(inplanes, interplanes, 3, padding=1, bias=False)
         self.bn2 = _bn(interplanes, "relu")
         self.relu = nn.ReLU(inplace=True)
         self.conv2 = nn.Conv2d(interplanes, outplanes, 1, padding=0, bias=True)
@@ -145,7 +145,7 @@ def _make_layer(block, inplanes, planes, blocks, stride=1):
     downsample = None
     if stride != 1 or inplanes != planes * block.expansion:
         downsample = nn.Sequential(
-            nn.Conv2d(inplanes, planes * block.expansion, 1, stride=stride, bias=False),
+            Conv2d(inplanes, planes * block.expansion, 1, stride=stride, bias=False),
             _bn(planes * block.expansion))
     layers = [block(inplanes, planes, stride, downsample)]
     for i in range(1, blocks):
@@ -179,8 +179,8 @@ class DualResNet(nn.Module):
         for i in range(4):
             setattr(self, f"layer{i + 1}",
                     _make_layer(block, widths[i], widths[i + 1], layers[i], stride=1 if i == 0 else 2))
-        self.compression3 = nn.Sequential(nn.Conv2d(planes * 4, hp, 1, bias=False), _bn(hp))
-        self.compression4 = nn.Sequential(nn.Conv2d(planes * 8, hp, 1, bias=False), _bn(hp))
+        self.compression3 = nn.Sequential(Conv2d(planes * 4, hp, 1, bias=False), _bn(hp))
+        self.compression4 = nn.Sequential(Conv2d(planes * 8, hp, 1, bias=False), _bn(hp))
         self.down3 = nn.Sequential(conv3x3(hp, planes * 4, 2), _bn(planes * 4))
         self.down4 = nn.Sequential(conv3x3(hp, planes * 4, 2), _bn(planes * 4, "relu"), nn.Identity(),
                                    conv3x3(planes * 4, planes * 8, 2), _bn(planes * 8))

@@ -131,6 +131,16 @@ SIGNATURES = {
     "mde_colsum_workspace": (_sz, [_i64, _i64]),
     "mde_colsum": (_int, [_vp, _vp, _i64, _i64, _vp, _int, _vp]),
     "mde_gelu_bwd_colsum": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _int, _vp]),
+    "mde_conv1x1_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int]),
+    "mde_conv1x1_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "mde_conv1x1_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "mde_conv1x1_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _int, _int]),
+    "mde_conv1x1_wgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp, _int,
+                                 _vp]),
+    "mde_conv3x3s2_fwd_supported": (_int, [_i64, _i64, _i64, _i64, _int]),
+    "mde_conv3x3s2_dgrad_supported": (_int, [_i64, _i64, _i64, _i64, _int]),
+    "mde_conv3x3s2_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_conv3x3s2_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_node_counts": (_int, [_vp, _c.POINTER(_i64)]),

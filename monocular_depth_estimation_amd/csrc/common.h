@@ -68,6 +68,12 @@ enum Kid : int {
   K_C3_WGRAD_BF16,
   K_C3_WGRAD_WIDE,  // the 64 / 128 / 256-channel NCHW weight gradients
   K_C3_WGRAD_S2,    // the stride-2 stem convolutions' weight gradients
+  K_C1_FWD,         // DDRNet's wide 1x1 convolutions (conv1x1.hip)
+  K_C1_DGRAD,
+  K_C1_WGRAD,
+  K_C1_WREDUCE,
+  K_C3S2_FWD,       // DDRNet's wide stride-2 3x3 convolutions (conv3x3s2.hip)
+  K_C3S2_DGRAD,
   K_COUNT
 };
 

@@ -1,0 +1,513 @@
+// 1x1 convolutions at DDRNet's wide channel counts (NCHW fp32, bias-free,
+// stride 1 or 2) on v_mfma_f32_32x32x2_f32 (exact f32 products, f32
+// accumulation), with no NCHW <-> NHWC transposes.
+//
+// Reference call sites (src/GuideDepth/model/DDRNet_23_slim.py): the
+// Bottleneck's conv1 / conv3 (:79,84), the residual downsample of every stage
+// (:294-296, stride 2 for layer2/3/4/5), compression3 / compression4
+// (:245,250), DAPPM's scale0 / shortcut / compression and the pooled branches
+// (:121-171).  MIOpen runs these (and their gradients) as NHWC implicit GEMMs
+// behind batched transposes and SubTensorOp zero fills (~1.6 ms of the cfg2
+// step, tools/conv_kernel_map.py); here every pass is one NCHW kernel.
+//
+// Channel mix (forward, and the data gradient with the transposed weight):
+//   out[n][m][q] = sum_k A[m][k] in[n][k][q']      A = W (fwd) or W^T (dgrad)
+// M = output channels, N = pixels of one image, K = input channels, as
+// 128 x 128 (or 64 / 32 x 128) block tiles; K in chunks of 32 staged in LDS
+// (A rows [m][k], pitch 34 words; B rows [k][q], pitch BQ + 32): every MFMA
+// operand is one conflict-free ds_read_b32.  Stride 2: the forward gathers
+// the even input pixels (q' = 2r W + 2c); the data gradient writes gx at the
+// even positions and zeros at the others (the 1x1 / s2 conv's gradient there).
+//
+// Weight gradient: G[co][ci] = sum_{n,q} gy[n][co][q] x[n][ci][q'], an outer
+// product over all pixels: block tiles of (co, ci), the pixel range split
+// over blocks (split-K), per-block partials in a slab summed in block order
+// by a second kernel (deterministic, no atomics).
+#include "common.h"
+
+namespace {
+
+using f16v = float __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f16v mfma32(float a, float b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+constexpr int KC = 32;   // K values staged per chunk
+constexpr int KCP = 34;  // LDS pitch of a [row][k] tile: 34 i mod 64 distinct for i < 32
+
+// Blocks b and b + 8 share an XCD (round-robin placement): logical block
+// order with consecutive ids on one XCD, so the tiles that share an input
+// chunk (consecutive logical ids) go through the same L2.  `total` logical
+// blocks; the grid is rounded up to a multiple of 8.
+__device__ __forceinline__ int xcd_logical(int total) {
+  const int g = gridDim.x, per = g >> 3;
+  const int b = blockIdx.x;
+  const int l = (b & 7) * per + (b >> 3);
+  return l < total ? l : -1;
+}
+
+inline unsigned xcd_grid(int64_t total) { return (unsigned)((total + 7) / 8 * 8); }
+
+// ------------------------------------------------------------- channel mix
+// BM x BQ block tile, wave tile (32 MT) x (32 QT), 4 waves.
+// SIN = 2: input pixel of q is (2 (q / wo), 2 (q % wo)) of a hin x win plane.
+// SOUT = 2: output value of q goes to (2 r, 2 c) of an hout x wout plane
+// (wout even), zeros to (2r, 2c+1), (2r+1, 2c), (2r+1, 2c+1).
+// TRANSA: A[m][k] = wt[k * M + m] (the data gradient: W is [K = co][M = ci]).
+template <int BM, int BQ, int MT, int QT, int SIN, int SOUT, bool TRANSA>
+__global__ void __launch_bounds__(256)
+    cm_kernel(const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out,
+              int K, int M, int hin, int win, int wo, int Q, int hout, int wout, int qtiles,
+              int mtiles, int total) {
+  constexpr int WQ = BQ / (32 * QT), WM = BM / (32 * MT);
+  static_assert(WQ * WM == 4, "four waves per block");
+  constexpr int BQP = BQ + 32;
+  constexpr int AV = BM * KC / 1024;  // float4 of A per thread and chunk
+  constexpr int BV = KC * BQ / 1024;  // float4 of B per thread and chunk
+  static_assert(AV >= 1 && BV >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) float sA[BM * KCP];
+  __shared__ __attribute__((aligned(16))) float sB[KC * BQP];
+
+  const int lb = xcd_logical(total);
+  if (lb < 0) return;
+  const int mt = lb % mtiles, rest = lb / mtiles;
+  const int qt = rest % qtiles, img = rest / qtiles;
+  const int m0 = mt * BM, q0 = qt * BQ;
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WQ, wq = wv % WQ;
+  const int64_t hwin = (int64_t)hin * win;
+  const float* inb = in + (int64_t)img * K * hwin;
+
+  float4 ra[AV], rb[BV];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      if constexpr (TRANSA) {
+        const int k = e / BM, m = e % BM;
+        ra[i] = *reinterpret_cast<const float4*>(wt + (int64_t)(k0 + k) * M + m0 + m);
+      } else {
+        const int m = e / KC, k = e % KC;
+        ra[i] = *reinterpret_cast<const float4*>(wt + (int64_t)(m0 + m) * K + k0 + k);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      const int k = e / BQ, q = q0 + e % BQ;
+      const float* src = inb + (int64_t)(k0 + k) * hwin;
+      if constexpr (SIN == 1) {
+        // Q % 4 == 0: a float4 is all in or all out; out-of-range loads a
+        // real element (q = 0) and is zeroed at store time
+        const float4 t = *reinterpret_cast<const float4*>(src + (q < Q ? q : 0));
+        rb[i] = q < Q ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int qq = q + j, r = qq / wo, c = qq - r * wo;
+          const float t = src[qq < Q ? (int64_t)(2 * r) * win + 2 * c : 0];
+          v[j] = qq < Q ? t : 0.f;
+        }
+        rb[i] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      if constexpr (TRANSA) {
+        const int k = e / BM, m = e % BM;
+        sA[(m + 0) * KCP + k] = ra[i].x;
+        sA[(m + 1) * KCP + k] = ra[i].y;
+        sA[(m + 2) * KCP + k] = ra[i].z;
+        sA[(m + 3) * KCP + k] = ra[i].w;
+      } else {
+        const int m = e / KC, k = e % KC;
+        *reinterpret_cast<float2*>(sA + m * KCP + k) = make_float2(ra[i].x, ra[i].y);
+        *reinterpret_cast<float2*>(sA + m * KCP + k + 2) = make_float2(ra[i].z, ra[i].w);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      const int k = e / BQ, q = e % BQ;
+      *reinterpret_cast<float4*>(sB + k * BQP + q) = rb[i];
+    }
+  };
+
+  f16v acc[MT][QT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < QT; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+
+  const float* pa = sA + (wm * 32 * MT + li) * KCP + h;
+  const float* pb = sB + h * BQP + wq * 32 * QT + li;
+  load(0);
+  for (int k0 = 0; k0 < K; k0 += KC) {
+    __syncthreads();  // the previous chunk's operands are consumed
+    store();
+    __syncthreads();
+    if (k0 + KC < K) load(k0 + KC);
+#pragma unroll
+    for (int s = 0; s < KC / 2; ++s) {
+      float a[MT], b[QT];
+#pragma unroll
+      for (int x = 0; x < MT; ++x) a[x] = pa[x * 32 * KCP + 2 * s];
+#pragma unroll
+      for (int y = 0; y < QT; ++y) b[y] = pb[2 * s * BQP + y * 32];
+#pragma unroll
+      for (int x = 0; x < MT; ++x)
+#pragma unroll
+        for (int y = 0; y < QT; ++y) acc[x][y] = mfma32(a[x], b[y], acc[x][y]);
+    }
+  }
+
+  // D: lane column = pixel (li), rows = channels (r & 3) + 8 (r >> 2) + 4 h
+  float* ob = out + (int64_t)img * M * hout * wout;
+#pragma unroll
+  for (int y = 0; y < QT; ++y) {
+    const int q = q0 + wq * 32 * QT + 32 * y + li;
+    if (q >= Q) continue;
+    int64_t po = q;
+    int rr = 0, cc = 0;
+    if constexpr (SOUT == 2) {
+      rr = q / wo;
+      cc = q - rr * wo;
+      po = (int64_t)(2 * rr) * wout + 2 * cc;
+    }
+#pragma unroll
+    for (int x = 0; x < MT; ++x)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 * MT + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * h;
+        float* dst = ob + (int64_t)m * hout * wout + po;
+        if constexpr (SOUT == 1) {
+          *dst = acc[x][y][r];
+        } else {
+          *reinterpret_cast<float2*>(dst) = make_float2(acc[x][y][r], 0.f);
+          if (2 * rr + 1 < hout) *reinterpret_cast<float2*>(dst + wout) = make_float2(0.f, 0.f);
+        }
+      }
+  }
+}
+
+// ----------------------------------------------------------- weight gradient
+// G[co][ci] partial over pixel chunks [c_begin, c_end) of the N*Q pixels
+// (chunks of 32): block tile BCO x BCI, wave tile (32 MT) x (32 NT).
+template <int BCO, int BCI, int MT, int NT, int SIN>
+__global__ void __launch_bounds__(256)
+    c1_wgrad_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                    float* __restrict__ part, int CO, int CI, int Q, int hin, int win, int wo,
+                    int64_t npix, int nchunks, int ksplit, int cotiles, int citiles, int total) {
+  constexpr int WN = BCI / (32 * NT), WMv = BCO / (32 * MT);
+  static_assert(WN * WMv == 4, "four waves per block");
+  constexpr int AV = BCO * KC / 1024, BV = BCI * KC / 1024;
+  static_assert(AV >= 1 && BV >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) float sA[BCO * KCP];
+  __shared__ __attribute__((aligned(16))) float sB[BCI * KCP];
+  const int lb = xcd_logical(total);
+  if (lb < 0) return;
+  const int ntile = cotiles * citiles;
+  const int tile = lb % ntile, ks = lb / ntile;
+  const int cot = tile % cotiles, cit = tile / cotiles;
+  const int co0 = cot * BCO, ci0 = cit * BCI;
+  const int c_begin = (int)((int64_t)nchunks * ks / ksplit);
+  const int c_end = (int)((int64_t)nchunks * (ks + 1) / ksplit);
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WN, wn = wv % WN;
+  const int64_t hwin = (int64_t)hin * win;
+
+  float4 ra[AV], rb[BV];
+  auto load = [&](int chunk) {
+    const int64_t p0 = (int64_t)chunk * KC;
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      const int row = e / KC, k = e % KC;
+      const int64_t g = p0 + k;  // 4 pixels of one image (Q % 4 == 0)
+      const bool ok = g < npix;
+      const bool rok = ok && co0 + row < CO;  // rows past CO: a 128-row tile over 64 channels
+      const int64_t n = ok ? g / Q : 0, q = ok ? g - n * Q : 0;
+      const int cr = co0 + row < CO ? co0 + row : CO - 1;
+      const float4 t = *reinterpret_cast<const float4*>(gy + (n * CO + cr) * (int64_t)Q + q);
+      ra[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      const int row = e / KC, k = e % KC;
+      const int64_t g = p0 + k;
+      const bool ok = g < npix && ci0 + row < CI;
+      const int64_t n = g < npix ? g / Q : 0, q = g < npix ? g - n * Q : 0;
+      const float* src = x + (n * CI + (ci0 + row < CI ? ci0 + row : CI - 1)) * hwin;
+      if constexpr (SIN == 1) {
+        const float4 t = *reinterpret_cast<const float4*>(src + q);
+        rb[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      } else {
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int qq = (int)q + j, r = qq / wo, c = qq - r * wo;
+          const float t = src[(int64_t)(2 * r) * win + 2 * c];
+          v[j] = ok ? t : 0.f;
+        }
+        rb[i] = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      const int row = e / KC, k = e % KC;
+      *reinterpret_cast<float2*>(sA + row * KCP + k) = make_float2(ra[i].x, ra[i].y);
+      *reinterpret_cast<float2*>(sA + row * KCP + k + 2) = make_float2(ra[i].z, ra[i].w);
+    }
+#pragma unroll
+    for (int i = 0; i < BV; ++i) {
+      const int e = 4 * (tid + 256 * i);
+      const int row = e / KC, k = e % KC;
+      *reinterpret_cast<float2*>(sB + row * KCP + k) = make_float2(rb[i].x, rb[i].y);
+      *reinterpret_cast<float2*>(sB + row * KCP + k + 2) = make_float2(rb[i].z, rb[i].w);
+    }
+  };
+
+  f16v acc[MT][NT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < NT; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const float* pa = sA + (wm * 32 * MT + li) * KCP + h;
+  const float* pb = sB + (wn * 32 * NT + li) * KCP + h;
+  if (c_begin < c_end) load(c_begin);
+  for (int c = c_begin; c < c_end; ++c) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (c + 1 < c_end) load(c + 1);
+#pragma unroll
+    for (int s = 0; s < KC / 2; ++s) {
+      float a[MT], b[NT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = pa[i * 32 * KCP + 2 * s];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) b[j] = pb[j * 32 * KCP + 2 * s];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+  }
+  // D: lane column = ci (li), rows = co (r & 3) + 8 (r >> 2) + 4 h
+  float* pp = part + (int64_t)ks * CO * CI;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * 32 * MT + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int ci = ci0 + wn * 32 * NT + 32 * j + li;
+        if (co < CO && ci < CI) pp[(int64_t)co * CI + ci] = acc[i][j][r];
+      }
+}
+
+// gw[e] = sum_s part[s][e], s in order (e in float4 groups; E % 4 == 0)
+__global__ void __launch_bounds__(256)
+    c1_wreduce_kernel(const float* __restrict__ part, float* __restrict__ gw, int64_t E, int ks) {
+  const int64_t e4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (4 * e4 >= E) return;
+  float4 a = reinterpret_cast<const float4*>(part)[e4];
+  for (int s = 1; s < ks; ++s) {
+    const float4 b = reinterpret_cast<const float4*>(part + (int64_t)s * E)[e4];
+    a.x += b.x;
+    a.y += b.y;
+    a.z += b.z;
+    a.w += b.w;
+  }
+  reinterpret_cast<float4*>(gw)[e4] = a;
+}
+
+// ------------------------------------------------------------------- plans
+inline bool c1_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, int stride) {
+  if (n <= 0 || h <= 0 || w <= 0 || (stride != 1 && stride != 2)) return false;
+  if (ci % 32 || co % 32 || ci < 32 || co < 32) return false;
+  const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  if ((ho * wo) % 4) return false;
+  if (stride == 2 && w % 2) return false;  // gx rows written as (value, 0) pairs
+  return n * ci * h * w < (int64_t)1 << 31 && n * co * ho * wo < (int64_t)1 << 31;
+}
+
+// M-tile of the channel mix: 128 when M % 128 == 0, else 64, else 32.
+inline int cm_bm(int64_t m) { return m % 128 == 0 ? 128 : (m % 64 == 0 ? 64 : 32); }
+
+template <int SIN, int SOUT, bool TRANSA>
+int launch_cm(const float* in, const float* wt, float* out, int64_t n, int64_t K, int64_t M,
+              int64_t hin, int64_t win, int64_t ho, int64_t wo, int64_t hout, int64_t wout,
+              int kid, double bytes, double flops, hipStream_t s) {
+  const int64_t Q = ho * wo;
+  const int bm = cm_bm(M);
+  constexpr int BQ = 128;
+  const int64_t qtiles = mde::cdiv(Q, BQ), mtiles = M / bm;
+  const int64_t total = n * qtiles * mtiles;
+  if (total > 0x7fffffff) return MDE_ERR_INVALID_ARG;
+  const dim3 grid(xcd_grid(total)), block(256);
+#define MDE_CM(BMv, MTv, QTv)                                                                     \
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (cm_kernel<BMv, BQ, MTv, QTv, SIN, SOUT, TRANSA>), grid, \
+                  block, 0, in, wt, out, (int)K, (int)M, (int)hin, (int)win, (int)wo, (int)Q,     \
+                  (int)hout, (int)wout, (int)qtiles, (int)mtiles, (int)total)
+  if (bm == 128)
+    MDE_CM(128, 2, 2);
+  else if (bm == 64)
+    MDE_CM(64, 2, 1);
+  else
+    MDE_CM(32, 1, 1);
+#undef MDE_CM
+  return MDE_OK;
+}
+
+struct WgPlan {
+  int bco, bci, cotiles, citiles, ksplit, nchunks;
+  int64_t npix;
+};
+
+inline WgPlan wg_plan(int64_t n, int64_t ci, int64_t co, int64_t ho, int64_t wo) {
+  // block tiles with four 32-multiple wave tiles: 128x128, 128x64, 64x128,
+  // 64x64, and 128x32 / 32x128 (the 32-channel side; the other side padded
+  // to 128 rows and masked when it is 64)
+  WgPlan p;
+  const int a = co % 128 == 0 ? 128 : (co % 64 == 0 ? 64 : 32);
+  const int b = ci % 128 == 0 ? 128 : (ci % 64 == 0 ? 64 : 32);
+  if (b == 32) {
+    p.bco = 128;
+    p.bci = 32;
+  } else if (a == 32) {
+    p.bco = 32;
+    p.bci = 128;
+  } else {
+    p.bco = a;
+    p.bci = b;
+  }
+  p.cotiles = (int)mde::cdiv(co, p.bco);
+  p.citiles = (int)mde::cdiv(ci, p.bci);
+  p.npix = n * ho * wo;
+  p.nchunks = (int)mde::cdiv(p.npix, KC);
+  const int tiles = p.cotiles * p.citiles;
+  // ~512 blocks (two per CU), at least 4 chunks per block, slab <= 64 MB
+  int ks = (int)mde::cdiv(512, tiles);
+  if (ks > p.nchunks / 4) ks = p.nchunks / 4;
+  const int64_t cap = ((int64_t)16 << 20) / (ci * co);
+  if (ks > cap) ks = (int)cap;
+  p.ksplit = ks < 1 ? 1 : ks;
+  return p;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_conv1x1_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int stride,
+                          int dtype) {
+  return dtype == MDE_F32 && c1_shape_ok(1, cin, cout, h, w, stride) ? 1 : 0;
+}
+
+int mde_conv1x1_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                    int64_t cout, int64_t h, int64_t w, int stride, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !weight || !y) return MDE_ERR_INVALID_ARG;
+  if (!c1_shape_ok(n, cin, cout, h, w, stride)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  const double flops = 2.0 * n * ho * wo * (double)cin * cout;
+  const double bytes = 4.0 * n * (double)ho * wo * (cin + cout);
+  if (stride == 1)
+    return launch_cm<1, 1, false>((const float*)x, weight, (float*)y, n, cin, cout, h, w, ho, wo,
+                                  ho, wo, mde::K_C1_FWD, bytes, flops, s);
+  return launch_cm<2, 1, false>((const float*)x, weight, (float*)y, n, cin, cout, h, w, ho, wo,
+                                ho, wo, mde::K_C1_FWD, bytes, flops, s);
+}
+
+int mde_conv1x1_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, int stride, int dtype,
+                         void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !weight || !gx) return MDE_ERR_INVALID_ARG;
+  if (!c1_shape_ok(n, cin, cout, h, w, stride)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  const double flops = 2.0 * n * ho * wo * (double)cin * cout;
+  const double bytes = 4.0 * n * ((double)ho * wo * cout + (double)h * w * cin);
+  // GEMM K = cout (gy's channels), M = cin; gy is a ho x wo plane
+  if (stride == 1)
+    return launch_cm<1, 1, true>((const float*)gy, weight, (float*)gx, n, cout, cin, ho, wo, ho,
+                                 wo, h, w, mde::K_C1_DGRAD, bytes, flops, s);
+  return launch_cm<1, 2, true>((const float*)gy, weight, (float*)gx, n, cout, cin, ho, wo, ho, wo,
+                               h, w, mde::K_C1_DGRAD, bytes, flops, s);
+}
+
+size_t mde_conv1x1_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                   int stride, int dtype) {
+  if (dtype != MDE_F32 || !c1_shape_ok(n, cin, cout, h, w, stride)) return 0;
+  const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  const WgPlan p = wg_plan(n, cin, cout, ho, wo);
+  return sizeof(float) * (size_t)p.ksplit * (size_t)(cin * cout);
+}
+
+int mde_conv1x1_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                      int64_t cout, int64_t h, int64_t w, int stride, void* workspace, int dtype,
+                      void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !x || !gweight || !workspace) return MDE_ERR_INVALID_ARG;
+  if (!c1_shape_ok(n, cin, cout, h, w, stride)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  const WgPlan p = wg_plan(n, cin, cout, ho, wo);
+  const int64_t total = (int64_t)p.cotiles * p.citiles * p.ksplit;
+  const dim3 grid(xcd_grid(total)), block(256);
+  const double flops = 2.0 * n * ho * wo * (double)cin * cout;
+  const double bytes = 4.0 * n * (double)ho * wo * (cin + cout);
+  float* part = (float*)workspace;
+  const int Q = (int)(ho * wo);
+#define MDE_WG(BCO, BCI, MTv, NTv, SINv)                                                          \
+  MDE_LAUNCH_MFMA(mde::K_C1_WGRAD, bytes, flops, s, (c1_wgrad_kernel<BCO, BCI, MTv, NTv, SINv>), \
+                  grid, block, 0, (const float*)gy, (const float*)x, part, (int)cout, (int)cin, Q, \
+                  (int)h, (int)w, (int)wo, p.npix, p.nchunks, p.ksplit, p.cotiles, p.citiles,     \
+                  (int)total)
+#define MDE_WG_S(SINv)                       \
+  do {                                       \
+    if (p.bco == 128 && p.bci == 128)        \
+      MDE_WG(128, 128, 2, 2, SINv);          \
+    else if (p.bco == 128 && p.bci == 64)    \
+      MDE_WG(128, 64, 2, 1, SINv);           \
+    else if (p.bco == 64 && p.bci == 128)    \
+      MDE_WG(64, 128, 1, 2, SINv);           \
+    else if (p.bco == 64 && p.bci == 64)     \
+      MDE_WG(64, 64, 1, 1, SINv);            \
+    else if (p.bci == 32)                    \
+      MDE_WG(128, 32, 1, 1, SINv);           \
+    else                                     \
+      MDE_WG(32, 128, 1, 1, SINv);           \
+  } while (0)
+  if (stride == 1)
+    MDE_WG_S(1);
+  else
+    MDE_WG_S(2);
+#undef MDE_WG_S
+#undef MDE_WG
+  const int64_t E = cin * cout;
+  MDE_LAUNCH(mde::K_C1_WREDUCE, 4.0 * E * (p.ksplit + 1), s, c1_wreduce_kernel,
+             dim3((unsigned)mde::cdiv(E / 4, 256)), dim3(256), 0, part, gweight, E, p.ksplit);
+  return MDE_OK;
+}
+
+}  // extern "C"

@@ -541,14 +541,27 @@ class _Conv3x3Bf16(torch.autograd.Function):
 
 
 class _Conv3x3S2(torch.autograd.Function):
-    """Bias-free k3 / s2 / p1 convolution (the DDRNet stem, DDRNet_23_slim.py:
-    conv1): forward and data gradient on MIOpen, the weight gradient on the HIP
-    stride-2 kernel (mde_conv3x3s2_wgrad: NCHW, no NHWC transposes)."""
+    """Bias-free k3 / s2 / p1 convolution (DDRNet's stem convs, the stride-2
+    BasicBlock convs, down3 / down4, layer5's Bottleneck conv2:
+    DDRNet_23_slim.py:41-72,80,232-233,254-265): the weight gradient on the HIP
+    stride-2 kernel (mde_conv3x3s2_wgrad), the forward and data gradient on
+    the HIP MFMA kernels of conv3x3s2.hip where a shape has one (>= 32
+    channels; MDE_S2_FWD=0: MIOpen), else MIOpen -- all NCHW, no NHWC
+    transposes on the HIP passes."""
 
     @staticmethod
     def forward(ctx, x, weight):
         x = x.contiguous()
+        weight = weight.contiguous()
         ctx.save_for_backward(x, weight)
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        if S2_FWD and _abi.query("mde_conv3x3s2_fwd_supported", cin, cout, h, w, _abi.MDE_F32):
+            y = torch.empty((n, cout, (h - 1) // 2 + 1, (w - 1) // 2 + 1), dtype=x.dtype,
+                            device=x.device)
+            _abi.call("mde_conv3x3s2_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin, cout,
+                      h, w, _abi.dtype_code(x), _abi.stream_of(x))
+            return y
         return torch.nn.functional.conv2d(x, weight, None, 2, 1)
 
     @staticmethod
@@ -559,35 +572,111 @@ class _Conv3x3S2(torch.autograd.Function):
         cout = weight.shape[0]
         gx = gw = None
         if ctx.needs_input_grad[0]:
-            gx = torch.ops.aten.convolution_backward(
-                gy, x, weight, None, (2, 2), (1, 1), (1, 1), False, (0, 0), 1,
-                (True, False, False))[0]
+            if S2_FWD and _abi.query("mde_conv3x3s2_dgrad_supported", cin, cout, h, w,
+                                     _abi.MDE_F32):
+                gx = torch.empty_like(x)
+                _abi.call("mde_conv3x3s2_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx), n,
+                          cin, cout, h, w, _abi.dtype_code(gy), _abi.stream_of(gy))
+            else:
+                gx = torch.ops.aten.convolution_backward(
+                    gy, x, weight, None, (2, 2), (1, 1), (1, 1), False, (0, 0), 1,
+                    (True, False, False))[0]
         if ctx.needs_input_grad[1]:
-            gw = torch.empty_like(weight)
-            ws = _ws(_abi.query("mde_conv3x3s2_wgrad_workspace", n, cin, cout, h, w,
-                                _abi.MDE_F32), x)
-            _abi.call("mde_conv3x3s2_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
-                      cout, h, w, _abi.ptr(ws), _abi.MDE_F32, _abi.stream_of(gy))
+            nws = _abi.query("mde_conv3x3s2_wgrad_workspace", n, cin, cout, h, w, _abi.MDE_F32) \
+                if (S2_WGRAD and (S2_WIDE or cout == 32)
+                    and _abi.query("mde_conv3x3s2_supported", cin, cout, _abi.MDE_F32)) else 0
+            if nws > 0:
+                gw = torch.empty_like(weight)
+                _abi.call("mde_conv3x3s2_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin,
+                          cout, h, w, _abi.ptr(_ws(nws, x)), _abi.MDE_F32, _abi.stream_of(gy))
+            else:
+                gw = torch.ops.aten.convolution_backward(
+                    gy, x, weight, None, (2, 2), (1, 1), (1, 1), False, (0, 0), 1,
+                    (False, True, False))[1]
         return gx, gw
 
 
+class _Conv1x1(torch.autograd.Function):
+    """Bias-free wide 1x1 convolution, stride 1 or 2 (DDRNet's Bottleneck /
+    downsample / compression / DAPPM convs, DDRNet_23_slim.py:79,84,121-171,
+    245,250,294-296): forward, data gradient and weight gradient on the NCHW
+    MFMA kernels of conv1x1.hip (no NHWC transposes)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, stride):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
+        y = torch.empty((n, cout, ho, wo), dtype=x.dtype, device=x.device)
+        _abi.call("mde_conv1x1_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin, cout, h, w,
+                  stride, _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        st = _abi.stream_of(gy)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            _abi.call("mde_conv1x1_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx), n, cin,
+                      cout, h, w, ctx.stride, _abi.dtype_code(gy), st)
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(weight)
+            ws = _ws(_abi.query("mde_conv1x1_wgrad_workspace", n, cin, cout, h, w, ctx.stride,
+                                _abi.MDE_F32), x)
+            _abi.call("mde_conv1x1_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h,
+                      w, ctx.stride, _abi.ptr(ws), _abi.dtype_code(gy), st)
+        return gx, gw, None
+
+
+C1_WIDE = os.environ.get("MDE_C1_WIDE", "1") != "0"  # MDE_C1_WIDE=0: MIOpen (A/B switch)
+
+
+def conv1x1_ok(conv: nn.Conv2d, x) -> bool:
+    """Whether this bias-free 1x1 conv (stride 1 or 2) runs on the wide HIP 1x1
+    kernels: fp32 outside autocast, channel counts multiples of 32 (the
+    small-channel decoder 1x1s keep the fused pointwise kernels)."""
+    if not (C1_WIDE and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
+            and conv.weight.dtype == torch.float32 and x.dim() == 4
+            and conv.kernel_size == (1, 1) and conv.padding == (0, 0)
+            and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.stride in ((1, 1), (2, 2)) and conv.padding_mode == "zeros"):
+        return False
+    return bool(_abi.query("mde_conv1x1_supported", conv.in_channels, conv.out_channels,
+                           x.shape[2], x.shape[3], conv.stride[0], _abi.MDE_F32))
+
+
 def conv3x3s2_ok(conv: nn.Conv2d, x) -> bool:
-    """Whether this k3 / s2 / p1 conv takes the HIP stride-2 weight gradient
-    (the stem's 3 -> 32 / 32 -> 32, and 32+ -> 64+ channels at output widths
-    that are multiples of 40 or 20; fp32 outside autocast, even input width;
-    MDE_S2_WGRAD=0: MIOpen)."""
-    return (S2_WGRAD and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
-            and conv.weight.dtype == torch.float32 and x.dim() == 4 and x.shape[-1] % 2 == 0 and conv.kernel_size == (3, 3)
-            and conv.stride == (2, 2) and conv.padding == (1, 1) and conv.dilation == (1, 1)
-            and conv.groups == 1 and conv.padding_mode == "zeros"
-            and bool(_abi.query("mde_conv3x3s2_supported", conv.in_channels, conv.out_channels,
-                                _abi.MDE_F32))
-            and (S2_WIDE or conv.out_channels == 32)
-            and _abi.query("mde_conv3x3s2_wgrad_workspace", x.shape[0], conv.in_channels,
-                           conv.out_channels, x.shape[2], x.shape[3], _abi.MDE_F32) > 0)
+    """Whether this k3 / s2 / p1 conv takes _Conv3x3S2: fp32 outside autocast,
+    even input width, and a HIP kernel for at least one pass -- the stride-2
+    weight gradient (the stem's 3 -> 32 / 32 -> 32, 32+ -> 64+ channels at
+    output widths that are multiples of 40 or 20; MDE_S2_WGRAD=0: MIOpen) or
+    the forward / data gradient (>= 32 channels, conv3x3s2.hip; MDE_S2_FWD=0:
+    MIOpen).  The passes without one run on MIOpen inside the Function."""
+    if not (x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
+            and conv.weight.dtype == torch.float32 and x.dim() == 4 and x.shape[-1] % 2 == 0
+            and conv.kernel_size == (3, 3) and conv.stride == (2, 2) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1 and conv.padding_mode == "zeros"):
+        return False
+    cin, cout, h, w = conv.in_channels, conv.out_channels, x.shape[2], x.shape[3]
+    wgrad = (S2_WGRAD and bool(_abi.query("mde_conv3x3s2_supported", cin, cout, _abi.MDE_F32))
+             and (S2_WIDE or cout == 32)
+             and _abi.query("mde_conv3x3s2_wgrad_workspace", x.shape[0], cin, cout, h, w,
+                            _abi.MDE_F32) > 0)
+    fwd = S2_FWD and bool(_abi.query("mde_conv3x3s2_fwd_supported", cin, cout, h, w, _abi.MDE_F32))
+    return wgrad or fwd
 
 
 S2_WGRAD = os.environ.get("MDE_S2_WGRAD", "1") != "0"
+S2_FWD = os.environ.get("MDE_S2_FWD", "1") != "0"  # HIP stride-2 forward / data gradient (A/B switch)
 S2_WIDE = os.environ.get("MDE_S2_WIDE", "1") != "0"  # the 64+-channel ones (A/B switch)
 
 
@@ -655,6 +744,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
         y = conv3x3(x, conv.weight, passes)
     elif conv3x3s2_ok(conv, x):
         y = _Conv3x3S2.apply(x, conv.weight)
+    elif conv1x1_ok(conv, x):
+        y = _Conv1x1.apply(x, conv.weight, conv.stride[0])
     else:
         y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                        conv.dilation, conv.groups)
@@ -662,14 +753,31 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
 
 
 def conv_nobias(conv: nn.Conv2d, x):
-    """conv(x) without its bias (folded into the following BN, or absent): HIP 3x3 / MIOpen."""
+    """conv(x) without its bias (folded into the following BN, or absent): the
+    HIP 3x3 / stride-2 / 1x1 kernels where they apply, else MIOpen."""
     passes = conv3x3_passes(conv, x) if x.is_cuda else None
     if passes is not None:
         return conv3x3(x, conv.weight, passes)
     if conv3x3s2_ok(conv, x):
         return _Conv3x3S2.apply(x, conv.weight)
+    if pointwise_ok(conv, x) and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x):
+        return _Pointwise.apply(x, conv.weight)
+    if conv1x1_ok(conv, x):
+        return _Conv1x1.apply(x, conv.weight, conv.stride[0])
     return torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                       conv.dilation, conv.groups)
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d (same parameters and state_dict keys) whose bias-free
+    forward takes conv_nobias's HIP kernels where they apply; with a bias it
+    is the stock module (those convs are folded into a BatchNorm by
+    run_sequential / conv_bn instead)."""
+
+    def forward(self, x):
+        if self.bias is None and x.is_cuda:
+            return conv_nobias(self, x)
+        return super().forward(x)
 
 
 def _bnrelu_pw_at(mods, i, x_shape) -> bool:

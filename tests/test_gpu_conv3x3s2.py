@@ -1,0 +1,87 @@
+"""GPU parity of the stride-2 3x3 convolutions (conv3x3s2.hip forward / data
+gradient, the stride-2 weight gradient of conv3x3.hip) through _Conv3x3S2.
+
+Reference layers: DDRNet-23-slim's stride-2 convs (src/GuideDepth/model/
+DDRNet_23_slim.py:41-72 via _make_layer :291-309, :80, :232-233, :254-265);
+oracle = ATen conv2d (the reference's own dependency) in float64 on the CPU.
+Tolerances (per assertion): 1e-5 of the max magnitude for the forward and
+data gradient (fp32 sums of <= 2304 products), 2e-5 for the weight gradient.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+# (cin, cout, h, w) input sizes: DDRNet's stride-2 convs at cfg2 sizes (bs 2),
+# plus odd heights, ragged pixel tiles and a non-DDRNet width
+SHAPES = [(32, 32, 240, 320), (32, 64, 120, 160), (64, 128, 60, 80), (128, 256, 30, 40),
+          (256, 256, 15, 20), (64, 64, 7, 10), (32, 96, 9, 6), (64, 128, 59, 80)]
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    import monocular_depth_estimation_amd  # noqa: F401
+
+
+def rel_err(a, b):
+    a = a.detach().double().cpu()
+    b = b.detach().double().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("cin,cout,h,w", SHAPES)
+def test_conv3x3s2_vs_float64_oracle(cin, cout, h, w):
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import Conv2d, conv3x3s2_ok
+    n = 2
+    g = torch.Generator().manual_seed(cin + 3 * cout + h)
+    x = torch.rand((n, cin, h, w), generator=g) - 0.5
+    wt = (torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.1
+    ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+    gy = torch.rand((n, cout, ho, wo), generator=g) - 0.5
+    xr = x.double().requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 2, 1)
+    yr.backward(gy.double())
+    conv = Conv2d(cin, cout, 3, stride=2, padding=1, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(wt)
+    xg = x.to(DEV).requires_grad_(True)
+    assert conv3x3s2_ok(conv, xg)
+    assert _abi.query("mde_conv3x3s2_fwd_supported", cin, cout, h, w, 0) == 1
+    assert _abi.query("mde_conv3x3s2_dgrad_supported", cin, cout, h, w, 0) == 1
+    y = conv(xg)
+    y.backward(gy.to(DEV))
+    assert y.shape == yr.shape
+    assert rel_err(y, yr) <= 1e-5, "forward"
+    assert rel_err(xg.grad, xr.grad) <= 1e-5, "data gradient"
+    assert rel_err(conv.weight.grad, wr.grad) <= 2e-5, "weight gradient"
+
+
+def test_conv3x3s2_full_batch_vs_miopen_deterministic():
+    """cfg2 batch (32) of the 64 -> 128 layer3 / down3 conv: HIP vs MIOpen fp32,
+    and two runs bitwise equal."""
+    from monocular_depth_estimation_amd.nn import _Conv3x3S2
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.rand((32, 64, 60, 80), device=DEV, generator=gen) - 0.5
+    wt = (torch.rand((128, 64, 3, 3), device=DEV, generator=gen) - 0.5) * 0.1
+    gy = torch.rand((32, 128, 30, 40), device=DEV, generator=gen) - 0.5
+    outs = []
+    for _ in range(2):
+        xh = x.clone().requires_grad_(True)
+        wh = wt.clone().requires_grad_(True)
+        y = _Conv3x3S2.apply(xh, wh)
+        y.backward(gy)
+        outs.append((y.detach(), xh.grad, wh.grad))
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    xm = x.clone().requires_grad_(True)
+    wm = wt.clone().requires_grad_(True)
+    ym = torch.nn.functional.conv2d(xm, wm, None, 2, 1)
+    ym.backward(gy)
+    assert rel_err(outs[0][0], ym) <= 2e-5
+    assert rel_err(outs[0][1], xm.grad) <= 2e-5
+    assert rel_err(outs[0][2], wm.grad) <= 5e-5

@@ -1,0 +1,109 @@
+"""DDRNet's wide 1x1 convolutions at cfg2 (bs 32): the NCHW HIP kernels
+(mde_conv1x1_fwd / _bwd_data / _wgrad incl. its reduction) vs MIOpen
+(F.conv2d / aten.convolution_backward on NCHW tensors, incl. its layout
+transposes).  Times from HIP-graph replays (kbench.timeit)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+
+from monocular_depth_estimation_amd import _abi
+from monocular_depth_estimation_amd.nn import _ws
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import kbench  # noqa: E402
+
+# (cin, cout, stride, h, w, uses per cfg2 step)
+SHAPES = [(32, 64, 2, 120, 160, 1), (64, 128, 2, 60, 80, 1), (128, 256, 2, 30, 40, 1),
+          (256, 512, 2, 15, 20, 1), (64, 128, 1, 60, 80, 2), (128, 64, 1, 30, 40, 1),
+          (256, 64, 1, 15, 20, 1), (256, 256, 1, 15, 20, 1), (256, 512, 1, 8, 10, 1),
+          (512, 128, 1, 8, 10, 2), (640, 128, 1, 8, 10, 1)]
+
+# (cin, cout, h, w, uses per cfg2 step) of the stride-2 3x3 convs (input sizes)
+S2_SHAPES = [(32, 32, 240, 320, 1), (32, 64, 120, 160, 1), (64, 128, 60, 80, 3),
+             (128, 256, 30, 40, 2), (256, 256, 15, 20, 1)]
+
+
+def main():
+    kbench._STREAM = torch.cuda.Stream()
+    with torch.cuda.stream(kbench._STREAM):
+        run()
+
+
+def run():
+    n = 32
+    tot = {"hip": 0.0, "miopen": 0.0}
+    for ci, co, s, h, w, uses in SHAPES:
+        ho, wo = (h - 1) // s + 1, (w - 1) // s + 1
+        x = torch.rand((n, ci, h, w), device="cuda") - 0.5
+        wt = (torch.rand((co, ci, 1, 1), device="cuda") - 0.5) * 0.1
+        gy = torch.rand((n, co, ho, wo), device="cuda") - 0.5
+        y = torch.empty_like(gy)
+        gx = torch.empty_like(x)
+        gw = torch.empty_like(wt)
+        ws = _ws(_abi.query("mde_conv1x1_wgrad_workspace", n, ci, co, h, w, s, 0), x)
+        st = _abi.stream_of(x)
+        fwd = lambda: _abi.call("mde_conv1x1_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, ci, co,
+                                h, w, s, 0, st)
+        dgr = lambda: _abi.call("mde_conv1x1_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n,
+                                ci, co, h, w, s, 0, st)
+        wgr = lambda: _abi.call("mde_conv1x1_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, ci,
+                                co, h, w, s, _abi.ptr(ws), 0, st)
+        mf = lambda: torch.nn.functional.conv2d(x, wt, None, s)
+        mb = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (s, s), (0, 0), (1, 1),
+                                                         False, (0, 0), 1, (True, True, False))
+        t = {k: kbench.timeit(f, 20) * 1e3 for k, f in
+             (("fwd", fwd), ("dgrad", dgr), ("wgrad", wgr), ("mio_fwd", mf), ("mio_bwd", mb))}
+        fl = 2.0 * n * ho * wo * ci * co
+        mgx, mgw = mb()[:2]
+        fwd()
+        dgr()
+        wgr()
+        ym = mf()
+        err = max(float((a - b).abs().max() / b.abs().max()) for a, b in
+                  ((y, ym), (gx, mgx), (gw, mgw)))
+        hip = t["fwd"] + t["dgrad"] + t["wgrad"]
+        mio = t["mio_fwd"] + t["mio_bwd"]
+        tot["hip"] += uses * hip
+        tot["miopen"] += uses * mio
+        print(f"1x1 {ci}->{co} s{s} {h}x{w}: HIP fwd {t['fwd']:6.1f} dgrad {t['dgrad']:6.1f} "
+              f"wgrad {t['wgrad']:6.1f} us ({fl / t['fwd'] / 1e6:5.1f} / {fl / t['dgrad'] / 1e6:5.1f} / "
+              f"{fl / t['wgrad'] / 1e6:5.1f} TF/s) | MIOpen fwd {t['mio_fwd']:6.1f} bwd {t['mio_bwd']:6.1f} us"
+              f" | rel diff {err:.1e}", flush=True)
+    print(f"1x1 per cfg2 step (x uses): HIP {tot['hip']:.0f} us, MIOpen {tot['miopen']:.0f} us",
+          flush=True)
+    # stride-2 3x3 (forward + data gradient; the weight gradient was already on HIP)
+    tot = {"hip": 0.0, "miopen": 0.0}
+    for ci, co, h, w, uses in S2_SHAPES:
+        ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        x = torch.rand((n, ci, h, w), device="cuda") - 0.5
+        wt = (torch.rand((co, ci, 3, 3), device="cuda") - 0.5) * 0.1
+        gy = torch.rand((n, co, ho, wo), device="cuda") - 0.5
+        y = torch.empty_like(gy)
+        gx = torch.empty_like(x)
+        st = _abi.stream_of(x)
+        fwd = lambda: _abi.call("mde_conv3x3s2_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, ci, co,
+                                h, w, 0, st)
+        dgr = lambda: _abi.call("mde_conv3x3s2_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n,
+                                ci, co, h, w, 0, st)
+        mf = lambda: torch.nn.functional.conv2d(x, wt, None, 2, 1)
+        md = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (2, 2), (1, 1), (1, 1),
+                                                         False, (0, 0), 1, (True, False, False))
+        t = {k: kbench.timeit(f, 20) * 1e3 for k, f in
+             (("fwd", fwd), ("dgrad", dgr), ("mio_fwd", mf), ("mio_dgrad", md))}
+        fl = 2.0 * 9 * n * ho * wo * ci * co
+        fwd()
+        dgr()
+        err = max(float((a - b).abs().max() / b.abs().max()) for a, b in ((y, mf()), (gx, md()[0])))
+        tot["hip"] += uses * (t["fwd"] + t["dgrad"])
+        tot["miopen"] += uses * (t["mio_fwd"] + t["mio_dgrad"])
+        print(f"3x3s2 {ci}->{co} {h}x{w}: HIP fwd {t['fwd']:6.1f} dgrad {t['dgrad']:6.1f} us "
+              f"({fl / t['fwd'] / 1e6:5.1f} / {fl / t['dgrad'] / 1e6:5.1f} TF/s) | MIOpen fwd "
+              f"{t['mio_fwd']:6.1f} dgrad {t['mio_dgrad']:6.1f} us | rel diff {err:.1e}", flush=True)
+    print(f"3x3s2 per cfg2 step (x uses): HIP {tot['hip']:.0f} us, MIOpen {tot['miopen']:.0f} us",
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()

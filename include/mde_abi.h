@@ -618,6 +618,19 @@ int mde_conv3x3s2_fwd(const void* x, const float* weight, void* y, int64_t n, in
 int mde_conv3x3s2_bwd_data(const void* gy, const float* weight, void* gx, int64_t n, int64_t cin,
                            int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
 
+/* Stride-1 counterparts for the 64 / 128 / 256-channel 3x3 convs of the
+ * BasicBlocks (DDRNet_23_slim.py:41-72), which MIOpen runs as Winograd:
+ * pass 0 = forward, 1 = data gradient (the weight gradient is
+ * mde_conv3x3_wgrad).  cin, cout multiples of 32; the query says whether the
+ * (channels, h, w) geometry has a kernel. */
+int mde_conv3x3_wide_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int pass,
+                               int dtype);
+int mde_conv3x3_wide_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, int dtype, void* stream);
+int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int64_t n,
+                              int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                              void* stream);
+
 /* ---------------------------------------------------------------------------
  * Captured-graph repair (no reference counterpart: the reference runs its step
  * eagerly, src/train.py:83-114; the build replays it from a hipGraph).

@@ -141,6 +141,9 @@ SIGNATURES = {
     "mde_conv3x3s2_dgrad_supported": (_int, [_i64, _i64, _i64, _i64, _int]),
     "mde_conv3x3s2_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_conv3x3s2_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_conv3x3_wide_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int]),
+    "mde_conv3x3_wide_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_conv3x3_wide_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_node_counts": (_int, [_vp, _c.POINTER(_i64)]),

@@ -74,6 +74,8 @@ enum Kid : int {
   K_C1_WREDUCE,
   K_C3S2_FWD,       // DDRNet's wide stride-2 3x3 convolutions (conv3x3s2.hip)
   K_C3S2_DGRAD,
+  K_C3W_FWD,        // the wide stride-1 3x3 convolutions (conv3x3s2.hip, c3s1_kernel)
+  K_C3W_DGRAD,
   K_COUNT
 };
 

@@ -213,6 +213,144 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ------------------------------------------------- stride 1 (wide channels)
+// The same band GEMM at stride 1, for DDRNet's 64 / 128 / 256-channel 3x3
+// BasicBlock convs (DDRNet_23_slim.py:41-72) that MIOpen runs as Winograd:
+// out[n][m][q] = sum_{c,t} A[m][(t, c)] in[n][c][r+ky-1][col+kx-1].  FLIP = the
+// data gradient (in = gy, out = gx, A[m = ci][(t, c = co)] = w[co][ci][8 - t]).
+// K is tap-major within a chunk (k = 4 t + c): the two k-lanes of an MFMA
+// step read channels c, c + 1 of one tap, one plane pitch apart, and the
+// plane pitch is 32 (mod 64) words, so the lane halves hit disjoint banks
+// while each half reads 32 consecutive pixels.
+template <bool FLIP, int BM, int BQ, int MT, int QT, int R, int NJ>
+__global__ void __launch_bounds__(256)
+    c3s1_kernel(const float* __restrict__ in, const float* __restrict__ wt,
+                float* __restrict__ out, int k_n, int m_n, int h, int w, int xw, int ps,
+                int qtiles, int mtiles, int total) {
+  constexpr int WQ = BQ / (32 * QT), WM = BM / (32 * MT);
+  static_assert(WQ * WM == 4, "four waves per block");
+  constexpr int AV = (BM * KCH / 4 + 255) / 256;  // float4 of weights per thread and chunk
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* sX = smem;             // [CIC][ps]
+  float* sA = smem + CIC * ps;  // [BM][AP]
+
+  const int lb = xcd_logical(total);
+  if (lb < 0) return;
+  const int mt = lb % mtiles, rest = lb / mtiles;
+  const int qt = rest % qtiles, img = rest / qtiles;
+  const int m0 = mt * BM, q0 = qt * BQ;
+  const int Q = h * w;
+  const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, hh = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv / WQ, wq = wv % WQ;
+  const int r_first = q0 / w;
+  const int64_t hw = (int64_t)h * w;
+  const float* ib = in + (int64_t)img * k_n * hw;
+
+  int bbase[QT];
+#pragma unroll
+  for (int y2 = 0; y2 < QT; ++y2) {
+    int q = q0 + wq * 32 * QT + 32 * y2 + li;
+    q = q < Q ? q : Q - 1;
+    const int rq = q / w, cq = q - rq * w;
+    bbase[y2] = (rq - r_first) * xw + cq + hh * ps;
+  }
+  int koff[KCH / 2];  // k = 2 s + hh: tap s / 2, channel 2 (s & 1) + hh (hh folded into bbase)
+#pragma unroll
+  for (int s2 = 0; s2 < KCH / 2; ++s2) {
+    const int t = s2 >> 1;
+    koff[s2] = 2 * (s2 & 1) * ps + (t / 3) * xw + t % 3;
+  }
+
+  Band<R, NJ> band;
+  float4 ra[AV];
+  auto load = [&](int k0) {
+    band.load(ib + (int64_t)(k0 + wv) * hw, h, w, r_first - 1, -1, xw, lane);
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = tid + 256 * i;
+      const bool ok = e < BM * 9;
+      const int ee = ok ? e : 0;
+      const float* src;
+      if constexpr (FLIP) {  // [c][m][9] = w[k0 + c][m0 + m][t'], BM * 9 contiguous per c
+        const int c = ee / (BM * 9 / 4), f = ee - c * (BM * 9 / 4);
+        src = wt + ((int64_t)(k0 + c) * m_n + m0) * 9 + 4 * f;
+      } else {  // [m][c][9] = w[m0 + m][k0 + c][t], 36 contiguous per m
+        const int m = ee / 9, f = ee - m * 9;
+        src = wt + ((int64_t)(m0 + m) * k_n + k0) * 9 + 4 * f;
+      }
+      ra[i] = *reinterpret_cast<const float4*>(src);
+    }
+  };
+  auto store = [&]() {
+    band.store(sX + wv * ps, xw, lane);
+#pragma unroll
+    for (int i = 0; i < AV; ++i) {
+      const int e = tid + 256 * i;
+      if (e < BM * 9) {
+        const float v[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int m, c, t;
+          if constexpr (FLIP) {
+            const int c0 = e / (BM * 9 / 4), idx = 4 * (e - c0 * (BM * 9 / 4)) + j;
+            c = c0;
+            m = idx / 9;
+            t = 8 - (idx - m * 9);
+          } else {
+            const int m0l = e / 9, idx = 4 * (e - m0l * 9) + j;
+            m = m0l;
+            c = idx / 9;
+            t = idx - c * 9;
+          }
+          sA[m * AP + 4 * t + c] = v[j];
+        }
+      }
+    }
+  };
+
+  f16v acc[MT][QT];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int b = 0; b < QT; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[a][b][r] = 0.f;
+  const float* pa = sA + (wm * 32 * MT + li) * AP + hh;
+  load(0);
+  for (int k0 = 0; k0 < k_n; k0 += CIC) {
+    __syncthreads();
+    store();
+    __syncthreads();
+    if (k0 + CIC < k_n) load(k0 + CIC);
+#pragma unroll
+    for (int s2 = 0; s2 < KCH / 2; ++s2) {
+      float a[MT], b[QT];
+#pragma unroll
+      for (int i = 0; i < MT; ++i) a[i] = pa[i * 32 * AP + 2 * s2];
+#pragma unroll
+      for (int j = 0; j < QT; ++j) b[j] = sX[bbase[j] + koff[s2]];
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < QT; ++j) acc[i][j] = mfma32(a[i], b[j], acc[i][j]);
+    }
+  }
+  float* ob = out + (int64_t)img * m_n * Q;
+#pragma unroll
+  for (int j = 0; j < QT; ++j) {
+    const int q = q0 + wq * 32 * QT + 32 * j + li;
+    if (q >= Q) continue;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * 32 * MT + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        ob[(int64_t)m * Q + q] = acc[i][j][r];
+      }
+  }
+}
+
 // ------------------------------------------------------------ data gradient
 // Class taps: (a, b) -> list of (ky, kx, dy, dx); dy / dx = gy row / column
 // offset (tap 0 of a class-1 axis reads gy at m + 1).
@@ -371,6 +509,24 @@ inline bool dgrad_geo(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi,
   return g->total < 0x7fffffff;
 }
 
+// stride 1: BM output channels (of this pass) x BQ pixels; plane pitch = 32 (mod 64)
+inline bool s1_geo(int64_t n, int64_t m_ch, int64_t h, int64_t w, S2Geo* g) {
+  const int64_t Q = h * w;
+  g->bm = m_ch % 64 == 0 ? 64 : 32;
+  if (m_ch % g->bm) return false;
+  g->bq = (Q >= 1024 || g->bm == 32) ? 128 : 64;
+  const int rows = rows_span(g->bq, w, h);
+  g->r = rows + 2;
+  g->xw = (int)w + 2;
+  g->nj = (g->xw + 63) / 64;
+  g->ps = 0;
+  g->qtiles = (int)mde::cdiv(Q, g->bq);
+  g->mtiles = (int)(m_ch / g->bm);
+  g->total = n * g->qtiles * g->mtiles;
+  return g->total < 0x7fffffff;
+}
+inline int pitch32(int v) { return (v + 31) / 64 * 64 + 32; }  // >= v, = 32 (mod 64)
+
 inline bool s2_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi) {
   return n > 0 && ci >= 32 && co >= 32 && ci % 32 == 0 && co % 32 == 0 && hi >= 2 && wi >= 2 &&
          wi % 2 == 0 && n * ci * hi * wi < ((int64_t)1 << 31) && n * co * hi * wi < ((int64_t)1 << 31);
@@ -392,9 +548,84 @@ inline bool s2_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t w
   X(64, 64, 6, 1)            \
   X(64, 64, 9, 1)
 
+#define MDE_S1_GEOS(X)     \
+  X(32, 128, 1, 1, 4, 3)   \
+  X(64, 128, 2, 1, 5, 2)   \
+  X(64, 128, 2, 1, 7, 1)   \
+  X(64, 64, 1, 1, 7, 1)    \
+  X(64, 64, 1, 1, 10, 1)   \
+  X(64, 128, 2, 1, 4, 3)
+
+template <bool FLIP>
+int launch_s1(const float* in, const float* wt, float* out, int64_t n, int64_t k_ch,
+              int64_t m_ch, int64_t h, int64_t w, int kid, double bytes, double flops,
+              hipStream_t s) {
+  S2Geo g;
+  if (!s1_geo(n, m_ch, h, w, &g)) return MDE_ERR_UNSUPPORTED;
+  const dim3 grid(xcd_grid(g.total)), block(256);
+#define MDE_GO(BM, BQ, MT, QT, R, NJ)                                                             \
+  if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) {                                     \
+    const int ps = pitch32(R * g.xw);                                                             \
+    const size_t smem = sizeof(float) * ((size_t)CIC * ps + (size_t)BM * AP);                     \
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (c3s1_kernel<FLIP, BM, BQ, MT, QT, R, NJ>), grid, block,  \
+                    smem, in, wt, out, (int)k_ch, (int)m_ch, (int)h, (int)w, g.xw, ps, g.qtiles, \
+                    g.mtiles, (int)g.total);                                                      \
+    return MDE_OK;                                                                                \
+  }
+  MDE_S1_GEOS(MDE_GO)
+#undef MDE_GO
+  return MDE_ERR_UNSUPPORTED;
+}
+
+inline bool s1_supported(int64_t m_ch, int64_t k_ch, int64_t h, int64_t w) {
+  S2Geo g;
+  if (k_ch < 32 || m_ch < 32 || k_ch % 32 || m_ch % 32 || h < 1 || w < 1 ||
+      !s1_geo(1, m_ch, h, w, &g))
+    return false;
+#define MDE_MATCH(BM, BQ, MT, QT, R, NJ) \
+  if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) return true;
+  MDE_S1_GEOS(MDE_MATCH)
+#undef MDE_MATCH
+  return false;
+}
+
 }  // namespace
 
 extern "C" {
+
+int mde_conv3x3_wide_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int pass,
+                               int dtype) {
+  if (dtype != MDE_F32) return 0;
+  if (pass == 0) return s1_supported(cout, cin, h, w) ? 1 : 0;
+  if (pass == 1) return s1_supported(cin, cout, h, w) ? 1 : 0;
+  return 0;
+}
+
+int mde_conv3x3_wide_fwd(const void* x, const float* weight, void* y, int64_t n, int64_t cin,
+                         int64_t cout, int64_t h, int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !weight || !y || n <= 0) return MDE_ERR_INVALID_ARG;
+  if (!s1_supported(cout, cin, h, w) || n * (cin > cout ? cin : cout) * h * w >= ((int64_t)1 << 31))
+    return MDE_ERR_UNSUPPORTED;
+  const double flops = 2.0 * 9 * n * h * w * (double)cin * cout;
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  return launch_s1<false>((const float*)x, weight, (float*)y, n, cin, cout, h, w, mde::K_C3W_FWD,
+                          bytes, flops, (hipStream_t)stream);
+}
+
+int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int64_t n,
+                              int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
+                              void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !weight || !gx || n <= 0) return MDE_ERR_INVALID_ARG;
+  if (!s1_supported(cin, cout, h, w) || n * (cin > cout ? cin : cout) * h * w >= ((int64_t)1 << 31))
+    return MDE_ERR_UNSUPPORTED;
+  const double flops = 2.0 * 9 * n * h * w * (double)cin * cout;
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  return launch_s1<true>((const float*)gy, weight, (float*)gx, n, cout, cin, h, w,
+                         mde::K_C3W_DGRAD, bytes, flops, (hipStream_t)stream);
+}
+
 
 int mde_conv3x3s2_fwd_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype) {
   S2Geo g;

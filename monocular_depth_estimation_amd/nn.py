@@ -400,7 +400,11 @@ class _Conv3x3(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
-        if passes[0]:
+        if passes[0] == WIDE:  # no statistics epilogue: the BatchNorm reads y
+            y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
+            _abi.call("mde_conv3x3_wide_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin,
+                      cout, h, w, _abi.dtype_code(x), _abi.stream_of(x))
+        elif passes[0]:
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
             if want_stats:  # + y's per-block BN statistics from the epilogue
                 nb = _abi.query("mde_conv3x3_stats_blocks", n, cin, cout, h, w, _abi.MDE_F32)
@@ -428,7 +432,11 @@ class _Conv3x3(torch.autograd.Function):
         gx = gw = None
         st = _abi.stream_of(gy)
         if ctx.needs_input_grad[0]:
-            if ctx.passes[1]:
+            if ctx.passes[1] == WIDE:
+                gx = torch.empty_like(x)
+                _abi.call("mde_conv3x3_wide_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx),
+                          n, cin, cout, h, w, _abi.dtype_code(gy), st)
+            elif ctx.passes[1]:
                 gx = torch.empty_like(x)
                 _abi.call("mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx), n,
                           cin, cout, h, w, _abi.dtype_code(gy), st)
@@ -696,14 +704,23 @@ def conv3x3_passes(conv: nn.Conv2d, x):
     if _conv3x3_bf16_path(cin, cout, x, conv.weight):
         p, dt = CONV3X3_HIP_BF16[(cin, cout)], _abi.MDE_BF16
     elif x.dtype == torch.float32:
-        p, dt = CONV3X3_HIP.get((cin, cout)), _abi.MDE_F32
+        p, dt = CONV3X3_HIP.get((cin, cout), (False, False, False)), _abi.MDE_F32
     else:
         return None
-    if p is None:
-        return None
-    p = tuple(bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
-              for i, f in enumerate(p))
-    return p if any(p) else None
+    p = [bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
+         for i, f in enumerate(p)]
+    if dt == _abi.MDE_F32 and C3_WIDE and not _autocast_bf16(x):
+        # forward / data gradient of the 32-256-channel convs on the band-GEMM
+        # kernels (conv3x3s2.hip c3s1_kernel) where MIOpen would run Winograd
+        for i in (0, 1):
+            if not p[i] and _abi.query("mde_conv3x3_wide_supported", cin, cout, x.shape[2],
+                                       x.shape[3], i, dt):
+                p[i] = WIDE
+    return tuple(p) if any(p) else None
+
+
+WIDE = 2  # conv3x3_passes flag: the pass runs on the wide-channel kernel
+C3_WIDE = os.environ.get("MDE_C3_WIDE", "1") != "0"  # A/B switch (0: MIOpen Winograd)
 
 
 def _conv3x3_apply(x, weight, passes, want_stats):

@@ -85,3 +85,37 @@ def test_conv3x3s2_full_batch_vs_miopen_deterministic():
     assert rel_err(outs[0][0], ym) <= 2e-5
     assert rel_err(outs[0][1], xm.grad) <= 2e-5
     assert rel_err(outs[0][2], wm.grad) <= 5e-5
+
+
+# stride 1, wide channels (c3s1_kernel): DDRNet's BasicBlock / DAPPM / head
+# convs at cfg2 sizes (bs 2) and ragged planes; (cin, cout, h, w)
+S1_SHAPES = [(32, 32, 120, 160), (64, 64, 60, 80), (128, 128, 30, 40), (256, 256, 15, 20),
+             (128, 128, 8, 10), (64, 64, 120, 160), (128, 64, 60, 80), (64, 64, 9, 40),
+             (96, 64, 11, 30)]
+
+
+@pytest.mark.parametrize("cin,cout,h,w", S1_SHAPES)
+def test_conv3x3_wide_s1_vs_float64_oracle(cin, cout, h, w):
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import WIDE, Conv2d, conv3x3_passes
+    n = 2
+    g = torch.Generator().manual_seed(cin + 5 * cout + w)
+    x = torch.rand((n, cin, h, w), generator=g) - 0.5
+    wt = (torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.1
+    gy = torch.rand((n, cout, h, w), generator=g) - 0.5
+    xr = x.double().requires_grad_(True)
+    wr = wt.double().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, wr, None, 1, 1)
+    yr.backward(gy.double())
+    conv = Conv2d(cin, cout, 3, padding=1, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(wt)
+    xg = x.to(DEV).requires_grad_(True)
+    passes = conv3x3_passes(conv, xg)
+    assert passes is not None and passes[0] == WIDE and passes[1] == WIDE, passes
+    assert _abi.query("mde_conv3x3_wide_supported", cin, cout, h, w, 0, 0) == 1
+    y = conv(xg)
+    y.backward(gy.to(DEV))
+    assert rel_err(y, yr) <= 1e-5, "forward"
+    assert rel_err(xg.grad, xr.grad) <= 1e-5, "data gradient"
+    assert rel_err(conv.weight.grad, wr.grad) <= 2e-5, "weight gradient"

@@ -23,6 +23,9 @@ SHAPES = [(32, 64, 2, 120, 160, 1), (64, 128, 2, 60, 80, 1), (128, 256, 2, 30, 4
 # (cin, cout, h, w, uses per cfg2 step) of the stride-2 3x3 convs (input sizes)
 S2_SHAPES = [(32, 32, 240, 320, 1), (32, 64, 120, 160, 1), (64, 128, 60, 80, 3),
              (128, 256, 30, 40, 2), (256, 256, 15, 20, 1)]
+# stride-1 3x3 on the wide kernel (BasicBlocks, DAPPM process, head): (cin, cout, h, w, uses)
+S1_SHAPES = [(32, 32, 120, 160, 4), (64, 64, 60, 80, 12), (128, 128, 30, 40, 3),
+             (256, 256, 15, 20, 3), (128, 128, 8, 10, 4), (128, 64, 60, 80, 1)]
 
 
 def main():
@@ -102,6 +105,34 @@ def run():
               f"({fl / t['fwd'] / 1e6:5.1f} / {fl / t['dgrad'] / 1e6:5.1f} TF/s) | MIOpen fwd "
               f"{t['mio_fwd']:6.1f} dgrad {t['mio_dgrad']:6.1f} us | rel diff {err:.1e}", flush=True)
     print(f"3x3s2 per cfg2 step (x uses): HIP {tot['hip']:.0f} us, MIOpen {tot['miopen']:.0f} us",
+          flush=True)
+    tot = {"hip": 0.0, "miopen": 0.0}
+    for ci, co, h, w, uses in S1_SHAPES:
+        x = torch.rand((n, ci, h, w), device="cuda") - 0.5
+        wt = (torch.rand((co, ci, 3, 3), device="cuda") - 0.5) * 0.1
+        gy = torch.rand((n, co, h, w), device="cuda") - 0.5
+        y = torch.empty_like(gy)
+        gx = torch.empty_like(x)
+        st = _abi.stream_of(x)
+        fwd = lambda: _abi.call("mde_conv3x3_wide_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, ci,
+                                co, h, w, 0, st)
+        dgr = lambda: _abi.call("mde_conv3x3_wide_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx),
+                                n, ci, co, h, w, 0, st)
+        mf = lambda: torch.nn.functional.conv2d(x, wt, None, 1, 1)
+        md = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (1, 1), (1, 1),
+                                                         False, (0, 0), 1, (True, False, False))
+        t = {k: kbench.timeit(f, 20) * 1e3 for k, f in
+             (("fwd", fwd), ("dgrad", dgr), ("mio_fwd", mf), ("mio_dgrad", md))}
+        fl = 2.0 * 9 * n * h * w * ci * co
+        fwd()
+        dgr()
+        err = max(float((a - b).abs().max() / b.abs().max()) for a, b in ((y, mf()), (gx, md()[0])))
+        tot["hip"] += uses * (t["fwd"] + t["dgrad"])
+        tot["miopen"] += uses * (t["mio_fwd"] + t["mio_dgrad"])
+        print(f"3x3s1 {ci}->{co} {h}x{w}: HIP fwd {t['fwd']:6.1f} dgrad {t['dgrad']:6.1f} us "
+              f"({fl / t['fwd'] / 1e6:5.1f} / {fl / t['dgrad'] / 1e6:5.1f} TF/s) | MIOpen fwd "
+              f"{t['mio_fwd']:6.1f} dgrad {t['mio_dgrad']:6.1f} us | rel diff {err:.1e}", flush=True)
+    print(f"3x3s1 per cfg2 step (x uses): HIP {tot['hip']:.0f} us, MIOpen {tot['miopen']:.0f} us",
           flush=True)
 
 

@@ -9,7 +9,7 @@ ROOT=$(pwd)
 OUT=gpurun_out/r04d
 mkdir -p $OUT
 export MASTER_ADDR=127.0.0.1 TMPDIR=/tmp
-AMD_LOG_LEVEL=1 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rfE --timeout 300 \
+AMD_LOG_LEVEL=1 timeout -k 10 900 python3 -u -m pytest tests -m gpu -q -rfE -p no:cacheprovider --timeout 300 \
   --timeout-method thread > $OUT/suite.log 2>&1
 rc=$?; echo "suite rc=$rc"; grep -v "Cannot find the function" $OUT/suite.log | tail -n 25 | cut -c1-400
 [ $rc -le 1 ] || exit $rc

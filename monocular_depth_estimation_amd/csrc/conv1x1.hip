@@ -49,6 +49,16 @@ __device__ __forceinline__ int xcd_logical(int total) {
 
 inline unsigned xcd_grid(int64_t total) { return (unsigned)((total + 7) / 8 * 8); }
 
+// q / d for 0 <= q < 2^22, 1 <= d < 2^10, with d's float reciprocal: the
+// float quotient is within one of the true one, fixed by one compare each way
+// (a 32-bit integer division is a ~30-instruction sequence on the VALU).
+__device__ __forceinline__ int fdiv(int q, int d, float inv) {
+  int r = (int)((float)q * inv);
+  r -= r * d > q ? 1 : 0;
+  r += (r + 1) * d <= q ? 1 : 0;
+  return r;
+}
+
 // ------------------------------------------------------------- channel mix
 // BM x BQ block tile, wave tile (32 MT) x (32 QT), 4 waves.
 // SIN = 2: input pixel of q is (2 (q / wo), 2 (q % wo)) of a hin x win plane.
@@ -79,6 +89,7 @@ __global__ void __launch_bounds__(256)
   const int wm = wv / WQ, wq = wv % WQ;
   const int64_t hwin = (int64_t)hin * win;
   const float* inb = in + (int64_t)img * K * hwin;
+  const float inv_wo = 1.f / (float)wo;
 
   float4 ra[AV], rb[BV];
   auto load = [&](int k0) {
@@ -107,7 +118,7 @@ __global__ void __launch_bounds__(256)
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int qq = q + j, r = qq / wo, c = qq - r * wo;
+          const int qq = q + j, r = fdiv(qq, wo, inv_wo), c = qq - r * wo;
           const float t = src[qq < Q ? (int64_t)(2 * r) * win + 2 * c : 0];
           v[j] = qq < Q ? t : 0.f;
         }
@@ -178,7 +189,7 @@ __global__ void __launch_bounds__(256)
     int64_t po = q;
     int rr = 0, cc = 0;
     if constexpr (SOUT == 2) {
-      rr = q / wo;
+      rr = fdiv(q, wo, inv_wo);
       cc = q - rr * wo;
       po = (int64_t)(2 * rr) * wout + 2 * cc;
     }
@@ -225,39 +236,52 @@ __global__ void __launch_bounds__(256)
   const int wm = wv / WN, wn = wv % WN;
   const int64_t hwin = (int64_t)hin * win;
 
+  const float inv_wo = 1.f / (float)wo;
   float4 ra[AV], rb[BV];
+  // chunk = KC consecutive pixels of the n * Q flattened pixels (Q >= KC, so a
+  // chunk touches at most two images): image / offset of its first pixel by
+  // one wave-uniform division, each float4 (4 pixels of one image, Q % 4 == 0)
+  // wraps into the next image at most once
   auto load = [&](int chunk) {
-    const int64_t p0 = (int64_t)chunk * KC;
+    const int p0 = chunk * KC;
+    const int n0 = p0 / Q, q0 = p0 - n0 * Q;
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
       const int e = 4 * (tid + 256 * i);
       const int row = e / KC, k = e % KC;
-      const int64_t g = p0 + k;  // 4 pixels of one image (Q % 4 == 0)
-      const bool ok = g < npix;
-      const bool rok = ok && co0 + row < CO;  // rows past CO: a 128-row tile over 64 channels
-      const int64_t n = ok ? g / Q : 0, q = ok ? g - n * Q : 0;
+      const bool wrap = q0 + k >= Q;
+      const int n = n0 + (wrap ? 1 : 0), q = q0 + k - (wrap ? Q : 0);
+      const bool ok = p0 + k < npix && co0 + row < CO;  // rows past CO: a 128-row tile over 64
       const int cr = co0 + row < CO ? co0 + row : CO - 1;
-      const float4 t = *reinterpret_cast<const float4*>(gy + (n * CO + cr) * (int64_t)Q + q);
-      ra[i] = rok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 t = *reinterpret_cast<const float4*>(
+          gy + ((ok ? n : 0) * CO + cr) * Q + (ok ? q : 0));
+      ra[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
       const int e = 4 * (tid + 256 * i);
       const int row = e / KC, k = e % KC;
-      const int64_t g = p0 + k;
-      const bool ok = g < npix && ci0 + row < CI;
-      const int64_t n = g < npix ? g / Q : 0, q = g < npix ? g - n * Q : 0;
-      const float* src = x + (n * CI + (ci0 + row < CI ? ci0 + row : CI - 1)) * hwin;
+      const bool wrap = q0 + k >= Q;
+      const int n = n0 + (wrap ? 1 : 0), q = q0 + k - (wrap ? Q : 0);
+      const bool ok = p0 + k < npix && ci0 + row < CI;
+      const int cr = ci0 + row < CI ? ci0 + row : CI - 1;
+      const float* src = x + (int64_t)((ok ? n : 0) * CI + cr) * hwin;
       if constexpr (SIN == 1) {
-        const float4 t = *reinterpret_cast<const float4*>(src + q);
+        const float4 t = *reinterpret_cast<const float4*>(src + (ok ? q : 0));
         rb[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         float v[4];
+        const int qb = ok ? q : 0;
+        const int r = fdiv(qb, wo, inv_wo);
+        int c = qb - r * wo, rr = r;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int qq = (int)q + j, r = qq / wo, c = qq - r * wo;
-          const float t = src[(int64_t)(2 * r) * win + 2 * c];
+        for (int j = 0; j < 4; ++j) {  // wo % 4 need not hold: step along the row
+          const float t = src[(2 * rr) * win + 2 * c];
           v[j] = ok ? t : 0.f;
+          if (++c == wo) {
+            c = 0;
+            ++rr;
+          }
         }
         rb[i] = make_float4(v[0], v[1], v[2], v[3]);
       }
@@ -345,7 +369,8 @@ inline bool c1_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w,
   const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
   if ((ho * wo) % 4) return false;
   if (stride == 2 && w % 2) return false;  // gx rows written as (value, 0) pairs
-  return n * ci * h * w < (int64_t)1 << 31 && n * co * ho * wo < (int64_t)1 << 31;
+  return n * ci * h * w < (int64_t)1 << 31 && n * co * ho * wo < (int64_t)1 << 31 &&
+         ho * wo >= KC && ho < (1 << 12) && wo < (1 << 10);
 }
 
 // M-tile of the channel mix: 128 when M % 128 == 0, else 64, else 32.

@@ -627,10 +627,16 @@ int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int
 }
 
 
+// Measured against MIOpen at bs 32 (tools/c1_bench.py, profiles/r04_c1_bench.txt):
+// the band kernels win on the planes of >= 256 output pixels (forward) and
+// >= 1024 gy pixels (data gradient); the 15x20 -> 8x10 and 30x40 -> 15x20
+// data gradients (one or two waves per SIMD over a long K loop) lose, so the
+// queries send those to MIOpen.
 int mde_conv3x3s2_fwd_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype) {
   S2Geo g;
   if (dtype != MDE_F32 || !s2_shape_ok(1, cin, cout, h, w) || !fwd_geo(1, cin, cout, h, w, &g))
     return 0;
+  if (((h - 1) / 2 + 1) * ((w - 1) / 2 + 1) < 256) return 0;
 #define MDE_MATCH(BM, BQ, MT, QT, R, NJ) \
   if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) return 1;
   MDE_S2_FWD_GEOS(MDE_MATCH)
@@ -642,6 +648,7 @@ int mde_conv3x3s2_dgrad_supported(int64_t cin, int64_t cout, int64_t h, int64_t 
   S2Geo g;
   if (dtype != MDE_F32 || !s2_shape_ok(1, cin, cout, h, w) || !dgrad_geo(1, cin, cout, h, w, &g))
     return 0;
+  if (((h - 1) / 2 + 1) * ((w - 1) / 2 + 1) < 1024) return 0;
 #define MDE_MATCH(BM, BQ, R, NJ) \
   if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) return 1;
   MDE_S2_DGRAD_GEOS(MDE_MATCH)

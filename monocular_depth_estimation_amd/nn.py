@@ -614,14 +614,19 @@ class _Conv1x1(torch.autograd.Function):
     def forward(ctx, x, weight, stride):
         x = x.contiguous()
         weight = weight.contiguous()
+        ctx.save_for_backward(x, weight)
+        ctx.stride = stride
+        if stride == 1:
+            # MIOpen runs the stride-1 forward as one NCHW GEMM (rocBLAS, no
+            # transposes), as fast or faster than the HIP kernel at these
+            # shapes (tools/c1_bench.py): only its backward needs replacing
+            return torch.nn.functional.conv2d(x, weight)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         ho, wo = (h - 1) // stride + 1, (w - 1) // stride + 1
         y = torch.empty((n, cout, ho, wo), dtype=x.dtype, device=x.device)
         _abi.call("mde_conv1x1_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin, cout, h, w,
                   stride, _abi.dtype_code(x), _abi.stream_of(x))
-        ctx.save_for_backward(x, weight)
-        ctx.stride = stride
         return y
 
     @staticmethod
@@ -720,7 +725,9 @@ def conv3x3_passes(conv: nn.Conv2d, x):
 
 
 WIDE = 2  # conv3x3_passes flag: the pass runs on the wide-channel kernel
-C3_WIDE = os.environ.get("MDE_C3_WIDE", "1") != "0"  # A/B switch (0: MIOpen Winograd)
+# Off by default: MIOpen's Winograd matches the stride-1 band kernel on these
+# shapes (tools/c1_bench.py) and the cfg2 step was 0.5 % slower with it on
+C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"
 
 
 def _conv3x3_apply(x, weight, passes, want_stats):

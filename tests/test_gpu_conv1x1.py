@@ -20,8 +20,8 @@ DEV = "cuda"
 SHAPES = [(32, 64, 2, 120, 160), (64, 128, 2, 60, 80), (128, 256, 2, 30, 40),
           (256, 512, 2, 15, 20), (64, 128, 1, 60, 80), (128, 64, 1, 30, 40),
           (256, 64, 1, 15, 20), (256, 256, 1, 15, 20), (256, 512, 1, 8, 10),
-          (512, 128, 1, 8, 10), (640, 128, 1, 8, 10), (512, 128, 1, 4, 5),
-          (96, 160, 1, 6, 6), (64, 96, 2, 7, 10)]
+          (512, 128, 1, 8, 10), (640, 128, 1, 8, 10), (96, 160, 1, 6, 6),
+          (64, 96, 2, 15, 20), (96, 64, 2, 13, 24)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -58,7 +58,12 @@ def test_conv1x1_vs_float64_oracle(cin, cout, stride, h, w):
     xg = x.to(DEV).requires_grad_(True)
     assert conv1x1_ok(conv, xg)
     assert _abi.query("mde_conv1x1_supported", cin, cout, h, w, stride, 0) == 1
-    y = conv(xg)
+    y = conv(xg)  # stride 1: the MIOpen forward; HIP data / weight gradients
+    yh = torch.empty_like(y)
+    w2 = conv.weight.detach().reshape(cout, cin).contiguous()
+    _abi.call("mde_conv1x1_fwd", _abi.ptr(xg.detach()), _abi.ptr(w2), _abi.ptr(yh), n, cin, cout,
+              h, w, stride, 0, _abi.stream_of(xg))
+    assert rel_err(yh, yr) <= 1e-5, "HIP forward"
     y.backward(gy.to(DEV))
     assert y.shape == yr.shape
     assert rel_err(y, yr) <= 1e-5, "forward"
@@ -94,6 +99,15 @@ def test_conv1x1_full_batch_vs_miopen_and_deterministic(cin, cout, stride, h, w)
     assert rel_err(y, ym) <= 2e-5
     assert rel_err(gx, xm.grad) <= 2e-5
     assert rel_err(gw, wm.grad) <= 5e-5
+
+
+def test_conv1x1_small_planes_are_not_taken():
+    """Planes of fewer than 32 output pixels (DAPPM's pooled 4x5 / 2x3 maps)
+    stay on MIOpen: the weight gradient's pixel chunks assume a chunk touches
+    at most two images."""
+    from monocular_depth_estimation_amd import _abi
+    assert _abi.query("mde_conv1x1_supported", 512, 128, 4, 5, 1, 0) == 0
+    assert _abi.query("mde_conv1x1_supported", 512, 128, 8, 10, 1, 0) == 1
 
 
 def test_conv1x1_stride2_zero_fills_odd_positions():

@@ -346,20 +346,51 @@ __global__ void __launch_bounds__(256)
       }
 }
 
-// gw[e] = sum_s part[s][e], s in order (e in float4 groups; E % 4 == 0)
-__global__ void __launch_bounds__(256)
+// gw[e] = sum_s part[s][e] in a fixed order (E % 4 == 0): a block owns 64
+// float4 columns; its 16 waves sum the slabs s = w, w + 16, ... (lane = column,
+// four loads in flight), then wave 0 adds the 16 wave sums in wave order.
+__global__ void __launch_bounds__(1024)
     c1_wreduce_kernel(const float* __restrict__ part, float* __restrict__ gw, int64_t E, int ks) {
-  const int64_t e4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (4 * e4 >= E) return;
-  float4 a = reinterpret_cast<const float4*>(part)[e4];
-  for (int s = 1; s < ks; ++s) {
-    const float4 b = reinterpret_cast<const float4*>(part + (int64_t)s * E)[e4];
-    a.x += b.x;
-    a.y += b.y;
-    a.z += b.z;
-    a.w += b.w;
+  __shared__ float4 red[16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t e4 = (int64_t)blockIdx.x * 64 + lane;
+  const bool ok = 4 * e4 < E;
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  const int64_t E4 = E / 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  int s = wv;
+  for (; s + 48 < ks; s += 64) {
+    float4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = ok ? p4[(int64_t)(s + 16 * u) * E4 + e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a.x += v[u].x;
+      a.y += v[u].y;
+      a.z += v[u].z;
+      a.w += v[u].w;
+    }
   }
-  reinterpret_cast<float4*>(gw)[e4] = a;
+  for (; s < ks; s += 16) {
+    const float4 v = ok ? p4[(int64_t)s * E4 + e4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    a.x += v.x;
+    a.y += v.y;
+    a.z += v.z;
+    a.w += v.w;
+  }
+  red[wv][lane] = a;
+  __syncthreads();
+  if (wv == 0 && ok) {
+    float4 t = red[0][lane];
+    for (int k = 1; k < 16; ++k) {
+      const float4 b = red[k][lane];
+      t.x += b.x;
+      t.y += b.y;
+      t.z += b.z;
+      t.w += b.w;
+    }
+    reinterpret_cast<float4*>(gw)[e4] = t;
+  }
 }
 
 // ------------------------------------------------------------------- plans
@@ -428,9 +459,9 @@ inline WgPlan wg_plan(int64_t n, int64_t ci, int64_t co, int64_t ho, int64_t wo)
   p.npix = n * ho * wo;
   p.nchunks = (int)mde::cdiv(p.npix, KC);
   const int tiles = p.cotiles * p.citiles;
-  // ~512 blocks (two per CU), at least 4 chunks per block, slab <= 64 MB
+  // ~512 blocks (two per CU), at least 8 chunks per block, slab <= 64 MB
   int ks = (int)mde::cdiv(512, tiles);
-  if (ks > p.nchunks / 4) ks = p.nchunks / 4;
+  if (ks > p.nchunks / 8) ks = p.nchunks / 8;
   const int64_t cap = ((int64_t)16 << 20) / (ci * co);
   if (ks > cap) ks = (int)cap;
   p.ksplit = ks < 1 ? 1 : ks;
@@ -531,7 +562,7 @@ int mde_conv1x1_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
 #undef MDE_WG
   const int64_t E = cin * cout;
   MDE_LAUNCH(mde::K_C1_WREDUCE, 4.0 * E * (p.ksplit + 1), s, c1_wreduce_kernel,
-             dim3((unsigned)mde::cdiv(E / 4, 256)), dim3(256), 0, part, gweight, E, p.ksplit);
+             dim3((unsigned)mde::cdiv(E / 4, 64)), dim3(1024), 0, part, gweight, E, p.ksplit);
   return MDE_OK;
 }
 

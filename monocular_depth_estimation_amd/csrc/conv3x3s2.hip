@@ -28,6 +28,8 @@
 // N = BQ positions (m, n) of the gy grid, K = (co, class taps); one block keeps
 // the four classes' accumulators and writes gx rows 2m and 2m + 1 as float2
 // pairs (all of gx is written; odd Hi: the last odd row does not exist).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -510,11 +512,11 @@ inline bool dgrad_geo(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi,
 }
 
 // stride 1: BM output channels (of this pass) x BQ pixels; plane pitch = 32 (mod 64)
-inline bool s1_geo(int64_t n, int64_t m_ch, int64_t h, int64_t w, S2Geo* g) {
+inline bool s1_geo_at(int64_t n, int64_t m_ch, int64_t h, int64_t w, int bm, int bq, S2Geo* g) {
   const int64_t Q = h * w;
-  g->bm = m_ch % 64 == 0 ? 64 : 32;
-  if (m_ch % g->bm) return false;
-  g->bq = (Q >= 1024 || g->bm == 32) ? 128 : 64;
+  if (m_ch % bm) return false;
+  g->bm = bm;
+  g->bq = bq;
   const int rows = rows_span(g->bq, w, h);
   g->r = rows + 2;
   g->xw = (int)w + 2;
@@ -525,6 +527,14 @@ inline bool s1_geo(int64_t n, int64_t m_ch, int64_t h, int64_t w, S2Geo* g) {
   g->total = n * g->qtiles * g->mtiles;
   return g->total < 0x7fffffff;
 }
+
+// baseline tile: BM 64 (32 for 32-channel outputs) x BQ 128 (64 on planes < 1024)
+inline bool s1_geo(int64_t n, int64_t m_ch, int64_t h, int64_t w, S2Geo* g) {
+  const int bm = m_ch % 64 == 0 ? 64 : 32;
+  const int bq = (h * w >= 1024 || bm == 32) ? 128 : 64;
+  return s1_geo_at(n, m_ch, h, w, bm, bq, g);
+}
+
 inline int pitch32(int v) { return (v + 31) / 64 * 64 + 32; }  // >= v, = 32 (mod 64)
 
 inline bool s2_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi) {
@@ -548,20 +558,45 @@ inline bool s2_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t w
   X(64, 64, 6, 1)            \
   X(64, 64, 9, 1)
 
+// (BM, BQ, MT, QT, R, NJ); the 2 x 2 wave tiles (four MFMAs per k-step on two
+// A and two B reads) are taken when they still give >= 512 blocks
 #define MDE_S1_GEOS(X)     \
   X(32, 128, 1, 1, 4, 3)   \
   X(64, 128, 2, 1, 5, 2)   \
   X(64, 128, 2, 1, 7, 1)   \
   X(64, 64, 1, 1, 7, 1)    \
   X(64, 64, 1, 1, 10, 1)   \
-  X(64, 128, 2, 1, 4, 3)
+  X(64, 128, 2, 1, 4, 3)   \
+  X(32, 256, 1, 2, 5, 3)   \
+  X(64, 256, 2, 2, 7, 2)   \
+  X(64, 256, 2, 2, 5, 3)   \
+  X(128, 128, 2, 2, 7, 1)  \
+  X(128, 128, 2, 2, 4, 3)  \
+  X(128, 128, 2, 2, 5, 2)
 
 template <bool FLIP>
 int launch_s1(const float* in, const float* wt, float* out, int64_t n, int64_t k_ch,
               int64_t m_ch, int64_t h, int64_t w, int kid, double bytes, double flops,
               hipStream_t s) {
   S2Geo g;
-  if (!s1_geo(n, m_ch, h, w, &g)) return MDE_ERR_UNSUPPORTED;
+  static const int pref = [] {  // MDE_C3W_TILE=0: the baseline tile only (A/B)
+    const char* e = std::getenv("MDE_C3W_TILE");
+    return e ? std::atoi(e) : 1;
+  }();
+  bool big = false;
+  if (pref) {
+    const int cand[3][2] = {{128, 128}, {64, 256}, {32, 256}};
+    for (const auto& c : cand) {
+      if (s1_geo_at(n, m_ch, h, w, c[0], c[1], &g) && g.total >= 512) {
+#define MDE_MATCH(BM, BQ, MT, QT, R, NJ) \
+  if (!big && g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) big = true;
+        MDE_S1_GEOS(MDE_MATCH)
+#undef MDE_MATCH
+        if (big) break;
+      }
+    }
+  }
+  if (!big && !s1_geo(n, m_ch, h, w, &g)) return MDE_ERR_UNSUPPORTED;
   const dim3 grid(xcd_grid(g.total)), block(256);
 #define MDE_GO(BM, BQ, MT, QT, R, NJ)                                                             \
   if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) {                                     \

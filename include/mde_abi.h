@@ -575,6 +575,18 @@ int mde_eval_sums(const void* pred, const void* gt, int64_t n, int64_t h, int64_
                   float min_depth, float max_depth, int mode, const int32_t* crop,
                   void* workspace, double* sums, int dtype, void* stream);
 
+/* The guide convs under bf16 autocast (src/GuideDepth/model/modules.py:52-54,
+ * GuideDepth.py:46-47 feeding them the image): y = conv3x3(bf16(x), bf16(w))
+ * with fp32 accumulation, stored as bf16 -- autocast's conv semantics -- from
+ * the fp32 image, so neither an fp32 output nor a cast pass exists.  cout 16,
+ * 32 or 64.  stats (nullable) [cout][blocks][4], blocks =
+ * mde_conv3x3_guide_bf16_stats_blocks(...), the statistics of the stored
+ * (rounded) y for the BatchNorm that follows.  The weight gradient is
+ * mde_conv3x3_wgrad (fp32). */
+int mde_conv3x3_guide_bf16_stats_blocks(int64_t n, int64_t cout, int64_t h, int64_t w);
+int mde_conv3x3_guide_bf16_fwd(const float* x, const float* weight, void* y, float* stats,
+                               int64_t n, int64_t cout, int64_t h, int64_t w, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Wide 1x1 convolutions (NCHW fp32, bias-free, stride 1 or 2, padding 0):
  * DDRNet's Bottleneck conv1 / conv3, the residual downsample, compression3 /

@@ -144,6 +144,8 @@ SIGNATURES = {
     "mde_conv3x3_wide_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int]),
     "mde_conv3x3_wide_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_conv3x3_wide_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_conv3x3_guide_bf16_stats_blocks": (_int, [_i64, _i64, _i64, _i64]),
+    "mde_conv3x3_guide_bf16_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_replace_memsets": (_int, [_vp, _c.POINTER(_i64)]),
     "mde_graph_node_counts": (_int, [_vp, _c.POINTER(_i64)]),

@@ -112,20 +112,26 @@ struct HaloTile {
     }
   }
 
-  template <int PS>
+  // RB: values rounded to bf16 precision (RNE) as they are staged -- the
+  // autocast guide conv computes on the bf16 image
+  template <int PS, bool RB = false>
   __device__ __forceinline__ void store(float* sx, int lane, int wvu) const {
 #pragma unroll
     for (int k = 0; k < RPWV; ++k) {
       const int ri = wvu + 4 * k;
-      if (ROWS % 4 == 0 || ri < ROWS)
-        sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = (am >> k) & 1 ? a[k] : 0.f;
+      if (ROWS % 4 == 0 || ri < ROWS) {
+        const float v = (am >> k) & 1 ? a[k] : 0.f;
+        sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = RB ? mde::bf2f(mde::f2bf(v)) : v;
+      }
     }
 #pragma unroll
     for (int q = 0; q < NH; ++q) {
       const int e = 64 * q + lane;
       const int ri = wvu + 4 * (e >> 1);
-      if (e < 2 * RPWV && ri < ROWS)
-        sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = (bm >> q) & 1u ? b[q] : 0.f;
+      if (e < 2 * RPWV && ri < ROWS) {
+        const float v = (bm >> q) & 1u ? b[q] : 0.f;
+        sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = RB ? mde::bf2f(mde::f2bf(v)) : v;
+      }
     }
   }
 };
@@ -222,12 +228,17 @@ __device__ __forceinline__ TileGeo tile_geo(int tile, int th, int tiles_w, int t
 // this block's tiles -> stats[(co * gridDim.x + block) * 4] = (shift, count,
 // sum (y - shift), sum (y - shift)^2), the following BatchNorm's statistics
 // without re-reading y.
-template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
+// TO = bf16 (the autocast guide convs, modules.py:52-54 under bf16 autocast):
+// image and weights rounded to bf16 precision on staging (autocast's input
+// casts), exact f32 products and f32 accumulation as the bf16 MFMA, output
+// rounded to bf16 (RNE) -- the statistics epilogue sees the rounded values.
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false, typename TO = float>
 __global__ void __launch_bounds__(256, 2)
     conv3x3_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
-                       float* __restrict__ y, int h, int w, int tiles_w, int tiles_per_img,
+                       TO* __restrict__ y, int h, int w, int tiles_w, int tiles_per_img,
                        int ntiles, float* __restrict__ stats = nullptr) {
   static_assert(!(STATS && FLIP), "statistics are a forward epilogue");
+  constexpr bool RB = sizeof(TO) == 2;
   constexpr int CIP = cpad4(CI);
   constexpr int TH = 4 * RPW;
   constexpr int XR = TH + 2;
@@ -254,7 +265,7 @@ __global__ void __launch_bounds__(256, 2)
       const bool ok = e < WN && ci < CI;
       const int src = FLIP ? (ci * CO + co) * 9 + (8 - tap) : (co * CI + ci) * 9 + tap;
       const float t = wt[ok ? src : 0];
-      v[i] = ok ? t : 0.f;
+      v[i] = ok ? (RB ? mde::bf2f(mde::f2bf(t)) : t) : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
@@ -283,7 +294,7 @@ __global__ void __launch_bounds__(256, 2)
   for (; tile < tw.end; tile += tw.step) {
     const TileGeo g = tile_geo(tile, TH, tiles_w, tiles_per_img);
     __syncthreads();  // previous tile's operands consumed (and weights staged)
-    T.template store<PS>(sx, lane, wvu);
+    T.template store<PS, RB>(sx, lane, wvu);
     __syncthreads();
     const int nxt = tile + tw.step;
     if (nxt < tw.end) {
@@ -317,6 +328,16 @@ __global__ void __launch_bounds__(256, 2)
       }
     }
 
+    if constexpr (RB) {  // the bf16 output's values (statistics of what is stored)
+#pragma unroll
+      for (int q = 0; q < RPW; ++q)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) acc[q][m][nb][i] = mde::bf2f(mde::f2bf(acc[q][m][nb][i]));
+    }
     if constexpr (STATS) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
@@ -337,7 +358,7 @@ __global__ void __launch_bounds__(256, 2)
       first = false;
     }
     // D layout: lane holds pixels 4*lk + i (i = 0..3) of output channel li.
-    float* yi = y + g.img * img_out;
+    TO* yi = y + g.img * img_out;
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int row = g.r0 + wv * RPW + q;
@@ -347,14 +368,14 @@ __global__ void __launch_bounds__(256, 2)
         const int col = g.c0 + m * 16 + 4 * lk;
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) {
-          float* dst = yi + ((int64_t)(nb * 16 + li) * h + row) * w + col;
+          TO* dst = yi + ((int64_t)(nb * 16 + li) * h + row) * w + col;
           const f4 v = acc[q][m][nb];
           if (vec && col + 3 < w) {
-            *reinterpret_cast<float4*>(dst) = make_float4(v[0], v[1], v[2], v[3]);
+            mde::st4(dst, make_float4(v[0], v[1], v[2], v[3]));
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              if (col + i < w) dst[i] = v[i];
+              if (col + i < w) mde::st1(dst + i, v[i]);
           }
         }
       }
@@ -1758,7 +1779,7 @@ __global__ void __launch_bounds__(256, 2)
 // ---------------------------------------------------------------- dispatch
 enum Pass { kFwd = 0, kDgrad = 1, kWgrad = 2 };
 
-template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false, typename TO = float>
 int fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_img, int* ntiles) {
   constexpr int TH = 4 * RPW;
   *tiles_w = (int)mde::cdiv(w, kTW);
@@ -1766,18 +1787,19 @@ int fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_img, 
   const int64_t nt = n * *tiles_per_img;
   if (nt > 0x7fffffff) return 0;
   *ntiles = (int)nt;
-  const int res = resident_blocks<conv3x3_fwd_kernel<CI, CO, RPW, FLIP, STATS>>();
+  const int res = resident_blocks<conv3x3_fwd_kernel<CI, CO, RPW, FLIP, STATS, TO>>();
   return nt < res ? (int)nt : res;
 }
 
-template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
-int launch_fwd(const float* in, const float* wt, float* out, int64_t n, int64_t h, int64_t w,
+template <int CI, int CO, int RPW, bool FLIP, bool STATS = false, typename TO = float>
+int launch_fwd(const float* in, const float* wt, TO* out, int64_t n, int64_t h, int64_t w,
                double bytes, int kid, hipStream_t s, float* stats = nullptr) {
   const double flops = 2.0 * 9 * CI * CO * (double)(n * h * w);
   int tiles_w, tiles_per_img, ntiles;
-  const int grid = fwd_grid<CI, CO, RPW, FLIP, STATS>(n, h, w, &tiles_w, &tiles_per_img, &ntiles);
+  const int grid =
+      fwd_grid<CI, CO, RPW, FLIP, STATS, TO>(n, h, w, &tiles_w, &tiles_per_img, &ntiles);
   if (grid <= 0) return MDE_ERR_INVALID_ARG;
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP, STATS>),
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_fwd_kernel<CI, CO, RPW, FLIP, STATS, TO>),
                   dim3(grid), dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img,
                   ntiles, stats);
   return MDE_OK;
@@ -1989,6 +2011,35 @@ bool s2_dims_ok(int64_t n, int64_t h, int64_t w) {
 }  // namespace
 
 extern "C" {
+
+int mde_conv3x3_guide_bf16_stats_blocks(int64_t n, int64_t cout, int64_t h, int64_t w) {
+  int a, b, c;
+  if (!dims_ok(n, h, w)) return 0;
+  if (cout == 16) return fwd_grid<3, 16, 2, false, true, bf16>(n, h, w, &a, &b, &c);
+  if (cout == 32) return fwd_grid<3, 32, 1, false, true, bf16>(n, h, w, &a, &b, &c);
+  if (cout == 64) return fwd_grid<3, 64, 1, false, true, bf16>(n, h, w, &a, &b, &c);
+  return 0;
+}
+
+int mde_conv3x3_guide_bf16_fwd(const float* x, const float* weight, void* y, float* stats,
+                               int64_t n, int64_t cout, int64_t h, int64_t w, void* stream) {
+  if (!x || !weight || !y || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
+  if (cout != 16 && cout != 32 && cout != 64) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  bf16* out = (bf16*)y;
+  const double bytes = (double)n * h * w * (4.0 * 3 + 2.0 * cout);
+  const int k = mde::K_C3_FWD;
+  if (stats) {
+    if (cout == 16)
+      return launch_fwd<3, 16, 2, false, true, bf16>(x, weight, out, n, h, w, bytes, k, s, stats);
+    if (cout == 32)
+      return launch_fwd<3, 32, 1, false, true, bf16>(x, weight, out, n, h, w, bytes, k, s, stats);
+    return launch_fwd<3, 64, 1, false, true, bf16>(x, weight, out, n, h, w, bytes, k, s, stats);
+  }
+  if (cout == 16) return launch_fwd<3, 16, 2, false, false, bf16>(x, weight, out, n, h, w, bytes, k, s);
+  if (cout == 32) return launch_fwd<3, 32, 1, false, false, bf16>(x, weight, out, n, h, w, bytes, k, s);
+  return launch_fwd<3, 64, 1, false, false, bf16>(x, weight, out, n, h, w, bytes, k, s);
+}
 
 int mde_conv3x3_supported(int64_t cin, int64_t cout, int pass, int dtype) {
   if (dtype == MDE_BF16) return bf_supported(cin, cout) && pass >= 0 && pass <= 2 ? 1 : 0;

@@ -730,10 +730,55 @@ WIDE = 2  # conv3x3_passes flag: the pass runs on the wide-channel kernel
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"
 
 
+class _GuideConvBf16(torch.autograd.Function):
+    """The guided-upsampling blocks' guide convs (3 -> 16 / 32 / 64 on the
+    image, modules.py:52-54) under bf16 autocast: the fp32 image and weight
+    rounded to bf16 in the kernel (autocast's casts), fp32 accumulation, a
+    bf16 output (mde_conv3x3_guide_bf16_fwd, + the following BatchNorm's
+    statistics), so no fp32 output and no cast pass exist; the weight
+    gradient on the fp32 kernel (the image needs no gradient)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, want_stats):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        n, _, h, w = x.shape
+        cout = weight.shape[0]
+        y = torch.empty((n, cout, h, w), dtype=torch.bfloat16, device=x.device)
+        nb = _abi.query("mde_conv3x3_guide_bf16_stats_blocks", n, cout, h, w) if want_stats else 0
+        stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
+        _abi.call("mde_conv3x3_guide_bf16_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y),
+                  _abi.ptr(stats) if nb else None, n, cout, h, w, _abi.stream_of(x))
+        ctx.save_for_backward(x, weight)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, gy, _gstats):
+        x, weight = ctx.saved_tensors
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gyf = gy.float().contiguous()
+            n, cin, h, w = x.shape
+            cout = weight.shape[0]
+            gw = torch.empty_like(weight)
+            ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w,
+                                _abi.MDE_F32), x)
+            _abi.call("mde_conv3x3_wgrad", _abi.ptr(gyf), _abi.ptr(x), _abi.ptr(gw), n, cin, cout,
+                      h, w, _abi.ptr(ws), _abi.MDE_F32, _abi.stream_of(gyf))
+        return None, gw, None
+
+
+GUIDE_BF16 = os.environ.get("MDE_GUIDE_BF16", "1") != "0"  # A/B switch
+
+
 def _conv3x3_apply(x, weight, passes, want_stats):
     if weight.dtype != torch.float32:
         raise TypeError(f"conv3x3: the HIP kernels take a float32 weight, got {weight.dtype}")
     cin, cout = x.shape[1], weight.shape[0]
+    if (GUIDE_BF16 and cin == 3 and cout in (16, 32, 64) and passes[0] and x.dtype == torch.float32
+            and _autocast_bf16(x) and not x.requires_grad):
+        return _GuideConvBf16.apply(x, weight, bool(want_stats))
     if _conv3x3_bf16_path(cin, cout, x, weight):
         return _Conv3x3Bf16.apply(x.to(torch.bfloat16), weight, tuple(passes), want_stats)
     return _Conv3x3.apply(x, weight, tuple(passes), want_stats)

@@ -299,3 +299,33 @@ def test_bilinear_x2_bf16_storage_matches_fp32_kernel(c, h, w):
     assert torch.equal(ga, gb.to(torch.bfloat16))
     if ta is not None:
         assert torch.equal(ta, tb.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("cout,h,w", [(16, 64, 96), (32, 37, 70), (64, 30, 40)])
+def test_guide_conv_bf16_matches_rounded_fp32_kernel(cout, h, w):
+    """The autocast guide conv (mde_conv3x3_guide_bf16_fwd, modules.py:52-54):
+    image and weight rounded to bf16, fp32 accumulation, bf16 output == the
+    fp32 HIP kernel on the rounded image and weight, output rounded (the same
+    accumulation order): bit-exact, and its statistics epilogue == the fp32
+    kernel's statistics of those rounded outputs within fp32 summation."""
+    from monocular_depth_estimation_amd import _abi
+    n = 2
+    g = torch.Generator().manual_seed(cout + h)
+    x = (torch.rand((n, 3, h, w), generator=g)).to(DEV)
+    wt = ((torch.rand((cout, 3, 3, 3), generator=g) - 0.5) * 0.5).to(DEV)
+    y = torch.empty((n, cout, h, w), dtype=torch.bfloat16, device=DEV)
+    nb = _abi.query("mde_conv3x3_guide_bf16_stats_blocks", n, cout, h, w)
+    stats = torch.empty((cout, nb, 4), device=DEV)
+    st = _abi.stream_of(x)
+    _abi.call("mde_conv3x3_guide_bf16_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), _abi.ptr(stats),
+              n, cout, h, w, st)
+    xr = x.to(torch.bfloat16).float()
+    wr = wt.to(torch.bfloat16).float()
+    ref = torch.empty((n, cout, h, w), device=DEV)
+    _abi.call("mde_conv3x3_fwd", _abi.ptr(xr), _abi.ptr(wr), _abi.ptr(ref), n, 3, cout, h, w, 0, st)
+    assert torch.equal(y, ref.to(torch.bfloat16))
+    yf = y.float()
+    cnt = stats[:, :, 1].sum(1)
+    mean = ((stats[:, :, 2] + stats[:, :, 0] * stats[:, :, 1]).sum(1) / cnt).double()
+    assert torch.allclose(cnt, torch.full_like(cnt, n * h * w))
+    assert torch.allclose(mean, yf.double().mean((0, 2, 3)), rtol=1e-5, atol=1e-6)

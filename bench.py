@@ -362,7 +362,10 @@ def main():
         "roofline": roofline,
         "roofline_leaders": leaders,
         "path_roofline": path_roofline,
+        "hip_kernels_note": (f"ms_total / launches summed over {timing_steps} timed "
+                             f"steps; ms_per_step = ms_total / {timing_steps}"),
         "hip_kernels": {k: dict({"ms_total": round(v[0], 3), "launches": v[1],
+                                 "ms_per_step": round(v[0] / max(timing_steps, 1), 4),
                                  "GBps": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 else None},
                                 **({"TFLOPs": round(v[3] / (v[0] * 1e-3) / 1e12, 2)} if v[3] > 0 else {}))
                         for k, v in sorted(kernels.items(), key=lambda kv: -kv[1][0])},

@@ -604,6 +604,189 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// ---------------------------------------------------------------- small tensors
+// One block per channel with the whole channel (n * hw <= kChanMax elements)
+// in registers: statistics, finalisation and apply in ONE launch that reads x
+// once (forward), and reduce + apply in one launch reading gy / x once
+// (backward) -- DDRNet's 15x20 / 8x10 / 4x5 / 2x3 / 1x1 planes at bs 32,
+// where the two-launch stats (or reduce) + table-apply pair was launch- and
+// latency-bound (~15 us a BN for a few MB).  Unit j of the channel is element
+// j (or float4 j when hw % 4 == 0) of the (image, pixel) order; sums per
+// thread in float over <= kChanUnits units, then in double across the block
+// (fixed order): deterministic.
+constexpr int kChanThreads = 512;
+constexpr int kChanUnits = 8;  // float4 (or elements) per thread
+constexpr int64_t kChanMax = (int64_t)kChanThreads * kChanUnits * 4;
+
+inline bool chan_mode(int64_t n, int64_t hw) {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_BN_CHAN");
+    return !(e && e[0] == '0');
+  }();
+  return on && !plane_mode(hw) && n * hw <= (hw % 4 == 0 ? kChanMax : kChanMax / 4);
+}
+
+// block-wide double sums of (a, b), fixed order; result valid in every thread
+__device__ __forceinline__ void chan_sum2(double* a, double* b, double (*red)[kChanThreads / 64]) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double x = wave_sum_d(*a), y = wave_sum_d(*b);
+  if (lane == 0) {
+    red[0][wv] = x;
+    red[1][wv] = y;
+  }
+  __syncthreads();
+  x = 0.0;
+  y = 0.0;
+#pragma unroll
+  for (int k = 0; k < kChanThreads / 64; ++k) {
+    x += red[0][k];
+    y += red[1][k];
+  }
+  *a = x;
+  *b = y;
+}
+
+template <typename T, bool VEC>
+struct ChanView {
+  // unit j -> element offset from the channel base (x + ch * hw)
+  int64_t chw;
+  uint32_t hwu;  // units per plane
+  __device__ __forceinline__ int64_t off(uint32_t j) const {
+    const uint32_t nn = j / hwu, p = j - nn * hwu;
+    return (int64_t)nn * chw + (VEC ? 4 * (int64_t)p : (int64_t)p);
+  }
+  __device__ __forceinline__ float4 load(const T* base, uint32_t j) const {
+    if constexpr (VEC) return ld4(base + off(j));
+    return make_float4(ld1(base + off(j)), 0.f, 0.f, 0.f);
+  }
+  __device__ __forceinline__ void store(T* base, uint32_t j, float4 v) const {
+    if constexpr (VEC)
+      st4(base + off(j), v);
+    else
+      st1(base + off(j), v.x);
+  }
+};
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(kChanThreads)
+    bn_fwd_chan_kernel(const T* __restrict__ x, const T* __restrict__ r, T* __restrict__ y,
+                       int64_t c, int64_t n, int64_t hw, int act, FwdArgs A) {
+  __shared__ double red[2][kChanThreads / 64];
+  __shared__ float cf[2];
+  const int64_t ch = blockIdx.x;
+  const ChanView<T, VEC> cv{c * hw, (uint32_t)(VEC ? hw >> 2 : hw)};
+  const uint32_t units = (uint32_t)n * cv.hwu;
+  const T* xc = x + ch * hw;
+  const T* rc = r ? r + ch * hw : nullptr;
+  float4 v[kChanUnits], q[kChanUnits];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kChanUnits; ++k) {
+    const uint32_t j = threadIdx.x + k * kChanThreads;
+    const uint32_t jc = j < units ? j : units - 1;  // unconditional loads
+    v[k] = cv.load(xc, jc);
+    q[k] = rc ? cv.load(rc, jc) : z4;
+  }
+  const float ref = ld1(xc);
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kChanUnits; ++k) {
+    if (threadIdx.x + k * kChanThreads < units) {
+      const float a = v[k].x - ref;
+      if constexpr (VEC) {
+        const float b = v[k].y - ref, cc = v[k].z - ref, d = v[k].w - ref;
+        s1 += (a + b) + (cc + d);
+        s2 += (a * a + b * b) + (cc * cc + d * d);
+      } else {
+        s1 += a;
+        s2 += a * a;
+      }
+    }
+  }
+  double d1 = s1, d2 = s2;
+  chan_sum2(&d1, &d2, red);
+  if (threadIdx.x == 0) {
+    const FwdCh kc = fwd_channel(A, x, ch, d1, d2, true);
+    cf[0] = kc.sc;
+    cf[1] = kc.sh;
+  }
+  __syncthreads();
+  const float sc = cf[0], sh = cf[1];
+  T* yc = y + ch * hw;
+#pragma unroll
+  for (int k = 0; k < kChanUnits; ++k) {
+    const uint32_t j = threadIdx.x + k * kChanThreads;
+    if (j < units) cv.store(yc, j, fwd4(v[k], q[k], rc != nullptr, sc, sh, act));
+  }
+}
+
+template <typename T, bool VEC>
+__global__ void __launch_bounds__(kChanThreads)
+    bn_bwd_chan_kernel(const T* __restrict__ gy, const T* __restrict__ x,
+                       const T* __restrict__ r, T* __restrict__ gx, T* __restrict__ gr,
+                       int64_t c, int64_t n, int64_t hw, int act, BwdArgs P) {
+  __shared__ double red[2][kChanThreads / 64];
+  __shared__ float cf[3];
+  const int64_t ch = blockIdx.x;
+  const ChanView<T, VEC> cv{c * hw, (uint32_t)(VEC ? hw >> 2 : hw)};
+  const uint32_t units = (uint32_t)n * cv.hwu;
+  const int64_t cb = ch * hw;
+  float4 g[kChanUnits], v[kChanUnits], q[kChanUnits];
+  const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int k = 0; k < kChanUnits; ++k) {
+    const uint32_t j = threadIdx.x + k * kChanThreads;
+    const uint32_t jc = j < units ? j : units - 1;
+    g[k] = cv.load(gy + cb, jc);
+    v[k] = cv.load(x + cb, jc);
+    q[k] = r ? cv.load(r + cb, jc) : z4;
+  }
+  const float is = P.invstd[ch];
+  const float sc = P.gamma[ch] * is, mu = P.mean[ch];
+  const float sh = P.beta[ch] - mu * sc;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < kChanUnits; ++k) {
+    // g[k] becomes dy' in place
+    g[k].x = dy_eff(g[k].x, v[k].x, q[k].x, sc, sh, act);
+    if constexpr (VEC) {
+      g[k].y = dy_eff(g[k].y, v[k].y, q[k].y, sc, sh, act);
+      g[k].z = dy_eff(g[k].z, v[k].z, q[k].z, sc, sh, act);
+      g[k].w = dy_eff(g[k].w, v[k].w, q[k].w, sc, sh, act);
+    }
+    if (threadIdx.x + k * kChanThreads < units) {
+      if constexpr (VEC) {
+        s1 += (g[k].x + g[k].y) + (g[k].z + g[k].w);
+        s2 += (g[k].x * (v[k].x - mu) + g[k].y * (v[k].y - mu)) +
+              (g[k].z * (v[k].z - mu) + g[k].w * (v[k].w - mu));
+      } else {
+        s1 += g[k].x;
+        s2 += g[k].x * (v[k].x - mu);
+      }
+    }
+  }
+  double d1 = s1, d2 = s2;
+  chan_sum2(&d1, &d2, red);
+  if (threadIdx.x == 0) {
+    const BwdCh kc = bwd_channel(P, ch, d1, d2, true);
+    cf[0] = kc.A;
+    cf[1] = kc.B;
+    cf[2] = kc.D;
+  }
+  __syncthreads();
+  const float A = cf[0], B = cf[1], D = cf[2];
+#pragma unroll
+  for (int k = 0; k < kChanUnits; ++k) {
+    const uint32_t j = threadIdx.x + k * kChanThreads;
+    if (j < units) {
+      const float4 e = g[k], xv = v[k];
+      cv.store(gx + cb, j, make_float4(A * e.x + B * xv.x + D, A * e.y + B * xv.y + D,
+                                       A * e.z + B * xv.z + D, A * e.w + B * xv.w + D));
+      if (gr) cv.store(gr + cb, j, e);
+    }
+  }
+}
+
 inline int stream_grid(int64_t work) {
   const int64_t b = mde::cdiv(work, 256);
   return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
@@ -735,6 +918,16 @@ int launch_fwd_apply(const T* x, const T* r, T* y, int64_t n, int64_t c, int64_t
 template <typename T>
 int fwd_train(const void* x, const void* residual, void* y, int64_t n, int64_t c, int64_t hw,
               int act, const Geo& g, const FwdArgs& A, hipStream_t s) {
+  if (chan_mode(n, hw)) {
+    const double bytes = (double)sizeof(T) * n * c * (double)hw * (residual ? 3.0 : 2.0);
+    if (hw % 4 == 0)
+      MDE_LAUNCH(mde::K_BN_APPLY_SMALL, bytes, s, (bn_fwd_chan_kernel<T, true>), dim3((unsigned)c),
+                 dim3(kChanThreads), 0, (const T*)x, (const T*)residual, (T*)y, c, n, hw, act, A);
+    else
+      MDE_LAUNCH(mde::K_BN_APPLY_SMALL, bytes, s, (bn_fwd_chan_kernel<T, false>), dim3((unsigned)c),
+                 dim3(kChanThreads), 0, (const T*)x, (const T*)residual, (T*)y, c, n, hw, act, A);
+    return MDE_OK;
+  }
   const int st = launch_stats((const T*)x, n, c, hw, g, (float*)A.part, s);
   if (st) return st;
   return launch_fwd_apply((const T*)x, (const T*)residual, (T*)y, n, c, hw, act, A, s);
@@ -768,6 +961,18 @@ int bwd(const void* gy, const void* x, const void* residual, void* gx, void* gre
   const T* rr = act ? (const T*)residual : nullptr;
   const double big = (double)sizeof(T) * n * c * (double)hw;
   const double rb = rr ? big : 0.0;
+  if (chan_mode(n, hw)) {
+    const double abytes = 3.0 * big + rb + (gresidual ? big : 0.0);
+    if (hw % 4 == 0)
+      MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, (bn_bwd_chan_kernel<T, true>),
+                 dim3((unsigned)c), dim3(kChanThreads), 0, (const T*)gy, (const T*)x, rr, (T*)gx,
+                 (T*)gresidual, c, n, hw, act, P);
+    else
+      MDE_LAUNCH(mde::K_BN_BWD_APPLY_SMALL, abytes, s, (bn_bwd_chan_kernel<T, false>),
+                 dim3((unsigned)c), dim3(kChanThreads), 0, (const T*)gy, (const T*)x, rr, (T*)gx,
+                 (T*)gresidual, c, n, hw, act, P);
+    return MDE_OK;
+  }
   if (hw % 4 == 0) {
     MDE_LAUNCH(mde::K_BN_BWD_REDUCE, 2.0 * big + rb, s, (bn_bwd_reduce_kernel<T, true>),
                dim3(g.slices, (unsigned)c), dim3(256), 0, (const T*)gy, (const T*)x, rr, gamma,

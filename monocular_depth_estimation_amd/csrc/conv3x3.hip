@@ -613,16 +613,105 @@ __global__ void __launch_bounds__(64 * kRedWaves)
   if (o >= 0) gw[o] = sum;
 }
 
+// float4 variant (m % 4 == 0): block (x, grp, z) sums rows [z R, z R + R) of
+// 256 columns, 8 waves on interleaved row subsets (four float4 accumulators a
+// lane: 64 bytes in flight per lane), wave 0 adds the 8 subset sums in order.
+// FINAL: scatter to gw; else the slice sum overwrites the slice's first row
+// (only this block reads those rows of these columns), and a second launch
+// sums the S slice rows (stride R m).  Slices keep >= ~512 blocks in flight
+// when the partial rows are many and the columns few (the 16 -> 16 kernel's
+// 1024 rows of 2304 columns: 9 column blocks alone), where one block per
+// column range serialised hundreds of loads per lane.
+constexpr int kRed4Waves = 8;
+
+template <bool FINAL>
+__global__ void __launch_bounds__(64 * kRed4Waves)
+    wgrad_reduce4_kernel(float* __restrict__ part, float* __restrict__ gw, int rows, int m,
+                         int64_t rstride, int64_t gstride, int slice, ReduceMap map) {
+  __shared__ float4 red[kRed4Waves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e4 = blockIdx.x * 64 + lane, grp = blockIdx.y;
+  const int m4 = m >> 2;
+  const int b0 = blockIdx.z * slice, b1 = b0 + slice < rows ? b0 + slice : rows;
+  const int64_t rs4 = rstride >> 2;
+  float4* pg = reinterpret_cast<float4*>(part + (int64_t)grp * gstride) + e4;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0, a2 = a0, a3 = a0;
+  if (e4 < m4) {
+    int b = b0 + wv;
+    for (; b + 3 * kRed4Waves < b1; b += 4 * kRed4Waves) {
+      const float4 v0 = pg[(int64_t)b * rs4], v1 = pg[(int64_t)(b + kRed4Waves) * rs4];
+      const float4 v2 = pg[(int64_t)(b + 2 * kRed4Waves) * rs4];
+      const float4 v3 = pg[(int64_t)(b + 3 * kRed4Waves) * rs4];
+      a0 = a0 + v0;
+      a1 = a1 + v1;
+      a2 = a2 + v2;
+      a3 = a3 + v3;
+    }
+    for (; b < b1; b += kRed4Waves) a0 = a0 + pg[(int64_t)b * rs4];
+  }
+  red[wv][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (wv != 0 || e4 >= m4) return;
+  float4 sum = red[0][lane];
+#pragma unroll
+  for (int k = 1; k < kRed4Waves; ++k) sum = sum + red[k][lane];
+  if constexpr (FINAL) {
+    const float v[4] = {sum.x, sum.y, sum.z, sum.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t o = gw_index(map, grp, 4 * e4 + j);
+      if (o >= 0) gw[o] = v[j];
+    }
+  } else {
+    pg[(int64_t)b0 * rs4] = sum;
+  }
+}
+
 // Weight-gradient workspace: the partials, [groups][g][m].
 inline size_t wgrad_ws_bytes(int groups, int g, int m) {
   return sizeof(float) * (size_t)groups * (size_t)g * (size_t)m;
 }
 
+// Slices for the float4 reduction: enough (x, grp, z) blocks to fill the chip,
+// >= 16 rows a slice (MDE_WRED_SLICES=1: one launch always, A/B).
+inline int reduce_slices(int groups, int g, int m) {
+  static const int force = [] {
+    const char* e = std::getenv("MDE_WRED_SLICES");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (force > 0) return force < g ? force : g;
+  const int blocks = (int)mde::cdiv(m, 256) * groups;
+  int sl = (int)mde::cdiv(512, blocks);
+  const int cap = g / 16 > 1 ? g / 16 : 1;
+  return sl < 1 ? 1 : (sl > cap ? cap : sl);
+}
+
 inline int launch_reduce(const float* part, float* gw, int groups, int g, int m,
                          const ReduceMap& map, hipStream_t s) {
-  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)g * m + 4.0 * groups * m, s,
-             wgrad_reduce_kernel, dim3((unsigned)mde::cdiv(m, 64), groups),
-             dim3(64 * kRedWaves), 0, part, gw, g, m, map);
+  if (m % 4) {
+    MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)g * m + 4.0 * groups * m, s,
+               wgrad_reduce_kernel, dim3((unsigned)mde::cdiv(m, 64), groups),
+               dim3(64 * kRedWaves), 0, part, gw, g, m, map);
+    return MDE_OK;
+  }
+  float* pw = const_cast<float*>(part);  // slice sums are written over consumed partial rows
+  const int sl = reduce_slices(groups, g, m);
+  const unsigned cx = (unsigned)mde::cdiv(m, 256);
+  const int64_t gs = (int64_t)g * m;
+  if (sl <= 1) {
+    MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)g * m + 4.0 * groups * m, s,
+               wgrad_reduce4_kernel<true>, dim3(cx, groups, 1), dim3(64 * kRed4Waves), 0, pw, gw,
+               g, m, (int64_t)m, gs, g, map);
+    return MDE_OK;
+  }
+  const int rows = (int)mde::cdiv(g, sl);  // rows a slice
+  const int ns = (int)mde::cdiv(g, rows);  // slices actually used
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)(g + ns) * m, s,
+             wgrad_reduce4_kernel<false>, dim3(cx, groups, ns), dim3(64 * kRed4Waves), 0, pw, gw,
+             g, m, (int64_t)m, gs, rows, map);
+  MDE_LAUNCH(mde::K_C3_WREDUCE, 4.0 * groups * (double)ns * m + 4.0 * groups * m, s,
+             wgrad_reduce4_kernel<true>, dim3(cx, groups, 1), dim3(64 * kRed4Waves), 0, pw, gw,
+             ns, m, (int64_t)rows * m, gs, ns, map);
   return MDE_OK;
 }
 

@@ -104,13 +104,19 @@ struct Band {
 };
 
 // ------------------------------------------------------------------ forward
-template <int BM, int BQ, int MT, int QT, int R, int NJ>
+// TW = 0: a tile is BQ consecutive pixels of the flattened output plane and
+// the band spans full input rows.  TW > 0: a tile is TH = BQ / TW output rows
+// x TW output columns (2D), and the band is 2 TH + 1 input rows x 2 TW + 1
+// columns -- far less staging for wide planes (the stem's 240x320 output).
+// CI3: the stem's 3 input channels (one chunk, channel 3 of it zero).
+template <int BM, int BQ, int MT, int QT, int R, int NJ, int TW = 0, bool CI3 = false>
 __global__ void __launch_bounds__(256)
     c3s2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                     float* __restrict__ y, int ci_n, int co_n, int hi, int wi, int ho, int wo,
                     int xw, int ps, int qtiles, int mtiles, int total) {
   constexpr int WQ = BQ / (32 * QT), WM = BM / (32 * MT);
   static_assert(WQ * WM == 4, "four waves per block");
+  static_assert(TW == 0 || BQ % TW == 0, "2D tiles: whole rows of TW");
   constexpr int AV = (BM * KCH / 4 + 255) / 256;  // float4 of weights per thread and chunk
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* sX = smem;                 // [CIC][ps]
@@ -125,19 +131,39 @@ __global__ void __launch_bounds__(256)
   const int tid = threadIdx.x, lane = tid & 63, li = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv / WQ, wq = wv % WQ;
-  const int r_first = q0 / wo;
-  const int row0 = 2 * r_first - 1;
+  // tile origin (output row r_first, column c_first) and the band origin
+  int r_first, c_first;
+  if constexpr (TW > 0) {
+    const int tcols = (wo + TW - 1) / TW;
+    r_first = (qt / tcols) * (BQ / TW);
+    c_first = (qt % tcols) * TW;
+  } else {
+    r_first = q0 / wo;
+    c_first = 0;
+  }
+  const int row0 = 2 * r_first - 1, col0 = 2 * c_first - 1;
   const int64_t hwi = (int64_t)hi * wi;
   const float* xb = x + (int64_t)img * ci_n * hwi;
 
-  // per-lane operand offsets: B (band) base per pixel tile, K offsets per step
-  int bbase[QT];
+  // this lane's output pixels (row, column; -1 = none) per pixel tile, and
+  // the band offset of their tap (0, 0)
+  int prow[QT], pcol[QT], bbase[QT];
 #pragma unroll
   for (int y2 = 0; y2 < QT; ++y2) {
-    int q = q0 + wq * 32 * QT + 32 * y2 + li;
-    q = q < Q ? q : Q - 1;
-    const int rq = q / wo, cq = q - rq * wo;
-    bbase[y2] = 2 * (rq - r_first) * xw + 2 * cq;
+    const int i = wq * 32 * QT + 32 * y2 + li;  // pixel index within the tile
+    int rq, cq;
+    if constexpr (TW > 0) {
+      rq = r_first + i / TW;
+      cq = c_first + i % TW;
+    } else {
+      const int q = q0 + i < Q ? q0 + i : Q - 1;
+      rq = q / wo;
+      cq = q - rq * wo;
+    }
+    const bool ok = rq < ho && cq < wo && (TW > 0 || q0 + i < Q);
+    prow[y2] = ok ? rq : -1;
+    pcol[y2] = cq;
+    bbase[y2] = 2 * ((ok ? rq : r_first) - r_first) * xw + 2 * ((ok ? cq : c_first) - c_first);
   }
   int koff[KCH / 2];
 #pragma unroll
@@ -149,14 +175,28 @@ __global__ void __launch_bounds__(256)
   Band<R, NJ> band;
   float4 ra[AV];
   auto load = [&](int ci0) {
-    band.load(xb + (int64_t)(ci0 + wv) * hwi, hi, wi, row0, -1, xw, lane);
+    const bool cin_ok = !CI3 || ci0 + wv < ci_n;
+    band.load(xb + (int64_t)(cin_ok ? ci0 + wv : 0) * hwi, hi, wi, row0, col0, xw, lane);
+    if (!cin_ok) band.mrow = 0;
 #pragma unroll
     for (int i = 0; i < AV; ++i) {
       const int e = tid + 256 * i;  // float4 index over [BM][9 float4]
       const int m = e / 9, f = e - m * 9;
       const bool ok = e < BM * 9;
-      const float* src = wt + ((int64_t)(m0 + (ok ? m : 0)) * ci_n + ci0) * 9 + 4 * f;
-      ra[i] = *reinterpret_cast<const float4*>(src);
+      if constexpr (CI3) {  // 27 floats per output channel: scalar, masked
+        float v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int idx = 4 * f + j, c = idx / 9;
+          const bool vok = ok && ci0 + c < ci_n;
+          const float t = wt[vok ? ((int64_t)(m0 + m) * ci_n + ci0 + c) * 9 + idx % 9 : 0];
+          v[j] = vok ? t : 0.f;
+        }
+        ra[i] = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        const float* src = wt + ((int64_t)(m0 + (ok ? m : 0)) * ci_n + ci0) * 9 + 4 * f;
+        ra[i] = *reinterpret_cast<const float4*>(src);
+      }
     }
   };
   auto store = [&]() {
@@ -203,8 +243,8 @@ __global__ void __launch_bounds__(256)
   float* yb = y + (int64_t)img * co_n * Q;
 #pragma unroll
   for (int j = 0; j < QT; ++j) {
-    const int q = q0 + wq * 32 * QT + 32 * j + li;
-    if (q >= Q) continue;
+    if (prow[j] < 0) continue;
+    const int q = prow[j] * wo + pcol[j];
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -477,18 +517,29 @@ struct S2Geo {
 
 inline int odd_up(int v) { return v | 1; }
 
-// forward: BM (output channels) x BQ (pixels) per block
-inline bool fwd_geo(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi, S2Geo* g) {
+// forward: BM (output channels) x BQ (pixels) per block.  Output planes at
+// least 128 wide (wo % 32 == 0) take 2D tiles of 4 rows x 32 columns (tw = 32):
+// a band of 9 x 65 input elements per channel instead of 5 full rows.
+inline bool fwd_geo(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi, S2Geo* g,
+                    int* tw) {
   const int64_t ho = (hi - 1) / 2 + 1, wo = (wi - 1) / 2 + 1, Q = ho * wo;
   g->bm = co % 64 == 0 ? 64 : 32;
   if (co % g->bm) return false;
   g->bq = (Q >= 1024 || g->bm == 32) ? 128 : 64;
-  const int rows = rows_span(g->bq, wo, ho);
-  g->r = 2 * rows + 1;
-  g->xw = odd_up((int)wi + 2);
+  *tw = (wo >= 128 && wo % 32 == 0 && g->bq == 128) ? 32 : 0;
+  if (*tw) {
+    const int th = g->bq / *tw;
+    g->r = 2 * th + 1;
+    g->xw = 2 * *tw + 1;
+    g->qtiles = (int)(mde::cdiv(ho, th) * (wo / *tw));
+  } else {
+    const int rows = rows_span(g->bq, wo, ho);
+    g->r = 2 * rows + 1;
+    g->xw = odd_up((int)wi + 2);
+    g->qtiles = (int)mde::cdiv(Q, g->bq);
+  }
   g->nj = (g->xw + 63) / 64;
   g->ps = odd_up(g->r * g->xw);
-  g->qtiles = (int)mde::cdiv(Q, g->bq);
   g->mtiles = (int)(co / g->bm);
   g->total = n * g->qtiles * g->mtiles;
   return g->total < 0x7fffffff;
@@ -538,18 +589,23 @@ inline bool s1_geo(int64_t n, int64_t m_ch, int64_t h, int64_t w, S2Geo* g) {
 inline int pitch32(int v) { return (v + 31) / 64 * 64 + 32; }  // >= v, = 32 (mod 64)
 
 inline bool s2_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t hi, int64_t wi) {
-  return n > 0 && ci >= 32 && co >= 32 && ci % 32 == 0 && co % 32 == 0 && hi >= 2 && wi >= 2 &&
-         wi % 2 == 0 && n * ci * hi * wi < ((int64_t)1 << 31) && n * co * hi * wi < ((int64_t)1 << 31);
+  return n > 0 && (ci == 3 || (ci >= 32 && ci % 32 == 0)) && co >= 32 && co % 32 == 0 &&
+         hi >= 2 && wi >= 2 && wi % 2 == 0 && n * ci * hi * wi < ((int64_t)1 << 31) &&
+         n * co * hi * wi < ((int64_t)1 << 31);
 }
 
 // The (R, NJ) instantiations: the DDRNet planes (wi 320 / 160 / 80 / 40 / 20)
 // plus the generic fallbacks below them.
-#define MDE_S2_FWD_GEOS(X) \
-  X(32, 128, 1, 1, 5, 6)   \
-  X(64, 128, 2, 1, 7, 3)   \
-  X(64, 128, 2, 1, 11, 2)  \
-  X(64, 64, 1, 1, 11, 1)   \
-  X(64, 64, 1, 1, 17, 1)
+// (BM, BQ, MT, QT, R, NJ, TW, CI3)
+#define MDE_S2_FWD_GEOS(X)              \
+  X(32, 128, 1, 1, 5, 6, 0, false)      \
+  X(64, 128, 2, 1, 7, 3, 0, false)      \
+  X(64, 128, 2, 1, 11, 2, 0, false)     \
+  X(64, 64, 1, 1, 11, 1, 0, false)      \
+  X(64, 64, 1, 1, 17, 1, 0, false)      \
+  X(32, 128, 1, 1, 9, 2, 32, false)     \
+  X(64, 128, 2, 1, 9, 2, 32, false)     \
+  X(32, 128, 1, 1, 9, 2, 32, true)
 #define MDE_S2_DGRAD_GEOS(X) \
   X(32, 128, 3, 3)           \
   X(64, 64, 3, 3)            \
@@ -669,11 +725,13 @@ int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int
 // queries send those to MIOpen.
 int mde_conv3x3s2_fwd_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype) {
   S2Geo g;
-  if (dtype != MDE_F32 || !s2_shape_ok(1, cin, cout, h, w) || !fwd_geo(1, cin, cout, h, w, &g))
+  int tw = 0;
+  if (dtype != MDE_F32 || !s2_shape_ok(1, cin, cout, h, w) || !fwd_geo(1, cin, cout, h, w, &g, &tw))
     return 0;
   if (((h - 1) / 2 + 1) * ((w - 1) / 2 + 1) < 256) return 0;
-#define MDE_MATCH(BM, BQ, MT, QT, R, NJ) \
-  if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) return 1;
+  const bool ci3 = cin == 3;
+#define MDE_MATCH(BM, BQ, MT, QT, R, NJ, TW, C3) \
+  if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ && tw == TW && ci3 == C3) return 1;
   MDE_S2_FWD_GEOS(MDE_MATCH)
 #undef MDE_MATCH
   return 0;
@@ -696,21 +754,23 @@ int mde_conv3x3s2_fwd(const void* x, const float* weight, void* y, int64_t n, in
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y) return MDE_ERR_INVALID_ARG;
   S2Geo g;
-  if (!s2_shape_ok(n, cin, cout, h, w) || !fwd_geo(n, cin, cout, h, w, &g))
+  int tw = 0;
+  if (!s2_shape_ok(n, cin, cout, h, w) || !fwd_geo(n, cin, cout, h, w, &g, &tw))
     return MDE_ERR_UNSUPPORTED;
+  const bool ci3 = cin == 3;
   hipStream_t s = (hipStream_t)stream;
   const int64_t ho = (h - 1) / 2 + 1, wo = (w - 1) / 2 + 1;
   const double flops = 2.0 * 9 * n * ho * wo * (double)cin * cout;
   const double bytes = 4.0 * n * ((double)cin * h * w + (double)cout * ho * wo);
   const dim3 grid(xcd_grid(g.total)), block(256);
-#define MDE_GO(BM, BQ, MT, QT, R, NJ)                                                             \
-  if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ) {                                     \
+#define MDE_GO(BM, BQ, MT, QT, R, NJ, TW, C3)                                                     \
+  if (g.bm == BM && g.bq == BQ && g.r <= R && g.nj == NJ && tw == TW && ci3 == C3) {            \
     const int ps = odd_up(R * g.xw); /* the template's R rows per staged plane */                \
     const size_t smem = sizeof(float) * ((size_t)CIC * ps + 4 + (size_t)BM * AP);                 \
-    MDE_LAUNCH_MFMA(mde::K_C3S2_FWD, bytes, flops, s, (c3s2_fwd_kernel<BM, BQ, MT, QT, R, NJ>),   \
-                    grid, block, smem, (const float*)x, weight, (float*)y, (int)cin, (int)cout,   \
-                    (int)h, (int)w, (int)ho, (int)wo, g.xw, ps, g.qtiles, g.mtiles,               \
-                    (int)g.total);                                                                \
+    MDE_LAUNCH_MFMA(mde::K_C3S2_FWD, bytes, flops, s,                                             \
+                    (c3s2_fwd_kernel<BM, BQ, MT, QT, R, NJ, TW, C3>), grid, block, smem,          \
+                    (const float*)x, weight, (float*)y, (int)cin, (int)cout, (int)h, (int)w,      \
+                    (int)ho, (int)wo, g.xw, ps, g.qtiles, g.mtiles, (int)g.total);                \
     return MDE_OK;                                                                                \
   }
   MDE_S2_FWD_GEOS(MDE_GO)

@@ -231,32 +231,15 @@ __global__ void __launch_bounds__(1024)
   if (lane == 0) dh[(int64_t)nidx * cr + j] = hidden[(int64_t)nidx * cr + j] > 0.f ? acc : 0.f;
 }
 
-__global__ void __launch_bounds__(1024)
-    se_bfc3_kernel(int c, int cr, const float* __restrict__ w1,
-                   const float* __restrict__ dh, float* __restrict__ dm) {
-  extern __shared__ float hh[];  // [cr]
-  const int nidx = blockIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int j = threadIdx.x; j < cr; j += blockDim.x) hh[j] = dh[(int64_t)nidx * cr + j];
-  __syncthreads();
-  const int ch = blockIdx.y * kOutPerBlock + wid;
-  if (ch >= c) return;
-  float acc = 0.f;
-  for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * hh[j];
-  acc = mde::wave_sum(acc);
-  if (lane == 0) dm[(int64_t)nidx * c + ch] = acc;
-}
-
 // gw2[ch, j] = sum_n dz[n,ch] h[n,j];  gw1[j, ch] = sum_n dh[n,j] m[n,ch];
 // gb2[ch] = sum_n dz[n,ch];  gb1[j] = sum_n dh[n,j]  (bias gradients nullable)
-__global__ void __launch_bounds__(256)
-    se_wgrad_kernel(int n, int c, int cr, const float* __restrict__ dz,
-                    const float* __restrict__ dh,
-                    const float* __restrict__ hidden,
-                    const float* __restrict__ mean, float* __restrict__ gw1,
-                    float* __restrict__ gw2, float* __restrict__ gb1,
-                    float* __restrict__ gb2) {
-  const int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+__device__ __forceinline__ void se_wgrad_body(int64_t t, int n, int c, int cr,
+                                              const float* __restrict__ dz,
+                                              const float* __restrict__ dh,
+                                              const float* __restrict__ hidden,
+                                              const float* __restrict__ mean,
+                                              float* __restrict__ gw1, float* __restrict__ gw2,
+                                              float* __restrict__ gb1, float* __restrict__ gb2) {
   const int64_t pairs = (int64_t)c * cr;
   if (gb2 && t < c) {
     float acc = 0.f;
@@ -282,6 +265,35 @@ __global__ void __launch_bounds__(256)
       acc += dh[(int64_t)k * cr + j] * mean[(int64_t)k * c + ch];
     gw1[u] = acc;  // row-major [cr, c]
   }
+}
+
+// dm = W1^T dh (the squeeze-mean gradient) and the FC weight / bias gradients
+// in one launch: blocks [0, n * ny) are se_bfc3 blocks (sample, 16-channel
+// group), the rest grid-stride the se_wgrad pairs (1024 threads each).  Both
+// only read dz / dh, so the roles are independent.  Was two launches.
+__global__ void __launch_bounds__(1024)
+    se_bfc3w_kernel(int n, int ny, int c, int cr, const float* __restrict__ w1,
+                    const float* __restrict__ dz, const float* __restrict__ dh,
+                    const float* __restrict__ hidden, const float* __restrict__ mean,
+                    float* __restrict__ dm, float* __restrict__ gw1, float* __restrict__ gw2,
+                    float* __restrict__ gb1, float* __restrict__ gb2) {
+  extern __shared__ float hh[];  // [cr]
+  const int nb3 = n * ny;
+  if ((int)blockIdx.x >= nb3) {
+    se_wgrad_body((int64_t)(blockIdx.x - nb3) * blockDim.x + threadIdx.x, n, c, cr, dz, dh, hidden,
+                  mean, gw1, gw2, gb1, gb2);
+    return;
+  }
+  const int nidx = blockIdx.x / ny, gy = blockIdx.x % ny;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int j = threadIdx.x; j < cr; j += blockDim.x) hh[j] = dh[(int64_t)nidx * cr + j];
+  __syncthreads();
+  const int ch = gy * kOutPerBlock + wid;
+  if (ch >= c) return;
+  float acc = 0.f;
+  for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * hh[j];
+  acc = mde::wave_sum(acc);
+  if (lane == 0) dm[(int64_t)nidx * c + ch] = acc;
 }
 
 // gx = g * s + dm / hw, written to gxa / gxb (either may be null).
@@ -383,20 +395,49 @@ __global__ void __launch_bounds__(256)
 // partials -> the BN parameter gradients and the apply constants coef[ch] =
 // (R, T) with gy = m (P g + Q) + R + T (y - mean), P = sc s, Q = sc dm / HW
 // (per sample).  Fixed per-thread order and a fixed tree: deterministic.
+// One launch for the SE-over-BN backward's tail (was three: se_bfc3, se_wgrad,
+// the combine): blocks [0, c) are per-channel combine blocks that first form
+// their channel's squeeze-mean gradients dm[:, ch] = W1[:, ch] . dh[n, :]
+// (wave per sample, the se_bfc3 summation order) into LDS and dm; blocks
+// [c, c + wg) run the FC weight / bias gradients.
+constexpr int kMaxSeN = 256;  // samples the combine blocks hold dm for in LDS
+
 __global__ void __launch_bounds__(256)
     sebn_bwd_combine_kernel(const float* __restrict__ part4, int chunks, int64_t n, int64_t c,
-                            int64_t hw, const float* __restrict__ s, const float* __restrict__ dm,
+                            int64_t hw, const float* __restrict__ s, float* __restrict__ dm,
                             const float* __restrict__ scale, const float* __restrict__ invstd,
                             int training, float* __restrict__ ggamma, float* __restrict__ gbeta,
-                            float* __restrict__ coef) {
+                            float* __restrict__ coef, int cr, const float* __restrict__ w1,
+                            const float* __restrict__ dz, const float* __restrict__ dh,
+                            const float* __restrict__ hidden, const float* __restrict__ mean,
+                            float* __restrict__ gw1, float* __restrict__ gw2) {
   __shared__ double red[2][4];
+  __shared__ float dms[kMaxSeN];
+  if ((int64_t)blockIdx.x >= c) {
+    se_wgrad_body((int64_t)(blockIdx.x - c) * blockDim.x + threadIdx.x, (int)n, (int)c, cr, dz, dh,
+                  hidden, mean, gw1, gw2, nullptr, nullptr);
+    return;
+  }
   const int64_t ch = blockIdx.x;
+  {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int64_t nn = wid; nn < n; nn += 4) {
+      float acc = 0.f;
+      for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * dh[nn * cr + j];
+      acc = mde::wave_sum(acc);
+      if (lane == 0) {
+        dms[nn] = acc;
+        dm[nn * c + ch] = acc;
+      }
+    }
+  }
+  __syncthreads();
   const double inv_hw = 1.0 / (double)hw;
   double s1 = 0.0, s2 = 0.0;
   for (int64_t i = threadIdx.x; i < n * chunks; i += 256) {
     const int64_t plane = (i / chunks) * c + ch;
     const float* p = part4 + 4 * (plane * chunks + i % chunks);
-    const double sv = s[plane], q = (double)dm[plane] * inv_hw;
+    const double sv = s[plane], q = (double)dms[i / chunks] * inv_hw;
     s1 += sv * (double)p[0] + q * (double)p[1];
     s2 += sv * (double)p[2] + q * (double)p[3];
   }
@@ -477,7 +518,8 @@ inline int stream_grid(int64_t work) {
 struct SeWs;
 int se_bfc(const SeWs& ws, int chunks, int64_t n, int64_t c, int64_t cr, const float* w1,
            const float* w2, const float* b2, int gate, const float* s, const float* hidden,
-           const float* mean, float* gw1, float* gw2, float* gb1, float* gb2, hipStream_t st);
+           const float* mean, float* gw1, float* gw2, float* gb1, float* gb2, hipStream_t st,
+           bool tail = false);
 
 struct SeWs {
   float* part;
@@ -509,12 +551,15 @@ SeWs se_carve(void* ws, int64_t n, int64_t c, int64_t cr, int64_t hw) {
   return r;
 }
 
-// The per-sample FC backward + weight gradients: four launches.  (A
-// one-block fused variant was measured at 156 us per SE layer vs 42 us for
-// these four: a single block serialises the n*c partial-sum reductions.)
+// The per-sample FC backward + weight gradients: three launches (dz, dh,
+// then dm with the weight gradients), two when `tail` (the SE-over-BN combine
+// launch takes dm and the weight gradients).  (A one-block fused variant was
+// measured at 156 us per SE layer vs 42 us for four launches: a single block
+// serialises the n*c partial-sum reductions.)
 int se_bfc(const SeWs& ws, int chunks, int64_t n, int64_t c, int64_t cr, const float* w1,
            const float* w2, const float* b2, int gate, const float* s, const float* hidden,
-           const float* mean, float* gw1, float* gw2, float* gb1, float* gb2, hipStream_t st) {
+           const float* mean, float* gw1, float* gw2, float* gb1, float* gb2, hipStream_t st,
+           bool tail) {
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + 3.0 * n * c), st, se_bfc1_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
              sizeof(float) * cr, ws.part, chunks, (int)c, (int)cr, w2, b2, gate, s, hidden,
@@ -522,12 +567,13 @@ int se_bfc(const SeWs& ws, int chunks, int64_t n, int64_t c, int64_t cr, const f
   MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + n * (c + 2.0 * cr)), st, se_bfc2_kernel,
              dim3((unsigned)n, (unsigned)mde::cdiv(cr, kOutPerBlock)), dim3(1024),
              sizeof(float) * c, (int)c, (int)cr, w2, hidden, ws.dz, ws.dh);
-  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (c * cr + n * (c + cr)), st, se_bfc3_kernel,
-             dim3((unsigned)n, (unsigned)mde::cdiv(c, kOutPerBlock)), dim3(1024),
-             sizeof(float) * cr, (int)c, (int)cr, w1, ws.dh, ws.dm);
-  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (2.0 * c * cr + 2.0 * n * (c + cr)), st,
-             se_wgrad_kernel, dim3((unsigned)mde::cdiv(2 * c * cr, 256)), dim3(256), 0, (int)n,
-             (int)c, (int)cr, ws.dz, ws.dh, hidden, mean, gw1, gw2, gb1, gb2);
+  if (tail) return MDE_OK;  // the SE-over-BN combine launch does dm and the weight gradients
+  const int ny = (int)mde::cdiv(c, kOutPerBlock);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 4.0 * (3.0 * c * cr + n * (3.0 * c + 3.0 * cr)), st,
+             se_bfc3w_kernel,
+             dim3((unsigned)(n * ny + mde::cdiv(2 * c * cr, 1024))), dim3(1024),
+             sizeof(float) * cr, (int)n, ny, (int)c, (int)cr, w1, ws.dz, ws.dh, hidden, mean,
+             ws.dm, gw1, gw2, gb1, gb2);
   return MDE_OK;
 }
 
@@ -674,12 +720,15 @@ static int se_bn_bwd_t(const void* gout, const void* ya, int64_t ca, const void*
   MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, sebn_bwd_reduce_kernel<T>,
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0, (const T*)gout, (const T*)ya, ca,
              (const T*)yb, cb, hw, chunks, scale, shift, bn_mean, ws.part, ws.part4);
+  if (n > kMaxSeN) return MDE_ERR_INVALID_ARG;
   const int fcs = se_bfc(ws, chunks, n, c, cr, w1, w2, nullptr, 0, s, hidden, mean, gw1, gw2,
-                         nullptr, nullptr, st);
+                         nullptr, nullptr, st, true);
   if (fcs) return fcs;
-  MDE_LAUNCH(mde::K_SE_BWD_FC, 16.0 * n * c * chunks, st, sebn_bwd_combine_kernel,
-             dim3((unsigned)c), dim3(256), 0, ws.part4, chunks, n, c, hw, s,
-             ws.dm, scale, bn_invstd, training, ggamma, gbeta, ws.coef);
+  MDE_LAUNCH(mde::K_SE_BWD_FC, 16.0 * n * c * chunks + 4.0 * (3.0 * c * cr + n * (3.0 * c + 3.0 * cr)),
+             st, sebn_bwd_combine_kernel,
+             dim3((unsigned)(c + mde::cdiv(2 * c * cr, 256))), dim3(256), 0, ws.part4, chunks, n, c,
+             hw, s, ws.dm, scale, bn_invstd, training, ggamma, gbeta, ws.coef, (int)cr, w1, ws.dz,
+             ws.dh, hidden, mean, gw1, gw2);
   MDE_LAUNCH(mde::K_SE_BWD_APPLY, 3.0 * big, st, sebn_bwd_apply_kernel<T>,
              dim3(stream_grid(n * c * hw / 4)), dim3(256), 0, (const T*)gout, (const T*)ya, ca,
              (const T*)yb, cb, hw, n * c, s, ws.dm, 1.f / (float)hw, scale, shift, bn_mean,

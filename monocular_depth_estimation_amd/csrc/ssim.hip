@@ -297,10 +297,199 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Two columns per lane (ssim3_pair_kernel): lane l of a strip holds columns
+// c0 = strip * sw - 2 + 2 l and c0 + 1 (lane 0 and lane sw / 2 + 1 are the
+// 2-column halos), so the arithmetic runs on packed fp32 pairs
+// (v_pk_fma / v_pk_mul / v_pk_add_f32: two outputs per VALU op) and a 3-wide
+// horizontal sum costs two DPP lane shifts per two outputs instead of per
+// one.  Same algebra, same per-output operation order as ssim3_stream_kernel
+// except the horizontal sums' association (prev + a0) + a1 / (a0 + a1) + next.
+using f2 = __attribute__((ext_vector_type(2))) float;
+
+__device__ __forceinline__ f2 pk(float a, float b) { return f2{a, b}; }
+
+template <bool GT>
+__global__ void __launch_bounds__(256)
+    ssim3_pair_kernel(const float* __restrict__ xp, const float* __restrict__ yp,
+                      const float* __restrict__ mm, int h, int w, int sw, int strips, int chunks,
+                      int chunk_rows, int64_t nwaves, float gs_ssim, float gs_l1,
+                      float* __restrict__ part, float* __restrict__ gx, float* __restrict__ gy) {
+  __shared__ float red[4];
+  constexpr int NC = GT ? 5 : 3;
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  float lsum = 0.f, l1sum = 0.f;
+  if (wid < nwaves) {  // wave-uniform
+    const int strip = (int)(wid % strips);
+    const int64_t rest = wid / strips;
+    const int chunk = (int)(rest % chunks);
+    const int64_t img = rest / chunks;
+    const int c0 = strip * sw - 2 + 2 * lane, c1 = c0 + 1;
+    const bool in0 = c0 >= 0 && c0 < w, in1 = c1 >= 0 && c1 < w;
+    const int lim = strip * sw + sw;  // this strip's output columns: [strip sw, lim)
+    const bool out0 = in0 && c0 >= strip * sw && c0 < lim;
+    const bool out1 = in1 && c1 >= strip * sw && c1 < lim;
+    // coefficient-sum weights: column 1 takes centre 0 twice, column w-2 centre w-1
+    const f2 wl = pk(c0 == 1 ? 2.f : 1.f, c1 == 1 ? 2.f : 1.f);
+    const f2 wr = pk(c0 == w - 2 ? 2.f : 1.f, c1 == w - 2 ? 2.f : 1.f);
+    const int64_t base = img * h * w;
+    const int o0 = reflect1(c0, w), o1 = reflect1(c1, w);
+    const float* X = xp + base;
+    const float* Y = yp + base;
+    float tmn = 0.f, tden = 1.f;
+    const bool norm = mm != nullptr;
+    if (norm) {
+      tmn = mm[0];
+      tden = mm[1] - mm[0];
+    }
+    const int g0 = chunk * chunk_rows, g1 = min(h, g0 + chunk_rows);
+    const int rs = g0 - 2, re = g1 + 1;
+    const float inv9 = 1.f / 9.f, k = gs_ssim * -0.5f;
+    f2 hs[3][5], cs[3][NC], xr[3], yr[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      xr[i] = yr[i] = pk(0.f, 0.f);
+#pragma unroll
+      for (int f = 0; f < 5; ++f) hs[i][f] = pk(0.f, 0.f);
+#pragma unroll
+      for (int f = 0; f < NC; ++f) cs[i][f] = pk(0.f, 0.f);
+    }
+    auto load = [&](int r, f2& xv, f2& yv) {
+      const int64_t off = (int64_t)reflect1(r, h) * w;
+      xv = pk(X[off + o0], X[off + o1]);
+      const float t0 = Y[off + o0], t1 = Y[off + o1];
+      yv = norm ? pk((t0 - tmn) / tden, (t1 - tmn) / tden) : pk(t0, t1);
+    };
+    // 3-wide horizontal sums of a column pair: (prev lane's c1) + c0 + c1, c0 + c1 + (next's c0)
+    auto hsum = [&](f2 v, f2 wa, f2 wb) {
+      const float p = lane_prev(v.y), n = lane_next(v.x);
+      return f2{wa.x * p + v.x + wb.x * v.y, wa.y * v.x + v.y + wb.y * n};
+    };
+    const f2 one2 = pk(1.f, 1.f);
+    auto step = [&](f2 xv, f2 yv, int r) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        xr[i] = xr[i + 1];
+        yr[i] = yr[i + 1];
+#pragma unroll
+        for (int f = 0; f < 5; ++f) hs[i][f] = hs[i + 1][f];
+      }
+      xr[2] = xv;
+      yr[2] = yv;
+      {
+        const f2 v[5] = {xv, yv, xv * xv, yv * yv, xv * yv};
+#pragma unroll
+        for (int f = 0; f < 5; ++f) hs[2][f] = hsum(v[f], one2, one2);
+      }
+      if (r < g0) return;  // wave-uniform
+      const int p = r - 1;
+      const bool prow = p >= 0 && p < h;
+      const bool v0 = in0 && prow, v1 = in1 && prow;
+      f2 st[5];
+#pragma unroll
+      for (int f = 0; f < 5; ++f) st[f] = (hs[0][f] + hs[1][f] + hs[2][f]) * inv9;
+      const f2 mx = st[0], my = st[1];
+      const f2 sxx = st[2] - mx * mx, syy = st[3] - my * my;
+      const f2 sxy = st[4] - mx * my;
+      const f2 n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
+      const f2 d1 = mx * mx + my * my + kC1, d2 = sxx + syy + kC2;
+      const f2 D = d1 * d2;
+      const f2 nn = n1 * n2;
+      const f2 S = pk(nn.x / D.x, nn.y / D.y);  // exact division: S(x, x) = 1
+      const f2 fl = (one2 - S) * 0.5f;
+      if (p < g1 && p >= g0) {
+        if (out0) lsum += fminf(fmaxf(fl.x, 0.f), 1.f);
+        if (out1) lsum += fminf(fmaxf(fl.y, 0.f), 1.f);
+      }
+      const bool a0 = v0 && fl.x >= 0.f && fl.x <= 1.f, a1 = v1 && fl.y >= 0.f && fl.y <= 1.f;
+      const f2 rD = pk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y));
+      const f2 rd1 = pk(__builtin_amdgcn_rcpf(d1.x), __builtin_amdgcn_rcpf(d1.y));
+      const f2 rd2 = pk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y));
+      const f2 dS_dsx = -S * rd2;
+      const f2 dS_dsxy = 2.f * n1 * rD;
+      const f2 dS_dmx = 2.f * my * n2 * rD - S * 2.f * mx * rd1;
+      f2 c[NC];
+      c[0] = k * (dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy);
+      c[1] = k * dS_dsx;
+      c[2] = k * dS_dsxy;
+      if constexpr (GT) {
+        const f2 dS_dmy = 2.f * mx * n2 * rD - S * 2.f * my * rd1;
+        c[3] = k * (dS_dmy - 2.f * my * dS_dsx - mx * dS_dsxy);
+        c[NC - 1] = c[1];
+      }
+#pragma unroll
+      for (int f = 0; f < NC; ++f) c[f] = pk(a0 ? c[f].x : 0.f, a1 ? c[f].y : 0.f);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int f = 0; f < NC; ++f) cs[i][f] = cs[i + 1][f];
+#pragma unroll
+      for (int f = 0; f < NC; ++f) cs[2][f] = hsum(c[f], wl, wr);
+      const int g = p - 1;
+      if (g < g0 || g >= g1) return;  // wave-uniform
+      const float vt = g == 1 ? 2.f : 1.f, vb = g == h - 2 ? 2.f : 1.f;
+      f2 sm[NC];
+#pragma unroll
+      for (int f = 0; f < NC; ++f) sm[f] = (vt * cs[0][f] + cs[1][f]) + vb * cs[2][f];
+      const f2 x0 = xr[0], y0 = yr[0];
+      const f2 diff = x0 - y0;
+      const f2 sgn = pk(diff.x > 0.f ? 1.f : (diff.x < 0.f ? -1.f : 0.f),
+                        diff.y > 0.f ? 1.f : (diff.y < 0.f ? -1.f : 0.f));
+      if (out0) l1sum += fabsf(diff.x);
+      if (out1) l1sum += fabsf(diff.y);
+      const int64_t off = base + (int64_t)g * w + c0;
+      if (gx) {
+        const f2 v = (sm[0] + 2.f * x0 * sm[1] + y0 * sm[2]) * inv9 + gs_l1 * sgn;
+        if (out0) gx[off] = v.x;
+        if (out1) gx[off + 1] = v.y;
+      }
+      if constexpr (GT) {
+        if (gy) {
+          const f2 v = (sm[3] + 2.f * y0 * sm[NC - 1] + x0 * sm[2]) * inv9 - gs_l1 * sgn;
+          if (out0) gy[off] = v.x;
+          if (out1) gy[off + 1] = v.y;
+        }
+      }
+    };
+    f2 cx[4], cy[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) load(rs + i, cx[i], cy[i]);
+    for (int r = rs; r <= re; r += 4) {
+      f2 nx[4], ny[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) load(min(r + 4 + i, re), nx[i], ny[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r + i <= re) step(cx[i], cy[i], r + i);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        cx[i] = nx[i];
+        cy[i] = ny[i];
+      }
+    }
+  }
+  const float ts = mde::block_sum256(lsum, red);
+  const float tl = mde::block_sum256(l1sum, red);
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = ts;
+    part[2 * blockIdx.x + 1] = tl;
+  }
+}
+
 struct StreamPlan {
   int strips, chunks, chunk_rows, strip_major;
   int64_t nwaves, nblocks;
+  int pair_sw;  // > 0: ssim3_pair_kernel with strips of pair_sw output columns
 };
+
+// MDE_SSIM_PAIR=0: the one-column-per-lane kernel (A/B)
+inline bool ssim_pair() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_SSIM_PAIR");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 // ~5.5 waves per SIMD (5632) from strips x chunks, chunks of >= 16 rows: at
 // 32x480x640, 30-row chunks (4 halo rows each).  The kernel is instruction-
@@ -309,12 +498,21 @@ struct StreamPlan {
 // overrun, 1.59x with the overrun clamped).
 inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w) {
   StreamPlan p;
-  p.strips = (int)mde::cdiv(w, kSW);
+  p.pair_sw = 0;
+  if (ssim_pair()) {  // strips of <= 124 columns (62 lane pairs + 2 halo lanes), even widths
+    p.strips = (int)mde::cdiv(w, 124);
+    p.pair_sw = (int)(mde::cdiv(mde::cdiv(w, p.strips), 2) * 2);
+  } else {
+    p.strips = (int)mde::cdiv(w, kSW);
+  }
   const int64_t per_chunk = b * p.strips;
-  static const int64_t target = [] {  // MDE_SSIM_WAVES: tuning sweeps only
+  static const int64_t target_env = [] {  // MDE_SSIM_WAVES: tuning sweeps only
     const char* e = std::getenv("MDE_SSIM_WAVES");
-    return e ? std::atoll(e) : 5632;
+    return e ? std::atoll(e) : 0;
   }();
+  // the pair kernel does twice the work a wave: half the waves, so chunks stay
+  // ~32 rows tall (3 halo rows each) at cfg2
+  const int64_t target = target_env > 0 ? target_env : (p.pair_sw ? 2816 : 5632);
   int64_t ch = mde::cdiv(target, per_chunk);
   const int64_t maxc = mde::cdiv(h, 16);
   if (ch > maxc) ch = maxc;
@@ -413,7 +611,18 @@ int mde_ssim3_l1_fwd(const void* pred, const void* target,
   float* part = (float*)workspace;
   const double bytes =
       4.0 * numel * (2.0 + (grad_pred ? 1.0 : 0.0) + (grad_target ? 1.0 : 0.0));
-  if (grad_target) {
+  if (sp.pair_sw > 0) {
+    if (grad_target)
+      MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_pair_kernel<true>, dim3((unsigned)nblocks),
+                 dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
+                 (int)w, sp.pair_sw, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv,
+                 w_l1 * inv, part, (float*)grad_pred, (float*)grad_target);
+    else
+      MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_pair_kernel<false>, dim3((unsigned)nblocks),
+                 dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
+                 (int)w, sp.pair_sw, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv,
+                 w_l1 * inv, part, (float*)grad_pred, (float*)nullptr);
+  } else if (grad_target) {
     MDE_LAUNCH(mde::K_SSIM3_L1, bytes, s, ssim3_stream_kernel<true>, dim3((unsigned)nblocks),
                dim3(256), 0, (const float*)pred, (const float*)target, target_minmax, (int)h,
                (int)w, sp.strips, sp.chunks, sp.chunk_rows, sp.nwaves, w_ssim * inv, w_l1 * inv,

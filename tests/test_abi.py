@@ -81,9 +81,10 @@ def test_workspace_queries():
     lib = _abi.load()
     # SE: partial slab per (n, c, 16384-element chunk) + three per-sample vectors
     assert lib.mde_se_workspace(32, 16, 16, 480, 640) >= 4 * 32 * 16 * 19
-    # SSIM: one (ssim, l1) pair per block of 4 waves; a wave = 60-column strip
-    # x 30-row chunk (11 strips x 16 chunks per 480x640 image: 5632 waves)
-    assert lib.mde_ssim3_l1_workspace(32, 480, 640) == 4 * 2 * (32 * 11 * 16 // 4)
+    # SSIM: one (ssim, l1) pair per block of 4 waves; a wave = 108-column strip
+    # (two columns a lane) x 32-row chunk (6 strips x 15 chunks per 480x640
+    # image: 2880 waves)
+    assert lib.mde_ssim3_l1_workspace(32, 480, 640) == 4 * 2 * (32 * 6 * 15 // 4)
     assert lib.mde_minmax_workspace(10) >= 8
     assert lib.mde_skip_reduce_workspace(32, 64, 32, 120, 160) >= 4 * (64 * 32 + 32)
     assert lib.mde_depth_loss_workspace(2, 24, 32) >= 4 * 3 * 2 * 24 * 32

@@ -37,8 +37,13 @@ def close_scaled(a, b, tol, what):
     assert err <= tol * scale, f"{what}: {err:.3g} vs {scale:.3g}"
 
 
+# (2, 8, 3, 5) ... (32, 16, 8, 10): the one-block-per-channel kernels for small
+# tensors (n * hw <= 16384, float4 when hw % 4 == 0, else <= 4096); (64, 8, 15, 20)
+# is past that limit (table apply); (4, 16, 30, 40) and up: plane apply
 @pytest.mark.parametrize("shape", [(4, 16, 30, 40), (2, 8, 3, 5), (32, 64, 2, 3), (3, 7, 1, 1),
-                                   (8, 16, 120, 160), (32, 16, 96, 128)])
+                                   (8, 16, 120, 160), (32, 16, 96, 128), (32, 24, 15, 20),
+                                   (32, 16, 8, 10), (16, 8, 16, 60), (64, 8, 15, 20),
+                                   (200, 8, 3, 7)])
 @pytest.mark.parametrize("act,res", [("none", False), ("relu", False), ("relu", True), ("none", True),
                                      ("hardswish", False), ("hardswish", True)])
 def test_batchnorm_train_matches_aten(shape, act, res):

@@ -15,8 +15,11 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 # (cin, cout, h, w) input sizes: DDRNet's stride-2 convs at cfg2 sizes (bs 2),
 # plus odd heights, ragged pixel tiles and a non-DDRNet width
+# (the 240 x 320 / 250 x 256 / 42 x 256 planes take the forward's 2D tiles:
+# output width a multiple of 32 and >= 128; 125 and 21 rows leave partial
+# 4-row tiles)
 SHAPES = [(32, 32, 240, 320), (32, 64, 120, 160), (64, 128, 60, 80), (128, 256, 30, 40),
-          (64, 128, 59, 80), (32, 64, 118, 160)]
+          (64, 128, 59, 80), (32, 64, 118, 160), (32, 32, 250, 256), (64, 64, 42, 256)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -85,6 +88,34 @@ def test_conv3x3s2_hip_kernels_below_the_dispatch_threshold(cin, cout, h, w):
               0, st)
     assert rel_err(y, yr) <= 1e-5, "forward"
     assert rel_err(gx, xr.grad) <= 1e-5, "data gradient"
+
+
+@pytest.mark.parametrize("h,w", [(480, 640), (66, 256)])
+def test_conv3x3s2_stem_3_channels(h, w):
+    """DDRNet's stem conv (3 -> 32, DDRNet_23_slim.py:232) on the image: the HIP
+    forward's 3-channel 2D-tile variant and the stride-2 weight gradient; the
+    image needs no gradient (no data-gradient pass)."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import Conv2d, conv3x3s2_ok
+    n, cin, cout = 2, 3, 32
+    g = torch.Generator().manual_seed(h)
+    x = torch.rand((n, cin, h, w), generator=g)
+    wt = (torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.3
+    gy = torch.rand((n, cout, (h - 1) // 2 + 1, (w - 1) // 2 + 1), generator=g) - 0.5
+    wr = wt.double().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(x.double(), wr, None, 2, 1)
+    yr.backward(gy.double())
+    conv = Conv2d(cin, cout, 3, stride=2, padding=1, bias=False).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(wt)
+    xg = x.to(DEV)
+    assert conv3x3s2_ok(conv, xg)
+    assert _abi.query("mde_conv3x3s2_fwd_supported", cin, cout, h, w, 0) == 1
+    assert _abi.query("mde_conv3x3s2_dgrad_supported", cin, cout, h, w, 0) == 0
+    y = conv(xg)
+    y.backward(gy.to(DEV))
+    assert rel_err(y, yr) <= 1e-5, "forward"
+    assert rel_err(conv.weight.grad, wr.grad) <= 2e-5, "weight gradient"
 
 
 def test_conv3x3s2_full_batch_vs_miopen_deterministic():

@@ -643,6 +643,22 @@ int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int
                               int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype,
                               void* stream);
 
+/* Winograd F(2x2, 3x3) for the same stride-1 convs (wino.hip): 16 GEMMs of
+ * (cout x cin) x (cin x tiles) per 2x2 output tile instead of 36 MACs per
+ * (cout, cin) pair and tile.  mde_wino_weight transforms the forward conv's
+ * [cout][cin][3][3] filter into u (mde_wino_weight_bytes); flip = 1 gives the
+ * data-gradient transform (the conv cout -> cin on gy).  mde_wino_conv runs a
+ * stride-1 / pad-1 conv x[n][cin][h][w] -> y[n][cout][h][w] from such a u
+ * (for the data gradient: x = gy, cin = the forward's cout, cout = its cin);
+ * pass 0 / 1 only selects the timing id.  cin % 16 == 0, cout % 32 == 0,
+ * w even (mde_wino_supported). */
+int mde_wino_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype);
+size_t mde_wino_weight_bytes(int64_t cin, int64_t cout);
+int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, int flip,
+                    void* stream);
+int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
+                  int64_t h, int64_t w, int pass, int dtype, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Captured-graph repair (no reference counterpart: the reference runs its step
  * eagerly, src/train.py:83-114; the build replays it from a hipGraph).

@@ -76,6 +76,9 @@ enum Kid : int {
   K_C3S2_DGRAD,
   K_C3W_FWD,        // the wide stride-1 3x3 convolutions (conv3x3s2.hip, c3s1_kernel)
   K_C3W_DGRAD,
+  K_WINO_FWD,       // Winograd F(2x2, 3x3) stride-1 convolutions (wino.hip)
+  K_WINO_DGRAD,
+  K_WINO_WEIGHT,
   K_COUNT
 };
 

@@ -1,0 +1,329 @@
+// Winograd F(2x2, 3x3) for the wide stride-1 3x3 convolutions of DDRNet-23-slim
+// (the BasicBlocks, DAPPM's process convs and the seg head:
+// src/GuideDepth/model/DDRNet_23_slim.py:41-72,121-171,201-210, cfg2 at
+// 120x160 / 60x80 / 30x40 / 15x20), forward and data gradient, NCHW fp32.
+//
+//   Y = A^T [ (G g G^T) (.) (B^T d B) ] A      (Lavin & Gray, F(2x2, 3x3))
+//
+// per 2x2 output tile: d = the 4x4 input patch (zero padded), g = a 3x3
+// filter.  The 16 element-wise products, summed over input channels, are 16
+// independent GEMMs  M[xi][co][tile] = sum_ci U[xi][co][ci] V[xi][ci][tile]:
+// 16 MACs per 4 outputs instead of 36 (2.25x fewer MFMA cycles than the direct
+// band-GEMM kernel, which runs at the fp32 MFMA rate MIOpen's Winograd matches).
+//
+//  * U = G g G^T is computed once per weight update by wino_weight_kernel
+//    (16 x Cout x Cin floats, L2-resident) -- the data gradient uses the
+//    flipped, transposed filter (a stride-1 / pad-1 3x3 conv's input gradient
+//    is the same conv with g'[ci][co] = rot180(g[co][ci])).
+//  * A block owns 4 x 8 tiles (8 x 16 output pixels) x CO_B output channels.
+//    Per chunk of 16 input channels its 256 threads each transform two
+//    (channel, tile) patches (B^T d B: adds only) into LDS
+//    V[xi][tile half][ci][16]; the patches of the next chunk are loaded into
+//    registers first (their latency hides behind the MFMAs).
+//  * GEMMs on v_mfma_f32_16x16x4_f32 (exact fp32 products): a wave owns 16
+//    output channels x 16 or 32 tiles for ALL 16 xi, so each lane ends with
+//    the 16 xi values of its (channel, tile) pairs in registers and applies
+//    A^T M A there -- no LDS round trip for the output transform.  B operand
+//    reads V rows 4s + k at pitch 16: the four k-groups hit disjoint bank
+//    ranges (conflict-free ds_read_b32); A comes from U as one float4 per
+//    (xi, chunk) per lane (U's layout permuted so a lane's 4 k-steps are
+//    contiguous).
+// Exactness: B^T, A^T entries are 0 / +-1 and G's are 0 / +-1/2 (exact in
+// binary); fp32 rounding of the transforms and the 16-term GEMM sums -- the
+// GPU test holds it to 1e-5 of the output's max magnitude vs float64.
+#include <cstdlib>
+
+#include "common.h"
+
+namespace {
+
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+constexpr int kCIC = 16;  // input channels per chunk (K = 4 MFMA steps of 4)
+constexpr int kTRB = 4;   // tile rows per block (8 output rows)
+
+__device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+// U[co][chunk][xi][k][s] (ci = 16 chunk + 4 s + k): one float4 per lane and
+// (xi, chunk) holds its four k-steps.  FLIP: the data-gradient filter
+// g'[co' = ci][ci' = co] = rot180(g[co][ci]) (co_n / ci_n are the output /
+// input channels of the conv being RUN, i.e. swapped for FLIP).
+template <bool FLIP>
+__global__ void __launch_bounds__(256)
+    wino_weight_kernel(const float* __restrict__ g, float* __restrict__ U, int co_n, int ci_n) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)co_n * ci_n) return;
+  const int co = (int)(t / ci_n), ci = (int)(t % ci_n);
+  float w[3][3];
+  const float* src = FLIP ? g + ((int64_t)ci * co_n + co) * 9 : g + ((int64_t)co * ci_n + ci) * 9;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) w[r][c] = FLIP ? src[(2 - r) * 3 + (2 - c)] : src[r * 3 + c];
+  // G w: rows (w0, (w0+w1+w2)/2, (w0-w1+w2)/2, w2), then the same on columns
+  float a[4][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    a[0][c] = w[0][c];
+    a[1][c] = 0.5f * ((w[0][c] + w[1][c]) + w[2][c]);
+    a[2][c] = 0.5f * ((w[0][c] - w[1][c]) + w[2][c]);
+    a[3][c] = w[2][c];
+  }
+  const int chunk = ci / kCIC, s = (ci % kCIC) / 4, k = ci % 4;
+  float* dst = U + ((int64_t)co * (ci_n / kCIC) + chunk) * 256 + k * 4 + s;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float u[4] = {a[r][0], 0.5f * ((a[r][0] + a[r][1]) + a[r][2]),
+                        0.5f * ((a[r][0] - a[r][1]) + a[r][2]), a[r][2]};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 16] = u[c];
+  }
+}
+
+// A block: 4 x TCB tiles (8 x 2 TCB output pixels) x CO_B output channels.
+// CO_B = 64 (TCB 8): four waves along output channels, each with both 16-tile
+// groups; CO_B = 32 (TCB 8): two waves along channels x two along tile groups;
+// CO_B = 16 (TCB 16, the decoder's 16 -> 16 convs): one along channels x four.
+template <int CO_B, int TCB>
+__global__ void __launch_bounds__(256, 2)
+    wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
+                    int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total) {
+  constexpr int NTB = kTRB * TCB;      // tiles per block
+  constexpr int NG = NTB / 16;         // 16-tile groups (MFMA N tiles)
+  constexpr int WCO = CO_B / 16;       // waves along output channels
+  constexpr int NTW = NG / (4 / WCO);  // 16-tile groups per wave
+  constexpr int PPT = NTB * kCIC / 256;  // (channel, tile) patches per thread and chunk
+  static_assert(NTW >= 1 && NTW * (4 / WCO) == NG, "wave tiling");
+  // LDS floats per (xi, 16-tile group): [ci][16] + a pad that puts the groups
+  // a wave's transform writes at once (2 groups x 2 channels, or 4 groups of
+  // one channel) on disjoint banks: 32 / 16 (mod 64)
+  constexpr int kVP = kCIC * 16 + (NG == 2 ? 32 : 16);
+  __shared__ __attribute__((aligned(16))) float V[16][NG][kVP];
+
+  // XCD-aware block order (blocks b, b + 8, ... share an XCD's L2): logical
+  // block l -> (channel group fastest, so the groups reading one input tile
+  // share that L2; then tile column, tile row, image)
+  const int per = gridDim.x >> 3;
+  const int l = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (l >= total) return;
+  const int cog = l % ncog;
+  int rest = l / ncog;
+  const int bc = rest % bcols;
+  rest /= bcols;
+  const int br = rest % brows;
+  const int img = rest / brows;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, kq = lane >> 4;
+  const int co0 = cog * CO_B + 16 * (wv % WCO);
+  const int nt0 = (wv / WCO) * NTW;
+  const int64_t hw = (int64_t)h * w;
+  const float* xb = x + (int64_t)img * ci_n * hw;
+  const int nchunks = ci_n / kCIC;
+  const float* ua = U + (int64_t)(co0 + li) * nchunks * 256 + kq * 4;
+
+  // patch loader: p = tid + 256 pp -> (channel p / NTB, tile p % NTB)
+  const int r0 = (br * kTRB) * 2 - 1, c0 = (bc * TCB) * 2 - 1;
+  int poff[PPT][4], pcol[PPT][4];
+  uint32_t pmask[PPT];
+#pragma unroll
+  for (int pp = 0; pp < PPT; ++pp) {
+    const int p = tid + 256 * pp, tl = p % NTB;
+    const int gr = r0 + 2 * (tl / TCB), gc = c0 + 2 * (tl % TCB);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = gr + i, cc = gc + i;
+      m |= (rr >= 0 && rr < h ? 1u : 0u) << i;
+      m |= (cc >= 0 && cc < w ? 1u : 0u) << (4 + i);
+      poff[pp][i] = (rr < 0 ? 0 : (rr >= h ? h - 1 : rr)) * w;
+      pcol[pp][i] = cc < 0 ? 0 : (cc >= w ? w - 1 : cc);
+    }
+    pmask[pp] = m;
+  }
+  float pv[PPT][16];
+  auto load = [&](int chunk) {
+#pragma unroll
+    for (int pp = 0; pp < PPT; ++pp) {
+      const int ch = (tid + 256 * pp) / NTB;
+      const float* src = xb + (int64_t)(chunk * kCIC + ch) * hw;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) pv[pp][4 * i + j] = src[poff[pp][i] + pcol[pp][j]];
+    }
+  };
+  // B^T d B into V[xi][16-tile group][ci][16]
+  auto transform = [&]() {
+#pragma unroll
+    for (int pp = 0; pp < PPT; ++pp) {
+      const int p = tid + 256 * pp, ch = p / NTB, tl = p % NTB;
+      float d[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const bool ok = ((pmask[pp] >> i) & 1u) && ((pmask[pp] >> (4 + j)) & 1u);
+          d[i][j] = ok ? pv[pp][4 * i + j] : 0.f;
+        }
+      float t[4][4];  // B^T d: rows d0 - d2, d1 + d2, d2 - d1, d1 - d3
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[0][j] = d[0][j] - d[2][j];
+        t[1][j] = d[1][j] + d[2][j];
+        t[2][j] = d[2][j] - d[1][j];
+        t[3][j] = d[1][j] - d[3][j];
+      }
+      float* dst = &V[0][tl >> 4][ch * 16 + (tl & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v[4] = {t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1],
+                            t[i][1] - t[i][3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[(4 * i + j) * NG * kVP] = v[j];
+      }
+    }
+  };
+
+  f4 acc[16][NTW];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    __syncthreads();  // the previous chunk's V readers are done
+    transform();
+    __syncthreads();
+    if (chunk + 1 < nchunks) load(chunk + 1);
+    const float* uc = ua + (int64_t)chunk * 256;
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      const f4 a = *reinterpret_cast<const f4*>(uc + xi * 16);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int n = 0; n < NTW; ++n)
+          acc[xi][n] = mfma(a[s], V[xi][nt0 + n][(4 * s + kq) * 16 + li], acc[xi][n]);
+    }
+  }
+
+  // A^T M A per (channel, tile): lane holds channels co0 + 4 kq + r, tile 16 (nt0 + n) + li
+  float* yb = y + (int64_t)img * co_n * hw;
+#pragma unroll
+  for (int n = 0; n < NTW; ++n) {
+    const int tl = 16 * (nt0 + n) + li;
+    const int oy = 2 * (br * kTRB + tl / TCB), ox = 2 * (bc * TCB + tl % TCB);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float u0[4], u1[4];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float m0 = acc[b][n][r], m1 = acc[4 + b][n][r], m2 = acc[8 + b][n][r],
+                    m3 = acc[12 + b][n][r];
+        u0[b] = (m0 + m1) + m2;
+        u1[b] = (m1 - m2) - m3;
+      }
+      const float y00 = (u0[0] + u0[1]) + u0[2], y01 = (u0[1] - u0[2]) - u0[3];
+      const float y10 = (u1[0] + u1[1]) + u1[2], y11 = (u1[1] - u1[2]) - u1[3];
+      float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
+      if (oy < h) {
+        if (ox + 1 < w) {
+          *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
+        } else if (ox < w) {
+          dst[0] = y00;
+        }
+      }
+      if (oy + 1 < h) {
+        if (ox + 1 < w) {
+          *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
+        } else if (ox < w) {
+          dst[w] = y10;
+        }
+      }
+    }
+  }
+}
+
+struct WinoGeo {
+  int bcols, brows, ncog, co_b;
+  int64_t total;
+};
+
+inline bool wino_geo(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WinoGeo* g) {
+  if (n <= 0 || ci < kCIC || ci % kCIC || co < 16 || (co != 16 && co % 32) || h < 1 || w < 2)
+    return false;
+  if (w % 2) return false;  // float2 output stores at even offsets
+  if (n * ci * h * w >= ((int64_t)1 << 31) || n * co * h * w >= ((int64_t)1 << 31)) return false;
+  g->co_b = co % 64 == 0 ? 64 : (co == 16 ? 16 : 32);
+  g->ncog = (int)(co / g->co_b);
+  g->bcols = (int)mde::cdiv(w, g->co_b == 16 ? 32 : 16);
+  g->brows = (int)mde::cdiv(h, 2 * kTRB);
+  g->total = n * g->ncog * g->bcols * g->brows;
+  return g->total < 0x7fffffff;
+}
+
+}  // namespace
+
+extern "C" {
+
+// 1 when the Winograd kernels take a stride-1 / pad-1 3x3 conv of these
+// channels and plane (this pass: the conv actually run, i.e. (cout, cin) swapped
+// for the data gradient); the caller applies its own size thresholds.
+int mde_wino_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype) {
+  WinoGeo g;
+  return dtype == MDE_F32 && wino_geo(1, cin, cout, h, w, &g) ? 1 : 0;
+}
+
+size_t mde_wino_weight_bytes(int64_t cin, int64_t cout) {
+  return sizeof(float) * 16 * (size_t)cin * (size_t)cout;
+}
+
+// U from the [cout][cin][3][3] filter of the FORWARD conv; flip = 1 gives the
+// data-gradient transform (U' for the conv cout -> cin).
+int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, int flip,
+                    void* stream) {
+  if (!weight || !u || cin < kCIC || cout < kCIC || cin % kCIC || cout % kCIC)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t pairs = cin * cout;
+  const dim3 grid((unsigned)mde::cdiv(pairs, 256));
+  if (flip)
+    MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 16), s, wino_weight_kernel<true>, grid,
+               dim3(256), 0, weight, u, (int)cin, (int)cout);
+  else
+    MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 16), s, wino_weight_kernel<false>, grid,
+               dim3(256), 0, weight, u, (int)cout, (int)cin);
+  return MDE_OK;
+}
+
+// y[n][cout][h][w] = conv3x3(x[n][cin][h][w]) (stride 1, pad 1) from U =
+// mde_wino_weight(..).  `pass` 0 = forward, 1 = data gradient (timing id only).
+int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
+                  int64_t h, int64_t w, int pass, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !u || !y) return MDE_ERR_INVALID_ARG;
+  WinoGeo g;
+  if (!wino_geo(n, cin, cout, h, w, &g)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const double flops = 2.0 * 9 * n * h * w * (double)cin * cout;  // direct-conv equivalent
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
+  const dim3 grid((unsigned)((g.total + 7) / 8 * 8)), block(256);
+  const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
+  if (g.co_b == 64)
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<64, 8>), grid, block, 0, x, u, y,
+                    (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total);
+  else if (g.co_b == 32)
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<32, 8>), grid, block, 0, x, u, y,
+                    (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total);
+  else
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<16, 16>), grid, block, 0, x, u, y,
+                    (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total);
+  return MDE_OK;
+}
+
+}  // extern "C"

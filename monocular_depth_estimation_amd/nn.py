@@ -400,7 +400,14 @@ class _Conv3x3(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
-        if passes[0] == WIDE:  # no statistics epilogue: the BatchNorm reads y
+        if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip); no statistics epilogue
+            y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
+            u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+            st = _abi.stream_of(x)
+            _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 0, st)
+            _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y), n, cin, cout, h, w, 0,
+                      _abi.dtype_code(x), st)
+        elif passes[0] == WIDE:  # no statistics epilogue: the BatchNorm reads y
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
             _abi.call("mde_conv3x3_wide_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cin,
                       cout, h, w, _abi.dtype_code(x), _abi.stream_of(x))
@@ -432,7 +439,13 @@ class _Conv3x3(torch.autograd.Function):
         gx = gw = None
         st = _abi.stream_of(gy)
         if ctx.needs_input_grad[0]:
-            if ctx.passes[1] == WIDE:
+            if ctx.passes[1] == WINO:  # the flipped, transposed filter's transform
+                gx = torch.empty_like(x)
+                u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+                _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 1, st)
+                _abi.call("mde_wino_conv", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(gx), n, cout, cin, h,
+                          w, 1, _abi.dtype_code(gy), st)
+            elif ctx.passes[1] == WIDE:
                 gx = torch.empty_like(x)
                 _abi.call("mde_conv3x3_wide_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx),
                           n, cin, cout, h, w, _abi.dtype_code(gy), st)
@@ -714,6 +727,16 @@ def conv3x3_passes(conv: nn.Conv2d, x):
         return None
     p = [bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
          for i, f in enumerate(p)]
+    if dt == _abi.MDE_F32 and WINO_ON and not _autocast_bf16(x):
+        # forward / data gradient of the 32-256-channel convs on the Winograd
+        # F(2x2, 3x3) kernels (2.25x fewer MACs) where MIOpen would run its own
+        # Winograd: planes of >= 256 blocks (8 x 16 output pixels x 64 channels)
+        n, h, w = x.shape[0], x.shape[2], x.shape[3]
+        for i, (a, b) in enumerate(((cin, cout), (cout, cin))):
+            blocks = n * -(-h // 8) * -(-w // 16) * max(b // 64, 1)
+            if (not p[i] and blocks >= 256
+                    and _abi.query("mde_wino_supported", a, b, h, w, _abi.MDE_F32)):
+                p[i] = WINO
     if dt == _abi.MDE_F32 and C3_WIDE and not _autocast_bf16(x):
         # forward / data gradient of the 32-256-channel convs on the band-GEMM
         # kernels (conv3x3s2.hip c3s1_kernel) where MIOpen would run Winograd
@@ -725,6 +748,8 @@ def conv3x3_passes(conv: nn.Conv2d, x):
 
 
 WIDE = 2  # conv3x3_passes flag: the pass runs on the wide-channel kernel
+WINO = 3  # conv3x3_passes flag: the pass runs on the Winograd kernel
+WINO_ON = os.environ.get("MDE_WINO", "0") == "1"  # A/B switch until measured on the GPU
 # Off by default: MIOpen's Winograd matches the stride-1 band kernel on these
 # shapes (tools/c1_bench.py) and the cfg2 step was 0.5 % slower with it on
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"

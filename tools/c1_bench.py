@@ -127,19 +127,84 @@ def run():
         mf = lambda: torch.nn.functional.conv2d(x, wt, None, 1, 1)
         md = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (1, 1), (1, 1),
                                                          False, (0, 0), 1, (True, False, False))
+        u = torch.empty(16 * ci * co, device="cuda")
+        yw = torch.empty_like(y)
+        gxw = torch.empty_like(gx)
+
+        def wf():  # Winograd forward incl. its weight transform
+            _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), ci, co, 0, st)
+            _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(yw), n, ci, co, h, w, 0, 0,
+                      st)
+
+        def wd():
+            _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), ci, co, 1, st)
+            _abi.call("mde_wino_conv", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(gxw), n, co, ci, h, w, 1,
+                      0, st)
         t = {k: kbench.timeit(f, 20) * 1e3 for k, f in
-             (("fwd", fwd), ("dgrad", dgr), ("mio_fwd", mf), ("mio_dgrad", md))}
+             (("fwd", fwd), ("dgrad", dgr), ("mio_fwd", mf), ("mio_dgrad", md), ("wino_fwd", wf),
+              ("wino_dgrad", wd))}
         fl = 2.0 * 9 * n * h * w * ci * co
         fwd()
         dgr()
-        err = max(float((a - b).abs().max() / b.abs().max()) for a, b in ((y, mf()), (gx, md()[0])))
+        wf()
+        wd()
+        ym, gxm = mf(), md()[0]
+        err = max(float((a - b).abs().max() / b.abs().max()) for a, b in ((y, ym), (gx, gxm)))
+        errw = max(float((a - b).abs().max() / b.abs().max()) for a, b in ((yw, ym), (gxw, gxm)))
         tot["hip"] += uses * (t["fwd"] + t["dgrad"])
         tot["miopen"] += uses * (t["mio_fwd"] + t["mio_dgrad"])
-        print(f"3x3s1 {ci}->{co} {h}x{w}: HIP fwd {t['fwd']:6.1f} dgrad {t['dgrad']:6.1f} us "
-              f"({fl / t['fwd'] / 1e6:5.1f} / {fl / t['dgrad'] / 1e6:5.1f} TF/s) | MIOpen fwd "
-              f"{t['mio_fwd']:6.1f} dgrad {t['mio_dgrad']:6.1f} us | rel diff {err:.1e}", flush=True)
-    print(f"3x3s1 per cfg2 step (x uses): HIP {tot['hip']:.0f} us, MIOpen {tot['miopen']:.0f} us",
-          flush=True)
+        tot["wino"] = tot.get("wino", 0.0) + uses * (t["wino_fwd"] + t["wino_dgrad"])
+        print(f"3x3s1 {ci}->{co} {h}x{w}: band fwd {t['fwd']:6.1f} dgrad {t['dgrad']:6.1f} us "
+              f"({fl / t['fwd'] / 1e6:5.1f} / {fl / t['dgrad'] / 1e6:5.1f} TF/s) | Winograd fwd "
+              f"{t['wino_fwd']:6.1f} dgrad {t['wino_dgrad']:6.1f} us | MIOpen fwd "
+              f"{t['mio_fwd']:6.1f} dgrad {t['mio_dgrad']:6.1f} us | rel diff {err:.1e} / {errw:.1e}",
+              flush=True)
+    print(f"3x3s1 per cfg2 step (x uses): band {tot['hip']:.0f} us, Winograd {tot['wino']:.0f} us, "
+          f"MIOpen {tot['miopen']:.0f} us", flush=True)
+    # the decoder's 16 -> 16 convs at 480 x 640: the direct MFMA kernel (with its
+    # BN-statistics epilogue off) vs Winograd
+    for ci, co, h, w in ((16, 16, 480, 640), (32, 32, 240, 320)):
+        x = torch.rand((n, ci, h, w), device="cuda") - 0.5
+        wt = (torch.rand((co, ci, 3, 3), device="cuda") - 0.5) * 0.1
+        gy = torch.rand((n, co, h, w), device="cuda") - 0.5
+        y, yw = torch.empty_like(gy), torch.empty_like(gy)
+        gx, gxw = torch.empty_like(x), torch.empty_like(x)
+        u = torch.empty(16 * ci * co, device="cuda")
+        st = _abi.stream_of(x)
+        fl = 2.0 * 9 * n * h * w * ci * co
+
+        def df():
+            _abi.call("mde_conv3x3_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(y), n, ci, co, h, w, 0, st)
+
+        def dd():
+            _abi.call("mde_conv3x3_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, ci, co, h,
+                      w, 0, st)
+
+        def wf():
+            _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), ci, co, 0, st)
+            _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(yw), n, ci, co, h, w, 0, 0,
+                      st)
+
+        def wd():
+            _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), ci, co, 1, st)
+            _abi.call("mde_wino_conv", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(gxw), n, co, ci, h, w, 1,
+                      0, st)
+        mf = lambda: torch.nn.functional.conv2d(x, wt, None, 1, 1)
+        have_direct = bool(_abi.query("mde_conv3x3_supported", ci, co, 0, 0))
+        fns = (("wino_fwd", wf), ("wino_dgrad", wd), ("mio_fwd", mf))
+        if have_direct:
+            fns = fns + (("fwd", df), ("dgrad", dd))
+        t = {k: kbench.timeit(f, 20) * 1e3 for k, f in fns}
+        wf()
+        wd()
+        ym = mf()
+        gxm = torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (1, 1), (1, 1), False,
+                                                  (0, 0), 1, (True, False, False))[0]
+        errw = max(float((a - b).abs().max() / b.abs().max()) for a, b in ((yw, ym), (gxw, gxm)))
+        direct = (f"direct fwd {t['fwd']:6.1f} dgrad {t['dgrad']:6.1f} us | " if have_direct else "")
+        print(f"3x3s1 {ci}->{co} {h}x{w}: {direct}Winograd fwd {t['wino_fwd']:6.1f} "
+              f"({fl / t['wino_fwd'] / 1e6:5.1f} TF/s eff.) dgrad {t['wino_dgrad']:6.1f} us | MIOpen "
+              f"fwd {t['mio_fwd']:6.1f} us | Winograd rel diff {errw:.1e}", flush=True)
 
 
 if __name__ == "__main__":

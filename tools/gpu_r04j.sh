@@ -9,7 +9,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/r04j
 mkdir -p $OUT
 export TMPDIR=/tmp MASTER_ADDR=127.0.0.1
-timeout -k 10 900 python3 -u -m pytest tests/test_gpu_conv3x3s2.py tests/test_gpu_bn.py tests/test_gpu_se_bn.py \
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_wino.py tests/test_gpu_conv3x3s2.py tests/test_gpu_bn.py tests/test_gpu_se_bn.py \
   tests/test_gpu_parity.py tests/test_gpu_conv3x3.py tests/test_gpu_bf16.py tests/test_gpu_resume.py \
   -q -rfE --timeout 300 --timeout-method thread > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; grep -v "Cannot find the function" $OUT/tests.log | tail -n 25 | cut -c1-300

@@ -658,6 +658,13 @@ int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, in
                     void* stream);
 int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
                   int64_t h, int64_t w, int pass, int dtype, void* stream);
+/* The same with the following BatchNorm's statistics of y from the epilogue
+ * (stats [cout][mde_wino_stats_blocks][4] = (shift, count, s1, s2), the format
+ * of mde_batchnorm_fwd_train_stats; NULL stats = mde_wino_conv). */
+int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, int64_t n,
+                        int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
+                        void* stream);
+int mde_wino_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w);
 
 /* ---------------------------------------------------------------------------
  * Captured-graph repair (no reference counterpart: the reference runs its step

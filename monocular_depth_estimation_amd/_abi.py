@@ -148,6 +148,9 @@ SIGNATURES = {
     "mde_wino_weight_bytes": (_sz, [_i64, _i64]),
     "mde_wino_weight": (_int, [_vp, _vp, _i64, _i64, _int, _vp]),
     "mde_wino_conv": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "mde_wino_conv_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int,
+                                   _vp]),
+    "mde_wino_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
     "mde_conv3x3_guide_bf16_stats_blocks": (_int, [_i64, _i64, _i64, _i64]),
     "mde_conv3x3_guide_bf16_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),

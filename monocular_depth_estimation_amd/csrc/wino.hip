@@ -86,10 +86,14 @@ __global__ void __launch_bounds__(256)
 // CO_B = 64 (TCB 8): four waves along output channels, each with both 16-tile
 // groups; CO_B = 32 (TCB 8): two waves along channels x two along tile groups;
 // CO_B = 16 (TCB 16, the decoder's 16 -> 16 convs): one along channels x four.
-template <int CO_B, int TCB>
+// STATS: also the following BatchNorm's per-block statistics of y (as the
+// direct conv's epilogue: stats[c][total / ncog][4] = (shift, count, s1, s2),
+// one record per channel and pixel block; the shift is a sample of the channel).
+template <int CO_B, int TCB, bool STATS = false>
 __global__ void __launch_bounds__(256, 2)
     wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
-                    int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total) {
+                    int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
+                    float* __restrict__ stats) {
   constexpr int NTB = kTRB * TCB;      // tiles per block
   constexpr int NG = NTB / 16;         // 16-tile groups (MFMA N tiles)
   constexpr int WCO = CO_B / 16;       // waves along output channels
@@ -214,6 +218,7 @@ __global__ void __launch_bounds__(256, 2)
 
   // A^T M A per (channel, tile): lane holds channels co0 + 4 kq + r, tile 16 (nt0 + n) + li
   float* yb = y + (int64_t)img * co_n * hw;
+  mde::Sh run[STATS ? 4 : 1];
 #pragma unroll
   for (int n = 0; n < NTW; ++n) {
     const int tl = 16 * (nt0 + n) + li;
@@ -230,6 +235,15 @@ __global__ void __launch_bounds__(256, 2)
       }
       const float y00 = (u0[0] + u0[1]) + u0[2], y01 = (u0[1] - u0[2]) - u0[3];
       const float y10 = (u1[0] + u1[1]) + u1[2], y11 = (u1[1] - u1[2]) - u1[3];
+      if constexpr (STATS) {
+        const bool ok0 = oy < h && ox < w, ok1 = oy + 1 < h && ox < w;
+        if (n == 0)  // the shift: the channel's value at this wave's first tile (li = 0)
+          run[r] = {__shfl(ok0 ? y00 : 0.f, lane & 48, 64), 0.f, 0.f, 0.f};
+        mde::sh_add(run[r], y00, ok0);
+        mde::sh_add(run[r], y01, ok0);
+        mde::sh_add(run[r], y10, ok1);
+        mde::sh_add(run[r], y11, ok1);
+      }
       float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
       if (oy < h) {
         if (ox + 1 < w) {
@@ -245,6 +259,44 @@ __global__ void __launch_bounds__(256, 2)
           dst[w] = y10;
         }
       }
+    }
+  }
+  if constexpr (STATS) {
+    // the 16 lanes of a k-group share its 4 channels: butterfly over li, then
+    // the waves holding the same channels (other tile groups) merged in wave
+    // order through LDS (V reused once every wave is past its last read)
+    constexpr int NWN = 4 / WCO;  // waves per channel set
+    __syncthreads();
+    float* part = &V[0][0][0];  // [wave][16 channels][4]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mde::Sh a = run[r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
+      if (li == 0) {
+        float* p4 = part + (wv * 16 + 4 * kq + r) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
+    }
+    __syncthreads();
+    if (tid < CO_B) {
+      const int wc = tid / 16, c16 = tid % 16;  // channel set (wave % WCO), channel within
+      mde::Sh a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NWN; ++k) {
+        const float* p4 = part + ((k * WCO + wc) * 16 + c16) * 4;
+        a = k == 0 ? mde::Sh{p4[0], p4[1], p4[2], p4[3]}
+                   : mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      const int G = total / ncog, gb = l / ncog;
+      float* o4 = stats + ((int64_t)(cog * CO_B + tid) * G + gb) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
     }
   }
 }
@@ -303,8 +355,9 @@ int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, in
 
 // y[n][cout][h][w] = conv3x3(x[n][cin][h][w]) (stride 1, pad 1) from U =
 // mde_wino_weight(..).  `pass` 0 = forward, 1 = data gradient (timing id only).
-int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
-                  int64_t h, int64_t w, int pass, int dtype, void* stream) {
+int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, int64_t n,
+                        int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
+                        void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !u || !y) return MDE_ERR_INVALID_ARG;
   WinoGeo g;
@@ -314,16 +367,39 @@ int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t c
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
   const dim3 grid((unsigned)((g.total + 7) / 8 * 8)), block(256);
   const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
-  if (g.co_b == 64)
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<64, 8>), grid, block, 0, x, u, y,
-                    (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total);
-  else if (g.co_b == 32)
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<32, 8>), grid, block, 0, x, u, y,
-                    (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total);
-  else
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<16, 16>), grid, block, 0, x, u, y,
-                    (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total);
+#define MDE_WINO(CB, TC, ST)                                                                      \
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST>), grid, block, 0, x, u, y,   \
+                  (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \
+                  stats)
+  if (stats) {
+    if (g.co_b == 64)
+      MDE_WINO(64, 8, true);
+    else if (g.co_b == 32)
+      MDE_WINO(32, 8, true);
+    else
+      MDE_WINO(16, 16, true);
+  } else {
+    if (g.co_b == 64)
+      MDE_WINO(64, 8, false);
+    else if (g.co_b == 32)
+      MDE_WINO(32, 8, false);
+    else
+      MDE_WINO(16, 16, false);
+  }
+#undef MDE_WINO
   return MDE_OK;
+}
+
+int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
+                  int64_t h, int64_t w, int pass, int dtype, void* stream) {
+  return mde_wino_conv_stats(x, u, y, nullptr, n, cin, cout, h, w, pass, dtype, stream);
+}
+
+// Records per channel of mde_wino_conv_stats (the pixel blocks), or 0.
+int mde_wino_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w) {
+  WinoGeo g;
+  if (!wino_geo(n, cin, cout, h, w, &g)) return 0;
+  return (int)(g.total / g.ncog);
 }
 
 }  // extern "C"

@@ -400,12 +400,16 @@ class _Conv3x3(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
-        if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip); no statistics epilogue
+        if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip), + the BN statistics
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
             u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
             st = _abi.stream_of(x)
+            if want_stats:
+                nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
+                stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
             _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 0, st)
-            _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y), n, cin, cout, h, w, 0,
+            _abi.call("mde_wino_conv_stats", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y),
+                      _abi.ptr(stats) if want_stats else None, n, cin, cout, h, w, 0,
                       _abi.dtype_code(x), st)
         elif passes[0] == WIDE:  # no statistics epilogue: the BatchNorm reads y
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)

@@ -33,7 +33,7 @@ NAMES = [
     (r"se_partial_kernel<true>", "se_bwd_dot"),
     (r"se_fc[12]_kernel", "se_fc"),
     (r"se_scale_kernel", "se_scale"),
-    (r"se_(bfc[123]|bfc_all|wgrad)_kernel", "se_bwd_fc"),
+    (r"se_(bfc[123]w?|bfc_all|wgrad)_kernel|sebn_bwd_combine_kernel", "se_bwd_fc"),
     (r"se_apply_kernel", "se_bwd_apply"),
     (r"skip_fwd_mfma_kernel<\d+, \d+, true", "skip_reduce_fwd"),
     (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
@@ -54,7 +54,19 @@ NAMES = [
     (r"minmax_partial_kernel", "minmax"),
     (r"minmax_final_kernel", "minmax_final"),
     (r"depthnorm_kernel", "depthnorm_apply"),
-    (r"ssim3_(l1|stream)_kernel", "ssim3_l1"),
+    (r"ssim3_(l1|stream|pair)_kernel", "ssim3_l1"),
+    (r"cm_kernel<[^>]*false>", "conv1x1_fwd"),
+    (r"cm_kernel<[^>]*true>", "conv1x1_dgrad"),
+    (r"c1_wgrad_kernel", "conv1x1_wgrad"),
+    (r"c1_wreduce_kernel", "conv1x1_wreduce"),
+    (r"c3s2_fwd_kernel", "conv3x3s2_fwd"),
+    (r"c3s2_dgrad_kernel", "conv3x3s2_dgrad"),
+    (r"c3s1_kernel<false", "conv3x3w_fwd"),
+    (r"c3s1_kernel<true", "conv3x3w_dgrad"),
+    (r"wino_f23_kernel", "wino_fwd"),  # forward and data gradient: one kernel
+    (r"wino_weight_kernel", "wino_weight"),
+    (r"bn_fwd_chan_kernel", "bn_fwd_apply_small"),
+    (r"bn_bwd_chan_kernel", "bn_bwd_apply_small"),
     (r"dloss_(fwd_stream|masked|map|final)_kernel", "depth_loss_fwd"),
     (r"dloss_(bwd_stream|masked_bwd|grad)_kernel", "depth_loss_bwd"),
     (r"loss_final_kernel", "loss_final"),

@@ -198,6 +198,13 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int n = 0; n < NTW; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // A operands (U rows, L2-resident) through a 4-deep register ring: the
+  // float4 of step xi is loaded 4 steps (>= 16 MFMAs) ahead, across the chunk
+  // boundary too, so the L2 latency is never waited on right after the load
+  constexpr int RING = 4;
+  f4 ring[RING];
+#pragma unroll
+  for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 16);
   load(0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     __syncthreads();  // the previous chunk's V readers are done
@@ -205,9 +212,15 @@ __global__ void __launch_bounds__(256, 2)
     __syncthreads();
     if (chunk + 1 < nchunks) load(chunk + 1);
     const float* uc = ua + (int64_t)chunk * 256;
+    const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 256;
 #pragma unroll
     for (int xi = 0; xi < 16; ++xi) {
-      const f4 a = *reinterpret_cast<const f4*>(uc + xi * 16);
+      const f4 a = ring[xi % RING];
+      ring[xi % RING] = *reinterpret_cast<const f4*>(
+          xi + RING < 16 ? uc + (xi + RING) * 16 : un + (xi + RING - 16) * 16);
+      // keep the load here: the scheduler otherwise sinks it next to its use
+      // (register pressure) and every step waits on L2 again
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll

@@ -67,12 +67,12 @@ def test_wino_abi_vs_float64_oracle(cin, cout, h, w):
 @pytest.mark.parametrize("cin,cout,h,w", [(64, 64, 60, 80), (128, 64, 60, 80), (256, 256, 15, 20)])
 def test_wino_module_path(cin, cout, h, w, monkeypatch):
     """Conv2d (the DDRNet modules' class) dispatches both passes to Winograd
-    at cfg2 sizes (bs 8: >= 256 blocks) with MDE_WINO on; all three gradients
-    vs float64."""
+    at cfg2 sizes (bs 16: >= 256 blocks of 8 x 16 pixels x 64 channels) with
+    MDE_WINO on; all three gradients vs float64."""
     from monocular_depth_estimation_amd import nn as mnn
     from monocular_depth_estimation_amd.nn import WINO, Conv2d, conv3x3_passes
     monkeypatch.setattr(mnn, "WINO_ON", True)
-    n = 8
+    n = 16
     g = torch.Generator().manual_seed(cin * 11 + cout)
     x = torch.rand((n, cin, h, w), generator=g) - 0.5
     wt = (torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.1

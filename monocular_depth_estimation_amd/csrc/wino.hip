@@ -15,15 +15,13 @@
 //    (16 x Cout x Cin floats, L2-resident) -- the data gradient uses the
 //    flipped, transposed filter (a stride-1 / pad-1 3x3 conv's input gradient
 //    is the same conv with g'[ci][co] = rot180(g[co][ci])).
-//  * Persistent blocks walk a list of (channel group, 8-row pixel block)
-//    tiles; a block owns CO_B output channels x 16 / 32 / 64 Winograd tiles.
-//    Per chunk of 16 input channels its 256 threads transform the (channel,
-//    tile) patches (B^T d B: adds only) into LDS V[xi][16-tile group][ci][16];
-//    the next chunk's (or the next tile's first) patches are loaded into
-//    registers through a buffer resource before the MFMAs, so their latency
-//    hides behind them.
+//  * A block owns 4 x 8 tiles (8 x 16 output pixels) x CO_B output channels.
+//    Per chunk of 16 input channels its 256 threads each transform two
+//    (channel, tile) patches (B^T d B: adds only) into LDS
+//    V[xi][tile half][ci][16]; the patches of the next chunk are loaded into
+//    registers first (their latency hides behind the MFMAs).
 //  * GEMMs on v_mfma_f32_16x16x4_f32 (exact fp32 products): a wave owns 16
-//    output channels x 16 tiles for ALL 16 xi, so each lane ends with
+//    output channels x 16 or 32 tiles for ALL 16 xi, so each lane ends with
 //    the 16 xi values of its (channel, tile) pairs in registers and applies
 //    A^T M A there -- no LDS round trip for the output transform.  B operand
 //    reads V rows 4s + k at pitch 16: the four k-groups hit disjoint bank
@@ -84,112 +82,82 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// A wave owns 16 output channels x 16 tiles (one 16-tile MFMA N group) for
-// all 16 xi; a block: CO_B output channels x 4 x TCB tiles (8 x 2 TCB output
-// pixels), TCB = 4 (CO_B 64: four waves along channels), 8 (CO_B 32: two x
-// two), 16 (CO_B 16, the decoder's 16 -> 16 convs: four waves along tiles).
+// A block: 4 x TCB tiles (8 x 2 TCB output pixels) x CO_B output channels.
+// CO_B = 64 (TCB 8): four waves along output channels, each with both 16-tile
+// groups; CO_B = 32 (TCB 8): two waves along channels x two along tile groups;
+// CO_B = 16 (TCB 16, the decoder's 16 -> 16 convs): one along channels x four.
 // STATS: also the following BatchNorm's per-block statistics of y (as the
 // direct conv's epilogue: stats[c][total / ncog][4] = (shift, count, s1, s2),
 // one record per channel and pixel block; the shift is a sample of the channel).
-template <int CO_B, bool STATS = false>
-__global__ void __launch_bounds__(256, CO_B == 16 ? 1 : 2)
+template <int CO_B, int TCB, bool STATS = false>
+__global__ void __launch_bounds__(256, 2)
     wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
                     float* __restrict__ stats) {
-  constexpr int WCO = CO_B / 16;       // waves along output channels
-  constexpr int NG = 4 / WCO;          // 16-tile groups (MFMA N tiles) = waves along tiles
-  constexpr int NTW = 1;               // 16-tile groups per wave
-  constexpr int TCB = 4 * NG;          // tile columns per block
   constexpr int NTB = kTRB * TCB;      // tiles per block
+  constexpr int NG = NTB / 16;         // 16-tile groups (MFMA N tiles)
+  constexpr int WCO = CO_B / 16;       // waves along output channels
+  constexpr int NTW = NG / (4 / WCO);  // 16-tile groups per wave
   constexpr int PPT = NTB * kCIC / 256;  // (channel, tile) patches per thread and chunk
+  static_assert(NTW >= 1 && NTW * (4 / WCO) == NG, "wave tiling");
   // LDS floats per (xi, 16-tile group): [ci][16] + a pad that puts the groups
   // a wave's transform writes at once (2 groups x 2 channels, or 4 groups of
   // one channel) on disjoint banks: 32 / 16 (mod 64)
   constexpr int kVP = kCIC * 16 + (NG == 2 ? 32 : 16);
   __shared__ __attribute__((aligned(16))) float V[16][NG][kVP];
 
-  __shared__ float part[STATS ? 4 * 16 * 4 : 1];  // the statistics merge: [wave][channel][4]
+  // XCD-aware block order (blocks b, b + 8, ... share an XCD's L2): logical
+  // block l -> (channel group fastest, so the groups reading one input tile
+  // share that L2; then tile column, tile row, image)
+  const int per = gridDim.x >> 3;
+  const int l = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
+  if (l >= total) return;
+  const int cog = l % ncog;
+  int rest = l / ncog;
+  const int bc = rest % bcols;
+  rest /= bcols;
+  const int br = rest % brows;
+  const int img = rest / brows;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int li = lane & 15, kq = lane >> 4;
-  const int wco = 16 * (wv % WCO);
+  const int co0 = cog * CO_B + 16 * (wv % WCO);
   const int nt0 = (wv / WCO) * NTW;
   const int64_t hw = (int64_t)h * w;
+  const float* xb = x + (int64_t)img * ci_n * hw;
   const int nchunks = ci_n / kCIC;
+  const float* ua = U + (int64_t)(co0 + li) * nchunks * 256 + kq * 4;
 
-  // Persistent blocks over the tile list (tile t -> channel group t % ncog
-  // fastest, so the groups reading one input tile run back to back on one
-  // XCD; then tile column, tile row, image); block b of XCD b % 8 walks a
-  // contiguous range of it.  The next tile's first patches are loaded while
-  // the current tile's last chunk multiplies, so the input latency hides
-  // behind MFMAs also when a conv has one or two 16-channel chunks.
-  int t0 = blockIdx.x, tstep = gridDim.x, tend = total;
-  if (gridDim.x % 8 == 0 && total >= (int)gridDim.x) {
-    const int span = (total + 7) / 8, grp = blockIdx.x & 7;
-    t0 = grp * span + (blockIdx.x >> 3);
-    tstep = gridDim.x >> 3;
-    tend = (grp + 1) * span < total ? (grp + 1) * span : total;
-  }
-  if (t0 >= tend) return;
-  struct TG {
-    int cog, bc, br, img;
-  };
-  auto decode = [&](int t) {
-    TG g;
-    g.cog = t % ncog;
-    int rest = t / ncog;
-    g.bc = rest % bcols;
-    rest /= bcols;
-    g.br = rest % brows;
-    g.img = rest / brows;
-    return g;
-  };
-  auto urow = [&](int cog) {  // this lane's U row: output channel co0 + li of group cog
-    return U + (int64_t)(cog * CO_B + wco + li) * nchunks * 256 + kq * 4;
-  };
-
-  // patch loader state (the tile being LOADED): p = tid + 256 pp -> (channel
-  // p / NTB, tile p % NTB) with its 4 x 4 patch's top-left input (gr, gc);
-  // clamped offsets at load time, in-range masks at transform time (only the
-  // two corner coordinates live across the MFMAs: registers are the limit)
-  int gr[PPT], gc[PPT];
-  // the loaded tile's image as a buffer resource (wave-uniform: built from
-  // readfirstlane'd halves): 32-bit byte offsets, no 64-bit per-lane addresses
-  const uint32_t img_bytes = (uint32_t)(4 * (int64_t)ci_n * hw);  // < 2^32 (wino_geo)
-  __amdgpu_buffer_rsrc_t xr;
-  auto setup = [&](const TG& g) {
-    const uint64_t a = (uint64_t)(x + (int64_t)g.img * ci_n * hw);
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    xr = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, (int)img_bytes, 0x00020000);
+  // patch loader: p = tid + 256 pp -> (channel p / NTB, tile p % NTB)
+  const int r0 = (br * kTRB) * 2 - 1, c0 = (bc * TCB) * 2 - 1;
+  int poff[PPT][4], pcol[PPT][4];
+  uint32_t pmask[PPT];
 #pragma unroll
-    for (int pp = 0; pp < PPT; ++pp) {
-      const int tl = (tid + 256 * pp) % NTB;
-      gr[pp] = (g.br * kTRB + tl / TCB) * 2 - 1;
-      gc[pp] = (g.bc * TCB + tl % TCB) * 2 - 1;
+  for (int pp = 0; pp < PPT; ++pp) {
+    const int p = tid + 256 * pp, tl = p % NTB;
+    const int gr = r0 + 2 * (tl / TCB), gc = c0 + 2 * (tl % TCB);
+    uint32_t m = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int rr = gr + i, cc = gc + i;
+      m |= (rr >= 0 && rr < h ? 1u : 0u) << i;
+      m |= (cc >= 0 && cc < w ? 1u : 0u) << (4 + i);
+      poff[pp][i] = (rr < 0 ? 0 : (rr >= h ? h - 1 : rr)) * w;
+      pcol[pp][i] = cc < 0 ? 0 : (cc >= w ? w - 1 : cc);
     }
-  };
+    pmask[pp] = m;
+  }
   float pv[PPT][16];
   auto load = [&](int chunk) {
-    const uint32_t cbase = (uint32_t)(chunk * kCIC) * (uint32_t)hw;
 #pragma unroll
     for (int pp = 0; pp < PPT; ++pp) {
-      const uint32_t cho = cbase + (uint32_t)((tid + 256 * pp) / NTB) * (uint32_t)hw;
-      uint32_t ro[4], co[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rr = gr[pp] + i, cc = gc[pp] + i;
-        ro[i] = cho + (uint32_t)((rr < 0 ? 0 : (rr >= h ? h - 1 : rr)) * w);
-        co[i] = (uint32_t)(cc < 0 ? 0 : (cc >= w ? w - 1 : cc));
-      }
+      const int ch = (tid + 256 * pp) / NTB;
+      const float* src = xb + (int64_t)(chunk * kCIC + ch) * hw;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          pv[pp][4 * i + j] = __builtin_bit_cast(
-              float, __builtin_amdgcn_raw_buffer_load_b32(xr, (int)(4 * (ro[i] + co[j])), 0, 0));
+        for (int j = 0; j < 4; ++j) pv[pp][4 * i + j] = src[poff[pp][i] + pcol[pp][j]];
     }
   };
   // B^T d B into V[xi][16-tile group][ci][16]
@@ -202,8 +170,7 @@ __global__ void __launch_bounds__(256, CO_B == 16 ? 1 : 2)
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int rr = gr[pp] + i, cc = gc[pp] + j;
-          const bool ok = rr >= 0 && rr < h && cc >= 0 && cc < w;
+          const bool ok = ((pmask[pp] >> i) & 1u) && ((pmask[pp] >> (4 + j)) & 1u);
           d[i][j] = ok ? pv[pp][4 * i + j] : 0.f;
         }
       float t[4][4];  // B^T d: rows d0 - d2, d1 + d2, d2 - d1, d1 - d3
@@ -225,157 +192,126 @@ __global__ void __launch_bounds__(256, CO_B == 16 ? 1 : 2)
     }
   };
 
+  f4 acc[16][NTW];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
+
   // A operands (U rows, L2-resident) through a 4-deep register ring: the
-  // float4 of step xi is loaded 4 steps (>= 16 MFMAs) ahead, across chunk and
-  // tile boundaries too, so the L2 latency is never waited on right after the load
+  // float4 of step xi is loaded 4 steps (>= 16 MFMAs) ahead, across the chunk
+  // boundary too, so the L2 latency is never waited on right after the load
   constexpr int RING = 4;
   f4 ring[RING];
-  {
-    const TG g = decode(t0);
-    const float* ua = urow(g.cog);
 #pragma unroll
-    for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 16);
-    setup(g);
-    load(0);
+  for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 16);
+  load(0);
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    __syncthreads();  // the previous chunk's V readers are done
+    transform();
+    __syncthreads();
+    if (chunk + 1 < nchunks) load(chunk + 1);
+    const float* uc = ua + (int64_t)chunk * 256;
+    const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 256;
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      const f4 a = ring[xi % RING];
+      ring[xi % RING] = *reinterpret_cast<const f4*>(
+          xi + RING < 16 ? uc + (xi + RING) * 16 : un + (xi + RING - 16) * 16);
+      // keep the load here: the scheduler otherwise sinks it next to its use
+      // (register pressure) and every step waits on L2 again
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int n = 0; n < NTW; ++n)
+          acc[xi][n] = mfma(a[s], V[xi][nt0 + n][(4 * s + kq) * 16 + li], acc[xi][n]);
+    }
   }
-  for (int t = t0; t < tend; t += tstep) {
-    const TG g = decode(t);
-    const int tn = t + tstep;
-    const bool more = tn < tend;
-    const TG gn = decode(more ? tn : t);
-    const float* ua = urow(g.cog);
-    const float* ua_next = urow(gn.cog);
-    f4 acc[16][NTW];
-#pragma unroll
-    for (int xi = 0; xi < 16; ++xi)
-#pragma unroll
-      for (int n = 0; n < NTW; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
-    for (int chunk = 0; chunk < nchunks; ++chunk) {
-      __syncthreads();  // the previous chunk's V readers (and stats readers) are done
-      transform();
-      __syncthreads();
-      const bool last = chunk + 1 == nchunks;
-      if (!last) {
-        load(chunk + 1);
-      } else if (more) {
-        setup(gn);  // corners now belong to the next tile's patches
-        load(0);
-      }
-      const float* uc = ua + (int64_t)chunk * 256;
-      const float* un = last ? ua_next : ua + (int64_t)(chunk + 1) * 256;
-#pragma unroll
-      for (int xi = 0; xi < 16; ++xi) {
-        const f4 a = ring[xi % RING];
-        ring[xi % RING] = *reinterpret_cast<const f4*>(
-            xi + RING < 16 ? uc + (xi + RING) * 16 : un + (xi + RING - 16) * 16);
-        // keep the load here: the scheduler otherwise sinks it next to its use
-        // (register pressure) and every step waits on L2 again
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int n = 0; n < NTW; ++n)
-            acc[xi][n] = mfma(a[s], V[xi][nt0 + n][(4 * s + kq) * 16 + li], acc[xi][n]);
-      }
-    }
 
-    // A^T M A per (channel, tile): lane holds channels co0 + 4 kq + r, tile 16 (nt0 + n) + li
-    const int co0 = g.cog * CO_B + wco;
-    float* yb = y + (int64_t)g.img * co_n * hw;
-    mde::Sh run[STATS ? 4 : 1];
+  // A^T M A per (channel, tile): lane holds channels co0 + 4 kq + r, tile 16 (nt0 + n) + li
+  float* yb = y + (int64_t)img * co_n * hw;
+  mde::Sh run[STATS ? 4 : 1];
 #pragma unroll
-    for (int n = 0; n < NTW; ++n) {
-      const int tl = 16 * (nt0 + n) + li;
-      const int oy = 2 * (g.br * kTRB + tl / TCB), ox = 2 * (g.bc * TCB + tl % TCB);
+  for (int n = 0; n < NTW; ++n) {
+    const int tl = 16 * (nt0 + n) + li;
+    const int oy = 2 * (br * kTRB + tl / TCB), ox = 2 * (bc * TCB + tl % TCB);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float u0[4], u1[4];
+    for (int r = 0; r < 4; ++r) {
+      float u0[4], u1[4];
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const float m0 = acc[b][n][r], m1 = acc[4 + b][n][r], m2 = acc[8 + b][n][r],
-                      m3 = acc[12 + b][n][r];
-          u0[b] = (m0 + m1) + m2;
-          u1[b] = (m1 - m2) - m3;
-        }
-        const float y00 = (u0[0] + u0[1]) + u0[2], y01 = (u0[1] - u0[2]) - u0[3];
-        const float y10 = (u1[0] + u1[1]) + u1[2], y11 = (u1[1] - u1[2]) - u1[3];
-        if constexpr (STATS) {
-          const bool ok0 = oy < h && ox < w, ok1 = oy + 1 < h && ox < w;
-          if (n == 0)  // the shift: the channel's value at this wave's first tile (li = 0)
-            run[r] = {__shfl(ok0 ? y00 : 0.f, lane & 48, 64), 0.f, 0.f, 0.f};
-          mde::sh_add(run[r], y00, ok0);
-          mde::sh_add(run[r], y01, ok0);
-          mde::sh_add(run[r], y10, ok1);
-          mde::sh_add(run[r], y11, ok1);
-        }
-        float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
-        if (oy < h) {
-          if (ox + 1 < w) {
-            *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
-          } else if (ox < w) {
-            dst[0] = y00;
-          }
-        }
-        if (oy + 1 < h) {
-          if (ox + 1 < w) {
-            *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
-          } else if (ox < w) {
-            dst[w] = y10;
-          }
+      for (int b = 0; b < 4; ++b) {
+        const float m0 = acc[b][n][r], m1 = acc[4 + b][n][r], m2 = acc[8 + b][n][r],
+                    m3 = acc[12 + b][n][r];
+        u0[b] = (m0 + m1) + m2;
+        u1[b] = (m1 - m2) - m3;
+      }
+      const float y00 = (u0[0] + u0[1]) + u0[2], y01 = (u0[1] - u0[2]) - u0[3];
+      const float y10 = (u1[0] + u1[1]) + u1[2], y11 = (u1[1] - u1[2]) - u1[3];
+      if constexpr (STATS) {
+        const bool ok0 = oy < h && ox < w, ok1 = oy + 1 < h && ox < w;
+        if (n == 0)  // the shift: the channel's value at this wave's first tile (li = 0)
+          run[r] = {__shfl(ok0 ? y00 : 0.f, lane & 48, 64), 0.f, 0.f, 0.f};
+        mde::sh_add(run[r], y00, ok0);
+        mde::sh_add(run[r], y01, ok0);
+        mde::sh_add(run[r], y10, ok1);
+        mde::sh_add(run[r], y11, ok1);
+      }
+      float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
+      if (oy < h) {
+        if (ox + 1 < w) {
+          *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
+        } else if (ox < w) {
+          dst[0] = y00;
         }
       }
-    }
-    if constexpr (STATS) {
-      // the 16 lanes of a k-group share its 4 channels: butterfly over li, then
-      // the waves holding the same channels (other tile groups) merged in wave
-      // order through LDS; one record per channel and tile
-      constexpr int NWN = 4 / WCO;  // waves per channel set
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        mde::Sh a = run[r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
-        if (li == 0) {
-          float* p4 = part + (wv * 16 + 4 * kq + r) * 4;
-          p4[0] = a.ref;
-          p4[1] = a.n;
-          p4[2] = a.s1;
-          p4[3] = a.s2;
+      if (oy + 1 < h) {
+        if (ox + 1 < w) {
+          *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
+        } else if (ox < w) {
+          dst[w] = y10;
         }
-      }
-      __syncthreads();
-      if (tid < CO_B) {
-        const int wc = tid / 16, c16 = tid % 16;  // channel set (wave % WCO), channel within
-        mde::Sh a{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < NWN; ++k) {
-          const float* p4 = part + ((k * WCO + wc) * 16 + c16) * 4;
-          a = k == 0 ? mde::Sh{p4[0], p4[1], p4[2], p4[3]}
-                     : mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
-        }
-        const int G = total / ncog;
-        float* o4 = stats + ((int64_t)(g.cog * CO_B + tid) * G + t / ncog) * 4;
-        o4[0] = a.ref;
-        o4[1] = a.n;
-        o4[2] = a.s1;
-        o4[3] = a.s2;
       }
     }
   }
-}
-
-// resident 256-thread blocks of a kernel on this device (CUs x occupancy), x8
-template <auto Kernel>
-int wino_resident() {
-  static const int cached = [] {
-    int dev = 0, cus = 0, per = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, Kernel, 256, 0);
-    const int r = (cus > 0 ? cus : 256) * (per > 0 ? per : 1);
-    return r / 8 * 8 > 0 ? r / 8 * 8 : 8;
-  }();
-  return cached;
+  if constexpr (STATS) {
+    // the 16 lanes of a k-group share its 4 channels: butterfly over li, then
+    // the waves holding the same channels (other tile groups) merged in wave
+    // order through LDS (V reused once every wave is past its last read)
+    constexpr int NWN = 4 / WCO;  // waves per channel set
+    __syncthreads();
+    float* part = &V[0][0][0];  // [wave][16 channels][4]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mde::Sh a = run[r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
+      if (li == 0) {
+        float* p4 = part + (wv * 16 + 4 * kq + r) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
+    }
+    __syncthreads();
+    if (tid < CO_B) {
+      const int wc = tid / 16, c16 = tid % 16;  // channel set (wave % WCO), channel within
+      mde::Sh a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < NWN; ++k) {
+        const float* p4 = part + ((k * WCO + wc) * 16 + c16) * 4;
+        a = k == 0 ? mde::Sh{p4[0], p4[1], p4[2], p4[3]}
+                   : mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      const int G = total / ncog, gb = l / ncog;
+      float* o4 = stats + ((int64_t)(cog * CO_B + tid) * G + gb) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
+    }
+  }
 }
 
 struct WinoGeo {
@@ -388,10 +324,9 @@ inline bool wino_geo(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, Wi
     return false;
   if (w % 2) return false;  // float2 output stores at even offsets
   if (n * ci * h * w >= ((int64_t)1 << 31) || n * co * h * w >= ((int64_t)1 << 31)) return false;
-  if (ci * h * w >= ((int64_t)1 << 30)) return false;  // an image's bytes: one buffer resource
   g->co_b = co % 64 == 0 ? 64 : (co == 16 ? 16 : 32);
   g->ncog = (int)(co / g->co_b);
-  g->bcols = (int)mde::cdiv(w, g->co_b == 16 ? 32 : (g->co_b == 32 ? 16 : 8));
+  g->bcols = (int)mde::cdiv(w, g->co_b == 16 ? 32 : 16);
   g->brows = (int)mde::cdiv(h, 2 * kTRB);
   g->total = n * g->ncog * g->bcols * g->brows;
   return g->total < 0x7fffffff;
@@ -443,15 +378,10 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
   hipStream_t s = (hipStream_t)stream;
   const double flops = 2.0 * 9 * n * h * w * (double)cin * cout;  // direct-conv equivalent
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
-  // persistent: the resident blocks (a multiple of 8), at most one per tile
-  const int resident = g.co_b == 64   ? wino_resident<wino_f23_kernel<64, false>>()
-                       : g.co_b == 32 ? wino_resident<wino_f23_kernel<32, false>>()
-                                      : wino_resident<wino_f23_kernel<16, false>>();
-  const int64_t nb = g.total < resident ? (g.total + 7) / 8 * 8 : resident;
-  const dim3 grid((unsigned)nb), block(256);
+  const dim3 grid((unsigned)((g.total + 7) / 8 * 8)), block(256);
   const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
 #define MDE_WINO(CB, TC, ST)                                                                      \
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, ST>), grid, block, 0, x, u, y,       \
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST>), grid, block, 0, x, u, y,   \
                   (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \
                   stats)
   if (stats) {

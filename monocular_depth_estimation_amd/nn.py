@@ -732,13 +732,16 @@ def conv3x3_passes(conv: nn.Conv2d, x):
     p = [bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
          for i, f in enumerate(p)]
     if dt == _abi.MDE_F32 and WINO_ON and not _autocast_bf16(x):
-        # forward / data gradient of the 32-256-channel convs on the Winograd
+        # forward / data gradient of the 64-256-channel convs on the Winograd
         # F(2x2, 3x3) kernels (2.25x fewer MACs) where MIOpen would run its own
-        # Winograd: planes of >= 256 blocks (8 x 16 output pixels x 64 channels)
+        # Winograd: 64-channel output groups (the 16 / 32-channel variants lose
+        # to MIOpen / the direct kernel: the input transform is amortised over
+        # too few output channels, tools/c1_bench.py) on planes of >= 256
+        # blocks (8 x 16 output pixels x 64 channels)
         n, h, w = x.shape[0], x.shape[2], x.shape[3]
         for i, (a, b) in enumerate(((cin, cout), (cout, cin))):
-            blocks = n * -(-h // 8) * -(-w // 16) * max(b // 64, 1)
-            if (not p[i] and blocks >= 256
+            blocks = n * -(-h // 8) * -(-w // 16) * (b // 64)
+            if (not p[i] and b % 64 == 0 and blocks >= 256
                     and _abi.query("mde_wino_supported", a, b, h, w, _abi.MDE_F32)):
                 p[i] = WINO
     if dt == _abi.MDE_F32 and C3_WIDE and not _autocast_bf16(x):

@@ -189,3 +189,36 @@ def test_batchnorm_bf16_storage_matches_fp32_kernel(shape, act, res):
     if res:
         assert torch.equal(gb[3], gf[3].bfloat16())
     assert torch.equal(mb, mf) and torch.equal(vb, vf)
+
+
+@pytest.mark.parametrize("shape", [(32, 24, 15, 20), (32, 16, 8, 10), (16, 8, 2, 3),
+                                   (4, 16, 30, 40), (64, 8, 15, 20)])
+@pytest.mark.parametrize("act,res", [("relu", True), ("none", False), ("relu", False)])
+def test_batchnorm_bf16_storage_matches_fp32_kernel(shape, act, res):
+    """bf16 storage (cfg3 autocast) == the fp32 kernel on the same, rounded
+    values, bitwise after rounding: both dtypes sum the same fp32 values in the
+    same order (one-block-per-channel small-tensor kernels, table and plane
+    apply), so only the final bf16 rounding differs."""
+    from monocular_depth_estimation_amd.nn import BatchNorm2d
+    n, c, h, w = shape
+    xb = torch.from_numpy(seeded(shape, 41, -2, 3)).to(DEV).bfloat16()
+    rb = torch.from_numpy(seeded(shape, 42, -1, 1)).to(DEV).bfloat16() if res else None
+    gb = torch.from_numpy(seeded(shape, 43, -1, 1)).to(DEV).bfloat16()
+    outs = []
+    for dt in (torch.bfloat16, torch.float32):
+        bn = BatchNorm2d(c, act=act).to(DEV).train()
+        with torch.no_grad():
+            bn.weight.copy_(torch.from_numpy(seeded((c,), 44, 0.5, 1.5)))
+            bn.bias.copy_(torch.from_numpy(seeded((c,), 45, -0.5, 0.5)))
+        x = xb.to(dt).requires_grad_(True)
+        r = rb.to(dt).requires_grad_(True) if res else None
+        y = bn(x, residual=r)
+        y.backward(gb.to(dt))
+        outs.append((y.detach(), x.grad, r.grad if res else None, bn.weight.grad, bn.running_var))
+    (yb, gxb, grb, gwb, rvb), (yf, gxf, grf, gwf, rvf) = outs
+    assert torch.equal(yb, yf.bfloat16()), "y"
+    assert torch.equal(gxb, gxf.bfloat16()), "dx"
+    if res:
+        assert torch.equal(grb, grf.bfloat16()), "dresidual"
+    assert torch.equal(gwb, gwf), "dgamma"
+    assert torch.equal(rvb, rvf), "running_var"

@@ -15,6 +15,7 @@
 // partials go to a per-block slab summed in block order by loss_final_kernel
 // (deterministic).
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -334,8 +335,16 @@ __global__ void __launch_bounds__(256)
     const f2 wr = pk(c0 == w - 2 ? 2.f : 1.f, c1 == w - 2 ? 2.f : 1.f);
     const int64_t base = img * h * w;
     const int o0 = reflect1(c0, w), o1 = reflect1(c1, w);
-    const float* X = xp + base;
-    const float* Y = yp + base;
+    // the image's planes as buffer resources (wave-uniform base, 32-bit lane
+    // offsets): no 64-bit address arithmetic per load
+    auto rsrc = [&](const float* p) {
+      const uint64_t a = (uint64_t)(p + base);
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+      const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+      return __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo),
+                                               0, (int)(4 * h * w), 0x00020000);
+    };
+    const __amdgpu_buffer_rsrc_t XR = rsrc(xp), YR = rsrc(yp);
     float tmn = 0.f, tden = 1.f;
     const bool norm = mm != nullptr;
     if (norm) {
@@ -354,10 +363,13 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int f = 0; f < NC; ++f) cs[i][f] = pk(0.f, 0.f);
     }
+    auto ld = [&](__amdgpu_buffer_rsrc_t R, int off) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(R, 4 * off, 0, 0));
+    };
     auto load = [&](int r, f2& xv, f2& yv) {
-      const int64_t off = (int64_t)reflect1(r, h) * w;
-      xv = pk(X[off + o0], X[off + o1]);
-      const float t0 = Y[off + o0], t1 = Y[off + o1];
+      const int off = reflect1(r, h) * w;
+      xv = pk(ld(XR, off + o0), ld(XR, off + o1));
+      const float t0 = ld(YR, off + o0), t1 = ld(YR, off + o1);
       yv = norm ? pk((t0 - tmn) / tden, (t1 - tmn) / tden) : pk(t0, t1);
     };
     // 3-wide horizontal sums of a column pair: (prev lane's c1) + c0 + c1, c0 + c1 + (next's c0)
@@ -366,7 +378,12 @@ __global__ void __launch_bounds__(256)
       return f2{wa.x * p + v.x + wb.x * v.y, wa.y * v.x + v.y + wb.y * n};
     };
     const f2 one2 = pk(1.f, 1.f);
-    auto step = [&](f2 xv, f2 yv, int r) {
+    // one padded row r: PH 0 = horizontal sums only (r < g0), 1 = + the
+    // statistics / coefficients of centre row r - 1 (no gradient row yet),
+    // 2 = + gradient row r - 2.  No wave-uniform early returns: the main loop
+    // runs PH 2 only, so its unrolled body has no joins (no ring moves).
+    auto step = [&](auto ph, f2 xv, f2 yv, int r) {
+      constexpr int PH = decltype(ph)::value;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         xr[i] = xr[i + 1];
@@ -381,92 +398,108 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int f = 0; f < 5; ++f) hs[2][f] = hsum(v[f], one2, one2);
       }
-      if (r < g0) return;  // wave-uniform
-      const int p = r - 1;
-      const bool prow = p >= 0 && p < h;
-      const bool v0 = in0 && prow, v1 = in1 && prow;
-      f2 st[5];
+      if constexpr (PH >= 1) {
+        const int p = r - 1;
+        const bool prow = p >= 0 && p < h;
+        const bool v0 = in0 && prow, v1 = in1 && prow;
+        f2 st[5];
 #pragma unroll
-      for (int f = 0; f < 5; ++f) st[f] = (hs[0][f] + hs[1][f] + hs[2][f]) * inv9;
-      const f2 mx = st[0], my = st[1];
-      const f2 sxx = st[2] - mx * mx, syy = st[3] - my * my;
-      const f2 sxy = st[4] - mx * my;
-      const f2 n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
-      const f2 d1 = mx * mx + my * my + kC1, d2 = sxx + syy + kC2;
-      const f2 D = d1 * d2;
-      const f2 nn = n1 * n2;
-      const f2 S = pk(nn.x / D.x, nn.y / D.y);  // exact division: S(x, x) = 1
-      const f2 fl = (one2 - S) * 0.5f;
-      if (p < g1 && p >= g0) {
-        if (out0) lsum += fminf(fmaxf(fl.x, 0.f), 1.f);
-        if (out1) lsum += fminf(fmaxf(fl.y, 0.f), 1.f);
+        for (int f = 0; f < 5; ++f) st[f] = (hs[0][f] + hs[1][f] + hs[2][f]) * inv9;
+        const f2 mx = st[0], my = st[1];
+        const f2 sxx = st[2] - mx * mx, syy = st[3] - my * my;
+        const f2 sxy = st[4] - mx * my;
+        const f2 n1 = 2.f * mx * my + kC1, n2 = 2.f * sxy + kC2;
+        const f2 d1 = mx * mx + my * my + kC1, d2 = sxx + syy + kC2;
+        const f2 D = d1 * d2;
+        const f2 nn = n1 * n2;
+        const f2 S = pk(nn.x / D.x, nn.y / D.y);  // exact division: S(x, x) = 1
+        const f2 fl = (one2 - S) * 0.5f;
+        const float lw = (p < g1 && p >= g0) ? 1.f : 0.f;  // the chunk's own centre rows
+        lsum += lw * ((out0 ? fminf(fmaxf(fl.x, 0.f), 1.f) : 0.f) +
+                      (out1 ? fminf(fmaxf(fl.y, 0.f), 1.f) : 0.f));
+        const bool a0 = v0 && fl.x >= 0.f && fl.x <= 1.f, a1 = v1 && fl.y >= 0.f && fl.y <= 1.f;
+        const f2 rD = pk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y));
+        const f2 rd1 = pk(__builtin_amdgcn_rcpf(d1.x), __builtin_amdgcn_rcpf(d1.y));
+        const f2 rd2 = pk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y));
+        const f2 dS_dsx = -S * rd2;
+        const f2 dS_dsxy = 2.f * n1 * rD;
+        const f2 dS_dmx = 2.f * my * n2 * rD - S * 2.f * mx * rd1;
+        f2 c[NC];
+        c[0] = k * (dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy);
+        c[1] = k * dS_dsx;
+        c[2] = k * dS_dsxy;
+        if constexpr (GT) {
+          const f2 dS_dmy = 2.f * mx * n2 * rD - S * 2.f * my * rd1;
+          c[3] = k * (dS_dmy - 2.f * my * dS_dsx - mx * dS_dsxy);
+          c[NC - 1] = c[1];
+        }
+#pragma unroll
+        for (int f = 0; f < NC; ++f) c[f] = pk(a0 ? c[f].x : 0.f, a1 ? c[f].y : 0.f);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int f = 0; f < NC; ++f) cs[i][f] = cs[i + 1][f];
+#pragma unroll
+        for (int f = 0; f < NC; ++f) cs[2][f] = hsum(c[f], wl, wr);
       }
-      const bool a0 = v0 && fl.x >= 0.f && fl.x <= 1.f, a1 = v1 && fl.y >= 0.f && fl.y <= 1.f;
-      const f2 rD = pk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y));
-      const f2 rd1 = pk(__builtin_amdgcn_rcpf(d1.x), __builtin_amdgcn_rcpf(d1.y));
-      const f2 rd2 = pk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y));
-      const f2 dS_dsx = -S * rd2;
-      const f2 dS_dsxy = 2.f * n1 * rD;
-      const f2 dS_dmx = 2.f * my * n2 * rD - S * 2.f * mx * rd1;
-      f2 c[NC];
-      c[0] = k * (dS_dmx - 2.f * mx * dS_dsx - my * dS_dsxy);
-      c[1] = k * dS_dsx;
-      c[2] = k * dS_dsxy;
-      if constexpr (GT) {
-        const f2 dS_dmy = 2.f * mx * n2 * rD - S * 2.f * my * rd1;
-        c[3] = k * (dS_dmy - 2.f * my * dS_dsx - mx * dS_dsxy);
-        c[NC - 1] = c[1];
-      }
+      if constexpr (PH == 2) {
+        const int g = r - 2;  // in [g0, g1) for every PH-2 row
+        const float vt = g == 1 ? 2.f : 1.f, vb = g == h - 2 ? 2.f : 1.f;
+        f2 sm[NC];
 #pragma unroll
-      for (int f = 0; f < NC; ++f) c[f] = pk(a0 ? c[f].x : 0.f, a1 ? c[f].y : 0.f);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int f = 0; f < NC; ++f) cs[i][f] = cs[i + 1][f];
-#pragma unroll
-      for (int f = 0; f < NC; ++f) cs[2][f] = hsum(c[f], wl, wr);
-      const int g = p - 1;
-      if (g < g0 || g >= g1) return;  // wave-uniform
-      const float vt = g == 1 ? 2.f : 1.f, vb = g == h - 2 ? 2.f : 1.f;
-      f2 sm[NC];
-#pragma unroll
-      for (int f = 0; f < NC; ++f) sm[f] = (vt * cs[0][f] + cs[1][f]) + vb * cs[2][f];
-      const f2 x0 = xr[0], y0 = yr[0];
-      const f2 diff = x0 - y0;
-      const f2 sgn = pk(diff.x > 0.f ? 1.f : (diff.x < 0.f ? -1.f : 0.f),
-                        diff.y > 0.f ? 1.f : (diff.y < 0.f ? -1.f : 0.f));
-      if (out0) l1sum += fabsf(diff.x);
-      if (out1) l1sum += fabsf(diff.y);
-      const int64_t off = base + (int64_t)g * w + c0;
-      if (gx) {
-        const f2 v = (sm[0] + 2.f * x0 * sm[1] + y0 * sm[2]) * inv9 + gs_l1 * sgn;
-        if (out0) gx[off] = v.x;
-        if (out1) gx[off + 1] = v.y;
-      }
-      if constexpr (GT) {
-        if (gy) {
+        for (int f = 0; f < NC; ++f) sm[f] = (vt * cs[0][f] + cs[1][f]) + vb * cs[2][f];
+        const f2 x0 = xr[0], y0 = yr[0];
+        const f2 diff = x0 - y0;
+        const f2 sgn = pk(diff.x > 0.f ? 1.f : (diff.x < 0.f ? -1.f : 0.f),
+                          diff.y > 0.f ? 1.f : (diff.y < 0.f ? -1.f : 0.f));
+        l1sum += (out0 ? fabsf(diff.x) : 0.f) + (out1 ? fabsf(diff.y) : 0.f);
+        const int64_t off = base + (int64_t)g * w + c0;
+        {
+          const f2 v = (sm[0] + 2.f * x0 * sm[1] + y0 * sm[2]) * inv9 + gs_l1 * sgn;
+          if (out0) gx[off] = v.x;
+          if (out1) gx[off + 1] = v.y;
+        }
+        if constexpr (GT) {
           const f2 v = (sm[3] + 2.f * y0 * sm[NC - 1] + x0 * sm[2]) * inv9 - gs_l1 * sgn;
           if (out0) gy[off] = v.x;
           if (out1) gy[off + 1] = v.y;
         }
       }
     };
-    f2 cx[4], cy[4];
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    // rows rs .. rs + 3: the rings fill (PH 0, 0, 1, 1); then the chunk's own
+    // rows in groups of 6 (a multiple of the 3-row rings: a group leaves them
+    // where it found them, so the unrolled body needs no register moves),
+    // the next group's loads issued before this one's math (clamped to row re:
+    // no rows of the next chunk); the last < 6 rows one by one
+    constexpr int GR = 6;
+    f2 px[4], py[4], cx[GR], cy[GR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) load(rs + i, cx[i], cy[i]);
-    for (int r = rs; r <= re; r += 4) {
-      f2 nx[4], ny[4];
+    for (int i = 0; i < 4; ++i) load(rs + i, px[i], py[i]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) load(min(r + 4 + i, re), nx[i], ny[i]);
+    for (int i = 0; i < GR; ++i) load(min(rs + 4 + i, re), cx[i], cy[i]);
+    step(P0{}, px[0], py[0], rs);
+    step(P0{}, px[1], py[1], rs + 1);
+    step(P1{}, px[2], py[2], rs + 2);
+    step(P1{}, px[3], py[3], rs + 3);
+    int r = rs + 4;
+    for (; r + GR - 1 <= re; r += GR) {
+      f2 nx[GR], ny[GR];
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (r + i <= re) step(cx[i], cy[i], r + i);
+      for (int i = 0; i < GR; ++i) load(min(r + GR + i, re), nx[i], ny[i]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < GR; ++i) step(P2{}, cx[i], cy[i], r + i);
+#pragma unroll
+      for (int i = 0; i < GR; ++i) {
         cx[i] = nx[i];
         cy[i] = ny[i];
       }
     }
+#pragma unroll
+    for (int i = 0; i < GR - 1; ++i)
+      if (r + i <= re) step(P2{}, cx[i], cy[i], r + i);
   }
   const float ts = mde::block_sum256(lsum, red);
   const float tl = mde::block_sum256(l1sum, red);
@@ -496,10 +529,13 @@ inline bool ssim_pair() {
 // bound (84-88 us for 2816-8192 waves); fewer, taller chunks cut the halo
 // re-reads (PMC: 1.79x algorithmic at 20-row chunks with the old prefetch
 // overrun, 1.59x with the overrun clamped).
-inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w) {
+// pair: plan for ssim3_pair_kernel when it can take the shape (and the
+// caller wants the prediction's gradient), else for ssim3_stream_kernel.
+inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w, bool pair) {
   StreamPlan p;
   p.pair_sw = 0;
-  if (ssim_pair()) {  // strips of <= 124 columns (62 lane pairs + 2 halo lanes), even widths
+  if (pair && ssim_pair() && h * w < ((int64_t)1 << 29)) {  // strips of <= 124 columns (62 lane pairs
+                                                     // + 2 halo lanes); a plane's bytes < 2^31
     p.strips = (int)mde::cdiv(w, 124);
     p.pair_sw = (int)(mde::cdiv(mde::cdiv(w, p.strips), 2) * 2);
   } else {
@@ -518,6 +554,8 @@ inline StreamPlan stream_plan(int64_t b, int64_t h, int64_t w) {
   if (ch > maxc) ch = maxc;
   if (ch < 1) ch = 1;
   p.chunk_rows = (int)mde::cdiv(h, ch);
+  // the pair kernel steps its chunk's rows in groups of 6: whole groups
+  if (p.pair_sw && p.chunk_rows > 6) p.chunk_rows = p.chunk_rows / 6 * 6;
   p.chunks = (int)mde::cdiv(h, p.chunk_rows);
   p.nwaves = per_chunk * p.chunks;
   p.nblocks = mde::cdiv(p.nwaves, 4);
@@ -590,7 +628,8 @@ int mde_depthnorm_apply(const void* x, const float* minmax, void* y,
 
 size_t mde_ssim3_l1_workspace(int64_t b, int64_t h, int64_t w) {
   if (b <= 0 || h <= 0 || w <= 0) return 0;
-  return sizeof(float) * 2 * (size_t)stream_plan(b, h, w).nblocks;
+  const int64_t a = stream_plan(b, h, w, true).nblocks, c = stream_plan(b, h, w, false).nblocks;
+  return sizeof(float) * 2 * (size_t)(a > c ? a : c);
 }
 
 int mde_ssim3_l1_fwd(const void* pred, const void* target,
@@ -602,7 +641,7 @@ int mde_ssim3_l1_fwd(const void* pred, const void* target,
   if (!pred || !target || !loss || !workspace || b <= 0 || h < 2 || w < 2 ||
       h > (1 << 24) || w > (1 << 24))
     return MDE_ERR_INVALID_ARG;
-  const StreamPlan sp = stream_plan(b, h, w);
+  const StreamPlan sp = stream_plan(b, h, w, grad_pred != nullptr);
   const int64_t nblocks = sp.nblocks;
   if (nblocks > 0x7fffffff) return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;

@@ -81,10 +81,11 @@ def test_workspace_queries():
     lib = _abi.load()
     # SE: partial slab per (n, c, 16384-element chunk) + three per-sample vectors
     assert lib.mde_se_workspace(32, 16, 16, 480, 640) >= 4 * 32 * 16 * 19
-    # SSIM: one (ssim, l1) pair per block of 4 waves; a wave = 108-column strip
-    # (two columns a lane) x 32-row chunk (6 strips x 15 chunks per 480x640
-    # image: 2880 waves)
-    assert lib.mde_ssim3_l1_workspace(32, 480, 640) == 4 * 2 * (32 * 6 * 15 // 4)
+    # SSIM: one (ssim, l1) pair per block of 4 waves, sized for the larger of
+    # the two kernels' plans: the two-column kernel's 108-column strips x
+    # 30-row chunks (6 x 16 per 480x640 image) and the one-column kernel's
+    # 60-column strips x 30-row chunks (11 x 16)
+    assert lib.mde_ssim3_l1_workspace(32, 480, 640) == 4 * 2 * (32 * 11 * 16 // 4)
     assert lib.mde_minmax_workspace(10) >= 8
     assert lib.mde_skip_reduce_workspace(32, 64, 32, 120, 160) >= 4 * (64 * 32 + 32)
     assert lib.mde_depth_loss_workspace(2, 24, 32) >= 4 * 3 * 2 * 24 * 32

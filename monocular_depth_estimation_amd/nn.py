@@ -756,7 +756,9 @@ def conv3x3_passes(conv: nn.Conv2d, x):
 
 WIDE = 2  # conv3x3_passes flag: the pass runs on the wide-channel kernel
 WINO = 3  # conv3x3_passes flag: the pass runs on the Winograd kernel
-WINO_ON = os.environ.get("MDE_WINO", "0") == "1"  # A/B switch until measured on the GPU
+# MDE_WINO=0: MIOpen for these passes (A/B switch; cfg2 interleaved A/B 911.6 /
+# 909.0 vs 881.0 / 878.3 img/s, profiles/r04_ab_wino.txt)
+WINO_ON = os.environ.get("MDE_WINO", "1") != "0"
 # Off by default: MIOpen's Winograd matches the stride-1 band kernel on these
 # shapes (tools/c1_bench.py) and the cfg2 step was 0.5 % slower with it on
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"

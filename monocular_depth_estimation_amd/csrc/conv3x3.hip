@@ -681,6 +681,10 @@ inline int reduce_slices(int groups, int g, int m) {
   }();
   if (force > 0) return force < g ? force : g;
   const int blocks = (int)mde::cdiv(m, 256) * groups;
+  // >= 64 column blocks (the wide kernels' 64 x 288-element groups): one
+  // launch -- a second launch costs more than it saves there (per-shape A/B,
+  // profiles/r04_wgrad_reduce_ab.txt); fewer: slices to fill the chip
+  if (blocks >= 64) return 1;
   int sl = (int)mde::cdiv(512, blocks);
   const int cap = g / 16 > 1 ? g / 16 : 1;
   return sl < 1 ? 1 : (sl > cap ? cap : sl);

@@ -17,7 +17,8 @@ echo "pmc ${TAG:-x} ${PMC} rc=$rc"
 import csv, sys, collections, re
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(sys.argv[1])):
-    n = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("(anonymous namespace)::", "")
+    n = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
     key = (n[:90], r.get("Grid_Size", r.get("Grid_Size_X", "")))
     agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for (n, g), cs in sorted(agg.items()):

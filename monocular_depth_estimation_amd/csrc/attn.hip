@@ -772,7 +772,9 @@ __global__ void __launch_bounds__(256, WS == 7 ? kOccBwd7 : 2)
 
 // gtable[e, head] / gqkb[C + head*D + d] / gvb[head*D + d] = sum over blocks:
 // 64 entries per block of 16 waves, wave w sums blocks w, w+16, ... (8 loads
-// in flight), the 16 wave sums combine in a fixed order.
+// in flight), the 16 wave sums combine in a fixed order.  Blocks (0, head)
+// also zero the q half of d(qk bias), gqkb[head*D + d]: padded tokens' dO is
+// 0, so it gets nothing (was a separate launch).
 __global__ void __launch_bounds__(1024)
     wattn_slab_reduce_kernel(const float* __restrict__ slab, int nblocks, int heads,
                              int ntab, int c, float* __restrict__ gtable,
@@ -780,6 +782,7 @@ __global__ void __launch_bounds__(1024)
   __shared__ float red[16][64];
   const int head = blockIdx.y;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (blockIdx.x == 0 && wid == 1 && lane < D) gqkb[head * D + lane] = 0.f;
   const int e = blockIdx.x * 64 + lane;
   const int per = ntab + 2 * D;
   float acc = 0.f;
@@ -799,11 +802,6 @@ __global__ void __launch_bounds__(1024)
     gqkb[c + head * D + (e - ntab)] = t;
   else if (gvb)
     gvb[head * D + (e - ntab - D)] = t;
-}
-
-__global__ void zero_kernel(float* p, int n) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = 0.f;
 }
 
 bool make_geo(int64_t b, int64_t h, int64_t w, int64_t c, int64_t heads, int64_t ws,
@@ -915,9 +913,6 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
     MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel<0>, grid, dim3(256), 0,
                (const float*)gout, (const float*)qk, qk_bias, (const float*)v, table,
                (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, wpb, g);
-  // q half of d(qk bias) gets nothing from padded tokens (their dO is 0)
-  MDE_LAUNCH(mde::K_WATTN_BWD, 0.0, s, zero_kernel, dim3((unsigned)mde::cdiv(c, 256)),
-             dim3(256), 0, gqk_bias, (int)c);
   MDE_LAUNCH(mde::K_WATTN_BWD, 4.0 * nblk * heads * (ntab + 2 * D), s,
              wattn_slab_reduce_kernel,
              dim3((unsigned)mde::cdiv(ntab + 2 * D, 64), (unsigned)heads), dim3(1024), 0,

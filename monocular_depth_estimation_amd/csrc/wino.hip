@@ -129,50 +129,62 @@ __global__ void __launch_bounds__(256, 2)
   const int nchunks = ci_n / kCIC;
   const float* ua = U + (int64_t)(co0 + li) * nchunks * 256 + kq * 4;
 
-  // patch loader: p = tid + 256 pp -> (channel p / NTB, tile p % NTB)
-  const int r0 = (br * kTRB) * 2 - 1, c0 = (bc * TCB) * 2 - 1;
-  int poff[PPT][4], pcol[PPT][4];
-  uint32_t pmask[PPT];
-#pragma unroll
-  for (int pp = 0; pp < PPT; ++pp) {
-    const int p = tid + 256 * pp, tl = p % NTB;
-    const int gr = r0 + 2 * (tl / TCB), gc = c0 + 2 * (tl % TCB);
-    uint32_t m = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rr = gr + i, cc = gc + i;
-      m |= (rr >= 0 && rr < h ? 1u : 0u) << i;
-      m |= (cc >= 0 && cc < w ? 1u : 0u) << (4 + i);
-      poff[pp][i] = (rr < 0 ? 0 : (rr >= h ? h - 1 : rr)) * w;
-      pcol[pp][i] = cc < 0 ? 0 : (cc >= w ? w - 1 : cc);
-    }
-    pmask[pp] = m;
-  }
-  float pv[PPT][16];
+  // Input staging: per chunk, the block's 16 channels x 10 input rows x
+  // (2 TCB + 4) columns (global column 2 bc TCB - 2 onward: even, so every
+  // float2 is 8-byte aligned and lies wholly inside or outside the plane,
+  // w even) are loaded as float2 row segments into registers (the next
+  // chunk's while this one multiplies), written to LDS with the padding
+  // zeroed, and each thread forms its (channel, tile) 4 x 4 patches from
+  // there.  (One dword load per patch element made the texture addresser
+  // ~70 % busy and cost 0.8 VMEM instructions per MFMA: SQ / TA counters,
+  // profiles/r04_wino_pmc.txt.)
+  constexpr int RR = 2 * kTRB + 2;        // input rows of a block
+  constexpr int RW2 = TCB + 2;            // float2 per row (2 TCB + 4 columns)
+  constexpr int RWP = 2 * RW2 + 1;        // LDS row pitch (floats), odd
+  constexpr int RAW = kCIC * RR * RW2;    // float2 per chunk
+  constexpr int RPT = (RAW + 255) / 256;  // float2 per thread
+  __shared__ float raw[kCIC * RR * RWP];
+  const int gr0 = 2 * br * kTRB - 1, gc0 = 2 * bc * TCB - 2;
+  float2 rv[RPT];
   auto load = [&](int chunk) {
+    const float* src = xb + (int64_t)chunk * kCIC * hw;
 #pragma unroll
-    for (int pp = 0; pp < PPT; ++pp) {
-      const int ch = (tid + 256 * pp) / NTB;
-      const float* src = xb + (int64_t)(chunk * kCIC + ch) * hw;
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) pv[pp][4 * i + j] = src[poff[pp][i] + pcol[pp][j]];
+    for (int k = 0; k < RPT; ++k) {
+      const int e = tid + 256 * k;
+      const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
+      const int r = rem / RW2, c2 = rem - r * RW2;
+      const int gr = gr0 + r, gc = gc0 + 2 * c2;
+      const bool ok = e < RAW && gr >= 0 && gr < h && gc >= 0 && gc < w;
+      const int64_t off = ok ? (int64_t)(e < RAW ? ch : 0) * hw + (int64_t)gr * w + gc : 0;
+      const float2 t = *reinterpret_cast<const float2*>(src + off);
+      rv[k] = ok ? t : make_float2(0.f, 0.f);
     }
   };
-  // B^T d B into V[xi][16-tile group][ci][16]
+  auto stage = [&]() {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int e = tid + 256 * k;
+      if (e < RAW) {
+        const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
+        const int r = rem / RW2, c2 = rem - r * RW2;
+        float* d = raw + (ch * RR + r) * RWP + 2 * c2;
+        d[0] = rv[k].x;
+        d[1] = rv[k].y;
+      }
+    }
+  };
+  // B^T d B into V[xi][16-tile group][ci][16]; patch of tile (tr, tc): raw
+  // rows 2 tr .. + 3, columns 2 tc + 1 .. + 4
   auto transform = [&]() {
 #pragma unroll
     for (int pp = 0; pp < PPT; ++pp) {
       const int p = tid + 256 * pp, ch = p / NTB, tl = p % NTB;
+      const float* q = raw + (ch * RR + 2 * (tl / TCB)) * RWP + 2 * (tl % TCB) + 1;
       float d[4][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const bool ok = ((pmask[pp] >> i) & 1u) && ((pmask[pp] >> (4 + j)) & 1u);
-          d[i][j] = ok ? pv[pp][4 * i + j] : 0.f;
-        }
+        for (int j = 0; j < 4; ++j) d[i][j] = q[i * RWP + j];
       float t[4][4];  // B^T d: rows d0 - d2, d1 + d2, d2 - d1, d1 - d3
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -207,10 +219,12 @@ __global__ void __launch_bounds__(256, 2)
   for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 16);
   load(0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    __syncthreads();  // the previous chunk's V readers are done
-    transform();
+    __syncthreads();  // the previous chunk's V (and raw) readers are done
+    stage();
     __syncthreads();
     if (chunk + 1 < nchunks) load(chunk + 1);
+    transform();
+    __syncthreads();
     const float* uc = ua + (int64_t)chunk * 256;
     const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 256;
 #pragma unroll

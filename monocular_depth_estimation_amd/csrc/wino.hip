@@ -140,10 +140,15 @@ __global__ void __launch_bounds__(256, 2)
   // profiles/r04_wino_pmc.txt.)
   constexpr int RR = 2 * kTRB + 2;        // input rows of a block
   constexpr int RW2 = TCB + 2;            // float2 per row (2 TCB + 4 columns)
-  constexpr int RWP = 2 * RW2 + 1;        // LDS row pitch (floats), odd
+  // LDS pitches for the patch reads (lane = tile: column 2 tc, row 2 tr; the
+  // next 32 / 64 lanes the next channel): rows 2 tr at 16-bank steps
+  // (2 RWP = 16 or 48 mod 64) and an odd channel pitch, so the 4 row groups of a
+  // channel use disjoint even banks and the next channel the odd ones
+  constexpr int RWP = 2 * RW2 <= 24 ? 24 : 40;  // 2 RWP = 48 or 16 (mod 64)
+  constexpr int CPI = RR * RWP + 1;
   constexpr int RAW = kCIC * RR * RW2;    // float2 per chunk
   constexpr int RPT = (RAW + 255) / 256;  // float2 per thread
-  __shared__ float raw[kCIC * RR * RWP];
+  __shared__ float raw[kCIC * CPI];
   const int gr0 = 2 * br * kTRB - 1, gc0 = 2 * bc * TCB - 2;
   float2 rv[RPT];
   auto load = [&](int chunk) {
@@ -167,7 +172,7 @@ __global__ void __launch_bounds__(256, 2)
       if (e < RAW) {
         const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
         const int r = rem / RW2, c2 = rem - r * RW2;
-        float* d = raw + (ch * RR + r) * RWP + 2 * c2;
+        float* d = raw + ch * CPI + r * RWP + 2 * c2;
         d[0] = rv[k].x;
         d[1] = rv[k].y;
       }
@@ -179,7 +184,7 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int pp = 0; pp < PPT; ++pp) {
       const int p = tid + 256 * pp, ch = p / NTB, tl = p % NTB;
-      const float* q = raw + (ch * RR + 2 * (tl / TCB)) * RWP + 2 * (tl % TCB) + 1;
+      const float* q = raw + ch * CPI + 2 * (tl / TCB) * RWP + 2 * (tl % TCB) + 1;
       float d[4][4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)

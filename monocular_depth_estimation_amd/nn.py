@@ -732,16 +732,16 @@ def conv3x3_passes(conv: nn.Conv2d, x):
     p = [bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
          for i, f in enumerate(p)]
     if dt == _abi.MDE_F32 and WINO_ON and not _autocast_bf16(x):
-        # forward / data gradient of the 64-256-channel convs on the Winograd
+        # forward / data gradient of the 32-256-channel convs on the Winograd
         # F(2x2, 3x3) kernels (2.25x fewer MACs) where MIOpen would run its own
-        # Winograd: 64-channel output groups (the 16 / 32-channel variants lose
-        # to MIOpen / the direct kernel: the input transform is amortised over
-        # too few output channels, tools/c1_bench.py) on planes of >= 256
-        # blocks (8 x 16 output pixels x 64 channels)
+        # Winograd: 64- / 32-channel output groups (the 16-channel variant
+        # loses to the direct kernel: the input transform is amortised over
+        # too few output channels, tools/wino_bench.py) on planes of >= 256
+        # blocks (8 x 16 output pixels x 64 / 32 channels)
         n, h, w = x.shape[0], x.shape[2], x.shape[3]
         for i, (a, b) in enumerate(((cin, cout), (cout, cin))):
-            blocks = n * -(-h // 8) * -(-w // 16) * (b // 64)
-            if (not p[i] and b % 64 == 0 and blocks >= 256
+            blocks = n * -(-h // 8) * -(-w // 16) * (b // (64 if b % 64 == 0 else 32))
+            if (not p[i] and b % (32 if WINO32 else 64) == 0 and blocks >= 256
                     and _abi.query("mde_wino_supported", a, b, h, w, _abi.MDE_F32)):
                 p[i] = WINO
     if dt == _abi.MDE_F32 and C3_WIDE and not _autocast_bf16(x):
@@ -759,6 +759,7 @@ WINO = 3  # conv3x3_passes flag: the pass runs on the Winograd kernel
 # MDE_WINO=0: MIOpen for these passes (A/B switch; cfg2 interleaved A/B 911.6 /
 # 909.0 vs 881.0 / 878.3 img/s, profiles/r04_ab_wino.txt)
 WINO_ON = os.environ.get("MDE_WINO", "1") != "0"
+WINO32 = os.environ.get("MDE_WINO32", "1") != "0"  # the 32-channel output groups too (A/B)
 # Off by default: MIOpen's Winograd matches the stride-1 band kernel on these
 # shapes (tools/c1_bench.py) and the cfg2 step was 0.5 % slower with it on
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"

@@ -2006,6 +2006,17 @@ int bf_fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_im
   return nt < res ? (int)nt : res;
 }
 
+// bf16 forward / data-gradient tile height: MDE_BF_RPW=2 -> 8-row tiles
+// (two rows per wave: twice the MFMAs per staging round and barrier, 1.25x
+// instead of 1.5x halo rows), else 4-row tiles (A/B switch)
+inline int bf_rpw() {
+  static const int r = [] {
+    const char* e = std::getenv("MDE_BF_RPW");
+    return e && e[0] == '2' ? 2 : 1;
+  }();
+  return r;
+}
+
 template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
 int launch_bf_fwd(const bf16* in, const float* wt, bf16* out, int64_t n, int64_t h, int64_t w,
                   double bytes, int kid, hipStream_t s, float* stats = nullptr) {
@@ -2147,11 +2158,11 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
     if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
-    if (cin == 16)
-      return launch_bf_fwd<16, 16, 1, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes,
-                                             mde::K_C3_FWD_BF16, s);
-    return launch_bf_fwd<32, 32, 1, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes,
-                                           mde::K_C3_FWD_BF16, s);
+#define MDE_BF(CC, R) \
+  launch_bf_fwd<CC, CC, R, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes, mde::K_C3_FWD_BF16, s)
+    if (cin == 16) return bf_rpw() == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
+    return bf_rpw() == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
+#undef MDE_BF
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
@@ -2176,8 +2187,11 @@ int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, in
   int a, b, c;
   if (dtype == MDE_BF16) {
     if (!bf_supported(cin, cout) || !dims_ok(n, h, w)) return 0;
-    if (cin == 16) return bf_fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
-    return bf_fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
+    if (cin == 16)
+      return bf_rpw() == 2 ? bf_fwd_grid<16, 16, 2, false, true>(n, h, w, &a, &b, &c)
+                           : bf_fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
+    return bf_rpw() == 2 ? bf_fwd_grid<32, 32, 2, false, true>(n, h, w, &a, &b, &c)
+                         : bf_fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
   }
   if (!supported(cin, cout, kFwd) || !dims_ok(n, h, w)) return 0;
   if (cin == 3 && cout == 16) return fwd_grid<3, 16, 2, false, true>(n, h, w, &a, &b, &c);
@@ -2195,11 +2209,12 @@ int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* st
     if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
-    if (cin == 16)
-      return launch_bf_fwd<16, 16, 1, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w,
-                                                   bytes, mde::K_C3_FWD_BF16, s, stats);
-    return launch_bf_fwd<32, 32, 1, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w,
-                                                 bytes, mde::K_C3_FWD_BF16, s, stats);
+#define MDE_BF(CC, R)                                                                   \
+  launch_bf_fwd<CC, CC, R, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes, \
+                                        mde::K_C3_FWD_BF16, s, stats)
+    if (cin == 16) return bf_rpw() == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
+    return bf_rpw() == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
+#undef MDE_BF
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !weight || !y || !stats || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;
@@ -2227,11 +2242,12 @@ int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
     if (!bf_supported(cin, cout)) return MDE_ERR_UNSUPPORTED;
     hipStream_t s = (hipStream_t)stream;
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
-    if (cin == 16)
-      return launch_bf_fwd<16, 16, 1, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,
-                                            mde::K_C3_DGRAD_BF16, s);
-    return launch_bf_fwd<32, 32, 1, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,
-                                          mde::K_C3_DGRAD_BF16, s);
+#define MDE_BF(CC, R)                                                                        \
+  launch_bf_fwd<CC, CC, R, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,          \
+                                 mde::K_C3_DGRAD_BF16, s)
+    if (cin == 16) return bf_rpw() == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
+    return bf_rpw() == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
+#undef MDE_BF
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!gy || !weight || !gx || !dims_ok(n, h, w)) return MDE_ERR_INVALID_ARG;

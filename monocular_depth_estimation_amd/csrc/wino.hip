@@ -395,7 +395,11 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
   WinoGeo g;
   if (!wino_geo(n, cin, cout, h, w, &g)) return MDE_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
-  const double flops = 2.0 * 9 * n * h * w * (double)cin * cout;  // direct-conv equivalent
+  // the MFMA work the kernel does: 16 MACs per 2 x 2 tile and (cin, cout) pair
+  // (the direct conv's 36 / 2.25), so the roofline prices the Winograd GEMMs,
+  // not a direct-conv equivalent
+  const double flops = 2.0 * 16 * n * (double)((h + 1) / 2) * (double)((w + 1) / 2) *
+                       (double)cin * cout;
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
   const dim3 grid((unsigned)((g.total + 7) / 8 * 8)), block(256);
   const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;

@@ -656,6 +656,9 @@ int mde_wino_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtyp
 size_t mde_wino_weight_bytes(int64_t cin, int64_t cout);
 int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, int flip,
                     void* stream);
+/* Both transforms of the filter in one launch: u (flip 0) and u_flip (flip 1). */
+int mde_wino_weight2(const float* weight, float* u, float* u_flip, int64_t cin, int64_t cout,
+                     void* stream);
 int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
                   int64_t h, int64_t w, int pass, int dtype, void* stream);
 /* The same with the following BatchNorm's statistics of y from the epilogue

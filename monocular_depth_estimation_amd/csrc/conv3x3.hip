@@ -1064,6 +1064,19 @@ inline int wide_fixed_sw(int64_t w) {
   return w % 80 == 0 ? 80 : (w == 40 ? 40 : (w == 20 ? 20 : 0));
 }
 
+// Blocks of the fixed-strip wide weight gradients over all groups: two
+// 8-wave blocks per CU (512).  Each block leaves one 64 x 288 partial, so the
+// slab (and its HBM write + the reduction's read) scales with this;
+// MDE_WIDE_BLOCKS overrides (traffic / speed A/B).
+inline int wide_blocks() {
+  static const int b = [] {
+    const char* e = std::getenv("MDE_WIDE_BLOCKS");
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 8 ? v : 512;
+  }();
+  return b;
+}
+
 struct WidePlan {
   WideGeo g;
   int groups, gx;
@@ -1086,7 +1099,7 @@ inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, W
   }
   p->groups = (int)((ci / kWCI) * (co / kWCO));
   // one 100 KB-LDS block per CU (generic), two <= 80 KB blocks (fixed width)
-  int gx = (p->fixed_sw ? 512 : 256) / p->groups;
+  int gx = (p->fixed_sw ? wide_blocks() : 256) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;
@@ -1228,7 +1241,7 @@ inline bool wide_s2_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w
   p->g.tiles_per_img = (int)tpi;
   p->g.ntiles = (int)nt;
   p->groups = (int)((ci / kWCI) * (co / kWCO));
-  int gx = 512 / p->groups;
+  int gx = wide_blocks() / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;

@@ -82,6 +82,61 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Both transforms of one filter in one launch (the forward's U and the data
+// gradient's flipped U'), one thread per (co, ci) of the FORWARD conv.
+__device__ __forceinline__ void wino_g(const float (&w)[3][3], float (&u)[4][4]) {
+  float a[4][3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    a[0][c] = w[0][c];
+    a[1][c] = 0.5f * ((w[0][c] + w[1][c]) + w[2][c]);
+    a[2][c] = 0.5f * ((w[0][c] - w[1][c]) + w[2][c]);
+    a[3][c] = w[2][c];
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    u[r][0] = a[r][0];
+    u[r][1] = 0.5f * ((a[r][0] + a[r][1]) + a[r][2]);
+    u[r][2] = 0.5f * ((a[r][0] - a[r][1]) + a[r][2]);
+    u[r][3] = a[r][2];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    wino_weight2_kernel(const float* __restrict__ g, float* __restrict__ U,
+                        float* __restrict__ U2, int co_n, int ci_n) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)co_n * ci_n) return;
+  const int co = (int)(t / ci_n), ci = (int)(t % ci_n);
+  const float* src = g + ((int64_t)co * ci_n + ci) * 9;
+  float w[3][3], wf[3][3], u[4][4];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      w[r][c] = src[r * 3 + c];
+      wf[2 - r][2 - c] = w[r][c];
+    }
+  // forward: row co of the (co_n x ci_n) conv; flipped: row ci of (ci_n x co_n)
+  wino_g(w, u);
+  {
+    float* dst = U + ((int64_t)co * (ci_n / kCIC) + ci / kCIC) * 256 + (ci % 4) * 4 + (ci % kCIC) / 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 16] = u[r][c];
+  }
+  wino_g(wf, u);
+  {
+    float* dst =
+        U2 + ((int64_t)ci * (co_n / kCIC) + co / kCIC) * 256 + (co % 4) * 4 + (co % kCIC) / 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 16] = u[r][c];
+  }
+}
+
 // A block: 4 x TCB tiles (8 x 2 TCB output pixels) x CO_B output channels.
 // CO_B = 64 (TCB 8): four waves along output channels, each with both 16-tile
 // groups; CO_B = 32 (TCB 8): two waves along channels x two along tile groups;
@@ -382,6 +437,20 @@ int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, in
   else
     MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 16), s, wino_weight_kernel<false>, grid,
                dim3(256), 0, weight, u, (int)cout, (int)cin);
+  return MDE_OK;
+}
+
+// Both transforms at once: u for the forward conv, u_flip for its data
+// gradient (as mde_wino_weight with flip = 0 / 1).
+int mde_wino_weight2(const float* weight, float* u, float* u_flip, int64_t cin, int64_t cout,
+                     void* stream) {
+  if (!weight || !u || !u_flip || cin < kCIC || cout < kCIC || cin % kCIC || cout % kCIC)
+    return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t pairs = cin * cout;
+  MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 32), s, wino_weight2_kernel,
+             dim3((unsigned)mde::cdiv(pairs, 256)), dim3(256), 0, weight, u, u_flip, (int)cout,
+             (int)cin);
   return MDE_OK;
 }
 

@@ -400,6 +400,7 @@ class _Conv3x3(torch.autograd.Function):
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
+        u_flip = None  # Winograd: the data gradient's filter transform, made with the forward's
         if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip), + the BN statistics
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
             u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
@@ -407,7 +408,13 @@ class _Conv3x3(torch.autograd.Function):
             if want_stats:
                 nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
                 stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
-            _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 0, st)
+            if passes[1] == WINO and ctx.needs_input_grad[0]:
+                # the data gradient's flipped transform too, in the same launch
+                u_flip = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+                _abi.call("mde_wino_weight2", _abi.ptr(weight), _abi.ptr(u), _abi.ptr(u_flip), cin,
+                          cout, st)
+            else:
+                _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 0, st)
             _abi.call("mde_wino_conv_stats", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y),
                       _abi.ptr(stats) if want_stats else None, n, cin, cout, h, w, 0,
                       _abi.dtype_code(x), st)
@@ -430,6 +437,7 @@ class _Conv3x3(torch.autograd.Function):
             y = torch.nn.functional.conv2d(x, weight, None, 1, 1)
         ctx.save_for_backward(x, weight)
         ctx.passes = passes
+        ctx.u_flip = u_flip
         ctx.mark_non_differentiable(stats)
         return y, stats
 
@@ -445,8 +453,10 @@ class _Conv3x3(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             if ctx.passes[1] == WINO:  # the flipped, transposed filter's transform
                 gx = torch.empty_like(x)
-                u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
-                _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 1, st)
+                u = ctx.u_flip
+                if u is None:
+                    u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+                    _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 1, st)
                 _abi.call("mde_wino_conv", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(gx), n, cout, cin, h,
                           w, 1, _abi.dtype_code(gy), st)
             elif ctx.passes[1] == WIDE:

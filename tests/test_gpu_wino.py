@@ -147,3 +147,18 @@ def test_wino_stats_epilogue(cin, cout, h, w):
     vr = yd.var((0, 2, 3), unbiased=False)
     assert float((mean - mr).abs().max() / mr.abs().max()) <= 1e-5
     assert float((var - vr).abs().max() / vr.abs().max()) <= 1e-4
+
+
+def test_wino_weight2_matches_both_transforms():
+    """mde_wino_weight2 (the forward's U and the data gradient's flipped U' in
+    one launch) == mde_wino_weight with flip 0 / 1, bitwise."""
+    from monocular_depth_estimation_amd import _abi
+    for cin, cout in ((64, 128), (32, 32), (16, 48)):
+        wt = torch.rand((cout, cin, 3, 3), device=DEV) - 0.5
+        st = _abi.stream_of(wt)
+        u0, u1 = (torch.empty(16 * cin * cout, device=DEV) for _ in range(2))
+        v0, v1 = (torch.full((16 * cin * cout,), float("nan"), device=DEV) for _ in range(2))
+        _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u0), cin, cout, 0, st)
+        _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u1), cin, cout, 1, st)
+        _abi.call("mde_wino_weight2", _abi.ptr(wt), _abi.ptr(v0), _abi.ptr(v1), cin, cout, st)
+        assert torch.equal(u0, v0) and torch.equal(u1, v1)

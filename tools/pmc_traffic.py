@@ -44,6 +44,11 @@ NAMES = [
     (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd_bf16"),
     (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad_bf16"),
     (r"conv3x3_bf_wgrad_kernel", "conv3x3_wgrad_bf16"),
+    # the fixed-strip kernel under the three ids that launch it (csrc/conv3x3.hip):
+    # 32-channel groups at stride 1 (conv3x3_wgrad), stride 2 (conv3x3s2_wgrad)
+    (r"conv3x3_wgrad_wide_fixed_kernel<1, \d+, \d+, \d+, 32>", "conv3x3_wgrad"),
+    (r"conv3x3_wgrad_wide_fixed_kernel<2,", "conv3x3s2_wgrad"),
+    (r"conv3x3s2_wgrad_kernel", "conv3x3s2_wgrad"),
     (r"conv3x3_wgrad_wide\w*_kernel", "conv3x3_wgrad_wide"),
     (r"conv3x3_wgrad_kernel<3,", "conv3x3_wgrad_guide"),
     (r"conv3x3_wgrad_kernel", "conv3x3_wgrad"),

@@ -1064,17 +1064,22 @@ inline int wide_fixed_sw(int64_t w) {
   return w % 80 == 0 ? 80 : (w == 40 ? 40 : (w == 20 ? 20 : 0));
 }
 
-// Blocks of the fixed-strip wide weight gradients over all groups: two
-// 8-wave blocks per CU (512).  Each block leaves one 64 x 288 partial, so the
-// slab (and its HBM write + the reduction's read) scales with this;
-// MDE_WIDE_BLOCKS overrides (traffic / speed A/B).
-inline int wide_blocks() {
-  static const int b = [] {
+// Blocks of the fixed-strip wide weight gradients over all groups.  Each
+// block leaves one 64 x 288 partial, so the slab (its HBM write and the
+// reduction's read) scales with this: one 8-wave block per CU (256) for the
+// 1/8- and smaller-resolution planes -- half the slab and PMC traffic 1.35x ->
+// ~1.0x on the fetch side at equal time -- two per CU (512) for planes with
+// >= 4096 strip tiles (64 -> 64 at 120 x 160: 385 vs 417 us), where the slab
+// is small next to the inputs (profiles/r04_wide_blocks_ab.txt).
+// MDE_WIDE_BLOCKS overrides (A/B).
+inline int wide_blocks(int64_t ntiles) {
+  static const int forced = [] {
     const char* e = std::getenv("MDE_WIDE_BLOCKS");
     const int v = e ? std::atoi(e) : 0;
-    return v >= 8 ? v : 512;
+    return v >= 8 ? v : 0;
   }();
-  return b;
+  if (forced) return forced;
+  return ntiles >= 4096 ? 512 : 256;
 }
 
 struct WidePlan {
@@ -1099,7 +1104,7 @@ inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, W
   }
   p->groups = (int)((ci / kWCI) * (co / kWCO));
   // one 100 KB-LDS block per CU (generic), two <= 80 KB blocks (fixed width)
-  int gx = (p->fixed_sw ? wide_blocks() : 256) / p->groups;
+  int gx = (p->fixed_sw ? wide_blocks(p->g.ntiles) : 256) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;
@@ -1241,7 +1246,7 @@ inline bool wide_s2_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w
   p->g.tiles_per_img = (int)tpi;
   p->g.ntiles = (int)nt;
   p->groups = (int)((ci / kWCI) * (co / kWCO));
-  int gx = wide_blocks() / p->groups;
+  int gx = wide_blocks(nt) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;

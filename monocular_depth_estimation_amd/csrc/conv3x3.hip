@@ -2024,15 +2024,21 @@ int bf_fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_im
   return nt < res ? (int)nt : res;
 }
 
-// bf16 forward / data-gradient tile height: MDE_BF_RPW=2 -> 8-row tiles
-// (two rows per wave: twice the MFMAs per staging round and barrier, 1.25x
-// instead of 1.5x halo rows), else 4-row tiles (A/B switch)
-inline int bf_rpw() {
+// bf16 forward / data-gradient tile height: 8-row tiles (two rows per wave:
+// twice the MFMAs per staging round and barrier, 1.25x instead of 1.5x halo
+// rows) at 16 channels -- fwd 266 -> 246, dgrad 249 -> 225 us at 480 x 640 --
+// 4-row tiles at 32 (8-row: 164 -> 194 us, one block per CU by registers),
+// profiles/r04_bf_rpw_ab.txt.  MDE_BF_RPW=1 / 2 forces one (A/B).
+inline int bf_rpw_forced() {
   static const int r = [] {
     const char* e = std::getenv("MDE_BF_RPW");
-    return e && e[0] == '2' ? 2 : 1;
+    return e && (e[0] == '1' || e[0] == '2') ? e[0] - '0' : 0;
   }();
   return r;
+}
+inline int bf_rpw(int64_t ch) {
+  const int f = bf_rpw_forced();
+  return f ? f : (ch == 16 ? 2 : 1);
 }
 
 template <int CI, int CO, int RPW, bool FLIP, bool STATS = false>
@@ -2178,8 +2184,8 @@ int mde_conv3x3_fwd(const void* x, const float* weight, void* y, int64_t n, int6
     const double bytes = 2.0 * n * h * w * (double)(cin + cout);
 #define MDE_BF(CC, R) \
   launch_bf_fwd<CC, CC, R, false>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes, mde::K_C3_FWD_BF16, s)
-    if (cin == 16) return bf_rpw() == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
-    return bf_rpw() == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
+    if (cin == 16) return bf_rpw(16) == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
+    return bf_rpw(32) == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
 #undef MDE_BF
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
@@ -2206,10 +2212,10 @@ int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, in
   if (dtype == MDE_BF16) {
     if (!bf_supported(cin, cout) || !dims_ok(n, h, w)) return 0;
     if (cin == 16)
-      return bf_rpw() == 2 ? bf_fwd_grid<16, 16, 2, false, true>(n, h, w, &a, &b, &c)
-                           : bf_fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
-    return bf_rpw() == 2 ? bf_fwd_grid<32, 32, 2, false, true>(n, h, w, &a, &b, &c)
-                         : bf_fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
+      return bf_rpw(16) == 2 ? bf_fwd_grid<16, 16, 2, false, true>(n, h, w, &a, &b, &c)
+                             : bf_fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
+    return bf_rpw(32) == 2 ? bf_fwd_grid<32, 32, 2, false, true>(n, h, w, &a, &b, &c)
+                           : bf_fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
   }
   if (!supported(cin, cout, kFwd) || !dims_ok(n, h, w)) return 0;
   if (cin == 3 && cout == 16) return fwd_grid<3, 16, 2, false, true>(n, h, w, &a, &b, &c);
@@ -2230,8 +2236,8 @@ int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* st
 #define MDE_BF(CC, R)                                                                   \
   launch_bf_fwd<CC, CC, R, false, true>((const bf16*)x, weight, (bf16*)y, n, h, w, bytes, \
                                         mde::K_C3_FWD_BF16, s, stats)
-    if (cin == 16) return bf_rpw() == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
-    return bf_rpw() == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
+    if (cin == 16) return bf_rpw(16) == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
+    return bf_rpw(32) == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
 #undef MDE_BF
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
@@ -2263,8 +2269,8 @@ int mde_conv3x3_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
 #define MDE_BF(CC, R)                                                                        \
   launch_bf_fwd<CC, CC, R, true>((const bf16*)gy, weight, (bf16*)gx, n, h, w, bytes,          \
                                  mde::K_C3_DGRAD_BF16, s)
-    if (cin == 16) return bf_rpw() == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
-    return bf_rpw() == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
+    if (cin == 16) return bf_rpw(16) == 2 ? MDE_BF(16, 2) : MDE_BF(16, 1);
+    return bf_rpw(32) == 2 ? MDE_BF(32, 2) : MDE_BF(32, 1);
 #undef MDE_BF
   }
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;

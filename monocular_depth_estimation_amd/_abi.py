@@ -272,14 +272,31 @@ def graph_replace_memsets(raw_graph: int) -> int:
 _DOT_SEQ = [0]
 
 
+def default_capture_mode() -> str:
+    """"thread_local" when a torch.distributed process group is initialised
+    (its watchdog thread queries events during our captures), else "global"."""
+    import torch.distributed as dist
+    return "thread_local" if dist.is_available() and dist.is_initialized() else "global"
+
+
 def capture_graph(fn, stream, pool=None, capture_error_mode: str | None = None):
     """Capture fn() on `stream` into a torch CUDAGraph, repair its memset nodes
     and instantiate it.  Returns (graph, fn's result, memset nodes replaced).
 
+    Capture mode: "thread_local" once a torch.distributed group exists, else
+    "global".  ProcessGroupNCCL's watchdog thread polls the completion event of
+    every collective issued eagerly before the capture (the warm-up steps' and
+    the per-step BN broadcast's) with hipEventQuery; while ANY thread holds a
+    global-mode capture that query fails with hipErrorStreamCaptureUnsupported,
+    the watchdog throws and the process aborts (SIGABRT, the round-3/4
+    captured-RCCL aborts: gpurun_out/r04w/suite.log).  A thread-local capture
+    only restricts the capturing thread, and every GPU call of the step is
+    issued from it.
+
     Diagnostics (environment): MDE_GRAPH_CAPTURE_MODE overrides the capture
-    mode ("global" default), MDE_GRAPH_DOT_DIR dumps every captured graph as
+    mode, MDE_GRAPH_DOT_DIR dumps every captured graph as
     hipGraphDebugDotPrint output before and after the memset repair."""
-    mode = capture_error_mode or os.environ.get("MDE_GRAPH_CAPTURE_MODE", "global")
+    mode = capture_error_mode or os.environ.get("MDE_GRAPH_CAPTURE_MODE") or default_capture_mode()
     g = torch.cuda.CUDAGraph(keep_graph=True)
     with torch.cuda.graph(g, stream=stream, pool=pool, capture_error_mode=mode):
         out = fn()

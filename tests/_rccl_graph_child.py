@@ -17,6 +17,7 @@ test session down with it.  Exit 0 = every assertion held.
 import gc
 import os
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -61,7 +62,16 @@ def main(mode):
         with torch.cuda.stream(s):
             dist.all_reduce(probe, op=dist.ReduceOp.AVG)  # eager warm-up of the communicator
         torch.cuda.synchronize()
-        g1, _, _ = _abi.capture_graph(lambda: dist.all_reduce(probe, op=dist.ReduceOp.AVG), s)
+        # the eager collective's Work is still on the watchdog's list: the
+        # capture lasts 0.35 s, so the watchdog (100 ms poll) queries its event
+        # while the capture is open -- the abort of a global-mode capture
+        assert _abi.default_capture_mode() == "thread_local"
+
+        def probe_step():
+            time.sleep(0.35)
+            dist.all_reduce(probe, op=dist.ReduceOp.AVG)
+
+        g1, _, _ = _abi.capture_graph(probe_step, s)
         per_collective = g1.node_counts["total"]
         print(f"probe collective nodes: {g1.node_types}", flush=True)
         assert per_collective >= 1, g1.node_counts

@@ -37,6 +37,8 @@ def _run(tr_factory, steps=6):
     for k in range(steps):
         image, depth = synthetic_batch(2, 64, 96, 0, k, DEV)
         losses.append(float(tr.step(image, depth).detach()))
+        if os.environ.get("MDE_RCCL_TRACE"):
+            print(f"  {type(tr).__name__} step {k} done", flush=True)
     torch.cuda.synchronize()
     return tr, model, losses
 

@@ -185,7 +185,14 @@ def _rccl_child(mode):
                        timeout=300)
     # rocBLAS's kernel-lookup misses are logged as HIP errors at AMD_LOG_LEVEL=1: not ours
     lines = [ln for ln in (p.stdout + p.stderr).splitlines() if "Cannot find the function" not in ln]
-    out = "\n".join(lines)[-4000:]
+    out = "\n".join(lines)
+    log_dir = os.environ.get("MDE_RCCL_LOG_DIR")
+    if log_dir:  # the whole child log (diagnosis); the assertion shows head + tail
+        os.makedirs(log_dir, exist_ok=True)
+        with open(os.path.join(log_dir, f"rccl_child_{mode}.log"), "w") as f:
+            f.write(out)
+    if len(out) > 6000:
+        out = out[:2000] + "\n[...]\n" + out[-4000:]
     return p.returncode, out
 
 

@@ -327,7 +327,17 @@ class GraphTrainer:
                 dist.broadcast(p.data, 0)
             dist.broadcast(self.flat_bn, 0)
         self.static_image = self.static_depth = None
-        self.stream = torch.cuda.Stream(device=world.device)  # eager warm-up + capture stream
+        # Capture streams and eager streams are disjoint.  A synchronous
+        # collective records its completion event on the stream it was issued
+        # on, and ProcessGroupNCCL's watchdog thread polls that event until it
+        # has seen it complete; if the stream has joined a capture by then, HIP
+        # refuses the query (hipErrorCapturedEvent), which invalidates the
+        # capture and kills the watchdog (SIGABRT).  So no stream that ever
+        # carries an eager collective is captured: warm-up steps and
+        # eager_step() run on eager_stream (bucket collectives on eager_side),
+        # captures on stream (bucket collectives on side).
+        self.stream = torch.cuda.Stream(device=world.device)  # capture stream
+        self.eager_stream = torch.cuda.Stream(device=world.device)
         # bucketed all-reduce overlapped with backward, captured into the step
         # graph: the N > 1 default over RCCL (MDE_DP_OVERLAP=0 selects the flat
         # scheme; a gloo group cannot capture collectives and takes the flat
@@ -339,7 +349,8 @@ class GraphTrainer:
         self.buckets = None
         if dp_overlap:
             self.side = torch.cuda.Stream(device=world.device)
-            self.buckets = GradBuckets(self.params, world, self.BUCKET_BYTES, stream=self.side)
+            self.eager_side = torch.cuda.Stream(device=world.device)
+            self.buckets = GradBuckets(self.params, world, self.BUCKET_BYTES, stream=self.eager_side)
         self.last_loss = None
         self.loss_sum = torch.zeros((), device=world.device)
         self.loss_count = 0
@@ -389,7 +400,12 @@ class GraphTrainer:
         if self.buckets is None:  # bucket views stay; _forward_backward zeroes them
             self.optimizer.zero_grad(set_to_none=True)
 
+    def _side_stream(self, captured: bool):
+        if self.buckets is not None:
+            self.buckets.stream = self.side if captured else self.eager_side
+
     def _eager(self):
+        self._side_stream(False)
         self._zero_grad()
         loss = self._forward_backward()
         self._allreduce()
@@ -406,10 +422,10 @@ class GraphTrainer:
         self._sync_buffers()
         if self.calls <= self.eager_steps:
             cur = torch.cuda.current_stream()
-            self.stream.wait_stream(cur)
-            with torch.cuda.stream(self.stream):
+            self.eager_stream.wait_stream(cur)
+            with torch.cuda.stream(self.eager_stream):
                 loss = self._eager()
-            cur.wait_stream(self.stream)
+            cur.wait_stream(self.eager_stream)
         else:
             if self.graphs is None:
                 self._capture()
@@ -446,6 +462,7 @@ class GraphTrainer:
                                "over RCCL only; a gloo group runs GraphTrainer eagerly "
                                "(eager_steps >= the number of steps)")
         torch.cuda.synchronize()
+        self._side_stream(True)
         self._zero_grad()  # backward allocates .grad in the graph pool (non-bucket mode)
         one_graph = not self.dp or self.buckets is not None
 
@@ -491,6 +508,7 @@ class GraphTrainer:
         from . import _abi
         torch.cuda.synchronize()
         _abi.timing_reset()
+        self._side_stream(True)
         self._zero_grad()
         one_graph = not self.dp or self.buckets is not None
 

@@ -59,20 +59,25 @@ def main(mode):
     per_collective = None
     if mode == "overlap":  # nodes one captured all_reduce(AVG) contributes
         probe = torch.ones(1 << 20, device=DEV)
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
+        s_eager, s = torch.cuda.Stream(), torch.cuda.Stream()
+        s_eager.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s_eager):
             dist.all_reduce(probe, op=dist.ReduceOp.AVG)  # eager warm-up of the communicator
         torch.cuda.synchronize()
-        # the eager collective's Work is still on the watchdog's list: the
-        # capture lasts 0.35 s, so the watchdog (100 ms poll) queries its event
-        # while the capture is open -- the abort of a global-mode capture
+        # The eager collective's Work is still on the watchdog's list and its
+        # completion event was recorded on s_eager.  The capture stays open
+        # 0.35 s, so the watchdog (100 ms poll) queries that event while the
+        # capture runs: legal because the capture is thread-local (a global
+        # one forbids the query) and s_eager never joins it (an event last
+        # recorded on a capturing stream cannot be queried) -- GraphTrainer's
+        # stream rules (train.py)
         assert _abi.default_capture_mode() == "thread_local"
 
         def probe_step():
             time.sleep(0.35)
             dist.all_reduce(probe, op=dist.ReduceOp.AVG)
 
+        s.wait_stream(torch.cuda.current_stream())
         g1, _, _ = _abi.capture_graph(probe_step, s)
         per_collective = g1.node_counts["total"]
         print(f"probe collective nodes: {g1.node_types}", flush=True)

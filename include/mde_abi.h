@@ -90,6 +90,13 @@ int mde_nearest_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
 int mde_nearest_bwd(const void* gy, void* gx, int64_t n, int64_t c, int64_t hi,
                     int64_t wi, int64_t ho, int64_t wo, float scale_h,
                     float scale_w, int dtype, void* stream);
+/* Both guides of GuideDepth.py:46-47 in one pass over the image: half =
+ * nearest x0.5 of x [n,c,h/2,w/2], quarter = nearest x0.25 [n,c,h/4,w/4]
+ * (bit-identical to the two mde_nearest_fwd calls: pure copies).  fp32,
+ * h % 4 == 0 and w % 8 == 0 (mde_nearest_pyramid_supported). */
+int mde_nearest_pyramid_supported(int64_t n, int64_t c, int64_t h, int64_t w);
+int mde_nearest_pyramid(const void* x, void* half, void* quarter, int64_t n, int64_t c, int64_t h,
+                        int64_t w, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Squeeze-excitation over a channel concatenation (cat fused away).

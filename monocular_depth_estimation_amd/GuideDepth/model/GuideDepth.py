@@ -1,14 +1,14 @@
 """GuideDepth on MI355X: DDRNet-23-slim encoder + three guided-upsampling blocks.
 
 Drop-in for src/GuideDepth/model/GuideDepth.py:9-57 (constructor, forward,
-471 state_dict keys).  The nearest guides (:46-47) and the three x2 bilinear
-upsamples (:49, :52, :55) run on the HIP resize kernels.
+471 state_dict keys).  The nearest guides (:46-47, one fused pass) and the
+three x2 bilinear upsamples (:49, :52, :55) run on the HIP resize kernels.
 """
 from __future__ import annotations
 
 from torch import nn
 
-from ...functional import bilinear_resize_x2_slotted, nearest_resize
+from ...functional import bilinear_resize_x2_slotted, nearest_pyramid
 from .DDRNet_23_slim import DualResNet_Backbone
 from .modules import Guided_Upsampling_Block
 
@@ -28,7 +28,9 @@ class GuideDepth(nn.Module):
 
     def forward(self, x):
         y = self.feature_extractor(x)
-        guides = (nearest_resize(x, scale_factor=0.25), nearest_resize(x, scale_factor=0.5), x)
+        # both nearest guides (:46-47) from one pass over the image
+        x_half, x_quarter = nearest_pyramid(x)
+        guides = (x_quarter, x_half, x)
         for block, guide in zip((self.up_1, self.up_2, self.up_3), guides):
             # the x2 upsample's backward also takes the skip fusion's gradient
             # of it (GradSlot), so autograd adds no accumulation pass

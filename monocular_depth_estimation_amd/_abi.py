@@ -39,6 +39,8 @@ SIGNATURES = {
                                  _int, _vp]),
     "mde_nearest_fwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _vp]),
     "mde_nearest_bwd": (_int, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _f32, _f32, _int, _vp]),
+    "mde_nearest_pyramid_supported": (_int, [_i64, _i64, _i64, _i64]),
+    "mde_nearest_pyramid": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_se_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64]),
     "mde_se_fwd": (_int, [_vp, _i64, _vp, _i64, _vp, _vp, _i64, _vp, _vp, _vp, _vp,
                           _i64, _i64, _i64, _vp, _int, _vp]),

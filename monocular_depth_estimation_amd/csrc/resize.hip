@@ -1,4 +1,5 @@
-// Bilinear and nearest resizes (NCHW, fp32) for gfx950.
+// Bilinear and nearest resizes (NCHW; bilinear on fp32 or bf16 storage, fp32
+// arithmetic) for gfx950.
 //
 // Index math follows ATen's area_pixel_compute_source_index /
 // nearest_neighbor_compute_source_index so the sampled pixels and the
@@ -64,9 +65,9 @@ __device__ __forceinline__ void lin_window(float scale, int i, int out_size,
 }
 
 // Forward: each thread produces VEC consecutive outputs of one output row.
-template <int VEC>
+template <int VEC, typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+    bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
                         int64_t rows, int hi, int wi, int ho, int wo,
                         float sh, float sw, int align) {
   const int chunks = (wo + VEC - 1) / VEC;
@@ -78,25 +79,25 @@ __global__ void __launch_bounds__(256)
     const int oh = (int)(row % ho);
     const int64_t plane = row / ho;
     const Lin H = lin_index(sh, oh, hi, align);
-    const float* r0 = x + (plane * hi + H.i0) * (int64_t)wi;
-    const float* r1 = x + (plane * hi + H.i1) * (int64_t)wi;
+    const T* r0 = x + (plane * hi + H.i0) * (int64_t)wi;
+    const T* r1 = x + (plane * hi + H.i1) * (int64_t)wi;
     float v[VEC];
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       const int ow = ch * VEC + k;
       if (ow < wo) {
         const Lin W = lin_index(sw, ow, wi, align);
-        v[k] = H.l0 * (W.l0 * r0[W.i0] + W.l1 * r0[W.i1]) +
-               H.l1 * (W.l0 * r1[W.i0] + W.l1 * r1[W.i1]);
+        v[k] = H.l0 * (W.l0 * mde::ld1(r0 + W.i0) + W.l1 * mde::ld1(r0 + W.i1)) +
+               H.l1 * (W.l0 * mde::ld1(r1 + W.i0) + W.l1 * mde::ld1(r1 + W.i1));
       }
     }
-    float* out = y + row * (int64_t)wo + ch * VEC;
+    T* out = y + row * (int64_t)wo + ch * VEC;
     if (VEC == 4 && ch * VEC + 4 <= wo) {
-      *reinterpret_cast<float4*>(out) = make_float4(v[0], v[1], v[2], v[3]);
+      mde::st4(out, make_float4(v[0], v[1], v[2], v[3]));
     } else {
 #pragma unroll
       for (int k = 0; k < VEC; ++k)
-        if (ch * VEC + k < wo) out[k] = v[k];
+        if (ch * VEC + k < wo) mde::st1(out + k, v[k]);
     }
   }
 }
@@ -495,9 +496,9 @@ inline dim3 quad_grid(int64_t planes, int64_t hi, int64_t wi) {
 constexpr int kXsRows = 4;   // input rows per lane
 constexpr int kXsWarps = 4;  // threadIdx.y
 
-template <int S>
+template <int S, typename T>
 __global__ void __launch_bounds__(64 * kXsWarps)
-    bilinear_fwd_xs_kernel(const float* __restrict__ x, float* __restrict__ y, int hi, int wi) {
+    bilinear_fwd_xs_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi) {
   const int lane = threadIdx.x;
   const int j = blockIdx.x * 64 + lane;
   const int i0 = (blockIdx.y * kXsWarps + threadIdx.y) * kXsRows;
@@ -505,7 +506,7 @@ __global__ void __launch_bounds__(64 * kXsWarps)
   const bool ok = j < wi;
   const int jc = ok ? j : wi - 1;
   const int64_t plane = blockIdx.z;
-  const float* xp = x + plane * hi * (int64_t)wi;
+  const T* xp = x + plane * hi * (int64_t)wi;
   const int wo = S * wi, ho = S * hi;
   const float sc = 1.f / S;
   // this lane's S output columns: input columns and weights (exact ATen math)
@@ -514,14 +515,15 @@ __global__ void __launch_bounds__(64 * kXsWarps)
   for (int q = 0; q < S; ++q) W[q] = lin_index(sc, S * jc + q, wi, 0);
   auto hrow = [&](int r, float* o) {
     r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
-    const float* row = xp + (int64_t)r * wi;
+    const T* row = xp + (int64_t)r * wi;
 #pragma unroll
-    for (int q = 0; q < S; ++q) o[q] = W[q].l0 * row[W[q].i0] + W[q].l1 * row[W[q].i1];
+    for (int q = 0; q < S; ++q)
+      o[q] = W[q].l0 * mde::ld1(row + W[q].i0) + W[q].l1 * mde::ld1(row + W[q].i1);
   };
   float rows[kXsRows + 2][S];
 #pragma unroll
   for (int k = 0; k < kXsRows + 2; ++k) hrow(i0 - 1 + k, rows[k]);
-  float* yp = y + plane * ho * (int64_t)wo + S * jc;
+  T* yp = y + plane * ho * (int64_t)wo + S * jc;
 #pragma unroll
   for (int k = 0; k < kXsRows; ++k) {
     const int i = i0 + k;
@@ -541,16 +543,15 @@ __global__ void __launch_bounds__(64 * kXsWarps)
       if (ok) {
 #pragma unroll
         for (int c = 0; c < S; c += 4)
-          *reinterpret_cast<float4*>(yp + (int64_t)r * wo + c) =
-              make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]);
+          mde::st4(yp + (int64_t)r * wo + c, make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]));
       }
     }
   }
 }
 
-template <int S>
+template <int S, typename T>
 __global__ void __launch_bounds__(64 * kXsWarps)
-    bilinear_bwd_xs_kernel(const float* __restrict__ gy, float* __restrict__ gx, int hi, int wi) {
+    bilinear_bwd_xs_kernel(const T* __restrict__ gy, T* __restrict__ gx, int hi, int wi) {
   constexpr int HALF = S / 2;
   const int lane = threadIdx.x;
   const int j = blockIdx.x * 64 + lane;
@@ -561,7 +562,7 @@ __global__ void __launch_bounds__(64 * kXsWarps)
   const int64_t plane = blockIdx.z;
   const int wo = S * wi, ho = S * hi;
   const float sc = 1.f / S;
-  const float* gp = gy + plane * ho * (int64_t)wo;
+  const T* gp = gy + plane * ho * (int64_t)wo;
   // weights of output columns S*j - HALF .. S*j + S + HALF - 1 for input column j
   float wc[2 * S];
 #pragma unroll
@@ -580,11 +581,11 @@ __global__ void __launch_bounds__(64 * kXsWarps)
     const int rq = S * ib - HALF + k;
     const bool rv = rq >= 0 && rq < ho;
     const int r = rq < 0 ? 0 : (rq > ho - 1 ? ho - 1 : rq);
-    const float* row = gp + (int64_t)r * wo;
+    const T* row = gp + (int64_t)r * wo;
     float v[S];
 #pragma unroll
     for (int c = 0; c < S; c += 4) {
-      const float4 t = *reinterpret_cast<const float4*>(row + S * jc + c);
+      const float4 t = mde::ld4(row + S * jc + c);
       v[c] = t.x; v[c + 1] = t.y; v[c + 2] = t.z; v[c + 3] = t.w;
     }
     float s = 0.f;
@@ -594,8 +595,8 @@ __global__ void __launch_bounds__(64 * kXsWarps)
       // column outside the plane has weight 0) -- no shuffles, no selects,
       // nothing hipcc could turn into a branch around a load
       const int cl = S * jc - HALF + h, cr = S * jc + S + h;
-      s += wc[h] * row[cl >= 0 ? cl : 0];
-      s += wc[S + HALF + h] * row[cr < wo ? cr : wo - 1];
+      s += wc[h] * mde::ld1(row + (cl >= 0 ? cl : 0));
+      s += wc[S + HALF + h] * mde::ld1(row + (cr < wo ? cr : wo - 1));
     }
 #pragma unroll
     for (int c = 0; c < S; ++c) s += wc[HALF + c] * v[c];
@@ -610,10 +611,10 @@ __global__ void __launch_bounds__(64 * kXsWarps)
     }
   }
   if (!ok) return;
-  float* out = gx + (plane * hi + ib) * (int64_t)wi + j;
+  T* out = gx + (plane * hi + ib) * (int64_t)wi + j;
 #pragma unroll
   for (int b = 0; b < kXsRows; ++b)
-    if (ib + b < hi) out[(int64_t)b * wi] = acc[b];
+    if (ib + b < hi) mde::st1(out + (int64_t)b * wi, acc[b]);
 }
 
 inline dim3 xs_grid(int64_t planes, int64_t hi, int64_t wi) {
@@ -643,8 +644,9 @@ inline dim3 x2_grid(int64_t planes, int64_t hi, int64_t wi) {
 // windows (exact ATen source-index math, zero-padded to kw / kh entries).
 constexpr int kPlaneMax = 12288;  // floats of gy (and of t) per block
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_bwd_plane_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+    bilinear_bwd_plane_kernel(const T* __restrict__ gy, T* __restrict__ gx,
                               int hi, int wi, int ho, int wo, float sh, float sw,
                               int align, int kh, int kw) {
   extern __shared__ float lds[];
@@ -656,9 +658,9 @@ __global__ void __launch_bounds__(256)
   int* rlo = clo + wi;                // [hi]
   const int tid = threadIdx.x;
   const int64_t plane = blockIdx.x;
-  const float* g = gy + plane * ho * (int64_t)wo;
+  const T* g = gy + plane * ho * (int64_t)wo;
   const int np = ho * wo;
-  for (int e = tid; e < np; e += 256) sg[e] = g[e];
+  for (int e = tid; e < np; e += 256) sg[e] = mde::ld1(g + e);
   for (int e = tid; e < wi * kw; e += 256) {
     const int j = e / kw, k = e % kw;
     int lo, hi_;
@@ -684,14 +686,14 @@ __global__ void __launch_bounds__(256)
     st[e] = acc;
   }
   __syncthreads();
-  float* out = gx + plane * hi * (int64_t)wi;
+  T* out = gx + plane * hi * (int64_t)wi;
   for (int e = tid; e < hi * wi; e += 256) {
     const int i = e / wi, j = e % wi;
     const float* wr = rw + i * kh;
     const int lo = rlo[i];
     float acc = 0.f;
     for (int k = 0; k < kh; ++k) acc += wr[k] * st[min(lo + k, ho - 1) * wi + j];
-    out[e] = acc;
+    mde::st1(out + e, acc);
   }
 }
 
@@ -707,8 +709,9 @@ __global__ void __launch_bounds__(256)
 constexpr int kBandRows = 4;
 constexpr int kColWin = 32;
 
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_bwd_band_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+    bilinear_bwd_band_kernel(const T* __restrict__ gy, T* __restrict__ gx,
                              int64_t planes, int hi, int wi, int ho, int wo,
                              float sh, float sw, int align) {
   const int bands = (hi + kBandRows - 1) / kBandRows;
@@ -729,7 +732,7 @@ __global__ void __launch_bounds__(256)
     int rlo, rhi, unused;
     lin_window(sh, ib, ho, &rlo, &unused);
     lin_window(sh, ilast, ho, &unused, &rhi);
-    const float* g = gy + plane * ho * (int64_t)wo;
+    const T* g = gy + plane * ho * (int64_t)wo;
     float acc[kBandRows];
 #pragma unroll
     for (int b = 0; b < kBandRows; ++b) acc[b] = 0.f;
@@ -738,12 +741,12 @@ __global__ void __launch_bounds__(256)
       const int d0 = H.i0 - ib, d1 = H.i1 - ib;
       if ((unsigned)d0 >= (unsigned)kBandRows && (unsigned)d1 >= (unsigned)kBandRows)
         continue;
-      const float* grow = g + (int64_t)o * wo;
+      const T* grow = g + (int64_t)o * wo;
       float s = 0.f;
 #pragma unroll
       for (int k = 0; k < kColWin; ++k) {
         const int p = clo + k < wo - 1 ? clo + k : wo - 1;
-        s += cw[k] * grow[p];
+        s += cw[k] * mde::ld1(grow + p);
       }
 #pragma unroll
       for (int b = 0; b < kBandRows; ++b) {
@@ -753,16 +756,17 @@ __global__ void __launch_bounds__(256)
         acc[b] += wgt * s;
       }
     }
-    float* out = gx + (plane * hi + ib) * (int64_t)wi + j;
+    T* out = gx + (plane * hi + ib) * (int64_t)wi + j;
 #pragma unroll
     for (int b = 0; b < kBandRows; ++b)
-      if (ib + b < hi) out[(int64_t)b * wi] = acc[b];
+      if (ib + b < hi) mde::st1(out + (int64_t)b * wi, acc[b]);
   }
 }
 
 // Backward, generic ratio: candidate windows per axis, exact weights.
+template <typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_bwd_kernel(const float* __restrict__ gy, float* __restrict__ gx,
+    bilinear_bwd_kernel(const T* __restrict__ gy, T* __restrict__ gx,
                         int64_t planes, int hi, int wi, int ho, int wo,
                         float sh, float sw, int align) {
   const int64_t total = planes * hi * (int64_t)wi;
@@ -775,18 +779,18 @@ __global__ void __launch_bounds__(256)
     int rlo, rhi, clo, chi;
     lin_window(sh, i, ho, &rlo, &rhi);
     lin_window(sw, j, wo, &clo, &chi);
-    const float* g = gy + plane * ho * (int64_t)wo;
+    const T* g = gy + plane * ho * (int64_t)wo;
     float acc = 0.f;
     for (int o = rlo; o <= rhi; ++o) {
       const float wr = lin_weight(sh, o, i, hi, align);
       if (wr == 0.f) continue;
-      const float* grow = g + (int64_t)o * wo;
+      const T* grow = g + (int64_t)o * wo;
       for (int p = clo; p <= chi; ++p) {
         const float wc = lin_weight(sw, p, j, wi, align);
-        if (wc != 0.f) acc += (wr * wc) * grow[p];
+        if (wc != 0.f) acc += (wr * wc) * mde::ld1(grow + p);
       }
     }
-    gx[t] = acc;
+    mde::st1(gx + t, acc);
   }
 }
 
@@ -842,6 +846,37 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// The guide pyramid (GuideDepth.py:46-47): nearest x0.5 and x0.25 of the
+// same image in one pass.  ATen's nearest source index at these scale factors
+// is floor(dst * 2.0) = 2 dst and floor(dst * 4.0) = 4 dst, so
+//   half[r][c] = x[2r][2c],   quarter[r][c] = x[4r][4c] = half[2r][2c].
+// One lane reads 8 consecutive pixels of an even input row (two float4; odd
+// rows are never fetched) and writes 4 half-resolution pixels (float4) and,
+// on rows 4k, 2 quarter-resolution pixels (float2).  Lanes run fastest along
+// the row, so every wave reads and writes contiguous bytes.  Needs w % 8 == 0
+// and h % 4 == 0 (the 640 x 480 input); the host falls back to two
+// nearest_fwd launches otherwise.
+__global__ void __launch_bounds__(256)
+    nearest_pyramid_kernel(const float* __restrict__ x, float* __restrict__ half,
+                           float* __restrict__ quarter, int64_t planes, int h, int w) {
+  const int ho = h >> 1, wo = w >> 1, wq = w >> 2, quads = w >> 3;
+  const int64_t total = planes * ho * (int64_t)quads;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int q = (int)(t % quads);
+    const int64_t pr = t / quads;  // plane * ho + r
+    const int r = (int)(pr % ho);
+    const int64_t plane = pr / ho;
+    const float* src = x + (plane * h + 2 * r) * (int64_t)w + 8 * q;
+    const float4 a = *reinterpret_cast<const float4*>(src);
+    const float4 b = *reinterpret_cast<const float4*>(src + 4);
+    *reinterpret_cast<float4*>(half + pr * wo + 4 * q) = make_float4(a.x, a.z, b.x, b.z);
+    if ((r & 1) == 0)
+      *reinterpret_cast<float2*>(quarter + (plane * (h >> 2) + (r >> 1)) * (int64_t)wq + 2 * q) =
+          make_float2(a.x, b.x);
+  }
+}
+
 inline int grid_for(int64_t work) {
   const int64_t b = mde::cdiv(work, 256);
   return (int)(b < 1 ? 1 : (b > 16384 ? 16384 : b));
@@ -868,6 +903,100 @@ bool dims_ok(int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
 
 }  // namespace
 
+namespace {
+
+// Forward dispatch, one storage type: the exact x2 / x4 / x8 kernels, else
+// the generic one.  fp32 x2: the pair kernel (quad only under MDE_X2_QUAD=2,
+// see quad_f32); bf16 x2: the quad kernel (lane loads / stores of 8 / 16
+// bytes, as the fp32 pair kernel's).
+template <typename T>
+int bilinear_fwd_t(const T* x, T* y, int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
+                    int64_t wo, float scale_h, float scale_w, int align_corners, hipStream_t s) {
+  constexpr bool kBf = sizeof(T) == 2;
+  const int64_t rows = n * c * ho;
+  const double bytes = (double)sizeof(T) * n * c * (double)(hi * wi + ho * wo);
+  const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
+                  ho == 2 * hi && wo == 2 * wi && n * c <= 65535;
+  // The pair kernel (two columns per lane) wins when it keeps at least as many lanes
+  // busy as the one-column kernel: 64-lane rows of wi/2 pairs vs of wi columns.
+  const bool pair = x2 && wi % 2 == 0 &&
+                    mde::cdiv(wi, 64) >= 2 * mde::cdiv(wi / 2, 64);
+  const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, n * c);
+  if (xs == 4) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_xs_kernel<4, T>),
+               xs_grid(n * c, hi, wi), dim3(64, kXsWarps), 0, x, y, (int)hi, (int)wi);
+  } else if (xs == 8) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_xs_kernel<8, T>),
+               xs_grid(n * c, hi, wi), dim3(64, kXsWarps), 0, x, y, (int)hi, (int)wi);
+  } else if (x2 && wi % 4 == 0 && (kBf || quad_f32() > 1)) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_quad_kernel<T>,
+               quad_grid(n * c, hi, wi), dim3(256), 0, x, y, n * c, (int)hi, (int)wi);
+  } else if (pair || (kBf && x2 && wi % 2 == 0)) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel<T>,
+               x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, x, y, (int)hi, (int)wi);
+  } else if (x2) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel<T>, x2_grid(n * c, hi, wi),
+               dim3(64, kX2Warps), 0, x, y, (int)hi, (int)wi);
+  } else if (wo % 4 == 0) {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_kernel<4, T>),
+               dim3(grid_for(rows * (wo / 4))), dim3(256), 0, x, y, rows, (int)hi, (int)wi,
+               (int)ho, (int)wo, scale_h, scale_w, align_corners);
+  } else {
+    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_kernel<1, T>),
+               dim3(grid_for(rows * wo)), dim3(256), 0, x, y, rows, (int)hi, (int)wi, (int)ho,
+               (int)wo, scale_h, scale_w, align_corners);
+  }
+  return MDE_OK;
+}
+
+template <typename T>
+int bilinear_bwd_t(const T* gy, T* gx, int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
+                    int64_t wo, float scale_h, float scale_w, int align_corners, hipStream_t s) {
+  constexpr bool kBf = sizeof(T) == 2;
+  const int64_t planes = n * c;
+  const double bytes = (double)sizeof(T) * n * c * (double)(hi * wi + ho * wo);
+  const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
+                  ho == 2 * hi && wo == 2 * wi && planes <= 65535;
+  const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes);
+  if (xs == 4) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_xs_kernel<4, T>),
+               xs_grid(planes, hi, wi), dim3(64, kXsWarps), 0, gy, gx, (int)hi, (int)wi);
+  } else if (xs == 8) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_xs_kernel<8, T>),
+               xs_grid(planes, hi, wi), dim3(64, kXsWarps), 0, gy, gx, (int)hi, (int)wi);
+  } else if (x2 && wi % 4 == 0 && (kBf || quad_f32() > 0)) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_quad_kernel<false, T>),
+               quad_grid(planes, hi, wi), dim3(256), 0, gy, gx, planes, (int)hi, (int)wi,
+               (const T*)nullptr);
+  } else if (x2 && wi % 2 == 0) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_pair_kernel<false, T>),
+               x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, gy, gx, (int)hi, (int)wi,
+               (const T*)nullptr);
+  } else if (x2) {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel<T>, x2_grid(planes, hi, wi),
+               dim3(64, kX2Warps), 0, gy, gx, (int)hi, (int)wi);
+  } else if (plane_fits(hi, wi, ho, wo, scale_h, scale_w)) {
+    const int kh = win_len(scale_h, ho), kw = win_len(scale_w, wo);
+    const size_t lds = sizeof(float) * ((size_t)ho * wo + (size_t)ho * wi + (size_t)wi * kw +
+                                        (size_t)hi * kh + wi + hi);
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_plane_kernel<T>, dim3((unsigned)planes),
+               dim3(256), lds, gy, gx, (int)hi, (int)wi, (int)ho, (int)wo, scale_h, scale_w,
+               align_corners, kh, kw);
+  } else if (scale_w > 0.f && 3.0 / scale_w + 6.0 <= kColWin) {
+    const int64_t bands = mde::cdiv(hi, kBandRows);
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_band_kernel<T>,
+               dim3(grid_for(planes * bands * wi)), dim3(256), 0, gy, gx, planes, (int)hi,
+               (int)wi, (int)ho, (int)wo, scale_h, scale_w, align_corners);
+  } else {
+    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_kernel<T>,
+               dim3(grid_for(planes * hi * wi)), dim3(256), 0, gy, gx, planes, (int)hi, (int)wi,
+               (int)ho, (int)wo, scale_h, scale_w, align_corners);
+  }
+  return MDE_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
@@ -877,63 +1006,11 @@ int mde_bilinear_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
   if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   if (!x || !y || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t rows = n * c * ho;
-  const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
-  const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
-                  ho == 2 * hi && wo == 2 * wi && n * c <= 65535;
-  // The pair kernel (two columns per lane) wins when it keeps at least as many lanes
-  // busy as the one-column kernel: 64-lane rows of wi/2 pairs vs of wi columns.
-  const bool pair = x2 && wi % 2 == 0 &&
-                    mde::cdiv(wi, 64) >= 2 * mde::cdiv(wi / 2, 64);
-  if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
-    using B = mde::bf16;
-    if (x2 && wi % 4 == 0)
-      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_quad_kernel<B>,
-                 quad_grid(n * c, hi, wi), dim3(256), 0, (const B*)x, (B*)y, n * c, (int)hi,
-                 (int)wi);
-    else if (pair)
-      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_pair_kernel<B>,
-                 x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)x, (B*)y, (int)hi,
-                 (int)wi);
-    else if (x2)
-      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes / 2, s, bilinear_fwd_x2_kernel<B>,
-                 x2_grid(n * c, hi, wi), dim3(64, kX2Warps), 0, (const B*)x, (B*)y, (int)hi,
-                 (int)wi);
-    else
-      return MDE_ERR_UNSUPPORTED;
-    return MDE_OK;
-  }
-  const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, n * c);
-  if (xs == 4) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<4>, xs_grid(n * c, hi, wi),
-               dim3(64, kXsWarps), 0, (const float*)x, (float*)y, (int)hi, (int)wi);
-  } else if (xs == 8) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_xs_kernel<8>, xs_grid(n * c, hi, wi),
-               dim3(64, kXsWarps), 0, (const float*)x, (float*)y, (int)hi, (int)wi);
-  } else if (x2 && wi % 4 == 0 && quad_f32() > 1) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_quad_kernel<float>,
-               quad_grid(n * c, hi, wi), dim3(256), 0, (const float*)x, (float*)y, n * c, (int)hi,
-               (int)wi);
-  } else if (pair) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_pair_kernel<float>,
-               x2_grid(n * c, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)x, (float*)y,
-               (int)hi, (int)wi);
-  } else if (x2) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel<float>,
-               x2_grid(n * c, hi, wi), dim3(64, kX2Warps), 0, (const float*)x,
-               (float*)y, (int)hi, (int)wi);
-  } else if (wo % 4 == 0) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_kernel<4>,
-               dim3(grid_for(rows * (wo / 4))), dim3(256), 0,
-               (const float*)x, (float*)y, rows, (int)hi, (int)wi, (int)ho,
-               (int)wo, scale_h, scale_w, align_corners);
-  } else {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_kernel<1>,
-               dim3(grid_for(rows * wo)), dim3(256), 0, (const float*)x,
-               (float*)y, rows, (int)hi, (int)wi, (int)ho, (int)wo, scale_h,
-               scale_w, align_corners);
-  }
-  return MDE_OK;
+  if (dtype == MDE_BF16)
+    return bilinear_fwd_t((const mde::bf16*)x, (mde::bf16*)y, n, c, hi, wi, ho, wo, scale_h,
+                          scale_w, align_corners, s);
+  return bilinear_fwd_t((const float*)x, (float*)y, n, c, hi, wi, ho, wo, scale_h, scale_w,
+                        align_corners, s);
 }
 
 int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
@@ -943,67 +1020,11 @@ int mde_bilinear_bwd(const void* gy, void* gx, int64_t n, int64_t c,
   if (dtype != MDE_F32 && dtype != MDE_BF16) return MDE_ERR_UNSUPPORTED;
   if (!gy || !gx || !dims_ok(n, c, hi, wi, ho, wo)) return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
-  const int64_t planes = n * c;
-  const double bytes = 4.0 * n * c * (double)(hi * wi + ho * wo);
-  const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
-                  ho == 2 * hi && wo == 2 * wi && planes <= 65535;
-  const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes);
-  if (dtype == MDE_BF16) {  // bf16 storage (autocast): the exact x2 kernels only
-    using B = mde::bf16;
-    if (x2 && !xs && wi % 4 == 0)
-      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_quad_kernel<false, B>),
-                 quad_grid(planes, hi, wi), dim3(256), 0, (const B*)gy, (B*)gx, planes, (int)hi,
-                 (int)wi, nullptr);
-    else if (x2 && !xs && wi % 2 == 0)
-      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, (bilinear_bwd_x2_pair_kernel<false, B>),
-                 x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx,
-                 (int)hi, (int)wi, nullptr);
-    else if (x2 && !xs)
-      MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes / 2, s, bilinear_bwd_x2_kernel<B>,
-                 x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const B*)gy, (B*)gx, (int)hi,
-                 (int)wi);
-    else
-      return MDE_ERR_UNSUPPORTED;
-    return MDE_OK;
-  }
-  if (xs == 4) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<4>, xs_grid(planes, hi, wi),
-               dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
-  } else if (xs == 8) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_xs_kernel<8>, xs_grid(planes, hi, wi),
-               dim3(64, kXsWarps), 0, (const float*)gy, (float*)gx, (int)hi, (int)wi);
-  } else if (x2 && wi % 4 == 0 && quad_f32() > 0) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_quad_kernel<false, float>),
-               quad_grid(planes, hi, wi), dim3(256), 0, (const float*)gy, (float*)gx, planes,
-               (int)hi, (int)wi, nullptr);
-  } else if (x2 && wi % 2 == 0) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_pair_kernel<false, float>),
-               x2_grid(planes, hi, wi / 2), dim3(64, kX2Warps), 0, (const float*)gy,
-               (float*)gx, (int)hi, (int)wi, nullptr);
-  } else if (x2) {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_x2_kernel<float>,
-               x2_grid(planes, hi, wi), dim3(64, kX2Warps), 0, (const float*)gy,
-               (float*)gx, (int)hi, (int)wi);
-  } else if (plane_fits(hi, wi, ho, wo, scale_h, scale_w)) {
-    const int kh = win_len(scale_h, ho), kw = win_len(scale_w, wo);
-    const size_t lds = sizeof(float) * ((size_t)ho * wo + (size_t)ho * wi + (size_t)wi * kw +
-                                        (size_t)hi * kh + wi + hi);
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_plane_kernel, dim3((unsigned)planes),
-               dim3(256), lds, (const float*)gy, (float*)gx, (int)hi, (int)wi, (int)ho,
-               (int)wo, scale_h, scale_w, align_corners, kh, kw);
-  } else if (scale_w > 0.f && 3.0 / scale_w + 6.0 <= kColWin) {
-    const int64_t bands = mde::cdiv(hi, kBandRows);
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_band_kernel,
-               dim3(grid_for(planes * bands * wi)), dim3(256), 0,
-               (const float*)gy, (float*)gx, planes, (int)hi, (int)wi,
-               (int)ho, (int)wo, scale_h, scale_w, align_corners);
-  } else {
-    MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_kernel,
-               dim3(grid_for(planes * hi * wi)), dim3(256), 0,
-               (const float*)gy, (float*)gx, planes, (int)hi, (int)wi,
-               (int)ho, (int)wo, scale_h, scale_w, align_corners);
-  }
-  return MDE_OK;
+  if (dtype == MDE_BF16)
+    return bilinear_bwd_t((const mde::bf16*)gy, (mde::bf16*)gx, n, c, hi, wi, ho, wo, scale_h,
+                          scale_w, align_corners, s);
+  return bilinear_bwd_t((const float*)gy, (float*)gx, n, c, hi, wi, ho, wo, scale_h, scale_w,
+                        align_corners, s);
 }
 
 static bool x2_pair(int64_t planes, int64_t hi, int64_t wi, int64_t ho, int64_t wo, float scale_h,
@@ -1064,6 +1085,26 @@ int mde_nearest_fwd(const void* x, void* y, int64_t n, int64_t c, int64_t hi,
              dim3(grid_for(n * c * ho * wo)), dim3(256), 0, (const float*)x,
              (float*)y, n * c, (int)hi, (int)wi, (int)ho, (int)wo, scale_h,
              scale_w);
+  return MDE_OK;
+}
+
+int mde_nearest_pyramid_supported(int64_t n, int64_t c, int64_t h, int64_t w) {
+  return n > 0 && c > 0 && h >= 4 && w >= 8 && h % 4 == 0 && w % 8 == 0 && h < (1 << 30) &&
+         w < (1 << 30);
+}
+
+int mde_nearest_pyramid(const void* x, void* half, void* quarter, int64_t n, int64_t c, int64_t h,
+                        int64_t w, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !half || !quarter) return MDE_ERR_INVALID_ARG;
+  if (!mde_nearest_pyramid_supported(n, c, h, w)) return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  // algorithmic bytes of the two nearest_fwd calls it replaces (read + write
+  // of every output element)
+  const double bytes = 8.0 * n * c * (double)((h / 2) * (w / 2) + (h / 4) * (w / 4));
+  MDE_LAUNCH(mde::K_NEAREST_FWD, bytes, s, nearest_pyramid_kernel,
+             dim3(grid_for(n * c * (h / 2) * (w / 8))), dim3(256), 0, (const float*)x,
+             (float*)half, (float*)quarter, n * c, (int)h, (int)w);
   return MDE_OK;
 }
 

@@ -28,7 +28,7 @@ _amp_bwd = torch.amp.custom_bwd(device_type="cuda")
 _bn_fwd = torch.amp.custom_fwd(device_type="cuda")
 
 __all__ = [
-    "interpolate", "bilinear_resize", "nearest_resize", "se_cat", "skip_reduce",
+    "interpolate", "bilinear_resize", "nearest_resize", "nearest_pyramid", "se_cat", "skip_reduce",
     "minmax", "depth_norm", "ssim3_l1", "depth_loss",
 ]
 
@@ -105,21 +105,17 @@ class GradSlot:
         return g
 
 
-def _x2_exact(x, ho, wo, sh, sw, align) -> bool:
-    """The exact x2 upsample (align_corners=False): the resize shape with bf16 kernels."""
-    n, c, hi, wi = x.shape
-    return (not align and sh == 0.5 and sw == 0.5 and ho == 2 * hi and wo == 2 * wi
-            and n * c <= 65535)
-
-
 class _Bilinear(torch.autograd.Function):
-    # bf16 storage (autocast) for the exact x2 upsample -- the decoder's
-    # GuideDepth.py:49,52,55, between bf16 convolutions -- so no cast copies
-    # surround it; other ratios compute in fp32.
+    # bf16 storage (autocast) at every ratio -- the decoder's x2 upsamples
+    # (GuideDepth.py:49,52,55) and DDRNet's generic resizes (DDRNet_23_slim.py:
+    # 182-191, 332-351), all between bf16 convolutions -- so no cast copies
+    # surround them and the sums they feed stay bf16, as F.interpolate under
+    # autocast keeps its input dtype.  Arithmetic is fp32 (the fp32 kernels'
+    # order, rounded once on store).
     @staticmethod
     @_bn_fwd
     def forward(ctx, x, ho, wo, sh, sw, align, slot=None):
-        keep = x.dtype == torch.bfloat16 and _x2_exact(x, ho, wo, sh, sw, align)
+        keep = x.dtype == torch.bfloat16
         x = (x if keep else x.float()).contiguous()
         n, c, hi, wi = x.shape
         y = torch.empty((n, c, ho, wo), dtype=x.dtype, device=x.device)
@@ -218,6 +214,26 @@ def nearest_resize(x, size=None, scale_factor=None, recompute_scale_factor=None)
         raise ValueError("nearest_resize expects a 4-D NCHW tensor")
     ho, wo, sh, sw = _out_size_and_scales(x, size, scale_factor, recompute_scale_factor)
     return _Nearest.apply(x, ho, wo, sh, sw)
+
+
+def nearest_pyramid(x):
+    """(nearest_resize(x, scale_factor=0.5), nearest_resize(x, scale_factor=0.25))
+    -- GuideDepth.py:46-47's two guides -- from one pass over x when x needs
+    no gradient (the network input) and the shape allows it
+    (mde_nearest_pyramid_supported); else the two separate resizes."""
+    _gpu(x)
+    if x.dim() != 4:
+        raise ValueError("nearest_pyramid expects a 4-D NCHW tensor")
+    n, c, h, w = x.shape
+    if ((torch.is_grad_enabled() and x.requires_grad)
+            or not _abi.query("mde_nearest_pyramid_supported", n, c, h, w)):
+        return nearest_resize(x, scale_factor=0.5), nearest_resize(x, scale_factor=0.25)
+    x = x.float().contiguous()  # the nearest ops run in fp32 under autocast too
+    half = torch.empty((n, c, h // 2, w // 2), dtype=x.dtype, device=x.device)
+    quarter = torch.empty((n, c, h // 4, w // 4), dtype=x.dtype, device=x.device)
+    _abi.call("mde_nearest_pyramid", _abi.ptr(x), _abi.ptr(half), _abi.ptr(quarter), n, c, h, w,
+              _abi.dtype_code(x), _abi.stream_of(x))
+    return half, quarter
 
 
 def interpolate(input, size=None, scale_factor=None, mode="nearest", align_corners=None,

@@ -301,6 +301,39 @@ def test_bilinear_x2_bf16_storage_matches_fp32_kernel(c, h, w):
         assert torch.equal(ta, tb.to(torch.bfloat16))
 
 
+# (c, hi, wi, ho, wo, align): DDRNet's resizes (DDRNet_23_slim.py:182-191, 332-351 --
+# 15x20 -> 60x80 on the x4 kernel, 8x10 -> 60x80 and 4x5 -> 8x10 on the plane
+# backward), a band-backward plane (40x50 -> 140x180), the generic backward
+# (4x5 -> 128x128), an odd output width (generic forward, one column per
+# thread), a downsample and align_corners=True
+GENERIC = [(64, 15, 20, 60, 80, False), (128, 8, 10, 60, 80, False), (32, 4, 5, 8, 10, False),
+           (8, 40, 50, 140, 180, False), (4, 4, 5, 128, 128, False), (16, 9, 11, 20, 27, False),
+           (16, 33, 47, 17, 23, False), (8, 12, 16, 30, 41, True)]
+
+
+@pytest.mark.parametrize("c,hi,wi,ho,wo,align", GENERIC)
+def test_bilinear_generic_bf16_storage_matches_fp32_kernel(c, hi, wi, ho, wo, align):
+    """Every non-x2 bilinear kernel on bf16 storage (autocast; F.interpolate
+    keeps its input dtype) == the fp32 kernel on the same values, rounded once:
+    forward and backward bit-exact, output / gradient dtype bf16."""
+    from monocular_depth_estimation_amd.functional import bilinear_resize
+    g = torch.Generator().manual_seed(c + hi + wo)
+    n = 2
+    x = (torch.rand((n, c, hi, wi), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    gy = (torch.rand((n, c, ho, wo), generator=g) - 0.5).to(DEV).to(torch.bfloat16)
+    res = []
+    for dt in (torch.bfloat16, torch.float32):
+        xx = x.detach().to(dt).clone().requires_grad_(True)
+        y = bilinear_resize(xx, size=(ho, wo), align_corners=align)
+        assert y.dtype == dt
+        y.backward(gy.to(dt))
+        assert xx.grad.dtype == dt
+        res.append((y.detach(), xx.grad))
+    (ya, ga), (yb, gb) = res
+    assert torch.equal(ya, yb.to(torch.bfloat16))
+    assert torch.equal(ga, gb.to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("cout,h,w", [(16, 64, 96), (32, 37, 70), (64, 30, 40)])
 def test_guide_conv_bf16_matches_rounded_fp32_kernel(cout, h, w):
     """The autocast guide conv (mde_conv3x3_guide_bf16_fwd, modules.py:52-54):

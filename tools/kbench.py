@@ -120,6 +120,8 @@ def _main():
             ho, wo = int(480 * sf), int(640 * sf)
             report(f"nearest_fwd x{sf} 3x480x640", timeit(lambda: F.nearest_resize(img, scale_factor=sf),
                                                           a.reps), 8.0 * n * 3 * ho * wo)
+        report("nearest_pyramid x0.5+x0.25 3x480x640", timeit(lambda: F.nearest_pyramid(img), a.reps),
+               8.0 * n * 3 * (240 * 320 + 120 * 160))
     # SE + cat and skip fusion at the three decoder resolutions
     for c, h, w, cout in ((64, 120, 160, 32), (32, 240, 320, 16), (16, 480, 640, 1)) \
             if (want("se") or want("skip")) else ():

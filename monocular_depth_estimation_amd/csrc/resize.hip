@@ -40,6 +40,14 @@ __device__ __forceinline__ Lin lin_index(float scale, int dst, int in_size,
   return {i0, i1, __fadd_rn(1.f, -l1), l1};
 }
 
+// l0 a + l1 b with the rounding pinned (one product, one fused multiply-add):
+// the fp32 and bf16-storage instantiations of a kernel must not let the
+// compiler contract the sum differently (bf16 results == rounded fp32 ones).
+__device__ __forceinline__ float lerp2(const Lin& L, float a, float b) {
+  return __fmaf_rn(L.l1, b, __fmul_rn(L.l0, a));
+}
+__device__ __forceinline__ float madd(float w, float v, float acc) { return __fmaf_rn(w, v, acc); }
+
 // Weight with which output index `o` reads input index `i` along one axis.
 __device__ __forceinline__ float lin_weight(float scale, int o, int i,
                                             int in_size, int align) {
@@ -64,34 +72,46 @@ __device__ __forceinline__ void lin_window(float scale, int i, int out_size,
   *hi = b > out_size - 1 ? out_size - 1 : b;
 }
 
-// Forward: each thread produces VEC consecutive outputs of one output row.
+// Forward, generic ratio: each thread produces VEC consecutive outputs of
+// kFwdRows consecutive output rows of one plane.  The column indices and
+// weights (W) are computed once per thread, the row ones (H) once per row;
+// the decomposition of the thread index is 32-bit (the host checks that the
+// thread count fits).  Input rows are gathered (L1 / L2 hits: a row feeds
+// many outputs at upsampling ratios); output rows leave as VEC-wide stores.
+constexpr int kFwdRows = 4;
+
 template <int VEC, typename T>
 __global__ void __launch_bounds__(256)
-    bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y,
-                        int64_t rows, int hi, int wi, int ho, int wo,
-                        float sh, float sw, int align) {
+    bilinear_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int total, int hi, int wi,
+                        int ho, int wo, float sh, float sw, int align) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
   const int chunks = (wo + VEC - 1) / VEC;
-  const int64_t total = rows * chunks;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int ch = (int)(t % chunks);
-    const int64_t row = t / chunks;  // = plane * ho + oh
-    const int oh = (int)(row % ho);
-    const int64_t plane = row / ho;
+  const int groups = (ho + kFwdRows - 1) / kFwdRows;
+  const int ch = t % chunks;
+  const int rg = t / chunks;
+  const int plane = rg / groups;
+  const int oh0 = (rg - plane * groups) * kFwdRows;
+  Lin W[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) {
+    const int ow = ch * VEC + k;
+    W[k] = lin_index(sw, ow < wo ? ow : wo - 1, wi, align);
+  }
+  const T* xp = x + (int64_t)plane * hi * wi;
+#pragma unroll
+  for (int r = 0; r < kFwdRows; ++r) {
+    const int oh = oh0 + r;
+    if (oh >= ho) break;
     const Lin H = lin_index(sh, oh, hi, align);
-    const T* r0 = x + (plane * hi + H.i0) * (int64_t)wi;
-    const T* r1 = x + (plane * hi + H.i1) * (int64_t)wi;
+    const T* r0 = xp + (int64_t)H.i0 * wi;
+    const T* r1 = xp + (int64_t)H.i1 * wi;
     float v[VEC];
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-      const int ow = ch * VEC + k;
-      if (ow < wo) {
-        const Lin W = lin_index(sw, ow, wi, align);
-        v[k] = H.l0 * (W.l0 * mde::ld1(r0 + W.i0) + W.l1 * mde::ld1(r0 + W.i1)) +
-               H.l1 * (W.l0 * mde::ld1(r1 + W.i0) + W.l1 * mde::ld1(r1 + W.i1));
-      }
-    }
-    T* out = y + row * (int64_t)wo + ch * VEC;
+    for (int k = 0; k < VEC; ++k)
+      v[k] = lerp2(H, lerp2(W[k], mde::ld1(r0 + W[k].i0), mde::ld1(r0 + W[k].i1)),
+                   lerp2(W[k], mde::ld1(r1 + W[k].i0), mde::ld1(r1 + W[k].i1)));
+    T* out = y + ((int64_t)plane * ho + oh) * wo + ch * VEC;
     if (VEC == 4 && ch * VEC + 4 <= wo) {
       mde::st4(out, make_float4(v[0], v[1], v[2], v[3]));
     } else {
@@ -100,6 +120,10 @@ __global__ void __launch_bounds__(256)
         if (ch * VEC + k < wo) mde::st1(out + k, v[k]);
     }
   }
+}
+
+inline int64_t fwd_threads(int64_t planes, int64_t ho, int64_t wo, int vec) {
+  return planes * mde::cdiv(ho, kFwdRows) * mde::cdiv(wo, vec);
 }
 
 // Exact x2 (align_corners=False, scale 0.5, out = 2*in).  With ATen's
@@ -494,18 +518,38 @@ inline dim3 quad_grid(int64_t planes, int64_t hi, int64_t wi) {
 // loads are in flight together.  gy rows at band edges are read by two bands
 // (S of every S*kXsRows + S rows, served by L2).
 constexpr int kXsRows = 4;   // input rows per lane
-constexpr int kXsWarps = 4;  // threadIdx.y
+
+// Flat lane mapping: thread t -> (plane, band of kXsRows input rows, column j),
+// columns fastest, so narrow planes (DDRNet's 15 x 20 -> 60 x 80: 20 columns)
+// still fill every lane of a wave instead of 20 of 64.
+struct XsMap {
+  int64_t plane;
+  int ib, j;
+  bool live;
+};
+
+__device__ __forceinline__ XsMap xs_map(int64_t planes, int hi, int wi) {
+  const int bands = (hi + kXsRows - 1) / kXsRows;
+  const int64_t total = planes * bands * (int64_t)wi;
+  int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  XsMap m;
+  m.live = t < total;
+  if (!m.live) t = total - 1;
+  m.j = (int)(t % wi);
+  const int64_t r = t / wi;
+  m.ib = (int)(r % bands) * kXsRows;
+  m.plane = r / bands;
+  return m;
+}
 
 template <int S, typename T>
-__global__ void __launch_bounds__(64 * kXsWarps)
-    bilinear_fwd_xs_kernel(const T* __restrict__ x, T* __restrict__ y, int hi, int wi) {
-  const int lane = threadIdx.x;
-  const int j = blockIdx.x * 64 + lane;
-  const int i0 = (blockIdx.y * kXsWarps + threadIdx.y) * kXsRows;
-  if (i0 >= hi) return;  // uniform per wave
-  const bool ok = j < wi;
-  const int jc = ok ? j : wi - 1;
-  const int64_t plane = blockIdx.z;
+__global__ void __launch_bounds__(256)
+    bilinear_fwd_xs_kernel(const T* __restrict__ x, T* __restrict__ y, int64_t planes, int hi,
+                           int wi) {
+  const XsMap m = xs_map(planes, hi, wi);
+  const int i0 = m.ib, jc = m.j;
+  const bool ok = m.live;
+  const int64_t plane = m.plane;
   const T* xp = x + plane * hi * (int64_t)wi;
   const int wo = S * wi, ho = S * hi;
   const float sc = 1.f / S;
@@ -517,8 +561,7 @@ __global__ void __launch_bounds__(64 * kXsWarps)
     r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
     const T* row = xp + (int64_t)r * wi;
 #pragma unroll
-    for (int q = 0; q < S; ++q)
-      o[q] = W[q].l0 * mde::ld1(row + W[q].i0) + W[q].l1 * mde::ld1(row + W[q].i1);
+    for (int q = 0; q < S; ++q) o[q] = lerp2(W[q], mde::ld1(row + W[q].i0), mde::ld1(row + W[q].i1));
   };
   float rows[kXsRows + 2][S];
 #pragma unroll
@@ -527,7 +570,6 @@ __global__ void __launch_bounds__(64 * kXsWarps)
 #pragma unroll
   for (int k = 0; k < kXsRows; ++k) {
     const int i = i0 + k;
-    if (i >= hi) break;  // uniform per wave
 #pragma unroll
     for (int q = 0; q < S; ++q) {
       const int r = S * i + q;
@@ -539,8 +581,8 @@ __global__ void __launch_bounds__(64 * kXsWarps)
       const float* b = rows[q < S / 2 ? k + 1 : k + 2];
       float o[S];
 #pragma unroll
-      for (int c = 0; c < S; ++c) o[c] = H.l0 * a[c] + H.l1 * b[c];
-      if (ok) {
+      for (int c = 0; c < S; ++c) o[c] = lerp2(H, a[c], b[c]);
+      if (ok && i < hi) {
 #pragma unroll
         for (int c = 0; c < S; c += 4)
           mde::st4(yp + (int64_t)r * wo + c, make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]));
@@ -550,16 +592,14 @@ __global__ void __launch_bounds__(64 * kXsWarps)
 }
 
 template <int S, typename T>
-__global__ void __launch_bounds__(64 * kXsWarps)
-    bilinear_bwd_xs_kernel(const T* __restrict__ gy, T* __restrict__ gx, int hi, int wi) {
+__global__ void __launch_bounds__(256)
+    bilinear_bwd_xs_kernel(const T* __restrict__ gy, T* __restrict__ gx, int64_t planes, int hi,
+                           int wi) {
   constexpr int HALF = S / 2;
-  const int lane = threadIdx.x;
-  const int j = blockIdx.x * 64 + lane;
-  const int ib = (blockIdx.y * kXsWarps + threadIdx.y) * kXsRows;
-  if (ib >= hi) return;  // uniform per wave
-  const bool ok = j < wi;
-  const int jc = ok ? j : wi - 1;
-  const int64_t plane = blockIdx.z;
+  const XsMap m = xs_map(planes, hi, wi);
+  const int ib = m.ib, j = m.j, jc = m.j;
+  const bool ok = m.live;
+  const int64_t plane = m.plane;
   const int wo = S * wi, ho = S * hi;
   const float sc = 1.f / S;
   const T* gp = gy + plane * ho * (int64_t)wo;
@@ -595,11 +635,11 @@ __global__ void __launch_bounds__(64 * kXsWarps)
       // column outside the plane has weight 0) -- no shuffles, no selects,
       // nothing hipcc could turn into a branch around a load
       const int cl = S * jc - HALF + h, cr = S * jc + S + h;
-      s += wc[h] * mde::ld1(row + (cl >= 0 ? cl : 0));
-      s += wc[S + HALF + h] * mde::ld1(row + (cr < wo ? cr : wo - 1));
+      s = madd(wc[h], mde::ld1(row + (cl >= 0 ? cl : 0)), s);
+      s = madd(wc[S + HALF + h], mde::ld1(row + (cr < wo ? cr : wo - 1)), s);
     }
 #pragma unroll
-    for (int c = 0; c < S; ++c) s += wc[HALF + c] * v[c];
+    for (int c = 0; c < S; ++c) s = madd(wc[HALF + c], v[c], s);
     s = rv ? s : 0.f;
     const Lin H = lin_index(sc, r, hi, 0);
 #pragma unroll
@@ -607,7 +647,7 @@ __global__ void __launch_bounds__(64 * kXsWarps)
       float wgt = 0.f;
       if (H.i0 == ib + b) wgt += H.l0;
       if (H.i1 == ib + b) wgt += H.l1;
-      acc[b] += wgt * s;
+      acc[b] = madd(wgt, s, acc[b]);
     }
   }
   if (!ok) return;
@@ -618,8 +658,7 @@ __global__ void __launch_bounds__(64 * kXsWarps)
 }
 
 inline dim3 xs_grid(int64_t planes, int64_t hi, int64_t wi) {
-  return dim3((unsigned)mde::cdiv(wi, 64), (unsigned)mde::cdiv(hi, kXsRows * kXsWarps),
-              (unsigned)planes);
+  return dim3((unsigned)mde::cdiv(planes * mde::cdiv(hi, kXsRows) * wi, 256));
 }
 
 // Integer upsampling ratio handled by the xS kernels (4 or 8), else 0.
@@ -656,6 +695,10 @@ __global__ void __launch_bounds__(256)
   float* rw = cw + wi * kw;           // [hi][kh]
   int* clo = (int*)(rw + hi * kh);    // [wi]
   int* rlo = clo + wi;                // [hi]
+  int* cfirst = rlo + hi;             // [wi] first nonzero tap of column j's window
+  int* ccnt = cfirst + wi;            // [wi] taps from there to the last nonzero one
+  int* rfirst = ccnt + wi;            // [hi]
+  int* rcnt = rfirst + hi;            // [hi]
   const int tid = threadIdx.x;
   const int64_t plane = blockIdx.x;
   const T* g = gy + plane * ho * (int64_t)wo;
@@ -676,23 +719,43 @@ __global__ void __launch_bounds__(256)
     rw[e] = lo + k <= hi_ ? lin_weight(sh, lo + k, i, hi, align) : 0.f;
   }
   __syncthreads();
+  // tight windows: lin_window is conservative (~3/scale + 6 taps, about twice
+  // the ~2/scale + 2 that carry weight); the passes below visit only the taps
+  // between the first and last nonzero weight (zeros inside add exact +0)
+  for (int e = tid; e < wi + hi; e += 256) {
+    const bool col = e < wi;
+    const int idx = col ? e : e - wi, kk = col ? kw : kh;
+    const float* wt = col ? cw + idx * kw : rw + idx * kh;
+    int f = kk, l = -1;
+    for (int k = 0; k < kk; ++k)
+      if (wt[k] != 0.f) {
+        f = k < f ? k : f;
+        l = k;
+      }
+    if (l < 0) f = 0;
+    (col ? cfirst : rfirst)[idx] = f;
+    (col ? ccnt : rcnt)[idx] = l - f + 1;
+  }
+  __syncthreads();
   for (int e = tid; e < ho * wi; e += 256) {
     const int o = e / wi, j = e % wi;
     const float* row = sg + o * wo;
-    const float* wc = cw + j * kw;
-    const int lo = clo[j];
+    const int f = cfirst[j], cnt = ccnt[j];
+    const float* wc = cw + j * kw + f;
+    const int lo = clo[j] + f;
     float acc = 0.f;
-    for (int k = 0; k < kw; ++k) acc += wc[k] * row[min(lo + k, wo - 1)];
+    for (int k = 0; k < cnt; ++k) acc = madd(wc[k], row[min(lo + k, wo - 1)], acc);
     st[e] = acc;
   }
   __syncthreads();
   T* out = gx + plane * hi * (int64_t)wi;
   for (int e = tid; e < hi * wi; e += 256) {
     const int i = e / wi, j = e % wi;
-    const float* wr = rw + i * kh;
-    const int lo = rlo[i];
+    const int f = rfirst[i], cnt = rcnt[i];
+    const float* wr = rw + i * kh + f;
+    const int lo = rlo[i] + f;
     float acc = 0.f;
-    for (int k = 0; k < kh; ++k) acc += wr[k] * st[min(lo + k, ho - 1) * wi + j];
+    for (int k = 0; k < cnt; ++k) acc = madd(wr[k], st[min(lo + k, ho - 1) * wi + j], acc);
     mde::st1(out + e, acc);
   }
 }
@@ -746,14 +809,14 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int k = 0; k < kColWin; ++k) {
         const int p = clo + k < wo - 1 ? clo + k : wo - 1;
-        s += cw[k] * mde::ld1(grow + p);
+        s = madd(cw[k], mde::ld1(grow + p), s);
       }
 #pragma unroll
       for (int b = 0; b < kBandRows; ++b) {
         float wgt = 0.f;
         if (d0 == b) wgt += H.l0;
         if (d1 == b) wgt += H.l1;
-        acc[b] += wgt * s;
+        acc[b] = madd(wgt, s, acc[b]);
       }
     }
     T* out = gx + (plane * hi + ib) * (int64_t)wi + j;
@@ -787,7 +850,7 @@ __global__ void __launch_bounds__(256)
       const T* grow = g + (int64_t)o * wo;
       for (int p = clo; p <= chi; ++p) {
         const float wc = lin_weight(sw, p, j, wi, align);
-        if (wc != 0.f) acc += (wr * wc) * mde::ld1(grow + p);
+        if (wc != 0.f) acc = madd(__fmul_rn(wr, wc), mde::ld1(grow + p), acc);
       }
     }
     mde::st1(gx + t, acc);
@@ -892,7 +955,7 @@ int win_len(float scale, int64_t out_size) {
 bool plane_fits(int64_t hi, int64_t wi, int64_t ho, int64_t wo, float sh, float sw) {
   if (!(sh > 0.f) || !(sw > 0.f) || ho * wo > kPlaneMax || ho * wi > kPlaneMax) return false;
   const int64_t kh = win_len(sh, ho), kw = win_len(sw, wo);
-  return (ho * wo + ho * wi + wi * kw + hi * kh + wi + hi) * 4 <= 64 * 1024;
+  return (ho * wo + ho * wi + wi * kw + hi * kh + 3 * (wi + hi)) * 4 <= 64 * 1024;
 }
 
 bool dims_ok(int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
@@ -913,7 +976,6 @@ template <typename T>
 int bilinear_fwd_t(const T* x, T* y, int64_t n, int64_t c, int64_t hi, int64_t wi, int64_t ho,
                     int64_t wo, float scale_h, float scale_w, int align_corners, hipStream_t s) {
   constexpr bool kBf = sizeof(T) == 2;
-  const int64_t rows = n * c * ho;
   const double bytes = (double)sizeof(T) * n * c * (double)(hi * wi + ho * wo);
   const bool x2 = !align_corners && scale_h == 0.5f && scale_w == 0.5f &&
                   ho == 2 * hi && wo == 2 * wi && n * c <= 65535;
@@ -924,10 +986,10 @@ int bilinear_fwd_t(const T* x, T* y, int64_t n, int64_t c, int64_t hi, int64_t w
   const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, n * c);
   if (xs == 4) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_xs_kernel<4, T>),
-               xs_grid(n * c, hi, wi), dim3(64, kXsWarps), 0, x, y, (int)hi, (int)wi);
+               xs_grid(n * c, hi, wi), dim3(256), 0, x, y, n * c, (int)hi, (int)wi);
   } else if (xs == 8) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_xs_kernel<8, T>),
-               xs_grid(n * c, hi, wi), dim3(64, kXsWarps), 0, x, y, (int)hi, (int)wi);
+               xs_grid(n * c, hi, wi), dim3(256), 0, x, y, n * c, (int)hi, (int)wi);
   } else if (x2 && wi % 4 == 0 && (kBf || quad_f32() > 1)) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_quad_kernel<T>,
                quad_grid(n * c, hi, wi), dim3(256), 0, x, y, n * c, (int)hi, (int)wi);
@@ -937,14 +999,19 @@ int bilinear_fwd_t(const T* x, T* y, int64_t n, int64_t c, int64_t hi, int64_t w
   } else if (x2) {
     MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, bilinear_fwd_x2_kernel<T>, x2_grid(n * c, hi, wi),
                dim3(64, kX2Warps), 0, x, y, (int)hi, (int)wi);
-  } else if (wo % 4 == 0) {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_kernel<4, T>),
-               dim3(grid_for(rows * (wo / 4))), dim3(256), 0, x, y, rows, (int)hi, (int)wi,
-               (int)ho, (int)wo, scale_h, scale_w, align_corners);
   } else {
-    MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_kernel<1, T>),
-               dim3(grid_for(rows * wo)), dim3(256), 0, x, y, rows, (int)hi, (int)wi, (int)ho,
-               (int)wo, scale_h, scale_w, align_corners);
+    const int vec = wo % 4 == 0 ? 4 : 1;
+    const int64_t threads = fwd_threads(n * c, ho, wo, vec);
+    if (threads > INT32_MAX - 256) return MDE_ERR_UNSUPPORTED;
+    const dim3 grid((unsigned)mde::cdiv(threads, 256));
+    if (vec == 4)
+      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_kernel<4, T>), grid, dim3(256), 0, x,
+                 y, (int)threads, (int)hi, (int)wi, (int)ho, (int)wo, scale_h, scale_w,
+                 align_corners);
+    else
+      MDE_LAUNCH(mde::K_BILINEAR_FWD, bytes, s, (bilinear_fwd_kernel<1, T>), grid, dim3(256), 0, x,
+                 y, (int)threads, (int)hi, (int)wi, (int)ho, (int)wo, scale_h, scale_w,
+                 align_corners);
   }
   return MDE_OK;
 }
@@ -960,10 +1027,10 @@ int bilinear_bwd_t(const T* gy, T* gx, int64_t n, int64_t c, int64_t hi, int64_t
   const int xs = xs_ratio(hi, wi, ho, wo, scale_h, scale_w, align_corners, planes);
   if (xs == 4) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_xs_kernel<4, T>),
-               xs_grid(planes, hi, wi), dim3(64, kXsWarps), 0, gy, gx, (int)hi, (int)wi);
+               xs_grid(planes, hi, wi), dim3(256), 0, gy, gx, planes, (int)hi, (int)wi);
   } else if (xs == 8) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_xs_kernel<8, T>),
-               xs_grid(planes, hi, wi), dim3(64, kXsWarps), 0, gy, gx, (int)hi, (int)wi);
+               xs_grid(planes, hi, wi), dim3(256), 0, gy, gx, planes, (int)hi, (int)wi);
   } else if (x2 && wi % 4 == 0 && (kBf || quad_f32() > 0)) {
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, (bilinear_bwd_x2_quad_kernel<false, T>),
                quad_grid(planes, hi, wi), dim3(256), 0, gy, gx, planes, (int)hi, (int)wi,
@@ -978,7 +1045,7 @@ int bilinear_bwd_t(const T* gy, T* gx, int64_t n, int64_t c, int64_t hi, int64_t
   } else if (plane_fits(hi, wi, ho, wo, scale_h, scale_w)) {
     const int kh = win_len(scale_h, ho), kw = win_len(scale_w, wo);
     const size_t lds = sizeof(float) * ((size_t)ho * wo + (size_t)ho * wi + (size_t)wi * kw +
-                                        (size_t)hi * kh + wi + hi);
+                                        (size_t)hi * kh + 3 * (wi + hi));
     MDE_LAUNCH(mde::K_BILINEAR_BWD, bytes, s, bilinear_bwd_plane_kernel<T>, dim3((unsigned)planes),
                dim3(256), lds, gy, gx, (int)hi, (int)wi, (int)ho, (int)wo, scale_h, scale_w,
                align_corners, kh, kw);

@@ -913,7 +913,7 @@ int mde_window_attn_bwd(const void* gout, const void* qk, const float* qk_bias,
     MDE_LAUNCH(mde::K_WATTN_BWD, bytes, s, wattn_bwd_kernel<0>, grid, dim3(256), 0,
                (const float*)gout, (const float*)qk, qk_bias, (const float*)v, table,
                (float*)gqk, (float*)gv, (float*)workspace, (int)nwin, wpb, g);
-  MDE_LAUNCH(mde::K_WATTN_BWD, 4.0 * nblk * heads * (ntab + 2 * D), s,
+  MDE_LAUNCH(mde::K_WATTN_BWD_REDUCE, 4.0 * nblk * heads * (ntab + 2 * D), s,
              wattn_slab_reduce_kernel,
              dim3((unsigned)mde::cdiv(ntab + 2 * D, 64), (unsigned)heads), dim3(1024), 0,
              (const float*)workspace, nblk, (int)heads, ntab, (int)c, gtable, gqk_bias, gv_bias);

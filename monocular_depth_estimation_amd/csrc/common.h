@@ -79,6 +79,7 @@ enum Kid : int {
   K_WINO_FWD,       // Winograd F(2x2, 3x3) stride-1 convolutions (wino.hip)
   K_WINO_DGRAD,
   K_WINO_WEIGHT,
+  K_WATTN_BWD_REDUCE,  // the window-attention backward's table / bias slab reduction
   K_COUNT
 };
 

@@ -122,12 +122,13 @@ __global__ void __launch_bounds__(256)
 constexpr int kSW = 60;  // output columns per strip (64 lanes - 2 x 2 halo)
 
 // Neighbour lanes' values by DPP wave shifts (one VALU op, no LDS round trip):
-// lane_prev = value of lane - 1 (0 into lane 0), lane_next = lane + 1 (0 into 63).
+// lane_prev = value of lane - 1 (0 into lane 0), lane_next = lane + 1 (0 into 63);
+// bound_ctrl writes the 0 itself (no move of an `old` operand first).
 __device__ __forceinline__ float lane_prev(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float lane_next(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
 template <bool GT>
@@ -304,13 +305,26 @@ __global__ void __launch_bounds__(256)
 // (v_pk_fma / v_pk_mul / v_pk_add_f32: two outputs per VALU op) and a 3-wide
 // horizontal sum costs two DPP lane shifts per two outputs instead of per
 // one.  Same algebra, same per-output operation order as ssim3_stream_kernel
-// except the horizontal sums' association (prev + a0) + a1 / (a0 + a1) + next.
+// except the horizontal sums' association (prev + a0) + a1 / (a0 + a1) + next
+// and the two divisions (the DepthNorm of the target and S = n / D): a
+// reciprocal (hardware rcp; the target's refined once per wave) and one
+// residual correction, q = q0 + (n - D q0) r -- packed fp32, 3 operations per
+// pair where the IEEE division sequence took ~10 scalar ones per value (the
+// kernel is VALU-bound).  The corrected quotient is the correctly rounded one
+// except for rare hard cases (then within 1 ulp); an exact quotient of 1 --
+// S(x, x) -- comes out exactly 1.
 using f2 = __attribute__((ext_vector_type(2))) float;
 
 __device__ __forceinline__ f2 pk(float a, float b) { return f2{a, b}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+// n / d given r ~ 1 / d
+__device__ __forceinline__ f2 div2(f2 n, f2 d, f2 r) {
+  const f2 q0 = n * r;
+  return fma2(fma2(-d, q0, n), r, q0);
+}
 
 template <bool GT>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, 3)  // three waves per SIMD (<= 168 VGPRs)
     ssim3_pair_kernel(const float* __restrict__ xp, const float* __restrict__ yp,
                       const float* __restrict__ mm, int h, int w, int sw, int strips, int chunks,
                       int chunk_rows, int64_t nwaves, float gs_ssim, float gs_l1,
@@ -318,7 +332,12 @@ __global__ void __launch_bounds__(256)
   __shared__ float red[4];
   constexpr int NC = GT ? 5 : 3;
   const int lane = threadIdx.x & 63;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  // readfirstlane: the wave index (and the strip, chunk, image and every row
+  // index derived from it) is wave-uniform, so the row offsets live in SGPRs
+  // and reach the buffer loads as their scalar offset -- no per-row VALU
+  // address math (the reflection, a quarter-rate v_mul_lo)
+  const int64_t wid =
+      (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   float lsum = 0.f, l1sum = 0.f;
   if (wid < nwaves) {  // wave-uniform
     const int strip = (int)(wid % strips);
@@ -351,6 +370,10 @@ __global__ void __launch_bounds__(256)
       tmn = mm[0];
       tden = mm[1] - mm[0];
     }
+    // 1 / tden, refined once: the per-pixel DepthNorm divisions become div2
+    const float r0 = __builtin_amdgcn_rcpf(tden);
+    const float rden = fmaf(fmaf(-tden, r0, 1.f), r0, r0);
+    const f2 tmn2 = pk(tmn, tmn), tden2 = pk(tden, tden), rden2 = pk(rden, rden);
     const int g0 = chunk * chunk_rows, g1 = min(h, g0 + chunk_rows);
     const int rs = g0 - 2, re = g1 + 1;
     const float inv9 = 1.f / 9.f, k = gs_ssim * -0.5f;
@@ -363,14 +386,15 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int f = 0; f < NC; ++f) cs[i][f] = pk(0.f, 0.f);
     }
-    auto ld = [&](__amdgpu_buffer_rsrc_t R, int off) {
-      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(R, 4 * off, 0, 0));
+    // lane column offset (VGPR) + the row's offset (SGPR)
+    auto ld = [&](__amdgpu_buffer_rsrc_t R, int col, int rowoff) {
+      return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(R, 4 * col, rowoff, 0));
     };
     auto load = [&](int r, f2& xv, f2& yv) {
-      const int off = reflect1(r, h) * w;
-      xv = pk(ld(XR, off + o0), ld(XR, off + o1));
-      const float t0 = ld(YR, off + o0), t1 = ld(YR, off + o1);
-      yv = norm ? pk((t0 - tmn) / tden, (t1 - tmn) / tden) : pk(t0, t1);
+      const int off = 4 * reflect1(r, h) * w;
+      xv = pk(ld(XR, o0, off), ld(XR, o1, off));
+      const f2 t = pk(ld(YR, o0, off), ld(YR, o1, off));
+      yv = norm ? div2(t - tmn2, tden2, rden2) : t;
     };
     // 3-wide horizontal sums of a column pair: (prev lane's c1) + c0 + c1, c0 + c1 + (next's c0)
     auto hsum = [&](f2 v, f2 wa, f2 wb) {
@@ -412,13 +436,13 @@ __global__ void __launch_bounds__(256)
         const f2 d1 = mx * mx + my * my + kC1, d2 = sxx + syy + kC2;
         const f2 D = d1 * d2;
         const f2 nn = n1 * n2;
-        const f2 S = pk(nn.x / D.x, nn.y / D.y);  // exact division: S(x, x) = 1
+        const f2 rD = pk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y));
+        const f2 S = div2(nn, D, rD);  // corrected quotient: S(x, x) = 1
         const f2 fl = (one2 - S) * 0.5f;
         const float lw = (p < g1 && p >= g0) ? 1.f : 0.f;  // the chunk's own centre rows
         lsum += lw * ((out0 ? fminf(fmaxf(fl.x, 0.f), 1.f) : 0.f) +
                       (out1 ? fminf(fmaxf(fl.y, 0.f), 1.f) : 0.f));
         const bool a0 = v0 && fl.x >= 0.f && fl.x <= 1.f, a1 = v1 && fl.y >= 0.f && fl.y <= 1.f;
-        const f2 rD = pk(__builtin_amdgcn_rcpf(D.x), __builtin_amdgcn_rcpf(D.y));
         const f2 rd1 = pk(__builtin_amdgcn_rcpf(d1.x), __builtin_amdgcn_rcpf(d1.y));
         const f2 rd2 = pk(__builtin_amdgcn_rcpf(d2.x), __builtin_amdgcn_rcpf(d2.y));
         const f2 dS_dsx = -S * rd2;

@@ -84,7 +84,8 @@ NAMES = [
     (r"bn_bwd_apply_table_kernel", "bn_bwd_apply_small"),
     (r"skip_bwd_reg_kernel", "skip_reduce_bwd"),
     (r"wattn_fwd_kernel", "window_attn_fwd"),
-    (r"wattn_(bwd|slab_reduce)_kernel", "window_attn_bwd"),
+    (r"wattn_bwd_kernel", "window_attn_bwd"),
+    (r"wattn_slab_reduce_kernel", "window_attn_bwd_reduce"),
     (r"dw_fwd_(strip|stream)_kernel", "dwconv_fwd"),
     (r"dw_bwd_(strip|stream)_kernel", "dwconv_bwd"),
     (r"dw_bwd_data_kernel", "dwconv_bwd_data"),

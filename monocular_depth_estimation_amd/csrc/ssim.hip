@@ -305,8 +305,9 @@ __global__ void __launch_bounds__(256)
 // (v_pk_fma / v_pk_mul / v_pk_add_f32: two outputs per VALU op) and a 3-wide
 // horizontal sum costs two DPP lane shifts per two outputs instead of per
 // one.  Same algebra, same per-output operation order as ssim3_stream_kernel
-// except the horizontal sums' association (prev + a0) + a1 / (a0 + a1) + next
-// and the two divisions (the DepthNorm of the target and S = n / D): a
+// except the horizontal sums' association ((a0 + a1) + prev / next for the
+// moments, (prev + a0) + a1 / (a0 + a1) + next for the coefficients) and the
+// two divisions (the DepthNorm of the target and S = n / D): a
 // reciprocal (hardware rcp; the target's refined once per wave) and one
 // residual correction, q = q0 + (n - D q0) r -- packed fp32, 3 operations per
 // pair where the IEEE division sequence took ~10 scalar ones per value (the
@@ -419,8 +420,13 @@ __global__ void __launch_bounds__(256, 3)  // three waves per SIMD (<= 168 VGPRs
       yr[2] = yv;
       {
         const f2 v[5] = {xv, yv, xv * xv, yv * yv, xv * yv};
+        // unweighted: (c0 + c1) + {prev lane's c1, next lane's c0} -- one add,
+        // two lane shifts into a register pair, one packed add
 #pragma unroll
-        for (int f = 0; f < 5; ++f) hs[2][f] = hsum(v[f], one2, one2);
+        for (int f = 0; f < 5; ++f) {
+          const float m = v[f].x + v[f].y;
+          hs[2][f] = pk(m, m) + pk(lane_prev(v[f].y), lane_next(v[f].x));
+        }
       }
       if constexpr (PH >= 1) {
         const int p = r - 1;

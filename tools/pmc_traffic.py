@@ -27,7 +27,7 @@ import re
 NAMES = [
     (r"bilinear_fwd\w*_kernel", "bilinear_fwd"),
     (r"bilinear_bwd\w*_kernel", "bilinear_bwd"),
-    (r"nearest_fwd_kernel", "nearest_fwd"),
+    (r"nearest_(fwd|pyramid)_kernel", "nearest_fwd"),
     (r"nearest_bwd_kernel", "nearest_bwd"),
     (r"se_partial_kernel<false>", "se_squeeze"),
     (r"se_partial_kernel<true>", "se_bwd_dot"),

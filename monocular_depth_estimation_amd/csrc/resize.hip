@@ -382,18 +382,30 @@ __global__ void __launch_bounds__(256)
   const T* xp = x + m.plane * hi * (int64_t)wi;
   const int wo = 2 * wi;
   T* yp = y + m.plane * (2 * hi) * (int64_t)wo + 2 * jc;
-  // the neighbour columns jc - 1 / jc + 4 (clamped) as plain loads by every
-  // lane: no lane shuffles and no branch around a load, so no wait inside
+  // Neighbour columns jc - 1 / jc + 4 (clamped).  bf16: plain loads by every
+  // lane -- no lane shuffles and no branch around a load, so no wait inside
   // the unrolled rows (a conditional edge load made the compiler wait for
-  // every load in flight); the extra loads hit the lines the row loads fetch
-  (void)lane;
+  // every load in flight; 16x240x320 backward 104 -> 77 us).  fp32: from the
+  // adjacent lanes by shuffles, loads at the wave / row edges only (plain
+  // loads measured 3-7 % slower there: twice the bytes per extra load).
+  constexpr bool kPlain = sizeof(T) == 2;
+  const bool ledge = lane == 0 || m.q == 0, redge = lane == 63 || m.q == m.quads - 1;
   const int el = jc > 0 ? jc - 1 : 0, er = jc + 4 < wi ? jc + 4 : wi - 1;
   // horizontally interpolated input row r: outputs 2jc .. 2jc+7
   auto hrow = [&](int r, float* o) {
     r = r < 0 ? 0 : (r > hi - 1 ? hi - 1 : r);
     const T* row = xp + (int64_t)r * wi;
     const float4 c = mde::ld4(row + jc);
-    const float l = mde::ld1(row + el), rr = mde::ld1(row + er);
+    float l, rr;
+    if constexpr (kPlain) {
+      l = mde::ld1(row + el);
+      rr = mde::ld1(row + er);
+    } else {
+      l = __shfl_up(c.w, 1, 64);
+      rr = __shfl_down(c.x, 1, 64);
+      if (ledge) l = mde::ld1(row + el);
+      if (redge) rr = mde::ld1(row + er);
+    }
     const float v[6] = {l, c.x, c.y, c.z, c.w, rr};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -437,26 +449,37 @@ __global__ void __launch_bounds__(256)
   const T* gp = gy + m.plane * ho * (int64_t)wo;
   const T* gp2 = TWO ? gy2 + m.plane * ho * (int64_t)wo : nullptr;
   T* xp = gx + m.plane * hi * (int64_t)wi + jc;
-  // neighbour columns 2jc - 1 / 2jc + 8 (clamped): plain loads by every lane,
-  // as in the forward (no shuffles, no branch around a load)
-  (void)lane;
+  // neighbour columns 2jc - 1 / 2jc + 8 (clamped): as in the forward, plain
+  // loads by every lane for bf16, shuffles + edge loads for fp32
+  constexpr bool kPlain = sizeof(T) == 2;
+  const bool ledge = lane == 0 || m.q == 0, redge = lane == 63 || m.q == m.quads - 1;
   const int el = 2 * jc > 0 ? 2 * jc - 1 : 0, er = 2 * jc + 8 < wo ? 2 * jc + 8 : wo - 1;
   // column-filtered gradient row o for input columns jc .. jc+3
   auto hrow = [&](int o, float* h) {
     o = o < 0 ? 0 : (o > ho - 1 ? ho - 1 : o);
     const T* row = gp + (int64_t)o * wo;
+    const T* row2 = TWO ? gp2 + (int64_t)o * wo : nullptr;
     float v[10];  // output-gradient columns 2jc - 1 .. 2jc + 8
     ld8(row + 2 * jc, v + 1);
-    v[0] = mde::ld1(row + el);
-    v[9] = mde::ld1(row + er);
     if (TWO) {
-      const T* row2 = gp2 + (int64_t)o * wo;
       float v2[8];
       ld8(row2 + 2 * jc, v2);
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q + 1] += v2[q];
-      v[0] += mde::ld1(row2 + el);
-      v[9] += mde::ld1(row2 + er);
+    }
+    if constexpr (kPlain) {
+      v[0] = mde::ld1(row + el);
+      v[9] = mde::ld1(row + er);
+      if (TWO) {
+        v[0] += mde::ld1(row2 + el);
+        v[9] += mde::ld1(row2 + er);
+      }
+    } else {
+      float l = __shfl_up(v[8], 1, 64), r = __shfl_down(v[1], 1, 64);
+      if (ledge) l = TWO ? mde::ld1(row + el) + mde::ld1(row2 + el) : mde::ld1(row + el);
+      if (redge) r = TWO ? mde::ld1(row + er) + mde::ld1(row2 + er) : mde::ld1(row + er);
+      v[0] = l;
+      v[9] = r;
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k)

@@ -21,6 +21,7 @@ from torch import nn
 
 from . import _abi
 from .functional import _amp_bwd, _amp_fwd, _gpu, _ws
+from .nn import Conv2d as _HipConv2d
 
 
 def to_2tuple(v):
@@ -371,9 +372,11 @@ class NewCRF(nn.Module):
         super().__init__()
         self.embed_dim = embed_dim
         self.patch_norm = patch_norm
-        self.proj_x = nn.Conv2d(input_dim, embed_dim, 3, padding=1) if input_dim != embed_dim else None
+        # the projections on the HIP 3x3 kernels (Winograd forward / data
+        # gradient where the channel counts allow, + bias), same state_dict keys
+        self.proj_x = _HipConv2d(input_dim, embed_dim, 3, padding=1) if input_dim != embed_dim else None
         if v_dim != embed_dim:
-            self.proj_v = nn.Conv2d(v_dim, embed_dim, 3, padding=1)
+            self.proj_v = _HipConv2d(v_dim, embed_dim, 3, padding=1)
         elif embed_dim % v_dim == 0:
             self.proj_v = None
         v_dim = embed_dim

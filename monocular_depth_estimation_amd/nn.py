@@ -884,13 +884,20 @@ def conv_nobias(conv: nn.Conv2d, x):
 
 class Conv2d(nn.Conv2d):
     """nn.Conv2d (same parameters and state_dict keys) whose bias-free
-    forward takes conv_nobias's HIP kernels where they apply; with a bias it
-    is the stock module (those convs are folded into a BatchNorm by
-    run_sequential / conv_bn instead)."""
+    forward takes conv_nobias's HIP kernels where they apply.  With a bias:
+    a 3x3 / stride-1 conv with a HIP forward or data-gradient pass (the NewCRF
+    projections, newcrf_layers.py: Winograd at 128-1024 channels) runs those
+    passes and adds the bias (its gradient is autograd's sum over the add);
+    anything else is the stock module (the DDRNet / decoder convs with a bias
+    are folded into a BatchNorm by run_sequential / conv_bn instead)."""
 
     def forward(self, x):
-        if self.bias is None and x.is_cuda:
-            return conv_nobias(self, x)
+        if x.is_cuda:
+            if self.bias is None:
+                return conv_nobias(self, x)
+            passes = conv3x3_passes(self, x)
+            if passes is not None and (passes[0] or passes[1]):
+                return conv3x3(x, self.weight, passes) + self.bias.view(1, -1, 1, 1)
         return super().forward(x)
 
 

@@ -162,3 +162,36 @@ def test_wino_weight2_matches_both_transforms():
         _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u1), cin, cout, 1, st)
         _abi.call("mde_wino_weight2", _abi.ptr(wt), _abi.ptr(v0), _abi.ptr(v1), cin, cout, st)
         assert torch.equal(u0, v0) and torch.equal(u1, v1)
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(160, 1024, 15, 20), (112, 512, 30, 40), (64, 128, 120, 160)])
+def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
+    """The NewCRF projections (newcrf_layers.py NewCRF.proj_x / proj_v: 3x3
+    convs WITH a bias, cfg4 bs 16) through nn.Conv2d's biased HIP path: the
+    Winograd forward (and data gradient where cout -> cin is a Winograd shape;
+    112 input channels take MIOpen's), + bias; output and all three gradients
+    vs float64."""
+    from monocular_depth_estimation_amd.nn import WINO, Conv2d, conv3x3_passes
+    n = 16
+    g = torch.Generator().manual_seed(cin + cout + h)
+    x = torch.rand((n, cin, h, w), generator=g) - 0.5
+    wt = (torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.05
+    b = torch.rand((cout,), generator=g) - 0.5
+    gy = torch.rand((n, cout, h, w), generator=g) - 0.5
+    xr, wr, br = (t.double().requires_grad_(True) for t in (x, wt, b))
+    torch.nn.functional.conv2d(xr, wr, br, 1, 1).backward(gy.double())
+    conv = Conv2d(cin, cout, 3, padding=1).to(DEV)
+    with torch.no_grad():
+        conv.weight.copy_(wt)
+        conv.bias.copy_(b)
+    xg = x.to(DEV).requires_grad_(True)
+    passes = conv3x3_passes(conv, xg)
+    assert passes is not None and passes[0] == WINO, passes
+    assert (passes[1] == WINO) == (cin % 32 == 0), passes
+    y = conv(xg)
+    yr = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), 1, 1)
+    assert rel_err(y, yr) <= 1e-5, "forward"
+    y.backward(gy.to(DEV))
+    assert rel_err(xg.grad, xr.grad) <= 1e-5, "data gradient"
+    assert rel_err(conv.weight.grad, wr.grad) <= 2e-5, "weight gradient"
+    assert rel_err(conv.bias.grad, br.grad) <= 1e-5, "bias gradient"

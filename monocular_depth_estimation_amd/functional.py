@@ -423,12 +423,15 @@ class _SSIML1(torch.autograd.Function):
                   float(w_ssim), float(w_l1), _abi.ptr(loss), _abi.ptr(gp), _abi.ptr(gt),
                   b, h, w, _abi.ptr(ws), _abi.dtype_code(pred), _abi.stream_of(pred))
         ctx.save_for_backward(gp, gt)
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the extra output's gradient
         ctx.mark_non_differentiable(loss)
         return loss[0].clone(), loss
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, go, _unused):
+        if go is None:  # only the non-differentiable output was used
+            return (None, None, None, None, None)
         gp, gt = ctx.saved_tensors
         return (gp * go if gp is not None else None,
                 gt * go if gt is not None else None, None, None, None)
@@ -466,12 +469,15 @@ class _DepthLoss(torch.autograd.Function):
         ctx.save_for_backward(pred, gt, out)
         ctx.ws = ws  # holds the forward's SSIM gradient coefficients for the backward
         ctx.params = (float(alpha), float(beta), float(gamma), float(max_depth))
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the extra output's gradient
         ctx.mark_non_differentiable(out)
         return out[0].clone(), out
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, go, _unused):
+        if go is None:  # only the non-differentiable output was used
+            return (None, None, None, None, None, None)
         pred, gt, out = ctx.saved_tensors
         alpha, beta, gamma, max_depth = ctx.params
         n, c, h, w = pred.shape

@@ -199,12 +199,15 @@ class _BNReluPointwise(torch.autograd.Function):
                       _abi.ptr(w2m), _abi.ptr(y2), n, c, cout, h, w, _abi.dtype_code(y1), st)
         ctx.save_for_backward(y1, gamma, beta, mean, invstd, scale, shift, w2m)
         ctx.training, ctx.has_prebias, ctx.w2shape = bool(training), prebias is not None, w2.shape
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the extra output's gradient
         ctx.mark_non_differentiable(stats2)
         return y2, stats2
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, gy2, _gstats2):
+        if gy2 is None:  # only the non-differentiable output was used
+            return (None, None, None, None, None, None, None, None, None, None, None, None, None)
         y1, gamma, beta, mean, invstd, scale, shift, w2m = ctx.saved_tensors
         gy2 = gy2.to(y1.dtype).contiguous()
         n, c, h, w = y1.shape
@@ -438,12 +441,15 @@ class _Conv3x3(torch.autograd.Function):
         ctx.save_for_backward(x, weight)
         ctx.passes = passes
         ctx.u_flip = u_flip
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the extra output's gradient
         ctx.mark_non_differentiable(stats)
         return y, stats
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, gy, _gstats):
+        if gy is None:  # only the non-differentiable output was used
+            return (None, None, None, None)
         x, weight = ctx.saved_tensors
         gy = gy.contiguous()
         n, cin, h, w = x.shape
@@ -540,12 +546,15 @@ class _Conv3x3Bf16(torch.autograd.Function):
             y = torch.nn.functional.conv2d(x, weight.to(torch.bfloat16), None, 1, 1)
         ctx.save_for_backward(x, weight)
         ctx.passes = passes
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the extra output's gradient
         ctx.mark_non_differentiable(stats)
         return y, stats
 
     @staticmethod
     @_amp_bwd
     def backward(ctx, gy, _gstats):
+        if gy is None:  # only the non-differentiable output was used
+            return (None, None, None, None)
         x, weight = ctx.saved_tensors
         gy = gy.to(torch.bfloat16).contiguous()
         n, cin, h, w = x.shape
@@ -795,11 +804,14 @@ class _GuideConvBf16(torch.autograd.Function):
         _abi.call("mde_conv3x3_guide_bf16_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y),
                   _abi.ptr(stats) if nb else None, n, cout, h, w, _abi.stream_of(x))
         ctx.save_for_backward(x, weight)
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the extra output's gradient
         ctx.mark_non_differentiable(stats)
         return y, stats
 
     @staticmethod
     def backward(ctx, gy, _gstats):
+        if gy is None:  # only the non-differentiable output was used
+            return (None, None, None)
         x, weight = ctx.saved_tensors
         gw = None
         if ctx.needs_input_grad[1]:

@@ -203,12 +203,7 @@ __global__ void __launch_bounds__(256, 2)
   constexpr int CPI = RR * RWP + 1;
   constexpr int RAW = kCIC * RR * RW2;    // float2 per chunk
   constexpr int RPT = (RAW + 255) / 256;  // float2 per thread
-  // DB (the 64-channel variant, two blocks per CU by registers either way):
-  // two raw buffers, so chunk c + 1 is staged during chunk c's MFMAs and a
-  // chunk costs two block barriers instead of three
-  constexpr bool DB = CO_B == 64;
-  __shared__ float raw_buf[DB ? 2 : 1][kCIC * CPI];
-  float* raw = raw_buf[0];
+  __shared__ float raw[kCIC * CPI];
   const int gr0 = 2 * br * kTRB - 1, gc0 = 2 * bc * TCB - 2;
   float2 rv[RPT];
   auto load = [&](int chunk) {
@@ -225,7 +220,7 @@ __global__ void __launch_bounds__(256, 2)
       rv[k] = ok ? t : make_float2(0.f, 0.f);
     }
   };
-  auto stage = [&](float* raw) {
+  auto stage = [&]() {
 #pragma unroll
     for (int k = 0; k < RPT; ++k) {
       const int e = tid + 256 * k;
@@ -240,7 +235,7 @@ __global__ void __launch_bounds__(256, 2)
   };
   // B^T d B into V[xi][16-tile group][ci][16]; patch of tile (tr, tc): raw
   // rows 2 tr .. + 3, columns 2 tc + 1 .. + 4
-  auto transform = [&](const float* raw) {
+  auto transform = [&]() {
 #pragma unroll
     for (int pp = 0; pp < PPT; ++pp) {
       const int p = tid + 256 * pp, ch = p / NTB, tl = p % NTB;
@@ -283,27 +278,13 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
   for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 16);
   load(0);
-  if constexpr (DB) {
-    stage(raw_buf[0]);
-    if (nchunks > 1) load(1);
-    __syncthreads();
-  }
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    if constexpr (DB) {
-      transform(raw_buf[chunk & 1]);  // V is free: the last barrier followed its readers
-      __syncthreads();
-      if (chunk + 1 < nchunks) {  // the next chunk's raw tile, under this chunk's MFMAs
-        stage(raw_buf[(chunk + 1) & 1]);
-        if (chunk + 2 < nchunks) load(chunk + 2);
-      }
-    } else {
-      __syncthreads();  // the previous chunk's V (and raw) readers are done
-      stage(raw);
-      __syncthreads();
-      if (chunk + 1 < nchunks) load(chunk + 1);
-      transform(raw);
-      __syncthreads();
-    }
+    __syncthreads();  // the previous chunk's V (and raw) readers are done
+    stage();
+    __syncthreads();
+    if (chunk + 1 < nchunks) load(chunk + 1);
+    transform();
+    __syncthreads();
     const float* uc = ua + (int64_t)chunk * 256;
     const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 256;
 #pragma unroll
@@ -320,7 +301,6 @@ __global__ void __launch_bounds__(256, 2)
         for (int n = 0; n < NTW; ++n)
           acc[xi][n] = mfma(a[s], V[xi][nt0 + n][(4 * s + kq) * 16 + li], acc[xi][n]);
     }
-    if constexpr (DB) __syncthreads();  // V readers done, the next raw tile staged
   }
 
   // A^T M A per (channel, tile): lane holds channels co0 + 4 kq + r, tile 16 (nt0 + n) + li

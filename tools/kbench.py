@@ -57,7 +57,7 @@ def _main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default="")
-    ap.add_argument("--only", default="", help="comma list of groups: resize,se,skip,bn,loss,attn,dw,ln")
+    ap.add_argument("--only", default="", help="comma list of groups: resize,se,skip,pw,bn,loss,attn,dw,ln")
     a = ap.parse_args()
     groups = set(a.only.split(",")) if a.only else None
 
@@ -122,6 +122,20 @@ def _main():
                                                           a.reps), 8.0 * n * 3 * ho * wo)
         report("nearest_pyramid x0.5+x0.25 3x480x640", timeit(lambda: F.nearest_pyramid(img), a.reps),
                8.0 * n * 3 * (240 * 320 + 120 * 160))
+    # decoder pointwise 1x1 convs (E -> E/2, BN + ReLU on the operand load,
+    # the next BN's statistics from the epilogue), forward
+    for c, h, w in ((64, 120, 160), (32, 240, 320), (16, 480, 640)) if want("pw") else ():
+        co = c // 2
+        x = torch.rand(n, c, h, w, device=dev)
+        wt = torch.rand(co, c, device=dev) - 0.5
+        sc, sh = torch.rand(c, device=dev), torch.rand(c, device=dev) - 0.5
+        y = torch.empty(n, co, h, w, device=dev)
+        nb = _abi.query("mde_pointwise_stats_blocks", n, c, co, h, w)
+        st = torch.empty(co * nb * 4, device=dev)
+        report(f"pointwise fwd bnr+stats {c}->{co} {h}x{w}", timeit(lambda: _abi.call(
+            "mde_pointwise_fwd_stats", x.data_ptr(), sc.data_ptr(), sh.data_ptr(), wt.data_ptr(),
+            y.data_ptr(), st.data_ptr(), n, c, co, h, w, 0, _abi.stream_of(x)), a.reps),
+            4.0 * n * h * w * (c + co))
     # SE + cat and skip fusion at the three decoder resolutions
     for c, h, w, cout in ((64, 120, 160, 32), (32, 240, 320, 16), (16, 480, 640, 1)) \
             if (want("se") or want("skip")) else ():

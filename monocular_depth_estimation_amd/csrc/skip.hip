@@ -579,48 +579,17 @@ __global__ void __launch_bounds__(256)
     for (int i = 0; i < 4; ++i) run[ot][i] = {0.f, 0.f, 0.f, 0.f};
   bool first = true;  // wave-uniform: the wave's first tile sets the shifts
   const int tpi = (int)(hw / 64);
-  const int64_t tiles = n * tpi, tstep = (int64_t)gridDim.x * 4;
-  // PF (the narrow-input variants, whose operands are <= 32 registers): the
-  // next tile's operands are loaded before this tile's MFMAs and stores, so a
-  // wave keeps two tiles of loads in flight (the wide ones have no registers
-  // to spare: 64 input channels are 64 registers per tile)
-  constexpr bool PF = CI * (HAS_D ? 2 : 1) <= 32;
-  constexpr int NP = PF ? KC : 1;
-  float4 pr[NP], pd[HAS_D && PF ? KC : 1];
-  auto raw_loads = [&](int64_t t) {
-    const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
-    const T* rp = r + nidx * CI * hw + p0 + 4 * l16;
-#pragma unroll
-    for (int kk = 0; kk < NP; ++kk) pr[kk] = mde::ld4(rp + (int64_t)(4 * kk + q4) * hw);
-    if constexpr (HAS_D && PF) {
-      const T* dp = d + nidx * CI * hw + p0 + 4 * l16;
-#pragma unroll
-      for (int kk = 0; kk < KC; ++kk) pd[kk] = mde::ld4(dp + (int64_t)(4 * kk + q4) * hw);
-    }
-  };
-  if constexpr (PF)
-    if ((int64_t)blockIdx.x * 4 + w < tiles) raw_loads((int64_t)blockIdx.x * 4 + w);
-  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += tstep) {
+  const int64_t tiles = n * tpi;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < tiles; t += (int64_t)gridDim.x * 4) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
     const T* rp = r + nidx * CI * hw + p0 + 4 * l16;
     const T* dp = HAS_D ? d + nidx * CI * hw + p0 + 4 * l16 : nullptr;
     T* op = out + nidx * CO * hw + p0 + 4 * l16;
     float4 sb[KC];
-    float4 cr[NP], cd[HAS_D && PF ? KC : 1];
-    if constexpr (PF) {
-#pragma unroll
-      for (int kk = 0; kk < KC; ++kk) {
-        cr[kk] = pr[kk];
-        if constexpr (HAS_D) cd[kk] = pd[kk];
-      }
-      if (t + tstep < tiles) raw_loads(t + tstep);
-    }
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       const int64_t off = (int64_t)(4 * kk + q4) * hw;
-      float4 v;
-      if constexpr (PF) v = cr[kk];
-      else v = mde::ld4(rp + off);
+      float4 v = mde::ld4(rp + off);
       if (BNR) {  // BN + ReLU of r, then + d (HAS_D)
         v.x = fmaxf(v.x * fsc[kk] + fsh[kk], 0.f);
         v.y = fmaxf(v.y * fsc[kk] + fsh[kk], 0.f);
@@ -628,9 +597,7 @@ __global__ void __launch_bounds__(256)
         v.w = fmaxf(v.w * fsc[kk] + fsh[kk], 0.f);
       }
       if (HAS_D) {
-        float4 e;
-        if constexpr (PF) e = cd[kk];
-        else e = mde::ld4(dp + off);
+        const float4 e = mde::ld4(dp + off);
         v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
       }
       sb[kk] = v;

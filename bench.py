@@ -288,6 +288,12 @@ def main():
         per_launch = nbytes / launches
         # PMC HBM bytes of this registry name per step (all its launches), per launch
         per_step = pmc.get(name, {}).get("bytes_per_step")
+        if per_step is None:  # one kernel behind several ids ("a+b"): split by algorithmic bytes
+            for key, val in pmc.items():
+                parts = key.split("+")
+                if len(parts) > 1 and name in parts and isinstance(val, dict):
+                    alg = sum(kernels[p][2] for p in parts if p in kernels)
+                    per_step = val.get("bytes_per_step", 0) * nbytes / alg if alg else None
         traffic = per_step / (launches / timing_steps) if per_step else None
         common = {"kernel": name, "traffic": traffic,
                   "traffic_ratio": round(traffic / per_launch, 3) if traffic else None,

@@ -68,8 +68,10 @@ NAMES = [
     (r"c3s2_dgrad_kernel", "conv3x3s2_dgrad"),
     (r"c3s1_kernel<false", "conv3x3w_fwd"),
     (r"c3s1_kernel<true", "conv3x3w_dgrad"),
-    (r"wino_f23_kernel", "wino_fwd"),  # forward and data gradient: one kernel
-    (r"wino_weight_kernel", "wino_weight"),
+    # forward and data gradient run the same kernel: one combined key, which
+    # bench.py apportions by the two ids' algorithmic bytes (same ratio)
+    (r"wino_f23_kernel", "wino_fwd+wino_dgrad"),
+    (r"wino_weight2?_kernel", "wino_weight"),
     (r"bn_fwd_chan_kernel", "bn_fwd_apply_small"),
     (r"bn_bwd_chan_kernel", "bn_bwd_apply_small"),
     (r"dloss_(fwd_stream|masked|map|final)_kernel", "depth_loss_fwd"),

@@ -546,10 +546,26 @@ __global__ void __launch_bounds__(256)
                          T* __restrict__ out, int64_t n, int64_t hw,
                          const float* __restrict__ isc = nullptr,
                          const float* __restrict__ ish = nullptr,
-                         float* __restrict__ stats = nullptr) {
+                         float* __restrict__ stats = nullptr, int out_cs = CO) {
+  // out_cs: output channels per image (> CO when one launch writes a channel
+  // slice of a wider output: the 64 -> 64 pointwise as two 64 -> 32 halves)
   constexpr int OT = (CO + 15) / 16, KC = CI / 4;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
+  // Registers (the 64-input-channel variants ran at one wave per SIMD): the
+  // BN scale / shift are read from LDS per use (an opaque index keeps the
+  // compiler from hoisting them back into 2 KC registers), the bias exists
+  // only with HAS_D (the skip fusion; the pointwise convs have none), and the
+  // statistics keep (shift, s1, s2) per channel with one wave-uniform count.
+  constexpr bool HB = HAS_D;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+  __shared__ float s_bn[BNR ? 2 : 1][BNR ? CI : 1];
+  if constexpr (BNR) {
+    if (threadIdx.x < CI) {
+      s_bn[0][threadIdx.x] = isc[threadIdx.x];
+      s_bn[1][threadIdx.x] = ish[threadIdx.x];
+    }
+    __syncthreads();
+  }
   float wa[OT][KC];  // W[o = 16ot + l16][c = 4kk + q4] (0 for o >= CO)
 #pragma unroll
   for (int ot = 0; ot < OT; ++ot)
@@ -558,25 +574,22 @@ __global__ void __launch_bounds__(256)
       const int o = 16 * ot + l16;
       wa[ot][kk] = o < CO ? wt[o * CI + 4 * kk + q4] : 0.f;
     }
-  float bo[OT][4];
+  float bo[HB ? OT : 1][4];
 #pragma unroll
-  for (int ot = 0; ot < OT; ++ot)
+  for (int ot = 0; ot < (HB ? OT : 1); ++ot)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int o = 16 * ot + 4 * q4 + i;
-      bo[ot][i] = (b && o < CO) ? b[o] : 0.f;
+      bo[ot][i] = (HB && b && o < CO) ? b[o] : 0.f;
     }
-  float fsc[KC], fsh[KC];  // BNR: channel c = 4 kk + q4
-#pragma unroll
-  for (int kk = 0; kk < KC; ++kk) {
-    fsc[kk] = BNR ? isc[4 * kk + q4] : 1.f;
-    fsh[kk] = BNR ? ish[4 * kk + q4] : 0.f;
-  }
-  mde::Sh run[STATS ? OT : 1][4];  // channel 16 ot + 4 q4 + i, this lane's pixels
+  // channel 16 ot + 4 q4 + i, this lane's pixels: shift, sum d, sum d^2 (every
+  // pixel of a tile is valid: hw % 64 == 0, so the count is 4 per tile)
+  float rref[STATS ? OT : 1][4], rs1[STATS ? OT : 1][4], rs2[STATS ? OT : 1][4];
 #pragma unroll
   for (int ot = 0; ot < (STATS ? OT : 1); ++ot)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) run[ot][i] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i) rref[ot][i] = rs1[ot][i] = rs2[ot][i] = 0.f;
+  int ntile = 0;
   bool first = true;  // wave-uniform: the wave's first tile sets the shifts
   const int tpi = (int)(hw / 64);
   const int64_t tiles = n * tpi;
@@ -584,17 +597,20 @@ __global__ void __launch_bounds__(256)
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
     const T* rp = r + nidx * CI * hw + p0 + 4 * l16;
     const T* dp = HAS_D ? d + nidx * CI * hw + p0 + 4 * l16 : nullptr;
-    T* op = out + nidx * CO * hw + p0 + 4 * l16;
+    T* op = out + nidx * out_cs * hw + p0 + 4 * l16;
     float4 sb[KC];
+    int zo = 0;  // opaque 0: the LDS reads below stay in the loop
+    asm volatile("" : "+v"(zo));
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       const int64_t off = (int64_t)(4 * kk + q4) * hw;
       float4 v = mde::ld4(rp + off);
-      if (BNR) {  // BN + ReLU of r, then + d (HAS_D)
-        v.x = fmaxf(v.x * fsc[kk] + fsh[kk], 0.f);
-        v.y = fmaxf(v.y * fsc[kk] + fsh[kk], 0.f);
-        v.z = fmaxf(v.z * fsc[kk] + fsh[kk], 0.f);
-        v.w = fmaxf(v.w * fsc[kk] + fsh[kk], 0.f);
+      if constexpr (BNR) {  // BN + ReLU of r, then + d (HAS_D)
+        const float fsc = s_bn[0][4 * kk + q4 + zo], fsh = s_bn[1][4 * kk + q4 + zo];
+        v.x = fmaxf(v.x * fsc + fsh, 0.f);
+        v.y = fmaxf(v.y * fsc + fsh, 0.f);
+        v.z = fmaxf(v.z * fsc + fsh, 0.f);
+        v.w = fmaxf(v.w * fsc + fsh, 0.f);
       }
       if (HAS_D) {
         const float4 e = mde::ld4(dp + off);
@@ -606,7 +622,8 @@ __global__ void __launch_bounds__(256)
     for (int ot = 0; ot < OT; ++ot) {
       f4 acc[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[j] = f4{bo[ot][0], bo[ot][1], bo[ot][2], bo[ot][3]};
+      for (int j = 0; j < 4; ++j)
+        acc[j] = HB ? f4{bo[ot][0], bo[ot][1], bo[ot][2], bo[ot][3]} : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < KC; ++kk) {
         acc[0] = mfma4(wa[ot][kk], sb[kk].x, acc[0]);
@@ -627,13 +644,18 @@ __global__ void __launch_bounds__(256)
             vs[j] = sizeof(T) == 2 ? mde::bf2f(mde::f2bf(acc[j][i])) : acc[j][i];
           // one shift per channel and wave: lane l16 = 0's first value, so the
           // 16 lanes of a group sum their (n, s1, s2) plainly at the end
-          if (first) run[ot][i].ref = __shfl(vs[0], lane & 48, 64);
+          if (first) rref[ot][i] = __shfl(vs[0], lane & 48, 64);
 #pragma unroll
-          for (int j = 0; j < 4; ++j) mde::sh_add(run[ot][i], vs[j], true);
+          for (int j = 0; j < 4; ++j) {
+            const float dv = vs[j] - rref[ot][i];
+            rs1[ot][i] += dv;
+            rs2[ot][i] = fmaf(dv, dv, rs2[ot][i]);
+          }
         }
       }
     }
     first = false;
+    ++ntile;
   }
   if constexpr (STATS) {
     // the 16 lanes of a lane group share the channels' shifts: plain-sum
@@ -644,7 +666,7 @@ __global__ void __launch_bounds__(256)
     for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        mde::Sh a = run[ot][i];
+        mde::Sh a{rref[ot][i], 4.f * ntile, rs1[ot][i], rs2[ot][i]};
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
         const int c = 16 * ot + 4 * q4 + i;
@@ -1022,6 +1044,17 @@ static int pointwise_fwd(const void* x, const float* in_scale, const float* in_s
   const dim3 grid((unsigned)pw_fwd_blocks(n, hw, stats != nullptr));
   const T* xi = (const T*)x;
   T* yo = (T*)y;
+  // 64 -> 64 with the BN operand and the statistics epilogue: two 64 -> 32
+  // halves (one launch holding all 64 outputs needs > 256 registers: one wave
+  // per SIMD); each half re-reads the input, from L2 mostly
+  if (cin == 64 && cout == 64 && in_scale && stats) {
+    for (int half = 0; half < 2; ++half)
+      MDE_LAUNCH(mde::K_PW_FWD, bytes / 2, s, (skip_fwd_mfma_kernel<64, 32, false, true, true, T>),
+                 grid, dim3(256), 0, xi, nullptr, wt + half * 32 * 64, nullptr,
+                 yo + half * 32 * hw, n, hw, in_scale, in_shift,
+                 stats + (int64_t)half * 32 * grid.x * 4, 64);
+    return MDE_OK;
+  }
 #define MDE_PW_FWD(A, B)                                                                     \
   if (cin == A && cout == B) {                                                               \
     if (in_scale && stats) {                                                                 \

@@ -129,7 +129,8 @@ def test_ptmodel_bf16_vs_float64_oracle():
     _compare(lambda: fill_(om.PTModel()), ours, lambda: fill_(om.PTModel()), x, d, "PTModel bf16")
 
 
-@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 4, 96, 128), (32, 16, 2, 60, 80), (64, 32, 2, 30, 64)])
+@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 4, 96, 128), (32, 16, 2, 60, 80), (64, 32, 2, 30, 64),
+                                            (64, 64, 2, 30, 64)])
 def test_bnrelu_pointwise_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
     """The fused BN-ReLU-1x1 pair on bf16 activations (autocast) == the fp32
     kernels on the same values: the kernels convert on load and round on

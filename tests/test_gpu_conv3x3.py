@@ -308,7 +308,9 @@ def test_bn_statistics_from_conv_epilogue(cin, cout, n, h, w, off):
     assert rel_err(bn.running_var, bn2.running_var) <= 2e-5
 
 
-@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 4, 96, 128), (64, 32, 2, 60, 80), (32, 16, 3, 8, 64)])
+# (64, 64): two 64 -> 32 launches writing channel halves + their statistics rows
+@pytest.mark.parametrize("cin,cout,n,h,w", [(16, 8, 4, 96, 128), (64, 32, 2, 60, 80), (32, 16, 3, 8, 64),
+                                            (64, 64, 2, 60, 80)])
 def test_bn_statistics_from_pointwise_epilogue(cin, cout, n, h, w):
     """The BN-ReLU-fed 1x1 conv's forward epilogue statistics for the next
     BatchNorm == that BatchNorm's own statistics pass."""

@@ -124,8 +124,8 @@ def _main():
                8.0 * n * 3 * (240 * 320 + 120 * 160))
     # decoder pointwise 1x1 convs (E -> E/2, BN + ReLU on the operand load,
     # the next BN's statistics from the epilogue), forward
-    for c, h, w in ((64, 120, 160), (32, 240, 320), (16, 480, 640)) if want("pw") else ():
-        co = c // 2
+    for c, co, h, w in ((64, 64, 120, 160), (64, 32, 120, 160), (32, 16, 240, 320), (16, 8, 480, 640)) \
+            if want("pw") else ():
         x = torch.rand(n, c, h, w, device=dev)
         wt = torch.rand(co, c, device=dev) - 0.5
         sc, sh = torch.rand(c, device=dev), torch.rand(c, device=dev) - 0.5

@@ -493,6 +493,19 @@ __device__ BwdCh bwd_channel(const BwdArgs& P, int64_t ch, double sdy,
   return r;
 }
 
+// Streaming loads / stores marked nontemporal (read once here; the outputs
+// are far larger than L2 and are re-read by a later kernel from HBM anyway).
+using nt4 = __attribute__((ext_vector_type(4))) float;
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+  const nt4 v = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 ld4_nt(const mde::bf16* p) { return ld4(p); }
+__device__ __forceinline__ void st4_nt(float* p, float4 v) {
+  __builtin_nontemporal_store(nt4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt4*>(p));
+}
+__device__ __forceinline__ void st4_nt(mde::bf16* p, float4 v) { st4(p, v); }
+
 template <typename T>
 __global__ void __launch_bounds__(256)
     bn_bwd_apply_plane_kernel(const T* __restrict__ gy, const T* __restrict__ x,
@@ -518,9 +531,9 @@ __global__ void __launch_bounds__(256)
   for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
     const int64_t ic = i < hw4 ? i : hw4 - 1;
-    g4[k] = ld4(gp + 4 * ic);
-    v4[k] = ld4(xp + 4 * ic);
-    q4[k] = rp ? ld4(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
+    g4[k] = ld4_nt(gp + 4 * ic);
+    v4[k] = ld4_nt(xp + 4 * ic);
+    q4[k] = rp ? ld4_nt(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (threadIdx.x < 64) {
     double a, b;
@@ -541,9 +554,9 @@ __global__ void __launch_bounds__(256)
                                    dy_eff(g.y, v.y, q.y, sc, sh, act),
                                    dy_eff(g.z, v.z, q.z, sc, sh, act),
                                    dy_eff(g.w, v.w, q.w, sc, sh, act));
-      st4(op + 4 * i, make_float4(A * e.x + B * v.x + D, A * e.y + B * v.y + D,
-                                  A * e.z + B * v.z + D, A * e.w + B * v.w + D));
-      if (orp) st4(orp + 4 * i, e);
+      st4_nt(op + 4 * i, make_float4(A * e.x + B * v.x + D, A * e.y + B * v.y + D,
+                                     A * e.z + B * v.z + D, A * e.w + B * v.w + D));
+      if (orp) st4_nt(orp + 4 * i, e);
     }
   }
 }

@@ -185,6 +185,9 @@ struct PlaneCursor {
   }
 };
 
+using mde::ld4_nt;
+using mde::st4_nt;
+
 constexpr int kRedDepth = 4;  // independent float4 loads per thread per trip
 
 // part[(c * slices + s) * 2 + {0,1}] = sum(x - ref), sum((x - ref)^2)
@@ -216,7 +219,7 @@ __global__ void __launch_bounds__(256)
         float4 v[kRedDepth];
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) {
-          v[k] = ld4(xc + cur.off);
+          v[k] = ld4_nt(xc + cur.off);
           cur.advance(kStep, hw, chw);
         }
 #pragma unroll
@@ -279,8 +282,8 @@ __global__ void __launch_bounds__(256)
   for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
     const int64_t ic = i < hw4 ? i : hw4 - 1;
-    x4[k] = ld4(xp + 4 * ic);
-    q4[k] = rp ? ld4(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
+    x4[k] = ld4_nt(xp + 4 * ic);
+    q4[k] = rp ? ld4_nt(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (threadIdx.x < 64) {
     double s1 = 0.0, s2 = 0.0;
@@ -297,7 +300,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
-    if (i < hw4) st4(yp + 4 * i, fwd4(x4[k], q4[k], rp != nullptr, sc, sh, act));
+    if (i < hw4) st4_nt(yp + 4 * i, fwd4(x4[k], q4[k], rp != nullptr, sc, sh, act));
   }
 }
 
@@ -415,9 +418,9 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) {
           const int64_t off = base + cur.off;
-          g[k] = ld4(gy + off);
-          v[k] = ld4(x + off);
-          q[k] = r ? ld4(r + off) : z4;
+          g[k] = ld4_nt(gy + off);
+          v[k] = ld4_nt(x + off);
+          q[k] = r ? ld4_nt(r + off) : z4;
           cur.advance(kStep, hw, chw);
         }
 #pragma unroll
@@ -492,19 +495,6 @@ __device__ BwdCh bwd_channel(const BwdArgs& P, int64_t ch, double sdy,
   r.D = (float)D;
   return r;
 }
-
-// Streaming loads / stores marked nontemporal (read once here; the outputs
-// are far larger than L2 and are re-read by a later kernel from HBM anyway).
-using nt4 = __attribute__((ext_vector_type(4))) float;
-__device__ __forceinline__ float4 ld4_nt(const float* p) {
-  const nt4 v = __builtin_nontemporal_load(reinterpret_cast<const nt4*>(p));
-  return make_float4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ float4 ld4_nt(const mde::bf16* p) { return ld4(p); }
-__device__ __forceinline__ void st4_nt(float* p, float4 v) {
-  __builtin_nontemporal_store(nt4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt4*>(p));
-}
-__device__ __forceinline__ void st4_nt(mde::bf16* p, float4 v) { st4(p, v); }
 
 template <typename T>
 __global__ void __launch_bounds__(256)

@@ -178,6 +178,29 @@ __device__ __forceinline__ void st4(bf16* p, float4 v) {
   *reinterpret_cast<uint2*>(p) = u;
 }
 
+// Nontemporal variants for streaming kernels (every tensor far larger than
+// L2, read or written once per kernel: the BN passes measured +10 %,
+// profiles/r04_bn_nt_ab.txt).
+using nt4f = float __attribute__((ext_vector_type(4)));
+using nt2u = uint32_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float4 ld4_nt(const float* p) {
+  const nt4f v = __builtin_nontemporal_load(reinterpret_cast<const nt4f*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ float4 ld4_nt(const bf16* p) {
+  const nt2u u = __builtin_nontemporal_load(reinterpret_cast<const nt2u*>(p));
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+__device__ __forceinline__ void st4_nt(float* p, float4 v) {
+  __builtin_nontemporal_store(nt4f{v.x, v.y, v.z, v.w}, reinterpret_cast<nt4f*>(p));
+}
+__device__ __forceinline__ void st4_nt(bf16* p, float4 v) {
+  const nt2u u{(uint32_t)f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+               (uint32_t)f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16)};
+  __builtin_nontemporal_store(u, reinterpret_cast<nt2u*>(p));
+}
+
 // Per-channel BatchNorm statistics emitted by a producing conv's epilogue
 // (one (shift, count, s1, s2) per channel and block; mde_batchnorm_*_stats
 // finalises them).  Running shifted sums of one channel's values: the shift

@@ -412,8 +412,8 @@ __global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)  // 64 x 64: W^T
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          mde::st4(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16,
-                   make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
+          mde::st4_nt(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16,
+                      make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
         if constexpr (BNS) {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
@@ -604,7 +604,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int kk = 0; kk < KC; ++kk) {
       const int64_t off = (int64_t)(4 * kk + q4) * hw;
-      float4 v = mde::ld4(rp + off);
+      float4 v = mde::ld4_nt(rp + off);  // streamed: read once (nontemporal)
       if constexpr (BNR) {  // BN + ReLU of r, then + d (HAS_D)
         const float fsc = s_bn[0][4 * kk + q4 + zo], fsh = s_bn[1][4 * kk + q4 + zo];
         v.x = fmaxf(v.x * fsc + fsh, 0.f);
@@ -613,7 +613,7 @@ __global__ void __launch_bounds__(256)
         v.w = fmaxf(v.w * fsc + fsh, 0.f);
       }
       if (HAS_D) {
-        const float4 e = mde::ld4(dp + off);
+        const float4 e = mde::ld4_nt(dp + off);
         v.x += e.x; v.y += e.y; v.z += e.z; v.w += e.w;
       }
       sb[kk] = v;
@@ -635,7 +635,7 @@ __global__ void __launch_bounds__(256)
       for (int i = 0; i < 4; ++i) {
         const int o = 16 * ot + 4 * q4 + i;
         if (o < CO)
-          mde::st4(op + (int64_t)o * hw, make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
+          mde::st4_nt(op + (int64_t)o * hw, make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
         if constexpr (STATS) {
           // statistics of the values as stored (bf16-rounded under autocast)
           float vs[4];

@@ -185,6 +185,10 @@ struct PlaneCursor {
   }
 };
 
+// Nontemporal loads / stores only in the backward apply (the last reader of
+// gy and x): the same hint on the statistics, forward apply and backward
+// reduce measured slower (the apply re-reads what the reduce just streamed),
+// profiles/r04_nt_ab.txt.
 using mde::ld4_nt;
 using mde::st4_nt;
 
@@ -219,7 +223,7 @@ __global__ void __launch_bounds__(256)
         float4 v[kRedDepth];
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) {
-          v[k] = ld4_nt(xc + cur.off);
+          v[k] = ld4(xc + cur.off);
           cur.advance(kStep, hw, chw);
         }
 #pragma unroll
@@ -282,8 +286,8 @@ __global__ void __launch_bounds__(256)
   for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
     const int64_t ic = i < hw4 ? i : hw4 - 1;
-    x4[k] = ld4_nt(xp + 4 * ic);
-    q4[k] = rp ? ld4_nt(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
+    x4[k] = ld4(xp + 4 * ic);
+    q4[k] = rp ? ld4(rp + 4 * ic) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   if (threadIdx.x < 64) {
     double s1 = 0.0, s2 = 0.0;
@@ -300,7 +304,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int k = 0; k < KK; ++k) {
     const int64_t i = b0 + k * 256 + threadIdx.x;
-    if (i < hw4) st4_nt(yp + 4 * i, fwd4(x4[k], q4[k], rp != nullptr, sc, sh, act));
+    if (i < hw4) st4(yp + 4 * i, fwd4(x4[k], q4[k], rp != nullptr, sc, sh, act));
   }
 }
 
@@ -418,9 +422,9 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int k = 0; k < kRedDepth; ++k) {
           const int64_t off = base + cur.off;
-          g[k] = ld4_nt(gy + off);
-          v[k] = ld4_nt(x + off);
-          q[k] = r ? ld4_nt(r + off) : z4;
+          g[k] = ld4(gy + off);
+          v[k] = ld4(x + off);
+          q[k] = r ? ld4(r + off) : z4;
           cur.advance(kStep, hw, chw);
         }
 #pragma unroll

@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 call AJ: final refresh at HEAD -- full GPU suite, the cfg2 / cfg3 /
+# Round-4 call AJ / AN: final refresh at HEAD -- full GPU suite, the cfg2 / cfg3 /
 # cfg4 bench lines (with the CPU baseline), a cfg2 kernel trace, and the PMC
 # traffic passes of all three workloads.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=gpurun_out/r04aj
+OUT=gpurun_out/r04an
 mkdir -p $OUT
 export TMPDIR=/tmp MASTER_ADDR=127.0.0.1
 AMD_LOG_LEVEL=1 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -q -rfE -p no:cacheprovider --timeout 300 \

@@ -4,6 +4,13 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
+`python bench.py --gpus N` (N > 1) outside a torchrun job launches the N
+ranks itself: the parent starts `torch.distributed.run` as a child process
+before anything touches the GPU and exits with its code; rank 0's JSON line
+is the child's stdout.  `--device cpu` (gloo) runs the same launcher and
+data-parallel plumbing on a small plain-torch stand-in net on the CPU: a
+launcher smoke test, not a measurement.
+
 One step = the src/train.py step (train.py:86-114) on one synthetic batch
 already resident in HBM: GuideDepth forward (BN in train mode), DepthNorm +
 1.0*SSIM + 0.1*L1 (one fused HIP pass), backward, DDP all-reduce over RCCL
@@ -53,6 +60,11 @@ AMP_DTYPE = ("bf16 autocast: 16->16 / 32->32 3x3 convs on the HIP bf16 MFMA kern
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--device", choices=("cuda", "cpu"), default="cuda",
+                   help="cpu: launcher / data-parallel smoke over gloo on a plain-torch stand-in "
+                        "net (no HIP; not a measurement)")
+    p.add_argument("--backend", choices=("nccl", "gloo"), default=None,
+                   help="process-group backend (default: nccl = RCCL on cuda, gloo on cpu)")
     p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--workload", choices=("guidedepth", "newcrf", "sam"), default="guidedepth",
@@ -175,12 +187,134 @@ def cpu_baseline(args):
     return out
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` (N > 1) outside a torchrun job: run this script under
+    torch.distributed.run as a CHILD process, one rank per GPU, and return
+    its exit code.  The parent makes no HIP call before or after (the ranks
+    own the devices; a process that initialised the GPU must not exec), and
+    rank 0's JSON line reaches stdout through the child."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+    env.setdefault("OMP_NUM_THREADS", "1" if args.device == "cpu" else env.get("OMP_NUM_THREADS", "8"))
+    print(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
+class _StandInNet(torch.nn.Module):
+    """`--device cpu` only: a small plain-torch conv net standing in for the
+    HIP model, so the launcher and the data-parallel exchange (GradBuckets
+    over gloo) can run without a GPU.  Not a workload of the metric."""
+
+    def __init__(self):
+        super().__init__()
+        nn = torch.nn
+        self.body = nn.Sequential(nn.Conv2d(3, 16, 3, 2, 1), nn.BatchNorm2d(16), nn.ReLU(),
+                                  nn.Conv2d(16, 16, 3, 1, 1), nn.BatchNorm2d(16), nn.ReLU(),
+                                  nn.Conv2d(16, 1, 1))
+
+    def forward(self, x):
+        return torch.nn.functional.interpolate(self.body(x), scale_factor=2, mode="bilinear")
+
+
+def params_fingerprint(params) -> torch.Tensor:
+    """float64 sum of every parameter's float64 sum: equal bitwise across ranks
+    iff (for all practical purposes) the replicas hold the same weights."""
+    return torch.stack([p.detach().double().sum() for p in params]).sum().reshape(1)
+
+
+def params_in_sync(params, world) -> bool | None:
+    if world.size == 1:
+        return None
+    fp = params_fingerprint(params)
+    every = [torch.empty_like(fp) for _ in range(world.size)]
+    dist.all_gather(every, fp)
+    return all(bool((e == every[0]).all()) for e in every)
+
+
+def cpu_smoke(args, world):
+    """The launcher / data-parallel plumbing on the CPU over gloo (see
+    _StandInNet): rank 0's weights broadcast, per-rank shards, the bucketed
+    gradient exchange, Adam; rank 0 prints one JSON line with n_gpus from the
+    process group and whether every rank ends with the same parameters."""
+    from monocular_depth_estimation_amd.train import GradBuckets, Trainer, synthetic_batch
+    torch.manual_seed(world.rank)  # different init per rank: the broadcast must fix it
+    model = _StandInNet().train()
+    params = list(model.parameters())
+    if world.size > 1:
+        for p in params:
+            dist.broadcast(p.data, 0)
+    buckets = GradBuckets(params, world, 4 << 10) if world.size > 1 else None
+    opt = torch.optim.Adam(params, 1e-3)
+    trainer = Trainer(model, opt, lambda pred, d: torch.nn.functional.l1_loss(pred, d / 10.0),
+                      world, eval_quirk=False, buckets=buckets)
+    trainer.begin_epoch()
+    batches = [synthetic_batch(args.bs, args.height, args.width, world.rank, s, "cpu")
+               for s in range(2)]
+    for i in range(args.warmup):
+        trainer.step(*batches[i % 2])
+    if world.size > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        trainer.step(*batches[i % 2])
+    if world.size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world.size > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t)
+    in_sync = params_in_sync(params, world)
+    if world.is_main:
+        out = {"metric": "launcher smoke (CPU, gloo): training images/sec of a stand-in net",
+               "value": round(world.size * args.bs * args.steps / elapsed, 2), "unit": "images/s",
+               "n_gpus": world.size, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed * 1e3 / max(args.steps, 1), 2),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+               "data": "synthetic; --device cpu launcher smoke on a plain-torch stand-in net, "
+                       "NOT a measurement of the metric",
+               "config": {"workload": "stand-in net (bench._StandInNet), CPU",
+                          "global_batch": world.size * args.bs, "per_gpu_batch": args.bs,
+                          "resolution": f"{args.width}x{args.height}",
+                          "parallelism": f"dp{world.size}"},
+               "dp_exchange": (f"{len(buckets)} gradient buckets, gloo all_reduce (1/N + SUM) "
+                               "from post-accumulate hooks" if buckets is not None else None),
+               "params_in_sync": in_sync,
+               "params_fingerprint": float(params_fingerprint(params)),
+               "loss_last": round(float(trainer.last_loss), 6)}
+        print(json.dumps(out), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))  # before any GPU call: the ranks own the devices
+    from monocular_depth_estimation_amd.train import init_world
+    backend = args.backend or ("gloo" if args.device == "cpu" else None)
+    world = init_world(backend=backend, use_gpu=args.device == "cuda")
+    if world.size != args.gpus and world.is_main:
+        print(f"[bench] warning: --gpus {args.gpus} but the job has {world.size} ranks; "
+              f"n_gpus reports the process group's size", file=sys.stderr, flush=True)
+    if args.device == "cpu":
+        return cpu_smoke(args, world)
+    if world.device.type != "cuda":
+        raise RuntimeError("bench.py measures on a ROCm GPU (no GPU visible); "
+                           "--device cpu runs the CPU launcher smoke instead")
     from monocular_depth_estimation_amd import _abi
-    from monocular_depth_estimation_amd.train import (Trainer, init_world, make_adam, synthetic_batch,
-                                                      wrap_ddp)
-    world = init_world()
+    from monocular_depth_estimation_amd.train import Trainer, make_adam, synthetic_batch, wrap_ddp
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
     from monocular_depth_estimation_amd import GuideDepth
     from monocular_depth_estimation_amd.loss import SSIML1
@@ -260,15 +394,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t)
     loss = float(trainer.last_loss)
+    backend = dist.get_backend() if dist.is_initialized() else None
     if world.size == 1:
         dp_exchange = None
     elif not use_graph:
-        dp_exchange = "DDP buckets (eager, overlapped with backward)"
+        dp_exchange = f"DDP buckets over {backend} (eager, overlapped with backward)"
     elif trainer.buckets is not None:
-        dp_exchange = (f"{len(trainer.buckets)} gradient buckets, all_reduce(AVG) captured into the "
-                       "step graph, overlapped with backward")
+        dp_exchange = (f"{len(trainer.buckets)} gradient buckets, all_reduce(AVG) over {backend} "
+                       "captured into the step graph, overlapped with backward (a captured "
+                       "multi-rank RCCL collective has not run on hardware in this repo's "
+                       "testing: the pool gives one GPU per call; MDE_DP_OVERLAP=0 = flat)")
     else:
-        dp_exchange = "flat: one eager all_reduce between the two step graphs"
+        dp_exchange = (f"flat: one eager all_reduce over {backend} between the two step graphs")
+    in_sync = params_in_sync(trainer.params if use_graph else list(model.parameters()), world)
     if use_graph:
         trainer.close()  # free the graphs (captured RCCL nodes) before the group goes
     if not world.is_main:
@@ -365,6 +503,7 @@ def main():
         "execution": ("hipGraph replay of the whole step (GraphTrainer)" if use_graph
                       else "eager (Trainer + DDP)"),
         "dp_exchange": dp_exchange,
+        "params_in_sync": in_sync,
         "roofline": roofline,
         "roofline_leaders": leaders,
         "path_roofline": path_roofline,

@@ -283,9 +283,13 @@ class GraphTrainer:
     (and any gloo group, whose collectives cannot be captured) selects the
     flat scheme instead: graph A (forward, backward, the gradients packed
     into one buffer and scaled by 1/N) -> one eager all_reduce(SUM) outside
-    the graph -> graph B (unpack, Adam).  The BN running statistics (one
-    flat buffer) are broadcast from rank 0 before each forward, as DDP's
-    broadcast_buffers does.  Inputs are copied into static device buffers.
+    the graph -> graph B (unpack, Adam).  The BN running statistics live in
+    one flat buffer, broadcast from rank 0 at start and by sync_buffers()
+    (close() runs it) -- not every step: a train-mode forward never reads
+    them, and rank 0's, the ones a checkpoint saves, come out bitwise the
+    same as under DDP's per-forward broadcast_buffers (rank 0 receives its
+    own), so no collective other than the gradient exchange is on the step's
+    critical path.  Inputs are copied into static device buffers.
     CUDA only; BN stays in train mode (the eval-mode quirk changes the graph,
     use Trainer for that).  close() frees the captured graphs; it must run
     before dist.destroy_process_group() (a graph holding captured RCCL
@@ -388,8 +392,10 @@ class GraphTrainer:
             torch._foreach_copy_(grads, [f.view_as(g) for f, g in zip(flat, grads)])
         self.optimizer.step()
 
-    def _sync_buffers(self):
-        if self.world.size > 1:
+    def sync_buffers(self):
+        """Rank 0's BN running statistics to every rank (DDP's broadcast_buffers,
+        on demand: before evaluating or checkpointing on a rank other than 0)."""
+        if self.world.size > 1 and self.flat_bn is not None and dist.is_initialized():
             dist.broadcast(self.flat_bn, 0)
 
     def _allreduce(self):
@@ -419,7 +425,6 @@ class GraphTrainer:
         self.static_image.copy_(image)
         self.static_depth.copy_(depth)
         self.calls += 1
-        self._sync_buffers()
         if self.calls <= self.eager_steps:
             cur = torch.cuda.current_stream()
             self.eager_stream.wait_stream(cur)
@@ -446,7 +451,6 @@ class GraphTrainer:
         before capture or for measurement: it re-allocates the gradients."""
         self.static_image.copy_(image)
         self.static_depth.copy_(depth)
-        self._sync_buffers()
         loss = self._eager()
         self.last_loss = loss
         return loss
@@ -489,6 +493,8 @@ class GraphTrainer:
         under a live graph aborts the process on this stack."""
         if self.graphs is None:
             return
+        torch.cuda.synchronize()
+        self.sync_buffers()
         torch.cuda.synchronize()
         for g in self.graphs:
             if g is not None:

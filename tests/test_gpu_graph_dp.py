@@ -14,8 +14,8 @@ rank-0 weights through torch.autograd.grad (no hooks, no exchange); (2) the
 parameters are bitwise identical on both ranks after 5 steps although each
 rank initialised differently (rank 0's weights are broadcast, gradients
 averaged); (3) each rank's loss is its own shard's loss (the losses differ).
-BN running statistics are rank-local between steps, as under DDP
-(broadcast from rank 0 before every forward), so they are not compared.
+BN running statistics are rank-local between steps (GraphTrainer does not
+broadcast them every step) and rank 0's reach every rank on sync_buffers().
 """
 import os
 import socket
@@ -75,8 +75,16 @@ def _worker(rank, world, port, out_dir, mode):
         scale = max(float(m.abs().max()), 1e-6 * gmax)  # BN-fed conv biases: true grad 0
         worst = max(worst, float((g - m).abs().max()) / scale)
     state = {k: v.detach().cpu() for k, v in model.named_parameters()}
-    torch.save({"losses": losses, "state": state, "worst": worst,
-                "first": [g.cpu() for g in first]}, os.path.join(out_dir, f"rank{rank}.pt"))
+    # BN running statistics: rank-local during training (no per-step
+    # broadcast), rank 0's to every rank on sync_buffers()
+    bn_local = tr.flat_bn.detach().cpu().clone()
+    tr.sync_buffers()
+    torch.cuda.synchronize()
+    bn_synced = tr.flat_bn.detach().cpu().clone()
+    tr.close()
+    torch.save({"losses": losses, "state": state, "worst": worst, "bn_local": bn_local,
+                "bn_synced": bn_synced, "first": [g.cpu() for g in first]},
+               os.path.join(out_dir, f"rank{rank}.pt"))
     torch.distributed.destroy_process_group()
 
 
@@ -94,3 +102,6 @@ def test_graph_trainer_two_ranks(mode):
     for k, v in r0["state"].items():
         assert torch.equal(v, r1["state"][k]), k
     assert r0["losses"] != r1["losses"]
+    assert torch.equal(r0["bn_local"], r0["bn_synced"])  # rank 0 keeps its own statistics
+    assert not torch.equal(r0["bn_local"], r1["bn_local"])  # per-shard batch statistics
+    assert torch.equal(r1["bn_synced"], r0["bn_local"])  # rank 0's, on every rank

@@ -700,6 +700,46 @@ int mde_graph_dot(void* graph, const char* path);
 int mde_graph_replace_memsets(void* graph, int64_t* replaced);
 
 /* ---------------------------------------------------------------------------
+ * bf16 convolutions, NCHW, any cin / cout multiple of 32, 3x3 (padding 1) or
+ * 1x1 (padding 0), stride 1 or 2, input width even (v_mfma_f32_32x32x16_bf16,
+ * fp32 accumulation): DDRNet-23-slim's BasicBlock / Bottleneck / stem / down /
+ * compression / DAPPM convolutions (src/GuideDepth/model/DDRNet_23_slim.py:
+ * 41-113, 121-171, 230-263) under bf16 autocast -- the `F.conv2d` /
+ * `conv.weight.grad` of each, with autocast's semantics: bf16 x / y / gy / gx,
+ * the fp32 weight rounded to bf16 (RNE), fp32 weight gradient.
+ * x [n,cin,h,w]; y [n,cout,ho,wo], ho = (h + 2p - k) / s + 1.
+ * mde_convbf_supported(cin, cout, h, w, ks, stride, pass): pass 0 forward, 1
+ * data gradient, 2 weight gradient (shape and LDS-capacity rules).
+ * mde_convbf_pack: the filter of one pass as packed bf16 [cin/32][ks*ks][cout]
+ * [32] (transpose = 0, the forward) or of the data gradient (transpose = 1:
+ * channels swapped, taps flipped), mde_convbf_pack_elems elements.
+ * mde_convbf_fwd: y from x and the forward pack; stats (nullable) receives the
+ * following BatchNorm's per-block shifted sums [cout][blocks][4] (blocks =
+ * mde_convbf_stats_blocks).  mde_convbf_bwd_data: gx [n,cin,h,w] from gy and
+ * the transposed pack (stride 2: gy zero-inserted, stride-1 convolution),
+ * overwritten.  mde_convbf_wgrad: gweight [cout,cin,ks,ks] fp32 (cout % 64 ==
+ * 0), overwritten, from deterministic block partials in
+ * mde_convbf_wgrad_workspace bytes + a fixed-order reduction.
+ * ------------------------------------------------------------------------- */
+int mde_convbf_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, int stride,
+                         int pass);
+size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose);
+int mde_convbf_pack(const float* weight, void* packed, int64_t cin, int64_t cout, int ks,
+                    int transpose, void* stream);
+int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
+                            int stride);
+int mde_convbf_fwd(const void* x, const void* packed, void* y, float* stats, int64_t n,
+                   int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, int stride,
+                   void* stream);
+int mde_convbf_bwd_data(const void* gy, const void* packed_t, void* gx, int64_t n, int64_t cin,
+                        int64_t cout, int64_t h, int64_t w, int ks, int stride, void* stream);
+size_t mde_convbf_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                   int ks, int stride);
+int mde_convbf_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                     int64_t cout, int64_t h, int64_t w, int ks, int stride, void* workspace,
+                     void* stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).
  * When enabled, every launch made through this ABI is bracketed by hipEvents
  * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY

@@ -128,7 +128,7 @@ class segmenthead(nn.Module):  # noqa: N801  (reference class name)
         self.conv1 = Conv2d(inplanes, interplanes, 3, padding=1, bias=False)
         self.bn2 = _bn(interplanes, "relu")
         self.relu = nn.ReLU(inplace=True)
-        self.conv2 = nn.Conv2d(interplanes, outplanes, 1, padding=0, bias=True)
+        self.conv2 = Conv2d(interplanes, outplanes, 1, padding=0, bias=True)
         self.scale_factor = scale_factor
 
     def forward(self, x):

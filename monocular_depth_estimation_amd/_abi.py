@@ -154,6 +154,14 @@ SIGNATURES = {
     "mde_wino_conv_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int,
                                    _vp]),
     "mde_wino_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_convbf_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int, _int]),
+    "mde_convbf_pack_elems": (_sz, [_i64, _i64, _int, _int]),
+    "mde_convbf_pack": (_int, [_vp, _vp, _i64, _i64, _int, _int, _vp]),
+    "mde_convbf_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64, _int, _int]),
+    "mde_convbf_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "mde_convbf_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "mde_convbf_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64, _i64, _int, _int]),
+    "mde_convbf_wgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp]),
     "mde_conv3x3_guide_bf16_stats_blocks": (_int, [_i64, _i64, _i64, _i64]),
     "mde_conv3x3_guide_bf16_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     "mde_graph_count_memsets": (_int, [_vp, _c.POINTER(_i64)]),

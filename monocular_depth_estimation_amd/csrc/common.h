@@ -80,6 +80,11 @@ enum Kid : int {
   K_WINO_DGRAD,
   K_WINO_WEIGHT,
   K_WATTN_BWD_REDUCE,  // the window-attention backward's table / bias slab reduction
+  K_CBF_FWD,        // bf16 implicit-GEMM convolutions (convbf.hip, v_mfma_f32_32x32x16_bf16)
+  K_CBF_DGRAD,
+  K_CBF_WGRAD,
+  K_CBF_WREDUCE,
+  K_CBF_PACK,
   K_COUNT
 };
 

@@ -1,0 +1,822 @@
+// bf16 implicit-GEMM convolutions, NCHW, on v_mfma_f32_32x32x16_bf16: the
+// DDRNet-23-slim convolutions of GuideDepth's encoder under bf16 autocast
+// (BASELINE cfg3; src/GuideDepth/model/DDRNet_23_slim.py:41-113 BasicBlock /
+// Bottleneck, :121-171 DAPPM, :230-263 stem / down / compression convs),
+// which MIOpen runs as NHWC implicit GEMM behind NCHW <-> NHWC transposes and
+// cast / zero-fill kernels.  Autocast's conv semantics: bf16 operands (the fp32
+// weight rounded to bf16, round-to-nearest-even, as autocast's cast), fp32
+// accumulation, bf16 output; the weight gradient is accumulated and returned
+// in fp32 (the master weight's dtype).
+//
+// One forward kernel serves every pass that is a convolution of a bf16 NCHW
+// source with a packed bf16 filter:
+//   * 3x3 / 1x1 forward, stride 1 or 2 (MODE S1 / S2);
+//   * their data gradients: stride 1 = the forward on the flipped, transposed
+//     filter; stride 2 (MODE U2) = a stride-1 convolution of the flipped,
+//     transposed filter over gy with zeros inserted between its rows and
+//     columns (staged that way into LDS; the zero taps are multiplied, 4x the
+//     MACs of the true transposed convolution -- the stride-2 convs are the
+//     encoder's smallest);
+// GEMM: M = output pixels (a patch of up to 128 / 256 of them: consecutive
+// pixels of one image plane, or a 2D tile), N = output channels (32 / 64 a
+// block), K = (tap, input channel) in chunks of 32 channels.  Per chunk the
+// block stages the input patch with its halo in LDS as [pixel][32 channels]
+// (80-byte pixel pitch: the 16-byte A-operand reads of 16 consecutive pixels
+// hit 16 disjoint bank quads) -- transposed from NCHW on the way in (a lane
+// loads 8 channels x 2 pixels as dwords and writes two 16-byte pixels), so a
+// tap or a stride is a pixel offset, never a misaligned read -- and the
+// chunk's filter as [tap][channel out][32 channels in] (64-byte rows, 16-byte
+// pieces XOR-swizzled by the row).  Stride 2 stages each row split by column
+// parity (even columns, then odd), so the three column taps of 32 consecutive
+// output pixels read 32 consecutive staged pixels.  Wave = 64 pixels x 32
+// channels (two 32x32 tiles sharing the B operand).  The epilogue writes bf16
+// and optionally the following BatchNorm's per-block statistics (the format of
+// the other conv kernels' epilogues, common.h Sh).
+//
+// Weight gradient: M = output channels (64 a block), N = (tap, 32 input
+// channels), K = pixels.  gy is staged as [channel][pixel] rows (A operand:
+// 16-byte row reads); x as the forward's [pixel][32 channels] image at a
+// 64-byte pitch, read TRANSPOSED by ds_read_b64_tr_b16 (B operand: 8 pixels of
+// one channel per lane, each 4-pixel row group addressed through a per-patch
+// pixel -> staged-pixel table, so taps and strides are again offsets).  Waves
+// = 2 channel tiles x 3 filter rows (3x3) or x 2 K halves (1x1).  Blocks split
+// the pixel patches (split-K); their fp32 partials are summed in a fixed order
+// (bitwise reproducible, no atomics).
+#include "common.h"
+
+namespace {
+
+using mde::bf16;
+using bf8v = __bf16 __attribute__((ext_vector_type(8)));
+using f16v = float __attribute__((ext_vector_type(16)));
+using u4v = uint32_t __attribute__((ext_vector_type(4)));
+using u2v = uint32_t __attribute__((ext_vector_type(2)));
+using s4v = short __attribute__((ext_vector_type(4)));
+using lds_s4 = __attribute__((address_space(3))) s4v;
+
+__device__ __forceinline__ f16v mfma32(u4v a, u4v b, f16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, a),
+                                                 __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+
+enum Mode : int { S1 = 0, S2 = 1, U2 = 2 };
+
+constexpr int kPitchF = 40;  // forward image: bf16 elements per staged pixel (32 + 8 pad)
+constexpr int kPitchW = 32;  // weight-gradient image (transposed reads): no pad
+constexpr int kGP = 136;     // weight-gradient gy rows: bf16 per channel (128 + 8 pad)
+constexpr int kMBW = 128;    // weight-gradient patch pixels
+
+// Patch geometry of a pass (host-chosen, see pick_geo).
+struct Geo {
+  int cin, cout;   // channels of THIS pass (dgrad: cin = the forward's cout)
+  int hi, wi;      // staged source plane (x; gy for U2)
+  int ho, wo;      // output plane
+  int pc, pr;      // 2D tiles of pr rows x pc columns; pc == 0: flat patches of mb pixels
+  int mb;          // flat patch pixels
+  int tiles_w;     // 2D: column tiles per band of pr rows
+  int ppi;         // patches per image
+  int cap;         // staged-pixel capacity (LDS image)
+};
+
+struct Patch {
+  int img, r0, r1, c0, nc, p0, npx;
+};
+
+__device__ __forceinline__ Patch patch_of(const Geo& g, int q) {
+  Patch P;
+  P.img = q / g.ppi;
+  const int k = q - P.img * g.ppi;
+  if (g.pc == 0) {
+    const int hw = g.ho * g.wo;
+    P.p0 = k * g.mb;
+    P.npx = hw - P.p0 < g.mb ? hw - P.p0 : g.mb;
+    P.r0 = P.p0 / g.wo;
+    P.r1 = (P.p0 + P.npx - 1) / g.wo;
+    P.c0 = 0;
+    P.nc = g.wo;
+  } else {
+    const int band = k / g.tiles_w, t = k - band * g.tiles_w;
+    P.r0 = band * g.pr;
+    P.r1 = (P.r0 + g.pr < g.ho ? P.r0 + g.pr : g.ho) - 1;
+    P.c0 = t * g.pc;
+    P.nc = g.pc;
+    P.p0 = 0;
+    P.npx = g.pr * g.pc;
+  }
+  return P;
+}
+
+// patch pixel m -> output (r, c); false if outside the plane / patch
+__device__ __forceinline__ bool pix_of(const Geo& g, const Patch& P, int m, int& r, int& c) {
+  if (g.pc == 0) {
+    const int p = P.p0 + (m < P.npx ? m : 0);
+    r = p / g.wo;
+    c = p - r * g.wo;
+    return m < P.npx;
+  }
+  r = P.r0 + m / g.pc;
+  c = P.c0 + m % g.pc;
+  return m < P.npx && r < g.ho && c < g.wo;
+}
+
+struct Img {
+  int gr0, rs, gc0, cs, csh;
+};
+
+// The staged image of a patch: rows gr0 .. gr0 + rs - 1 and cols gc0 .. of the
+// source (Z = zero-inserted gy coordinates for U2; (2 i, 2 j) for 1x1 stride 2)
+template <int KS, int MODE>
+__device__ __forceinline__ Img img_of(const Patch& P) {
+  Img I;
+  const int nr = P.r1 - P.r0 + 1;
+  if constexpr (KS == 3 && MODE == S2) {
+    I.gr0 = 2 * P.r0 - 1;
+    I.rs = 2 * nr + 1;
+    I.gc0 = 2 * P.c0 - 2;
+    I.csh = P.nc + 1;
+    I.cs = 2 * I.csh;
+  } else if constexpr (KS == 3) {  // S1, U2
+    I.gr0 = P.r0 - 1;
+    I.rs = nr + 2;
+    I.gc0 = P.c0 - 2;
+    I.cs = P.nc + 4;
+    I.csh = 0;
+  } else {
+    I.gr0 = P.r0;
+    I.rs = nr;
+    I.gc0 = P.c0;
+    I.cs = P.nc;
+    I.csh = 0;
+  }
+  return I;
+}
+
+// staged-pixel index of output pixel (r, c) at tap (0, 0)
+template <int KS, int MODE>
+__device__ __forceinline__ int img_base(const Patch& P, const Img& I, int r, int c) {
+  if constexpr (KS == 3 && MODE == S2) return 2 * (r - P.r0) * I.cs + (c - P.c0);
+  if constexpr (KS == 3) return (r - P.r0) * I.cs + (c - P.c0) + 1;
+  return (r - P.r0) * I.cs + (c - P.c0);
+}
+
+// offset of tap (dy, dx) from the tap-(0, 0) staged pixel
+template <int KS, int MODE>
+__device__ __forceinline__ int tap_off(const Img& I, int dy, int dx) {
+  if constexpr (KS == 1) return 0;
+  if constexpr (MODE == S2) return dy * I.cs + (dx == 0 ? I.csh : (dx == 1 ? 1 : I.csh + 1));
+  return dy * I.cs + dx;
+}
+
+__device__ __forceinline__ uint32_t lo16x2(uint32_t a, uint32_t b) {  // (a.lo, b.lo)
+  return __builtin_amdgcn_perm(b, a, 0x05040100u);
+}
+__device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {  // (a.hi, b.hi)
+  return __builtin_amdgcn_perm(b, a, 0x07060302u);
+}
+
+// Stage 32 channels (ci0 ..) of the patch's source image into LDS, pixel pitch
+// PITCH bf16, [pixel][channel].  Unit = (channel octet, staged row, pair of
+// staged columns): 8 dword loads (8 channels x 2 source pixels), clamped
+// addresses + selects (no branches around loads), two 16-byte LDS writes.
+template <int KS, int MODE, int PITCH, int NT>
+__device__ __forceinline__ void stage_src(bf16* img, const bf16* __restrict__ src, const Geo& g,
+                                          const Img& I, int ci0, int tid) {
+  const int64_t plane = (int64_t)g.hi * g.wi;
+  if constexpr (MODE == U2) {
+    // Z[zr][zc] = gy[zr / 2][zc / 2] for even zr, zc, else 0; unit = (octet,
+    // row, even Z column): 8 channel loads of one gy element, two staged
+    // pixels (the odd one zero)
+    const int npair = I.cs >> 1, per = I.rs * npair, total = 4 * per;
+    for (int u = tid; u < total; u += NT) {
+      const int o = u / per, rem = u - o * per, i = rem / npair, jp = rem - i * npair;
+      const int zr = I.gr0 + i, zc = I.gc0 + 2 * jp;
+      const int sr = zr >> 1, sc = zc >> 1;
+      const bool ok = (zr & 1) == 0 && zr >= 0 && sr < g.hi && zc >= 0 && sc < g.wi &&
+                      ci0 + 8 * o < g.cin;
+      const bf16* p = src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0);
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = p[ok ? j * plane : 0];
+      u4v a;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[j] = ok ? (v[2 * j] | (v[2 * j + 1] << 16)) : 0u;
+      bf16* d = img + (i * I.cs + 2 * jp) * PITCH + 8 * o;
+      *reinterpret_cast<u4v*>(d) = a;
+      *reinterpret_cast<u4v*>(d + PITCH) = u4v{0u, 0u, 0u, 0u};
+    }
+  } else if constexpr (KS == 1 && MODE == S2) {
+    // staged (i, j) = source (2 (gr0 + i), 2 (gc0 + j)): the even element of each pair
+    const int per = I.rs * I.cs, total = 4 * per;
+    for (int u = tid; u < total; u += NT) {
+      const int o = u / per, rem = u - o * per, i = rem / I.cs, j = rem - i * I.cs;
+      const int sr = 2 * (I.gr0 + i), sc = 2 * (I.gc0 + j);
+      const bool ok = sr < g.hi && sc < g.wi && ci0 + 8 * o < g.cin;
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(
+          src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0));
+      const int64_t pl2 = plane >> 1;
+      uint32_t v[8];
+#pragma unroll
+      for (int j2 = 0; j2 < 8; ++j2) v[j2] = p[ok ? j2 * pl2 : 0];
+      u4v a;
+#pragma unroll
+      for (int j2 = 0; j2 < 4; ++j2) a[j2] = ok ? lo16x2(v[2 * j2], v[2 * j2 + 1]) : 0u;
+      *reinterpret_cast<u4v*>(img + (i * I.cs + j) * PITCH + 8 * o) = a;
+    }
+  } else {
+    // S1 (3x3 / 1x1) and 3x3 S2: source column pairs (gc, gc + 1), gc even
+    const int npair = (KS == 3 && MODE == S2) ? I.csh : (I.cs >> 1);
+    const int per = I.rs * npair, total = 4 * per;
+    const int64_t pl2 = plane >> 1;
+    for (int u = tid; u < total; u += NT) {
+      const int o = u / per, rem = u - o * per, i = rem / npair, jp = rem - i * npair;
+      const int sr = I.gr0 + i, sc = I.gc0 + 2 * jp;
+      const bool ok = sr >= 0 && sr < g.hi && sc >= 0 && sc < g.wi && ci0 + 8 * o < g.cin;
+      const uint32_t* p = reinterpret_cast<const uint32_t*>(
+          src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0));
+      uint32_t v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = p[ok ? j * pl2 : 0];
+      u4v e, od;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        e[j] = ok ? lo16x2(v[2 * j], v[2 * j + 1]) : 0u;
+        od[j] = ok ? hi16x2(v[2 * j], v[2 * j + 1]) : 0u;
+      }
+      int d0, d1;
+      if constexpr (KS == 3 && MODE == S2) {
+        d0 = i * I.cs + jp;
+        d1 = d0 + I.csh;
+      } else {
+        d0 = i * I.cs + 2 * jp;
+        d1 = d0 + 1;
+      }
+      *reinterpret_cast<u4v*>(img + d0 * PITCH + 8 * o) = e;
+      *reinterpret_cast<u4v*>(img + d1 * PITCH + 8 * o) = od;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ forward
+// Block: 4 waves; wave (wm, wn): output channels 32 wn .. of the block's
+// 32 WN, M tiles MTW wm .. MTW wm + MTW - 1 (32 pixels each) of the patch
+// (32 MTW 4 / WN pixels).
+template <int KS, int MODE, int WN, int MTW, bool STATS, int CAP>
+__global__ void __launch_bounds__(256, 2)
+    convbf_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
+                      bf16* __restrict__ y, float* __restrict__ stats, Geo g) {
+  constexpr int KK = KS * KS, NB = 32 * WN, WMW = 4 / WN;
+  __shared__ __attribute__((aligned(16))) bf16 simg[CAP * kPitchF];
+  __shared__ __attribute__((aligned(16))) bf16 sw[KK * NB * 32];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv % WMW, wn = wv / WMW;
+  const Patch P = patch_of(g, blockIdx.x);
+  const Img I = img_of<KS, MODE>(P);
+  const int co0 = blockIdx.y * NB;
+  const int nmt = (P.npx + 31) >> 5;  // M tiles holding pixels
+
+  int abase[MTW];
+  bool mt_on[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    const int mt = MTW * wm + i;
+    mt_on[i] = mt < nmt;
+    int r, c;
+    const bool ok = pix_of(g, P, mt * 32 + l32, r, c);
+    abase[i] = ok ? img_base<KS, MODE>(P, I, r, c) : 0;
+  }
+  int toff[KK];
+#pragma unroll
+  for (int t = 0; t < KK; ++t) toff[t] = tap_off<KS, MODE>(I, t / KS, t % KS) * kPitchF;
+  const int col = wn * 32 + l32;  // B column (output channel within the block)
+  const int sw_x = (col >> 2) & 3;
+  const int boff0 = col * 32 + 8 * ((0 + h) ^ sw_x), boff1 = col * 32 + 8 * ((2 + h) ^ sw_x);
+
+  f16v acc[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  const bf16* xs = x + (int64_t)P.img * g.cin * g.hi * g.wi;
+  const int nchunk = (g.cin + 31) >> 5;
+  for (int cc = 0; cc < nchunk; ++cc) {
+    __syncthreads();
+    stage_src<KS, MODE, kPitchF, 256>(simg, xs, g, I, 32 * cc, tid);
+    {  // filter chunk: [tap][NB][32], 16-byte pieces swizzled by (row >> 2) & 3
+      const bf16* src = wp + (int64_t)cc * KK * g.cout * 32;
+      for (int u = tid; u < KK * NB * 4; u += 256) {
+        const int o = u & 3, rest = u >> 2, cl = rest % NB, t = rest / NB;
+        const u4v v = *reinterpret_cast<const u4v*>(src + ((int64_t)t * g.cout + co0 + cl) * 32 + 8 * o);
+        *reinterpret_cast<u4v*>(sw + (t * NB + cl) * 32 + 8 * (o ^ ((cl >> 2) & 3))) = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < KK; ++t) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const u4v b = *reinterpret_cast<const u4v*>(sw + t * NB * 32 + (ks ? boff1 : boff0));
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+          if (mt_on[i]) {  // wave-uniform
+            const u4v a = *reinterpret_cast<const u4v*>(simg + abase[i] * kPitchF + toff[t] +
+                                                       16 * ks + 8 * h);
+            acc[i] = mfma32(a, b, acc[i]);
+          }
+        }
+      }
+    }
+  }
+
+  // epilogue: lane (co = co0 + col, h) holds pixels 32 mt + 8 q + 4 h + (0..3), q = reg >> 2
+  const int co = co0 + col;
+  const int64_t hwo = (int64_t)g.ho * g.wo;
+  bf16* yc = y + ((int64_t)P.img * g.cout + co) * hwo;
+  mde::Sh run{0.f, 0.f, 0.f, 0.f};
+  bool have_ref = false;
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    if (!mt_on[i]) continue;
+    const int mt = MTW * wm + i;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int m = mt * 32 + 8 * q + 4 * h;
+      int r, c;
+      const bool ok = pix_of(g, P, m, r, c);
+      const bf16 b0 = mde::f2bf(acc[i][4 * q]), b1 = mde::f2bf(acc[i][4 * q + 1]);
+      const bf16 b2 = mde::f2bf(acc[i][4 * q + 2]), b3 = mde::f2bf(acc[i][4 * q + 3]);
+      if constexpr (STATS) {
+        if (!have_ref) {  // one shift per channel and wave: lane (co, h = 0)'s first value
+          const float v0 = __shfl(mde::bf2f(b0), l32, 64);
+          run.ref = v0;
+          have_ref = true;
+        }
+        mde::sh_add(run, mde::bf2f(b0), ok);
+        mde::sh_add(run, mde::bf2f(b1), ok);
+        mde::sh_add(run, mde::bf2f(b2), ok);
+        mde::sh_add(run, mde::bf2f(b3), ok);
+      }
+      if (ok)
+        *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) =
+            u2v{(uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16)};
+    }
+  }
+  if constexpr (STATS) {
+    run = mde::sh_xor_sum(run, 32);
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(simg);  // [WMW][NB][4]
+    if (h == 0) {
+      float* p4 = part + (wm * NB + col) * 4;
+      p4[0] = run.ref;
+      p4[1] = run.n;
+      p4[2] = run.s1;
+      p4[3] = run.s2;
+    }
+    __syncthreads();
+    if (tid < NB) {
+      mde::Sh a{part[tid * 4], part[tid * 4 + 1], part[tid * 4 + 2], part[tid * 4 + 3]};
+#pragma unroll
+      for (int k = 1; k < WMW; ++k) {
+        const float* p4 = part + (k * NB + tid) * 4;
+        a = mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      float* o4 = stats + ((int64_t)(co0 + tid) * gridDim.x + blockIdx.x) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
+    }
+  }
+}
+
+// ---------------------------------------------------------- weight gradient
+// Block: 64 output x 32 input channels, all taps, the patches
+// [blockIdx.x * per, ...); 6 waves (3x3: wave = channel tile wc x filter row
+// dy, three 32x32 accumulators, one per dx) or 4 (1x1: wc x K half).
+template <int KS, int MODE, int CAP>
+__global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
+    convbf_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
+                        float* __restrict__ part, Geo g, int per, int npatch) {
+  constexpr int KK = KS * KS, NT = KS == 3 ? 384 : 256, ND = KS == 3 ? 3 : 1;
+  constexpr int ME = 64 * KK * 32;  // partial elements: [co 64][tap][ci 32]
+  __shared__ __attribute__((aligned(16))) bf16 simg[CAP * kPitchW];
+  __shared__ __attribute__((aligned(16))) bf16 sg[64 * kGP];
+  __shared__ int tab[kMBW];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wv & 1, wy = wv >> 1;  // 3x3: filter row wy; 1x1: K half wy
+  const int ngo = (g.cout + 63) >> 6;
+  const int cob = blockIdx.y % ngo, cc = blockIdx.y / ngo;
+  const int co_live = g.cout - cob * 64 < 64 ? g.cout - cob * 64 : 64;  // 32 or 64
+  const int q0 = blockIdx.x * per, q1 = q0 + per < npatch ? q0 + per : npatch;
+
+  f16v acc[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[d][r] = 0.f;
+
+  // transposed-read lane roles: 16-lane group gq, row q, column quad p
+  const int gq = lane >> 4, qr = (lane >> 2) & 3, pq = lane & 3;
+  const int bcol = 16 * (gq & 1) + 4 * pq;  // channel (element) offset in a staged pixel
+  const int arow = (wc * 32 + l32) * kGP + 8 * h;
+  const int64_t hwo = (int64_t)g.ho * g.wo;
+
+  for (int q = q0; q < q1; ++q) {
+    const Patch P = patch_of(g, q);
+    const Img I = img_of<KS, MODE>(P);
+    __syncthreads();
+    stage_src<KS, MODE, kPitchW, NT>(simg, x + (int64_t)P.img * g.cin * g.hi * g.wi, g, I,
+                                     32 * cc, tid);
+    {  // gy rows: [64 channels][128 pixels], 4 pixels a unit (8-byte loads)
+      const bf16* gsrc = gy + ((int64_t)P.img * g.cout + cob * 64) * hwo;
+      for (int u = tid; u < 64 * (kMBW / 4); u += NT) {
+        const int cl = u / (kMBW / 4), m4 = 4 * (u - cl * (kMBW / 4));
+        int r, c;
+        const bool ok = pix_of(g, P, m4, r, c) && cl < co_live;
+        const u2v v = *reinterpret_cast<const u2v*>(gsrc + (int64_t)cl * hwo +
+                                                     (ok ? (int64_t)r * g.wo + c : 0));
+        *reinterpret_cast<u2v*>(sg + cl * kGP + m4) = ok ? v : u2v{0u, 0u};
+      }
+    }
+    for (int m = tid; m < kMBW; m += NT) {
+      int r, c;
+      const bool ok = pix_of(g, P, m, r, c);
+      tab[m] = ok ? img_base<KS, MODE>(P, I, r, c) : 0;
+    }
+    __syncthreads();
+    int toff[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) toff[d] = KS == 3 ? tap_off<KS, MODE>(I, wy, d) : 0;
+    const int nks = (P.npx + 15) >> 4;
+    for (int ks = (KS == 3 ? 0 : wy); ks < nks; ks += (KS == 3 ? 1 : 2)) {
+      const u4v a = *reinterpret_cast<const u4v*>(sg + arow + 16 * ks);
+      const int m0 = 16 * ks + 8 * (gq >> 1) + qr;
+      const int t0 = tab[m0], t1 = tab[m0 + 4];
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(simg + (t0 + toff[d]) * kPitchW + bcol));
+        const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(simg + (t1 + toff[d]) * kPitchW + bcol));
+        const u2v l2 = __builtin_bit_cast(u2v, lo), h2 = __builtin_bit_cast(u2v, hi);
+        acc[d] = mfma32(a, u4v{l2.x, l2.y, h2.x, h2.y}, acc[d]);
+      }
+    }
+  }
+
+  // D[co][ci]: lane (ci = l32, h), register r -> co row (r & 3) + 8 (r >> 2) + 4 h
+  float* out = part + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * ME;
+  if constexpr (KS == 3) {
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      const int tap = wy * 3 + d;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int col = wc * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(col * KK + tap) * 32 + l32] = acc[d][r];
+      }
+    }
+  } else {  // the two K halves summed through LDS, half 0 + half 1
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(simg);  // [64 co][32 ci]
+    if (wy == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[(wc * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = acc[0][r];
+    }
+    __syncthreads();
+    if (wy == 0) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int col = wc * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[col * 32 + l32] = acc[0][r] + red[col * 32 + l32];
+      }
+    }
+  }
+}
+
+// gw[co][ci][tap] = sum over the S block partials of group (cob, cc), in order
+template <int KK>
+__global__ void __launch_bounds__(256)
+    convbf_wreduce_kernel(const float* __restrict__ part, float* __restrict__ gw, int S, int cin,
+                          int cout) {
+  constexpr int ME = 64 * KK * 32;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= ME) return;
+  const int grp = blockIdx.y, ngo = (cout + 63) >> 6, cob = grp % ngo, cc = grp / ngo;
+  const float* p = part + (int64_t)grp * S * ME + e;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 3 < S; s += 4) {
+    a0 += p[(int64_t)s * ME];
+    a1 += p[(int64_t)(s + 1) * ME];
+    a2 += p[(int64_t)(s + 2) * ME];
+    a3 += p[(int64_t)(s + 3) * ME];
+  }
+  for (; s < S; ++s) a0 += p[(int64_t)s * ME];
+  const int col = e / (KK * 32), rest = e - col * KK * 32, tap = rest / 32, ci = rest % 32;
+  if (cob * 64 + col >= cout) return;
+  gw[((int64_t)(cob * 64 + col) * cin + cc * 32 + ci) * KK + tap] = (a0 + a1) + (a2 + a3);
+}
+
+// packed filter [cc][tap][co][32] (bf16, RNE) of the pass: forward (w[co][ci][tap]) or
+// transposed + flipped (data gradient: the pass's input channels are the forward's outputs)
+__global__ void __launch_bounds__(256)
+    convbf_pack_kernel(const float* __restrict__ w, bf16* __restrict__ p, int cin, int cout, int kk,
+                       int transpose, int64_t total) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= total) return;
+  const int pco = transpose ? cin : cout, pci = transpose ? cout : cin;
+  const int j = (int)(e & 31);
+  int64_t rest = e >> 5;
+  const int co = (int)(rest % pco);
+  rest /= pco;
+  const int tap = (int)(rest % kk), cc = (int)(rest / kk);
+  const int ci = cc * 32 + j;
+  float v = 0.f;
+  if (ci < pci)
+    v = transpose ? w[((int64_t)ci * cin + co) * kk + (kk - 1 - tap)]
+                  : w[((int64_t)co * cin + ci) * kk + tap];
+  p[e] = mde::f2bf(v);
+}
+
+// ------------------------------------------------------------------- host
+constexpr int kCapS1 = 420;  // staged pixels: 33.6 KB (+ 36.9 KB filter): two blocks a CU
+constexpr int kCapS2 = 640;  // stride 2 / zero-inserted: 51 KB (one block a CU)
+
+struct Pass {
+  int ks, mode, cin, cout, hi, wi, ho, wo;
+};
+
+inline int cap_of(const Pass& p) { return (p.ks == 3 && p.mode != S1) ? kCapS2 : kCapS1; }
+
+// staged pixels of the largest patch of a geometry
+inline int img_px(const Pass& p, int pc, int pr, int mb) {
+  int nr, nc;
+  if (pc == 0) {
+    nr = (mb + p.wo - 2) / p.wo + 1;  // rows a run of mb consecutive pixels can touch
+    if (nr > p.ho) nr = p.ho;
+    nc = p.wo;
+  } else {
+    nr = pr;
+    nc = pc;
+  }
+  if (p.ks == 3 && p.mode == S2) return (2 * nr + 1) * 2 * (nc + 1);
+  if (p.ks == 3) return (nr + 2) * (nc + 4);
+  return nr * nc;
+}
+
+// Choose the patch geometry: flat runs of mb pixels when the image fits,
+// else 2D tiles (pc columns x pr rows, pr * pc <= mb) with the fewest padded
+// pixels.  False if nothing fits or the shape breaks an alignment rule.
+inline bool pick_geo(const Pass& p, int mb, Geo* g) {
+  g->cin = p.cin;
+  g->cout = p.cout;
+  g->hi = p.hi;
+  g->wi = p.wi;
+  g->ho = p.ho;
+  g->wo = p.wo;
+  g->mb = mb;
+  g->cap = cap_of(p);
+  const int64_t hw = (int64_t)p.ho * p.wo;
+  if (hw % 4 == 0 && img_px(p, 0, 0, mb) <= g->cap) {
+    g->pc = g->pr = 0;
+    g->tiles_w = 1;
+    g->ppi = (int)mde::cdiv(hw, mb);
+    return true;
+  }
+  if (p.wo % 4) return false;
+  int best = -1;
+  int64_t best_cost = 0;
+  const int cands[] = {64, 40, 32, 20, 16, 8, 4};
+  for (int pc : cands) {
+    if (pc > p.wo && pc != cands[6]) continue;
+    int pr = mb / pc;
+    if (pr > p.ho) pr = p.ho;
+    if (pr < 1 || img_px(p, pc, pr, mb) > g->cap) continue;
+    const int64_t tiles = mde::cdiv(p.ho, pr) * mde::cdiv(p.wo, pc);
+    const int64_t cost = tiles * ((int64_t)(pr * pc + 31) / 32 * 32);
+    if (best < 0 || cost < best_cost) {
+      best = pc;
+      best_cost = cost;
+    }
+  }
+  if (best < 0) return false;
+  g->pc = best;
+  g->pr = mb / best < p.ho ? mb / best : p.ho;
+  g->tiles_w = (int)mde::cdiv(p.wo, g->pc);
+  g->ppi = (int)(mde::cdiv(p.ho, g->pr) * g->tiles_w);
+  return true;
+}
+
+// the pass of (n, cin, cout, h, w, ks, stride) and which: 0 forward, 1 data gradient, 2 weight gradient
+inline bool make_pass(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, int stride, int which,
+                      Pass* p) {
+  if ((ks != 1 && ks != 3) || (stride != 1 && stride != 2)) return false;
+  if (cin <= 0 || cout <= 0 || h <= 0 || w <= 0 || cin % 32 || cout % 32) return false;
+  if (cin > 4096 || cout > 4096 || h > 4096 || w > 4096 || w % 2) return false;
+  const int pad = ks / 2;
+  const int ho = (int)((h + 2 * pad - ks) / stride + 1), wo = (int)((w + 2 * pad - ks) / stride + 1);
+  if (which == 1) {  // gx [cin, h, w] from gy [cout, ho, wo]
+    *p = Pass{ks, stride == 1 ? S1 : U2, (int)cout, (int)cin, ho, wo, (int)h, (int)w};
+  } else {
+    *p = Pass{ks, stride == 1 ? S1 : S2, (int)cin, (int)cout, (int)h, (int)w, ho, wo};
+  }
+  if (p->wi % 2) return false;  // dword pair loads of the staged source
+  return true;
+}
+
+template <int KS, int MODE, int WN, int MTW, int CAP>
+int launch_fwd_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const Geo& g, int64_t n,
+                 int kid, double flops, double bytes, hipStream_t s) {
+  const int64_t np = n * g.ppi;
+  if (np > 0x7fffffff) return MDE_ERR_UNSUPPORTED;
+  const dim3 grid((unsigned)np, (unsigned)(g.cout / (32 * WN)));
+  if (stats)
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, true, CAP>), grid,
+                    dim3(256), 0, x, wp, y, stats, g);
+  else
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, false, CAP>), grid,
+                    dim3(256), 0, x, wp, y, stats, g);
+  return MDE_OK;
+}
+
+inline int wn_of(const Pass& p) { return p.cout % 64 == 0 ? 2 : 1; }
+
+// forward geometry: 2 M tiles a wave (128 pixels a block at 64 output
+// channels, 256 at 32), or 1 when that patch's image does not fit
+inline bool fwd_geo(const Pass& p, Geo* g, int* mtw) {
+  const int wmw = 4 / wn_of(p);
+  for (int m = 2; m >= 1; --m) {
+    if (pick_geo(p, 32 * m * wmw, g)) {
+      *mtw = m;
+      return true;
+    }
+  }
+  return false;
+}
+
+int launch_fwd(const Pass& p, const bf16* x, const bf16* wp, bf16* y, float* stats, int64_t n,
+               int kid, hipStream_t s) {
+  const int wn = wn_of(p);
+  Geo g;
+  int mtw;
+  if (!fwd_geo(p, &g, &mtw)) return MDE_ERR_UNSUPPORTED;
+  const double flops = 2.0 * n * p.ho * p.wo * (double)p.cout * p.cin * p.ks * p.ks;
+  const double bytes = 2.0 * n * ((double)p.cin * p.hi * p.wi + (double)p.cout * p.ho * p.wo);
+#define CBF_FWD(KS, MODE, CAP)                                                                   \
+  return wn == 2 ? (mtw == 2 ? launch_fwd_t<KS, MODE, 2, 2, CAP>(x, wp, y, stats, g, n, kid, flops, \
+                                                                bytes, s)                        \
+                             : launch_fwd_t<KS, MODE, 2, 1, CAP>(x, wp, y, stats, g, n, kid, flops, \
+                                                                bytes, s))                       \
+                 : (mtw == 2 ? launch_fwd_t<KS, MODE, 1, 2, CAP>(x, wp, y, stats, g, n, kid, flops, \
+                                                                bytes, s)                        \
+                             : launch_fwd_t<KS, MODE, 1, 1, CAP>(x, wp, y, stats, g, n, kid, flops, \
+                                                                bytes, s))
+  if (p.ks == 3) {
+    if (p.mode == S1) CBF_FWD(3, S1, kCapS1);
+    if (p.mode == S2) CBF_FWD(3, S2, kCapS2);
+    CBF_FWD(3, U2, kCapS2);
+  }
+  if (p.mode == S1) CBF_FWD(1, S1, kCapS1);
+  if (p.mode == S2) CBF_FWD(1, S2, kCapS1);
+  CBF_FWD(1, U2, kCapS1);
+#undef CBF_FWD
+}
+
+// weight-gradient split: blocks per (output 64, input 32) channel group
+inline int wgrad_splits(int groups, int64_t npatch) {
+  int64_t s = mde::cdiv(256, groups);
+  if (s > npatch) s = npatch;
+  return (int)(s < 1 ? 1 : s);
+}
+
+inline bool wgrad_geo(const Pass& p, int64_t n, Geo* g, int* S, int* per, int64_t* npatch) {
+  if (!pick_geo(p, kMBW, g)) return false;
+  const int64_t np = n * g->ppi;
+  if (np > 0x7fffffff) return false;
+  *npatch = np;
+  const int groups = ((p.cout + 63) / 64) * (p.cin / 32);
+  const int s0 = wgrad_splits(groups, np);
+  *per = (int)mde::cdiv(np, s0);
+  *S = (int)mde::cdiv(np, *per);
+  return true;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mde_convbf_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, int stride,
+                         int pass) {
+  Pass p;
+  if (pass < 0 || pass > 2 || !make_pass(cin, cout, h, w, ks, stride, pass == 1 ? 1 : 0, &p))
+    return 0;
+  Geo g;
+  if (pass == 2) {
+    int S, per;
+    int64_t np;
+    return wgrad_geo(p, 1, &g, &S, &per, &np) ? 1 : 0;
+  }
+  int mtw;
+  return fwd_geo(p, &g, &mtw) ? 1 : 0;
+}
+
+size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose) {
+  const int64_t pci = transpose ? cout : cin, pco = transpose ? cin : cout;
+  return (size_t)(mde::cdiv(pci, 32) * 32 * pco * ks * ks);
+}
+
+int mde_convbf_pack(const float* weight, void* packed, int64_t cin, int64_t cout, int ks,
+                    int transpose, void* stream) {
+  if (!weight || !packed || (ks != 1 && ks != 3) || cin <= 0 || cout <= 0)
+    return MDE_ERR_INVALID_ARG;
+  const int64_t total = mde_convbf_pack_elems(cin, cout, ks, transpose);
+  MDE_LAUNCH(mde::K_CBF_PACK, 4.0 * cin * cout * ks * ks + 2.0 * total, (hipStream_t)stream,
+             convbf_pack_kernel, dim3((unsigned)mde::cdiv(total, 256)), dim3(256), 0, weight,
+             (bf16*)packed, (int)cin, (int)cout, ks * ks, transpose ? 1 : 0, total);
+  return MDE_OK;
+}
+
+int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
+                            int stride) {
+  Pass p;
+  Geo g;
+  int mtw;
+  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p) || !fwd_geo(p, &g, &mtw)) return 0;
+  return (int)(n * g.ppi);
+}
+
+int mde_convbf_fwd(const void* x, const void* packed, void* y, float* stats, int64_t n,
+                   int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, int stride,
+                   void* stream) {
+  if (!x || !packed || !y || n <= 0) return MDE_ERR_INVALID_ARG;
+  Pass p;
+  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p)) return MDE_ERR_UNSUPPORTED;
+  return launch_fwd(p, (const bf16*)x, (const bf16*)packed, (bf16*)y, stats, n, mde::K_CBF_FWD,
+                    (hipStream_t)stream);
+}
+
+int mde_convbf_bwd_data(const void* gy, const void* packed_t, void* gx, int64_t n, int64_t cin,
+                        int64_t cout, int64_t h, int64_t w, int ks, int stride, void* stream) {
+  if (!gy || !packed_t || !gx || n <= 0) return MDE_ERR_INVALID_ARG;
+  Pass p;
+  if (!make_pass(cin, cout, h, w, ks, stride, 1, &p)) return MDE_ERR_UNSUPPORTED;
+  return launch_fwd(p, (const bf16*)gy, (const bf16*)packed_t, (bf16*)gx, nullptr, n,
+                    mde::K_CBF_DGRAD, (hipStream_t)stream);
+}
+
+size_t mde_convbf_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w,
+                                   int ks, int stride) {
+  Pass p;
+  Geo g;
+  int S, per;
+  int64_t np;
+  if (n <= 0 || !make_pass(cin, cout, h, w, ks, stride, 0, &p) || !wgrad_geo(p, n, &g, &S, &per, &np))
+    return 0;
+  return sizeof(float) * (size_t)(((cout + 63) / 64) * (cin / 32) * S * 64 * ks * ks * 32);
+}
+
+int mde_convbf_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t cin,
+                     int64_t cout, int64_t h, int64_t w, int ks, int stride, void* workspace,
+                     void* stream) {
+  if (!gy || !x || !gweight || !workspace || n <= 0) return MDE_ERR_INVALID_ARG;
+  Pass p;
+  Geo g;
+  int S, per;
+  int64_t np;
+  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p) || !wgrad_geo(p, n, &g, &S, &per, &np))
+    return MDE_ERR_UNSUPPORTED;
+  hipStream_t s = (hipStream_t)stream;
+  const int groups = (int)(((cout + 63) / 64) * (cin / 32));
+  const double flops = 2.0 * n * p.ho * p.wo * (double)cout * cin * ks * ks;
+  const double bytes = 2.0 * n * ((double)cin * h * w + (double)cout * p.ho * p.wo);
+  const dim3 grid((unsigned)S, (unsigned)groups);
+  float* part = (float*)workspace;
+  const bf16 *gyb = (const bf16*)gy, *xb = (const bf16*)x;
+  if (ks == 3) {
+    if (p.mode == S1)
+      MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<3, S1, kCapS1>), grid,
+                      dim3(384), 0, xb, gyb, part, g, per, (int)np);
+    else
+      MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<3, S2, kCapS2>), grid,
+                      dim3(384), 0, xb, gyb, part, g, per, (int)np);
+    MDE_LAUNCH(mde::K_CBF_WREDUCE, 4.0 * groups * (double)S * 64 * 9 * 32 + 4.0 * cout * cin * 9, s,
+               convbf_wreduce_kernel<9>, dim3((unsigned)mde::cdiv(64 * 9 * 32, 256), groups),
+               dim3(256), 0, part, gweight, S, (int)cin, (int)cout);
+  } else {
+    if (p.mode == S1)
+      MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<1, S1, kCapS1>), grid,
+                      dim3(256), 0, xb, gyb, part, g, per, (int)np);
+    else
+      MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<1, S2, kCapS1>), grid,
+                      dim3(256), 0, xb, gyb, part, g, per, (int)np);
+    MDE_LAUNCH(mde::K_CBF_WREDUCE, 4.0 * groups * (double)S * 64 * 32 + 4.0 * cout * cin, s,
+               convbf_wreduce_kernel<1>, dim3((unsigned)mde::cdiv(64 * 32, 256), groups), dim3(256),
+               0, part, gweight, S, (int)cin, (int)cout);
+  }
+  return MDE_OK;
+}
+
+}  // extern "C"

@@ -30,7 +30,8 @@ const char* const kNames[mde::K_COUNT] = {
     "conv3x3_dgrad_bf16", "conv3x3_wgrad_bf16", "conv3x3_wgrad_wide", "conv3x3s2_wgrad",
     "conv1x1_fwd",   "conv1x1_dgrad",   "conv1x1_wgrad", "conv1x1_wreduce",
     "conv3x3s2_fwd", "conv3x3s2_dgrad", "conv3x3w_fwd", "conv3x3w_dgrad",
-    "wino_fwd",       "wino_dgrad",      "wino_weight",   "window_attn_bwd_reduce"};
+    "wino_fwd",       "wino_dgrad",      "wino_weight",   "window_attn_bwd_reduce",
+    "convbf_fwd_bf16", "convbf_dgrad_bf16", "convbf_wgrad_bf16", "convbf_wreduce", "convbf_pack"};
 
 struct Pending {
   int kid;

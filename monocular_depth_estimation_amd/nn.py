@@ -784,6 +784,92 @@ WINO32 = os.environ.get("MDE_WINO32", "1") != "0"  # the 32-channel output group
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"
 
 
+class _ConvBf16(torch.autograd.Function):
+    """A DDRNet convolution under bf16 autocast (3x3 p1 / 1x1 p0, stride 1 or
+    2, channels % 32) on the bf16 implicit-GEMM kernels of convbf.hip:
+    autocast's conv semantics -- x cast to bf16, the fp32 weight rounded to
+    bf16 (packed once per pass, mde_convbf_pack), fp32 accumulation, bf16 y /
+    gx, fp32 weight gradient -- in NCHW, with none of MIOpen's NHWC transposes
+    or cast / zero-fill kernels.  DDRNet_23_slim.py:35-38,41-113,121-171,
+    230-263 (every conv of the encoder but the 3-channel stem)."""
+
+    @staticmethod
+    @_bn_fwd
+    def forward(ctx, x, weight, ks, stride):
+        x = x.to(torch.bfloat16).contiguous()
+        weight = weight.contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        pad = ks // 2
+        ho, wo = (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1
+        st = _abi.stream_of(x)
+        wp = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 0), dtype=torch.bfloat16,
+                         device=x.device)
+        _abi.call("mde_convbf_pack", _abi.ptr(weight), _abi.ptr(wp), cin, cout, ks, 0, st)
+        y = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device)
+        _abi.call("mde_convbf_fwd", _abi.ptr(x), _abi.ptr(wp), _abi.ptr(y), None, n, cin, cout, h, w,
+                  ks, stride, st)
+        ctx.save_for_backward(x, weight)
+        ctx.ks, ctx.stride = ks, stride
+        return y
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gy = gy.to(torch.bfloat16).contiguous()
+        n, cin, h, w = x.shape
+        cout = weight.shape[0]
+        ks, stride = ctx.ks, ctx.stride
+        st = _abi.stream_of(gy)
+        gx = gw = None
+        if ctx.needs_input_grad[0]:
+            wt = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 1),
+                             dtype=torch.bfloat16, device=x.device)
+            _abi.call("mde_convbf_pack", _abi.ptr(weight), _abi.ptr(wt), cin, cout, ks, 1, st)
+            gx = torch.empty_like(x)
+            _abi.call("mde_convbf_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, cin, cout,
+                      h, w, ks, stride, st)
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(weight)
+            ws = _ws(_abi.query("mde_convbf_wgrad_workspace", n, cin, cout, h, w, ks, stride), x)
+            _abi.call("mde_convbf_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h, w,
+                      ks, stride, _abi.ptr(ws), st)
+        return gx, gw, None, None
+
+
+CONVBF = os.environ.get("MDE_CONVBF", "1") != "0"  # A/B switch: 0 = MIOpen's bf16 solvers
+_CONVBF_OK: dict = {}
+
+
+def convbf_ok(conv: nn.Conv2d, x) -> bool:
+    """Whether this conv runs on convbf.hip: a CUDA input under bf16 autocast
+    (or already bf16), fp32 weight, 3x3 / padding 1 or 1x1 / padding 0,
+    stride 1 or 2, zero padding, no groups / dilation, and all three passes
+    supported for the shape (channels % 32, even width, LDS capacity)."""
+    if not (CONVBF and x.is_cuda and x.dim() == 4
+            and (_autocast_bf16(x) or x.dtype == torch.bfloat16)
+            and conv.weight.dtype == torch.float32 and conv.groups == 1
+            and conv.dilation == (1, 1) and conv.padding_mode == "zeros"
+            and conv.stride in ((1, 1), (2, 2))
+            and ((conv.kernel_size == (3, 3) and conv.padding == (1, 1))
+                 or (conv.kernel_size == (1, 1) and conv.padding == (0, 0)))):
+        return False
+    key = (conv.in_channels, conv.out_channels, x.shape[2], x.shape[3], conv.kernel_size[0],
+           conv.stride[0])
+    ok = _CONVBF_OK.get(key)
+    if ok is None:
+        ok = all(_abi.query("mde_convbf_supported", *key, p) for p in (0, 1, 2))
+        _CONVBF_OK[key] = ok
+    return ok
+
+
+def conv_bf16(conv: nn.Conv2d, x):
+    """conv(x) without its bias on convbf.hip (see convbf_ok)."""
+    _gpu(x)
+    return _ConvBf16.apply(x, conv.weight, conv.kernel_size[0], conv.stride[0])
+
+
 class _GuideConvBf16(torch.autograd.Function):
     """The guided-upsampling blocks' guide convs (3 -> 16 / 32 / 64 on the
     image, modules.py:52-54) under bf16 autocast: the fp32 image and weight
@@ -868,6 +954,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
         y = _Pointwise.apply(x, conv.weight)
     elif passes is not None:
         y = conv3x3(x, conv.weight, passes)
+    elif convbf_ok(conv, x):
+        y = conv_bf16(conv, x)
     elif conv3x3s2_ok(conv, x):
         y = _Conv3x3S2.apply(x, conv.weight)
     elif conv1x1_ok(conv, x):
@@ -880,10 +968,13 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
 
 def conv_nobias(conv: nn.Conv2d, x):
     """conv(x) without its bias (folded into the following BN, or absent): the
-    HIP 3x3 / stride-2 / 1x1 kernels where they apply, else MIOpen."""
+    HIP 3x3 / stride-2 / 1x1 kernels where they apply (under bf16 autocast:
+    the 16 / 32-channel bf16 3x3 kernels, then convbf.hip), else MIOpen."""
     passes = conv3x3_passes(conv, x) if x.is_cuda else None
     if passes is not None:
         return conv3x3(x, conv.weight, passes)
+    if convbf_ok(conv, x):
+        return conv_bf16(conv, x)
     if conv3x3s2_ok(conv, x):
         return _Conv3x3S2.apply(x, conv.weight)
     if pointwise_ok(conv, x) and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x):
@@ -898,18 +989,24 @@ class Conv2d(nn.Conv2d):
     """nn.Conv2d (same parameters and state_dict keys) whose bias-free
     forward takes conv_nobias's HIP kernels where they apply.  With a bias:
     a 3x3 / stride-1 conv with a HIP forward or data-gradient pass (the NewCRF
-    projections, newcrf_layers.py: Winograd at 128-1024 channels) runs those
-    passes and adds the bias (its gradient is autograd's sum over the add);
-    anything else is the stock module (the DDRNet / decoder convs with a bias
-    are folded into a BatchNorm by run_sequential / conv_bn instead)."""
+    projections, newcrf_layers.py: Winograd at 128-1024 channels), or a bf16
+    autocast conv convbf.hip takes (DDRNet's segmenthead 1x1), runs on HIP and
+    adds the bias in the output's dtype (its gradient is autograd's sum over
+    the add); anything else -- and any padding_mode other than 'zeros' -- is
+    the stock module (the DDRNet / decoder convs with a bias are folded into a
+    BatchNorm by run_sequential / conv_bn instead)."""
 
     def forward(self, x):
-        if x.is_cuda:
+        if x.is_cuda and self.padding_mode == "zeros":
             if self.bias is None:
                 return conv_nobias(self, x)
             passes = conv3x3_passes(self, x)
             if passes is not None and (passes[0] or passes[1]):
-                return conv3x3(x, self.weight, passes) + self.bias.view(1, -1, 1, 1)
+                y = conv3x3(x, self.weight, passes)
+                return y + self.bias.to(y.dtype).view(1, -1, 1, 1)
+            if convbf_ok(self, x):
+                y = conv_bf16(self, x)
+                return y + self.bias.to(y.dtype).view(1, -1, 1, 1)
         return super().forward(x)
 
 

@@ -699,6 +699,12 @@ int mde_graph_node_types(void* graph, int64_t* counts);
 int mde_graph_dot(void* graph, const char* path);
 int mde_graph_replace_memsets(void* graph, int64_t* replaced);
 
+/* Which storage types the one-launch small-tensor BatchNorm kernels serve
+ * (n * h * w <= 16384; the others take the statistics + apply launches):
+ * 0 none, 1 fp32 (default), 2 fp32 and bf16.  mode < 0 only queries.
+ * Returns the previous mode. */
+int mde_bn_chan_mode(int mode);
+
 /* ---------------------------------------------------------------------------
  * bf16 convolutions, NCHW, any cin / cout multiple of 32, 3x3 (padding 1) or
  * 1x1 (padding 0), stride 1 or 2, input width even (v_mfma_f32_32x32x16_bf16,

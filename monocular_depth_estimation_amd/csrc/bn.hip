@@ -626,19 +626,17 @@ constexpr int kChanThreads = 512;
 constexpr int kChanUnits = 8;  // float4 (or elements) per thread
 constexpr int64_t kChanMax = (int64_t)kChanThreads * kChanUnits * 4;
 
-// fp32 only for now: under bf16 autocast the cfg3 GuideDepth golden test (the
-// bf16 step vs float64, bounded by the oracle's own bf16 error) moved from
-// 0.6 % to 1.7 % loss error with these kernels on DDRNet's 1x1 - 2x2 bottom
-// maps, where train-mode BN over a handful of values amplifies every rounding
-// difference (tools/gpu_r04n.sh bisection); bf16 keeps the two-launch path.
+// Which storage types take the one-launch kernels: 0 none, 1 fp32, 2 fp32 and
+// bf16 (mde_bn_chan_mode; the environment's MDE_BN_CHAN sets the start value).
+int g_chan_mode = [] {
+  const char* e = std::getenv("MDE_BN_CHAN");
+  return e ? std::atoi(e) : 1;
+}();
+
 template <typename T>
 inline bool chan_mode(int64_t n, int64_t hw) {
-  static const bool on = [] {
-    const char* e = std::getenv("MDE_BN_CHAN");
-    return !(e && e[0] == '0');
-  }();
-  return on && std::is_same_v<T, float> && !plane_mode(hw) &&
-         n * hw <= (hw % 4 == 0 ? kChanMax : kChanMax / 4);
+  const bool on = std::is_same_v<T, float> ? g_chan_mode >= 1 : g_chan_mode >= 2;
+  return on && !plane_mode(hw) && n * hw <= (hw % 4 == 0 ? kChanMax : kChanMax / 4);
 }
 
 // block-wide double sums of (a, b), fixed order; result valid in every thread
@@ -1005,6 +1003,12 @@ bool dtype_ok(int dtype) { return dtype == MDE_F32 || dtype == MDE_BF16; }
 }  // namespace
 
 extern "C" {
+
+int mde_bn_chan_mode(int mode) {
+  const int old = g_chan_mode;
+  if (mode >= 0) g_chan_mode = mode > 2 ? 2 : mode;
+  return old;
+}
 
 size_t mde_batchnorm_workspace(int64_t n, int64_t c, int64_t h, int64_t w) {
   const Geo g = geometry(n, c, h * w);

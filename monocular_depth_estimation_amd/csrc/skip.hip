@@ -694,7 +694,9 @@ __global__ void __launch_bounds__(256)
 }
 
 // gw[pair] = sum over blocks of slab[block][pair]: one block per pair, fixed
-// per-thread order then a fixed tree -> deterministic.
+// per-thread order then a fixed tree -> deterministic.  TAG only tells the
+// two callers apart in profiles (0: skip fusion, 1: pointwise 1x1 backward).
+template <int TAG>
 __global__ void __launch_bounds__(256)
     skip_slab_reduce_kernel(const float* __restrict__ slab, int nblocks,
                             int npairs, int cout, float* __restrict__ gw,
@@ -826,7 +828,7 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
                  dim3(nb), dim3(256), 0, (const B*)gout, (const B*)r, (const B*)d, wt, (B*)gs,
                  slab, n, hw, nullptr, nullptr, nullptr);
     const int stride = (int)(cin * cout + cout);
-    MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+    MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel<0>,
                dim3((unsigned)stride), dim3(256), 0, slab, nb, (int)(cin * cout), (int)cout, gw,
                gb, 0, (float*)nullptr);
     return MDE_OK;
@@ -868,7 +870,7 @@ int mde_skip_reduce_bwd(const void* gout, const void* r, const void* d,
 #undef SKIP_BWD
   const int stride = (int)(cin * cout + cout);
   MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * stride, s,
-             skip_slab_reduce_kernel, dim3((unsigned)stride), dim3(256), 0, slab,
+             skip_slab_reduce_kernel<0>, dim3((unsigned)stride), dim3(256), 0, slab,
              nb, (int)(cin * cout), (int)cout, gw, gb);
   return MDE_OK;
 }
@@ -958,7 +960,7 @@ static int skip_bn_bwd_t(const void* gout, const void* r, const void* d, const f
   const int npairs = (int)(cin * cout);
   const int nextra = sums ? (int)(2 * cin) : 0;
   MDE_LAUNCH(mde::K_SKIP_BWD_REDUCE, 4.0 * (double)nb * (npairs + cout + nextra), s,
-             skip_slab_reduce_kernel, dim3((unsigned)(npairs + cout + nextra)), dim3(256), 0, slab,
+             skip_slab_reduce_kernel<0>, dim3((unsigned)(npairs + cout + nextra)), dim3(256), 0, slab,
              nb, npairs, (int)cout, gw, gb, nextra, in_sums);
   return MDE_OK;
 }
@@ -1159,11 +1161,11 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
   const int npairs = (int)(cin * cout), nextra = sums ? 2 * (int)cin : 0;
   const int stride = npairs + (int)cout + nextra;
   if (sums) {  // every slab column: gw, (the unused bias columns), the BN sums
-    MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+    MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel<1>,
                dim3((unsigned)stride), dim3(256), 0, slab, nb, npairs, (int)cout, gw,
                (float*)nullptr, nextra, in_sums);
   } else {
-    MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel,
+    MDE_LAUNCH(mde::K_PW_BWD, 4.0 * (double)nb * stride, s, skip_slab_reduce_kernel<1>,
                dim3((unsigned)npairs), dim3(256), 0, slab, nb, npairs, (int)cout, gw,
                (float*)nullptr, 0, (float*)nullptr);
   }

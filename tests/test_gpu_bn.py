@@ -195,3 +195,54 @@ def test_batchnorm_bf16_storage_matches_fp32_kernel(shape, act, res):
         one_rounding(grb, grf, "dresidual")
     close_scaled(gwb, gwf, 1e-5, "dgamma")
     close_scaled(rvb, rvf, 1e-5, "running_var")
+
+
+@pytest.mark.parametrize("shape", [(32, 64, 15, 20), (32, 128, 8, 10), (2, 512, 1, 1), (2, 128, 2, 3),
+                                   (8, 256, 4, 5), (32, 256, 1, 1)])
+@pytest.mark.parametrize("act,res", [("relu", True), ("none", False)])
+def test_batchnorm_bf16_one_launch_matches_two_launch(shape, act, res):
+    """The one-launch small-tensor kernels (bn_fwd_chan / bn_bwd_chan) on bf16
+    storage vs the statistics + apply launches on the SAME bf16 tensors
+    (DDRNet's 15x20 .. 1x1 planes at cfg3): the same algorithm with another
+    summation order, so every bf16 output within one bf16 rounding of the
+    other path's, the fp32 statistics, running statistics and parameter
+    gradients within 1e-5 (verdict r4 #6: the golden test's loss moved when
+    bf16 took these kernels; this pins what each BN computes)."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import BatchNorm2d
+    n, c, h, w = shape
+    xb = torch.from_numpy(seeded(shape, 51, -2, 3)).to(DEV).bfloat16()
+    rb = torch.from_numpy(seeded(shape, 52, -1, 1)).to(DEV).bfloat16() if res else None
+    gb = torch.from_numpy(seeded(shape, 53, -1, 1)).to(DEV).bfloat16()
+    outs = []
+    old = _abi.query("mde_bn_chan_mode", -1)
+    try:
+        for mode in (2, 1):
+            _abi.query("mde_bn_chan_mode", mode)
+            bn = BatchNorm2d(c, act=act).to(DEV).train()
+            with torch.no_grad():
+                bn.weight.copy_(torch.from_numpy(seeded((c,), 54, 0.5, 1.5)))
+                bn.bias.copy_(torch.from_numpy(seeded((c,), 55, -0.5, 0.5)))
+            x = xb.detach().clone().requires_grad_(True)
+            r = rb.detach().clone().requires_grad_(True) if res else None
+            y = bn(x, residual=r)
+            y.backward(gb)
+            torch.cuda.synchronize()
+            outs.append((y.detach(), x.grad, r.grad if res else None, bn.weight.grad,
+                         bn.bias.grad, bn.running_mean, bn.running_var))
+    finally:
+        _abi.query("mde_bn_chan_mode", old)
+    (y1, gx1, gr1, gw1, gb1, rm1, rv1), (y2, gx2, gr2, gw2, gb2, rm2, rv2) = outs
+
+    def one_rounding(a, b, what):
+        a, b = a.double(), b.double()
+        bound = 2.0 ** -8 * b.abs() + 1e-6 * float(b.abs().max())
+        assert bool(((a - b).abs() <= bound).all()), f"{what}: {float(((a - b).abs() - bound).max()):.3g} over"
+    one_rounding(y1, y2, "y")
+    one_rounding(gx1, gx2, "dx")
+    if res:
+        one_rounding(gr1, gr2, "dresidual")
+    close_scaled(gw1, gw2, 1e-5, "dgamma")
+    close_scaled(gb1, gb2, 1e-5, "dbeta")
+    close_scaled(rm1, rm2, 1e-5, "running_mean")
+    close_scaled(rv1, rv2, 1e-5, "running_var")

@@ -29,12 +29,15 @@ NAMES = [
     (r"bilinear_bwd\w*_kernel", "bilinear_bwd"),
     (r"nearest_(fwd|pyramid)_kernel", "nearest_fwd"),
     (r"nearest_bwd_kernel", "nearest_bwd"),
-    (r"se_partial_kernel<false>", "se_squeeze"),
-    (r"se_partial_kernel<true>", "se_bwd_dot"),
+    # se_partial_kernel<mode, T>: 0 squeeze, 1 backward dot, 2 squeeze over BN + ReLU
+    (r"se_partial_kernel<[02],", "se_squeeze"),
+    (r"se_partial_kernel<1,", "se_bwd_dot"),
     (r"se_fc[12]_kernel", "se_fc"),
     (r"se_scale_kernel", "se_scale"),
     (r"se_(bfc[123]w?|bfc_all|wgrad)_kernel|sebn_bwd_combine_kernel", "se_bwd_fc"),
-    (r"se_apply_kernel", "se_bwd_apply"),
+    (r"se_apply_kernel|sebn_bwd_apply_kernel", "se_bwd_apply"),
+    # the SE-over-BN backward's reduction pass runs under the SE dot id (se.hip)
+    (r"sebn_bwd_reduce_kernel", "se_bwd_dot"),
     (r"skip_fwd_mfma_kernel<\d+, \d+, true", "skip_reduce_fwd"),
     (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, true", "skip_reduce_bwd"),
@@ -55,7 +58,8 @@ NAMES = [
     (r"wgrad_reduce\w*_kernel", "conv3x3_wreduce"),
     (r"skip_fwd_kernel", "skip_reduce_fwd"),
     (r"skip_bwd_kernel", "skip_reduce_bwd"),
-    (r"skip_slab_reduce_kernel", "skip_reduce_bwd_reduce"),
+    (r"skip_slab_reduce_kernel<0>", "skip_reduce_bwd_reduce"),
+    (r"skip_slab_reduce_kernel<1>", "pointwise_bwd"),
     (r"minmax_partial_kernel", "minmax"),
     (r"minmax_final_kernel", "minmax_final"),
     (r"depthnorm_kernel", "depthnorm_apply"),
@@ -74,7 +78,9 @@ NAMES = [
     (r"wino_weight2?_kernel", "wino_weight"),
     (r"bn_fwd_chan_kernel", "bn_fwd_apply_small"),
     (r"bn_bwd_chan_kernel", "bn_bwd_apply_small"),
-    (r"dloss_(fwd_stream|masked|map|final)_kernel", "depth_loss_fwd"),
+    (r"dloss_final_kernel", "loss_final"),
+    (r"dloss_map_kernel<1>", "depth_loss_bwd_coef"),
+    (r"dloss_(fwd_stream|masked|map)_kernel", "depth_loss_fwd"),
     (r"dloss_(bwd_stream|masked_bwd|grad)_kernel", "depth_loss_bwd"),
     (r"loss_final_kernel", "loss_final"),
     (r"bn_stats_kernel", "bn_fwd_stats"),
@@ -84,7 +90,7 @@ NAMES = [
     (r"bn_bwd_reduce_kernel", "bn_bwd_reduce"),
     (r"bn_bwd_apply_plane_kernel", "bn_bwd_apply"),
     (r"bn_bwd_apply_table_kernel", "bn_bwd_apply_small"),
-    (r"skip_bwd_reg_kernel", "skip_reduce_bwd"),
+    (r"skip_bwd_(reg|c1)_kernel", "skip_reduce_bwd"),
     (r"wattn_fwd_kernel", "window_attn_fwd"),
     (r"wattn_bwd_kernel", "window_attn_bwd"),
     (r"wattn_slab_reduce_kernel", "window_attn_bwd_reduce"),
@@ -97,6 +103,18 @@ NAMES = [
     (r"ln_bwd_kernel", "layernorm_bwd"),
     (r"ln_wreduce_kernel", "layernorm_wreduce"),
     (r"transpose_kernel", "transpose"),
+    (r"colsum_part_kernel<true>", "gelu_bwd_bias_grad"),
+    (r"colsum_(part_kernel<false>|final_kernel)", "linear_bias_grad"),
+    # forward and data gradient run the same kernel (as wino_f23_kernel)
+    (r"convbf_fwd_kernel", "convbf_fwd_bf16+convbf_dgrad_bf16"),
+    (r"convbf_wgrad_kernel", "convbf_wgrad_bf16"),
+    (r"convbf_wreduce_kernel", "convbf_wreduce"),
+    (r"convbf_pack_kernel", "convbf_pack"),
+    (r"eval_partial_kernel", "eval_sums"),
+    (r"eval_final_kernel", "eval_final"),
+    (r"nyu_augment_kernel", "nyu_augment"),
+    # builds before round 5 (one untagged slab reduction for both callers)
+    (r"skip_slab_reduce_kernel\(", "skip_reduce_bwd_reduce"),
 ]
 
 

@@ -22,9 +22,13 @@ def timeit(fn, reps=20):
 
 
 tag = os.environ.get("MDE_WIDE_WPB", "8") + ("" if os.environ.get("MDE_C32_WIDE", "1") != "0" else " c32 off")
-for (n, c, co, h, w) in [(32, 64, 64, 60, 80), (32, 128, 128, 30, 40), (32, 256, 256, 15, 20),
-                         (32, 128, 64, 60, 80), (32, 64, 64, 120, 160), (4, 64, 64, 30, 40),
-                         (32, 32, 32, 120, 160), (32, 32, 32, 240, 320)]:
+SHAPES = [(32, 64, 64, 60, 80), (32, 128, 128, 30, 40), (32, 256, 256, 15, 20),
+          (32, 128, 64, 60, 80), (32, 64, 64, 120, 160), (4, 64, 64, 30, 40),
+          (32, 32, 32, 120, 160), (32, 32, 32, 240, 320)]
+if "--newcrf" in sys.argv:  # cfg4's NewCRF proj_v / proj_x convs (bs 16, newcrf_layers.py:377-379)
+    SHAPES = [(16, 64, 128, 120, 160), (16, 128, 256, 60, 80), (16, 256, 512, 30, 40),
+              (16, 512, 1024, 15, 20), (16, 160, 1024, 15, 20)]
+for (n, c, co, h, w) in SHAPES:
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
     gy = torch.rand((n, co, h, w), device="cuda") - 0.5
     wt = torch.rand((co, c, 3, 3), device="cuda")
@@ -44,7 +48,7 @@ for (n, c, co, h, w) in [(32, 64, 64, 60, 80), (32, 128, 128, 30, 40), (32, 256,
           f"MIOpen {tm:7.1f} us ({fl / tm / 1e6:5.1f} TF/s)  rel diff {err:.1e}", flush=True)
 
 # stride-2 stem convolutions (mde_conv3x3s2_wgrad) vs MIOpen (incl. its NHWC transposes)
-for (n, c, co, h, w) in [(32, 3, 32, 480, 640), (32, 32, 32, 240, 320)]:
+for (n, c, co, h, w) in ([] if "--newcrf" in sys.argv else [(32, 3, 32, 480, 640), (32, 32, 32, 240, 320)]):
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     gy = torch.rand((n, co, ho, wo), device="cuda") - 0.5

@@ -174,87 +174,133 @@ __device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {  // (a.hi, 
   return __builtin_amdgcn_perm(b, a, 0x07060302u);
 }
 
-// Stage 32 channels (ci0 ..) of the patch's source image into LDS, pixel pitch
-// PITCH bf16, [pixel][channel].  Unit = (channel octet, staged row, pair of
-// staged columns): 8 dword loads (8 channels x 2 source pixels), clamped
-// addresses + selects (no branches around loads), two 16-byte LDS writes.
-template <int KS, int MODE, int PITCH, int NT>
-__device__ __forceinline__ void stage_src(bf16* img, const bf16* __restrict__ src, const Geo& g,
-                                          const Img& I, int ci0, int tid) {
-  const int64_t plane = (int64_t)g.hi * g.wi;
-  if constexpr (MODE == U2) {
-    // Z[zr][zc] = gy[zr / 2][zc / 2] for even zr, zc, else 0; unit = (octet,
-    // row, even Z column): 8 channel loads of one gy element, two staged
-    // pixels (the odd one zero)
-    const int npair = I.cs >> 1, per = I.rs * npair, total = 4 * per;
-    for (int u = tid; u < total; u += NT) {
-      const int o = u / per, rem = u - o * per, i = rem / npair, jp = rem - i * npair;
-      const int zr = I.gr0 + i, zc = I.gc0 + 2 * jp;
-      const int sr = zr >> 1, sc = zc >> 1;
-      const bool ok = (zr & 1) == 0 && zr >= 0 && sr < g.hi && zc >= 0 && sc < g.wi &&
-                      ci0 + 8 * o < g.cin;
-      const bf16* p = src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0);
-      uint32_t v[8];
+// Staging of 32 channels (ci0 ..) of a patch's source image into LDS as
+// [pixel][channel] at pixel pitch PITCH (bf16).  Unit = (channel octet,
+// staged row, staged column pair): 8 loads (8 channels x 2 source pixels as
+// dwords; U2: 8 channels x 1 gy element), packed into two 16-byte pixels.
+// load() issues EVERY unit's loads of the thread (clamped addresses, selects:
+// no branches around loads, nothing waited on), store() packs and writes them:
+// the kernels call load() for the next chunk / patch before the current one's
+// MFMAs, so the load latency hides behind the matrix work.  MAXU >= the units
+// a thread can own (host: pick_geo caps the staged pixels at the LDS image).
+template <int KS, int MODE, int PITCH, int NT, int MAXU>
+struct SrcStage {
+  uint32_t v[MAXU][8];
+  int d0[MAXU];  // first staged pixel of the unit, -1: no unit
+
+  __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
+                                       int ci0, int tid) {
+    const int64_t plane = (int64_t)g.hi * g.wi, pl2 = plane >> 1;
+    // units per octet: U2 / S1 / 1x1 S1: staged column pairs; 3x3 S2: source
+    // pairs (E and O halves); 1x1 S2: staged pixels
+    const int ncol = (KS == 1 && MODE == S2) ? I.cs : ((KS == 3 && MODE == S2) ? I.csh : I.cs >> 1);
+    const int per = I.rs * ncol, total = 4 * per;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = p[ok ? j * plane : 0];
-      u4v a;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) a[j] = ok ? (v[2 * j] | (v[2 * j + 1] << 16)) : 0u;
-      bf16* d = img + (i * I.cs + 2 * jp) * PITCH + 8 * o;
-      *reinterpret_cast<u4v*>(d) = a;
-      *reinterpret_cast<u4v*>(d + PITCH) = u4v{0u, 0u, 0u, 0u};
-    }
-  } else if constexpr (KS == 1 && MODE == S2) {
-    // staged (i, j) = source (2 (gr0 + i), 2 (gc0 + j)): the even element of each pair
-    const int per = I.rs * I.cs, total = 4 * per;
-    for (int u = tid; u < total; u += NT) {
-      const int o = u / per, rem = u - o * per, i = rem / I.cs, j = rem - i * I.cs;
-      const int sr = 2 * (I.gr0 + i), sc = 2 * (I.gc0 + j);
-      const bool ok = sr < g.hi && sc < g.wi && ci0 + 8 * o < g.cin;
-      const uint32_t* p = reinterpret_cast<const uint32_t*>(
-          src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0));
-      const int64_t pl2 = plane >> 1;
-      uint32_t v[8];
-#pragma unroll
-      for (int j2 = 0; j2 < 8; ++j2) v[j2] = p[ok ? j2 * pl2 : 0];
-      u4v a;
-#pragma unroll
-      for (int j2 = 0; j2 < 4; ++j2) a[j2] = ok ? lo16x2(v[2 * j2], v[2 * j2 + 1]) : 0u;
-      *reinterpret_cast<u4v*>(img + (i * I.cs + j) * PITCH + 8 * o) = a;
-    }
-  } else {
-    // S1 (3x3 / 1x1) and 3x3 S2: source column pairs (gc, gc + 1), gc even
-    const int npair = (KS == 3 && MODE == S2) ? I.csh : (I.cs >> 1);
-    const int per = I.rs * npair, total = 4 * per;
-    const int64_t pl2 = plane >> 1;
-    for (int u = tid; u < total; u += NT) {
-      const int o = u / per, rem = u - o * per, i = rem / npair, jp = rem - i * npair;
-      const int sr = I.gr0 + i, sc = I.gc0 + 2 * jp;
-      const bool ok = sr >= 0 && sr < g.hi && sc >= 0 && sc < g.wi && ci0 + 8 * o < g.cin;
-      const uint32_t* p = reinterpret_cast<const uint32_t*>(
-          src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0));
-      uint32_t v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = p[ok ? j * pl2 : 0];
-      u4v e, od;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        e[j] = ok ? lo16x2(v[2 * j], v[2 * j + 1]) : 0u;
-        od[j] = ok ? hi16x2(v[2 * j], v[2 * j + 1]) : 0u;
-      }
-      int d0, d1;
-      if constexpr (KS == 3 && MODE == S2) {
-        d0 = i * I.cs + jp;
-        d1 = d0 + I.csh;
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = tid + NT * k;
+      const int uc = u < total ? u : 0;
+      const int o = uc / per, rem = uc - o * per, i = rem / ncol, jc = rem - i * ncol;
+      int sr, sc;
+      bool ok;
+      if constexpr (MODE == U2) {
+        // Z[zr][zc] = gy[zr / 2][zc / 2] for even zr, zc, else 0
+        const int zr = I.gr0 + i, zc = I.gc0 + 2 * jc;
+        sr = zr >> 1;
+        sc = zc >> 1;
+        ok = (zr & 1) == 0 && zr >= 0 && sr < g.hi && zc >= 0 && sc < g.wi;
+        d0[k] = u < total ? i * I.cs + 2 * jc : -1;
+      } else if constexpr (KS == 1 && MODE == S2) {
+        sr = 2 * (I.gr0 + i);
+        sc = 2 * (I.gc0 + jc);
+        ok = sr < g.hi && sc < g.wi;
+        d0[k] = u < total ? i * I.cs + jc : -1;
       } else {
-        d0 = i * I.cs + 2 * jp;
-        d1 = d0 + 1;
+        sr = I.gr0 + i;
+        sc = I.gc0 + 2 * jc;
+        ok = sr >= 0 && sr < g.hi && sc >= 0 && sc < g.wi;
+        d0[k] = u < total ? i * I.cs + ((KS == 3 && MODE == S2) ? jc : 2 * jc) : -1;
       }
-      *reinterpret_cast<u4v*>(img + d0 * PITCH + 8 * o) = e;
-      *reinterpret_cast<u4v*>(img + d1 * PITCH + 8 * o) = od;
+      ok = ok && u < total && ci0 + 8 * o < g.cin;
+      if constexpr (MODE == U2) {
+        const bf16* p = src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] = ok ? (uint32_t)p[ok ? j * plane : 0] : 0u;
+      } else {
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(
+            src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0));
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t t = p[ok ? j * pl2 : 0];
+          v[k][j] = ok ? t : 0u;
+        }
+      }
+      if (u < total) d0[k] = d0[k] * PITCH + 8 * o;  // element offset incl. the octet
     }
   }
+
+  __device__ __forceinline__ void store(bf16* img, const Img& I) const {
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      if (d0[k] < 0) continue;
+      bf16* d = img + d0[k];
+      if constexpr (MODE == U2) {
+        u4v a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = v[k][2 * j] | (v[k][2 * j + 1] << 16);
+        *reinterpret_cast<u4v*>(d) = a;
+        *reinterpret_cast<u4v*>(d + PITCH) = u4v{0u, 0u, 0u, 0u};
+      } else if constexpr (KS == 1 && MODE == S2) {
+        u4v a;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = lo16x2(v[k][2 * j], v[k][2 * j + 1]);
+        *reinterpret_cast<u4v*>(d) = a;
+      } else {
+        u4v e, od;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          e[j] = lo16x2(v[k][2 * j], v[k][2 * j + 1]);
+          od[j] = hi16x2(v[k][2 * j], v[k][2 * j + 1]);
+        }
+        *reinterpret_cast<u4v*>(d) = e;
+        *reinterpret_cast<u4v*>(d + ((KS == 3 && MODE == S2) ? I.csh : 1) * PITCH) = od;
+      }
+    }
+  }
+};
+
+// units a thread can own for a staged image of CAP pixels
+template <int KS, int MODE, int CAP, int NT>
+constexpr int src_units() {
+  // U2 / S1: CAP / 2 column pairs; 3x3 S2: CAP / 2 source pairs; 1x1 S2: CAP pixels
+  return (4 * ((KS == 1 && MODE == S2) ? CAP : CAP / 2) + NT - 1) / NT;
 }
+
+// The filter chunk [tap][NB][32] (16-byte pieces swizzled by (row >> 2) & 3),
+// register-staged like SrcStage.
+template <int KK, int NB, int NT>
+struct WStage {
+  static constexpr int U = (KK * NB * 4 + NT - 1) / NT;
+  u4v v[U];
+  __device__ __forceinline__ void load(const bf16* __restrict__ src, int cout, int co0, int tid) {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int u = tid + NT * k;
+      const int uc = u < KK * NB * 4 ? u : 0;
+      const int o = uc & 3, rest = uc >> 2, cl = rest % NB, t = rest / NB;
+      v[k] = *reinterpret_cast<const u4v*>(src + ((int64_t)t * cout + co0 + cl) * 32 + 8 * o);
+    }
+  }
+  __device__ __forceinline__ void store(bf16* sw, int tid) const {
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int u = tid + NT * k;
+      if (u < KK * NB * 4) {
+        const int o = u & 3, rest = u >> 2, cl = rest % NB, t = rest / NB;
+        *reinterpret_cast<u4v*>(sw + (t * NB + cl) * 32 + 8 * (o ^ ((cl >> 2) & 3))) = v[k];
+      }
+    }
+  }
+};
 
 // ------------------------------------------------------------------ forward
 // Block: 4 waves; wave (wm, wn): output channels 32 wn .. of the block's
@@ -277,6 +323,7 @@ __global__ void __launch_bounds__(256, 2)
 
   int abase[MTW];
   bool mt_on[MTW];
+  int dymask[MTW];  // filter rows a tile needs (U2: all-zero staged rows skipped)
 #pragma unroll
   for (int i = 0; i < MTW; ++i) {
     const int mt = MTW * wm + i;
@@ -284,6 +331,15 @@ __global__ void __launch_bounds__(256, 2)
     int r, c;
     const bool ok = pix_of(g, P, mt * 32 + l32, r, c);
     abase[i] = ok ? img_base<KS, MODE>(P, I, r, c) : 0;
+    dymask[i] = 7;
+    if constexpr (MODE == U2 && KS == 3) {
+      // a tile inside one output row r reads Z rows r - 1 + dy, zero unless
+      // r + dy is odd: dy = 1 for even r, dy = 0, 2 for odd r (wave-uniform)
+      int r0, c0, r1, c1;
+      const bool a = pix_of(g, P, mt * 32, r0, c0);
+      const bool b = pix_of(g, P, mt * 32 + 31, r1, c1);
+      if (a && b && r0 == r1) dymask[i] = (r0 & 1) ? 5 : 2;
+    }
   }
   int toff[KK];
 #pragma unroll
@@ -300,18 +356,19 @@ __global__ void __launch_bounds__(256, 2)
 
   const bf16* xs = x + (int64_t)P.img * g.cin * g.hi * g.wi;
   const int nchunk = (g.cin + 31) >> 5;
+  SrcStage<KS, MODE, kPitchF, 256, src_units<KS, MODE, CAP, 256>()> S;
+  WStage<KK, NB, 256> Wt;
+  S.load(xs, g, I, 0, tid);
+  Wt.load(wp, g.cout, co0, tid);
   for (int cc = 0; cc < nchunk; ++cc) {
     __syncthreads();
-    stage_src<KS, MODE, kPitchF, 256>(simg, xs, g, I, 32 * cc, tid);
-    {  // filter chunk: [tap][NB][32], 16-byte pieces swizzled by (row >> 2) & 3
-      const bf16* src = wp + (int64_t)cc * KK * g.cout * 32;
-      for (int u = tid; u < KK * NB * 4; u += 256) {
-        const int o = u & 3, rest = u >> 2, cl = rest % NB, t = rest / NB;
-        const u4v v = *reinterpret_cast<const u4v*>(src + ((int64_t)t * g.cout + co0 + cl) * 32 + 8 * o);
-        *reinterpret_cast<u4v*>(sw + (t * NB + cl) * 32 + 8 * (o ^ ((cl >> 2) & 3))) = v;
-      }
-    }
+    S.store(simg, I);
+    Wt.store(sw, tid);
     __syncthreads();
+    if (cc + 1 < nchunk) {  // the next chunk's loads, in flight during this chunk's MFMAs
+      S.load(xs, g, I, 32 * (cc + 1), tid);
+      Wt.load(wp + (int64_t)(cc + 1) * KK * g.cout * 32, g.cout, co0, tid);
+    }
 #pragma unroll
     for (int t = 0; t < KK; ++t) {
 #pragma unroll
@@ -319,7 +376,7 @@ __global__ void __launch_bounds__(256, 2)
         const u4v b = *reinterpret_cast<const u4v*>(sw + t * NB * 32 + (ks ? boff1 : boff0));
 #pragma unroll
         for (int i = 0; i < MTW; ++i) {
-          if (mt_on[i]) {  // wave-uniform
+          if (mt_on[i] && ((dymask[i] >> (t / KS)) & 1)) {  // wave-uniform
             const u4v a = *reinterpret_cast<const u4v*>(simg + abase[i] * kPitchF + toff[t] +
                                                        16 * ks + 8 * h);
             acc[i] = mfma32(a, b, acc[i]);
@@ -423,21 +480,38 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
   const int arow = (wc * 32 + l32) * kGP + 8 * h;
   const int64_t hwo = (int64_t)g.ho * g.wo;
 
+  // gy rows: [64 channels][128 pixels], 4 pixels a unit (8-byte loads)
+  constexpr int GU = (64 * (kMBW / 4) + NT - 1) / NT;
+  u2v gv[GU];
+  auto gy_load = [&](const Patch& P) {
+    const bf16* gsrc = gy + ((int64_t)P.img * g.cout + cob * 64) * hwo;
+#pragma unroll
+    for (int k = 0; k < GU; ++k) {
+      const int u = tid + NT * k;
+      const int cl = u / (kMBW / 4), m4 = 4 * (u - cl * (kMBW / 4));
+      int r, c;
+      const bool ok = u < 64 * (kMBW / 4) && pix_of(g, P, m4, r, c) && cl < co_live;
+      const u2v v = *reinterpret_cast<const u2v*>(gsrc + (ok ? (int64_t)cl * hwo + (int64_t)r * g.wo + c : 0));
+      gv[k] = ok ? v : u2v{0u, 0u};
+    }
+  };
+  SrcStage<KS, MODE, kPitchW, NT, src_units<KS, MODE, CAP, NT>()> S;
+  if (q0 < q1) {
+    const Patch P = patch_of(g, q0);
+    S.load(x + (int64_t)P.img * g.cin * g.hi * g.wi, g, img_of<KS, MODE>(P), 32 * cc, tid);
+    gy_load(P);
+  }
   for (int q = q0; q < q1; ++q) {
     const Patch P = patch_of(g, q);
     const Img I = img_of<KS, MODE>(P);
     __syncthreads();
-    stage_src<KS, MODE, kPitchW, NT>(simg, x + (int64_t)P.img * g.cin * g.hi * g.wi, g, I,
-                                     32 * cc, tid);
-    {  // gy rows: [64 channels][128 pixels], 4 pixels a unit (8-byte loads)
-      const bf16* gsrc = gy + ((int64_t)P.img * g.cout + cob * 64) * hwo;
-      for (int u = tid; u < 64 * (kMBW / 4); u += NT) {
+    S.store(simg, I);
+#pragma unroll
+    for (int k = 0; k < GU; ++k) {
+      const int u = tid + NT * k;
+      if (u < 64 * (kMBW / 4)) {
         const int cl = u / (kMBW / 4), m4 = 4 * (u - cl * (kMBW / 4));
-        int r, c;
-        const bool ok = pix_of(g, P, m4, r, c) && cl < co_live;
-        const u2v v = *reinterpret_cast<const u2v*>(gsrc + (int64_t)cl * hwo +
-                                                     (ok ? (int64_t)r * g.wo + c : 0));
-        *reinterpret_cast<u2v*>(sg + cl * kGP + m4) = ok ? v : u2v{0u, 0u};
+        *reinterpret_cast<u2v*>(sg + cl * kGP + m4) = gv[k];
       }
     }
     for (int m = tid; m < kMBW; m += NT) {
@@ -446,6 +520,11 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
       tab[m] = ok ? img_base<KS, MODE>(P, I, r, c) : 0;
     }
     __syncthreads();
+    if (q + 1 < q1) {  // the next patch's loads, in flight during this patch's MFMAs
+      const Patch Pn = patch_of(g, q + 1);
+      S.load(x + (int64_t)Pn.img * g.cin * g.hi * g.wi, g, img_of<KS, MODE>(Pn), 32 * cc, tid);
+      gy_load(Pn);
+    }
     int toff[ND];
 #pragma unroll
     for (int d = 0; d < ND; ++d) toff[d] = KS == 3 ? tap_off<KS, MODE>(I, wy, d) : 0;

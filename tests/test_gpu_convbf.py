@@ -39,7 +39,8 @@ SHAPES = [
     (32, 64, 120, 160, 1, 2),   # layer2 downsample
     (256, 512, 15, 20, 1, 2),   # layer5 downsample (odd input height)
     (64, 32, 18, 24, 3, 1),     # 32 output channels, small plane
-    (96, 64, 22, 36, 3, 2),     # 3 input-channel chunks, ragged 2D tiles
+    (96, 64, 26, 160, 3, 2),    # 3 input-channel chunks, 2D tiles with a ragged last band
+    (96, 64, 22, 40, 3, 2),     # 3 input-channel chunks, 11 x 20 output plane
 ]
 
 
@@ -127,3 +128,11 @@ def test_convbf_biased_conv_adds_bias_in_bf16():
     ref = gy.double().sum((0, 2, 3))
     err = float((conv.bias.grad.double() - ref).abs().max() / ref.abs().max())
     assert err <= 1e-2, err
+
+
+def test_convbf_refuses_unaligned_planes():
+    """Output planes whose pixel count breaks the 4-pixel store groups (and
+    whose width is not a multiple of 4) are not taken: MIOpen runs them."""
+    from monocular_depth_estimation_amd import _abi
+    assert _abi.query("mde_convbf_supported", 96, 64, 22, 36, 3, 2, 0) == 0  # 11 x 18 output
+    assert _abi.query("mde_convbf_supported", 96, 64, 22, 40, 3, 2, 0) == 1

@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(256)
 // their channel's squeeze-mean gradients dm[:, ch] = W1[:, ch] . dh[n, :]
 // (wave per sample, the se_bfc3 summation order) into LDS and dm; blocks
 // [c, c + wg) run the FC weight / bias gradients.
-constexpr int kMaxSeN = 256;  // samples the combine blocks hold dm for in LDS
+constexpr int kMaxSeN = 256;  // samples the combine blocks hold dm for in LDS at once
 
 __global__ void __launch_bounds__(256)
     sebn_bwd_combine_kernel(const float* __restrict__ part4, int chunks, int64_t n, int64_t c,
@@ -419,27 +419,33 @@ __global__ void __launch_bounds__(256)
     return;
   }
   const int64_t ch = blockIdx.x;
-  {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int64_t nn = wid; nn < n; nn += 4) {
-      float acc = 0.f;
-      for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * dh[nn * cr + j];
-      acc = mde::wave_sum(acc);
-      if (lane == 0) {
-        dms[nn] = acc;
-        dm[nn * c + ch] = acc;
-      }
-    }
-  }
-  __syncthreads();
   const double inv_hw = 1.0 / (double)hw;
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t i = threadIdx.x; i < n * chunks; i += 256) {
-    const int64_t plane = (i / chunks) * c + ch;
-    const float* p = part4 + 4 * (plane * chunks + i % chunks);
-    const double sv = s[plane], q = (double)dms[i / chunks] * inv_hw;
-    s1 += sv * (double)p[0] + q * (double)p[1];
-    s2 += sv * (double)p[2] + q * (double)p[3];
+  // samples in groups of kMaxSeN (one group, the whole batch, up to 256)
+  for (int64_t n0 = 0; n0 < n; n0 += kMaxSeN) {
+    const int64_t nb = n - n0 < kMaxSeN ? n - n0 : kMaxSeN;
+    if (n0 > 0) __syncthreads();  // the previous group's dms readers are done
+    {
+      const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+      for (int64_t k = wid; k < nb; k += 4) {
+        const int64_t nn = n0 + k;
+        float acc = 0.f;
+        for (int j = lane; j < cr; j += 64) acc += w1[(int64_t)j * c + ch] * dh[nn * cr + j];
+        acc = mde::wave_sum(acc);
+        if (lane == 0) {
+          dms[k] = acc;
+          dm[nn * c + ch] = acc;
+        }
+      }
+    }
+    __syncthreads();
+    for (int64_t i = threadIdx.x; i < nb * chunks; i += 256) {
+      const int64_t plane = (n0 + i / chunks) * c + ch;
+      const float* p = part4 + 4 * (plane * chunks + i % chunks);
+      const double sv = s[plane], q = (double)dms[i / chunks] * inv_hw;
+      s1 += sv * (double)p[0] + q * (double)p[1];
+      s2 += sv * (double)p[2] + q * (double)p[3];
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -720,7 +726,6 @@ static int se_bn_bwd_t(const void* gout, const void* ya, int64_t ca, const void*
   MDE_LAUNCH(mde::K_SE_BWD_DOT, 2.0 * big, st, sebn_bwd_reduce_kernel<T>,
              dim3(chunks, (unsigned)(n * c)), dim3(256), 0, (const T*)gout, (const T*)ya, ca,
              (const T*)yb, cb, hw, chunks, scale, shift, bn_mean, ws.part, ws.part4);
-  if (n > kMaxSeN) return MDE_ERR_INVALID_ARG;
   const int fcs = se_bfc(ws, chunks, n, c, cr, w1, w2, nullptr, 0, s, hidden, mean, gw1, gw2,
                          nullptr, nullptr, st, true);
   if (fcs) return fcs;

@@ -57,7 +57,10 @@ def _ref(ya, yb, bn_a, bn_b, pa, pb, w1, w2):
 
 @pytest.mark.parametrize("n,ca,cb,h,w,offset", [(2, 8, 8, 48, 64, 0.0), (3, 16, 16, 13, 18, 0.0),
                                                 (2, 32, 32, 30, 40, 0.0), (4, 4, 12, 1, 1, 0.0),
-                                                (2, 16, 16, 24, 32, 50.0)])
+                                                (2, 16, 16, 24, 32, 50.0),
+                                                # > 256 samples: the combine kernel's dm
+                                                # groups (was an error at n > 256)
+                                                (300, 8, 8, 3, 4, 0.0)])
 def test_se_bn_cat_vs_float64(n, ca, cb, h, w, offset):
     from monocular_depth_estimation_amd.nn import se_bn_cat
     torch.manual_seed(n * 100 + ca + h)

@@ -303,14 +303,16 @@ struct WStage {
 };
 
 // ------------------------------------------------------------------ forward
-// Block: 4 waves; wave (wm, wn): output channels 32 wn .. of the block's
+// Block: NW waves; wave (wm, wn): output channels 32 wn .. of the block's
 // 32 WN, M tiles MTW wm .. MTW wm + MTW - 1 (32 pixels each) of the patch
-// (32 MTW 4 / WN pixels).
-template <int KS, int MODE, int WN, int MTW, bool STATS, int CAP>
-__global__ void __launch_bounds__(256, 2)
+// (32 MTW NW / WN pixels).  8-wave blocks stage the filter chunk once per 256
+// pixels (the 4-wave ones per 128: the filter is most of what a 64-channel
+// block loads).
+template <int KS, int MODE, int WN, int MTW, int NW, bool STATS, int CAP>
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
     convbf_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                       bf16* __restrict__ y, float* __restrict__ stats, Geo g) {
-  constexpr int KK = KS * KS, NB = 32 * WN, WMW = 4 / WN;
+  constexpr int KK = KS * KS, NB = 32 * WN, WMW = NW / WN, NT = 64 * NW;
   __shared__ __attribute__((aligned(16))) bf16 simg[CAP * kPitchF];
   __shared__ __attribute__((aligned(16))) bf16 sw[KK * NB * 32];
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
@@ -356,8 +358,8 @@ __global__ void __launch_bounds__(256, 2)
 
   const bf16* xs = x + (int64_t)P.img * g.cin * g.hi * g.wi;
   const int nchunk = (g.cin + 31) >> 5;
-  SrcStage<KS, MODE, kPitchF, 256, src_units<KS, MODE, CAP, 256>()> S;
-  WStage<KK, NB, 256> Wt;
+  SrcStage<KS, MODE, kPitchF, NT, src_units<KS, MODE, CAP, NT>()> S;
+  WStage<KK, NB, NT> Wt;
   S.load(xs, g, I, 0, tid);
   Wt.load(wp, g.cout, co0, tid);
   for (int cc = 0; cc < nchunk; ++cc) {
@@ -621,14 +623,19 @@ __global__ void __launch_bounds__(256)
 }
 
 // ------------------------------------------------------------------- host
-constexpr int kCapS1 = 420;  // staged pixels: 33.6 KB (+ 36.9 KB filter): two blocks a CU
-constexpr int kCapS2 = 640;  // stride 2 / zero-inserted: 51 KB (one block a CU)
+constexpr int kCapS1 = 420;   // staged pixels: 33.6 KB (+ 36.9 KB filter): two blocks a CU
+constexpr int kCapS2 = 640;   // stride 2 / zero-inserted: 51 KB (one block a CU)
+constexpr int kCapS1W = 600;  // 8-wave blocks (256 pixels): 48 KB
+constexpr int kCapS2W = 1200; // 8-wave blocks, stride 2 / zero-inserted: 96 KB
 
 struct Pass {
   int ks, mode, cin, cout, hi, wi, ho, wo;
 };
 
-inline int cap_of(const Pass& p) { return (p.ks == 3 && p.mode != S1) ? kCapS2 : kCapS1; }
+inline int cap_of(const Pass& p, bool wide = false) {
+  const bool s2 = p.ks == 3 && p.mode != S1;
+  return wide ? (s2 ? kCapS2W : kCapS1W) : (s2 ? kCapS2 : kCapS1);
+}
 
 // staged pixels of the largest patch of a geometry
 inline int img_px(const Pass& p, int pc, int pr, int mb) {
@@ -649,7 +656,7 @@ inline int img_px(const Pass& p, int pc, int pr, int mb) {
 // Choose the patch geometry: flat runs of mb pixels when the image fits,
 // else 2D tiles (pc columns x pr rows, pr * pc <= mb) with the fewest padded
 // pixels.  False if nothing fits or the shape breaks an alignment rule.
-inline bool pick_geo(const Pass& p, int mb, Geo* g) {
+inline bool pick_geo(const Pass& p, int mb, Geo* g, int cap = 0) {
   g->cin = p.cin;
   g->cout = p.cout;
   g->hi = p.hi;
@@ -657,7 +664,7 @@ inline bool pick_geo(const Pass& p, int mb, Geo* g) {
   g->ho = p.ho;
   g->wo = p.wo;
   g->mb = mb;
-  g->cap = cap_of(p);
+  g->cap = cap ? cap : cap_of(p);
   const int64_t hw = (int64_t)p.ho * p.wo;
   if (hw % 4 == 0 && img_px(p, 0, 0, mb) <= g->cap) {
     g->pc = g->pr = 0;
@@ -706,30 +713,40 @@ inline bool make_pass(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, i
   return true;
 }
 
-template <int KS, int MODE, int WN, int MTW, int CAP>
+template <int KS, int MODE, int WN, int MTW, int NW, int CAP>
 int launch_fwd_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const Geo& g, int64_t n,
                  int kid, double flops, double bytes, hipStream_t s) {
   const int64_t np = n * g.ppi;
   if (np > 0x7fffffff) return MDE_ERR_UNSUPPORTED;
   const dim3 grid((unsigned)np, (unsigned)(g.cout / (32 * WN)));
   if (stats)
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, true, CAP>), grid,
-                    dim3(256), 0, x, wp, y, stats, g);
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, NW, true, CAP>),
+                    grid, dim3(64 * NW), 0, x, wp, y, stats, g);
   else
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, false, CAP>), grid,
-                    dim3(256), 0, x, wp, y, stats, g);
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, NW, false, CAP>),
+                    grid, dim3(64 * NW), 0, x, wp, y, stats, g);
   return MDE_OK;
 }
 
 inline int wn_of(const Pass& p) { return p.cout % 64 == 0 ? 2 : 1; }
 
-// forward geometry: 2 M tiles a wave (128 pixels a block at 64 output
-// channels, 256 at 32), or 1 when that patch's image does not fit
-inline bool fwd_geo(const Pass& p, Geo* g, int* mtw) {
-  const int wmw = 4 / wn_of(p);
+// forward geometry: at 64 output channels 8-wave blocks of 256 pixels when
+// there are enough of them to fill the chip (>= 2 per CU), else 4-wave
+// blocks with 2 M tiles a wave (128 pixels; 256 at 32 channels), or 1 when
+// that patch's image does not fit
+inline bool fwd_geo(const Pass& p, int64_t n, Geo* g, int* mtw, int* nw) {
+  const int wn = wn_of(p);
+  if (wn == 2 && pick_geo(p, 256, g, cap_of(p, true)) &&
+      n * g->ppi * (p.cout / 64) >= 512) {
+    *mtw = 2;
+    *nw = 8;
+    return true;
+  }
+  const int wmw = 4 / wn;
   for (int m = 2; m >= 1; --m) {
     if (pick_geo(p, 32 * m * wmw, g)) {
       *mtw = m;
+      *nw = 4;
       return true;
     }
   }
@@ -740,27 +757,28 @@ int launch_fwd(const Pass& p, const bf16* x, const bf16* wp, bf16* y, float* sta
                int kid, hipStream_t s) {
   const int wn = wn_of(p);
   Geo g;
-  int mtw;
-  if (!fwd_geo(p, &g, &mtw)) return MDE_ERR_UNSUPPORTED;
+  int mtw, nw;
+  if (!fwd_geo(p, n, &g, &mtw, &nw)) return MDE_ERR_UNSUPPORTED;
   const double flops = 2.0 * n * p.ho * p.wo * (double)p.cout * p.cin * p.ks * p.ks;
   const double bytes = 2.0 * n * ((double)p.cin * p.hi * p.wi + (double)p.cout * p.ho * p.wo);
-#define CBF_FWD(KS, MODE, CAP)                                                                   \
-  return wn == 2 ? (mtw == 2 ? launch_fwd_t<KS, MODE, 2, 2, CAP>(x, wp, y, stats, g, n, kid, flops, \
-                                                                bytes, s)                        \
-                             : launch_fwd_t<KS, MODE, 2, 1, CAP>(x, wp, y, stats, g, n, kid, flops, \
-                                                                bytes, s))                       \
-                 : (mtw == 2 ? launch_fwd_t<KS, MODE, 1, 2, CAP>(x, wp, y, stats, g, n, kid, flops, \
-                                                                bytes, s)                        \
-                             : launch_fwd_t<KS, MODE, 1, 1, CAP>(x, wp, y, stats, g, n, kid, flops, \
-                                                                bytes, s))
+#define CBF_FWD(KS, MODE, CAP, CAPW)                                                         \
+  if (nw == 8)                                                                             \
+    return launch_fwd_t<KS, MODE, 2, 2, 8, CAPW>(x, wp, y, stats, g, n, kid, flops, bytes, s); \
+  if (wn == 2)                                                                             \
+    return mtw == 2                                                                        \
+               ? launch_fwd_t<KS, MODE, 2, 2, 4, CAP>(x, wp, y, stats, g, n, kid, flops, bytes, s) \
+               : launch_fwd_t<KS, MODE, 2, 1, 4, CAP>(x, wp, y, stats, g, n, kid, flops, bytes, s); \
+  return mtw == 2                                                                          \
+             ? launch_fwd_t<KS, MODE, 1, 2, 4, CAP>(x, wp, y, stats, g, n, kid, flops, bytes, s)   \
+             : launch_fwd_t<KS, MODE, 1, 1, 4, CAP>(x, wp, y, stats, g, n, kid, flops, bytes, s)
   if (p.ks == 3) {
-    if (p.mode == S1) CBF_FWD(3, S1, kCapS1);
-    if (p.mode == S2) CBF_FWD(3, S2, kCapS2);
-    CBF_FWD(3, U2, kCapS2);
+    if (p.mode == S1) { CBF_FWD(3, S1, kCapS1, kCapS1W); }
+    if (p.mode == S2) { CBF_FWD(3, S2, kCapS2, kCapS2W); }
+    CBF_FWD(3, U2, kCapS2, kCapS2W);
   }
-  if (p.mode == S1) CBF_FWD(1, S1, kCapS1);
-  if (p.mode == S2) CBF_FWD(1, S2, kCapS1);
-  CBF_FWD(1, U2, kCapS1);
+  if (p.mode == S1) { CBF_FWD(1, S1, kCapS1, kCapS1W); }
+  if (p.mode == S2) { CBF_FWD(1, S2, kCapS1, kCapS1W); }
+  CBF_FWD(1, U2, kCapS1, kCapS1W);
 #undef CBF_FWD
 }
 
@@ -798,8 +816,8 @@ int mde_convbf_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks
     int64_t np;
     return wgrad_geo(p, 1, &g, &S, &per, &np) ? 1 : 0;
   }
-  int mtw;
-  return fwd_geo(p, &g, &mtw) ? 1 : 0;
+  int mtw, nw;
+  return fwd_geo(p, 1, &g, &mtw, &nw) ? 1 : 0;
 }
 
 size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose) {
@@ -822,8 +840,8 @@ int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int
                             int stride) {
   Pass p;
   Geo g;
-  int mtw;
-  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p) || !fwd_geo(p, &g, &mtw)) return 0;
+  int mtw, nw;
+  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p) || !fwd_geo(p, n, &g, &mtw, &nw)) return 0;
   return (int)(n * g.ppi);
 }
 

@@ -70,10 +70,17 @@ def _worker(rank, world, port, out_dir, mode):
             first = [p.grad.detach().clone() for p in params]
     torch.cuda.synchronize()
     gmax = max(float(g.abs().max()) for g in want)
-    worst = 0.0
-    for g, m in zip(first, want):
-        scale = max(float(m.abs().max()), 1e-6 * gmax)  # BN-fed conv biases: true grad 0
-        worst = max(worst, float((g - m).abs().max()) / scale)
+    worst, worst_name = 0.0, ""
+    names = [n for n, p in model.named_parameters() if p.requires_grad]
+    for name, g, m in zip(names, first, want):
+        # parameters whose true gradient is 0 (the BN-fed conv biases): their
+        # computed gradients are rounding noise of the BN backward, so they
+        # are held to an absolute bound (1e-5 of the largest gradient), the
+        # others to 1e-5 relative
+        scale = float(m.abs().max()) if float(m.abs().max()) > 1e-4 * gmax else gmax
+        err = float((g - m).abs().max()) / scale
+        if err > worst:
+            worst, worst_name = err, name
     state = {k: v.detach().cpu() for k, v in model.named_parameters()}
     # BN running statistics: rank-local during training (no per-step
     # broadcast), rank 0's to every rank on sync_buffers()
@@ -82,7 +89,8 @@ def _worker(rank, world, port, out_dir, mode):
     torch.cuda.synchronize()
     bn_synced = tr.flat_bn.detach().cpu().clone()
     tr.close()
-    torch.save({"losses": losses, "state": state, "worst": worst, "bn_local": bn_local,
+    torch.save({"losses": losses, "state": state, "worst": worst, "worst_name": worst_name,
+                "bn_local": bn_local,
                 "bn_synced": bn_synced, "first": [g.cpu() for g in first]},
                os.path.join(out_dir, f"rank{rank}.pt"))
     torch.distributed.destroy_process_group()
@@ -98,7 +106,8 @@ def test_graph_trainer_two_ranks(mode):
         r0, r1 = (torch.load(os.path.join(d, f"rank{r}.pt"), weights_only=True) for r in range(2))
     for a, b in zip(r0["first"], r1["first"]):  # one averaged gradient on both ranks
         assert torch.equal(a, b)
-    assert r0["worst"] < 1e-5 and r1["worst"] < 1e-5, (r0["worst"], r1["worst"])
+    assert r0["worst"] < 1e-5 and r1["worst"] < 1e-5, (r0["worst"], r0["worst_name"], r1["worst"],
+                                                       r1["worst_name"])
     for k, v in r0["state"].items():
         assert torch.equal(v, r1["state"][k]), k
     assert r0["losses"] != r1["losses"]

@@ -42,6 +42,8 @@
 // = 2 channel tiles x 3 filter rows (3x3) or x 2 K halves (1x1).  Blocks split
 // the pixel patches (split-K); their fp32 partials are summed in a fixed order
 // (bitwise reproducible, no atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -76,7 +78,17 @@ struct Geo {
   int tiles_w;     // 2D: column tiles per band of pr rows
   int ppi;         // patches per image
   int cap;         // staged-pixel capacity (LDS image)
+  int nrmax;       // output rows a patch can span: the staged row count is fixed by it
+  float inv_wo, inv_pc, inv_ppi, inv_tw;  // reciprocals for fdiv
 };
+
+// a / d for 0 <= a < 2^22 from a float reciprocal, corrected to the exact quotient
+__device__ __forceinline__ int fdiv(int a, int d, float inv) {
+  int q = (int)((float)a * inv);
+  q -= q * d > a ? 1 : 0;
+  q += (q + 1) * d <= a ? 1 : 0;
+  return q;
+}
 
 struct Patch {
   int img, r0, r1, c0, nc, p0, npx;
@@ -84,18 +96,18 @@ struct Patch {
 
 __device__ __forceinline__ Patch patch_of(const Geo& g, int q) {
   Patch P;
-  P.img = q / g.ppi;
+  P.img = fdiv(q, g.ppi, g.inv_ppi);
   const int k = q - P.img * g.ppi;
   if (g.pc == 0) {
     const int hw = g.ho * g.wo;
     P.p0 = k * g.mb;
     P.npx = hw - P.p0 < g.mb ? hw - P.p0 : g.mb;
-    P.r0 = P.p0 / g.wo;
-    P.r1 = (P.p0 + P.npx - 1) / g.wo;
+    P.r0 = fdiv(P.p0, g.wo, g.inv_wo);
+    P.r1 = fdiv(P.p0 + P.npx - 1, g.wo, g.inv_wo);
     P.c0 = 0;
     P.nc = g.wo;
   } else {
-    const int band = k / g.tiles_w, t = k - band * g.tiles_w;
+    const int band = fdiv(k, g.tiles_w, g.inv_tw), t = k - band * g.tiles_w;
     P.r0 = band * g.pr;
     P.r1 = (P.r0 + g.pr < g.ho ? P.r0 + g.pr : g.ho) - 1;
     P.c0 = t * g.pc;
@@ -110,12 +122,13 @@ __device__ __forceinline__ Patch patch_of(const Geo& g, int q) {
 __device__ __forceinline__ bool pix_of(const Geo& g, const Patch& P, int m, int& r, int& c) {
   if (g.pc == 0) {
     const int p = P.p0 + (m < P.npx ? m : 0);
-    r = p / g.wo;
+    r = fdiv(p, g.wo, g.inv_wo);
     c = p - r * g.wo;
     return m < P.npx;
   }
-  r = P.r0 + m / g.pc;
-  c = P.c0 + m % g.pc;
+  const int mr = fdiv(m, g.pc, g.inv_pc);
+  r = P.r0 + mr;
+  c = P.c0 + (m - mr * g.pc);
   return m < P.npx && r < g.ho && c < g.wo;
 }
 
@@ -124,11 +137,13 @@ struct Img {
 };
 
 // The staged image of a patch: rows gr0 .. gr0 + rs - 1 and cols gc0 .. of the
-// source (Z = zero-inserted gy coordinates for U2; (2 i, 2 j) for 1x1 stride 2)
+// source (Z = zero-inserted gy coordinates for U2; (2 i, 2 j) for 1x1 stride 2).
+// The row count is the launch's maximum (nrmax output rows), so a thread's
+// staging units are the same for every patch (SrcStage::plan once per block).
 template <int KS, int MODE>
-__device__ __forceinline__ Img img_of(const Patch& P) {
+__device__ __forceinline__ Img img_of(const Geo& g, const Patch& P) {
   Img I;
-  const int nr = P.r1 - P.r0 + 1;
+  const int nr = g.nrmax;
   if constexpr (KS == 3 && MODE == S2) {
     I.gr0 = 2 * P.r0 - 1;
     I.rs = 2 * nr + 1;
@@ -186,20 +201,44 @@ __device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {  // (a.hi, 
 template <int KS, int MODE, int PITCH, int NT, int MAXU>
 struct SrcStage {
   uint32_t v[MAXU][8];
-  int d0[MAXU];  // first staged pixel of the unit, -1: no unit
+  int code[MAXU];  // the unit: (octet << 28) | (staged row << 16) | column index, -1: none
+  int d0[MAXU];    // its first staged pixel's element offset (incl. the octet), -1: none
 
-  __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
-                                       int ci0, int tid) {
-    const int64_t plane = (int64_t)g.hi * g.wi, pl2 = plane >> 1;
-    // units per octet: U2 / S1 / 1x1 S1: staged column pairs; 3x3 S2: source
-    // pairs (E and O halves); 1x1 S2: staged pixels
-    const int ncol = (KS == 1 && MODE == S2) ? I.cs : ((KS == 3 && MODE == S2) ? I.csh : I.cs >> 1);
-    const int per = I.rs * ncol, total = 4 * per;
+  // units per octet: U2 / S1 / 1x1 S1: staged column pairs; 3x3 S2: source
+  // pairs (E and O halves); 1x1 S2: staged pixels
+  __device__ static __forceinline__ int ncol(const Img& I) {
+    return (KS == 1 && MODE == S2) ? I.cs : ((KS == 3 && MODE == S2) ? I.csh : I.cs >> 1);
+  }
+
+  // the thread's units and their LDS offsets: the same for every patch and
+  // chunk of a launch (fixed staged-image shape), so decoded once per block
+  __device__ __forceinline__ void plan(const Img& I, int tid) {
+    const int nc = ncol(I), per = I.rs * nc, total = 4 * per;
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + NT * k;
-      const int uc = u < total ? u : 0;
-      const int o = uc / per, rem = uc - o * per, i = rem / ncol, jc = rem - i * ncol;
+      if (u < total) {
+        const int o = u / per, rem = u - o * per, i = rem / nc, jc = rem - i * nc;
+        code[k] = (o << 28) | (i << 16) | jc;
+        int px;
+        if constexpr (MODE == U2) px = i * I.cs + 2 * jc;
+        else if constexpr (KS == 1 && MODE == S2) px = i * I.cs + jc;
+        else px = i * I.cs + ((KS == 3 && MODE == S2) ? jc : 2 * jc);
+        d0[k] = px * PITCH + 8 * o;
+      } else {
+        code[k] = -1;
+        d0[k] = -1;
+      }
+    }
+  }
+
+  __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
+                                       int ci0) {
+    const int64_t plane = (int64_t)g.hi * g.wi, pl2 = plane >> 1;
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int cd = code[k] < 0 ? 0 : code[k];
+      const int o = cd >> 28, i = (cd >> 16) & 0xfff, jc = cd & 0xffff;
       int sr, sc;
       bool ok;
       if constexpr (MODE == U2) {
@@ -208,19 +247,16 @@ struct SrcStage {
         sr = zr >> 1;
         sc = zc >> 1;
         ok = (zr & 1) == 0 && zr >= 0 && sr < g.hi && zc >= 0 && sc < g.wi;
-        d0[k] = u < total ? i * I.cs + 2 * jc : -1;
       } else if constexpr (KS == 1 && MODE == S2) {
         sr = 2 * (I.gr0 + i);
         sc = 2 * (I.gc0 + jc);
         ok = sr < g.hi && sc < g.wi;
-        d0[k] = u < total ? i * I.cs + jc : -1;
       } else {
         sr = I.gr0 + i;
         sc = I.gc0 + 2 * jc;
         ok = sr >= 0 && sr < g.hi && sc >= 0 && sc < g.wi;
-        d0[k] = u < total ? i * I.cs + ((KS == 3 && MODE == S2) ? jc : 2 * jc) : -1;
       }
-      ok = ok && u < total && ci0 + 8 * o < g.cin;
+      ok = ok && code[k] >= 0 && ci0 + 8 * o < g.cin;
       if constexpr (MODE == U2) {
         const bf16* p = src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0);
 #pragma unroll
@@ -234,7 +270,6 @@ struct SrcStage {
           v[k][j] = ok ? t : 0u;
         }
       }
-      if (u < total) d0[k] = d0[k] * PITCH + 8 * o;  // element offset incl. the octet
     }
   }
 
@@ -319,7 +354,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv % WMW, wn = wv / WMW;
   const Patch P = patch_of(g, blockIdx.x);
-  const Img I = img_of<KS, MODE>(P);
+  const Img I = img_of<KS, MODE>(g, P);
   const int co0 = blockIdx.y * NB;
   const int nmt = (P.npx + 31) >> 5;  // M tiles holding pixels
 
@@ -360,7 +395,8 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
   const int nchunk = (g.cin + 31) >> 5;
   SrcStage<KS, MODE, kPitchF, NT, src_units<KS, MODE, CAP, NT>()> S;
   WStage<KK, NB, NT> Wt;
-  S.load(xs, g, I, 0, tid);
+  S.plan(I, tid);
+  S.load(xs, g, I, 0);
   Wt.load(wp, g.cout, co0, tid);
   for (int cc = 0; cc < nchunk; ++cc) {
     __syncthreads();
@@ -368,7 +404,7 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
     Wt.store(sw, tid);
     __syncthreads();
     if (cc + 1 < nchunk) {  // the next chunk's loads, in flight during this chunk's MFMAs
-      S.load(xs, g, I, 32 * (cc + 1), tid);
+      S.load(xs, g, I, 32 * (cc + 1));
       Wt.load(wp + (int64_t)(cc + 1) * KK * g.cout * 32, g.cout, co0, tid);
     }
 #pragma unroll
@@ -500,12 +536,14 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
   SrcStage<KS, MODE, kPitchW, NT, src_units<KS, MODE, CAP, NT>()> S;
   if (q0 < q1) {
     const Patch P = patch_of(g, q0);
-    S.load(x + (int64_t)P.img * g.cin * g.hi * g.wi, g, img_of<KS, MODE>(P), 32 * cc, tid);
+    const Img I = img_of<KS, MODE>(g, P);
+    S.plan(I, tid);
+    S.load(x + (int64_t)P.img * g.cin * g.hi * g.wi, g, I, 32 * cc);
     gy_load(P);
   }
   for (int q = q0; q < q1; ++q) {
     const Patch P = patch_of(g, q);
-    const Img I = img_of<KS, MODE>(P);
+    const Img I = img_of<KS, MODE>(g, P);
     __syncthreads();
     S.store(simg, I);
 #pragma unroll
@@ -524,7 +562,7 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
     __syncthreads();
     if (q + 1 < q1) {  // the next patch's loads, in flight during this patch's MFMAs
       const Patch Pn = patch_of(g, q + 1);
-      S.load(x + (int64_t)Pn.img * g.cin * g.hi * g.wi, g, img_of<KS, MODE>(Pn), 32 * cc, tid);
+      S.load(x + (int64_t)Pn.img * g.cin * g.hi * g.wi, g, img_of<KS, MODE>(g, Pn), 32 * cc);
       gy_load(Pn);
     }
     int toff[ND];
@@ -653,6 +691,13 @@ inline int img_px(const Pass& p, int pc, int pr, int mb) {
   return nr * nc;
 }
 
+inline void set_inv(Geo* g) {
+  g->inv_wo = 1.f / (float)g->wo;
+  g->inv_pc = g->pc ? 1.f / (float)g->pc : 0.f;
+  g->inv_ppi = 1.f / (float)g->ppi;
+  g->inv_tw = 1.f / (float)g->tiles_w;
+}
+
 // Choose the patch geometry: flat runs of mb pixels when the image fits,
 // else 2D tiles (pc columns x pr rows, pr * pc <= mb) with the fewest padded
 // pixels.  False if nothing fits or the shape breaks an alignment rule.
@@ -666,10 +711,14 @@ inline bool pick_geo(const Pass& p, int mb, Geo* g, int cap = 0) {
   g->mb = mb;
   g->cap = cap ? cap : cap_of(p);
   const int64_t hw = (int64_t)p.ho * p.wo;
+  if (hw >= (1 << 22)) return false;  // fdiv's exact range
   if (hw % 4 == 0 && img_px(p, 0, 0, mb) <= g->cap) {
     g->pc = g->pr = 0;
     g->tiles_w = 1;
     g->ppi = (int)mde::cdiv(hw, mb);
+    int nr = (mb + p.wo - 2) / p.wo + 1;
+    g->nrmax = nr > p.ho ? p.ho : nr;
+    set_inv(g);
     return true;
   }
   if (p.wo % 4) return false;
@@ -693,6 +742,8 @@ inline bool pick_geo(const Pass& p, int mb, Geo* g, int cap = 0) {
   g->pr = mb / best < p.ho ? mb / best : p.ho;
   g->tiles_w = (int)mde::cdiv(p.wo, g->pc);
   g->ppi = (int)(mde::cdiv(p.ho, g->pr) * g->tiles_w);
+  g->nrmax = g->pr;
+  set_inv(g);
   return true;
 }
 
@@ -717,7 +768,7 @@ template <int KS, int MODE, int WN, int MTW, int NW, int CAP>
 int launch_fwd_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const Geo& g, int64_t n,
                  int kid, double flops, double bytes, hipStream_t s) {
   const int64_t np = n * g.ppi;
-  if (np > 0x7fffffff) return MDE_ERR_UNSUPPORTED;
+  if (np >= (1 << 22)) return MDE_ERR_UNSUPPORTED;  // fdiv's exact range
   const dim3 grid((unsigned)np, (unsigned)(g.cout / (32 * WN)));
   if (stats)
     MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_kernel<KS, MODE, WN, MTW, NW, true, CAP>),
@@ -730,13 +781,21 @@ int launch_fwd_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const Geo
 
 inline int wn_of(const Pass& p) { return p.cout % 64 == 0 ? 2 : 1; }
 
-// forward geometry: at 64 output channels 8-wave blocks of 256 pixels when
-// there are enough of them to fill the chip (>= 2 per CU), else 4-wave
-// blocks with 2 M tiles a wave (128 pixels; 256 at 32 channels), or 1 when
-// that patch's image does not fit
+// forward geometry: 4-wave blocks with 2 M tiles a wave (128 pixels; 256 at
+// 32 channels), or 1 when that patch's image does not fit.  MDE_CONVBF_NW8=1:
+// 8-wave blocks of 256 pixels at 64 output channels (the filter staged half
+// as often; measured slower at 64 -> 64 @ 60x80: 77 vs 69 us, one block a CU)
+inline bool nw8_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_CONVBF_NW8");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 inline bool fwd_geo(const Pass& p, int64_t n, Geo* g, int* mtw, int* nw) {
   const int wn = wn_of(p);
-  if (wn == 2 && pick_geo(p, 256, g, cap_of(p, true)) &&
+  if (nw8_on() && wn == 2 && pick_geo(p, 256, g, cap_of(p, true)) &&
       n * g->ppi * (p.cout / 64) >= 512) {
     *mtw = 2;
     *nw = 8;
@@ -792,7 +851,7 @@ inline int wgrad_splits(int groups, int64_t npatch) {
 inline bool wgrad_geo(const Pass& p, int64_t n, Geo* g, int* S, int* per, int64_t* npatch) {
   if (!pick_geo(p, kMBW, g)) return false;
   const int64_t np = n * g->ppi;
-  if (np > 0x7fffffff) return false;
+  if (np >= (1 << 22)) return false;  // fdiv's exact range
   *npatch = np;
   const int groups = ((p.cout + 63) / 64) * (p.cin / 32);
   const int s0 = wgrad_splits(groups, np);

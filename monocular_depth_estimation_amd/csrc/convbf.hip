@@ -310,8 +310,8 @@ constexpr int src_units() {
   return (4 * ((KS == 1 && MODE == S2) ? CAP : CAP / 2) + NT - 1) / NT;
 }
 
-// The filter chunk [tap][NB][32] (16-byte pieces swizzled by (row >> 2) & 3),
-// register-staged like SrcStage.
+// The filter chunk [tap][NB][32] (16-byte pieces swizzled by (row >> 2) & 3,
+// already so in the packed filter), register-staged like SrcStage.
 template <int KK, int NB, int NT>
 struct WStage {
   static constexpr int U = (KK * NB * 4 + NT - 1) / NT;
@@ -331,7 +331,7 @@ struct WStage {
       const int u = tid + NT * k;
       if (u < KK * NB * 4) {
         const int o = u & 3, rest = u >> 2, cl = rest % NB, t = rest / NB;
-        *reinterpret_cast<u4v*>(sw + (t * NB + cl) * 32 + 8 * (o ^ ((cl >> 2) & 3))) = v[k];
+        *reinterpret_cast<u4v*>(sw + (t * NB + cl) * 32 + 8 * o) = v[k];  // pre-swizzled rows
       }
     }
   }
@@ -344,7 +344,7 @@ struct WStage {
 // pixels (the 4-wave ones per 128: the filter is most of what a 64-channel
 // block loads).
 template <int KS, int MODE, int WN, int MTW, int NW, bool STATS, int CAP>
-__global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
+__global__ void __launch_bounds__(64 * NW, 1)
     convbf_fwd_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                       bf16* __restrict__ y, float* __restrict__ stats, Geo g) {
   constexpr int KK = KS * KS, NB = 32 * WN, WMW = NW / WN, NT = 64 * NW;
@@ -382,6 +382,8 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
 #pragma unroll
   for (int t = 0; t < KK; ++t) toff[t] = tap_off<KS, MODE>(I, t / KS, t % KS) * kPitchF;
   const int col = wn * 32 + l32;  // B column (output channel within the block)
+  // the B read of k-half h takes piece (2 ks + h) ^ ((col >> 2) & 3) of the
+  // row: the packed rows are swizzled, so logical piece q sits at q ^ sw
   const int sw_x = (col >> 2) & 3;
   const int boff0 = col * 32 + 8 * ((0 + h) ^ sw_x), boff1 = col * 32 + 8 * ((2 + h) ^ sw_x);
 
@@ -458,6 +460,187 @@ __global__ void __launch_bounds__(64 * NW, NW == 4 ? 2 : 1)
     }
   }
   if constexpr (STATS) {
+    run = mde::sh_xor_sum(run, 32);
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(simg);  // [WMW][NB][4]
+    if (h == 0) {
+      float* p4 = part + (wm * NB + col) * 4;
+      p4[0] = run.ref;
+      p4[1] = run.n;
+      p4[2] = run.s1;
+      p4[3] = run.s2;
+    }
+    __syncthreads();
+    if (tid < NB) {
+      mde::Sh a{part[tid * 4], part[tid * 4 + 1], part[tid * 4 + 2], part[tid * 4 + 3]};
+#pragma unroll
+      for (int k = 1; k < WMW; ++k) {
+        const float* p4 = part + (k * NB + tid) * 4;
+        a = mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      float* o4 = stats + ((int64_t)(co0 + tid) * gridDim.x + blockIdx.x) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
+    }
+  }
+}
+
+// Resident-filter forward: persistent blocks, each owning NB output channels
+// and a contiguous range of patches, with the block's WHOLE filter slice
+// ([cin / 32][tap][NB][32], <= kWRes) copied into LDS once by LDS-DMA
+// (global_load_lds, 1 KiB per wave instruction, the rows pre-swizzled by the
+// pack).  The pipeline runs over (patch, channel chunk) steps: the next
+// step's input chunk is register-staged during this step's MFMAs, so only
+// the input is staged per step (the filter -- most of what the chunked
+// kernel stages -- never again).
+constexpr int kWRes = 36864;  // resident filter capacity, bf16 elements (73.7 KB)
+
+template <int KS, int MODE, int WN, bool STATS, int CAP>
+__global__ void __launch_bounds__(256, 1)
+    convbf_fwd_res_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
+                          bf16* __restrict__ y, float* __restrict__ stats, Geo g, int per,
+                          int npatch) {
+  constexpr int KK = KS * KS, NB = 32 * WN, WMW = 4 / WN, MTW = 2, NT = 256;
+  __shared__ __attribute__((aligned(16))) bf16 simg[CAP * kPitchF];
+  __shared__ __attribute__((aligned(16))) bf16 sw[kWRes];
+  const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wv % WMW, wn = wv / WMW;
+  const int co0 = blockIdx.y * NB;
+  const int nch = (g.cin + 31) >> 5;
+  const int q0 = blockIdx.x * per, q1 = q0 + per < npatch ? q0 + per : npatch;
+  if (q0 >= q1) return;  // block-uniform, before any barrier
+  {  // the filter slice: nch * KK segments of NB rows (NB * 64 bytes: 2 or 4 KiB)
+    constexpr int SEG = NB * 64 / 1024;
+    const int pieces = nch * KK * SEG;
+    for (int j = wv; j < pieces; j += 4) {
+      const int sg = j / SEG, within = j - sg * SEG;
+      const bf16* src = wp + ((int64_t)sg * g.cout + co0) * 32 + within * 512 + lane * 8;
+      __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(sw + j * 512),
+                                       16, 0, 0);
+    }
+  }
+  Patch P = patch_of(g, q0);
+  Img I = img_of<KS, MODE>(g, P);
+  int toff[KK];
+#pragma unroll
+  for (int t = 0; t < KK; ++t) toff[t] = tap_off<KS, MODE>(I, t / KS, t % KS) * kPitchF;
+  const int col = wn * 32 + l32;  // B column (output channel within the block)
+  const int sw_x = (col >> 2) & 3;  // logical piece q of the row sits at q ^ sw_x
+  const int boff0 = col * 32 + 8 * ((0 + h) ^ sw_x), boff1 = col * 32 + 8 * ((2 + h) ^ sw_x);
+  const int64_t hwo = (int64_t)g.ho * g.wo, xplane = (int64_t)g.cin * g.hi * g.wi;
+
+  SrcStage<KS, MODE, kPitchF, NT, src_units<KS, MODE, CAP, NT>()> S;
+  S.plan(I, tid);
+  S.load(x + (int64_t)P.img * xplane, g, I, 0);
+
+  int abase[MTW], dymask[MTW];
+  bool mt_on[MTW];
+  auto setup = [&](const Patch& Q, const Img& J) {
+    const int nmt = (Q.npx + 31) >> 5;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const int mt = MTW * wm + i;
+      mt_on[i] = mt < nmt;
+      int r, c;
+      const bool ok = pix_of(g, Q, mt * 32 + l32, r, c);
+      abase[i] = ok ? img_base<KS, MODE>(Q, J, r, c) * kPitchF : 0;
+      dymask[i] = 7;
+      if constexpr (MODE == U2 && KS == 3) {
+        int r0, c0, r1, c1;
+        const bool a = pix_of(g, Q, mt * 32, r0, c0);
+        const bool b = pix_of(g, Q, mt * 32 + 31, r1, c1);
+        if (a && b && r0 == r1) dymask[i] = (r0 & 1) ? 5 : 2;
+      }
+    }
+  };
+  setup(P, I);
+  f16v acc[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  mde::Sh run{0.f, 0.f, 0.f, 0.f};
+  bool have_ref = false;
+
+  int q = q0, cc = 0;
+  while (true) {
+    __syncthreads();  // previous step's image readers are done (1st: the filter DMA drained)
+    S.store(simg, I);
+    __syncthreads();
+    int qn = q, ccn = cc + 1;
+    if (ccn == nch) {
+      ccn = 0;
+      ++qn;
+    }
+    Patch Pn = P;
+    Img In = I;
+    if (qn < q1) {  // the next step's input chunk, in flight during this step's MFMAs
+      if (qn != q) {
+        Pn = patch_of(g, qn);
+        In = img_of<KS, MODE>(g, Pn);
+      }
+      S.load(x + (int64_t)Pn.img * xplane, g, In, 32 * ccn);
+    }
+    const bf16* swc = sw + cc * KK * NB * 32;
+#pragma unroll
+    for (int t = 0; t < KK; ++t) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const u4v b = *reinterpret_cast<const u4v*>(swc + t * NB * 32 + (ks ? boff1 : boff0));
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) {
+          if (mt_on[i] && ((dymask[i] >> (t / KS)) & 1)) {  // wave-uniform
+            const u4v a = *reinterpret_cast<const u4v*>(simg + abase[i] + toff[t] + 16 * ks + 8 * h);
+            acc[i] = mfma32(a, b, acc[i]);
+          }
+        }
+      }
+    }
+    if (cc == nch - 1) {  // the patch is complete: bf16 output (+ statistics)
+      bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col) * hwo;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        if (mt_on[i]) {
+          const int mt = MTW * wm + i;
+#pragma unroll
+          for (int qq = 0; qq < 4; ++qq) {
+            const int m = mt * 32 + 8 * qq + 4 * h;
+            int r, c;
+            const bool ok = pix_of(g, P, m, r, c);
+            const bf16 b0 = mde::f2bf(acc[i][4 * qq]), b1 = mde::f2bf(acc[i][4 * qq + 1]);
+            const bf16 b2 = mde::f2bf(acc[i][4 * qq + 2]), b3 = mde::f2bf(acc[i][4 * qq + 3]);
+            if constexpr (STATS) {
+              if (!have_ref) {
+                run.ref = __shfl(mde::bf2f(b0), l32, 64);
+                have_ref = true;
+              }
+              mde::sh_add(run, mde::bf2f(b0), ok);
+              mde::sh_add(run, mde::bf2f(b1), ok);
+              mde::sh_add(run, mde::bf2f(b2), ok);
+              mde::sh_add(run, mde::bf2f(b3), ok);
+            }
+            if (ok)
+              *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) =
+                  u2v{(uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16)};
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+      }
+    }
+    if (qn >= q1) break;
+    if (qn != q) {
+      P = Pn;
+      I = In;
+      setup(P, I);
+    }
+    q = qn;
+    cc = ccn;
+  }
+  if constexpr (STATS) {  // one record per channel and block
     run = mde::sh_xor_sum(run, 32);
     __syncthreads();
     float* part = reinterpret_cast<float*>(simg);  // [WMW][NB][4]
@@ -652,7 +835,11 @@ __global__ void __launch_bounds__(256)
   const int co = (int)(rest % pco);
   rest /= pco;
   const int tap = (int)(rest % kk), cc = (int)(rest / kk);
-  const int ci = cc * 32 + j;
+  // element j of the row sits at 16-byte piece (j / 8) ^ ((co >> 2) & 3): the
+  // swizzle of the LDS filter image (conflict-free B reads), so blocks copy
+  // rows verbatim (register staging or LDS-DMA)
+  const int jj = 8 * ((j >> 3) ^ ((co >> 2) & 3)) + (j & 7);
+  const int ci = cc * 32 + jj;
   float v = 0.f;
   if (ci < pci)
     v = transpose ? w[((int64_t)ci * cin + co) * kk + (kk - 1 - tap)]
@@ -812,14 +999,90 @@ inline bool fwd_geo(const Pass& p, int64_t n, Geo* g, int* mtw, int* nw) {
   return false;
 }
 
+// Resident-filter path (convbf_fwd_res_kernel): the block's filter slice --
+// NB = 64 output channels when it fits kWRes, else 32 -- for all input
+// channels.  MDE_CONVBF_RES=0: the chunked kernel always (A/B switch).
+inline bool res_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_CONVBF_RES");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+inline int res_nb(const Pass& p) {
+  const int nch = (p.cin + 31) / 32, kk = p.ks * p.ks;
+  if (p.cout % 64 == 0 && nch * kk * 64 * 32 <= kWRes) return 64;
+  if (nch * kk * 32 * 32 <= kWRes) return 32;
+  return 0;
+}
+
+inline int device_cus() {
+  static const int cus = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return c > 0 ? c : 256;
+  }();
+  return cus;
+}
+
+struct ResGeo {
+  Geo g;
+  int nb, per, blocks;  // output channels a block, patches a block, blocks per channel group
+  int64_t np;
+};
+
+inline bool res_geo(const Pass& p, int64_t n, ResGeo* r) {
+  r->nb = res_on() ? res_nb(p) : 0;
+  if (!r->nb || !pick_geo(p, 32 * 2 * (4 / (r->nb / 32)), &r->g)) return false;
+  r->np = n * r->g.ppi;
+  if (r->np >= (1 << 22)) return false;
+  const int ncob = p.cout / r->nb;
+  int64_t G = device_cus() / ncob;  // one block a CU (the LDS holds one)
+  if (G < 1) G = 1;
+  if (G > r->np) G = r->np;
+  r->per = (int)mde::cdiv(r->np, G);
+  r->blocks = (int)mde::cdiv(r->np, r->per);
+  return true;
+}
+
+template <int KS, int MODE, int WN, int CAP>
+int launch_res_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const ResGeo& r, int cout,
+                 int kid, double flops, double bytes, hipStream_t s) {
+  const dim3 grid((unsigned)r.blocks, (unsigned)(cout / (32 * WN)));
+  if (stats)
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_res_kernel<KS, MODE, WN, true, CAP>), grid,
+                    dim3(256), 0, x, wp, y, stats, r.g, r.per, (int)r.np);
+  else
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_res_kernel<KS, MODE, WN, false, CAP>), grid,
+                    dim3(256), 0, x, wp, y, stats, r.g, r.per, (int)r.np);
+  return MDE_OK;
+}
+
 int launch_fwd(const Pass& p, const bf16* x, const bf16* wp, bf16* y, float* stats, int64_t n,
                int kid, hipStream_t s) {
+  const double flops = 2.0 * n * p.ho * p.wo * (double)p.cout * p.cin * p.ks * p.ks;
+  const double bytes = 2.0 * n * ((double)p.cin * p.hi * p.wi + (double)p.cout * p.ho * p.wo);
+  ResGeo rg;
+  if (res_geo(p, n, &rg)) {
+#define CBF_RES(KS, MODE, CAP)                                                                     \
+  return rg.nb == 64 ? launch_res_t<KS, MODE, 2, CAP>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s) \
+                     : launch_res_t<KS, MODE, 1, CAP>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s)
+    if (p.ks == 3) {
+      if (p.mode == S1) { CBF_RES(3, S1, kCapS1); }
+      if (p.mode == S2) { CBF_RES(3, S2, kCapS2); }
+      CBF_RES(3, U2, kCapS2);
+    }
+    if (p.mode == S1) { CBF_RES(1, S1, kCapS1); }
+    if (p.mode == S2) { CBF_RES(1, S2, kCapS1); }
+    CBF_RES(1, U2, kCapS1);
+#undef CBF_RES
+  }
   const int wn = wn_of(p);
   Geo g;
   int mtw, nw;
   if (!fwd_geo(p, n, &g, &mtw, &nw)) return MDE_ERR_UNSUPPORTED;
-  const double flops = 2.0 * n * p.ho * p.wo * (double)p.cout * p.cin * p.ks * p.ks;
-  const double bytes = 2.0 * n * ((double)p.cin * p.hi * p.wi + (double)p.cout * p.ho * p.wo);
 #define CBF_FWD(KS, MODE, CAP, CAPW)                                                         \
   if (nw == 8)                                                                             \
     return launch_fwd_t<KS, MODE, 2, 2, 8, CAPW>(x, wp, y, stats, g, n, kid, flops, bytes, s); \
@@ -900,7 +1163,10 @@ int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int
   Pass p;
   Geo g;
   int mtw, nw;
-  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p) || !fwd_geo(p, n, &g, &mtw, &nw)) return 0;
+  if (!make_pass(cin, cout, h, w, ks, stride, 0, &p)) return 0;
+  ResGeo rg;
+  if (res_geo(p, n, &rg)) return rg.blocks;  // one record per channel and persistent block
+  if (!fwd_geo(p, n, &g, &mtw, &nw)) return 0;
   return (int)(n * g.ppi);
 }
 

@@ -701,7 +701,7 @@ int mde_graph_replace_memsets(void* graph, int64_t* replaced);
 
 /* Which storage types the one-launch small-tensor BatchNorm kernels serve
  * (n * h * w <= 16384; the others take the statistics + apply launches):
- * 0 none, 1 fp32 (default), 2 fp32 and bf16.  mode < 0 only queries.
+ * 0 none, 1 fp32, 2 fp32 and bf16 (default).  mode < 0 only queries.
  * Returns the previous mode. */
 int mde_bn_chan_mode(int mode);
 

@@ -628,9 +628,17 @@ constexpr int64_t kChanMax = (int64_t)kChanThreads * kChanUnits * 4;
 
 // Which storage types take the one-launch kernels: 0 none, 1 fp32, 2 fp32 and
 // bf16 (mde_bn_chan_mode; the environment's MDE_BN_CHAN sets the start value).
+// Round 4 kept bf16 on the two-launch path after the cfg3 golden's loss error
+// moved 0.6 -> 1.7 %: both paths compute the same statistics in another
+// summation order (tests/test_gpu_bn.py: every output within one bf16 ulp of
+// the other path's, parameter gradients / running statistics within 1e-5),
+// and that golden (64 x 96, bs 2) is ill-conditioned -- DAPPM's 1x1
+// BatchNorms over two values turn one bf16 ulp into percents; with the r05
+// kernels both bf16 goldens pass on this path (64x96 loss 0.34 % vs the
+// oracle's own 0.31 %, gpurun_out/r05b/bf16_chan.log).
 int g_chan_mode = [] {
   const char* e = std::getenv("MDE_BN_CHAN");
-  return e ? std::atoi(e) : 1;
+  return e ? std::atoi(e) : 2;
 }();
 
 template <typename T>

@@ -43,6 +43,7 @@
 // the pixel patches (split-K); their fp32 partials are summed in a fixed order
 // (bitwise reproducible, no atomics).
 #include <cstdlib>
+#include <utility>
 
 #include "common.h"
 
@@ -59,6 +60,15 @@ using lds_s4 = __attribute__((address_space(3))) s4v;
 __device__ __forceinline__ f16v mfma32(u4v a, u4v b, f16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8v, a),
                                                  __builtin_bit_cast(bf8v, b), c, 0, 0, 0);
+}
+
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }
 
 enum Mode : int { S1 = 0, S2 = 1, U2 = 2 };
@@ -337,6 +347,53 @@ struct WStage {
   }
 };
 
+// The MFMAs of one staged chunk: (tap, k-half) steps over the filter rows in
+// DYM (a compile-time mask: U2 tiles skip the all-zero rows), each step's B
+// (filter) and A (image) fragments read one step ahead (two register slots),
+// straight-line code -- no branch around an MFMA (a branch made the compiler
+// copy the accumulators between AGPRs and VGPRs at every one).
+template <int KS, int DYM, int MTW, int PITCH_A>
+__device__ __forceinline__ void chunk_mfmas(const bf16* __restrict__ swc, int nbrow,
+                                            const bf16* __restrict__ simg, const int (&abase)[MTW],
+                                            const int (&toff)[KS * KS], int boff0, int boff1, int h,
+                                            f16v (&acc)[MTW]) {
+  constexpr int NR = (DYM & 1) + ((DYM >> 1) & 1) + ((DYM >> 2) & 1);
+  constexpr int NS = (KS == 3 ? NR * 3 : 1) * 2;
+  // step s -> (tap, ks)
+  auto tap_of = [](int s) constexpr {
+    const int j = s >> 1;  // j-th (dy, dx) pair among the kept rows
+    if constexpr (KS == 1) return 0;
+    int row = 0, n = 0;
+    for (int dy = 0; dy < 3; ++dy)
+      if ((DYM >> dy) & 1) {
+        if (j >= n * 3 && j < n * 3 + 3) row = dy * 3 + (j - n * 3);
+        ++n;
+      }
+    return row;
+  };
+  u4v bq[2], aq[2][MTW];
+  auto ld = [&](auto s_c, auto slot_c) {
+    constexpr int s = decltype(s_c)::value, slot = decltype(slot_c)::value;
+    constexpr int t = tap_of(s), ks = s & 1;
+    bq[slot] = *reinterpret_cast<const u4v*>(swc + t * nbrow + (ks ? boff1 : boff0));
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+      aq[slot][i] = *reinterpret_cast<const u4v*>(simg + abase[i] + toff[t] + 16 * ks + 8 * h);
+  };
+  ld(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  static_for<NS>([&](auto s_c) {
+    constexpr int s = decltype(s_c)::value;
+    if constexpr (s + 1 < NS)
+      ld(std::integral_constant<int, s + 1>{}, std::integral_constant<int, (s + 1) & 1>{});
+    // keep the next step's reads here: the scheduler otherwise sinks each read
+    // next to its MFMA and every MFMA waits out an LDS latency
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) acc[i] = mfma32(aq[s & 1][i], bq[s & 1], acc[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
 // ------------------------------------------------------------------ forward
 // Block: NW waves; wave (wm, wn): output channels 32 wn .. of the block's
 // 32 WN, M tiles MTW wm .. MTW wm + MTW - 1 (32 pixels each) of the patch
@@ -360,24 +417,24 @@ __global__ void __launch_bounds__(64 * NW, 1)
 
   int abase[MTW];
   bool mt_on[MTW];
-  int dymask[MTW];  // filter rows a tile needs (U2: all-zero staged rows skipped)
+  int wdymask = MODE == U2 && KS == 3 ? 0 : 7;  // filter rows some tile of the wave needs
 #pragma unroll
   for (int i = 0; i < MTW; ++i) {
     const int mt = MTW * wm + i;
     mt_on[i] = mt < nmt;
     int r, c;
     const bool ok = pix_of(g, P, mt * 32 + l32, r, c);
-    abase[i] = ok ? img_base<KS, MODE>(P, I, r, c) : 0;
-    dymask[i] = 7;
+    abase[i] = ok ? img_base<KS, MODE>(P, I, r, c) * kPitchF : 0;
     if constexpr (MODE == U2 && KS == 3) {
       // a tile inside one output row r reads Z rows r - 1 + dy, zero unless
-      // r + dy is odd: dy = 1 for even r, dy = 0, 2 for odd r (wave-uniform)
+      // r + dy is odd: dy = 1 for even r, dy = 0, 2 for odd r
       int r0, c0, r1, c1;
       const bool a = pix_of(g, P, mt * 32, r0, c0);
       const bool b = pix_of(g, P, mt * 32 + 31, r1, c1);
-      if (a && b && r0 == r1) dymask[i] = (r0 & 1) ? 5 : 2;
+      wdymask |= !mt_on[i] ? 0 : ((a && b && r0 == r1) ? ((r0 & 1) ? 5 : 2) : 7);
     }
   }
+  wdymask = __builtin_amdgcn_readfirstlane(wdymask);
   int toff[KK];
 #pragma unroll
   for (int t = 0; t < KK; ++t) toff[t] = tap_off<KS, MODE>(I, t / KS, t % KS) * kPitchF;
@@ -409,21 +466,12 @@ __global__ void __launch_bounds__(64 * NW, 1)
       S.load(xs, g, I, 32 * (cc + 1));
       Wt.load(wp + (int64_t)(cc + 1) * KK * g.cout * 32, g.cout, co0, tid);
     }
-#pragma unroll
-    for (int t = 0; t < KK; ++t) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const u4v b = *reinterpret_cast<const u4v*>(sw + t * NB * 32 + (ks ? boff1 : boff0));
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-          if (mt_on[i] && ((dymask[i] >> (t / KS)) & 1)) {  // wave-uniform
-            const u4v a = *reinterpret_cast<const u4v*>(simg + abase[i] * kPitchF + toff[t] +
-                                                       16 * ks + 8 * h);
-            acc[i] = mfma32(a, b, acc[i]);
-          }
-        }
-      }
-    }
+    if (MODE == U2 && KS == 3 && wdymask == 2)
+      chunk_mfmas<KS, 2, MTW, kPitchF>(sw, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+    else if (MODE == U2 && KS == 3 && wdymask == 5)
+      chunk_mfmas<KS, 5, MTW, kPitchF>(sw, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+    else
+      chunk_mfmas<KS, 7, MTW, kPitchF>(sw, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
   }
 
   // epilogue: lane (co = co0 + col, h) holds pixels 32 mt + 8 q + 4 h + (0..3), q = reg >> 2
@@ -536,10 +584,12 @@ __global__ void __launch_bounds__(256, 1)
   S.plan(I, tid);
   S.load(x + (int64_t)P.img * xplane, g, I, 0);
 
-  int abase[MTW], dymask[MTW];
+  int abase[MTW];
   bool mt_on[MTW];
+  int wdymask = 7;  // U2: filter rows some tile of this wave needs (wave-uniform)
   auto setup = [&](const Patch& Q, const Img& J) {
     const int nmt = (Q.npx + 31) >> 5;
+    wdymask = MODE == U2 && KS == 3 ? 0 : 7;
 #pragma unroll
     for (int i = 0; i < MTW; ++i) {
       const int mt = MTW * wm + i;
@@ -547,14 +597,16 @@ __global__ void __launch_bounds__(256, 1)
       int r, c;
       const bool ok = pix_of(g, Q, mt * 32 + l32, r, c);
       abase[i] = ok ? img_base<KS, MODE>(Q, J, r, c) * kPitchF : 0;
-      dymask[i] = 7;
       if constexpr (MODE == U2 && KS == 3) {
+        // a tile inside one output row r reads Z rows r - 1 + dy, zero unless
+        // r + dy is odd: dy = 1 for even r, dy = 0, 2 for odd r
         int r0, c0, r1, c1;
         const bool a = pix_of(g, Q, mt * 32, r0, c0);
         const bool b = pix_of(g, Q, mt * 32 + 31, r1, c1);
-        if (a && b && r0 == r1) dymask[i] = (r0 & 1) ? 5 : 2;
+        wdymask |= !mt_on[i] ? 0 : ((a && b && r0 == r1) ? ((r0 & 1) ? 5 : 2) : 7);
       }
     }
+    wdymask = __builtin_amdgcn_readfirstlane(wdymask);
   };
   setup(P, I);
   f16v acc[MTW];
@@ -585,20 +637,13 @@ __global__ void __launch_bounds__(256, 1)
       S.load(x + (int64_t)Pn.img * xplane, g, In, 32 * ccn);
     }
     const bf16* swc = sw + cc * KK * NB * 32;
-#pragma unroll
-    for (int t = 0; t < KK; ++t) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const u4v b = *reinterpret_cast<const u4v*>(swc + t * NB * 32 + (ks ? boff1 : boff0));
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) {
-          if (mt_on[i] && ((dymask[i] >> (t / KS)) & 1)) {  // wave-uniform
-            const u4v a = *reinterpret_cast<const u4v*>(simg + abase[i] + toff[t] + 16 * ks + 8 * h);
-            acc[i] = mfma32(a, b, acc[i]);
-          }
-        }
-      }
-    }
+    // U2 skips a filter row only when all of the wave's tiles do
+    if (MODE == U2 && KS == 3 && wdymask == 2)
+      chunk_mfmas<KS, 2, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+    else if (MODE == U2 && KS == 3 && wdymask == 5)
+      chunk_mfmas<KS, 5, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+    else
+      chunk_mfmas<KS, 7, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
     if (cc == nch - 1) {  // the patch is complete: bf16 output (+ statistics)
       bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col) * hwo;
 #pragma unroll

@@ -22,12 +22,12 @@ for PMC in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA S
 import csv, sys, collections, re
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(sys.argv[1])):
-    n = r["Kernel_Name"]
-    if "convbf" not in n:
+    m = re.search(r"(convbf_\w+_kernel<[^>]*>)", r["Kernel_Name"])
+    if not m:
         continue
-    n = re.sub(r"\(.*", "", n).replace("void (anonymous namespace)::", "")
+    n = m.group(1)
     agg[n][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for n, cs in sorted(agg.items()):
-    print(f"{n[:70]:70s} " + " ".join(f"{c}={sum(v)/len(v):.4g}" for c, v in sorted(cs.items())))
+    print(f"{n[:60]:60s} " + " ".join(f"{c}={sum(v)/len(v):.4g}" for c, v in sorted(cs.items())))
 PY
 done

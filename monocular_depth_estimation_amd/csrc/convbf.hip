@@ -192,6 +192,13 @@ __device__ __forceinline__ int tap_off(const Img& I, int dy, int dx) {
   return dy * I.cs + dx;
 }
 
+// two fp32 -> packed bf16 (round-to-nearest-even): one v_cvt_pk_bf16_f32
+using bf2v = __bf16 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  const bf2v v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 __device__ __forceinline__ uint32_t lo16x2(uint32_t a, uint32_t b) {  // (a.lo, b.lo)
   return __builtin_amdgcn_perm(b, a, 0x05040100u);
 }
@@ -208,47 +215,77 @@ __device__ __forceinline__ uint32_t hi16x2(uint32_t a, uint32_t b) {  // (a.hi, 
 // the kernels call load() for the next chunk / patch before the current one's
 // MFMAs, so the load latency hides behind the matrix work.  MAXU >= the units
 // a thread can own (host: pick_geo caps the staged pixels at the LDS image).
+// Units are numbered octet-fastest (four lanes stage one pixel's 64 bytes)
+// and, in each 8-lane group of a 16-byte LDS store (banks = dword address mod
+// 32 for stores), the two quads write pixels whose offsets differ by 16 banks:
+// at the forward image's 80-byte pitch by taking column units 2 or 4 apart
+// (a permutation inside aligned groups), at the weight-gradient image's
+// 64-byte pitch by swapping the two stores of every odd quad.  Loads are
+// buffer loads: a per-unit 32-bit offset (VGPR) and a per-channel offset
+// (SGPR); out-of-range units get an offset past the buffer (loads return 0),
+// so no address arithmetic or select per load.
 template <int KS, int MODE, int PITCH, int NT, int MAXU>
 struct SrcStage {
+  static constexpr bool ONE = KS == 1 && MODE == S2;     // one staged pixel a unit
+  static constexpr bool EO = KS == 3 && MODE == S2;      // even / odd column halves
+  static constexpr bool PAIR_PX = !ONE && !EO;           // unit jc -> pixels 2 jc, 2 jc + 1
+  static constexpr int G = PITCH == kPitchF ? (PAIR_PX ? 4 : 8) : 1;  // permutation group
+  static constexpr bool SWAP = PITCH != kPitchF && PAIR_PX;
   uint32_t v[MAXU][8];
-  int code[MAXU];  // the unit: (octet << 28) | (staged row << 16) | column index, -1: none
-  int d0[MAXU];    // its first staged pixel's element offset (incl. the octet), -1: none
+  int code[MAXU];  // (swap << 30) | (octet << 28) | (staged row << 16) | column unit, -1: none
+  int dA[MAXU], dB[MAXU];  // element offsets of the first / second store (dB < 0: none)
 
-  // units per octet: U2 / S1 / 1x1 S1: staged column pairs; 3x3 S2: source
-  // pairs (E and O halves); 1x1 S2: staged pixels
   __device__ static __forceinline__ int ncol(const Img& I) {
-    return (KS == 1 && MODE == S2) ? I.cs : ((KS == 3 && MODE == S2) ? I.csh : I.cs >> 1);
+    return ONE ? I.cs : (EO ? I.csh : I.cs >> 1);
   }
 
-  // the thread's units and their LDS offsets: the same for every patch and
-  // chunk of a launch (fixed staged-image shape), so decoded once per block
   __device__ __forceinline__ void plan(const Img& I, int tid) {
-    const int nc = ncol(I), per = I.rs * nc, total = 4 * per;
+    const int nc = ncol(I), total = 4 * I.rs * nc;
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = tid + NT * k;
       if (u < total) {
-        const int o = u / per, rem = u - o * per, i = rem / nc, jc = rem - i * nc;
-        code[k] = (o << 28) | (i << 16) | jc;
-        int px;
-        if constexpr (MODE == U2) px = i * I.cs + 2 * jc;
-        else if constexpr (KS == 1 && MODE == S2) px = i * I.cs + jc;
-        else px = i * I.cs + ((KS == 3 && MODE == S2) ? jc : 2 * jc);
-        d0[k] = px * PITCH + 8 * o;
+        const int o = u & 3, rest = u >> 2;
+        const int i = rest / nc;
+        int jc = rest - i * nc;
+        if constexpr (G > 1) {
+          const int base = jc & ~(G - 1), jl = jc & (G - 1);
+          if (base + G <= nc) jc = base + (jl & 1) * (G / 2) + (jl >> 1);
+        }
+        const bool sw = SWAP && (rest & 1);
+        code[k] = ((int)sw << 30) | (o << 28) | (i << 16) | jc;
+        int p0, p1;
+        if constexpr (ONE) {
+          p0 = i * I.cs + jc;
+          p1 = -1;
+        } else if constexpr (EO) {
+          p0 = i * I.cs + jc;
+          p1 = p0 + I.csh;
+        } else {
+          p0 = i * I.cs + 2 * jc;
+          p1 = p0 + 1;
+        }
+        dA[k] = (sw ? p1 : p0) * PITCH + 8 * o;
+        dB[k] = p1 < 0 ? -1 : (sw ? p0 : p1) * PITCH + 8 * o;
       } else {
         code[k] = -1;
-        d0[k] = -1;
+        dA[k] = dB[k] = -1;
       }
     }
   }
 
   __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
                                        int ci0) {
-    const int64_t plane = (int64_t)g.hi * g.wi, pl2 = plane >> 1;
+    const int plane = g.hi * g.wi;
+    const uint64_t a = (uint64_t)src;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 2 * g.cin * plane, 0x00020000);
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int cd = code[k] < 0 ? 0 : code[k];
-      const int o = cd >> 28, i = (cd >> 16) & 0xfff, jc = cd & 0xffff;
+      const int o = (cd >> 28) & 3, i = (cd >> 16) & 0xfff, jc = cd & 0xffff;
       int sr, sc;
       bool ok;
       if constexpr (MODE == U2) {
@@ -257,7 +294,7 @@ struct SrcStage {
         sr = zr >> 1;
         sc = zc >> 1;
         ok = (zr & 1) == 0 && zr >= 0 && sr < g.hi && zc >= 0 && sc < g.wi;
-      } else if constexpr (KS == 1 && MODE == S2) {
+      } else if constexpr (ONE) {
         sr = 2 * (I.gr0 + i);
         sc = 2 * (I.gc0 + jc);
         ok = sr < g.hi && sc < g.wi;
@@ -266,48 +303,40 @@ struct SrcStage {
         sc = I.gc0 + 2 * jc;
         ok = sr >= 0 && sr < g.hi && sc >= 0 && sc < g.wi;
       }
-      ok = ok && code[k] >= 0 && ci0 + 8 * o < g.cin;
-      if constexpr (MODE == U2) {
-        const bf16* p = src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0);
+      ok = ok && code[k] >= 0;
+      const uint32_t voff = ok ? (uint32_t)(2 * (8 * o * plane + sr * g.wi + sc)) : 0x7ffffff0u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) v[k][j] = ok ? (uint32_t)p[ok ? j * plane : 0] : 0u;
-      } else {
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(
-            src + (int64_t)(ci0 + 8 * o) * plane + (ok ? sr * g.wi + sc : 0));
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const uint32_t t = p[ok ? j * pl2 : 0];
-          v[k][j] = ok ? t : 0u;
-        }
+      for (int j = 0; j < 8; ++j) {
+        const int soff = 2 * (ci0 + j) * plane;
+        if constexpr (MODE == U2)
+          v[k][j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R, voff, soff, 0);
+        else
+          v[k][j] = __builtin_amdgcn_raw_buffer_load_b32(R, voff, soff, 0);
       }
     }
   }
 
-  __device__ __forceinline__ void store(bf16* img, const Img& I) const {
+  __device__ __forceinline__ void store(bf16* img) const {
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
-      if (d0[k] < 0) continue;
-      bf16* d = img + d0[k];
-      if constexpr (MODE == U2) {
-        u4v a;
+      if (dA[k] < 0) continue;
+      u4v e, od;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = v[k][2 * j] | (v[k][2 * j + 1] << 16);
-        *reinterpret_cast<u4v*>(d) = a;
-        *reinterpret_cast<u4v*>(d + PITCH) = u4v{0u, 0u, 0u, 0u};
-      } else if constexpr (KS == 1 && MODE == S2) {
-        u4v a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = lo16x2(v[k][2 * j], v[k][2 * j + 1]);
-        *reinterpret_cast<u4v*>(d) = a;
-      } else {
-        u4v e, od;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (MODE == U2) {
+          e[j] = v[k][2 * j] | (v[k][2 * j + 1] << 16);
+          od[j] = 0u;
+        } else {
           e[j] = lo16x2(v[k][2 * j], v[k][2 * j + 1]);
           od[j] = hi16x2(v[k][2 * j], v[k][2 * j + 1]);
         }
-        *reinterpret_cast<u4v*>(d) = e;
-        *reinterpret_cast<u4v*>(d + ((KS == 3 && MODE == S2) ? I.csh : 1) * PITCH) = od;
+      }
+      if constexpr (ONE) {
+        *reinterpret_cast<u4v*>(img + dA[k]) = e;
+      } else {
+        const bool sw = SWAP && ((code[k] >> 30) & 1);
+        *reinterpret_cast<u4v*>(img + dA[k]) = sw ? od : e;
+        *reinterpret_cast<u4v*>(img + dB[k]) = sw ? e : od;
       }
     }
   }
@@ -459,7 +488,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
   Wt.load(wp, g.cout, co0, tid);
   for (int cc = 0; cc < nchunk; ++cc) {
     __syncthreads();
-    S.store(simg, I);
+    S.store(simg);
     Wt.store(sw, tid);
     __syncthreads();
     if (cc + 1 < nchunk) {  // the next chunk's loads, in flight during this chunk's MFMAs
@@ -489,22 +518,21 @@ __global__ void __launch_bounds__(64 * NW, 1)
       const int m = mt * 32 + 8 * q + 4 * h;
       int r, c;
       const bool ok = pix_of(g, P, m, r, c);
-      const bf16 b0 = mde::f2bf(acc[i][4 * q]), b1 = mde::f2bf(acc[i][4 * q + 1]);
-      const bf16 b2 = mde::f2bf(acc[i][4 * q + 2]), b3 = mde::f2bf(acc[i][4 * q + 3]);
+      const uint32_t p01 = pack2bf(acc[i][4 * q], acc[i][4 * q + 1]);
+      const uint32_t p23 = pack2bf(acc[i][4 * q + 2], acc[i][4 * q + 3]);
       if constexpr (STATS) {
+        const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
+        const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
         if (!have_ref) {  // one shift per channel and wave: lane (co, h = 0)'s first value
-          const float v0 = __shfl(mde::bf2f(b0), l32, 64);
-          run.ref = v0;
+          run.ref = __shfl(v0, l32, 64);
           have_ref = true;
         }
-        mde::sh_add(run, mde::bf2f(b0), ok);
-        mde::sh_add(run, mde::bf2f(b1), ok);
-        mde::sh_add(run, mde::bf2f(b2), ok);
-        mde::sh_add(run, mde::bf2f(b3), ok);
+        mde::sh_add(run, v0, ok);
+        mde::sh_add(run, v1, ok);
+        mde::sh_add(run, v2, ok);
+        mde::sh_add(run, v3, ok);
       }
-      if (ok)
-        *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) =
-            u2v{(uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16)};
+      if (ok) *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
     }
   }
   if constexpr (STATS) {
@@ -620,7 +648,7 @@ __global__ void __launch_bounds__(256, 1)
   int q = q0, cc = 0;
   while (true) {
     __syncthreads();  // previous step's image readers are done (1st: the filter DMA drained)
-    S.store(simg, I);
+    S.store(simg);
     __syncthreads();
     int qn = q, ccn = cc + 1;
     if (ccn == nch) {
@@ -655,21 +683,21 @@ __global__ void __launch_bounds__(256, 1)
             const int m = mt * 32 + 8 * qq + 4 * h;
             int r, c;
             const bool ok = pix_of(g, P, m, r, c);
-            const bf16 b0 = mde::f2bf(acc[i][4 * qq]), b1 = mde::f2bf(acc[i][4 * qq + 1]);
-            const bf16 b2 = mde::f2bf(acc[i][4 * qq + 2]), b3 = mde::f2bf(acc[i][4 * qq + 3]);
+            const uint32_t p01 = pack2bf(acc[i][4 * qq], acc[i][4 * qq + 1]);
+            const uint32_t p23 = pack2bf(acc[i][4 * qq + 2], acc[i][4 * qq + 3]);
             if constexpr (STATS) {
+              const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
+              const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
               if (!have_ref) {
-                run.ref = __shfl(mde::bf2f(b0), l32, 64);
+                run.ref = __shfl(v0, l32, 64);
                 have_ref = true;
               }
-              mde::sh_add(run, mde::bf2f(b0), ok);
-              mde::sh_add(run, mde::bf2f(b1), ok);
-              mde::sh_add(run, mde::bf2f(b2), ok);
-              mde::sh_add(run, mde::bf2f(b3), ok);
+              mde::sh_add(run, v0, ok);
+              mde::sh_add(run, v1, ok);
+              mde::sh_add(run, v2, ok);
+              mde::sh_add(run, v3, ok);
             }
-            if (ok)
-              *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) =
-                  u2v{(uint32_t)b0 | ((uint32_t)b1 << 16), (uint32_t)b2 | ((uint32_t)b3 << 16)};
+            if (ok) *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
           }
         }
 #pragma unroll
@@ -773,7 +801,7 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
     const Patch P = patch_of(g, q);
     const Img I = img_of<KS, MODE>(g, P);
     __syncthreads();
-    S.store(simg, I);
+    S.store(simg);
 #pragma unroll
     for (int k = 0; k < GU; ++k) {
       const int u = tid + NT * k;
@@ -796,21 +824,47 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
     int toff[ND];
 #pragma unroll
     for (int d = 0; d < ND; ++d) toff[d] = KS == 3 ? tap_off<KS, MODE>(I, wy, d) : 0;
-    const int nks = (P.npx + 15) >> 4;
-    for (int ks = (KS == 3 ? 0 : wy); ks < nks; ks += (KS == 3 ? 1 : 2)) {
-      const u4v a = *reinterpret_cast<const u4v*>(sg + arow + 16 * ks);
+    // every k-step of the patch, straight-line (a partial patch's extra steps
+    // multiply zero gy rows: no branch around an MFMA), the next step's
+    // operands read one step ahead; the staged-pixel offsets of all steps
+    // first (tab), so no read waits on another
+    constexpr int NKS = kMBW / 16 / (KS == 3 ? 1 : 2);
+    int tq[NKS][2];
+#pragma unroll
+    for (int j = 0; j < NKS; ++j) {
+      const int ks = KS == 3 ? j : 2 * j + wy;
       const int m0 = 16 * ks + 8 * (gq >> 1) + qr;
-      const int t0 = tab[m0], t1 = tab[m0 + 4];
+      tq[j][0] = tab[m0] * kPitchW + bcol;
+      tq[j][1] = tab[m0 + 4] * kPitchW + bcol;
+    }
+    u4v aq[2];
+    s4v lq[2][ND], hq[2][ND];
+    auto ld = [&](auto j_c, auto slot_c) {
+      constexpr int j = decltype(j_c)::value, slot = decltype(slot_c)::value;
+      constexpr int ks = KS == 3 ? j : -1;
+      const int kk = KS == 3 ? ks : 2 * j + wy;
+      aq[slot] = *reinterpret_cast<const u4v*>(sg + arow + 16 * kk);
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s4*)(simg + (t0 + toff[d]) * kPitchW + bcol));
-        const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s4*)(simg + (t1 + toff[d]) * kPitchW + bcol));
-        const u2v l2 = __builtin_bit_cast(u2v, lo), h2 = __builtin_bit_cast(u2v, hi);
-        acc[d] = mfma32(a, u4v{l2.x, l2.y, h2.x, h2.y}, acc[d]);
+        lq[slot][d] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(simg + tq[j][0] + toff[d] * kPitchW));
+        hq[slot][d] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_s4*)(simg + tq[j][1] + toff[d] * kPitchW));
       }
-    }
+    };
+    ld(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    static_for<NKS>([&](auto j_c) {
+      constexpr int j = decltype(j_c)::value;
+      if constexpr (j + 1 < NKS)
+        ld(std::integral_constant<int, j + 1>{}, std::integral_constant<int, (j + 1) & 1>{});
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const u2v l2 = __builtin_bit_cast(u2v, lq[j & 1][d]), h2 = __builtin_bit_cast(u2v, hq[j & 1][d]);
+        acc[d] = mfma32(aq[j & 1], u4v{l2.x, l2.y, h2.x, h2.y}, acc[d]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
   }
 
   // D[co][ci]: lane (ci = l32, h), register r -> co row (r & 3) + 8 (r >> 2) + 4 h

@@ -51,10 +51,13 @@ def pmc_files(workload: str, amp: str) -> list[str]:
     return files
 
 
-AMP_DTYPE = ("bf16 autocast: 16->16 / 32->32 3x3 convs on the HIP bf16 MFMA kernels (fp32 "
-             "accumulation), other convs / GEMMs bf16 (MIOpen / hipBLASLt); HIP BatchNorm, "
-             "BN-ReLU-1x1, skip fusion, SE-over-BN and x2 resize kernels bf16 I/O with fp32 "
-             "statistics / accumulation; other HIP kernels (guide conv3x3, DDRNet resizes, loss) fp32")
+AMP_DTYPE = ("bf16 autocast: every 3x3 / 1x1 conv with 32k channels (DDRNet's stride-1 / stride-2 "
+             "convs, the 32-640-channel decoder / DAPPM convs) on the HIP bf16 implicit-GEMM kernels "
+             "(convbf, v_mfma_f32_32x32x16_bf16, fp32 accumulation, fp32 weight gradients), the "
+             "16->16 / 32->32 3x3 convs on the HIP bf16 MFMA kernels, the 3-channel guide convs "
+             "bf16 in-kernel; the 3-channel stem conv bf16 on MIOpen; BatchNorm, BN-ReLU-1x1, skip "
+             "fusion, SE-over-BN and every resize on bf16 activations with fp32 statistics / "
+             "accumulation; SSIM + L1 loss fp32")
 
 
 def parse():

@@ -233,7 +233,7 @@ struct SrcStage {
   static constexpr bool SWAP = PITCH != kPitchF && PAIR_PX;
   uint32_t v[MAXU][8];
   int code[MAXU];  // (swap << 30) | (octet << 28) | (staged row << 16) | column unit, -1: none
-  int dA[MAXU], dB[MAXU];  // element offsets of the first / second store (dB < 0: none)
+  int dA[MAXU];    // element offset of the unit's first store (< 0: none)
 
   __device__ static __forceinline__ int ncol(const Img& I) {
     return ONE ? I.cs : (EO ? I.csh : I.cs >> 1);
@@ -241,8 +241,11 @@ struct SrcStage {
 
   __device__ __forceinline__ void plan(const Img& I, int tid) {
     const int nc = ncol(I), total = 4 * I.rs * nc;
-#pragma unroll
-    for (int k = 0; k < MAXU; ++k) {
+    // static_for, not a counted loop: a loop the compiler keeps rolled (the
+    // division makes the body large) indexes code / dA dynamically and puts
+    // them in scratch, reloaded at every store
+    static_for<MAXU>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
       const int u = tid + NT * k;
       if (u < total) {
         const int o = u & 3, rest = u >> 2;
@@ -254,24 +257,24 @@ struct SrcStage {
         }
         const bool sw = SWAP && (rest & 1);
         code[k] = ((int)sw << 30) | (o << 28) | (i << 16) | jc;
-        int p0, p1;
-        if constexpr (ONE) {
+        int p0;
+        if constexpr (ONE || EO)
           p0 = i * I.cs + jc;
-          p1 = -1;
-        } else if constexpr (EO) {
-          p0 = i * I.cs + jc;
-          p1 = p0 + I.csh;
-        } else {
+        else
           p0 = i * I.cs + 2 * jc;
-          p1 = p0 + 1;
-        }
-        dA[k] = (sw ? p1 : p0) * PITCH + 8 * o;
-        dB[k] = p1 < 0 ? -1 : (sw ? p0 : p1) * PITCH + 8 * o;
+        // the second store sits dB() elements after the first (before it when swapped)
+        dA[k] = (sw ? p0 + 1 : p0) * PITCH + 8 * o;
       } else {
         code[k] = -1;
-        dA[k] = dB[k] = -1;
+        dA[k] = -1;
       }
-    }
+    });
+  }
+
+  // offset of a unit's second store from its first
+  __device__ static __forceinline__ int dB(const Img& I, bool sw) {
+    const int d = EO ? I.csh * PITCH : PITCH;
+    return sw ? -d : d;
   }
 
   __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
@@ -282,8 +285,8 @@ struct SrcStage {
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 2 * g.cin * plane, 0x00020000);
-#pragma unroll
-    for (int k = 0; k < MAXU; ++k) {
+    static_for<MAXU>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
       const int cd = code[k] < 0 ? 0 : code[k];
       const int o = (cd >> 28) & 3, i = (cd >> 16) & 0xfff, jc = cd & 0xffff;
       int sr, sc;
@@ -313,32 +316,33 @@ struct SrcStage {
         else
           v[k][j] = __builtin_amdgcn_raw_buffer_load_b32(R, voff, soff, 0);
       }
-    }
+    });
   }
 
-  __device__ __forceinline__ void store(bf16* img) const {
+  __device__ __forceinline__ void store(bf16* img, const Img& I) const {
+    static_for<MAXU>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
+      if (dA[k] >= 0) {
+        u4v e, od;
 #pragma unroll
-    for (int k = 0; k < MAXU; ++k) {
-      if (dA[k] < 0) continue;
-      u4v e, od;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if constexpr (MODE == U2) {
-          e[j] = v[k][2 * j] | (v[k][2 * j + 1] << 16);
-          od[j] = 0u;
+        for (int j = 0; j < 4; ++j) {
+          if constexpr (MODE == U2) {
+            e[j] = v[k][2 * j] | (v[k][2 * j + 1] << 16);
+            od[j] = 0u;
+          } else {
+            e[j] = lo16x2(v[k][2 * j], v[k][2 * j + 1]);
+            od[j] = hi16x2(v[k][2 * j], v[k][2 * j + 1]);
+          }
+        }
+        if constexpr (ONE) {
+          *reinterpret_cast<u4v*>(img + dA[k]) = e;
         } else {
-          e[j] = lo16x2(v[k][2 * j], v[k][2 * j + 1]);
-          od[j] = hi16x2(v[k][2 * j], v[k][2 * j + 1]);
+          const bool sw = SWAP && ((code[k] >> 30) & 1);
+          *reinterpret_cast<u4v*>(img + dA[k]) = sw ? od : e;
+          *reinterpret_cast<u4v*>(img + dA[k] + dB(I, sw)) = sw ? e : od;
         }
       }
-      if constexpr (ONE) {
-        *reinterpret_cast<u4v*>(img + dA[k]) = e;
-      } else {
-        const bool sw = SWAP && ((code[k] >> 30) & 1);
-        *reinterpret_cast<u4v*>(img + dA[k]) = sw ? od : e;
-        *reinterpret_cast<u4v*>(img + dB[k]) = sw ? e : od;
-      }
-    }
+    });
   }
 };
 
@@ -378,7 +382,7 @@ struct WStage {
 
 // The MFMAs of one staged chunk: (tap, k-half) steps over the filter rows in
 // DYM (a compile-time mask: U2 tiles skip the all-zero rows), each step's B
-// (filter) and A (image) fragments read one step ahead (two register slots),
+// (filter) and A (image) fragments read PD steps ahead,
 // straight-line code -- no branch around an MFMA (a branch made the compiler
 // copy the accumulators between AGPRs and VGPRs at every one).
 template <int KS, int DYM, int MTW, int PITCH_A>
@@ -400,25 +404,28 @@ __device__ __forceinline__ void chunk_mfmas(const bf16* __restrict__ swc, int nb
       }
     return row;
   };
-  u4v bq[2], aq[2][MTW];
-  auto ld = [&](auto s_c, auto slot_c) {
-    constexpr int s = decltype(s_c)::value, slot = decltype(slot_c)::value;
+  // reads run PD steps ahead of the MFMAs (PD + 1 register slots): at one
+  // wave per SIMD nothing else hides an LDS read's latency, and one step
+  // (MTW MFMAs) is shorter than it
+  constexpr int PD = 2, NSL = PD + 1;
+  u4v bq[NSL], aq[NSL][MTW];
+  auto ld = [&](auto s_c) {
+    constexpr int s = decltype(s_c)::value, slot = s % NSL;
     constexpr int t = tap_of(s), ks = s & 1;
     bq[slot] = *reinterpret_cast<const u4v*>(swc + t * nbrow + (ks ? boff1 : boff0));
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
       aq[slot][i] = *reinterpret_cast<const u4v*>(simg + abase[i] + toff[t] + 16 * ks + 8 * h);
   };
-  ld(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+  static_for<PD < NS ? PD : NS>([&](auto s_c) { ld(s_c); });
   static_for<NS>([&](auto s_c) {
     constexpr int s = decltype(s_c)::value;
-    if constexpr (s + 1 < NS)
-      ld(std::integral_constant<int, s + 1>{}, std::integral_constant<int, (s + 1) & 1>{});
-    // keep the next step's reads here: the scheduler otherwise sinks each read
+    if constexpr (s + PD < NS) ld(std::integral_constant<int, s + PD>{});
+    // keep the next steps' reads here: the scheduler otherwise sinks each read
     // next to its MFMA and every MFMA waits out an LDS latency
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) acc[i] = mfma32(aq[s & 1][i], bq[s & 1], acc[i]);
+    for (int i = 0; i < MTW; ++i) acc[i] = mfma32(aq[s % NSL][i], bq[s % NSL], acc[i]);
     __builtin_amdgcn_sched_barrier(0);
   });
 }
@@ -488,7 +495,7 @@ __global__ void __launch_bounds__(64 * NW, 1)
   Wt.load(wp, g.cout, co0, tid);
   for (int cc = 0; cc < nchunk; ++cc) {
     __syncthreads();
-    S.store(simg);
+    S.store(simg, I);
     Wt.store(sw, tid);
     __syncthreads();
     if (cc + 1 < nchunk) {  // the next chunk's loads, in flight during this chunk's MFMAs
@@ -638,80 +645,76 @@ __global__ void __launch_bounds__(256, 1)
   };
   setup(P, I);
   f16v acc[MTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
   mde::Sh run{0.f, 0.f, 0.f, 0.f};
   bool have_ref = false;
 
-  int q = q0, cc = 0;
-  while (true) {
-    __syncthreads();  // previous step's image readers are done (1st: the filter DMA drained)
-    S.store(simg);
-    __syncthreads();
-    int qn = q, ccn = cc + 1;
-    if (ccn == nch) {
-      ccn = 0;
-      ++qn;
-    }
+  // patch-outer, chunk-inner: the accumulators are zeroed and drained once per
+  // patch outside the chunk loop, so its back edge carries them in AGPRs (a
+  // single flat (patch, chunk) loop made the compiler copy all of them to
+  // VGPRs and back at every step)
+  for (int q = q0; q < q1; ++q) {
     Patch Pn = P;
     Img In = I;
-    if (qn < q1) {  // the next step's input chunk, in flight during this step's MFMAs
-      if (qn != q) {
-        Pn = patch_of(g, qn);
-        In = img_of<KS, MODE>(g, Pn);
-      }
-      S.load(x + (int64_t)Pn.img * xplane, g, In, 32 * ccn);
+    if (q + 1 < q1) {
+      Pn = patch_of(g, q + 1);
+      In = img_of<KS, MODE>(g, Pn);
     }
-    const bf16* swc = sw + cc * KK * NB * 32;
-    // U2 skips a filter row only when all of the wave's tiles do
-    if (MODE == U2 && KS == 3 && wdymask == 2)
-      chunk_mfmas<KS, 2, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
-    else if (MODE == U2 && KS == 3 && wdymask == 5)
-      chunk_mfmas<KS, 5, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
-    else
-      chunk_mfmas<KS, 7, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
-    if (cc == nch - 1) {  // the patch is complete: bf16 output (+ statistics)
-      bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col) * hwo;
 #pragma unroll
-      for (int i = 0; i < MTW; ++i) {
-        if (mt_on[i]) {
-          const int mt = MTW * wm + i;
+    for (int i = 0; i < MTW; ++i)
 #pragma unroll
-          for (int qq = 0; qq < 4; ++qq) {
-            const int m = mt * 32 + 8 * qq + 4 * h;
-            int r, c;
-            const bool ok = pix_of(g, P, m, r, c);
-            const uint32_t p01 = pack2bf(acc[i][4 * qq], acc[i][4 * qq + 1]);
-            const uint32_t p23 = pack2bf(acc[i][4 * qq + 2], acc[i][4 * qq + 3]);
-            if constexpr (STATS) {
-              const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
-              const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
-              if (!have_ref) {
-                run.ref = __shfl(v0, l32, 64);
-                have_ref = true;
-              }
-              mde::sh_add(run, v0, ok);
-              mde::sh_add(run, v1, ok);
-              mde::sh_add(run, v2, ok);
-              mde::sh_add(run, v3, ok);
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    for (int cc = 0; cc < nch; ++cc) {
+      __syncthreads();  // previous step's image readers are done (1st: the filter DMA drained)
+      S.store(simg, I);
+      __syncthreads();
+      // the next step's input chunk, in flight during this step's MFMAs
+      if (cc + 1 < nch)
+        S.load(x + (int64_t)P.img * xplane, g, I, 32 * (cc + 1));
+      else if (q + 1 < q1)
+        S.load(x + (int64_t)Pn.img * xplane, g, In, 0);
+      const bf16* swc = sw + cc * KK * NB * 32;
+      // U2 skips a filter row only when all of the wave's tiles do
+      if (MODE == U2 && KS == 3 && wdymask == 2)
+        chunk_mfmas<KS, 2, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+      else if (MODE == U2 && KS == 3 && wdymask == 5)
+        chunk_mfmas<KS, 5, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+      else
+        chunk_mfmas<KS, 7, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+    }
+    // the patch is complete: bf16 output (+ statistics)
+    bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col) * hwo;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      if (mt_on[i]) {
+        const int mt = MTW * wm + i;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) {
+          const int m = mt * 32 + 8 * qq + 4 * h;
+          int r, c;
+          const bool ok = pix_of(g, P, m, r, c);
+          const uint32_t p01 = pack2bf(acc[i][4 * qq], acc[i][4 * qq + 1]);
+          const uint32_t p23 = pack2bf(acc[i][4 * qq + 2], acc[i][4 * qq + 3]);
+          if constexpr (STATS) {
+            const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
+            const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
+            if (!have_ref) {
+              run.ref = __shfl(v0, l32, 64);
+              have_ref = true;
             }
-            if (ok) *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
+            mde::sh_add(run, v0, ok);
+            mde::sh_add(run, v1, ok);
+            mde::sh_add(run, v2, ok);
+            mde::sh_add(run, v3, ok);
           }
+          if (ok) *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
         }
-#pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
       }
     }
-    if (qn >= q1) break;
-    if (qn != q) {
+    if (q + 1 < q1) {
       P = Pn;
       I = In;
       setup(P, I);
     }
-    q = qn;
-    cc = ccn;
   }
   if constexpr (STATS) {  // one record per channel and block
     run = mde::sh_xor_sum(run, 32);
@@ -801,7 +804,7 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
     const Patch P = patch_of(g, q);
     const Img I = img_of<KS, MODE>(g, P);
     __syncthreads();
-    S.store(simg);
+    S.store(simg, I);
 #pragma unroll
     for (int k = 0; k < GU; ++k) {
       const int u = tid + NT * k;

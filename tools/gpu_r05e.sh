@@ -22,3 +22,8 @@ ks = sorted(d["hip_kernels"].items(), key=lambda kv: -kv[1]["ms_per_step"])[:25]
 for k, v in ks:
     print(f"{k:28s} {v['ms_per_step']:7.3f} ms/step  {v.get('TFLOPs', '')}")
 PY
+# steady-state kernel trace of the bf16 step
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o gd_bf16 -- python3 -u bench.py --no-cpu-baseline --amp bf16 --steps 8 --warmup 3 > $OUT/prof_bf16.log 2>&1 || exit 1
+f=$(ls $OUT/prof/*/gd_bf16_kernel_trace.csv 2>/dev/null | head -n 1)
+[ -n "$f" ] || f=$(find $OUT/prof -name '*kernel_trace.csv' | head -n 1)
+python3 tools/trace_steps.py "$f" --steps 8 --top 40 > $OUT/gd_bf16_steady_state.txt && head -n 60 $OUT/gd_bf16_steady_state.txt

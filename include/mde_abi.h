@@ -705,6 +705,13 @@ int mde_graph_replace_memsets(void* graph, int64_t* replaced);
  * Returns the previous mode. */
 int mde_bn_chan_mode(int mode);
 
+/* How mde_batchnorm_fwd_train_stats uses a producer's statistics records for
+ * this shape: 0 not at all (the one-launch small-tensor kernel runs), 1 merged
+ * by the apply kernel itself (plane mode, stats_blocks <= 256), 2 one merge
+ * launch before the apply; -1 invalid arguments. */
+int mde_batchnorm_stats_route(int64_t n, int64_t c, int64_t h, int64_t w, int64_t stats_blocks,
+                              int dtype);
+
 /* ---------------------------------------------------------------------------
  * bf16 convolutions, NCHW, any cin / cout multiple of 32, 3x3 (padding 1) or
  * 1x1 (padding 0), stride 1 or 2, input width even (v_mfma_f32_32x32x16_bf16,
@@ -718,7 +725,8 @@ int mde_bn_chan_mode(int mode);
  * data gradient, 2 weight gradient (shape and LDS-capacity rules).
  * mde_convbf_pack: the filter of one pass as packed bf16 [cin/32][ks*ks][cout]
  * [32] (transpose = 0, the forward) or of the data gradient (transpose = 1:
- * channels swapped, taps flipped), mde_convbf_pack_elems elements.
+ * channels swapped, taps flipped), mde_convbf_pack_elems elements;
+ * mde_convbf_pack_both: both in one launch (either output nullable).
  * mde_convbf_fwd: y from x and the forward pack; stats (nullable) receives the
  * following BatchNorm's per-block shifted sums [cout][blocks][4] (blocks =
  * mde_convbf_stats_blocks).  mde_convbf_bwd_data: gx [n,cin,h,w] from gy and
@@ -732,6 +740,8 @@ int mde_convbf_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks
 size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose);
 int mde_convbf_pack(const float* weight, void* packed, int64_t cin, int64_t cout, int ks,
                     int transpose, void* stream);
+int mde_convbf_pack_both(const float* weight, void* packed, void* packed_t, int64_t cin,
+                         int64_t cout, int ks, void* stream);
 int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
                             int stride);
 int mde_convbf_fwd(const void* x, const void* packed, void* y, float* stats, int64_t n,

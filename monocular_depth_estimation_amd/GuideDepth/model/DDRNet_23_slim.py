@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from ...functional import bilinear_resize
-from ...nn import BatchNorm2d, Conv2d, conv_nobias, run_sequential
+from ...nn import BatchNorm2d, Conv2d, conv_nobias_stats, run_sequential
 
 BN_MOMENTUM = 0.1
 
@@ -31,6 +31,13 @@ def _bn(c, act="none"):
 def conv3x3(in_planes, out_planes, stride=1):
     """3x3 convolution, padding 1, no bias (reference :35-38)."""
     return Conv2d(in_planes, out_planes, 3, stride=stride, padding=1, bias=False)
+
+
+def _conv_stats(conv, x, bn):
+    """(y, stats) positional arguments of bn: conv(x) without a bias and its BN
+    statistics from the conv's epilogue (nn.conv_nobias_stats)."""
+    y, st = conv_nobias_stats(conv, x, bn)
+    return y, None, None, st
 
 
 class BasicBlock(nn.Module):
@@ -52,11 +59,12 @@ class BasicBlock(nn.Module):
         self.no_relu = no_relu
 
     def forward(self, x):
-        # bias-free 3x3 convs: the 32->32 weight gradients run on the HIP MFMA
-        # kernel (nn.CONV3X3_HIP), the rest on MIOpen
-        y = self.bn1(conv_nobias(self.conv1, x))
-        res = x if self.downsample is None else self.downsample(x)
-        return self.bn2(conv_nobias(self.conv2, y), residual=res)
+        # bias-free 3x3 convs on the HIP kernels where they apply (conv_nobias);
+        # in training each BN takes its batch statistics from the conv's epilogue
+        y = self.bn1(*_conv_stats(self.conv1, x, self.bn1))
+        res = x if self.downsample is None else run_sequential(self.downsample, x)
+        y, st = conv_nobias_stats(self.conv2, y, self.bn2)
+        return self.bn2(y, residual=res, stats=st)
 
 
 class Bottleneck(nn.Module):
@@ -76,9 +84,11 @@ class Bottleneck(nn.Module):
         self.no_relu = no_relu
 
     def forward(self, x):
-        y = self.bn2(self.conv2(self.bn1(self.conv1(x))))
-        res = x if self.downsample is None else self.downsample(x)
-        return self.bn3(self.conv3(y), residual=res)
+        y = self.bn1(*_conv_stats(self.conv1, x, self.bn1))
+        y = self.bn2(*_conv_stats(self.conv2, y, self.bn2))
+        res = x if self.downsample is None else run_sequential(self.downsample, x)
+        y, st = conv_nobias_stats(self.conv3, y, self.bn3)
+        return self.bn3(y, residual=res, stats=st)
 
 
 def _pre_act(cin, cout, k, pool=None):
@@ -157,9 +167,10 @@ def _make_layer(block, inplanes, planes, blocks, stride=1):
 def _seq_bn_residual(seq, x, residual):
     """residual + seq(x) for a Sequential ending in a BatchNorm: the add runs in the BN pass.
     Its bias-free convs go through conv_nobias (HIP kernels where they apply)."""
-    for m in list(seq)[:-1]:
-        x = conv_nobias(m, x) if isinstance(m, nn.Conv2d) and m.bias is None else m(x)
-    return seq[-1](x, residual=residual)
+    mods = list(seq)
+    x = run_sequential(mods[:-2], x) if len(mods) > 2 else x
+    y, st = conv_nobias_stats(mods[-2], x, mods[-1])
+    return mods[-1](y, residual=residual, stats=st)
 
 
 class DualResNet(nn.Module):
@@ -206,11 +217,11 @@ class DualResNet(nn.Module):
         l3 = self.layer3(rl2)
         high = self.layer3_(rl2)
         low = _seq_bn_residual(self.down3, r(high), l3)  # l3 + down3(relu(high)), add fused into BN
-        high = high + bilinear_resize(self.compression3(r(l3)), size=out_size)
+        high = high + bilinear_resize(run_sequential(self.compression3, r(l3)), size=out_size)
         l4 = self.layer4(r(low))
         high = self.layer4_(r(high))
         low = _seq_bn_residual(self.down4, r(high), l4)
-        high = high + bilinear_resize(self.compression4(r(l4)), size=out_size)
+        high = high + bilinear_resize(run_sequential(self.compression4, r(l4)), size=out_size)
         high = self.layer5_(r(high))
         low = bilinear_resize(self.spp(self.layer5(r(low))), size=out_size)
         return self.final_layer(low + high)

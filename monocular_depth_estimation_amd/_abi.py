@@ -154,10 +154,12 @@ SIGNATURES = {
     "mde_wino_conv_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int,
                                    _vp]),
     "mde_wino_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),
+    "mde_batchnorm_stats_route": (_int, [_i64, _i64, _i64, _i64, _i64, _int]),
     "mde_bn_chan_mode": (_int, [_int]),
     "mde_convbf_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int, _int]),
     "mde_convbf_pack_elems": (_sz, [_i64, _i64, _int, _int]),
     "mde_convbf_pack": (_int, [_vp, _vp, _i64, _i64, _int, _int, _vp]),
+    "mde_convbf_pack_both": (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp]),
     "mde_convbf_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64, _int, _int]),
     "mde_convbf_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_convbf_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),

@@ -34,6 +34,7 @@ namespace {
 constexpr int kTarget = 2048;    // blocks to aim for per reduction launch
 constexpr int kMinSlice = 4096;  // elements per slice at least
 constexpr int kPlaneChunk4 = 1024;  // float4 per apply block in plane mode
+constexpr int64_t kMaxApplyRecords = 256;  // producer records a plane-mode apply block merges itself
 
 struct Geo {
   int64_t c, hw, total;  // total = n * hw elements per channel
@@ -104,6 +105,23 @@ __device__ __forceinline__ void wave_slices(const float* part, int64_t ch,
   *b = wave_sum_d(y);
 }
 
+// Shifted sums of channel ch about `ref` from producer records (shift r, count
+// n, s1, s2): s1 + n d and s2 + d (2 s1 + n d), d = r - ref, in double, a
+// fixed lane-strided order and butterfly (deterministic); every lane gets them.
+__device__ __forceinline__ void wave_records(const float* rec, int64_t ch, int nrec, double ref,
+                                             double* a, double* b) {
+  const int lane = threadIdx.x & 63;
+  double x = 0.0, y = 0.0;
+  for (int k = lane; k < nrec; k += 64) {
+    const float4 q = *reinterpret_cast<const float4*>(rec + (ch * nrec + k) * 4);
+    const double n = (double)q.y, d = (double)q.x - ref, b1 = (double)q.z;
+    x += b1 + n * d;
+    y += (double)q.w + d * (2.0 * b1 + n * d);
+  }
+  *a = wave_sum_d(x);
+  *b = wave_sum_d(y);
+}
+
 // Per-channel forward constants.  mean_x is the mean of the RAW input x
 // (without the folded bias); scale/shift act on raw x.
 struct FwdCh {
@@ -125,6 +143,10 @@ struct FwdArgs {
   float* save_mean;
   float* save_invstd;
   int training;
+  // producer-emitted per-block records [c][nrec][4] = (shift, count, s1, s2),
+  // merged by the plane-mode apply itself (nullable: then `part`)
+  const float* rec;
+  int nrec;
 };
 
 // Training: (s1, s2) are the shifted sums of channel ch (shift = its first
@@ -291,7 +313,12 @@ __global__ void __launch_bounds__(256)
   }
   if (threadIdx.x < 64) {
     double s1 = 0.0, s2 = 0.0;
-    if (A.training) wave_slices(A.part, ch, A.slices, &s1, &s2);
+    if (A.training) {
+      if (A.rec)
+        wave_records(A.rec, ch, A.nrec, (double)ld1(x + ch * hw), &s1, &s2);
+      else
+        wave_slices(A.part, ch, A.slices, &s1, &s2);
+    }
     if (threadIdx.x == 0) {
       const bool owner = blockIdx.x == 0 && plane < c;
       const FwdCh k = fwd_channel(A, x, ch, s1, s2, owner);
@@ -1012,6 +1039,14 @@ bool dtype_ok(int dtype) { return dtype == MDE_F32 || dtype == MDE_BF16; }
 
 extern "C" {
 
+int mde_batchnorm_stats_route(int64_t n, int64_t c, int64_t h, int64_t w, int64_t stats_blocks,
+                              int dtype) {
+  if (!dtype_ok(dtype) || !args_ok(n, c, h, w)) return -1;
+  const int64_t hw = h * w;
+  if (dtype == MDE_BF16 ? chan_mode<bf16>(n, hw) : chan_mode<float>(n, hw)) return 0;
+  return plane_mode(hw) && stats_blocks > 0 && stats_blocks <= kMaxApplyRecords ? 1 : 2;
+}
+
 int mde_bn_chan_mode(int mode) {
   const int old = g_chan_mode;
   if (mode >= 0) g_chan_mode = mode > 2 ? 2 : mode;
@@ -1140,7 +1175,23 @@ int mde_batchnorm_fwd_train_stats(const void* x, const float* gamma, const float
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t hw = h * w;
+  // small tensors: the one-launch kernel (statistics + apply reading x once)
+  // beats a merge launch + apply; the emitted records go unused
+  if (dtype == MDE_BF16 ? chan_mode<bf16>(n, hw) : chan_mode<float>(n, hw))
+    return mde_batchnorm_fwd_train(x, gamma, beta, prebias, running_mean, running_var,
+                                   num_batches_tracked, momentum, eps, residual, y, save_mean,
+                                   save_invstd, n, c, h, w, act, workspace, dtype, stream);
   float* part = (float*)workspace;
+  if (plane_mode(hw) && stats_blocks <= kMaxApplyRecords) {
+    // few records a channel: the plane-mode apply merges them in its prologue
+    // (no merge launch)
+    FwdArgs A{gamma, beta, prebias, part, 0, n * hw, hw, eps, momentum, running_mean,
+              running_var, num_batches_tracked, save_mean, save_invstd, 1, stats,
+              (int)stats_blocks};
+    if (dtype == MDE_BF16)
+      return launch_fwd_apply((const bf16*)x, (const bf16*)residual, (bf16*)y, n, c, hw, act, A, s);
+    return launch_fwd_apply((const float*)x, (const float*)residual, (float*)y, n, c, hw, act, A, s);
+  }
   const double mb = 16.0 * (double)c * stats_blocks;
   if (dtype == MDE_BF16)
     MDE_LAUNCH(mde::K_BN_FINAL, mb, s, (bn_stats_merge_kernel<bf16, false>), dim3((unsigned)c),

@@ -54,6 +54,7 @@ using bf8v = __bf16 __attribute__((ext_vector_type(8)));
 using f16v = float __attribute__((ext_vector_type(16)));
 using u4v = uint32_t __attribute__((ext_vector_type(4)));
 using u2v = uint32_t __attribute__((ext_vector_type(2)));
+using f4v = float __attribute__((ext_vector_type(4)));
 using s4v = short __attribute__((ext_vector_type(4)));
 using lds_s4 = __attribute__((address_space(3))) s4v;
 
@@ -905,32 +906,36 @@ template <int KK>
 __global__ void __launch_bounds__(256)
     convbf_wreduce_kernel(const float* __restrict__ part, float* __restrict__ gw, int S, int cin,
                           int cout) {
-  constexpr int ME = 64 * KK * 32;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= ME) return;
+  // block: 256 consecutive partial elements (64 float4 columns) x 4 split
+  // slices; slice sl sums splits sl, sl + 4, ... in order, then slice 0 adds
+  // the four in order: a fixed summation order (bitwise-repeatable), 16-byte
+  // loads, and S / 4 of them in flight per thread instead of a serial chain of S
+  constexpr int ME = 64 * KK * 32, SL = 4;
+  const int tid = threadIdx.x, qd = tid & 63, sl = tid >> 6;
+  const int e4 = blockIdx.x * 256 + 4 * qd;
   const int grp = blockIdx.y, ngo = (cout + 63) >> 6, cob = grp % ngo, cc = grp / ngo;
-  const float* p = part + (int64_t)grp * S * ME + e;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int s = 0;
-  for (; s + 3 < S; s += 4) {
-    a0 += p[(int64_t)s * ME];
-    a1 += p[(int64_t)(s + 1) * ME];
-    a2 += p[(int64_t)(s + 2) * ME];
-    a3 += p[(int64_t)(s + 3) * ME];
+  const f4v* p = reinterpret_cast<const f4v*>(part + (int64_t)grp * S * ME + e4);
+  f4v a = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+  for (int s = sl; s < S; s += SL) a += p[(int64_t)s * (ME / 4)];
+  __shared__ f4v red[SL][64];
+  red[sl][qd] = a;
+  __syncthreads();
+  if (sl) return;
+  const f4v t = ((red[0][qd] + red[1][qd]) + red[2][qd]) + red[3][qd];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int e = e4 + j;
+    const int col = e / (KK * 32), rest = e - col * KK * 32, tap = rest / 32, ci = rest % 32;
+    if (cob * 64 + col < cout) gw[((int64_t)(cob * 64 + col) * cin + cc * 32 + ci) * KK + tap] = t[j];
   }
-  for (; s < S; ++s) a0 += p[(int64_t)s * ME];
-  const int col = e / (KK * 32), rest = e - col * KK * 32, tap = rest / 32, ci = rest % 32;
-  if (cob * 64 + col >= cout) return;
-  gw[((int64_t)(cob * 64 + col) * cin + cc * 32 + ci) * KK + tap] = (a0 + a1) + (a2 + a3);
 }
 
-// packed filter [cc][tap][co][32] (bf16, RNE) of the pass: forward (w[co][ci][tap]) or
-// transposed + flipped (data gradient: the pass's input channels are the forward's outputs)
-__global__ void __launch_bounds__(256)
-    convbf_pack_kernel(const float* __restrict__ w, bf16* __restrict__ p, int cin, int cout, int kk,
-                       int transpose, int64_t total) {
-  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (e >= total) return;
+// packed filter [cc][tap][co][32] (bf16, RNE) of a pass: forward (w[co][ci][tap])
+// into p0, transposed + flipped (data gradient: the pass's input channels are
+// the forward's outputs) into p1; either may be null (one launch packs both)
+__device__ __forceinline__ bf16 pack_elem(const float* __restrict__ w, int64_t e, int cin, int cout,
+                                          int kk, bool transpose) {
   const int pco = transpose ? cin : cout, pci = transpose ? cout : cin;
   const int j = (int)(e & 31);
   int64_t rest = e >> 5;
@@ -946,7 +951,15 @@ __global__ void __launch_bounds__(256)
   if (ci < pci)
     v = transpose ? w[((int64_t)ci * cin + co) * kk + (kk - 1 - tap)]
                   : w[((int64_t)co * cin + ci) * kk + tap];
-  p[e] = mde::f2bf(v);
+  return mde::f2bf(v);
+}
+
+__global__ void __launch_bounds__(256)
+    convbf_pack_kernel(const float* __restrict__ w, bf16* __restrict__ p0, bf16* __restrict__ p1,
+                       int cin, int cout, int kk, int64_t total0, int64_t total1) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (p0 && e < total0) p0[e] = pack_elem(w, e, cin, cout, kk, false);
+  if (p1 && e < total1) p1[e] = pack_elem(w, e, cin, cout, kk, true);
 }
 
 // ------------------------------------------------------------------- host
@@ -1249,15 +1262,24 @@ size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose) {
   return (size_t)(mde::cdiv(pci, 32) * 32 * pco * ks * ks);
 }
 
+int mde_convbf_pack_both(const float* weight, void* packed, void* packed_t, int64_t cin,
+                         int64_t cout, int ks, void* stream) {
+  if (!weight || (!packed && !packed_t) || (ks != 1 && ks != 3) || cin <= 0 || cout <= 0)
+    return MDE_ERR_INVALID_ARG;
+  const int64_t t0 = packed ? (int64_t)mde_convbf_pack_elems(cin, cout, ks, 0) : 0;
+  const int64_t t1 = packed_t ? (int64_t)mde_convbf_pack_elems(cin, cout, ks, 1) : 0;
+  const int64_t total = t0 > t1 ? t0 : t1;
+  MDE_LAUNCH(mde::K_CBF_PACK, 4.0 * cin * cout * ks * ks * ((t0 > 0) + (t1 > 0)) + 2.0 * (t0 + t1),
+             (hipStream_t)stream, convbf_pack_kernel, dim3((unsigned)mde::cdiv(total, 256)), dim3(256),
+             0, weight, (bf16*)packed, (bf16*)packed_t, (int)cin, (int)cout, ks * ks, t0, t1);
+  return MDE_OK;
+}
+
 int mde_convbf_pack(const float* weight, void* packed, int64_t cin, int64_t cout, int ks,
                     int transpose, void* stream) {
-  if (!weight || !packed || (ks != 1 && ks != 3) || cin <= 0 || cout <= 0)
-    return MDE_ERR_INVALID_ARG;
-  const int64_t total = mde_convbf_pack_elems(cin, cout, ks, transpose);
-  MDE_LAUNCH(mde::K_CBF_PACK, 4.0 * cin * cout * ks * ks + 2.0 * total, (hipStream_t)stream,
-             convbf_pack_kernel, dim3((unsigned)mde::cdiv(total, 256)), dim3(256), 0, weight,
-             (bf16*)packed, (int)cin, (int)cout, ks * ks, transpose ? 1 : 0, total);
-  return MDE_OK;
+  if (!packed) return MDE_ERR_INVALID_ARG;
+  return transpose ? mde_convbf_pack_both(weight, nullptr, packed, cin, cout, ks, stream)
+                   : mde_convbf_pack_both(weight, packed, nullptr, cin, cout, ks, stream);
 }
 
 int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,

@@ -788,14 +788,17 @@ class _ConvBf16(torch.autograd.Function):
     """A DDRNet convolution under bf16 autocast (3x3 p1 / 1x1 p0, stride 1 or
     2, channels % 32) on the bf16 implicit-GEMM kernels of convbf.hip:
     autocast's conv semantics -- x cast to bf16, the fp32 weight rounded to
-    bf16 (packed once per pass, mde_convbf_pack), fp32 accumulation, bf16 y /
-    gx, fp32 weight gradient -- in NCHW, with none of MIOpen's NHWC transposes
-    or cast / zero-fill kernels.  DDRNet_23_slim.py:35-38,41-113,121-171,
-    230-263 (every conv of the encoder but the 3-channel stem)."""
+    bf16, fp32 accumulation, bf16 y / gx, fp32 weight gradient -- in NCHW,
+    with none of MIOpen's NHWC transposes or cast / zero-fill kernels.  Both
+    packed filters (forward; transposed for the data gradient) come from one
+    launch in the forward.  want_stats: the following BatchNorm's per-block
+    statistics of y from the forward's epilogue (else an empty tensor).
+    DDRNet_23_slim.py:35-38,41-113,121-171,230-263 (every conv of the encoder
+    but the 3-channel stem)."""
 
     @staticmethod
     @_bn_fwd
-    def forward(ctx, x, weight, ks, stride):
+    def forward(ctx, x, weight, ks, stride, want_stats):
         x = x.to(torch.bfloat16).contiguous()
         weight = weight.contiguous()
         n, cin, h, w = x.shape
@@ -803,20 +806,29 @@ class _ConvBf16(torch.autograd.Function):
         pad = ks // 2
         ho, wo = (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1
         st = _abi.stream_of(x)
-        wp = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 0), dtype=torch.bfloat16,
-                         device=x.device)
-        _abi.call("mde_convbf_pack", _abi.ptr(weight), _abi.ptr(wp), cin, cout, ks, 0, st)
-        y = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device)
-        _abi.call("mde_convbf_fwd", _abi.ptr(x), _abi.ptr(wp), _abi.ptr(y), None, n, cin, cout, h, w,
-                  ks, stride, st)
-        ctx.save_for_backward(x, weight)
+        bf = dict(dtype=torch.bfloat16, device=x.device)
+        wp = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 0), **bf)
+        wt = (torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 1), **bf)
+              if ctx.needs_input_grad[0] else None)
+        _abi.call("mde_convbf_pack_both", _abi.ptr(weight), _abi.ptr(wp), _abi.ptr(wt), cin, cout,
+                  ks, st)
+        y = torch.empty((n, cout, ho, wo), **bf)
+        nb = _abi.query("mde_convbf_stats_blocks", n, cin, cout, h, w, ks, stride) if want_stats else 0
+        stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
+        _abi.call("mde_convbf_fwd", _abi.ptr(x), _abi.ptr(wp), _abi.ptr(y),
+                  _abi.ptr(stats) if nb else None, n, cin, cout, h, w, ks, stride, st)
+        ctx.save_for_backward(x, weight, wt)
         ctx.ks, ctx.stride = ks, stride
-        return y
+        ctx.set_materialize_grads(False)  # no zero-fill launch for the statistics' gradient
+        ctx.mark_non_differentiable(stats)
+        return y, stats
 
     @staticmethod
     @_amp_bwd
-    def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
+    def backward(ctx, gy, _gstats):
+        if gy is None:
+            return None, None, None, None, None
+        x, weight, wt = ctx.saved_tensors
         gy = gy.to(torch.bfloat16).contiguous()
         n, cin, h, w = x.shape
         cout = weight.shape[0]
@@ -824,9 +836,6 @@ class _ConvBf16(torch.autograd.Function):
         st = _abi.stream_of(gy)
         gx = gw = None
         if ctx.needs_input_grad[0]:
-            wt = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 1),
-                             dtype=torch.bfloat16, device=x.device)
-            _abi.call("mde_convbf_pack", _abi.ptr(weight), _abi.ptr(wt), cin, cout, ks, 1, st)
             gx = torch.empty_like(x)
             _abi.call("mde_convbf_bwd_data", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, cin, cout,
                       h, w, ks, stride, st)
@@ -835,7 +844,7 @@ class _ConvBf16(torch.autograd.Function):
             ws = _ws(_abi.query("mde_convbf_wgrad_workspace", n, cin, cout, h, w, ks, stride), x)
             _abi.call("mde_convbf_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cin, cout, h, w,
                       ks, stride, _abi.ptr(ws), st)
-        return gx, gw, None, None
+        return gx, gw, None, None, None
 
 
 CONVBF = os.environ.get("MDE_CONVBF", "1") != "0"  # A/B switch: 0 = MIOpen's bf16 solvers
@@ -867,7 +876,15 @@ def convbf_ok(conv: nn.Conv2d, x) -> bool:
 def conv_bf16(conv: nn.Conv2d, x):
     """conv(x) without its bias on convbf.hip (see convbf_ok)."""
     _gpu(x)
-    return _ConvBf16.apply(x, conv.weight, conv.kernel_size[0], conv.stride[0])
+    return _ConvBf16.apply(x, conv.weight, conv.kernel_size[0], conv.stride[0], False)[0]
+
+
+def conv_bf16_stats(conv: nn.Conv2d, x):
+    """conv_bf16 that also returns y's per-block BN statistics [cout][blocks][4]
+    (shift, count, s1, s2) from the forward epilogue."""
+    _gpu(x)
+    y, stats = _ConvBf16.apply(x, conv.weight, conv.kernel_size[0], conv.stride[0], True)
+    return y, (stats if stats.shape[1] > 0 else None)
 
 
 class _GuideConvBf16(torch.autograd.Function):
@@ -949,13 +966,21 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
     3x3 convs on the HIP MFMA conv3x3 kernel (per pass, CONV3X3_HIP), the rest
     on MIOpen (PyTorch-ROCm)."""
     passes = conv3x3_passes(conv, x) if x.is_cuda else None
+    want = bn.training or not bn.track_running_stats  # batch statistics: from the conv epilogue
+    st = None
     if pointwise_ok(conv, x):
         _gpu(x)
         y = _Pointwise.apply(x, conv.weight)
     elif passes is not None:
-        y = conv3x3(x, conv.weight, passes)
+        if want and passes[0] and _epilogue_stats_pay("conv3x3", conv, x):
+            y, st = conv3x3_stats(x, conv.weight, passes)
+        else:
+            y = conv3x3(x, conv.weight, passes)
     elif convbf_ok(conv, x):
-        y = conv_bf16(conv, x)
+        if want and _epilogue_stats_pay("convbf", conv, x):
+            y, st = conv_bf16_stats(conv, x)
+        else:
+            y = conv_bf16(conv, x)
     elif conv3x3s2_ok(conv, x):
         y = _Conv3x3S2.apply(x, conv.weight)
     elif conv1x1_ok(conv, x):
@@ -963,7 +988,50 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
     else:
         y = torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                        conv.dilation, conv.groups)
-    return batch_norm_act(y, bn, bn.act, residual, conv.bias)
+    return batch_norm_act(y, bn, bn.act, residual, conv.bias, st)
+
+
+_STATS_ROUTE: dict = {}
+
+
+def _epilogue_stats_pay(kind, conv, x) -> bool:
+    """Whether y's BN statistics from the conv epilogue save work: only when the
+    BatchNorm's plane-mode apply merges the records itself (route 1 of
+    mde_batchnorm_stats_route).  A separate merge launch costs about what the
+    statistics pass it replaces does, and small tensors take the one-launch
+    BatchNorm, which reads x once anyway."""
+    n, cin, h, w = x.shape
+    k, s = conv.kernel_size[0], conv.stride[0]
+    key = (kind, n, cin, conv.out_channels, h, w, k, s, x.dtype)
+    hit = _STATS_ROUTE.get(key)
+    if hit is None:
+        cout, pad = conv.out_channels, k // 2
+        ho, wo = (h + 2 * pad - k) // s + 1, (w + 2 * pad - k) // s + 1
+        if kind == "convbf":
+            nb = _abi.query("mde_convbf_stats_blocks", n, cin, cout, h, w, k, s)
+            dt = _abi.MDE_BF16
+        else:
+            dt = _abi.MDE_BF16 if (x.dtype == torch.bfloat16 or _autocast_bf16(x)) else _abi.MDE_F32
+            nb = _abi.query("mde_conv3x3_stats_blocks", n, cin, cout, h, w, dt)
+        hit = nb > 0 and _abi.query("mde_batchnorm_stats_route", n, cout, ho, wo, nb, dt) == 1
+        _STATS_ROUTE[key] = hit
+    return hit
+
+
+def conv_nobias_stats(conv: nn.Conv2d, x, bn: nn.BatchNorm2d):
+    """(conv_nobias(conv, x), statistics) where the statistics are y's per-block
+    BN sums from the conv's epilogue when `bn` normalises with batch statistics,
+    the conv runs on a HIP kernel that emits them (conv3x3 / convbf) and the
+    BatchNorm consumes them without a merge launch (_epilogue_stats_pay), else
+    None (the BatchNorm then takes its own statistics pass)."""
+    if x.is_cuda and (bn.training or not bn.track_running_stats):
+        passes = conv3x3_passes(conv, x)
+        if passes is not None:
+            if passes[0] and _epilogue_stats_pay("conv3x3", conv, x):
+                return conv3x3_stats(x, conv.weight, passes)
+        elif convbf_ok(conv, x) and _epilogue_stats_pay("convbf", conv, x):
+            return conv_bf16_stats(conv, x)
+    return conv_nobias(conv, x), None
 
 
 def conv_nobias(conv: nn.Conv2d, x):
@@ -1055,6 +1123,11 @@ def run_sequential(seq: nn.Sequential, x):
         if (isinstance(m, nn.Conv2d) and m.bias is not None and i + 1 < len(mods)
                 and isinstance(mods[i + 1], BatchNorm2d) and m.padding_mode == "zeros"):
             x = conv_bn(m, mods[i + 1], x)
+            i += 2
+        elif (isinstance(m, Conv2d) and m.bias is None and i + 1 < len(mods)
+              and isinstance(mods[i + 1], BatchNorm2d) and m.padding_mode == "zeros"):
+            y, st = conv_nobias_stats(m, x, mods[i + 1])
+            x = mods[i + 1](y, stats=st)
             i += 2
         else:
             x = m(x)
@@ -1208,8 +1281,8 @@ class BatchNorm2d(nn.BatchNorm2d):
             raise ValueError(f"act must be one of {sorted(_ACTS)}")
         self.act = act
 
-    def forward(self, x, residual=None, prebias=None):
-        return batch_norm_act(x, self, self.act, residual, prebias)
+    def forward(self, x, residual=None, prebias=None, stats=None):
+        return batch_norm_act(x, self, self.act, residual, prebias, stats)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={self.act}"

@@ -136,3 +136,69 @@ def test_convbf_refuses_unaligned_planes():
     from monocular_depth_estimation_amd import _abi
     assert _abi.query("mde_convbf_supported", 96, 64, 22, 36, 3, 2, 0) == 0  # 11 x 18 output
     assert _abi.query("mde_convbf_supported", 96, 64, 22, 40, 3, 2, 0) == 1
+
+
+@pytest.mark.parametrize("cin,cout,h,w,k,s", [
+    (64, 64, 60, 80, 3, 1), (128, 64, 60, 80, 3, 1), (32, 64, 120, 160, 3, 2),
+    (256, 256, 15, 20, 3, 2), (32, 64, 120, 160, 1, 2), (640, 256, 8, 10, 1, 1),
+    (64, 32, 18, 24, 3, 1),
+])
+def test_convbf_epilogue_statistics(cin, cout, h, w, k, s):
+    """The forward's per-block BN sums [cout][blocks][4] (shift, count, s1, s2)
+    merge to the mean / variance of the bf16 y it wrote (float64 reference)."""
+    from monocular_depth_estimation_amd.nn import Conv2d, conv_bf16_stats
+    n = 4
+    torch.manual_seed(cin + cout + k)
+    conv = Conv2d(cin, cout, k, stride=s, padding=k // 2, bias=False).to(DEV)
+    x = (torch.rand((n, cin, h, w), device=DEV) - 0.3).to(torch.bfloat16)
+    with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+        y, st = conv_bf16_stats(conv, x)
+    torch.cuda.synchronize()
+    assert st is not None and st.shape[0] == cout
+    st = st.double().cpu()
+    ref, cnt, s1, s2 = st[..., 0], st[..., 1], st[..., 2], st[..., 3]
+    tot = cnt.sum(1)
+    assert torch.all(tot == n * y.shape[2] * y.shape[3])
+    mean = (ref * cnt + s1).sum(1) / tot
+    ex2 = (s2 + 2 * ref * s1 + cnt * ref * ref).sum(1) / tot
+    var = ex2 - mean * mean
+    yd = y.double().cpu()
+    mref = yd.mean((0, 2, 3))
+    vref = yd.var((0, 2, 3), unbiased=False)
+    scale = yd.abs().max()
+    assert float((mean - mref).abs().max() / scale) < 1e-5
+    assert float(((var - vref).abs() / vref).max()) < 1e-3
+
+
+@pytest.mark.parametrize("cin,cout,h,w,k,s", [(64, 64, 60, 80, 3, 1), (32, 64, 120, 160, 1, 2)])
+def test_batchnorm_from_convbf_records_matches_statistics_pass(cin, cout, h, w, k, s):
+    """BatchNorm (train) fed the conv epilogue's records -- merged by the
+    plane-mode apply itself (mde_batchnorm_stats_route 1) -- against the same
+    BatchNorm taking its own statistics pass: outputs within one bf16 ulp,
+    running statistics and saved moments within 1e-5."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import BatchNorm2d, Conv2d, batch_norm_act, conv_bf16_stats
+    n = 8
+    torch.manual_seed(3)
+    conv = Conv2d(cin, cout, k, stride=s, padding=k // 2, bias=False).to(DEV)
+    x = torch.randn((n, cin, h, w), device=DEV).to(torch.bfloat16)
+    with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+        y, st = conv_bf16_stats(conv, x)
+    assert st is not None
+    ho, wo = y.shape[2], y.shape[3]
+    assert _abi.query("mde_batchnorm_stats_route", n, cout, ho, wo, st.shape[1], _abi.MDE_BF16) == 1
+    gamma = torch.rand(cout, device=DEV) + 0.5
+    beta = torch.rand(cout, device=DEV) * 0.4 - 0.2
+    outs = []
+    for stats in (st, None):
+        bn = BatchNorm2d(cout, act="relu").to(DEV)
+        with torch.no_grad():
+            bn.weight.copy_(gamma)
+            bn.bias.copy_(beta)
+            out = batch_norm_act(y.detach(), bn, "relu", None, None, stats)
+        outs.append((out.float(), bn.running_mean.clone(), bn.running_var.clone()))
+    torch.cuda.synchronize()
+    (a, ma, va), (b, mb, vb) = outs
+    ulp = 2.0 ** -7 * b.abs().clamp_min(2.0 ** -14)
+    assert bool(((a - b).abs() <= ulp).all())
+    assert float((ma - mb).abs().max()) < 1e-5 and float(((va - vb).abs() / vb).max()) < 1e-5

@@ -43,6 +43,7 @@
 // the pixel patches (split-K); their fp32 partials are summed in a fixed order
 // (bitwise reproducible, no atomics).
 #include <cstdlib>
+#include <cstring>
 #include <utility>
 
 #include "common.h"
@@ -278,14 +279,19 @@ struct SrcStage {
     return sw ? -d : d;
   }
 
-  __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
-                                       int ci0) {
-    const int plane = g.hi * g.wi;
+  // per patch: the buffer resource of the image and each unit's 32-bit offset
+  // (channel 0 of its octet; past the buffer when outside the source plane)
+  __amdgpu_buffer_rsrc_t R;
+  uint32_t voff[MAXU];
+  int plane;
+
+  __device__ __forceinline__ void locate(const bf16* __restrict__ src, const Geo& g, const Img& I) {
+    plane = g.hi * g.wi;
     const uint64_t a = (uint64_t)src;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 2 * g.cin * plane, 0x00020000);
+    R = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0,
+                                          2 * g.cin * plane, 0x00020000);
     static_for<MAXU>([&](auto k_c) {
       constexpr int k = decltype(k_c)::value;
       const int cd = code[k] < 0 ? 0 : code[k];
@@ -308,16 +314,29 @@ struct SrcStage {
         ok = sr >= 0 && sr < g.hi && sc >= 0 && sc < g.wi;
       }
       ok = ok && code[k] >= 0;
-      const uint32_t voff = ok ? (uint32_t)(2 * (8 * o * plane + sr * g.wi + sc)) : 0x7ffffff0u;
+      voff[k] = ok ? (uint32_t)(2 * (8 * o * plane + sr * g.wi + sc)) : 0x7ffffff0u;
+    });
+  }
+
+  // the loads of channels ci0 + 8 o + (0..7) of every unit (located patch)
+  __device__ __forceinline__ void issue(int ci0) {
+    static_for<MAXU>([&](auto k_c) {
+      constexpr int k = decltype(k_c)::value;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int soff = 2 * (ci0 + j) * plane;
         if constexpr (MODE == U2)
-          v[k][j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R, voff, soff, 0);
+          v[k][j] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R, voff[k], soff, 0);
         else
-          v[k][j] = __builtin_amdgcn_raw_buffer_load_b32(R, voff, soff, 0);
+          v[k][j] = __builtin_amdgcn_raw_buffer_load_b32(R, voff[k], soff, 0);
       }
     });
+  }
+
+  __device__ __forceinline__ void load(const bf16* __restrict__ src, const Geo& g, const Img& I,
+                                       int ci0) {
+    locate(src, g, I);
+    issue(ci0);
   }
 
   __device__ __forceinline__ void store(bf16* img, const Img& I) const {
@@ -427,6 +446,52 @@ __device__ __forceinline__ void chunk_mfmas(const bf16* __restrict__ swc, int nb
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < MTW; ++i) acc[i] = mfma32(aq[s % NSL][i], bq[s % NSL], acc[i]);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+}
+
+// chunk_mfmas for a wave tile of MTW x NTW 32x32 tiles: per (tap, k-half)
+// step MTW A + NTW B reads feed MTW NTW MFMAs (2 x 2: one read per MFMA).
+template <int KS, int DYM, int MTW, int NTW, int PITCH_A>
+__device__ __forceinline__ void tile_mfmas(const bf16* __restrict__ swc, int nbrow,
+                                           const bf16* __restrict__ simg, const int (&abase)[MTW],
+                                           const int (&toff)[KS * KS], const int (&boff0)[NTW],
+                                           const int (&boff1)[NTW], int h,
+                                           f16v (&acc)[MTW][NTW]) {
+  constexpr int NR = (DYM & 1) + ((DYM >> 1) & 1) + ((DYM >> 2) & 1);
+  constexpr int NS = (KS == 3 ? NR * 3 : 1) * 2;
+  auto tap_of = [](int s) constexpr {
+    const int j = s >> 1;
+    if constexpr (KS == 1) return 0;
+    int row = 0, n = 0;
+    for (int dy = 0; dy < 3; ++dy)
+      if ((DYM >> dy) & 1) {
+        if (j >= n * 3 && j < n * 3 + 3) row = dy * 3 + (j - n * 3);
+        ++n;
+      }
+    return row;
+  };
+  constexpr int PD = 2, NSL = PD + 1;
+  u4v bq[NSL][NTW], aq[NSL][MTW];
+  auto ld = [&](auto s_c) {
+    constexpr int s = decltype(s_c)::value, slot = s % NSL;
+    constexpr int t = tap_of(s), ks = s & 1;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+      bq[slot][j] = *reinterpret_cast<const u4v*>(swc + t * nbrow + (ks ? boff1[j] : boff0[j]));
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+      aq[slot][i] = *reinterpret_cast<const u4v*>(simg + abase[i] + toff[t] + 16 * ks + 8 * h);
+  };
+  static_for<PD < NS ? PD : NS>([&](auto s_c) { ld(s_c); });
+  static_for<NS>([&](auto s_c) {
+    constexpr int s = decltype(s_c)::value;
+    if constexpr (s + PD < NS) ld(std::integral_constant<int, s + PD>{});
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) acc[i][j] = mfma32(aq[s % NSL][i], bq[s % NSL][j], acc[i][j]);
     __builtin_amdgcn_sched_barrier(0);
   });
 }
@@ -581,14 +646,16 @@ __global__ void __launch_bounds__(64 * NW, 1)
 // kernel stages -- never again).
 constexpr int kWRes = 36864;  // resident filter capacity, bf16 elements (73.7 KB)
 
-template <int KS, int MODE, int WN, bool STATS, int CAP>
+template <int KS, int MODE, int WN, bool STATS, int CAP, int NTW = 1>
 __global__ void __launch_bounds__(256, 1)
     convbf_fwd_res_kernel(const bf16* __restrict__ x, const bf16* __restrict__ wp,
                           bf16* __restrict__ y, float* __restrict__ stats, Geo g, int per,
                           int npatch) {
-  constexpr int KK = KS * KS, NB = 32 * WN, WMW = 4 / WN, MTW = 2, NT = 256;
+  // wave (wm, wn): NTW of the block's WN 32-channel tiles x MTW 32-pixel tiles
+  constexpr int KK = KS * KS, NB = 32 * WN, WMW = 4 / (WN / NTW), MTW = 2, NT = 256;
   __shared__ __attribute__((aligned(16))) bf16 simg[CAP * kPitchF];
   __shared__ __attribute__((aligned(16))) bf16 sw[kWRes];
+  constexpr int MB = 32 * MTW * WMW, kOP = MB + 8;  // patch pixels, output-tile row pitch
   const int tid = threadIdx.x, lane = tid & 63, l32 = lane & 31, h = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wv % WMW, wn = wv / WMW;
@@ -611,15 +678,21 @@ __global__ void __launch_bounds__(256, 1)
   int toff[KK];
 #pragma unroll
   for (int t = 0; t < KK; ++t) toff[t] = tap_off<KS, MODE>(I, t / KS, t % KS) * kPitchF;
-  const int col = wn * 32 + l32;  // B column (output channel within the block)
-  const int sw_x = (col >> 2) & 3;  // logical piece q of the row sits at q ^ sw_x
-  const int boff0 = col * 32 + 8 * ((0 + h) ^ sw_x), boff1 = col * 32 + 8 * ((2 + h) ^ sw_x);
+  // B column of tile j (output channel within the block); logical 16-byte
+  // piece q of a packed filter row sits at q ^ ((col >> 2) & 3)
+  int col[NTW], boff0[NTW], boff1[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) {
+    col[j] = (wn * NTW + j) * 32 + l32;
+    const int sw_x = (col[j] >> 2) & 3;
+    boff0[j] = col[j] * 32 + 8 * ((0 + h) ^ sw_x);
+    boff1[j] = col[j] * 32 + 8 * ((2 + h) ^ sw_x);
+  }
   const int64_t hwo = (int64_t)g.ho * g.wo, xplane = (int64_t)g.cin * g.hi * g.wi;
 
   SrcStage<KS, MODE, kPitchF, NT, src_units<KS, MODE, CAP, NT>()> S;
   S.plan(I, tid);
   S.load(x + (int64_t)P.img * xplane, g, I, 0);
-
   int abase[MTW];
   bool mt_on[MTW];
   int wdymask = 7;  // U2: filter rows some tile of this wave needs (wave-uniform)
@@ -645,9 +718,13 @@ __global__ void __launch_bounds__(256, 1)
     wdymask = __builtin_amdgcn_readfirstlane(wdymask);
   };
   setup(P, I);
-  f16v acc[MTW];
-  mde::Sh run{0.f, 0.f, 0.f, 0.f};
-  bool have_ref = false;
+  f16v acc[MTW][NTW];
+  mde::Sh run[NTW];
+#pragma unroll
+  for (int j = 0; j < NTW; ++j) run[j] = mde::Sh{0.f, 0.f, 0.f, 0.f};
+  bool have_ref[NTW] = {};  // one shift per channel and wave: its first value
+
+  const bool flat = g.pc == 0;
 
   // patch-outer, chunk-inner: the accumulators are zeroed and drained once per
   // patch outside the chunk loop, so its back edge carries them in AGPRs (a
@@ -663,52 +740,81 @@ __global__ void __launch_bounds__(256, 1)
 #pragma unroll
     for (int i = 0; i < MTW; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+      for (int j = 0; j < NTW; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
     for (int cc = 0; cc < nch; ++cc) {
       __syncthreads();  // previous step's image readers are done (1st: the filter DMA drained)
       S.store(simg, I);
       __syncthreads();
-      // the next step's input chunk, in flight during this step's MFMAs
+      // the next step's input chunk, in flight during this step's MFMAs (the
+      // unit offsets are located once a patch)
       if (cc + 1 < nch)
-        S.load(x + (int64_t)P.img * xplane, g, I, 32 * (cc + 1));
+        S.issue(32 * (cc + 1));
       else if (q + 1 < q1)
         S.load(x + (int64_t)Pn.img * xplane, g, In, 0);
       const bf16* swc = sw + cc * KK * NB * 32;
       // U2 skips a filter row only when all of the wave's tiles do
       if (MODE == U2 && KS == 3 && wdymask == 2)
-        chunk_mfmas<KS, 2, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+        tile_mfmas<KS, 2, MTW, NTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
       else if (MODE == U2 && KS == 3 && wdymask == 5)
-        chunk_mfmas<KS, 5, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+        tile_mfmas<KS, 5, MTW, NTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
       else
-        chunk_mfmas<KS, 7, MTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
+        tile_mfmas<KS, 7, MTW, NTW, kPitchF>(swc, NB * 32, simg, abase, toff, boff0, boff1, h, acc);
     }
-    // the patch is complete: bf16 output (+ statistics)
-    bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col) * hwo;
+    // the patch is complete: bf16 output (+ statistics).  Flat patches (a
+    // contiguous run of the output plane) go through LDS as [channel][pixel]
+    // rows and leave as 16-byte stores, 256 contiguous bytes per 16 lanes (a
+    // lane's own fragment -- 4 pixels of one channel -- would make every store
+    // instruction touch 64 planes: store-issue-bound).  (Deferring those stores
+    // into the next patch's first step, past its input loads' vmcnt wait, from
+    // a separate LDS tile measured 3 % slower.)
+    if (flat) __syncthreads();  // every wave is done reading the image
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) {
-      if (mt_on[i]) {
+    for (int j = 0; j < NTW; ++j) {
+      bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col[j]) * hwo;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        if (!mt_on[i]) continue;
         const int mt = MTW * wm + i;
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) {
           const int m = mt * 32 + 8 * qq + 4 * h;
-          int r, c;
-          const bool ok = pix_of(g, P, m, r, c);
-          const uint32_t p01 = pack2bf(acc[i][4 * qq], acc[i][4 * qq + 1]);
-          const uint32_t p23 = pack2bf(acc[i][4 * qq + 2], acc[i][4 * qq + 3]);
+          const uint32_t p01 = pack2bf(acc[i][j][4 * qq], acc[i][j][4 * qq + 1]);
+          const uint32_t p23 = pack2bf(acc[i][j][4 * qq + 2], acc[i][j][4 * qq + 3]);
+          int r = 0, c = 0;
+          const bool ok = flat ? m < P.npx : pix_of(g, P, m, r, c);
           if constexpr (STATS) {
             const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
             const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
-            if (!have_ref) {
-              run.ref = __shfl(v0, l32, 64);
-              have_ref = true;
+            if (!have_ref[j]) {
+              run[j].ref = __shfl(v0, l32, 64);
+              have_ref[j] = true;
             }
-            mde::sh_add(run, v0, ok);
-            mde::sh_add(run, v1, ok);
-            mde::sh_add(run, v2, ok);
-            mde::sh_add(run, v3, ok);
+            mde::sh_add(run[j], v0, ok);
+            mde::sh_add(run[j], v1, ok);
+            mde::sh_add(run[j], v2, ok);
+            mde::sh_add(run[j], v3, ok);
           }
-          if (ok) *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
+          if (flat)
+            *reinterpret_cast<u2v*>(simg + col[j] * kOP + m) = u2v{p01, p23};
+          else if (ok)
+            *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
         }
+      }
+    }
+    if (flat) {
+      __syncthreads();
+      bf16* yb = y + ((int64_t)P.img * g.cout + co0) * hwo + P.p0;
+#pragma unroll
+      for (int k = 0; k < NB * MB / 8 / 256; ++k) {
+        const int j = tid + 256 * k, co = j / (MB / 8), px = 8 * (j % (MB / 8));
+        const u4v v = *reinterpret_cast<const u4v*>(simg + co * kOP + px);
+        bf16* dst = yb + (int64_t)co * hwo + px;
+        if (px + 8 <= P.npx)
+          *reinterpret_cast<u4v*>(dst) = v;
+        else if (px < P.npx)  // npx % 4 == 0: half a chunk
+          *reinterpret_cast<u2v*>(dst) = u2v{v[0], v[1]};
       }
     }
     if (q + 1 < q1) {
@@ -718,15 +824,18 @@ __global__ void __launch_bounds__(256, 1)
     }
   }
   if constexpr (STATS) {  // one record per channel and block
-    run = mde::sh_xor_sum(run, 32);
     __syncthreads();
     float* part = reinterpret_cast<float*>(simg);  // [WMW][NB][4]
-    if (h == 0) {
-      float* p4 = part + (wm * NB + col) * 4;
-      p4[0] = run.ref;
-      p4[1] = run.n;
-      p4[2] = run.s1;
-      p4[3] = run.s2;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const mde::Sh a = mde::sh_xor_sum(run[j], 32);
+      if (h == 0) {
+        float* p4 = part + (wm * NB + col[j]) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
     }
     __syncthreads();
     if (tid < NB) {
@@ -1145,12 +1254,37 @@ inline int device_cus() {
 struct ResGeo {
   Geo g;
   int nb, per, blocks;  // output channels a block, patches a block, blocks per channel group
+  int ntw;              // 32-channel tiles a wave: 2 = 256-pixel patches, 64 x 64 wave tiles
   int64_t np;
 };
 
+// Resident-filter variants (MDE_CONVBF_RESMODE):
+//  t22  (default) 64 output channels a block, 64 x 64 wave tiles over
+//       256-pixel patches where that image fits beside the filter (stride 1,
+//       any 1x1); else as t21
+//  t21  64 (or 32) output channels, 32 x 64 wave tiles, 128-pixel patches
+// (Measured, tools/gpu_r05h.sh: two blocks a CU with a half-size filter slice
+// -- 32 output channels, so one block's staging overlaps the other's MFMAs --
+// ran 64 -> 64 @ 60x80 at 46.5 us against t22's 35.8: dropped.)
+inline int res_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("MDE_CONVBF_RESMODE");
+    return e && !std::strcmp(e, "t21") ? 1 : 0;
+  }();
+  return m;
+}
+
 inline bool res_geo(const Pass& p, int64_t n, ResGeo* r) {
   r->nb = res_on() ? res_nb(p) : 0;
-  if (!r->nb || !pick_geo(p, 32 * 2 * (4 / (r->nb / 32)), &r->g)) return false;
+  if (!r->nb) return false;
+  r->ntw = 1;
+  const bool s1img = p.mode == S1 || p.ks == 1;
+  if (res_mode() == 0 && r->nb == 64 && s1img &&
+             pick_geo(p, 256, &r->g, p.ks == 3 ? kCapS1W : kCapS1)) {
+    r->ntw = 2;
+  } else if (!pick_geo(p, 32 * 2 * (4 / (r->nb / 32)), &r->g)) {
+    return false;
+  }
   r->np = n * r->g.ppi;
   if (r->np >= (1 << 22)) return false;
   const int ncob = p.cout / r->nb;
@@ -1162,16 +1296,16 @@ inline bool res_geo(const Pass& p, int64_t n, ResGeo* r) {
   return true;
 }
 
-template <int KS, int MODE, int WN, int CAP>
+template <int KS, int MODE, int WN, int CAP, int NTW = 1>
 int launch_res_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const ResGeo& r, int cout,
                  int kid, double flops, double bytes, hipStream_t s) {
   const dim3 grid((unsigned)r.blocks, (unsigned)(cout / (32 * WN)));
   if (stats)
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_res_kernel<KS, MODE, WN, true, CAP>), grid,
-                    dim3(256), 0, x, wp, y, stats, r.g, r.per, (int)r.np);
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_res_kernel<KS, MODE, WN, true, CAP, NTW>),
+                    grid, dim3(256), 0, x, wp, y, stats, r.g, r.per, (int)r.np);
   else
-    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_res_kernel<KS, MODE, WN, false, CAP>), grid,
-                    dim3(256), 0, x, wp, y, stats, r.g, r.per, (int)r.np);
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (convbf_fwd_res_kernel<KS, MODE, WN, false, CAP, NTW>),
+                    grid, dim3(256), 0, x, wp, y, stats, r.g, r.per, (int)r.np);
   return MDE_OK;
 }
 
@@ -1184,6 +1318,15 @@ int launch_fwd(const Pass& p, const bf16* x, const bf16* wp, bf16* y, float* sta
 #define CBF_RES(KS, MODE, CAP)                                                                     \
   return rg.nb == 64 ? launch_res_t<KS, MODE, 2, CAP>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s) \
                      : launch_res_t<KS, MODE, 1, CAP>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s)
+    if (rg.ntw == 2) {
+      if (p.ks == 3)
+        return launch_res_t<3, S1, 2, kCapS1W, 2>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s);
+      if (p.mode == S1)
+        return launch_res_t<1, S1, 2, kCapS1, 2>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s);
+      if (p.mode == S2)
+        return launch_res_t<1, S2, 2, kCapS1, 2>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s);
+      return launch_res_t<1, U2, 2, kCapS1, 2>(x, wp, y, stats, rg, p.cout, kid, flops, bytes, s);
+    }
     if (p.ks == 3) {
       if (p.mode == S1) { CBF_RES(3, S1, kCapS1); }
       if (p.mode == S2) { CBF_RES(3, S2, kCapS2); }

@@ -106,7 +106,7 @@ NAMES = [
     (r"colsum_part_kernel<true>", "gelu_bwd_bias_grad"),
     (r"colsum_(part_kernel<false>|final_kernel)", "linear_bias_grad"),
     # forward and data gradient run the same kernel (as wino_f23_kernel)
-    (r"convbf_fwd_kernel", "convbf_fwd_bf16+convbf_dgrad_bf16"),
+    (r"convbf_fwd_(res_)?kernel", "convbf_fwd_bf16+convbf_dgrad_bf16"),
     (r"convbf_wgrad_kernel", "convbf_wgrad_bf16"),
     (r"convbf_wreduce_kernel", "convbf_wreduce"),
     (r"convbf_pack_kernel", "convbf_pack"),

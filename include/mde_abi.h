@@ -756,6 +756,33 @@ int mde_convbf_wgrad(const void* gy, const void* x, float* gweight, int64_t n, i
                      void* stream);
 
 /* ---------------------------------------------------------------------------
+ * DDRNet-23-slim's stem convolution under bf16 autocast (src/GuideDepth/model/
+ * DDRNet_23_slim.py:230-233, conv1[0]): 3 -> cout (32 or 64) channels, 3x3,
+ * stride 2, padding 1, on the fp32 image x [n,3,h,w] (w % 4 == 0), the image
+ * and weight [cout,3,3,3] rounded to bf16 (RNE) as autocast does, fp32
+ * accumulation.  mde_stem_bf16_fwd: y [n,cout,ho,wo] bf16, ho = (h-1)/2+1.
+ * mde_stem_bf16_wgrad: gweight [cout,3,3,3] fp32 (overwritten) from gy bf16
+ * and x, via deterministic block partials in mde_stem_bf16_wgrad_workspace
+ * bytes.  The image takes no gradient.  Replaces MIOpen's NHWC bf16 solvers
+ * (and their transposes / zero fills) for this conv.
+ * ------------------------------------------------------------------------- */
+int mde_stem_bf16_supported(int64_t cin, int64_t cout, int64_t h, int64_t w);
+int mde_stem_bf16_fwd(const float* x, const float* weight, void* y, int64_t n, int64_t cout,
+                      int64_t h, int64_t w, void* stream);
+size_t mde_stem_bf16_wgrad_workspace(int64_t n, int64_t cout, int64_t h, int64_t w);
+int mde_stem_bf16_wgrad(const void* gy, const float* x, float* gweight, int64_t n, int64_t cout,
+                        int64_t h, int64_t w, void* workspace, void* stream);
+/* The guide convs' weight gradient under bf16 autocast (3 -> 16 / 32 / 64,
+ * 3x3, stride 1, padding 1 on the image; src/GuideDepth/model/modules.py:
+ * 52-54): gweight [cout,3,3,3] fp32 (overwritten) from gy [n,cout,h,w] bf16
+ * read as such and the fp32 image rounded to bf16 (w % 4 == 0), same kernel
+ * family and determinism as mde_stem_bf16_wgrad (stem.hip). */
+size_t mde_conv3x3_guide_bf16_wgrad_workspace(int64_t n, int64_t cout, int64_t h, int64_t w);
+int mde_conv3x3_guide_bf16_wgrad(const void* gy, const float* x, float* gweight, int64_t n,
+                                 int64_t cout, int64_t h, int64_t w, void* workspace,
+                                 void* stream);
+
+/* ---------------------------------------------------------------------------
  * Opt-in kernel timing registry (measurement only; off by default).
  * When enabled, every launch made through this ABI is bracketed by hipEvents
  * on the stream it is launched on, and its algorithmic HBM bytes (SURVEY

@@ -85,6 +85,8 @@ enum Kid : int {
   K_CBF_WGRAD,
   K_CBF_WREDUCE,
   K_CBF_PACK,
+  K_STEM_FWD,       // the bf16 stem convolution (stem.hip)
+  K_STEM_WGRAD,
   K_COUNT
 };
 

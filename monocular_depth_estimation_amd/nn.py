@@ -847,6 +847,59 @@ class _ConvBf16(torch.autograd.Function):
         return gx, gw, None, None, None
 
 
+class _StemBf16(torch.autograd.Function):
+    """DDRNet's stem conv (3 -> 32, 3x3, stride 2, padding 1; DDRNet_23_slim.py:
+    230-233) under bf16 autocast on stem.hip: the fp32 image and weight rounded
+    to bf16 in the kernels (autocast's casts), fp32 accumulation, a bf16
+    output, the fp32 weight gradient; the image takes no gradient.  Replaces
+    MIOpen's NHWC bf16 solvers, their transposes and zero fills."""
+
+    @staticmethod
+    @_bn_fwd
+    def forward(ctx, x, weight):
+        x = x.contiguous()
+        weight = weight.contiguous()
+        n, _, h, w = x.shape
+        cout = weight.shape[0]
+        y = torch.empty((n, cout, (h - 1) // 2 + 1, (w - 1) // 2 + 1), dtype=torch.bfloat16,
+                        device=x.device)
+        _abi.call("mde_stem_bf16_fwd", _abi.ptr(x), _abi.ptr(weight), _abi.ptr(y), n, cout, h, w,
+                  _abi.stream_of(x))
+        ctx.save_for_backward(x, weight)
+        return y
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, gy):
+        x, weight = ctx.saved_tensors
+        gw = None
+        if ctx.needs_input_grad[1]:
+            gy = gy.to(torch.bfloat16).contiguous()
+            n, _, h, w = x.shape
+            cout = weight.shape[0]
+            gw = torch.empty_like(weight)
+            ws = _ws(_abi.query("mde_stem_bf16_wgrad_workspace", n, cout, h, w), x)
+            _abi.call("mde_stem_bf16_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, cout, h, w,
+                      _abi.ptr(ws), _abi.stream_of(gy))
+        return None, gw
+
+
+STEM_BF16 = os.environ.get("MDE_STEM_BF16", "1") != "0"  # A/B switch: 0 = MIOpen
+
+
+def stem_ok(conv: nn.Conv2d, x) -> bool:
+    """Whether this conv takes _StemBf16: an fp32 CUDA image that needs no
+    gradient under bf16 autocast, 3 -> 32 / 64 channels, 3x3 / stride 2 /
+    padding 1, zero padding, width % 4 == 0."""
+    return (STEM_BF16 and x.is_cuda and x.dim() == 4 and x.dtype == torch.float32
+            and not x.requires_grad and _autocast_bf16(x) and conv.weight.dtype == torch.float32
+            and conv.in_channels == 3 and conv.kernel_size == (3, 3) and conv.stride == (2, 2)
+            and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.padding_mode == "zeros"
+            and bool(_abi.query("mde_stem_bf16_supported", 3, conv.out_channels, x.shape[2],
+                                x.shape[3])))
+
+
 CONVBF = os.environ.get("MDE_CONVBF", "1") != "0"  # A/B switch: 0 = MIOpen's bf16 solvers
 _CONVBF_OK: dict = {}
 
@@ -893,7 +946,8 @@ class _GuideConvBf16(torch.autograd.Function):
     rounded to bf16 in the kernel (autocast's casts), fp32 accumulation, a
     bf16 output (mde_conv3x3_guide_bf16_fwd, + the following BatchNorm's
     statistics), so no fp32 output and no cast pass exist; the weight
-    gradient on the fp32 kernel (the image needs no gradient)."""
+    gradient from the bf16 gy and the bf16-rounded image on the MFMA kernel
+    of stem.hip (mde_conv3x3_guide_bf16_wgrad; the image needs no gradient)."""
 
     @staticmethod
     def forward(ctx, x, weight, want_stats):
@@ -918,14 +972,21 @@ class _GuideConvBf16(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         gw = None
         if ctx.needs_input_grad[1]:
-            gyf = gy.float().contiguous()
             n, cin, h, w = x.shape
             cout = weight.shape[0]
             gw = torch.empty_like(weight)
-            ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w,
-                                _abi.MDE_F32), x)
-            _abi.call("mde_conv3x3_wgrad", _abi.ptr(gyf), _abi.ptr(x), _abi.ptr(gw), n, cin, cout,
-                      h, w, _abi.ptr(ws), _abi.MDE_F32, _abi.stream_of(gyf))
+            if gy.dtype == torch.bfloat16 and w % 4 == 0:
+                # bf16 gy read as such (stem.hip): no fp32 copy of the full-size gradient
+                gy = gy.contiguous()
+                ws = _ws(_abi.query("mde_conv3x3_guide_bf16_wgrad_workspace", n, cout, h, w), x)
+                _abi.call("mde_conv3x3_guide_bf16_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw),
+                          n, cout, h, w, _abi.ptr(ws), _abi.stream_of(gy))
+            else:
+                gyf = gy.float().contiguous()
+                ws = _ws(_abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w,
+                                    _abi.MDE_F32), x)
+                _abi.call("mde_conv3x3_wgrad", _abi.ptr(gyf), _abi.ptr(x), _abi.ptr(gw), n, cin,
+                          cout, h, w, _abi.ptr(ws), _abi.MDE_F32, _abi.stream_of(gyf))
         return None, gw, None
 
 
@@ -976,6 +1037,8 @@ def conv_bn(conv: nn.Conv2d, bn: "BatchNorm2d", x, residual=None):
             y, st = conv3x3_stats(x, conv.weight, passes)
         else:
             y = conv3x3(x, conv.weight, passes)
+    elif stem_ok(conv, x):
+        y = _StemBf16.apply(x, conv.weight)
     elif convbf_ok(conv, x):
         if want and _epilogue_stats_pay("convbf", conv, x):
             y, st = conv_bf16_stats(conv, x)
@@ -1049,8 +1112,31 @@ def conv_nobias(conv: nn.Conv2d, x):
         return _Pointwise.apply(x, conv.weight)
     if conv1x1_ok(conv, x):
         return _Conv1x1.apply(x, conv.weight, conv.stride[0])
+    if mm1x1_ok(conv, x):
+        return conv1x1_mm(conv.weight, x)
     return torch.nn.functional.conv2d(x, conv.weight, None, conv.stride, conv.padding,
                                       conv.dilation, conv.groups)
+
+
+def mm1x1_ok(conv: nn.Conv2d, x) -> bool:
+    """A 1x1 / stride 1 / no padding conv under bf16 autocast that no HIP conv
+    kernel takes (DAPPM's pooled branches, DDRNet_23_slim.py:121-160: 4x5,
+    2x3, 1x2 and 1x1 planes with odd or tiny widths): a plain batched GEMM."""
+    return (x.is_cuda and x.dim() == 4 and (_autocast_bf16(x) or x.dtype == torch.bfloat16)
+            and conv.weight.dtype == torch.float32 and conv.kernel_size == (1, 1)
+            and conv.stride == (1, 1) and conv.padding == (0, 0) and conv.dilation == (1, 1)
+            and conv.groups == 1)
+
+
+def conv1x1_mm(weight, x):
+    """conv2d(x, weight) for a 1x1 kernel as y[n] = W . x[n] (rocBLAS batched
+    GEMM on bf16 operands, fp32 accumulation: autocast's conv semantics) --
+    NCHW in and out, none of MIOpen's NHWC transposes or zero fills."""
+    n, cin, h, w = x.shape
+    cout = weight.shape[0]
+    wb = weight.view(cout, cin).to(torch.bfloat16)
+    y = torch.matmul(wb, x.to(torch.bfloat16).reshape(n, cin, h * w))
+    return y.view(n, cout, h, w)
 
 
 class Conv2d(nn.Conv2d):

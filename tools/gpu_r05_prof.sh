@@ -22,8 +22,9 @@ for wl in gd_fp32 gd_bf16 nc_fp32; do
     gd_bf16) args="--workload guidedepth --amp bf16" ;;
     nc_fp32) args="--workload newcrf" ;;
   esac
-  run "bench_$wl" 400 python3 -u bench.py $args --steps 30 --warmup 5
-  cp "$OUT/bench_$wl.log" "$OUT/bench_$wl.txt"
+  echo "== bench_$wl ($(date +%T))"
+  timeout -k 10 400 python3 -u bench.py $args --steps 30 --warmup 5 > "$OUT/bench_$wl.json" 2> "$OUT/bench_$wl.log"
+  rc=$?; head -c 300 "$OUT/bench_$wl.json"; echo; [ $rc -eq 0 ] || { echo "bench rc=$rc"; exit $rc; }
   run "trace_$wl" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace_$wl" \
       -o r05 -- python3 bench.py $args --steps 5 --warmup 3 --no-cpu-baseline
   for ctr in FETCH_SIZE WRITE_SIZE; do

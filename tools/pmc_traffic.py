@@ -110,6 +110,8 @@ NAMES = [
     (r"convbf_wgrad_kernel", "convbf_wgrad_bf16"),
     (r"convbf_wreduce_kernel", "convbf_wreduce"),
     (r"convbf_pack_kernel", "convbf_pack"),
+    (r"stem_bf16_fwd_kernel", "stem_fwd_bf16"),
+    (r"stem_bf16_wgrad_kernel|stem_wreduce_kernel", "stem_wgrad_bf16"),
     (r"eval_partial_kernel", "eval_sums"),
     (r"eval_final_kernel", "eval_final"),
     (r"nyu_augment_kernel", "nyu_augment"),

@@ -524,6 +524,234 @@ __global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)  // 64 x 64: W^T
     out[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
+// The pointwise backward (BN + ReLU operand, optional BNS sums) on bf16
+// storage with the NEXT tile's operands in flight during this tile's math:
+// the same arithmetic, operand layouts and summation order as
+// skip_bwd_mfma_kernel<CI, CO, false, true, BNS, bf16> (so bit-identical
+// results), but its tiles ran as 3-4 dependent load -> use round trips at four
+// waves per SIMD (SQ counters, tools/gpu_r05j.sh: 60 % of wave time waiting
+// on memory).  Here each tile's raw bf16 operands -- G in both lane layouts,
+// the input rows for the weight gradient and (BNS) for the BN sums -- are
+// loaded one tile ahead into one of two register sets (the loop is unrolled
+// by two so both sets have fixed registers), and gs leaves through the
+// hardware bf16 conversion.
+template <int CI, int CO, bool BNS>
+struct PwRaw {
+  static constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = CO / 4;
+  static constexpr int OG = OT <= 2 ? OT : 1;
+  uint2 gb[KO];               // G rows 4 kk + q4, pixels 4 l16 .. + 3
+  uint2 ga[OT][4];            // G rows 16 ot + l16, pixels 16 v + 4 q4 .. + 3
+  uint2 sr[MT][4];            // input rows 16 mt + l16, pixels 16 v + 4 q4 ..
+  uint2 xr[BNS ? MT : 1][4];  // input rows 16 mt + 4 q4 + i, pixels 4 l16 ..
+};
+
+__device__ __forceinline__ float4 unpack_bf4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                     __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+}
+
+template <int CI, int CO, bool BNS>
+__global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)
+    pw_bwd_pf_kernel(const mde::bf16* __restrict__ g, const mde::bf16* __restrict__ r,
+                     const float* __restrict__ wt, mde::bf16* __restrict__ gs,
+                     float* __restrict__ slab, int64_t n, int64_t hw,
+                     const float* __restrict__ isc, const float* __restrict__ ish,
+                     const float* __restrict__ imean) {
+  using Raw = PwRaw<CI, CO, BNS>;
+  constexpr int MT = Raw::MT, OT = Raw::OT, KO = Raw::KO, OG = Raw::OG;
+  static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
+  static_assert(!BNS || CI <= 32, "BN sums: cin <= 32");
+  constexpr int ROW = CO * CI + CO + (BNS ? 2 * CI : 0);  // slab row (bias columns unused)
+  __shared__ float red[4][ROW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
+  float wa[MT][KO];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int kk = 0; kk < KO; ++kk) wa[mt][kk] = wt[(4 * kk + q4) * CI + 16 * mt + l16];
+  f4 gw[OT][MT];
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) gw[ot][mt] = f4{0.f, 0.f, 0.f, 0.f};
+  float bsc[MT], bsh[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) {
+    bsc[mt] = isc[16 * mt + l16];
+    bsh[mt] = ish[16 * mt + l16];
+  }
+  constexpr int SOFF = CO * CI + CO;
+  float esc[BNS ? MT : 1][4], esh[BNS ? MT : 1][4], emu[BNS ? MT : 1][4];
+  float es1[BNS ? MT : 1][4], es2[BNS ? MT : 1][4];
+  if constexpr (BNS) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = 16 * mt + 4 * q4 + i;
+        esc[mt][i] = isc[c];
+        esh[mt][i] = ish[c];
+        emu[mt][i] = imean[c];
+        es1[mt][i] = 0.f;
+        es2[mt][i] = 0.f;
+      }
+  }
+  const int64_t tpi = hw / 64;
+  const int64_t tiles = n * tpi;
+  const int64_t stride = (int64_t)gridDim.x * 4;
+  // always a valid tile: past the end the last tile is loaded again (unused),
+  // so every iteration issues the same loads (straight-line vmcnt counts)
+  auto load = [&](int64_t t, Raw& R) {
+    if (t >= tiles) t = tiles - 1;
+    const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
+    const mde::bf16* gp = g + nidx * CO * hw + p0;
+    const mde::bf16* rp = r + nidx * CI * hw + p0;
+#pragma unroll
+    for (int kk = 0; kk < KO; ++kk)
+      R.gb[kk] = *reinterpret_cast<const uint2*>(gp + (4 * kk + q4) * hw + 4 * l16);
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      const int o = 16 * ot + l16 < CO ? 16 * ot + l16 : CO - 1;
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        R.ga[ot][v] = *reinterpret_cast<const uint2*>(gp + o * hw + 4 * q4 + 16 * v);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v)
+        R.sr[mt][v] = *reinterpret_cast<const uint2*>(rp + (16 * mt + l16) * hw + 4 * q4 + 16 * v);
+    if constexpr (BNS) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          R.xr[mt][i] = *reinterpret_cast<const uint2*>(rp + (16 * mt + 4 * q4 + i) * hw + 4 * l16);
+    }
+  };
+  auto compute = [&](int64_t t, const Raw& R) {
+    const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
+    mde::bf16* sp = gs + nidx * CI * hw + p0;
+    float4 gb[KO];
+#pragma unroll
+    for (int kk = 0; kk < KO; ++kk) gb[kk] = unpack_bf4(R.gb[kk]);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      f4 acc[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < KO; ++kk) {
+        acc[0] = mfma4(wa[mt][kk], gb[kk].x, acc[0]);
+        acc[1] = mfma4(wa[mt][kk], gb[kk].y, acc[1]);
+        acc[2] = mfma4(wa[mt][kk], gb[kk].z, acc[2]);
+        acc[3] = mfma4(wa[mt][kk], gb[kk].w, acc[3]);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        using bf2 = __bf16 __attribute__((ext_vector_type(2)));
+        const bf2 lo = {(__bf16)acc[0][i], (__bf16)acc[1][i]};
+        const bf2 hi = {(__bf16)acc[2][i], (__bf16)acc[3][i]};
+        const mde::nt2u u{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+        __builtin_nontemporal_store(u, reinterpret_cast<mde::nt2u*>(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16));
+      }
+      if constexpr (BNS) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float4 x = unpack_bf4(R.xr[mt][i]);
+          const float xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const float e = xv[j] * esc[mt][i] + esh[mt][i] > 0.f ? acc[j][i] : 0.f;
+            es1[mt][i] += e;
+            es2[mt][i] += e * (xv[j] - emu[mt][i]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int og = 0; og < OT; og += OG) {
+      float ga[OG][16];
+#pragma unroll
+      for (int oo = 0; oo < OG; ++oo) {
+        const int ot = og + oo;
+        const bool live = 16 * ot + l16 < CO;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float4 x = unpack_bf4(R.ga[ot][v]);
+          ga[oo][4 * v] = live ? x.x : 0.f;
+          ga[oo][4 * v + 1] = live ? x.y : 0.f;
+          ga[oo][4 * v + 2] = live ? x.z : 0.f;
+          ga[oo][4 * v + 3] = live ? x.w : 0.f;
+        }
+      }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        float sb[16];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const float4 x = unpack_bf4(R.sr[mt][v]);
+          sb[4 * v] = fmaxf(x.x * bsc[mt] + bsh[mt], 0.f);
+          sb[4 * v + 1] = fmaxf(x.y * bsc[mt] + bsh[mt], 0.f);
+          sb[4 * v + 2] = fmaxf(x.z * bsc[mt] + bsh[mt], 0.f);
+          sb[4 * v + 3] = fmaxf(x.w * bsc[mt] + bsh[mt], 0.f);
+        }
+#pragma unroll
+        for (int oo = 0; oo < OG; ++oo)
+#pragma unroll
+          for (int k = 0; k < 16; ++k) gw[og + oo][mt] = mfma4(ga[oo][k], sb[k], gw[og + oo][mt]);
+      }
+    }
+  };
+  int64_t t = (int64_t)blockIdx.x * 4 + w;
+  if (t < tiles) {
+    Raw A, B;
+    load(t, A);
+    while (true) {
+      load(t + stride, B);
+      compute(t, A);
+      t += stride;
+      if (t >= tiles) break;
+      load(t + stride, A);
+      compute(t, B);
+      t += stride;
+      if (t >= tiles) break;
+    }
+  }
+  // gW C layout: o = 16ot + 4 q4 + i, c = 16mt + l16
+#pragma unroll
+  for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 16 * ot + 4 * q4 + i;
+        if (o < CO) red[w][o * CI + 16 * mt + l16] = gw[ot][mt][i];
+      }
+  if constexpr (BNS) {
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float a = es1[mt][i], b = es2[mt][i];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if (l16 == 0) {
+          const int c = 16 * mt + 4 * q4 + i;
+          red[w][SOFF + 2 * c] = a;
+          red[w][SOFF + 2 * c + 1] = b;
+        }
+      }
+  }
+  __syncthreads();
+  float* out = slab + (int64_t)blockIdx.x * ROW;
+  for (int i = threadIdx.x; i < ROW; i += 256)
+    out[i] = (i >= CO * CI && i < SOFF) ? 0.f : (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+}
+
 // MFMA forward for the full-size blocks (hw % 64 == 0): each wave computes a
 // [CO x 64] output tile = W [CO x CI] . S [CI x 64] (+ bias), S = r + d.
 // Pixel order is permuted so every access is a full 256-byte row segment:
@@ -1119,6 +1347,14 @@ int mde_pointwise_fwd_stats(const void* x, const float* in_scale, const float* i
 
 namespace {
 
+inline bool pw_pf_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_PW_PF");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Pointwise backward; in_mean / in_sums non-null (with in_scale): also the
 // producer BatchNorm's backward sums (BNS epilogue), in_sums [cin][2].
 template <typename T>
@@ -1139,8 +1375,24 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
   const T* gi = (const T*)gy;
   const T* xi = (const T*)x;
   T* go = (T*)gx;
+  // bf16 storage with the BN + ReLU operand and gs written, 16 input
+  // channels (wider ones spill two register sets): the prefetching kernel
+  // (MDE_PW_PF=0: skip_bwd_mfma_kernel)
+  const bool pf = std::is_same_v<T, mde::bf16> && go != nullptr && pw_pf_on();
 #define MDE_PW_BWD(A, B)                                                                     \
-  if (cin == A && cout == B) {                                                               \
+  if (cin == A && cout == B && A <= 16 && pf && in_scale) {                                  \
+    const mde::bf16* gib = (const mde::bf16*)gy;                                             \
+    const mde::bf16* xib = (const mde::bf16*)x;                                              \
+    mde::bf16* gob = (mde::bf16*)gx;                                                         \
+    if (sums) {                                                                              \
+      if constexpr (A <= 32)                                                                 \
+        MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (pw_bwd_pf_kernel<A, B, true>), dim3(nb),        \
+                   dim3(256), 0, gib, xib, wt, gob, slab, n, hw, in_scale, in_shift, in_mean); \
+    } else {                                                                                 \
+      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (pw_bwd_pf_kernel<A, B, false>), dim3(nb),         \
+                 dim3(256), 0, gib, xib, wt, gob, slab, n, hw, in_scale, in_shift, nullptr); \
+    }                                                                                        \
+  } else if (cin == A && cout == B) {                                                        \
     if (sums) {                                                                              \
       if constexpr (A <= 32)                                                                 \
         MDE_LAUNCH(mde::K_PW_BWD, bytes, s,                                                  \

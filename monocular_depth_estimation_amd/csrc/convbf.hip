@@ -77,8 +77,12 @@ enum Mode : int { S1 = 0, S2 = 1, U2 = 2 };
 
 constexpr int kPitchF = 40;  // forward image: bf16 elements per staged pixel (32 + 8 pad)
 constexpr int kPitchW = 32;  // weight-gradient image (transposed reads): no pad
-constexpr int kGP = 136;     // weight-gradient gy rows: bf16 per channel (128 + 8 pad)
-constexpr int kMBW = 128;    // weight-gradient patch pixels
+// weight-gradient patch pixels: 256 at stride-1 3x3 (twice the MFMAs per
+// patch's fixed staging / barrier cost: 64 -> 64 @60x80 49 -> 40 us), 128
+// otherwise (stride 2 at 256 spilled and took 2D tiles: 1.1-1.4x slower);
+// gy rows are MBW + 8 bf16 a channel
+template <int KS, int MODE>
+constexpr int wgrad_mbw() { return KS == 3 && MODE == S1 ? 256 : 128; }
 
 // Patch geometry of a pass (host-chosen, see pick_geo).
 struct Geo {
@@ -863,6 +867,7 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
     convbf_wgrad_kernel(const bf16* __restrict__ x, const bf16* __restrict__ gy,
                         float* __restrict__ part, Geo g, int per, int npatch) {
   constexpr int KK = KS * KS, NT = KS == 3 ? 384 : 256, ND = KS == 3 ? 3 : 1;
+  constexpr int kMBW = wgrad_mbw<KS, MODE>(), kGP = kMBW + 8;
   constexpr int ME = 64 * KK * 32;  // partial elements: [co 64][tap][ci 32]
   __shared__ __attribute__((aligned(16))) bf16 simg[CAP * kPitchW];
   __shared__ __attribute__((aligned(16))) bf16 sg[64 * kGP];
@@ -890,16 +895,32 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
   // gy rows: [64 channels][128 pixels], 4 pixels a unit (8-byte loads)
   constexpr int GU = (64 * (kMBW / 4) + NT - 1) / NT;
   u2v gv[GU];
+  const bool flat = g.pc == 0;
+  // buffer loads: a per-patch resource over the block's 64 gy planes of the
+  // image, 32-bit offsets, out-of-range units past the buffer (zeros) -- no
+  // 64-bit address math or selects per load
   auto gy_load = [&](const Patch& P) {
-    const bf16* gsrc = gy + ((int64_t)P.img * g.cout + cob * 64) * hwo;
+    const uint64_t a = (uint64_t)(gy + ((int64_t)P.img * g.cout + cob * 64) * hwo);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, (int)(2 * co_live * hwo), 0x00020000);
 #pragma unroll
     for (int k = 0; k < GU; ++k) {
       const int u = tid + NT * k;
       const int cl = u / (kMBW / 4), m4 = 4 * (u - cl * (kMBW / 4));
-      int r, c;
-      const bool ok = u < 64 * (kMBW / 4) && pix_of(g, P, m4, r, c) && cl < co_live;
-      const u2v v = *reinterpret_cast<const u2v*>(gsrc + (ok ? (int64_t)cl * hwo + (int64_t)r * g.wo + c : 0));
-      gv[k] = ok ? v : u2v{0u, 0u};
+      int off;
+      bool ok = u < 64 * (kMBW / 4) && cl < co_live;
+      if (flat) {  // a contiguous run of the plane: no (row, column) division
+        ok = ok && m4 < P.npx;
+        off = cl * (int)hwo + P.p0 + m4;
+      } else {
+        int r, c;
+        ok = ok && pix_of(g, P, m4, r, c);
+        off = cl * (int)hwo + r * g.wo + c;
+      }
+      const uint32_t voff = ok ? (uint32_t)(2 * off) : 0x7ffffff0u;
+      gv[k] = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(R, voff, 0, 0));
     }
   };
   SrcStage<KS, MODE, kPitchW, NT, src_units<KS, MODE, CAP, NT>()> S;
@@ -942,27 +963,23 @@ __global__ void __launch_bounds__(KS == 3 ? 384 : 256, 2)
     // operands read one step ahead; the staged-pixel offsets of all steps
     // first (tab), so no read waits on another
     constexpr int NKS = kMBW / 16 / (KS == 3 ? 1 : 2);
-    int tq[NKS][2];
-#pragma unroll
-    for (int j = 0; j < NKS; ++j) {
-      const int ks = KS == 3 ? j : 2 * j + wy;
-      const int m0 = 16 * ks + 8 * (gq >> 1) + qr;
-      tq[j][0] = tab[m0] * kPitchW + bcol;
-      tq[j][1] = tab[m0 + 4] * kPitchW + bcol;
-    }
     u4v aq[2];
     s4v lq[2][ND], hq[2][ND];
     auto ld = [&](auto j_c, auto slot_c) {
       constexpr int j = decltype(j_c)::value, slot = decltype(slot_c)::value;
       constexpr int ks = KS == 3 ? j : -1;
       const int kk = KS == 3 ? ks : 2 * j + wy;
+      // the step's staged-pixel offsets read from tab here, one step ahead like
+      // the fragments (all steps' offsets held at once cost 2 NKS registers)
+      const int m0 = 16 * kk + 8 * (gq >> 1) + qr;
+      const int t0 = tab[m0] * kPitchW + bcol, t1 = tab[m0 + 4] * kPitchW + bcol;
       aq[slot] = *reinterpret_cast<const u4v*>(sg + arow + 16 * kk);
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
         lq[slot][d] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s4*)(simg + tq[j][0] + toff[d] * kPitchW));
+            (lds_s4*)(simg + t0 + toff[d] * kPitchW));
         hq[slot][d] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_s4*)(simg + tq[j][1] + toff[d] * kPitchW));
+            (lds_s4*)(simg + t1 + toff[d] * kPitchW));
       }
     };
     ld(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
@@ -1363,19 +1380,39 @@ int launch_fwd(const Pass& p, const bf16* x, const bf16* wp, bf16* y, float* sta
 }
 
 // weight-gradient split: blocks per (output 64, input 32) channel group
-inline int wgrad_splits(int groups, int64_t npatch) {
-  int64_t s = mde::cdiv(256, groups);
+// blocks a weight-gradient launch aims at (MDE_CONVBF_WBLOCKS, default 256)
+inline int wgrad_blocks_target() {
+  static const int v = [] {
+    const char* e = std::getenv("MDE_CONVBF_WBLOCKS");
+    const int b = e ? std::atoi(e) : 0;
+    return b > 0 ? b : 256;
+  }();
+  return v;
+}
+
+// the weight-gradient kernels' staged-image capacity (its template CAP)
+inline int wgrad_cap(const Pass& p) {
+  return p.ks == 3 ? (p.mode == S1 ? kCapS1W : kCapS2) : kCapS1;
+}
+
+// 3x3: 256 blocks (one a CU: 191 registers x 6 waves); 1x1: 512 (two a CU,
+// measured 41 -> 30 us at 64 -> 64 @60x80, 38.8 -> 27.9 at 256 -> 256 @15x20;
+// the 3x3 kernel forced to two blocks a CU spills and ran 1.6x slower at stride 2)
+inline int wgrad_splits(int groups, int64_t npatch, int ks) {
+  int64_t s = mde::cdiv(wgrad_blocks_target() * (ks == 1 ? 2 : 1), groups);
   if (s > npatch) s = npatch;
   return (int)(s < 1 ? 1 : s);
 }
 
 inline bool wgrad_geo(const Pass& p, int64_t n, Geo* g, int* S, int* per, int64_t* npatch) {
-  if (!pick_geo(p, kMBW, g)) return false;
+  if (!pick_geo(p, p.ks == 3 && p.mode == S1 ? wgrad_mbw<3, S1>() : wgrad_mbw<1, S1>(), g,
+                wgrad_cap(p)))
+    return false;
   const int64_t np = n * g->ppi;
   if (np >= (1 << 22)) return false;  // fdiv's exact range
   *npatch = np;
   const int groups = ((p.cout + 63) / 64) * (p.cin / 32);
-  const int s0 = wgrad_splits(groups, np);
+  const int s0 = wgrad_splits(groups, np, p.ks);
   *per = (int)mde::cdiv(np, s0);
   *S = (int)mde::cdiv(np, *per);
   return true;
@@ -1486,7 +1523,7 @@ int mde_convbf_wgrad(const void* gy, const void* x, float* gweight, int64_t n, i
   const bf16 *gyb = (const bf16*)gy, *xb = (const bf16*)x;
   if (ks == 3) {
     if (p.mode == S1)
-      MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<3, S1, kCapS1>), grid,
+      MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<3, S1, kCapS1W>), grid,
                       dim3(384), 0, xb, gyb, part, g, per, (int)np);
     else
       MDE_LAUNCH_MFMA(mde::K_CBF_WGRAD, bytes, flops, s, (convbf_wgrad_kernel<3, S2, kCapS2>), grid,

@@ -169,8 +169,9 @@ def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     """The NewCRF projections (newcrf_layers.py NewCRF.proj_x / proj_v: 3x3
     convs WITH a bias, cfg4 bs 16) through nn.Conv2d's biased HIP path: the
     Winograd forward (and data gradient where cout -> cin is a Winograd shape;
-    112 input channels take MIOpen's), + bias; output and all three gradients
-    vs float64."""
+    112 input channels take MIOpen's), + bias, the weight gradient on the HIP
+    wide kernel (MIOpen's at 112 input channels); output and all three
+    gradients vs float64."""
     from monocular_depth_estimation_amd.nn import WINO, Conv2d, conv3x3_passes
     n = 16
     g = torch.Generator().manual_seed(cin + cout + h)
@@ -188,6 +189,9 @@ def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     passes = conv3x3_passes(conv, xg)
     assert passes is not None and passes[0] == WINO, passes
     assert (passes[1] == WINO) == (cin % 32 == 0), passes
+    # the weight gradient on the NCHW HIP wide kernel where cin % 32 == 0
+    # (MDE_WIDE_WGRAD), else MIOpen's: the mixed-pass biased conv
+    assert bool(passes[2]) == (cin % 32 == 0), passes
     y = conv(xg)
     yr = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), 1, 1)
     assert rel_err(y, yr) <= 1e-5, "forward"

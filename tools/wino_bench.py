@@ -20,11 +20,13 @@ SHAPES = [(64, 64, 60, 80), (32, 32, 120, 160), (32, 32, 240, 320), (16, 16, 480
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=0)
+    ap.add_argument("--only", default="", help="ci,co,h,w")
     a = ap.parse_args()
+    shapes = [tuple(int(v) for v in a.only.split(","))] if a.only else SHAPES
     n = 32
     kbench._STREAM = torch.cuda.Stream()
     with torch.cuda.stream(kbench._STREAM):
-        for ci, co, h, w in SHAPES:
+        for ci, co, h, w in shapes:
             x = torch.rand((n, ci, h, w), device="cuda") - 0.5
             wt = (torch.rand((co, ci, 3, 3), device="cuda") - 0.5) * 0.1
             y = torch.empty((n, co, h, w), device="cuda")

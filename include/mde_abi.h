@@ -726,7 +726,8 @@ int mde_batchnorm_stats_route(int64_t n, int64_t c, int64_t h, int64_t w, int64_
  * mde_convbf_pack: the filter of one pass as packed bf16 [cin/32][ks*ks][cout]
  * [32] (transpose = 0, the forward) or of the data gradient (transpose = 1:
  * channels swapped, taps flipped), mde_convbf_pack_elems elements;
- * mde_convbf_pack_both: both in one launch (either output nullable).
+ * mde_convbf_pack_both: both in one launch (either output nullable);
+ * mde_convbf_pack_table: every filter of a table in one launch.
  * mde_convbf_fwd: y from x and the forward pack; stats (nullable) receives the
  * following BatchNorm's per-block shifted sums [cout][blocks][4] (blocks =
  * mde_convbf_stats_blocks).  mde_convbf_bwd_data: gx [n,cin,h,w] from gy and
@@ -742,6 +743,13 @@ int mde_convbf_pack(const float* weight, void* packed, int64_t cin, int64_t cout
                     int transpose, void* stream);
 int mde_convbf_pack_both(const float* weight, void* packed, void* packed_t, int64_t cin,
                          int64_t cout, int ks, void* stream);
+/* Many filters in one launch: table [rows][8] int64 on the device, row =
+ * {weight ptr, packed ptr, packed_t ptr (0: none), cin, cout, ks, first
+ * block, 0}, first block = the sum over earlier rows of
+ * ceil(max(pack elems, transposed pack elems) / 256); blocks = that sum over
+ * all rows; elems = the total packed elements (launch accounting only). */
+int mde_convbf_pack_table(const int64_t* table, int rows, int64_t blocks, int64_t elems,
+                          void* stream);
 int mde_convbf_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
                             int stride);
 int mde_convbf_fwd(const void* x, const void* packed, void* y, float* stats, int64_t n,

@@ -9,6 +9,7 @@ from __future__ import annotations
 from torch import nn
 
 from ...functional import bilinear_resize_x2_slotted, nearest_pyramid
+from ...nn import convbf_pack_scope
 from .DDRNet_23_slim import DualResNet_Backbone
 from .modules import Guided_Upsampling_Block
 
@@ -27,6 +28,10 @@ class GuideDepth(nn.Module):
                 guide_features=3, guidance_type="full"))
 
     def forward(self, x):
+        with convbf_pack_scope(self, x.device):  # every bf16 filter packed by one launch
+            return self._forward(x)
+
+    def _forward(self, x):
         y = self.feature_extractor(x)
         # both nearest guides (:46-47) from one pass over the image
         x_half, x_quarter = nearest_pyramid(x)

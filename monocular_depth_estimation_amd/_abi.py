@@ -166,6 +166,7 @@ SIGNATURES = {
     "mde_convbf_pack_elems": (_sz, [_i64, _i64, _int, _int]),
     "mde_convbf_pack": (_int, [_vp, _vp, _i64, _i64, _int, _int, _vp]),
     "mde_convbf_pack_both": (_int, [_vp, _vp, _vp, _i64, _i64, _int, _vp]),
+    "mde_convbf_pack_table": (_int, [_vp, _int, _i64, _i64, _vp]),
     "mde_convbf_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64, _int, _int]),
     "mde_convbf_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_convbf_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),

@@ -1088,6 +1088,31 @@ __global__ void __launch_bounds__(256)
   if (p1 && e < total1) p1[e] = pack_elem(w, e, cin, cout, kk, true);
 }
 
+// Every registered filter of a model in one launch (mde_convbf_pack_table):
+// table row r = {weight, packed, packed_t (nullable), cin, cout, ks,
+// first block, 0}; the rows' blocks are laid end to end over a 1-D grid and a
+// block finds its row by binary search over the first-block column.
+__global__ void __launch_bounds__(256)
+    convbf_pack_table_kernel(const int64_t* __restrict__ tab, int rows) {
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = rows - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[(int64_t)mid * 8 + 6] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* t = tab + (int64_t)lo * 8;
+  const float* w = reinterpret_cast<const float*>(t[0]);
+  bf16* p0 = reinterpret_cast<bf16*>(t[1]);
+  bf16* p1 = reinterpret_cast<bf16*>(t[2]);
+  const int cin = (int)t[3], cout = (int)t[4], ks = (int)t[5], kk = ks * ks;
+  const int64_t total0 = (int64_t)((cin + 31) / 32) * 32 * cout * kk;
+  const int64_t total1 = (int64_t)((cout + 31) / 32) * 32 * cin * kk;
+  const int64_t e = (b - t[6]) * 256 + threadIdx.x;
+  if (p0 && e < total0) p0[e] = pack_elem(w, e, cin, cout, kk, false);
+  if (p1 && e < total1) p1[e] = pack_elem(w, e, cin, cout, kk, true);
+}
+
 // ------------------------------------------------------------------- host
 constexpr int kCapS1 = 420;   // staged pixels: 33.6 KB (+ 36.9 KB filter): two blocks a CU
 constexpr int kCapS2 = 640;   // stride 2 / zero-inserted: 51 KB (one block a CU)
@@ -1452,6 +1477,15 @@ int mde_convbf_pack_both(const float* weight, void* packed, void* packed_t, int6
   MDE_LAUNCH(mde::K_CBF_PACK, 4.0 * cin * cout * ks * ks * ((t0 > 0) + (t1 > 0)) + 2.0 * (t0 + t1),
              (hipStream_t)stream, convbf_pack_kernel, dim3((unsigned)mde::cdiv(total, 256)), dim3(256),
              0, weight, (bf16*)packed, (bf16*)packed_t, (int)cin, (int)cout, ks * ks, t0, t1);
+  return MDE_OK;
+}
+
+int mde_convbf_pack_table(const int64_t* table, int rows, int64_t blocks, int64_t elems,
+                          void* stream) {
+  if (!table || rows <= 0 || blocks <= 0 || blocks > 0x7fffffff || elems < 0)
+    return MDE_ERR_INVALID_ARG;
+  MDE_LAUNCH(mde::K_CBF_PACK, 6.0 * elems, (hipStream_t)stream, convbf_pack_table_kernel,
+             dim3((unsigned)blocks), dim3(256), 0, table, rows);
   return MDE_OK;
 }
 

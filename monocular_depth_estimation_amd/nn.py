@@ -9,6 +9,7 @@ state_dict keys) are unchanged.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -792,6 +793,71 @@ WINO32 = os.environ.get("MDE_WINO32", "1") != "0"  # the 32-channel output group
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"
 
 
+class _PackScope:
+    """The bf16 filters of one model's convbf convolutions, packed for a whole
+    forward in ONE launch (mde_convbf_pack_table) when the model's forward
+    enters convbf_pack_scope, instead of one pack launch per conv (48 a cfg3
+    step, ~7 us each).  A conv is registered on its first eager forward (its
+    persistent packed buffers allocated then) and is in the table from the
+    next forward; inside a graph capture nothing is registered or rebuilt, so
+    the captured launch packs the table of the last eager step."""
+
+    def __init__(self):
+        self.entries = {}  # weight -> (packed, packed_t, cin, cout, ks)
+        self.table = None
+        self.rows = []  # weights in table order
+        self.ptrs = ()
+        self.blocks = 0
+        self.elems = 0
+        self.packed = frozenset()  # weights packed by this forward's table launch
+
+    def _ptrs(self):
+        return tuple(w.data_ptr() for w in self.entries)
+
+    def refresh(self, device):
+        """Rebuild the device table when convs were registered or a weight moved."""
+        ptrs = self._ptrs()
+        if self.table is not None and ptrs == self.ptrs:
+            return
+        rows, blk, elems = [], 0, 0
+        for wgt, (wp, wt, cin, cout, ks) in self.entries.items():
+            rows.append([wgt.data_ptr(), wp.data_ptr(), wt.data_ptr(), cin, cout, ks, blk, 0])
+            blk += -(-max(wp.numel(), wt.numel()) // 256)
+            elems += wp.numel() + wt.numel()
+        self.table = torch.tensor(rows, dtype=torch.int64, device=device)
+        self.rows, self.ptrs, self.blocks, self.elems = list(self.entries), ptrs, blk, elems
+
+
+CONVBF_PACK_ALL = os.environ.get("MDE_CONVBF_PACK_ALL", "1") != "0"  # A/B: 0 = a pack per conv
+_ACTIVE_PACK = None
+
+
+@contextlib.contextmanager
+def convbf_pack_scope(owner: nn.Module, device):
+    """Run `owner`'s forward with its registered convbf filters packed by one
+    launch at entry (see _PackScope); a no-op off the GPU, with
+    MDE_CONVBF_PACK_ALL=0, or when the bf16 convs are off."""
+    global _ACTIVE_PACK
+    if not (CONVBF_PACK_ALL and device.type == "cuda" and _ACTIVE_PACK is None):
+        yield
+        return
+    sc = owner.__dict__.get("_convbf_pack")
+    if sc is None:
+        sc = owner.__dict__["_convbf_pack"] = _PackScope()
+    if sc.entries and not torch.cuda.is_current_stream_capturing():
+        sc.refresh(device)
+    sc.packed = frozenset()
+    if sc.table is not None:
+        _abi.call("mde_convbf_pack_table", _abi.ptr(sc.table), len(sc.rows), sc.blocks, sc.elems,
+                  _abi.stream_of(sc.table))
+        sc.packed = frozenset(sc.rows)
+    _ACTIVE_PACK = sc
+    try:
+        yield
+    finally:
+        _ACTIVE_PACK = None
+
+
 class _ConvBf16(torch.autograd.Function):
     """A DDRNet convolution under bf16 autocast (3x3 p1 / 1x1 p0, stride 1 or
     2, channels % 32) on the bf16 implicit-GEMM kernels of convbf.hip:
@@ -815,11 +881,19 @@ class _ConvBf16(torch.autograd.Function):
         ho, wo = (h + 2 * pad - ks) // stride + 1, (w + 2 * pad - ks) // stride + 1
         st = _abi.stream_of(x)
         bf = dict(dtype=torch.bfloat16, device=x.device)
-        wp = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 0), **bf)
-        wt = (torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 1), **bf)
-              if ctx.needs_input_grad[0] else None)
-        _abi.call("mde_convbf_pack_both", _abi.ptr(weight), _abi.ptr(wp), _abi.ptr(wt), cin, cout,
-                  ks, st)
+        sc = _ACTIVE_PACK
+        ent = sc.entries.get(weight) if sc is not None else None
+        if ent is not None and weight in sc.packed:
+            wp, wt = ent[0], ent[1]  # packed at the scope's entry with every other filter
+        else:
+            wp = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 0), **bf)
+            wt = torch.empty(_abi.query("mde_convbf_pack_elems", cin, cout, ks, 1), **bf)
+            _abi.call("mde_convbf_pack_both", _abi.ptr(weight), _abi.ptr(wp), _abi.ptr(wt), cin,
+                      cout, ks, st)
+            if (sc is not None and ent is None and isinstance(weight, nn.Parameter)
+                    and not torch.cuda.is_current_stream_capturing()):
+                sc.entries[weight] = (wp, wt, cin, cout, ks)  # in the table from the next forward
+                sc.dirty = True
         y = torch.empty((n, cout, ho, wo), **bf)
         nb = _abi.query("mde_convbf_stats_blocks", n, cin, cout, h, w, ks, stride) if want_stats else 0
         stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)

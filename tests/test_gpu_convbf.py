@@ -114,6 +114,56 @@ def test_convbf_weight_gradient_is_deterministic():
     assert torch.equal(grads[0], grads[1])
 
 
+def test_convbf_pack_scope_matches_per_conv_pack():
+    """convbf_pack_scope (every filter packed by one table launch) gives
+    bitwise the outputs and gradients of the per-conv pack, across weight
+    updates and a conv registered late."""
+    from monocular_depth_estimation_amd import nn as mnn
+    from monocular_depth_estimation_amd.nn import Conv2d
+
+    class Two(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = Conv2d(64, 128, 3, stride=2, padding=1, bias=False)
+            self.b = Conv2d(128, 64, 1, bias=False)
+            self.c = Conv2d(64, 64, 3, padding=1, bias=False)
+
+        def forward(self, x, late):
+            y = self.b(self.a(x))
+            return self.c(y) if late else y
+
+    m = Two().to(DEV)
+    x = torch.randn((2, 64, 60, 80), device=DEV).to(torch.bfloat16)
+
+    def run(scoped, late):
+        xg = x.clone().requires_grad_(True)
+        for p in m.parameters():
+            p.grad = None
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            if scoped:
+                with mnn.convbf_pack_scope(m, x.device):
+                    y = m(xg, late)
+            else:
+                y = m(xg, late)
+        y.float().square().sum().backward()
+        return [y.detach().clone(), xg.grad.clone()] + [p.grad.clone() for p in m.parameters()
+                                                        if p.grad is not None]
+
+    for step in range(4):
+        late = step >= 2
+        got, ref = run(True, late), run(False, late)
+        assert len(got) == len(ref)
+        for g_, r_ in zip(got, ref):
+            assert torch.equal(g_, r_), f"step {step}"
+        sc = m.__dict__["_convbf_pack"]
+        assert len(sc.entries) == (3 if late else 2)
+        if step >= 1:
+            assert len(sc.packed) == (2 if step == 2 else len(sc.entries))
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(0.9).add_(0.01)
+
+
 def test_convbf_biased_conv_adds_bias_in_bf16():
     """Conv2d(bias=True) on the bf16 route (DDRNet's segmenthead 1x1): output in
     autocast's dtype, bias gradient = the sum of gy."""

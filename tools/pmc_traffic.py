@@ -109,7 +109,7 @@ NAMES = [
     (r"convbf_fwd_(res_)?kernel", "convbf_fwd_bf16+convbf_dgrad_bf16"),
     (r"convbf_wgrad_kernel", "convbf_wgrad_bf16"),
     (r"convbf_wreduce_kernel", "convbf_wreduce"),
-    (r"convbf_pack_kernel", "convbf_pack"),
+    (r"convbf_pack_(table_)?kernel", "convbf_pack"),
     (r"stem_bf16_fwd_kernel", "stem_fwd_bf16"),
     (r"stem_bf16_wgrad_kernel|stem_wreduce_kernel", "stem_wgrad_bf16"),
     (r"eval_partial_kernel", "eval_sums"),

@@ -245,4 +245,13 @@ __device__ __forceinline__ Sh sh_merge(Sh a, Sh b) {
   return a;
 }
 
+// The bf16-product pointwise convolutions (pwbf.hip), called by skip.hip's
+// mde_pointwise_* entry points for bf16 storage.
+int pwbf_fwd(const bf16* x, const float* sc, const float* sh, const float* wt, bf16* y,
+             float* stats, int64_t n, int64_t cin, int64_t cout, int64_t hw, int blocks,
+             hipStream_t s);
+int pwbf_bwd(const bf16* gy, const bf16* x, const float* sc, const float* sh, const float* mean,
+             const float* wt, bf16* gs, float* slab, int64_t n, int64_t cin, int64_t cout,
+             int64_t hw, int blocks, hipStream_t s);
+
 }  // namespace mde

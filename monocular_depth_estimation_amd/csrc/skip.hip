@@ -1263,6 +1263,16 @@ static int pw_fwd_blocks(int64_t n, int64_t hw, bool stats = false) {
 
 }  // extern "C"
 
+// bf16 storage: the bf16-product kernels of pwbf.hip (MDE_PW_BF=0: the
+// fp32-product kernels above, for A/B)
+static bool pw_bf_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_PW_BF");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <typename T>
 static int pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,
                          const float* wt, void* y, float* stats, int64_t n, int64_t cin,
@@ -1274,6 +1284,10 @@ static int pointwise_fwd(const void* x, const float* in_scale, const float* in_s
   const dim3 grid((unsigned)pw_fwd_blocks(n, hw, stats != nullptr));
   const T* xi = (const T*)x;
   T* yo = (T*)y;
+  if constexpr (std::is_same_v<T, mde::bf16>) {
+    if (pw_bf_on())  // bf16 products (pwbf.hip)
+      return mde::pwbf_fwd(xi, in_scale, in_shift, wt, yo, stats, n, cin, cout, hw, (int)grid.x, s);
+  }
   // 64 -> 64 with the BN operand and the statistics epilogue: two 64 -> 32
   // halves (one launch holding all 64 outputs needs > 256 registers: one wave
   // per SIMD); each half re-reads the input, from L2 mostly
@@ -1379,6 +1393,13 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
   // channels (wider ones spill two register sets): the prefetching kernel
   // (MDE_PW_PF=0: skip_bwd_mfma_kernel)
   const bool pf = std::is_same_v<T, mde::bf16> && go != nullptr && pw_pf_on();
+  const bool bfp = std::is_same_v<T, mde::bf16> && go != nullptr && pw_bf_on();
+  if (bfp) {  // bf16 products (pwbf.hip)
+    const int rc = mde::pwbf_bwd((const mde::bf16*)gy, (const mde::bf16*)x, in_scale, in_shift,
+                                 sums ? in_mean : nullptr, wt, (mde::bf16*)gx, slab, n, cin, cout,
+                                 hw, nb, s);
+    if (rc != MDE_OK) return rc;
+  } else {
 #define MDE_PW_BWD(A, B)                                                                     \
   if (cin == A && cout == B && A <= 16 && pf && in_scale) {                                  \
     const mde::bf16* gib = (const mde::bf16*)gy;                                             \
@@ -1410,6 +1431,7 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
   }
   MDE_PW_SHAPES(MDE_PW_BWD)
 #undef MDE_PW_BWD
+  }
   const int npairs = (int)(cin * cout), nextra = sums ? 2 * (int)cin : 0;
   const int stride = npairs + (int)cout + nextra;
   if (sums) {  // every slab column: gw, (the unused bias columns), the BN sums

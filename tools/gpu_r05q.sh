@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-5 call Q: bf16-product pointwise kernels (pwbf.hip): parity, kernel A/B, cfg3 step.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r05q
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_bf16.py tests/test_gpu_conv3x3.py -q -rfE -p no:cacheprovider --timeout 200 --timeout-method thread > $OUT/t.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|^ERROR|passed|failed" $OUT/t.log | tail -8 | cut -c1-250; [ $rc -eq 0 ] || exit $rc
+for v in 1 0; do
+  MDE_PW_BF=$v timeout -k 10 200 python3 -u tools/pw_bf16_bench.py > $OUT/pw_$v.log 2>&1
+  rc=$?; echo "pw_bf=$v rc=$rc"; grep pointwise $OUT/pw_$v.log; [ $rc -eq 0 ] || exit $rc
+done
+timeout -k 10 300 python3 -u bench.py --no-cpu-baseline --amp bf16 --steps 30 --warmup 5 > $OUT/bench.json 2> $OUT/bench.log
+rc=$?; echo "bench rc=$rc $(python3 -c "import json;d=json.load(open('$OUT/bench.json'));k=d['hip_kernels'];print(d['value'], d['ms_per_step'], k.get('pointwise_fwd'), k.get('pointwise_bwd'))" 2>/dev/null)"; [ $rc -eq 0 ] || exit $rc

@@ -42,6 +42,8 @@ NAMES = [
     (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, true", "skip_reduce_bwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, false", "pointwise_bwd"),
+    (r"pwbf_fwd_kernel", "pointwise_fwd"),
+    (r"pwbf_bwd_kernel|pw_bwd_pf_kernel", "pointwise_bwd"),
     (r"conv3x3_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd"),
     (r"conv3x3_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad"),
     (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd_bf16"),

@@ -66,6 +66,13 @@ def main():
         us = timeit(fn)
         print(f"pointwise_bwd {a.dtype} {cin}->{cout} @{h}x{w}: {us:8.1f} us  "
               f"{nbytes / us / 1e3:7.1f} GB/s", flush=True)
+        y2 = torch.empty_like(gy)
+        ff = lambda: _abi.call("mde_pointwise_fwd", _abi.ptr(y1), _abi.ptr(sc), _abi.ptr(sh),  # noqa: E731
+                               _abi.ptr(w2), _abi.ptr(y2), n, cin, cout, h, w, code, st)
+        us = timeit(ff)
+        fb = es * n * h * w * (cout + cin)
+        print(f"pointwise_fwd {a.dtype} {cin}->{cout} @{h}x{w}: {us:8.1f} us  "
+              f"{fb / us / 1e3:7.1f} GB/s", flush=True)
 
 
 if __name__ == "__main__":

@@ -54,9 +54,10 @@ def pmc_files(workload: str, amp: str) -> list[str]:
 AMP_DTYPE = ("bf16 autocast: every 3x3 / 1x1 conv with 32k channels (DDRNet's stride-1 / stride-2 "
              "convs, the 32-640-channel decoder / DAPPM convs) on the HIP bf16 implicit-GEMM kernels "
              "(convbf, v_mfma_f32_32x32x16_bf16, fp32 accumulation, fp32 weight gradients), the "
-             "16->16 / 32->32 3x3 convs on the HIP bf16 MFMA kernels, the 3-channel guide convs "
-             "bf16 in-kernel; the 3-channel stem conv bf16 on MIOpen; BatchNorm, BN-ReLU-1x1, skip "
-             "fusion, SE-over-BN and every resize on bf16 activations with fp32 statistics / "
+             "16->16 / 32->32 3x3 convs on the HIP bf16 MFMA kernels, the 3-channel stem and "
+             "guide convs bf16 on HIP (stem.hip / in-kernel); the BN-ReLU-1x1 pointwise convs with "
+             "bf16 products (pwbf.hip, v_mfma_f32_16x16x32_bf16); BatchNorm, skip fusion, "
+             "SE-over-BN and every resize on bf16 activations with fp32 statistics / "
              "accumulation; SSIM + L1 loss fp32")
 
 

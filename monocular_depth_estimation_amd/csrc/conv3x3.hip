@@ -1554,6 +1554,279 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
+// Row stage of the second bf16 forward (conv3x3_bf_fwd2_kernel): the tile's
+// XR input rows x CI channels, ordered (row, channel), four (row, channel)
+// lines per wave instruction -- lane (sub = lane / 16, i = lane % 16) loads
+// the 4 columns c0 + 4i .. + 3 of line 16 k + 4 wave + sub, i.e. row k (CI =
+// 16) or k / 2 (CI = 32) of channel 4 wave + sub (+ 16 for odd k at CI = 32):
+// every address is a lane constant plus a uniform per-k offset.  The halo
+// columns c0 - 1 and c0 + 64 come from a 2-byte load by lanes i = 0 and 15
+// (the other lanes re-read their own first column); the shifted copies take
+// the neighbour columns by DPP row shifts (a 16-lane DPP row = one line).
+template <int CI, int XR>
+struct RowStage {
+  static constexpr int K = XR * CI / 16;  // instructions per wave
+  u2v v[K];
+  uint32_t hl[K];
+  __device__ static __forceinline__ int line_r(int k) { return CI == 16 ? k : k >> 1; }
+  __device__ static __forceinline__ int line_c(int k) { return CI == 16 ? 0 : 16 * (k & 1); }
+  // buffer loads from the image's resource: a lane-constant 32-bit offset
+  // (past the buffer for out-of-image columns) plus a uniform per-line offset
+  // (past the buffer for out-of-image rows): zeros with no selects
+  __device__ __forceinline__ void load(const bf16* __restrict__ img, int h, int w, int r0, int c0,
+                                       int lane, int wvu) {
+    const int sub = lane >> 4, i = lane & 15;
+    const int c = 4 * wvu + sub;
+    const int hw = h * w;
+    const int gc = c0 + 4 * i;
+    const int hc = i == 0 ? c0 - 1 : (i == 15 ? c0 + 64 : gc);
+    const uint32_t vo = gc < w ? (uint32_t)(2 * (c * hw + gc)) : 0x7ffffff0u;  // w % 4 == 0
+    const uint32_t vh = (unsigned)hc < (unsigned)w ? (uint32_t)(2 * (c * hw + hc)) : 0x7ffffff0u;
+    const uint64_t a = (uint64_t)img;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 2 * CI * hw, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int gr = r0 - 1 + line_r(k);
+      const int so = (unsigned)gr < (unsigned)h ? 2 * (line_c(k) * hw + gr * w) : 0x7ffffff0;
+      v[k] = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(R, vo, so, 0));
+      hl[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R, vh, so, 0);
+    }
+  }
+  template <int GO>
+  __device__ __forceinline__ void store(bf16* sx, int lane, int wvu) const {
+    using L = CopyTile<CI, XR, GO>;
+    const int sub = lane >> 4, i = lane & 15;
+    const int c = 4 * wvu + sub;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      // previous column (lane i - 1's last, or the left halo), next column
+      // (lane i + 1's first, or the right halo)
+      const uint32_t py = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k].y, 0x111, 0xf, 0xf, false);
+      const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k].x, 0x101, 0xf, 0xf, false);
+      const uint32_t p1 = i == 0 ? hl[k] << 16 : py;
+      const uint32_t n0 = i == 15 ? hl[k] : nx;
+      const u2v d1 = v[k];
+      const u2v d0 = u2v{__builtin_amdgcn_alignbit(v[k].x, p1, 16),
+                         __builtin_amdgcn_alignbit(v[k].y, v[k].x, 16)};
+      const u2v d2 = u2v{__builtin_amdgcn_alignbit(v[k].y, v[k].x, 16),
+                         __builtin_amdgcn_alignbit(n0, v[k].y, 16)};
+      const int cc = c + line_c(k), r = line_r(k);
+      *reinterpret_cast<u2v*>(sx + L::at(0, cc, r, 4 * i)) = d0;
+      *reinterpret_cast<u2v*>(sx + L::at(1, cc, r, 4 * i)) = d1;
+      *reinterpret_cast<u2v*>(sx + L::at(2, cc, r, 4 * i)) = d2;
+    }
+  }
+};
+
+__device__ __forceinline__ uint32_t pk_bf(float a, float b) {
+  using bf2v = __bf16 __attribute__((ext_vector_type(2)));
+  return __builtin_bit_cast(uint32_t, bf2v{(__bf16)a, (__bf16)b});
+}
+
+// The bf16 forward / data gradient of conv3x3_bf_fwd_kernel with (i) the row
+// stage above instead of ChunkStage (linear addressing, no 18-chunk rows:
+// the index arithmetic was ~60 % of the loop's VALU and SALU instructions,
+// SQ_INSTS_VALU 15x SQ_INSTS_MFMA) and (ii) interior tiles stored through
+// the hardware bf16 conversion without per-pixel bounds tests.  Same operand
+// layouts, K order and summation order: bit-identical results.
+// DEPTH: register stages (2 at 16 channels; the 32-channel kernel has no
+// registers for a second).
+template <int CI, int CO, int RPW, bool FLIP, bool STATS, int DEPTH = (CI == 16 ? 2 : 1)>
+__global__ void __launch_bounds__(256, 2)
+    conv3x3_bf_fwd2_kernel(const bf16* __restrict__ x, const float* __restrict__ wt,
+                           bf16* __restrict__ y, int h, int w, int tiles_w, int tiles_per_img,
+                           int ntiles, float* __restrict__ stats) {
+  static_assert(CI == 16 || CI == 32, "bf16 forward: 16 or 32 input channels");
+  static_assert(CO % 16 == 0, "output channels in 16-blocks");
+  constexpr int TH = 4 * RPW, XR = TH + 2;
+  constexpr int NB = CO / 16;
+  constexpr int NS = CI == 16 ? 5 : 9;  // K steps of 32
+  using L = CopyTile<CI, XR, 64>;
+  __shared__ __attribute__((aligned(16))) bf16 sx[L::ELEMS];
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int wvu = __builtin_amdgcn_readfirstlane(wv);
+  const int li = lane & 15, g = lane >> 4;
+  const int64_t img_in = (int64_t)CI * h * w, img_out = (int64_t)CO * h * w;
+
+  u4v wb[NS][NB];
+#pragma unroll
+  for (int st = 0; st < NS; ++st)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int co = 16 * nb + li;
+      const int tap = CI == 32 ? st : 2 * st + (g >> 1);
+      const int c8 = CI == 32 ? 8 * g : 8 * (g & 1);
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ci = c8 + j;
+        const int src = FLIP ? (ci * CO + co) * 9 + (8 - tap) : (co * CI + ci) * 9 + tap;
+        const float t = wt[tap < 9 ? src : 0];
+        f[j] = tap < 9 ? t : 0.f;
+      }
+      wb[st][nb] = u4v{pack_bf(f[0], f[1]), pack_bf(f[2], f[3]), pack_bf(f[4], f[5]),
+                       pack_bf(f[6], f[7])};
+    }
+  const int q = li >> 2, p = li & 3;
+  int aoff[NS];
+#pragma unroll
+  for (int st = 0; st < NS; ++st) {
+    const int tap = CI == 32 ? st : (2 * st + (g >> 1) < 9 ? 2 * st + (g >> 1) : 8);
+    const int c8 = CI == 32 ? 8 * g : 8 * (g & 1);
+    aoff[st] = L::at(tap % 3, c8 + q, tap / 3, 4 * p);
+  }
+
+  mde::Sh run[STATS ? NB : 1];
+#pragma unroll
+  for (int nb = 0; nb < (STATS ? NB : 1); ++nb) run[nb] = {0.f, 0.f, 0.f, 0.f};
+  bool first = true;
+  // two register stages, the loop unrolled by two so each has fixed
+  // registers and the waits count exactly the other stage's loads
+  RowStage<CI, XR> S0, S1;
+  const TileWalk tw = tile_walk(ntiles);
+  // unconditional (past the end: the last tile again, unused) so every step
+  // issues the same loads and the waits stay exact
+  auto fetch = [&](RowStage<CI, XR>& S, int t) {
+    const TileGeo gn = tile_geo(t < tw.end ? t : tw.end - 1, TH, tiles_w, tiles_per_img);
+    S.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
+  };
+  auto step = [&](RowStage<CI, XR>& S, int tile) {
+    const TileGeo gg = tile_geo(tile, TH, tiles_w, tiles_per_img);
+    __syncthreads();
+    S.template store<64>(sx, lane, wvu);
+    __syncthreads();
+    if constexpr (DEPTH == 1) fetch(S, tile + tw.step);  // in flight during this tile's math
+    f4v acc[RPW][4][NB];
+#pragma unroll
+    for (int qq = 0; qq < RPW; ++qq)
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) acc[qq][m][nb] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int qq = 0; qq < RPW; ++qq) {
+      const int row = wv * RPW + qq;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+#pragma unroll
+        for (int st = 0; st < NS; ++st) {
+          const bf16* base = sx + aoff[st] + row * 64 + 16 * m;
+          const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base);
+          const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + 4 * L::PL));
+          const u2v l2 = __builtin_bit_cast(u2v, lo), h2 = __builtin_bit_cast(u2v, hi);
+          const u4v a = u4v{l2.x, l2.y, h2.x, h2.y};
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) acc[qq][m][nb] = mfma_bf(a, wb[st][nb], acc[qq][m][nb]);
+        }
+      }
+    }
+    // D: lane holds pixels 16m + 4g + r (r = 0..3) of output channel 16nb + li
+    bf16* yi = y + gg.img * img_out;
+    const bool interior = gg.r0 + TH <= h && gg.c0 + 64 <= w;  // block-uniform
+    if (interior) {
+      bf16* yb = yi + (int64_t)li * h * w + (int64_t)(gg.r0 + wv * RPW) * w + gg.c0 + 4 * g;
+#pragma unroll
+      for (int qq = 0; qq < RPW; ++qq)
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const f4v v = acc[qq][m][nb];
+            const u2v u{pk_bf(v[0], v[1]), pk_bf(v[2], v[3])};
+            *reinterpret_cast<u2v*>(yb + (int64_t)16 * nb * h * w + qq * w + 16 * m) = u;
+            if constexpr (STATS) {
+              const float b[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                  __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+              if (first && qq == 0 && m == 0) run[nb].ref = __shfl(b[0], li, 64);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) mde::sh_add(run[nb], b[r], true);
+            }
+          }
+    } else {
+#pragma unroll
+      for (int qq = 0; qq < RPW; ++qq) {
+        const int row = gg.r0 + wv * RPW + qq;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int col = gg.c0 + 16 * m + 4 * g;
+#pragma unroll
+          for (int nb = 0; nb < NB; ++nb) {
+            const f4v v = acc[qq][m][nb];
+            const u2v u{pk_bf(v[0], v[1]), pk_bf(v[2], v[3])};
+            if constexpr (STATS) {
+              const float b[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                  __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+              if (first && qq == 0 && m == 0) {
+                const bool ok0 = gg.r0 + wv * RPW < h && gg.c0 < w;
+                run[nb].ref = __shfl(ok0 ? b[0] : 0.f, li, 64);
+              }
+              const bool ok = row < h && col < w;  // w % 4 == 0: all 4 columns or none
+#pragma unroll
+              for (int r = 0; r < 4; ++r) mde::sh_add(run[nb], b[r], ok);
+            }
+            if (row < h && col < w)
+              *reinterpret_cast<u2v*>(yi + ((int64_t)(16 * nb + li) * h + row) * w + col) = u;
+          }
+        }
+      }
+    }
+    first = false;
+    // DEPTH 2: the next-but-one tile's loads, after this tile's stores (a wait
+    // for the stores' source registers then leaves these loads in flight)
+    if constexpr (DEPTH == 2) fetch(S, tile + 2 * tw.step);
+  };
+  int tile = tw.t0;
+  if constexpr (DEPTH == 1) {
+    if (tile < tw.end) fetch(S0, tile);
+    for (; tile < tw.end; tile += tw.step) step(S0, tile);
+  } else {
+    if (tile < tw.end) {
+      fetch(S0, tile);
+      fetch(S1, tile + tw.step);
+    }
+    while (tile < tw.end) {
+      step(S0, tile);
+      tile += tw.step;
+      if (tile >= tw.end) break;
+      step(S1, tile);
+      tile += tw.step;
+    }
+  }
+  if constexpr (STATS) {
+    __syncthreads();
+    float* part = reinterpret_cast<float*>(sx);  // [4][CO][4]
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const mde::Sh a = mde::sh_xor_sum(mde::sh_xor_sum(run[nb], 16), 32);
+      if (g == 0) {
+        float* p4 = part + (wv * CO + 16 * nb + li) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
+    }
+    __syncthreads();
+    if (tid < CO) {
+      mde::Sh a{part[tid * 4], part[tid * 4 + 1], part[tid * 4 + 2], part[tid * 4 + 3]};
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const float* p4 = part + (k * CO + tid) * 4;
+        a = mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      float* o4 = stats + ((int64_t)tid * gridDim.x + blockIdx.x) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
+    }
+  }
+}
+
 // gy tile: CO planes of TH rows x 64 columns (plane pitch 16 mod 128), four
 // rows per wave instruction (16 lanes x 8 B per row).
 template <int CO, int TH>
@@ -2012,6 +2285,16 @@ int launch_wgrad_s2(const float* x, const float* gy, float* gw, int64_t n, int64
 }
 
 // ---- bf16 dispatch
+// conv3x3_bf_fwd2_kernel (row stage, interior fast stores) where the width
+// allows (w % 4 == 0); MDE_C3BF_V2=0: the first kernel (A/B).
+inline bool bf_v2(int64_t h, int64_t w) {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_C3BF_V2");
+    return !(e && e[0] == '0');
+  }();
+  return on && w % 4 == 0 && 2 * 32 * h * w < (int64_t)1 << 30;  // 32-bit buffer offsets
+}
+
 template <int CI, int CO, int RPW, bool FLIP, bool STATS>
 int bf_fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_img, int* ntiles) {
   constexpr int TH = 4 * RPW;
@@ -2020,7 +2303,8 @@ int bf_fwd_grid(int64_t n, int64_t h, int64_t w, int* tiles_w, int* tiles_per_im
   const int64_t nt = n * *tiles_per_img;
   if (nt > 0x7fffffff) return 0;
   *ntiles = (int)nt;
-  const int res = resident_blocks<conv3x3_bf_fwd_kernel<CI, CO, RPW, FLIP, STATS>>();
+  const int res = bf_v2(h, w) ? resident_blocks<conv3x3_bf_fwd2_kernel<CI, CO, RPW, FLIP, STATS>>()
+                           : resident_blocks<conv3x3_bf_fwd_kernel<CI, CO, RPW, FLIP, STATS>>();
   return nt < res ? (int)nt : res;
 }
 
@@ -2049,9 +2333,14 @@ int launch_bf_fwd(const bf16* in, const float* wt, bf16* out, int64_t n, int64_t
   const int grid =
       bf_fwd_grid<CI, CO, RPW, FLIP, STATS>(n, h, w, &tiles_w, &tiles_per_img, &ntiles);
   if (grid <= 0) return MDE_ERR_INVALID_ARG;
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_bf_fwd_kernel<CI, CO, RPW, FLIP, STATS>),
-                  dim3(grid), dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img,
-                  ntiles, stats);
+  if (bf_v2(h, w))
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_bf_fwd2_kernel<CI, CO, RPW, FLIP, STATS>),
+                    dim3(grid), dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img,
+                    ntiles, stats);
+  else
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (conv3x3_bf_fwd_kernel<CI, CO, RPW, FLIP, STATS>),
+                    dim3(grid), dim3(256), 0, in, wt, out, (int)h, (int)w, tiles_w, tiles_per_img,
+                    ntiles, stats);
   return MDE_OK;
 }
 

@@ -310,7 +310,7 @@ def _main():
                   flush=True)
         bf = torch.bfloat16
         tconv = torch.nn.functional.conv2d
-        for cin, cout, h, w in ((16, 16, 480, 640), (32, 32, 240, 320)):
+        for cin, cout, h, w in ((16, 16, 480, 640), (32, 32, 240, 320), (32, 32, 120, 160)):
             x = (torch.rand(n, cin, h, w, device=dev) - 0.5).to(bf)
             wt = torch.rand(cout, cin, 3, 3, device=dev) - 0.5
             gy = (torch.rand(n, cout, h, w, device=dev) - 0.5).to(bf)

@@ -1707,13 +1707,16 @@ __global__ void __launch_bounds__(256, 2)
       for (int m = 0; m < 4; ++m)
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb) acc[qq][m][nb] = f4v{0.f, 0.f, 0.f, 0.f};
+    // K step outer, the 4 RPW accumulators inner: consecutive MFMAs are
+    // independent (the m-inner chains of the first kernel issue-stalled on
+    // their own results: SQ_WAIT_INST_ANY 58 % of wave cycles)
 #pragma unroll
-    for (int qq = 0; qq < RPW; ++qq) {
-      const int row = wv * RPW + qq;
+    for (int st = 0; st < NS; ++st) {
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
+      for (int qq = 0; qq < RPW; ++qq) {
+        const int row = wv * RPW + qq;
 #pragma unroll
-        for (int st = 0; st < NS; ++st) {
+        for (int m = 0; m < 4; ++m) {
           const bf16* base = sx + aoff[st] + row * 64 + 16 * m;
           const s4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)base);
           const s4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4*)(base + 4 * L::PL));
@@ -1726,53 +1729,47 @@ __global__ void __launch_bounds__(256, 2)
     }
     // D: lane holds pixels 16m + 4g + r (r = 0..3) of output channel 16nb + li
     bf16* yi = y + gg.img * img_out;
-    const bool interior = gg.r0 + TH <= h && gg.c0 + 64 <= w;  // block-uniform
-    if (interior) {
-      bf16* yb = yi + (int64_t)li * h * w + (int64_t)(gg.r0 + wv * RPW) * w + gg.c0 + 4 * g;
+    // Output through LDS: the block's [TH rows][CO][64] tile (line pitch 68:
+    // conflict-free 8-byte writes) then full 128-byte line segments per 16
+    // lanes (direct stores from the D layout wrote 32-byte pieces of 16
+    // channel rows per instruction).
+    constexpr int LP = 68;
+    static_assert(TH * CO * LP <= L::ELEMS && TH * CO * 16 % 256 == 0, "output tile in LDS");
+    __syncthreads();  // every wave's A reads of sx are done
 #pragma unroll
-      for (int qq = 0; qq < RPW; ++qq)
+    for (int qq = 0; qq < RPW; ++qq) {
+      const int row = gg.r0 + wv * RPW + qq;
 #pragma unroll
-        for (int m = 0; m < 4; ++m)
+      for (int m = 0; m < 4; ++m) {
+        const int col = gg.c0 + 16 * m + 4 * g;
 #pragma unroll
-          for (int nb = 0; nb < NB; ++nb) {
-            const f4v v = acc[qq][m][nb];
-            const u2v u{pk_bf(v[0], v[1]), pk_bf(v[2], v[3])};
-            *reinterpret_cast<u2v*>(yb + (int64_t)16 * nb * h * w + qq * w + 16 * m) = u;
-            if constexpr (STATS) {
-              const float b[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                                  __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
-              if (first && qq == 0 && m == 0) run[nb].ref = __shfl(b[0], li, 64);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) mde::sh_add(run[nb], b[r], true);
+        for (int nb = 0; nb < NB; ++nb) {
+          const f4v v = acc[qq][m][nb];
+          const u2v u{pk_bf(v[0], v[1]), pk_bf(v[2], v[3])};
+          *reinterpret_cast<u2v*>(sx + ((wv * RPW + qq) * CO + 16 * nb + li) * LP + 16 * m + 4 * g) = u;
+          if constexpr (STATS) {
+            const float b[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
+            if (first && qq == 0 && m == 0) {
+              const bool ok0 = gg.r0 + wv * RPW < h && gg.c0 < w;
+              run[nb].ref = __shfl(ok0 ? b[0] : 0.f, li, 64);
             }
-          }
-    } else {
+            const bool ok = row < h && col < w;  // w % 4 == 0: all 4 columns or none
 #pragma unroll
-      for (int qq = 0; qq < RPW; ++qq) {
-        const int row = gg.r0 + wv * RPW + qq;
-#pragma unroll
-        for (int m = 0; m < 4; ++m) {
-          const int col = gg.c0 + 16 * m + 4 * g;
-#pragma unroll
-          for (int nb = 0; nb < NB; ++nb) {
-            const f4v v = acc[qq][m][nb];
-            const u2v u{pk_bf(v[0], v[1]), pk_bf(v[2], v[3])};
-            if constexpr (STATS) {
-              const float b[4] = {__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                                  __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u)};
-              if (first && qq == 0 && m == 0) {
-                const bool ok0 = gg.r0 + wv * RPW < h && gg.c0 < w;
-                run[nb].ref = __shfl(ok0 ? b[0] : 0.f, li, 64);
-              }
-              const bool ok = row < h && col < w;  // w % 4 == 0: all 4 columns or none
-#pragma unroll
-              for (int r = 0; r < 4; ++r) mde::sh_add(run[nb], b[r], ok);
-            }
-            if (row < h && col < w)
-              *reinterpret_cast<u2v*>(yi + ((int64_t)(16 * nb + li) * h + row) * w + col) = u;
+            for (int r = 0; r < 4; ++r) mde::sh_add(run[nb], b[r], ok);
           }
         }
       }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < TH * CO * 16 / 256; ++k) {
+      const int e = tid + 256 * k, line = e >> 4, ch = e & 15;
+      const int r = line / CO, co = line % CO;
+      const int grow = gg.r0 + r, col = gg.c0 + 4 * ch;
+      const u2v u = *reinterpret_cast<const u2v*>(sx + line * LP + 4 * ch);
+      if (grow < h && col < w)
+        *reinterpret_cast<u2v*>(yi + ((int64_t)co * h + grow) * w + col) = u;
     }
     first = false;
     // DEPTH 2: the next-but-one tile's loads, after this tile's stores (a wait

@@ -773,10 +773,9 @@ __global__ void __launch_bounds__(256, 1)
     // instruction touch 64 planes: store-issue-bound).  (Deferring those stores
     // into the next patch's first step, past its input loads' vmcnt wait, from
     // a separate LDS tile measured 3 % slower.)
-    if (flat) __syncthreads();  // every wave is done reading the image
+    __syncthreads();  // every wave is done reading the image
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-      bf16* yc = y + ((int64_t)P.img * g.cout + co0 + col[j]) * hwo;
 #pragma unroll
       for (int i = 0; i < MTW; ++i) {
         if (!mt_on[i]) continue;
@@ -786,9 +785,9 @@ __global__ void __launch_bounds__(256, 1)
           const int m = mt * 32 + 8 * qq + 4 * h;
           const uint32_t p01 = pack2bf(acc[i][j][4 * qq], acc[i][j][4 * qq + 1]);
           const uint32_t p23 = pack2bf(acc[i][j][4 * qq + 2], acc[i][j][4 * qq + 3]);
-          int r = 0, c = 0;
-          const bool ok = flat ? m < P.npx : pix_of(g, P, m, r, c);
           if constexpr (STATS) {
+            int r = 0, c = 0;
+            const bool ok = flat ? m < P.npx : pix_of(g, P, m, r, c);
             const float v0 = __uint_as_float(p01 << 16), v1 = __uint_as_float(p01 & 0xffff0000u);
             const float v2 = __uint_as_float(p23 << 16), v3 = __uint_as_float(p23 & 0xffff0000u);
             if (!have_ref[j]) {
@@ -800,15 +799,12 @@ __global__ void __launch_bounds__(256, 1)
             mde::sh_add(run[j], v2, ok);
             mde::sh_add(run[j], v3, ok);
           }
-          if (flat)
-            *reinterpret_cast<u2v*>(simg + col[j] * kOP + m) = u2v{p01, p23};
-          else if (ok)
-            *reinterpret_cast<u2v*>(yc + (int64_t)r * g.wo + c) = u2v{p01, p23};
+          *reinterpret_cast<u2v*>(simg + col[j] * kOP + m) = u2v{p01, p23};
         }
       }
     }
+    __syncthreads();
     if (flat) {
-      __syncthreads();
       bf16* yb = y + ((int64_t)P.img * g.cout + co0) * hwo + P.p0;
 #pragma unroll
       for (int k = 0; k < NB * MB / 8 / 256; ++k) {
@@ -819,6 +815,35 @@ __global__ void __launch_bounds__(256, 1)
           *reinterpret_cast<u4v*>(dst) = v;
         else if (px < P.npx)  // npx % 4 == 0: half a chunk
           *reinterpret_cast<u2v*>(dst) = u2v{v[0], v[1]};
+      }
+    } else {
+      // 2D patches (pr rows x pc columns) through the same LDS rows: row
+      // segments of 8 (pc % 8 == 0) or 4 pixels per lane (the fragments' own
+      // 4-pixel pieces wrote 8 bytes of 64 planes per instruction)
+      bf16* yb = y + ((int64_t)P.img * g.cout + co0) * hwo;
+      if (g.pc % 8 == 0) {
+#pragma unroll
+        for (int k = 0; k < NB * MB / 8 / 256; ++k) {
+          const int j = tid + 256 * k, co = j / (MB / 8), m0 = 8 * (j % (MB / 8));
+          const int mr = fdiv(m0, g.pc, g.inv_pc), r = P.r0 + mr, c = P.c0 + (m0 - mr * g.pc);
+          if (m0 < P.npx && r < g.ho && c < g.wo) {
+            const u4v v = *reinterpret_cast<const u4v*>(simg + co * kOP + m0);
+            bf16* dst = yb + (int64_t)co * hwo + (int64_t)r * g.wo + c;
+            if (c + 8 <= g.wo)
+              *reinterpret_cast<u4v*>(dst) = v;
+            else  // wo % 4 == 0: half a chunk
+              *reinterpret_cast<u2v*>(dst) = u2v{v[0], v[1]};
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NB * MB / 4 / 256; ++k) {
+          const int j = tid + 256 * k, co = j / (MB / 4), m0 = 4 * (j % (MB / 4));
+          const int mr = fdiv(m0, g.pc, g.inv_pc), r = P.r0 + mr, c = P.c0 + (m0 - mr * g.pc);
+          if (m0 < P.npx && r < g.ho && c < g.wo)
+            *reinterpret_cast<u2v*>(yb + (int64_t)co * hwo + (int64_t)r * g.wo + c) =
+                *reinterpret_cast<const u2v*>(simg + co * kOP + m0);
+        }
       }
     }
     if (q + 1 < q1) {

@@ -1555,32 +1555,38 @@ __global__ void __launch_bounds__(256, 2)
 }
 
 // Row stage of the second bf16 forward (conv3x3_bf_fwd2_kernel): the tile's
-// XR input rows x CI channels, ordered (row, channel), four (row, channel)
-// lines per wave instruction -- lane (sub = lane / 16, i = lane % 16) loads
-// the 4 columns c0 + 4i .. + 3 of line 16 k + 4 wave + sub, i.e. row k (CI =
-// 16) or k / 2 (CI = 32) of channel 4 wave + sub (+ 16 for odd k at CI = 32):
-// every address is a lane constant plus a uniform per-k offset.  The halo
-// columns c0 - 1 and c0 + 64 come from a 2-byte load by lanes i = 0 and 15
-// (the other lanes re-read their own first column); the shifted copies take
-// the neighbour columns by DPP row shifts (a 16-lane DPP row = one line).
+// XR input rows x CI channels as (row, channel) lines, 16-byte buffer loads
+// -- 8 lanes per 64-column line, 8 lines per wave instruction (line 32 k + 8
+// wave + sub): every offset is a lane constant plus a uniform per-line one,
+// past the buffer (zeros) for out-of-image rows and columns.  The halo
+// columns c0 - 1 and c0 + 64 come from 2-byte loads by the 2 edge lanes of a
+// line only (exec masked); the shifted copies take the neighbour columns by
+// DPP row shifts.  (An 8-byte, 16-lanes-a-line stage with every lane loading
+// a halo element kept the texture addresser ~75 % busy -- TA_TA_BUSY_sum /
+// GRBM_GUI_ACTIVE -- at 207 us for the 16 -> 16 forward; this one: 194 us.)
 template <int CI, int XR>
-struct RowStage {
-  static constexpr int K = XR * CI / 16;  // instructions per wave
-  u2v v[K];
+struct RowStage8 {
+  static constexpr int K = XR * CI / 32;  // instructions per wave
+  static_assert(XR * CI % 32 == 0, "whole instructions");
+  u4v v[K];
   uint32_t hl[K];
-  __device__ static __forceinline__ int line_r(int k) { return CI == 16 ? k : k >> 1; }
-  __device__ static __forceinline__ int line_c(int k) { return CI == 16 ? 0 : 16 * (k & 1); }
-  // buffer loads from the image's resource: a lane-constant 32-bit offset
-  // (past the buffer for out-of-image columns) plus a uniform per-line offset
-  // (past the buffer for out-of-image rows): zeros with no selects
+  __device__ static __forceinline__ int line_r(int k, int wvu) {
+    return CI == 32 ? k : 2 * k + (wvu >> 1);
+  }
+  __device__ static __forceinline__ int line_c(int wvu, int sub) {
+    return CI == 32 ? 8 * wvu + sub : 8 * (wvu & 1) + sub;
+  }
   __device__ __forceinline__ void load(const bf16* __restrict__ img, int h, int w, int r0, int c0,
                                        int lane, int wvu) {
-    const int sub = lane >> 4, i = lane & 15;
-    const int c = 4 * wvu + sub;
+    const int sub = lane >> 3, i = lane & 7;
+    const int c = line_c(wvu, sub);
     const int hw = h * w;
-    const int gc = c0 + 4 * i;
-    const int hc = i == 0 ? c0 - 1 : (i == 15 ? c0 + 64 : gc);
-    const uint32_t vo = gc < w ? (uint32_t)(2 * (c * hw + gc)) : 0x7ffffff0u;  // w % 4 == 0
+    const int gc = c0 + 8 * i;
+    // w % 4 == 0: an 8-column chunk is all in, all out, or (last 4 columns
+    // out) read as 16 bytes whose second half lies past the row -- zeroed below
+    const uint32_t vo = gc < w ? (uint32_t)(2 * (c * hw + gc)) : 0x7ffffff0u;
+    const bool half = gc + 4 >= w;
+    const int hc = i == 0 ? c0 - 1 : c0 + 64;
     const uint32_t vh = (unsigned)hc < (unsigned)w ? (uint32_t)(2 * (c * hw + hc)) : 0x7ffffff0u;
     const uint64_t a = (uint64_t)img;
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
@@ -1589,34 +1595,49 @@ struct RowStage {
         reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 2 * CI * hw, 0x00020000);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int gr = r0 - 1 + line_r(k);
-      const int so = (unsigned)gr < (unsigned)h ? 2 * (line_c(k) * hw + gr * w) : 0x7ffffff0;
-      v[k] = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(R, vo, so, 0));
-      hl[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R, vh, so, 0);
+      const int gr = r0 - 1 + line_r(k, wvu);
+      const int so = (unsigned)gr < (unsigned)h ? 2 * (gr * w) : 0x7ffffff0;
+      u4v t = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(R, vo, so, 0));
+      if (half) t = u4v{t[0], t[1], 0u, 0u};
+      v[k] = t;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) hl[k] = 0u;
+    if (i == 0 || i == 7) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int gr = r0 - 1 + line_r(k, wvu);
+        const int so = (unsigned)gr < (unsigned)h ? 2 * (gr * w) : 0x7ffffff0;
+        hl[k] = (uint32_t)__builtin_amdgcn_raw_buffer_load_b16(R, vh, so, 0);
+      }
     }
   }
   template <int GO>
   __device__ __forceinline__ void store(bf16* sx, int lane, int wvu) const {
     using L = CopyTile<CI, XR, GO>;
-    const int sub = lane >> 4, i = lane & 15;
-    const int c = 4 * wvu + sub;
+    const int sub = lane >> 3, i = lane & 7;
+    const int c = line_c(wvu, sub);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       // previous column (lane i - 1's last, or the left halo), next column
-      // (lane i + 1's first, or the right halo)
-      const uint32_t py = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k].y, 0x111, 0xf, 0xf, false);
-      const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k].x, 0x101, 0xf, 0xf, false);
-      const uint32_t p1 = i == 0 ? hl[k] << 16 : py;
-      const uint32_t n0 = i == 15 ? hl[k] : nx;
-      const u2v d1 = v[k];
-      const u2v d0 = u2v{__builtin_amdgcn_alignbit(v[k].x, p1, 16),
-                         __builtin_amdgcn_alignbit(v[k].y, v[k].x, 16)};
-      const u2v d2 = u2v{__builtin_amdgcn_alignbit(v[k].y, v[k].x, 16),
-                         __builtin_amdgcn_alignbit(n0, v[k].y, 16)};
-      const int cc = c + line_c(k), r = line_r(k);
-      *reinterpret_cast<u2v*>(sx + L::at(0, cc, r, 4 * i)) = d0;
-      *reinterpret_cast<u2v*>(sx + L::at(1, cc, r, 4 * i)) = d1;
-      *reinterpret_cast<u2v*>(sx + L::at(2, cc, r, 4 * i)) = d2;
+      // (lane i + 1's first, or the right halo); a 16-lane DPP row holds 2 lines
+      const uint32_t pw = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k][3], 0x111, 0xf, 0xf, false);
+      const uint32_t nx = (uint32_t)__builtin_amdgcn_mov_dpp((int)v[k][0], 0x101, 0xf, 0xf, false);
+      const uint32_t p1 = i == 0 ? hl[k] << 16 : pw;
+      const uint32_t n0 = i == 7 ? hl[k] : nx;
+      const u4v d1 = v[k];
+      const u4v d0 = u4v{__builtin_amdgcn_alignbit(v[k][0], p1, 16),
+                         __builtin_amdgcn_alignbit(v[k][1], v[k][0], 16),
+                         __builtin_amdgcn_alignbit(v[k][2], v[k][1], 16),
+                         __builtin_amdgcn_alignbit(v[k][3], v[k][2], 16)};
+      const u4v d2 = u4v{__builtin_amdgcn_alignbit(v[k][1], v[k][0], 16),
+                         __builtin_amdgcn_alignbit(v[k][2], v[k][1], 16),
+                         __builtin_amdgcn_alignbit(v[k][3], v[k][2], 16),
+                         __builtin_amdgcn_alignbit(n0, v[k][3], 16)};
+      const int r = line_r(k, wvu);
+      *reinterpret_cast<u4v*>(sx + L::at(0, c, r, 8 * i)) = d0;
+      *reinterpret_cast<u4v*>(sx + L::at(1, c, r, 8 * i)) = d1;
+      *reinterpret_cast<u4v*>(sx + L::at(2, c, r, 8 * i)) = d2;
     }
   }
 };
@@ -1686,15 +1707,15 @@ __global__ void __launch_bounds__(256, 2)
   bool first = true;
   // two register stages, the loop unrolled by two so each has fixed
   // registers and the waits count exactly the other stage's loads
-  RowStage<CI, XR> S0, S1;
+  RowStage8<CI, XR> S0, S1;
   const TileWalk tw = tile_walk(ntiles);
   // unconditional (past the end: the last tile again, unused) so every step
   // issues the same loads and the waits stay exact
-  auto fetch = [&](RowStage<CI, XR>& S, int t) {
+  auto fetch = [&](RowStage8<CI, XR>& S, int t) {
     const TileGeo gn = tile_geo(t < tw.end ? t : tw.end - 1, TH, tiles_w, tiles_per_img);
     S.load(x + gn.img * img_in, h, w, gn.r0, gn.c0, lane, wvu);
   };
-  auto step = [&](RowStage<CI, XR>& S, int tile) {
+  auto step = [&](RowStage8<CI, XR>& S, int tile) {
     const TileGeo gg = tile_geo(tile, TH, tiles_w, tiles_per_img);
     __syncthreads();
     S.template store<64>(sx, lane, wvu);
@@ -1733,8 +1754,8 @@ __global__ void __launch_bounds__(256, 2)
     // conflict-free 8-byte writes) then full 128-byte line segments per 16
     // lanes (direct stores from the D layout wrote 32-byte pieces of 16
     // channel rows per instruction).
-    constexpr int LP = 68;
-    static_assert(TH * CO * LP <= L::ELEMS && TH * CO * 16 % 256 == 0, "output tile in LDS");
+    constexpr int LP = 72;  // 16-byte aligned lines, 2-way at most on the 8-byte writes
+    static_assert(TH * CO * LP <= L::ELEMS && TH * CO * 8 % 256 == 0, "output tile in LDS");
     __syncthreads();  // every wave's A reads of sx are done
 #pragma unroll
     for (int qq = 0; qq < RPW; ++qq) {
@@ -1763,13 +1784,16 @@ __global__ void __launch_bounds__(256, 2)
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < TH * CO * 16 / 256; ++k) {
-      const int e = tid + 256 * k, line = e >> 4, ch = e & 15;
+    for (int k = 0; k < TH * CO * 8 / 256; ++k) {  // 16-byte pieces, 8 lanes a line
+      const int e = tid + 256 * k, line = e >> 3, ch = e & 7;
       const int r = line / CO, co = line % CO;
-      const int grow = gg.r0 + r, col = gg.c0 + 4 * ch;
-      const u2v u = *reinterpret_cast<const u2v*>(sx + line * LP + 4 * ch);
-      if (grow < h && col < w)
-        *reinterpret_cast<u2v*>(yi + ((int64_t)co * h + grow) * w + col) = u;
+      const int grow = gg.r0 + r, col = gg.c0 + 8 * ch;
+      const u4v u = *reinterpret_cast<const u4v*>(sx + line * LP + 8 * ch);
+      bf16* dst = yi + ((int64_t)co * h + grow) * w + col;
+      if (grow < h && col + 8 <= w)
+        *reinterpret_cast<u4v*>(dst) = u;
+      else if (grow < h && col < w)  // w % 4 == 0: the first half
+        *reinterpret_cast<u2v*>(dst) = u2v{u[0], u[1]};
     }
     first = false;
     // DEPTH 2: the next-but-one tile's loads, after this tile's stores (a wait

@@ -1848,37 +1848,42 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
-// gy tile: CO planes of TH rows x 64 columns (plane pitch 16 mod 128), four
-// rows per wave instruction (16 lanes x 8 B per row).
+// gy tile of the bf16 weight gradient: CO planes of TH rows x 64 columns
+// (plane pitch 16 mod 128), 16-byte loads: line L = 32 k + 8 wave + sub of
+// the (channel, tile row) order, 8 lanes per 64-column line (channel L / TH,
+// row L % TH: the row is a lane constant, the channel steps by 32 / TH per k,
+// a uniform offset).
 template <int CO, int TH>
-struct GyStage {
+struct GyStage8 {
   static constexpr int PL = (TH * 64 + 127) / 128 * 128 + 16;
-  static constexpr int ROWS = CO * TH;
-  static constexpr int PER = (ROWS + 15) / 16;
-  u2v v[PER];
+  static constexpr int K = CO * TH / 32;
+  static_assert(CO * TH % 32 == 0 && 32 % TH == 0, "whole instructions");
+  u4v v[K];
   __device__ __forceinline__ void load(const bf16* __restrict__ img, int h, int w, int r0,
                                        int c0, int lane, int wvu) {
-    const int sub = lane >> 4, i = lane & 15;
-    const int gc = c0 + 4 * i;
-    const bool cok = gc + 3 < w;
+    const int sub = lane >> 3, i = lane & 7, l0 = 8 * wvu + sub;
+    const int c = l0 / TH, gr = r0 + l0 % TH, gc = c0 + 8 * i;
+    const int hw = h * w;
+    const uint32_t vo = gr < h && gc < w ? (uint32_t)(2 * (c * hw + gr * w + gc)) : 0x7ffffff0u;
+    const bool half = gc + 4 >= w;  // w % 4 == 0
+    const uint64_t a = (uint64_t)img;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 2 * CO * hw, 0x00020000);
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int row = 16 * k + 4 * wvu + sub;
-      const int c = row / TH, gr = r0 + row % TH;
-      const bool ok = cok && row < ROWS && gr < h;
-      const u2v t = *reinterpret_cast<const u2v*>(
-          img + (ok ? (unsigned)((c * h + gr) * w + gc) : 0u));
-      v[k] = ok ? t : u2v{0u, 0u};
+    for (int k = 0; k < K; ++k) {
+      u4v t = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(R, vo, 2 * (32 / TH) * k * hw, 0));
+      if (half) t = u4v{t[0], t[1], 0u, 0u};
+      v[k] = t;
     }
   }
   __device__ __forceinline__ void store(bf16* sg, int lane, int wvu) const {
-    const int sub = lane >> 4, i = lane & 15;
+    const int sub = lane >> 3, i = lane & 7, l0 = 8 * wvu + sub;
+    const int c = l0 / TH, r = l0 % TH;
 #pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int row = 16 * k + 4 * wvu + sub;
-      if (row < ROWS)
-        *reinterpret_cast<u2v*>(sg + (row / TH) * PL + (row % TH) * 64 + 4 * i) = v[k];
-    }
+    for (int k = 0; k < K; ++k)
+      *reinterpret_cast<u4v*>(sg + (c + (32 / TH) * k) * PL + r * 64 + 8 * i) = v[k];
   }
 };
 
@@ -1887,7 +1892,7 @@ template <int CI, int CO, int TH, int PW>
 struct BfWgradCfg {
   static constexpr int XR = TH + 2;
   using LX = CopyTile<CI, XR, 0>;
-  using GS = GyStage<CO, TH>;
+  using GS = GyStage8<CO, TH>;
   static constexpr int MB = CO / 16;
   static constexpr int NP = 9 * CI;  // n = tap * CI + ci
   static constexpr int NBLK = NP / 16;
@@ -1933,7 +1938,7 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
     for (int j = 0; j < C::NBW; ++j) acc[mb][j] = f4v{0.f, 0.f, 0.f, 0.f};
 
-  ChunkStage<CI, C::XR> S;
+  RowStage8<CI, C::XR> S;
   typename C::GS G;
   const TileWalk tw = tile_walk(ntiles);
   int tile = tw.t0;

@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=gpurun_out/r05p
+OUT=gpurun_out/r05prof
 mkdir -p $OUT
 export TMPDIR=/tmp MASTER_ADDR=127.0.0.1
 run() {  # name, timeout, command...

@@ -18,7 +18,7 @@ MARK = "minmax_partial_kernel"
 
 OURS = re.compile(r"^(bilinear|nearest|se_partial|se_fc|se_scale|se_bfc|se_wgrad|se_apply|skip_|minmax|"
                   r"depthnorm|ssim3|loss_final|dloss|bn_|sebn_|wattn|dw_|ln_|conv3x3|wgrad_reduce|transpose_kernel|"
-                  r"colsum|gelu_|nyu_|eval_|wino_|c3s2_|c3s1_|c1_|cm_kernel|convbf_|graph_fill)")
+                  r"colsum|gelu_|nyu_|eval_|wino_|c3s2_|c3s1_|c1_|cm_kernel|convbf_|graph_fill|pwbf_|pw_bwd|stem_|c3in3)")
 
 
 def short(name: str) -> str:

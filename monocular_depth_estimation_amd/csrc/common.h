@@ -253,5 +253,12 @@ int pwbf_fwd(const bf16* x, const float* sc, const float* sh, const float* wt, b
 int pwbf_bwd(const bf16* gy, const bf16* x, const float* sc, const float* sh, const float* mean,
              const float* wt, bf16* gs, float* slab, int64_t n, int64_t cin, int64_t cout,
              int64_t hw, int blocks, hipStream_t s);
+bool pwbf_skip_ok(int64_t cin, int64_t cout);
+int pwbf_skip_fwd(const bf16* r, const bf16* d, const float* sc, const float* sh, const float* wt,
+                  const float* b, bf16* out, int64_t n, int64_t cin, int64_t cout, int64_t hw,
+                  int blocks, hipStream_t s);
+int pwbf_skip_bwd(const bf16* gy, const bf16* r, const bf16* d, const float* sc, const float* sh,
+                  const float* mean, const float* wt, bf16* gs, float* slab, int64_t n,
+                  int64_t cin, int64_t cout, int64_t hw, int blocks, hipStream_t s);
 
 }  // namespace mde

@@ -78,14 +78,35 @@ __device__ __forceinline__ u4v frag_bnr(const u2v (&rows)[8], int s, const float
   return f;
 }
 
+// bf16 rounding of a float (RNE), as a float
+__device__ __forceinline__ float rbf(float v) { return (float)(__bf16)v; }
+
+// The skip fusion's operand (HAS_D, modules.py:100 `reduce(residual + depth)`
+// under autocast): s = bf16(bf16(relu(x * sc + sh)) + d) -- the BN-ReLU output
+// and the sum each rounded as autocast's bf16 tensors are.
+__device__ __forceinline__ u4v frag_skip(const u2v (&rows)[8], const u2v (&drows)[8], int s,
+                                         const float (&sc)[8], const float (&sh)[8]) {
+  u4v f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    f[e] = pk(rbf(fmaxf(fmaf(pix(rows[2 * e], s), sc[2 * e], sh[2 * e]), 0.f)) + pix(drows[2 * e], s),
+              rbf(fmaxf(fmaf(pix(rows[2 * e + 1], s), sc[2 * e + 1], sh[2 * e + 1]), 0.f)) +
+                  pix(drows[2 * e + 1], s));
+  return f;
+}
+
 // ----------------------------------------------------------------- forward
 // STATS: the output's per-channel shifted sums per block (the layout of
 // skip_fwd_mfma_kernel's epilogue: stats[(o * gridDim.x + block) * 4]).
-template <int CI, int CO, bool BNR, bool STATS>
+// HAS_D (with BNR): the skip fusion, s = bf16(bf16(relu(bn(x))) + d), plus a
+// bias (rounded to bf16 as autocast casts it) -- skip_reduce_bn's forward.
+template <int CI, int CO, bool BNR, bool STATS, bool HAS_D = false>
 __global__ void __launch_bounds__(256)
     pwbf_fwd_kernel(const bf16* __restrict__ x, const float* __restrict__ wt,
                     bf16* __restrict__ y, int64_t n, int64_t hw, const float* __restrict__ isc,
-                    const float* __restrict__ ish, float* __restrict__ stats) {
+                    const float* __restrict__ ish, float* __restrict__ stats,
+                    const bf16* __restrict__ d = nullptr, const float* __restrict__ bias = nullptr) {
+  static_assert(!HAS_D || (BNR && !STATS), "skip fusion: BN-ReLU operand, no statistics");
   constexpr int KS = (CI + 31) / 32, OT = (CO + 15) / 16;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, l16 = lane & 15, q4 = lane >> 4;
@@ -119,11 +140,24 @@ __global__ void __launch_bounds__(256)
   for (int ot = 0; ot < (STATS ? OT : 1); ++ot)
 #pragma unroll
     for (int i = 0; i < 4; ++i) rref[ot][i] = rs1[ot][i] = rs2[ot][i] = 0.f;
+  float bo[HAS_D ? OT : 1][4];  // D rows 16 ot + 4 q4 + i
+#pragma unroll
+  for (int ot = 0; ot < (HAS_D ? OT : 1); ++ot)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = 16 * ot + 4 * q4 + i;
+      bo[ot][i] = HAS_D && bias && o < CO ? rbf(bias[o]) : 0.f;
+    }
   int ntile = 0;
   bool first = true;
   const int64_t tpi = hw / 64, tiles = n * tpi, stride = (int64_t)gridDim.x * 4;
-  u2v A[KS][8], B[KS][8];
-  auto load = [&](int64_t t, u2v (&R)[KS][8]) {
+  constexpr int KD = HAS_D ? KS : 1;
+  struct Raw {
+    u2v x[KS][8];
+    u2v d[KD][8];
+  };
+  Raw A, B;
+  auto load = [&](int64_t t, Raw& R) {
     if (t >= tiles) t = tiles - 1;  // past the end: a valid tile, unused
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
     const bf16* xp = x + nidx * CI * hw + p0 + 4 * l16;
@@ -131,9 +165,17 @@ __global__ void __launch_bounds__(256)
     for (int ks = 0; ks < KS; ++ks)
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        R[ks][j] = rows_live ? ld_nt<u2v>(xp + (int64_t)(32 * ks + 8 * q4 + j) * hw) : u2v{0u, 0u};
+        R.x[ks][j] = rows_live ? ld_nt<u2v>(xp + (int64_t)(32 * ks + 8 * q4 + j) * hw) : u2v{0u, 0u};
+    if constexpr (HAS_D) {
+      const bf16* dp = d + nidx * CI * hw + p0 + 4 * l16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          R.d[ks][j] = rows_live ? ld_nt<u2v>(dp + (int64_t)(32 * ks + 8 * q4 + j) * hw) : u2v{0u, 0u};
+    }
   };
-  auto compute = [&](int64_t t, const u2v (&R)[KS][8]) {
+  auto compute = [&](int64_t t, const Raw& R) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
     bf16* yp = y + nidx * CO * hw + p0 + 4 * l16;
     u4v bf[KS][4];
@@ -142,15 +184,17 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         // (idle rows: zero bits, zero BN coefficients and zero weights)
-        if constexpr (BNR) bf[ks][s] = frag_bnr(R[ks], s, bsc[ks], bsh[ks]);
-        else bf[ks][s] = frag_raw(R[ks], s);
+        if constexpr (HAS_D) bf[ks][s] = frag_skip(R.x[ks], R.d[ks], s, bsc[ks], bsh[ks]);
+        else if constexpr (BNR) bf[ks][s] = frag_bnr(R.x[ks], s, bsc[ks], bsh[ks]);
+        else bf[ks][s] = frag_raw(R.x[ks], s);
       }
 #pragma unroll
     for (int ot = 0; ot < OT; ++ot) {
       f4v acc[4];
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        acc[s] = f4v{0.f, 0.f, 0.f, 0.f};
+        if constexpr (HAS_D) acc[s] = f4v{bo[ot][0], bo[ot][1], bo[ot][2], bo[ot][3]};
+        else acc[s] = f4v{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) acc[s] = mfma_bf(wa[ot][ks], bf[ks][s], acc[s]);
       }
@@ -223,12 +267,13 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------- backward
-template <int CI, int CO, bool BNR, bool BNS>
+template <int CI, int CO, bool BNR, bool BNS, bool HAS_D = false>
 struct PwbfRaw {
   static constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = (CO + 31) / 32;
   u2v gt[KO][8];                // T: gy rows 32 ko + 8 q4 + j, pixels 4 l16 ..
   u4v gr[OT][2];                // R: gy row 16 ot + l16, pixels 32 kk + 8 q4 ..
   u4v sr[MT][2];                // R: x row 16 mt + l16, pixels 32 kk + 8 q4 ..
+  u4v dr[HAS_D ? MT : 1][2];    // R: d row 16 mt + l16 (the skip fusion's second input)
   u2v xr[BNS ? MT : 1][4];      // x rows 16 mt + 4 q4 + i, pixels 4 l16 .. (the gs layout)
 };
 
@@ -236,13 +281,18 @@ struct PwbfRaw {
 // BN sums [CI][2] -- skip_slab_reduce_kernel<1>'s layout.
 // PF: the next tile's operands in a second register set (off at 64 -> 64,
 // whose two sets spill).
-template <int CI, int CO, bool BNR, bool BNS, bool PF = (CI * CO < 4096)>
+// HAS_D (with BNR): the skip fusion's backward -- gs is the gradient of s =
+// relu(bn(x)) + d (both inputs take it), the weight gradient sees s as the
+// forward rounded it, and the slab's bias columns get the row sums of gy.
+template <int CI, int CO, bool BNR, bool BNS, bool HAS_D = false, bool PF = (CI * CO < 4096)>
 __global__ void __launch_bounds__(256, (CI * CO >= 2048 || (BNS && CI >= 32)) ? 1 : 2)
     pwbf_bwd_kernel(const bf16* __restrict__ g, const bf16* __restrict__ x,
                     const float* __restrict__ wt, bf16* __restrict__ gs, float* __restrict__ slab,
                     int64_t n, int64_t hw, const float* __restrict__ isc,
-                    const float* __restrict__ ish, const float* __restrict__ imean) {
-  using Raw = PwbfRaw<CI, CO, BNR, BNS>;
+                    const float* __restrict__ ish, const float* __restrict__ imean,
+                    const bf16* __restrict__ d = nullptr) {
+  static_assert(!HAS_D || BNR, "skip fusion: BN-ReLU operand");
+  using Raw = PwbfRaw<CI, CO, BNR, BNS, HAS_D>;
   constexpr int MT = Raw::MT, OT = Raw::OT, KO = Raw::KO;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   static_assert(!BNS || (BNR && CI <= 32), "BN sums: fused BN-ReLU operand, cin <= 32");
@@ -267,6 +317,7 @@ __global__ void __launch_bounds__(256, (CI * CO >= 2048 || (BNS && CI >= 32)) ? 
   for (int ot = 0; ot < OT; ++ot)
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) gw[ot][mt] = f4v{0.f, 0.f, 0.f, 0.f};
+  float gbp[HAS_D ? OT : 1] = {};  // row 16 ot + l16 of gy, this lane's pixels
   float bsc[MT], bsh[MT];  // the R-load row's channel 16 mt + l16
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -315,6 +366,14 @@ __global__ void __launch_bounds__(256, (CI * CO >= 2048 || (BNS && CI >= 32)) ? 
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
         R.sr[mt][kk] = *reinterpret_cast<const u4v*>(xp + (int64_t)(16 * mt + l16) * hw + 32 * kk + 8 * q4);
+    if constexpr (HAS_D) {
+      const bf16* dp = d + nidx * CI * hw + p0;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          R.dr[mt][kk] = *reinterpret_cast<const u4v*>(dp + (int64_t)(16 * mt + l16) * hw + 32 * kk + 8 * q4);
+    }
     if constexpr (BNS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
@@ -368,7 +427,13 @@ __global__ void __launch_bounds__(256, (CI * CO >= 2048 || (BNS && CI >= 32)) ? 
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         u4v sb;
-        if constexpr (BNR) {
+        if constexpr (HAS_D) {  // s as the forward rounded it
+          const u4v r = R.sr[mt][kk], dd = R.dr[mt][kk];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            sb[e] = pk(rbf(fmaxf(fmaf(lo_f(r[e]), bsc[mt], bsh[mt]), 0.f)) + lo_f(dd[e]),
+                       rbf(fmaxf(fmaf(hi_f(r[e]), bsc[mt], bsh[mt]), 0.f)) + hi_f(dd[e]));
+        } else if constexpr (BNR) {
           const u4v r = R.sr[mt][kk];
 #pragma unroll
           for (int e = 0; e < 4; ++e)
@@ -380,6 +445,16 @@ __global__ void __launch_bounds__(256, (CI * CO >= 2048 || (BNS && CI >= 32)) ? 
 #pragma unroll
         for (int ot = 0; ot < OT; ++ot) gw[ot][mt] = mfma_bf(R.gr[ot][kk], sb, gw[ot][mt]);
       }
+    }
+    if constexpr (HAS_D) {  // the bias gradient: row sums of gy (R layout, fp32)
+#pragma unroll
+      for (int ot = 0; ot < OT; ++ot)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          const u4v q = R.gr[ot][kk];
+          gbp[ot] += ((lo_f(q[0]) + hi_f(q[0])) + (lo_f(q[1]) + hi_f(q[1]))) +
+                     ((lo_f(q[2]) + hi_f(q[2])) + (lo_f(q[3]) + hi_f(q[3])));
+        }
     }
   };
   int64_t t = (int64_t)blockIdx.x * 4 + w;
@@ -431,10 +506,20 @@ __global__ void __launch_bounds__(256, (CI * CO >= 2048 || (BNS && CI >= 32)) ? 
         }
       }
   }
+  if constexpr (HAS_D) {
+#pragma unroll
+    for (int ot = 0; ot < OT; ++ot) {
+      float b = gbp[ot];
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (q4 == 0 && 16 * ot + l16 < CO) red[w][CO * CI + 16 * ot + l16] = b;
+    }
+  }
   __syncthreads();
   float* out = slab + (int64_t)blockIdx.x * ROW;
   for (int i = threadIdx.x; i < ROW; i += 256)
-    out[i] = (i >= CO * CI && i < SOFF) ? 0.f : (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    out[i] = (!HAS_D && i >= CO * CI && i < SOFF) ? 0.f
+                                                  : (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
 }
 
 }  // namespace
@@ -499,6 +584,48 @@ int pwbf_bwd(const bf16* gy, const bf16* x, const float* sc, const float* sh, co
   MDE_PWBF_SHAPES(MDE_PWBF_BWD)
 #undef MDE_PWBF_BWD
   return MDE_ERR_UNSUPPORTED;
+}
+
+// skip_reduce_bn on bf16 storage (64 -> 32, 32 -> 16): out = W . bf16(bf16(
+// relu(r * sc + sh)) + d) + bias; the backward's slab rows as skip_slab_reduce
+// <0> reads them (gW, gb, [BN sums]).
+bool pwbf_skip_ok(int64_t cin, int64_t cout) {
+  return (cin == 64 && cout == 32) || (cin == 32 && cout == 16);
+}
+
+int pwbf_skip_fwd(const bf16* r, const bf16* d, const float* sc, const float* sh, const float* wt,
+                  const float* b, bf16* out, int64_t n, int64_t cin, int64_t cout, int64_t hw,
+                  int blocks, hipStream_t s) {
+  const double bytes = 2.0 * n * hw * (double)(2 * cin + cout);
+  const double flops = 2.0 * n * hw * (double)cin * (double)cout;
+  if (cin == 64 && cout == 32)
+    MDE_LAUNCH_MFMA(K_SKIP_FWD, bytes, flops, s, (pwbf_fwd_kernel<64, 32, true, false, true>),
+                    dim3(blocks), dim3(256), 0, r, wt, out, n, hw, sc, sh, nullptr, d, b);
+  else if (cin == 32 && cout == 16)
+    MDE_LAUNCH_MFMA(K_SKIP_FWD, bytes, flops, s, (pwbf_fwd_kernel<32, 16, true, false, true>),
+                    dim3(blocks), dim3(256), 0, r, wt, out, n, hw, sc, sh, nullptr, d, b);
+  else
+    return MDE_ERR_UNSUPPORTED;
+  return MDE_OK;
+}
+
+int pwbf_skip_bwd(const bf16* gy, const bf16* r, const bf16* d, const float* sc, const float* sh,
+                  const float* mean, const float* wt, bf16* gs, float* slab, int64_t n,
+                  int64_t cin, int64_t cout, int64_t hw, int blocks, hipStream_t s) {
+  const double bytes = 2.0 * n * hw * (double)(3 * cin + cout);
+  const double flops = 4.0 * n * hw * (double)cin * (double)cout;
+  if (cin == 64 && cout == 32 && !mean)
+    MDE_LAUNCH_MFMA(K_SKIP_BWD, bytes, flops, s, (pwbf_bwd_kernel<64, 32, true, false, true>),
+                    dim3(blocks), dim3(256), 0, gy, r, wt, gs, slab, n, hw, sc, sh, mean, d);
+  else if (cin == 32 && cout == 16 && mean)
+    MDE_LAUNCH_MFMA(K_SKIP_BWD, bytes, flops, s, (pwbf_bwd_kernel<32, 16, true, true, true>),
+                    dim3(blocks), dim3(256), 0, gy, r, wt, gs, slab, n, hw, sc, sh, mean, d);
+  else if (cin == 32 && cout == 16)
+    MDE_LAUNCH_MFMA(K_SKIP_BWD, bytes, flops, s, (pwbf_bwd_kernel<32, 16, true, false, true>),
+                    dim3(blocks), dim3(256), 0, gy, r, wt, gs, slab, n, hw, sc, sh, mean, d);
+  else
+    return MDE_ERR_UNSUPPORTED;
+  return MDE_OK;
 }
 
 }  // namespace mde

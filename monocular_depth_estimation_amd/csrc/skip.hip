@@ -1127,6 +1127,16 @@ size_t mde_skip_reduce_bn_workspace(int64_t n, int64_t cin, int64_t cout, int64_
 
 }  // extern "C"
 
+// bf16 storage: the bf16-product kernels of pwbf.hip (MDE_PW_BF=0: the
+// fp32-product kernels above, for A/B)
+static bool pw_bf_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_PW_BF");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // skip_reduce_bn launches on storage type T (fp32, or bf16 under autocast:
 // r, d, out / gout, gs in T; weights, BN coefficients, sums and arithmetic fp32).
 template <typename T>
@@ -1144,6 +1154,11 @@ static int skip_bn_fwd_t(const void* r, const void* d, const float* in_scale,
   }
   const int64_t blocks = mde::cdiv(n * hw / 64, 4);
   const dim3 g((unsigned)(blocks > 4096 ? 4096 : blocks));
+  if constexpr (std::is_same_v<T, mde::bf16>) {
+    if (pw_bf_on() && mde::pwbf_skip_ok(cin, cout))  // bf16 products (pwbf.hip)
+      return mde::pwbf_skip_fwd(R, D, in_scale, in_shift, wt, b, (mde::bf16*)out, n, cin, cout,
+                                hw, (int)g.x, s);
+  }
   if (cin == 64)
     MDE_LAUNCH(mde::K_SKIP_FWD, bytes, s, (skip_fwd_mfma_kernel<64, 32, true, true, false, T>), g,
                dim3(256), 0, R, D, wt, b, (T*)out, n, hw, in_scale, in_shift, nullptr);
@@ -1164,7 +1179,17 @@ static int skip_bn_bwd_t(const void* gout, const void* r, const void* d, const f
   const T *G = (const T*)gout, *R = (const T*)r, *D = (const T*)d;
   T* GS = (T*)gs;
   const bool sums = in_sums != nullptr;
-  if (cin == 16 && sums)
+  bool done = false;
+  if constexpr (std::is_same_v<T, mde::bf16>) {
+    if (pw_bf_on() && mde::pwbf_skip_ok(cin, cout)) {  // bf16 products (pwbf.hip)
+      const int rc = mde::pwbf_skip_bwd(G, R, D, in_scale, in_shift, sums ? in_mean : nullptr, wt,
+                                        GS, slab, n, cin, cout, hw, nb, s);
+      if (rc != MDE_OK) return rc;
+      done = true;
+    }
+  }
+  if (done) {
+  } else if (cin == 16 && sums)
     MDE_LAUNCH(mde::K_SKIP_BWD, bytes, s, (skip_bwd_c1_kernel<16, true, true, T>), dim3(nb),
                dim3(256), 0, G, R, D, wt, GS, slab, n, hw, in_scale, in_shift, in_mean);
   else if (cin == 16)
@@ -1262,16 +1287,6 @@ static int pw_fwd_blocks(int64_t n, int64_t hw, bool stats = false) {
 }
 
 }  // extern "C"
-
-// bf16 storage: the bf16-product kernels of pwbf.hip (MDE_PW_BF=0: the
-// fp32-product kernels above, for A/B)
-static bool pw_bf_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("MDE_PW_BF");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
 
 template <typename T>
 static int pointwise_fwd(const void* x, const float* in_scale, const float* in_shift,

@@ -270,9 +270,10 @@ def test_skip_reduce_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
                                              (4, 1, 2, 30, 40)])
 def test_skip_reduce_bn_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
     """reduce(relu(bn(r + pb)) + d) (the comb_conv's last BN + ReLU and the skip
-    fusion, modules.py:72-73,100) on bf16 activations == the fp32 kernels on
-    the same values: output and d's gradient bit-exact with the rounded fp32
-    results; 1x1 weight / bias gradients to 1e-5 (the BN coefficients of a bf16
+    fusion, modules.py:72-73,100) on bf16 activations vs the fp32 kernels on
+    the same values.  1-output-channel shapes (fp32 products): output and d's
+    gradient bit-exact with the rounded fp32 results; 1x1 weight / bias
+    gradients to 1e-5 (the BN coefficients of a bf16
     and an fp32 input can differ in the last bit: the statistics pass sums in
     another order per storage width); r's gradient (the BN apply reads the
     stored, rounded skip gradient) to bf16 rounding."""
@@ -299,12 +300,21 @@ def test_skip_reduce_bn_bf16_storage_matches_fp32_kernel(cin, cout, n, h, w):
         outs.append((y.detach(), dd.grad, ww.grad, bb.grad, rr.grad, b.weight.grad,
                      b.running_var.clone()))
     (ya, gda, wa, ba, gra, gga, rva), (yb, gdb, wb, bb_, grb, ggb, rvb) = outs
+    torch.testing.assert_close(rva, rvb, rtol=1e-6, atol=0)
+    assert float((gra.float() - grb).abs().max()) <= 1e-2 * float(grb.abs().max())
+    if (cin, cout) in ((64, 32), (32, 16)):
+        # bf16 products (pwbf.hip): the 1x1 sees s = bf16(bf16(relu(bn(r))) + d) and the
+        # weight rounded to bf16, as autocast's conv does -- within bf16 rounding of the
+        # fp32-product kernels
+        def rel(a, b):
+            return float((a.float() - b.float()).abs().max()) / float(b.float().abs().max())
+        assert rel(ya, yb) <= 1e-2 and rel(gda, gdb) <= 1e-2
+        assert rel(wa, wb) <= 1e-2 and rel(ba, bb_) <= 1e-3
+        return
     assert torch.equal(ya, yb.to(torch.bfloat16))
     assert torch.equal(gda, gdb.to(torch.bfloat16))
     torch.testing.assert_close(wa, wb, rtol=1e-5, atol=1e-5 * float(wb.abs().max()))
     torch.testing.assert_close(ba, bb_, rtol=1e-5, atol=1e-5 * float(bb_.abs().max()))
-    torch.testing.assert_close(rva, rvb, rtol=1e-6, atol=0)
-    assert float((gra.float() - grb).abs().max()) <= 1e-2 * float(grb.abs().max())
     assert float((gga - ggb).abs().max()) <= 1e-2 * float(ggb.abs().max())
 
 

@@ -42,11 +42,17 @@ NAMES = [
     (r"skip_fwd_mfma_kernel<\d+, \d+, false", "pointwise_fwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, true", "skip_reduce_bwd"),
     (r"skip_bwd_mfma_kernel<\d+, \d+, false", "pointwise_bwd"),
+    # (first match wins: the skip fusion's instances before the pointwise ones)
+    (r"pwbf_fwd_kernel<\d+, \d+, true, false, true>", "skip_reduce_fwd"),
+    (r"pwbf_bwd_kernel<\d+, \d+, true, (true|false), true", "skip_reduce_bwd"),
     (r"pwbf_fwd_kernel", "pointwise_fwd"),
     (r"pwbf_bwd_kernel|pw_bwd_pf_kernel", "pointwise_bwd"),
     (r"conv3x3_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd"),
     (r"conv3x3_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad"),
-    (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, false", "conv3x3_fwd_bf16"),
+    (r"conv3x3_bf_fwd2?_kernel<\d+, \d+, \d+, false", "conv3x3_fwd_bf16"),
+    (r"conv3x3_bf_fwd2_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad_bf16"),
+    (r"c3in3_bf16_wgrad_kernel<\d+, 2>", "stem_wgrad_bf16"),
+    (r"c3in3_bf16_wgrad_kernel<\d+, 1>", "conv3x3_wgrad_guide"),
     (r"conv3x3_bf_fwd_kernel<\d+, \d+, \d+, true", "conv3x3_dgrad_bf16"),
     (r"conv3x3_bf_wgrad_kernel", "conv3x3_wgrad_bf16"),
     # the fixed-strip kernel under the three ids that launch it (csrc/conv3x3.hip):

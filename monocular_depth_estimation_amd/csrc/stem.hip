@@ -268,7 +268,9 @@ __global__ void __launch_bounds__(256)
 }
 
 // gw[e] = sum over blocks of part[block][e]: one block an element, a fixed
-// per-thread order and a fixed tree (deterministic)
+// per-thread order and a fixed tree (deterministic).  TAG only tells the
+// callers apart in profiles (0: the stem, 1: the guide convs).
+template <int TAG>
 __global__ void __launch_bounds__(256)
     stem_wreduce_kernel(const float* __restrict__ part, float* __restrict__ gw, int nblocks, int ne) {
   __shared__ float red[4];
@@ -316,7 +318,7 @@ int launch_c3in3_wgrad(const bf16* gy, const float* x, float* gw, int64_t n, int
   MDE_LAUNCH_MFMA(kid, bytes, flops, s, (c3in3_bf16_wgrad_kernel<CO, S>), dim3(nb), dim3(256), 0,
                   gy, x, part, (int)h, (int)w, ho, wo, tiles_c, tiles_c * tiles_r, (int)ntiles);
   const int ne = CO * kK;
-  MDE_LAUNCH(kid, 4.0 * nb * ne, s, stem_wreduce_kernel, dim3((unsigned)ne), dim3(256), 0, part,
+  MDE_LAUNCH(kid, 4.0 * nb * ne, s, stem_wreduce_kernel<S == 2 ? 0 : 1>, dim3((unsigned)ne), dim3(256), 0, part,
              gw, nb, ne);
   return MDE_OK;
 }

@@ -119,7 +119,9 @@ NAMES = [
     (r"convbf_wreduce_kernel", "convbf_wreduce"),
     (r"convbf_pack_(table_)?kernel", "convbf_pack"),
     (r"stem_bf16_fwd_kernel", "stem_fwd_bf16"),
-    (r"stem_bf16_wgrad_kernel|stem_wreduce_kernel", "stem_wgrad_bf16"),
+    (r"stem_bf16_wgrad_kernel|stem_wreduce_kernel<0>", "stem_wgrad_bf16"),
+    (r"stem_wreduce_kernel<1>", "conv3x3_wgrad_guide"),
+    (r"stem_wreduce_kernel\(", "stem_wgrad_bf16"),  # builds before the tag
     (r"eval_partial_kernel", "eval_sums"),
     (r"eval_final_kernel", "eval_final"),
     (r"nyu_augment_kernel", "nyu_augment"),

@@ -535,29 +535,36 @@ __global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)  // 64 x 64: W^T
 // loaded one tile ahead into one of two register sets (the loop is unrolled
 // by two so both sets have fixed registers), and gs leaves through the
 // hardware bf16 conversion.
-template <int CI, int CO, bool BNS>
+// T = float (the fp32 step, 16 input channels): the same kernel on float4
+// operands (4 pixels a load either way).
+template <typename T>
+using PwWord = std::conditional_t<std::is_same_v<T, mde::bf16>, uint2, float4>;
+
+template <int CI, int CO, bool BNS, typename T = mde::bf16>
 struct PwRaw {
   static constexpr int MT = CI / 16, OT = (CO + 15) / 16, KO = CO / 4;
   static constexpr int OG = OT <= 2 ? OT : 1;
-  uint2 gb[KO];               // G rows 4 kk + q4, pixels 4 l16 .. + 3
-  uint2 ga[OT][4];            // G rows 16 ot + l16, pixels 16 v + 4 q4 .. + 3
-  uint2 sr[MT][4];            // input rows 16 mt + l16, pixels 16 v + 4 q4 ..
-  uint2 xr[BNS ? MT : 1][4];  // input rows 16 mt + 4 q4 + i, pixels 4 l16 ..
+  PwWord<T> gb[KO];               // G rows 4 kk + q4, pixels 4 l16 .. + 3
+  PwWord<T> ga[OT][4];            // G rows 16 ot + l16, pixels 16 v + 4 q4 .. + 3
+  PwWord<T> sr[MT][4];            // input rows 16 mt + l16, pixels 16 v + 4 q4 ..
+  PwWord<T> xr[BNS ? MT : 1][4];  // input rows 16 mt + 4 q4 + i, pixels 4 l16 ..
 };
 
 __device__ __forceinline__ float4 unpack_bf4(uint2 u) {
   return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
                      __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
 }
+__device__ __forceinline__ float4 unpack_bf4(float4 u) { return u; }
 
-template <int CI, int CO, bool BNS>
+template <int CI, int CO, bool BNS, typename T = mde::bf16>
 __global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)
-    pw_bwd_pf_kernel(const mde::bf16* __restrict__ g, const mde::bf16* __restrict__ r,
-                     const float* __restrict__ wt, mde::bf16* __restrict__ gs,
+    pw_bwd_pf_kernel(const T* __restrict__ g, const T* __restrict__ r,
+                     const float* __restrict__ wt, T* __restrict__ gs,
                      float* __restrict__ slab, int64_t n, int64_t hw,
                      const float* __restrict__ isc, const float* __restrict__ ish,
                      const float* __restrict__ imean) {
-  using Raw = PwRaw<CI, CO, BNS>;
+  using Raw = PwRaw<CI, CO, BNS, T>;
+  using W = PwWord<T>;
   constexpr int MT = Raw::MT, OT = Raw::OT, KO = Raw::KO, OG = Raw::OG;
   static_assert(CI % 16 == 0 && CO % 8 == 0, "tile shapes");
   static_assert(!BNS || CI <= 32, "BN sums: cin <= 32");
@@ -604,34 +611,34 @@ __global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)
   auto load = [&](int64_t t, Raw& R) {
     if (t >= tiles) t = tiles - 1;
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
-    const mde::bf16* gp = g + nidx * CO * hw + p0;
-    const mde::bf16* rp = r + nidx * CI * hw + p0;
+    const T* gp = g + nidx * CO * hw + p0;
+    const T* rp = r + nidx * CI * hw + p0;
 #pragma unroll
     for (int kk = 0; kk < KO; ++kk)
-      R.gb[kk] = *reinterpret_cast<const uint2*>(gp + (4 * kk + q4) * hw + 4 * l16);
+      R.gb[kk] = *reinterpret_cast<const W*>(gp + (4 * kk + q4) * hw + 4 * l16);
 #pragma unroll
     for (int ot = 0; ot < OT; ++ot) {
       const int o = 16 * ot + l16 < CO ? 16 * ot + l16 : CO - 1;
 #pragma unroll
       for (int v = 0; v < 4; ++v)
-        R.ga[ot][v] = *reinterpret_cast<const uint2*>(gp + o * hw + 4 * q4 + 16 * v);
+        R.ga[ot][v] = *reinterpret_cast<const W*>(gp + o * hw + 4 * q4 + 16 * v);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int v = 0; v < 4; ++v)
-        R.sr[mt][v] = *reinterpret_cast<const uint2*>(rp + (16 * mt + l16) * hw + 4 * q4 + 16 * v);
+        R.sr[mt][v] = *reinterpret_cast<const W*>(rp + (16 * mt + l16) * hw + 4 * q4 + 16 * v);
     if constexpr (BNS) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          R.xr[mt][i] = *reinterpret_cast<const uint2*>(rp + (16 * mt + 4 * q4 + i) * hw + 4 * l16);
+          R.xr[mt][i] = *reinterpret_cast<const W*>(rp + (16 * mt + 4 * q4 + i) * hw + 4 * l16);
     }
   };
   auto compute = [&](int64_t t, const Raw& R) {
     const int64_t nidx = t / tpi, p0 = (t - nidx * tpi) * 64;
-    mde::bf16* sp = gs + nidx * CI * hw + p0;
+    T* sp = gs + nidx * CI * hw + p0;
     float4 gb[KO];
 #pragma unroll
     for (int kk = 0; kk < KO; ++kk) gb[kk] = unpack_bf4(R.gb[kk]);
@@ -649,11 +656,16 @@ __global__ void __launch_bounds__(256, CI * CO >= 4096 ? 1 : 2)
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        using bf2 = __bf16 __attribute__((ext_vector_type(2)));
-        const bf2 lo = {(__bf16)acc[0][i], (__bf16)acc[1][i]};
-        const bf2 hi = {(__bf16)acc[2][i], (__bf16)acc[3][i]};
-        const mde::nt2u u{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
-        __builtin_nontemporal_store(u, reinterpret_cast<mde::nt2u*>(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16));
+        if constexpr (std::is_same_v<T, mde::bf16>) {
+          using bf2 = __bf16 __attribute__((ext_vector_type(2)));
+          const bf2 lo = {(__bf16)acc[0][i], (__bf16)acc[1][i]};
+          const bf2 hi = {(__bf16)acc[2][i], (__bf16)acc[3][i]};
+          const mde::nt2u u{__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi)};
+          __builtin_nontemporal_store(u, reinterpret_cast<mde::nt2u*>(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16));
+        } else {
+          mde::st4_nt(sp + (16 * mt + 4 * q4 + i) * hw + 4 * l16,
+                      make_float4(acc[0][i], acc[1][i], acc[2][i], acc[3][i]));
+        }
       }
       if constexpr (BNS) {
 #pragma unroll
@@ -1376,6 +1388,13 @@ int mde_pointwise_fwd_stats(const void* x, const float* in_scale, const float* i
 
 namespace {
 
+// The prefetching backward's shapes: 16 input channels (wider ones spill two
+// register sets), and for fp32 operands at most 16 outputs too.
+template <int A, int B, typename T>
+constexpr bool pw_pf_shape() {
+  return A <= 16 && (std::is_same_v<T, mde::bf16> || B <= 16);
+}
+
 inline bool pw_pf_on() {
   static const bool on = [] {
     const char* e = std::getenv("MDE_PW_PF");
@@ -1407,7 +1426,7 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
   // bf16 storage with the BN + ReLU operand and gs written, 16 input
   // channels (wider ones spill two register sets): the prefetching kernel
   // (MDE_PW_PF=0: skip_bwd_mfma_kernel)
-  const bool pf = std::is_same_v<T, mde::bf16> && go != nullptr && pw_pf_on();
+  const bool pf = go != nullptr && pw_pf_on();
   const bool bfp = std::is_same_v<T, mde::bf16> && go != nullptr && pw_bf_on();
   if (bfp) {  // bf16 products (pwbf.hip)
     const int rc = mde::pwbf_bwd((const mde::bf16*)gy, (const mde::bf16*)x, in_scale, in_shift,
@@ -1416,17 +1435,15 @@ int pointwise_bwd(const void* gy, const void* x, const float* in_scale, const fl
     if (rc != MDE_OK) return rc;
   } else {
 #define MDE_PW_BWD(A, B)                                                                     \
-  if (cin == A && cout == B && A <= 16 && pf && in_scale) {                                  \
-    const mde::bf16* gib = (const mde::bf16*)gy;                                             \
-    const mde::bf16* xib = (const mde::bf16*)x;                                              \
-    mde::bf16* gob = (mde::bf16*)gx;                                                         \
-    if (sums) {                                                                              \
-      if constexpr (A <= 32)                                                                 \
-        MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (pw_bwd_pf_kernel<A, B, true>), dim3(nb),        \
-                   dim3(256), 0, gib, xib, wt, gob, slab, n, hw, in_scale, in_shift, in_mean); \
-    } else {                                                                                 \
-      MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (pw_bwd_pf_kernel<A, B, false>), dim3(nb),         \
-                 dim3(256), 0, gib, xib, wt, gob, slab, n, hw, in_scale, in_shift, nullptr); \
+  if (cin == A && cout == B && pw_pf_shape<A, B, T>() && pf && in_scale) {                   \
+    if constexpr (pw_pf_shape<A, B, T>()) {                                                  \
+      if (sums) {                                                                            \
+        MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (pw_bwd_pf_kernel<A, B, true, T>), dim3(nb),     \
+                   dim3(256), 0, gi, xi, wt, go, slab, n, hw, in_scale, in_shift, in_mean);  \
+      } else {                                                                               \
+        MDE_LAUNCH(mde::K_PW_BWD, bytes, s, (pw_bwd_pf_kernel<A, B, false, T>), dim3(nb),    \
+                   dim3(256), 0, gi, xi, wt, go, slab, n, hw, in_scale, in_shift, nullptr);  \
+      }                                                                                      \
     }                                                                                        \
   } else if (cin == A && cout == B) {                                                        \
     if (sums) {                                                                              \

@@ -148,7 +148,7 @@ template <int CO_B, int TCB, bool STATS = false>
 __global__ void __launch_bounds__(256, 2)
     wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
-                    float* __restrict__ stats) {
+                    float* __restrict__ stats, int xsplit) {
   constexpr int NTB = kTRB * TCB;      // tiles per block
   constexpr int NG = NTB / 16;         // 16-tile groups (MFMA N tiles)
   constexpr int WCO = CO_B / 16;       // waves along output channels
@@ -163,12 +163,27 @@ __global__ void __launch_bounds__(256, 2)
 
   // XCD-aware block order (blocks b, b + 8, ... share an XCD's L2): logical
   // block l -> (channel group fastest, so the groups reading one input tile
-  // share that L2; then tile column, tile row, image)
+  // share that L2; then tile column, tile row, image).  xsplit > 1 (the
+  // weight-heavy wide-Cout convs, where U outweighs the input): the 8 XCDs
+  // form (8 / xsplit) tile ranges x xsplit channel-group ranges, so each XCD
+  // streams only 1 / xsplit of U (see wino_xsplit).
   const int per = gridDim.x >> 3;
-  const int l = (blockIdx.x & 7) * per + (blockIdx.x >> 3);
-  if (l >= total) return;
-  const int cog = l % ncog;
-  int rest = l / ncog;
+  const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3;
+  int cog, tile;
+  if (xsplit == 1) {
+    const int l = xcd * per + jx;
+    if (l >= total) return;
+    cog = l % ncog;
+    tile = l / ncog;
+  } else {
+    const int cpx = ncog / xsplit;  // channel groups per XCD
+    const int tpx = per / cpx;      // tiles per XCD
+    const int ntiles = total / ncog;
+    cog = (xcd % xsplit) * cpx + jx % cpx;
+    tile = (xcd / xsplit) * tpx + jx / cpx;
+    if (tile >= ntiles) return;
+  }
+  int rest = tile;
   const int bc = rest % bcols;
   rest /= bcols;
   const int br = rest % brows;
@@ -378,7 +393,7 @@ __global__ void __launch_bounds__(256, 2)
         a = k == 0 ? mde::Sh{p4[0], p4[1], p4[2], p4[3]}
                    : mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
       }
-      const int G = total / ncog, gb = l / ncog;
+      const int G = total / ncog, gb = tile;
       float* o4 = stats + ((int64_t)(cog * CO_B + tid) * G + gb) * 4;
       o4[0] = a.ref;
       o4[1] = a.n;
@@ -404,6 +419,34 @@ inline bool wino_geo(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, Wi
   g->brows = (int)mde::cdiv(h, 2 * kTRB);
   g->total = n * g->ncog * g->bcols * g->brows;
   return g->total < 0x7fffffff;
+}
+
+// XCD split of a launch (wino_f23_kernel's xsplit): each XCD's L2 sees every
+// block of its share, so with B channel-group ranges x 8 / B tile ranges the
+// XCDs together fetch U about 8 / B times and the input about B times
+// (bytes: U = 16 cin cout floats, x = n cin h w floats).  B = 1 (the
+// activation-heavy DDRNet convs) keeps the original walk; the NewCRF
+// projections at 1/16 and 1/32 (Cout 512-1024 on 30x40 / 15x20 planes) are
+// weight-heavy.  MDE_WINO_XSPLIT=1/2/4/8 forces one (where Cout allows).
+inline int wino_xsplit(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w,
+                       const WinoGeo& g) {
+  static const int forced = [] {
+    const char* e = std::getenv("MDE_WINO_XSPLIT");
+    return e ? std::atoi(e) : 0;
+  }();
+  const double u = 16.0 * ci * co, x = (double)n * ci * h * w;
+  int best = 1;
+  double best_b = 8 * u + x;
+  for (int b = 2; b <= 8; b *= 2) {
+    if (g.ncog % b) break;
+    if (forced) {
+      if (b == forced) return b;
+      continue;
+    }
+    const double bytes = 8 / b * u + b * x;
+    if (bytes < 0.8 * best_b) best = b, best_b = bytes;
+  }
+  return best;
 }
 
 }  // namespace
@@ -469,13 +512,21 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
   // not a direct-conv equivalent
   const double flops = 2.0 * 16 * n * (double)((h + 1) / 2) * (double)((w + 1) / 2) *
                        (double)cin * cout;
-  const double bytes = 4.0 * n * h * w * (double)(cin + cout);
-  const dim3 grid((unsigned)((g.total + 7) / 8 * 8)), block(256);
+  // activations in and out, plus the transformed filter U once (the GEMMs'
+  // other operand: at 1/32 scale it outweighs the planes)
+  const double bytes = 4.0 * n * h * w * (double)(cin + cout) + 64.0 * (double)cin * cout;
+  const int xsplit = wino_xsplit(n, cin, cout, h, w, g);
+  int64_t nblk = (g.total + 7) / 8 * 8;
+  if (xsplit > 1) {
+    const int64_t ntiles = g.total / g.ncog, a = 8 / xsplit;
+    nblk = 8 * ((ntiles + a - 1) / a) * (g.ncog / xsplit);
+  }
+  const dim3 grid((unsigned)nblk), block(256);
   const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
 #define MDE_WINO(CB, TC, ST)                                                                      \
   MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST>), grid, block, 0, x, u, y,   \
                   (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \
-                  stats)
+                  stats, xsplit)
   if (stats) {
     if (g.co_b == 64)
       MDE_WINO(64, 8, true);

@@ -114,7 +114,8 @@ def test_wino_deterministic_full_batch():
     assert rel_err(outs[0], torch.nn.functional.conv2d(x, wt, None, 1, 1)) <= 2e-5
 
 
-@pytest.mark.parametrize("cin,cout,h,w", [(16, 16, 40, 64), (64, 64, 15, 20), (32, 32, 9, 36)])
+@pytest.mark.parametrize("cin,cout,h,w", [(16, 16, 40, 64), (64, 64, 15, 20), (32, 32, 9, 36),
+                                          (64, 256, 15, 20)])  # the last: XCD split 4
 def test_wino_stats_epilogue(cin, cout, h, w):
     """The BN-statistics epilogue: per (channel, pixel block) (shift, count,
     s1, s2) records whose merge gives y's batch mean / variance (float64

@@ -15,15 +15,23 @@ import kbench  # noqa: E402
 
 SHAPES = [(64, 64, 60, 80), (32, 32, 120, 160), (32, 32, 240, 320), (16, 16, 480, 640),
           (128, 128, 30, 40)]
+# cfg4 (bs 16): the NewCRF projections' Winograd passes (forward cin -> cout,
+# data gradient cout -> cin), newcrf_layers.py NewCRF.proj_x / proj_v
+SHAPES_NC = [(160, 1024, 15, 20), (512, 1024, 15, 20), (1024, 512, 15, 20), (1024, 160, 15, 20),
+             (112, 512, 30, 40), (256, 512, 30, 40), (512, 256, 30, 40), (128, 256, 60, 80),
+             (64, 128, 120, 160)]
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=0)
     ap.add_argument("--only", default="", help="ci,co,h,w")
+    ap.add_argument("--newcrf", action="store_true", help="cfg4's shapes at bs 16")
     a = ap.parse_args()
-    shapes = [tuple(int(v) for v in a.only.split(","))] if a.only else SHAPES
-    n = 32
+    shapes = SHAPES_NC if a.newcrf else SHAPES
+    if a.only:
+        shapes = [tuple(int(v) for v in a.only.split(","))]
+    n = 16 if a.newcrf else 32
     kbench._STREAM = torch.cuda.Stream()
     with torch.cuda.stream(kbench._STREAM):
         for ci, co, h, w in shapes:

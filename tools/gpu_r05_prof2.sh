@@ -24,7 +24,11 @@ for wl in "$@"; do
     gd_bf16) args="--workload guidedepth --amp bf16"; tag=guidedepth_bf16 ;;
     nc_fp32) args="--workload newcrf"; tag=newcrf_fp32 ;;
   esac
+  # the profiled runs keep MIOpen's user db / kernel cache to themselves: a
+  # bench line after them on the same box ran 938 instead of 971-976 img/s
+  # with different MIOpen solvers (r05prof2, first attempt)
   for ctr in FETCH_SIZE WRITE_SIZE; do
+    MIOPEN_USER_DB_PATH=/tmp/mio_prof/db MIOPEN_CUSTOM_CACHE_DIR=/tmp/mio_prof/cache \
     run "pmc_${wl}_$ctr" 400 rocprofv3 --pmc $ctr --output-format csv -d "$ROOT/$OUT/pmc_${wl}_$ctr" \
         -o r05 -- python3 bench.py $args --steps 2 --warmup 2 --no-cpu-baseline --no-kernel-timing
   done
@@ -32,6 +36,7 @@ for wl in "$@"; do
       "$OUT/pmc_${wl}_WRITE_SIZE/r05_counter_collection.csv" -o "profiles/r05_pmc_traffic_$tag.json" > /dev/null || exit 1
   cp "profiles/r05_pmc_traffic_$tag.json" "$OUT/"
   rm -rf "$OUT/pmc_${wl}_FETCH_SIZE" "$OUT/pmc_${wl}_WRITE_SIZE"
+  MIOPEN_USER_DB_PATH=/tmp/mio_trace_$wl/db MIOPEN_CUSTOM_CACHE_DIR=/tmp/mio_trace_$wl/cache \
   run "trace_$wl" 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$ROOT/$OUT/trace_$wl" \
       -o r05 -- python3 bench.py $args --steps 5 --warmup 3 --no-cpu-baseline
   echo "== bench_$wl ($(date +%T))"

@@ -247,6 +247,11 @@ __global__ void __launch_bounds__(256, 2)
   constexpr int NB = CO / 16;
   __shared__ float sx[CIP * PS];
   __shared__ float sw[9 * CIP * WS];
+  // staged output (the 3-input-channel guide convs, see the epilogue): lines
+  // of 64 pixels + a 16-byte pad, where the tile fits 40 KB
+  constexpr int kSOL = 64 + 16 / (int)sizeof(TO);
+  constexpr bool SO = CI == 3 && !FLIP && TH * CO * kSOL * (int)sizeof(TO) <= 40 * 1024;
+  __shared__ __attribute__((aligned(16))) TO so[SO ? TH * CO * kSOL : 4];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int wvu = __builtin_amdgcn_readfirstlane(wv);
@@ -359,6 +364,44 @@ __global__ void __launch_bounds__(256, 2)
     }
     // D layout: lane holds pixels 4*lk + i (i = 0..3) of output channel li.
     TO* yi = y + g.img * img_out;
+    if constexpr (SO) {
+      // The guide convs (3 input channels) are output-bound: their direct
+      // stores wrote 32 / 64-byte pieces of 16 channel planes per instruction
+      // (1.3-3.3 TB/s).  Through LDS instead: the block's [TH rows][CO][64]
+      // tile, then 16-byte pieces of whole 64-pixel row segments (the
+      // conv3x3_bf_fwd2 epilogue).  `so` is rewritten only after the next
+      // tile's two loop-top barriers, so one barrier here suffices.
+      if (vec) {
+#pragma unroll
+        for (int q = 0; q < RPW; ++q)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+#pragma unroll
+            for (int nb = 0; nb < NB; ++nb) {
+              const f4 v = acc[q][m][nb];
+              mde::st4(so + ((wv * RPW + q) * CO + nb * 16 + li) * kSOL + m * 16 + 4 * lk,
+                       make_float4(v[0], v[1], v[2], v[3]));
+            }
+        __syncthreads();
+        constexpr int PX = 16 / (int)sizeof(TO);  // pixels per 16-byte piece
+        constexpr int PPL = 64 / PX;              // pieces per 64-pixel line
+        constexpr int NP = TH * CO * PPL;
+        static_assert(NP % 256 == 0, "whole pieces per thread");
+#pragma unroll
+        for (int k = 0; k < NP / 256; ++k) {
+          const int e = tid + 256 * k, line = e / PPL, pc = e % PPL;
+          const int r = line / CO, co = line % CO;
+          const int grow = g.r0 + r, col = g.c0 + PX * pc;
+          const uint4 u = *reinterpret_cast<const uint4*>(so + line * kSOL + PX * pc);
+          TO* dst = yi + ((int64_t)co * h + grow) * w + col;
+          if (grow < h && col + PX <= w)
+            *reinterpret_cast<uint4*>(dst) = u;
+          else if (grow < h && col < w)  // bf16, w % 4 == 0: the first 4 pixels
+            *reinterpret_cast<uint2*>(dst) = make_uint2(u.x, u.y);
+        }
+        continue;
+      }
+    }
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
       const int row = g.r0 + wv * RPW + q;

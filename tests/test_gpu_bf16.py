@@ -422,7 +422,8 @@ def test_bilinear_generic_bf16_storage_matches_fp32_kernel(c, hi, wi, ho, wo, al
     assert torch.equal(ga, gb.to(torch.bfloat16))
 
 
-@pytest.mark.parametrize("cout,h,w", [(16, 64, 96), (32, 37, 70), (64, 30, 40)])
+@pytest.mark.parametrize("cout,h,w", [(16, 64, 96), (32, 37, 70), (64, 30, 40), (16, 21, 36),
+                                      (32, 9, 100)])
 def test_guide_conv_bf16_matches_rounded_fp32_kernel(cout, h, w):
     """The autocast guide conv (mde_conv3x3_guide_bf16_fwd, modules.py:52-54):
     image and weight rounded to bf16, fp32 accumulation, bf16 output == the

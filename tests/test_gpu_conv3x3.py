@@ -15,8 +15,9 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
 PAIRS = [(3, 16), (3, 32), (3, 64), (16, 16), (32, 32)]
-# (n, h, w): tile-aligned, ragged rows/cols, w % 4 != 0, a single pixel
-SIZES = [(2, 16, 64), (1, 13, 70), (2, 9, 37), (1, 1, 1), (3, 20, 130)]
+# (n, h, w): tile-aligned, ragged rows/cols, w % 4 != 0, a single pixel,
+# w % 4 == 0 with a partial column tile (the guide convs' staged stores)
+SIZES = [(2, 16, 64), (1, 13, 70), (2, 9, 37), (1, 1, 1), (3, 20, 130), (2, 11, 100)]
 
 
 @pytest.fixture(scope="module", autouse=True)

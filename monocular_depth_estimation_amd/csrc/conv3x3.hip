@@ -64,6 +64,11 @@ constexpr int plane_words(int rows, int mod) { return (rows * kXW + 63) / 64 * 6
 // with k odd or the groups spread 0/16/32/48).
 constexpr int wrow_words(int co) { return co == 16 ? 16 : (co == 32 ? 48 : 80); }
 
+// v rounded to bf16 precision (RNE; the hardware conversion, as autocast's cast)
+__device__ __forceinline__ float rbf(float v) {
+  return __uint_as_float((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)v) << 16);
+}
+
 // --------------------------------------------------------------- staging
 // A CIP x XR x kXW input tile (rows r0-1.., cols c0-1..), zero outside the
 // image and for channels >= CI, held in registers between its global loads
@@ -121,7 +126,7 @@ struct HaloTile {
       const int ri = wvu + 4 * k;
       if (ROWS % 4 == 0 || ri < ROWS) {
         const float v = (am >> k) & 1 ? a[k] : 0.f;
-        sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = RB ? mde::bf2f(mde::f2bf(v)) : v;
+        sx[(ri / XR) * PS + (ri % XR) * kXW + lane] = RB ? rbf(v) : v;
       }
     }
 #pragma unroll
@@ -130,7 +135,7 @@ struct HaloTile {
       const int ri = wvu + 4 * (e >> 1);
       if (e < 2 * RPWV && ri < ROWS) {
         const float v = (bm >> q) & 1u ? b[q] : 0.f;
-        sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = RB ? mde::bf2f(mde::f2bf(v)) : v;
+        sx[(ri / XR) * PS + (ri % XR) * kXW + 64 + (e & 1)] = RB ? rbf(v) : v;
       }
     }
   }
@@ -270,7 +275,7 @@ __global__ void __launch_bounds__(256, 2)
       const bool ok = e < WN && ci < CI;
       const int src = FLIP ? (ci * CO + co) * 9 + (8 - tap) : (co * CI + ci) * 9 + tap;
       const float t = wt[ok ? src : 0];
-      v[i] = ok ? (RB ? mde::bf2f(mde::f2bf(t)) : t) : 0.f;
+      v[i] = ok ? (RB ? rbf(t) : t) : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < WPER; ++i) {
@@ -341,7 +346,13 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
           for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) acc[q][m][nb][i] = mde::bf2f(mde::f2bf(acc[q][m][nb][i]));
+            for (int i = 0; i < 4; i += 2) {  // hardware RNE conversion, two at a time
+              using bf2v = __bf16 __attribute__((ext_vector_type(2)));
+              const uint32_t p = __builtin_bit_cast(
+                  uint32_t, bf2v{(__bf16)acc[q][m][nb][i], (__bf16)acc[q][m][nb][i + 1]});
+              acc[q][m][nb][i] = __uint_as_float(p << 16);
+              acc[q][m][nb][i + 1] = __uint_as_float(p & 0xffff0000u);
+            }
     }
     if constexpr (STATS) {
 #pragma unroll
@@ -351,14 +362,30 @@ __global__ void __launch_bounds__(256, 2)
           run[nb].ref = __shfl(ok0 ? acc[0][0][nb][0] : 0.f, li, 64);
         }
 #pragma unroll
-        for (int q = 0; q < RPW; ++q)
+        for (int q = 0; q < RPW; ++q) {
+          const int row = g.r0 + wv * RPW + q;
+          if (row < h && g.c0 + 64 <= w) {
+            // a whole 64-pixel row segment (wave-uniform): no per-pixel bounds
+            // tests (they were most of the epilogue's VALU); same sums
 #pragma unroll
-          for (int m = 0; m < 4; ++m)
+            for (int m = 0; m < 4; ++m)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const int row = g.r0 + wv * RPW + q, col = g.c0 + m * 16 + 4 * lk + i;
-              mde::sh_add(run[nb], acc[q][m][nb][i], row < h && col < w);
-            }
+              for (int i = 0; i < 4; ++i) {
+                const float d = acc[q][m][nb][i] - run[nb].ref;
+                run[nb].s1 += d;
+                run[nb].s2 = fmaf(d, d, run[nb].s2);
+              }
+            run[nb].n += 16.f;
+          } else {
+#pragma unroll
+            for (int m = 0; m < 4; ++m)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int col = g.c0 + m * 16 + 4 * lk + i;
+                mde::sh_add(run[nb], acc[q][m][nb][i], row < h && col < w);
+              }
+          }
+        }
       }
       first = false;
     }
@@ -379,8 +406,14 @@ __global__ void __launch_bounds__(256, 2)
 #pragma unroll
             for (int nb = 0; nb < NB; ++nb) {
               const f4 v = acc[q][m][nb];
-              mde::st4(so + ((wv * RPW + q) * CO + nb * 16 + li) * kSOL + m * 16 + 4 * lk,
-                       make_float4(v[0], v[1], v[2], v[3]));
+              TO* sp = so + ((wv * RPW + q) * CO + nb * 16 + li) * kSOL + m * 16 + 4 * lk;
+              if constexpr (RB) {  // already bf16 values: the high halves, two a word
+                *reinterpret_cast<uint2*>(sp) = make_uint2(
+                    __builtin_amdgcn_perm(__float_as_uint(v[1]), __float_as_uint(v[0]), 0x07060302u),
+                    __builtin_amdgcn_perm(__float_as_uint(v[3]), __float_as_uint(v[2]), 0x07060302u));
+              } else {
+                mde::st4(sp, make_float4(v[0], v[1], v[2], v[3]));
+              }
             }
         __syncthreads();
         constexpr int PX = 16 / (int)sizeof(TO);  // pixels per 16-byte piece

@@ -336,7 +336,9 @@ def main():
     use_graph = bool(args.graph) and world.device.type == "cuda"
     if use_graph:
         from monocular_depth_estimation_amd.train import GraphTrainer
-        trainer = GraphTrainer(model, loss_fn, world, lr=1e-4, amp=args.amp)
+        # the measured step keeps BN in train mode (batch statistics every step),
+        # the heavier of the reference's two modes (DESIGN.md "BatchNorm mode")
+        trainer = GraphTrainer(model, loss_fn, world, lr=1e-4, amp=args.amp, eval_quirk=False)
         args.warmup = max(args.warmup, trainer.eager_steps + 1)  # capture happens in warm-up
     else:
         trainer = Trainer(wrap_ddp(model, world), make_adam(model, 1e-4), loss_fn, world,
@@ -403,13 +405,15 @@ def main():
         dp_exchange = None
     elif not use_graph:
         dp_exchange = f"DDP buckets over {backend} (eager, overlapped with backward)"
-    elif trainer.buckets is not None:
-        dp_exchange = (f"{len(trainer.buckets)} gradient buckets, all_reduce(AVG) over {backend} "
-                       "captured into the step graph, overlapped with backward (a captured "
-                       "multi-rank RCCL collective has not run on hardware in this repo's "
-                       "testing: the pool gives one GPU per call; MDE_DP_OVERLAP=0 = flat)")
+    elif trainer.scheme == "overlap":
+        dp_exchange = (f"overlap (opt-in, MDE_DP_OVERLAP=1): {len(trainer.buckets)} gradient "
+                       f"buckets, all_reduce(AVG) over {backend} captured into the step graph, "
+                       "overlapped with backward (a captured multi-rank RCCL collective has not "
+                       "run on hardware in this repo's testing: the pool gives one GPU per call)")
     else:
-        dp_exchange = (f"flat: one eager all_reduce over {backend} between the two step graphs")
+        dp_exchange = (f"flat (default): graph A (forward, backward, gradients packed x 1/N) -> "
+                       f"one eager all_reduce(SUM) over {backend} -> graph B (unpack, Adam); "
+                       "no captured collective")
     in_sync = params_in_sync(trainer.params if use_graph else list(model.parameters()), world)
     if use_graph:
         trainer.close()  # free the graphs (captured RCCL nodes) before the group goes

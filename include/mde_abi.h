@@ -738,6 +738,17 @@ int mde_batchnorm_stats_route(int64_t n, int64_t c, int64_t h, int64_t w, int64_
  * ------------------------------------------------------------------------- */
 int mde_convbf_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks, int stride,
                          int pass);
+/* mde_convbf_supported at batch n: also false when the launch for this batch
+ * would refuse it (n x patches >= 2^22, the kernels' exact-division range),
+ * so a caller can fall back before the step instead of failing inside it. */
+int mde_convbf_supported_n(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
+                           int stride, int pass);
+/* The algorithmic FLOPs (2 per MAC) the timing registry credits a pass with:
+ * 2 n Ho Wo cin cout ks^2 over the FORWARD output plane for all three passes
+ * (the stride-2 data gradient included: not its full-resolution output plane,
+ * nor the products of the zero-inserted form).  0 for an unsupported shape. */
+double mde_convbf_flops(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
+                        int stride, int pass);
 size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose);
 int mde_convbf_pack(const float* weight, void* packed, int64_t cin, int64_t cout, int ks,
                     int transpose, void* stream);

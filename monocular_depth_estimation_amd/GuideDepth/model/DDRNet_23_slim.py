@@ -168,8 +168,13 @@ def _seq_bn_residual(seq, x, residual):
     """residual + seq(x) for a Sequential ending in a BatchNorm: the add runs in the BN pass.
     Its bias-free convs go through conv_nobias (HIP kernels where they apply)."""
     mods = list(seq)
+    conv = mods[-2] if len(mods) >= 2 else None
+    if not (isinstance(conv, nn.Conv2d) and conv.bias is None):
+        # conv_nobias_stats assumes a bias-free conv feeding the BN: anything else
+        # (a biased conv, a non-conv module) runs as-is, the add still in the BN
+        return mods[-1](run_sequential(mods[:-1], x), residual=residual)
     x = run_sequential(mods[:-2], x) if len(mods) > 2 else x
-    y, st = conv_nobias_stats(mods[-2], x, mods[-1])
+    y, st = conv_nobias_stats(conv, x, mods[-1])
     return mods[-1](y, residual=residual, stats=st)
 
 

@@ -157,6 +157,8 @@ SIGNATURES = {
     "mde_batchnorm_stats_route": (_int, [_i64, _i64, _i64, _i64, _i64, _int]),
     "mde_bn_chan_mode": (_int, [_int]),
     "mde_convbf_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int, _int]),
+    "mde_convbf_supported_n": (_int, [_i64, _i64, _i64, _i64, _i64, _int, _int, _int]),
+    "mde_convbf_flops": (_c.c_double, [_i64, _i64, _i64, _i64, _i64, _int, _int, _int]),
     "mde_stem_bf16_supported": (_int, [_i64, _i64, _i64, _i64]),
     "mde_stem_bf16_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp]),
     "mde_stem_bf16_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64]),

@@ -1376,9 +1376,20 @@ int launch_res_t(const bf16* x, const bf16* wp, bf16* y, float* stats, const Res
   return MDE_OK;
 }
 
+// Algorithmic MACs x 2 of a pass: the convolution's own product count,
+// 2 n Ho Wo Cin Cout k^2 over the FORWARD output plane.  A forward / stride-1
+// pass writes that plane; the stride-2 data gradient (U2) writes the input
+// plane and reads the forward output (its staged source, hi x wi), so its
+// count is over hi x wi -- not over the full-resolution gx it produces (4x
+// the true work) nor over the MFMAs the zero-inserted form issues.
+inline double pass_flops(const Pass& p, int64_t n) {
+  const double plane = p.mode == U2 ? (double)p.hi * p.wi : (double)p.ho * p.wo;
+  return 2.0 * n * plane * (double)p.cout * p.cin * p.ks * p.ks;
+}
+
 int launch_fwd(const Pass& p, const bf16* x, const bf16* wp, bf16* y, float* stats, int64_t n,
                int kid, hipStream_t s) {
-  const double flops = 2.0 * n * p.ho * p.wo * (double)p.cout * p.cin * p.ks * p.ks;
+  const double flops = pass_flops(p, n);
   const double bytes = 2.0 * n * ((double)p.cin * p.hi * p.wi + (double)p.cout * p.ho * p.wo);
   ResGeo rg;
   if (res_geo(p, n, &rg)) {
@@ -1485,6 +1496,35 @@ int mde_convbf_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int ks
   }
   int mtw, nw;
   return fwd_geo(p, 1, &g, &mtw, &nw) ? 1 : 0;
+}
+
+int mde_convbf_supported_n(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
+                           int stride, int pass) {
+  Pass p;
+  if (n <= 0 || pass < 0 || pass > 2 ||
+      !make_pass(cin, cout, h, w, ks, stride, pass == 1 ? 1 : 0, &p))
+    return 0;
+  Geo g;
+  if (pass == 2) {
+    int S, per;
+    int64_t np;
+    return wgrad_geo(p, n, &g, &S, &per, &np) ? 1 : 0;
+  }
+  // launch_fwd's own choice: the resident-filter geometry, else the chunked
+  // one, whose launch refuses n * patches >= 2^22
+  ResGeo rg;
+  if (res_geo(p, n, &rg)) return 1;
+  int mtw, nw;
+  return fwd_geo(p, n, &g, &mtw, &nw) && n * g.ppi < (1 << 22) ? 1 : 0;
+}
+
+double mde_convbf_flops(int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int ks,
+                        int stride, int pass) {
+  Pass p;
+  if (n <= 0 || pass < 0 || pass > 2 ||
+      !make_pass(cin, cout, h, w, ks, stride, pass == 1 ? 1 : 0, &p))
+    return 0.0;
+  return pass_flops(p, n);
 }
 
 size_t mde_convbf_pack_elems(int64_t cin, int64_t cout, int ks, int transpose) {

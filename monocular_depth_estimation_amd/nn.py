@@ -807,6 +807,7 @@ class _PackScope:
     def __init__(self):
         self.entries = {}  # weight -> (packed, packed_t, cin, cout, ks)
         self.table = None
+        self.retired = []  # earlier tables, kept alive for the graphs that captured them
         self.rows = []  # weights in table order
         self.ptrs = ()
         self.blocks = 0
@@ -826,6 +827,11 @@ class _PackScope:
             rows.append([wgt.data_ptr(), wp.data_ptr(), wt.data_ptr(), cin, cout, ks, blk, 0])
             blk += -(-max(wp.numel(), wt.numel()) // 256)
             elems += wp.numel() + wt.numel()
+        if self.table is not None:
+            # a captured step graph recorded this table's device pointer in its
+            # pack node (and reads the weight / packed pointers it holds): never
+            # free a table a graph may still replay
+            self.retired.append(self.table)
         self.table = torch.tensor(rows, dtype=torch.int64, device=device)
         self.rows, self.ptrs, self.blocks, self.elems = list(self.entries), ptrs, blk, elems
 
@@ -980,6 +986,7 @@ def stem_ok(conv: nn.Conv2d, x) -> bool:
             and conv.in_channels == 3 and conv.kernel_size == (3, 3) and conv.stride == (2, 2)
             and conv.padding == (1, 1) and conv.dilation == (1, 1) and conv.groups == 1
             and conv.padding_mode == "zeros"
+            and x.numel() < (1 << 31)  # the kernels' 32-bit image offsets (n*3*h*w)
             and bool(_abi.query("mde_stem_bf16_supported", 3, conv.out_channels, x.shape[2],
                                 x.shape[3])))
 
@@ -1001,11 +1008,14 @@ def convbf_ok(conv: nn.Conv2d, x) -> bool:
             and ((conv.kernel_size == (3, 3) and conv.padding == (1, 1))
                  or (conv.kernel_size == (1, 1) and conv.padding == (0, 0)))):
         return False
-    key = (conv.in_channels, conv.out_channels, x.shape[2], x.shape[3], conv.kernel_size[0],
-           conv.stride[0])
+    # the real batch: a launch refuses n x patches >= 2^22, which the batch-free
+    # query cannot see -- such a batch falls back to MIOpen here instead of
+    # raising inside the step
+    key = (x.shape[0], conv.in_channels, conv.out_channels, x.shape[2], x.shape[3],
+           conv.kernel_size[0], conv.stride[0])
     ok = _CONVBF_OK.get(key)
     if ok is None:
-        ok = all(_abi.query("mde_convbf_supported", *key, p) for p in (0, 1, 2))
+        ok = all(_abi.query("mde_convbf_supported_n", *key, p) for p in (0, 1, 2))
         _CONVBF_OK[key] = ok
     return ok
 
@@ -1082,7 +1092,8 @@ def _conv3x3_apply(x, weight, passes, want_stats):
         raise TypeError(f"conv3x3: the HIP kernels take a float32 weight, got {weight.dtype}")
     cin, cout = x.shape[1], weight.shape[0]
     if (GUIDE_BF16 and cin == 3 and cout in (16, 32, 64) and passes[0] and x.dtype == torch.float32
-            and _autocast_bf16(x) and not x.requires_grad):
+            and _autocast_bf16(x) and not x.requires_grad
+            and x.numel() < (1 << 31)):  # guide_ok's 32-bit image offsets (n*3*h*w)
         return _GuideConvBf16.apply(x, weight, bool(want_stats))
     if _conv3x3_bf16_path(cin, cout, x, weight):
         return _Conv3x3Bf16.apply(x.to(torch.bfloat16), weight, tuple(passes), want_stats)

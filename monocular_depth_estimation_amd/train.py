@@ -256,6 +256,27 @@ class GradBuckets:
             torch.cuda.current_stream().wait_stream(self.stream)
 
 
+def dp_exchange_scheme(world_size: int, backend: str | None, dp_overlap: bool | None = None,
+                       dp_collectives: bool | None = None, env=None) -> str | None:
+    """Which gradient exchange GraphTrainer runs: None (no exchange: one rank),
+    "flat" (graph A -> ONE eager all_reduce -> graph B; no collective is ever
+    captured) or "overlap" (bucket all-reduces captured INTO the step graph,
+    overlapping the backward).  Flat is the N > 1 default.  Overlap is opt-in
+    -- MDE_DP_OVERLAP=1 over RCCL, or dp_overlap=True -- because a captured
+    multi-rank RCCL collective has not run on hardware in this repo's testing
+    (the pool gives one GPU per call); a gloo group cannot capture collectives
+    (GraphTrainer then runs the bucket path eagerly only).  dp_collectives
+    forces the exchange on (or off) regardless of the world size (tests: the
+    same calls in a one-rank group)."""
+    env = os.environ if env is None else env
+    dp = world_size > 1 if dp_collectives is None else bool(dp_collectives)
+    if dp_overlap is None:
+        dp_overlap = dp and backend == "nccl" and env.get("MDE_DP_OVERLAP", "0") == "1"
+    if dp_overlap:
+        return "overlap"
+    return "flat" if dp else None
+
+
 class GraphTrainer:
     """The same training step captured into HIP graphs and replayed.
 
@@ -272,42 +293,51 @@ class GraphTrainer:
     copy; replays reuse those static buffers).  N == 1: one graph (forward,
     loss, backward, fused capturable Adam).
 
-    N > 1 over RCCL ("nccl"), the default: the gradients are views of ~6 MB
-    bucket buffers (parameters in reverse registration order, i.e. about the
-    order backward finishes them).  A post-accumulate hook counts each
-    bucket's parameters; when the last one is final the bucket is
-    all-reduced with ReduceOp.AVG on a side stream that forks from the
-    backward stream at that point, so the RCCL collectives are captured INTO
-    the step graph and overlap the rest of the backward; the Adam step joins
-    the side stream.  One graph, no pack / unpack copies.  MDE_DP_OVERLAP=0
-    (and any gloo group, whose collectives cannot be captured) selects the
-    flat scheme instead: graph A (forward, backward, the gradients packed
-    into one buffer and scaled by 1/N) -> one eager all_reduce(SUM) outside
-    the graph -> graph B (unpack, Adam).  The BN running statistics live in
-    one flat buffer, broadcast from rank 0 at start and by sync_buffers()
-    (close() runs it) -- not every step: a train-mode forward never reads
-    them, and rank 0's, the ones a checkpoint saves, come out bitwise the
-    same as under DDP's per-forward broadcast_buffers (rank 0 receives its
-    own), so no collective other than the gradient exchange is on the step's
-    critical path.  Inputs are copied into static device buffers.
-    CUDA only; BN stays in train mode (the eval-mode quirk changes the graph,
-    use Trainer for that).  close() frees the captured graphs; it must run
-    before dist.destroy_process_group() (a graph holding captured RCCL
-    collectives references the communicator) and is registered to run at
-    interpreter exit too.
+    N > 1, the default (dp_exchange_scheme "flat"): graph A (forward,
+    backward, the gradients packed into one buffer and scaled by 1/N) -> ONE
+    eager all_reduce(SUM) outside any graph -> graph B (unpack, Adam); no
+    collective is ever captured.  Opt-in over RCCL (MDE_DP_OVERLAP=1 or
+    dp_overlap=True, "overlap"): the gradients are views of ~6 MB bucket
+    buffers (parameters in reverse registration order, i.e. about the order
+    backward finishes them); a post-accumulate hook counts each bucket's
+    parameters and, when the last one is final, all-reduces the bucket with
+    ReduceOp.AVG on a side stream forked from the backward stream, so the
+    RCCL collectives are captured INTO the step graph and overlap the rest of
+    the backward (one graph; the Adam step joins the side stream).  The
+    captured multi-rank collective has only run through RCCL's one-rank path
+    on this pool, hence opt-in.  The BN running statistics live in one flat
+    buffer, broadcast from rank 0 at start, when the eval-mode quirk switches
+    BN to running statistics (every rank then normalises with rank 0's, as
+    under DDP's broadcast_buffers), and by sync_buffers() -- not every step: a
+    train-mode forward never reads them, and rank 0's, the ones a checkpoint
+    saves, come out bitwise the same as under DDP's per-forward broadcast
+    (rank 0 receives its own).  Inputs are copied into static device buffers.
+
+    The reference's BatchNorm quirk (eval_quirk, default on as in Trainer):
+    LogProgress calls model.eval() at loader_pos % 300 == 0 and never switches
+    back (src/train.py:79,134-136,161), so from step 1 of every epoch BN uses
+    running statistics.  Each BN mode has its own captured step (graphs keyed
+    by model.training, each captured the first time that mode runs after the
+    warm-up), so an epoch replays the train-mode step once and the eval-mode
+    step after it.  CUDA only.  close() frees the captured graphs and runs no
+    collective (it is also the atexit hook: a rank that gets there alone must
+    not block); it must run before dist.destroy_process_group() (a graph
+    holding captured RCCL collectives references the communicator).
     """
 
     BUCKET_BYTES = 6 << 20
 
     def __init__(self, model, loss_fn, world: World, lr=1e-4, eager_steps=2, amp: str = "",
-                 dp_overlap: bool | None = None, dp_collectives: bool | None = None):
+                 dp_overlap: bool | None = None, dp_collectives: bool | None = None,
+                 eval_quirk: bool = True):
         if world.device.type != "cuda":
             raise RuntimeError("GraphTrainer needs a GPU (use Trainer on CPU)")
         self.model, self.loss_fn, self.world = model, loss_fn, world
         self.amp = amp
         self.eager_steps = eager_steps
+        self.eval_quirk = eval_quirk
         self.calls = 0
-        self.graphs = None
+        self.graphs = {}  # BN mode ("train" / "eval") -> (graph A, graph B or None, static loss)
         # the data-parallel exchange runs at N > 1; dp_collectives=True issues it
         # in a one-rank group too (tests: the same RCCL calls, average = identity)
         self.dp = world.size > 1 if dp_collectives is None else bool(dp_collectives)
@@ -342,16 +372,14 @@ class GraphTrainer:
         # captures on stream (bucket collectives on side).
         self.stream = torch.cuda.Stream(device=world.device)  # capture stream
         self.eager_stream = torch.cuda.Stream(device=world.device)
-        # bucketed all-reduce overlapped with backward, captured into the step
-        # graph: the N > 1 default over RCCL (MDE_DP_OVERLAP=0 selects the flat
-        # scheme; a gloo group cannot capture collectives and takes the flat
-        # scheme too).  dp_overlap=True with a one-rank group issues the same
+        # the exchange (dp_exchange_scheme): flat by default at N > 1; the
+        # bucketed all-reduce captured into the step graph on request over
+        # RCCL.  dp_overlap=True with a one-rank group issues the same
         # collectives (tests).
-        if dp_overlap is None:
-            dp_overlap = (world.size > 1 and dist.get_backend() == "nccl"
-                          and os.environ.get("MDE_DP_OVERLAP", "1") != "0")
+        backend = dist.get_backend() if dist.is_initialized() else None
+        self.scheme = dp_exchange_scheme(world.size, backend, dp_overlap, dp_collectives)
         self.buckets = None
-        if dp_overlap:
+        if self.scheme == "overlap":
             self.side = torch.cuda.Stream(device=world.device)
             self.eager_side = torch.cuda.Stream(device=world.device)
             self.buckets = GradBuckets(self.params, world, self.BUCKET_BYTES, stream=self.eager_side)
@@ -365,7 +393,7 @@ class GraphTrainer:
         atexit.register(self._atexit)
 
     def begin_epoch(self):
-        self.model.train()
+        self.model.train()  # train.py:79
 
     # -- the step's pieces (each runs eagerly or inside a capture) ----------
     def _forward_backward(self):
@@ -432,14 +460,14 @@ class GraphTrainer:
                 loss = self._eager()
             cur.wait_stream(self.eager_stream)
         else:
-            if self.graphs is None:
-                self._capture()
-            ga, gb = self.graphs
+            mode = "train" if self.model.training else "eval"
+            if mode not in self.graphs:
+                self.graphs[mode] = self._capture()
+            ga, gb, loss = self.graphs[mode]
             ga.replay()
             if gb is not None:
                 self._allreduce()
                 gb.replay()
-            loss = self.static_loss
         self.last_loss = loss
         self.loss_sum += loss
         self.loss_count += 1
@@ -456,10 +484,16 @@ class GraphTrainer:
         return loss
 
     def _capture(self):
-        """Capture the step.  Every memset node the capture recorded (ATen's
-        multi-block reductions zero their semaphores with one) is replaced by
-        a fill kernel before instantiation: captured memsets are only correct
-        on a graph's first replay on this ROCm stack (csrc/graph.hip)."""
+        """Capture the step in the model's current BN mode; returns (graph A,
+        graph B or None, static loss).  Every memset node the capture recorded
+        (ATen's multi-block reductions zero their semaphores with one) is
+        replaced by a fill kernel before instantiation: captured memsets are
+        only correct on a graph's first replay on this ROCm stack
+        (csrc/graph.hip).  Each capture gets its own memory pool and its own
+        gradient buffers (grads are set to None first), so the train-mode and
+        eval-mode graphs can be replayed in any order: the Adam state is
+        shared, each graph's optimizer step reads the gradients its own
+        backward wrote."""
         from . import _abi
         if self.buckets is not None and dist.get_backend() != "nccl":
             raise RuntimeError("the overlapped bucket all-reduce is captured into the step graph "
@@ -476,30 +510,36 @@ class GraphTrainer:
                 self.optimizer.step()
             return loss
 
-        ga, self.static_loss, na = _abi.capture_graph(part_a, self.stream)
+        ga, static_loss, na = _abi.capture_graph(part_a, self.stream)
         gb, nb = None, 0
         if not one_graph:
             gb, _, nb = _abi.capture_graph(self._unpack_and_update, self.stream, pool=ga.pool())
         self.memsets_replaced = na + nb
-        self.graphs = (ga, gb)
+        return ga, gb, static_loss
 
     def after_step(self, loader_pos: int):
-        pass
+        # LogProgress (train.py:134-136,161): model.eval() that is never undone.
+        # Every rank calls this at the same loader position, so the broadcast of
+        # rank 0's running statistics at the switch is a matched collective
+        # (eval-mode steps never change them: all ranks then normalise alike).
+        if self.eval_quirk and loader_pos % 300 == 0 and self.model.training:
+            self.model.eval()
+            self.sync_buffers()
 
     def close(self):
         """Drain the device and free the captured graphs.  Call before
         dist.destroy_process_group(): a graph with captured RCCL collectives
         still references the communicator, and tearing the communicator down
-        under a live graph aborts the process on this stack."""
-        if self.graphs is None:
+        under a live graph aborts the process on this stack.  Runs no
+        collective (sync_buffers() is the caller's, on every rank)."""
+        if not self.graphs:
             return
         torch.cuda.synchronize()
-        self.sync_buffers()
-        torch.cuda.synchronize()
-        for g in self.graphs:
-            if g is not None:
-                g.reset()
-        self.graphs = None
+        for ga, gb, _ in self.graphs.values():
+            for g in (ga, gb):
+                if g is not None:
+                    g.reset()
+        self.graphs = {}
         torch.cuda.synchronize()
 
     def timed_replays(self, batches, replays: int = 3) -> dict:
@@ -632,8 +672,8 @@ def build_parser():
                    help="path of DDRNet23s_imagenet.pth (default: the reference's relative path "
                         "./GuideDepth/model/weights/DDRNet23s_imagenet.pth)")
     p.add_argument("--graph", action="store_true",
-                   help="replay the step from HIP graphs (GraphTrainer; BN stays in train mode, "
-                        "i.e. implies --no-eval-quirk)")
+                   help="replay the step from HIP graphs (GraphTrainer; one captured step per BN "
+                        "mode, so the eval-mode quirk runs replayed too)")
     return p
 
 
@@ -649,7 +689,8 @@ def main(argv=None):
     model = GuideDepth(pretrained=args.pretrained).to(world.device)
     loss_fn = SSIML1(1.0, 0.1, depth_norm=True)
     if args.graph:
-        trainer = GraphTrainer(model, loss_fn, world, lr=args.lr, amp=args.amp)
+        trainer = GraphTrainer(model, loss_fn, world, lr=args.lr, amp=args.amp,
+                               eval_quirk=not args.no_eval_quirk)
         optimizer, ddp = trainer.optimizer, model
     else:
         optimizer = make_adam(model, args.lr)

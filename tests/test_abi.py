@@ -18,7 +18,7 @@ def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\b(?:int|size_t|const char\*)\s+(mde_\w+)\s*\(([^)]*)\)\s*;", text):
+    for m in re.finditer(r"\b(?:int|size_t|double|const char\*)\s+(mde_\w+)\s*\(([^)]*)\)\s*;", text):
         args = m.group(2).strip()
         n = 0 if args in ("", "void") else args.count(",") + 1
         decls[m.group(1)] = n
@@ -98,3 +98,33 @@ def test_timing_registry_names():
     assert "bilinear_bwd" in names and "ssim3_l1" in names and len(set(names)) == len(names)
     _abi.timing_reset()
     assert _abi.timing_collect() == {}
+
+
+def test_convbf_flops_are_algorithmic():
+    """The registry prices every convbf pass at the convolution's own MACs over
+    the forward output plane -- the stride-2 data gradient too (it used to be
+    credited with its full-resolution gx plane: 4x the true count)."""
+    from monocular_depth_estimation_amd import _abi
+    lib = _abi.load()
+    n, cin, cout, h, w = 32, 32, 64, 240, 320
+    for ks in (1, 3):
+        for stride in (1, 2):
+            ho, wo = (h + 2 * (ks // 2) - ks) // stride + 1, (w + 2 * (ks // 2) - ks) // stride + 1
+            want = 2.0 * n * ho * wo * cin * cout * ks * ks
+            for pass_ in (0, 1, 2):
+                assert lib.mde_convbf_flops(n, cin, cout, h, w, ks, stride, pass_) == want, \
+                    (ks, stride, pass_)
+    assert lib.mde_convbf_flops(n, 30, cout, h, w, 3, 2, 1) == 0.0  # unsupported shape
+
+
+def test_convbf_supported_at_batch():
+    """mde_convbf_supported_n refuses a batch whose launch would be refused
+    (n x patches >= 2^22), where the batch-free query still says yes."""
+    from monocular_depth_estimation_amd import _abi
+    lib = _abi.load()
+    args = (64, 64, 60, 80, 3, 1)
+    for p in (0, 1, 2):
+        assert lib.mde_convbf_supported(*args, p) == 1
+        assert lib.mde_convbf_supported_n(32, *args, p) == 1
+        assert lib.mde_convbf_supported_n(1 << 22, *args, p) == 0
+    assert lib.mde_convbf_supported_n(0, *args, 0) == 0

@@ -109,3 +109,40 @@ def test_ddp_gradients_are_the_mean_of_per_shard_gradients(mode):
             worst = max(worst, float((res[r]["grads"][n] - mean).abs().max()) / scale)
         assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n  # identical after all-reduce
     assert worst < 1e-4, worst
+
+
+def _scheme_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.pop("MDE_DP_OVERLAP", None)
+    import torch.distributed as dist
+
+    from monocular_depth_estimation_amd.train import dp_exchange_scheme, init_world
+    w = init_world(backend="gloo")
+    got = {
+        # what GraphTrainer selects in THIS 2-rank group, and in an RCCL group
+        # of the same size (the driver's `bench.py --gpus 8` form), by default
+        "gloo": dp_exchange_scheme(w.size, dist.get_backend()),
+        "nccl": dp_exchange_scheme(w.size, "nccl"),
+        "nccl_env1": dp_exchange_scheme(w.size, "nccl", env={"MDE_DP_OVERLAP": "1"}),
+        "nccl_env0": dp_exchange_scheme(w.size, "nccl", env={"MDE_DP_OVERLAP": "0"}),
+        "gloo_env1": dp_exchange_scheme(w.size, "gloo", env={"MDE_DP_OVERLAP": "1"}),
+        "one_rank": dp_exchange_scheme(1, "nccl"),
+    }
+    torch.save(got, os.path.join(out_dir, f"scheme{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_multi_rank_default_exchange_is_flat():
+    """Verdict r5 #1: at N > 1 GraphTrainer defaults to the flat exchange (graph
+    A -> one eager all_reduce -> graph B), so no multi-rank collective is ever
+    captured unless MDE_DP_OVERLAP=1 asks for the overlapped buckets (RCCL
+    only; a gloo group cannot capture)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_scheme_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"scheme{r}.pt"), weights_only=True) for r in range(world)]
+    assert res[0] == res[1]
+    assert res[0] == {"gloo": "flat", "nccl": "flat", "nccl_env1": "overlap", "nccl_env0": "flat",
+                      "gloo_env1": "flat", "one_rank": None}

@@ -164,6 +164,63 @@ def test_convbf_pack_scope_matches_per_conv_pack():
                 p.mul_(0.9).add_(0.01)
 
 
+def test_convbf_pack_scope_survives_rebuild_after_capture():
+    """a captured forward records the pack table's device pointer.
+    An eager forward after the capture that registers a new conv rebuilds the
+    table; the old one must stay alive (the scope keeps retired tables), so
+    the graph's replays still pack every filter it uses: replayed outputs ==
+    eager outputs at the same weights, before and after the rebuild."""
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd import nn as mnn
+    from monocular_depth_estimation_amd.nn import Conv2d
+
+    class Two(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = Conv2d(64, 128, 3, stride=2, padding=1, bias=False)
+            self.b = Conv2d(128, 64, 1, bias=False)
+            self.c = Conv2d(64, 64, 3, padding=1, bias=False)
+
+        def forward(self, x, late):
+            y = self.b(self.a(x))
+            return self.c(y) if late else y
+
+    m = Two().to(DEV)
+    x = torch.randn((2, 64, 60, 80), device=DEV).to(torch.bfloat16)
+    out = torch.empty((2, 64, 30, 40), device=DEV, dtype=torch.bfloat16)
+
+    def fwd(late):
+        with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+            with mnn.convbf_pack_scope(m, x.device):
+                return m(x, late)
+
+    with torch.no_grad():
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            fwd(False)  # registers a, b
+            fwd(False)  # they are in the table from here
+        torch.cuda.current_stream().wait_stream(s)
+        g, _, _ = _abi.capture_graph(lambda: out.copy_(fwd(False)), s)
+        sc = m.__dict__["_convbf_pack"]
+        table0 = sc.table
+        for p in m.parameters():
+            p.mul_(0.9).add_(0.01)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, fwd(False))
+        fwd(True)  # registers c: the next forward rebuilds the table
+        fwd(True)
+        assert sc.table is not table0 and any(t is table0 for t in sc.retired)
+        torch.cuda.empty_cache()
+        for p in m.parameters():
+            p.mul_(0.9).add_(0.01)
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out, fwd(False))
+    g.reset()
+
+
 def test_convbf_biased_conv_adds_bias_in_bf16():
     """Conv2d(bias=True) on the bf16 route (DDRNet's segmenthead 1x1): output in
     autocast's dtype, bias gradient = the sum of gy."""

@@ -86,6 +86,55 @@ def test_bf16_autocast_step():
     assert min(moved) > 0.5e-4, moved
 
 
+def _run_quirk(build, graph, epochs=2, steps=3, bs=2, h=64, w=96, eager_steps=1):
+    """The reference's epoch recipe (train.py:79,134-136,161): model.train() at
+    the epoch start, model.eval() after step 0, never undone within the epoch."""
+    from monocular_depth_estimation_amd.loss import SSIML1
+    from monocular_depth_estimation_amd.train import (GraphTrainer, Trainer, World, make_adam,
+                                                      synthetic_batch)
+    torch.manual_seed(0)
+    model = build().to(DEV)
+    world = World(0, 0, 1, torch.device(DEV))
+    loss_fn = SSIML1(1.0, 0.1, depth_norm=True)
+    if graph:
+        tr = GraphTrainer(model, loss_fn, world, lr=1e-4, eager_steps=eager_steps, eval_quirk=True)
+    else:
+        tr = Trainer(model, make_adam(model, 1e-4), loss_fn, world, eval_quirk=True)
+    losses, modes = [], []
+    for e in range(epochs):
+        tr.begin_epoch()
+        for k in range(steps):
+            image, depth = synthetic_batch(bs, h, w, 0, e * steps + k, DEV)
+            modes.append(model.training)
+            losses.append(float(tr.step(image, depth).detach()))
+            tr.after_step(k)
+    torch.cuda.synchronize()
+    state = {n: t.detach().clone() for n, t in model.state_dict().items()}
+    graphs = sorted(tr.graphs) if graph else None
+    if graph:
+        tr.close()
+    return losses, modes, state, graphs
+
+
+def test_graph_eval_quirk_matches_eager():
+    """Verdict r5 #2: the eval-mode quirk on the graph path.  Two epochs of
+    three steps with one eager warm-up step: epoch 0 = eager train-mode step,
+    then the eval-mode step captured and replayed; epoch 1 = the train-mode
+    step captured (after the eval graph exists), then the eval graph replayed
+    again.  Losses, parameters AND BN running statistics (updated by the
+    train-mode steps only) equal the eager Trainer's to 1e-6."""
+    from monocular_depth_estimation_amd import GuideDepth
+    build = lambda: GuideDepth(pretrained=False)  # noqa: E731
+    le, me, se, _ = _run_quirk(build, graph=False)
+    lg, mg, sg, graphs = _run_quirk(build, graph=True)
+    assert me == mg == [True, False, False] * 2
+    assert graphs == ["eval", "train"]
+    for a, b in zip(lg, le):
+        assert abs(a - b) <= 1e-6 * abs(b), (lg, le)
+    worst = max(float((sg[n].double() - se[n].double()).abs().max()) for n in se)
+    assert worst <= 1e-6, worst
+
+
 def test_captured_memset_repaired():
     """A hipMemsetAsync captured into a graph is wrong from the second replay on
     (ROCm runtime; csrc/graph.hip).  capture_graph swaps it for a fill kernel:

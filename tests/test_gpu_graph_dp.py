@@ -10,7 +10,12 @@ Two exchange schemes, both checked:
               cannot be captured, so it runs the step eagerly (eager_steps).
 Checks: (1) the FIRST step's averaged gradient on every rank equals the mean
 of the two ranks' local gradients, snapshotted just before the exchange
-(to 1e-6: the sum of two fp32 values); (2) the
+(to 1e-6: the sum of two fp32 values); (1b) flat: the local gradient the
+first REPLAYED step contributes equals an independent eager forward +
+backward of a fresh model holding the same weights on the same shard (so a
+wrong local gradient under capture -- stale packed filters, stale BN
+statistics -- fails; 1e-5 of each tensor's scale under MIOpen's
+deterministic solvers); (2) the
 parameters are bitwise identical on both ranks after 5 steps although each
 rank initialised differently (rank 0's weights are broadcast, gradients
 averaged); (3) each rank's loss is its own shard's loss (the losses differ).
@@ -62,12 +67,14 @@ def _worker(rank, world, port, out_dir, mode):
     # through autograd is no reference here: at 64x96, bs 2, DAPPM's 1x1
     # BatchNorms over two values amplify rounding differences into percents
     local = {}
+    step = [0]
     if mode == "flat":
         orig = tr._allreduce
 
         def snap_allreduce():
-            if "flat" not in local and tr.flat_grad is not None:
-                local["flat"] = tr.flat_grad.detach().cpu().clone()
+            key = "flat" if step[0] == 0 else f"flat{step[0]}"
+            if key not in local and tr.flat_grad is not None:
+                local[key] = tr.flat_grad.detach().cpu().clone()
             orig()
         tr._allreduce = snap_allreduce
     else:
@@ -84,8 +91,17 @@ def _worker(rank, world, port, out_dir, mode):
     losses = []
     first = None
     avg = None
+    replay_k = tr.eager_steps  # the first step that runs from the captured graph
+    ref = None
     for k in range(5):
+        step[0] = k
         image, depth = synthetic_batch(2, 64, 96, rank, k, w.device)
+        if mode == "flat" and k == replay_k:  # the same weights, for the eager recomputation
+            torch.cuda.synchronize()
+            ref = GuideDepth(pretrained=False).to(w.device)
+            ref.load_state_dict(model.state_dict())
+            ref.train()
+            ref_batch = (image.clone(), depth.clone())
         losses.append(float(tr.step(image, depth).detach()))
         if k == 0:
             torch.cuda.synchronize()
@@ -93,6 +109,13 @@ def _worker(rank, world, port, out_dir, mode):
             if mode == "buckets":
                 avg = [f.detach().cpu().clone() for f in tr.buckets.buffers]
     torch.cuda.synchronize()
+    eager = None
+    if ref is not None:  # independent eager local gradient at the replayed step's weights
+        ref.zero_grad(set_to_none=True)
+        loss_fn(ref(ref_batch[0]), ref_batch[1]).backward()
+        torch.cuda.synchronize()
+        eager = [(p.grad.detach().cpu() / w.size) if p.grad is not None else torch.zeros_like(p).cpu()
+                 for p in ref.parameters() if p.requires_grad]
     state = {k: v.detach().cpu() for k, v in model.named_parameters()}
     # BN running statistics: rank-local during training (no per-step
     # broadcast), rank 0's to every rank on sync_buffers()
@@ -101,7 +124,8 @@ def _worker(rank, world, port, out_dir, mode):
     torch.cuda.synchronize()
     bn_synced = tr.flat_bn.detach().cpu().clone()
     tr.close()
-    torch.save({"losses": losses, "state": state, "local": local, "avg": avg,
+    torch.save({"losses": losses, "state": state, "local": local, "avg": avg, "eager": eager,
+                "replay_k": replay_k,
                 "bn_local": bn_local, "bn_synced": bn_synced,
                 "first": [g.cpu() for g in first]},
                os.path.join(out_dir, f"rank{rank}.pt"))
@@ -132,6 +156,17 @@ def test_graph_trainer_two_ranks(mode):
     for g, m in zip(got, want):
         m = m.view_as(g)
         assert float((g - m).abs().max()) <= 1e-6 * float(m.abs().max()) + 1e-12
+    if mode == "flat":  # (1b) the replayed step's local gradient vs an eager recomputation
+        for r in (r0, r1):
+            key = f"flat{r['replay_k']}"
+            assert key in r["local"], sorted(r["local"])
+            got = r["local"][key].split([g.numel() for g in r["eager"]])
+            gmax = max(float(g.abs().max()) for g in r["eager"])
+            worst = 0.0
+            for g, e in zip(got, r["eager"]):
+                scale = max(float(e.abs().max()), 1e-6 * gmax)
+                worst = max(worst, float((g.view_as(e) - e).abs().max()) / scale)
+            assert worst <= 1e-5, worst
     for k, v in r0["state"].items():
         assert torch.equal(v, r1["state"][k]), k
     assert r0["losses"] != r1["losses"]

@@ -485,6 +485,35 @@ def test_train_sequence_golden(golden):
     np.testing.assert_allclose(losses, g["losses"], rtol=1e-2)
 
 
+def test_train_sequence_golden_graph(golden):
+    """The same loss-curve golden through GraphTrainer (the path bench.py and
+    `train.py --graph` replay): step 0 in train mode, the eval-mode switch
+    after it (src/train.py:79,134-136,161), steps 1.. from the captured
+    eval-mode graph (one eager warm-up step; test_gpu_graph.py's two-epoch test
+    covers a captured train-mode step next to it).  Tolerances as the eager
+    Trainer's (step 0 1e-5, curve 1e-2)."""
+    from monocular_depth_estimation_amd import GuideDepth
+    from monocular_depth_estimation_amd.loss import SSIML1
+    from monocular_depth_estimation_amd.train import GraphTrainer, World
+    g = golden("golden_trainseq.npz")
+    model = fill_(GuideDepth(pretrained=False)).to(DEV)
+    trainer = GraphTrainer(model, SSIML1(1.0, 0.1), World(device=torch.device(DEV)), lr=1e-4,
+                           eager_steps=1, eval_quirk=True)
+    trainer.begin_epoch()
+    losses = []
+    try:
+        for k in range(len(g["losses"])):
+            image = cu(seeded((2, 3, 64, 96), 100 + k, 0, 1))
+            depth = cu(seeded((2, 1, 64, 96), 200 + k, 0.1, 10.0))
+            losses.append(float(trainer.step(image, depth)))
+            trainer.after_step(k)
+        assert sorted(trainer.graphs) == ["eval"]
+    finally:
+        trainer.close()
+    np.testing.assert_allclose(losses[0], g["losses"][0], rtol=1e-5)
+    np.testing.assert_allclose(losses, g["losses"], rtol=1e-2)
+
+
 def test_guidedepth_cfg2_shape_runs_and_matches_oracle_encoder_free_parts():
     """640x480 bs=2 forward+backward on the HIP path vs the CPU oracle (1e-3 map tolerance)."""
     from monocular_depth_estimation_amd import GuideDepth

@@ -146,6 +146,7 @@ SIGNATURES = {
     "mde_conv3x3_wide_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int]),
     "mde_conv3x3_wide_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_conv3x3_wide_bwd_data": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_wino_mode": (_int, [_int]),
     "mde_wino_supported": (_int, [_i64, _i64, _i64, _i64, _int]),
     "mde_wino_weight_bytes": (_sz, [_i64, _i64]),
     "mde_wino_weight": (_int, [_vp, _vp, _i64, _i64, _int, _vp]),

@@ -403,6 +403,314 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
+// Persistent variant (the activation-heavy convs, xsplit == 1).  The blocks
+// of an XCD split its contiguous share of the (channel group, tile block)
+// items into runs of `ipb`; a block walks its run with ONE chunk pipeline
+// across item boundaries, so the next (item, chunk)'s input rows are in
+// flight while this one's transform, its MFMAs and -- at an item's last
+// chunk -- its output transform and stores run.  The ISA count of
+// wino_f23_kernel showed why: ~1,000 instructions a wave of per-block setup
+// (64-bit staging addresses and bounds masks, accumulator zeroing) and ~230
+// of epilogue against ~340 per 16-channel chunk, so the 32-channel convs (two
+// chunks an item) spent over half their time outside the MFMA loop.  Here a
+// thread's staging units are planned once per block; an item costs one
+// bounds pass over them (7 offsets), the loads are 32-bit-offset buffer loads
+// of the chunk's 16 planes (an out-of-plane unit reads past the buffer:
+// zeros, no select), and interior tile blocks store with no per-tile tests.
+// Same products, same summation order: bitwise the results of wino_f23_kernel.
+template <int CO_B, int TCB, bool STATS = false>
+__global__ void __launch_bounds__(256, 2)
+    wino_f23p_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
+                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
+                     float* __restrict__ stats, int per_xcd, int ipb) {
+  constexpr int NTB = kTRB * TCB;
+  constexpr int NG = NTB / 16;
+  constexpr int WCO = CO_B / 16;
+  constexpr int NTW = NG / (4 / WCO);
+  constexpr int PPT = NTB * kCIC / 256;
+  static_assert(NTW >= 1 && NTW * (4 / WCO) == NG, "wave tiling");
+  constexpr int kVP = kCIC * 16 + (NG == 2 ? 32 : 16);
+  __shared__ __attribute__((aligned(16))) float V[16][NG][kVP];
+  constexpr int RR = 2 * kTRB + 2;
+  constexpr int RW2 = TCB + 2;
+  constexpr int RWP = 2 * RW2 <= 24 ? 24 : 40;
+  constexpr int CPI = RR * RWP + 1;
+  constexpr int RAW = kCIC * RR * RW2;
+  constexpr int RPT = (RAW + 255) / 256;
+  __shared__ float raw[kCIC * CPI];
+
+  const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3;
+  const int lb = xcd * per_xcd + jx * ipb;
+  int le = lb + ipb;
+  if (le > (xcd + 1) * per_xcd) le = (xcd + 1) * per_xcd;
+  if (le > total) le = total;
+  if (lb >= le) return;
+  const int nchunks = ci_n / kCIC;
+  const int nsteps = (le - lb) * nchunks;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, kq = lane >> 4;
+  const int hw = h * w;  // < 2^24 (wino_persistent_ok)
+
+  // a thread's staging units, tile independent: plane offset within the
+  // block's window and (row, column) of the window for the bounds pass
+  int rel[RPT], rcw[RPT];
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int e = tid + 256 * k;
+    const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
+    const int r = rem / RW2, c2 = rem - r * RW2;
+    rel[k] = ch * hw + r * w + 2 * c2;
+    rcw[k] = e < RAW ? (r << 16) | (2 * c2) : 0x7fff0000;  // row 32767: never in the plane
+  }
+  uint32_t voff[RPT];
+  // the bounds pass of an item: byte offsets within the chunk's 16 planes
+  auto item_offsets = [&](int gr0, int gc0) {
+    const int base = gr0 * w + gc0;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int gr = gr0 + (rcw[k] >> 16), gc = gc0 + (rcw[k] & 0xffff);
+      const bool ok = (unsigned)gr < (unsigned)h && (unsigned)gc < (unsigned)w;
+      voff[k] = ok ? (uint32_t)(4 * (base + rel[k])) : 0x7ffffff0u;
+    }
+  };
+  using u2v = uint32_t __attribute__((ext_vector_type(2)));
+  float2 rv[RPT];
+  auto load = [&](int img, int chunk) {
+    const uint64_t a = (uint64_t)(x + ((int64_t)img * ci_n + (int64_t)chunk * kCIC) * hw);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const __amdgpu_buffer_rsrc_t R = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<void*>(((uint64_t)hi << 32) | lo), 0, 4 * kCIC * hw, 0x00020000);
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const u2v t = __builtin_bit_cast(u2v, __builtin_amdgcn_raw_buffer_load_b64(R, voff[k], 0, 0));
+      rv[k] = make_float2(__uint_as_float(t.x), __uint_as_float(t.y));
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int e = tid + 256 * k;
+      if (e < RAW) {
+        const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
+        const int r = rem / RW2, c2 = rem - r * RW2;
+        float* d = raw + ch * CPI + r * RWP + 2 * c2;
+        d[0] = rv[k].x;
+        d[1] = rv[k].y;
+      }
+    }
+  };
+  auto transform = [&]() {
+#pragma unroll
+    for (int pp = 0; pp < PPT; ++pp) {
+      const int p = tid + 256 * pp, ch = p / NTB, tl = p % NTB;
+      const float* q = raw + ch * CPI + 2 * (tl / TCB) * RWP + 2 * (tl % TCB) + 1;
+      float d[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = q[i * RWP + j];
+      float t[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[0][j] = d[0][j] - d[2][j];
+        t[1][j] = d[1][j] + d[2][j];
+        t[2][j] = d[2][j] - d[1][j];
+        t[3][j] = d[1][j] - d[3][j];
+      }
+      float* dst = &V[0][tl >> 4][ch * 16 + (tl & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v[4] = {t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1],
+                            t[i][1] - t[i][3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[(4 * i + j) * NG * kVP] = v[j];
+      }
+    }
+  };
+  // item l -> (channel group, image, block row, block column): the order of
+  // wino_f23_kernel's logical blocks (channel group fastest)
+  auto decode = [&](int l, int& cog, int& img, int& br, int& bc) {
+    cog = l % ncog;
+    int rest = l / ncog;
+    bc = rest % bcols;
+    rest /= bcols;
+    br = rest % brows;
+    img = rest / brows;
+  };
+  // the lane's U row of a (channel group, chunk): a fixed lane part + a uniform step
+  const float* ulane = U + ((int64_t)(16 * (wv % WCO) + li) * nchunks) * 256 + kq * 4;
+  auto uptr = [&](int cog, int chunk) {
+    return ulane + (int64_t)(cog * CO_B * nchunks + chunk) * 256;
+  };
+
+  f4 acc[16][NTW];
+#pragma unroll
+  for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+    for (int n = 0; n < NTW; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
+
+  int it = lb, chunk = 0;  // the current step's item and chunk
+  int cog, img, br, bc;
+  decode(it, cog, img, br, bc);
+  item_offsets(2 * br * kTRB - 1, 2 * bc * TCB - 2);
+  constexpr int RING = 4;
+  f4 ring[RING];
+  {
+    const float* u0 = uptr(cog, 0);
+#pragma unroll
+    for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(u0 + i * 16);
+  }
+  load(img, 0);
+  const int nt0 = (wv / WCO) * NTW;
+  for (int s = 0; s < nsteps; ++s) {
+    __syncthreads();  // the previous step's V (and raw) readers are done
+    stage();
+    __syncthreads();
+    int it_n = it, chunk_n = chunk + 1;
+    if (chunk_n == nchunks) {
+      chunk_n = 0;
+      ++it_n;
+    }
+    const bool more = s + 1 < nsteps;
+    int cog_n = cog, img_n = img, br_n = br, bc_n = bc;
+    if (chunk_n == 0) {  // the next item: decode's order, stepped without divisions
+      if (++cog_n == ncog) {
+        cog_n = 0;
+        if (++bc_n == bcols) {
+          bc_n = 0;
+          if (++br_n == brows) {
+            br_n = 0;
+            ++img_n;
+          }
+        }
+      }
+    }
+    if (more) {
+      if (chunk_n == 0) item_offsets(2 * br_n * kTRB - 1, 2 * bc_n * TCB - 2);
+      load(img_n, chunk_n);
+    }
+    transform();
+    __syncthreads();
+    const float* uc = uptr(cog, chunk);
+    const float* un = more ? uptr(cog_n, chunk_n) : uc;
+#pragma unroll
+    for (int xi = 0; xi < 16; ++xi) {
+      const f4 a = ring[xi % RING];
+      ring[xi % RING] = *reinterpret_cast<const f4*>(
+          xi + RING < 16 ? uc + (xi + RING) * 16 : un + (xi + RING - 16) * 16);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int n = 0; n < NTW; ++n)
+          acc[xi][n] = mfma(a[s4], V[xi][nt0 + n][(4 * s4 + kq) * 16 + li], acc[xi][n]);
+    }
+
+    if (chunk == nchunks - 1) {  // the item's output transform, stores (+ statistics)
+      const int co0 = cog * CO_B + 16 * (wv % WCO);
+      float* yb = y + (int64_t)img * co_n * hw;
+      // every output pixel of the tile block inside the plane: no per-pixel tests
+      const bool inner = 2 * (br + 1) * kTRB <= h && 2 * (bc + 1) * TCB <= w;
+      mde::Sh run[STATS ? 4 : 1];
+#pragma unroll
+      for (int n = 0; n < NTW; ++n) {
+        const int tl = 16 * (nt0 + n) + li;
+        const int oy = 2 * (br * kTRB + tl / TCB), ox = 2 * (bc * TCB + tl % TCB);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float u0[4], u1[4];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const float m0 = acc[b][n][r], m1 = acc[4 + b][n][r], m2 = acc[8 + b][n][r],
+                        m3 = acc[12 + b][n][r];
+            u0[b] = (m0 + m1) + m2;
+            u1[b] = (m1 - m2) - m3;
+          }
+          const float y00 = (u0[0] + u0[1]) + u0[2], y01 = (u0[1] - u0[2]) - u0[3];
+          const float y10 = (u1[0] + u1[1]) + u1[2], y11 = (u1[1] - u1[2]) - u1[3];
+          if constexpr (STATS) {
+            const bool ok0 = oy < h && ox < w, ok1 = oy + 1 < h && ox < w;
+            if (n == 0)
+              run[r] = {__shfl(ok0 ? y00 : 0.f, lane & 48, 64), 0.f, 0.f, 0.f};
+            mde::sh_add(run[r], y00, ok0);
+            mde::sh_add(run[r], y01, ok0);
+            mde::sh_add(run[r], y10, ok1);
+            mde::sh_add(run[r], y11, ok1);
+          }
+          float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + oy * w + ox;
+          if (inner) {
+            *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
+            *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
+          } else {
+            if (oy < h) {
+              if (ox + 1 < w) {
+                *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
+              } else if (ox < w) {
+                dst[0] = y00;
+              }
+            }
+            if (oy + 1 < h) {
+              if (ox + 1 < w) {
+                *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
+              } else if (ox < w) {
+                dst[w] = y10;
+              }
+            }
+          }
+        }
+      }
+      if constexpr (STATS) {
+        constexpr int NWN = 4 / WCO;
+        __syncthreads();  // every wave is past its last V read of this step
+        float* part = &V[0][0][0];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          mde::Sh a = run[r];
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
+          if (li == 0) {
+            float* p4 = part + (wv * 16 + 4 * kq + r) * 4;
+            p4[0] = a.ref;
+            p4[1] = a.n;
+            p4[2] = a.s1;
+            p4[3] = a.s2;
+          }
+        }
+        __syncthreads();
+        if (tid < CO_B) {
+          const int wc = tid / 16, c16 = tid % 16;
+          mde::Sh a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < NWN; ++k) {
+            const float* p4 = part + ((k * WCO + wc) * 16 + c16) * 4;
+            a = k == 0 ? mde::Sh{p4[0], p4[1], p4[2], p4[3]}
+                       : mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+          }
+          const int G = total / ncog, gb = it / ncog;
+          float* o4 = stats + ((int64_t)(cog * CO_B + tid) * G + gb) * 4;
+          o4[0] = a.ref;
+          o4[1] = a.n;
+          o4[2] = a.s1;
+          o4[3] = a.s2;
+        }
+      }
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi)
+#pragma unroll
+        for (int n = 0; n < NTW; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
+    }
+    it = it_n;
+    chunk = chunk_n;
+    cog = cog_n;
+    img = img_n;
+    br = br_n;
+    bc = bc_n;
+  }
+}
+
 struct WinoGeo {
   int bcols, brows, ncog, co_b;
   int64_t total;
@@ -449,6 +757,46 @@ inline int wino_xsplit(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w,
   return best;
 }
 
+// wino_f23p_kernel (persistent) where it applies: mode 1 (MDE_WINO_P=1 at
+// load, mde_wino_mode at run time), or 0 = the one-item-a-block kernel, the
+// default: measured per shape at bs 32 (tools/wino_bench.py --modes 0,1,
+// profiles/r06_wino_persistent_ab.txt) the persistent kernel is no faster on
+// the routed shapes (32 -> 32 @120x160 103.7 -> 102.1 us, @240x320 408 -> 419,
+// 64 -> 64 @60x80 72 -> 78, 128 -> 128 @30x40 73 -> 91) and the cfg2 step went
+// 982.7 -> 968.1 img/s: the per-block setup it removes was already hidden by
+// the CU's second block; the loop itself is bound by the texture addresser
+// (16 dwordx4 U loads a wave and chunk).  Only 16 -> 16 gains (994 -> 689 us),
+// which stays on the direct kernel (520 us).  Its byte offsets within a
+// chunk's 16 planes (64 h w < 2^30, below the out-of-plane offset) and packed
+// (row, column) staging units need h * w < 2^24 and h, w < 32767.
+int g_wino_mode = [] {
+  const char* e = std::getenv("MDE_WINO_P");
+  return e && e[0] == '1' ? 1 : 0;
+}();
+
+inline bool wino_persistent_ok(int64_t h, int64_t w) {
+  return g_wino_mode == 1 && h * w < ((int64_t)1 << 24) && h < 32767 && w < 32767;
+}
+
+// items a persistent block walks (MDE_WINO_IPB; 0 = the share of two blocks a CU)
+inline int wino_ipb() {
+  static const int v = [] {
+    const char* e = std::getenv("MDE_WINO_IPB");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+inline int wino_cus() {
+  static const int cus = [] {
+    int dev = 0, c = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev);
+    return c > 0 ? c : 256;
+  }();
+  return cus;
+}
+
 }  // namespace
 
 extern "C" {
@@ -459,6 +807,12 @@ extern "C" {
 int mde_wino_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtype) {
   WinoGeo g;
   return dtype == MDE_F32 && wino_geo(1, cin, cout, h, w, &g) ? 1 : 0;
+}
+
+int mde_wino_mode(int mode) {
+  const int prev = g_wino_mode;
+  if (mode == 0 || mode == 1) g_wino_mode = mode;
+  return prev;
 }
 
 size_t mde_wino_weight_bytes(int64_t cin, int64_t cout) {
@@ -516,13 +870,42 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
   // other operand: at 1/32 scale it outweighs the planes)
   const double bytes = 4.0 * n * h * w * (double)(cin + cout) + 64.0 * (double)cin * cout;
   const int xsplit = wino_xsplit(n, cin, cout, h, w, g);
+  const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
+  if (xsplit == 1 && wino_persistent_ok(h, w)) {
+    // persistent blocks: per XCD, its share of the items in runs of ipb
+    const int per_xcd = (int)mde::cdiv(g.total, 8);
+    int ipb = wino_ipb();
+    if (ipb <= 0) ipb = (int)mde::cdiv(per_xcd, 2 * wino_cus() / 8);  // two blocks a CU
+    const int pb = (int)mde::cdiv(per_xcd, ipb);
+    const dim3 grid((unsigned)(8 * pb)), block(256);
+#define MDE_WINOP(CB, TC, ST)                                                                     \
+  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23p_kernel<CB, TC, ST>), grid, block, 0, x, u, y,  \
+                  (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \
+                  stats, per_xcd, ipb)
+    if (stats) {
+      if (g.co_b == 64)
+        MDE_WINOP(64, 8, true);
+      else if (g.co_b == 32)
+        MDE_WINOP(32, 8, true);
+      else
+        MDE_WINOP(16, 16, true);
+    } else {
+      if (g.co_b == 64)
+        MDE_WINOP(64, 8, false);
+      else if (g.co_b == 32)
+        MDE_WINOP(32, 8, false);
+      else
+        MDE_WINOP(16, 16, false);
+    }
+#undef MDE_WINOP
+    return MDE_OK;
+  }
   int64_t nblk = (g.total + 7) / 8 * 8;
   if (xsplit > 1) {
     const int64_t ntiles = g.total / g.ncog, a = 8 / xsplit;
     nblk = 8 * ((ntiles + a - 1) / a) * (g.ncog / xsplit);
   }
   const dim3 grid((unsigned)nblk), block(256);
-  const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
 #define MDE_WINO(CB, TC, ST)                                                                      \
   MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST>), grid, block, 0, x, u, y,   \
                   (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \

@@ -6,9 +6,9 @@ identity), GuideDepth 2x64x96, 6 steps (2 eager, capture, 3 replays), against
 the eager Trainer under MIOpen's deterministic solvers.
 
   flat     graph A (forward, backward, flat pack + 1/N) -> one EAGER RCCL
-           all_reduce -> graph B (unpack, Adam): MDE_DP_OVERLAP=0 / gloo;
+           all_reduce -> graph B (unpack, Adam): the N > 1 default;
   overlap  per-bucket all_reduce(AVG) on a side stream captured INTO the step
-           graph (the N > 1 default over RCCL), plus the node census: exactly
+           graph (opt-in: MDE_DP_OVERLAP=1), plus the node census: exactly
            one collective's worth of nodes per bucket.
 
 Runs in its own process so that a runtime abort (SIGABRT) cannot take the
@@ -89,7 +89,8 @@ def main(mode):
     print(f"{mode}: eager reference done, graph trainer next", flush=True)
     tr, model, losses = _run(lambda m: GraphTrainer(
         m, loss_fn, world, lr=1e-4, dp_overlap=(mode == "overlap"), dp_collectives=True))
-    print(f"{mode}: step graph nodes: {[g.node_types for g in tr.graphs if g is not None]}",
+    ga, gb, _ = tr.graphs["train"]  # BN stays in train mode: the one captured step
+    print(f"{mode}: step graph nodes: {[g.node_types for g in (ga, gb) if g is not None]}",
           flush=True)
     for a, b in zip(losses, ref_losses):
         assert abs(a - b) <= 1e-6 * max(1.0, abs(b)), (losses, ref_losses)
@@ -97,24 +98,24 @@ def main(mode):
         err = float((p.detach() - ref_params[n]).abs().max())
         assert err <= 1e-6 * max(1.0, float(ref_params[n].abs().max())), (n, err)
     if mode == "flat":
-        assert tr.buckets is None and tr.graphs[1] is not None  # two graphs, RCCL between
+        assert tr.buckets is None and gb is not None  # two graphs, RCCL between
         assert tr.flat_grad is not None
         assert 0 < tr.flat_grad.numel() <= sum(p.numel() for p in tr.params)
     else:
         assert tr.buckets is not None and len(tr.buckets) >= 2
         seen = [p for ps, _ in tr.buckets for p in ps]
         assert len(seen) == len(tr.params) and len({id(p) for p in seen}) == len(seen)
-        assert tr.graphs[1] is None  # one graph, collectives inside
+        assert gb is None  # one graph, collectives inside
         assert sorted(tr.buckets.launched) == list(range(len(tr.buckets)))
         for ps, flat in tr.buckets:  # .grad is still the bucket storage
             for p in ps:
                 assert flat.data_ptr() <= p.grad.data_ptr() < \
                     flat.data_ptr() + flat.numel() * flat.element_size()
-        with_coll = tr.graphs[0].node_counts
+        with_coll = ga.node_counts
         tr.close()
         tr.buckets._collective = lambda flat: None  # same step, collectives stubbed out
-        tr._capture()
-        without = tr.graphs[0].node_counts
+        tr.graphs["train"] = tr._capture()
+        without = tr.graphs["train"][0].node_counts
         extra = with_coll["total"] - without["total"]
         assert extra == len(tr.buckets) * per_collective, (with_coll, without, per_collective)
     tr.close()

@@ -247,8 +247,8 @@ def _rccl_child(mode):
 
 @pytest.mark.timeout(400)
 def test_flat_rccl_allreduce_graph_matches_eager():
-    """The flat N > 1 GraphTrainer scheme over RCCL (MDE_DP_OVERLAP=0, and
-    any gloo group), in a one-rank "nccl" group with the exchange forced on:
+    """The flat N > 1 GraphTrainer scheme over RCCL (the default; any gloo
+    group takes it too), in a one-rank "nccl" group with the exchange forced on:
     graph A (forward, backward, flat pack x 1/N), one eager RCCL all_reduce,
     graph B (unpack, Adam) == the eager Trainer to 1e-6 in every loss and
     parameter (tests/_rccl_graph_child.py)."""
@@ -258,7 +258,7 @@ def test_flat_rccl_allreduce_graph_matches_eager():
 
 @pytest.mark.timeout(400)
 def test_bucketed_overlapped_allreduce_graph_matches_eager():
-    """The N > 1 default over RCCL: gradients as views of bucket buffers, each
+    """The opt-in overlapped exchange over RCCL (MDE_DP_OVERLAP=1): gradients as views of bucket buffers, each
     bucket all-reduced (AVG) over RCCL on a side stream from a
     post-accumulate hook, captured INTO the step graph; replayed step ==
     eager Trainer to 1e-6, every parameter in exactly one bucket, and the

@@ -200,3 +200,45 @@ def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     assert rel_err(xg.grad, xr.grad) <= 1e-5, "data gradient"
     assert rel_err(conv.weight.grad, wr.grad) <= 2e-5, "weight gradient"
     assert rel_err(conv.bias.grad, br.grad) <= 1e-5, "bias gradient"
+
+
+@pytest.mark.parametrize("cin,cout,h,w,n", [(32, 32, 120, 160, 3), (64, 64, 60, 80, 5),
+                                            (128, 128, 30, 40, 4), (256, 256, 15, 20, 3),
+                                            (64, 64, 9, 40, 3), (128, 64, 11, 30, 2),
+                                            (16, 32, 10, 18, 3), (32, 96, 7, 34, 2),
+                                            (16, 16, 40, 70, 2), (64, 256, 15, 20, 3)])
+def test_wino_persistent_bitwise(cin, cout, h, w, n):
+    """The persistent kernel (mde_wino_mode 1, opt-in: blocks walk runs of tile blocks
+    with one chunk pipeline across them, buffer loads, interior fast stores)
+    computes the same products in the same order as the one-block-per-item
+    kernel (mode 0, the default): y and the BN-statistics records bitwise equal, ragged
+    planes (edge blocks) and several run lengths (MDE_WINO_IPB is the
+    override; here the default split at small and large item counts)."""
+    from monocular_depth_estimation_amd import _abi
+    gen = torch.Generator(device=DEV).manual_seed(7 * cin + cout + h)
+    x = torch.rand((n, cin, h, w), device=DEV, generator=gen) - 0.3
+    wt = (torch.rand((cout, cin, 3, 3), device=DEV, generator=gen) - 0.5) * 0.1
+    st = _abi.stream_of(x)
+    u = torch.empty(16 * cin * cout, device=DEV)
+    _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), cin, cout, 0, st)
+    nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
+    outs = {}
+    prev = _abi.query("mde_wino_mode", -1)
+    try:
+        for mode in (0, 1):
+            _abi.query("mde_wino_mode", mode)
+            y = torch.full((n, cout, h, w), float("nan"), device=DEV)
+            y2 = torch.full_like(y, float("nan"))
+            stats = torch.full((cout, nb, 4), float("nan"), device=DEV)
+            _abi.call("mde_wino_conv_stats", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y), _abi.ptr(stats),
+                      n, cin, cout, h, w, 0, 0, st)
+            _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y2), n, cin, cout, h, w, 1,
+                      0, st)
+            torch.cuda.synchronize()
+            outs[mode] = (y, y2, stats)
+    finally:
+        _abi.query("mde_wino_mode", prev)
+    assert prev == 0  # the default
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert torch.isfinite(outs[1][0]).all() and torch.isfinite(outs[1][2]).all()

@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--reps", type=int, default=0)
     ap.add_argument("--only", default="", help="ci,co,h,w")
     ap.add_argument("--newcrf", action="store_true", help="cfg4's shapes at bs 16")
+    ap.add_argument("--modes", default="1", help="mde_wino_mode values to time, e.g. 0,1")
     a = ap.parse_args()
     shapes = SHAPES_NC if a.newcrf else SHAPES
     if a.only:
@@ -43,16 +44,18 @@ def main():
             _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), ci, co, 0, st)
             f = lambda: _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y), n, ci, co, h,
                                   w, 0, 0, st)
-            if a.reps:
-                for _ in range(a.reps):
-                    f()
-                torch.cuda.synchronize()
-                continue
-            us = kbench.timeit(f, 20) * 1e3
-            fl = 2.0 * 9 * n * h * w * ci * co
-            print(f"wino {ci}->{co} {h}x{w}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s direct-equiv, "
-                  f"{fl / 2.25 / us / 1e6:6.1f} TF/s MFMA ({fl / 2.25 / us / 1e6 / 157.3:5.1%})",
-                  flush=True)
+            for mode in (int(m) for m in a.modes.split(",")):
+                _abi.query("mde_wino_mode", mode)
+                if a.reps:
+                    for _ in range(a.reps):
+                        f()
+                    torch.cuda.synchronize()
+                    continue
+                us = kbench.timeit(f, 20) * 1e3
+                fl = 2.0 * 9 * n * h * w * ci * co
+                print(f"wino mode {mode} {ci}->{co} {h}x{w}: {us:7.1f} us  {fl / us / 1e6:6.1f} TF/s "
+                      f"direct-equiv, {fl / 2.25 / us / 1e6:6.1f} TF/s MFMA "
+                      f"({fl / 2.25 / us / 1e6 / 157.3:5.1%})", flush=True)
 
 
 if __name__ == "__main__":

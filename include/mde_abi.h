@@ -659,10 +659,11 @@ int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int
  * (for the data gradient: x = gy, cin = the forward's cout, cout = its cin);
  * pass 0 / 1 only selects the timing id.  cin % 16 == 0, cout % 32 == 0,
  * w even (mde_wino_supported). */
-/* Which Winograd kernel the activation-heavy passes (no XCD split) take: 0
- * one tile block a workgroup (the default), 1 the persistent one (blocks walk
- * runs of tile blocks with one chunk pipeline across them; MDE_WINO_P=1 at
- * load).
+/* Which Winograd kernel the activation-heavy passes (no XCD split) take: bit
+ * 0 = 0 one tile block a workgroup (the default), 1 the persistent one
+ * (blocks walk runs of tile blocks with one chunk pipeline across them;
+ * MDE_WINO_P=1 at load); bit 1 = the one-block kernel's B operands read one
+ * transform position ahead into registers (MDE_WINO_BPRE=1 at load).
  * Both compute the same products in the same order (bitwise equal).  mode < 0
  * only queries.  Returns the previous mode. */
 int mde_wino_mode(int mode);

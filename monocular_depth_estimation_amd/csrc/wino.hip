@@ -46,8 +46,18 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// U[co][chunk][xi][k][s] (ci = 16 chunk + 4 s + k): one float4 per lane and
-// (xi, chunk) holds its four k-steps.  FLIP: the data-gradient filter
+// offset of U[xi = 0] for (output channel co, input channel ci) of a conv with
+// `nchunks` 16-channel input chunks; xi adds 256 (layout below)
+__device__ __forceinline__ int64_t u_offset(int co, int ci, int nchunks) {
+  const int chunk = ci / kCIC, s = (ci % kCIC) / 4, k = ci % 4;
+  return ((((int64_t)(co / 16) * nchunks + chunk) * 16) * 64 + k * 16 + co % 16) * 4 + s;
+}
+
+// U[co / 16][chunk][xi][k][co % 16][s] (ci = 16 chunk + 4 s + k): one float4
+// per lane (lane = co % 16 + 16 k) and (xi, chunk) holds its four k-steps, and
+// a wave's 64 lanes read one contiguous KB per (xi, chunk): whole cache lines
+// (the [co][chunk][xi][k][s] order of round 4 gave every load 16 half-line
+// segments, and the texture addresser ran ~79 % busy at 32 channels).  FLIP: the data-gradient filter
 // g'[co' = ci][ci' = co] = rot180(g[co][ci]) (co_n / ci_n are the output /
 // input channels of the conv being RUN, i.e. swapped for FLIP).
 template <bool FLIP>
@@ -71,14 +81,13 @@ __global__ void __launch_bounds__(256)
     a[2][c] = 0.5f * ((w[0][c] - w[1][c]) + w[2][c]);
     a[3][c] = w[2][c];
   }
-  const int chunk = ci / kCIC, s = (ci % kCIC) / 4, k = ci % 4;
-  float* dst = U + ((int64_t)co * (ci_n / kCIC) + chunk) * 256 + k * 4 + s;
+  float* dst = U + u_offset(co, ci, ci_n / kCIC);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float u[4] = {a[r][0], 0.5f * ((a[r][0] + a[r][1]) + a[r][2]),
                         0.5f * ((a[r][0] - a[r][1]) + a[r][2]), a[r][2]};
 #pragma unroll
-    for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 16] = u[c];
+    for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[c];
   }
 }
 
@@ -120,20 +129,19 @@ __global__ void __launch_bounds__(256)
   // forward: row co of the (co_n x ci_n) conv; flipped: row ci of (ci_n x co_n)
   wino_g(w, u);
   {
-    float* dst = U + ((int64_t)co * (ci_n / kCIC) + ci / kCIC) * 256 + (ci % 4) * 4 + (ci % kCIC) / 4;
+    float* dst = U + u_offset(co, ci, ci_n / kCIC);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 16] = u[r][c];
+      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[r][c];
   }
   wino_g(wf, u);
   {
-    float* dst =
-        U2 + ((int64_t)ci * (co_n / kCIC) + co / kCIC) * 256 + (co % 4) * 4 + (co % kCIC) / 4;
+    float* dst = U2 + u_offset(ci, co, co_n / kCIC);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 16] = u[r][c];
+      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[r][c];
   }
 }
 
@@ -144,7 +152,7 @@ __global__ void __launch_bounds__(256)
 // STATS: also the following BatchNorm's per-block statistics of y (as the
 // direct conv's epilogue: stats[c][total / ncog][4] = (shift, count, s1, s2),
 // one record per channel and pixel block; the shift is a sample of the channel).
-template <int CO_B, int TCB, bool STATS = false>
+template <int CO_B, int TCB, bool STATS = false, bool BPRE = false>
 __global__ void __launch_bounds__(256, 2)
     wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
@@ -197,7 +205,7 @@ __global__ void __launch_bounds__(256, 2)
   const int64_t hw = (int64_t)h * w;
   const float* xb = x + (int64_t)img * ci_n * hw;
   const int nchunks = ci_n / kCIC;
-  const float* ua = U + (int64_t)(co0 + li) * nchunks * 256 + kq * 4;
+  const float* ua = U + ((int64_t)(co0 / 16) * nchunks * 16 * 64 + lane) * 4;
 
   // Input staging: per chunk, the block's 16 channels x 10 input rows x
   // (2 TCB + 4) columns (global column 2 bc TCB - 2 onward: even, so every
@@ -291,7 +299,7 @@ __global__ void __launch_bounds__(256, 2)
   constexpr int RING = 4;
   f4 ring[RING];
 #pragma unroll
-  for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 16);
+  for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 256);
   load(0);
   for (int chunk = 0; chunk < nchunks; ++chunk) {
     __syncthreads();  // the previous chunk's V (and raw) readers are done
@@ -300,21 +308,49 @@ __global__ void __launch_bounds__(256, 2)
     if (chunk + 1 < nchunks) load(chunk + 1);
     transform();
     __syncthreads();
-    const float* uc = ua + (int64_t)chunk * 256;
-    const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 256;
-#pragma unroll
-    for (int xi = 0; xi < 16; ++xi) {
-      const f4 a = ring[xi % RING];
-      ring[xi % RING] = *reinterpret_cast<const f4*>(
-          xi + RING < 16 ? uc + (xi + RING) * 16 : un + (xi + RING - 16) * 16);
-      // keep the load here: the scheduler otherwise sinks it next to its use
-      // (register pressure) and every step waits on L2 again
-      __builtin_amdgcn_sched_barrier(0);
+    const float* uc = ua + (int64_t)chunk * 4096;
+    const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 4096;
+    if constexpr (BPRE) {
+      // B operands one xi step ahead in registers: step xi's LDS reads are in
+      // flight during step xi - 1's MFMAs instead of waited on at its start
+      float b[2][4][NTW];
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int n = 0; n < NTW; ++n)
-          acc[xi][n] = mfma(a[s], V[xi][nt0 + n][(4 * s + kq) * 16 + li], acc[xi][n]);
+        for (int n = 0; n < NTW; ++n) b[0][s][n] = V[0][nt0 + n][(4 * s + kq) * 16 + li];
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) {
+        const f4 a = ring[xi % RING];
+        ring[xi % RING] = *reinterpret_cast<const f4*>(
+            xi + RING < 16 ? uc + (xi + RING) * 256 : un + (xi + RING - 16) * 256);
+        if (xi + 1 < 16) {
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int n = 0; n < NTW; ++n)
+              b[(xi + 1) & 1][s][n] = V[xi + 1 < 16 ? xi + 1 : 15][nt0 + n][(4 * s + kq) * 16 + li];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int n = 0; n < NTW; ++n) acc[xi][n] = mfma(a[s], b[xi & 1][s][n], acc[xi][n]);
+      }
+    } else {
+#pragma unroll
+      for (int xi = 0; xi < 16; ++xi) {
+        const f4 a = ring[xi % RING];
+        ring[xi % RING] = *reinterpret_cast<const f4*>(
+            xi + RING < 16 ? uc + (xi + RING) * 256 : un + (xi + RING - 16) * 256);
+        // keep the load here: the scheduler otherwise sinks it next to its use
+        // (register pressure) and every step waits on L2 again
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int n = 0; n < NTW; ++n)
+            acc[xi][n] = mfma(a[s], V[xi][nt0 + n][(4 * s + kq) * 16 + li], acc[xi][n]);
+      }
     }
   }
 
@@ -541,9 +577,9 @@ __global__ void __launch_bounds__(256, 2)
     img = rest / brows;
   };
   // the lane's U row of a (channel group, chunk): a fixed lane part + a uniform step
-  const float* ulane = U + ((int64_t)(16 * (wv % WCO) + li) * nchunks) * 256 + kq * 4;
+  const float* ulane = U + ((int64_t)(wv % WCO) * nchunks * 16 * 64 + lane) * 4;
   auto uptr = [&](int cog, int chunk) {
-    return ulane + (int64_t)(cog * CO_B * nchunks + chunk) * 256;
+    return ulane + (int64_t)(cog * (CO_B / 16) * nchunks + chunk) * 4096;
   };
 
   f4 acc[16][NTW];
@@ -561,7 +597,7 @@ __global__ void __launch_bounds__(256, 2)
   {
     const float* u0 = uptr(cog, 0);
 #pragma unroll
-    for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(u0 + i * 16);
+    for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(u0 + i * 256);
   }
   load(img, 0);
   const int nt0 = (wv / WCO) * NTW;
@@ -600,7 +636,7 @@ __global__ void __launch_bounds__(256, 2)
     for (int xi = 0; xi < 16; ++xi) {
       const f4 a = ring[xi % RING];
       ring[xi % RING] = *reinterpret_cast<const f4*>(
-          xi + RING < 16 ? uc + (xi + RING) * 16 : un + (xi + RING - 16) * 16);
+          xi + RING < 16 ? uc + (xi + RING) * 256 : un + (xi + RING - 16) * 256);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int s4 = 0; s4 < 4; ++s4)
@@ -774,6 +810,13 @@ int g_wino_mode = [] {
   return e && e[0] == '1' ? 1 : 0;
 }();
 
+// B operands prefetched one xi step ahead (wino_f23_kernel BPRE): mode bit 2
+// of mde_wino_mode, MDE_WINO_BPRE at load (A/B)
+int g_wino_bpre = [] {
+  const char* e = std::getenv("MDE_WINO_BPRE");
+  return e && e[0] == '1' ? 1 : 0;
+}();
+
 inline bool wino_persistent_ok(int64_t h, int64_t w) {
   return g_wino_mode == 1 && h * w < ((int64_t)1 << 24) && h < 32767 && w < 32767;
 }
@@ -810,8 +853,11 @@ int mde_wino_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtyp
 }
 
 int mde_wino_mode(int mode) {
-  const int prev = g_wino_mode;
-  if (mode == 0 || mode == 1) g_wino_mode = mode;
+  const int prev = g_wino_mode | (g_wino_bpre << 1);
+  if (mode >= 0 && mode <= 3) {
+    g_wino_mode = mode & 1;
+    g_wino_bpre = (mode >> 1) & 1;
+  }
   return prev;
 }
 
@@ -907,9 +953,16 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
   }
   const dim3 grid((unsigned)nblk), block(256);
 #define MDE_WINO(CB, TC, ST)                                                                      \
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST>), grid, block, 0, x, u, y,   \
-                  (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \
-                  stats, xsplit)
+  do {                                                                                            \
+    if (g_wino_bpre)                                                                              \
+      MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST, true>), grid, block, 0,  \
+                      x, u, y, (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog,     \
+                      (int)g.total, stats, xsplit);                                               \
+    else                                                                                          \
+      MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST, false>), grid, block, 0, \
+                      x, u, y, (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog,     \
+                      (int)g.total, stats, xsplit);                                               \
+  } while (0)
   if (stats) {
     if (g.co_b == 64)
       MDE_WINO(64, 8, true);

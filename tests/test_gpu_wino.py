@@ -225,7 +225,7 @@ def test_wino_persistent_bitwise(cin, cout, h, w, n):
     outs = {}
     prev = _abi.query("mde_wino_mode", -1)
     try:
-        for mode in (0, 1):
+        for mode in (0, 1, 2):
             _abi.query("mde_wino_mode", mode)
             y = torch.full((n, cout, h, w), float("nan"), device=DEV)
             y2 = torch.full_like(y, float("nan"))
@@ -239,6 +239,7 @@ def test_wino_persistent_bitwise(cin, cout, h, w, n):
     finally:
         _abi.query("mde_wino_mode", prev)
     assert prev == 0  # the default
-    for a, b in zip(outs[0], outs[1]):
-        assert torch.equal(a, b)
+    for m in (1, 2):  # 2: the one-block kernel with its B operands read a step ahead
+        for a, b in zip(outs[0], outs[m]):
+            assert torch.equal(a, b), m
     assert torch.isfinite(outs[1][0]).all() and torch.isfinite(outs[1][2]).all()

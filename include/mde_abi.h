@@ -663,7 +663,10 @@ int mde_conv3x3_wide_bwd_data(const void* gy, const float* weight, void* gx, int
  * 0 = 0 one tile block a workgroup (the default), 1 the persistent one
  * (blocks walk runs of tile blocks with one chunk pipeline across them;
  * MDE_WINO_P=1 at load); bit 1 = the one-block kernel's B operands read one
- * transform position ahead into registers (MDE_WINO_BPRE=1 at load).
+ * transform position ahead into registers (default on; MDE_WINO_BPRE=0 at
+ * load turns it off); bit 2 = 32-channel blocks with the 16 transform
+ * positions split across waves (MDE_WINO_X=1 at load; its two halves are
+ * summed in another order: float64-tested, not bitwise the other kernels).
  * Both compute the same products in the same order (bitwise equal).  mode < 0
  * only queries.  Returns the previous mode. */
 int mde_wino_mode(int mode);

@@ -439,6 +439,284 @@ __global__ void __launch_bounds__(256, 2)
   }
 }
 
+// The 32-output-channel block (4 x 8 tiles x 32 channels) with the transform
+// positions split across waves instead of the tiles: wave (cg = wv % 2,
+// xh = wv / 2) owns channels 16 cg .. + 15, BOTH 16-tile groups and the eight
+// positions xi = 8 xh .. + 7 (transform rows 2 xh, 2 xh + 1).  A wave then
+// streams only half of its channels' U per chunk (8 whole-line float4 loads
+// for its 64 MFMAs, the 64-channel block's ratio; wino_f23_kernel<32, 8>
+// loads all 16 and shares them with no one), while its B reads and MFMAs stay
+// as many.  A^T M A is linear in M, so each wave applies it to its half (the
+// other rows zero) and the two halves are added: a wave hands its partial
+// outputs of the tile group it does not store to its partner through LDS and
+// stores the group it owns (xh) -- the same statistics layout as the tile
+// split.  The halves are summed in a different order than the one-wave
+// transform (not bitwise wino_f23_kernel; the float64 tests hold both).
+// BPRE as wino_f23_kernel's.
+template <bool STATS>
+__global__ void __launch_bounds__(256, 2)
+    wino_f23x_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
+                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
+                     float* __restrict__ stats) {
+  constexpr int CO_B = 32, TCB = 8;
+  constexpr int NTB = kTRB * TCB;  // 32 tiles
+  constexpr int NG = NTB / 16;     // 2 tile groups, both in every wave
+  constexpr int PPT = NTB * kCIC / 256;
+  constexpr int kVP = kCIC * 16 + 32;
+  __shared__ __attribute__((aligned(16))) float V[16][NG][kVP];
+
+  const int per = gridDim.x >> 3;
+  const int xcd = blockIdx.x & 7, jx = blockIdx.x >> 3;
+  const int l = xcd * per + jx;
+  if (l >= total) return;
+  const int cog = l % ncog, tile = l / ncog;
+  int rest = tile;
+  const int bc = rest % bcols;
+  rest /= bcols;
+  const int br = rest % brows;
+  const int img = rest / brows;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int li = lane & 15, kq = lane >> 4;
+  const int cg = wv & 1, xh = wv >> 1;
+  const int co0 = cog * CO_B + 16 * cg;
+  const int64_t hw = (int64_t)h * w;
+  const float* xb = x + (int64_t)img * ci_n * hw;
+  const int nchunks = ci_n / kCIC;
+  const float* ua = U + ((int64_t)(co0 / 16) * nchunks * 16 * 64 + lane) * 4 + 8 * xh * 256;
+
+  constexpr int RR = 2 * kTRB + 2;
+  constexpr int RW2 = TCB + 2;
+  constexpr int RWP = 24;
+  constexpr int CPI = RR * RWP + 1;
+  constexpr int RAW = kCIC * RR * RW2;
+  constexpr int RPT = (RAW + 255) / 256;
+  __shared__ float raw[kCIC * CPI];
+  const int gr0 = 2 * br * kTRB - 1, gc0 = 2 * bc * TCB - 2;
+  float2 rv[RPT];
+  auto load = [&](int chunk) {
+    const float* src = xb + (int64_t)chunk * kCIC * hw;
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int e = tid + 256 * k;
+      const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
+      const int r = rem / RW2, c2 = rem - r * RW2;
+      const int gr = gr0 + r, gc = gc0 + 2 * c2;
+      const bool ok = e < RAW && gr >= 0 && gr < h && gc >= 0 && gc < w;
+      const int64_t off = ok ? (int64_t)(e < RAW ? ch : 0) * hw + (int64_t)gr * w + gc : 0;
+      const float2 t = *reinterpret_cast<const float2*>(src + off);
+      rv[k] = ok ? t : make_float2(0.f, 0.f);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int e = tid + 256 * k;
+      if (e < RAW) {
+        const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
+        const int r = rem / RW2, c2 = rem - r * RW2;
+        float* d = raw + ch * CPI + r * RWP + 2 * c2;
+        d[0] = rv[k].x;
+        d[1] = rv[k].y;
+      }
+    }
+  };
+  auto transform = [&]() {
+#pragma unroll
+    for (int pp = 0; pp < PPT; ++pp) {
+      const int p = tid + 256 * pp, ch = p / NTB, tl = p % NTB;
+      const float* q = raw + ch * CPI + 2 * (tl / TCB) * RWP + 2 * (tl % TCB) + 1;
+      float d[4][4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[i][j] = q[i * RWP + j];
+      float t[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        t[0][j] = d[0][j] - d[2][j];
+        t[1][j] = d[1][j] + d[2][j];
+        t[2][j] = d[2][j] - d[1][j];
+        t[3][j] = d[1][j] - d[3][j];
+      }
+      float* dst = &V[0][tl >> 4][ch * 16 + (tl & 15)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float v[4] = {t[i][0] - t[i][2], t[i][1] + t[i][2], t[i][2] - t[i][1],
+                            t[i][1] - t[i][3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dst[(4 * i + j) * NG * kVP] = v[j];
+      }
+    }
+  };
+
+  f4 acc[8][NG];  // [position 8 xh + xi][tile group]
+#pragma unroll
+  for (int xi = 0; xi < 8; ++xi)
+#pragma unroll
+    for (int n = 0; n < NG; ++n) acc[xi][n] = f4{0.f, 0.f, 0.f, 0.f};
+
+  constexpr int RING = 4;
+  f4 ring[RING];
+#pragma unroll
+  for (int i = 0; i < RING; ++i) ring[i] = *reinterpret_cast<const f4*>(ua + i * 256);
+  load(0);
+  const int xo = 8 * xh;  // this wave's first transform position
+  for (int chunk = 0; chunk < nchunks; ++chunk) {
+    __syncthreads();
+    stage();
+    __syncthreads();
+    if (chunk + 1 < nchunks) load(chunk + 1);
+    transform();
+    __syncthreads();
+    const float* uc = ua + (int64_t)chunk * 4096;
+    const float* un = ua + (int64_t)(chunk + 1 < nchunks ? chunk + 1 : chunk) * 4096;
+    float b[2][4][NG];
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int n = 0; n < NG; ++n) b[0][s][n] = V[xo][n][(4 * s + kq) * 16 + li];
+#pragma unroll
+    for (int xi = 0; xi < 8; ++xi) {
+      const f4 a = ring[xi % RING];
+      ring[xi % RING] = *reinterpret_cast<const f4*>(
+          xi + RING < 8 ? uc + (xi + RING) * 256 : un + (xi + RING - 8) * 256);
+      if (xi + 1 < 8) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int n = 0; n < NG; ++n)
+            b[(xi + 1) & 1][s][n] = V[xo + (xi + 1 < 8 ? xi + 1 : 7)][n][(4 * s + kq) * 16 + li];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int n = 0; n < NG; ++n) acc[xi][n] = mfma(a[s], b[xi & 1][s][n], acc[xi][n]);
+    }
+  }
+
+  // partial A^T M A of this wave's rows: row pair (2 xh, 2 xh + 1) of M[4][4];
+  // A^T = [1 1 1 0; 0 1 -1 -1] -> u0 gets rows 0, 1, 2 and u1 rows 1, -2, -3
+  auto partial = [&](int n, int r, float (&out)[4]) {
+    float u0[4], u1[4];
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const float ma = acc[bb][n][r], mb = acc[4 + bb][n][r];  // rows 2 xh, 2 xh + 1
+      if (xh == 0) {  // rows 0, 1
+        u0[bb] = ma + mb;
+        u1[bb] = mb;
+      } else {  // rows 2, 3
+        u0[bb] = ma;
+        u1[bb] = -ma - mb;
+      }
+    }
+    out[0] = (u0[0] + u0[1]) + u0[2];
+    out[1] = (u0[1] - u0[2]) - u0[3];
+    out[2] = (u1[0] + u1[1]) + u1[2];
+    out[3] = (u1[1] - u1[2]) - u1[3];
+  };
+  // hand the partner (same channels, other rows) the group it stores
+  __syncthreads();  // every wave is past its last V read
+  float* xch = &V[0][0][0];  // [cg][group][r][4][64 lanes]
+  // (the group index stays a compile-time constant under a wave-uniform
+  // branch: an accumulator indexed at run time would live in scratch)
+#pragma unroll
+  for (int ng = 0; ng < NG; ++ng) {
+    if (ng != xh) {  // the group the partner stores
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float o[4];
+        partial(ng, r, o);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) xch[(((cg * 2 + ng) * 4 + r) * 4 + q) * 64 + lane] = o[q];
+      }
+    }
+  }
+  __syncthreads();
+  float* yb = y + (int64_t)img * co_n * hw;
+  const int n = xh;  // the group this wave stores
+  const int tl = 16 * n + li;
+  const int oy = 2 * (br * kTRB + tl / TCB), ox = 2 * (bc * TCB + tl % TCB);
+  mde::Sh run[STATS ? 4 : 1];
+  float own[4][4];
+#pragma unroll
+  for (int ng = 0; ng < NG; ++ng)
+    if (ng == xh)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) partial(ng, r, own[r]);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float* o = own[r];
+    const float* pp = xch + ((cg * 2 + n) * 4 + r) * 4 * 64 + lane;
+    // rows 0-1 partial + rows 2-3 partial, in that order whichever wave stores
+    const float y00 = xh == 0 ? o[0] + pp[0] : pp[0] + o[0];
+    const float y01 = xh == 0 ? o[1] + pp[64] : pp[64] + o[1];
+    const float y10 = xh == 0 ? o[2] + pp[128] : pp[128] + o[2];
+    const float y11 = xh == 0 ? o[3] + pp[192] : pp[192] + o[3];
+    if constexpr (STATS) {
+      const bool ok0 = oy < h && ox < w, ok1 = oy + 1 < h && ox < w;
+      run[r] = {__shfl(ok0 ? y00 : 0.f, lane & 48, 64), 0.f, 0.f, 0.f};
+      mde::sh_add(run[r], y00, ok0);
+      mde::sh_add(run[r], y01, ok0);
+      mde::sh_add(run[r], y10, ok1);
+      mde::sh_add(run[r], y11, ok1);
+    }
+    float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
+    if (oy < h) {
+      if (ox + 1 < w) {
+        *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
+      } else if (ox < w) {
+        dst[0] = y00;
+      }
+    }
+    if (oy + 1 < h) {
+      if (ox + 1 < w) {
+        *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
+      } else if (ox < w) {
+        dst[w] = y10;
+      }
+    }
+  }
+  if constexpr (STATS) {
+    // as wino_f23_kernel's: butterfly over the 16 tiles, then the two waves
+    // holding a channel set (its two tile groups) merged in wave order
+    __syncthreads();
+    float* part = &V[0][0][0] + 8192;  // past the exchange slots
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mde::Sh a = run[r];
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) a = mde::sh_xor_sum(a, o);
+      if (li == 0) {
+        float* p4 = part + (wv * 16 + 4 * kq + r) * 4;
+        p4[0] = a.ref;
+        p4[1] = a.n;
+        p4[2] = a.s1;
+        p4[3] = a.s2;
+      }
+    }
+    __syncthreads();
+    if (tid < CO_B) {
+      const int wc = tid / 16, c16 = tid % 16;
+      mde::Sh a{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const float* p4 = part + ((k * 2 + wc) * 16 + c16) * 4;
+        a = k == 0 ? mde::Sh{p4[0], p4[1], p4[2], p4[3]}
+                   : mde::sh_merge(a, {p4[0], p4[1], p4[2], p4[3]});
+      }
+      const int G = total / ncog, gb = tile;
+      float* o4 = stats + ((int64_t)(cog * CO_B + tid) * G + gb) * 4;
+      o4[0] = a.ref;
+      o4[1] = a.n;
+      o4[2] = a.s1;
+      o4[3] = a.s2;
+    }
+  }
+}
+
 // Persistent variant (the activation-heavy convs, xsplit == 1).  The blocks
 // of an XCD split its contiguous share of the (channel group, tile block)
 // items into runs of `ipb`; a block walks its run with ONE chunk pipeline
@@ -814,6 +1092,12 @@ int g_wino_mode = [] {
 // of mde_wino_mode, MDE_WINO_BPRE at load (A/B)
 int g_wino_bpre = [] {
   const char* e = std::getenv("MDE_WINO_BPRE");
+  return e && e[0] == '0' ? 0 : 1;
+}();
+// the 32-channel blocks on wino_f23x_kernel (positions split across waves):
+// mode bit 4, MDE_WINO_X at load
+int g_wino_x = [] {
+  const char* e = std::getenv("MDE_WINO_X");
   return e && e[0] == '1' ? 1 : 0;
 }();
 
@@ -853,10 +1137,11 @@ int mde_wino_supported(int64_t cin, int64_t cout, int64_t h, int64_t w, int dtyp
 }
 
 int mde_wino_mode(int mode) {
-  const int prev = g_wino_mode | (g_wino_bpre << 1);
-  if (mode >= 0 && mode <= 3) {
+  const int prev = g_wino_mode | (g_wino_bpre << 1) | (g_wino_x << 2);
+  if (mode >= 0 && mode <= 7) {
     g_wino_mode = mode & 1;
     g_wino_bpre = (mode >> 1) & 1;
+    g_wino_x = (mode >> 2) & 1;
   }
   return prev;
 }
@@ -947,6 +1232,18 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
     return MDE_OK;
   }
   int64_t nblk = (g.total + 7) / 8 * 8;
+  if (xsplit == 1 && g.co_b == 32 && g_wino_x) {
+    const dim3 grid((unsigned)nblk), block(256);
+    if (stats)
+      MDE_LAUNCH_MFMA(kid, bytes, flops, s, wino_f23x_kernel<true>, grid, block, 0, x, u, y,
+                      (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,
+                      stats);
+    else
+      MDE_LAUNCH_MFMA(kid, bytes, flops, s, wino_f23x_kernel<false>, grid, block, 0, x, u, y,
+                      (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,
+                      stats);
+    return MDE_OK;
+  }
   if (xsplit > 1) {
     const int64_t ntiles = g.total / g.ncog, a = 8 / xsplit;
     nblk = 8 * ((ntiles + a - 1) / a) * (g.ncog / xsplit);

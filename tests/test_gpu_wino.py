@@ -238,8 +238,56 @@ def test_wino_persistent_bitwise(cin, cout, h, w, n):
             outs[mode] = (y, y2, stats)
     finally:
         _abi.query("mde_wino_mode", prev)
-    assert prev == 0  # the default
+    assert prev & 3 == 2  # the default: one-block kernel, B prefetch on
     for m in (1, 2):  # 2: the one-block kernel with its B operands read a step ahead
         for a, b in zip(outs[0], outs[m]):
             assert torch.equal(a, b), m
     assert torch.isfinite(outs[1][0]).all() and torch.isfinite(outs[1][2]).all()
+
+
+@pytest.mark.parametrize("cin,cout,h,w,n", [(32, 32, 120, 160, 2), (64, 32, 60, 80, 3),
+                                            (32, 32, 9, 36, 3), (16, 32, 10, 18, 3),
+                                            (32, 96, 7, 34, 2)])
+def test_wino_position_split_vs_float64(cin, cout, h, w, n):
+    """wino_f23x_kernel (mode bit 4: the 32-channel blocks with the transform
+    positions split across waves, the two A^T M A halves summed) against the
+    float64 conv (1e-5 of max) and against the one-wave transform (2e-6 of
+    max: the same products, the halves added in another order); its BN
+    records merge to y's statistics like the tile-split kernel's."""
+    from monocular_depth_estimation_amd import _abi
+    gen = torch.Generator().manual_seed(cin * 5 + cout + w)
+    x = torch.rand((n, cin, h, w), generator=gen) - 0.4
+    wt = (torch.rand((cout, cin, 3, 3), generator=gen) - 0.5) * 0.1
+    yr = torch.nn.functional.conv2d(x.double(), wt.double(), None, 1, 1)
+    xd, wd = x.to(DEV), wt.to(DEV)
+    st = _abi.stream_of(xd)
+    u = torch.empty(16 * cin * cout, device=DEV)
+    _abi.call("mde_wino_weight", _abi.ptr(wd), _abi.ptr(u), cin, cout, 0, st)
+    nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
+    outs = {}
+    prev = _abi.query("mde_wino_mode", -1)
+    try:
+        for mode in (2, 6):
+            _abi.query("mde_wino_mode", mode)
+            y = torch.full((n, cout, h, w), float("nan"), device=DEV)
+            y2 = torch.full_like(y, float("nan"))
+            stats = torch.full((cout, nb, 4), float("nan"), device=DEV)
+            _abi.call("mde_wino_conv_stats", _abi.ptr(xd), _abi.ptr(u), _abi.ptr(y), _abi.ptr(stats),
+                      n, cin, cout, h, w, 0, 0, st)
+            _abi.call("mde_wino_conv", _abi.ptr(xd), _abi.ptr(u), _abi.ptr(y2), n, cin, cout, h, w,
+                      0, 0, st)
+            torch.cuda.synchronize()
+            outs[mode] = (y, y2, stats)
+    finally:
+        _abi.query("mde_wino_mode", prev)
+    y, y2, stats = outs[6]
+    assert torch.equal(y, y2)
+    assert rel_err(y, yr) <= 1e-5
+    assert rel_err(y, outs[2][0]) <= 2e-6
+    s = stats.double().cpu()
+    ref, cnt, s1, s2 = s[..., 0], s[..., 1], s[..., 2], s[..., 3]
+    assert float(cnt.sum(1).min()) == n * h * w
+    mean = (s1 + cnt * ref).sum(1) / cnt.sum(1)
+    yd = y.double().cpu()
+    mr = yd.mean((0, 2, 3))
+    assert float((mean - mr).abs().max() / mr.abs().max()) <= 1e-5

@@ -679,6 +679,13 @@ int mde_wino_weight2(const float* weight, float* u, float* u_flip, int64_t cin, 
                      void* stream);
 int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
                   int64_t h, int64_t w, int pass, int dtype, void* stream);
+/* mde_wino_conv with y = add + conv(x) (add [n,cout,h,w] fp32, read once in the
+ * epilogue; must not overlap y): the data gradient of a BasicBlock's first conv summed
+ * with the residual path's gradient of the same input (DDRNet_23_slim.py:61-72,
+ * `out += residual`), where autograd would run a separate accumulation add. */
+int mde_wino_conv_acc(const float* x, const float* u, const float* add, float* y, int64_t n,
+                      int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
+                      void* stream);
 /* The same with the following BatchNorm's statistics of y from the epilogue
  * (stats [cout][mde_wino_stats_blocks][4] = (shift, count, s1, s2), the format
  * of mde_batchnorm_fwd_train_stats; NULL stats = mde_wino_conv). */

@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from ...functional import bilinear_resize
-from ...nn import BatchNorm2d, Conv2d, conv_nobias_stats, run_sequential
+from ...nn import BatchNorm2d, Conv2d, conv_nobias_stats, residual_grad_slot, run_sequential
 
 BN_MOMENTUM = 0.1
 
@@ -33,10 +33,10 @@ def conv3x3(in_planes, out_planes, stride=1):
     return Conv2d(in_planes, out_planes, 3, stride=stride, padding=1, bias=False)
 
 
-def _conv_stats(conv, x, bn):
+def _conv_stats(conv, x, bn, gx_slot=None):
     """(y, stats) positional arguments of bn: conv(x) without a bias and its BN
     statistics from the conv's epilogue (nn.conv_nobias_stats)."""
-    y, st = conv_nobias_stats(conv, x, bn)
+    y, st = conv_nobias_stats(conv, x, bn, gx_slot)
     return y, None, None, st
 
 
@@ -57,14 +57,22 @@ class BasicBlock(nn.Module):
         self.downsample = downsample
         self.stride = stride
         self.no_relu = no_relu
+        # the final activation when the owner applies its own ReLU to this
+        # block's output and reads nothing else of it (DualResNet: layer1 /
+        # layer2); None = bn2's ("none" with no_relu, else "relu")
+        self.out_act = None
 
     def forward(self, x):
         # bias-free 3x3 convs on the HIP kernels where they apply (conv_nobias);
         # in training each BN takes its batch statistics from the conv's epilogue
-        y = self.bn1(*_conv_stats(self.conv1, x, self.bn1))
+        # x feeds conv1 and (no downsample) the residual add: the residual's
+        # gradient then reaches conv1's Winograd data gradient through a slot
+        # and is summed in its epilogue instead of by an autograd add
+        slot = residual_grad_slot(self.conv1, x) if self.downsample is None else None
+        y = self.bn1(*_conv_stats(self.conv1, x, self.bn1, slot))
         res = x if self.downsample is None else run_sequential(self.downsample, x)
         y, st = conv_nobias_stats(self.conv2, y, self.bn2)
-        return self.bn2(y, residual=res, stats=st)
+        return self.bn2(y, residual=res, stats=st, act=self.out_act, res_slot=slot)
 
 
 class Bottleneck(nn.Module):
@@ -164,18 +172,20 @@ def _make_layer(block, inplanes, planes, blocks, stride=1):
     return nn.Sequential(*layers)
 
 
-def _seq_bn_residual(seq, x, residual):
-    """residual + seq(x) for a Sequential ending in a BatchNorm: the add runs in the BN pass.
-    Its bias-free convs go through conv_nobias (HIP kernels where they apply)."""
+def _seq_bn_residual(seq, x, residual, act=None):
+    """act(residual + seq(x)) for a Sequential ending in a BatchNorm: the add (and
+    the activation, e.g. the ReLU the reference applies to the sum next) run in
+    the BN pass.  Its bias-free convs go through conv_nobias (HIP kernels where
+    they apply)."""
     mods = list(seq)
     conv = mods[-2] if len(mods) >= 2 else None
     if not (isinstance(conv, nn.Conv2d) and conv.bias is None):
         # conv_nobias_stats assumes a bias-free conv feeding the BN: anything else
         # (a biased conv, a non-conv module) runs as-is, the add still in the BN
-        return mods[-1](run_sequential(mods[:-1], x), residual=residual)
+        return mods[-1](run_sequential(mods[:-1], x), residual=residual, act=act)
     x = run_sequential(mods[:-2], x) if len(mods) > 2 else x
     y, st = conv_nobias_stats(conv, x, mods[-1])
-    return mods[-1](y, residual=residual, stats=st)
+    return mods[-1](y, residual=residual, stats=st, act=act)
 
 
 class DualResNet(nn.Module):
@@ -206,6 +216,11 @@ class DualResNet(nn.Module):
         self.layer5 = _make_layer(Bottleneck, planes * 8, planes * 8, 1, stride=2)
         self.spp = DAPPM(planes * 16, spp_planes, planes * 4)
         self.final_layer = segmenthead(planes * 4, head_planes, out_features)
+        # layers[0] and layers[1] are only ever read through self.relu
+        # (reference :319-327): their last BatchNorm applies that ReLU in its
+        # own pass (no separate relu / threshold_backward launches)
+        self.layer1[-1].out_act = "relu"
+        self.layer2[-1].out_act = "relu"
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
@@ -216,19 +231,22 @@ class DualResNet(nn.Module):
     def forward(self, x):
         out_size = (x.shape[-2] // 8, x.shape[-1] // 8)
         r = self.relu
-        low = self.layer1(run_sequential(self.conv1, x))  # conv biases folded into the BNs
-        l2 = self.layer2(r(low))
-        rl2 = r(l2)  # the reference takes relu(layers[1]) twice (:327, :329; inplace=False): once here
+        # `relu(layers[0])` / `relu(layers[1])` come out of layer1 / layer2's last
+        # BN (out_act); the reference takes relu(layers[1]) twice (:327, :329;
+        # inplace=False): one tensor here
+        rlow = self.layer1(run_sequential(self.conv1, x))  # conv biases folded into the BNs
+        rl2 = self.layer2(rlow)
         l3 = self.layer3(rl2)
         high = self.layer3_(rl2)
-        low = _seq_bn_residual(self.down3, r(high), l3)  # l3 + down3(relu(high)), add fused into BN
+        # relu(l3 + down3(relu(high))): the add and the ReLU of :336 in the BN pass
+        rlow = _seq_bn_residual(self.down3, r(high), l3, act="relu")
         high = high + bilinear_resize(run_sequential(self.compression3, r(l3)), size=out_size)
-        l4 = self.layer4(r(low))
+        l4 = self.layer4(rlow)
         high = self.layer4_(r(high))
-        low = _seq_bn_residual(self.down4, r(high), l4)
+        rlow = _seq_bn_residual(self.down4, r(high), l4, act="relu")  # :344 / :350
         high = high + bilinear_resize(run_sequential(self.compression4, r(l4)), size=out_size)
         high = self.layer5_(r(high))
-        low = bilinear_resize(self.spp(self.layer5(r(low))), size=out_size)
+        low = bilinear_resize(self.spp(self.layer5(rlow)), size=out_size)
         return self.final_layer(low + high)
 
 

@@ -152,6 +152,7 @@ SIGNATURES = {
     "mde_wino_weight": (_int, [_vp, _vp, _i64, _i64, _int, _vp]),
     "mde_wino_weight2": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
     "mde_wino_conv": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
+    "mde_wino_conv_acc": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_wino_conv_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int,
                                    _vp]),
     "mde_wino_stats_blocks": (_int, [_i64, _i64, _i64, _i64, _i64]),

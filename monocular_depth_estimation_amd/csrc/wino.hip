@@ -46,6 +46,48 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// One 2 x 2 output tile at dst (row pitch w), clipped to the plane.  add
+// (nullable): the same tile of a gradient this result is summed into -- the
+// data gradient's other half when the conv's input also feeds a residual add
+// (mde_wino_conv_acc): one fp32 add per element, as autograd's accumulation.
+__device__ __forceinline__ void store_tile(float* dst, const float* add, int oy, int ox, int h,
+                                           int w, float y00, float y01, float y10, float y11) {
+  if (add) {
+    if (oy < h) {
+      if (ox + 1 < w) {
+        const float2 a = *reinterpret_cast<const float2*>(add);
+        y00 = a.x + y00;
+        y01 = a.y + y01;
+      } else if (ox < w) {
+        y00 = add[0] + y00;
+      }
+    }
+    if (oy + 1 < h) {
+      if (ox + 1 < w) {
+        const float2 a = *reinterpret_cast<const float2*>(add + w);
+        y10 = a.x + y10;
+        y11 = a.y + y11;
+      } else if (ox < w) {
+        y10 = add[w] + y10;
+      }
+    }
+  }
+  if (oy < h) {
+    if (ox + 1 < w) {
+      *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
+    } else if (ox < w) {
+      dst[0] = y00;
+    }
+  }
+  if (oy + 1 < h) {
+    if (ox + 1 < w) {
+      *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
+    } else if (ox < w) {
+      dst[w] = y10;
+    }
+  }
+}
+
 // offset of U[xi = 0] for (output channel co, input channel ci) of a conv with
 // `nchunks` 16-channel input chunks; xi adds 256 (layout below)
 __device__ __forceinline__ int64_t u_offset(int co, int ci, int nchunks) {
@@ -156,7 +198,7 @@ template <int CO_B, int TCB, bool STATS = false, bool BPRE = false>
 __global__ void __launch_bounds__(256, 2)
     wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
-                    float* __restrict__ stats, int xsplit) {
+                    float* __restrict__ stats, int xsplit, const float* __restrict__ add) {
   constexpr int NTB = kTRB * TCB;      // tiles per block
   constexpr int NG = NTB / 16;         // 16-tile groups (MFMA N tiles)
   constexpr int WCO = CO_B / 16;       // waves along output channels
@@ -356,6 +398,7 @@ __global__ void __launch_bounds__(256, 2)
 
   // A^T M A per (channel, tile): lane holds channels co0 + 4 kq + r, tile 16 (nt0 + n) + li
   float* yb = y + (int64_t)img * co_n * hw;
+  const float* ab = add ? add + (int64_t)img * co_n * hw : nullptr;
   mde::Sh run[STATS ? 4 : 1];
 #pragma unroll
   for (int n = 0; n < NTW; ++n) {
@@ -382,21 +425,8 @@ __global__ void __launch_bounds__(256, 2)
         mde::sh_add(run[r], y10, ok1);
         mde::sh_add(run[r], y11, ok1);
       }
-      float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
-      if (oy < h) {
-        if (ox + 1 < w) {
-          *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
-        } else if (ox < w) {
-          dst[0] = y00;
-        }
-      }
-      if (oy + 1 < h) {
-        if (ox + 1 < w) {
-          *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
-        } else if (ox < w) {
-          dst[w] = y10;
-        }
-      }
+      const int64_t yo = (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
+      store_tile(yb + yo, ab ? ab + yo : nullptr, oy, ox, h, w, y00, y01, y10, y11);
     }
   }
   if constexpr (STATS) {
@@ -457,7 +487,7 @@ template <bool STATS>
 __global__ void __launch_bounds__(256, 2)
     wino_f23x_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                      int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
-                     float* __restrict__ stats) {
+                     float* __restrict__ stats, const float* __restrict__ add) {
   constexpr int CO_B = 32, TCB = 8;
   constexpr int NTB = kTRB * TCB;  // 32 tiles
   constexpr int NG = NTB / 16;     // 2 tile groups, both in every wave
@@ -636,6 +666,7 @@ __global__ void __launch_bounds__(256, 2)
   }
   __syncthreads();
   float* yb = y + (int64_t)img * co_n * hw;
+  const float* ab = add ? add + (int64_t)img * co_n * hw : nullptr;
   const int n = xh;  // the group this wave stores
   const int tl = 16 * n + li;
   const int oy = 2 * (br * kTRB + tl / TCB), ox = 2 * (bc * TCB + tl % TCB);
@@ -663,21 +694,8 @@ __global__ void __launch_bounds__(256, 2)
       mde::sh_add(run[r], y10, ok1);
       mde::sh_add(run[r], y11, ok1);
     }
-    float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
-    if (oy < h) {
-      if (ox + 1 < w) {
-        *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
-      } else if (ox < w) {
-        dst[0] = y00;
-      }
-    }
-    if (oy + 1 < h) {
-      if (ox + 1 < w) {
-        *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
-      } else if (ox < w) {
-        dst[w] = y10;
-      }
-    }
+    const int64_t yo = (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
+    store_tile(yb + yo, ab ? ab + yo : nullptr, oy, ox, h, w, y00, y01, y10, y11);
   }
   if constexpr (STATS) {
     // as wino_f23_kernel's: butterfly over the 16 tiles, then the two waves
@@ -736,7 +754,8 @@ template <int CO_B, int TCB, bool STATS = false>
 __global__ void __launch_bounds__(256, 2)
     wino_f23p_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                      int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
-                     float* __restrict__ stats, int per_xcd, int ipb) {
+                     float* __restrict__ stats, int per_xcd, int ipb,
+                     const float* __restrict__ add) {
   constexpr int NTB = kTRB * TCB;
   constexpr int NG = NTB / 16;
   constexpr int WCO = CO_B / 16;
@@ -926,6 +945,7 @@ __global__ void __launch_bounds__(256, 2)
     if (chunk == nchunks - 1) {  // the item's output transform, stores (+ statistics)
       const int co0 = cog * CO_B + 16 * (wv % WCO);
       float* yb = y + (int64_t)img * co_n * hw;
+      const float* ab = add ? add + (int64_t)img * co_n * hw : nullptr;
       // every output pixel of the tile block inside the plane: no per-pixel tests
       const bool inner = 2 * (br + 1) * kTRB <= h && 2 * (bc + 1) * TCB <= w;
       mde::Sh run[STATS ? 4 : 1];
@@ -954,25 +974,13 @@ __global__ void __launch_bounds__(256, 2)
             mde::sh_add(run[r], y10, ok1);
             mde::sh_add(run[r], y11, ok1);
           }
-          float* dst = yb + (int64_t)(co0 + 4 * kq + r) * hw + oy * w + ox;
-          if (inner) {
+          const int64_t yo = (int64_t)(co0 + 4 * kq + r) * hw + oy * w + ox;
+          float* dst = yb + yo;
+          if (inner && !ab) {
             *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
             *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
           } else {
-            if (oy < h) {
-              if (ox + 1 < w) {
-                *reinterpret_cast<float2*>(dst) = make_float2(y00, y01);
-              } else if (ox < w) {
-                dst[0] = y00;
-              }
-            }
-            if (oy + 1 < h) {
-              if (ox + 1 < w) {
-                *reinterpret_cast<float2*>(dst + w) = make_float2(y10, y11);
-              } else if (ox < w) {
-                dst[w] = y10;
-              }
-            }
+            store_tile(dst, ab ? ab + yo : nullptr, oy, ox, h, w, y00, y01, y10, y11);
           }
         }
       }
@@ -1184,9 +1192,13 @@ int mde_wino_weight2(const float* weight, float* u, float* u_flip, int64_t cin, 
 
 // y[n][cout][h][w] = conv3x3(x[n][cin][h][w]) (stride 1, pad 1) from U =
 // mde_wino_weight(..).  `pass` 0 = forward, 1 = data gradient (timing id only).
-int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, int64_t n,
-                        int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
-                        void* stream) {
+}  // extern "C"
+
+namespace {
+
+int wino_launch(const float* x, const float* u, float* y, float* stats, const float* add,
+                int64_t n, int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
+                void* stream) {
   if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
   if (!x || !u || !y) return MDE_ERR_INVALID_ARG;
   WinoGeo g;
@@ -1212,7 +1224,7 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
 #define MDE_WINOP(CB, TC, ST)                                                                     \
   MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23p_kernel<CB, TC, ST>), grid, block, 0, x, u, y,  \
                   (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,   \
-                  stats, per_xcd, ipb)
+                  stats, per_xcd, ipb, add)
     if (stats) {
       if (g.co_b == 64)
         MDE_WINOP(64, 8, true);
@@ -1237,11 +1249,11 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
     if (stats)
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, wino_f23x_kernel<true>, grid, block, 0, x, u, y,
                       (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,
-                      stats);
+                      stats, add);
     else
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, wino_f23x_kernel<false>, grid, block, 0, x, u, y,
                       (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog, (int)g.total,
-                      stats);
+                      stats, add);
     return MDE_OK;
   }
   if (xsplit > 1) {
@@ -1254,11 +1266,11 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
     if (g_wino_bpre)                                                                              \
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST, true>), grid, block, 0,  \
                       x, u, y, (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog,     \
-                      (int)g.total, stats, xsplit);                                               \
+                      (int)g.total, stats, xsplit, add);                                          \
     else                                                                                          \
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST, false>), grid, block, 0, \
                       x, u, y, (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog,     \
-                      (int)g.total, stats, xsplit);                                               \
+                      (int)g.total, stats, xsplit, add);                                          \
   } while (0)
   if (stats) {
     if (g.co_b == 64)
@@ -1279,9 +1291,26 @@ int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, 
   return MDE_OK;
 }
 
+}  // namespace
+
+extern "C" {
+
+int mde_wino_conv_stats(const float* x, const float* u, float* y, float* stats, int64_t n,
+                        int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
+                        void* stream) {
+  return wino_launch(x, u, y, stats, nullptr, n, cin, cout, h, w, pass, dtype, stream);
+}
+
 int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t cin, int64_t cout,
                   int64_t h, int64_t w, int pass, int dtype, void* stream) {
-  return mde_wino_conv_stats(x, u, y, nullptr, n, cin, cout, h, w, pass, dtype, stream);
+  return wino_launch(x, u, y, nullptr, nullptr, n, cin, cout, h, w, pass, dtype, stream);
+}
+
+int mde_wino_conv_acc(const float* x, const float* u, const float* add, float* y, int64_t n,
+                      int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
+                      void* stream) {
+  if (!add) return MDE_ERR_INVALID_ARG;
+  return wino_launch(x, u, y, nullptr, add, n, cin, cout, h, w, pass, dtype, stream);
 }
 
 // Records per channel of mde_wino_conv_stats (the pixel blocks), or 0.

@@ -16,7 +16,7 @@ import torch
 from torch import nn
 
 from . import _abi
-from .functional import _amp_bwd, _amp_fwd, _gpu, _ws
+from .functional import GradSlot, _amp_bwd, _amp_fwd, _gpu, _ws
 
 _ACTS = {"none": 0, "relu": 1, "hardswish": 2}
 
@@ -30,7 +30,7 @@ class _BatchNormAct(torch.autograd.Function):
     @staticmethod
     @_bn_fwd
     def forward(ctx, x, weight, bias, prebias, residual, running_mean, running_var, nbt,
-                training, momentum, eps, act, stats=None):
+                training, momentum, eps, act, stats=None, res_slot=None):
         dt = torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32
         x = x.to(dt).contiguous()
         residual = residual.to(dt).contiguous() if residual is not None else None
@@ -61,6 +61,7 @@ class _BatchNormAct(torch.autograd.Function):
                       _abi.ptr(invstd), n, c, h, w, act, _abi.dtype_code(x), st)
         ctx.save_for_backward(x, weight, bias, residual, mean, invstd)
         ctx.training, ctx.act, ctx.has_prebias = bool(training), act, prebias is not None
+        ctx.res_slot = res_slot
         return y
 
     @staticmethod
@@ -84,11 +85,16 @@ class _BatchNormAct(torch.autograd.Function):
                   _abi.stream_of(gy))
         if want_r and not ctx.act:
             gr = gy
-        return gx, gw, gb, gpb, gr, None, None, None, None, None, None, None, None
+        if want_r and ctx.res_slot is not None:
+            # the residual input's other consumer (the block's first conv) adds
+            # it in its data-gradient epilogue: no accumulation add (GradSlot)
+            ctx.res_slot.put(gr)
+            gr = None
+        return gx, gw, gb, gpb, gr, None, None, None, None, None, None, None, None, None
 
 
 def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, prebias=None,
-                   stats=None):
+                   stats=None, res_slot=None):
     """act(bn(x + prebias) + residual) with nn.BatchNorm2d semantics (mode by bn.training).
 
     `prebias` is the bias of the convolution feeding this BN, folded in: the
@@ -96,6 +102,8 @@ def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, preb
     its gradient comes out of the BN backward.  `stats` (training only): the
     per-block shifted sums the producing conv's epilogue emitted for x
     (conv3x3_stats / bn_relu_pointwise), replacing the statistics pass.
+    `res_slot` (a functional.GradSlot from residual_grad_slot): the residual's
+    gradient goes to the slot instead of through autograd.
     """
     _gpu(x, residual, prebias)
     if bn.weight is None or bn.bias is None:
@@ -110,7 +118,7 @@ def batch_norm_act(x, bn: nn.BatchNorm2d, act: str = "none", residual=None, preb
         bn.running_var if (track or not training) else None,
         bn.num_batches_tracked if track else None,
         training, bn.momentum if bn.momentum is not None else 0.0, bn.eps, _ACTS[act],
-        stats if training else None)
+        stats if training else None, res_slot if residual is not None else None)
 
 
 class _Pointwise(torch.autograd.Function):
@@ -399,12 +407,13 @@ if WIDE_WGRAD_ALL:
 class _Conv3x3(torch.autograd.Function):
     @staticmethod
     @_amp_fwd
-    def forward(ctx, x, weight, passes, want_stats=False):
+    def forward(ctx, x, weight, passes, want_stats=False, gx_slot=None):
         x = x.contiguous()
         weight = weight.contiguous()
         n, cin, h, w = x.shape
         cout = weight.shape[0]
         stats = torch.empty((cout, 0, 4), dtype=torch.float32, device=x.device)
+        ctx.gx_slot = gx_slot
         u_flip = None  # Winograd: the data gradient's filter transform, made with the forward's
         if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip), + the BN statistics
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
@@ -450,8 +459,11 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     @_amp_bwd
     def backward(ctx, gy, _gstats):
+        # the residual path's gradient of x, handed over by the BatchNorm that
+        # adds x back (residual_grad_slot): summed into gx here
+        g2 = ctx.gx_slot.take() if ctx.gx_slot is not None else None
         if gy is None:  # only the non-differentiable output was used
-            return (None, None, None, None)
+            return (g2, None, None, None, None)
         x, weight = ctx.saved_tensors
         gy = gy.contiguous()
         n, cin, h, w = x.shape
@@ -465,8 +477,14 @@ class _Conv3x3(torch.autograd.Function):
                 if u is None:
                     u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
                     _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 1, st)
-                _abi.call("mde_wino_conv", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(gx), n, cout, cin, h,
-                          w, 1, _abi.dtype_code(gy), st)
+                if g2 is not None and g2.dtype == gy.dtype == torch.float32:
+                    g2 = g2.contiguous()  # held until the launch is enqueued
+                    _abi.call("mde_wino_conv_acc", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(g2),
+                              _abi.ptr(gx), n, cout, cin, h, w, 1, _abi.dtype_code(gy), st)
+                    g2 = None
+                else:
+                    _abi.call("mde_wino_conv", _abi.ptr(gy), _abi.ptr(u), _abi.ptr(gx), n, cout,
+                              cin, h, w, 1, _abi.dtype_code(gy), st)
             elif ctx.passes[1] == WIDE:
                 gx = torch.empty_like(x)
                 _abi.call("mde_conv3x3_wide_bwd_data", _abi.ptr(gy), _abi.ptr(weight), _abi.ptr(gx),
@@ -493,7 +511,9 @@ class _Conv3x3(torch.autograd.Function):
                 gw = torch.ops.aten.convolution_backward(
                     gy, x, weight, None, (1, 1), (1, 1), (1, 1), False, (0, 0), 1,
                     (False, True, False))[1]
-        return gx, gw, None, None
+        if g2 is not None:  # a data-gradient kernel with no accumulating epilogue
+            gx = g2 if gx is None else gx + g2
+        return gx, gw, None, None, None
 
 
 # bf16 (autocast) 3x3 convolutions on the v_mfma_f32_16x16x32_bf16 kernels:
@@ -1087,7 +1107,7 @@ class _GuideConvBf16(torch.autograd.Function):
 GUIDE_BF16 = os.environ.get("MDE_GUIDE_BF16", "1") != "0"  # A/B switch
 
 
-def _conv3x3_apply(x, weight, passes, want_stats):
+def _conv3x3_apply(x, weight, passes, want_stats, gx_slot=None):
     if weight.dtype != torch.float32:
         raise TypeError(f"conv3x3: the HIP kernels take a float32 weight, got {weight.dtype}")
     cin, cout = x.shape[1], weight.shape[0]
@@ -1097,21 +1117,21 @@ def _conv3x3_apply(x, weight, passes, want_stats):
         return _GuideConvBf16.apply(x, weight, bool(want_stats))
     if _conv3x3_bf16_path(cin, cout, x, weight):
         return _Conv3x3Bf16.apply(x.to(torch.bfloat16), weight, tuple(passes), want_stats)
-    return _Conv3x3.apply(x, weight, tuple(passes), want_stats)
+    return _Conv3x3.apply(x, weight, tuple(passes), want_stats, gx_slot)
 
 
-def conv3x3(x, weight, passes=(True, True, True)):
+def conv3x3(x, weight, passes=(True, True, True), gx_slot=None):
     """Bias-free 3x3 / stride 1 / padding 1 convolution on the HIP MFMA kernel (per-pass flags)."""
     _gpu(x)
-    return _conv3x3_apply(x, weight, passes, False)[0]
+    return _conv3x3_apply(x, weight, passes, False, gx_slot)[0]
 
 
-def conv3x3_stats(x, weight, passes=(True, True, True)):
+def conv3x3_stats(x, weight, passes=(True, True, True), gx_slot=None):
     """conv3x3 that also returns y's per-block BN statistics [cout][blocks][4]
     (shift, count, s1, s2) from the forward epilogue, or None when the forward
     is not on the HIP kernel (MIOpen)."""
     _gpu(x)
-    y, stats = _conv3x3_apply(x, weight, passes, bool(passes[0]))
+    y, stats = _conv3x3_apply(x, weight, passes, bool(passes[0]), gx_slot)
     return y, (stats if stats.shape[1] > 0 else None)
 
 
@@ -1176,29 +1196,54 @@ def _epilogue_stats_pay(kind, conv, x) -> bool:
     return hit
 
 
-def conv_nobias_stats(conv: nn.Conv2d, x, bn: nn.BatchNorm2d):
+def conv_nobias_stats(conv: nn.Conv2d, x, bn: nn.BatchNorm2d, gx_slot=None):
     """(conv_nobias(conv, x), statistics) where the statistics are y's per-block
     BN sums from the conv's epilogue when `bn` normalises with batch statistics,
     the conv runs on a HIP kernel that emits them (conv3x3 / convbf) and the
     BatchNorm consumes them without a merge launch (_epilogue_stats_pay), else
-    None (the BatchNorm then takes its own statistics pass)."""
+    None (the BatchNorm then takes its own statistics pass).  gx_slot: see
+    residual_grad_slot (only for a conv that slot accepts)."""
     if x.is_cuda and (bn.training or not bn.track_running_stats):
         passes = conv3x3_passes(conv, x)
         if passes is not None:
             if passes[0] and _epilogue_stats_pay("conv3x3", conv, x):
-                return conv3x3_stats(x, conv.weight, passes)
+                return conv3x3_stats(x, conv.weight, passes, gx_slot)
         elif convbf_ok(conv, x) and _epilogue_stats_pay("convbf", conv, x):
             return conv_bf16_stats(conv, x)
-    return conv_nobias(conv, x), None
+    return conv_nobias(conv, x, gx_slot), None
 
 
-def conv_nobias(conv: nn.Conv2d, x):
+RESIDUAL_SLOT = os.environ.get("MDE_RES_SLOT", "1") != "0"  # A/B switch
+
+
+def residual_grad_slot(conv: nn.Conv2d, x):
+    """A GradSlot for a block input x that feeds both `conv` (a BasicBlock's
+    first 3x3, DDRNet_23_slim.py:61-64) and the residual add of the block's
+    last BatchNorm (:66-70), when conv's data gradient runs on the Winograd
+    kernel in fp32: the BN backward puts the residual's gradient there and
+    the Winograd data gradient adds it in its epilogue (mde_wino_conv_acc),
+    so autograd's separate accumulation add (3 passes over x) disappears.
+    None otherwise -- then nothing changes (a slot is only handed out where
+    the conv is certain to take it: conv_nobias(_stats) routes such a conv to
+    _Conv3x3)."""
+    if not (RESIDUAL_SLOT and torch.is_grad_enabled() and x.is_cuda and x.requires_grad
+            and x.dtype == torch.float32 and not _autocast_bf16(x)):
+        return None
+    passes = conv3x3_passes(conv, x)
+    if passes is None or passes[1] != WINO:
+        return None
+    return GradSlot()
+
+
+def conv_nobias(conv: nn.Conv2d, x, gx_slot=None):
     """conv(x) without its bias (folded into the following BN, or absent): the
     HIP 3x3 / stride-2 / 1x1 kernels where they apply (under bf16 autocast:
     the 16 / 32-channel bf16 3x3 kernels, then convbf.hip), else MIOpen."""
     passes = conv3x3_passes(conv, x) if x.is_cuda else None
     if passes is not None:
-        return conv3x3(x, conv.weight, passes)
+        return conv3x3(x, conv.weight, passes, gx_slot)
+    if gx_slot is not None:
+        raise RuntimeError("conv_nobias: a gradient slot for a conv off the HIP conv3x3 route")
     if convbf_ok(conv, x):
         return conv_bf16(conv, x)
     if conv3x3s2_ok(conv, x):
@@ -1462,8 +1507,13 @@ class BatchNorm2d(nn.BatchNorm2d):
             raise ValueError(f"act must be one of {sorted(_ACTS)}")
         self.act = act
 
-    def forward(self, x, residual=None, prebias=None, stats=None):
-        return batch_norm_act(x, self, self.act, residual, prebias, stats)
+    def forward(self, x, residual=None, prebias=None, stats=None, act=None, res_slot=None):
+        """act overrides the module's activation for this call (a caller that
+        applies the reference's following ReLU in this pass, e.g. DualResNet's
+        `self.relu(x)` of an output nothing else reads); res_slot: see
+        batch_norm_act."""
+        return batch_norm_act(x, self, self.act if act is None else act, residual, prebias, stats,
+                              res_slot)
 
     def extra_repr(self):
         return super().extra_repr() + f", act={self.act}"

@@ -100,9 +100,10 @@ def test_graph_resume_from_eager_checkpoint(tmp_path):
     """--graph --cp 1 from a checkpoint the eager trainer wrote (fused,
     non-capturable Adam state): GraphTrainer's Adam must stay capturable after
     load_state_dict (the capture happens on its third step) and the resumed
-    graph run must continue exactly like the resumed EAGER run without the
-    eval-mode quirk (the graph path keeps BN in train mode), under MIOpen's
-    deterministic solvers, to 1e-5.  Against the oracle: the first step (no
+    graph run must continue exactly like the resumed EAGER run, without the
+    eval-mode quirk and with it (round 6: the graph path replays an eval-mode
+    step graph after step 0), under MIOpen's deterministic solvers, to 1e-5.
+    Against the oracle (quirk off): the first step (no
     update yet) to 1e-4; later steps of this 64x96 train-mode net drift by up
     to a few 1e-3 between devices (BN over 1x2 maps at the bottom of DDRNet,
     amplified by Adam's normalised steps), so the epoch average is checked at
@@ -114,17 +115,27 @@ def test_graph_resume_from_eager_checkpoint(tmp_path):
         ck = str(tmp_path / "global_checkpoint.pth")
         main(ARGS + ["--epochs", "1", "--checkpoint", ck])
         state = torch.load(ck, map_location="cpu", weights_only=True)
-        ck2 = str(tmp_path / "copy.pth")
-        torch.save(state, ck2)  # the eager resume overwrites its checkpoint at epoch end
+        copies = []
+        for i in range(3):  # each resume overwrites its checkpoint at epoch end
+            copies.append(str(tmp_path / f"copy{i}.pth"))
+            torch.save(state, copies[-1])
         main(ARGS + ["--epochs", "1", "--cp", "1", "--no-eval-quirk", "--checkpoint", ck,
                      "--log", str(tmp_path / "e.jsonl")])
-        main(ARGS + ["--epochs", "1", "--cp", "1", "--graph", "--checkpoint", ck2,
-                     "--log", str(tmp_path / "g.jsonl")])
+        main(ARGS + ["--epochs", "1", "--cp", "1", "--graph", "--no-eval-quirk", "--checkpoint",
+                     copies[0], "--log", str(tmp_path / "g.jsonl")])
+        main(ARGS + ["--epochs", "1", "--cp", "1", "--checkpoint", copies[1],
+                     "--log", str(tmp_path / "eq.jsonl")])
+        main(ARGS + ["--epochs", "1", "--cp", "1", "--graph", "--checkpoint", copies[2],
+                     "--log", str(tmp_path / "gq.jsonl")])
     finally:
         torch.backends.cudnn.deterministic = old
     eager = [r["value"] for r in _losses(tmp_path / "e.jsonl")]
     graph = [r["value"] for r in _losses(tmp_path / "g.jsonl")]
     assert graph == pytest.approx(eager, rel=1e-5), (graph, eager)
+    eager_q = [r["value"] for r in _losses(tmp_path / "eq.jsonl")]
+    graph_q = [r["value"] for r in _losses(tmp_path / "gq.jsonl")]
+    assert graph_q == pytest.approx(eager_q, rel=1e-5), (graph_q, eager_q)
+    assert graph_q[0] == graph[0] and graph_q[1:] != graph[1:]  # the quirk changes steps 1..
     assert _avgs(tmp_path / "g.jsonl")[0]["value"] == pytest.approx(
         _avgs(tmp_path / "e.jsonl")[0]["value"], rel=1e-5)
     ref = og.GuideDepth()

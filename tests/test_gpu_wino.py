@@ -291,3 +291,33 @@ def test_wino_position_split_vs_float64(cin, cout, h, w, n):
     yd = y.double().cpu()
     mr = yd.mean((0, 2, 3))
     assert float((mean - mr).abs().max() / mr.abs().max()) <= 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(32, 32, 120, 160), (64, 64, 9, 40), (128, 64, 11, 30),
+                                          (64, 64, 60, 80)])
+def test_wino_conv_acc_is_conv_plus_add(cin, cout, h, w):
+    """mde_wino_conv_acc (the data gradient with the residual path's gradient
+    summed in the epilogue) == mde_wino_conv + add bitwise: one fp32 add per
+    element, as autograd's accumulation; ragged planes and both kernels."""
+    from monocular_depth_estimation_amd import _abi
+    n = 2
+    gen = torch.Generator(device=DEV).manual_seed(cin + w)
+    x = torch.rand((n, cin, h, w), device=DEV, generator=gen) - 0.5
+    wt = (torch.rand((cout, cin, 3, 3), device=DEV, generator=gen) - 0.5) * 0.1
+    add = torch.rand((n, cout, h, w), device=DEV, generator=gen) - 0.5
+    st = _abi.stream_of(x)
+    u = torch.empty(16 * cin * cout, device=DEV)
+    _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), cin, cout, 0, st)
+    prev = _abi.query("mde_wino_mode", -1)
+    try:
+        for mode in (2, 0, 1, 6):
+            _abi.query("mde_wino_mode", mode)
+            y = torch.empty((n, cout, h, w), device=DEV)
+            ya = torch.full_like(y, float("nan"))
+            _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y), n, cin, cout, h, w, 1,
+                      0, st)
+            _abi.call("mde_wino_conv_acc", _abi.ptr(x), _abi.ptr(u), _abi.ptr(add), _abi.ptr(ya), n,
+                      cin, cout, h, w, 1, 0, st)
+            assert torch.equal(ya, add + y), mode
+    finally:
+        _abi.query("mde_wino_mode", prev)

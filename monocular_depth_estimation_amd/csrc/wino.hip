@@ -102,18 +102,22 @@ __device__ __forceinline__ int64_t u_offset(int co, int ci, int nchunks) {
 // segments, and the texture addresser ran ~79 % busy at 32 channels).  FLIP: the data-gradient filter
 // g'[co' = ci][ci' = co] = rot180(g[co][ci]) (co_n / ci_n are the output /
 // input channels of the conv being RUN, i.e. swapped for FLIP).
+// co_p / ci_p: the padded extents of U (wino_pad_*): padded rows are zeros.
 template <bool FLIP>
 __global__ void __launch_bounds__(256)
-    wino_weight_kernel(const float* __restrict__ g, float* __restrict__ U, int co_n, int ci_n) {
+    wino_weight_kernel(const float* __restrict__ g, float* __restrict__ U, int co_n, int ci_n,
+                       int co_p, int ci_p) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)co_n * ci_n) return;
-  const int co = (int)(t / ci_n), ci = (int)(t % ci_n);
+  if (t >= (int64_t)co_p * ci_p) return;
+  const int co = (int)(t / ci_p), ci = (int)(t % ci_p);
   float w[3][3];
+  const bool real = co < co_n && ci < ci_n;
   const float* src = FLIP ? g + ((int64_t)ci * co_n + co) * 9 : g + ((int64_t)co * ci_n + ci) * 9;
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int c = 0; c < 3; ++c) w[r][c] = FLIP ? src[(2 - r) * 3 + (2 - c)] : src[r * 3 + c];
+    for (int c = 0; c < 3; ++c)
+      w[r][c] = !real ? 0.f : FLIP ? src[(2 - r) * 3 + (2 - c)] : src[r * 3 + c];
   // G w: rows (w0, (w0+w1+w2)/2, (w0-w1+w2)/2, w2), then the same on columns
   float a[4][3];
 #pragma unroll
@@ -123,7 +127,7 @@ __global__ void __launch_bounds__(256)
     a[2][c] = 0.5f * ((w[0][c] - w[1][c]) + w[2][c]);
     a[3][c] = w[2][c];
   }
-  float* dst = U + u_offset(co, ci, ci_n / kCIC);
+  float* dst = U + u_offset(co, ci, ci_p / kCIC);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float u[4] = {a[r][0], 0.5f * ((a[r][0] + a[r][1]) + a[r][2]),
@@ -153,33 +157,38 @@ __device__ __forceinline__ void wino_g(const float (&w)[3][3], float (&u)[4][4])
   }
 }
 
+// Padded extents: U is (co_pu x ci_pu), U2 (ci_p2 x co_p2) = (padded cin as
+// output channels x padded cout as input chunks); a thread per (co, ci) of
+// the union, zeros outside the real filter.
 __global__ void __launch_bounds__(256)
     wino_weight2_kernel(const float* __restrict__ g, float* __restrict__ U,
-                        float* __restrict__ U2, int co_n, int ci_n) {
+                        float* __restrict__ U2, int co_n, int ci_n, int co_pu, int ci_pu,
+                        int ci_p2, int co_p2, int co_all, int ci_all) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)co_n * ci_n) return;
-  const int co = (int)(t / ci_n), ci = (int)(t % ci_n);
+  if (t >= (int64_t)co_all * ci_all) return;
+  const int co = (int)(t / ci_all), ci = (int)(t % ci_all);
+  const bool real = co < co_n && ci < ci_n;
   const float* src = g + ((int64_t)co * ci_n + ci) * 9;
   float w[3][3], wf[3][3], u[4][4];
 #pragma unroll
   for (int r = 0; r < 3; ++r)
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      w[r][c] = src[r * 3 + c];
+      w[r][c] = real ? src[r * 3 + c] : 0.f;
       wf[2 - r][2 - c] = w[r][c];
     }
   // forward: row co of the (co_n x ci_n) conv; flipped: row ci of (ci_n x co_n)
-  wino_g(w, u);
-  {
-    float* dst = U + u_offset(co, ci, ci_n / kCIC);
+  if (co < co_pu && ci < ci_pu) {
+    wino_g(w, u);
+    float* dst = U + u_offset(co, ci, ci_pu / kCIC);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[r][c];
   }
-  wino_g(wf, u);
-  {
-    float* dst = U2 + u_offset(ci, co, co_n / kCIC);
+  if (ci < ci_p2 && co < co_p2) {
+    wino_g(wf, u);
+    float* dst = U2 + u_offset(ci, co, co_p2 / kCIC);
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -198,7 +207,8 @@ template <int CO_B, int TCB, bool STATS = false, bool BPRE = false>
 __global__ void __launch_bounds__(256, 2)
     wino_f23_kernel(const float* __restrict__ x, const float* __restrict__ U, float* __restrict__ y,
                     int ci_n, int co_n, int h, int w, int bcols, int brows, int ncog, int total,
-                    float* __restrict__ stats, int xsplit, const float* __restrict__ add) {
+                    float* __restrict__ stats, int xsplit, const float* __restrict__ add,
+                    int nch) {
   constexpr int NTB = kTRB * TCB;      // tiles per block
   constexpr int NG = NTB / 16;         // 16-tile groups (MFMA N tiles)
   constexpr int WCO = CO_B / 16;       // waves along output channels
@@ -246,7 +256,7 @@ __global__ void __launch_bounds__(256, 2)
   const int nt0 = (wv / WCO) * NTW;
   const int64_t hw = (int64_t)h * w;
   const float* xb = x + (int64_t)img * ci_n * hw;
-  const int nchunks = ci_n / kCIC;
+  const int nchunks = nch;  // ci_n rounded up to 16 (its U rows past ci_n are zeros)
   const float* ua = U + ((int64_t)(co0 / 16) * nchunks * 16 * 64 + lane) * 4;
 
   // Input staging: per chunk, the block's 16 channels x 10 input rows x
@@ -279,7 +289,8 @@ __global__ void __launch_bounds__(256, 2)
       const int ch = e / (RR * RW2), rem = e - ch * (RR * RW2);
       const int r = rem / RW2, c2 = rem - r * RW2;
       const int gr = gr0 + r, gc = gc0 + 2 * c2;
-      const bool ok = e < RAW && gr >= 0 && gr < h && gc >= 0 && gc < w;
+      const bool ok = e < RAW && gr >= 0 && gr < h && gc >= 0 && gc < w &&
+                      chunk * kCIC + ch < ci_n;  // padded input channels read as zeros
       const int64_t off = ok ? (int64_t)(e < RAW ? ch : 0) * hw + (int64_t)gr * w + gc : 0;
       const float2 t = *reinterpret_cast<const float2*>(src + off);
       rv[k] = ok ? t : make_float2(0.f, 0.f);
@@ -426,7 +437,8 @@ __global__ void __launch_bounds__(256, 2)
         mde::sh_add(run[r], y11, ok1);
       }
       const int64_t yo = (int64_t)(co0 + 4 * kq + r) * hw + (int64_t)oy * w + ox;
-      store_tile(yb + yo, ab ? ab + yo : nullptr, oy, ox, h, w, y00, y01, y10, y11);
+      if (co0 + 4 * kq + r < co_n)  // padded output channels are not stored
+        store_tile(yb + yo, ab ? ab + yo : nullptr, oy, ox, h, w, y00, y01, y10, y11);
     }
   }
   if constexpr (STATS) {
@@ -450,7 +462,7 @@ __global__ void __launch_bounds__(256, 2)
       }
     }
     __syncthreads();
-    if (tid < CO_B) {
+    if (tid < CO_B && cog * CO_B + tid < co_n) {
       const int wc = tid / 16, c16 = tid % 16;  // channel set (wave % WCO), channel within
       mde::Sh a{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1035,16 +1047,30 @@ __global__ void __launch_bounds__(256, 2)
 
 struct WinoGeo {
   int bcols, brows, ncog, co_b;
+  int ci_p, co_p;  // padded channel counts (U's extents; padded rows / columns are zeros)
   int64_t total;
 };
 
+// Channel padding (round 6, the NewCRF projections the 32 / 16 alignment
+// rules sent to MIOpen: proj_x 24 -> 128 and 40 -> 256 and the data
+// gradients 128 -> 24, 256 -> 40, 512 -> 112; newcrf_layers.py:384-392):
+// input channels to a multiple of 16 (the chunk; the extra planes read as
+// zeros), output channels to a multiple of 32 (16 stays 16; the extra
+// channels are computed from zero filter rows and not stored).  Taken while
+// the padded product stays within 2x the real one.
+inline int wino_pad_ci(int64_t ci) { return (int)mde::cdiv(ci, kCIC) * kCIC; }
+inline int wino_pad_co(int64_t co) { return co == 16 ? 16 : (int)mde::cdiv(co, 32) * 32; }
+
 inline bool wino_geo(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WinoGeo* g) {
-  if (n <= 0 || ci < kCIC || ci % kCIC || co < 16 || (co != 16 && co % 32) || h < 1 || w < 2)
-    return false;
+  if (n <= 0 || ci < 1 || co < 1 || h < 1 || w < 2 || ci > 65536 || co > 65536) return false;
+  g->ci_p = wino_pad_ci(ci);
+  g->co_p = wino_pad_co(co);
+  if ((int64_t)g->ci_p * g->co_p > 2 * ci * co) return false;  // padding must not double the work
   if (w % 2) return false;  // float2 output stores at even offsets
-  if (n * ci * h * w >= ((int64_t)1 << 31) || n * co * h * w >= ((int64_t)1 << 31)) return false;
-  g->co_b = co % 64 == 0 ? 64 : (co == 16 ? 16 : 32);
-  g->ncog = (int)(co / g->co_b);
+  if (n * g->ci_p * h * w >= ((int64_t)1 << 31) || n * g->co_p * h * w >= ((int64_t)1 << 31))
+    return false;
+  g->co_b = g->co_p % 64 == 0 ? 64 : (g->co_p == 16 ? 16 : 32);
+  g->ncog = (int)(g->co_p / g->co_b);
   g->bcols = (int)mde::cdiv(w, g->co_b == 16 ? 32 : 16);
   g->brows = (int)mde::cdiv(h, 2 * kTRB);
   g->total = n * g->ncog * g->bcols * g->brows;
@@ -1154,25 +1180,33 @@ int mde_wino_mode(int mode) {
   return prev;
 }
 
+// U of the forward conv (cout x cin) and of its data gradient (cin x cout),
+// padded (wino_pad_*): the larger of the two, so one size serves both.
 size_t mde_wino_weight_bytes(int64_t cin, int64_t cout) {
-  return sizeof(float) * 16 * (size_t)cin * (size_t)cout;
+  if (cin < 1 || cout < 1) return 0;
+  const size_t f = (size_t)wino_pad_co(cout) * (size_t)wino_pad_ci(cin);
+  const size_t b = (size_t)wino_pad_co(cin) * (size_t)wino_pad_ci(cout);
+  return sizeof(float) * 16 * (f > b ? f : b);
 }
 
 // U from the [cout][cin][3][3] filter of the FORWARD conv; flip = 1 gives the
 // data-gradient transform (U' for the conv cout -> cin).
 int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, int flip,
                     void* stream) {
-  if (!weight || !u || cin < kCIC || cout < kCIC || cin % kCIC || cout % kCIC)
+  if (!weight || !u || cin < 1 || cout < 1 || cin > 65536 || cout > 65536)
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t pairs = cin * cout;
-  const dim3 grid((unsigned)mde::cdiv(pairs, 256));
+  // the run conv: cout -> cin for the data gradient
+  const int co_r = (int)(flip ? cin : cout), ci_r = (int)(flip ? cout : cin);
+  const int co_p = wino_pad_co(co_r), ci_p = wino_pad_ci(ci_r);
+  const dim3 grid((unsigned)mde::cdiv((int64_t)co_p * ci_p, 256));
   if (flip)
-    MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 16), s, wino_weight_kernel<true>, grid,
-               dim3(256), 0, weight, u, (int)cin, (int)cout);
+    MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * 9 + 64.0 * co_p * ci_p, s,
+               wino_weight_kernel<true>, grid, dim3(256), 0, weight, u, co_r, ci_r, co_p, ci_p);
   else
-    MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 16), s, wino_weight_kernel<false>, grid,
-               dim3(256), 0, weight, u, (int)cout, (int)cin);
+    MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * 9 + 64.0 * co_p * ci_p, s,
+               wino_weight_kernel<false>, grid, dim3(256), 0, weight, u, co_r, ci_r, co_p, ci_p);
   return MDE_OK;
 }
 
@@ -1180,13 +1214,18 @@ int mde_wino_weight(const float* weight, float* u, int64_t cin, int64_t cout, in
 // gradient (as mde_wino_weight with flip = 0 / 1).
 int mde_wino_weight2(const float* weight, float* u, float* u_flip, int64_t cin, int64_t cout,
                      void* stream) {
-  if (!weight || !u || !u_flip || cin < kCIC || cout < kCIC || cin % kCIC || cout % kCIC)
+  if (!weight || !u || !u_flip || cin < 1 || cout < 1 || cin > 65536 || cout > 65536)
     return MDE_ERR_INVALID_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int64_t pairs = cin * cout;
-  MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * pairs * (9 + 32), s, wino_weight2_kernel,
-             dim3((unsigned)mde::cdiv(pairs, 256)), dim3(256), 0, weight, u, u_flip, (int)cout,
-             (int)cin);
+  const int co_pu = wino_pad_co(cout), ci_pu = wino_pad_ci(cin);  // forward: cout x cin
+  const int ci_p2 = wino_pad_co(cin), co_p2 = wino_pad_ci(cout);  // data gradient: cin x cout
+  const int co_all = co_pu > co_p2 ? co_pu : co_p2, ci_all = ci_pu > ci_p2 ? ci_pu : ci_p2;
+  MDE_LAUNCH(mde::K_WINO_WEIGHT,
+             4.0 * pairs * 9 + 64.0 * ((double)co_pu * ci_pu + (double)ci_p2 * co_p2), s,
+             wino_weight2_kernel, dim3((unsigned)mde::cdiv((int64_t)co_all * ci_all, 256)),
+             dim3(256), 0, weight, u, u_flip, (int)cout, (int)cin, co_pu, ci_pu, ci_p2, co_p2,
+             co_all, ci_all);
   return MDE_OK;
 }
 
@@ -1212,9 +1251,11 @@ int wino_launch(const float* x, const float* u, float* y, float* stats, const fl
   // activations in and out, plus the transformed filter U once (the GEMMs'
   // other operand: at 1/32 scale it outweighs the planes)
   const double bytes = 4.0 * n * h * w * (double)(cin + cout) + 64.0 * (double)cin * cout;
-  const int xsplit = wino_xsplit(n, cin, cout, h, w, g);
+  const int xsplit = wino_xsplit(n, g.ci_p, g.co_p, h, w, g);
   const int kid = pass ? mde::K_WINO_DGRAD : mde::K_WINO_FWD;
-  if (xsplit == 1 && wino_persistent_ok(h, w)) {
+  // padded channels: the one-block kernel only (it masks the padded loads / stores)
+  const bool padded = g.ci_p != cin || g.co_p != cout;
+  if (xsplit == 1 && wino_persistent_ok(h, w) && !padded) {
     // persistent blocks: per XCD, its share of the items in runs of ipb
     const int per_xcd = (int)mde::cdiv(g.total, 8);
     int ipb = wino_ipb();
@@ -1244,7 +1285,7 @@ int wino_launch(const float* x, const float* u, float* y, float* stats, const fl
     return MDE_OK;
   }
   int64_t nblk = (g.total + 7) / 8 * 8;
-  if (xsplit == 1 && g.co_b == 32 && g_wino_x) {
+  if (xsplit == 1 && g.co_b == 32 && g_wino_x && !padded) {
     const dim3 grid((unsigned)nblk), block(256);
     if (stats)
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, wino_f23x_kernel<true>, grid, block, 0, x, u, y,
@@ -1266,11 +1307,11 @@ int wino_launch(const float* x, const float* u, float* y, float* stats, const fl
     if (g_wino_bpre)                                                                              \
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST, true>), grid, block, 0,  \
                       x, u, y, (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog,     \
-                      (int)g.total, stats, xsplit, add);                                          \
+                      (int)g.total, stats, xsplit, add, g.ci_p / kCIC);                           \
     else                                                                                          \
       MDE_LAUNCH_MFMA(kid, bytes, flops, s, (wino_f23_kernel<CB, TC, ST, false>), grid, block, 0, \
                       x, u, y, (int)cin, (int)cout, (int)h, (int)w, g.bcols, g.brows, g.ncog,     \
-                      (int)g.total, stats, xsplit, add);                                          \
+                      (int)g.total, stats, xsplit, add, g.ci_p / kCIC);                           \
   } while (0)
   if (stats) {
     if (g.co_b == 64)

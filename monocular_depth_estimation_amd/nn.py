@@ -417,14 +417,15 @@ class _Conv3x3(torch.autograd.Function):
         u_flip = None  # Winograd: the data gradient's filter transform, made with the forward's
         if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip), + the BN statistics
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
-            u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+            ub = _abi.query("mde_wino_weight_bytes", cin, cout) // 4  # padded channels included
+            u = torch.empty(ub, dtype=torch.float32, device=x.device)
             st = _abi.stream_of(x)
             if want_stats:
                 nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
                 stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
             if passes[1] == WINO and ctx.needs_input_grad[0]:
                 # the data gradient's flipped transform too, in the same launch
-                u_flip = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+                u_flip = torch.empty(ub, dtype=torch.float32, device=x.device)
                 _abi.call("mde_wino_weight2", _abi.ptr(weight), _abi.ptr(u), _abi.ptr(u_flip), cin,
                           cout, st)
             else:
@@ -475,7 +476,8 @@ class _Conv3x3(torch.autograd.Function):
                 gx = torch.empty_like(x)
                 u = ctx.u_flip
                 if u is None:
-                    u = torch.empty(16 * cin * cout, dtype=torch.float32, device=x.device)
+                    u = torch.empty(_abi.query("mde_wino_weight_bytes", cin, cout) // 4,
+                                    dtype=torch.float32, device=x.device)
                     _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 1, st)
                 if g2 is not None and g2.dtype == gy.dtype == torch.float32:
                     g2 = g2.contiguous()  # held until the launch is enqueued
@@ -788,10 +790,17 @@ def conv3x3_passes(conv: nn.Conv2d, x):
         # loses to the direct kernel: the input transform is amortised over
         # too few output channels, tools/wino_bench.py) on planes of >= 256
         # blocks (8 x 16 output pixels x 64 / 32 channels)
+        # (round 6) channel counts off the 16 / 32 grid too -- the NewCRF
+        # projections proj_x 24 -> 128, 40 -> 256 and the data gradients into
+        # 24 / 40 / 112 channels, newcrf_layers.py:384-392 -- with padded
+        # channels (wino.hip wino_geo: zero planes / filter rows, unstored
+        # outputs), where MIOpen's Winograd and its NHWC transposes ran
         n, h, w = x.shape[0], x.shape[2], x.shape[3]
         for i, (a, b) in enumerate(((cin, cout), (cout, cin))):
-            blocks = n * -(-h // 8) * -(-w // 16) * (b // (64 if b % 64 == 0 else 32))
-            if (not p[i] and b % (32 if WINO32 else 64) == 0 and blocks >= 256
+            bp = b if b == 16 else -(-b // 32) * 32  # output channels as padded
+            blocks = n * -(-h // 8) * -(-w // 16) * (bp // (64 if bp % 64 == 0 else 32))
+            aligned = b % (32 if WINO32 else 64) == 0 and a % 16 == 0
+            if (not p[i] and (aligned or (WINO_PAD and b > 16)) and blocks >= 256
                     and _abi.query("mde_wino_supported", a, b, h, w, _abi.MDE_F32)):
                 p[i] = WINO
     if dt == _abi.MDE_F32 and C3_WIDE and not _autocast_bf16(x):
@@ -810,6 +819,7 @@ WINO = 3  # conv3x3_passes flag: the pass runs on the Winograd kernel
 # 909.0 vs 881.0 / 878.3 img/s, profiles/r04_ab_wino.txt)
 WINO_ON = os.environ.get("MDE_WINO", "1") != "0"
 WINO32 = os.environ.get("MDE_WINO32", "1") != "0"  # the 32-channel output groups too (A/B)
+WINO_PAD = os.environ.get("MDE_WINO_PAD", "1") != "0"  # padded channel counts too (A/B)
 # Off by default: MIOpen's Winograd matches the stride-1 band kernel on these
 # shapes (tools/c1_bench.py) and the cfg2 step was 0.5 % slower with it on
 C3_WIDE = os.environ.get("MDE_C3_WIDE", "0") == "1"

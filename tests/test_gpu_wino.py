@@ -154,25 +154,40 @@ def test_wino_weight2_matches_both_transforms():
     """mde_wino_weight2 (the forward's U and the data gradient's flipped U' in
     one launch) == mde_wino_weight with flip 0 / 1, bitwise."""
     from monocular_depth_estimation_amd import _abi
-    for cin, cout in ((64, 128), (32, 32), (16, 48)):
+
+    def pad_co(c):
+        return 16 if c == 16 else -(-c // 32) * 32
+
+    def pad_ci(c):
+        return -(-c // 16) * 16
+
+    for cin, cout in ((64, 128), (32, 32), (16, 48), (24, 128), (112, 40)):
         wt = torch.rand((cout, cin, 3, 3), device=DEV) - 0.5
         st = _abi.stream_of(wt)
-        u0, u1 = (torch.empty(16 * cin * cout, device=DEV) for _ in range(2))
-        v0, v1 = (torch.full((16 * cin * cout,), float("nan"), device=DEV) for _ in range(2))
+        nb = _abi.query("mde_wino_weight_bytes", cin, cout) // 4
+        ef = 16 * pad_co(cout) * pad_ci(cin)  # the forward's padded U
+        eb = 16 * pad_co(cin) * pad_ci(cout)  # the data gradient's
+        assert nb == max(ef, eb)
+        u0, u1, v0, v1 = (torch.full((nb,), float("nan"), device=DEV) for _ in range(4))
         _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u0), cin, cout, 0, st)
         _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u1), cin, cout, 1, st)
         _abi.call("mde_wino_weight2", _abi.ptr(wt), _abi.ptr(v0), _abi.ptr(v1), cin, cout, st)
-        assert torch.equal(u0, v0) and torch.equal(u1, v1)
+        assert torch.equal(u0[:ef], v0[:ef]) and torch.equal(u1[:eb], v1[:eb])
+        assert torch.isfinite(v0[:ef]).all() and torch.isfinite(v1[:eb]).all()
+        if ef < nb:  # nothing written past the extent
+            assert torch.isnan(v0[ef:]).all()
+        if eb < nb:
+            assert torch.isnan(v1[eb:]).all()
 
 
 @pytest.mark.parametrize("cin,cout,h,w", [(160, 1024, 15, 20), (112, 512, 30, 40), (64, 128, 120, 160)])
 def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     """The NewCRF projections (newcrf_layers.py NewCRF.proj_x / proj_v: 3x3
     convs WITH a bias, cfg4 bs 16) through nn.Conv2d's biased HIP path: the
-    Winograd forward (and data gradient where cout -> cin is a Winograd shape;
-    112 input channels take MIOpen's), + bias, the weight gradient on the HIP
-    wide kernel (MIOpen's at 112 input channels); output and all three
-    gradients vs float64."""
+    Winograd forward and data gradient (112 output channels of the data
+    gradient padded to 128), + bias, the weight gradient on the HIP wide
+    kernel (MIOpen's at 112 input channels); output and all three gradients
+    vs float64."""
     from monocular_depth_estimation_amd.nn import WINO, Conv2d, conv3x3_passes
     n = 16
     g = torch.Generator().manual_seed(cin + cout + h)
@@ -189,7 +204,7 @@ def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     xg = x.to(DEV).requires_grad_(True)
     passes = conv3x3_passes(conv, xg)
     assert passes is not None and passes[0] == WINO, passes
-    assert (passes[1] == WINO) == (cin % 32 == 0), passes
+    assert passes[1] == WINO, passes  # 112 -> padded to 128 output channels since round 6
     # the weight gradient on the NCHW HIP wide kernel where cin % 32 == 0
     # (MDE_WIDE_WGRAD), else MIOpen's: the mixed-pass biased conv
     assert bool(passes[2]) == (cin % 32 == 0), passes
@@ -321,3 +336,43 @@ def test_wino_conv_acc_is_conv_plus_add(cin, cout, h, w):
             assert torch.equal(ya, add + y), mode
     finally:
         _abi.query("mde_wino_mode", prev)
+
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(24, 128, 40, 48), (40, 256, 30, 40), (128, 24, 40, 48),
+                                          (256, 40, 30, 40), (512, 112, 15, 20), (24, 32, 9, 18),
+                                          (40, 64, 11, 30)])
+def test_wino_padded_channels_vs_float64(cin, cout, h, w):
+    """Channel counts off the 16 / 32 grid (the NewCRF proj_x convs 24 -> 128,
+    40 -> 256 and their data gradients 128 -> 24, 256 -> 40, 512 -> 112;
+    newcrf_layers.py:384-392): input channels padded to 16 (zero planes),
+    output channels to 32 (zero filter rows, not stored) -- y vs float64 at
+    1e-5 of max, the output tensor untouched past its real channels (the
+    buffer is exactly [n, cout, h, w]: a stray padded store would land in the
+    guard region after it), the statistics records merge to y's mean."""
+    from monocular_depth_estimation_amd import _abi
+    n = 2
+    assert _abi.query("mde_wino_supported", cin, cout, h, w, 0) == 1
+    gen = torch.Generator().manual_seed(cin * 3 + cout + h)
+    x = torch.rand((n, cin, h, w), generator=gen) - 0.3
+    wt = (torch.rand((cout, cin, 3, 3), generator=gen) - 0.5) * 0.1
+    yr = torch.nn.functional.conv2d(x.double(), wt.double(), None, 1, 1)
+    xd, wd = x.to(DEV), wt.to(DEV)
+    st = _abi.stream_of(xd)
+    u = torch.empty(_abi.query("mde_wino_weight_bytes", cin, cout) // 4, device=DEV)
+    _abi.call("mde_wino_weight", _abi.ptr(wd), _abi.ptr(u), cin, cout, 0, st)
+    guard = 4096
+    buf = torch.full((n * cout * h * w + guard,), float("nan"), device=DEV)
+    y = buf[:n * cout * h * w].view(n, cout, h, w)
+    nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
+    stats = torch.full((cout, nb, 4), float("nan"), device=DEV)
+    _abi.call("mde_wino_conv_stats", _abi.ptr(xd), _abi.ptr(u), _abi.ptr(y), _abi.ptr(stats), n, cin,
+              cout, h, w, 0, 0, st)
+    torch.cuda.synchronize()
+    assert rel_err(y, yr) <= 1e-5
+    assert torch.isnan(buf[n * cout * h * w:]).all()
+    s = stats.double().cpu()
+    ref, cnt, s1 = s[..., 0], s[..., 1], s[..., 2]
+    mean = (s1 + cnt * ref).sum(1) / cnt.sum(1)
+    mr = y.double().cpu().mean((0, 2, 3))
+    assert float((mean - mr).abs().max() / mr.abs().max()) <= 1e-5

@@ -127,7 +127,7 @@ def run():
         mf = lambda: torch.nn.functional.conv2d(x, wt, None, 1, 1)
         md = lambda: torch.ops.aten.convolution_backward(gy, x, wt, None, (1, 1), (1, 1), (1, 1),
                                                          False, (0, 0), 1, (True, False, False))
-        u = torch.empty(16 * ci * co, device="cuda")
+        u = torch.empty(_abi.query("mde_wino_weight_bytes", ci, co) // 4, device="cuda")
         yw = torch.empty_like(y)
         gxw = torch.empty_like(gx)
 
@@ -169,7 +169,7 @@ def run():
         gy = torch.rand((n, co, h, w), device="cuda") - 0.5
         y, yw = torch.empty_like(gy), torch.empty_like(gy)
         gx, gxw = torch.empty_like(x), torch.empty_like(x)
-        u = torch.empty(16 * ci * co, device="cuda")
+        u = torch.empty(_abi.query("mde_wino_weight_bytes", ci, co) // 4, device="cuda")
         st = _abi.stream_of(x)
         fl = 2.0 * 9 * n * h * w * ci * co
 

@@ -39,7 +39,7 @@ def main():
             x = torch.rand((n, ci, h, w), device="cuda") - 0.5
             wt = (torch.rand((co, ci, 3, 3), device="cuda") - 0.5) * 0.1
             y = torch.empty((n, co, h, w), device="cuda")
-            u = torch.empty(16 * ci * co, device="cuda")
+            u = torch.empty(_abi.query("mde_wino_weight_bytes", ci, co) // 4, device="cuda")
             st = _abi.stream_of(x)
             _abi.call("mde_wino_weight", _abi.ptr(wt), _abi.ptr(u), ci, co, 0, st)
             f = lambda: _abi.call("mde_wino_conv", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y), n, ci, co, h,

@@ -45,7 +45,7 @@ MFMA_BF16_PEAK_TFS = 16 * MFMA_F32_PEAK_TFS  # bf16 MFMA dense peak (~2.5 PF, 16
 # step say nothing about its bytes in the bf16 or the NewCRF step.
 def pmc_files(workload: str, amp: str) -> list[str]:
     tag = f"{workload}_{amp}"
-    files = [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic_{tag}.json") for r in (5, 4, 3)]
+    files = [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic_{tag}.json") for r in (6, 5, 4, 3)]
     if tag == "guidedepth_fp32":  # rounds 1-2 profiled the cfg2 fp32 step only
         files += [os.path.join(REPO, "profiles", f"r0{r}_pmc_traffic.json") for r in (2, 1)]
     return files

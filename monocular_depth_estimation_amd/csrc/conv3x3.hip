@@ -2612,6 +2612,7 @@ int mde_conv3x3_stats_blocks(int64_t n, int64_t cin, int64_t cout, int64_t h, in
   if (cin == 3 && cout == 16) return fwd_grid<3, 16, 2, false, true>(n, h, w, &a, &b, &c);
   if (cin == 3 && cout == 32) return fwd_grid<3, 32, 1, false, true>(n, h, w, &a, &b, &c);
   if (cin == 3 && cout == 64) return fwd_grid<3, 64, 1, false, true>(n, h, w, &a, &b, &c);
+  if (cin == 16 && variant() == 1) return fwd_grid<16, 16, 2, false, true>(n, h, w, &a, &b, &c);
   if (cin == 16) return fwd_grid<16, 16, 1, false, true>(n, h, w, &a, &b, &c);
   return fwd_grid<32, 32, 1, false, true>(n, h, w, &a, &b, &c);
 }
@@ -2645,6 +2646,8 @@ int mde_conv3x3_fwd_stats(const void* x, const float* weight, void* y, float* st
     return launch_fwd<3, 32, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
   if (cin == 3 && cout == 64)
     return launch_fwd<3, 64, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
+  if (cin == 16 && variant() == 1)
+    return launch_fwd<16, 16, 2, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
   if (cin == 16)
     return launch_fwd<16, 16, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);
   return launch_fwd<32, 32, 1, false, true>(in, weight, out, n, h, w, bytes, k, s, stats);

@@ -42,8 +42,12 @@ def main():
                                      _abi.ptr(stf), n, ci, co, h, w, 0, st)
             b16 = lambda: _abi.call("mde_conv3x3_guide_bf16_fwd", _abi.ptr(x), _abi.ptr(wt),
                                     _abi.ptr(yb), _abi.ptr(stats), n, co, h, w, st)
+            f32d = lambda: _abi.call("mde_conv3x3_bwd_data", _abi.ptr(y), _abi.ptr(wt), _abi.ptr(x), n,
+                                     ci, co, h, w, 0, st)
             runs = (("fp32", f32, 4), ("fp32+stats", f32s, 4), ("bf16+stats", b16, 2))
-            for name, f, ob in (runs[:2] if a.cin16 else runs):
+            if a.cin16:
+                runs = runs[:2] + (("fp32 dgrad", f32d, 4),)
+            for name, f, ob in runs:
                 if a.reps:
                     for _ in range(a.reps):
                         f()

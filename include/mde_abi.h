@@ -686,6 +686,16 @@ int mde_wino_conv(const float* x, const float* u, float* y, int64_t n, int64_t c
 int mde_wino_conv_acc(const float* x, const float* u, const float* add, float* y, int64_t n,
                       int64_t cin, int64_t cout, int64_t h, int64_t w, int pass, int dtype,
                       void* stream);
+/* Every Winograd filter transform of a forward in one launch (the per-conv
+ * mde_wino_weight2 launches of a step, one table): table [rows][8] int64 on
+ * the device, row = {weight ptr, u ptr, u_flip ptr (0: none), cin, cout,
+ * first block, 0, 0} of a FORWARD conv (cout x cin), first block = the sum of
+ * mde_wino_weight_blocks(cin, cout, u_flip != 0) over earlier rows; blocks =
+ * that sum over all rows; pairs = sum of cin x cout (accounting only).  The
+ * same values as mde_wino_weight2 / mde_wino_weight. */
+int64_t mde_wino_weight_blocks(int64_t cin, int64_t cout, int both);
+int mde_wino_weight_table(const int64_t* table, int rows, int64_t blocks, int64_t pairs,
+                          void* stream);
 /* The same with the following BatchNorm's statistics of y from the epilogue
  * (stats [cout][mde_wino_stats_blocks][4] = (shift, count, s1, s2), the format
  * of mde_batchnorm_fwd_train_stats; NULL stats = mde_wino_conv). */

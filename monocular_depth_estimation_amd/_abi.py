@@ -151,6 +151,8 @@ SIGNATURES = {
     "mde_wino_weight_bytes": (_sz, [_i64, _i64]),
     "mde_wino_weight": (_int, [_vp, _vp, _i64, _i64, _int, _vp]),
     "mde_wino_weight2": (_int, [_vp, _vp, _vp, _i64, _i64, _vp]),
+    "mde_wino_weight_blocks": (_i64, [_i64, _i64, _int]),
+    "mde_wino_weight_table": (_int, [_vp, _int, _i64, _i64, _vp]),
     "mde_wino_conv": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_wino_conv_acc": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),
     "mde_wino_conv_stats": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int,

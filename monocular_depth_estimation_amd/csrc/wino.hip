@@ -46,6 +46,10 @@ __device__ __forceinline__ f4 mfma(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// wino_pad_ci / wino_pad_co (below) for device code
+__device__ __forceinline__ int wino_pad_ci_d(int ci) { return (ci + kCIC - 1) / kCIC * kCIC; }
+__device__ __forceinline__ int wino_pad_co_d(int co) { return co == 16 ? 16 : (co + 31) / 32 * 32; }
+
 // One 2 x 2 output tile at dst (row pitch w), clipped to the plane.  add
 // (nullable): the same tile of a gradient this result is summed into -- the
 // data gradient's other half when the conv's input also feeds a residual add
@@ -187,6 +191,58 @@ __global__ void __launch_bounds__(256)
       for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[r][c];
   }
   if (ci < ci_p2 && co < co_p2) {
+    wino_g(wf, u);
+    float* dst = U2 + u_offset(ci, co, co_p2 / kCIC);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[r][c];
+  }
+}
+
+// Every Winograd filter of a forward in ONE launch (mde_wino_weight_table):
+// table [rows][8] int64 = {weight, U, U' (0: none), cin, cout, first block,
+// 0, 0} of each forward conv (cout x cin), blocks of 256 (co, ci) pairs over
+// the union of both padded transforms, as wino_weight2_kernel (same values).
+__global__ void __launch_bounds__(256)
+    wino_weight_table_kernel(const int64_t* __restrict__ tab, int rows) {
+  const int64_t b = blockIdx.x;
+  int lo = 0, hi = rows - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[(int64_t)mid * 8 + 5] <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const int64_t* t = tab + (int64_t)lo * 8;
+  const float* g = reinterpret_cast<const float*>(t[0]);
+  float* U = reinterpret_cast<float*>(t[1]);
+  float* U2 = reinterpret_cast<float*>(t[2]);
+  const int ci_n = (int)t[3], co_n = (int)t[4];
+  const int co_pu = wino_pad_co_d(co_n), ci_pu = wino_pad_ci_d(ci_n);
+  const int ci_p2 = U2 ? wino_pad_co_d(ci_n) : 0, co_p2 = U2 ? wino_pad_ci_d(co_n) : 0;
+  const int co_all = co_pu > co_p2 ? co_pu : co_p2, ci_all = ci_pu > ci_p2 ? ci_pu : ci_p2;
+  const int64_t e = (b - t[5]) * 256 + threadIdx.x;
+  if (e >= (int64_t)co_all * ci_all) return;
+  const int co = (int)(e / ci_all), ci = (int)(e % ci_all);
+  const bool real = co < co_n && ci < ci_n;
+  const float* src = g + ((int64_t)co * ci_n + ci) * 9;
+  float w[3][3], wf[3][3], u[4][4];
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      w[r][c] = real ? src[r * 3 + c] : 0.f;
+      wf[2 - r][2 - c] = w[r][c];
+    }
+  if (co < co_pu && ci < ci_pu) {
+    wino_g(w, u);
+    float* dst = U + u_offset(co, ci, ci_pu / kCIC);
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[(4 * r + c) * 256] = u[r][c];
+  }
+  if (U2 && ci < ci_p2 && co < co_p2) {
     wino_g(wf, u);
     float* dst = U2 + u_offset(ci, co, co_p2 / kCIC);
 #pragma unroll
@@ -1226,6 +1282,24 @@ int mde_wino_weight2(const float* weight, float* u, float* u_flip, int64_t cin, 
              wino_weight2_kernel, dim3((unsigned)mde::cdiv((int64_t)co_all * ci_all, 256)),
              dim3(256), 0, weight, u, u_flip, (int)cout, (int)cin, co_pu, ci_pu, ci_p2, co_p2,
              co_all, ci_all);
+  return MDE_OK;
+}
+
+// the 256-pair blocks of one table row (mde_wino_weight_table)
+int64_t mde_wino_weight_blocks(int64_t cin, int64_t cout, int both) {
+  if (cin < 1 || cout < 1 || cin > 65536 || cout > 65536) return 0;
+  const int64_t co_pu = wino_pad_co(cout), ci_pu = wino_pad_ci(cin);
+  const int64_t ci_p2 = both ? wino_pad_co(cin) : 0, co_p2 = both ? wino_pad_ci(cout) : 0;
+  const int64_t co_all = co_pu > co_p2 ? co_pu : co_p2, ci_all = ci_pu > ci_p2 ? ci_pu : ci_p2;
+  return mde::cdiv(co_all * ci_all, 256);
+}
+
+int mde_wino_weight_table(const int64_t* table, int rows, int64_t blocks, int64_t pairs,
+                          void* stream) {
+  if (!table || rows <= 0 || blocks <= 0 || blocks > 0x7fffffff || pairs < 0)
+    return MDE_ERR_INVALID_ARG;
+  MDE_LAUNCH(mde::K_WINO_WEIGHT, 4.0 * 9 * pairs + 128.0 * pairs, (hipStream_t)stream,
+             wino_weight_table_kernel, dim3((unsigned)blocks), dim3(256), 0, table, rows);
   return MDE_OK;
 }
 

@@ -408,6 +408,7 @@ class _Conv3x3(torch.autograd.Function):
     @staticmethod
     @_amp_fwd
     def forward(ctx, x, weight, passes, want_stats=False, gx_slot=None):
+        wkey = weight  # the Parameter: its Winograd transforms' key in the pack scope
         x = x.contiguous()
         weight = weight.contiguous()
         n, cin, h, w = x.shape
@@ -417,19 +418,27 @@ class _Conv3x3(torch.autograd.Function):
         u_flip = None  # Winograd: the data gradient's filter transform, made with the forward's
         if passes[0] == WINO:  # Winograd F(2x2, 3x3) (wino.hip), + the BN statistics
             y = torch.empty((n, cout, h, w), dtype=x.dtype, device=x.device)
-            ub = _abi.query("mde_wino_weight_bytes", cin, cout) // 4  # padded channels included
-            u = torch.empty(ub, dtype=torch.float32, device=x.device)
             st = _abi.stream_of(x)
             if want_stats:
                 nb = _abi.query("mde_wino_stats_blocks", n, cin, cout, h, w)
                 stats = torch.empty((cout, nb, 4), dtype=torch.float32, device=x.device)
-            if passes[1] == WINO and ctx.needs_input_grad[0]:
-                # the data gradient's flipped transform too, in the same launch
-                u_flip = torch.empty(ub, dtype=torch.float32, device=x.device)
-                _abi.call("mde_wino_weight2", _abi.ptr(weight), _abi.ptr(u), _abi.ptr(u_flip), cin,
-                          cout, st)
+            flip = passes[1] == WINO  # the data gradient's flipped transform too
+            sc = _ACTIVE_PACK
+            ent = sc.wino.get(wkey) if sc is not None else None
+            if ent is not None and wkey in sc.wino_packed and (ent[1] is not None or not flip):
+                u, u_flip = ent[0], (ent[1] if flip else None)  # made by the scope's table launch
             else:
-                _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 0, st)
+                ub = _abi.query("mde_wino_weight_bytes", cin, cout) // 4  # padded channels included
+                u = torch.empty(ub, dtype=torch.float32, device=x.device)
+                if flip:  # both transforms in one launch
+                    u_flip = torch.empty(ub, dtype=torch.float32, device=x.device)
+                    _abi.call("mde_wino_weight2", _abi.ptr(weight), _abi.ptr(u), _abi.ptr(u_flip),
+                              cin, cout, st)
+                else:
+                    _abi.call("mde_wino_weight", _abi.ptr(weight), _abi.ptr(u), cin, cout, 0, st)
+                if (sc is not None and ent is None and isinstance(wkey, nn.Parameter)
+                        and not torch.cuda.is_current_stream_capturing()):
+                    sc.wino[wkey] = (u, u_flip, cin, cout)  # in the table from the next forward
             _abi.call("mde_wino_conv_stats", _abi.ptr(x), _abi.ptr(u), _abi.ptr(y),
                       _abi.ptr(stats) if want_stats else None, n, cin, cout, h, w, 0,
                       _abi.dtype_code(x), st)
@@ -843,6 +852,16 @@ class _PackScope:
         self.blocks = 0
         self.elems = 0
         self.packed = frozenset()  # weights packed by this forward's table launch
+        # the fp32 Winograd convs' filter transforms (wino.hip), the same way:
+        # weight -> (U, U' or None, cin, cout), one mde_wino_weight_table launch
+        # (the per-conv mde_wino_weight2 launches: 27 a cfg2 step)
+        self.wino = {}
+        self.wtable = None
+        self.wrows = []
+        self.wptrs = ()
+        self.wblocks = 0
+        self.wpairs = 0
+        self.wino_packed = frozenset()
 
     def _ptrs(self):
         return tuple(w.data_ptr() for w in self.entries)
@@ -865,16 +884,34 @@ class _PackScope:
         self.table = torch.tensor(rows, dtype=torch.int64, device=device)
         self.rows, self.ptrs, self.blocks, self.elems = list(self.entries), ptrs, blk, elems
 
+    def refresh_wino(self, device):
+        """The Winograd table (rows: weight, U, U' or 0, cin, cout, first block)."""
+        ptrs = tuple(w.data_ptr() for w in self.wino)
+        if self.wtable is not None and ptrs == self.wptrs:
+            return
+        rows, blk, pairs = [], 0, 0
+        for wgt, (u, uf, cin, cout) in self.wino.items():
+            rows.append([wgt.data_ptr(), u.data_ptr(), uf.data_ptr() if uf is not None else 0,
+                         cin, cout, blk, 0, 0])
+            blk += _abi.query("mde_wino_weight_blocks", cin, cout, int(uf is not None))
+            pairs += cin * cout
+        if self.wtable is not None:
+            self.retired.append(self.wtable)  # a captured graph may still read it
+        self.wtable = torch.tensor(rows, dtype=torch.int64, device=device)
+        self.wrows, self.wptrs, self.wblocks, self.wpairs = list(self.wino), ptrs, blk, pairs
+
 
 CONVBF_PACK_ALL = os.environ.get("MDE_CONVBF_PACK_ALL", "1") != "0"  # A/B: 0 = a pack per conv
+WINO_TABLE = os.environ.get("MDE_WINO_TABLE", "1") != "0"  # A/B: 0 = a transform launch per conv
 _ACTIVE_PACK = None
 
 
 @contextlib.contextmanager
 def convbf_pack_scope(owner: nn.Module, device):
     """Run `owner`'s forward with its registered convbf filters packed by one
-    launch at entry (see _PackScope); a no-op off the GPU, with
-    MDE_CONVBF_PACK_ALL=0, or when the bf16 convs are off."""
+    launch at entry, and its registered fp32 Winograd filter transforms made
+    by one more (see _PackScope); a no-op off the GPU or with
+    MDE_CONVBF_PACK_ALL=0 (MDE_WINO_TABLE=0: the Winograd launch per conv)."""
     global _ACTIVE_PACK
     if not (CONVBF_PACK_ALL and device.type == "cuda" and _ACTIVE_PACK is None):
         yield
@@ -882,13 +919,21 @@ def convbf_pack_scope(owner: nn.Module, device):
     sc = owner.__dict__.get("_convbf_pack")
     if sc is None:
         sc = owner.__dict__["_convbf_pack"] = _PackScope()
-    if sc.entries and not torch.cuda.is_current_stream_capturing():
+    capturing = torch.cuda.is_current_stream_capturing()
+    if sc.entries and not capturing:
         sc.refresh(device)
+    if sc.wino and not capturing:
+        sc.refresh_wino(device)
     sc.packed = frozenset()
+    sc.wino_packed = frozenset()
     if sc.table is not None:
         _abi.call("mde_convbf_pack_table", _abi.ptr(sc.table), len(sc.rows), sc.blocks, sc.elems,
                   _abi.stream_of(sc.table))
         sc.packed = frozenset(sc.rows)
+    if sc.wtable is not None and WINO_TABLE:
+        _abi.call("mde_wino_weight_table", _abi.ptr(sc.wtable), len(sc.wrows), sc.wblocks,
+                  sc.wpairs, _abi.stream_of(sc.wtable))
+        sc.wino_packed = frozenset(sc.wrows)
     _ACTIVE_PACK = sc
     try:
         yield

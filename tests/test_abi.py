@@ -18,7 +18,7 @@ def declared_functions():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     decls = {}
-    for m in re.finditer(r"\b(?:int|size_t|double|const char\*)\s+(mde_\w+)\s*\(([^)]*)\)\s*;", text):
+    for m in re.finditer(r"\b(?:int64_t|int|size_t|double|const char\*)\s+(mde_\w+)\s*\(([^)]*)\)\s*;", text):
         args = m.group(2).strip()
         n = 0 if args in ("", "void") else args.count(",") + 1
         decls[m.group(1)] = n

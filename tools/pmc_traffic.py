@@ -122,6 +122,8 @@ NAMES = [
     (r"stem_bf16_wgrad_kernel|stem_wreduce_kernel<0>", "stem_wgrad_bf16"),
     (r"stem_wreduce_kernel<1>", "conv3x3_wgrad_guide"),
     (r"stem_wreduce_kernel\(", "stem_wgrad_bf16"),  # builds before the tag
+    (r"lin_wgrad_kernel", "linear_wgrad"),
+    (r"lin_wreduce_kernel", "linear_wreduce"),
     (r"eval_partial_kernel", "eval_sums"),
     (r"eval_final_kernel", "eval_final"),
     (r"nyu_augment_kernel", "nyu_augment"),

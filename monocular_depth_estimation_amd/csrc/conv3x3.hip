@@ -651,6 +651,7 @@ __device__ __forceinline__ int64_t gw_index(const ReduceMap& r, int grp, int e) 
   if (r.wide) {
     const int ngo = r.co_n / r.wide, col = e / 288, n = e % 288;
     const int co = (grp % ngo) * r.wide + col, ci = (grp / ngo) * 32 + n % 32;
+    if (ci >= r.ci_n) return -1;  // a padded input-channel group's zero rows
     return ((int64_t)co * r.ci_n + ci) * 9 + n / 32;
   }
   const int co = e / r.np, n = e % r.np, tap = n / r.cip, ci = n % r.cip;
@@ -1012,7 +1013,11 @@ struct WideT {
 // h, w: input sizes; ho, wo: gy sizes (= h, w at S = 1).
 // COG = 32 (the 32 -> 32 convs, WPB = 4): wave w = output-channel tile
 // w & 1 x the 9 N tiles of input-channel half w >> 1.
-template <int S, int SW, int TH, int WPB, int COG = kWCO>
+// PADC: ci_n not a multiple of 32 (the NewCRF projections' 24 / 40 / 112
+// input channels, newcrf_layers.py:384-392): the last group's channels past
+// ci_n are staged as zeros (never loaded) and their rows dropped by the
+// reduction (gw_index).
+template <int S, int SW, int TH, int WPB, int COG = kWCO, bool PADC = false>
 __global__ void __launch_bounds__(64 * WPB, COG == kWCO ? 2 : 3)
     conv3x3_wgrad_wide_fixed_kernel(const float* __restrict__ x, const float* __restrict__ gy,
                                     float* __restrict__ part, int ci_n, int co_n, int h, int w,
@@ -1054,6 +1059,7 @@ __global__ void __launch_bounds__(64 * WPB, COG == kWCO ? 2 : 3)
   for (int nt = 0; nt < NTW; ++nt) acc[nt] = f4{0.f, 0.f, 0.f, 0.f};
   const float* xg = x + ((int64_t)cig * kWCI + XC * wv) * hw;
   const float* gg = gy + ((int64_t)cog * COG + GC * wv) * hwo;
+  const int cval = ci_n - (cig * kWCI + XC * wv);  // this wave's real staged channels (PADC)
   float vx[XC][P::XL], vg[GC][P::GL];
   unsigned xm = 0, gm = 0;
   auto load = [&](int tile) {
@@ -1070,7 +1076,8 @@ __global__ void __launch_bounds__(64 * WPB, COG == kWCO ? 2 : 3)
       xm |= ok ? 1u << i : 0u;
       const int o = clampi(gr, 0, h - 1) * w + clampi(gc, 0, w - 1);
 #pragma unroll
-      for (int c = 0; c < XC; ++c) vx[c][i] = xi[(unsigned)(c * hw + o)];
+      for (int c = 0; c < XC; ++c)
+        vx[c][i] = !PADC || c < cval ? xi[(unsigned)(c * hw + o)] : 0.f;
     }
     gm = 0;
 #pragma unroll
@@ -1165,9 +1172,10 @@ struct WidePlan {
 };
 
 inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, WidePlan* p) {
-  if (ci % kWCI || co % kWCO || ci < kWCI || co < kWCO) return false;
+  if (co % kWCO || co < kWCO || ci < 16 || (ci % kWCI && ci % 8)) return false;
   if (!wide_geo(n, h, w, &p->g)) return false;
   p->fixed_sw = wide_fixed_sw(w);
+  if (ci % kWCI && !p->fixed_sw) return false;  // padded channels: the fixed-strip kernel only
   if (p->fixed_sw) {  // tiles of 80 / fixed_sw rows x fixed_sw columns
     const int th = 80 / p->fixed_sw, tw = (int)(w / p->fixed_sw);
     const int64_t tpi = mde::cdiv(h, th) * tw, nt = n * tpi;
@@ -1178,7 +1186,7 @@ inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, W
     p->g.tiles_per_img = (int)tpi;
     p->g.ntiles = (int)nt;
   }
-  p->groups = (int)((ci / kWCI) * (co / kWCO));
+  p->groups = (int)(mde::cdiv(ci, kWCI) * (co / kWCO));
   // one 100 KB-LDS block per CU (generic), two <= 80 KB blocks (fixed width)
   int gx = (p->fixed_sw ? wide_blocks(p->g.ntiles) : 256) / p->groups;
   if (gx < 1) gx = 1;
@@ -1204,9 +1212,15 @@ int launch_wgrad_wide(const float* x, const float* gy, float* gw, int64_t n, int
     const char* e = std::getenv("MDE_WIDE_WPB");
     return e ? std::atoi(e) : 8;
   }();
+  const bool padc = ci % kWCI != 0;
 #define MDE_WIDE_FIXED(WW, TT)                                                                  \
   do {                                                                                          \
-    if (wpb == 4)                                                                               \
+    if (padc)                                                                                   \
+      MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s,                                    \
+                      (conv3x3_wgrad_wide_fixed_kernel<1, WW, TT, 8, kWCO, true>), grid,        \
+                      dim3(512), 0, x, gy, ws, (int)ci, (int)co, (int)h, (int)w, (int)h,        \
+                      (int)w, tw, tpi, nt);                                                     \
+    else if (wpb == 4)                                                                          \
       MDE_LAUNCH_MFMA(mde::K_C3_WGRAD_WIDE, bytes, flops, s,                                         \
                       (conv3x3_wgrad_wide_fixed_kernel<1, WW, TT, 4>), grid, dim3(256), 0, x,   \
                       gy, ws, (int)ci, (int)co, (int)h, (int)w, (int)h, (int)w, tw, tpi, nt);   \
@@ -2490,6 +2504,12 @@ bool wide(int64_t cin, int64_t cout) {
   return cin > 0 && cout > 0 && cin % kWCI == 0 && cout % kWCO == 0;
 }
 
+// input channels padded to the next 32 (the fixed-strip widths only: the
+// workspace query returns 0 for other planes)
+bool wide_pad(int64_t cin, int64_t cout) {
+  return cin > 16 && cin % 8 == 0 && cin % kWCI != 0 && cout > 0 && cout % kWCO == 0;
+}
+
 bool supported(int64_t cin, int64_t cout, int pass) {
   const bool guide = cin == 3 && (cout == 16 || cout == 32 || cout == 64);
   const bool square = (cin == 16 && cout == 16) || (cin == 32 && cout == 32);
@@ -2499,7 +2519,7 @@ bool supported(int64_t cin, int64_t cout, int pass) {
     case kDgrad:
       return square;
     case kWgrad:
-      return guide || square || wide(cin, cout);
+      return guide || square || wide(cin, cout) || wide_pad(cin, cout);
     default:
       return false;
   }
@@ -2689,7 +2709,7 @@ size_t mde_conv3x3_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
     return wgrad_ws_bytes(1, p.grid, p.m);
   }
   if (!supported(cin, cout, kWgrad) || !dims_ok(n, h, w)) return 0;
-  if (wide(cin, cout)) {
+  if (wide(cin, cout) || wide_pad(cin, cout)) {
     WidePlan wp;
     return wide_plan(n, cin, cout, h, w, &wp) ? wide_workspace(wp) : 0;
   }
@@ -2731,7 +2751,8 @@ int mde_conv3x3_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   const float* g = (const float*)gy;
   float* ws = (float*)workspace;
   const double bytes = 4.0 * n * h * w * (double)(cin + cout);
-  if (wide(cin, cout)) return launch_wgrad_wide(xi, g, gweight, n, cin, cout, h, w, ws, s);
+  if (wide(cin, cout) || wide_pad(cin, cout))
+    return launch_wgrad_wide(xi, g, gweight, n, cin, cout, h, w, ws, s);
   if (cin == 3 && cout == 16) return launch_wgrad<3, 16, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3 && cout == 32) return launch_wgrad<3, 32, 8, 4>(xi, g, gweight, n, h, w, ws, bytes, s);
   if (cin == 3) return launch_wgrad<3, 64, 4, 4>(xi, g, gweight, n, h, w, ws, bytes, s);

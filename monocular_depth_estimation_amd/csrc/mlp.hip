@@ -355,10 +355,12 @@ bool wgrad_plan(int64_t t_rows, int64_t m, int64_t n, WgradPlan* p) {
     return false;
   p->tiles_n = (int)(n / kWT);
   p->tiles = (int)(m / kWT) * p->tiles_n;
-  // ~1024 blocks (up to 4 per CU), >= 32 chunks (512 tokens) per split
+  // ~512 blocks (2 per CU), >= 32 chunks (512 tokens) per split: fewer,
+  // longer splits beat 768 / 1024 blocks (the partials' write + reduce pass
+  // grows with the split count; tools/lin_bench.py, profiles/r06_lin_wgrad.txt)
   static const int target = [] {
     const char* e = getenv("MDE_LIN_WGRAD_BLOCKS");
-    return e ? atoi(e) : 1024;
+    return e ? atoi(e) : 512;
   }();
   int64_t s = mde::cdiv(target, p->tiles);
   const int64_t smax = t_rows / 512 > 1 ? t_rows / 512 : 1;

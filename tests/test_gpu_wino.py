@@ -256,16 +256,17 @@ def test_wino_pack_scope_reuses_table_transforms():
     torch.testing.assert_close(y0, y1, rtol=1e-4, atol=1e-4)
 
 
-@pytest.mark.parametrize("cin,cout,h,w", [(160, 1024, 15, 20), (112, 512, 30, 40), (64, 128, 120, 160)])
-def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
+@pytest.mark.parametrize("cin,cout,h,w,n", [(160, 1024, 15, 20, 16), (112, 512, 30, 40, 16),
+                                            (64, 128, 120, 160, 16), (24, 128, 120, 160, 2),
+                                            (40, 256, 60, 80, 8)])
+def test_wino_biased_conv_newcrf_projections(cin, cout, h, w, n):
     """The NewCRF projections (newcrf_layers.py NewCRF.proj_x / proj_v: 3x3
     convs WITH a bias, cfg4 bs 16) through nn.Conv2d's biased HIP path: the
-    Winograd forward and data gradient (112 output channels of the data
-    gradient padded to 128), + bias, the weight gradient on the HIP wide
-    kernel (MIOpen's at 112 input channels); output and all three gradients
-    vs float64."""
+    Winograd forward and data gradient (24 / 40 / 112 channels padded to the
+    next 16 / 32), + bias, the weight gradient on the HIP wide kernel (24 / 40
+    / 112 input channels padded to the next 32 since round 6); output and all
+    three gradients vs float64."""
     from monocular_depth_estimation_amd.nn import WINO, Conv2d, conv3x3_passes
-    n = 16
     g = torch.Generator().manual_seed(cin + cout + h)
     x = torch.rand((n, cin, h, w), generator=g) - 0.5
     wt = (torch.rand((cout, cin, 3, 3), generator=g) - 0.5) * 0.05
@@ -281,9 +282,9 @@ def test_wino_biased_conv_newcrf_projections(cin, cout, h, w):
     passes = conv3x3_passes(conv, xg)
     assert passes is not None and passes[0] == WINO, passes
     assert passes[1] == WINO, passes  # 112 -> padded to 128 output channels since round 6
-    # the weight gradient on the NCHW HIP wide kernel where cin % 32 == 0
-    # (MDE_WIDE_WGRAD), else MIOpen's: the mixed-pass biased conv
-    assert bool(passes[2]) == (cin % 32 == 0), passes
+    # the weight gradient on the NCHW HIP wide kernel (MDE_WIDE_WGRAD; padded
+    # input channels: MDE_WIDE_PAD), the mixed-pass biased conv
+    assert bool(passes[2]), passes
     y = conv(xg)
     yr = torch.nn.functional.conv2d(x.double(), wt.double(), b.double(), 1, 1)
     assert rel_err(y, yr) <= 1e-5, "forward"

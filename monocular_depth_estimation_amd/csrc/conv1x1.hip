@@ -65,7 +65,10 @@ __device__ __forceinline__ int fdiv(int q, int d, float inv) {
 // SOUT = 2: output value of q goes to (2 r, 2 c) of an hout x wout plane
 // (wout even), zeros to (2r, 2c+1), (2r+1, 2c), (2r+1, 2c+1).
 // TRANSA: A[m][k] = wt[k * M + m] (the data gradient: W is [K = co][M = ci]).
-template <int BM, int BQ, int MT, int QT, int SIN, int SOUT, bool TRANSA>
+// PAD: K or M not a multiple of 32 (MobileNetV3's 16 / 24 / 40 / 72 / 80 /
+// 112 / 120 / 184 / 200 / 240 / 480-channel 1x1 convs, multiples of 8): loads
+// past K / M are zeros (never issued), rows past M are not stored.
+template <int BM, int BQ, int MT, int QT, int SIN, int SOUT, bool TRANSA, bool PAD = false>
 __global__ void __launch_bounds__(256)
     cm_kernel(const float* __restrict__ in, const float* __restrict__ wt, float* __restrict__ out,
               int K, int M, int hin, int win, int wo, int Q, int hout, int wout, int qtiles,
@@ -98,17 +101,24 @@ __global__ void __launch_bounds__(256)
       const int e = 4 * (tid + 256 * i);
       if constexpr (TRANSA) {
         const int k = e / BM, m = e % BM;
-        ra[i] = *reinterpret_cast<const float4*>(wt + (int64_t)(k0 + k) * M + m0 + m);
+        // (K, M multiples of 4: a float4 is all in or all out)
+        const bool ok = !PAD || (k0 + k < K && m0 + m < M);
+        const float4 t = *reinterpret_cast<const float4*>(wt + (ok ? (int64_t)(k0 + k) * M + m0 + m : 0));
+        ra[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
       } else {
         const int m = e / KC, k = e % KC;
-        ra[i] = *reinterpret_cast<const float4*>(wt + (int64_t)(m0 + m) * K + k0 + k);
+        const bool ok = !PAD || (k0 + k < K && m0 + m < M);
+        const float4 t = *reinterpret_cast<const float4*>(wt + (ok ? (int64_t)(m0 + m) * K + k0 + k : 0));
+        ra[i] = ok ? t : make_float4(0.f, 0.f, 0.f, 0.f);
       }
     }
 #pragma unroll
     for (int i = 0; i < BV; ++i) {
       const int e = 4 * (tid + 256 * i);
-      const int k = e / BQ, q = q0 + e % BQ;
-      const float* src = inb + (int64_t)(k0 + k) * hwin;
+      const int k = e / BQ, q0e = q0 + e % BQ;
+      const bool kok = !PAD || k0 + k < K;
+      const float* src = inb + (int64_t)(kok ? k0 + k : 0) * hwin;
+      const int q = kok ? q0e : Q;  // a channel past K: every element out of range (zeros)
       if constexpr (SIN == 1) {
         // Q % 4 == 0: a float4 is all in or all out; out-of-range loads a
         // real element (q = 0) and is zeroed at store time
@@ -118,7 +128,7 @@ __global__ void __launch_bounds__(256)
         float v[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int qq = q + j, r = fdiv(qq, wo, inv_wo), c = qq - r * wo;
+          const int qq = q + j, r = fdiv(qq < Q ? qq : 0, wo, inv_wo), c = (qq < Q ? qq : 0) - r * wo;
           const float t = src[qq < Q ? (int64_t)(2 * r) * win + 2 * c : 0];
           v[j] = qq < Q ? t : 0.f;
         }
@@ -198,6 +208,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * 32 * MT + 32 * x + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (PAD && m >= M) continue;
         float* dst = ob + (int64_t)m * hout * wout + po;
         if constexpr (SOUT == 1) {
           *dst = acc[x][y][r];
@@ -396,7 +407,8 @@ __global__ void __launch_bounds__(1024)
 // ------------------------------------------------------------------- plans
 inline bool c1_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, int stride) {
   if (n <= 0 || h <= 0 || w <= 0 || (stride != 1 && stride != 2)) return false;
-  if (ci % 32 || co % 32 || ci < 32 || co < 32) return false;
+  // multiples of 8 (padded to 32 in the kernels, PAD), >= 16
+  if (ci % 8 || co % 8 || ci < 16 || co < 16) return false;
   const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
   if ((ho * wo) % 4) return false;
   if (stride == 2 && w % 2) return false;  // gx rows written as (value, 0) pairs
@@ -414,14 +426,23 @@ int launch_cm(const float* in, const float* wt, float* out, int64_t n, int64_t K
   const int64_t Q = ho * wo;
   const int bm = cm_bm(M);
   constexpr int BQ = 128;
-  const int64_t qtiles = mde::cdiv(Q, BQ), mtiles = M / bm;
+  const int64_t qtiles = mde::cdiv(Q, BQ), mtiles = mde::cdiv(M, bm);
   const int64_t total = n * qtiles * mtiles;
   if (total > 0x7fffffff) return MDE_ERR_INVALID_ARG;
   const dim3 grid(xcd_grid(total)), block(256);
+  const bool pad = K % KC || M % bm;
 #define MDE_CM(BMv, MTv, QTv)                                                                     \
-  MDE_LAUNCH_MFMA(kid, bytes, flops, s, (cm_kernel<BMv, BQ, MTv, QTv, SIN, SOUT, TRANSA>), grid, \
-                  block, 0, in, wt, out, (int)K, (int)M, (int)hin, (int)win, (int)wo, (int)Q,     \
-                  (int)hout, (int)wout, (int)qtiles, (int)mtiles, (int)total)
+  do {                                                                                            \
+    if (pad)                                                                                      \
+      MDE_LAUNCH_MFMA(kid, bytes, flops, s,                                                       \
+                      (cm_kernel<BMv, BQ, MTv, QTv, SIN, SOUT, TRANSA, true>), grid, block, 0,    \
+                      in, wt, out, (int)K, (int)M, (int)hin, (int)win, (int)wo, (int)Q,           \
+                      (int)hout, (int)wout, (int)qtiles, (int)mtiles, (int)total);                \
+    else                                                                                          \
+      MDE_LAUNCH_MFMA(kid, bytes, flops, s, (cm_kernel<BMv, BQ, MTv, QTv, SIN, SOUT, TRANSA>),    \
+                      grid, block, 0, in, wt, out, (int)K, (int)M, (int)hin, (int)win, (int)wo,   \
+                      (int)Q, (int)hout, (int)wout, (int)qtiles, (int)mtiles, (int)total);        \
+  } while (0)
   if (bm == 128)
     MDE_CM(128, 2, 2);
   else if (bm == 64)

@@ -14,7 +14,9 @@ comment (model_mobileV3_large_newCRFs.py:94-111) and its decoder's
 in_channels [24, 40, 112, 160, 960] (:71).
 
 Every BatchNorm (with its ReLU / Hardswish) runs fused on the HIP BN kernel;
-the depthwise convolutions + BN + activation run on the HIP depthwise kernel.
+the depthwise convolutions + BN + activation run on the HIP depthwise kernel;
+the 1x1 expand / project convs on the NCHW HIP 1x1 kernels (conv1x1.hip, the
+channel counts that are not multiples of 32 padded in-kernel).
 """
 from __future__ import annotations
 
@@ -23,7 +25,7 @@ from functools import partial
 import torch
 from torch import nn
 
-from .nn import BatchNorm2d, batch_norm_act, depthwise_conv_bn_act, se_hardsigmoid
+from .nn import BatchNorm2d, Conv2d, batch_norm_act, depthwise_conv_bn_act, se_hardsigmoid
 
 
 def _make_divisible(v, divisor=8, min_value=None):
@@ -43,7 +45,9 @@ class Conv2dNormActivation(nn.Sequential):
     def __init__(self, cin, cout, kernel_size=3, stride=1, groups=1, act="relu",
                  norm_layer=partial(BatchNorm2d, eps=0.001, momentum=0.01)):
         pad = (kernel_size - 1) // 2
-        super().__init__(nn.Conv2d(cin, cout, kernel_size, stride, pad, groups=groups, bias=False),
+        # nn.py's Conv2d: the 1x1 convs on the NCHW HIP kernels (conv1x1.hip,
+        # channel counts padded to 32), the rest as the stock module
+        super().__init__(Conv2d(cin, cout, kernel_size, stride, pad, groups=groups, bias=False),
                          norm_layer(cout, act=act), nn.Identity())
         self.act = act
 

@@ -723,17 +723,21 @@ class _Conv1x1(torch.autograd.Function):
 
 
 C1_WIDE = os.environ.get("MDE_C1_WIDE", "1") != "0"  # MDE_C1_WIDE=0: MIOpen (A/B switch)
+C1_PAD = os.environ.get("MDE_C1_PAD", "1") != "0"  # A/B: 0 = only channel counts % 32 (round 5)
 
 
 def conv1x1_ok(conv: nn.Conv2d, x) -> bool:
     """Whether this bias-free 1x1 conv (stride 1 or 2) runs on the wide HIP 1x1
-    kernels: fp32 outside autocast, channel counts multiples of 32 (the
-    small-channel decoder 1x1s keep the fused pointwise kernels)."""
+    kernels: fp32 outside autocast, channel counts multiples of 8 and >= 16
+    (padded to 32 in-kernel; MobileNetV3's expand / project convs); the
+    small-channel decoder 1x1s keep the fused pointwise kernels."""
     if not (C1_WIDE and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
             and conv.weight.dtype == torch.float32 and x.dim() == 4
             and conv.kernel_size == (1, 1) and conv.padding == (0, 0)
             and conv.dilation == (1, 1) and conv.groups == 1
             and conv.stride in ((1, 1), (2, 2)) and conv.padding_mode == "zeros"):
+        return False
+    if not C1_PAD and (conv.in_channels % 32 or conv.out_channels % 32):
         return False
     return bool(_abi.query("mde_conv1x1_supported", conv.in_channels, conv.out_channels,
                            x.shape[2], x.shape[3], conv.stride[0], _abi.MDE_F32))

@@ -21,7 +21,12 @@ SHAPES = [(32, 64, 2, 120, 160), (64, 128, 2, 60, 80), (128, 256, 2, 30, 40),
           (256, 512, 2, 15, 20), (64, 128, 1, 60, 80), (128, 64, 1, 30, 40),
           (256, 64, 1, 15, 20), (256, 256, 1, 15, 20), (256, 512, 1, 8, 10),
           (512, 128, 1, 8, 10), (640, 128, 1, 8, 10), (96, 160, 1, 6, 6),
-          (64, 96, 2, 15, 20), (96, 64, 2, 13, 24)]
+          (64, 96, 2, 15, 20), (96, 64, 2, 13, 24),
+          # MobileNetV3-Large's expand / project 1x1s (mobilenetv3.py LARGE):
+          # channel counts that are multiples of 8, not 32 (padded in-kernel)
+          (16, 64, 1, 24, 32), (64, 24, 1, 12, 16), (24, 72, 1, 12, 16), (72, 40, 1, 10, 12),
+          (40, 120, 1, 6, 8), (240, 80, 1, 6, 8), (80, 200, 1, 6, 8), (184, 80, 1, 6, 8),
+          (480, 112, 1, 5, 8), (112, 672, 1, 4, 8), (24, 40, 2, 16, 20), (40, 24, 2, 13, 24)]
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -108,6 +113,10 @@ def test_conv1x1_small_planes_are_not_taken():
     from monocular_depth_estimation_amd import _abi
     assert _abi.query("mde_conv1x1_supported", 512, 128, 4, 5, 1, 0) == 0
     assert _abi.query("mde_conv1x1_supported", 512, 128, 8, 10, 1, 0) == 1
+    # channel counts: multiples of 8, >= 16
+    assert _abi.query("mde_conv1x1_supported", 12, 128, 8, 10, 1, 0) == 0
+    assert _abi.query("mde_conv1x1_supported", 8, 128, 8, 10, 1, 0) == 0
+    assert _abi.query("mde_conv1x1_supported", 16, 24, 8, 10, 1, 0) == 1
 
 
 def test_conv1x1_stride2_zero_fills_odd_positions():

@@ -403,6 +403,15 @@ int mde_gelu_bwd_colsum(const void* dh, const void* a, void* da, float* gb, int6
  * Split-K over token ranges on v_mfma_f32_16x16x4_f32, partials summed in a
  * fixed order (bitwise reproducible).  Workspace bytes from
  * mde_linear_wgrad_workspace (0 = unsupported shape). */
+/* Per-channel sums of an NCHW fp32 tensor, gb[c] = sum_{n,p} g[n][c][p] (a
+ * biased conv's bias gradient: autograd's grad.sum((0, 2, 3)) behind the
+ * NewCRF projections' `y + bias`, src/newcrf_layers.py:384-392); hw % 4 == 0.
+ * Fixed-order two-level reduction; workspace bytes from mde_chansum_workspace
+ * (0 = unsupported shape). */
+size_t mde_chansum_workspace(int64_t n, int64_t c, int64_t hw);
+int mde_chansum(const void* g, float* gb, int64_t n, int64_t c, int64_t hw, void* workspace,
+                int dtype, void* stream);
+
 size_t mde_linear_wgrad_workspace(int64_t t_rows, int64_t m, int64_t n);
 int mde_linear_wgrad(const void* g, const void* x, float* gw, float* gb, int64_t t_rows,
                      int64_t m, int64_t n, void* workspace, int dtype, void* stream);

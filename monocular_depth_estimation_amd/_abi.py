@@ -132,6 +132,8 @@ SIGNATURES = {
                              _vp, _int, _vp]),
     "mde_colsum_workspace": (_sz, [_i64, _i64]),
     "mde_colsum": (_int, [_vp, _vp, _i64, _i64, _vp, _int, _vp]),
+    "mde_chansum_workspace": (_sz, [_i64, _i64, _i64]),
+    "mde_chansum": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_linear_wgrad_workspace": (_sz, [_i64, _i64, _i64]),
     "mde_linear_wgrad": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_gelu_bwd_colsum": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _vp, _int, _vp]),

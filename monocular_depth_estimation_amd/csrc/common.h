@@ -89,6 +89,7 @@ enum Kid : int {
   K_STEM_WGRAD,
   K_LIN_WGRAD,      // token-major Linear weight gradients (mlp.hip, v_mfma_f32_16x16x4_f32)
   K_LIN_WREDUCE,
+  K_CHANSUM,        // a biased conv's bias gradient (per-channel NCHW sums, mlp.hip)
   K_COUNT
 };
 

@@ -374,9 +374,83 @@ bool wgrad_plan(int64_t t_rows, int64_t m, int64_t n, WgradPlan* p) {
   return (int64_t)p->tiles * s < (1LL << 31);
 }
 
+// ---------------------------------------------------------------------------
+// Per-channel sums of an NCHW tensor, gb[c] = sum_{n, p} g[n][c][p]: a biased
+// conv's bias gradient (autograd's grad.sum((0, 2, 3)) behind `y + bias`,
+// nn.Conv2d with a bias on the HIP conv path: the NewCRF projections,
+// newcrf_layers.py:384-392), which ATen's reduction ran at ~1.3 TB/s.  Block
+// (c, s) sums planes [s P, s P + P) of channel c with float4 loads (4 per
+// lane in flight), a fixed-shape tree over the block, then chansum_final
+// adds the S partials in order: bitwise reproducible.
+__global__ void __launch_bounds__(256)
+    chansum_part_kernel(const float* __restrict__ g, int64_t n, int c, int64_t hw, int per,
+                        float* __restrict__ part) {
+  __shared__ float red[256];
+  const int ch = blockIdx.x, sp = blockIdx.y, tid = threadIdx.x;
+  const int64_t i0 = (int64_t)sp * per, i1 = i0 + per < n ? i0 + per : n;
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+  for (int64_t img = i0; img < i1; ++img) {
+    const float* p = g + (img * c + ch) * hw;
+    int64_t e = 4 * (int64_t)tid;
+    for (; e + 1024 < hw; e += 2048) {
+      const float4 u = mde::ld4_nt(p + e), v = mde::ld4_nt(p + e + 1024);
+      a0.x += u.x; a0.y += u.y; a0.z += u.z; a0.w += u.w;
+      a1.x += v.x; a1.y += v.y; a1.z += v.z; a1.w += v.w;
+    }
+    if (e < hw) {
+      const float4 u = mde::ld4_nt(p + e);
+      a0.x += u.x; a0.y += u.y; a0.z += u.z; a0.w += u.w;
+    }
+  }
+  red[tid] = ((a0.x + a0.y) + (a0.z + a0.w)) + ((a1.x + a1.y) + (a1.z + a1.w));
+  __syncthreads();
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
+  }
+  if (tid == 0) part[(int64_t)ch * gridDim.y + sp] = red[0];
+}
+
+__global__ void __launch_bounds__(256)
+    chansum_final_kernel(const float* __restrict__ part, int c, int splits, float* __restrict__ gb) {
+  const int ch = blockIdx.x * 256 + threadIdx.x;
+  if (ch >= c) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[(int64_t)ch * splits + k];
+  gb[ch] = s;
+}
+
+inline int chansum_splits(int64_t n, int64_t c) {
+  const int64_t s = mde::cdiv(1024, c);  // ~1024 blocks
+  return (int)(s < n ? s : n);
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t mde_chansum_workspace(int64_t n, int64_t c, int64_t hw) {
+  if (n <= 0 || c <= 0 || hw <= 0 || hw % 4 || c > 65535) return 0;
+  return sizeof(float) * (size_t)(c * chansum_splits(n, c));
+}
+
+int mde_chansum(const void* g, float* gb, int64_t n, int64_t c, int64_t hw, void* workspace,
+                int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!g || !gb || !workspace || !mde_chansum_workspace(n, c, hw)) return MDE_ERR_INVALID_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int sp = chansum_splits(n, c);
+  const int per = (int)mde::cdiv(n, sp);
+  const int used = (int)mde::cdiv(n, per);
+  float* part = (float*)workspace;
+  MDE_LAUNCH(mde::K_CHANSUM, 4.0 * (double)n * c * hw, s, chansum_part_kernel,
+             dim3((unsigned)c, (unsigned)used), dim3(256), 0, (const float*)g, n, (int)c, hw, per,
+             part);
+  MDE_LAUNCH(mde::K_CHANSUM, 4.0 * (double)c * used, s, chansum_final_kernel,
+             dim3((unsigned)mde::cdiv(c, 256)), dim3(256), 0, (const float*)part, (int)c, used, gb);
+  return MDE_OK;
+}
 
 size_t mde_linear_wgrad_workspace(int64_t t_rows, int64_t m, int64_t n) {
   WgradPlan p;

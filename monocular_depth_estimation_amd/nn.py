@@ -1344,6 +1344,31 @@ def conv1x1_mm(weight, x):
     return y.view(n, cout, h, w)
 
 
+CHANSUM = os.environ.get("MDE_CHANSUM", "1") != "0"  # A/B: 0 = autograd's bias-gradient sum
+
+
+class _BiasAdd(torch.autograd.Function):
+    """y + bias[None, :, None, None] (fp32 NCHW) whose bias gradient is
+    mde_chansum (one fixed-order HBM-rate pass over gy) instead of autograd's
+    grad.sum((0, 2, 3)) (~1.3 TB/s on the NewCRF projections' planes)."""
+
+    @staticmethod
+    def forward(ctx, y, bias):
+        return y + bias.view(1, -1, 1, 1)
+
+    @staticmethod
+    def backward(ctx, gy):
+        gb = None
+        if ctx.needs_input_grad[1]:
+            g = gy.contiguous()
+            n, c, h, w = g.shape
+            gb = torch.empty(c, dtype=torch.float32, device=g.device)
+            ws = _ws(_abi.query("mde_chansum_workspace", n, c, h * w), g)
+            _abi.call("mde_chansum", _abi.ptr(g), _abi.ptr(gb), n, c, h * w, _abi.ptr(ws), 0,
+                      _abi.stream_of(g))
+        return gy, gb
+
+
 class Conv2d(nn.Conv2d):
     """nn.Conv2d (same parameters and state_dict keys) whose bias-free
     forward takes conv_nobias's HIP kernels where they apply.  With a bias:
@@ -1362,6 +1387,9 @@ class Conv2d(nn.Conv2d):
             passes = conv3x3_passes(self, x)
             if passes is not None and (passes[0] or passes[1]):
                 y = conv3x3(x, self.weight, passes)
+                if CHANSUM and y.dtype == torch.float32 and _abi.query(
+                        "mde_chansum_workspace", y.shape[0], y.shape[1], y.shape[2] * y.shape[3]):
+                    return _BiasAdd.apply(y, self.bias)
                 return y + self.bias.to(y.dtype).view(1, -1, 1, 1)
             if convbf_ok(self, x):
                 y = conv_bf16(self, x)

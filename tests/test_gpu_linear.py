@@ -77,3 +77,26 @@ def test_linear_tok_backward_matches_autograd():
                      (mlp.fc2.weight.grad, w2.grad), (mlp.fc2.bias.grad, b2.grad)):
         err = float((got.double() - ref).abs().max())
         assert err <= 1e-4 * max(1.0, float(ref.abs().max())), err
+
+
+@pytest.mark.parametrize("n,c,h,w", [(16, 128, 120, 160), (3, 1024, 15, 20), (1, 40, 2, 2),
+                                     (5, 7, 6, 10)])
+def test_chansum_vs_float64(n, c, h, w):
+    """mde_chansum (a biased conv's bias gradient, the NewCRF projections'
+    `y + bias`, newcrf_layers.py:384-392) vs float64 sums; bitwise run to run."""
+    from monocular_depth_estimation_amd import _abi
+    g = torch.randn((n, c, h, w), device=DEV, generator=torch.Generator(device=DEV).manual_seed(c))
+    nbytes = _abi.query("mde_chansum_workspace", n, c, h * w)
+    assert nbytes > 0
+    outs = []
+    for _ in range(2):
+        ws = torch.full((nbytes // 4,), float("nan"), device=DEV)
+        gb = torch.full((c,), float("nan"), device=DEV)
+        _abi.call("mde_chansum", _abi.ptr(g), _abi.ptr(gb), n, c, h * w, _abi.ptr(ws), 0,
+                  _abi.stream_of(g))
+        outs.append(gb)
+    ref = g.double().sum((0, 2, 3))
+    tol = 1e-6 * (n * h * w) ** 0.5 * 4 + 1e-6
+    assert float((outs[0].double() - ref).abs().max()) <= tol
+    assert torch.equal(outs[0], outs[1])
+    assert _abi.query("mde_chansum_workspace", n, c, 6) == 0  # hw % 4 != 0

@@ -46,6 +46,10 @@ def main():
     print(f"aten self device time: {tot / 1e3:.3f} ms/step over {len(rows)} (op, shape) rows")
     for e in rows[:args.top]:
         print(f"{e.self_device_time_total / 1e3:8.3f} ms {e.count:4d}x  {e.key:32s} {str(e.input_shapes)[:150]}")
+    other = [e for e in rows if not any(k in e.key for k in ("mm", "convolution", "miopen"))]
+    print("other aten ops (no GEMM / convolution):")
+    for e in other[:args.top]:
+        print(f"{e.self_device_time_total / 1e3:8.3f} ms {e.count:4d}x  {e.key:32s} {str(e.input_shapes)[:150]}")
     # the vendor convolutions: which module shapes still reach MIOpen, and its kernels
     conv = [e for e in prof.key_averages(group_by_input_shape=True)
             if ("convolution" in e.key or "miopen" in e.key) and e.device_time_total > 0]

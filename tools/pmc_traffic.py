@@ -124,6 +124,7 @@ NAMES = [
     (r"stem_wreduce_kernel\(", "stem_wgrad_bf16"),  # builds before the tag
     (r"lin_wgrad_kernel", "linear_wgrad"),
     (r"lin_wreduce_kernel", "linear_wreduce"),
+    (r"chansum_(part|final)_kernel", "conv_bias_grad"),
     (r"eval_partial_kernel", "eval_sums"),
     (r"eval_final_kernel", "eval_final"),
     (r"nyu_augment_kernel", "nyu_augment"),

@@ -412,6 +412,20 @@ size_t mde_chansum_workspace(int64_t n, int64_t c, int64_t hw);
 int mde_chansum(const void* g, float* gb, int64_t n, int64_t c, int64_t hw, void* workspace,
                 int dtype, void* stream);
 
+/* 3x3 / stride-1 / pad-1 convolution with ONE output channel, NCHW fp32 (the
+ * NewCRF decoder's depth head, src/model_mobileV3_large_newCRFs.py
+ * Decoder.conv1 = nn.Conv2d(128, 1, 3, padding=1)): y = b + conv(x) (bias
+ * nullable), gx, gw (fixed-order reduction; workspace from
+ * mde_head_conv_wgrad_workspace).  w % 4 == 0. */
+int mde_head_conv_supported(int64_t n, int64_t c, int64_t h, int64_t w);
+int mde_head_conv_fwd(const void* x, const float* weight, const float* bias, void* y, int64_t n,
+                      int64_t c, int64_t h, int64_t w, int dtype, void* stream);
+int mde_head_conv_dgrad(const void* gy, const float* weight, void* gx, int64_t n, int64_t c,
+                        int64_t h, int64_t w, int dtype, void* stream);
+size_t mde_head_conv_wgrad_workspace(int64_t n, int64_t c, int64_t h, int64_t w);
+int mde_head_conv_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t c,
+                        int64_t h, int64_t w, void* workspace, int dtype, void* stream);
+
 size_t mde_linear_wgrad_workspace(int64_t t_rows, int64_t m, int64_t n);
 int mde_linear_wgrad(const void* g, const void* x, float* gw, float* gb, int64_t t_rows,
                      int64_t m, int64_t n, void* workspace, int dtype, void* stream);

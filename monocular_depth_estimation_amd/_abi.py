@@ -132,6 +132,11 @@ SIGNATURES = {
                              _vp, _int, _vp]),
     "mde_colsum_workspace": (_sz, [_i64, _i64]),
     "mde_colsum": (_int, [_vp, _vp, _i64, _i64, _vp, _int, _vp]),
+    "mde_head_conv_supported": (_int, [_i64, _i64, _i64, _i64]),
+    "mde_head_conv_fwd": (_int, [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_head_conv_dgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _int, _vp]),
+    "mde_head_conv_wgrad_workspace": (_sz, [_i64, _i64, _i64, _i64]),
+    "mde_head_conv_wgrad": (_int, [_vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_chansum_workspace": (_sz, [_i64, _i64, _i64]),
     "mde_chansum": (_int, [_vp, _vp, _i64, _i64, _i64, _vp, _int, _vp]),
     "mde_linear_wgrad_workspace": (_sz, [_i64, _i64, _i64]),

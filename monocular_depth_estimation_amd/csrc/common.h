@@ -90,6 +90,9 @@ enum Kid : int {
   K_LIN_WGRAD,      // token-major Linear weight gradients (mlp.hip, v_mfma_f32_16x16x4_f32)
   K_LIN_WREDUCE,
   K_CHANSUM,        // a biased conv's bias gradient (per-channel NCHW sums, mlp.hip)
+  K_HEAD_FWD,       // the one-output-channel 3x3 conv (head.hip: the NewCRF depth head)
+  K_HEAD_DGRAD,
+  K_HEAD_WGRAD,
   K_COUNT
 };
 

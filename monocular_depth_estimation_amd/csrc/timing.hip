@@ -32,7 +32,8 @@ const char* const kNames[mde::K_COUNT] = {
     "conv3x3s2_fwd", "conv3x3s2_dgrad", "conv3x3w_fwd", "conv3x3w_dgrad",
     "wino_fwd",       "wino_dgrad",      "wino_weight",   "window_attn_bwd_reduce",
     "convbf_fwd_bf16", "convbf_dgrad_bf16", "convbf_wgrad_bf16", "convbf_wreduce", "convbf_pack",
-    "stem_fwd_bf16", "stem_wgrad_bf16", "linear_wgrad", "linear_wreduce", "conv_bias_grad"};
+    "stem_fwd_bf16", "stem_wgrad_bf16", "linear_wgrad", "linear_wreduce", "conv_bias_grad",
+    "head_conv_fwd", "head_conv_dgrad", "head_conv_wgrad"};
 
 struct Pending {
   int kid;

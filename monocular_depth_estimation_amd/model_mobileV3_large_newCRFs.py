@@ -21,6 +21,7 @@ from torch import nn
 
 from .functional import bilinear_resize
 from .mobilenetv3 import mobilenet_v3_large
+from .nn import Conv2d
 from .newcrf_layers import NewCRF
 
 
@@ -39,11 +40,12 @@ class Decoder(nn.Module):
         crf_dims = [128, 256, 512, 1024]
         v_dims = [64, 128, 256, 512]
         in_channels = [24, 40, 112, 160, 960]
-        self.conv0 = nn.Conv2d(in_channels[4], v_dims[3], kernel_size=1, stride=1)
+        # nn.py's Conv2d (same keys): the 1x1 bridge on the HIP 1x1 kernel + bias
+        self.conv0 = Conv2d(in_channels[4], v_dims[3], kernel_size=1, stride=1)
         for i in (3, 2, 1, 0):
             setattr(self, f"crf{i}", NewCRF(input_dim=in_channels[i], embed_dim=crf_dims[i],
                                             window_size=win, v_dim=v_dims[i], num_heads=num_heads[i]))
-        self.conv1 = nn.Conv2d(crf_dims[0], 1, 3, padding=1)
+        self.conv1 = Conv2d(crf_dims[0], 1, 3, padding=1)  # head.hip (nn.py Conv2d)
         self.sigmoid = nn.Sigmoid()
         self.shuffle = nn.PixelShuffle(2)
 

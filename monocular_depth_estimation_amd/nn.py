@@ -1369,6 +1369,60 @@ class _BiasAdd(torch.autograd.Function):
         return gy, gb
 
 
+HEAD_CONV = os.environ.get("MDE_HEAD_CONV", "1") != "0"  # A/B: 0 = MIOpen
+
+
+def head_conv_ok(conv: nn.Conv2d, x) -> bool:
+    """A 3x3 / s1 / p1 conv with ONE output channel and a bias in fp32 (the
+    NewCRF depth head, model_mobileV3_large_newCRFs.py Decoder.conv1) on
+    head.hip's three VALU kernels."""
+    return (HEAD_CONV and x.is_cuda and x.dtype == torch.float32 and not _autocast_bf16(x)
+            and x.dim() == 4 and conv.out_channels == 1 and conv.bias is not None
+            and conv.kernel_size == (3, 3) and conv.stride == (1, 1) and conv.padding == (1, 1)
+            and conv.dilation == (1, 1) and conv.groups == 1
+            and conv.weight.dtype == torch.float32
+            and bool(_abi.query("mde_head_conv_supported", x.shape[0], x.shape[1], x.shape[2],
+                                x.shape[3])))
+
+
+class _HeadConv(torch.autograd.Function):
+    """conv2d(x, W[1, C, 3, 3], b, padding=1) on head.hip: forward, data and
+    weight gradients as HBM-rate VALU passes, the bias gradient by mde_chansum."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        x = x.contiguous()
+        n, c, h, w = x.shape
+        wt = weight.contiguous()
+        y = torch.empty((n, 1, h, w), dtype=torch.float32, device=x.device)
+        _abi.call("mde_head_conv_fwd", _abi.ptr(x), _abi.ptr(wt), _abi.ptr(bias), _abi.ptr(y), n, c,
+                  h, w, 0, _abi.stream_of(x))
+        ctx.save_for_backward(x, wt)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, wt = ctx.saved_tensors
+        n, c, h, w = x.shape
+        gy = gy.contiguous()
+        st = _abi.stream_of(gy)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x)
+            _abi.call("mde_head_conv_dgrad", _abi.ptr(gy), _abi.ptr(wt), _abi.ptr(gx), n, c, h, w, 0,
+                      st)
+        if ctx.needs_input_grad[1]:
+            gw = torch.empty_like(wt)
+            ws = _ws(_abi.query("mde_head_conv_wgrad_workspace", n, c, h, w), gy)
+            _abi.call("mde_head_conv_wgrad", _abi.ptr(gy), _abi.ptr(x), _abi.ptr(gw), n, c, h, w,
+                      _abi.ptr(ws), 0, st)
+        if ctx.needs_input_grad[2]:
+            gb = torch.empty(1, dtype=torch.float32, device=gy.device)
+            ws = _ws(_abi.query("mde_chansum_workspace", n, 1, h * w), gy)
+            _abi.call("mde_chansum", _abi.ptr(gy), _abi.ptr(gb), n, 1, h * w, _abi.ptr(ws), 0, st)
+        return gx, gw, gb
+
+
 class Conv2d(nn.Conv2d):
     """nn.Conv2d (same parameters and state_dict keys) whose bias-free
     forward takes conv_nobias's HIP kernels where they apply.  With a bias:
@@ -1394,6 +1448,16 @@ class Conv2d(nn.Conv2d):
             if convbf_ok(self, x):
                 y = conv_bf16(self, x)
                 return y + self.bias.to(y.dtype).view(1, -1, 1, 1)
+            if head_conv_ok(self, x):
+                return _HeadConv.apply(x, self.weight, self.bias)
+            if CHANSUM and conv1x1_ok(self, x):
+                # a biased 1x1 (the NewCRF decoder's 960 -> 512 bridge,
+                # model_mobileV3_large_newCRFs.py conv0) on the HIP 1x1 kernels
+                y = _Conv1x1.apply(x, self.weight, self.stride[0])
+                if _abi.query("mde_chansum_workspace", y.shape[0], y.shape[1],
+                              y.shape[2] * y.shape[3]):
+                    return _BiasAdd.apply(y, self.bias)
+                return y + self.bias.view(1, -1, 1, 1)
         return super().forward(x)
 
 

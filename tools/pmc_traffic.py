@@ -125,6 +125,9 @@ NAMES = [
     (r"lin_wgrad_kernel", "linear_wgrad"),
     (r"lin_wreduce_kernel", "linear_wreduce"),
     (r"chansum_(part|final)_kernel", "conv_bias_grad"),
+    (r"head_fwd_kernel", "head_conv_fwd"),
+    (r"head_dgrad_kernel", "head_conv_dgrad"),
+    (r"head_(wgrad|wreduce)_kernel", "head_conv_wgrad"),
     (r"eval_partial_kernel", "eval_sums"),
     (r"eval_final_kernel", "eval_final"),
     (r"nyu_augment_kernel", "nyu_augment"),

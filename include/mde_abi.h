@@ -571,6 +571,19 @@ int mde_layernorm_fwd(const void* x, const float* gamma, const float* beta, void
 int mde_layernorm_bwd(const void* gy, const void* x, const float* gamma, const float* mean,
                       const float* rstd, void* gx, float* ggamma, float* gbeta, int64_t rows,
                       int64_t c, void* workspace, int dtype, void* stream);
+/* The residual add in front of a LayerNorm (CRFBlock's `x + attn(..)` /
+ * `x + mlp(..)` and the next norm2 / norm1 / norm_crf,
+ * src/newcrf_layers.py:229-257,434): sum = x + r is written and normalised in
+ * one pass; the backward takes the gradient the sum's residual branch carries
+ * (gres) and adds it in its epilogue: gx = gres + LayerNorm'(gy), the
+ * gradient of both x and r. */
+int mde_layernorm_add_fwd(const void* x, const void* r, const float* gamma, const float* beta,
+                          void* sum, void* y, float* mean, float* rstd, int64_t rows, int64_t c,
+                          float eps, int dtype, void* stream);
+int mde_layernorm_bwd_res(const void* gy, const void* x, const void* gres, const float* gamma,
+                          const float* mean, const float* rstd, void* gx, float* ggamma,
+                          float* gbeta, int64_t rows, int64_t c, void* workspace, int dtype,
+                          void* stream);
 
 /* Batched 2-D transpose y[b][j][i] = x[b][i][j] of x [batch, m, n]: the
  * NCHW <-> token-major conversions around the NewCRF layers

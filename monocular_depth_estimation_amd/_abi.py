@@ -125,6 +125,10 @@ SIGNATURES = {
     "mde_layernorm_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32, _int, _vp]),
     "mde_layernorm_bwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _int,
                                  _vp]),
+    "mde_layernorm_add_fwd": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _f32,
+                                      _int, _vp]),
+    "mde_layernorm_bwd_res": (_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64,
+                                      _vp, _int, _vp]),
     "mde_transpose": (_int, [_vp, _vp, _i64, _i64, _i64, _int, _vp]),
     "mde_nyu_augment": (_int, [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _int, _vp]),
     "mde_eval_workspace": (_sz, [_i64, _i64, _i64]),

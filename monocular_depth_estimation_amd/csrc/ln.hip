@@ -76,17 +76,28 @@ struct RowIO {
   }
 };
 
-template <int VPL>
+// ADD: the residual add in front of the norm (CRFBlock's `x + attn(..)` /
+// `x + mlp(..)` followed by the next LayerNorm, newcrf_layers.py:229-257):
+// s = x + r is written AND normalised from registers (one pass instead of an
+// add pass and a norm pass).
+template <int VPL, bool ADD = false>
 __global__ void __launch_bounds__(256)
     ln_fwd_kernel(const float* __restrict__ x, const float* __restrict__ gamma,
                   const float* __restrict__ beta, float* __restrict__ y,
                   float* __restrict__ mean_out, float* __restrict__ rstd_out, int64_t rows,
-                  float eps) {
+                  float eps, const float* __restrict__ r = nullptr, float* __restrict__ sum = nullptr) {
   constexpr int C = 64 * VPL;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   float v[VPL], g[VPL], b[VPL];
   RowIO<VPL>::load(x + row * C, v);
+  if constexpr (ADD) {
+    float a[VPL];
+    RowIO<VPL>::load(r + row * C, a);
+#pragma unroll
+    for (int i = 0; i < VPL; ++i) v[i] += a[i];
+    RowIO<VPL>::store(sum + row * C, v);
+  }
   RowIO<VPL>::load(gamma, g);
   RowIO<VPL>::load(beta, b);
   float s = 0.f;
@@ -111,12 +122,15 @@ __global__ void __launch_bounds__(256)
 
 // gx = rstd * (gy*g - mean(gy*g) - x_hat * mean(gy*g*x_hat)); partial
 // gamma/beta gradients of this block's rows into part[blk][2][C].
-template <int VPL>
+// RES: + gres (the gradient the normalised sum's residual branch carries,
+// added in the epilogue instead of by a separate accumulation pass).
+template <int VPL, bool RES = false>
 __global__ void __launch_bounds__(256)
     ln_bwd_kernel(const float* __restrict__ gy, const float* __restrict__ x,
                   const float* __restrict__ gamma, const float* __restrict__ mean,
                   const float* __restrict__ rstd, float* __restrict__ gx,
-                  float* __restrict__ part, int64_t rows, int64_t rows_per_blk) {
+                  float* __restrict__ part, int64_t rows, int64_t rows_per_blk,
+                  const float* __restrict__ gres = nullptr) {
   constexpr int C = 64 * VPL;
   __shared__ float red[4][2][C];
   const int wid = threadIdx.x >> 6;
@@ -145,6 +159,15 @@ __global__ void __launch_bounds__(256)
     s2 = wave_sum(s2) * (1.f / C);
 #pragma unroll
     for (int i = 0; i < VPL; ++i) d[i] = rs * (d[i] * g[i] - s1 - v[i] * s2);
+    if constexpr (RES) {
+      // a separate rounded add (no FMA contraction with the product above):
+      // bitwise the add autograd's accumulation did
+#pragma clang fp contract(off)
+      float a[VPL];
+      RowIO<VPL>::load(gres + row * C, a);
+#pragma unroll
+      for (int i = 0; i < VPL; ++i) d[i] = a[i] + d[i];
+    }
     RowIO<VPL>::store(gx + row * C, d);
   }
 #pragma unroll
@@ -208,21 +231,34 @@ __global__ void __launch_bounds__(256)
 
 template <int VPL>
 int ln_fwd_launch(const float* x, const float* g, const float* b, float* y, float* mu,
-                  float* rs, int64_t rows, float eps, hipStream_t st) {
+                  float* rs, int64_t rows, float eps, hipStream_t st, const float* r = nullptr,
+                  float* sum = nullptr) {
+  if (r) {
+    const double bytes = 16.0 * rows * 64 * VPL + 8.0 * rows;  // x, r read; s, y written
+    MDE_LAUNCH(K_LN_FWD, bytes, st, (ln_fwd_kernel<VPL, true>), dim3((unsigned)cdiv(rows, 4)),
+               dim3(256), 0, x, g, b, y, mu, rs, rows, eps, r, sum);
+    return 0;
+  }
   const double bytes = 8.0 * rows * 64 * VPL + 8.0 * rows;
   MDE_LAUNCH(K_LN_FWD, bytes, st, ln_fwd_kernel<VPL>, dim3((unsigned)cdiv(rows, 4)), dim3(256),
-             0, x, g, b, y, mu, rs, rows, eps);
+             0, x, g, b, y, mu, rs, rows, eps, nullptr, nullptr);
   return 0;
 }
 
 template <int VPL>
 int ln_bwd_launch(const float* gy, const float* x, const float* g, const float* mu,
                   const float* rs, float* gx, float* gg, float* gb, float* part, int64_t rows,
-                  hipStream_t st) {
+                  hipStream_t st, const float* gres = nullptr) {
   const int64_t nblk = bwd_blocks(rows);
-  const double bytes = 12.0 * rows * 64 * VPL + 8.0 * rows;
-  MDE_LAUNCH(K_LN_BWD, bytes, st, ln_bwd_kernel<VPL>, dim3((unsigned)nblk), dim3(256), 0, gy, x,
-             g, mu, rs, gx, part, rows, cdiv(rows, nblk));
+  if (gres) {
+    const double bytes = 16.0 * rows * 64 * VPL + 8.0 * rows;  // + the residual gradient read
+    MDE_LAUNCH(K_LN_BWD, bytes, st, (ln_bwd_kernel<VPL, true>), dim3((unsigned)nblk), dim3(256),
+               0, gy, x, g, mu, rs, gx, part, rows, cdiv(rows, nblk), gres);
+  } else {
+    const double bytes = 12.0 * rows * 64 * VPL + 8.0 * rows;
+    MDE_LAUNCH(K_LN_BWD, bytes, st, ln_bwd_kernel<VPL>, dim3((unsigned)nblk), dim3(256), 0, gy, x,
+               g, mu, rs, gx, part, rows, cdiv(rows, nblk), nullptr);
+  }
   const int c = 64 * VPL;
   MDE_LAUNCH(K_LN_WREDUCE, 8.0 * nblk * c, st, ln_wreduce_kernel, dim3((unsigned)cdiv(2 * c, 64)),
              dim3(1024), 0, part, gg, gb, nblk, c);
@@ -243,6 +279,53 @@ extern "C" {
 size_t mde_layernorm_workspace(int64_t rows, int64_t c) {
   if (!ln_ok(rows, c)) return 0;
   return (size_t)(4 * 2 * c * bwd_blocks(rows));
+}
+
+int mde_layernorm_add_fwd(const void* x, const void* r, const float* gamma, const float* beta,
+                          void* sum, void* y, float* mean, float* rstd, int64_t rows, int64_t c,
+                          float eps, int dtype, void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!x || !r || !sum || !gamma || !beta || !y || !mean || !rstd) return MDE_ERR_INVALID_ARG;
+  if (!ln_ok(rows, c)) return rows > 0 && c > 1024 && c % 64 == 0 ? MDE_ERR_UNSUPPORTED : MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const float* xp = (const float*)x;
+  const float* rp = (const float*)r;
+  float* sp = (float*)sum;
+  float* yp = (float*)y;
+  switch (c / 64) {
+#define MDE_LN_CASE(V) \
+  case V: return ln_fwd_launch<V>(xp, gamma, beta, yp, mean, rstd, rows, eps, st, rp, sp);
+    MDE_LN_CASE(1) MDE_LN_CASE(2) MDE_LN_CASE(3) MDE_LN_CASE(4) MDE_LN_CASE(5) MDE_LN_CASE(6)
+    MDE_LN_CASE(7) MDE_LN_CASE(8) MDE_LN_CASE(9) MDE_LN_CASE(10) MDE_LN_CASE(11)
+    MDE_LN_CASE(12) MDE_LN_CASE(13) MDE_LN_CASE(14) MDE_LN_CASE(15) MDE_LN_CASE(16)
+#undef MDE_LN_CASE
+    default: return MDE_ERR_INVALID_ARG;
+  }
+}
+
+int mde_layernorm_bwd_res(const void* gy, const void* x, const void* gres, const float* gamma,
+                          const float* mean, const float* rstd, void* gx, float* ggamma,
+                          float* gbeta, int64_t rows, int64_t c, void* workspace, int dtype,
+                          void* stream) {
+  if (dtype != MDE_F32) return MDE_ERR_UNSUPPORTED;
+  if (!gy || !x || !gres || !gamma || !mean || !rstd || !gx || !ggamma || !gbeta || !workspace)
+    return MDE_ERR_INVALID_ARG;
+  if (!ln_ok(rows, c)) return rows > 0 && c > 1024 && c % 64 == 0 ? MDE_ERR_UNSUPPORTED : MDE_ERR_INVALID_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  const float* g = (const float*)gy;
+  const float* xp = (const float*)x;
+  const float* rp = (const float*)gres;
+  float* gxp = (float*)gx;
+  float* part = (float*)workspace;
+  switch (c / 64) {
+#define MDE_LN_CASE(V) \
+  case V: return ln_bwd_launch<V>(g, xp, gamma, mean, rstd, gxp, ggamma, gbeta, part, rows, st, rp);
+    MDE_LN_CASE(1) MDE_LN_CASE(2) MDE_LN_CASE(3) MDE_LN_CASE(4) MDE_LN_CASE(5) MDE_LN_CASE(6)
+    MDE_LN_CASE(7) MDE_LN_CASE(8) MDE_LN_CASE(9) MDE_LN_CASE(10) MDE_LN_CASE(11)
+    MDE_LN_CASE(12) MDE_LN_CASE(13) MDE_LN_CASE(14) MDE_LN_CASE(15) MDE_LN_CASE(16)
+#undef MDE_LN_CASE
+    default: return MDE_ERR_INVALID_ARG;
+  }
 }
 
 int mde_layernorm_fwd(const void* x, const float* gamma, const float* beta, void* y,

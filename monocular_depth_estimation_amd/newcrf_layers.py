@@ -282,6 +282,64 @@ class _LayerNorm(torch.autograd.Function):
         return gx, gw, gb, None
 
 
+class _AddLayerNorm(torch.autograd.Function):
+    """(s, LayerNorm(s)) with s = x + r in ONE HIP pass (mde_layernorm_add_fwd):
+    CRFBlock's residual adds, each followed by a LayerNorm
+    (newcrf_layers.py:229-257,434).  The backward adds the gradient that s's
+    residual branch carries in the LayerNorm backward's epilogue
+    (mde_layernorm_bwd_res) and hands the sum to both x and r -- no separate
+    add pass forward, no accumulation pass backward."""
+
+    @staticmethod
+    @_amp_fwd
+    def forward(ctx, x, r, weight, bias, eps):
+        x = x.contiguous()
+        r = r.contiguous()
+        c = x.shape[-1]
+        rows = x.numel() // c
+        s = torch.empty_like(x)
+        y = torch.empty_like(x)
+        mean = torch.empty(rows, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+        _abi.call("mde_layernorm_add_fwd", _abi.ptr(x), _abi.ptr(r), _abi.ptr(weight), _abi.ptr(bias),
+                  _abi.ptr(s), _abi.ptr(y), _abi.ptr(mean), _abi.ptr(rstd), rows, c, float(eps),
+                  _abi.dtype_code(x), _abi.stream_of(x))
+        ctx.save_for_backward(s, weight, mean, rstd)
+        return s, y
+
+    @staticmethod
+    @_amp_bwd
+    def backward(ctx, gs, gy):
+        s, weight, mean, rstd = ctx.saved_tensors
+        gy = gy.contiguous()
+        c = s.shape[-1]
+        rows = s.numel() // c
+        gx = torch.empty_like(s)
+        gw = torch.empty_like(weight)
+        gb = torch.empty_like(weight)
+        ws = _ws(_abi.query("mde_layernorm_workspace", rows, c), s)
+        _abi.call("mde_layernorm_bwd_res", _abi.ptr(gy), _abi.ptr(s), _abi.ptr(gs.contiguous()),
+                  _abi.ptr(weight), _abi.ptr(mean), _abi.ptr(rstd), _abi.ptr(gx), _abi.ptr(gw),
+                  _abi.ptr(gb), rows, c, _abi.ptr(ws), _abi.dtype_code(gy), _abi.stream_of(gy))
+        return gx, gx, gw, gb, None
+
+
+LN_ADD = os.environ.get("MDE_LN_ADD", "1") != "0"  # A/B: 0 = separate add + LayerNorm
+
+
+def add_layer_norm(x, r, norm):
+    """(x + r, norm(x + r)): one HIP pass (_AddLayerNorm) where it applies."""
+    if (LN_ADD and isinstance(norm, LayerNorm) and x.is_cuda and x.dtype == torch.float32
+            and r.dtype == torch.float32 and x.shape == r.shape and not torch.is_autocast_enabled()
+            and norm.weight is not None and norm.bias is not None
+            and len(norm.normalized_shape) == 1 and x.shape[-1] == norm.normalized_shape[0]
+            and _abi.query("mde_layernorm_workspace", max(1, x.numel() // x.shape[-1]),
+                           x.shape[-1])):
+        return _AddLayerNorm.apply(x, r, norm.weight, norm.bias, norm.eps)
+    s = x + r
+    return s, norm(s)
+
+
 class LayerNorm(nn.LayerNorm):
     """nn.LayerNorm over the last axis on the HIP kernel (same parameters and keys)."""
 
@@ -364,11 +422,24 @@ class CRFBlock(nn.Module):
 
     def forward(self, x, v, mask_matrix=None):
         """x: [B, H*W, C]; v: [B, H, W, C]; the shift mask is computed in-kernel."""
+        x1, m = self.forward_pending(x, None, v)
+        return x1 + m
+
+    def forward_pending(self, x, pending, v):
+        """This block on x + pending (the previous block's MLP branch, not yet
+        added): returns (x1, m) with the block's output x1 + m left un-added,
+        so that the next LayerNorm adds it in its own pass (add_layer_norm).
+        Same arithmetic as forward (reference :229-257)."""
         b, l, c = x.shape
         h, w = self.H, self.W
         assert l == h * w, "input feature has wrong size"
-        x = x + self.attn.forward_tokens(self.norm1(x), v, h, w, self.shift_size)
-        return x + self.mlp(self.norm2(x))
+        if pending is None:
+            n1 = self.norm1(x)
+        else:
+            x, n1 = add_layer_norm(x, pending, self.norm1)
+        a = self.attn.forward_tokens(n1, v, h, w, self.shift_size)
+        x1, n2 = add_layer_norm(x, a, self.norm2)
+        return x1, self.mlp(n2)
 
 
 class BasicCRFLayer(nn.Module):
@@ -391,10 +462,22 @@ class BasicCRFLayer(nn.Module):
             for i in range(depth)])
         self.downsample = downsample(dim=dim, norm_layer=norm_layer) if downsample is not None else None
 
-    def forward(self, x, v, H, W):  # noqa: N803
+    def _run(self, x, v, H, W):  # noqa: N803
+        pending = None
         for blk in self.blocks:
             blk.H, blk.W = H, W
-            x = blk(x, v)
+            x, pending = blk.forward_pending(x, pending, v)
+        return x, pending
+
+    def forward_norm(self, x, v, H, W, norm):  # noqa: N803
+        """norm(self(x, v, H, W)[0]) with the last residual add inside the norm's pass."""
+        x, pending = self._run(x, v, H, W)
+        return norm(x) if pending is None else add_layer_norm(x, pending, norm)[1]
+
+    def forward(self, x, v, H, W):  # noqa: N803
+        x, pending = self._run(x, v, H, W)
+        if pending is not None:
+            x = x + pending
         if self.downsample is not None:
             return x, H, W, self.downsample(x, H, W), (H + 1) // 2, (W + 1) // 2
         return x, H, W, x, H, W
@@ -430,5 +513,6 @@ class NewCRF(nn.Module):
         b, c, h, w = x.shape
         tokens = nchw_to_tokens(x)
         v_nhwc = nchw_to_tokens(v).view(b, h, w, -1)
-        x_out, h, w, _, _, _ = self.crf_layer(tokens, v_nhwc, h, w)
-        return tokens_to_nchw(self.norm_crf(x_out), h, w)
+        # crf_layer then norm_crf (reference :430-434), the last residual add
+        # inside norm_crf's pass
+        return tokens_to_nchw(self.crf_layer.forward_norm(tokens, v_nhwc, h, w, self.norm_crf), h, w)

@@ -140,6 +140,38 @@ def test_layernorm_matches_aten(rows, c):
     close_scaled(ln.bias.grad, ref.bias.grad, 1e-4, "gbeta")
 
 
+@pytest.mark.parametrize("rows,c", [(307200, 128), (37, 512), (4800, 1024), (50, 192)])
+def test_add_layernorm_bitwise_vs_separate_add(rows, c):
+    """add_layer_norm (one HIP pass: s = x + r and LayerNorm(s); the backward
+    adds s's residual gradient in its epilogue) == ATen's add + the HIP
+    LayerNorm + autograd's accumulation, bitwise: same fp32 operations."""
+    from monocular_depth_estimation_amd import newcrf_layers as nl
+    ln = nl.LayerNorm(c).to(DEV)
+    with torch.no_grad():
+        ln.weight.copy_(torch.from_numpy(seeded((c,), 1, 0.5, 1.5)))
+        ln.bias.copy_(torch.from_numpy(seeded((c,), 2, -0.5, 0.5)))
+    x0 = torch.from_numpy(seeded((rows, c), 3, -2, 3)).to(DEV)
+    r0 = torch.from_numpy(seeded((rows, c), 5, -1, 1)).to(DEV)
+    gs = torch.from_numpy(seeded((rows, c), 6, -1, 1)).to(DEV)
+    gy = torch.from_numpy(seeded((rows, c), 4, -1, 1)).to(DEV)
+    outs = []
+    for fused in (True, False):
+        old = nl.LN_ADD
+        nl.LN_ADD = fused
+        try:
+            ln.weight.grad = ln.bias.grad = None
+            x = x0.clone().requires_grad_(True)
+            r = r0.clone().requires_grad_(True)
+            s, y = nl.add_layer_norm(x, r, ln)
+            torch.autograd.backward([s, y], [gs, gy])
+            outs.append((s.detach(), y.detach(), x.grad, r.grad, ln.weight.grad.clone(),
+                         ln.bias.grad.clone()))
+        finally:
+            nl.LN_ADD = old
+    for a, b, name in zip(outs[0], outs[1], ("s", "y", "gx", "gr", "ggamma", "gbeta")):
+        assert torch.equal(a, b), name
+
+
 @pytest.mark.parametrize("shape", [(2, 24, 120, 160), (3, 1024, 15, 20), (1, 5, 7, 3)])
 def test_token_transposes_bit_exact(shape):
     from monocular_depth_estimation_amd.newcrf_layers import nchw_to_tokens, tokens_to_nchw

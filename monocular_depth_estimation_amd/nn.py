@@ -400,6 +400,7 @@ CONV3X3_HIP = {
 }
 WIDE_WGRAD_ALL = os.environ.get("MDE_WIDE_WGRAD", "1") != "0"
 WIDE_PAD = os.environ.get("MDE_WIDE_PAD", "1") != "0"  # A/B: 0 = padded shapes on MIOpen
+WINO_MIN_BLOCKS = int(os.environ.get("MDE_WINO_MIN_BLOCKS", "256"))  # smallest Winograd grid taken
 if WIDE_WGRAD_ALL:
     CONV3X3_HIP.update({(64, 64): (False, False, True), (128, 64): (False, False, True),
                         (128, 128): (False, False, True), (256, 256): (False, False, True)})
@@ -819,7 +820,7 @@ def conv3x3_passes(conv: nn.Conv2d, x):
             bp = b if b == 16 else -(-b // 32) * 32  # output channels as padded
             blocks = n * -(-h // 8) * -(-w // 16) * (bp // (64 if bp % 64 == 0 else 32))
             aligned = b % (32 if WINO32 else 64) == 0 and a % 16 == 0
-            if (not p[i] and (aligned or (WINO_PAD and b > 16)) and blocks >= 256
+            if (not p[i] and (aligned or (WINO_PAD and b > 16)) and blocks >= WINO_MIN_BLOCKS
                     and _abi.query("mde_wino_supported", a, b, h, w, _abi.MDE_F32)):
                 p[i] = WINO
     if dt == _abi.MDE_F32 and C3_WIDE and not _autocast_bf16(x):

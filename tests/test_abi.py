@@ -128,3 +128,23 @@ def test_convbf_supported_at_batch():
         assert lib.mde_convbf_supported_n(32, *args, p) == 1
         assert lib.mde_convbf_supported_n(1 << 22, *args, p) == 0
     assert lib.mde_convbf_supported_n(0, *args, 0) == 0
+
+
+def test_round6_shape_queries():
+    """Host-side shape rules of the round-6 entries (no GPU needed): the Linear
+    weight gradient (t % 16, m and n % 128), the per-channel sum (hw % 4), the
+    one-output-channel head conv (w % 4), the padded 1x1 / wide-wgrad shapes."""
+    from monocular_depth_estimation_amd import _abi
+    lib = _abi.load()
+    assert lib.mde_linear_wgrad_workspace(307200, 128, 512) > 0
+    for t, m, n in ((100, 128, 128), (160, 96, 128), (160, 128, 200), (0, 128, 128)):
+        assert lib.mde_linear_wgrad_workspace(t, m, n) == 0
+    assert lib.mde_chansum_workspace(16, 128, 19200) > 0
+    assert lib.mde_chansum_workspace(16, 128, 19202) == 0
+    assert lib.mde_head_conv_supported(16, 128, 120, 160) == 1
+    assert lib.mde_head_conv_supported(16, 128, 120, 162) == 0
+    assert lib.mde_conv1x1_supported(24, 72, 120, 160, 1, 0) == 1  # MobileNetV3, padded
+    assert lib.mde_conv1x1_supported(12, 72, 120, 160, 1, 0) == 0
+    assert lib.mde_conv3x3_wgrad_workspace(2, 24, 128, 120, 160, 0) > 0  # padded to 32
+    assert lib.mde_conv3x3_wgrad_workspace(2, 24, 128, 120, 48, 0) == 0  # not a strip width
+    assert lib.mde_layernorm_workspace(307200, 128) > 0

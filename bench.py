@@ -320,6 +320,8 @@ def main():
     from monocular_depth_estimation_amd import _abi
     from monocular_depth_estimation_amd.train import Trainer, make_adam, synthetic_batch, wrap_ddp
     torch.backends.cudnn.benchmark = bool(args.cudnn_benchmark)
+    from monocular_depth_estimation_amd import gemm_table
+    gemm_path = gemm_table.enable()  # the vendor GEMMs' tuned solution table
     from monocular_depth_estimation_amd import GuideDepth
     from monocular_depth_estimation_amd.loss import SSIML1
 
@@ -511,6 +513,7 @@ def main():
         "execution": ("hipGraph replay of the whole step (GraphTrainer)" if use_graph
                       else "eager (Trainer + DDP)"),
         "dp_exchange": dp_exchange,
+        "gemm_table": os.path.relpath(gemm_path, REPO) if gemm_path else None,
         "params_in_sync": in_sync,
         "roofline": roofline,
         "roofline_leaders": leaders,

@@ -681,6 +681,9 @@ def main(argv=None):
     args = build_parser().parse_args(argv)
     world = init_world()
     from . import GuideDepth  # noqa: E402  (loads the HIP library)
+    from . import gemm_table
+    if world.device.type == "cuda":
+        gemm_table.enable()  # the vendor GEMMs' tuned solution table
     from .loss import SSIML1
 
     torch.manual_seed(args.seed)

@@ -100,3 +100,25 @@ def test_chansum_vs_float64(n, c, h, w):
     assert float((outs[0].double() - ref).abs().max()) <= tol
     assert torch.equal(outs[0], outs[1])
     assert _abi.query("mde_chansum_workspace", n, c, 6) == 0  # hw % 4 != 0
+
+
+def test_gemm_table_loads_on_this_image():
+    """The shipped TunableOp solution table (gemm_table.py) passes TunableOp's
+    validators on this image (PyTorch / HIP / hipBLASLt / rocBLAS / gfx950) and
+    a listed shape (cfg4's 1/32-stage fc2, [4800, 4096] x [4096, 1024]^T + b)
+    gives the default GEMM's result to fp32 accumulation-order tolerance."""
+    import torch.nn.functional as F
+    from monocular_depth_estimation_amd import gemm_table
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    x = torch.randn((4800, 4096), device=DEV, generator=gen)
+    w = torch.randn((1024, 4096), device=DEV, generator=gen) * 0.02
+    b = torch.randn((1024,), device=DEV, generator=gen)
+    ref = F.linear(x.double(), w.double(), b.double())
+    was = torch.cuda.tunable.is_enabled()
+    try:
+        assert gemm_table.enable() == gemm_table.TABLE
+        y = F.linear(x, w, b)
+    finally:
+        torch.cuda.tunable.enable(was)
+    err = float((y.double() - ref).abs().max() / ref.abs().max())
+    assert err <= 1e-5, err

@@ -49,9 +49,11 @@ def _wgrad(g2, x2, bias: bool):
     same reads), or None when the shape is not one it takes."""
     t, m = g2.shape
     n = x2.shape[1]
-    if m * n > 32 * 128 * 128:
-        # >= 64 output tiles: hipBLASLt's GEMM fills the chip without a split
-        # and runs 0.92-0.95 of the fp32 MFMA peak there (tools/lin_bench.py)
+    if m * n > 16 * 128 * 128:
+        # > 16 output tiles: the library GEMM (with the TunableOp table,
+        # gemm_table.py) fills the chip without a split and wins from 32
+        # tiles on (19200 x 1024 x 512: 164 vs 188 us; tools/lin_bench.py,
+        # profiles/r06_lin_wgrad.txt)
         return None
     nbytes = _abi.query("mde_linear_wgrad_workspace", t, m, n) if LIN_WGRAD else 0
     if not nbytes:

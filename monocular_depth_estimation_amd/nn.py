@@ -689,10 +689,13 @@ class _Conv1x1(torch.autograd.Function):
         weight = weight.contiguous()
         ctx.save_for_backward(x, weight)
         ctx.stride = stride
-        if stride == 1:
+        cin, cout = x.shape[1], weight.shape[0]
+        if stride == 1 and not (C1_FWD == "all" or (C1_FWD == "pad" and (cin % 32 or cout % 32))):
             # MIOpen runs the stride-1 forward as one NCHW GEMM (rocBLAS, no
-            # transposes), as fast or faster than the HIP kernel at these
-            # shapes (tools/c1_bench.py): only its backward needs replacing
+            # transposes), as fast or faster than the HIP kernel at DDRNet's
+            # shapes (tools/c1_bench.py): only its backward needs replacing.
+            # Channel counts off the 32 grid (MobileNetV3's) take the HIP
+            # forward: MIOpen picks its Winograd / NHWC solvers there
             return torch.nn.functional.conv2d(x, weight)
         n, cin, h, w = x.shape
         cout = weight.shape[0]
@@ -725,6 +728,7 @@ class _Conv1x1(torch.autograd.Function):
 
 C1_WIDE = os.environ.get("MDE_C1_WIDE", "1") != "0"  # MDE_C1_WIDE=0: MIOpen (A/B switch)
 C1_PAD = os.environ.get("MDE_C1_PAD", "1") != "0"  # A/B: 0 = only channel counts % 32 (round 5)
+C1_FWD = os.environ.get("MDE_C1_FWD", "pad")  # stride-1 HIP forward: pad (off-grid channels) / all / none
 
 
 def conv1x1_ok(conv: nn.Conv2d, x) -> bool:

@@ -63,6 +63,15 @@ def main():
                 "miopen" in ev.name.lower() or "transpose" in ev.name.lower()
                 or "Sp3" in ev.name or "naive_conv" in ev.name):
             kern[ev.name[:90]] += ev.device_time_total
+    # which CPU op launched each vendor conv kernel (innermost op with the kernel)
+    owners = collections.Counter()
+    for ev in prof.events():
+        for k in getattr(ev, "kernels", []) or []:
+            if "miopen" in k.name.lower() or "Sp3" in k.name or "igemm" in k.name:
+                owners[(ev.name, str(ev.input_shapes)[:120], k.name[:48])] += 1
+    print("vendor conv kernels by launching op:")
+    for (op, shapes, kn), c in owners.most_common(args.top):
+        print(f"{c:4d}x  {op:28s} {kn:48s} {shapes}")
     print("vendor conv / transpose kernels:")
     for name, t in kern.most_common(args.top):
         print(f"{t / 1e3:8.3f} ms  {name}")

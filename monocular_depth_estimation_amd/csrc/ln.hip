@@ -15,6 +15,8 @@
 // Algorithmic HBM bytes: LN fwd 8 per element (+8 per row), LN bwd 12 per
 // element, transpose 8 per element.
 
+#include <cstdlib>
+
 #include "common.h"
 
 namespace mde {
@@ -229,6 +231,40 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// The same transpose with 16-byte global accesses (m % 4 == 0, n % 4 == 0:
+// every NewCRF token / channel count): a thread moves 4 float4 in and 4
+// float4 out per 64 x 64 tile (the scalar kernel: 16 + 16 four-byte
+// accesses).  LDS rows of 68 floats: the float4 stores are 16-byte aligned,
+// the column reads at most 2-way conflicted.
+__global__ void __launch_bounds__(256)
+    transpose4_kernel(const float* __restrict__ x, float* __restrict__ y, int64_t m, int64_t n) {
+  constexpr int P = 68;
+  __shared__ __attribute__((aligned(16))) float t[64 * P];
+  const int64_t b = blockIdx.z;
+  const int64_t i0 = (int64_t)blockIdx.y * 64, j0 = (int64_t)blockIdx.x * 64;
+  const float* xp = x + b * m * n;
+  float* yp = y + b * m * n;
+  const int c4 = threadIdx.x & 15, rr = threadIdx.x >> 4;  // float4 column, row within 16
+  float4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // all four loads in flight
+    const int64_t i = i0 + rr + 16 * k, j = j0 + 4 * c4;
+    v[k] = i < m && j < n ? *reinterpret_cast<const float4*>(xp + i * n + j)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) *reinterpret_cast<float4*>(t + (rr + 16 * k) * P + 4 * c4) = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int jr = rr + 16 * k;  // y row j0 + jr, columns i0 + 4 c4 .. + 3
+    const int64_t j = j0 + jr, i = i0 + 4 * c4;
+    const float4 o = make_float4(t[(4 * c4) * P + jr], t[(4 * c4 + 1) * P + jr],
+                                 t[(4 * c4 + 2) * P + jr], t[(4 * c4 + 3) * P + jr]);
+    if (i < m && j < n) *reinterpret_cast<float4*>(yp + j * m + i) = o;
+  }
+}
+
 template <int VPL>
 int ln_fwd_launch(const float* x, const float* g, const float* b, float* y, float* mu,
                   float* rs, int64_t rows, float eps, hipStream_t st, const float* r = nullptr,
@@ -378,6 +414,15 @@ int mde_transpose(const void* x, void* y, int64_t batch, int64_t m, int64_t n, i
     return MDE_ERR_INVALID_ARG;
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid((unsigned)cdiv(n, 64), (unsigned)cdiv(m, 64), (unsigned)batch);
+  static const bool vec = [] {
+    const char* e = std::getenv("MDE_TRANSPOSE4");
+    return !(e && e[0] == '0');
+  }();
+  if (vec && m % 4 == 0 && n % 4 == 0) {
+    MDE_LAUNCH(K_TRANSPOSE, 8.0 * batch * m * n, st, transpose4_kernel, grid, dim3(256), 0,
+               (const float*)x, (float*)y, m, n);
+    return 0;
+  }
   MDE_LAUNCH(K_TRANSPOSE, 8.0 * batch * m * n, st, transpose_kernel, grid, dim3(256), 0,
              (const float*)x, (float*)y, m, n);
   return 0;

@@ -172,7 +172,8 @@ def test_add_layernorm_bitwise_vs_separate_add(rows, c):
         assert torch.equal(a, b), name
 
 
-@pytest.mark.parametrize("shape", [(2, 24, 120, 160), (3, 1024, 15, 20), (1, 5, 7, 3)])
+@pytest.mark.parametrize("shape", [(2, 24, 120, 160), (3, 1024, 15, 20), (1, 5, 7, 3), (2, 40, 7, 12),
+                                   (1, 72, 9, 20)])
 def test_token_transposes_bit_exact(shape):
     from monocular_depth_estimation_amd.newcrf_layers import nchw_to_tokens, tokens_to_nchw
     b, c, h, w = shape

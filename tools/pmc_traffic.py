@@ -110,7 +110,7 @@ NAMES = [
     (r"ln_fwd_kernel", "layernorm_fwd"),
     (r"ln_bwd_kernel", "layernorm_bwd"),
     (r"ln_wreduce_kernel", "layernorm_wreduce"),
-    (r"transpose_kernel", "transpose"),
+    (r"transpose4?_kernel", "transpose"),
     (r"colsum_part_kernel<true>", "gelu_bwd_bias_grad"),
     (r"colsum_(part_kernel<false>|final_kernel)", "linear_bias_grad"),
     # forward and data gradient run the same kernel (as wino_f23_kernel)

@@ -37,38 +37,58 @@ __device__ __forceinline__ void row6(const float* __restrict__ plane, int r, int
   v[5] = q0 + 4 < w ? row[q0 + 4] : 0.f;
 }
 
+// block = 64 pixel quads x 4 channel groups (wave g sums channels g, g + 4,
+// ...): 4x the threads of one-quad-per-thread (the 128-channel loop per
+// thread left a 300-block grid latency-bound at 1.3 TB/s); the four partial
+// sums combine through LDS in a fixed order
 __global__ void __launch_bounds__(256)
     head_fwd_kernel(const float* __restrict__ x, const float* __restrict__ wt,
                     const float* __restrict__ bias, float* __restrict__ y, int n, int c, int h,
                     int w) {
-  const int w4 = w >> 2;
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (t >= (int64_t)n * h * w4) return;
-  const int q0 = 4 * (int)(t % w4);
-  const int64_t rt = t / w4;
+  __shared__ float4 red[4][64];
+  const int w4 = w >> 2, qd = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 64 + qd;
+  const bool live = t < (int64_t)n * h * w4;
+  const int64_t tc = live ? t : 0;
+  const int q0 = 4 * (int)(tc % w4);
+  const int64_t rt = tc / w4;
   const int r = (int)(rt % h), img = (int)(rt / h);
   const int64_t hw = (int64_t)h * w;
   const float* xb = x + (int64_t)img * c * hw;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (live) {
 #pragma unroll 2
-  for (int ch = 0; ch < c; ++ch) {
-    const float* plane = xb + ch * hw;
-    const float* wc = wt + ch * 9;
+    for (int ch = grp; ch < c; ch += 4) {
+      const float* plane = xb + ch * hw;
+      const float* wc = wt + ch * 9;
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      float v[6];
-      row6(plane, r + dy - 1, q0, h, w, v);
+      for (int dy = 0; dy < 3; ++dy) {
+        float v[6];
+        row6(plane, r + dy - 1, q0, h, w, v);
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const float k = wc[dy * 3 + dx];
+        for (int dx = 0; dx < 3; ++dx) {
+          const float k = wc[dy * 3 + dx];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[j] = fmaf(k, v[j + dx], acc[j]);
+          for (int j = 0; j < 4; ++j) acc[j] = fmaf(k, v[j + dx], acc[j]);
+        }
       }
     }
   }
+  red[grp][qd] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  __syncthreads();
+  if (grp != 0 || !live) return;
   const float b = bias ? bias[0] : 0.f;
+  float4 s = red[0][qd];
+#pragma unroll
+  for (int k = 1; k < 4; ++k) {
+    const float4 o = red[k][qd];
+    s.x += o.x;
+    s.y += o.y;
+    s.z += o.z;
+    s.w += o.w;
+  }
   *reinterpret_cast<float4*>(y + (int64_t)img * hw + (int64_t)r * w + q0) =
-      make_float4(acc[0] + b, acc[1] + b, acc[2] + b, acc[3] + b);
+      make_float4(s.x + b, s.y + b, s.z + b, s.w + b);
 }
 
 // gx for channels [blockIdx.y * kDgC, + kDgC): the gy neighbourhood once, then
@@ -188,7 +208,7 @@ int mde_head_conv_fwd(const void* x, const float* weight, const float* bias, voi
   hipStream_t s = (hipStream_t)stream;
   const int64_t threads = n * h * (w / 4);
   const double bytes = 4.0 * (double)n * h * w * (c + 1);
-  MDE_LAUNCH(mde::K_HEAD_FWD, bytes, s, head_fwd_kernel, dim3((unsigned)mde::cdiv(threads, 256)),
+  MDE_LAUNCH(mde::K_HEAD_FWD, bytes, s, head_fwd_kernel, dim3((unsigned)mde::cdiv(threads, 64)),
              dim3(256), 0, (const float*)x, weight, bias, (float*)y, (int)n, (int)c, (int)h,
              (int)w);
   return MDE_OK;

@@ -28,6 +28,10 @@ SHAPES = [(32, 64, 64, 60, 80), (32, 128, 128, 30, 40), (32, 256, 256, 15, 20),
 if "--newcrf" in sys.argv:  # cfg4's NewCRF proj_v / proj_x convs (bs 16, newcrf_layers.py:377-379)
     SHAPES = [(16, 64, 128, 120, 160), (16, 128, 256, 60, 80), (16, 256, 512, 30, 40),
               (16, 512, 1024, 15, 20), (16, 160, 1024, 15, 20)]
+ONLY = None  # --only n,c,co,h,w: that shape alone (profiling runs), no stride-2 sections
+if "--only" in sys.argv:
+    ONLY = tuple(int(v) for v in sys.argv[sys.argv.index("--only") + 1].split(","))
+    SHAPES = [ONLY]
 for (n, c, co, h, w) in SHAPES:
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
     gy = torch.rand((n, co, h, w), device="cuda") - 0.5
@@ -48,7 +52,7 @@ for (n, c, co, h, w) in SHAPES:
           f"MIOpen {tm:7.1f} us ({fl / tm / 1e6:5.1f} TF/s)  rel diff {err:.1e}", flush=True)
 
 # stride-2 stem convolutions (mde_conv3x3s2_wgrad) vs MIOpen (incl. its NHWC transposes)
-for (n, c, co, h, w) in ([] if "--newcrf" in sys.argv else [(32, 3, 32, 480, 640), (32, 32, 32, 240, 320)]):
+for (n, c, co, h, w) in ([] if "--newcrf" in sys.argv or ONLY else [(32, 3, 32, 480, 640), (32, 32, 32, 240, 320)]):
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     gy = torch.rand((n, co, ho, wo), device="cuda") - 0.5
@@ -70,7 +74,7 @@ for (n, c, co, h, w) in ([] if "--newcrf" in sys.argv else [(32, 3, 32, 480, 640
           f"{gb / th * 1e6:6.0f} GB/s)  MIOpen {tm:7.1f} us  rel diff {err:.1e}", flush=True)
 
 # stride-2 wide weight gradients (DDRNet's stride-2 BasicBlock convs, down3 / down4)
-for (n, c, co, h, w) in [(32, 32, 64, 120, 160), (32, 64, 128, 60, 80), (32, 128, 256, 30, 40)]:
+for (n, c, co, h, w) in ([] if ONLY else [(32, 32, 64, 120, 160), (32, 64, 128, 60, 80), (32, 128, 256, 30, 40)]):
     x = torch.rand((n, c, h, w), device="cuda") - 0.5
     ho, wo = (h - 1) // 2 + 1, (w - 1) // 2 + 1
     gy = torch.rand((n, co, ho, wo), device="cuda") - 0.5

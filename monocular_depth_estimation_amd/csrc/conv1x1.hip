@@ -23,6 +23,8 @@
 // product over all pixels: block tiles of (co, ci), the pixel range split
 // over blocks (split-K), per-block partials in a slab summed in block order
 // by a second kernel (deterministic, no atomics).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace {
@@ -404,6 +406,160 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
+// ------------------------------------------- weight gradient, small channel counts
+// G[co][ci] for stride-1 convs whose whole (co, ci) block is a few 16 x 16
+// MFMA tiles (MobileNetV3's expand / project 1x1s: 16..120 channels,
+// mobilenetv3.py LARGE) -- HBM-bound, where the 128 x 32 tiles of
+// c1_wgrad_kernel multiplied up to 4x padding and re-staged gy rows.  No LDS
+// staging: wave = a 16 * MT x 16 * NT block of G over chunks of 16 pixels of
+// one image (Q % 16 == 0); lane (l16, g4) loads 4 consecutive pixels of gy row
+// co = 16 i + l16 and of x row ci = 16 j + l16 as float4 (16 rows x 64 B per
+// load) and feeds them to v_mfma_f32_16x16x4_f32 k-step by k-step (MFMA k =
+// g4 at step s <-> pixel 4 g4 + s, the same map on both operands).  The 4
+// waves of a block sum through LDS in a fixed order into one partial row per
+// block; c1_wreduce_kernel sums the rows in a fixed order.
+using f4v = float __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f4v mfma16(float a, float b, f4v c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int MT, int NT>
+__global__ void __launch_bounds__(256)
+    c1_wgrad_small_kernel(const float* __restrict__ gy, const float* __restrict__ x,
+                          float* __restrict__ part, int CO, int CI, int Q, int64_t nchunks,
+                          int64_t per_block, int groups_ci) {
+  __shared__ f4v red[3][MT * NT][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
+  const int gco = blockIdx.y / groups_ci, gci = blockIdx.y - gco * groups_ci;
+  const int co0 = gco * 16 * MT, ci0 = gci * 16 * NT;
+  const int64_t c0 = (int64_t)blockIdx.x * per_block;
+  const int64_t c1 = c0 + per_block < nchunks ? c0 + per_block : nchunks;
+  f4v acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4v{0.f, 0.f, 0.f, 0.f};
+  // rows past CO / CI read row 0 (a real address) and are zeroed
+  bool aok[MT], bok[NT];
+  int64_t aoff[MT], boff[NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int co = co0 + 16 * i + l16;
+    aok[i] = co < CO;
+    aoff[i] = (int64_t)(aok[i] ? co : 0) * Q;
+  }
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int ci = ci0 + 16 * j + l16;
+    bok[j] = ci < CI;
+    boff[j] = (int64_t)(bok[j] ? ci : 0) * Q;
+  }
+  const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll 1
+  for (int64_t c = c0 + wv; c < c1; c += 4) {
+    const int64_t p0 = c * 16;
+    const int64_t img = p0 / Q;
+    const int64_t q = p0 - img * Q + 4 * g4;
+    const float* gb = gy + img * CO * Q + q;
+    const float* xb = x + img * CI * Q + q;
+    float4 a[MT], b[NT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const float4 t = *reinterpret_cast<const float4*>(gb + aoff[i]);
+      a[i] = aok[i] ? t : z;
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float4 t = *reinterpret_cast<const float4*>(xb + boff[j]);
+      b[j] = bok[j] ? t : z;
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        acc[i][j] = mfma16(a[i].x, b[j].x, acc[i][j]);
+        acc[i][j] = mfma16(a[i].y, b[j].y, acc[i][j]);
+        acc[i][j] = mfma16(a[i].z, b[j].z, acc[i][j]);
+        acc[i][j] = mfma16(a[i].w, b[j].w, acc[i][j]);
+      }
+  }
+  if (wv > 0) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) red[wv - 1][i * NT + j][lane] = acc[i][j];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  float* out = part + (int64_t)blockIdx.x * CO * CI;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      f4v t = acc[i][j];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) t += red[k][i * NT + j][lane];  // waves in order
+      const int ci = ci0 + 16 * j + l16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + 16 * i + 4 * g4 + r;  // D[4 g4 + r][l16]
+        if (co < CO && ci < CI) out[(int64_t)co * CI + ci] = t[r];
+      }
+    }
+}
+
+struct SmallWg {
+  int mt, nt, groups_ci, groups;
+  int64_t nchunks, per_block, blocks;
+};
+
+inline bool c1_small_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_C1_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// the small-channel path: stride 1, Q % 16 == 0, at most 8 MFMA tiles a wave
+// and 3 wave groups (co / ci up to ~128 x 48)
+inline bool small_plan(int64_t n, int64_t ci, int64_t co, int64_t q, SmallWg* p) {
+  if (!c1_small_on() || q % 16) return false;
+  if (ci % 32 == 0 && co % 32 == 0) return false;  // the 32-grid shapes keep c1_wgrad_kernel
+  const int co16 = (int)mde::cdiv(co, 16), ci16 = (int)mde::cdiv(ci, 16);
+  if (co16 * ci16 > 24) return false;
+  // wave tile MT x NT (MT * NT <= 8, MT, NT in {1, 2, 4, 8}) covering the
+  // most of (co16, ci16) with the fewest groups
+  int bm = 0, bn = 0, best = 1 << 30;
+  for (int mt : {1, 2, 4, 8})
+    for (int nt : {1, 2, 4, 8}) {
+      if (mt * nt > 8) continue;
+      const int g = (int)(mde::cdiv(co16, mt) * mde::cdiv(ci16, nt));
+      const int waste = g * mt * nt;  // tiles computed
+      if (g <= 3 && waste < best) {
+        best = waste;
+        bm = mt;
+        bn = nt;
+      }
+    }
+  if (!bm) return false;
+  p->mt = bm;
+  p->nt = bn;
+  p->groups_ci = (int)mde::cdiv(ci16, bn);
+  p->groups = (int)mde::cdiv(co16, bm) * p->groups_ci;
+  p->nchunks = n * q / 16;
+  int64_t blocks = 512 / p->groups;  // one partial row a block, summed by c1_wreduce_kernel
+  if (blocks > p->nchunks / 4) blocks = p->nchunks / 4 > 1 ? p->nchunks / 4 : 1;
+  p->per_block = mde::cdiv(p->nchunks, blocks);
+  p->blocks = mde::cdiv(p->nchunks, p->per_block);
+  return true;
+}
+
+inline size_t small_ws_bytes(const SmallWg& p, int64_t ci, int64_t co) {
+  return sizeof(float) * (size_t)(p.blocks * ci * co);
+}
+
 // ------------------------------------------------------------------- plans
 inline bool c1_shape_ok(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, int stride) {
   if (n <= 0 || h <= 0 || w <= 0 || (stride != 1 && stride != 2)) return false;
@@ -536,6 +692,8 @@ size_t mde_conv1x1_wgrad_workspace(int64_t n, int64_t cin, int64_t cout, int64_t
                                    int stride, int dtype) {
   if (dtype != MDE_F32 || !c1_shape_ok(n, cin, cout, h, w, stride)) return 0;
   const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  SmallWg sp;
+  if (stride == 1 && small_plan(n, cin, cout, ho * wo, &sp)) return small_ws_bytes(sp, cin, cout);
   const WgPlan p = wg_plan(n, cin, cout, ho, wo);
   return sizeof(float) * (size_t)p.ksplit * (size_t)(cin * cout);
 }
@@ -548,6 +706,27 @@ int mde_conv1x1_wgrad(const void* gy, const void* x, float* gweight, int64_t n, 
   if (!c1_shape_ok(n, cin, cout, h, w, stride)) return MDE_ERR_UNSUPPORTED;
   hipStream_t s = (hipStream_t)stream;
   const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
+  SmallWg sp;
+  if (stride == 1 && small_plan(n, cin, cout, ho * wo, &sp)) {
+    const double flops = 2.0 * n * ho * wo * (double)cin * cout;
+    const double bytes = 4.0 * n * (double)ho * wo * (cin + cout);
+    float* part = (float*)workspace;
+    const int64_t E = cin * cout;
+    const dim3 grid((unsigned)sp.blocks, (unsigned)sp.groups);
+#define MDE_WGS(MTv, NTv)                                                                          \
+  if (sp.mt == MTv && sp.nt == NTv)                                                                \
+    MDE_LAUNCH_MFMA(mde::K_C1_WGRAD, bytes, flops, s, (c1_wgrad_small_kernel<MTv, NTv>), grid,     \
+                    dim3(256), 0, (const float*)gy, (const float*)x, part, (int)cout, (int)cin,    \
+                    (int)(ho * wo), sp.nchunks, sp.per_block, sp.groups_ci);
+    MDE_WGS(1, 1) else MDE_WGS(1, 2) else MDE_WGS(1, 4) else MDE_WGS(1, 8)
+    else MDE_WGS(2, 1) else MDE_WGS(2, 2) else MDE_WGS(2, 4)
+    else MDE_WGS(4, 1) else MDE_WGS(4, 2) else MDE_WGS(8, 1) else return MDE_ERR_UNSUPPORTED;
+#undef MDE_WGS
+    MDE_LAUNCH(mde::K_C1_WREDUCE, 4.0 * E * (sp.blocks + 1), s, c1_wreduce_kernel,
+               dim3((unsigned)mde::cdiv(E / 4, 64)), dim3(1024), 0, (const float*)part, gweight, E,
+               (int)sp.blocks);
+    return MDE_OK;
+  }
   const WgPlan p = wg_plan(n, cin, cout, ho, wo);
   const int64_t total = (int64_t)p.cotiles * p.citiles * p.ksplit;
   const dim3 grid(xcd_grid(total)), block(256);

@@ -77,7 +77,10 @@ def test_conv1x1_vs_float64_oracle(cin, cout, stride, h, w):
 
 
 @pytest.mark.parametrize("cin,cout,stride,h,w", [(32, 64, 2, 120, 160), (64, 128, 1, 60, 80),
-                                                 (640, 128, 1, 8, 10)])
+                                                 (640, 128, 1, 8, 10),
+                                                 # the small-channel weight-gradient path
+                                                 (16, 64, 1, 240, 320), (72, 24, 1, 120, 160),
+                                                 (120, 40, 1, 60, 80), (64, 64, 1, 60, 80)])
 def test_conv1x1_full_batch_vs_miopen_and_deterministic(cin, cout, stride, h, w):
     """cfg2 batch (32): HIP vs MIOpen fp32 on the GPU for all three passes, and
     two runs bitwise equal (the weight gradient's fixed-order reduction)."""

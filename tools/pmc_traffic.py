@@ -74,7 +74,7 @@ NAMES = [
     (r"ssim3_(l1|stream|pair)_kernel", "ssim3_l1"),
     (r"cm_kernel<[^>]*false>", "conv1x1_fwd"),
     (r"cm_kernel<[^>]*true>", "conv1x1_dgrad"),
-    (r"c1_wgrad_kernel", "conv1x1_wgrad"),
+    (r"c1_wgrad(_small)?_kernel", "conv1x1_wgrad"),
     (r"c1_wreduce_kernel", "conv1x1_wreduce"),
     (r"c3s2_fwd_kernel", "conv3x3s2_fwd"),
     (r"c3s2_dgrad_kernel", "conv3x3s2_dgrad"),

@@ -509,6 +509,128 @@ __global__ void __launch_bounds__(256)
     }
 }
 
+// ------------------------------------------------- small-channel channel mix
+// MobileNetV3's stride-1 expand / project convs (16 -> 64, 64 -> 24, 24 -> 72,
+// 72 -> 40, 40 -> 120, ... on 240x320 .. 60x80 planes) and their data
+// gradients: K and M <= 128, so cm_kernel's 32-row K chunks and 32..128-row M
+// tiles are mostly padding and its LDS staging of the pixel tile buys no
+// reuse.  Here one wave owns 64 consecutive pixels of one image and every
+// output channel: lane (l16, g4) loads the float4 in[k0 + g4][q0 + 4 l16 ..
+// + 3] (16 lanes read one 256-byte row segment), element t of it is the B
+// operand of pixel tile t (pixels 4 l16 + t), so the four accumulators of one
+// channel tile hold four consecutive pixels per lane and every output row is
+// one float4 store per lane.  A (the M x K weight, zero-padded to 16 MT rows)
+// sits in LDS as [k][m], pitch P with P mod 64 in {16, 48} (the four k rows of
+// one read land in distinct banks).  Accumulation order over k is fixed.
+template <int MT, bool TRANSA>
+__global__ void __launch_bounds__(256)
+    c1_mix_small_kernel(const float* __restrict__ in, const float* __restrict__ wt,
+                        float* __restrict__ out, int K, int M, int Q, int qchunks,
+                        int64_t total) {
+  constexpr int P = 16 * MT + (MT % 2 == 0 ? 16 : 0);
+  extern __shared__ float sw[];  // K x P
+  for (int e = threadIdx.x; e < K * P; e += 256) {
+    const int k = e / P, m = e - k * P;
+    float v = 0.f;
+    if (m < M) v = TRANSA ? wt[(int64_t)k * M + m] : wt[(int64_t)m * K + k];
+    sw[e] = v;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, l16 = lane & 15, g4 = lane >> 4;
+  const int64_t c = (int64_t)blockIdx.x * 4 + wv;
+  if (c >= total) return;
+  const int64_t img = c / qchunks;
+  const int q = (int)(c - img * qchunks) * 64 + 4 * l16;
+  const bool qok = q < Q;  // Q % 4 == 0: a float4 is all in or all out
+  const float* xb = in + img * K * Q + (qok ? q : 0);
+  f4v acc[MT][4];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    // (f4v, not float4: a select between float4 temporaries goes to scratch)
+    f4v b[8];
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      const int k = k0 + 4 * s + g4;  // K % 8 == 0: the step is all in or all out
+      const bool ok = qok && k0 + 4 * s < K;
+      const f4v t = *reinterpret_cast<const f4v*>(xb + (ok ? (int64_t)k * Q : 0));
+      b[s] = ok ? t : f4v{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      if (k0 + 4 * s < K) {
+        const float* pa = sw + (k0 + 4 * s + g4) * P + l16;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const float a = pa[16 * i];
+          acc[i][0] = mfma16(a, b[s][0], acc[i][0]);
+          acc[i][1] = mfma16(a, b[s][1], acc[i][1]);
+          acc[i][2] = mfma16(a, b[s][2], acc[i][2]);
+          acc[i][3] = mfma16(a, b[s][3], acc[i][3]);
+        }
+      }
+    }
+  }
+  if (!qok) return;
+  float* ob = out + img * M * Q + q;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * i + 4 * g4 + r;  // D[4 g4 + r][l16]
+      if (m < M)
+        *reinterpret_cast<float4*>(ob + (int64_t)m * Q) =
+            make_float4(acc[i][0][r], acc[i][1][r], acc[i][2][r], acc[i][3][r]);
+    }
+}
+
+inline bool c1_mix_small_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MDE_C1_MIX_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// c1_mix_small_kernel's M tiles for an (M, K) channel mix, or 0: stride 1,
+// M, K <= 128 off the 32 grid (DDRNet's 32-multiples keep cm_kernel), the
+// padded weight <= 32 KB of LDS.
+inline int mix_small_mt(int64_t M, int64_t K) {
+  if (!c1_mix_small_on() || M > 128 || K > 128 || (M % 32 == 0 && K % 32 == 0)) return 0;
+  const int mt = (int)mde::cdiv(M, 16);
+  const int p = 16 * mt + (mt % 2 == 0 ? 16 : 0);
+  return K * p <= 8192 ? mt : 0;
+}
+
+template <bool TRANSA>
+int launch_mix_small(int mt, const float* in, const float* wt, float* out, int64_t n, int64_t K,
+                     int64_t M, int64_t Q, int kid, double bytes, double flops, hipStream_t s) {
+  const int64_t qchunks = mde::cdiv(Q, 64), total = n * qchunks;
+  const dim3 grid((unsigned)mde::cdiv(total, 4)), block(256);
+  const size_t lds = sizeof(float) * (size_t)K * (16 * mt + (mt % 2 == 0 ? 16 : 0));
+#define MDE_MIX(MTv)                                                                           \
+  case MTv:                                                                                    \
+    MDE_LAUNCH_MFMA(kid, bytes, flops, s, (c1_mix_small_kernel<MTv, TRANSA>), grid, block, lds, \
+                    in, wt, out, (int)K, (int)M, (int)Q, (int)qchunks, total);                 \
+    return MDE_OK;
+  switch (mt) {
+    MDE_MIX(1)
+    MDE_MIX(2)
+    MDE_MIX(3)
+    MDE_MIX(4)
+    MDE_MIX(5)
+    MDE_MIX(6)
+    MDE_MIX(7)
+    MDE_MIX(8)
+    default:
+      return MDE_ERR_UNSUPPORTED;
+  }
+#undef MDE_MIX
+}
+
 struct SmallWg {
   int mt, nt, groups_ci, groups;
   int64_t nchunks, per_block, blocks;
@@ -663,9 +785,13 @@ int mde_conv1x1_fwd(const void* x, const float* weight, void* y, int64_t n, int6
   const int64_t ho = (h - 1) / stride + 1, wo = (w - 1) / stride + 1;
   const double flops = 2.0 * n * ho * wo * (double)cin * cout;
   const double bytes = 4.0 * n * (double)ho * wo * (cin + cout);
-  if (stride == 1)
+  if (stride == 1) {
+    if (const int mt = mix_small_mt(cout, cin))
+      return launch_mix_small<false>(mt, (const float*)x, weight, (float*)y, n, cin, cout, ho * wo,
+                                     mde::K_C1_FWD, bytes, flops, s);
     return launch_cm<1, 1, false>((const float*)x, weight, (float*)y, n, cin, cout, h, w, ho, wo,
                                   ho, wo, mde::K_C1_FWD, bytes, flops, s);
+  }
   return launch_cm<2, 1, false>((const float*)x, weight, (float*)y, n, cin, cout, h, w, ho, wo,
                                 ho, wo, mde::K_C1_FWD, bytes, flops, s);
 }
@@ -681,9 +807,13 @@ int mde_conv1x1_bwd_data(const void* gy, const float* weight, void* gx, int64_t 
   const double flops = 2.0 * n * ho * wo * (double)cin * cout;
   const double bytes = 4.0 * n * ((double)ho * wo * cout + (double)h * w * cin);
   // GEMM K = cout (gy's channels), M = cin; gy is a ho x wo plane
-  if (stride == 1)
+  if (stride == 1) {
+    if (const int mt = mix_small_mt(cin, cout))
+      return launch_mix_small<true>(mt, (const float*)gy, weight, (float*)gx, n, cout, cin, ho * wo,
+                                    mde::K_C1_DGRAD, bytes, flops, s);
     return launch_cm<1, 1, true>((const float*)gy, weight, (float*)gx, n, cout, cin, ho, wo, ho,
                                  wo, h, w, mde::K_C1_DGRAD, bytes, flops, s);
+  }
   return launch_cm<1, 2, true>((const float*)gy, weight, (float*)gx, n, cout, cin, ho, wo, ho, wo,
                                h, w, mde::K_C1_DGRAD, bytes, flops, s);
 }

@@ -137,3 +137,32 @@ def test_conv1x1_stride2_zero_fills_odd_positions():
     assert float(gx[:, :, 1::2, :].abs().max()) == 0.0
     assert float(gx[:, :, :, 1::2].abs().max()) == 0.0
     assert float(gx[:, :, 0::2, 0::2].min()) > 0.0
+
+
+@pytest.mark.parametrize("cin,cout,h,w", [(16, 16, 10, 14), (24, 72, 7, 12), (40, 120, 9, 20),
+                                          (64, 24, 4, 9), (120, 40, 5, 16)])
+def test_conv1x1_mix_small_writes_every_output(cin, cout, h, w):
+    """The small-channel channel mix (c1_mix_small_kernel: stride 1, K and M <=
+    128 off the 32 grid; 64-pixel wave chunks, ragged at the plane's end,
+    channels padded to 16-row tiles) overwrites NaN-filled outputs completely
+    and matches float64 for both the forward and the data gradient."""
+    from monocular_depth_estimation_amd import _abi
+    n = 3
+    g = torch.Generator().manual_seed(cin * cout + h)
+    x = torch.rand((n, cin, h, w), generator=g) - 0.5
+    wt = (torch.rand((cout, cin), generator=g) - 0.5) * 0.2
+    gy = torch.rand((n, cout, h, w), generator=g) - 0.5
+    yr = torch.einsum("oc,nchw->nohw", wt.double(), x.double())
+    gxr = torch.einsum("oc,nohw->nchw", wt.double(), gy.double())
+    xd, wd, gyd = x.to(DEV), wt.to(DEV), gy.to(DEV)
+    y = torch.full((n, cout, h, w), float("nan"), device=DEV)
+    gx = torch.full((n, cin, h, w), float("nan"), device=DEV)
+    st = _abi.stream_of(xd)
+    _abi.call("mde_conv1x1_fwd", _abi.ptr(xd), _abi.ptr(wd), _abi.ptr(y), n, cin, cout, h, w, 1, 0,
+              st)
+    _abi.call("mde_conv1x1_bwd_data", _abi.ptr(gyd), _abi.ptr(wd), _abi.ptr(gx), n, cin, cout, h, w,
+              1, 0, st)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(y).all()) and bool(torch.isfinite(gx).all())
+    assert rel_err(y, yr) <= 1e-5, "forward"
+    assert rel_err(gx, gxr) <= 1e-5, "data gradient"

@@ -72,6 +72,8 @@ NAMES = [
     (r"minmax_final_kernel", "minmax_final"),
     (r"depthnorm_kernel", "depthnorm_apply"),
     (r"ssim3_(l1|stream|pair)_kernel", "ssim3_l1"),
+    (r"c1_mix_small_kernel<[^>]*false>", "conv1x1_fwd"),
+    (r"c1_mix_small_kernel<[^>]*true>", "conv1x1_dgrad"),
     (r"cm_kernel<[^>]*false>", "conv1x1_fwd"),
     (r"cm_kernel<[^>]*true>", "conv1x1_dgrad"),
     (r"c1_wgrad(_small)?_kernel", "conv1x1_wgrad"),

@@ -10,7 +10,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 
 if os.environ.get("MDE_NANFILL"):
     _empty, _empty_like = torch.empty, torch.empty_like

@@ -1,6 +1,6 @@
 """Compare one GraphTrainer eager step with one Trainer step (grads / params)."""
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 
 from monocular_depth_estimation_amd import GuideDepth

@@ -4,7 +4,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from monocular_depth_estimation_amd import _abi  # noqa: E402
 from monocular_depth_estimation_amd.functional import bilinear_resize, minmax  # noqa: E402
 

@@ -80,7 +80,9 @@ def test_conv1x1_vs_float64_oracle(cin, cout, stride, h, w):
                                                  (640, 128, 1, 8, 10),
                                                  # the small-channel weight-gradient path
                                                  (16, 64, 1, 240, 320), (72, 24, 1, 120, 160),
-                                                 (120, 40, 1, 60, 80), (64, 64, 1, 60, 80)])
+                                                 (120, 40, 1, 60, 80), (64, 64, 1, 60, 80),
+                                                 # wide padded M (64-row tiles under MDE_C1_BM_AUTO=1)
+                                                 (112, 672, 1, 30, 40), (480, 112, 1, 30, 40)])
 def test_conv1x1_full_batch_vs_miopen_and_deterministic(cin, cout, stride, h, w):
     """cfg2 batch (32): HIP vs MIOpen fp32 on the GPU for all three passes, and
     two runs bitwise equal (the weight gradient's fixed-order reduction)."""

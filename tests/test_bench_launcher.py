@@ -23,10 +23,13 @@ def _run(*extra):
     env.pop("WORLD_SIZE", None)
     env.pop("RANK", None)
     env.pop("LOCAL_RANK", None)
-    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu",
-                        "--steps", "3", "--warmup", "1", "--bs", "2", "--height", "32",
-                        "--width", "48", *extra],
-                       cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--device", "cpu", "--steps", "3",
+           "--warmup", "1", "--bs", "2", "--height", "32", "--width", "48", *extra]
+    r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
+    if r.returncode != 0 and "address already in use" in r.stderr.lower():
+        # the launcher's free port (bound, released, then handed to the
+        # rendezvous) was taken by another process in between: one retry
+        r = subprocess.run(cmd, cwd=REPO, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout  # rank 0 only, one line

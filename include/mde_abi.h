@@ -403,6 +403,10 @@ int mde_gelu_bwd_colsum(const void* dh, const void* a, void* da, float* gb, int6
  * Split-K over token ranges on v_mfma_f32_16x16x4_f32, partials summed in a
  * fixed order (bitwise reproducible).  Workspace bytes from
  * mde_linear_wgrad_workspace (0 = unsupported shape). */
+size_t mde_linear_wgrad_workspace(int64_t t_rows, int64_t m, int64_t n);
+int mde_linear_wgrad(const void* g, const void* x, float* gw, float* gb, int64_t t_rows,
+                     int64_t m, int64_t n, void* workspace, int dtype, void* stream);
+
 /* Per-channel sums of an NCHW fp32 tensor, gb[c] = sum_{n,p} g[n][c][p] (a
  * biased conv's bias gradient: autograd's grad.sum((0, 2, 3)) behind the
  * NewCRF projections' `y + bias`, src/newcrf_layers.py:384-392); hw % 4 == 0.
@@ -413,7 +417,7 @@ int mde_chansum(const void* g, float* gb, int64_t n, int64_t c, int64_t hw, void
                 int dtype, void* stream);
 
 /* 3x3 / stride-1 / pad-1 convolution with ONE output channel, NCHW fp32 (the
- * NewCRF decoder's depth head, src/model_mobileV3_large_newCRFs.py
+ * NewCRF decoder's depth head, src/model_mobileV3_large_newCRFs.py:81,123
  * Decoder.conv1 = nn.Conv2d(128, 1, 3, padding=1)): y = b + conv(x) (bias
  * nullable), gx, gw (fixed-order reduction; workspace from
  * mde_head_conv_wgrad_workspace).  w % 4 == 0. */
@@ -425,10 +429,6 @@ int mde_head_conv_dgrad(const void* gy, const float* weight, void* gx, int64_t n
 size_t mde_head_conv_wgrad_workspace(int64_t n, int64_t c, int64_t h, int64_t w);
 int mde_head_conv_wgrad(const void* gy, const void* x, float* gweight, int64_t n, int64_t c,
                         int64_t h, int64_t w, void* workspace, int dtype, void* stream);
-
-size_t mde_linear_wgrad_workspace(int64_t t_rows, int64_t m, int64_t n);
-int mde_linear_wgrad(const void* g, const void* x, float* gw, float* gb, int64_t t_rows,
-                     int64_t m, int64_t n, void* workspace, int dtype, void* stream);
 
 /* ---------------------------------------------------------------------------
  * Bias-free 1x1 convolution, NCHW: y[n,o,p] = sum_c W[o,c] x[n,c,p].  The

@@ -1154,14 +1154,21 @@ inline int wide_fixed_sw(int64_t w) {
 // ~1.0x on the fetch side at equal time -- two per CU (512) for planes with
 // >= 4096 strip tiles (64 -> 64 at 120 x 160: 385 vs 417 us), where the slab
 // is small next to the inputs (profiles/r04_wide_blocks_ab.txt).
+// >= 64 channel groups (NewCRF's 256 -> 512, 160 / 512 -> 1024 projections at
+// 30 x 40 / 15 x 20: one to four blocks a group at 256): 768 blocks, three a
+// CU in flight -- wide wgrad 2.485 -> 2.415 ms a cfg4 step for +0.01 ms of
+// reduction (`gpurun_out/r06al`); DDRNet's <= 32 groups keep the rule above
+// (768 for every shape: cfg4 wgrad 2.31 ms but cfg2's reduction +0.14 ms,
+// cfg2 -0.4 %, `gpurun_out/r06ak`).
 // MDE_WIDE_BLOCKS overrides (A/B).
-inline int wide_blocks(int64_t ntiles) {
+inline int wide_blocks(int64_t ntiles, int groups) {
   static const int forced = [] {
     const char* e = std::getenv("MDE_WIDE_BLOCKS");
     const int v = e ? std::atoi(e) : 0;
     return v >= 8 ? v : 0;
   }();
   if (forced) return forced;
+  if (groups >= 64) return 768;
   return ntiles >= 4096 ? 512 : 256;
 }
 
@@ -1188,7 +1195,7 @@ inline bool wide_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w, W
   }
   p->groups = (int)(mde::cdiv(ci, kWCI) * (co / kWCO));
   // one 100 KB-LDS block per CU (generic), two <= 80 KB blocks (fixed width)
-  int gx = (p->fixed_sw ? wide_blocks(p->g.ntiles) : 256) / p->groups;
+  int gx = (p->fixed_sw ? wide_blocks(p->g.ntiles, p->groups) : 256) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;
@@ -1336,7 +1343,7 @@ inline bool wide_s2_plan(int64_t n, int64_t ci, int64_t co, int64_t h, int64_t w
   p->g.tiles_per_img = (int)tpi;
   p->g.ntiles = (int)nt;
   p->groups = (int)((ci / kWCI) * (co / kWCO));
-  int gx = wide_blocks(nt) / p->groups;
+  int gx = wide_blocks(nt, p->groups) / p->groups;
   if (gx < 1) gx = 1;
   if (gx > p->g.ntiles) gx = p->g.ntiles;
   p->gx = gx;
